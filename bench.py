@@ -1,0 +1,130 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node SHA-256 PoW hashrate (MH/s) on N MI355X (BASELINE.json metric).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched by
+``torch.distributed.run`` with one rank per GPU (RCCL over xGMI). One *step* = every rank sweeps the
+full 2^32 nonce space of its own synthetic v2 header (108 B, difficulty 6.3, per-rank timestamp:
+nonce-space data parallelism, upow_amd/parallel/miner_dp.py), exact-checks every candidate on the
+host, then the ranks agree on a winner with an all-reduce(MIN) and broadcast the winning header over
+RCCL; every rank re-verifies it. Nothing is skipped: every nonce of every step is hashed.
+
+Weak scaling: per-GPU work (2^32 nonces/step) is fixed as N grows; ``value`` is the aggregate MH/s
+of all N GPUs. ``vs_baseline`` divides by BASELINE.md's 0.99 MH/s (the reference miner.py inner loop,
+one process, measured in the survey sandbox — the reference publishes no number).
+
+``--mode verify`` measures the second BASELINE metric instead (tx-verify/s on a synthetic 2 MB block).
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+BASELINE_MHS = 0.99  # miner.py-style loop, 1 process (measured; nothing published)
+
+
+def _synthetic_job(seed: int = 2026):
+    import random
+
+    from upow_amd.utils import p256
+    from upow_amd.utils.codec import AddressFormat, point_to_string
+    rng = random.Random(seed)
+    prev_hash = hashlib.sha256(rng.randbytes(32)).hexdigest()
+    d = rng.randrange(1, p256.N)
+    address = point_to_string(p256.get_public_key(d), AddressFormat.COMPRESSED)
+    tx_hashes = sorted(hashlib.sha256(rng.randbytes(250)).hexdigest() for _ in range(10))
+    merkle = hashlib.sha256(b''.join(bytes.fromhex(h) for h in tx_hashes)).hexdigest()
+    return prev_hash, address, merkle
+
+
+def bench_mine(args, ctx):
+    from upow_amd.ops.native import gpu_available
+    from upow_amd.ops.pow import NONCE_SPACE
+    from upow_amd.parallel.miner_dp import DataParallelMiner
+
+    device = 'gpu' if gpu_available() else 'cpu'
+    count = args.nonces if args.nonces else (NONCE_SPACE if device == 'gpu' else 1 << 22)
+    prev_hash, address, merkle = _synthetic_job()
+    ts0 = 1_790_000_000
+    miner = DataParallelMiner(ctx, prev_hash, address, merkle, ts0, args.difficulty, device=device,
+                              variant=args.variant)
+    for _ in range(args.warmup):
+        miner.step(count)
+    ctx.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    hits = 0
+    winners = 0
+    for _ in range(args.steps):
+        r = miner.step(count)
+        hits += r.global_hits
+        winners += r.header is not None
+    ctx.synchronize()
+    ctx.barrier()
+    dt = time.perf_counter() - t0
+    dt = ctx.allreduce_max_f(dt)
+    total_hashes = count * args.steps * ctx.world
+    mhs = total_hashes / dt / 1e6
+    return {
+        'metric': 'sha256_pow_hashrate_MH/s',
+        'value': round(mhs, 3),
+        'unit': 'MH/s',
+        'n_gpus': ctx.world if device == 'gpu' else 0,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(dt * 1000 / max(1, args.steps), 3),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': round(mhs / BASELINE_MHS, 1),
+        'dtype': 'uint32',
+        'data': 'synthetic (random prev-hash, random P-256 miner key, 10 random tx hashes)',
+        'config': {
+            'model': 'upow v2 block header PoW (108 B, single SHA-256, nibble-prefix target)',
+            'difficulty': float(args.difficulty),
+            'global_batch': total_hashes // max(1, args.steps),
+            'seq_len': 108,
+            'parallelism': f'dp{ctx.world}',
+            'nonces_per_rank_step': count,
+            'device': device,
+            'kernel_variant': args.variant,
+        },
+        'solutions_found': hits,
+        'steps_with_block': winners,
+    }
+
+
+def bench_verify(args, ctx):
+    from upow_amd.bench_verify import run_verify_bench
+    return run_verify_bench(args, ctx)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--mode', choices=['mine', 'verify'], default='mine')
+    ap.add_argument('--difficulty', default='6.3')
+    ap.add_argument('--nonces', type=int, default=0, help='nonce words per rank per step (default 2^32)')
+    ap.add_argument('--variant', type=int, default=int(os.environ.get('UPOW_POW_VARIANT', '0')))
+    ap.add_argument('--txs', type=int, default=8300, help='verify mode: txs per block')
+    args = ap.parse_args(argv)
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from upow_amd.ops.native import lib
+    lib()  # loads torch's HIP runtime first, then the extension (fails loudly if not built)
+    from upow_amd.parallel.dist import init_from_env, shutdown
+    ctx = init_from_env()
+    try:
+        out = bench_mine(args, ctx) if args.mode == 'mine' else bench_verify(args, ctx)
+        if ctx.is_main:
+            print(json.dumps(out), flush=True)
+    finally:
+        shutdown(ctx)
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,36 @@
+// Declarations shared between the pybind11 bindings (bindings.cpp, host C++) and the HIP
+// translation units (*.hip). Only plain host types cross this boundary.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace upow {
+
+// ---------------------------------------------------------------- PoW (K1)
+struct PowJobHost {
+    std::vector<uint8_t> header;  // full 108-byte (v2) or 138-byte (v1) header; nonce bytes ignored
+    uint32_t tmask = 0, tword = 0, frac_shift = 0, frac_limit = 16;
+};
+
+struct PowResult {
+    uint64_t searched = 0;
+    uint32_t total_hits = 0;
+    std::vector<uint32_t> words;  // candidate nonce words (v2: bswap(nonce), v1: nonce)
+};
+
+bool pow_check_word_host(const PowJobHost& job, uint32_t v);
+PowResult pow_search_host(const PowJobHost& job, uint64_t start, uint64_t count, int threads);
+PowResult pow_search_gpu(const PowJobHost& job, uint64_t start, uint64_t count, int grid_blocks,
+                         uint32_t chunk_iters, uint32_t cap, int variant);
+
+// ---------------------------------------------------------------- batched SHA-256 (K3/K4/K12)
+// messages packed back to back in `data`, message i = data[offsets[i] .. offsets[i+1])
+std::vector<uint8_t> sha256_batch_host(const uint8_t* data, const int64_t* offsets, int64_t n, int threads);
+std::vector<uint8_t> sha256_batch_gpu(const uint8_t* data, int64_t nbytes, const int64_t* offsets, int64_t n);
+
+// ---------------------------------------------------------------- device info
+int gpu_device_count();
+std::string gpu_arch_name(int device);
+
+}  // namespace upow

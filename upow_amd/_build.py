@@ -1,0 +1,95 @@
+"""Build the native extension ``upow_amd/_native*.so`` in-tree for gfx950.
+
+* ``csrc/*.hip`` -> ``hipcc --offload-arch=gfx950 -O3`` (device + host code)
+* ``csrc/*.cpp`` -> host C++ (pybind11 bindings, CPU crypto)
+* link with ``hipcc -shared`` (libamdhip64)
+
+Objects are cached by content hash of the source + all headers, so re-running is cheap.
+Usage: ``python -m upow_amd._build [--force] [-j N]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / 'csrc'
+BUILD = ROOT / 'build' / 'native'
+PKG = ROOT / 'upow_amd'
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+ARCH = os.environ.get('UPOW_OFFLOAD_ARCH', 'gfx950')
+EXT_SUFFIX = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
+TARGET = PKG / f'_native{EXT_SUFFIX}'
+
+
+def _pybind_include() -> str:
+    import pybind11
+    return pybind11.get_include()
+
+
+def _headers_digest() -> str:
+    h = hashlib.sha256()
+    for p in sorted(CSRC.glob('*.h')):
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+def _flags_common():
+    return ['-O3', '-std=c++17', '-fPIC', '-Wall', '-Wno-unused-function', f'-I{CSRC}']
+
+
+def _compile(src: Path, hdr_digest: str, force: bool) -> Path:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    key = hashlib.sha256(src.read_bytes() + hdr_digest.encode() + ARCH.encode()).hexdigest()[:16]
+    obj = BUILD / f'{src.stem}.{key}.o'
+    if obj.exists() and not force:
+        return obj
+    if src.suffix == '.hip':
+        cmd = [HIPCC, f'--offload-arch={ARCH}', *_flags_common(), '-c', str(src), '-o', str(obj)]
+    else:
+        cmd = [HIPCC, *_flags_common(), f'-I{_pybind_include()}', f'-I{sysconfig.get_paths()["include"]}',
+               '-fvisibility=hidden', '-c', str(src), '-o', str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f'compile failed: {" ".join(cmd)}\n{r.stdout}\n{r.stderr}')
+    return obj
+
+
+def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> Path:
+    srcs = sorted(CSRC.glob('*.hip')) + sorted(CSRC.glob('*.cpp'))
+    hd = _headers_digest()
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hd, force), srcs))
+    link_key = hashlib.sha256(''.join(o.name for o in objs).encode()).hexdigest()[:16]
+    stamp = BUILD / 'link.stamp'
+    if TARGET.exists() and stamp.exists() and stamp.read_text() == link_key and not force:
+        if verbose:
+            print(f'[upow_amd._build] up to date: {TARGET.name}')
+        return TARGET
+    cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', str(TARGET), *map(str, objs)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f'link failed: {" ".join(cmd)}\n{r.stdout}\n{r.stderr}')
+    stamp.write_text(link_key)
+    if verbose:
+        print(f'[upow_amd._build] built {TARGET} from {len(objs)} objects')
+    return TARGET
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--force', action='store_true')
+    ap.add_argument('-j', '--jobs', type=int, default=min(8, os.cpu_count() or 4))
+    a = ap.parse_args(argv)
+    build(force=a.force, jobs=a.jobs)
+
+
+if __name__ == '__main__':
+    sys.exit(main())
