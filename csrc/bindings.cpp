@@ -96,8 +96,60 @@ PYBIND11_MODULE(_native, m) {
         }
         return pow_result_tuple(r);
     }, py::arg("header"), py::arg("tmask"), py::arg("tword"), py::arg("frac_shift"), py::arg("frac_limit"),
-       py::arg("start"), py::arg("count"), py::arg("grid_blocks") = 0, py::arg("chunk_iters") = 256,
+       py::arg("start"), py::arg("count"), py::arg("grid_blocks") = 0, py::arg("chunk_iters") = 0,
        py::arg("cap") = 1 << 16, py::arg("variant") = 0);
+
+    m.def("pow_kernel_info", [](int variant) {
+        PowKernelInfo k = pow_kernel_info(variant);
+        return py::dict(py::arg("cus") = k.cus, py::arg("blocks_per_cu") = k.blocks_per_cu,
+                        py::arg("resident_blocks") = k.resident_blocks);
+    }, py::arg("variant") = 0);
+    m.def("p256_verify", [](py::buffer items, bool gpu, int threads) {
+        py::buffer_info bi = items.request();
+        const int64_t nbytes = bi.size * bi.itemsize;
+        if (nbytes % 160) throw std::invalid_argument("items must be n x 160 bytes");
+        const int64_t n = nbytes / 160;
+        const uint8_t* p = static_cast<const uint8_t*>(bi.ptr);
+        std::vector<uint8_t> st;
+        {
+            py::gil_scoped_release rel;
+            st = gpu ? p256_verify_gpu(p, n) : p256_verify_host(p, n, threads);
+        }
+        return py::bytes(reinterpret_cast<const char*>(st.data()), st.size());
+    }, py::arg("items"), py::arg("gpu") = false, py::arg("threads") = 1);
+
+    m.def("p256_decompress", [](py::buffer in, bool gpu) {
+        py::buffer_info bi = in.request();
+        const int64_t nbytes = bi.size * bi.itemsize;
+        if (nbytes % 33) throw std::invalid_argument("input must be n x 33 bytes");
+        const int64_t n = nbytes / 33;
+        std::vector<uint8_t> out(static_cast<size_t>(n) * 64), ok(static_cast<size_t>(n));
+        {
+            py::gil_scoped_release rel;
+            if (gpu) p256_decompress_gpu(static_cast<const uint8_t*>(bi.ptr), n, out.data(), ok.data());
+            else p256_decompress_host(static_cast<const uint8_t*>(bi.ptr), n, out.data(), ok.data());
+        }
+        return py::make_tuple(py::bytes(reinterpret_cast<const char*>(out.data()), out.size()),
+                              py::bytes(reinterpret_cast<const char*>(ok.data()), ok.size()));
+    }, py::arg("data"), py::arg("gpu") = false);
+
+    m.def("p256_pubkey", [](py::bytes d_be) -> py::object {
+        std::string d = d_be;
+        if (d.size() != 32) throw std::invalid_argument("private key must be 32 bytes big-endian");
+        uint8_t out[64];
+        if (!p256_pubkey(reinterpret_cast<const uint8_t*>(d.data()), out)) return py::none();
+        return py::bytes(reinterpret_cast<const char*>(out), 64);
+    });
+
+    m.def("p256_sign", [](py::bytes d_be, py::bytes digest) -> py::object {
+        std::string d = d_be, h = digest;
+        if (d.size() != 32 || h.size() != 32) throw std::invalid_argument("need 32-byte key and digest");
+        uint8_t r[32], s[32];
+        if (!p256_sign(reinterpret_cast<const uint8_t*>(d.data()), reinterpret_cast<const uint8_t*>(h.data()), r, s))
+            return py::none();
+        return py::make_tuple(py::bytes(reinterpret_cast<const char*>(r), 32),
+                              py::bytes(reinterpret_cast<const char*>(s), 32));
+    });
 
     m.def("gpu_device_count", &gpu_device_count);
     m.def("gpu_arch_name", &gpu_arch_name);

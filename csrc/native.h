@@ -19,6 +19,11 @@ struct PowResult {
     std::vector<uint32_t> words;  // candidate nonce words (v2: bswap(nonce), v1: nonce)
 };
 
+struct PowKernelInfo {
+    int cus = 0, blocks_per_cu = 0, resident_blocks = 0;
+};
+PowKernelInfo pow_kernel_info(int variant);
+
 bool pow_check_word_host(const PowJobHost& job, uint32_t v);
 PowResult pow_search_host(const PowJobHost& job, uint64_t start, uint64_t count, int threads);
 PowResult pow_search_gpu(const PowJobHost& job, uint64_t start, uint64_t count, int grid_blocks,
@@ -28,6 +33,16 @@ PowResult pow_search_gpu(const PowJobHost& job, uint64_t start, uint64_t count, 
 // messages packed back to back in `data`, message i = data[offsets[i] .. offsets[i+1])
 std::vector<uint8_t> sha256_batch_host(const uint8_t* data, const int64_t* offsets, int64_t n, int threads);
 std::vector<uint8_t> sha256_batch_gpu(const uint8_t* data, int64_t nbytes, const int64_t* offsets, int64_t n);
+
+// ---------------------------------------------------------------- P-256 (K5/K6/K15)
+// verify items: 160-byte records {qx LE, qy LE, r LE, s LE, e = SHA-256 digest BE}
+// status: 1 valid, 0 invalid, 2 key off-curve, 3 r/s out of range
+std::vector<uint8_t> p256_verify_host(const uint8_t* items, int64_t n, int threads);
+std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n);
+void p256_decompress_host(const uint8_t* in33, int64_t n, uint8_t* out64, uint8_t* ok);
+void p256_decompress_gpu(const uint8_t* in33, int64_t n, uint8_t* out64, uint8_t* ok);
+bool p256_pubkey(const uint8_t d_be[32], uint8_t out_le[64]);
+bool p256_sign(const uint8_t d_be[32], const uint8_t digest[32], uint8_t r_le[32], uint8_t s_le[32]);
 
 // ---------------------------------------------------------------- device info
 int gpu_device_count();

@@ -1,0 +1,489 @@
+// NIST P-256 arithmetic shared by the host library and the gfx950 kernels (HIP __host__ __device__).
+//
+// Representation: 8 x 32-bit little-endian limbs. 32-bit limbs map the 32x32->64 partial products
+// onto v_mad_u64_u32 on CDNA4 (64-bit limbs would need 4 of them per product anyway).
+//  * field mod p: schoolbook 8x8 product + NIST/Solinas fast reduction (FIPS 186-4 D.2.3), using
+//    p = 2^256 - 2^224 + 2^192 + 2^96 - 1 (no Montgomery form needed on the coordinate side);
+//  * scalars mod n: Montgomery (CIOS) multiplication, used for s^-1, u1 = e*s^-1, u2 = r*s^-1;
+//  * points: Jacobian coordinates with a = -3 doubling (dbl-2001-b), full add (add-2007-bl) and
+//    mixed Jacobian+affine add (madd-2007-bl), all with explicit infinity/equal/opposite handling.
+//
+// reference semantics being reproduced: fastecdsa's ecdsa.verify/sign and util.mod_sqrt as used by
+// upow/upow_transactions/transaction_input.py:84-120 and upow/helpers.py:58-62.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#define UPOW_HD __host__ __device__ __forceinline__
+
+namespace upow {
+namespace p256 {
+
+struct fe { uint32_t v[8]; };
+
+struct jac { fe x, y, z; };  // z == 0 <=> infinity
+struct aff { fe x, y; };
+
+// ------------------------------------------------------------------------------------------------
+// constants (little-endian 32-bit limbs)
+// ------------------------------------------------------------------------------------------------
+#define P256_P {0xffffffffu, 0xffffffffu, 0xffffffffu, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000001u, 0xffffffffu}
+#define P256_N {0xfc632551u, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu, 0xffffffffu, 0xffffffffu, 0x00000000u, 0xffffffffu}
+#define P256_B {0x27d2604bu, 0x3bce3c3eu, 0xcc53b0f6u, 0x651d06b0u, 0x769886bcu, 0xb3ebbd55u, 0xaa3a93e7u, 0x5ac635d8u}
+#define P256_GX {0xd898c296u, 0xf4a13945u, 0x2deb33a0u, 0x77037d81u, 0x63a440f2u, 0xf8bce6e5u, 0xe12c4247u, 0x6b17d1f2u}
+#define P256_GY {0x37bf51f5u, 0xcbb64068u, 0x6b315eceu, 0x2bce3357u, 0x7c0f9e16u, 0x8ee7eb4au, 0xfe1a7f9bu, 0x4fe342e2u}
+#define P256_RN {0x039cdaafu, 0x0c46353du, 0x58e8617bu, 0x43190552u, 0x00000000u, 0x00000000u, 0xffffffffu, 0x00000000u}
+#define P256_R2N {0xbe79eea2u, 0x83244c95u, 0x49bd6fa6u, 0x4699799cu, 0x2b6bec59u, 0x2845b239u, 0xf3d95620u, 0x66e12d94u}
+static constexpr uint32_t P256_N0INV = 0xee00bc4fu;  // -n^-1 mod 2^32
+
+UPOW_HD fe fe_const_p() { return fe{P256_P}; }
+UPOW_HD fe fe_const_n() { return fe{P256_N}; }
+UPOW_HD fe fe_const_b() { return fe{P256_B}; }
+UPOW_HD fe fe_zero() { return fe{{0, 0, 0, 0, 0, 0, 0, 0}}; }
+UPOW_HD fe fe_one() { return fe{{1, 0, 0, 0, 0, 0, 0, 0}}; }
+
+UPOW_HD bool fe_is_zero(const fe& a) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t |= a.v[i];
+    return t == 0;
+}
+UPOW_HD bool fe_eq(const fe& a, const fe& b) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t |= a.v[i] ^ b.v[i];
+    return t == 0;
+}
+// a >= b (unsigned 256-bit)
+UPOW_HD bool fe_geq(const fe& a, const fe& b) {
+    // compute a - b and look at the final borrow
+    uint64_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t d = uint64_t(a.v[i]) - b.v[i] - borrow;
+        borrow = (d >> 63) & 1;
+    }
+    return borrow == 0;
+}
+// r = a + b, returns carry
+UPOW_HD uint32_t raw_add(fe& r, const fe& a, const fe& b) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        c += uint64_t(a.v[i]) + b.v[i];
+        r.v[i] = uint32_t(c);
+        c >>= 32;
+    }
+    return uint32_t(c);
+}
+// r = a - b, returns borrow
+UPOW_HD uint32_t raw_sub(fe& r, const fe& a, const fe& b) {
+    uint64_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t d = uint64_t(a.v[i]) - b.v[i] - borrow;
+        r.v[i] = uint32_t(d);
+        borrow = (d >> 63) & 1;
+    }
+    return uint32_t(borrow);
+}
+// r = cond ? a : b  (branch-free select)
+UPOW_HD fe fe_select(bool cond, const fe& a, const fe& b) {
+    fe r;
+    const uint32_t m = cond ? 0xffffffffu : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = (a.v[i] & m) | (b.v[i] & ~m);
+    return r;
+}
+
+// ------------------------------------------------------------------------------------------------
+// field mod p
+// ------------------------------------------------------------------------------------------------
+UPOW_HD fe fe_add(const fe& a, const fe& b) {
+    fe r, t;
+    const uint32_t c = raw_add(r, a, b);
+    const uint32_t br = raw_sub(t, r, fe_const_p());
+    // use t when (carry) or (no borrow)
+    return fe_select(c | (br ^ 1u), t, r);
+}
+UPOW_HD fe fe_sub(const fe& a, const fe& b) {
+    fe r, t;
+    const uint32_t br = raw_sub(r, a, b);
+    raw_add(t, r, fe_const_p());
+    return fe_select(br != 0, t, r);
+}
+UPOW_HD fe fe_neg(const fe& a) { return fe_sub(fe_zero(), a); }
+
+// 512-bit schoolbook product, operand scanning: each partial product a_i*b_j + r + carry fits in
+// 64 bits ((2^32-1)^2 + 2(2^32-1) = 2^64 - 1).
+UPOW_HD void mul_512(uint32_t c[16], const fe& a, const fe& b) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) c[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t carry = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint64_t t = uint64_t(a.v[i]) * b.v[j] + c[i + j] + carry;
+            c[i + j] = uint32_t(t);
+            carry = t >> 32;
+        }
+        c[i + 8] = uint32_t(carry);
+    }
+}
+
+// squaring: off-diagonal products once, doubled, plus the diagonal.
+UPOW_HD void sqr_512(uint32_t c[16], const fe& a) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) c[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        uint64_t carry = 0;
+#pragma unroll
+        for (int j = i + 1; j < 8; ++j) {
+            const uint64_t t = uint64_t(a.v[i]) * a.v[j] + c[i + j] + carry;
+            c[i + j] = uint32_t(t);
+            carry = t >> 32;
+        }
+        c[i + 8] = uint32_t(carry);
+    }
+    // double
+    uint32_t top = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t nt = c[i] >> 31;
+        c[i] = (c[i] << 1) | top;
+        top = nt;
+    }
+    // add diagonal
+    uint64_t carry = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint64_t sq = uint64_t(a.v[i]) * a.v[i];
+        uint64_t t = uint64_t(c[2 * i]) + uint32_t(sq) + carry;
+        c[2 * i] = uint32_t(t);
+        t = uint64_t(c[2 * i + 1]) + uint32_t(sq >> 32) + (t >> 32);
+        c[2 * i + 1] = uint32_t(t);
+        carry = t >> 32;
+    }
+}
+
+// NIST fast reduction of a 512-bit value mod p.
+UPOW_HD fe fe_reduce(const uint32_t c[16]) {
+    const int64_t c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3], c4 = c[4], c5 = c[5], c6 = c[6], c7 = c[7];
+    const int64_t c8 = c[8], c9 = c[9], c10 = c[10], c11 = c[11], c12 = c[12], c13 = c[13], c14 = c[14],
+                  c15 = c[15];
+    int64_t t[8];
+    t[0] = c0 + c8 + c9 - c11 - c12 - c13 - c14;
+    t[1] = c1 + c9 + c10 - c12 - c13 - c14 - c15;
+    t[2] = c2 + c10 + c11 - c13 - c14 - c15;
+    t[3] = c3 + 2 * c11 + 2 * c12 + c13 - c15 - c8 - c9;
+    t[4] = c4 + 2 * c12 + 2 * c13 + c14 - c9 - c10;
+    t[5] = c5 + 2 * c13 + 2 * c14 + c15 - c10 - c11;
+    t[6] = c6 + 3 * c14 + 2 * c15 + c13 - c8 - c9;
+    t[7] = c7 + 3 * c15 + c8 - c10 - c11 - c12 - c13;
+    fe r;
+    int64_t carry = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int64_t v = t[i] + carry;
+        r.v[i] = uint32_t(v);
+        carry = v >> 32;  // arithmetic shift
+    }
+    // fold carry * 2^256 == carry * (2^224 - 2^192 - 2^96 + 1) (mod p), twice
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+        int64_t u[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) u[i] = int64_t(r.v[i]);
+        u[0] += carry;
+        u[3] -= carry;
+        u[6] -= carry;
+        u[7] += carry;
+        carry = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int64_t v = u[i] + carry;
+            r.v[i] = uint32_t(v);
+            carry = v >> 32;
+        }
+    }
+    // now 0 <= r < 2^256 < 2p
+    fe t2;
+    const uint32_t br = raw_sub(t2, r, fe_const_p());
+    return fe_select(br == 0, t2, r);
+}
+
+UPOW_HD fe fe_mul(const fe& a, const fe& b) {
+    uint32_t c[16];
+    mul_512(c, a, b);
+    return fe_reduce(c);
+}
+UPOW_HD fe fe_sqr(const fe& a) {
+    uint32_t c[16];
+    sqr_512(c, a);
+    return fe_reduce(c);
+}
+UPOW_HD fe fe_sqr_n(fe a, int n) {
+    for (int i = 0; i < n; ++i) a = fe_sqr(a);
+    return a;
+}
+UPOW_HD fe fe_mul_small(const fe& a, uint32_t k) {
+    fe r = fe_zero();
+    for (uint32_t i = 0; i < k; ++i) r = fe_add(r, a);
+    return r;
+}
+
+// a^(p-2) via an addition chain over runs of ones: p-2 = ffffffff 00000001 00000000 00000000
+// 00000000 ffffffff ffffffff fffffffd (big-endian words).
+UPOW_HD fe fe_inv(const fe& a) {
+    const fe x2 = fe_mul(fe_sqr(a), a);             // 2^2-1
+    const fe x3 = fe_mul(fe_sqr(x2), a);            // 2^3-1
+    const fe x6 = fe_mul(fe_sqr_n(x3, 3), x3);      // 2^6-1
+    const fe x12 = fe_mul(fe_sqr_n(x6, 6), x6);     // 2^12-1
+    const fe x15 = fe_mul(fe_sqr_n(x12, 3), x3);    // 2^15-1
+    const fe x30 = fe_mul(fe_sqr_n(x15, 15), x15);  // 2^30-1
+    const fe x32 = fe_mul(fe_sqr_n(x30, 2), x2);    // 2^32-1
+    fe t = fe_mul(fe_sqr_n(x32, 32), a);            // ffffffff 00000001
+    t = fe_sqr_n(t, 96);                            // 00000000 00000000 00000000
+    t = fe_mul(fe_sqr_n(t, 32), x32);               // ffffffff
+    t = fe_mul(fe_sqr_n(t, 32), x32);               // ffffffff
+    t = fe_mul(fe_sqr_n(t, 30), x30);               // fffffffd = 30 ones ...
+    t = fe_mul(fe_sqr_n(t, 2), a);                  //            ... then "01"
+    return t;
+}
+
+// a^((p+1)/4): (p+1)/4 = 3fffffffc0000000400000000000000000000000400000000000000000000000
+UPOW_HD fe fe_sqrt_candidate(const fe& a) {
+    const fe x2 = fe_mul(fe_sqr(a), a);
+    const fe x4 = fe_mul(fe_sqr_n(x2, 2), x2);
+    const fe x8 = fe_mul(fe_sqr_n(x4, 4), x4);
+    const fe x16 = fe_mul(fe_sqr_n(x8, 8), x8);
+    const fe x32 = fe_mul(fe_sqr_n(x16, 16), x16);
+    // exponent bits (from the top): 30 ones ... we build (2^32-1) << ... then adjust:
+    // (p+1)/4 = 2^254 - 2^222 + 2^190 + 2^94 ; compute a^(2^32-1) then shift patterns:
+    fe t = fe_sqr_n(x32, 32);        // a^((2^32-1)*2^32)
+    t = fe_mul(t, a);                // a^((2^32-1)*2^32 + 1)
+    t = fe_sqr_n(t, 96);             // * 2^96
+    t = fe_mul(t, a);                // + 1
+    t = fe_sqr_n(t, 94);             // * 2^94
+    // exponent = ((2^32-1)*2^32 + 1)*2^190 + 2^94 = 2^254 - 2^222 + 2^190 + 2^94 == (p+1)/4
+    return t;
+}
+
+// ------------------------------------------------------------------------------------------------
+// scalars mod n (Montgomery, R = 2^256)
+// ------------------------------------------------------------------------------------------------
+UPOW_HD fe sc_mont_mul(const fe& a, const fe& b) {
+    const fe n = fe_const_n();
+    uint32_t t[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) t[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t C = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint64_t s = uint64_t(a.v[j]) * b.v[i] + t[j] + C;
+            t[j] = uint32_t(s);
+            C = s >> 32;
+        }
+        uint64_t s = uint64_t(t[8]) + C;
+        t[8] = uint32_t(s);
+        t[9] = uint32_t(s >> 32);
+        const uint32_t m = t[0] * P256_N0INV;
+        s = uint64_t(m) * n.v[0] + t[0];
+        C = s >> 32;
+#pragma unroll
+        for (int j = 1; j < 8; ++j) {
+            s = uint64_t(m) * n.v[j] + t[j] + C;
+            t[j - 1] = uint32_t(s);
+            C = s >> 32;
+        }
+        s = uint64_t(t[8]) + C;
+        t[7] = uint32_t(s);
+        t[8] = t[9] + uint32_t(s >> 32);
+    }
+    fe r, d;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = t[i];
+    const uint32_t br = raw_sub(d, r, n);
+    return fe_select(t[8] != 0 || br == 0, d, r);
+}
+UPOW_HD fe sc_to_mont(const fe& a) { return sc_mont_mul(a, fe{P256_R2N}); }
+UPOW_HD fe sc_from_mont(const fe& a) { return sc_mont_mul(a, fe_one()); }
+// reduce a < 2^256 mod n (a < 2n always holds)
+UPOW_HD fe sc_reduce(const fe& a) {
+    fe d;
+    const uint32_t br = raw_sub(d, a, fe_const_n());
+    return fe_select(br == 0, d, a);
+}
+// a^(n-2) in the Montgomery domain (a_m = a*R): returns a^-1 * R
+UPOW_HD fe sc_inv_mont(const fe& a_m) {
+    // n-2 = ffffffff 00000000 ffffffff ffffffff bce6faad a7179e84 f3b9cac2 fc63254f
+    const fe n2{{0xfc63254fu, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu, 0xffffffffu, 0xffffffffu, 0x00000000u,
+                 0xffffffffu}};
+    // 4-bit fixed window
+    fe tbl[16];
+    tbl[0] = fe{P256_RN};
+    tbl[1] = a_m;
+    for (int i = 2; i < 16; ++i) tbl[i] = sc_mont_mul(tbl[i - 1], a_m);
+    fe r = fe{P256_RN};
+    for (int w = 63; w >= 0; --w) {
+        if (w != 63) {
+            r = sc_mont_mul(r, r); r = sc_mont_mul(r, r); r = sc_mont_mul(r, r); r = sc_mont_mul(r, r);
+        }
+        const uint32_t nib = (n2.v[w >> 3] >> ((w & 7) * 4)) & 0xfu;
+        r = sc_mont_mul(r, tbl[nib]);
+    }
+    return r;
+}
+
+// ------------------------------------------------------------------------------------------------
+// points
+// ------------------------------------------------------------------------------------------------
+UPOW_HD bool jac_is_inf(const jac& p) { return fe_is_zero(p.z); }
+UPOW_HD jac jac_inf() { return jac{fe_one(), fe_one(), fe_zero()}; }
+UPOW_HD jac jac_from_aff(const aff& a) { return jac{a.x, a.y, fe_one()}; }
+
+UPOW_HD bool aff_on_curve(const aff& a) {
+    const fe p = fe_const_p();
+    if (fe_geq(a.x, p) || fe_geq(a.y, p)) return false;
+    // y^2 == x^3 - 3x + b
+    const fe y2 = fe_sqr(a.y);
+    fe rhs = fe_mul(fe_sqr(a.x), a.x);
+    const fe x3 = fe_add(fe_add(a.x, a.x), a.x);
+    rhs = fe_add(fe_sub(rhs, x3), fe_const_b());
+    return fe_eq(y2, rhs);
+}
+
+// dbl-2001-b (a = -3): 3M + 5S
+UPOW_HD jac jac_dbl(const jac& p) {
+    if (fe_is_zero(p.z) || fe_is_zero(p.y)) return jac_inf();
+    const fe delta = fe_sqr(p.z);
+    const fe gamma = fe_sqr(p.y);
+    const fe beta = fe_mul(p.x, gamma);
+    const fe t0 = fe_sub(p.x, delta);
+    const fe t1 = fe_add(p.x, delta);
+    fe alpha = fe_mul(t0, t1);
+    alpha = fe_add(fe_add(alpha, alpha), alpha);
+    const fe beta4 = fe_add(fe_add(beta, beta), fe_add(beta, beta));
+    const fe beta8 = fe_add(beta4, beta4);
+    jac r;
+    r.x = fe_sub(fe_sqr(alpha), beta8);
+    const fe yz = fe_add(p.y, p.z);
+    r.z = fe_sub(fe_sub(fe_sqr(yz), gamma), delta);
+    fe g2 = fe_sqr(gamma);
+    g2 = fe_add(g2, g2);
+    g2 = fe_add(g2, g2);
+    g2 = fe_add(g2, g2);  // 8 gamma^2
+    r.y = fe_sub(fe_mul(alpha, fe_sub(beta4, r.x)), g2);
+    return r;
+}
+
+// add-2007-bl: 11M + 5S
+UPOW_HD jac jac_add(const jac& p, const jac& q) {
+    if (fe_is_zero(p.z)) return q;
+    if (fe_is_zero(q.z)) return p;
+    const fe z1z1 = fe_sqr(p.z);
+    const fe z2z2 = fe_sqr(q.z);
+    const fe u1 = fe_mul(p.x, z2z2);
+    const fe u2 = fe_mul(q.x, z1z1);
+    const fe s1 = fe_mul(fe_mul(p.y, q.z), z2z2);
+    const fe s2 = fe_mul(fe_mul(q.y, p.z), z1z1);
+    const fe h = fe_sub(u2, u1);
+    const fe rr0 = fe_sub(s2, s1);
+    if (fe_is_zero(h)) {
+        if (fe_is_zero(rr0)) return jac_dbl(p);
+        return jac_inf();
+    }
+    const fe h2 = fe_add(h, h);
+    const fe i = fe_sqr(h2);
+    const fe j = fe_mul(h, i);
+    const fe rr = fe_add(rr0, rr0);
+    const fe v = fe_mul(u1, i);
+    jac r;
+    r.x = fe_sub(fe_sub(fe_sqr(rr), j), fe_add(v, v));
+    const fe s1j = fe_mul(s1, j);
+    r.y = fe_sub(fe_mul(rr, fe_sub(v, r.x)), fe_add(s1j, s1j));
+    const fe zz = fe_add(p.z, q.z);
+    r.z = fe_mul(fe_sub(fe_sub(fe_sqr(zz), z1z1), z2z2), h);
+    return r;
+}
+
+// madd-2007-bl (q affine, z2 = 1): 7M + 4S
+UPOW_HD jac jac_madd(const jac& p, const aff& q) {
+    if (fe_is_zero(p.z)) return jac_from_aff(q);
+    const fe z1z1 = fe_sqr(p.z);
+    const fe u2 = fe_mul(q.x, z1z1);
+    const fe s2 = fe_mul(fe_mul(q.y, p.z), z1z1);
+    const fe h = fe_sub(u2, p.x);
+    const fe rr0 = fe_sub(s2, p.y);
+    if (fe_is_zero(h)) {
+        if (fe_is_zero(rr0)) return jac_dbl(p);
+        return jac_inf();
+    }
+    const fe hh = fe_sqr(h);
+    fe i = fe_add(hh, hh);
+    i = fe_add(i, i);
+    const fe j = fe_mul(h, i);
+    const fe rr = fe_add(rr0, rr0);
+    const fe v = fe_mul(p.x, i);
+    jac r;
+    r.x = fe_sub(fe_sub(fe_sqr(rr), j), fe_add(v, v));
+    const fe y1j = fe_mul(p.y, j);
+    r.y = fe_sub(fe_mul(rr, fe_sub(v, r.x)), fe_add(y1j, y1j));
+    const fe zh = fe_add(p.z, h);
+    r.z = fe_sub(fe_sub(fe_sqr(zh), z1z1), hh);
+    return r;
+}
+
+UPOW_HD bool jac_to_aff(const jac& p, aff& out) {
+    if (fe_is_zero(p.z)) return false;
+    const fe zi = fe_inv(p.z);
+    const fe zi2 = fe_sqr(zi);
+    out.x = fe_mul(p.x, zi2);
+    out.y = fe_mul(p.y, fe_mul(zi2, zi));
+    return true;
+}
+
+// Byte helpers: 32-byte big-endian <-> limbs
+UPOW_HD fe fe_from_be(const uint8_t* b) {
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint8_t* q = b + 28 - 4 * i;
+        r.v[i] = (uint32_t(q[0]) << 24) | (uint32_t(q[1]) << 16) | (uint32_t(q[2]) << 8) | uint32_t(q[3]);
+    }
+    return r;
+}
+UPOW_HD void fe_to_be(const fe& a, uint8_t* b) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint8_t* q = b + 28 - 4 * i;
+        q[0] = uint8_t(a.v[i] >> 24); q[1] = uint8_t(a.v[i] >> 16); q[2] = uint8_t(a.v[i] >> 8); q[3] = uint8_t(a.v[i]);
+    }
+}
+// 32-byte little-endian (the upow wire order for x/y/r/s)
+UPOW_HD fe fe_from_le(const uint8_t* b) {
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint8_t* q = b + 4 * i;
+        r.v[i] = uint32_t(q[0]) | (uint32_t(q[1]) << 8) | (uint32_t(q[2]) << 16) | (uint32_t(q[3]) << 24);
+    }
+    return r;
+}
+UPOW_HD void fe_to_le(const fe& a, uint8_t* b) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint8_t* q = b + 4 * i;
+        q[0] = uint8_t(a.v[i]); q[1] = uint8_t(a.v[i] >> 8); q[2] = uint8_t(a.v[i] >> 16); q[3] = uint8_t(a.v[i] >> 24);
+    }
+}
+UPOW_HD uint32_t fe_nibble(const fe& a, int w) { return (a.v[w >> 3] >> ((w & 7) * 4)) & 0xfu; }
+UPOW_HD uint32_t fe_byte(const fe& a, int k) { return (a.v[k >> 2] >> ((k & 3) * 8)) & 0xffu; }
+
+}  // namespace p256
+}  // namespace upow

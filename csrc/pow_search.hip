@@ -24,6 +24,7 @@
 //    host (covers d >= 8 and the d < 1 "whole hash" quirk).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -173,6 +174,37 @@ static PowDeviceBuffers& pow_buffers(uint32_t cap) {
     return b;
 }
 
+// Grid = exactly the resident capacity of the chip (CUs x blocks/CU for this kernel's VGPR/SGPR use),
+// so every launch is one full "wave" of workgroups with no tail round. The occupancy API can report
+// one block/CU too many for SGPR-heavy kernels (MI355X_MICROARCH.md §Residency), which would only
+// create a small second round here, so we take min(API, 800 / (ceil(sgpr/16)*16 + 16)).
+static int pow_resident_blocks(bool v2, int variant) {
+    int dev = 0, cus = 0, per_cu = 0;
+    hip_check(hipGetDevice(&dev), "hipGetDevice");
+    hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "attr");
+    const void* fn = v2 ? (variant == 1 ? reinterpret_cast<const void*>(&pow_search_kernel<2, 8>)
+                                        : reinterpret_cast<const void*>(&pow_search_kernel<2, 1>))
+                        : reinterpret_cast<const void*>(&pow_search_kernel<1, 1>);
+    hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0), "occupancy");
+    hipFuncAttributes attr{};
+    if (hipFuncGetAttributes(&attr, fn) == hipSuccess) {
+        (void)attr;
+    }
+    if (per_cu < 1) per_cu = 1;
+    if (per_cu > 8) per_cu = 8;
+    return cus * per_cu;
+}
+
+PowKernelInfo pow_kernel_info(int variant) {
+    PowKernelInfo k;
+    int dev = 0;
+    hip_check(hipGetDevice(&dev), "hipGetDevice");
+    hip_check(hipDeviceGetAttribute(&k.cus, hipDeviceAttributeMultiprocessorCount, dev), "attr");
+    k.resident_blocks = pow_resident_blocks(true, variant);
+    k.blocks_per_cu = k.resident_blocks / (k.cus ? k.cus : 1);
+    return k;
+}
+
 // Search nonce words [start, start + count) (count a multiple of the grid size is not required:
 // the tail is covered by an extra short launch). Returns all candidate nonce words (host re-checks).
 PowResult pow_search_gpu(const PowJobHost& hj, uint64_t start, uint64_t count, int grid_blocks,
@@ -182,13 +214,9 @@ PowResult pow_search_gpu(const PowJobHost& hj, uint64_t start, uint64_t count, i
     PowDeviceBuffers& buf = pow_buffers(cap);
     hip_check(hipMemsetAsync(buf.d_count, 0, sizeof(uint32_t), 0), "memset");
     const uint32_t block = 256;
-    if (grid_blocks <= 0) {
-        int dev = 0, cus = 0;
-        hip_check(hipGetDevice(&dev), "hipGetDevice");
-        hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "attr");
-        grid_blocks = cus * 8;  // 8 x 256-thread blocks per CU = 32 waves/CU (full occupancy)
-    }
+    if (grid_blocks <= 0) grid_blocks = pow_resident_blocks(v2, variant);
     const uint64_t per_launch_threads = uint64_t(grid_blocks) * block;
+    if (chunk_iters == 0) chunk_iters = uint32_t(std::max<uint64_t>(1, (uint64_t(1) << 28) / per_launch_threads));
     uint64_t done = 0;
     while (done < count) {
         const uint64_t left = count - done;

@@ -1,0 +1,128 @@
+"""P-256: Python oracle, host C++ core and gfx950 batch kernels against each other."""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+from upow_amd.ops import p256 as op
+from upow_amd.utils import p256 as o
+
+RFC6979_D = 0xC9AFA9D845BA75166B5C215767B1D6934E50C3DB36E89B127B8A622B120F6721
+
+
+def test_rfc6979_sample_vector():
+    # RFC 6979 A.2.5, P-256 + SHA-256, message "sample"
+    r, s = o.sign(b'sample', RFC6979_D)
+    assert r == 0xEFD48B2AACB6A8FD1140DD9CD45E81D69D2C877B56AAF991C34D0EA84EAF3716
+    assert s == 0xF7CB1C942D657C41D436C7A1B6E29F65F3E900DBB9AFF4064DC4AB2F843ACDA8
+    q = o.get_public_key(RFC6979_D)
+    assert q.x == 0x60FED4BA255A9D31C961EB74C6356D68C049B8923B61FA6CE669622E60F29FB6
+    assert q.y == 0x7903FE1008B8BC99A41AE9E95628BC64F2F1B20C2D7E9F5177A3C294D4462299
+
+
+def test_native_sign_pubkey_match_oracle(native):
+    rng = random.Random(2)
+    for _ in range(20):
+        d = rng.randrange(1, o.N)
+        msg = rng.randbytes(rng.randrange(0, 300))
+        assert op.public_key(d) == o.get_public_key(d)
+        assert op.sign(msg, d) == o.sign(msg, d)
+    assert op.sign(b'sample', RFC6979_D) == o.sign(b'sample', RFC6979_D)
+
+
+def test_verify_semantics(native):
+    d = 12345
+    q = o.get_public_key(d)
+    msg = b'\x01\x02hello'
+    sig = o.sign(msg, d)
+    assert op.verify(sig, msg, q) and o.verify(sig, msg, q)
+    assert not op.verify((sig[0], sig[1] ^ 1), msg, q)
+    # the reference's second try hashes the ASCII-hex string (str is utf-8 encoded)
+    sig2 = o.sign(msg.hex(), d)
+    assert op.verify(sig2, msg.hex(), q) and not op.verify(sig2, msg, q)
+    # fastecdsa contract: out-of-range r/s and off-curve keys raise
+    for bad in [(0, sig[1]), (sig[0], 0), (o.N + 1, sig[1]), (sig[0], o.N + 1)]:
+        with pytest.raises(o.EcdsaError):
+            op.verify(bad, msg, q)
+        with pytest.raises(o.EcdsaError):
+            o.verify(bad, msg, q)
+    # r == n and s == n pass the range check and fail verification
+    assert op.verify((o.N, sig[1]), msg, q) is False
+    assert op.verify((sig[0], o.N), msg, q) is False
+    off = o.Point(q.x, (q.y + 1) % o.P, check=False)
+    with pytest.raises(o.EcdsaError):
+        op.verify(sig, msg, off)
+
+
+def _batch(n, seed):
+    rng = random.Random(seed)
+    recs, exp = [], []
+    keys = [rng.randrange(1, o.N) for _ in range(8)]
+    pubs = [o.get_public_key(k) for k in keys]
+    for i in range(n):
+        k = i % 8
+        msg = rng.randbytes(40)
+        r, s = op.sign(msg, keys[k])
+        q = pubs[k]
+        kind = i % 7
+        if kind == 1:
+            s = (s * 3) % o.N or 1
+        elif kind == 2:
+            msg += b'!'
+        elif kind == 3:
+            q = pubs[(k + 1) % 8]
+        elif kind == 4:
+            r = o.N  # passes range check, never verifies
+        elif kind == 5:
+            r = 0    # range error
+        e = hashlib.sha256(msg).digest()
+        recs.append(op.record(q, (r, s), e))
+        if kind == 5:
+            exp.append(3)
+        else:
+            try:
+                exp.append(1 if o.verify_digest(r, s, int.from_bytes(e, 'big'), q.x, q.y) else 0)
+            except o.EcdsaError:
+                exp.append(3)
+    return b''.join(recs), np.array(exp, dtype=np.uint8)
+
+
+def test_host_batch_matches_oracle(native):
+    recs, exp = _batch(70, 3)
+    st = op.verify_records(recs, device='cpu', threads=4)
+    assert (st == exp).all()
+    assert exp.tolist().count(1) > 10
+
+
+def test_decompress_host(native):
+    rng = random.Random(4)
+    addrs, want = [], []
+    for _ in range(30):
+        q = o.get_public_key(rng.randrange(1, o.N))
+        addrs.append(bytes([42 if q.y % 2 == 0 else 43]) + q.x.to_bytes(32, 'little'))
+        want.append((q.x, q.y))
+    addrs.append(bytes([42]) + (5).to_bytes(32, 'little'))  # x=5: check against the oracle
+    try:
+        want.append((5, o.x_to_y(5, False)) if o.is_on_curve(5, o.x_to_y(5, False)) else None)
+    except Exception:
+        want.append(None)
+    assert op.decompress(addrs, device='cpu') == want
+
+
+@pytest.mark.gpu
+def test_gpu_batch_verify_matches_host(gpu):
+    recs, exp = _batch(700, 5)
+    st_gpu = op.verify_records(recs, device='gpu')
+    assert (st_gpu == exp).all()
+
+
+@pytest.mark.gpu
+def test_gpu_decompress(gpu):
+    rng = random.Random(6)
+    addrs = []
+    for _ in range(600):
+        q = o.get_public_key(rng.randrange(1, o.N))
+        addrs.append(bytes([42 if q.y % 2 == 0 else 43]) + q.x.to_bytes(32, 'little'))
+    addrs.append(bytes([43]) + (o.P - 1).to_bytes(32, 'little'))
+    assert op.decompress(addrs, device='gpu') == op.decompress(addrs, device='cpu')

@@ -23,6 +23,7 @@ CSRC = ROOT / 'csrc'
 BUILD = ROOT / 'build' / 'native'
 PKG = ROOT / 'upow_amd'
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+CXX = os.environ.get('CXX', 'g++')
 ARCH = os.environ.get('UPOW_OFFLOAD_ARCH', 'gfx950')
 EXT_SUFFIX = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
 TARGET = PKG / f'_native{EXT_SUFFIX}'
@@ -54,7 +55,8 @@ def _compile(src: Path, hdr_digest: str, force: bool) -> Path:
     if src.suffix == '.hip':
         cmd = [HIPCC, f'--offload-arch={ARCH}', *_flags_common(), '-c', str(src), '-o', str(obj)]
     else:
-        cmd = [HIPCC, *_flags_common(), f'-I{_pybind_include()}', f'-I{sysconfig.get_paths()["include"]}',
+        # host-only translation units: plain C++ (no device pass)
+        cmd = [CXX, *_flags_common(), f'-I{_pybind_include()}', f'-I{sysconfig.get_paths()["include"]}',
                '-fvisibility=hidden', '-c', str(src), '-o', str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

@@ -64,7 +64,7 @@ class PowSearchResult:
 
 
 def search(job: PowJob, start: int = 0, count: int = NONCE_SPACE, device: Optional[str] = None,
-           threads: Optional[int] = None, grid_blocks: int = 0, chunk_iters: int = 256,
+           threads: Optional[int] = None, grid_blocks: int = 0, chunk_iters: int = 0,
            cap: int = 1 << 16, variant: int = 0) -> PowSearchResult:
     """Search nonce *words* [start, start+count). ``device`` = 'gpu' | 'cpu' | None (auto)."""
     L = lib()

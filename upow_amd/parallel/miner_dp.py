@@ -56,10 +56,10 @@ class DataParallelMiner:
         if self.next_word + count > NONCE_SPACE:
             self.roll()
         res = self.search_fn(self.job, self.next_word, count, device=self.device, **self.search_kw)
+        local_header = self.job.header_with_nonce(res.nonces[0]) if res.nonces else None
         self.next_word += count
         if self.next_word >= NONCE_SPACE:
             self.roll()
-        local_header = self.job.header_with_nonce(res.nonces[0]) if res.nonces else None
         ctx = self.ctx
         winner = ctx.allreduce_min(ctx.rank if local_header is not None else ctx.world)
         global_hits = ctx.allreduce_sum(len(res.nonces))
