@@ -151,6 +151,39 @@ PYBIND11_MODULE(_native, m) {
                               py::bytes(reinterpret_cast<const char*>(s), 32));
     });
 
+    auto recs_arg = [](py::buffer b, int64_t& n) {
+        py::buffer_info bi = b.request();
+        const int64_t nb = bi.size * bi.itemsize;
+        if (nb % 40) throw std::invalid_argument("utxo key records must be n x 40 bytes");
+        n = nb / 40;
+        return static_cast<const uint8_t*>(bi.ptr);
+    };
+    m.def("utxo_create", &utxo_create);
+    m.def("utxo_destroy", &utxo_destroy);
+    m.def("utxo_capacity", &utxo_capacity);
+    m.def("utxo_insert", [recs_arg](int64_t h, py::buffer recs) {
+        int64_t n; const uint8_t* p = recs_arg(recs, n);
+        py::gil_scoped_release rel;
+        return utxo_insert(h, p, n);
+    });
+    m.def("utxo_probe", [recs_arg](int64_t h, py::buffer recs) {
+        int64_t n; const uint8_t* p = recs_arg(recs, n);
+        std::vector<uint8_t> o;
+        { py::gil_scoped_release rel; o = utxo_probe(h, p, n); }
+        return py::bytes(reinterpret_cast<const char*>(o.data()), o.size());
+    });
+    m.def("utxo_erase", [recs_arg](int64_t h, py::buffer recs) {
+        int64_t n; const uint8_t* p = recs_arg(recs, n);
+        std::vector<uint8_t> o;
+        { py::gil_scoped_release rel; o = utxo_erase(h, p, n); }
+        return py::bytes(reinterpret_cast<const char*>(o.data()), o.size());
+    });
+    m.def("utxo_dump", [](int64_t h) {
+        std::vector<uint8_t> o;
+        { py::gil_scoped_release rel; o = utxo_dump(h); }
+        return py::bytes(reinterpret_cast<const char*>(o.data()), o.size());
+    });
+
     m.def("gpu_device_count", &gpu_device_count);
     m.def("gpu_arch_name", &gpu_arch_name);
 }

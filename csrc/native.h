@@ -44,6 +44,16 @@ void p256_decompress_gpu(const uint8_t* in33, int64_t n, uint8_t* out64, uint8_t
 bool p256_pubkey(const uint8_t d_be[32], uint8_t out_le[64]);
 bool p256_sign(const uint8_t d_be[32], const uint8_t digest[32], uint8_t r_le[32], uint8_t s_le[32]);
 
+// ---------------------------------------------------------------- HBM UTXO index (K7/K8/K9)
+// key records: 40 bytes {txid[32] raw, uint32 index, uint32 tag}
+int64_t utxo_create(uint32_t log2_cap);
+void utxo_destroy(int64_t h);
+uint32_t utxo_capacity(int64_t h);
+uint32_t utxo_insert(int64_t h, const uint8_t* recs, int64_t n);  // returns #failed (table full)
+std::vector<uint8_t> utxo_probe(int64_t h, const uint8_t* recs, int64_t n);  // tag or 0xff
+std::vector<uint8_t> utxo_erase(int64_t h, const uint8_t* recs, int64_t n);  // 1 if erased
+std::vector<uint8_t> utxo_dump(int64_t h);
+
 // ---------------------------------------------------------------- device info
 int gpu_device_count();
 std::string gpu_arch_name(int device);

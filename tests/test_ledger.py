@@ -1,0 +1,117 @@
+"""Ledger + consensus on an in-memory devnet (host backends): blocks, transfers, staking, UTXO hash."""
+import asyncio
+import hashlib
+from decimal import Decimal
+
+import pytest
+
+from upow_amd import devnet
+from upow_amd.ledger import manager
+from upow_amd.ledger.database import Database
+from upow_amd.models.transaction import Transaction
+from upow_amd.ops import p256 as op
+from upow_amd.utils.codec import point_to_string
+from upow_amd.wallet import builders
+
+
+def run(coro):
+    return asyncio.get_event_loop().run_until_complete(coro) if False else asyncio.run(coro)
+
+
+@pytest.fixture
+def chain(monkeypatch):
+    monkeypatch.setattr(manager, 'START_DIFFICULTY', Decimal('1.5'))
+    manager.Manager.difficulty = None
+    manager.cache.clear()
+
+    async def setup():
+        db = await Database.create(utxo_backend='host')
+        return db
+    db = asyncio.run(setup())
+    yield db
+    db.close()
+
+
+KEY_A = 0x1111111111111111111111111111111111111111111111111111111111111111
+KEY_B = 0x2222222222222222222222222222222222222222222222222222222222222222
+
+
+def test_mine_transfer_and_balances(chain):
+    async def go():
+        a = builders.address_of(KEY_A)
+        b = builders.address_of(KEY_B)
+        base = 1_700_000_000
+        await devnet.mine_block(a, ts=base + 1)
+        await devnet.mine_block(a, ts=base + 2)
+        assert await chain.get_next_block_id() == 3
+        bal = await chain.get_address_balance(a)
+        assert bal == Decimal(12)
+        tx = await builders.create_transaction(KEY_A, b, '2.5')
+        assert await chain.add_pending_transaction(tx)
+        # the same input cannot be spent twice in the mempool
+        tx2 = await builders.create_transaction(KEY_A, b, '1')
+        assert tx2.inputs[0].tx_hash != tx.inputs[0].tx_hash or tx2.inputs[0].index != tx.inputs[0].index
+        pend = await chain.get_pending_transactions_limit()
+        assert [t.hash() for t in pend] == [tx.hash()]
+        await devnet.mine_block(a, pend, ts=base + 3)
+        assert await chain.get_address_balance(b) == Decimal('2.5')
+        assert await chain.get_address_balance(a) == Decimal(18) - Decimal('2.5')
+        assert await chain.get_pending_transactions_limit() == []
+        # UTXO-set hash matches a recomputation from the full replay
+        outs = await chain.get_unspent_outputs_from_all_transactions()
+        h = hashlib.sha256(b''.join(bytes.fromhex(t) + bytes([i]) for t, i in sorted(outs))).hexdigest()
+        assert await chain.get_unspent_outputs_hash() == h
+        # parse round trip of every stored tx
+        for blk in await chain.get_blocks(1, 10):
+            for hx in blk['transactions']:
+                t = await Transaction.from_hex(hx)
+                assert t.hex() == hx
+        nice = await chain.get_nice_transaction(tx.hash(), address=b)
+        assert nice['delta'] == Decimal('2.5') and nice['is_confirm'] is True
+    asyncio.run(go())
+
+
+def test_double_spend_and_bad_signature_rejected(chain):
+    async def go():
+        a = builders.address_of(KEY_A)
+        b = builders.address_of(KEY_B)
+        base = 1_700_000_000
+        await devnet.mine_block(a, ts=base + 1)
+        await devnet.mine_block(a, ts=base + 2)
+        tx = await builders.create_transaction(KEY_A, b, '1')
+        # tamper the signature -> block rejected
+        bad = await Transaction.from_hex(tx.hex())
+        r, s = bad.inputs[0].signed
+        for i in bad.inputs:
+            i.signed = (r, (s + 1) % op.oracle.N)
+        bad.tx_hash = None
+        with pytest.raises(RuntimeError, match='has been not verified'):
+            await devnet.mine_block(a, [bad], ts=base + 3)
+        # the same tx twice in one block -> double spend
+        with pytest.raises(RuntimeError, match='double spend'):
+            await devnet.mine_block(a, [tx, await Transaction.from_hex(tx.hex())], ts=base + 3)
+        await devnet.mine_block(a, [tx], ts=base + 3)
+        with pytest.raises(RuntimeError, match='double spend'):
+            await devnet.mine_block(a, [await Transaction.from_hex(tx.hex())], ts=base + 4)
+    asyncio.run(go())
+
+
+def test_stake_and_validator_flow(chain):
+    async def go():
+        a = builders.address_of(KEY_A)
+        base = 1_700_000_000
+        for k in range(1, 25):
+            await devnet.mine_block(a, ts=base + k)
+        stake = await builders.create_stake_transaction(KEY_A, '10')
+        assert await chain.add_pending_transaction(stake)
+        await devnet.mine_block(a, await chain.get_pending_transactions_limit(), ts=base + 30)
+        assert await chain.get_address_stake(a) == Decimal(10)
+        assert len(await chain.get_delegates_voting_power(a)) == 1
+        val = await builders.create_validator_registration_transaction(KEY_A)
+        assert await chain.add_pending_transaction(val)
+        await devnet.mine_block(a, await chain.get_pending_transactions_limit(), ts=base + 31)
+        assert await chain.is_validator_registered(a)
+        assert len(await chain.get_validators_voting_power(a)) == 1
+        with pytest.raises(Exception, match='Already staked'):
+            await builders.create_stake_transaction(KEY_A, '5')
+    asyncio.run(go())

@@ -1,0 +1,1170 @@
+"""Embedded ledger store with the reference's query API (reference: upow/database.py:26-1654).
+
+The reference keeps everything in PostgreSQL through asyncpg. This build keeps the exact
+``schema.sql`` table/column layout (reference: schema.sql:1-84) in an embedded SQLite database
+(TEXT[]/BIGINT[] columns stored as JSON, NUMERIC stored as canonical decimal text with PostgreSQL's
+NUMERIC(p,s) rounding), so a restart resumes from the last block with no server, and keeps the UTXO
+set additionally in an in-memory / HBM hash index (:mod:`upow_amd.ledger.utxo`) that the batched
+block validator probes instead of issuing SQL per input.
+
+Method names, arguments, return shapes and ordering follow the reference one-for-one (each method
+cites its reference line range) so the consensus and node layers read the same.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sqlite3
+import threading
+from collections import defaultdict
+from datetime import datetime, timedelta, timezone
+from decimal import ROUND_HALF_UP, Decimal
+from statistics import mean
+from time import perf_counter
+from typing import Any, Dict, Iterable, List, Optional, Set, Tuple, Union
+
+from ..constants import MAX_BLOCK_SIZE_HEX, SMALLEST
+from ..models.transaction import CoinbaseTransaction, Transaction, TransactionInput
+from ..utils import codec
+from ..utils.codec import (AddressFormat, OutputType, TransactionType, normalize_block, point_to_bytes,
+                           point_to_string, round_up_decimal, sha256, string_to_point)
+from ..utils.jsonstore import JsonStore
+from ..utils.logger import get_logger
+from .utxo import TAG_BY_TABLE, UtxoIndex
+
+logger = get_logger(__name__)
+
+OUTPUT_TABLES = ('unspent_outputs', 'inode_registration_output', 'validator_registration_output',
+                 'validators_voting_power', 'delegates_voting_power', 'validators_ballot', 'inodes_ballot')
+
+SCHEMA = """
+CREATE TABLE IF NOT EXISTS blocks (
+    id INTEGER PRIMARY KEY,
+    hash TEXT UNIQUE,
+    content TEXT NOT NULL,
+    address TEXT NOT NULL,
+    random INTEGER NOT NULL,
+    difficulty TEXT NOT NULL,
+    reward TEXT NOT NULL,
+    timestamp INTEGER
+);
+CREATE TABLE IF NOT EXISTS transactions (
+    block_hash TEXT NOT NULL REFERENCES blocks(hash) ON DELETE CASCADE,
+    tx_hash TEXT UNIQUE,
+    tx_hex TEXT,
+    inputs_addresses TEXT,
+    outputs_addresses TEXT,
+    outputs_amounts TEXT,
+    fees TEXT NOT NULL
+);
+CREATE TABLE IF NOT EXISTS unspent_outputs (
+    tx_hash TEXT REFERENCES transactions(tx_hash) ON DELETE CASCADE,
+    "index" INTEGER NOT NULL,
+    address TEXT NULL,
+    is_stake INTEGER
+);
+CREATE TABLE IF NOT EXISTS pending_transactions (
+    tx_hash TEXT UNIQUE,
+    tx_hex TEXT,
+    inputs_addresses TEXT,
+    fees TEXT NOT NULL,
+    propagation_time INTEGER NOT NULL
+);
+CREATE TABLE IF NOT EXISTS pending_spent_outputs (
+    tx_hash TEXT REFERENCES transactions(tx_hash) ON DELETE CASCADE,
+    "index" INTEGER NOT NULL
+);
+CREATE TABLE IF NOT EXISTS address_transactions (
+    address TEXT NOT NULL,
+    tx_hash TEXT NOT NULL REFERENCES transactions(tx_hash) ON DELETE CASCADE
+);
+"""
+for _t in OUTPUT_TABLES[1:]:
+    SCHEMA += f"""
+CREATE TABLE IF NOT EXISTS {_t} (
+    tx_hash TEXT REFERENCES transactions(tx_hash) ON DELETE CASCADE,
+    "index" INTEGER NOT NULL,
+    address TEXT NULL
+);"""
+SCHEMA += """
+CREATE INDEX IF NOT EXISTS tx_hash_idx ON unspent_outputs (tx_hash);
+CREATE INDEX IF NOT EXISTS block_hash_idx ON transactions (block_hash);
+CREATE INDEX IF NOT EXISTS unspent_outpoint_idx ON unspent_outputs (tx_hash, "index");
+CREATE INDEX IF NOT EXISTS unspent_address_idx ON unspent_outputs (address);
+CREATE INDEX IF NOT EXISTS pending_spent_idx ON pending_spent_outputs (tx_hash, "index");
+CREATE INDEX IF NOT EXISTS address_transactions_idx ON address_transactions (address);
+CREATE INDEX IF NOT EXISTS address_transactions_tx_idx ON address_transactions (tx_hash);
+"""
+for _t in OUTPUT_TABLES[1:]:
+    SCHEMA += f'CREATE INDEX IF NOT EXISTS {_t}_outpoint_idx ON {_t} (tx_hash, "index");\n'
+    SCHEMA += f'CREATE INDEX IF NOT EXISTS {_t}_address_idx ON {_t} (address);\n'
+
+
+def numeric(value, scale: int) -> str:
+    """PostgreSQL NUMERIC(p, scale) storage: round half away from zero to ``scale`` digits."""
+    q = Decimal(1).scaleb(-scale)
+    return str(Decimal(value).quantize(q, rounding=ROUND_HALF_UP))
+
+
+def _utcnow() -> datetime:
+    return datetime.now(timezone.utc).replace(tzinfo=None)
+
+
+def _dt(ts: int) -> datetime:
+    return datetime.fromtimestamp(int(ts), timezone.utc).replace(tzinfo=None)
+
+
+def _j(x) -> str:
+    return json.dumps(x, separators=(',', ':'))
+
+
+def _arr(s) -> list:
+    return json.loads(s) if s else []
+
+
+def _at(arr: list, index: int):
+    """PostgreSQL 1-based array subscript semantics for ``arr[index + 1]`` (NULL when out of range)."""
+    return arr[index] if 0 <= index < len(arr) else None
+
+
+class Database:
+    """SQLite-backed ledger. ``Database.instance`` is the process singleton (as in the reference)."""
+    instance: 'Database' = None
+    credentials: dict = {}
+    is_indexed = True
+
+    def __init__(self, path: str = ':memory:', utxo_backend: Optional[str] = None):
+        self.path = path
+        self.conn = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
+        self.conn.row_factory = sqlite3.Row
+        self.lock = threading.RLock()
+        self.conn.execute('PRAGMA foreign_keys = ON')
+        if path != ':memory:':
+            self.conn.execute('PRAGMA journal_mode = WAL')
+            self.conn.execute('PRAGMA synchronous = NORMAL')
+        self.conn.executescript(SCHEMA)
+        store_dir = os.path.dirname(path) if path != ':memory:' else None
+        self.emission_details = JsonStore(os.path.join(store_dir, 'emission_details.json') if store_dir else None)
+        self.utxo = UtxoIndex(backend=utxo_backend)
+        self._rebuild_utxo_index()
+
+    # ------------------------------------------------------------------ lifecycle
+    @staticmethod
+    async def create(path: Optional[str] = None, ignore: bool = False, utxo_backend: Optional[str] = None,
+                     **_ignored) -> 'Database':
+        """reference: database.py:34-85 (asyncpg pool + migrations) -> embedded store + UTXO index."""
+        path = path or os.environ.get('UPOW_DATABASE_PATH') or ':memory:'
+        if path != ':memory:':
+            os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        self = Database(path, utxo_backend=utxo_backend)
+        Database.instance = self
+        return self
+
+    @staticmethod
+    async def get() -> 'Database':
+        if Database.instance is None:
+            await Database.create(**Database.credentials)
+        return Database.instance
+
+    def close(self):
+        with self.lock:
+            self.conn.close()
+
+    # ------------------------------------------------------------------ SQL helpers
+    def _q(self, sql: str, args: Iterable = ()) -> List[sqlite3.Row]:
+        with self.lock:
+            return self.conn.execute(sql, tuple(args)).fetchall()
+
+    def _q1(self, sql: str, args: Iterable = ()):
+        with self.lock:
+            return self.conn.execute(sql, tuple(args)).fetchone()
+
+    def _x(self, sql: str, args: Iterable = ()):
+        with self.lock:
+            return self.conn.execute(sql, tuple(args))
+
+    def _xm(self, sql: str, rows: Iterable):
+        with self.lock:
+            self.conn.executemany(sql, rows)
+
+    class _Tx:
+        def __init__(self, db):
+            self.db = db
+
+        def __enter__(self):
+            self.db.lock.acquire()
+            self.db.conn.execute('BEGIN')
+            return self.db
+
+        def __exit__(self, et, ev, tb):
+            try:
+                self.db.conn.execute('COMMIT' if et is None else 'ROLLBACK')
+            finally:
+                self.db.lock.release()
+            return False
+
+    def transaction(self):
+        return Database._Tx(self)
+
+    def _rebuild_utxo_index(self):
+        keys, tags = [], []
+        for table in OUTPUT_TABLES:
+            tag = TAG_BY_TABLE[table]
+            for r in self._q(f'SELECT tx_hash, "index" FROM {table}'):
+                keys.append((r[0], r[1]))
+                tags.append(tag)
+        self.utxo.reset(keys, tags)
+
+    def _select_outpoints(self, table: str, outputs: List[Tuple[str, int]]) -> List[Tuple[str, int]]:
+        """``SELECT tx_hash, index FROM <table> WHERE (tx_hash, index) = ANY($1)`` (rows in table order)."""
+        if not outputs:
+            return []
+        want = {(str(h), int(i)) for h, i in outputs}
+        hashes = sorted({h for h, _ in want})
+        out = []
+        for k in range(0, len(hashes), 500):
+            chunk = hashes[k:k + 500]
+            ph = ','.join('?' * len(chunk))
+            for r in self._q(f'SELECT rowid, tx_hash, "index" FROM {table} WHERE tx_hash IN ({ph})', chunk):
+                if (r[1], r[2]) in want:
+                    out.append((r[0], (r[1], r[2])))
+        out.sort()
+        return [o for _, o in out]
+
+    def _delete_outpoints(self, table: str, inputs: List[Tuple[str, int]]) -> int:
+        n = 0
+        with self.lock:
+            for h, i in inputs:
+                n += self.conn.execute(f'DELETE FROM {table} WHERE tx_hash = ? AND "index" = ?', (h, int(i))).rowcount
+        return n
+
+    def _pending_spent_set(self) -> Set[Tuple[str, int]]:
+        return {(r[0], r[1]) for r in self._q('SELECT tx_hash, "index" FROM pending_spent_outputs')}
+
+    # ------------------------------------------------------------------ mempool (database.py:93-231)
+    async def add_pending_transaction(self, transaction: Transaction, verify: bool = True) -> bool:
+        logger.info('Adding in pending transaction')
+        if isinstance(transaction, CoinbaseTransaction):
+            logger.error('CoinbaseTransaction in add_pending_transaction')
+            return False
+        tx_hex = transaction.hex()
+        if verify and not await transaction.verify_pending():
+            logger.error('Error in adding transaction.')
+            return False
+        inputs_addresses = [point_to_string(await i.get_public_key()) for i in transaction.inputs]
+        try:
+            self._x('INSERT INTO pending_transactions (tx_hash, tx_hex, inputs_addresses, fees, propagation_time) '
+                    'VALUES (?, ?, ?, ?, ?)',
+                    (sha256(tx_hex), tx_hex, _j(inputs_addresses), numeric(transaction.fees, 6),
+                     int(_utcnow().replace(tzinfo=timezone.utc).timestamp())))
+        except sqlite3.IntegrityError as e:
+            raise UniqueViolationError(str(e)) from e
+        await self.add_transactions_pending_spent_outputs([transaction])
+        return True
+
+    async def remove_pending_transaction(self, tx_hash: str):
+        self._x('DELETE FROM pending_transactions WHERE tx_hash = ?', (tx_hash,))
+
+    async def remove_pending_transactions_by_hash(self, tx_hashes: List[str]):
+        with self.lock:
+            self.conn.executemany('DELETE FROM pending_transactions WHERE tx_hash = ?', [(h,) for h in tx_hashes])
+
+    async def remove_pending_transactions(self):
+        with self.transaction():
+            deleted = [r[0] for r in self.conn.execute('SELECT tx_hash FROM pending_transactions').fetchall()]
+            self.conn.execute('DELETE FROM pending_transactions')
+            self.conn.execute('DELETE FROM pending_spent_outputs')
+        if deleted:
+            logger.info(f'remove_pending_transactions: removed {len(deleted)} transactions: {deleted}')
+        else:
+            logger.info('remove_pending_transactions: no transactions to remove')
+
+    async def delete_blockchain(self):
+        with self.transaction():
+            self.conn.execute('DELETE FROM transactions')
+            self.conn.execute('DELETE FROM blocks')
+        self._rebuild_utxo_index()
+
+    async def delete_block(self, id: int):
+        self._x('DELETE FROM blocks WHERE id = ?', (id,))
+        self._rebuild_utxo_index()
+
+    async def delete_blocks(self, offset: int):
+        self._x('DELETE FROM blocks WHERE id > ?', (offset,))
+        self._rebuild_utxo_index()
+
+    async def remove_blocks(self, block_no: int):
+        """database.py:146-169: roll back blocks >= block_no and restore the outputs they spent."""
+        blocks_to_remove = await self.get_blocks(block_no, 500)
+        transactions_to_remove, transactions_hashes = [], []
+        for b in blocks_to_remove:
+            transactions_to_remove.extend([await Transaction.from_hex(tx, False) for tx in b['transactions']])
+            transactions_hashes.extend([sha256(tx) for tx in b['transactions']])
+        hashes = set(transactions_hashes)
+        outputs_to_be_restored = []
+        for tx in transactions_to_remove:
+            if isinstance(tx, Transaction):
+                outputs_to_be_restored.extend([(i.tx_hash, i.index) for i in tx.inputs if i.tx_hash not in hashes])
+        self._x('DELETE FROM blocks WHERE id >= ?', (block_no,))
+        await self.add_unspent_outputs(outputs_to_be_restored)
+        self._rebuild_utxo_index()
+
+    def _pending_rows_ordered(self):
+        """``ORDER BY fees / LENGTH(tx_hex) DESC, LENGTH(tx_hex), tx_hex`` (database.py:173-174)."""
+        rows = self._q('SELECT tx_hash, tx_hex, fees, propagation_time FROM pending_transactions')
+        return sorted(rows, key=lambda r: (-(Decimal(r['fees']) / len(r['tx_hex'])), len(r['tx_hex']), r['tx_hex']))
+
+    async def get_pending_transactions_limit(self, limit: int = MAX_BLOCK_SIZE_HEX, hex_only: bool = False,
+                                             check_signatures: bool = True) -> List[Union[Transaction, str]]:
+        return_txs, size = [], 0
+        for r in self._pending_rows_ordered():
+            tx = r['tx_hex']
+            if size + len(tx) > limit:
+                break
+            return_txs.append(tx)
+            size += len(tx)
+        if hex_only:
+            return return_txs
+        return [await Transaction.from_hex(t, check_signatures) for t in return_txs]
+
+    async def get_need_propagate_transactions(self, last_propagation_delta: int = 600,
+                                              limit: int = MAX_BLOCK_SIZE_HEX) -> List[str]:
+        now = int(_utcnow().replace(tzinfo=timezone.utc).timestamp())
+        return_txs, size = [], 0
+        for r in self._pending_rows_ordered():
+            tx_hex = r['tx_hex']
+            if size + len(tx_hex) > limit:
+                break
+            size += len(tx_hex)
+            if now - r['propagation_time'] > last_propagation_delta:
+                return_txs.append(tx_hex)
+        return return_txs
+
+    async def update_pending_transactions_propagation_time(self, txs_hash: List[str]):
+        now = int(_utcnow().replace(tzinfo=timezone.utc).timestamp())
+        with self.lock:
+            self.conn.executemany('UPDATE pending_transactions SET propagation_time = ? WHERE tx_hash = ?',
+                                  [(now, h) for h in txs_hash])
+
+    async def get_next_block_average_fee(self):
+        rows = sorted(self._q('SELECT LENGTH(tx_hex) AS size, fees FROM pending_transactions'),
+                      key=lambda r: (-(Decimal(r['fees']) / r['size']), r['size']))
+        fees, size = [], 0
+        for r in rows:
+            if size + r['size'] > MAX_BLOCK_SIZE_HEX:
+                break
+            fees.append(Decimal(r['fees']))
+            size += r['size']
+        return int(mean(fees) * SMALLEST) // Decimal(SMALLEST)
+
+    async def get_pending_blocks_count(self):
+        rows = self._q('SELECT LENGTH(tx_hex) AS size FROM pending_transactions')
+        return int(sum(r['size'] for r in rows) / MAX_BLOCK_SIZE_HEX + 1)
+
+    async def clear_duplicate_pending_transactions(self):
+        self._x('DELETE FROM pending_transactions WHERE tx_hash IN (SELECT tx_hash FROM transactions)')
+
+    # ------------------------------------------------------------------ blocks / txs (database.py:233-437)
+    async def add_transaction(self, transaction, block_hash: str):
+        await self.add_transactions([transaction], block_hash)
+
+    async def _tx_row(self, transaction, block_hash):
+        if isinstance(transaction, Transaction):
+            inputs_addresses = [point_to_string(await i.get_public_key()) for i in transaction.inputs]
+        else:
+            inputs_addresses = []
+        return (block_hash, transaction.hash(), transaction.hex(), _j(inputs_addresses),
+                _j([o.address for o in transaction.outputs]),
+                _j([int(o.amount * SMALLEST) for o in transaction.outputs]),
+                numeric(transaction.fees if isinstance(transaction, Transaction) else 0, 6))
+
+    async def add_transactions(self, transactions, block_hash: str):
+        rows = [await self._tx_row(t, block_hash) for t in transactions]
+        self.insert_transaction_rows(rows)
+
+    def insert_transaction_rows(self, rows: List[tuple]):
+        addr_rows = []
+        for r in rows:
+            tx_hash = r[1]
+            addrs = set(_arr(r[3])) | set(_arr(r[4]))
+            addr_rows.extend((a, tx_hash) for a in addrs)
+        try:
+            with self.transaction():
+                self.conn.executemany('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, '
+                                      'outputs_addresses, outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)', rows)
+                self.conn.executemany('INSERT INTO address_transactions (address, tx_hash) VALUES (?, ?)', addr_rows)
+        except sqlite3.IntegrityError as e:
+            raise UniqueViolationError(str(e)) from e
+
+    async def add_block(self, id: int, block_hash: str, block_content: str, address: str, random: int,
+                        difficulty: Decimal, reward: Decimal, timestamp: Union[datetime, int]):
+        if isinstance(timestamp, datetime):
+            timestamp = int(timestamp.replace(tzinfo=timezone.utc).timestamp())
+        try:
+            self._x('INSERT INTO blocks (id, hash, content, address, random, difficulty, reward, timestamp) '
+                    'VALUES (?, ?, ?, ?, ?, ?, ?, ?)',
+                    (id, block_hash, block_content, address, int(random), numeric(difficulty, 1),
+                     numeric(reward, 6), int(timestamp)))
+        except sqlite3.IntegrityError as e:
+            raise UniqueViolationError(str(e)) from e
+        from .manager import Manager
+        Manager.difficulty = None
+
+    @staticmethod
+    def _block_row(row) -> Optional[dict]:
+        if row is None:
+            return None
+        d = dict(row)
+        d['difficulty'] = Decimal(d['difficulty'])
+        d['reward'] = Decimal(d['reward'])
+        return normalize_block(d)
+
+    async def get_transaction(self, tx_hash: str, check_signatures: bool = True):
+        res = self._q1('SELECT tx_hex, block_hash FROM transactions WHERE tx_hash = ?', (tx_hash,))
+        if res is None:
+            return None
+        tx = await Transaction.from_hex(res['tx_hex'], check_signatures)
+        tx.block_hash = res['block_hash']
+        return tx
+
+    @staticmethod
+    def _info_row(row) -> dict:
+        d = dict(row)
+        d['inputs_addresses'] = _arr(d['inputs_addresses'])
+        d['outputs_addresses'] = _arr(d['outputs_addresses'])
+        d['outputs_amounts'] = _arr(d['outputs_amounts'])
+        d['fees'] = Decimal(d['fees'])
+        return d
+
+    async def get_transaction_info(self, tx_hash: str) -> Optional[dict]:
+        res = self._q1('SELECT * FROM transactions WHERE tx_hash = ?', (tx_hash,))
+        return self._info_row(res) if res is not None else None
+
+    async def get_transactions_info(self, tx_hashes: List[str]) -> Dict[str, dict]:
+        out = {}
+        hashes = list(dict.fromkeys(tx_hashes))
+        for k in range(0, len(hashes), 500):
+            chunk = hashes[k:k + 500]
+            for r in self._q(f'SELECT * FROM transactions WHERE tx_hash IN ({",".join("?" * len(chunk))})', chunk):
+                out[r['tx_hash']] = self._info_row(r)
+        return out
+
+    async def get_pending_transaction(self, tx_hash: str, check_signatures: bool = True):
+        res = self._q1('SELECT tx_hex FROM pending_transactions WHERE tx_hash = ?', (tx_hash,))
+        return await Transaction.from_hex(res['tx_hex'], check_signatures) if res is not None else None
+
+    async def get_pending_transactions_by_hash(self, hashes: List[str], check_signatures: bool = True):
+        if not hashes:
+            return []
+        want = set(hashes)
+        rows = [r for r in self._q('SELECT tx_hash, tx_hex FROM pending_transactions') if r['tx_hash'] in want]
+        return [await Transaction.from_hex(r['tx_hex'], check_signatures) for r in rows]
+
+    async def get_transactions(self, tx_hashes: List[str]):
+        infos = await self.get_transactions_info(tx_hashes)
+        return {sha256(i['tx_hex']): await Transaction.from_hex(i['tx_hex']) for i in infos.values()}
+
+    async def get_transaction_hash_by_contains_multi(self, contains: List[str], ignore: str = None):
+        for r in self._q('SELECT tx_hash, tx_hex FROM transactions'):
+            if ignore is not None and r['tx_hash'] == ignore:
+                continue
+            if any(c in r['tx_hex'] for c in contains):
+                return r['tx_hash']
+        return None
+
+    async def get_pending_transactions_by_contains(self, contains: str):
+        rows = self._q('SELECT tx_hash, tx_hex FROM pending_transactions')
+        return [await Transaction.from_hex(r['tx_hex']) for r in rows
+                if contains in r['tx_hex'] and r['tx_hash'] != contains]
+
+    async def remove_pending_transactions_by_contains(self, search: List[str]) -> None:
+        with self.transaction():
+            rows = self.conn.execute('SELECT tx_hash, tx_hex FROM pending_transactions').fetchall()
+            deleted = [r['tx_hash'] for r in rows if any(c in r['tx_hex'] for c in search)]
+            self.conn.executemany('DELETE FROM pending_transactions WHERE tx_hash = ?', [(h,) for h in deleted])
+        if deleted:
+            logger.info(f'remove_pending_transactions_by_contains: removed {len(deleted)} transactions '
+                        f'deleted_tx_hashes: {deleted}')
+        else:
+            logger.info(f'remove_pending_transactions_by_contains: no transactions matched patterns {search}')
+
+    async def get_pending_transaction_by_contains_multi(self, contains: List[str], ignore: str = None):
+        for r in self._q('SELECT tx_hash, tx_hex FROM pending_transactions'):
+            if ignore is not None and r['tx_hash'] == ignore:
+                continue
+            if any(c in r['tx_hex'] for c in contains):
+                return await Transaction.from_hex(r['tx_hex'])
+        return None
+
+    async def get_last_block(self) -> Optional[dict]:
+        return self._block_row(self._q1('SELECT * FROM blocks ORDER BY id DESC LIMIT 1'))
+
+    async def get_next_block_id(self) -> int:
+        r = self._q1('SELECT id FROM blocks ORDER BY id DESC LIMIT 1')
+        return (r[0] if r is not None else 0) + 1
+
+    async def get_block(self, block_hash: str) -> Optional[dict]:
+        return self._block_row(self._q1('SELECT * FROM blocks WHERE hash = ?', (block_hash,)))
+
+    async def get_blocks(self, offset: int, limit: int, tx_details: bool = False) -> list:
+        blocks = self._q('SELECT * FROM blocks WHERE id >= ? ORDER BY id LIMIT ?', (offset, limit))
+        index = {b['hash']: [] for b in blocks}
+        index_tx_hash = {b['hash']: [] for b in blocks}
+        if blocks:
+            for t in self._q('SELECT transactions.tx_hex, transactions.tx_hash, transactions.block_hash FROM '
+                             'transactions INNER JOIN blocks ON blocks.hash = transactions.block_hash '
+                             'WHERE blocks.id >= ? AND blocks.id <= ? ORDER BY transactions.rowid',
+                             (blocks[0]['id'], blocks[-1]['id'])):
+                if t['block_hash'] in index:
+                    index[t['block_hash']].append(t['tx_hex'])
+                    index_tx_hash[t['block_hash']].append(t['tx_hash'])
+        result, size = [], 0
+        for b in blocks:
+            block = self._block_row(b)
+            txs = index[block['hash']]
+            size += sum(len(tx) for tx in txs)
+            if size > MAX_BLOCK_SIZE_HEX * 8:
+                break
+            result.append({'block': block,
+                           'transactions': txs if not tx_details else
+                           [await self.get_nice_transaction(h) for h in index_tx_hash[block['hash']]]})
+        return result
+
+    async def get_block_by_id(self, block_id: int) -> Optional[dict]:
+        return self._block_row(self._q1('SELECT * FROM blocks WHERE id = ?', (block_id,)))
+
+    async def get_block_transactions(self, block_hash: str, check_signatures: bool = True, hex_only: bool = False):
+        rows = self._q('SELECT tx_hex FROM transactions WHERE block_hash = ? ORDER BY rowid', (block_hash,))
+        return [r['tx_hex'] if hex_only else await Transaction.from_hex(r['tx_hex'], check_signatures) for r in rows]
+
+    async def get_block_transactions_hashes(self, block_hash: str) -> List[str]:
+        return [r[0] for r in self._q('SELECT tx_hash FROM transactions WHERE block_hash = ? ORDER BY rowid',
+                                      (block_hash,))]
+
+    async def get_block_transaction_hashes(self, block_hash: str) -> List[str]:
+        """Hashes of the block's non-coinbase txs (the coinbase hex contains the block hash)."""
+        rows = self._q('SELECT tx_hash, tx_hex FROM transactions WHERE block_hash = ? ORDER BY rowid', (block_hash,))
+        return [r['tx_hash'] for r in rows if block_hash not in r['tx_hex']]
+
+    async def get_block_nice_transactions(self, block_hash: str) -> List[dict]:
+        rows = self._q('SELECT tx_hash, inputs_addresses FROM transactions WHERE block_hash = ? ORDER BY rowid',
+                       (block_hash,))
+        return [{'hash': r['tx_hash'], 'is_coinbase': not _arr(r['inputs_addresses'])} for r in rows]
+
+    # ------------------------------------------------------------------ outputs (database.py:439-580)
+    async def add_unspent_outputs(self, outputs: List[tuple]) -> None:
+        if not outputs:
+            return
+        if len(outputs[0]) == 2:
+            # restored outpoints: address is re-derived from the creating tx (database.py:500-505)
+            rows = []
+            infos = await self.get_transactions_info([h for h, _ in outputs])
+            for h, i in outputs:
+                info = infos.get(h)
+                addr = _at(info['outputs_addresses'], i) if info else None
+                rows.append((h, i, addr, None))
+        else:
+            rows = [(h, i, a, None if s is None else int(bool(s))) for h, i, a, s in outputs]
+        with self.lock:
+            self.conn.executemany('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) '
+                                  'VALUES (?, ?, ?, ?)', rows)
+        self.utxo.insert([(r[0], r[1]) for r in rows], TAG_BY_TABLE['unspent_outputs'])
+
+    async def _add_gov_outputs(self, table: str, outputs: List[tuple]):
+        if not outputs:
+            return
+        rows = [(o[0], o[1], o[2] if len(o) > 2 else None) for o in outputs]
+        with self.lock:
+            self.conn.executemany(f'INSERT INTO {table} (tx_hash, "index", address) VALUES (?, ?, ?)', rows)
+        self.utxo.insert([(r[0], r[1]) for r in rows], TAG_BY_TABLE[table])
+
+    async def add_inode_registration_outputs(self, outputs):
+        await self._add_gov_outputs('inode_registration_output', outputs)
+
+    async def add_validator_registration_outputs(self, outputs):
+        await self._add_gov_outputs('validator_registration_output', outputs)
+
+    async def add_validator_voting_power(self, outputs):
+        await self._add_gov_outputs('validators_voting_power', outputs)
+
+    async def add_delegates_voting_power(self, outputs):
+        await self._add_gov_outputs('delegates_voting_power', outputs)
+
+    async def add_vote_to_inode_ballots(self, outputs):
+        await self._add_gov_outputs('inodes_ballot', outputs)
+
+    async def add_vote_to_validators_ballot(self, outputs):
+        await self._add_gov_outputs('validators_ballot', outputs)
+
+    async def add_pending_spent_outputs(self, outputs: List[Tuple[str, int]]) -> None:
+        with self.lock:
+            self.conn.executemany('INSERT INTO pending_spent_outputs (tx_hash, "index") VALUES (?, ?)', outputs)
+
+    async def add_transactions_pending_spent_outputs(self, transactions: List[Transaction]) -> None:
+        outputs = [(i.tx_hash, i.index) for t in transactions for i in t.inputs]
+        try:
+            with self.lock:
+                self.conn.executemany('INSERT INTO pending_spent_outputs (tx_hash, "index") VALUES (?, ?)', outputs)
+        except sqlite3.IntegrityError as e:  # FK: spent output must belong to a confirmed tx
+            raise ForeignKeyViolationError(str(e)) from e
+
+    @staticmethod
+    def split_outputs(transactions) -> Dict[str, list]:
+        """Bucket every output into its table (database.py:524-580)."""
+        b = {t: [] for t in OUTPUT_TABLES}
+        for tx in transactions:
+            h = tx.hash()
+            for index, o in enumerate(tx.outputs):
+                t = o.transaction_type
+                if t in (OutputType.REGULAR, OutputType.STAKE, OutputType.UN_STAKE):
+                    b['unspent_outputs'].append((h, index, o.address, o.is_stake))
+                elif t == OutputType.INODE_REGISTRATION:
+                    b['inode_registration_output'].append((h, index, o.address))
+                elif t == OutputType.VALIDATOR_REGISTRATION:
+                    b['validator_registration_output'].append((h, index, o.address))
+                elif t == OutputType.VALIDATOR_VOTING_POWER:
+                    b['validators_voting_power'].append((h, index, o.address))
+                elif t == OutputType.DELEGATE_VOTING_POWER:
+                    b['delegates_voting_power'].append((h, index, o.address))
+                elif t == OutputType.VOTE_AS_VALIDATOR:
+                    b['inodes_ballot'].append((h, index, o.address))
+                elif t == OutputType.VOTE_AS_DELEGATE:
+                    b['validators_ballot'].append((h, index, o.address))
+        return b
+
+    async def add_transaction_outputs(self, transactions):
+        b = self.split_outputs(transactions)
+        await self.add_unspent_outputs(b['unspent_outputs'])
+        await self.add_inode_registration_outputs(b['inode_registration_output'])
+        await self.add_validator_voting_power(b['validators_voting_power'])
+        await self.add_delegates_voting_power(b['delegates_voting_power'])
+        await self.add_validator_registration_outputs(b['validator_registration_output'])
+        await self.add_vote_to_inode_ballots(b['inodes_ballot'])
+        await self.add_vote_to_validators_ballot(b['validators_ballot'])
+
+    async def add_unspent_transactions_outputs(self, transactions) -> None:
+        await self.add_unspent_outputs([(t.hash(), i, o.address, o.is_stake)
+                                        for t in transactions for i, o in enumerate(t.outputs)])
+
+    @staticmethod
+    def spend_table(tx_type) -> str:
+        """Which table a tx type spends from (database.py:589-621)."""
+        return {TransactionType.INODE_DE_REGISTRATION: 'inode_registration_output',
+                TransactionType.VOTE_AS_VALIDATOR: 'validators_voting_power',
+                TransactionType.VOTE_AS_DELEGATE: 'delegates_voting_power',
+                TransactionType.REVOKE_AS_VALIDATOR: 'inodes_ballot',
+                TransactionType.REVOKE_AS_DELEGATE: 'validators_ballot'}.get(tx_type, 'unspent_outputs')
+
+    async def remove_outputs(self, transactions):
+        by_table = defaultdict(list)
+        for t in transactions:
+            by_table[self.spend_table(t.transaction_type)].append(t)
+        for table in ('inode_registration_output', 'unspent_outputs', 'validators_voting_power',
+                      'delegates_voting_power', 'inodes_ballot', 'validators_ballot'):
+            if by_table[table]:
+                if table == 'unspent_outputs':
+                    await self.remove_unspent_outputs(by_table[table])
+                else:
+                    self._remove_table_inputs(table, by_table[table])
+
+    def _remove_table_inputs(self, table, transactions):
+        inputs = [(i.tx_hash, i.index) for t in transactions for i in t.inputs]
+        self._delete_outpoints(table, inputs)
+        self.utxo.erase(inputs)
+
+    async def remove_unspent_outputs(self, transactions, max_retries: int = 3) -> bool:
+        """database.py:589-621: all-or-nothing delete, checks the deleted count."""
+        start = perf_counter()
+        inputs = [(i.tx_hash, i.index) for t in transactions for i in t.inputs]
+        if not inputs:
+            return True
+        try:
+            with self.transaction():
+                n = 0
+                for h, i in inputs:
+                    n += self.conn.execute('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
+                                           (h, int(i))).rowcount
+                if n != len(inputs):
+                    logger.error(f'Failed to delete all UTXOs: {n} of {len(inputs)} deleted')
+                    raise _Rollback()
+        except _Rollback:
+            return False
+        self.utxo.erase(inputs)
+        logger.info(f'Successfully removed {len(inputs)} unspent outputs in {perf_counter() - start:.3f} seconds')
+        return True
+
+    async def remove_inode_registration_output(self, transactions):
+        self._remove_table_inputs('inode_registration_output', transactions)
+
+    async def remove_validators_voting_power(self, transactions):
+        self._remove_table_inputs('validators_voting_power', transactions)
+
+    async def remove_delegates_voting_power(self, transactions):
+        self._remove_table_inputs('delegates_voting_power', transactions)
+
+    async def remove_inode_ballot_votes(self, transactions):
+        self._remove_table_inputs('inodes_ballot', transactions)
+
+    async def remove_validator_ballot_votes(self, transactions):
+        self._remove_table_inputs('validators_ballot', transactions)
+
+    async def remove_pending_spent_outputs(self, transactions) -> None:
+        self._delete_outpoints('pending_spent_outputs', [(i.tx_hash, i.index) for t in transactions for i in t.inputs])
+
+    async def remove_pending_spent_outputs_by_tuple(self, inputs: List[Tuple[str, int]], max_retries: int = 3) -> bool:
+        if not inputs:
+            return True
+        start = perf_counter()
+        try:
+            with self.transaction():
+                n = 0
+                for h, i in inputs:
+                    n += self.conn.execute('DELETE FROM pending_spent_outputs WHERE tx_hash = ? AND "index" = ?',
+                                           (h, int(i))).rowcount
+                if n != len(inputs):
+                    logger.error(f'Failed to delete all pending_spent_outputs: {n} of {len(inputs)} deleted')
+                    raise _Rollback()
+        except _Rollback:
+            return False
+        logger.info(f'Successfully removed {len(inputs)} pending_spent_outputs in {perf_counter() - start:.3f} seconds')
+        return True
+
+    # lookups (database.py:788-825); the HBM/host index answers these without SQL
+    async def get_unspent_outputs(self, outputs):
+        return self.utxo.filter(outputs, TAG_BY_TABLE['unspent_outputs'])
+
+    async def get_inode_outputs(self, outputs):
+        return self.utxo.filter(outputs, TAG_BY_TABLE['inode_registration_output'])
+
+    async def get_validator_voting_power_outputs(self, outputs):
+        return self.utxo.filter(outputs, TAG_BY_TABLE['validators_voting_power'])
+
+    async def get_delegates_voting_power_outputs(self, outputs):
+        return self.utxo.filter(outputs, TAG_BY_TABLE['delegates_voting_power'])
+
+    async def get_inodes_ballot_outputs(self, outputs):
+        return self.utxo.filter(outputs, TAG_BY_TABLE['inodes_ballot'])
+
+    async def get_validators_ballot_outputs(self, outputs):
+        return self.utxo.filter(outputs, TAG_BY_TABLE['validators_ballot'])
+
+    async def get_unspent_outputs_hash(self) -> str:
+        """database.py:827-830: SHA256 over (tx_hash bytes || index byte) sorted by (tx_hash, index)."""
+        rows = self._q('SELECT tx_hash, "index" FROM unspent_outputs ORDER BY tx_hash, "index"')
+        return sha256(''.join(r[0] + bytes([r[1]]).hex() for r in rows))
+
+    async def get_pending_spent_outputs(self, outputs):
+        return self._select_outpoints('pending_spent_outputs', outputs)
+
+    async def set_unspent_outputs_addresses(self):
+        rows = self._q('SELECT rowid, tx_hash, "index" FROM unspent_outputs WHERE address IS NULL')
+        infos = await self.get_transactions_info([r['tx_hash'] for r in rows])
+        with self.lock:
+            self.conn.executemany('UPDATE unspent_outputs SET address = ? WHERE rowid = ?',
+                                  [(_at(infos[r['tx_hash']]['outputs_addresses'], r['index'])
+                                    if r['tx_hash'] in infos else None, r['rowid']) for r in rows])
+
+    async def get_unspent_outputs_from_all_transactions(self):
+        """database.py:846-862: replay every tx in block order (UTXO rebuild tool)."""
+        outputs = set()
+        rows = self._q('SELECT tx_hex, blocks.id AS block_no FROM transactions INNER JOIN blocks ON '
+                       '(transactions.block_hash = blocks.hash) ORDER BY blocks.id ASC, transactions.rowid ASC')
+        last_block_no = 0
+        for r in rows:
+            if r['block_no'] != last_block_no:
+                last_block_no = r['block_no']
+            tx_hash = sha256(r['tx_hex'])
+            tx = await Transaction.from_hex(r['tx_hex'], check_signatures=False)
+            if isinstance(tx, Transaction):
+                outputs = outputs.difference({(i.tx_hash, i.index) for i in tx.inputs})
+            outputs.update({(tx_hash, index) for index in range(len(tx.outputs))})
+        return list(outputs)
+
+    # ------------------------------------------------------------------ address queries
+    @staticmethod
+    def _forms(address: str) -> List[str]:
+        return codec.address_forms(address)
+
+    @staticmethod
+    def _search(address: str) -> List[str]:
+        return codec.address_search_hex(address)
+
+    def _pending_matching(self, address: str, include_inputs: bool = True) -> List[sqlite3.Row]:
+        search, forms = self._search(address), set(self._forms(address))
+        out = []
+        for r in self._q('SELECT tx_hash, tx_hex, inputs_addresses FROM pending_transactions ORDER BY rowid'):
+            if any(s in r['tx_hex'] for s in search) or (include_inputs and forms & set(_arr(r['inputs_addresses']))):
+                out.append(r)
+        return out
+
+    async def get_address_transactions(self, address: str, check_pending_txs: bool = False,
+                                       check_signatures: bool = False, limit: int = 50, offset: int = 0):
+        forms = self._forms(address)
+        ph = ','.join('?' * len(forms))
+        rows = self._q(f'SELECT DISTINCT transactions.tx_hex, blocks.id AS block_no, transactions.rowid AS rid '
+                       f'FROM address_transactions INNER JOIN transactions ON '
+                       f'(address_transactions.tx_hash = transactions.tx_hash) INNER JOIN blocks ON '
+                       f'(transactions.block_hash = blocks.hash) WHERE address_transactions.address IN ({ph}) '
+                       f'ORDER BY block_no DESC, rid LIMIT ? OFFSET ?', (*forms, limit, offset))
+        txs = [r['tx_hex'] for r in rows]
+        if check_pending_txs:
+            txs = [r['tx_hex'] for r in self._pending_matching(address)] + txs
+        return [await Transaction.from_hex(t, check_signatures) for t in txs]
+
+    async def get_address_pending_transactions(self, address: str, check_signatures: bool = False):
+        return [await Transaction.from_hex(r['tx_hex'], check_signatures) for r in self._pending_matching(address)]
+
+    async def get_address_pending_spent_outputs(self, address: str, check_signatures: bool = False):
+        txs = [await Transaction.from_hex(r['tx_hex'], check_signatures) for r in self._pending_matching(address)]
+        return [{'tx_hash': i.tx_hash, 'index': i.index} for tx in txs for i in tx.inputs]
+
+    def _amount_rows(self, table: str, forms: List[str], where: str = '', check_pending: bool = False,
+                     args: tuple = ()):
+        """``SELECT t.tx_hash, index, transactions.outputs_amounts[index + 1] FROM t JOIN transactions``."""
+        ph = ','.join('?' * len(forms))
+        rows = self._q(f'SELECT {table}.tx_hash AS tx_hash, {table}."index" AS idx, transactions.outputs_amounts AS am '
+                       f'FROM {table} INNER JOIN transactions ON (transactions.tx_hash = {table}.tx_hash) '
+                       f'WHERE {table}.address IN ({ph}) {where} ORDER BY {table}.rowid', (*forms, *args))
+        pend = self._pending_spent_set() if check_pending else set()
+        out = []
+        for r in rows:
+            if (r['tx_hash'], r['idx']) in pend:
+                continue
+            out.append((r['tx_hash'], r['idx'], _at(_arr(r['am']), r['idx'])))
+        return out
+
+    async def get_spendable_outputs(self, address: str, check_pending_txs: bool = False) -> List[TransactionInput]:
+        point = string_to_point(address)
+        forms = list(reversed(self._forms(address)))
+        if self._q1('SELECT tx_hash FROM unspent_outputs WHERE address IS NULL LIMIT 1') is not None:
+            await self.set_unspent_outputs_addresses()
+        rows = self._amount_rows('unspent_outputs', forms,
+                                 'AND (unspent_outputs.is_stake IS NULL OR unspent_outputs.is_stake = 0)',
+                                 check_pending_txs)
+        return [TransactionInput(h, i, amount=Decimal(a) / SMALLEST, public_key=point) for h, i, a in rows]
+
+    async def get_stake_outputs(self, address: str, check_pending_txs: bool = False) -> List[TransactionInput]:
+        point = string_to_point(address)
+        forms = list(reversed(self._forms(address)))
+        if self._q1('SELECT tx_hash FROM unspent_outputs WHERE address IS NULL LIMIT 1') is not None:
+            await self.set_unspent_outputs_addresses()
+        rows = self._amount_rows('unspent_outputs', forms, 'AND (unspent_outputs.is_stake = 1)', check_pending_txs)
+        return [TransactionInput(h, i, amount=Decimal(a) / SMALLEST, public_key=point) for h, i, a in rows]
+
+    async def _table_inputs(self, table: str, address: str, check_pending_txs: bool) -> List[TransactionInput]:
+        point = string_to_point(address)
+        rows = self._amount_rows(table, list(reversed(self._forms(address))), '', check_pending_txs)
+        return [TransactionInput(h, i, amount=Decimal(a) / SMALLEST, public_key=point) for h, i, a in rows]
+
+    async def get_inode_registration_outputs(self, address: str, check_pending_txs: bool = False):
+        return await self._table_inputs('inode_registration_output', address, check_pending_txs)
+
+    async def get_validator_registration_outputs(self, address: str, check_pending_txs: bool = False):
+        return await self._table_inputs('validator_registration_output', address, check_pending_txs)
+
+    async def get_validators_voting_power(self, address: str, check_pending_txs: bool = False):
+        return await self._table_inputs('validators_voting_power', address, check_pending_txs)
+
+    async def get_delegates_voting_power(self, address: str, check_pending_txs: bool = False):
+        return await self._table_inputs('delegates_voting_power', address, check_pending_txs)
+
+    async def is_inode_registered(self, address: str, check_pending_txs: bool = False) -> bool:
+        return len(await self.get_inode_registration_outputs(address, check_pending_txs)) > 0
+
+    async def is_validator_registered(self, address: str, check_pending_txs: bool = False) -> bool:
+        return len(await self.get_validator_registration_outputs(address, check_pending_txs)) > 0
+
+    def _spent_votes(self, table: str, address: str, check_pending: bool) -> List[TransactionInput]:
+        """Ballots cast by ``address``: ``transactions.inputs_addresses[index + 1] = ANY(forms)``
+        (database.py:1479-1500, 1526-1547; the ballot *output* index subscripts the inputs array)."""
+        point = string_to_point(address)
+        forms = set(self._forms(address))
+        pend = self._pending_spent_set() if check_pending else set()
+        rows = self._q(f'SELECT {table}.tx_hash AS tx_hash, {table}."index" AS idx, transactions.outputs_amounts AS am, '
+                       f'transactions.inputs_addresses AS ia FROM transactions INNER JOIN {table} ON '
+                       f'(transactions.tx_hash = {table}.tx_hash) ORDER BY {table}.rowid')
+        out = []
+        for r in rows:
+            if _at(_arr(r['ia']), r['idx']) in forms and (r['tx_hash'], r['idx']) not in pend:
+                out.append(TransactionInput(r['tx_hash'], r['idx'], amount=Decimal(_at(_arr(r['am']), r['idx'])) / SMALLEST,
+                                            public_key=point))
+        return out
+
+    async def get_validators_spent_votes(self, address: str, check_pending_txs: bool = False):
+        return self._spent_votes('inodes_ballot', address, check_pending_txs)
+
+    async def get_delegates_spent_votes(self, address: str, check_pending_txs: bool = False):
+        return self._spent_votes('validators_ballot', address, check_pending_txs)
+
+    async def get_delegates_all_power(self, address: str, check_pending_txs: bool = False):
+        unspent = await self.get_delegates_voting_power(address, check_pending_txs)
+        unspent.extend(await self.get_delegates_spent_votes(address, check_pending_txs))
+        return unspent
+
+    # ------------------------------------------------------------------ ballots (database.py:939-1136)
+    def _ballot_rows(self, table: str, receiver_forms: Optional[List[str]], check_pending: bool,
+                     limit: Optional[int] = None, offset: int = 0, voter_forms: Optional[Set[str]] = None,
+                     order: bool = True):
+        where, args = '', []
+        if receiver_forms is not None:
+            where = f'WHERE {table}.address IN ({",".join("?" * len(receiver_forms))})'
+            args = list(receiver_forms)
+        rows = self._q(f'SELECT {table}.tx_hash AS tx_hash, {table}.address AS receiver, {table}."index" AS idx, '
+                       f'transactions.outputs_amounts AS am, transactions.inputs_addresses AS ia FROM {table} '
+                       f'INNER JOIN transactions ON (transactions.tx_hash = {table}.tx_hash) {where} '
+                       f'ORDER BY {(table + ".tx_hash, ") if order else ""}{table}.rowid', args)
+        pend = self._pending_spent_set() if check_pending else set()
+        out = []
+        for r in rows:
+            if (r['tx_hash'], r['idx']) in pend:
+                continue
+            voter = _at(_arr(r['ia']), r['idx'])
+            if voter_forms is not None and voter not in voter_forms:
+                continue
+            vote = _at(_arr(r['am']), r['idx'])
+            out.append((r['tx_hash'], r['receiver'], Decimal(vote) / SMALLEST if vote is not None else None,
+                        voter, r['idx']))
+        if limit is not None:
+            out = out[offset:offset + limit]
+        return out
+
+    async def get_inode_ballot(self, offset: int, limit: int, check_pending_txs: bool = False):
+        return self._ballot_rows('inodes_ballot', None, check_pending_txs, limit, offset)
+
+    async def get_inode_ballot_by_address(self, offset: int, limit: int, inode: str, check_pending_txs: bool = False):
+        return self._ballot_rows('inodes_ballot', self._forms(inode), check_pending_txs, limit, offset)
+
+    async def get_inode_ballot_input_by_address(self, validator_address: str, vote_receiver_address: str,
+                                                check_pending_txs: bool = False) -> List[TransactionInput]:
+        point = string_to_point(validator_address)
+        rows = self._ballot_rows('inodes_ballot', list(reversed(self._forms(vote_receiver_address))), check_pending_txs,
+                                 voter_forms=set(self._forms(validator_address)), order=False)
+        return [TransactionInput(h, i, amount=v, public_key=point) for h, _, v, _, i in rows]
+
+    async def get_validator_ballot_input_by_address(self, delegate_address: str, vote_receiver_address: str,
+                                                    check_pending_txs: bool = False) -> List[TransactionInput]:
+        point = string_to_point(delegate_address)
+        rows = self._ballot_rows('validators_ballot', list(reversed(self._forms(vote_receiver_address))),
+                                 check_pending_txs, voter_forms=set(self._forms(delegate_address)), order=False)
+        return [TransactionInput(h, i, amount=v, public_key=point) for h, _, v, _, i in rows]
+
+    async def get_validator_ballot(self, offset: int, limit: int, check_pending_txs: bool = False):
+        return self._ballot_rows('validators_ballot', None, check_pending_txs, limit, offset)
+
+    async def get_validator_ballot_by_address(self, offset: int, limit: int, validator: str,
+                                              check_pending_txs: bool = False):
+        return self._ballot_rows('validators_ballot', self._forms(validator), check_pending_txs, limit, offset)
+
+    async def get_transaction_time(self, tx_hash) -> datetime:
+        r = self._q1('SELECT blocks.timestamp FROM blocks INNER JOIN transactions ON '
+                     '(blocks.hash = transactions.block_hash) WHERE transactions.tx_hash = ?', (tx_hash,))
+        assert r is not None
+        return _dt(r[0])
+
+    async def is_revoke_valid(self, tx_hash) -> bool:
+        return _utcnow() - await self.get_transaction_time(tx_hash) >= timedelta(hours=48)
+
+    async def get_validators_stake(self, validator: str, check_pending_txs: bool = False):
+        ballot = await self.get_validator_ballot_by_address(0, 100000, validator=validator,
+                                                            check_pending_txs=check_pending_txs)
+        ratio = [(vote * await self.get_address_stake(delegate)) / 10 for _, _, vote, delegate, _ in ballot]
+        return round_up_decimal(sum(ratio, Decimal(0)))
+
+    async def get_address_balance(self, address: str, check_pending_txs: bool = False) -> Decimal:
+        forms = self._forms(address)
+        balance = sum([i.amount for i in await self.get_spendable_outputs(address, check_pending_txs)], Decimal(0))
+        if check_pending_txs:
+            search = self._search(address)
+            for r in self._q('SELECT tx_hex FROM pending_transactions ORDER BY rowid'):
+                if not any(s in r['tx_hex'] for s in search):
+                    continue
+                tx = await Transaction.from_hex(r['tx_hex'], check_signatures=False)
+                for o in tx.outputs:
+                    if o.address in forms and o.transaction_type is OutputType.REGULAR and \
+                            (o.is_stake is False or o.is_stake is None):
+                        balance += o.amount
+        return balance
+
+    async def get_pending_stake_transaction(self, address: str):
+        search = self._search(address)
+        out = []
+        for r in self._q('SELECT tx_hex FROM pending_transactions ORDER BY rowid'):
+            if not any(s in r['tx_hex'] for s in search):
+                continue
+            tx = await Transaction.from_hex(r['tx_hex'], check_signatures=False)
+            for o in tx.outputs:
+                if o.address == address and o.transaction_type is OutputType.STAKE:
+                    out.append(tx)
+        assert len(out) < 2
+        return out
+
+    async def get_pending_vote_as_delegate_transaction(self, address: str):
+        search = self._search(address)
+        out = []
+        for r in self._q('SELECT tx_hex FROM pending_transactions ORDER BY rowid'):
+            if not any(s in r['tx_hex'] for s in search):
+                continue
+            tx = await Transaction.from_hex(r['tx_hex'], check_signatures=False)
+            if tx.transaction_type == TransactionType.VOTE_AS_DELEGATE and await tx.inputs[0].get_address() == address:
+                out.append(tx)
+        return out
+
+    async def get_address_stake(self, address: str, check_pending_txs: bool = False) -> Decimal:
+        forms = self._forms(address)
+        stake = sum([i.amount for i in await self.get_stake_outputs(address, check_pending_txs)], Decimal(0))
+        if check_pending_txs:
+            search = self._search(address)
+            for r in self._q('SELECT tx_hex FROM pending_transactions ORDER BY rowid'):
+                if not any(s in r['tx_hex'] for s in search):
+                    continue
+                tx = await Transaction.from_hex(r['tx_hex'], check_signatures=False)
+                for o in tx.outputs:
+                    if o.address in forms and o.is_stake is True:
+                        stake += o.amount
+        return stake
+
+    async def get_multiple_address_stakes(self, addresses: Set[str], check_pending_txs: bool = False
+                                          ) -> Dict[str, Decimal]:
+        if not addresses:
+            return {}
+        data = {a: {'formats': self._forms(a), 'searches': self._search(a)} for a in addresses}
+        all_forms = [f for d in data.values() for f in d['formats']]
+        if self._q1('SELECT tx_hash FROM unspent_outputs WHERE address IS NULL LIMIT 1') is not None:
+            await self.set_unspent_outputs_addresses()
+        rows = self._amount_rows('unspent_outputs', all_forms, 'AND unspent_outputs.is_stake = 1', check_pending_txs)
+        addr_of = {}
+        for r in self._q(f'SELECT tx_hash, "index", address FROM unspent_outputs WHERE address IN '
+                         f'({",".join("?" * len(all_forms))}) AND is_stake = 1', all_forms):
+            addr_of[(r[0], r[1])] = r[2]
+        stake_map = defaultdict(Decimal)
+        for h, i, a in rows:
+            address = addr_of.get((h, i))
+            original = next(k for k, d in data.items() if address in d['formats'])
+            stake_map[original] += Decimal(a) / SMALLEST
+        if check_pending_txs:
+            searches = [s for d in data.values() for s in d['searches']]
+            for r in self._q('SELECT tx_hex FROM pending_transactions ORDER BY rowid'):
+                if not any(s in r['tx_hex'] for s in searches):
+                    continue
+                tx = await Transaction.from_hex(r['tx_hex'], check_signatures=False)
+                for o in tx.outputs:
+                    if o.is_stake:
+                        for original, d in data.items():
+                            if o.address in d['formats']:
+                                stake_map[original] += o.amount
+        return dict(stake_map)
+
+    # ------------------------------------------------------------------ inodes (database.py:1348-1438)
+    async def get_genesis_block(self):
+        r = self._q1('SELECT content FROM blocks WHERE id = 1')
+        return r[0] if r else None
+
+    async def get_all_registered_inode(self, check_pending_txs: bool = False):
+        rows = self._q('SELECT inode_registration_output.address AS address, inode_registration_output.tx_hash AS h, '
+                       'inode_registration_output."index" AS idx, blocks.timestamp AS ts FROM inode_registration_output '
+                       'INNER JOIN transactions ON inode_registration_output.tx_hash = transactions.tx_hash '
+                       'INNER JOIN blocks ON transactions.block_hash = blocks.hash ORDER BY inode_registration_output.rowid')
+        pend = self._pending_spent_set() if check_pending_txs else set()
+        return [(r['address'], _dt(r['ts'])) for r in rows if (r['h'], r['idx']) not in pend]
+
+    async def get_active_inodes(self, check_pending_txs: bool = False):
+        codec.getting_active_inodes = True
+        try:
+            inode_with_vote = await self.get_all_registered_inode_with_vote(check_pending_txs)
+            total_power = sum(item['power'] for item in inode_with_vote)
+            now = _utcnow()
+            for item in inode_with_vote:
+                item['emission'] = (item['power'] / total_power) * 100 if total_power > 0 else item['power']
+                item['emission'] = round_up_decimal(item['emission'], round_up_length='0.01')
+                item['is_active'] = item['emission'] >= 1 or now - item['registered_at'] <= timedelta(hours=48)
+            return [item for item in inode_with_vote if item['is_active'] is True]
+        finally:
+            codec.getting_active_inodes = False
+
+    async def get_inode_vote_ratio_by_address(self, address: str, check_pending_txs: bool = False):
+        rows = self._ballot_rows('inodes_ballot', list(reversed(self._forms(address))), check_pending_txs,
+                                 order=False)
+        votes = [(vote, validator) for _, _, vote, validator, _ in rows]
+        ratio = [(vote * await self.get_validators_stake(validator)) / 10 for vote, validator in votes]
+        return round_up_decimal(sum(ratio, Decimal(0)))
+
+    async def get_all_registered_inode_with_vote(self, check_pending_txs: bool = False):
+        return [{'wallet': address, 'power': await self.get_inode_vote_ratio_by_address(address, check_pending_txs),
+                 'registered_at': ts} for address, ts in await self.get_all_registered_inode(check_pending_txs)]
+
+    async def get_inode_count(self, check_pending_txs: bool = False):
+        rows = self._q('SELECT tx_hash, "index" FROM inode_registration_output')
+        pend = self._pending_spent_set() if check_pending_txs else set()
+        return [{'count': sum(1 for r in rows if (r[0], r[1]) not in pend)}]
+
+    async def get_address_spendable_outputs_delta(self, address: str, block_no: int):
+        point = string_to_point(address)
+        forms = self._forms(address)
+        ph = ','.join('?' * len(forms))
+        rows = self._q(f'SELECT unspent_outputs.tx_hash AS h, unspent_outputs."index" AS idx, transactions.outputs_amounts AS am '
+                       f'FROM unspent_outputs INNER JOIN transactions ON (transactions.tx_hash = unspent_outputs.tx_hash) '
+                       f'INNER JOIN blocks ON (blocks.hash = transactions.block_hash) WHERE unspent_outputs.address IN ({ph}) '
+                       f'AND blocks.id >= ? ORDER BY unspent_outputs.rowid', (*forms, block_no))
+        unspent = [TransactionInput(r['h'], r['idx'], amount=Decimal(_at(_arr(r['am']), r['idx'])) / SMALLEST,
+                                    public_key=point) for r in rows]
+        srows = self._q('SELECT transactions.tx_hex AS tx_hex, transactions.inputs_addresses AS ia FROM transactions '
+                        'INNER JOIN blocks ON (transactions.block_hash = blocks.hash) WHERE blocks.id >= ? '
+                        'ORDER BY transactions.rowid', (block_no,))
+        spending = [await Transaction.from_hex(r['tx_hex'], False) for r in srows if address in _arr(r['ia'])][:block_no]
+        return unspent, [i for tx in spending for i in tx.inputs]
+
+    async def get_nice_transaction(self, tx_hash: str, address: str = None):
+        """database.py:1606-1654."""
+        is_confirm = True
+        res = self._q1('SELECT transactions.tx_hex AS tx_hex, transactions.tx_hash AS tx_hash, transactions.block_hash '
+                       'AS block_hash, transactions.inputs_addresses AS inputs_addresses, blocks.id AS block_no, '
+                       'blocks.timestamp AS timestamp FROM transactions INNER JOIN blocks ON '
+                       '(transactions.block_hash = blocks.hash) WHERE tx_hash = ?', (tx_hash,))
+        if res is None:
+            res = self._q1('SELECT tx_hex, tx_hash, inputs_addresses FROM pending_transactions WHERE tx_hash = ?',
+                           (tx_hash,))
+            is_confirm = False
+        if res is None:
+            return None
+        res = dict(res)
+        inputs_addresses = _arr(res['inputs_addresses'])
+        ts = _dt(res['timestamp']) if res.get('timestamp') is not None else None
+        tx = await Transaction.from_hex(res['tx_hex'], False)
+        if isinstance(tx, CoinbaseTransaction):
+            transaction = {'is_coinbase': True, 'hash': res['tx_hash'], 'block_hash': res.get('block_hash'),
+                           'block_no': res.get('block_no'), 'datetime': ts}
+        else:
+            delta = None
+            if address is not None:
+                public_key = string_to_point(address)
+                delta = 0
+                for i, tx_input in enumerate(tx.inputs):
+                    if string_to_point(inputs_addresses[i]) == public_key:
+                        delta -= await tx_input.get_amount()
+                for o in tx.outputs:
+                    if o.public_key == public_key:
+                        delta += o.amount
+            transaction = {'is_coinbase': False, 'hash': res['tx_hash'], 'block_hash': res.get('block_hash'),
+                           'block_no': res.get('block_no'), 'datetime': ts,
+                           'message': tx.message.hex() if tx.message is not None else None,
+                           'transaction_type': tx.transaction_type.name, 'is_confirm': is_confirm,
+                           'inputs': [], 'delta': delta, 'fees': await tx.get_fees()}
+            for i, tx_input in enumerate(tx.inputs):
+                transaction['inputs'].append({'index': tx_input.index, 'tx_hash': tx_input.tx_hash,
+                                              'address': _at(inputs_addresses, i),
+                                              'amount': await tx_input.get_amount()})
+        transaction['outputs'] = [{'address': o.address, 'amount': o.amount, 'type': o.transaction_type.name}
+                                  for o in tx.outputs]
+        return transaction
+
+
+class _Rollback(Exception):
+    pass
+
+
+class UniqueViolationError(Exception):
+    """Stand-in for asyncpg.UniqueViolationError (reference main.py:10,455)."""
+
+
+class ForeignKeyViolationError(Exception):
+    pass

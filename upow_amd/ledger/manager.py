@@ -1,0 +1,526 @@
+"""Consensus manager: difficulty, emission, block validation/application, mempool GC.
+
+reference: upow/manager.py:26-904. Same rules, same constants, same consensus exception tables.
+The per-transaction validation loop of ``check_block`` (manager.py:628-632) is replaced by
+:func:`upow_amd.ledger.validate.verify_block_transactions`, which runs every signature of the block
+as ONE batched P-256 verify on the GPU (with the reference's raw-bytes-then-ASCII-hex fallback),
+prefetches all point decompressions in one kernel, and still runs each tx's rule checks in order.
+"""
+from __future__ import annotations
+
+import asyncio
+import decimal
+from datetime import datetime, timedelta
+from decimal import Decimal
+from math import ceil, floor, log
+from time import perf_counter
+from typing import List, Optional, Tuple, Union
+
+from ..constants import (BLOCK_TIME, BLOCKS_COUNT, LAST_BLOCK_FOR_GENESIS_KEY, MAX_BLOCK_SIZE_HEX, MAX_SUPPLY,
+                         START_DIFFICULTY)
+from ..models.block import (block_to_bytes, check_pow, get_transactions_merkle_tree,
+                            get_transactions_merkle_tree_ordered, split_block_content)
+from ..models.transaction import CoinbaseTransaction, Transaction, TransactionOutput
+from ..utils import codec
+from ..utils.codec import TransactionType, round_up_decimal, round_up_decimal_new, sha256, timestamp
+from ..utils.logger import get_logger
+from .database import Database
+
+logger = get_logger(__name__)
+
+cache: dict = {}
+cache_expiration = timedelta(minutes=5)
+cache_updating = False
+
+# stage timers of the last validated block (tracing)
+last_block_timings: dict = {}
+
+
+class Manager:
+    difficulty: Optional[Tuple[Decimal, dict]] = None
+
+
+# ---------------------------------------------------------------------------------------------- difficulty
+def difficulty_to_hashrate_old(difficulty: Decimal) -> Decimal:
+    decimal_ = difficulty % 1 or 1 / 16
+    return Decimal(16 ** int(difficulty) * (16 * decimal_))
+
+
+def difficulty_to_hashrate(difficulty: Decimal) -> Decimal:
+    """manager.py:44-46."""
+    decimal_ = difficulty % 1
+    return Decimal(16 ** int(difficulty) * (16 / ceil(16 * (1 - decimal_))))
+
+
+def hashrate_to_difficulty_old(hashrate: int) -> Decimal:
+    difficulty = int(log(hashrate, 16))
+    if hashrate == 16 ** difficulty:
+        return Decimal(difficulty)
+    return Decimal(difficulty + (hashrate / Decimal(16) ** difficulty) / 16)
+
+
+def hashrate_to_difficulty(hashrate) -> Decimal:
+    """manager.py:67-80 (quantised to 0.1)."""
+    difficulty = int(log(hashrate, 16))
+    ratio = hashrate / 16 ** difficulty
+    for i in range(0, 10):
+        coeff = 16 / ceil(16 * (1 - i / 10))
+        if coeff > ratio:
+            return Decimal(difficulty + (i - 1) / Decimal(10))
+        if coeff == ratio:
+            return Decimal(difficulty + i / Decimal(10))
+    return Decimal(difficulty) + Decimal('0.9')
+
+
+async def calculate_difficulty() -> Tuple[Decimal, dict]:
+    """manager.py:83-121: retarget every 100 blocks toward 60 s."""
+    database = Database.instance
+    last_block = await database.get_last_block()
+    if last_block is None:
+        return START_DIFFICULTY, dict()
+    last_block = dict(last_block)
+    last_block['address'] = last_block['address'].strip(' ')
+    if last_block['id'] < BLOCKS_COUNT:
+        return START_DIFFICULTY, last_block
+    if last_block['id'] % BLOCKS_COUNT == 0:
+        last_adjust_block = await database.get_block_by_id(last_block['id'] - BLOCKS_COUNT + 1)
+        elapsed = last_block['timestamp'] - last_adjust_block['timestamp']
+        average_per_block = elapsed / BLOCKS_COUNT
+        last_difficulty = last_block['difficulty']
+        hashrate = difficulty_to_hashrate(last_difficulty)
+        ratio = BLOCK_TIME / average_per_block
+        if last_block['id'] >= 180_000:
+            ratio = min(ratio, 2)
+        hashrate *= ratio
+        new_difficulty = hashrate_to_difficulty(hashrate)
+        if new_difficulty < START_DIFFICULTY and last_block['id'] >= 590600:
+            return START_DIFFICULTY, last_block
+        logger.info(f'calculate_difficulty hashrate_to_difficulty block {last_block["id"]}, '
+                    f'new_difficulty {new_difficulty}')
+        return new_difficulty, last_block
+    return last_block['difficulty'], last_block
+
+
+async def get_difficulty() -> Tuple[Decimal, dict]:
+    if Manager.difficulty is None:
+        Manager.difficulty = await calculate_difficulty()
+    return Manager.difficulty
+
+
+async def check_block_is_valid(block_content: str, mining_info: tuple = None) -> bool:
+    """manager.py:130-151."""
+    if mining_info is None:
+        mining_info = await get_difficulty()
+    difficulty, last_block = mining_info
+    if 'hash' not in last_block:
+        return True
+    return check_pow(block_content, last_block['hash'], difficulty)
+
+
+# ---------------------------------------------------------------------------------------------- emission
+def get_block_reward(block_no) -> Decimal:
+    """manager.py:154-168."""
+    assert block_no > 0
+    halving_interval = 1576800
+    nine_halving_interval = 14191200
+    if block_no > nine_halving_interval:
+        return Decimal(0)
+    coins_per_block = 6
+    num_halvings = block_no // halving_interval
+    if block_no % halving_interval == 0:
+        num_halvings = num_halvings - 1
+    return Decimal(coins_per_block / (2 ** num_halvings))
+
+
+def get_inode_rewards(reward, inode_address_details, block_no=1):
+    """manager.py:171-212 (Decimal contexts and the <1 % redistribution reproduced verbatim)."""
+    total_percent = sum(entry['emission'] for entry in inode_address_details)
+    if not inode_address_details or total_percent <= 0:
+        return reward, {}
+    miner_reward = reward * Decimal(0.5)
+    distribution_reward = reward * Decimal(0.5)
+    distributed_rewards = {}
+    redistribution_reward = Decimal(0)
+    with decimal.localcontext() as ctx:
+        ctx.prec = 9 if block_no > 39000 else ctx.prec
+        for address_detail in inode_address_details:
+            percent = address_detail['emission']
+            address_reward = distribution_reward * Decimal(percent) / Decimal(total_percent)
+            if block_no > 39000:
+                address_reward = round_up_decimal_new(address_reward)
+            else:
+                address_reward = round_up_decimal(address_reward)
+            if percent >= 1:
+                distributed_rewards[address_detail['wallet']] = address_reward
+            else:
+                redistribution_reward += distribution_reward * Decimal(percent) / Decimal(total_percent)
+            if redistribution_reward > 0:
+                num_eligible = sum(1 for e in inode_address_details if e['emission'] >= 1)
+                redistribution_amount = redistribution_reward / num_eligible
+                if block_no > 39000:
+                    redistribution_amount = round_up_decimal_new(redistribution_amount)
+                else:
+                    redistribution_amount = round_up_decimal(redistribution_amount)
+                for d in inode_address_details:
+                    if d['emission'] >= 1:
+                        distributed_rewards[d['wallet']] += redistribution_amount
+    return miner_reward, distributed_rewards
+
+
+def get_circulating_supply(block_no):
+    """manager.py:215-234."""
+    halving_interval = 3 * 365 * 24 * 60
+    initial_coins_per_block = 6
+    if block_no > halving_interval * 9:
+        return Decimal(MAX_SUPPLY)
+    circulating_supply = 0
+    num_halvings = block_no // halving_interval
+    remaining_blocks = block_no % halving_interval
+    if remaining_blocks == 0:
+        num_halvings = num_halvings - 1
+    for i in range(num_halvings + 1):
+        current_reward = initial_coins_per_block / (2 ** i)
+        if i == num_halvings and remaining_blocks > 0:
+            circulating_supply += current_reward * remaining_blocks
+        else:
+            circulating_supply += current_reward * halving_interval
+    return circulating_supply
+
+
+# ---------------------------------------------------------------------------------------------- mempool GC
+async def clear_pending_transactions(transactions=None):
+    """manager.py:253-330. The reference restarts from scratch after every removal (O(n^2));
+    here a conflict removes the tx and the scan continues with the remaining ones (same result set)."""
+    database: Database = Database.instance
+    await database.clear_duplicate_pending_transactions()
+    while True:
+        restart = False
+        txs = transactions or await database.get_pending_transactions_limit(hex_only=True)
+        transactions = None
+        used_inputs = set()
+        buckets = {k: [] for k in ('inode', 'vpower', 'dpower', 'iballot', 'vballot', 'regular')}
+        for transaction in txs:
+            if isinstance(transaction, str):
+                tx_hash = sha256(transaction)
+                transaction = await Transaction.from_hex(transaction, check_signatures=False)
+            else:
+                tx_hash = sha256(transaction.hex())
+            tx_inputs = [(i.tx_hash, i.index) for i in transaction.inputs]
+            if any(u in used_inputs for u in tx_inputs):
+                await database.remove_pending_spent_outputs_by_tuple(tx_inputs)
+                await database.remove_pending_transaction(tx_hash)
+                logger.info(f'clear_pending_transactions: removed {tx_hash}')
+                restart = True
+                break
+            used_inputs.update(tx_inputs)
+            t = transaction.transaction_type
+            key = {TransactionType.INODE_DE_REGISTRATION: 'inode', TransactionType.VOTE_AS_VALIDATOR: 'vpower',
+                   TransactionType.VOTE_AS_DELEGATE: 'dpower', TransactionType.REVOKE_AS_VALIDATOR: 'iballot',
+                   TransactionType.REVOKE_AS_DELEGATE: 'vballot'}.get(t, 'regular')
+            buckets[key].extend(tx_inputs)
+        if restart:
+            continue
+        lookups = (('regular', database.get_unspent_outputs), ('inode', database.get_inode_outputs),
+                   ('vpower', database.get_validator_voting_power_outputs),
+                   ('dpower', database.get_delegates_voting_power_outputs),
+                   ('iballot', database.get_inodes_ballot_outputs), ('vballot', database.get_validators_ballot_outputs))
+        for key, fn in lookups:
+            if buckets[key]:
+                await verify_outputs(buckets[key], await fn(buckets[key]))
+        return None
+
+
+async def verify_outputs(used_inputs, outputs):
+    """manager.py:333-349."""
+    database: Database = Database.instance
+    double_spend_inputs = set(used_inputs) - set(outputs)
+    if double_spend_inputs == set(used_inputs):
+        await database.remove_pending_transactions()
+    elif double_spend_inputs:
+        await database.remove_pending_spent_outputs_by_tuple(list(double_spend_inputs))
+        await database.remove_pending_transactions_by_contains(
+            [tx_input[0] + bytes([tx_input[1]]).hex() for tx_input in double_spend_inputs])
+        logger.info(f'clear_pending_transactions verify_outputs: removed {double_spend_inputs}')
+
+
+def get_transactions_size(transactions: List[Transaction]) -> int:
+    return sum(len(t.hex()) for t in transactions)
+
+
+# ---------------------------------------------------------------------------------------------- blocks
+_GOV_SPEND = (TransactionType.INODE_DE_REGISTRATION, TransactionType.VOTE_AS_VALIDATOR,
+              TransactionType.VOTE_AS_DELEGATE, TransactionType.REVOKE_AS_VALIDATOR,
+              TransactionType.REVOKE_AS_DELEGATE)
+
+
+async def check_block(block_content: str, transactions: List[Transaction], mining_info: tuple = None,
+                      error_list=None) -> bool:
+    """manager.py:422-647."""
+    from .validate import verify_block_transactions
+    if error_list is None:
+        error_list = []
+    t0 = perf_counter()
+    if mining_info is None:
+        mining_info = await calculate_difficulty()
+    difficulty, last_block = mining_info
+    block_no = last_block['id'] + 1 if last_block != {} else 1
+    previous_hash, address, merkle_tree, content_time, content_difficulty, random = split_block_content(block_content)
+    if not await check_block_is_valid(block_content, mining_info):
+        error_list.append('block not valid')
+        logger.error('block not valid')
+        return False
+    content_time = int(content_time)
+    if last_block != {} and previous_hash != last_block['hash']:
+        error_list.append(error := 'Previous hash is not matched')
+        logger.error(error)
+        return False
+    last_ts = last_block['timestamp'] if 'timestamp' in last_block else 0
+    if last_ts > content_time or last_ts == content_time:
+        error_list.append(error := 'timestamp younger than previous block')
+        logger.error(error)
+        return False
+    current_timestamp = timestamp()
+    if content_time > current_timestamp:
+        error_list.append(error := f'timestamp in the future content_time: {content_time}, '
+                                   f'current_timestamp {current_timestamp}')
+        logger.error(error)
+        return False
+    database: Database = Database.instance
+    transactions = [tx for tx in transactions if isinstance(tx, Transaction)]
+    if get_transactions_size(transactions) > MAX_BLOCK_SIZE_HEX:
+        error_list.append(error := 'block is too big')
+        logger.error(error)
+        return False
+    t_utxo = perf_counter()
+    if transactions:
+        def bucket(pred):
+            return [(i.tx_hash, i.index) for tx in transactions if pred(tx.transaction_type) for i in tx.inputs]
+
+        check_inputs = bucket(lambda t: t not in _GOV_SPEND)
+        categories = [
+            (check_inputs, await database.get_unspent_outputs(check_inputs), None),
+            (bucket(lambda t: t == TransactionType.INODE_DE_REGISTRATION), None,
+             'double spend in inode transaction in block'),
+            (bucket(lambda t: t == TransactionType.VOTE_AS_VALIDATOR), None,
+             'double spend in validator power transaction in block'),
+            (bucket(lambda t: t == TransactionType.VOTE_AS_DELEGATE), None,
+             'double spend in delegate power transaction in block'),
+            (bucket(lambda t: t == TransactionType.REVOKE_AS_VALIDATOR), None,
+             'double spend in inode_ballot revoke transaction in block'),
+            (bucket(lambda t: t == TransactionType.REVOKE_AS_DELEGATE), None,
+             'double spend in validators_ballot revoke transaction in block'),
+        ]
+        fns = [None, database.get_inode_outputs, database.get_validator_voting_power_outputs,
+               database.get_delegates_voting_power_outputs, database.get_inodes_ballot_outputs,
+               database.get_validators_ballot_outputs]
+        for k in range(1, 6):
+            inputs, _, msg = categories[k]
+            categories[k] = (inputs, await fns[k](inputs), msg)
+        unspent = categories[0][1]
+        if len(set(check_inputs)) != len(check_inputs) or set(check_inputs) - set(unspent) != set():
+            spent_outputs = set(check_inputs) - set(unspent)
+            allowed = double_spend_dict.get(block_no)
+            if allowed is None or spent_outputs - set(allowed) != set():
+                error_list.append(error := f'double spend in block: {block_no}, utxo: {spent_outputs}')
+                logger.error(error)
+                return False
+        for inputs, found, msg in categories[1:]:
+            if len(set(inputs)) != len(inputs) or set(inputs) - set(found) != set():
+                error_list.append(msg)
+                logger.error(msg)
+                return False
+        input_txs = await database.get_transactions_info([i.tx_hash for tx in transactions for i in tx.inputs])
+        for tx in transactions:
+            await tx._fill_transaction_inputs(input_txs)
+    t_verify = perf_counter()
+    bad = await verify_block_transactions(transactions)
+    if bad is not None:
+        error_list.append(error := f'transaction {bad.hash()} has been not verified')
+        logger.error(error)
+        return False
+    t_merkle = perf_counter()
+    transactions_merkle_tree = get_transactions_merkle_tree(transactions)
+    last_block_timings.update({'utxo_s': t_verify - t_utxo, 'verify_s': t_merkle - t_verify,
+                               'merkle_s': perf_counter() - t_merkle, 'total_s': perf_counter() - t0,
+                               'txs': len(transactions)})
+    if merkle_tree != transactions_merkle_tree:
+        if block_no == 340510 and merkle_tree == '54e7e3fbfe5c3c7b2a74d14efd22a61c231d157b2c5c2476fca67736736b9ac8':
+            return True
+        error_list.append(error := 'merkle tree does not match')
+        logger.error(error)
+        return False
+    return True
+
+
+async def _apply_block(block_no, block_hash, block_content, address, random, difficulty, block_reward, fees,
+                       content_time, coinbase_transaction, transactions) -> bool:
+    """DB writes of manager.py:706-730 (shared by create_block and the sync path)."""
+    database: Database = Database.instance
+    await database.add_block(block_no, block_hash, block_content, address, random, difficulty,
+                             block_reward + fees, content_time)
+    await database.add_transaction(coinbase_transaction, block_hash)
+    try:
+        await database.add_transactions(transactions, block_hash)
+    except Exception as e:
+        logger.error(f'Transaction of {block_no} has not been added in block {e}')
+        await database.delete_block(block_no)
+        return False
+    await database.add_transaction_outputs(transactions + [coinbase_transaction])
+    if transactions:
+        await database.remove_pending_transactions_by_hash([t.hash() for t in transactions])
+        await database.remove_outputs(transactions)
+        await database.remove_pending_spent_outputs(transactions)
+    return True
+
+
+async def create_block(block_content: str, transactions: List[Transaction], last_block: dict = None,
+                       error_list=None) -> bool:
+    """manager.py:650-757."""
+    if error_list is None:
+        error_list = []
+    create_start_time = perf_counter()
+    Manager.difficulty = None
+    if last_block is None or last_block['id'] % BLOCKS_COUNT == 0:
+        difficulty, last_block = await calculate_difficulty()
+    else:
+        difficulty, last_block = await get_difficulty()
+    block_no = last_block['id'] + 1 if last_block != {} else 1
+    logger.info(f'Creating block no. {block_no}')
+    if not await check_block(block_content, transactions, (difficulty, last_block), error_list=error_list):
+        return False
+    database: Database = Database.instance
+    block_hash = sha256(block_content)
+    previous_hash, address, merkle_tree, content_time, content_difficulty, random = split_block_content(block_content)
+    active_inodes = await database.get_active_inodes()
+    await update_active_inodes_cache_with_data(active_inodes)
+    block_reward = get_block_reward(block_no)
+    miner_reward, inode_rewards = get_inode_rewards(block_reward, active_inodes, block_no=block_no)
+    genesis_block_content = await database.get_genesis_block()
+    if genesis_block_content is not None:
+        _, genesis_address, _, _, _, _ = split_block_content(genesis_block_content)
+        if not ((address == genesis_address and block_no <= LAST_BLOCK_FOR_GENESIS_KEY) or inode_rewards):
+            error_list.append(error := 'Emission detail is not formed. Hence you cannot mine currently.')
+            logger.error(error)
+            return False
+    fees = sum(t.fees for t in transactions)
+    coinbase_transaction = CoinbaseTransaction(block_hash, address, miner_reward + fees)
+    if inode_rewards:
+        coinbase_transaction.outputs.extend([TransactionOutput(a, r) for a, r in inode_rewards.items()])
+    if not all(o.verify() for o in coinbase_transaction.outputs):
+        return False
+    if not await _apply_block(block_no, block_hash, block_content, address, random, difficulty, block_reward, fees,
+                              content_time, coinbase_transaction, transactions):
+        return False
+    logger.info(f'Added {len(transactions)} transactions in block {block_no}. Reward: {block_reward}, Fees: {fees} '
+                f'in {perf_counter() - create_start_time:.3f} seconds')
+    if block_no % 10 == 0:
+        logger.info(f'unspent_outputs_hash on block no. {block_no}: {await database.get_unspent_outputs_hash()}')
+    Manager.difficulty = None
+    try:
+        details = [{'power': str(i['power']), 'emission': str(i['emission']), 'wallet': i['wallet'],
+                    'inode_reward': str(inode_rewards.get(i['wallet'], ''))} for i in active_inodes]
+        database.emission_details.set(str(block_no), details)
+    except Exception as e:
+        logger.error(f'Error in creating block: {block_no} {str(e)}')
+    return True
+
+
+async def create_block_in_syncing_old(block_content: str, transactions: List[Transaction],
+                                      cb_transaction: CoinbaseTransaction, last_block: dict = None,
+                                      error_list=None) -> bool:
+    """manager.py:760-835: sync path, trusts the supplied coinbase."""
+    if error_list is None:
+        error_list = []
+    create_start_time = perf_counter()
+    Manager.difficulty = None
+    if last_block is None or last_block['id'] % BLOCKS_COUNT == 0:
+        difficulty, last_block = await calculate_difficulty()
+    else:
+        difficulty, last_block = await get_difficulty()
+    block_no = last_block['id'] + 1 if last_block != {} else 1
+    logger.info(f'Syncing block no. {block_no}')
+    if not await check_block(block_content, transactions, (difficulty, last_block), error_list=error_list):
+        return False
+    block_hash = sha256(block_content)
+    previous_hash, address, merkle_tree, content_time, content_difficulty, random = split_block_content(block_content)
+    block_reward = get_block_reward(block_no)
+    fees = sum(t.fees for t in transactions)
+    if cb_transaction is None or not all(o.verify() for o in cb_transaction.outputs):
+        return False
+    if not await _apply_block(block_no, block_hash, block_content, address, random, difficulty, block_reward, fees,
+                              content_time, cb_transaction, transactions):
+        return False
+    logger.info(f'Added {len(transactions)} transactions in block {block_no}. Reward: {block_reward}, Fees: {fees} '
+                f'in {perf_counter() - create_start_time:.3f} seconds')
+    if block_no % 10 == 0:
+        logger.info(f'unspent_outputs_hash on block no. {block_no}: '
+                    f'{await Database.instance.get_unspent_outputs_hash()}')
+    Manager.difficulty = None
+    return True
+
+
+double_spend_dict = {
+    286523: [
+        ('16c519171bfa7ee7d42af0d84fe731433048a1aedfd5df692b8beaa755ef6eb9', 0),
+        ('747d753fcfecdce5d3a080666ff139ca9123d72d2eb529386f2c3f9f4a55f983', 1),
+        ('856b36ecd55a3a427cc988550457435ee9dd7580a423bc3177c1d173b50ff101', 1),
+        ('af33808f839698734d801e907f1eb1c24c3547d4cdd984ed0f2e41c58c6d1d9a', 1),
+        ('db843078e1fd5f1bbf1c2f550f87548df6fe714ccd12a0ba4a1e25e10fea3ae0', 1),
+        ('eb10fd11319aeee7a21766b85c89580f6c3f509a6afaf743df717ca91d33e0da', 1),
+    ],
+    347027: [
+        ('4fd22d5ca99eaa044288de9f850385cbf758efdc4967a92623138e986ce4316e', 2),
+        ('b88e9beef7559d48d99ea82e71f7c0601981d6972021feb929c04bc7b52368c2', 1),
+        ('ed0f9e07d97ab8a5dc7b8e68ad631a5e78f3cfb6ee6f2aa013854caa64a7b1ae', 1),
+    ],
+    347034: [('047f5c343dcd15a16c44b3f05fe98bc467002405490ecfb517652207e5425858', 2)],
+    349122: [
+        ('691695269d8baa441b8e1638a17b3b8497295ec8322c750e8b5312768d4b9ce5', 1),
+        ('f7894d0cab92445bd1bb7681106d8fb18d9b4af2465db8a73efbdb97431f855f', 1),
+    ],
+    395735: [
+        ('461c359b956773ff97af6d2189ae84bcc52740e077224efc80b8b5826b51cb92', 1),
+        ('ef573f3543ef22b087387fd81493cc7bc977adcc1ff4198483a98a67a6d10e6b', 1),
+        ('9efcb290e4c24843bab40dc50591680ac897e52a28db62c7594e4a2b07702291', 1),
+    ],
+    395736: [
+        ('d8421370cef17939c4a2b17c21c7674059c0c24766e80d6129c666f11e886e08', 1),
+        ('af2422540ef2f4570b998b262c242b37f7f0e44fbadabcb0f52684dd0ce1ace5', 1),
+    ],
+}
+
+
+# ---------------------------------------------------------------------------------------------- inode cache
+async def update_cache() -> None:
+    global cache_updating
+    if cache_updating:
+        return
+    cache_updating = True
+    try:
+        cache['inodes'] = await Database.instance.get_active_inodes()
+        cache['timestamp'] = datetime.utcnow()
+    finally:
+        cache_updating = False
+
+
+async def update_active_inodes_cache_with_data(active_inodes) -> None:
+    cache['inodes'] = active_inodes
+    cache['timestamp'] = datetime.utcnow()
+
+
+async def get_inodes_from_cache() -> list:
+    """manager.py:886-900 (5 min cache, refreshed in the background)."""
+    now = datetime.utcnow()
+    if 'inodes' in cache and (now - cache['timestamp']) < cache_expiration:
+        return cache['inodes']
+    if not cache:
+        await update_cache()
+    else:
+        asyncio.create_task(update_cache())
+    return cache.get('inodes', [])
+
+
+__all__ = ['Manager', 'calculate_difficulty', 'get_difficulty', 'check_block_is_valid', 'get_block_reward',
+           'get_inode_rewards', 'get_circulating_supply', 'clear_pending_transactions', 'check_block',
+           'create_block', 'create_block_in_syncing_old', 'get_transactions_merkle_tree', 'block_to_bytes',
+           'split_block_content', 'get_inodes_from_cache', 'double_spend_dict', 'get_transactions_merkle_tree_ordered']

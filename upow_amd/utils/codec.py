@@ -152,25 +152,63 @@ def point_to_bytes(point: Point, address_format: AddressFormat = AddressFormat.F
     raise NotImplementedError()
 
 
-@lru_cache(maxsize=1 << 16)
-def _decompress(point_bytes: bytes) -> Point:
+_POINT_CACHE: dict = {}
+_POINT_CACHE_MAX = 1 << 20
+
+
+def _cache_put(key: bytes, value):
+    if len(_POINT_CACHE) >= _POINT_CACHE_MAX:
+        _POINT_CACHE.clear()
+    _POINT_CACHE[key] = value
+
+
+def _decode_point(point_bytes: bytes) -> Point:
+    if len(point_bytes) == 64:
+        return Point(int.from_bytes(point_bytes[:32], ENDIAN), int.from_bytes(point_bytes[32:], ENDIAN))
     specifier = point_bytes[0]
     x = int.from_bytes(point_bytes[1:], ENDIAN)
     return Point(x, p256.x_to_y(x, specifier == 43))
 
 
-@lru_cache(maxsize=1 << 16)
-def _full_point(point_bytes: bytes) -> Point:
-    return Point(int.from_bytes(point_bytes[:32], ENDIAN), int.from_bytes(point_bytes[32:], ENDIAN))
-
-
 def bytes_to_point(point_bytes: bytes) -> Point:
     """helpers.py:135-144. Raises ValueError for off-curve coordinates (fastecdsa Point ctor)."""
-    if len(point_bytes) == 64:
-        return _full_point(bytes(point_bytes))
-    elif len(point_bytes) == 33:
-        return _decompress(bytes(point_bytes))
-    raise NotImplementedError()
+    point_bytes = bytes(point_bytes)
+    if len(point_bytes) not in (33, 64):
+        raise NotImplementedError()
+    hit = _POINT_CACHE.get(point_bytes)
+    if hit is None:
+        try:
+            hit = _decode_point(point_bytes)
+        except ValueError as e:
+            hit = e
+        _cache_put(point_bytes, hit)
+    if isinstance(hit, Exception):
+        raise ValueError(str(hit))
+    return hit
+
+
+def prefetch_points(addresses_bytes) -> None:
+    """Batch-decompress every uncached 33-byte address (gfx950 kernel for large batches, host C++
+    otherwise) so the per-tx validation code never runs a Python square root."""
+    todo = []
+    for b in addresses_bytes:
+        b = bytes(b)
+        if len(b) == 33 and b not in _POINT_CACHE:
+            todo.append(b)
+        elif len(b) == 64 and b not in _POINT_CACHE:
+            try:
+                _cache_put(b, _decode_point(b))
+            except ValueError as e:
+                _cache_put(b, e)
+    todo = list(dict.fromkeys(todo))
+    if not todo:
+        return
+    from ..ops.p256 import decompress
+    for b, xy in zip(todo, decompress(todo)):
+        if xy is None:
+            _cache_put(b, ValueError('coordinates are not on curve P256'))
+        else:
+            _cache_put(b, Point(xy[0], xy[1], check=False))
 
 
 def round_up_decimal(decimal: Decimal, round_up_length: str = '0.00000001'):
