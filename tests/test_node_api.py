@@ -1,0 +1,123 @@
+"""Node REST + WebSocket API through starlette's TestClient (single node, in-process)."""
+import asyncio
+import hashlib
+import os
+from decimal import Decimal
+
+import pytest
+
+KEY_A = 0x1111111111111111111111111111111111111111111111111111111111111111
+KEY_B = 0x2222222222222222222222222222222222222222222222222222222222222222
+
+
+@pytest.fixture
+def node(tmp_path, monkeypatch):
+    monkeypatch.setenv('UPOW_DATA_DIR', str(tmp_path))
+    monkeypatch.setenv('UPOW_CORE_URL', '')
+    monkeypatch.setenv('UPOW_DATABASE_PATH', str(tmp_path / 'ledger.sqlite3'))
+    monkeypatch.setenv('UPOW_UTXO_BACKEND', 'host')
+    from upow_amd.ledger import manager
+    monkeypatch.setattr(manager, 'START_DIFFICULTY', Decimal('1.5'))
+    manager.Manager.difficulty = None
+    from upow_amd.node import main
+    from upow_amd.node.nodes_manager import NodesManager
+    NodesManager.path = None
+    main.limiter.reset()
+    main.transactions_cache.clear()
+    from starlette.testclient import TestClient
+    with TestClient(main.app, base_url='http://testserver') as c:
+        yield c, main
+    main.db.close()
+
+
+def _mine(client, address, ts, txs=()):
+    from upow_amd.models.block import PowTarget, header_prefix
+    from upow_amd.ops.pow import PowJob, search
+    info = client.get('/get_mining_info').json()['result']
+    last = info['last_block']
+    prev = last.get('hash', (18_884_643).to_bytes(32, 'little').hex())
+    hashes = info['pending_transactions_hashes'] if not txs else sorted(hashlib.sha256(bytes.fromhex(t)).hexdigest() for t in txs)
+    merkle = hashlib.sha256(b''.join(bytes.fromhex(h) for h in hashes)).hexdigest()
+    job = PowJob.create(header_prefix(prev, address, merkle, ts, info['difficulty']),
+                        PowTarget.from_difficulty(prev, info['difficulty']))
+    r = search(job, 0, 1 << 20, device='cpu', threads=2)
+    content = job.header_with_nonce(r.nonces[0]).hex()
+    return client.post('/push_block', json={'block_content': content, 'txs': hashes, 'block_no': last.get('id', 0) + 1}).json()
+
+
+def test_mining_flow_and_queries(node):
+    client, main = node
+    from upow_amd.wallet.builders import address_of
+    a, b = address_of(KEY_A), address_of(KEY_B)
+    r = client.get('/get_mining_info').json()
+    assert r['ok'] and r['result']['difficulty'] == 1.5 and r['result']['last_block'] == {}
+    base = 1_700_000_000
+    for k in range(1, 4):
+        assert _mine(client, a, base + k) == {'ok': True}
+    info = client.get('/get_address_info', params={'address': a}).json()
+    assert info['result']['balance'] == '18'
+    assert len(info['result']['spendable_outputs']) == 3
+    blk = client.get('/get_block', params={'block': '2'}).json()['result']
+    assert blk['block']['id'] == 2 and len(blk['transactions']) == 1
+    assert client.get('/get_block', params={'block': blk['block']['hash']}).json()['result']['block']['id'] == 2
+    blocks = client.get('/get_blocks', params={'offset': 1, 'limit': 10}).json()['result']
+    assert [x['block']['id'] for x in blocks] == [1, 2, 3]
+    # push a transfer and mine it by hash
+    async def mk():
+        from upow_amd.wallet.builders import create_transaction
+        return await create_transaction(KEY_A, b, '1.25')
+    tx = asyncio.run(mk())
+    res = client.post('/push_tx', json={'tx_hex': tx.hex()}).json()
+    assert res['ok'], res
+    assert client.get('/push_tx', params={'tx_hex': tx.hex()}).json() == {'ok': False, 'error': 'Transaction just added'}
+    assert client.get('/get_pending_transactions').json()['result'] == [tx.hex()]
+    mi = client.get('/get_mining_info').json()['result']
+    assert mi['pending_transactions_hashes'] == [tx.hash()]
+    assert _mine(client, a, base + 10) == {'ok': True}
+    assert client.get('/get_address_info', params={'address': b}).json()['result']['balance'] == '1.25'
+    t = client.get('/get_transaction', params={'tx_hash': tx.hash()}).json()
+    assert t['ok'] and t['result']['outputs'][0]['amount'] == 1.25
+    txs = client.get('/get_address_transactions', params={'address': b}).json()['result']['transactions']
+    assert [x['hash'] for x in txs] == [tx.hash()]
+    root = client.get('/').json()
+    assert root['ok'] and root['version'] == 2 and len(root['unspent_outputs_hash']) == 64
+    sup = client.get('/get_supply_info').json()['result']
+    assert sup['circulating_supply'] == 24 and sup['max_supply'] == 18884643.75
+    # errors / envelopes
+    assert client.get('/get_block', params={'block': '99'}).json() == {'ok': False, 'error': 'Block not found'}
+    old = _mine(client, a, base + 5)
+    assert old['ok'] is False
+    assert client.get('/get_transaction', params={'tx_hash': '00' * 32}).json()['ok'] is False
+
+
+def test_rate_limit_and_ip_filter(node):
+    client, main = node
+    for _ in range(3):
+        assert client.get('/').status_code == 200
+    r = client.get('/')
+    assert r.status_code == 429 and r.json()['error'].startswith('Rate limit exceeded')
+    r = client.get('/get_nodes//', follow_redirects=False)
+    assert r.status_code in (302, 307)
+    main.ip_filter.block_endpoints = {'/get_nodes'}
+    main.ip_filter.last_update = 1e18
+    assert client.get('/get_nodes').status_code == 403
+    main.ip_filter.block_endpoints = set()
+    assert client.get('/send_to_address', params={'to_address': 'x', 'amount': 1}).status_code == 403
+
+
+def test_websocket_protocol(node):
+    client, main = node
+    with client.websocket_connect('/ws') as ws:
+        ws.send_json({'type': 'ping'})
+        assert ws.receive_json()['type'] == 'pong'
+        ws.send_json({'type': 'subscribe_block'})
+        m1, m2 = ws.receive_json(), ws.receive_json()
+        assert m1['type'] == 'success' and m1['data'] == {'channel': 'block'}
+        assert m2['message'] == 'Subscribed to block updates'
+        from upow_amd.wallet.builders import address_of
+        assert _mine(client, address_of(KEY_A), 1_700_000_001) == {'ok': True}
+        ev = ws.receive_json()
+        assert ev['type'] == 'new_block' and ev['data']['block_no'] == 1
+        ws.send_json({'type': 'subscribe_transaction'})
+        err = ws.receive_json()
+        assert err['type'] == 'error' and err['error_code'] == 'INVALID_MESSAGE_TYPE'

@@ -1,0 +1,648 @@
+"""uPow full-node HTTP service (reference: upow/node/main.py:55-1102).
+
+Same routes, parameters, rate limits, response envelopes, middleware behaviour (IP filter, path
+normalisation, Sender-Node peer learning, localhost-only /send_to_address, peer bootstrap,
+re-propagation of stale mempool txs), gossip fan-out, chain sync with fork rollback and the /ws
+WebSocket. The ledger is the embedded store + HBM UTXO index (:mod:`upow_amd.ledger.database`) and
+block validation runs the batched GPU pipeline (:mod:`upow_amd.ledger.validate`).
+
+Run: ``python -m upow_amd.node --host 0.0.0.0 --port 3006`` (uvicorn).
+"""
+from __future__ import annotations
+
+import json
+import os
+import random
+import re
+from asyncio import gather
+from collections import defaultdict, deque
+from contextlib import asynccontextmanager
+from decimal import Decimal
+from typing import Annotated, Union
+
+from fastapi import Body, FastAPI, Header, Query
+from fastapi.responses import RedirectResponse
+from starlette.background import BackgroundTask, BackgroundTasks
+from starlette.middleware.cors import CORSMiddleware
+from starlette.requests import Request
+from starlette.responses import JSONResponse
+
+from .. import config
+from ..constants import ENDIAN, GENESIS_PREV_HASH, MAX_SUPPLY, VERSION
+from ..ledger import manager as mgr
+from ..ledger.database import Database, UniqueViolationError
+from ..ledger.manager import (Manager, block_to_bytes, calculate_difficulty, clear_pending_transactions, create_block,
+                              create_block_in_syncing_old, get_circulating_supply, get_difficulty,
+                              get_inodes_from_cache, get_transactions_merkle_tree, split_block_content)
+from ..models.transaction import CoinbaseTransaction, Transaction
+from ..utils import codec
+from ..utils.codec import sha256, timestamp
+from ..utils.logger import get_logger
+from ..websocket.endpoint import (broadcast_new_block, broadcast_new_transaction, shutdown_websocket_manager,
+                                  start_websocket_manager, websocket_router)
+from .ip_manager import IPManager
+from .nodes_manager import NodeInterface, NodesManager
+from .ratelimit import Limiter, RateLimitExceeded, get_remote_address, rate_limit_exceeded_handler
+from .utils import ip_is_local
+
+logger = get_logger(__name__)
+limiter = Limiter(key_func=get_remote_address, enabled=os.environ.get('UPOW_RATE_LIMIT', '1') == '1')
+
+db: Database = None
+started = False
+is_syncing = False
+self_url = None
+ip_filter: IPManager = None
+transactions_cache = deque(maxlen=100)
+LAST_PENDING_TRANSACTIONS_CLEAN = [0]
+BANNED_SENDERS = ['DgQKikeDqS2Fzue23KuA36L4eJSFh649zA9jJ6zwbzUMp']  # main.py:426
+
+
+@asynccontextmanager
+async def lifespan(app: FastAPI):
+    await startup()
+    try:
+        yield
+    finally:
+        await shutdown_websocket_manager()
+
+
+async def startup():
+    """main.py:246-257: open the ledger (UPOW_DATABASE_PATH, default <data dir>/ledger.sqlite3)."""
+    global db, ip_filter
+    NodesManager.init()
+    ip_filter = IPManager()
+    path = os.environ.get('UPOW_DATABASE_PATH') or config.data_path('ledger.sqlite3')
+    db = await Database.create(path=path)
+    await start_websocket_manager()
+
+
+app = FastAPI(lifespan=lifespan)
+app.state.limiter = limiter
+app.add_exception_handler(RateLimitExceeded, rate_limit_exceeded_handler)
+app.add_middleware(CORSMiddleware, allow_origins=['*'], allow_methods=['GET', 'POST'], allow_headers=['*'])
+app.include_router(websocket_router)
+
+
+# ---------------------------------------------------------------------------------------------- gossip
+async def propagate(path: str, args: dict, ignore_url=None, nodes: list = None):
+    """main.py:79-94: fan out to <=10 recent + <=10 never-heard-from peers."""
+    self_node = NodeInterface(self_url or '')
+    ignore_node = NodeInterface(ignore_url or '')
+    aws = []
+    for node_url in nodes or NodesManager.get_propagate_nodes():
+        ni = NodeInterface(node_url)
+        if ni.base_url == self_node.base_url or ni.base_url == ignore_node.base_url:
+            continue
+        aws.append(ni.request(path, args, self_node.url))
+    await gather(*aws, return_exceptions=True)
+
+
+# ---------------------------------------------------------------------------------------------- sync
+async def create_blocks(blocks: list, error_list=None) -> bool:
+    """main.py:97-150."""
+    if error_list is None:
+        error_list = []
+    _, last_block = await calculate_difficulty()
+    last_block['id'] = last_block['id'] if last_block != {} else 0
+    last_block['hash'] = last_block['hash'] if 'hash' in last_block else GENESIS_PREV_HASH
+    i = last_block['id'] + 1
+    for block_info in blocks:
+        block = block_info['block']
+        txs = [await Transaction.from_hex(tx) for tx in block_info['transactions']]
+        cb_tx = None
+        for tx in txs:
+            if isinstance(tx, CoinbaseTransaction):
+                txs.remove(tx)
+                cb_tx = tx
+                break
+        block['merkle_tree'] = get_transactions_merkle_tree([tx.hex() for tx in txs])
+        block_content = block.get('content') or block_to_bytes(last_block['hash'], block)
+        assert i == block['id']
+        if not await create_block_in_syncing_old(
+                block_content.hex() if isinstance(block_content, bytes) else block_content, txs, cb_tx, last_block,
+                error_list=error_list):
+            return False
+        last_block = block
+        i += 1
+    return True
+
+
+async def _sync_blockchain(node_url: str = None):
+    """main.py:153-227: pull pages of 1000 blocks; on a fork (height > 500) roll back to the last
+    common block among the last 500 and re-apply; on failure restore the cached local chain."""
+    logger.info('sync blockchain')
+    error = []
+    if not node_url:
+        nodes = NodesManager.get_recent_nodes()
+        if not nodes:
+            logger.error(msg := 'No nodes found.')
+            return msg
+        node_url = random.choice(nodes)
+    node_url = node_url.strip('/')
+    _, last_block = await calculate_difficulty()
+    starting_from = i = await db.get_next_block_id()
+    node_interface = NodeInterface(node_url)
+    local_cache = None
+    last_common_block = None
+    if last_block != {} and last_block['id'] > 500:
+        remote_last_block = (await node_interface.get_block(i - 1))['block']
+        if remote_last_block['hash'] != last_block['hash']:
+            offset, limit = i - 500, 500
+            remote_blocks = await node_interface.get_blocks(offset, limit)
+            local_blocks = await db.get_blocks(offset, limit)
+            local_blocks = local_blocks[:len(remote_blocks)]
+            local_blocks.reverse()
+            remote_blocks.reverse()
+            for n, local_block in enumerate(local_blocks):
+                if local_block['block']['hash'] == remote_blocks[n]['block']['hash']:
+                    last_common_block = local_block['block']['id']
+                    local_cache = local_blocks[:n]
+                    local_cache.reverse()
+                    await db.remove_blocks(last_common_block + 1)
+                    break
+    limit = 1000
+    while True:
+        i = await db.get_next_block_id()
+        try:
+            blocks = await node_interface.get_blocks(i, limit)
+        except Exception as e:
+            logger.error(e)
+            NodesManager.sync()
+            break
+        try:
+            _, last_block = await calculate_difficulty()
+            if not blocks:
+                logger.info('syncing complete')
+                if last_block['id'] > starting_from:
+                    NodesManager.update_last_message(node_url)
+                    if timestamp() - last_block['timestamp'] < 86400:
+                        txs_hashes = await db.get_block_transaction_hashes(last_block['hash'])
+                        await propagate('push_block', {'block_content': last_block['content'], 'txs': txs_hashes,
+                                                       'block_no': last_block['id']}, node_url)
+                return True
+            assert await create_blocks(blocks, error_list=error)
+        except Exception as e:
+            logger.error(error[0] if error else e)
+            if local_cache is not None:
+                logger.info('sync failed, reverting back to previous chain')
+                await db.delete_blocks(last_common_block)
+                await create_blocks(local_cache)
+            return error[0] if error else e
+
+
+async def sync_blockchain(node_url: str = None):
+    global is_syncing
+    sync_status = None
+    try:
+        is_syncing = True
+        codec.is_blockchain_syncing = True
+        sync_status = await _sync_blockchain(node_url)
+    except Exception as e:
+        logger.error(f'sync_blockchain error: {e}')
+    finally:
+        is_syncing = False
+        codec.is_blockchain_syncing = False
+    return sync_status
+
+
+# ---------------------------------------------------------------------------------------------- middleware
+async def propagate_old_transactions(propagate_txs):
+    await db.update_pending_transactions_propagation_time([sha256(tx_hex) for tx_hex in propagate_txs])
+    for tx_hex in propagate_txs:
+        await propagate('push_tx', {'tx_hex': tx_hex})
+
+
+async def get_ip_address_from_header(request: Request):
+    xff = request.headers.get('x-forwarded-for', '')
+    visitor_ip = xff.split(',')[0].strip() if xff else request.headers.get('x-real-ip', None)
+    if not visitor_ip and request.client:
+        visitor_ip = request.client.host
+    return visitor_ip
+
+
+@app.middleware('http')
+async def middleware(request: Request, call_next):
+    """main.py:286-372."""
+    global started, self_url
+    nodes = NodesManager.get_recent_nodes()
+    hostname = request.base_url.hostname
+    client_ip = await get_ip_address_from_header(request)
+    if not ip_filter.is_ip_allowed(client_ip):
+        return JSONResponse(status_code=403, content={'ok': False, 'error': 'Access forbidden.'})
+    normalized_path = re.sub('/+', '/', request.scope['path'])
+    if normalized_path != request.scope['path']:
+        return RedirectResponse(str(request.url).replace(request.scope['path'], normalized_path))
+    if ip_filter.is_endpoint_blocked(normalized_path):
+        return JSONResponse(status_code=403, content={'ok': False, 'error': 'Access forbidden temporarily.'})
+    if 'Sender-Node' in request.headers and request.headers['Sender-Node']:
+        NodesManager.add_node(request.headers['Sender-Node'])
+    local = ip_is_local(hostname) or hostname == 'localhost'
+    if normalized_path == '/send_to_address' and not local:
+        return JSONResponse(status_code=403, content={
+            'ok': False, 'error': 'Access forbidden. This endpoint can only be accessed from localhost.'})
+    if normalized_path != '/get_nodes' and (nodes and not started or local):
+        try:
+            if not started:
+                node_url = nodes[0]
+                j = await NodesManager.request(f'{node_url}/get_nodes')
+                nodes.extend(j['result'])
+                NodesManager.sync()
+                if not local:
+                    started = True
+                    self_url = str(request.base_url).strip('/')
+                    for candidate in (self_url, self_url.replace('http://', 'https://')):
+                        try:
+                            nodes.remove(candidate)
+                        except ValueError:
+                            pass
+                    NodesManager.sync()
+                    try:
+                        await propagate('add_node', {'url': self_url})
+                        cousin_nodes = await NodeInterface(node_url).get_nodes()
+                        await propagate('add_node', {'url': self_url}, nodes=cousin_nodes)
+                    except Exception:
+                        pass
+        except Exception:
+            pass
+    propagate_txs = await db.get_need_propagate_transactions()
+    response = await call_next(request)
+    response.headers['Access-Control-Allow-Origin'] = '*'
+    if propagate_txs:
+        response.background = BackgroundTask(propagate_old_transactions, propagate_txs)
+    return response
+
+
+@app.exception_handler(Exception)
+async def exception_handler(request: Request, e: Exception):
+    """main.py:393-405."""
+    logger.error(f"Error on {request.scope['path']}, {type(e).__name__}: {str(e)}")
+    if type(e).__name__ in ('Exception', 'AssertionError'):
+        return JSONResponse(status_code=500, content={'ok': False, 'error': f'Exception: {str(e)}'})
+    return JSONResponse(status_code=500, content={'ok': False, 'error': f'Uncaught {type(e).__name__} exception'})
+
+
+# ---------------------------------------------------------------------------------------------- endpoints
+@app.get('/')
+@limiter.limit('3/minute')
+async def root(request: Request):
+    unspent_outputs_hash = await db.get_unspent_outputs_hash()
+    logger.info(f'unspent_outputs_hash: {unspent_outputs_hash}')
+    return {'ok': True, 'version': VERSION, 'unspent_outputs_hash': unspent_outputs_hash}
+
+
+async def verify_and_push_tx(tx: Transaction, request: Request, background_tasks: BackgroundTasks):
+    """main.py:417-458."""
+    tx_hash = tx.hash()
+    if tx_hash in transactions_cache:
+        logger.error(error_msg := 'Transaction just added')
+        return {'ok': False, 'error': error_msg}
+    try:
+        sender = await tx.inputs[0].get_address()
+        if sender in BANNED_SENDERS:
+            return JSONResponse(status_code=403, content={'ok': False, 'error': 'Access forbidden temporarily.'})
+        if await db.add_pending_transaction(tx):
+            if 'Sender-Node' in request.headers:
+                NodesManager.update_last_message(request.headers['Sender-Node'])
+            background_tasks.add_task(propagate, 'push_tx', {'tx_hex': tx.hex()})
+            tx_data = {'tx_hash': tx_hash, 'from': await tx.inputs[0].get_address() if tx.inputs else None,
+                       'to': [o.address for o in tx.outputs], 'amount': sum(o.amount for o in tx.outputs),
+                       'fees': tx.fees}
+            background_tasks.add_task(broadcast_new_transaction, tx_data)
+            transactions_cache.append(tx_hash)
+            logger.info(f'Transaction has been accepted: {tx_hash}')
+            return {'ok': True, 'result': 'Transaction has been accepted', 'tx_hash': tx_hash}
+        logger.error(error_msg := 'Transaction has not been added')
+        return {'ok': False, 'error': error_msg}
+    except UniqueViolationError:
+        logger.error(error_msg := 'Transaction already present')
+        return {'ok': False, 'error': error_msg}
+
+
+@app.get('/push_tx')
+@app.post('/push_tx')
+async def push_tx(request: Request, background_tasks: BackgroundTasks, tx_hex: str = None, body=Body(False)):
+    if is_syncing:
+        logger.warning(error := 'Node is already syncing')
+        return {'ok': False, 'error': error}
+    if body and tx_hex is None:
+        tx_hex = body['tx_hex']
+    tx = await Transaction.from_hex(tx_hex)
+    return await verify_and_push_tx(tx, request, background_tasks)
+
+
+@app.get('/send_to_address')
+@app.post('/send_to_address')
+async def send_to_address(request: Request, background_tasks: BackgroundTasks, to_address: str = None, amount=None,
+                          body=Body(False), authorization: Annotated[Union[str, None], Header()] = None):
+    """main.py:481-518: spend from a key in key_pair_list.json (localhost only, see middleware)."""
+    from ..wallet.builders import create_transaction
+    if body:
+        to_address = body.get('to_address', to_address)
+        amount = body.get('amount', amount)
+    if not to_address or not amount:
+        return JSONResponse(status_code=422, content={'ok': False, 'error': 'Missing required params.'})
+    amount = str(amount)
+    selected_private_key = None
+    key_file = os.environ.get('UPOW_KEY_FILE') or config.data_path('key_pair_list.json')
+    with open(key_file) as f:
+        data = json.load(f)
+    for key in data.get('keys') or []:
+        if key.get('public_key') == authorization:
+            selected_private_key = key.get('private_key')
+    if not selected_private_key:
+        return {'ok': False, 'error': 'Unauthorized'}
+    if isinstance(selected_private_key, str):
+        selected_private_key = int(selected_private_key, 16) if not selected_private_key.isdigit() \
+            else int(selected_private_key)
+    tx = await create_transaction(selected_private_key, to_address, amount, None)
+    return await verify_and_push_tx(tx, request, background_tasks)
+
+
+@app.post('/push_block')
+@app.get('/push_block')
+async def push_block(request: Request, background_tasks: BackgroundTasks, block_content: str = '', txs='',
+                     block_no: int = None, body=Body(False)):
+    """main.py:521-652."""
+    if is_syncing:
+        return {'ok': False, 'error': 'Node is already syncing'}
+    if codec.getting_active_inodes:
+        return {'ok': False, 'error': 'Server is busy'}
+    if body:
+        txs = body['txs']
+        if 'block_content' in body:
+            block_content = body['block_content']
+        if 'id' in body:
+            return {'ok': False, 'error': 'Deprecated'}
+        if 'block_no' in body:
+            block_no = body['block_no']
+    if isinstance(txs, str):
+        txs = txs.split(',')
+        if txs == ['']:
+            txs = []
+    previous_hash = split_block_content(block_content)[0]
+    next_block_id = await db.get_next_block_id()
+    sender = request.headers.get('Sender-Node')
+    if block_no is None:
+        previous_block = await db.get_block(previous_hash)
+        if previous_block is None:
+            if sender:
+                background_tasks.add_task(sync_blockchain, sender)
+                return {'ok': False, 'error': 'Previous hash not found, had to sync according to sender node, '
+                                              'block may have been accepted'}
+            return {'ok': False, 'error': 'Previous hash not found'}
+        block_no = previous_block['id'] + 1
+    if next_block_id < block_no:
+        background_tasks.add_task(sync_blockchain, sender if sender else None)
+        return {'ok': False, 'error': 'Blocks missing, had to sync according to sender node, block may have been '
+                                      'accepted'}
+    if next_block_id > block_no:
+        return {'ok': False, 'error': 'Too old block'}
+    final_transactions, hashes = [], []
+    for tx_hex in txs:
+        if len(tx_hex) == 64:
+            hashes.append(tx_hex)
+        else:
+            final_transactions.append(await Transaction.from_hex(tx_hex))
+    if hashes:
+        pending_transactions = await db.get_pending_transactions_by_hash(hashes)
+        if len(pending_transactions) < len(hashes):
+            if sender:
+                background_tasks.add_task(sync_blockchain, sender)
+                return {'ok': False, 'error': 'Transaction hash not found, had to sync according to sender node, '
+                                              'block may have been accepted'}
+            return {'ok': False, 'error': 'Transaction hash not found'}
+        final_transactions.extend(pending_transactions)
+    error_list = []
+    if not await create_block(block_content, final_transactions, error_list=error_list):
+        return {'ok': False, 'error': error_list[0]} if error_list else {'ok': False}
+    block_hash = sha256(block_content)
+    Manager.difficulty = None
+    difficulty, last_block = await get_difficulty()
+    pending = sorted(await db.get_pending_transactions_limit(hex_only=True))
+    if LAST_PENDING_TRANSACTIONS_CLEAN[0] < timestamp() - 600:
+        LAST_PENDING_TRANSACTIONS_CLEAN[0] = timestamp()
+        background_tasks.add_task(clear_pending_transactions, pending)
+    block_data = {'block_no': block_no, 'block_hash': block_hash, 'transactions_count': len(final_transactions),
+                  'timestamp': timestamp(), 'difficulty': difficulty, 'last_block': last_block,
+                  'pending_transactions': pending[:10], 'pending_transactions_hashes': [sha256(t) for t in pending],
+                  'merkle_root': get_transactions_merkle_tree(pending[:10])}
+    background_tasks.add_task(broadcast_new_block, block_data)
+    if sender:
+        NodesManager.update_last_message(sender)
+    background_tasks.add_task(propagate, 'push_block', {
+        'block_content': block_content,
+        'txs': [tx.hex() for tx in final_transactions] if len(final_transactions) < 10 else txs,
+        'block_no': block_no})
+    return {'ok': True}
+
+
+@app.get('/sync_blockchain')
+@limiter.limit('10/minute')
+async def sync(request: Request, node_url: str = None):
+    if is_syncing:
+        logger.warning(msg := 'Node is already syncing')
+        return {'ok': False, 'error': msg}
+    resp = await sync_blockchain(node_url)
+    if isinstance(resp, str):
+        return {'ok': False, 'error': resp}
+    if isinstance(resp, Exception):
+        return {'ok': False, 'error': str(resp)}
+    return {'ok': resp}
+
+
+@app.get('/get_mining_info')
+@limiter.limit('30/minute')
+async def get_mining_info(request: Request, background_tasks: BackgroundTasks):
+    """main.py:675-695."""
+    Manager.difficulty = None
+    difficulty, last_block = await get_difficulty()
+    pending = sorted(await db.get_pending_transactions_limit(hex_only=True))
+    if LAST_PENDING_TRANSACTIONS_CLEAN[0] < timestamp() - 600:
+        LAST_PENDING_TRANSACTIONS_CLEAN[0] = timestamp()
+        background_tasks.add_task(clear_pending_transactions, pending)
+    return {'ok': True, 'result': {
+        'difficulty': difficulty, 'last_block': last_block, 'pending_transactions': pending[:10],
+        'pending_transactions_hashes': [sha256(t) for t in pending],
+        'merkle_root': get_transactions_merkle_tree(pending[:10])}}
+
+
+@app.get('/get_validators_info')
+async def get_validators_info(background_tasks: BackgroundTasks, inode: str = None, offset: int = 0,
+                              limit: int = Query(default=100, le=1000)):
+    ballot = await db.get_inode_ballot_by_address(offset, limit, inode=inode) if inode else \
+        await db.get_inode_ballot(offset, limit)
+    result = defaultdict(lambda: {'validator': '', 'vote': []})
+    for tx_hash, inode_address, votes, validator, index in ballot:
+        result[validator]['validator'] = validator
+        result[validator]['vote'].append({'wallet': inode_address, 'vote_count': votes, 'tx_hash': tx_hash,
+                                          'index': index})
+        result[validator]['totalStake'] = await db.get_validators_stake(validator, check_pending_txs=True)
+    return list(result.values())
+
+
+@app.get('/get_delegates_info')
+async def get_delegates_info(background_tasks: BackgroundTasks, validator: str = None, offset: int = 0,
+                             limit: int = Query(default=100, le=1000)):
+    ballot = await db.get_validator_ballot_by_address(offset, limit, validator=validator) if validator else \
+        await db.get_validator_ballot(offset, limit)
+    stakes = await db.get_multiple_address_stakes({d for _, _, _, d, _ in ballot}, check_pending_txs=True)
+    result = defaultdict(lambda: {'delegate': '', 'vote': [], 'totalStake': Decimal(0)})
+    for tx_hash, validator_address, votes, delegate, index in ballot:
+        result[delegate]['delegate'] = delegate
+        result[delegate]['vote'].append({'wallet': validator_address, 'vote_count': votes, 'tx_hash': tx_hash,
+                                         'index': index})
+        result[delegate]['totalStake'] = stakes.get(delegate, Decimal(0))
+    return list(result.values())
+
+
+def _outs(outputs):
+    return [{'amount': '{:f}'.format(o.amount), 'tx_hash': o.tx_hash, 'index': o.index} for o in outputs]
+
+
+@app.get('/get_address_info')
+@limiter.limit('15/second')
+async def get_address_info(request: Request, address: str, show_pending: bool = False, verify: bool = False,
+                           stake_outputs: bool = False, delegate_spent_votes: bool = False,
+                           delegate_unspent_votes: bool = False, address_state: bool = False,
+                           inode_registration_outputs: bool = False, validator_unspent_votes: bool = False,
+                           validator_spent_votes: bool = False):
+    """main.py:768-921."""
+    outputs = await db.get_spendable_outputs(address)
+    stake = await db.get_address_stake(address)
+    balance = sum(o.amount for o in outputs)
+    pending_transactions = [await db.get_nice_transaction(tx.hash(), address if verify else None)
+                            for tx in await db.get_address_pending_transactions(address, True)] \
+        if show_pending else None
+    pending_spent_outputs = await db.get_address_pending_spent_outputs(address) if show_pending else None
+    is_inode = await db.is_inode_registered(address) if address_state else None
+    is_inode_active = None
+    if address_state:
+        is_inode_active = any(e.get('wallet') == address for e in await get_inodes_from_cache()) if is_inode \
+            else False
+    is_validator = await db.is_validator_registered(address) if address_state else None
+    return {'ok': True, 'result': {
+        'balance': '{:f}'.format(balance),
+        'stake': '{:f}'.format(stake),
+        'spendable_outputs': _outs(outputs),
+        'pending_transactions': pending_transactions,
+        'pending_spent_outputs': pending_spent_outputs,
+        'stake_outputs': _outs(await db.get_stake_outputs(address)) if stake_outputs else None,
+        'delegate_spent_votes': _outs(await db.get_delegates_spent_votes(address)) if delegate_spent_votes else None,
+        'delegate_unspent_votes': _outs(await db.get_delegates_voting_power(address))
+        if delegate_unspent_votes else None,
+        'inode_registration_outputs': _outs(await db.get_inode_registration_outputs(address))
+        if inode_registration_outputs else None,
+        'validator_unspent_votes': _outs(await db.get_validators_voting_power(address))
+        if validator_unspent_votes else None,
+        'validator_spent_votes': _outs(await db.get_validators_spent_votes(address))
+        if validator_spent_votes else None,
+        'is_inode': is_inode,
+        'is_inode_active': is_inode_active,
+        'is_validator': is_validator,
+    }}
+
+
+@app.get('/get_address_transactions')
+async def get_address_transactions(request: Request, address: str, page: int = Query(default=1, ge=1),
+                                   limit: int = Query(default=5, le=1000)):
+    offset = (page - 1) * limit
+    txs = await db.get_address_transactions(address, limit=limit, offset=offset, check_signatures=True) \
+        if limit > 0 else []
+    return {'ok': True, 'result': {'transactions': [await db.get_nice_transaction(tx.hash()) for tx in txs]}}
+
+
+@app.get('/add_node')
+@limiter.limit('10/minute')
+async def add_node(request: Request, url: str, background_tasks: BackgroundTasks):
+    nodes = NodesManager.get_nodes()
+    url = url.strip('/')
+    if url == self_url:
+        return {'ok': False, 'error': 'Recursively adding node'}
+    if url in nodes:
+        return {'ok': False, 'error': 'Node already present'}
+    try:
+        assert await NodesManager.is_node_working(url)
+        background_tasks.add_task(propagate, 'add_node', {'url': url}, url)
+        NodesManager.add_node(url)
+        return {'ok': True, 'result': 'Node added'}
+    except Exception:
+        return {'ok': False, 'error': 'Could not add node'}
+
+
+@app.get('/get_nodes')
+async def get_nodes():
+    return {'ok': True, 'result': NodesManager.get_recent_nodes()[:100]}
+
+
+@app.get('/get_pending_transactions')
+async def get_pending_transactions():
+    # the reference passes 1000 as the hex-size limit (main.py:982)
+    return {'ok': True, 'result': [tx.hex() for tx in await db.get_pending_transactions_limit(1000)]}
+
+
+@app.get('/get_transaction')
+@limiter.limit('2/second')
+async def get_transaction(request: Request, tx_hash: str, verify: bool = False):
+    tx = await db.get_nice_transaction(tx_hash)
+    if tx is None:
+        return {'ok': False, 'error': 'Transaction not found'}
+    return {'ok': True, 'result': tx}
+
+
+async def _resolve_block(block: str):
+    if block.isdecimal():
+        info = await db.get_block_by_id(int(block))
+        return (info['hash'], info) if info is not None else (None, None)
+    return block, await db.get_block(block)
+
+
+@app.get('/get_block')
+@limiter.limit('30/minute')
+async def get_block(request: Request, block: str, full_transactions: bool = False):
+    block_hash, block_info = await _resolve_block(block)
+    if not block_info:
+        return {'ok': False, 'error': 'Block not found'}
+    return {'ok': True, 'result': {
+        'block': block_info,
+        'transactions': await db.get_block_transactions(block_hash, hex_only=True) if not full_transactions else None,
+        'full_transactions': await db.get_block_nice_transactions(block_hash) if full_transactions else None}}
+
+
+@app.get('/get_block_details')
+@limiter.limit('10/minute')
+async def get_block_details(request: Request, block: str):
+    block_hash, block_info = await _resolve_block(block)
+    if not block_info:
+        return {'ok': False, 'error': 'Block not found'}
+    return {'ok': True, 'result': {'block': block_info, 'transactions': [
+        await db.get_nice_transaction(h) for h in await db.get_block_transactions_hashes(block_hash)]}}
+
+
+@app.get('/get_blocks')
+@limiter.limit('40/minute')
+async def get_blocks(request: Request, offset: int, limit: int = Query(default=..., le=1000)):
+    return {'ok': True, 'result': await db.get_blocks(offset, limit)}
+
+
+@app.get('/get_blocks_details')
+@limiter.limit('10/minute')
+async def get_blocks_details(request: Request, offset: int, limit: int = Query(default=..., le=1000)):
+    return {'ok': True, 'result': await db.get_blocks(offset, limit, tx_details=True)}
+
+
+@app.get('/dobby_info')
+@limiter.limit('20/minute')
+async def dobby_info(request: Request):
+    inodes = await get_inodes_from_cache()
+    return {'ok': True, 'result': [{**item, 'emission': f"{item['emission']:.2f}%"
+                                    if isinstance(item['emission'], Decimal) else str(item['emission']) + '%'}
+                                   for item in inodes]}
+
+
+@app.get('/get_supply_info')
+@limiter.limit('20/minute')
+async def get_supply_info(request: Request):
+    last_block = await db.get_last_block()
+    return {'ok': True, 'result': {'max_supply': MAX_SUPPLY, 'circulating_supply': get_circulating_supply(
+        last_block['id']), 'last_block': last_block}}
