@@ -16,7 +16,8 @@ MAX_INODES = 12
 BLOCK_TIME = 60
 BLOCKS_COUNT = Decimal(100)
 LAST_BLOCK_FOR_GENESIS_KEY = 10000
-START_DIFFICULTY = Decimal("6.0")
+# 6.0 on mainnet; UPOW_START_DIFFICULTY overrides it for private devnets and tests only
+START_DIFFICULTY = Decimal(__import__('os').environ.get('UPOW_START_DIFFICULTY', '6.0'))
 
 # genesis "previous hash" used by miners/sync when the chain is empty (miner.py:40, main.py:105)
 GENESIS_PREV_HASH = (18_884_643).to_bytes(32, ENDIAN).hex()

@@ -1,0 +1,113 @@
+"""GPU miner CLI — same argv as the reference ``miner.py <address> [workers] [node_url]``.
+
+reference: miner.py:126-156 (fetch /get_mining_info, fork N CPU workers striding the nonce space,
+POST /push_block, refresh every <= 100 s).
+
+MI355X version:
+* one process per GPU. Single GPU: ``python -m upow_amd.miner ADDRESS``. A node with 8 GPUs:
+  ``torchrun --nproc-per-node 8 -m upow_amd.miner ADDRESS`` — rank 0 fetches the job and broadcasts it
+  over RCCL, every rank sweeps its slice of the nonce space on its GPU (``csrc/pow_search.hip``), the
+  winner's header is agreed by all-reduce and broadcast, and rank 0 submits it;
+* ``workers`` is accepted for argv compatibility and ignored on GPUs (the kernel already runs one
+  nonce per lane); on a CPU-only host it is the host-search thread count;
+* the job is refreshed every ``--refresh`` seconds (default 90, like the reference's window).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import httpx
+
+from .constants import GENESIS_PREV_HASH
+from .models.block import miner_merkle_root
+from .utils.codec import timestamp
+
+
+def fetch_mining_info(node_url: str) -> dict:
+    r = httpx.get(node_url + 'get_mining_info', timeout=5)
+    return r.json()['result']
+
+
+def submit(node_url: str, header: bytes, hashes, block_no: int) -> dict:
+    r = httpx.post(node_url + 'push_block', json={'block_content': header.hex(), 'txs': hashes, 'block_no': block_no},
+                   timeout=20 + int((len(hashes) or 1) / 3))
+    return r.json()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description='uPow MI355X miner')
+    ap.add_argument('address')
+    ap.add_argument('workers', nargs='?', type=int, default=1)
+    ap.add_argument('node_url', nargs='?', default=None)
+    ap.add_argument('--device', choices=['gpu', 'cpu'], default=None)
+    ap.add_argument('--refresh', type=float, default=90.0)
+    ap.add_argument('--chunk', type=int, default=1 << 28)
+    ap.add_argument('--extranonce', action='store_true',
+                    help='also vary the (unchecked) header difficulty field once timestamps are exhausted')
+    ap.add_argument('--blocks', type=int, default=0, help='stop after this many accepted blocks (0 = forever)')
+    a = ap.parse_args(argv)
+    from . import config
+    node_url = (a.node_url or os.environ.get('UPOW_MINING_NODE_URL') or 'http://localhost:3006/').strip('/') + '/'
+
+    from .ops.native import gpu_available, lib
+    lib()
+    from .parallel.dist import init_from_env, shutdown
+    from .parallel.miner_dp import ClusterMiner
+    ctx = init_from_env(want_gpu=a.device != 'cpu')
+    device = a.device or ('gpu' if gpu_available() else 'cpu')
+    kw = {} if device == 'gpu' else {'threads': max(1, a.workers)}
+    accepted = 0
+    try:
+        while True:
+            job = None
+            if ctx.is_main:
+                while job is None:
+                    try:
+                        job = fetch_mining_info(node_url)
+                    except Exception as e:
+                        print(e, flush=True)
+                        time.sleep(1)
+            job = json.loads(ctx.broadcast_bytes(json.dumps(job).encode() if ctx.is_main else None, src=0,
+                                                 max_len=0).decode())
+            last = job['last_block']
+            prev = last.get('hash', GENESIS_PREV_HASH)
+            block_no = last.get('id', 0) + 1
+            hashes = job['pending_transactions_hashes']
+            merkle = miner_merkle_root(hashes)
+            now = timestamp()
+            ts_min = min(now, last.get('timestamp', now - 60) + 1)
+            if ctx.is_main:
+                print(f"difficulty: {job['difficulty']}\nblock number: {last.get('id', 0)}\n"
+                      f"Confirming {len(hashes)} transactions", flush=True)
+            miner = ClusterMiner(ctx, prev, a.address, merkle, job['difficulty'], ts_max=now, ts_min=ts_min,
+                                 extranonce=a.extranonce, device=device, chunk=a.chunk, **kw)
+            t0 = time.time()
+            header = miner.mine(should_stop=lambda: time.time() - t0 > a.refresh)
+            dt = max(time.time() - t0, 1e-9)
+            rate = ctx.allreduce_sum(miner.hashes) / dt
+            if ctx.is_main:
+                print(f'{rate / 1e6:.1f} MH/s ({ctx.world} x {device})', flush=True)
+                if header is not None:
+                    print(header.hex())
+                    print(','.join(hashes))
+                    try:
+                        result = submit(node_url, header, hashes, block_no)
+                    except Exception as e:
+                        result = {'ok': False, 'error': str(e)}
+                    print(result, flush=True)
+                    if result.get('ok'):
+                        print('BLOCK MINED\n', flush=True)
+                        accepted += 1
+            accepted = ctx.allreduce_sum(accepted if ctx.is_main else 0)
+            if a.blocks and accepted >= a.blocks:
+                break
+    finally:
+        shutdown(ctx)
+
+
+if __name__ == '__main__':
+    sys.exit(main())

@@ -155,3 +155,14 @@ def header_prefix(prev_hash: str, address: str, merkle_root: str, ts: int, diffi
     if len(wallet) == 33:
         pre = bytes([2]) + pre
     return pre
+
+
+def header_prefix_raw(prev_hash: str, address: str, merkle_root: str, ts: int, difficulty_field: int) -> bytes:
+    """Like :func:`header_prefix` but with an explicit u16 difficulty field. The reference node parses
+    but never checks that field (upow/manager.py:431), so miners may use it as an extra nonce."""
+    wallet = string_to_bytes(address)
+    pre = (bytes.fromhex(prev_hash) + wallet + bytes.fromhex(merkle_root) + int(ts).to_bytes(4, ENDIAN)
+           + int(difficulty_field).to_bytes(2, ENDIAN))
+    if len(wallet) == 33:
+        pre = bytes([2]) + pre
+    return pre

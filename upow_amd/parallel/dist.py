@@ -61,14 +61,22 @@ class DistContext:
         return int(t.item())
 
     def broadcast_bytes(self, data: Optional[bytes], src: int, max_len: int = 256) -> bytes:
-        """Broadcast a short byte string (e.g. a 108-byte header) from ``src``."""
+        """Broadcast a byte string from ``src``. Payloads up to ``max_len`` (e.g. the 108-byte header)
+        take ONE fixed-size RCCL broadcast; longer ones (a mining job with thousands of tx hashes)
+        first broadcast their length."""
         if not self.is_distributed:
             return bytes(data or b'')
         import torch
         import torch.distributed as dist
-        buf = torch.zeros(max_len + 4, dtype=torch.uint8, device=self.device)
+        n_src = len(data) if (self.rank == src and data is not None) else 0
+        size = max_len
+        if max_len <= 0:
+            t = self._t([n_src])
+            dist.broadcast(t, src=src)
+            size = int(t.item())
+        buf = torch.zeros(size + 4, dtype=torch.uint8, device=self.device)
         if self.rank == src:
-            assert data is not None and len(data) <= max_len
+            assert data is not None and len(data) <= size, 'payload larger than max_len (use max_len=0)'
             payload = len(data).to_bytes(4, 'little') + data
             buf[:len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(self.device)
         dist.broadcast(buf, src=src)

@@ -76,3 +76,70 @@ class DataParallelMiner:
             if r.header is not None:
                 return r
         raise TimeoutError('no block found')
+
+
+class ClusterMiner:
+    """Real-network nonce-space DP (used by the miner CLI).
+
+    Work units are header variants (timestamp in ``[ts_min, ts_max]`` newest first, then — only with
+    ``extranonce=True`` — the unchecked u16 difficulty field). Every unit's 2^32 nonce words are
+    split into ``world`` contiguous slices, one per rank; the ranks sweep their slice in ``chunk``
+    pieces and after each piece agree on a winner (all-reduce MIN) and broadcast its header.
+    """
+
+    def __init__(self, ctx: DistContext, prev_hash: str, address: str, merkle_root: str, difficulty,
+                 ts_max: int, ts_min: int, extranonce: bool = False, device: Optional[str] = None,
+                 chunk: int = 1 << 28, search_fn: Callable = search, **search_kw):
+        from ..models.block import header_prefix_raw
+        self.ctx = ctx
+        self.prev_hash, self.address, self.merkle = prev_hash, address, merkle_root
+        self.target = PowTarget.from_difficulty(prev_hash, difficulty)
+        self.dfield = int(float(difficulty) * 10)
+        self.ts_max, self.ts_min = int(ts_max), int(ts_min)
+        self.extranonce = extranonce
+        self.device = device
+        self.chunk = chunk
+        self.search_fn = search_fn
+        self.search_kw = search_kw
+        self._hp = header_prefix_raw
+        self.hashes = 0
+
+    def units(self):
+        for ts in range(self.ts_max, self.ts_min - 1, -1):
+            yield ts, self.dfield
+        if self.extranonce:
+            for ts in range(self.ts_max, self.ts_min - 1, -1):
+                for d in range(1 << 16):
+                    if d != self.dfield:
+                        yield ts, d
+
+    def mine(self, should_stop: Callable[[], bool] = lambda: False) -> Optional[bytes]:
+        ctx = self.ctx
+        slice_len = NONCE_SPACE // ctx.world
+        lo = ctx.rank * slice_len
+        hi = NONCE_SPACE if ctx.rank == ctx.world - 1 else lo + slice_len
+        for ts, d in self.units():
+            job = PowJob.create(self._hp(self.prev_hash, self.address, self.merkle, ts, d), self.target)
+            pos = lo
+            while True:
+                n = min(self.chunk, hi - pos)
+                nonces = []
+                if n > 0:
+                    res = self.search_fn(job, pos, n, device=self.device, **self.search_kw)
+                    nonces = res.nonces
+                    self.hashes += n
+                    pos += n
+                local = job.header_with_nonce(nonces[0]) if nonces else None
+                winner = ctx.allreduce_min(ctx.rank if local is not None else ctx.world)
+                if winner < ctx.world:
+                    header = ctx.broadcast_bytes(local if ctx.rank == winner else None, src=winner)
+                    if not self.target.check_hex(hashlib.sha256(header).hexdigest()):
+                        raise RuntimeError('broadcast header failed the PoW re-check')
+                    return header
+                stop = ctx.allreduce_min(0 if should_stop() else 1) == 0
+                done = ctx.allreduce_min(1 if pos >= hi else 0) == 1
+                if stop:
+                    return None
+                if done:
+                    break
+        return None
