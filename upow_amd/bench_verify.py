@@ -1,0 +1,156 @@
+"""Second headline metric: tx-verify/s on a synthetic 2 MB block (BASELINE.json config 4).
+
+Setup (untimed): an in-memory ledger with a funding block of P-256-owned outputs, then ``steps +
+warmup`` full blocks of ~8,300 transactions (2 inputs of one random key, 2 outputs, 1 signature:
+216 B each -> 1.79 MB per block, under the 2 MB cap). Every block header is mined at the chain's
+difficulty (6.0) on the GPU.
+
+Timed: for each block exactly what ``POST /push_block`` does with full tx hex — parse every tx
+(``Transaction.from_hex``) and ``manager.create_block``: PoW/prev/timestamp/size checks, per-category
+UTXO probes against the HBM index, batched point decompression, ONE batched P-256 verify launch
+(+ ASCII-hex fallback pass), per-tx rule checks, merkle root, then the ledger writes and the UTXO
+index insert/erase. Weak scaling: each rank validates its own chain on its own GPU.
+"""
+from __future__ import annotations
+
+import asyncio
+import hashlib
+import random
+import time
+from decimal import Decimal
+
+from .constants import SMALLEST
+
+
+def _funding_tx(owner_addrs, amount: Decimal, rng):
+    from .models.transaction import Transaction, TransactionInput, TransactionOutput
+    inp = TransactionInput(rng.randbytes(32).hex(), 0)
+    inp.signed = (1, 1)
+    return Transaction([inp], [TransactionOutput(a, amount) for a in owner_addrs])
+
+
+async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None, device=None):
+    from . import devnet
+    from .ledger import manager
+    from .ledger.database import Database
+    from .models.transaction import CoinbaseTransaction, Transaction, TransactionInput, TransactionOutput
+    from .ops import p256 as op
+    from .utils.codec import point_to_string
+    rng = random.Random(seed)
+    db = await Database.create(utxo_backend=utxo_backend)
+    manager.Manager.difficulty = None
+    keys = [rng.randrange(1, op.oracle.N) for _ in range(256)]
+    addrs = [point_to_string(op.public_key(k)) for k in keys]
+    base_ts = int(time.time()) - 10_000
+    genesis_addr = addrs[0]
+    await devnet.mine_block(genesis_addr, ts=base_ts, device=device)
+    # funding block written straight into the ledger (trusted setup, not part of the measurement)
+    n_out = n_blocks * txs_per_block * 2
+    owners = [(i // 2) % 256 for i in range(n_out)]  # outputs 2j and 2j+1 share an owner
+    funding = []
+    for k in range(0, n_out, 255):
+        funding.append(_funding_tx([addrs[o] for o in owners[k:k + 255]], Decimal(10), rng))
+    block_hash = rng.randbytes(32).hex()
+    last = await db.get_last_block()
+    await db.add_block(2, block_hash, last['content'], genesis_addr, 0, Decimal('6.0'), Decimal(6), base_ts + 1)
+    cb = CoinbaseTransaction(block_hash, genesis_addr, Decimal(6))
+    await db.add_transaction(cb, block_hash)
+    rows = []
+    for t in funding:
+        rows.append((block_hash, t.hash(), t.hex(), '[]', __import__('json').dumps([o.address for o in t.outputs]),
+                     __import__('json').dumps([int(o.amount * SMALLEST) for o in t.outputs]), '0.000000'))
+    db.insert_transaction_rows(rows)
+    await db.add_transaction_outputs(funding + [cb])
+    outpoints = [(t.hash(), i) for t in funding for i in range(len(t.outputs))]
+    # spending blocks
+    blocks = []
+    j = 0
+    for b in range(n_blocks):
+        txs = []
+        for _ in range(txs_per_block):
+            (h1, i1), (h2, i2) = outpoints[2 * j], outpoints[2 * j + 1]
+            owner = owners[2 * j]
+            j += 1
+            ins = [TransactionInput(h1, i1, amount=Decimal(10)), TransactionInput(h2, i2, amount=Decimal(10))]
+            for i in ins:
+                i.public_key = op.public_key(keys[owner])
+            outs = [TransactionOutput(addrs[rng.randrange(256)], Decimal('12.5')),
+                    TransactionOutput(addrs[owner], Decimal('7.49'))]
+            tx = Transaction(ins, outs)
+            tx.sign([keys[owner]])
+            txs.append(tx.hex())
+        blocks.append(txs)
+    return db, genesis_addr, blocks, base_ts
+
+
+async def _run(args, ctx, device, utxo_backend):
+    from . import devnet
+    from .ledger import manager, validate
+    from .models.transaction import Transaction
+    n_blocks = args.steps + args.warmup
+    db, addr, blocks, base_ts = await _setup(n_blocks, args.txs, 1234 + ctx.rank, utxo_backend, device)
+    # mine every header up front (untimed): block b+1's previous hash is sha256(header_b) and the
+    # difficulty stays at START_DIFFICULTY below block 100
+    from .constants import START_DIFFICULTY
+    from .models.block import get_transactions_merkle_tree
+    last = await db.get_last_block()
+    prev = last['hash']
+    headers = []
+    for b, txs_hex in enumerate(blocks):
+        content = devnet.mine_header_raw(prev, addr, get_transactions_merkle_tree(txs_hex), base_ts + 10 + b,
+                                         START_DIFFICULTY, device=device)
+        headers.append(content)
+        prev = hashlib.sha256(bytes.fromhex(content)).hexdigest()
+    stages = []
+    total_txs = 0
+    for b, txs_hex in enumerate(blocks):
+        if b == args.warmup:
+            ctx.barrier()
+            ctx.synchronize()
+            t_start = time.perf_counter()
+        t0 = time.perf_counter()
+        txs = [await Transaction.from_hex(h) for h in txs_hex]
+        t1 = time.perf_counter()
+        errors = []
+        ok = await manager.create_block(headers[b], txs, error_list=errors)
+        if not ok:
+            raise RuntimeError(f'synthetic block rejected: {errors}')
+        t2 = time.perf_counter()
+        if b >= args.warmup:
+            total_txs += len(txs)
+            stages.append({'parse_s': t1 - t0, 'create_block_s': t2 - t1, **manager.last_block_timings,
+                           **{k: v for k, v in validate.timings.items() if k.endswith('_s')}})
+    ctx.synchronize()
+    ctx.barrier()
+    wall = time.perf_counter() - t_start
+    wall = ctx.allreduce_max_f(wall)
+    return total_txs, wall, stages, len(blocks[0])
+
+
+def run_verify_bench(args, ctx):
+    from .ops.native import gpu_available
+    device = 'gpu' if gpu_available() else 'cpu'
+    utxo_backend = 'gpu' if device == 'gpu' else 'host'
+    total_txs, wall, stages, txs_per_block = asyncio.run(_run(args, ctx, device, utxo_backend))
+    total = ctx.allreduce_sum(total_txs)
+    tps = total / wall
+    avg = {k: round(sum(s[k] for s in stages) / len(stages) * 1000, 2) for k in stages[0]
+           if isinstance(stages[0][k], float)}
+    return {
+        'metric': 'block_tx_verify_per_s',
+        'value': round(tps, 1),
+        'unit': 'tx/s',
+        'n_gpus': ctx.world if device == 'gpu' else 0,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(wall * 1000 / max(1, args.steps), 2),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'uint32',
+        'data': 'synthetic 2 MB blocks: random P-256 keys, 2-in/2-out signed txs, funding UTXOs',
+        'config': {'model': 'upow block validation + apply (push_block path)', 'global_batch': total // max(1, args.steps),
+                   'seq_len': txs_per_block, 'parallelism': f'dp{ctx.world}', 'device': device,
+                   'utxo_backend': utxo_backend},
+        'stage_ms_avg': avg,
+    }

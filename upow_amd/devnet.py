@@ -41,6 +41,21 @@ async def mine_header(address: str, transactions: List, ts: Optional[int] = None
     raise RuntimeError('nonce space exhausted')
 
 
+def mine_header_raw(prev: str, address: str, merkle: str, ts: int, difficulty, device: Optional[str] = None,
+                    chunk: int = 1 << 24) -> str:
+    """Mine a header on an explicit previous hash (no ledger access)."""
+    job = PowJob.create(header_prefix(prev, address, merkle, ts, difficulty), PowTarget.from_difficulty(prev, difficulty))
+    start, step = 0, 1 << 12
+    while start < 1 << 32:
+        n = min(step, (1 << 32) - start)
+        r = search(job, start, n, device=device)
+        if r.nonces:
+            return job.header_with_nonce(r.nonces[0]).hex()
+        start += n
+        step = min(step * 8, chunk)
+    raise RuntimeError('nonce space exhausted')
+
+
 async def mine_block(address: str, transactions: List = (), ts: Optional[int] = None,
                      device: Optional[str] = None) -> str:
     """Mine and apply one block; returns its hash. Raises with the node's error on rejection."""
