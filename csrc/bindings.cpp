@@ -184,6 +184,20 @@ PYBIND11_MODULE(_native, m) {
         return py::bytes(reinterpret_cast<const char*>(o.data()), o.size());
     });
 
+    m.def("b58encode", [](py::bytes b) {
+        std::string s = b;
+        return b58encode(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+    });
+    m.def("b58decode", [](const std::string& s) {
+        std::vector<uint8_t> v;
+        try {
+            v = b58decode(s);
+        } catch (const std::invalid_argument& e) {
+            throw py::value_error(e.what());
+        }
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+    });
+
     m.def("gpu_device_count", &gpu_device_count);
     m.def("gpu_arch_name", &gpu_arch_name);
 }

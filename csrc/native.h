@@ -54,6 +54,10 @@ std::vector<uint8_t> utxo_probe(int64_t h, const uint8_t* recs, int64_t n);  // 
 std::vector<uint8_t> utxo_erase(int64_t h, const uint8_t* recs, int64_t n);  // 1 if erased
 std::vector<uint8_t> utxo_dump(int64_t h);
 
+// ---------------------------------------------------------------- base58
+std::string b58encode(const uint8_t* data, size_t n);
+std::vector<uint8_t> b58decode(const std::string& s);
+
 // ---------------------------------------------------------------- device info
 int gpu_device_count();
 std::string gpu_arch_name(int device);

@@ -25,7 +25,7 @@ def _exercise(backend):
     assert (idx.probe(_keys(100, 2)) == MISSING).all()
     # erase with tag filter + duplicate keys in one batch: each outpoint erased once
     er = idx.erase(keys[:10] + keys[:10], tag=None)
-    assert er[:10].all() and not er[10:].any()
+    assert ((er[:10] + er[10:]) == 1).all()  # exactly one copy wins (on the GPU either lane may)
     assert (idx.probe(keys[:10]) == MISSING).all()
     # tag-filtered erase leaves other tables alone
     k7 = [k for k, t in zip(keys[3000:3100], tags[3000:3100]) if t == 3]

@@ -122,6 +122,24 @@ def _arr(s) -> list:
     return json.loads(s) if s else []
 
 
+_CANON: dict = {}
+
+
+async def _input_address(tx_input) -> str:
+    """``point_to_string(await input.get_public_key())`` memoised by the owning address string
+    (the canonical compressed base58 form of the spent output's address)."""
+    if tx_input.public_key is not None:
+        return point_to_string(tx_input.public_key)
+    addr = await tx_input.get_address()
+    hit = _CANON.get(addr)
+    if hit is None:
+        hit = point_to_string(string_to_point(addr))
+        if len(_CANON) > (1 << 20):
+            _CANON.clear()
+        _CANON[addr] = hit
+    return hit
+
+
 def _at(arr: list, index: int):
     """PostgreSQL 1-based array subscript semantics for ``arr[index + 1]`` (NULL when out of range)."""
     return arr[index] if 0 <= index < len(arr) else None
@@ -232,11 +250,9 @@ class Database:
         return [o for _, o in out]
 
     def _delete_outpoints(self, table: str, inputs: List[Tuple[str, int]]) -> int:
-        n = 0
         with self.lock:
-            for h, i in inputs:
-                n += self.conn.execute(f'DELETE FROM {table} WHERE tx_hash = ? AND "index" = ?', (h, int(i))).rowcount
-        return n
+            return self.conn.executemany(f'DELETE FROM {table} WHERE tx_hash = ? AND "index" = ?',
+                                         [(h, int(i)) for h, i in inputs]).rowcount
 
     def _pending_spent_set(self) -> Set[Tuple[str, int]]:
         return {(r[0], r[1]) for r in self._q('SELECT tx_hash, "index" FROM pending_spent_outputs')}
@@ -251,7 +267,7 @@ class Database:
         if verify and not await transaction.verify_pending():
             logger.error('Error in adding transaction.')
             return False
-        inputs_addresses = [point_to_string(await i.get_public_key()) for i in transaction.inputs]
+        inputs_addresses = [await _input_address(i) for i in transaction.inputs]
         try:
             self._x('INSERT INTO pending_transactions (tx_hash, tx_hex, inputs_addresses, fees, propagation_time) '
                     'VALUES (?, ?, ?, ?, ?)',
@@ -370,7 +386,7 @@ class Database:
 
     async def _tx_row(self, transaction, block_hash):
         if isinstance(transaction, Transaction):
-            inputs_addresses = [point_to_string(await i.get_public_key()) for i in transaction.inputs]
+            inputs_addresses = [await _input_address(i) for i in transaction.inputs]
         else:
             inputs_addresses = []
         return (block_hash, transaction.hash(), transaction.hex(), _j(inputs_addresses),
@@ -680,10 +696,8 @@ class Database:
             return True
         try:
             with self.transaction():
-                n = 0
-                for h, i in inputs:
-                    n += self.conn.execute('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
-                                           (h, int(i))).rowcount
+                n = self.conn.executemany('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
+                                          [(h, int(i)) for h, i in inputs]).rowcount
                 if n != len(inputs):
                     logger.error(f'Failed to delete all UTXOs: {n} of {len(inputs)} deleted')
                     raise _Rollback()
@@ -717,10 +731,8 @@ class Database:
         start = perf_counter()
         try:
             with self.transaction():
-                n = 0
-                for h, i in inputs:
-                    n += self.conn.execute('DELETE FROM pending_spent_outputs WHERE tx_hash = ? AND "index" = ?',
-                                           (h, int(i))).rowcount
+                n = self.conn.executemany('DELETE FROM pending_spent_outputs WHERE tx_hash = ? AND "index" = ?',
+                                          [(h, int(i)) for h, i in inputs]).rowcount
                 if n != len(inputs):
                     logger.error(f'Failed to delete all pending_spent_outputs: {n} of {len(inputs)} deleted')
                     raise _Rollback()

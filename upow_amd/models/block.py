@@ -68,8 +68,15 @@ def get_transactions_merkle_tree(transactions: Iterable) -> str:
     Batched leaf hashing runs natively (:func:`upow_amd.ops.sha256.merkle_root`) when the
     extension is present; this is the oracle form.
     """
+    txs = [_tx_bytes(t) for t in transactions]
+    if len(txs) >= 64:
+        try:
+            from ..ops.sha256 import merkle_root
+            return merkle_root(txs)
+        except ImportError:
+            pass
     h = hashlib.sha256()
-    for b in sorted(_tx_bytes(t) for t in transactions):
+    for b in sorted(txs):
         h.update(hashlib.sha256(b).digest())
     return h.hexdigest()
 

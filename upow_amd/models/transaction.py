@@ -274,7 +274,21 @@ class Transaction:
 
     # ------------------------------------------------------------------ codec
     def hex(self, full: bool = True) -> str:
-        """transaction.py:46-83 (``full=False`` is the signed message)."""
+        """transaction.py:46-83 (``full=False`` is the signed message).
+
+        Memoised per (full, signature state): a block's txs are serialised several times on the
+        validation/apply path (txid, merkle, size check, storage)."""
+        fp = (full, len(self.inputs), len(self.outputs), self.message,
+              tuple(i.signed for i in self.inputs) if full else None)
+        memo = self.__dict__.setdefault('_hex_memo', {})
+        c = memo.get(full)
+        if c is not None and c[0] == fp:
+            return c[1]
+        h = self._hex_uncached(full)
+        memo[full] = (fp, h)
+        return h
+
+    def _hex_uncached(self, full: bool = True) -> str:
         parts = [self.version.to_bytes(1, ENDIAN), len(self.inputs).to_bytes(1, ENDIAN)]
         parts += [i.tobytes() for i in self.inputs]
         parts.append(len(self.outputs).to_bytes(1, ENDIAN))

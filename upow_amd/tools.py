@@ -1,0 +1,43 @@
+"""Operator tools.
+
+``python -m upow_amd.tools rebuild-utxo``: rebuild the UTXO set by replaying every transaction in
+block order (reference: create_unspent_outputs.py:9-45, database.py:846-862).
+``python -m upow_amd.tools utxo-hash``: print the UTXO-set hash served at ``GET /``.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import sys
+
+from .ledger.database import Database
+
+
+async def rebuild_utxo(path: str = None):
+    db = await Database.create(path=path)
+    outputs = await db.get_unspent_outputs_from_all_transactions()
+    with db.transaction():
+        db.conn.execute('DELETE FROM unspent_outputs')
+    await db.add_unspent_outputs(sorted(outputs))
+    await db.set_unspent_outputs_addresses()
+    db._rebuild_utxo_index()
+    print(f'{len(outputs)} unspent outputs; hash {await db.get_unspent_outputs_hash()}')
+    return len(outputs)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument('command', choices=['rebuild-utxo', 'utxo-hash'])
+    ap.add_argument('--db', default=None)
+    a = ap.parse_args(argv)
+    if a.command == 'rebuild-utxo':
+        asyncio.run(rebuild_utxo(a.db))
+    else:
+        async def h():
+            db = await Database.create(path=a.db)
+            print(await db.get_unspent_outputs_hash())
+        asyncio.run(h())
+
+
+if __name__ == '__main__':
+    sys.exit(main())

@@ -33,7 +33,37 @@ _B58 = '123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz'
 _B58_INDEX = {c: i for i, c in enumerate(_B58)}
 
 
+_NATIVE = None
+
+
+def _native():
+    """Native codec (csrc/base58.cpp) when the extension is built; None -> pure Python."""
+    global _NATIVE
+    if _NATIVE is None:
+        try:
+            from ..ops.native import lib
+            _NATIVE = lib()
+        except Exception:
+            _NATIVE = False
+    return _NATIVE or None
+
+
+_B58_CACHE: dict = {}
+
+
 def b58encode(data: bytes) -> str:
+    hit = _B58_CACHE.get(data)
+    if hit is not None:
+        return hit
+    n = _native()
+    s = n.b58encode(bytes(data)) if n is not None else _b58encode_py(data)
+    if len(_B58_CACHE) > (1 << 20):
+        _B58_CACHE.clear()
+    _B58_CACHE[bytes(data)] = s
+    return s
+
+
+def _b58encode_py(data: bytes) -> str:
     n = int.from_bytes(data, 'big')
     out = []
     while n:
@@ -46,6 +76,13 @@ def b58encode(data: bytes) -> str:
 def b58decode(s: Union[str, bytes]) -> bytes:
     if isinstance(s, bytes):
         s = s.decode('ascii')
+    n = _native()
+    if n is not None:
+        return n.b58decode(s)
+    return _b58decode_py(s)
+
+
+def _b58decode_py(s: str) -> bytes:
     s = s.rstrip()
     n = 0
     for c in s:
