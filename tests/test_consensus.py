@@ -1,0 +1,111 @@
+"""Consensus math (reference upow/manager.py:39-250): difficulty retarget, rewards, inode split."""
+import asyncio
+import decimal
+from decimal import Decimal
+from math import ceil, log
+
+import pytest
+
+from upow_amd.ledger import manager as m
+from upow_amd.ledger.database import Database
+
+
+def test_difficulty_hashrate_roundtrip():
+    for d in ['6.0', '6.1', '6.3', '6.5', '6.9', '7.0', '10.9']:
+        d = Decimal(d)
+        hr = m.difficulty_to_hashrate(d)
+        assert hr == Decimal(16 ** int(d) * (16 / ceil(16 * (1 - d % 1))))
+        assert m.hashrate_to_difficulty(hr) == d
+    # the reference mixes float and Decimal here; 8.4 does not survive the round trip there either
+    assert m.hashrate_to_difficulty(m.difficulty_to_hashrate(Decimal('8.4'))) == Decimal('8.3')
+    # expected hashes at 6.3: 16^6 * 16/12
+    assert m.difficulty_to_hashrate(Decimal('6.3')) == Decimal(16 ** 6 * 16 / 12)
+
+
+def test_block_reward_schedule():
+    H = 1576800
+    assert m.get_block_reward(1) == 6
+    assert m.get_block_reward(H) == 6          # exactly at a multiple: one halving less
+    assert m.get_block_reward(H + 1) == 3
+    assert m.get_block_reward(2 * H + 1) == Decimal(1.5)
+    assert m.get_block_reward(14191200) == Decimal(6 / 2 ** 8)
+    assert m.get_block_reward(14191201) == 0
+    with pytest.raises(AssertionError):
+        m.get_block_reward(0)
+
+
+def test_circulating_supply():
+    H = 3 * 365 * 24 * 60
+    assert m.get_circulating_supply(10) == 60
+    assert m.get_circulating_supply(H) == 6 * H
+    assert m.get_circulating_supply(H + 10) == 6 * H + 3 * 10
+    assert m.get_circulating_supply(H * 9 + 1) == Decimal(18_884_643.75)
+
+
+def _ref_inode_rewards(reward, inodes, block_no):
+    """Literal transcription of upow/manager.py:171-212 (independent of the implementation)."""
+    total_percent = sum(e['emission'] for e in inodes)
+    if not inodes or total_percent <= 0:
+        return reward, {}
+    miner = reward * Decimal(0.5)
+    dist = reward * Decimal(0.5)
+    out = {}
+    redis = Decimal(0)
+    with decimal.localcontext() as ctx:
+        ctx.prec = 9 if block_no > 39000 else ctx.prec
+        for d in inodes:
+            p = d['emission']
+            r = dist * Decimal(p) / Decimal(total_percent)
+            r = r.quantize(Decimal('0.00000001')) if block_no > 39000 else (
+                r.quantize(Decimal('0.00000001')) if (r * 100000000) % 1 != 0 else r)
+            if p >= 1:
+                out[d['wallet']] = r
+            else:
+                redis += dist * Decimal(p) / Decimal(total_percent)
+            if redis > 0:
+                n = sum(1 for e in inodes if e['emission'] >= 1)
+                ra = redis / n
+                ra = ra.quantize(Decimal('0.00000001')) if block_no > 39000 else (
+                    ra.quantize(Decimal('0.00000001')) if (ra * 100000000) % 1 != 0 else ra)
+                for e in inodes:
+                    if e['emission'] >= 1:
+                        out[e['wallet']] += ra
+    return miner, out
+
+
+@pytest.mark.parametrize('block_no', [100, 39001])
+def test_inode_rewards_split(block_no):
+    inodes = [{'wallet': 'a', 'emission': Decimal('60.00')}, {'wallet': 'b', 'emission': Decimal('39.50')},
+              {'wallet': 'c', 'emission': Decimal('0.50')}]
+    got = m.get_inode_rewards(Decimal(6), inodes, block_no)
+    assert got == _ref_inode_rewards(Decimal(6), inodes, block_no)
+    miner, dist = got
+    assert miner == 3 and set(dist) == {'a', 'b'}
+    assert m.get_inode_rewards(Decimal(6), [], block_no) == (6, {})
+
+
+def test_pow_check_genesis_and_predicate():
+    async def go():
+        assert await m.check_block_is_valid('00' * 108, (Decimal(6), {}))  # no previous block: no PoW check
+        assert not await m.check_block_is_valid('00' * 108, (Decimal(6), {'hash': 'ff' * 32}))
+    asyncio.run(go())
+
+
+def test_calculate_difficulty_retarget(monkeypatch):
+    monkeypatch.setattr(m, 'START_DIFFICULTY', Decimal('6.0'))
+
+    async def go():
+        db = await Database.create(utxo_backend='host')
+        assert await m.calculate_difficulty() == (Decimal('6.0'), {})
+        ts = 1_700_000_000
+        # 100 blocks, 30 s apart -> twice too fast -> hashrate x2 -> difficulty 6.0 -> 6.5 (16/8)
+        for i in range(1, 101):
+            await db.add_block(i, f'{i:064x}', '00', 'addr', 0, Decimal('6.0'), Decimal(6), ts + 30 * (i - 1))
+        d, last = await m.calculate_difficulty()
+        elapsed = 30 * 99
+        hr = m.difficulty_to_hashrate(Decimal('6.0')) * (60 / (elapsed / Decimal(100)))
+        assert d == m.hashrate_to_difficulty(hr) and last['id'] == 100
+        await db.add_block(101, f'{101:064x}', '00', 'addr', 0, d, Decimal(6), ts + 30 * 100)
+        assert (await m.calculate_difficulty())[0] == d  # no retarget off the 100 boundary
+        db.close()
+    asyncio.run(go())

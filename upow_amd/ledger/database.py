@@ -547,7 +547,8 @@ class Database:
         return result
 
     async def get_block_by_id(self, block_id: int) -> Optional[dict]:
-        return self._block_row(self._q1('SELECT * FROM blocks WHERE id = ?', (block_id,)))
+        # calculate_difficulty passes `id - BLOCKS_COUNT + 1` as a Decimal (manager.py:95-97)
+        return self._block_row(self._q1('SELECT * FROM blocks WHERE id = ?', (int(block_id),)))
 
     async def get_block_transactions(self, block_hash: str, check_signatures: bool = True, hex_only: bool = False):
         rows = self._q('SELECT tx_hex FROM transactions WHERE block_hash = ? ORDER BY rowid', (block_hash,))
