@@ -22,9 +22,12 @@ class DistContext:
     backend: Optional[str] = None
     device: str = 'cpu'
 
+    comm_device: str = 'cpu'  # where collective tensors live: cuda:N for RCCL, cpu for gloo
+    forced: bool = False  # run collectives even for world == 1 (exercises the RCCL path on one GPU)
+
     @property
     def is_distributed(self) -> bool:
-        return self.world > 1
+        return self.world > 1 or self.forced
 
     @property
     def is_main(self) -> bool:
@@ -33,7 +36,7 @@ class DistContext:
     # ---------------------------------------------------------------- collectives (thin wrappers)
     def _t(self, values, dtype=None):
         import torch
-        return torch.tensor(values, dtype=dtype or torch.int64, device=self.device)
+        return torch.tensor(values, dtype=dtype or torch.int64, device=self.comm_device)
 
     def allreduce_min(self, v: int) -> int:
         if not self.is_distributed:
@@ -74,11 +77,11 @@ class DistContext:
             t = self._t([n_src])
             dist.broadcast(t, src=src)
             size = int(t.item())
-        buf = torch.zeros(size + 4, dtype=torch.uint8, device=self.device)
+        buf = torch.zeros(size + 4, dtype=torch.uint8, device=self.comm_device)
         if self.rank == src:
             assert data is not None and len(data) <= size, 'payload larger than max_len (use max_len=0)'
             payload = len(data).to_bytes(4, 'little') + data
-            buf[:len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(self.device)
+            buf[:len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(self.comm_device)
         dist.broadcast(buf, src=src)
         raw = bytes(buf.cpu().numpy().tobytes())
         n = int.from_bytes(raw[:4], 'little')
@@ -94,9 +97,9 @@ class DistContext:
         sizes = [torch.zeros_like(n) for _ in range(self.world)]
         dist.all_gather(sizes, n)
         mx = max(int(s.item()) for s in sizes)
-        buf = torch.zeros(max(mx, 1), dtype=torch.uint8, device=self.device)
+        buf = torch.zeros(max(mx, 1), dtype=torch.uint8, device=self.comm_device)
         if data:
-            buf[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(self.device)
+            buf[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(self.comm_device)
         outs = [torch.zeros_like(buf) for _ in range(self.world)]
         dist.all_gather(outs, buf)
         return [bytes(o.cpu().numpy().tobytes()[:int(s.item())]) for o, s in zip(outs, sizes)]
@@ -132,7 +135,9 @@ def init_from_env(backend: Optional[str] = None, want_gpu: bool = True) -> DistC
                 ctx.device = f'cuda:{torch.cuda.current_device()}'
         except Exception:
             gpu = False
-    if world > 1:
+    force = os.environ.get('UPOW_FORCE_DIST', '0') == '1' and 'MASTER_PORT' in os.environ
+    if world > 1 or force:
+        ctx.forced = world == 1
         import torch.distributed as dist
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         be = backend or ('nccl' if gpu else 'gloo')
@@ -144,8 +149,7 @@ def init_from_env(backend: Optional[str] = None, want_gpu: bool = True) -> DistC
             else:
                 dist.init_process_group(be, rank=rank, world_size=world)
         ctx.backend = be
-        if be != 'nccl':
-            ctx.device = 'cpu' if not gpu else ctx.device
+        ctx.comm_device = ctx.device if be == 'nccl' else 'cpu'
     return ctx
 
 
