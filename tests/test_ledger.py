@@ -115,3 +115,27 @@ def test_stake_and_validator_flow(chain):
         with pytest.raises(Exception, match='Already staked'):
             await builders.create_stake_transaction(KEY_A, '5')
     asyncio.run(go())
+
+
+@pytest.mark.parametrize('stage', ['block', 'transactions', 'outputs', 'spent'])
+def test_block_apply_is_atomic_under_injected_failure(chain, stage):
+    async def go():
+        a = builders.address_of(KEY_A)
+        b = builders.address_of(KEY_B)
+        base = 1_700_000_000
+        await devnet.mine_block(a, ts=base + 1)
+        await devnet.mine_block(a, ts=base + 2)
+        tx = await builders.create_transaction(KEY_A, b, '1')
+        assert await chain.add_pending_transaction(tx)
+        before = (await chain.get_next_block_id(), await chain.get_unspent_outputs_hash(), len(chain.utxo),
+                  await chain.get_pending_transactions_limit(hex_only=True))
+        chain.fail_after_stage = stage
+        with pytest.raises(RuntimeError, match='block rejected'):
+            await devnet.mine_block(a, [tx], ts=base + 3)
+        after = (await chain.get_next_block_id(), await chain.get_unspent_outputs_hash(), len(chain.utxo),
+                 await chain.get_pending_transactions_limit(hex_only=True))
+        assert after == before
+        chain.fail_after_stage = None
+        await devnet.mine_block(a, [tx], ts=base + 3)
+        assert await chain.get_address_balance(b) == 1
+    asyncio.run(go())

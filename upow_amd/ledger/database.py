@@ -206,23 +206,42 @@ class Database:
             self.conn.executemany(sql, rows)
 
     class _Tx:
+        """Re-entrant SQL transaction: only the outermost level issues BEGIN/COMMIT/ROLLBACK, so a
+        whole block application (many helper calls) commits or rolls back as one unit."""
+
         def __init__(self, db):
             self.db = db
 
         def __enter__(self):
             self.db.lock.acquire()
-            self.db.conn.execute('BEGIN')
+            if self.db._tx_depth == 0:
+                self.db.conn.execute('BEGIN')
+            self.db._tx_depth += 1
             return self.db
 
         def __exit__(self, et, ev, tb):
             try:
-                self.db.conn.execute('COMMIT' if et is None else 'ROLLBACK')
+                self.db._tx_depth -= 1
+                if self.db._tx_depth == 0:
+                    self.db.conn.execute('COMMIT' if et is None else 'ROLLBACK')
+                elif et is not None:
+                    self.db._tx_failed = True
             finally:
                 self.db.lock.release()
             return False
 
+    _tx_depth = 0
+    _tx_failed = False
+
     def transaction(self):
         return Database._Tx(self)
+
+    # fault injection (tests): raise inside block application after the named stage
+    fail_after_stage: Optional[str] = None
+
+    def checkpoint(self, stage: str):
+        if self.fail_after_stage == stage:
+            raise RuntimeError(f'injected failure after {stage}')
 
     def _rebuild_utxo_index(self):
         keys, tags = [], []
@@ -690,21 +709,20 @@ class Database:
         self.utxo.erase(inputs)
 
     async def remove_unspent_outputs(self, transactions, max_retries: int = 3) -> bool:
-        """database.py:589-621: all-or-nothing delete, checks the deleted count."""
+        """database.py:589-621: delete the spent outpoints and report whether every one was there.
+        Like the reference (which returns from inside its transaction block, i.e. commits), the
+        deletions that did happen stand — blocks in ``double_spend_dict`` rely on this."""
         start = perf_counter()
         inputs = [(i.tx_hash, i.index) for t in transactions for i in t.inputs]
         if not inputs:
             return True
-        try:
-            with self.transaction():
-                n = self.conn.executemany('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
-                                          [(h, int(i)) for h, i in inputs]).rowcount
-                if n != len(inputs):
-                    logger.error(f'Failed to delete all UTXOs: {n} of {len(inputs)} deleted')
-                    raise _Rollback()
-        except _Rollback:
+        with self.transaction():
+            n = self.conn.executemany('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
+                                      [(h, int(i)) for h, i in inputs]).rowcount
+        self.utxo.erase(inputs, TAG_BY_TABLE['unspent_outputs'])
+        if n != len(inputs):
+            logger.error(f'Failed to delete all UTXOs: {n} of {len(inputs)} deleted')
             return False
-        self.utxo.erase(inputs)
         logger.info(f'Successfully removed {len(inputs)} unspent outputs in {perf_counter() - start:.3f} seconds')
         return True
 
@@ -730,14 +748,11 @@ class Database:
         if not inputs:
             return True
         start = perf_counter()
-        try:
-            with self.transaction():
-                n = self.conn.executemany('DELETE FROM pending_spent_outputs WHERE tx_hash = ? AND "index" = ?',
-                                          [(h, int(i)) for h, i in inputs]).rowcount
-                if n != len(inputs):
-                    logger.error(f'Failed to delete all pending_spent_outputs: {n} of {len(inputs)} deleted')
-                    raise _Rollback()
-        except _Rollback:
+        with self.transaction():
+            n = self.conn.executemany('DELETE FROM pending_spent_outputs WHERE tx_hash = ? AND "index" = ?',
+                                      [(h, int(i)) for h, i in inputs]).rowcount
+        if n != len(inputs):
+            logger.error(f'Failed to delete all pending_spent_outputs: {n} of {len(inputs)} deleted')
             return False
         logger.info(f'Successfully removed {len(inputs)} pending_spent_outputs in {perf_counter() - start:.3f} seconds')
         return True

@@ -354,22 +354,30 @@ async def check_block(block_content: str, transactions: List[Transaction], minin
 
 async def _apply_block(block_no, block_hash, block_content, address, random, difficulty, block_reward, fees,
                        content_time, coinbase_transaction, transactions) -> bool:
-    """DB writes of manager.py:706-730 (shared by create_block and the sync path)."""
+    """DB writes of manager.py:706-730 (shared by create_block and the sync path), applied as ONE
+    SQLite transaction: a failure at any stage leaves the ledger and the UTXO index untouched (the
+    reference deletes the half-written block instead, manager.py:718-723)."""
     database: Database = Database.instance
-    await database.add_block(block_no, block_hash, block_content, address, random, difficulty,
-                             block_reward + fees, content_time)
-    await database.add_transaction(coinbase_transaction, block_hash)
     try:
-        await database.add_transactions(transactions, block_hash)
+        with database.transaction():
+            await database.add_block(block_no, block_hash, block_content, address, random, difficulty,
+                                     block_reward + fees, content_time)
+            database.checkpoint('block')
+            await database.add_transaction(coinbase_transaction, block_hash)
+            await database.add_transactions(transactions, block_hash)
+            database.checkpoint('transactions')
+            await database.add_transaction_outputs(transactions + [coinbase_transaction])
+            database.checkpoint('outputs')
+            if transactions:
+                await database.remove_pending_transactions_by_hash([t.hash() for t in transactions])
+                await database.remove_outputs(transactions)
+                await database.remove_pending_spent_outputs(transactions)
+            database.checkpoint('spent')
     except Exception as e:
         logger.error(f'Transaction of {block_no} has not been added in block {e}')
-        await database.delete_block(block_no)
+        database._rebuild_utxo_index()
+        Manager.difficulty = None
         return False
-    await database.add_transaction_outputs(transactions + [coinbase_transaction])
-    if transactions:
-        await database.remove_pending_transactions_by_hash([t.hash() for t in transactions])
-        await database.remove_outputs(transactions)
-        await database.remove_pending_spent_outputs(transactions)
     return True
 
 
