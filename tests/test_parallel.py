@@ -69,3 +69,101 @@ def test_dp_miner_gloo_world2():
     for p in procs:
         p.join(60)
     assert results == {0: 'ok', 1: 'ok'}, results
+
+
+def test_shard_bounds_partition():
+    from upow_amd.parallel.verify_dp import shard_bounds
+    for n in (0, 1, 7, 8300):
+        for world in (1, 2, 3, 8):
+            spans = [shard_bounds(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def _replica_worker(rank, world, port, tmp, q):
+    os.environ.update({'RANK': str(rank), 'WORLD_SIZE': str(world), 'LOCAL_RANK': str(rank),
+                       'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port), 'UPOW_DISABLE_GPU': '1',
+                       'UPOW_START_DIFFICULTY': '1.0', 'UPOW_CORE_URL': ''})
+    try:
+        import asyncio
+        import hashlib as hl
+
+        from upow_amd import devnet
+        from upow_amd.ledger import validate
+        from upow_amd.ledger.database import Database
+        from upow_amd.models.transaction import Transaction
+        from upow_amd.ops import p256 as op
+        from upow_amd.parallel.dist import init_from_env, shutdown
+        from upow_amd.parallel import verify_dp
+        from upow_amd.wallet.builders import address_of, create_transaction
+
+        ctx = init_from_env(backend='gloo', want_gpu=False)
+        # sharded raw-record verify: one bad signature in the last shard
+        d = 0x1234567
+        qpt = op.public_key(d)
+        recs = []
+        for i in range(9):
+            dig = hl.sha256(b'm%d' % i).digest()
+            r, s = op.sign(b'm%d' % i, d)
+            recs.append(op.record(qpt, (r, s + (1 if i == 7 else 0)), dig))
+        st = verify_dp.verify_records_dp(ctx, b''.join(recs))
+        assert list(st) == [1] * 7 + [0, 1], list(st)
+        assert verify_dp.verify_shard_first_failure(ctx, b''.join(recs)) == 7
+        assert verify_dp.verify_shard_first_failure(ctx, b''.join(recs[:7])) == -1
+        # mempool all-gather
+        assert verify_dp.gather_mempool(ctx, ['aa', 'bb'] if rank == 0 else ['bb', 'cc']) == ['aa', 'bb', 'cc']
+
+        async def go():
+            db = await Database.create(path=os.path.join(tmp, f'r{rank}.sqlite3'), utxo_backend='host')
+            validate.set_dist_context(ctx)
+            key = 0x61
+            addr = address_of(key)
+            base = 1_700_000_000
+            for b in range(3):
+                content = await devnet.mine_header(addr, [], ts=base + 60 * b, device='cpu') if rank == 0 else None
+                assert await verify_dp.replicate_block(ctx, content, [])
+            txs = []
+            if rank == 0:
+                for j in range(3):
+                    tx = await create_transaction(key, address_of(0x100 + j), '1.5')
+                    await db.add_pending_transaction(tx)
+                    txs.append(tx)
+            # a block whose last signature (rank 1's shard) is forged: both replicas reject it
+            bad_hex = None
+            if rank == 0:
+                forged, _ = Transaction.parse(txs[-1].hex())
+                r, s = forged.inputs[0].signed
+                forged.inputs[0].signed = (r, s + 1 if s + 1 < op.oracle.N else s - 1)
+                bad = txs[:-1] + [forged]
+                bad_hex = [t.hex() for t in bad]
+                content = await devnet.mine_header(addr, bad, ts=base + 60 * 3, device='cpu')
+            assert not await verify_dp.replicate_block(ctx, content if rank == 0 else None, bad_hex)
+            good = None
+            if rank == 0:
+                good = [t.hex() for t in txs]
+                content = await devnet.mine_header(addr, txs, ts=base + 60 * 3, device='cpu')
+            assert await verify_dp.replicate_block(ctx, content if rank == 0 else None, good)
+            h = await db.get_unspent_outputs_hash()
+            hs = ctx.all_gather_bytes(h.encode())
+            assert len(set(hs)) == 1 and (await db.get_next_block_id()) == 5
+            db.close()
+        asyncio.run(go())
+        shutdown(ctx)
+        q.put((rank, 'ok'))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_sharded_verify_and_replicated_ledger_gloo_world2(tmp_path):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_replica_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert results == {0: 'ok', 1: 'ok'}, results

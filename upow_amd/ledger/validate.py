@@ -29,6 +29,21 @@ from ..utils.logger import get_logger
 
 logger = get_logger(__name__)
 timings: dict = {}
+_dist_ctx = None  # set on multi-GPU nodes: the signature batch is sharded across ranks (parallel/verify_dp.py)
+
+
+def set_dist_context(ctx) -> None:
+    """Shard block signature verification over the ranks of ``ctx`` (every rank must call
+    :func:`verify_block_transactions` on the same block)."""
+    global _dist_ctx
+    _dist_ctx = ctx if (ctx is not None and ctx.is_distributed) else None
+
+
+def _verify(recs: bytes, device):
+    if _dist_ctx is not None:
+        from ..parallel.verify_dp import verify_records_dp
+        return verify_records_dp(_dist_ctx, recs, device=device)
+    return op.verify_records(recs, device=device)
 
 _REVOKE = (TransactionType.REVOKE_AS_VALIDATOR, TransactionType.REVOKE_AS_DELEGATE)
 
@@ -101,7 +116,7 @@ async def verify_block_transactions(transactions: List[Transaction], device: Opt
                 bad_range[j] = True
                 continue
             recs[160 * j:160 * j + 160] = op.record(q, (r, s), hashlib.sha256(bytes.fromhex(jobs_msg[j])).digest())
-        status = op.verify_records(bytes(recs), device=device).copy()
+        status = _verify(bytes(recs), device).copy()
         status[bad_range] = op.BAD_RANGE
         retry = np.nonzero(status == op.INVALID)[0]
         if len(retry):
@@ -109,7 +124,7 @@ async def verify_block_transactions(transactions: List[Transaction], device: Opt
             for m, j in enumerate(retry):
                 recs2[160 * m:160 * m + 160] = op.record(jobs_q[j], jobs_sig[j],
                                                          hashlib.sha256(jobs_msg[j].encode()).digest())
-            st2 = op.verify_records(bytes(recs2), device=device)
+            st2 = _verify(bytes(recs2), device)
             status[retry] = np.where(st2 == op.VALID, op.VALID, status[retry])
     t3 = perf_counter()
 
