@@ -18,3 +18,31 @@ def test_verify_bench_pipeline_on_gpu(gpu, monkeypatch):
     out = run_verify_bench(args, DistContext())
     assert out['config']['utxo_backend'] == 'gpu' and out['config']['device'] == 'gpu'
     assert out['value'] > 0
+
+
+@pytest.mark.gpu
+def test_gpu_index_snapshot_roundtrip(gpu, tmp_path, monkeypatch):
+    """HBM index: dump -> canonical records -> K12 equals SQL; snapshot restore into a fresh table."""
+    from decimal import Decimal
+    from upow_amd import devnet
+    from upow_amd.ledger import manager, snapshot
+    from upow_amd.ledger.database import Database
+    from upow_amd.wallet.builders import address_of, create_transaction
+    monkeypatch.setattr(manager, 'START_DIFFICULTY', Decimal('2.0'))
+
+    async def go():
+        path = str(tmp_path / 'g.sqlite3')
+        db = await Database.create(path=path, utxo_backend='gpu')
+        addr = address_of(0x4242)
+        for b in range(6):
+            await devnet.mine_block(addr, ts=1_700_000_000 + 60 * b)
+        tx = await create_transaction(0x4242, address_of(0x99), '7')
+        await devnet.mine_block(addr, [tx], ts=1_700_000_000 + 600)
+        assert db.utxo.set_hash() == await db.get_unspent_outputs_hash()
+        snapshot.save(db)
+        n = len(db.utxo)
+        db.close()
+        db2 = await Database.create(path=path, utxo_backend='gpu')
+        assert db2.utxo_source == 'snapshot' and len(db2.utxo) == n and snapshot.verify(db2)['ok']
+        db2.close()
+    asyncio.run(go())

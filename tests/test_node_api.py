@@ -88,6 +88,14 @@ def test_mining_flow_and_queries(node):
     old = _mine(client, a, base + 5)
     assert old['ok'] is False
     assert client.get('/get_transaction', params={'tx_hash': '00' * 32}).json()['ok'] is False
+    # observability: Prometheus text with the block/tx/signature counters
+    m = client.get('/metrics')
+    assert m.status_code == 200 and m.headers['content-type'].startswith('text/plain')
+    series = {ln.split(' ')[0]: float(ln.split(' ')[1]) for ln in m.text.splitlines() if ln and not ln.startswith('#')}
+    assert series['upow_chain_height'] == 4 and series['upow_mempool_size'] == 0
+    assert series['upow_blocks_applied_total{path="push"}'] >= 4
+    assert series['upow_signatures_verified_total'] >= 1
+    assert series['upow_blocks_rejected_total{path="push"}'] >= 1
 
 
 def test_rate_limit_and_ip_filter(node):

@@ -1,0 +1,85 @@
+"""UTXO-index checkpoint/resume (ledger/snapshot.py), index-side K12 hash, and the ledger lock."""
+import asyncio
+from decimal import Decimal
+
+import pytest
+
+from upow_amd import devnet
+from upow_amd.ledger import manager, snapshot
+from upow_amd.ledger.database import Database
+from upow_amd.wallet.builders import address_of, create_stake_transaction, create_transaction
+
+KEY = 0x5A5A
+
+
+@pytest.fixture(autouse=True)
+def _low_difficulty(monkeypatch):
+    monkeypatch.setattr(manager, 'START_DIFFICULTY', Decimal('1.0'))
+
+
+async def _chain(path, blocks=4):
+    db = await Database.create(path=str(path), utxo_backend='host')
+    manager.Manager.difficulty = None
+    addr = address_of(KEY)
+    for b in range(blocks):
+        await devnet.mine_block(addr, ts=1_700_000_000 + 60 * b, device='cpu')
+    tx = await create_transaction(KEY, address_of(0x77), '2.5')
+    await db.add_pending_transaction(tx)
+    st = await create_stake_transaction(KEY, '1')
+    await db.add_pending_transaction(st)
+    await devnet.mine_block(addr, [tx, st], ts=1_700_000_000 + 60 * blocks, device='cpu')
+    return db
+
+
+def test_snapshot_roundtrip_and_stale_fallback(tmp_path):
+    async def go():
+        path = tmp_path / 'ledger.sqlite3'
+        db = await _chain(path)
+        sql_hash = await db.get_unspent_outputs_hash()
+        assert db.utxo.set_hash() == sql_hash  # index-side K12 == SQL K12
+        hdr = snapshot.save(db)
+        assert hdr['height'] == 5 and hdr['utxo_hash'] == sql_hash and hdr['count'] == len(db.utxo)
+        db.close()
+        db2 = await Database.create(path=str(path), utxo_backend='host')
+        assert db2.utxo_source == 'snapshot'
+        assert db2.utxo.set_hash() == sql_hash and snapshot.verify(db2)['ok']
+        # a block after the snapshot makes it stale -> rebuild from SQL
+        await devnet.mine_block(address_of(KEY), ts=1_700_000_000 + 60 * 9, device='cpu')
+        db2.close()
+        db3 = await Database.create(path=str(path), utxo_backend='host')
+        assert db3.utxo_source == 'sql' and snapshot.verify(db3)['ok']
+        snapshot.save(db3)
+        db3.close()
+        # corrupt payload -> rejected
+        raw = bytearray(open(snapshot.default_path(db3), 'rb').read())
+        raw[-3] ^= 0xFF
+        open(snapshot.default_path(db3), 'wb').write(bytes(raw))
+        db4 = await Database.create(path=str(path), utxo_backend='host')
+        assert db4.utxo_source == 'sql' and snapshot.verify(db4)['ok']
+        db4.close()
+    asyncio.run(go())
+
+
+def test_verify_detects_index_drift(tmp_path):
+    async def go():
+        db = await _chain(tmp_path / 'l.sqlite3', blocks=2)
+        assert snapshot.verify(db)['ok']
+        victim = next(iter(db.utxo.be.d))
+        del db.utxo.be.d[victim]
+        rep = snapshot.verify(db)
+        assert not rep['ok'] and rep['mismatched_tables']
+        db.close()
+    asyncio.run(go())
+
+
+def test_concurrent_blocks_at_same_height_serialised(tmp_path):
+    async def go():
+        db = await _chain(tmp_path / 'c.sqlite3', blocks=2)
+        addr = address_of(KEY)
+        a = await devnet.mine_header(addr, [], ts=1_700_000_000 + 600, device='cpu')
+        b = await devnet.mine_header(addr, [], ts=1_700_000_000 + 601, device='cpu')
+        res = await asyncio.gather(manager.create_block(a, []), manager.create_block(b, []))
+        assert sorted(res) == [False, True]
+        assert await db.get_next_block_id() == 5
+        db.close()
+    asyncio.run(go())

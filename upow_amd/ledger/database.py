@@ -164,7 +164,13 @@ class Database:
         store_dir = os.path.dirname(path) if path != ':memory:' else None
         self.emission_details = JsonStore(os.path.join(store_dir, 'emission_details.json') if store_dir else None)
         self.utxo = UtxoIndex(backend=utxo_backend)
-        self._rebuild_utxo_index()
+        self.utxo_source = 'sql'
+        if path != ':memory:' and os.environ.get('UPOW_SNAPSHOT', '1') != '0':
+            from . import snapshot
+            if snapshot.try_restore(self):
+                self.utxo_source = 'snapshot'
+        if self.utxo_source == 'sql':
+            self._rebuild_utxo_index()
 
     # ------------------------------------------------------------------ lifecycle
     @staticmethod
@@ -183,6 +189,10 @@ class Database:
         if Database.instance is None:
             await Database.create(**Database.credentials)
         return Database.instance
+
+    def _tip_id(self) -> int:
+        row = self._q1('SELECT MAX(id) FROM blocks')
+        return int(row[0] or 0)
 
     def close(self):
         with self.lock:

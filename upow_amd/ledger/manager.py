@@ -10,6 +10,8 @@ from __future__ import annotations
 
 import asyncio
 import decimal
+import os
+import weakref
 from datetime import datetime, timedelta
 from decimal import Decimal
 from math import ceil, floor, log
@@ -21,7 +23,7 @@ from ..constants import (BLOCK_TIME, BLOCKS_COUNT, LAST_BLOCK_FOR_GENESIS_KEY, M
 from ..models.block import (block_to_bytes, check_pow, get_transactions_merkle_tree,
                             get_transactions_merkle_tree_ordered, split_block_content)
 from ..models.transaction import CoinbaseTransaction, Transaction, TransactionOutput
-from ..utils import codec
+from ..utils import codec, metrics
 from ..utils.codec import TransactionType, round_up_decimal, round_up_decimal_new, sha256, timestamp
 from ..utils.logger import get_logger
 from .database import Database
@@ -381,9 +383,46 @@ async def _apply_block(block_no, block_hash, block_content, address, random, dif
     return True
 
 
+_ledger_locks: 'weakref.WeakKeyDictionary' = weakref.WeakKeyDictionary()
+
+
+def ledger_lock() -> asyncio.Lock:
+    """One lock per event loop serialising every ledger mutation (block apply, rollback).
+
+    The reference guards nothing: two concurrent ``/push_block`` calls can both pass ``check_block``
+    on the same parent (race detection). Here check+apply is one critical section,
+    so the second block at a height is checked against the first one's result."""
+    loop = asyncio.get_running_loop()
+    lk = _ledger_locks.get(loop)
+    if lk is None:
+        lk = _ledger_locks[loop] = asyncio.Lock()
+    return lk
+
+
 async def create_block(block_content: str, transactions: List[Transaction], last_block: dict = None,
                        error_list=None) -> bool:
-    """manager.py:650-757."""
+    """manager.py:650-757 (serialised by :func:`ledger_lock`)."""
+    async with ledger_lock():
+        t0 = perf_counter()
+        ok = await _create_block(block_content, transactions, last_block, error_list)
+        _record_block_metrics(ok, perf_counter() - t0, len(transactions), 'push')
+        return ok
+
+
+def _record_block_metrics(ok: bool, seconds: float, n_txs: int, path: str):
+    if ok:
+        metrics.inc('upow_blocks_applied_total', labels={'path': path}, help='blocks validated and applied')
+        metrics.inc('upow_transactions_applied_total', n_txs, help='non-coinbase transactions applied')
+        metrics.observe('upow_block_apply_seconds', seconds, labels={'path': path},
+                        help='check_block + ledger apply wall time')
+        metrics.set_gauge('upow_chain_height', (Database.instance._tip_id() if Database.instance else 0),
+                          help='id of the last applied block')
+    else:
+        metrics.inc('upow_blocks_rejected_total', labels={'path': path}, help='blocks rejected by validation')
+
+
+async def _create_block(block_content: str, transactions: List[Transaction], last_block: dict = None,
+                        error_list=None) -> bool:
     if error_list is None:
         error_list = []
     create_start_time = perf_counter()
@@ -423,6 +462,7 @@ async def create_block(block_content: str, transactions: List[Transaction], last
                 f'in {perf_counter() - create_start_time:.3f} seconds')
     if block_no % 10 == 0:
         logger.info(f'unspent_outputs_hash on block no. {block_no}: {await database.get_unspent_outputs_hash()}')
+    _maybe_snapshot(database, block_no)
     Manager.difficulty = None
     try:
         details = [{'power': str(i['power']), 'emission': str(i['emission']), 'wallet': i['wallet'],
@@ -433,9 +473,33 @@ async def create_block(block_content: str, transactions: List[Transaction], last
     return True
 
 
+SNAPSHOT_EVERY = int(os.environ.get('UPOW_SNAPSHOT_EVERY', '1000'))
+
+
+def _maybe_snapshot(database, block_no: int):
+    """Periodic UTXO-index checkpoint (ledger/snapshot.py); never fails the block."""
+    if SNAPSHOT_EVERY <= 0 or block_no % SNAPSHOT_EVERY or database.path == ':memory:':
+        return
+    try:
+        from . import snapshot
+        snapshot.save(database)
+    except Exception as e:
+        logger.error(f'UTXO snapshot at block {block_no} failed: {e}')
+
+
 async def create_block_in_syncing_old(block_content: str, transactions: List[Transaction],
                                       cb_transaction: CoinbaseTransaction, last_block: dict = None,
                                       error_list=None) -> bool:
+    async with ledger_lock():
+        t0 = perf_counter()
+        ok = await _create_block_in_syncing_old(block_content, transactions, cb_transaction, last_block, error_list)
+        _record_block_metrics(ok, perf_counter() - t0, len(transactions), 'sync')
+        return ok
+
+
+async def _create_block_in_syncing_old(block_content: str, transactions: List[Transaction],
+                                       cb_transaction: CoinbaseTransaction, last_block: dict = None,
+                                       error_list=None) -> bool:
     """manager.py:760-835: sync path, trusts the supplied coinbase."""
     if error_list is None:
         error_list = []
@@ -463,6 +527,7 @@ async def create_block_in_syncing_old(block_content: str, transactions: List[Tra
     if block_no % 10 == 0:
         logger.info(f'unspent_outputs_hash on block no. {block_no}: '
                     f'{await Database.instance.get_unspent_outputs_hash()}')
+    _maybe_snapshot(Database.instance, block_no)
     Manager.difficulty = None
     return True
 

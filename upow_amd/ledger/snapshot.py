@@ -1,0 +1,121 @@
+"""UTXO-index snapshots: checkpoint / resume of the HBM outpoint table (SURVEY.md §5 "Checkpoint / resume").
+
+The reference keeps all state in PostgreSQL and has no snapshots: a restart re-reads the tables, a
+damaged UTXO set is rebuilt by replaying every transaction (create_unspent_outputs.py:9-45). Here the
+SQLite ledger stays authoritative and durable; what a restart has to rebuild is the GPU index
+(every row of the seven output tables → HBM). A snapshot is the index itself:
+
+    line 1   JSON header {magic, version, height, tip_hash, count, utxo_hash, payload_sha256}
+    rest     count × 40-byte records {txid 32 B, u32 index, u32 table tag}, canonical (txid, index) order
+
+written atomically (tmp file + rename) at the tip. On start, :func:`try_restore` loads it only when
+the snapshot's (height, tip hash) equals the ledger's tip, the payload checksum matches and the
+per-table row counts match the SQL tables; the index's K12 hash (``UtxoIndex.set_hash``) must equal
+the header's. Anything else — another chain, a partial write, a stale height — falls back to the
+full rebuild from SQL, so a bad snapshot can cost time but never correctness.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+from typing import Optional
+
+import numpy as np
+
+from ..utils.logger import get_logger
+from .utxo import TAG_BY_TABLE
+
+logger = get_logger(__name__)
+MAGIC, VERSION = 'upow-utxo-snapshot', 1
+FILE_NAME = 'utxo_snapshot.bin'
+
+
+def default_path(db) -> Optional[str]:
+    if db.path == ':memory:':
+        return None
+    return os.environ.get('UPOW_SNAPSHOT_PATH') or os.path.join(os.path.dirname(os.path.abspath(db.path)), FILE_NAME)
+
+
+def _tip(db):
+    row = db._q1('SELECT id, hash FROM blocks ORDER BY id DESC LIMIT 1')
+    return (int(row[0]), row[1]) if row else (0, '')
+
+
+def save(db, path: Optional[str] = None) -> dict:
+    """Write the index at the current tip. Returns the header."""
+    path = path or default_path(db)
+    if path is None:
+        raise ValueError('in-memory ledger: give an explicit snapshot path')
+    with db.lock:
+        height, tip = _tip(db)
+        recs = db.utxo.records()
+    payload = recs.tobytes()
+    header = {'magic': MAGIC, 'version': VERSION, 'height': height, 'tip_hash': tip, 'count': int(len(recs)),
+              'utxo_hash': db.utxo.set_hash(TAG_BY_TABLE['unspent_outputs']),
+              'payload_sha256': hashlib.sha256(payload).hexdigest()}
+    tmp = path + '.tmp'
+    with open(tmp, 'wb') as f:
+        f.write(json.dumps(header, separators=(',', ':')).encode() + b'\n')
+        f.write(payload)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
+    return header
+
+
+def read(path: str):
+    """-> (header, records) after checking the payload checksum; raises ValueError on a bad file."""
+    with open(path, 'rb') as f:
+        header = json.loads(f.readline().decode())
+        payload = f.read()
+    if header.get('magic') != MAGIC or header.get('version') != VERSION:
+        raise ValueError('not a uPow UTXO snapshot')
+    if len(payload) != 40 * header['count'] or hashlib.sha256(payload).hexdigest() != header['payload_sha256']:
+        raise ValueError('snapshot payload truncated or corrupted')
+    return header, np.frombuffer(payload, dtype=np.uint8).reshape(-1, 40)
+
+
+def try_restore(db, path: Optional[str] = None) -> bool:
+    """Load the snapshot into ``db.utxo`` if it matches the ledger tip; False (index untouched) otherwise."""
+    path = path or default_path(db)
+    if not path or not os.path.exists(path):
+        return False
+    try:
+        header, recs = read(path)
+    except (ValueError, OSError, json.JSONDecodeError) as e:
+        logger.warning(f'ignoring UTXO snapshot {path}: {e}')
+        return False
+    if (header['height'], header['tip_hash']) != _tip(db):
+        logger.info(f'UTXO snapshot at height {header["height"]} does not match the ledger tip; rebuilding')
+        return False
+    tags = recs[:, 36:40].copy().view(np.uint32).ravel()
+    for table, tag in TAG_BY_TABLE.items():
+        if int((tags == tag).sum()) != int(db._q1(f'SELECT COUNT(*) FROM {table}')[0]):
+            logger.warning(f'UTXO snapshot row count differs from table {table}; rebuilding')
+            return False
+    db.utxo.reset_records(recs)
+    if db.utxo.set_hash(TAG_BY_TABLE['unspent_outputs']) != header['utxo_hash']:
+        logger.warning('UTXO snapshot hash mismatch after load; rebuilding')
+        return False
+    return True
+
+
+def verify(db) -> dict:
+    """Full audit: index vs SQL (K12 hash of the unspent table + per-table outpoint sets)."""
+    sql_hash = db._q('SELECT tx_hash, "index" FROM unspent_outputs ORDER BY tx_hash, "index"')
+    want = hashlib.sha256(b''.join(bytes.fromhex(r[0]) + bytes([r[1]]) for r in sql_hash)).hexdigest()
+    got = db.utxo.set_hash(TAG_BY_TABLE['unspent_outputs'])
+    recs = db.utxo.records()
+    idx = recs[:, 32:36].copy().view(np.uint32).ravel()
+    tags = recs[:, 36:40].copy().view(np.uint32).ravel()
+    index_sets = {}
+    for n in range(len(recs)):
+        index_sets.setdefault(int(tags[n]), set()).add((bytes(recs[n, :32]).hex(), int(idx[n])))
+    mismatched = [t for t, tag in TAG_BY_TABLE.items()
+                  if index_sets.get(tag, set()) != {(r[0], int(r[1])) for r in db._q(f'SELECT tx_hash, "index" FROM {t}')}]
+    return {'ok': want == got and not mismatched, 'sql_hash': want, 'index_hash': got, 'mismatched_tables': mismatched,
+            'entries': int(len(recs))}
+
+
+__all__ = ['save', 'read', 'try_restore', 'verify', 'default_path']

@@ -77,6 +77,9 @@ class _HostBackend:
                 out[n] = 1
         return out
 
+    def records(self) -> np.ndarray:
+        return pack_records(list(self.d.keys()), list(self.d.values()))
+
     def __len__(self):
         return len(self.d)
 
@@ -151,6 +154,9 @@ class _GpuBackend:
         self.tombs += k
         return out
 
+    def records(self) -> np.ndarray:
+        return np.frombuffer(self.L.utxo_dump(self.h), dtype=np.uint8).reshape(-1, 40)
+
     def __len__(self):
         return self.count
 
@@ -193,5 +199,40 @@ class UtxoIndex:
         t = self.probe(uniq)
         return [k for k, v in zip(uniq, t) if v == tag]
 
+    def records(self) -> np.ndarray:
+        """All live entries as 40-byte records, in canonical (txid, index) order."""
+        return sort_records(np.ascontiguousarray(self.be.records()))
+
+    def reset_records(self, recs: np.ndarray):
+        """Replace the whole index with packed records (snapshot restore: one H2D copy + insert launch)."""
+        recs = np.ascontiguousarray(recs, dtype=np.uint8).reshape(-1, 40)
+        if isinstance(self.be, _GpuBackend):
+            self.be.reset([], [])
+            if len(recs):
+                self.be.insert_records(recs)
+        else:
+            idx = recs[:, 32:36].copy().view(np.uint32).ravel()
+            tags = recs[:, 36:40].copy().view(np.uint32).ravel()
+            self.be.d = {(bytes(recs[n, :32]).hex(), int(idx[n])): int(tags[n]) for n in range(len(recs))}
+
+    def set_hash(self, tag: int = 0) -> str:
+        """K12 from the index: SHA-256 over (txid || index byte) of table ``tag`` sorted by (txid, index)
+        — byte-identical to ``Database.get_unspent_outputs_hash`` (reference database.py:827-830)."""
+        import hashlib
+        recs = self.records()
+        recs = recs[recs[:, 36:40].copy().view(np.uint32).ravel() == tag]
+        payload = np.concatenate([recs[:, :32], recs[:, 32:33]], axis=1)  # index byte (the reference's bytes([i]))
+        return hashlib.sha256(payload.tobytes()).hexdigest()
+
     def __len__(self):
         return len(self.be)
+
+
+def sort_records(recs: np.ndarray) -> np.ndarray:
+    """Sort packed records by (txid bytes, index): the SQL ``ORDER BY tx_hash, index`` order."""
+    if len(recs) < 2:
+        return recs
+    be = recs[:, :32].copy().view('>u8')  # 4 big-endian words compare like the hex strings
+    idx = recs[:, 32:36].copy().view(np.uint32).ravel()
+    order = np.lexsort((idx, be[:, 3], be[:, 2], be[:, 1], be[:, 0]))
+    return recs[order]

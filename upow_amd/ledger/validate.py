@@ -23,7 +23,7 @@ import numpy as np
 
 from ..models.transaction import Transaction
 from ..ops import p256 as op
-from ..utils import codec
+from ..utils import codec, metrics
 from ..utils.codec import TransactionType
 from ..utils.logger import get_logger
 
@@ -171,4 +171,8 @@ async def verify_block_transactions(transactions: List[Transaction], device: Opt
     t4 = perf_counter()
     timings.update({'decompress_s': t1 - t0, 'collect_s': t2 - t1, 'ecdsa_s': t3 - t2, 'rules_s': t4 - t3,
                     'signatures': n, 'txs': len(transactions)})
+    metrics.inc('upow_signatures_verified_total', n, help='P-256 signatures verified in block validation')
+    for stage in ('decompress', 'collect', 'ecdsa', 'rules'):
+        metrics.set_gauge('upow_block_stage_seconds', timings[stage + '_s'], labels={'stage': stage},
+                          help='stage wall time of the last validated block')
     return bad

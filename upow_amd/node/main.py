@@ -21,7 +21,7 @@ from decimal import Decimal
 from typing import Annotated, Union
 
 from fastapi import Body, FastAPI, Header, Query
-from fastapi.responses import RedirectResponse
+from fastapi.responses import PlainTextResponse, RedirectResponse
 from starlette.background import BackgroundTask, BackgroundTasks
 from starlette.middleware.cors import CORSMiddleware
 from starlette.requests import Request
@@ -32,6 +32,7 @@ from ..constants import ENDIAN, GENESIS_PREV_HASH, MAX_SUPPLY, VERSION
 from ..ledger import manager as mgr
 from ..ledger.database import Database, UniqueViolationError
 from ..ledger.manager import (Manager, block_to_bytes, calculate_difficulty, clear_pending_transactions, create_block,
+                              ledger_lock,
                               create_block_in_syncing_old, get_circulating_supply, get_difficulty,
                               get_inodes_from_cache, get_transactions_merkle_tree, split_block_content)
 from ..models.transaction import CoinbaseTransaction, Transaction
@@ -65,6 +66,12 @@ async def lifespan(app: FastAPI):
         yield
     finally:
         await shutdown_websocket_manager()
+        if db is not None and db.path != ':memory:' and os.environ.get('UPOW_SNAPSHOT', '1') != '0':
+            try:  # checkpoint the UTXO index so the next start skips the SQL rebuild (ledger/snapshot.py)
+                from ..ledger import snapshot
+                snapshot.save(db)
+            except Exception as e:
+                logger.error(f'UTXO snapshot on shutdown failed: {e}')
 
 
 async def startup():
@@ -159,7 +166,8 @@ async def _sync_blockchain(node_url: str = None):
                     last_common_block = local_block['block']['id']
                     local_cache = local_blocks[:n]
                     local_cache.reverse()
-                    await db.remove_blocks(last_common_block + 1)
+                    async with ledger_lock():
+                        await db.remove_blocks(last_common_block + 1)
                     break
     limit = 1000
     while True:
@@ -186,7 +194,8 @@ async def _sync_blockchain(node_url: str = None):
             logger.error(error[0] if error else e)
             if local_cache is not None:
                 logger.info('sync failed, reverting back to previous chain')
-                await db.delete_blocks(last_common_block)
+                async with ledger_lock():
+                    await db.delete_blocks(last_common_block)
                 await create_blocks(local_cache)
             return error[0] if error else e
 
@@ -573,6 +582,16 @@ async def add_node(request: Request, url: str, background_tasks: BackgroundTasks
 @app.get('/get_nodes')
 async def get_nodes():
     return {'ok': True, 'result': NodesManager.get_recent_nodes()[:100]}
+
+
+@app.get('/metrics')
+async def metrics_endpoint():
+    """Prometheus text exposition of the node's counters (utils/metrics.py). Not in the reference."""
+    from ..utils import metrics
+    metrics.set_gauge('upow_mempool_size', db._q1('SELECT COUNT(*) FROM pending_transactions')[0],
+                      help='pending transactions')
+    metrics.set_gauge('upow_chain_height', db._tip_id(), help='id of the last applied block')
+    return PlainTextResponse(metrics.prometheus_text(), media_type='text/plain; version=0.0.4')
 
 
 @app.get('/get_pending_transactions')

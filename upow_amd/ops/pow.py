@@ -8,10 +8,12 @@ from __future__ import annotations
 
 import hashlib
 import os
+import time
 from dataclasses import dataclass
 from typing import List, Optional
 
 from ..models.block import PowTarget
+from ..utils import metrics
 from .native import gpu_available, lib
 
 NONCE_SPACE = 1 << 32
@@ -70,12 +72,18 @@ def search(job: PowJob, start: int = 0, count: int = NONCE_SPACE, device: Option
     L = lib()
     if device is None:
         device = 'gpu' if gpu_available() else 'cpu'
+    t0 = time.perf_counter()
     if device == 'gpu':
         searched, hits, words = L.pow_search_gpu(*job.native_args(), start, count, grid_blocks, chunk_iters,
                                                  cap, variant)
     else:
         searched, hits, words = L.pow_search_host(*job.native_args(), start, count,
                                                   threads or max(1, os.cpu_count() or 1))
+    dt = time.perf_counter() - t0
+    metrics.inc('upow_pow_hashes_total', searched, labels={'device': device}, help='nonces hashed by PoW search')
+    if dt > 0:
+        metrics.set_gauge('upow_pow_hashrate', searched / dt, labels={'device': device},
+                          help='H/s of the last PoW search call')
     nonces = []
     for w in sorted(words):
         n = job.word_to_nonce(w)

@@ -3,11 +3,14 @@
 ``python -m upow_amd.tools rebuild-utxo``: rebuild the UTXO set by replaying every transaction in
 block order (reference: create_unspent_outputs.py:9-45, database.py:846-862).
 ``python -m upow_amd.tools utxo-hash``: print the UTXO-set hash served at ``GET /``.
+``python -m upow_amd.tools snapshot [--out FILE]``: checkpoint the UTXO index at the tip (ledger/snapshot.py).
+``python -m upow_amd.tools verify-utxo``: audit the UTXO index against the SQL tables (K12 hash + sets).
 """
 from __future__ import annotations
 
 import argparse
 import asyncio
+import json
 import sys
 
 from .ledger.database import Database
@@ -27,11 +30,21 @@ async def rebuild_utxo(path: str = None):
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument('command', choices=['rebuild-utxo', 'utxo-hash'])
+    ap.add_argument('command', choices=['rebuild-utxo', 'utxo-hash', 'snapshot', 'verify-utxo'])
     ap.add_argument('--db', default=None)
+    ap.add_argument('--out', default=None)
     a = ap.parse_args(argv)
     if a.command == 'rebuild-utxo':
         asyncio.run(rebuild_utxo(a.db))
+    elif a.command in ('snapshot', 'verify-utxo'):
+        from .ledger import snapshot
+
+        async def s():
+            db = await Database.create(path=a.db)
+            res = snapshot.save(db, a.out) if a.command == 'snapshot' else snapshot.verify(db)
+            print(json.dumps(res))
+            return 0 if res.get('ok', True) else 1
+        return asyncio.run(s())
     else:
         async def h():
             db = await Database.create(path=a.db)
