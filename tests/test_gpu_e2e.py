@@ -53,3 +53,16 @@ def test_gpu_miner_against_node(gpu, tmp_path):
             node.wait(20)
         except subprocess.TimeoutExpired:
             node.kill()
+
+
+@pytest.mark.gpu
+def test_rccl_collectives_and_sharded_verify(gpu):
+    """Every collective of parallel/ on a real RCCL process group (1 rank, forced)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, UPOW_FORCE_DIST='1', PYTHONPATH=ROOT + os.pathsep + os.environ.get('PYTHONPATH', ''))
+    r = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '1',
+                        '--master-addr', '127.0.0.1', '--master-port', '29541', 'scripts/rccl_selfcheck.py'],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert '"rccl_selfcheck": "ok"' in r.stdout and '"backend": "nccl"' in r.stdout
