@@ -11,6 +11,10 @@
 namespace py = pybind11;
 using namespace upow;
 
+namespace upow {
+void register_txcodec(py::module_& m);  // txcodec.cpp
+}
+
 static PowJobHost make_job(py::bytes header, uint32_t tmask, uint32_t tword, uint32_t frac_shift,
                            uint32_t frac_limit) {
     PowJobHost j;
@@ -42,6 +46,7 @@ static void packed_args(py::buffer data, py::buffer offsets, const uint8_t*& d, 
 
 PYBIND11_MODULE(_native, m) {
     m.doc() = "upow_amd native core: host C++ crypto + gfx950 HIP kernels";
+    register_txcodec(m);
 
     m.def("sha256", [](py::bytes msg) {
         std::string s = msg;
@@ -161,10 +166,24 @@ PYBIND11_MODULE(_native, m) {
     m.def("utxo_create", &utxo_create);
     m.def("utxo_destroy", &utxo_destroy);
     m.def("utxo_capacity", &utxo_capacity);
-    m.def("utxo_insert", [recs_arg](int64_t h, py::buffer recs) {
+    m.def("utxo_insert", [recs_arg](int64_t h, py::buffer recs, py::object payload) {
         int64_t n; const uint8_t* p = recs_arg(recs, n);
+        const uint8_t* pp = nullptr;
+        py::buffer_info pi;
+        if (!payload.is_none()) {
+            pi = payload.cast<py::buffer>().request();
+            if (pi.size * pi.itemsize != n * 80) throw std::invalid_argument("payload must be n x 80 bytes");
+            pp = static_cast<const uint8_t*>(pi.ptr);
+        }
         py::gil_scoped_release rel;
-        return utxo_insert(h, p, n);
+        return utxo_insert(h, p, n, pp);
+    }, py::arg("h"), py::arg("recs"), py::arg("payload") = py::none());
+    m.def("utxo_lookup", [recs_arg](int64_t h, py::buffer recs) {
+        int64_t n; const uint8_t* p = recs_arg(recs, n);
+        std::vector<uint8_t> o, pay;
+        { py::gil_scoped_release rel; o = utxo_lookup(h, p, n, pay); }
+        return py::make_tuple(py::bytes(reinterpret_cast<const char*>(o.data()), o.size()),
+                              py::bytes(reinterpret_cast<const char*>(pay.data()), pay.size()));
     });
     m.def("utxo_probe", [recs_arg](int64_t h, py::buffer recs) {
         int64_t n; const uint8_t* p = recs_arg(recs, n);
@@ -180,8 +199,14 @@ PYBIND11_MODULE(_native, m) {
     });
     m.def("utxo_dump", [](int64_t h) {
         std::vector<uint8_t> o;
-        { py::gil_scoped_release rel; o = utxo_dump(h); }
+        { py::gil_scoped_release rel; o = utxo_dump(h, nullptr); }
         return py::bytes(reinterpret_cast<const char*>(o.data()), o.size());
+    });
+    m.def("utxo_dump_payload", [](int64_t h) {
+        std::vector<uint8_t> o, pay;
+        { py::gil_scoped_release rel; o = utxo_dump(h, &pay); }
+        return py::make_tuple(py::bytes(reinterpret_cast<const char*>(o.data()), o.size()),
+                              py::bytes(reinterpret_cast<const char*>(pay.data()), pay.size()));
     });
 
     m.def("b58encode", [](py::bytes b) {

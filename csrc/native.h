@@ -49,10 +49,12 @@ bool p256_sign(const uint8_t d_be[32], const uint8_t digest[32], uint8_t r_le[32
 int64_t utxo_create(uint32_t log2_cap);
 void utxo_destroy(int64_t h);
 uint32_t utxo_capacity(int64_t h);
-uint32_t utxo_insert(int64_t h, const uint8_t* recs, int64_t n);  // returns #failed (table full)
+// payload records: 80 bytes {u64 amount, u32 address length, u32 pad, address[64]} (nullptr = zeros)
+uint32_t utxo_insert(int64_t h, const uint8_t* recs, int64_t n, const uint8_t* payload);  // #failed (full)
 std::vector<uint8_t> utxo_probe(int64_t h, const uint8_t* recs, int64_t n);  // tag or 0xff
+std::vector<uint8_t> utxo_lookup(int64_t h, const uint8_t* recs, int64_t n, std::vector<uint8_t>& payload_out);
 std::vector<uint8_t> utxo_erase(int64_t h, const uint8_t* recs, int64_t n);  // 1 if erased
-std::vector<uint8_t> utxo_dump(int64_t h);
+std::vector<uint8_t> utxo_dump(int64_t h, std::vector<uint8_t>* payload_out);
 
 // ---------------------------------------------------------------- base58
 std::string b58encode(const uint8_t* data, size_t n);

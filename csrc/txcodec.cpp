@@ -1,0 +1,506 @@
+// Native block-transaction codec: the whole-block replacement of Transaction.parse + hex() + txid.
+//
+// reference: upow/upow_transactions/transaction.py:46-88 (hex / hash), 520-592 (from_hex),
+// transaction_output.py (tobytes), helpers.py:160-192 (address strings). The node receives a block
+// as a list of tx hex strings (POST /push_block, sync pages); the Python object model costs ~20 µs
+// per tx just to parse and re-serialise. Here one call, threaded over the txs with the GIL released:
+//
+//   hex -> bytes -> fields (same reading rules as Transaction.parse)
+//       -> canonical re-serialisation (exactly what Transaction.hex() would produce: normalised
+//          address prefix, minimal amount length, de-duplicated signatures)
+//       -> txid = SHA-256(canonical bytes), signed-message digest = SHA-256(hex(False) bytes)
+//       -> address strings (base58 / hex), outputs JSON columns, merkle root
+//
+// A tx the fast path does not cover (coinbase specifier, grouped signatures that need ledger public
+// keys, amounts wider than 64 bits, governance output types, malformed encodings, ...) is flagged;
+// the caller then runs the general Python path for the whole block, which reproduces the
+// reference's exact behaviour and error messages.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "native.h"
+#include "sha256_common.h"
+
+namespace py = pybind11;
+
+namespace upow {
+
+enum TxFlag : uint8_t {
+    TX_FAST = 0,      // fully decoded, regular outputs, 1-or-n signatures
+    TX_GENERAL = 1,   // valid encoding the fast path does not handle
+    TX_MALFORMED = 2  // the Python parser has to see it (it raises or reads it leniently)
+};
+
+struct DecIn {
+    uint8_t txid[32];
+    uint8_t index, type;
+    int32_t sig;  // index into the tx's unique-signature list
+};
+struct DecOut {
+    uint8_t addr[64];
+    uint8_t len;
+    uint8_t type;
+    uint64_t amount;
+};
+struct DecTx {
+    uint8_t flag = TX_MALFORMED;
+    uint8_t version = 0;
+    bool canonical = false;
+    int32_t msg_off = -1, msg_len = 0;  // into canon bytes
+    int32_t signed_len = 0;             // hex(False) byte length (a prefix of canon)
+    std::vector<DecIn> ins;
+    std::vector<DecOut> outs;
+    std::vector<uint8_t> sigs;  // unique signatures, 64 B each (r LE | s LE)
+    std::vector<uint8_t> canon;
+    uint8_t txid[32];
+    uint8_t digest[32];
+    std::vector<std::string> out_addr;  // bytes_to_string form
+    std::string out_addr_json, out_amount_json;
+};
+
+static inline int hexval(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+}
+
+static const char kHex[] = "0123456789abcdef";
+
+static std::string to_hex(const uint8_t* p, size_t n) {
+    std::string s(2 * n, '0');
+    for (size_t i = 0; i < n; ++i) {
+        s[2 * i] = kHex[p[i] >> 4];
+        s[2 * i + 1] = kHex[p[i] & 15];
+    }
+    return s;
+}
+
+// base58 of a 33-byte compressed address, memoised per thread (blocks pay the same few addresses
+// over and over: change outputs, exchanges, pools)
+static std::string b58_33(const uint8_t b[33]) {
+    thread_local std::unordered_map<std::string, std::string> cache;
+    std::string key(reinterpret_cast<const char*>(b), 33);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    if (cache.size() > (1u << 16)) cache.clear();
+    std::string s = b58encode(b, 33);
+    cache.emplace(std::move(key), s);
+    return s;
+}
+
+// bytes_to_string (codec.py): 64 B -> hex, 33 B -> base58 of normalised prefix || x
+static std::string addr_string(const uint8_t* a, int len) {
+    if (len == 64) return to_hex(a, 64);
+    uint8_t b[33];
+    b[0] = a[0] == 43 ? 43 : 42;
+    std::memcpy(b + 1, a + 1, 32);
+    return b58_33(b);
+}
+
+// True when string_to_bytes(s) would take the bytes.fromhex branch (an all-hex base58 string of even
+// length): the Python path would then misread the address, so leave such outputs to it.
+static bool hex_ambiguous(const std::string& s) {
+    if (s.size() % 2) return false;
+    for (char c : s)
+        if (hexval(c) < 0) return false;
+    return true;
+}
+
+static void decode_one(const char* hx, size_t hlen, DecTx& t) {
+    t = DecTx();
+    if (hlen % 2) return;
+    std::vector<uint8_t> b(hlen / 2);
+    for (size_t i = 0; i < b.size(); ++i) {
+        const int hi = hexval(hx[2 * i]), lo = hexval(hx[2 * i + 1]);
+        if (hi < 0 || lo < 0) return;  // whitespace etc.: bytes.fromhex semantics are the parser's business
+        b[i] = uint8_t(hi << 4 | lo);
+    }
+    const size_t n = b.size();
+    size_t p = 0;
+    auto need = [&](size_t k) { return p + k <= n; };
+    if (!need(2)) return;
+    t.version = b[p++];
+    if (t.version > 3) return;  // NotImplementedError in the parser
+    const int n_in = b[p++];
+    t.ins.resize(static_cast<size_t>(n_in));
+    for (auto& in : t.ins) {
+        if (!need(34)) return;
+        std::memcpy(in.txid, &b[p], 32);
+        in.index = b[p + 32];
+        in.type = b[p + 33];
+        p += 34;
+        if (in.type != 0 && in.type != 10) return;  // InputType(..) raises
+    }
+    if (!need(1)) return;
+    const int n_out = b[p++];
+    t.outs.resize(size_t(n_out));
+    bool general = false;
+    const int alen = t.version == 1 ? 64 : 33;
+    for (auto& o : t.outs) {
+        if (!need(size_t(alen) + 1)) return;
+        std::memcpy(o.addr, &b[p], size_t(alen));
+        o.len = uint8_t(alen);
+        p += size_t(alen);
+        const int amount_len = b[p++];
+        if (!need(size_t(amount_len) + 1)) return;
+        uint64_t amount = 0;
+        for (int k = 0; k < amount_len; ++k) {
+            if (k >= 8) {
+                if (b[p + size_t(k)]) general = true;  // wider than 64 bits
+                continue;
+            }
+            amount |= uint64_t(b[p + size_t(k)]) << (8 * k);
+        }
+        o.amount = amount;
+        p += size_t(amount_len);
+        o.type = b[p++];
+        if (o.type > 9 || o.type == 4) return;  // OutputType(..) raises (values 0-3, 5-9)
+        if (o.type != 0) general = true;         // governance / stake outputs: general path
+    }
+    if (!need(1)) return;
+    const uint8_t spec = b[p++];
+    const uint8_t* msg = nullptr;
+    size_t mlen = 0;
+    bool has_msg = false;
+    if (spec == 36) {  // coinbase inside the tx list
+        t.flag = TX_GENERAL;
+        return;
+    }
+    if (spec == 1) {
+        const int lbytes = t.version <= 2 ? 1 : 2;
+        if (!need(size_t(lbytes))) return;
+        mlen = b[p] | (lbytes == 2 ? size_t(b[p + 1]) << 8 : 0);
+        p += size_t(lbytes);
+        if (!need(mlen)) return;
+        msg = &b[p];
+        p += mlen;
+        has_msg = true;
+    } else if (spec != 0) {
+        return;  // AssertionError in the parser
+    }
+    // signatures: 64-byte (r, s) pairs up to the end; a zero r or a ragged tail is parser territory
+    if ((n - p) % 64) return;
+    const size_t n_sig = (n - p) / 64;
+    std::vector<const uint8_t*> sig_ptr(n_sig);
+    for (size_t k = 0; k < n_sig; ++k) {
+        const uint8_t* s = &b[p + 64 * k];
+        bool rz = true;
+        for (int q = 0; q < 32; ++q) rz &= s[q] == 0;
+        if (rz) return;
+        sig_ptr[k] = s;
+    }
+    // signature -> input assignment (transaction.py:566-590)
+    std::vector<const uint8_t*> in_sig(static_cast<size_t>(n_in));
+    if (n_sig == 1) {
+        for (auto& s : in_sig) s = sig_ptr[0];
+    } else if (n_sig == size_t(n_in)) {
+        for (size_t k = 0; k < n_sig; ++k) in_sig[k] = sig_ptr[k];
+    } else {
+        t.flag = TX_GENERAL;  // grouped by public key: needs the ledger
+        return;
+    }
+    if (n_in == 0 || n_out == 0) general = true;
+    // canonical re-serialisation (Transaction.hex)
+    std::vector<uint8_t>& c = t.canon;
+    c.reserve(n + 16);
+    c.push_back(t.version);
+    c.push_back(uint8_t(n_in));
+    for (auto& in : t.ins) {
+        c.insert(c.end(), in.txid, in.txid + 32);
+        c.push_back(in.index);
+        c.push_back(in.type);
+    }
+    c.push_back(uint8_t(n_out));
+    for (auto& o : t.outs) {
+        if (o.len == 33) {
+            c.push_back(o.addr[0] == 43 ? 43 : 42);
+            c.insert(c.end(), o.addr + 1, o.addr + 33);
+        } else {
+            c.insert(c.end(), o.addr, o.addr + 64);
+        }
+        int bl = 0;
+        for (uint64_t a = o.amount; a; a >>= 8) ++bl;
+        c.push_back(uint8_t(bl));
+        for (int k = 0; k < bl; ++k) c.push_back(uint8_t(o.amount >> (8 * k)));
+        c.push_back(o.type);
+    }
+    t.signed_len = int32_t(c.size());
+    if (has_msg) {
+        c.push_back(1);
+        if (t.version <= 2) {
+            c.push_back(uint8_t(mlen));
+        } else {
+            c.push_back(uint8_t(mlen));
+            c.push_back(uint8_t(mlen >> 8));
+        }
+        t.msg_off = int32_t(c.size());
+        t.msg_len = int32_t(mlen);
+        c.insert(c.end(), msg, msg + mlen);
+        if (t.version >= 3) t.signed_len = int32_t(c.size());
+    } else {
+        c.push_back(0);
+    }
+    for (size_t i = 0; i < size_t(n_in); ++i) {
+        int found = -1;
+        const size_t ns = t.sigs.size() / 64;
+        for (size_t k = 0; k < ns; ++k)
+            if (std::memcmp(&t.sigs[64 * k], in_sig[i], 64) == 0) {
+                found = int(k);
+                break;
+            }
+        if (found < 0) {
+            found = int(ns);
+            t.sigs.insert(t.sigs.end(), in_sig[i], in_sig[i] + 64);
+            c.insert(c.end(), in_sig[i], in_sig[i] + 64);
+        }
+        t.ins[i].sig = found;
+    }
+    t.canonical = c.size() == n && std::memcmp(c.data(), b.data(), n) == 0;
+    host_sha256(c.data(), c.size(), t.txid);
+    host_sha256(c.data(), size_t(t.signed_len), t.digest);
+    // output address strings + JSON columns (database.add_transactions)
+    t.out_addr.reserve(t.outs.size());
+    t.out_addr_json = "[";
+    t.out_amount_json = "[";
+    for (size_t k = 0; k < t.outs.size(); ++k) {
+        std::string s = addr_string(t.outs[k].addr, t.outs[k].len);
+        if (t.outs[k].len == 33 && hex_ambiguous(s)) general = true;
+        if (k) {
+            t.out_addr_json += ',';
+            t.out_amount_json += ',';
+        }
+        t.out_addr_json += '"';
+        t.out_addr_json += s;
+        t.out_addr_json += '"';
+        t.out_amount_json += std::to_string(t.outs[k].amount);
+        t.out_addr.push_back(std::move(s));
+    }
+    t.out_addr_json += ']';
+    t.out_amount_json += ']';
+    t.flag = general ? TX_GENERAL : TX_FAST;
+}
+
+template <typename F>
+static void parallel_for(int64_t n, int threads, F&& f) {
+    threads = int(std::max<int64_t>(1, std::min<int64_t>(threads, n)));
+    if (threads == 1) {
+        for (int64_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads; ++t)
+        pool.emplace_back([&, t] {
+            for (int64_t i = t; i < n; i += threads) f(i);
+        });
+    for (auto& th : pool) th.join();
+}
+
+// merkle root: SHA-256 over the txids of the txs sorted by their canonical bytes (manager.py:365-378)
+static std::string merkle_of(const std::vector<DecTx>& txs) {
+    std::vector<int> order(txs.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = int(i);
+    std::sort(order.begin(), order.end(), [&](int a, int b) {
+        const auto& x = txs[size_t(a)].canon;
+        const auto& y = txs[size_t(b)].canon;
+        return std::lexicographical_compare(x.begin(), x.end(), y.begin(), y.end());
+    });
+    HostSha256 h;
+    for (int i : order) h.update(txs[size_t(i)].txid, 32);
+    uint8_t out[32];
+    h.final(out);
+    return to_hex(out, 32);
+}
+
+static py::bytes as_bytes(const std::vector<uint8_t>& v) {
+    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+}
+
+// decode_block_txs(hexes, threads) -> dict (see module docstring of upow_amd/ledger/fastpath.py)
+static py::dict decode_block_txs(py::list hexes, int threads) {
+    const int64_t n = int64_t(hexes.size());
+    const size_t N = static_cast<size_t>(n);
+    std::vector<std::string> src(N);
+    for (int64_t i = 0; i < n; ++i) src[size_t(i)] = hexes[size_t(i)].cast<std::string>();
+    std::vector<DecTx> txs(N);
+    const bool prof = std::getenv("UPOW_TXCODEC_PROFILE") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    {
+        py::gil_scoped_release rel;
+        parallel_for(n, threads, [&](int64_t i) { decode_one(src[size_t(i)].data(), src[size_t(i)].size(), txs[size_t(i)]); });
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    py::dict d;
+    std::vector<uint8_t> flags(N), version(N);
+    std::vector<int32_t> in_start(N + 1), out_start(N + 1), sig_start(N + 1), signed_len(N), msg_off(N), msg_len(N),
+        hex_len(N);
+    int64_t n_in = 0, n_out = 0, n_sig = 0;
+    bool all_fast = true;
+    for (int64_t i = 0; i < n; ++i) {
+        const DecTx& t = txs[size_t(i)];
+        flags[size_t(i)] = t.flag;
+        all_fast &= t.flag == TX_FAST;
+        version[size_t(i)] = t.version;
+        in_start[size_t(i)] = int32_t(n_in);
+        out_start[size_t(i)] = int32_t(n_out);
+        sig_start[size_t(i)] = int32_t(n_sig);
+        n_in += int64_t(t.ins.size());
+        n_out += int64_t(t.outs.size());
+        n_sig += int64_t(t.sigs.size() / 64);
+        signed_len[size_t(i)] = t.signed_len;
+        msg_off[size_t(i)] = t.msg_off;
+        msg_len[size_t(i)] = t.msg_len;
+        hex_len[size_t(i)] = int32_t(2 * t.canon.size());
+    }
+    in_start[size_t(n)] = int32_t(n_in);
+    out_start[size_t(n)] = int32_t(n_out);
+    sig_start[size_t(n)] = int32_t(n_sig);
+    auto i32 = [](const std::vector<int32_t>& v) {
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size() * 4);
+    };
+    d["n"] = n;
+    d["all_fast"] = all_fast;
+    d["flags"] = as_bytes(flags);
+    d["version"] = as_bytes(version);
+    d["in_start"] = i32(in_start);
+    d["out_start"] = i32(out_start);
+    d["sig_start"] = i32(sig_start);
+    d["signed_len"] = i32(signed_len);
+    d["msg_off"] = i32(msg_off);
+    d["msg_len"] = i32(msg_len);
+    d["hex_len"] = i32(hex_len);
+    if (!all_fast) return d;  // the caller takes the general path; skip building the rest
+
+    const size_t NI = static_cast<size_t>(n_in), NO = static_cast<size_t>(n_out), NS = static_cast<size_t>(n_sig);
+    std::vector<uint8_t> in_keys(NI * 40, 0), in_type(NI), sigs(NS * 64), txid(N * 32), digest(N * 32),
+        out_addr(NO * 64, 0), out_len(NO), out_type(NO);
+    std::vector<int32_t> in_sig(NI), in_tx(NI), out_tx(NO);
+    std::vector<uint64_t> out_amount(NO);
+    py::list canon_hex(N), tx_hash(N), out_addr_str(NO), out_addr_json(N), out_amount_json(N);
+    for (int64_t i = 0; i < n; ++i) {
+        const DecTx& t = txs[size_t(i)];
+        std::memcpy(&txid[32 * size_t(i)], t.txid, 32);
+        std::memcpy(&digest[32 * size_t(i)], t.digest, 32);
+        size_t k = size_t(in_start[size_t(i)]);
+        for (const DecIn& in : t.ins) {
+            std::memcpy(&in_keys[40 * k], in.txid, 32);
+            const uint32_t idx = in.index, tag = 0xffu;
+            std::memcpy(&in_keys[40 * k + 32], &idx, 4);
+            std::memcpy(&in_keys[40 * k + 36], &tag, 4);
+            in_type[k] = in.type;
+            in_sig[k] = sig_start[size_t(i)] + in.sig;
+            in_tx[k] = int32_t(i);
+            ++k;
+        }
+        std::memcpy(&sigs[64 * size_t(sig_start[size_t(i)])], t.sigs.data(), t.sigs.size());
+        size_t o = size_t(out_start[size_t(i)]);
+        for (size_t j = 0; j < t.outs.size(); ++j, ++o) {
+            std::memcpy(&out_addr[64 * o], t.outs[j].addr, t.outs[j].len);
+            out_len[o] = t.outs[j].len;
+            out_type[o] = t.outs[j].type;
+            out_amount[o] = t.outs[j].amount;
+            out_tx[o] = int32_t(i);
+            out_addr_str[o] = py::str(t.out_addr[j]);
+        }
+        canon_hex[size_t(i)] = t.canonical && src[size_t(i)].size() == 2 * t.canon.size() &&
+                                       std::all_of(src[size_t(i)].begin(), src[size_t(i)].end(),
+                                                   [](char ch) { return !(ch >= 'A' && ch <= 'F'); })
+                                   ? py::object(hexes[size_t(i)])
+                                   : py::object(py::str(to_hex(t.canon.data(), t.canon.size())));
+        tx_hash[size_t(i)] = py::str(to_hex(t.txid, 32));
+        out_addr_json[size_t(i)] = py::str(t.out_addr_json);
+        out_amount_json[size_t(i)] = py::str(t.out_amount_json);
+    }
+    d["in_keys"] = as_bytes(in_keys);
+    d["in_type"] = as_bytes(in_type);
+    d["in_sig"] = i32(in_sig);
+    d["in_tx"] = i32(in_tx);
+    d["sigs"] = as_bytes(sigs);
+    d["txid"] = as_bytes(txid);
+    d["digest"] = as_bytes(digest);
+    d["out_addr"] = as_bytes(out_addr);
+    d["out_len"] = as_bytes(out_len);
+    d["out_type"] = as_bytes(out_type);
+    d["out_tx"] = i32(out_tx);
+    d["out_amount"] = py::bytes(reinterpret_cast<const char*>(out_amount.data()), out_amount.size() * 8);
+    d["hex"] = canon_hex;
+    d["tx_hash"] = tx_hash;
+    d["out_addr_str"] = out_addr_str;
+    d["out_addr_json"] = out_addr_json;
+    d["out_amount_json"] = out_amount_json;
+    auto t2 = std::chrono::steady_clock::now();
+    d["merkle"] = merkle_of(txs);
+    if (prof) {
+        auto t3 = std::chrono::steady_clock::now();
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "[txcodec] decode %.2f ms, python objects %.2f ms, merkle %.2f ms\n", ms(t0, t1),
+                     ms(t1, t2), ms(t2, t3));
+    }
+    return d;
+}
+
+// Canonical compressed address strings for spent outputs (database._input_address): 33-byte
+// addresses keep x with the normalised prefix, 64-byte ones take the parity of y. Returns the
+// per-input strings and, per tx, the inputs_addresses JSON column.
+static py::tuple input_address_strings(py::bytes addrs64, py::bytes lens, py::bytes in_start_b, int threads) {
+    std::string a = addrs64, l = lens, s = in_start_b;
+    const size_t n_in = l.size();
+    const size_t n_tx = s.size() / 4 - 1;
+    if (a.size() != 64 * n_in) throw std::invalid_argument("addrs64 must be 64 bytes per input");
+    const int32_t* st = reinterpret_cast<const int32_t*>(s.data());
+    std::vector<std::string> out(n_in);
+    std::vector<uint8_t> bad(n_in, 0);
+    {
+        py::gil_scoped_release rel;
+        parallel_for(int64_t(n_in), threads, [&](int64_t i) {
+            const uint8_t* p = reinterpret_cast<const uint8_t*>(a.data()) + 64 * size_t(i);
+            uint8_t c[33];
+            if (uint8_t(l[size_t(i)]) == 33) {
+                c[0] = p[0] == 43 ? 43 : 42;
+                std::memcpy(c + 1, p + 1, 32);
+            } else if (uint8_t(l[size_t(i)]) == 64) {
+                c[0] = (p[32] & 1) ? 43 : 42;  // y little-endian: parity is bit 0 of byte 32
+                std::memcpy(c + 1, p, 32);
+            } else {
+                bad[size_t(i)] = 1;
+                return;
+            }
+            out[size_t(i)] = b58_33(c);
+        });
+    }
+    for (size_t i = 0; i < n_in; ++i)
+        if (bad[i]) throw std::invalid_argument("input address payload missing");
+    py::list strs(n_in), json(n_tx);
+    for (size_t i = 0; i < n_in; ++i) strs[i] = py::str(out[i]);
+    for (size_t t = 0; t < n_tx; ++t) {
+        std::string j = "[";
+        for (int32_t k = st[t]; k < st[t + 1]; ++k) {
+            if (k > st[t]) j += ',';
+            j += '"';
+            j += out[size_t(k)];
+            j += '"';
+        }
+        j += ']';
+        json[t] = py::str(j);
+    }
+    return py::make_tuple(strs, json);
+}
+
+void register_txcodec(py::module_& m) {
+    m.def("decode_block_txs", &decode_block_txs, py::arg("hexes"), py::arg("threads") = 8,
+          "Decode, canonicalise and hash a block's transactions (see csrc/txcodec.cpp)");
+    m.def("input_address_strings", &input_address_strings, py::arg("addrs64"), py::arg("lens"), py::arg("in_start"),
+          py::arg("threads") = 8);
+}
+
+}  // namespace upow

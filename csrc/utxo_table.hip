@@ -1,4 +1,4 @@
-// K7/K8/K9: HBM-resident UTXO hash index (outpoint -> output-table tag) for gfx950.
+// K7/K8/K9: HBM-resident UTXO set (outpoint -> output-table tag, amount, owner address) for gfx950.
 //
 // reference: the seven per-type output tables queried/inserted/deleted with
 // `(tx_hash, index) = ANY($1::tx_output[])` (upow/database.py:439-825, used by upow/manager.py:531-543
@@ -11,6 +11,11 @@
 // CAS on its meta word and publish it with an atomic exchange after the key words.
 // The table lives in HBM for the life of the node (288 GB leaves room for ~10^9 outpoints); the
 // txid's first word is already uniformly random, so it is the hash.
+//
+// Each slot has an 80-byte payload in a parallel array {amount u64, address length u32, pad,
+// address bytes[64]} — what block validation needs from a spent output (fees, signature key,
+// inputs_addresses) without touching the SQL tables. Probing scans only the compact 48-byte key
+// slots; the payload line is read once, on a hit.
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -40,6 +45,14 @@ struct UtxoKeyRec {  // 40 bytes: txid (raw bytes), index, tag
 };
 static_assert(sizeof(UtxoKeyRec) == 40, "key record");
 
+struct alignas(16) UtxoPayload {  // 80 bytes
+    uint64_t amount;
+    uint32_t addr_len;
+    uint32_t pad;
+    uint8_t addr[64];
+};
+static_assert(sizeof(UtxoPayload) == 80, "payload");
+
 __device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) {
     return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
 }
@@ -61,8 +74,9 @@ __device__ __forceinline__ bool key_eq(const UtxoSlot& s, const uint32_t k[8]) {
     return d == 0;
 }
 
-__global__ __launch_bounds__(256) void utxo_insert_kernel(UtxoSlot* __restrict__ tab, uint32_t mask,
-                                                          const UtxoKeyRec* __restrict__ recs, int64_t n,
+__global__ __launch_bounds__(256) void utxo_insert_kernel(UtxoSlot* __restrict__ tab, UtxoPayload* __restrict__ pay,
+                                                          uint32_t mask, const UtxoKeyRec* __restrict__ recs,
+                                                          const UtxoPayload* __restrict__ in_pay, int64_t n,
                                                           uint32_t* __restrict__ failed) {
     const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -78,6 +92,12 @@ __global__ __launch_bounds__(256) void utxo_insert_kernel(UtxoSlot* __restrict__
             if (atomicCAS(mp, m, ST_BUSY) == m) {
 #pragma unroll
                 for (int w = 0; w < 8; ++w) tab[s].k[w] = k[w];
+                if (in_pay) {
+                    pay[s] = in_pay[i];
+                } else {
+                    pay[s].amount = 0;
+                    pay[s].addr_len = 0;
+                }
                 __threadfence();
                 atomicExch(mp, ST_FULL | (idx << 8) | (tag << 16));
                 return;
@@ -114,6 +134,40 @@ __global__ __launch_bounds__(256) void utxo_probe_kernel(const UtxoSlot* __restr
     tags_out[i] = res;
 }
 
+// lookup = probe + payload gather (payload zeroed when absent)
+__global__ __launch_bounds__(256) void utxo_lookup_kernel(const UtxoSlot* __restrict__ tab,
+                                                          const UtxoPayload* __restrict__ pay, uint32_t mask,
+                                                          const UtxoKeyRec* __restrict__ recs, int64_t n,
+                                                          uint8_t* __restrict__ tags_out,
+                                                          UtxoPayload* __restrict__ pay_out) {
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t k[8];
+    load_key(recs[i], k);
+    const uint32_t idx = recs[i].index & 0xffu;
+    uint32_t s = slot_hash(k, idx) & mask;
+    uint8_t res = 0xff;
+    int64_t hit = -1;
+    for (uint32_t probe = 0; probe <= mask; ++probe) {
+        const uint32_t m = tab[s].meta;
+        const uint32_t st = m & 3u;
+        if (st == ST_EMPTY) break;
+        if (st == ST_FULL && ((m >> 8) & 0xffu) == idx && key_eq(tab[s], k)) {
+            res = uint8_t((m >> 16) & 0xffu);
+            hit = s;
+            break;
+        }
+        s = (s + 1) & mask;
+    }
+    tags_out[i] = res;
+    if (hit >= 0) {
+        pay_out[i] = pay[hit];
+    } else {
+        UtxoPayload z{};
+        pay_out[i] = z;
+    }
+}
+
 // erase: only entries whose tag matches recs[i].tag (0xff = any); erased[i] = 1 when removed
 __global__ __launch_bounds__(256) void utxo_erase_kernel(UtxoSlot* __restrict__ tab, uint32_t mask,
                                                          const UtxoKeyRec* __restrict__ recs, int64_t n,
@@ -144,8 +198,10 @@ __global__ __launch_bounds__(256) void utxo_erase_kernel(UtxoSlot* __restrict__ 
     erased[i] = res;
 }
 
-__global__ __launch_bounds__(256) void utxo_dump_kernel(const UtxoSlot* __restrict__ tab, uint32_t cap,
-                                                        UtxoKeyRec* __restrict__ out, uint32_t* __restrict__ count) {
+__global__ __launch_bounds__(256) void utxo_dump_kernel(const UtxoSlot* __restrict__ tab,
+                                                        const UtxoPayload* __restrict__ pay, uint32_t cap,
+                                                        UtxoKeyRec* __restrict__ out, UtxoPayload* __restrict__ pay_out,
+                                                        uint32_t* __restrict__ count) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= cap) return;
     const uint32_t m = tab[s].meta;
@@ -162,6 +218,7 @@ __global__ __launch_bounds__(256) void utxo_dump_kernel(const UtxoSlot* __restri
     r.index = (m >> 8) & 0xffu;
     r.tag = (m >> 16) & 0xffu;
     out[o] = r;
+    if (pay_out) pay_out[o] = pay[s];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -172,6 +229,7 @@ static void uck(hipError_t e, const char* what) {
 struct UtxoTableDev {
     int device = 0;
     UtxoSlot* tab = nullptr;
+    UtxoPayload* pay = nullptr;
     uint32_t cap = 0;
     uint32_t* d_counter = nullptr;
 };
@@ -196,6 +254,7 @@ int64_t utxo_create(uint32_t log2_cap) {
     t.cap = 1u << log2_cap;
     uck(hipMalloc(&t.tab, sizeof(UtxoSlot) * size_t(t.cap)), "hipMalloc utxo table");
     uck(hipMemset(t.tab, 0, sizeof(UtxoSlot) * size_t(t.cap)), "memset utxo table");
+    uck(hipMalloc(&t.pay, sizeof(UtxoPayload) * size_t(t.cap)), "hipMalloc utxo payload");
     uck(hipMalloc(&t.d_counter, sizeof(uint32_t)), "hipMalloc counter");
     std::lock_guard<std::mutex> lk(g_ut_mu);
     const int64_t h = g_next_handle++;
@@ -208,6 +267,7 @@ void utxo_destroy(int64_t h) {
     auto it = g_tables.find(h);
     if (it == g_tables.end()) return;
     (void)hipFree(it->second.tab);
+    (void)hipFree(it->second.pay);
     (void)hipFree(it->second.d_counter);
     g_tables.erase(it);
 }
@@ -224,19 +284,39 @@ struct DevBuf {
     ~DevBuf() { (void)hipFree(p); }
 };
 
-uint32_t utxo_insert(int64_t h, const uint8_t* recs, int64_t n) {
+uint32_t utxo_insert(int64_t h, const uint8_t* recs, int64_t n, const uint8_t* payload) {
     std::lock_guard<std::mutex> lk(g_ut_mu);
     UtxoTableDev& t = table(h);
     if (n == 0) return 0;
     DevBuf<UtxoKeyRec> d(n);
     uck(hipMemcpy(d.p, recs, sizeof(UtxoKeyRec) * n, hipMemcpyHostToDevice), "h2d recs");
+    DevBuf<UtxoPayload> dp(payload ? n : 0);
+    if (payload) uck(hipMemcpy(dp.p, payload, sizeof(UtxoPayload) * n, hipMemcpyHostToDevice), "h2d payload");
     uck(hipMemset(t.d_counter, 0, sizeof(uint32_t)), "memset");
-    hipLaunchKernelGGL(utxo_insert_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, 0, t.tab, t.cap - 1, d.p, n,
-                       t.d_counter);
+    hipLaunchKernelGGL(utxo_insert_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, 0, t.tab, t.pay, t.cap - 1, d.p,
+                       payload ? dp.p : nullptr, n, t.d_counter);
     uck(hipGetLastError(), "utxo_insert_kernel");
     uint32_t failed = 0;
     uck(hipMemcpy(&failed, t.d_counter, sizeof(uint32_t), hipMemcpyDeviceToHost), "d2h failed");
     return failed;
+}
+
+std::vector<uint8_t> utxo_lookup(int64_t h, const uint8_t* recs, int64_t n, std::vector<uint8_t>& payload_out) {
+    std::lock_guard<std::mutex> lk(g_ut_mu);
+    UtxoTableDev& t = table(h);
+    std::vector<uint8_t> out(static_cast<size_t>(n));
+    payload_out.assign(static_cast<size_t>(n) * sizeof(UtxoPayload), 0);
+    if (n == 0) return out;
+    DevBuf<UtxoKeyRec> d(n);
+    DevBuf<uint8_t> o(n);
+    DevBuf<UtxoPayload> po(n);
+    uck(hipMemcpy(d.p, recs, sizeof(UtxoKeyRec) * n, hipMemcpyHostToDevice), "h2d recs");
+    hipLaunchKernelGGL(utxo_lookup_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, 0, t.tab, t.pay, t.cap - 1, d.p, n,
+                       o.p, po.p);
+    uck(hipGetLastError(), "utxo_lookup_kernel");
+    uck(hipMemcpy(out.data(), o.p, size_t(n), hipMemcpyDeviceToHost), "d2h tags");
+    uck(hipMemcpy(payload_out.data(), po.p, payload_out.size(), hipMemcpyDeviceToHost), "d2h payload");
+    return out;
 }
 
 std::vector<uint8_t> utxo_probe(int64_t h, const uint8_t* recs, int64_t n) {
@@ -269,18 +349,23 @@ std::vector<uint8_t> utxo_erase(int64_t h, const uint8_t* recs, int64_t n) {
     return out;
 }
 
-std::vector<uint8_t> utxo_dump(int64_t h) {
+std::vector<uint8_t> utxo_dump(int64_t h, std::vector<uint8_t>* payload_out) {
     std::lock_guard<std::mutex> lk(g_ut_mu);
     UtxoTableDev& t = table(h);
     DevBuf<UtxoKeyRec> d(t.cap);
+    DevBuf<UtxoPayload> dp(payload_out ? t.cap : 0);
     uck(hipMemset(t.d_counter, 0, sizeof(uint32_t)), "memset");
-    hipLaunchKernelGGL(utxo_dump_kernel, dim3(int((t.cap + 255) / 256)), dim3(256), 0, 0, t.tab, t.cap, d.p,
-                       t.d_counter);
+    hipLaunchKernelGGL(utxo_dump_kernel, dim3(int((t.cap + 255) / 256)), dim3(256), 0, 0, t.tab, t.pay, t.cap, d.p,
+                       payload_out ? dp.p : nullptr, t.d_counter);
     uck(hipGetLastError(), "utxo_dump_kernel");
     uint32_t n = 0;
     uck(hipMemcpy(&n, t.d_counter, sizeof(uint32_t), hipMemcpyDeviceToHost), "d2h n");
     std::vector<uint8_t> out(size_t(n) * sizeof(UtxoKeyRec));
     if (n) uck(hipMemcpy(out.data(), d.p, out.size(), hipMemcpyDeviceToHost), "d2h dump");
+    if (payload_out) {
+        payload_out->assign(size_t(n) * sizeof(UtxoPayload), 0);
+        if (n) uck(hipMemcpy(payload_out->data(), dp.p, payload_out->size(), hipMemcpyDeviceToHost), "d2h payload");
+    }
     return out;
 }
 

@@ -1,0 +1,144 @@
+"""Native block codec (csrc/txcodec.cpp) against the Python Transaction model, byte for byte."""
+import hashlib
+import json
+import random
+from decimal import Decimal
+
+import numpy as np
+import pytest
+from hypothesis import HealthCheck, given, settings, strategies as st
+
+from upow_amd.models.block import get_transactions_merkle_tree
+from upow_amd.models.transaction import Transaction, TransactionInput, TransactionOutput
+from upow_amd.utils.codec import OutputType, point_to_string
+from upow_amd.utils.p256 import GX, GY, Point
+
+
+@pytest.fixture(scope='module')
+def L(native):
+    return native
+
+
+def _addr(rng, compressed=True):
+    from upow_amd.ops import p256 as op
+    pt = op.public_key(rng.randrange(1, 1 << 200))
+    return point_to_string(pt) if compressed else (pt.x.to_bytes(32, 'little') + pt.y.to_bytes(32, 'little')).hex()
+
+
+def _tx(rng, version=None, n_in=None, n_out=None, msg=None, one_sig=None):
+    n_in = n_in or rng.randint(1, 4)
+    n_out = n_out or rng.randint(1, 3)
+    v1 = version == 1
+    ins = [TransactionInput(rng.randbytes(32).hex(), rng.randrange(256)) for _ in range(n_in)]
+    outs = [TransactionOutput(_addr(rng, not v1), Decimal(rng.randrange(1, 10 ** 12)) / 10 ** 8) for _ in range(n_out)]
+    tx = Transaction(ins, outs, msg, version)
+    one = one_sig if one_sig is not None else rng.random() < 0.5
+    if one:
+        s = (rng.randrange(1, 1 << 256), rng.randrange(1, 1 << 256))
+        for i in ins:
+            i.signed = s
+    else:
+        for i in ins:
+            i.signed = (rng.randrange(1, 1 << 256), rng.randrange(1, 1 << 256))
+    return tx
+
+
+def _check_fast(d, hexes):
+    assert d['all_fast'], list(d['flags'])
+    i32 = lambda k: np.frombuffer(d[k], dtype=np.int32)
+    in_start, out_start = i32('in_start'), i32('out_start')
+    in_keys = np.frombuffer(d['in_keys'], dtype=np.uint8).reshape(-1, 40)
+    out_amount = np.frombuffer(d['out_amount'], dtype=np.uint64)
+    for k, h in enumerate(hexes):
+        tx, _ = Transaction.parse(h)
+        assert d['hex'][k] == tx.hex()
+        assert d['tx_hash'][k] == tx.hash()
+        assert d['digest'][32 * k:32 * k + 32] == hashlib.sha256(bytes.fromhex(tx.hex(False))).digest()
+        assert i32('signed_len')[k] * 2 == len(tx.hex(False))
+        assert d['out_addr_json'][k] == json.dumps([o.address for o in tx.outputs], separators=(',', ':'))
+        assert d['out_amount_json'][k] == json.dumps([int(o.amount * 10 ** 8) for o in tx.outputs], separators=(',', ':'))
+        assert d['out_addr_str'][out_start[k]:out_start[k + 1]] == [o.address for o in tx.outputs]
+        assert [int(a) for a in out_amount[out_start[k]:out_start[k + 1]]] == [int(o.amount * 10 ** 8) for o in tx.outputs]
+        for j, i in enumerate(tx.inputs):
+            rec = in_keys[in_start[k] + j]
+            assert bytes(rec[:32]).hex() == i.tx_hash and int(rec[32]) == i.index
+            sig = d['sigs'][64 * i32('in_sig')[in_start[k] + j]:][:64]
+            assert (int.from_bytes(sig[:32], 'little'), int.from_bytes(sig[32:], 'little')) == i.signed
+    assert d['merkle'] == get_transactions_merkle_tree([Transaction.parse(h)[0] for h in hexes])
+
+
+def test_decode_matches_python_model(L):
+    rng = random.Random(5)
+    txs = [_tx(rng) for _ in range(60)]
+    txs += [_tx(rng, version=1) for _ in range(5)]
+    txs += [_tx(rng, msg=b'hello world') for _ in range(5)]
+    txs += [_tx(rng, version=2, msg=b'x' * 200) for _ in range(3)]
+    txs += [_tx(rng, msg=b'') for _ in range(2)]
+    hexes = [t.hex() for t in txs]
+    _check_fast(L.decode_block_txs(hexes, 4), hexes)
+
+
+def test_non_canonical_encodings_are_canonicalised(L):
+    rng = random.Random(9)
+    tx = _tx(rng, n_in=2, n_out=1, one_sig=True)
+    h = tx.hex()
+    b = bytearray(bytes.fromhex(h))
+    # widen the amount to 8 bytes (non-minimal) and use prefix 0x07 instead of 42 for the address
+    pos = 2 + 2 * 34 + 1
+    addr, alen = b[pos:pos + 33], b[pos + 33]
+    amount = int.from_bytes(b[pos + 34:pos + 34 + alen], 'little')
+    wide = bytes(addr[:1] if addr[0] == 43 else b'\x07') + bytes(addr[1:]) + bytes([8]) + amount.to_bytes(8, 'little')
+    b2 = b[:pos] + wide + b[pos + 34 + alen:]
+    for variant in (bytes(b2).hex(), bytes(b2).hex().upper()):
+        d = L.decode_block_txs([variant], 1)
+        _check_fast(d, [variant])
+        assert d['hex'][0] == Transaction.parse(variant)[0].hex() != variant
+
+
+def test_general_and_malformed_flags(L):
+    rng = random.Random(2)
+    coinbase_like = _tx(rng, n_in=1).hex()[:-128 - 2] + '24'
+    gov = Transaction([TransactionInput(rng.randbytes(32).hex(), 0)],
+                      [TransactionOutput(_addr(rng), Decimal(1), OutputType.STAKE)])
+    gov.inputs[0].signed = (1, 2)
+    grouped = _tx(rng, n_in=3, one_sig=False)
+    gh = grouped.hex()[:-128]  # 2 signatures for 3 inputs -> assignment by public key
+    cases = {'coinbase': coinbase_like, 'stake output': gov.hex(), 'grouped sigs': gh,
+             'odd hex': 'abc', 'bad char': 'zz' + _tx(rng).hex()[2:], 'version 4': '04' + _tx(rng).hex()[2:],
+             'truncated': _tx(rng).hex()[:100]}
+    d = L.decode_block_txs(list(cases.values()), 2)
+    assert not d['all_fast']
+    assert all(f != 0 for f in d['flags']), dict(zip(cases, d['flags']))
+
+
+@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(st.binary(min_size=1, max_size=400), st.integers(0, 10 ** 6))
+def test_fuzz_fast_implies_python_agrees(native, data, seed):
+    """Random byte strings and mutated valid txs: whenever the native codec claims the fast path,
+    the Python parser must accept the same bytes and serialise/hash them identically."""
+    rng = random.Random(seed)
+    base = bytearray(bytes.fromhex(_tx(rng, n_in=1, n_out=1, one_sig=True).hex()))
+    for _ in range(rng.randint(0, 3)):
+        base[rng.randrange(len(base))] = rng.randrange(256)
+    for cand in (bytes(data).hex(), bytes(base).hex()):
+        d = native.decode_block_txs([cand], 1)
+        if d['all_fast']:
+            _check_fast(d, [cand])
+
+
+def test_input_address_strings(L):
+    from upow_amd.ops import p256 as op
+    rng = random.Random(3)
+    pts = [op.public_key(rng.randrange(1, 1 << 200)) for _ in range(6)]
+    addrs, lens = bytearray(), bytearray()
+    for k, p in enumerate(pts):
+        if k % 2:
+            raw = p.x.to_bytes(32, 'little') + p.y.to_bytes(32, 'little')
+        else:
+            raw = bytes([42 if p.y % 2 == 0 else 43]) + p.x.to_bytes(32, 'little')
+        addrs += raw + bytes(64 - len(raw))
+        lens.append(len(raw))
+    starts = np.array([0, 2, 6], dtype=np.int32).tobytes()
+    strs, js = L.input_address_strings(bytes(addrs), bytes(lens), starts, 2)
+    assert strs == [point_to_string(p) for p in pts]
+    assert js == [json.dumps(strs[:2], separators=(',', ':')), json.dumps(strs[2:], separators=(',', ':'))]

@@ -4,7 +4,7 @@ import random
 import numpy as np
 import pytest
 
-from upow_amd.ledger.utxo import MISSING, UtxoIndex
+from upow_amd.ledger.utxo import MISSING, UtxoIndex, make_payload, pack_records
 
 
 def _keys(n, seed):
@@ -38,12 +38,26 @@ def _exercise(backend):
     # re-insert after tombstones
     idx.insert(keys[:10], 5)
     assert (idx.probe(keys[:10]) == 5).all()
+    # payloads: (amount, address bytes) come back with the tag; absent -> len 0
+    rng = random.Random(4)
+    pk = _keys(300, 3)
+    amounts = [rng.randrange(1 << 63) for _ in pk]
+    addrs = [bytes([42]) + rng.randbytes(32) if k % 3 else rng.randbytes(64) for k in range(300)]
+    idx.insert(pk, 0, make_payload(amounts, addrs))
+    tags, pay = idx.lookup(pk + _keys(5, 77))
+    assert (tags[:300] == 0).all() and (tags[300:] == MISSING).all()
+    assert [int(a) for a in pay['amount'][:300]] == amounts and (pay['len'][300:] == 0).all()
+    assert all(bytes(pay['addr'][k][:pay['len'][k]]) == addrs[k] for k in range(300))
+    t2, p2 = idx.lookup_records(pack_records(pk[:50]))
+    assert (t2 == 0).all() and [int(a) for a in p2['amount']] == amounts[:50]
+    recs, allpay = idx.records_payload()
+    assert len(recs) == len(idx) and len(allpay) == len(idx)
     return idx
 
 
 def test_host_backend():
     idx = _exercise('host')
-    assert len(idx) == 5000 - len([1 for t in range(3000, 3100) if t % 7 == 3])
+    assert len(idx) == 5000 + 300 - len([1 for t in range(3000, 3100) if t % 7 == 3])
 
 
 @pytest.mark.gpu
@@ -52,6 +66,9 @@ def test_gpu_backend_matches_host(gpu):
     # growth past 50% load triggers a rehash on device
     idx = UtxoIndex(backend='gpu')
     keys = _keys(1 << 19 | 12345, 9)
-    idx.insert(keys, 1)
+    amounts = list(range(len(keys)))
+    idx.insert(keys, 1, make_payload(amounts, [bytes([43]) + bytes(32)] * len(keys)))
     assert len(idx) == len(keys)
     assert (idx.probe(keys[::97]) == 1).all()
+    t, p = idx.lookup(keys[::97])  # payloads survive the device rehash
+    assert (t == 1).all() and [int(a) for a in p['amount']] == amounts[::97]

@@ -27,10 +27,10 @@ from ..constants import MAX_BLOCK_SIZE_HEX, SMALLEST
 from ..models.transaction import CoinbaseTransaction, Transaction, TransactionInput
 from ..utils import codec
 from ..utils.codec import (AddressFormat, OutputType, TransactionType, normalize_block, point_to_bytes,
-                           point_to_string, round_up_decimal, sha256, string_to_point)
+                           point_to_string, round_up_decimal, sha256, string_to_bytes, string_to_point)
 from ..utils.jsonstore import JsonStore
 from ..utils.logger import get_logger
-from .utxo import TAG_BY_TABLE, UtxoIndex
+from .utxo import TAG_BY_TABLE, UtxoIndex, make_payload
 
 logger = get_logger(__name__)
 
@@ -138,6 +138,15 @@ async def _input_address(tx_input) -> str:
             _CANON.clear()
         _CANON[addr] = hit
     return hit
+
+
+def _addr_bytes(address: Optional[str]) -> Optional[bytes]:
+    if not address:
+        return None
+    try:
+        return string_to_bytes(address)
+    except ValueError:
+        return None
 
 
 def _at(arr: list, index: int):
@@ -254,13 +263,29 @@ class Database:
             raise RuntimeError(f'injected failure after {stage}')
 
     def _rebuild_utxo_index(self):
-        keys, tags = [], []
+        """Rebuild the HBM/host UTXO set from the output tables; each entry's payload (amount,
+        address bytes) comes from its creating tx's JSON columns, read with SQLite's json_extract."""
+        keys, tags, amounts, addrs = [], [], [], []
         for table in OUTPUT_TABLES:
             tag = TAG_BY_TABLE[table]
-            for r in self._q(f'SELECT tx_hash, "index" FROM {table}'):
+            for r in self._q(f'SELECT u.tx_hash, u."index", '
+                             f'json_extract(t.outputs_amounts, \'$[\' || u."index" || \']\'), '
+                             f'json_extract(t.outputs_addresses, \'$[\' || u."index" || \']\') '
+                             f'FROM {table} u LEFT JOIN transactions t ON t.tx_hash = u.tx_hash'):
                 keys.append((r[0], r[1]))
                 tags.append(tag)
-        self.utxo.reset(keys, tags)
+                amounts.append(r[2])
+                addrs.append(_addr_bytes(r[3]))
+        self.utxo.reset(keys, tags, make_payload(amounts, addrs))
+
+    async def _payload_from_ledger(self, outpoints: List[Tuple[str, int]]):
+        infos = await self.get_transactions_info([h for h, _ in outpoints])
+        amounts, addrs = [], []
+        for h, i in outpoints:
+            info = infos.get(h)
+            amounts.append(_at(info['outputs_amounts'], i) if info else None)
+            addrs.append(_addr_bytes(_at(info['outputs_addresses'], i)) if info else None)
+        return make_payload(amounts, addrs)
 
     def _select_outpoints(self, table: str, outputs: List[Tuple[str, int]]) -> List[Tuple[str, int]]:
         """``SELECT tx_hash, index FROM <table> WHERE (tx_hash, index) = ANY($1)`` (rows in table order)."""
@@ -601,20 +626,29 @@ class Database:
     async def add_unspent_outputs(self, outputs: List[tuple]) -> None:
         if not outputs:
             return
+        payload = None
         if len(outputs[0]) == 2:
             # restored outpoints: address is re-derived from the creating tx (database.py:500-505)
             rows = []
             infos = await self.get_transactions_info([h for h, _ in outputs])
+            amounts, addrs = [], []
             for h, i in outputs:
                 info = infos.get(h)
                 addr = _at(info['outputs_addresses'], i) if info else None
                 rows.append((h, i, addr, None))
+                amounts.append(_at(info['outputs_amounts'], i) if info else None)
+                addrs.append(_addr_bytes(addr))
+            payload = make_payload(amounts, addrs)
         else:
-            rows = [(h, i, a, None if s is None else int(bool(s))) for h, i, a, s in outputs]
+            rows = [(o[0], o[1], o[2], None if o[3] is None else int(bool(o[3]))) for o in outputs]
+            if len(outputs[0]) >= 5:  # (tx_hash, index, address, is_stake, amount in smallest units)
+                payload = make_payload([o[4] for o in outputs], [_addr_bytes(o[2]) for o in outputs])
         with self.lock:
             self.conn.executemany('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) '
                                   'VALUES (?, ?, ?, ?)', rows)
-        self.utxo.insert([(r[0], r[1]) for r in rows], TAG_BY_TABLE['unspent_outputs'])
+        if payload is None:
+            payload = await self._payload_from_ledger([(r[0], r[1]) for r in rows])
+        self.utxo.insert([(r[0], r[1]) for r in rows], TAG_BY_TABLE['unspent_outputs'], payload)
 
     async def _add_gov_outputs(self, table: str, outputs: List[tuple]):
         if not outputs:
@@ -622,7 +656,11 @@ class Database:
         rows = [(o[0], o[1], o[2] if len(o) > 2 else None) for o in outputs]
         with self.lock:
             self.conn.executemany(f'INSERT INTO {table} (tx_hash, "index", address) VALUES (?, ?, ?)', rows)
-        self.utxo.insert([(r[0], r[1]) for r in rows], TAG_BY_TABLE[table])
+        if len(outputs[0]) >= 4:  # (tx_hash, index, address, amount in smallest units)
+            payload = make_payload([o[3] for o in outputs], [_addr_bytes(o[2]) for o in outputs])
+        else:
+            payload = await self._payload_from_ledger([(r[0], r[1]) for r in rows])
+        self.utxo.insert([(r[0], r[1]) for r in rows], TAG_BY_TABLE[table], payload)
 
     async def add_inode_registration_outputs(self, outputs):
         await self._add_gov_outputs('inode_registration_output', outputs)
@@ -658,24 +696,20 @@ class Database:
     def split_outputs(transactions) -> Dict[str, list]:
         """Bucket every output into its table (database.py:524-580)."""
         b = {t: [] for t in OUTPUT_TABLES}
+        gov = {OutputType.INODE_REGISTRATION: 'inode_registration_output',
+               OutputType.VALIDATOR_REGISTRATION: 'validator_registration_output',
+               OutputType.VALIDATOR_VOTING_POWER: 'validators_voting_power',
+               OutputType.DELEGATE_VOTING_POWER: 'delegates_voting_power',
+               OutputType.VOTE_AS_VALIDATOR: 'inodes_ballot', OutputType.VOTE_AS_DELEGATE: 'validators_ballot'}
         for tx in transactions:
             h = tx.hash()
             for index, o in enumerate(tx.outputs):
                 t = o.transaction_type
+                amount = int(o.amount * SMALLEST)
                 if t in (OutputType.REGULAR, OutputType.STAKE, OutputType.UN_STAKE):
-                    b['unspent_outputs'].append((h, index, o.address, o.is_stake))
-                elif t == OutputType.INODE_REGISTRATION:
-                    b['inode_registration_output'].append((h, index, o.address))
-                elif t == OutputType.VALIDATOR_REGISTRATION:
-                    b['validator_registration_output'].append((h, index, o.address))
-                elif t == OutputType.VALIDATOR_VOTING_POWER:
-                    b['validators_voting_power'].append((h, index, o.address))
-                elif t == OutputType.DELEGATE_VOTING_POWER:
-                    b['delegates_voting_power'].append((h, index, o.address))
-                elif t == OutputType.VOTE_AS_VALIDATOR:
-                    b['inodes_ballot'].append((h, index, o.address))
-                elif t == OutputType.VOTE_AS_DELEGATE:
-                    b['validators_ballot'].append((h, index, o.address))
+                    b['unspent_outputs'].append((h, index, o.address, o.is_stake, amount))
+                elif t in gov:
+                    b[gov[t]].append((h, index, o.address, amount))
         return b
 
     async def add_transaction_outputs(self, transactions):

@@ -6,7 +6,8 @@ SQLite ledger stays authoritative and durable; what a restart has to rebuild is 
 (every row of the seven output tables → HBM). A snapshot is the index itself:
 
     line 1   JSON header {magic, version, height, tip_hash, count, utxo_hash, payload_sha256}
-    rest     count × 40-byte records {txid 32 B, u32 index, u32 table tag}, canonical (txid, index) order
+    then     count × 40-byte records {txid 32 B, u32 index, u32 table tag}, canonical (txid, index) order
+    then     count × 80-byte payloads {u64 amount, u32 address length, pad, address[64]} (same order)
 
 written atomically (tmp file + rename) at the tip. On start, :func:`try_restore` loads it only when
 the snapshot's (height, tip hash) equals the ledger's tip, the payload checksum matches and the
@@ -24,10 +25,10 @@ from typing import Optional
 import numpy as np
 
 from ..utils.logger import get_logger
-from .utxo import TAG_BY_TABLE
+from .utxo import PAYLOAD_DTYPE, TAG_BY_TABLE
 
 logger = get_logger(__name__)
-MAGIC, VERSION = 'upow-utxo-snapshot', 1
+MAGIC, VERSION = 'upow-utxo-snapshot', 2
 FILE_NAME = 'utxo_snapshot.bin'
 
 
@@ -49,8 +50,8 @@ def save(db, path: Optional[str] = None) -> dict:
         raise ValueError('in-memory ledger: give an explicit snapshot path')
     with db.lock:
         height, tip = _tip(db)
-        recs = db.utxo.records()
-    payload = recs.tobytes()
+        recs, pay = db.utxo.records_payload()
+    payload = recs.tobytes() + pay.tobytes()
     header = {'magic': MAGIC, 'version': VERSION, 'height': height, 'tip_hash': tip, 'count': int(len(recs)),
               'utxo_hash': db.utxo.set_hash(TAG_BY_TABLE['unspent_outputs']),
               'payload_sha256': hashlib.sha256(payload).hexdigest()}
@@ -65,15 +66,17 @@ def save(db, path: Optional[str] = None) -> dict:
 
 
 def read(path: str):
-    """-> (header, records) after checking the payload checksum; raises ValueError on a bad file."""
+    """-> (header, records, payloads) after checking the checksum; raises ValueError on a bad file."""
     with open(path, 'rb') as f:
         header = json.loads(f.readline().decode())
         payload = f.read()
     if header.get('magic') != MAGIC or header.get('version') != VERSION:
         raise ValueError('not a uPow UTXO snapshot')
-    if len(payload) != 40 * header['count'] or hashlib.sha256(payload).hexdigest() != header['payload_sha256']:
+    n = header['count']
+    if len(payload) != 120 * n or hashlib.sha256(payload).hexdigest() != header['payload_sha256']:
         raise ValueError('snapshot payload truncated or corrupted')
-    return header, np.frombuffer(payload, dtype=np.uint8).reshape(-1, 40)
+    recs = np.frombuffer(payload[:40 * n], dtype=np.uint8).reshape(-1, 40)
+    return header, recs, np.frombuffer(payload[40 * n:], dtype=PAYLOAD_DTYPE)
 
 
 def try_restore(db, path: Optional[str] = None) -> bool:
@@ -82,7 +85,7 @@ def try_restore(db, path: Optional[str] = None) -> bool:
     if not path or not os.path.exists(path):
         return False
     try:
-        header, recs = read(path)
+        header, recs, pay = read(path)
     except (ValueError, OSError, json.JSONDecodeError) as e:
         logger.warning(f'ignoring UTXO snapshot {path}: {e}')
         return False
@@ -94,7 +97,7 @@ def try_restore(db, path: Optional[str] = None) -> bool:
         if int((tags == tag).sum()) != int(db._q1(f'SELECT COUNT(*) FROM {table}')[0]):
             logger.warning(f'UTXO snapshot row count differs from table {table}; rebuilding')
             return False
-    db.utxo.reset_records(recs)
+    db.utxo.reset_records(recs, pay)
     if db.utxo.set_hash(TAG_BY_TABLE['unspent_outputs']) != header['utxo_hash']:
         logger.warning('UTXO snapshot hash mismatch after load; rebuilding')
         return False
@@ -114,8 +117,23 @@ def verify(db) -> dict:
         index_sets.setdefault(int(tags[n]), set()).add((bytes(recs[n, :32]).hex(), int(idx[n])))
     mismatched = [t for t, tag in TAG_BY_TABLE.items()
                   if index_sets.get(tag, set()) != {(r[0], int(r[1])) for r in db._q(f'SELECT tx_hash, "index" FROM {t}')}]
-    return {'ok': want == got and not mismatched, 'sql_hash': want, 'index_hash': got, 'mismatched_tables': mismatched,
-            'entries': int(len(recs))}
+    # payloads: amount + address bytes of every entry against the creating tx's JSON columns
+    from .database import _addr_bytes
+    recs_p, pay = db.utxo.records_payload()
+    idx_p = recs_p[:, 32:36].copy().view(np.uint32).ravel()
+    bad_payload = 0
+    for n in range(len(recs_p)):
+        h, i = bytes(recs_p[n, :32]).hex(), int(idx_p[n])
+        row = db._q1('SELECT json_extract(outputs_amounts, ?), json_extract(outputs_addresses, ?) FROM transactions '
+                     'WHERE tx_hash = ?', (f'$[{i}]', f'$[{i}]', h))
+        want_addr = _addr_bytes(row[1]) if row else None
+        if row is None or row[0] is None or want_addr is None:
+            bad_payload += int(pay['len'][n] != 0)
+            continue
+        ln = int(pay['len'][n])
+        bad_payload += int(int(pay['amount'][n]) != int(row[0]) or bytes(pay['addr'][n][:ln]) != want_addr)
+    return {'ok': want == got and not mismatched and bad_payload == 0, 'sql_hash': want, 'index_hash': got,
+            'mismatched_tables': mismatched, 'payload_mismatches': bad_payload, 'entries': int(len(recs))}
 
 
 __all__ = ['save', 'read', 'try_restore', 'verify', 'default_path']

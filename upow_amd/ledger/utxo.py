@@ -30,6 +30,32 @@ TAG_BY_TABLE = {
 TABLE_BY_TAG = {v: k for k, v in TAG_BY_TABLE.items()}
 MISSING = 0xFF
 
+# per-outpoint payload carried by the index (csrc/utxo_table.hip UtxoPayload): the spent output's
+# amount in smallest units and its raw address bytes (33 compressed / 64 uncompressed)
+PAYLOAD_DTYPE = np.dtype([('amount', '<u8'), ('len', '<u4'), ('pad', '<u4'), ('addr', 'u1', (64,))])
+assert PAYLOAD_DTYPE.itemsize == 80
+
+
+def make_payload(amounts: Sequence[Optional[int]], addrs: Sequence[Optional[bytes]]) -> np.ndarray:
+    """Payload records; an unknown amount/address gives len 0 (consumers then fall back to SQL)."""
+    n = len(amounts)
+    p = np.zeros(n, dtype=PAYLOAD_DTYPE)
+    if n == 0:
+        return p
+    raw = np.zeros((n, 64), dtype=np.uint8)
+    lens = np.zeros(n, dtype=np.uint32)
+    amt = np.zeros(n, dtype=np.uint64)
+    for k, (a, b) in enumerate(zip(amounts, addrs)):
+        if a is None or b is None or len(b) not in (33, 64) or a < 0 or a >= 1 << 64:
+            continue
+        raw[k, :len(b)] = np.frombuffer(bytes(b), dtype=np.uint8)
+        lens[k] = len(b)
+        amt[k] = a
+    p['amount'] = amt
+    p['len'] = lens
+    p['addr'] = raw
+    return p
+
 Outpoint = Tuple[str, int]
 
 
@@ -56,16 +82,27 @@ def pack_records(keys: Sequence[Outpoint], tags=None) -> np.ndarray:
 class _HostBackend:
     def __init__(self):
         self.d: Dict[Outpoint, int] = {}
+        self.p: Dict[Outpoint, bytes] = {}  # raw 80-byte payloads
 
-    def reset(self, keys, tags):
-        self.d = {(h, int(i)): int(t) for (h, i), t in zip(keys, tags)}
+    def reset(self, keys, tags, payload=None):
+        self.d, self.p = {}, {}
+        self.insert(keys, tags, payload)
 
-    def insert(self, keys, tags):
-        for (h, i), t in zip(keys, tags):
-            self.d[(h, int(i))] = int(t)
+    def insert(self, keys, tags, payload=None):
+        raw = payload.tobytes() if payload is not None else None
+        for n, ((h, i), t) in enumerate(zip(keys, tags)):
+            k = (h, int(i))
+            self.d[k] = int(t)
+            self.p[k] = raw[80 * n:80 * n + 80] if raw is not None else bytes(80)
 
     def probe(self, keys) -> np.ndarray:
         return np.array([self.d.get((h, int(i)), MISSING) for h, i in keys], dtype=np.uint8)
+
+    def lookup(self, keys):
+        zero = bytes(80)
+        tags = np.array([self.d.get((h, int(i)), MISSING) for h, i in keys], dtype=np.uint8)
+        pay = np.frombuffer(b''.join(self.p.get((h, int(i)), zero) for h, i in keys), dtype=PAYLOAD_DTYPE)
+        return tags, pay
 
     def erase(self, keys, tag=None) -> np.ndarray:
         out = np.zeros(len(keys), dtype=np.uint8)
@@ -74,11 +111,17 @@ class _HostBackend:
             t = self.d.get(k)
             if t is not None and (tag is None or t == tag):
                 del self.d[k]
+                self.p.pop(k, None)
                 out[n] = 1
         return out
 
     def records(self) -> np.ndarray:
         return pack_records(list(self.d.keys()), list(self.d.values()))
+
+    def records_payload(self):
+        keys = list(self.d.keys())
+        pay = np.frombuffer(b''.join(self.p.get(k, bytes(80)) for k in keys), dtype=PAYLOAD_DTYPE)
+        return pack_records(keys, [self.d[k] for k in keys]), pay
 
     def __len__(self):
         return len(self.d)
@@ -105,36 +148,46 @@ class _GpuBackend:
         need = self.count + self.tombs + extra
         if need * 2 <= (1 << self.log2):
             return
-        recs = np.frombuffer(self.L.utxo_dump(self.h), dtype=np.uint8).reshape(-1, 40)
+        raw, pay = self.L.utxo_dump_payload(self.h)
+        recs = np.frombuffer(raw, dtype=np.uint8).reshape(-1, 40)
         while (len(recs) + extra) * 2 > (1 << self.log2):
             self.log2 += 1
         self.L.utxo_destroy(self.h)
         self.h = self.L.utxo_create(self.log2)
         if len(recs):
-            assert self.L.utxo_insert(self.h, np.ascontiguousarray(recs)) == 0
+            assert self.L.utxo_insert(self.h, np.ascontiguousarray(recs), pay) == 0
         self.count, self.tombs = len(recs), 0
 
-    def reset(self, keys, tags):
+    def reset(self, keys, tags, payload=None):
         self.L.utxo_destroy(self.h)
         self.log2 = int(np.ceil(np.log2(max(2 * len(keys), 1 << 20))))
         self.h = self.L.utxo_create(self.log2)
         self.count = self.tombs = 0
-        self.insert(keys, tags)
+        self.insert(keys, tags, payload)
 
-    def insert(self, keys, tags):
+    def insert(self, keys, tags, payload=None):
         if not len(keys):
             return
-        self._ensure(len(keys))
-        failed = self.L.utxo_insert(self.h, pack_records(keys, list(tags)))
+        self.insert_records(pack_records(keys, list(tags)), payload)
+
+    def insert_records(self, recs: np.ndarray, payload=None):
+        if not len(recs):
+            return
+        self._ensure(len(recs))
+        pay = None if payload is None else np.ascontiguousarray(payload).view(np.uint8)
+        failed = self.L.utxo_insert(self.h, np.ascontiguousarray(recs), pay)
         if failed:
             raise RuntimeError(f'UTXO table insert failed for {failed} entries')
-        self.count += len(keys)
-
-    def insert_records(self, recs: np.ndarray):
-        self._ensure(len(recs))
-        if self.L.utxo_insert(self.h, recs):
-            raise RuntimeError('UTXO table insert failed')
         self.count += len(recs)
+
+    def lookup_records(self, recs: np.ndarray):
+        tags, pay = self.L.utxo_lookup(self.h, np.ascontiguousarray(recs))
+        return np.frombuffer(tags, dtype=np.uint8), np.frombuffer(pay, dtype=PAYLOAD_DTYPE)
+
+    def lookup(self, keys):
+        if not len(keys):
+            return np.zeros(0, dtype=np.uint8), np.zeros(0, dtype=PAYLOAD_DTYPE)
+        return self.lookup_records(pack_records(keys))
 
     def probe(self, keys) -> np.ndarray:
         if not len(keys):
@@ -157,6 +210,10 @@ class _GpuBackend:
     def records(self) -> np.ndarray:
         return np.frombuffer(self.L.utxo_dump(self.h), dtype=np.uint8).reshape(-1, 40)
 
+    def records_payload(self):
+        raw, pay = self.L.utxo_dump_payload(self.h)
+        return np.frombuffer(raw, dtype=np.uint8).reshape(-1, 40), np.frombuffer(pay, dtype=PAYLOAD_DTYPE)
+
     def __len__(self):
         return self.count
 
@@ -177,13 +234,49 @@ class UtxoIndex:
         self.backend_name = backend or default_backend()
         self.be = _GpuBackend() if self.backend_name == 'gpu' else _HostBackend()
 
-    def reset(self, keys: Sequence[Outpoint], tags: Sequence[int]):
-        self.be.reset(list(keys), list(tags))
+    def reset(self, keys: Sequence[Outpoint], tags: Sequence[int], payload: Optional[np.ndarray] = None):
+        self.be.reset(list(keys), list(tags), payload)
 
-    def insert(self, keys: Sequence[Outpoint], tag):
+    def insert(self, keys: Sequence[Outpoint], tag, payload: Optional[np.ndarray] = None):
         keys = list(keys)
         tags = [tag] * len(keys) if isinstance(tag, int) else list(tag)
-        self.be.insert(keys, tags)
+        self.be.insert(keys, tags, payload)
+
+    def insert_records(self, recs: np.ndarray, payload: Optional[np.ndarray] = None):
+        """Insert packed 40-byte key records (tags inside) — the block fast path's form."""
+        if isinstance(self.be, _GpuBackend):
+            self.be.insert_records(recs, payload)
+            return
+        idx = recs[:, 32:36].copy().view(np.uint32).ravel()
+        tags = recs[:, 36:40].copy().view(np.uint32).ravel()
+        keys = [(bytes(recs[n, :32]).hex(), int(idx[n])) for n in range(len(recs))]
+        self.be.insert(keys, [int(t) for t in tags], payload)
+
+    def lookup(self, keys: Sequence[Outpoint]):
+        """(tags uint8[n], payload PAYLOAD_DTYPE[n]) for each outpoint (tag 0xff / len 0 when absent)."""
+        return self.be.lookup(list(keys))
+
+    def lookup_records(self, recs: np.ndarray):
+        if isinstance(self.be, _GpuBackend):
+            return self.be.lookup_records(recs)
+        idx = recs[:, 32:36].copy().view(np.uint32).ravel()
+        return self.be.lookup([(bytes(recs[n, :32]).hex(), int(idx[n])) for n in range(len(recs))])
+
+    def erase_records(self, recs: np.ndarray) -> np.ndarray:
+        if isinstance(self.be, _GpuBackend):
+            if not len(recs):
+                return np.zeros(0, dtype=np.uint8)
+            out = np.frombuffer(self.be.L.utxo_erase(self.be.h, np.ascontiguousarray(recs)), dtype=np.uint8)
+            k = int(out.sum())
+            self.be.count -= k
+            self.be.tombs += k
+            return out
+        if not len(recs):
+            return np.zeros(0, dtype=np.uint8)
+        idx = recs[:, 32:36].copy().view(np.uint32).ravel()
+        tag = int(recs[0, 36:40].copy().view(np.uint32)[0])  # one tag filter per batch
+        return self.be.erase([(bytes(recs[n, :32]).hex(), int(idx[n])) for n in range(len(recs))],
+                             None if tag == MISSING else tag)
 
     def probe(self, keys: Sequence[Outpoint]) -> np.ndarray:
         return self.be.probe(list(keys))
@@ -203,17 +296,24 @@ class UtxoIndex:
         """All live entries as 40-byte records, in canonical (txid, index) order."""
         return sort_records(np.ascontiguousarray(self.be.records()))
 
-    def reset_records(self, recs: np.ndarray):
+    def records_payload(self):
+        """(records, payloads) of every live entry, in canonical (txid, index) order."""
+        recs, pay = self.be.records_payload()
+        order = sort_order(np.ascontiguousarray(recs))
+        return np.ascontiguousarray(recs[order]), np.ascontiguousarray(pay[order])
+
+    def reset_records(self, recs: np.ndarray, payload: Optional[np.ndarray] = None):
         """Replace the whole index with packed records (snapshot restore: one H2D copy + insert launch)."""
         recs = np.ascontiguousarray(recs, dtype=np.uint8).reshape(-1, 40)
         if isinstance(self.be, _GpuBackend):
             self.be.reset([], [])
             if len(recs):
-                self.be.insert_records(recs)
+                self.be.insert_records(recs, payload)
         else:
             idx = recs[:, 32:36].copy().view(np.uint32).ravel()
             tags = recs[:, 36:40].copy().view(np.uint32).ravel()
-            self.be.d = {(bytes(recs[n, :32]).hex(), int(idx[n])): int(tags[n]) for n in range(len(recs))}
+            keys = [(bytes(recs[n, :32]).hex(), int(idx[n])) for n in range(len(recs))]
+            self.be.reset(keys, [int(t) for t in tags], payload)
 
     def set_hash(self, tag: int = 0) -> str:
         """K12 from the index: SHA-256 over (txid || index byte) of table ``tag`` sorted by (txid, index)
@@ -228,11 +328,14 @@ class UtxoIndex:
         return len(self.be)
 
 
-def sort_records(recs: np.ndarray) -> np.ndarray:
-    """Sort packed records by (txid bytes, index): the SQL ``ORDER BY tx_hash, index`` order."""
+def sort_order(recs: np.ndarray) -> np.ndarray:
+    """Permutation sorting packed records by (txid bytes, index): SQL ``ORDER BY tx_hash, index``."""
     if len(recs) < 2:
-        return recs
+        return np.arange(len(recs))
     be = recs[:, :32].copy().view('>u8')  # 4 big-endian words compare like the hex strings
     idx = recs[:, 32:36].copy().view(np.uint32).ravel()
-    order = np.lexsort((idx, be[:, 3], be[:, 2], be[:, 1], be[:, 0]))
-    return recs[order]
+    return np.lexsort((idx, be[:, 3], be[:, 2], be[:, 1], be[:, 0]))
+
+
+def sort_records(recs: np.ndarray) -> np.ndarray:
+    return recs[sort_order(recs)] if len(recs) >= 2 else recs
