@@ -1,0 +1,170 @@
+"""Native block path (ledger/fastpath.py) vs the object path: same verdicts, same errors, same ledger.
+
+Two ledgers receive the same blocks — one through ``manager.create_block`` with Transaction objects,
+one through ``fastpath.create_block_from_hex`` — and every table, the UTXO index (with payloads)
+and the UTXO-set hash must end up identical."""
+import asyncio
+import random
+from decimal import Decimal
+
+import numpy as np
+import pytest
+
+from upow_amd import devnet
+from upow_amd.ledger import fastpath, manager
+from upow_amd.ledger.database import OUTPUT_TABLES, Database
+from upow_amd.models.transaction import Transaction, TransactionInput, TransactionOutput
+from upow_amd.wallet.builders import address_of, create_stake_transaction, create_transaction
+
+GENESIS = 0xA11CE
+KEYS = [0xB0B + k for k in range(6)]
+TABLES = ['blocks', 'transactions', 'pending_transactions', 'pending_spent_outputs', 'address_transactions',
+          *OUTPUT_TABLES]
+
+
+@pytest.fixture(autouse=True)
+def _low_difficulty(monkeypatch):
+    monkeypatch.setattr(manager, 'START_DIFFICULTY', Decimal('1.0'))
+
+
+def _dump(db):
+    out = {}
+    for t in TABLES:
+        rows = db._q(f'SELECT * FROM {t}')
+        out[t] = sorted(tuple(r) for r in rows)
+    recs, pay = db.utxo.records_payload()
+    out['index'] = (recs.tobytes(), pay.tobytes())
+    return out
+
+
+class Pair:
+    def __init__(self, a, b):
+        self.a, self.b = a, b
+
+    def use(self, db):
+        Database.instance = db
+        manager.Manager.difficulty = None
+
+    async def push(self, content, txs, expect=None):
+        hexes = [t.hex() if not isinstance(t, str) else t for t in txs]
+        self.use(self.a)
+        ea = []
+        ra = await manager.create_block(content, [await Transaction.from_hex(h) for h in hexes], error_list=ea)
+        self.use(self.b)
+        eb = []
+        rb = await fastpath.create_block_from_hex(content, hexes, error_list=eb)
+        assert ra == rb, (ra, rb, ea, eb)
+        assert ea == eb
+        if expect is not None:
+            assert ra == expect, ea
+        da, dbb = _dump(self.a), _dump(self.b)
+        for k in da:
+            assert da[k] == dbb[k], k
+        self.use(self.a)
+        assert await self.a.get_unspent_outputs_hash() == await self.b.get_unspent_outputs_hash()
+        return ra, ea
+
+    async def mine(self, txs=(), ts=None):
+        self.use(self.a)
+        return await devnet.mine_header(address_of(GENESIS), list(txs), ts=ts, device='cpu')
+
+
+async def _setup():
+    a = await Database.create(utxo_backend='host')
+    b = await Database.create(utxo_backend='host')
+    p = Pair(a, b)
+    base = 1_700_000_000
+    for k in range(8):
+        c = await p.mine(ts=base + 60 * k)
+        await p.push(c, [], expect=True)
+    return p, base
+
+
+def _signed(inputs, outputs, keys, message=None):
+    tx = Transaction(inputs, outputs, message)
+    return tx.sign(keys)
+
+
+def test_fast_path_matches_object_path():
+    async def go():
+        p, base = await _setup()
+        ts = base + 60 * 10
+        p.use(p.a)
+        txs = []
+        for k in KEYS:  # fan out from the genesis coinbases: 1-in txs, change back to genesis
+            tx = await create_transaction(GENESIS, address_of(k), '2.5')
+            await p.a.add_pending_transaction(tx)
+            txs.append(tx)
+        txs.append(await create_transaction(GENESIS, address_of(KEYS[0]), '0.125', message=b'hello, block'))
+        await p.a.add_pending_transaction(txs[-1])
+        p.use(p.b)
+        for t in txs:  # mirror the mempool so the pending-table cleanup is exercised on both sides
+            await p.b.add_pending_transaction(t)
+        c = await p.mine(txs, ts=ts)
+        assert fastpath.decode([t.hex() for t in txs]) is not None
+        await p.push(c, txs, expect=True)
+        assert fastpath.last_path == 'native'
+        # second block: multi-input spends with per-input signatures, one shared-signature tx
+        p.use(p.a)
+        txs2 = []
+        for k in KEYS[:3]:
+            tx = await create_transaction(k, address_of(KEYS[-1]), '1')
+            txs2.append(tx)
+        key = KEYS[4]
+        outs = await p.a.get_spendable_outputs(address_of(key))
+        tx = Transaction(outs, [TransactionOutput(address_of(GENESIS), Decimal('2.4'))])
+        tx.sign([key])
+        txs2.append(tx)
+        c2 = await p.mine(txs2, ts=ts + 60)
+        await p.push(c2, txs2, expect=True)
+        assert fastpath.last_path == 'native'
+    asyncio.run(go())
+
+
+def test_rejections_match():
+    async def go():
+        p, base = await _setup()
+        ts = base + 60 * 10
+        p.use(p.a)
+        good = await create_transaction(GENESIS, address_of(KEYS[0]), '3')
+        # double spend across two txs of the block
+        dup = Transaction([TransactionInput(good.inputs[0].tx_hash, good.inputs[0].index)],
+                          [TransactionOutput(address_of(KEYS[1]), Decimal('1'))])
+        dup.inputs[0].public_key = good.inputs[0].public_key
+        dup.sign([GENESIS])
+        # forged signature
+        forged, _ = Transaction.parse(good.hex())
+        r, s = forged.inputs[0].signed
+        forged.inputs[0].signed = (r, s ^ 0x10)
+        # negative fee
+        greedy = Transaction([TransactionInput(good.inputs[0].tx_hash, good.inputs[0].index)],
+                             [TransactionOutput(address_of(KEYS[1]), Decimal('100'))])
+        greedy.inputs[0].public_key = good.inputs[0].public_key
+        greedy.sign([GENESIS])
+        # unknown input
+        ghost = Transaction([TransactionInput('ab' * 32, 0)], [TransactionOutput(address_of(KEYS[1]), Decimal('1'))])
+        ghost.inputs[0].signed = good.inputs[0].signed
+        for bad in ([good, dup], [forged], [greedy], [ghost]):
+            c = await p.mine(bad, ts=ts)
+            res, err = await p.push(c, bad, expect=False)
+            assert fastpath.last_path == 'object' and err
+        # merkle mismatch: header committed to other txs
+        c = await p.mine([good], ts=ts)
+        other = await create_transaction(GENESIS, address_of(KEYS[2]), '1')
+        await p.push(c, [other], expect=False)
+        # and the honest block still goes through on both
+        c = await p.mine([good], ts=ts)
+        await p.push(c, [good], expect=True)
+        assert fastpath.last_path == 'native'
+    asyncio.run(go())
+
+
+def test_governance_block_takes_object_path():
+    async def go():
+        p, base = await _setup()
+        p.use(p.a)
+        st = await create_stake_transaction(GENESIS, '1')
+        assert fastpath.decode([st.hex()]) is None
+        c = await p.mine([st], ts=base + 600)
+        await p.push(c, [st], expect=True)
+    asyncio.run(go())

@@ -93,7 +93,8 @@ def test_mining_flow_and_queries(node):
     assert m.status_code == 200 and m.headers['content-type'].startswith('text/plain')
     series = {ln.split(' ')[0]: float(ln.split(' ')[1]) for ln in m.text.splitlines() if ln and not ln.startswith('#')}
     assert series['upow_chain_height'] == 4 and series['upow_mempool_size'] == 0
-    assert series['upow_blocks_applied_total{path="push"}'] >= 4
+    assert sum(v for k, v in series.items() if k.startswith('upow_blocks_applied_total')) >= 4
+    assert series['upow_blocks_applied_total{path="native"}'] >= 1  # the transfer block took the native path
     assert series['upow_signatures_verified_total'] >= 1
     assert series['upow_blocks_rejected_total{path="push"}'] >= 1
 

@@ -85,7 +85,7 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
 
 async def _run(args, ctx, device, utxo_backend):
     from . import devnet
-    from .ledger import manager, validate
+    from .ledger import fastpath, manager, validate
     from .models.transaction import Transaction
     n_blocks = args.steps + args.warmup
     db, addr, blocks, base_ts = await _setup(n_blocks, args.txs, 1234 + ctx.rank, utxo_backend, device)
@@ -102,6 +102,7 @@ async def _run(args, ctx, device, utxo_backend):
         headers.append(content)
         prev = hashlib.sha256(bytes.fromhex(content)).hexdigest()
     stages = []
+    paths = set()
     total_txs = 0
     for b, txs_hex in enumerate(blocks):
         if b == args.warmup:
@@ -109,29 +110,35 @@ async def _run(args, ctx, device, utxo_backend):
             ctx.synchronize()
             t_start = time.perf_counter()
         t0 = time.perf_counter()
-        txs = [await Transaction.from_hex(h) for h in txs_hex]
-        t1 = time.perf_counter()
         errors = []
-        ok = await manager.create_block(headers[b], txs, error_list=errors)
+        if args.object_path:
+            txs = [await Transaction.from_hex(h) for h in txs_hex]
+            ok = await manager.create_block(headers[b], txs, error_list=errors)
+        else:
+            ok = await fastpath.create_block_from_hex(headers[b], txs_hex, error_list=errors)
         if not ok:
             raise RuntimeError(f'synthetic block rejected: {errors}')
         t2 = time.perf_counter()
         if b >= args.warmup:
-            total_txs += len(txs)
-            stages.append({'parse_s': t1 - t0, 'create_block_s': t2 - t1, **manager.last_block_timings,
-                           **{k: v for k, v in validate.timings.items() if k.endswith('_s')}})
+            total_txs += len(txs_hex)
+            stages.append({'block_s': t2 - t0, **manager.last_block_timings,
+                           **{k: v for k, v in validate.timings.items() if k.endswith('_s')},
+                           **({} if args.object_path else fastpath.timings)})
+            paths.add('object' if args.object_path else fastpath.last_path)
     ctx.synchronize()
     ctx.barrier()
     wall = time.perf_counter() - t_start
     wall = ctx.allreduce_max_f(wall)
-    return total_txs, wall, stages, len(blocks[0])
+    return total_txs, wall, stages, len(blocks[0]), sorted(paths)
 
 
 def run_verify_bench(args, ctx):
     from .ops.native import gpu_available
     device = 'gpu' if gpu_available() else 'cpu'
     utxo_backend = 'gpu' if device == 'gpu' else 'host'
-    total_txs, wall, stages, txs_per_block = asyncio.run(_run(args, ctx, device, utxo_backend))
+    if not hasattr(args, 'object_path'):
+        args.object_path = False
+    total_txs, wall, stages, txs_per_block, paths = asyncio.run(_run(args, ctx, device, utxo_backend))
     total = ctx.allreduce_sum(total_txs)
     tps = total / wall
     avg = {k: round(sum(s[k] for s in stages) / len(stages) * 1000, 2) for k in stages[0]
@@ -151,6 +158,6 @@ def run_verify_bench(args, ctx):
         'data': 'synthetic 2 MB blocks: random P-256 keys, 2-in/2-out signed txs, funding UTXOs',
         'config': {'model': 'upow block validation + apply (push_block path)', 'global_batch': total // max(1, args.steps),
                    'seq_len': txs_per_block, 'parallelism': f'dp{ctx.world}', 'device': device,
-                   'utxo_backend': utxo_backend},
+                   'utxo_backend': utxo_backend, 'block_path': '+'.join(paths)},
         'stage_ms_avg': avg,
     }

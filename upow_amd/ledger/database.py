@@ -23,6 +23,8 @@ from statistics import mean
 from time import perf_counter
 from typing import Any, Dict, Iterable, List, Optional, Set, Tuple, Union
 
+import numpy as np
+
 from ..constants import MAX_BLOCK_SIZE_HEX, SMALLEST
 from ..models.transaction import CoinbaseTransaction, Transaction, TransactionInput
 from ..utils import codec
@@ -30,7 +32,7 @@ from ..utils.codec import (AddressFormat, OutputType, TransactionType, normalize
                            point_to_string, round_up_decimal, sha256, string_to_bytes, string_to_point)
 from ..utils.jsonstore import JsonStore
 from ..utils.logger import get_logger
-from .utxo import TAG_BY_TABLE, UtxoIndex, make_payload
+from .utxo import PAYLOAD_DTYPE, TAG_BY_TABLE, UtxoIndex, make_payload
 
 logger = get_logger(__name__)
 
@@ -87,9 +89,8 @@ CREATE TABLE IF NOT EXISTS {_t} (
     address TEXT NULL
 );"""
 SCHEMA += """
-CREATE INDEX IF NOT EXISTS tx_hash_idx ON unspent_outputs (tx_hash);
+CREATE INDEX IF NOT EXISTS tx_hash_idx ON unspent_outputs (tx_hash, "index");
 CREATE INDEX IF NOT EXISTS block_hash_idx ON transactions (block_hash);
-CREATE INDEX IF NOT EXISTS unspent_outpoint_idx ON unspent_outputs (tx_hash, "index");
 CREATE INDEX IF NOT EXISTS unspent_address_idx ON unspent_outputs (address);
 CREATE INDEX IF NOT EXISTS pending_spent_idx ON pending_spent_outputs (tx_hash, "index");
 CREATE INDEX IF NOT EXISTS address_transactions_idx ON address_transactions (address);
@@ -228,13 +229,17 @@ class Database:
         """Re-entrant SQL transaction: only the outermost level issues BEGIN/COMMIT/ROLLBACK, so a
         whole block application (many helper calls) commits or rolls back as one unit."""
 
-        def __init__(self, db):
+        def __init__(self, db, foreign_keys: bool = True):
             self.db = db
+            self.fk = foreign_keys
 
         def __enter__(self):
             self.db.lock.acquire()
             if self.db._tx_depth == 0:
+                if not self.fk:  # only settable outside a transaction
+                    self.db.conn.execute('PRAGMA foreign_keys = OFF')
                 self.db.conn.execute('BEGIN')
+                self.db._fk_off = not self.fk
             self.db._tx_depth += 1
             return self.db
 
@@ -243,6 +248,9 @@ class Database:
                 self.db._tx_depth -= 1
                 if self.db._tx_depth == 0:
                     self.db.conn.execute('COMMIT' if et is None else 'ROLLBACK')
+                    if self.db._fk_off:
+                        self.db.conn.execute('PRAGMA foreign_keys = ON')
+                        self.db._fk_off = False
                 elif et is not None:
                     self.db._tx_failed = True
             finally:
@@ -251,9 +259,13 @@ class Database:
 
     _tx_depth = 0
     _tx_failed = False
+    _fk_off = False
 
-    def transaction(self):
-        return Database._Tx(self)
+    def transaction(self, foreign_keys: bool = True):
+        """``foreign_keys=False``: skip FK enforcement for this (outermost) transaction — the native
+        block path, which only inserts rows whose parents it inserted in the same transaction and
+        deletes nothing that cascades."""
+        return Database._Tx(self, foreign_keys)
 
     # fault injection (tests): raise inside block application after the named stage
     fail_after_stage: Optional[str] = None
@@ -452,12 +464,13 @@ class Database:
         rows = [await self._tx_row(t, block_hash) for t in transactions]
         self.insert_transaction_rows(rows)
 
-    def insert_transaction_rows(self, rows: List[tuple]):
-        addr_rows = []
-        for r in rows:
-            tx_hash = r[1]
-            addrs = set(_arr(r[3])) | set(_arr(r[4]))
-            addr_rows.extend((a, tx_hash) for a in addrs)
+    def insert_transaction_rows(self, rows: List[tuple], addr_rows: Optional[List[tuple]] = None):
+        if addr_rows is None:
+            addr_rows = []
+            for r in rows:
+                tx_hash = r[1]
+                addrs = set(_arr(r[3])) | set(_arr(r[4]))
+                addr_rows.extend((a, tx_hash) for a in addrs)
         try:
             with self.transaction():
                 self.conn.executemany('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, '
@@ -524,11 +537,14 @@ class Database:
         return await Transaction.from_hex(res['tx_hex'], check_signatures) if res is not None else None
 
     async def get_pending_transactions_by_hash(self, hashes: List[str], check_signatures: bool = True):
+        return [await Transaction.from_hex(h, check_signatures) for h in await self.get_pending_transactions_hex_by_hash(hashes)]
+
+    async def get_pending_transactions_hex_by_hash(self, hashes: List[str]) -> List[str]:
+        """tx hex of the pending txs among ``hashes``, in mempool (table) order like database.py:297-301."""
         if not hashes:
             return []
         want = set(hashes)
-        rows = [r for r in self._q('SELECT tx_hash, tx_hex FROM pending_transactions') if r['tx_hash'] in want]
-        return [await Transaction.from_hex(r['tx_hex'], check_signatures) for r in rows]
+        return [r['tx_hex'] for r in self._q('SELECT tx_hash, tx_hex FROM pending_transactions') if r['tx_hash'] in want]
 
     async def get_transactions(self, tx_hashes: List[str]):
         infos = await self.get_transactions_info(tx_hashes)
@@ -649,6 +665,43 @@ class Database:
         if payload is None:
             payload = await self._payload_from_ledger([(r[0], r[1]) for r in rows])
         self.utxo.insert([(r[0], r[1]) for r in rows], TAG_BY_TABLE['unspent_outputs'], payload)
+
+    def insert_regular_outputs(self, rows: List[tuple], txids: np.ndarray, indexes: np.ndarray, amounts: np.ndarray,
+                               addrs: np.ndarray, lens: np.ndarray) -> None:
+        """Native block path: REGULAR outputs as (tx_hash, index, address, is_stake) rows + one index
+        insert with their payloads (amount, normalised address bytes) — ``add_unspent_outputs`` in bulk."""
+        if not rows:
+            return
+        with self.lock:
+            self.conn.executemany('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) '
+                                  'VALUES (?, ?, ?, ?)', rows)
+        n = len(rows)
+        recs = np.zeros((n, 40), dtype=np.uint8)
+        recs[:, :32] = txids
+        recs[:, 32:36] = np.asarray(indexes, dtype=np.uint32).reshape(n, 1).view(np.uint8)
+        recs[:, 36:40] = np.full((n, 1), TAG_BY_TABLE['unspent_outputs'], dtype=np.uint32).view(np.uint8)
+        pay = np.zeros(n, dtype=PAYLOAD_DTYPE)
+        pay['amount'] = amounts
+        pay['len'] = lens
+        a = np.array(addrs, dtype=np.uint8, copy=True)
+        c33 = lens == 33
+        a[c33, 0] = np.where(a[c33, 0] == 43, 43, 42)  # bytes_to_string normalises the prefix
+        pay['addr'] = a
+        self.utxo.insert_records(recs, pay)
+
+    def remove_spent_regular(self, inputs: List[Tuple[str, int]], in_keys: np.ndarray) -> bool:
+        """Native block path: ``remove_unspent_outputs`` for REGULAR spends (same partial-delete semantics)."""
+        if not inputs:
+            return True
+        with self.transaction():
+            n = self.conn.executemany('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?', inputs).rowcount
+        recs = np.array(in_keys, dtype=np.uint8, copy=True)
+        recs[:, 36:40] = np.full((len(recs), 1), TAG_BY_TABLE['unspent_outputs'], dtype=np.uint32).view(np.uint8)
+        self.utxo.erase_records(recs)
+        if n != len(inputs):
+            logger.error(f'Failed to delete all UTXOs: {n} of {len(inputs)} deleted')
+            return False
+        return True
 
     async def _add_gov_outputs(self, table: str, outputs: List[tuple]):
         if not outputs:

@@ -1,0 +1,257 @@
+"""Native block path: validate and apply a block given as tx hex strings, without Transaction objects.
+
+reference: ``POST /push_block`` → ``manager.create_block`` (upow/manager.py:422-757), which builds one
+Python object graph per tx, checks it input by input and writes it row by row. This module runs the
+same checks over whole-block arrays:
+
+  1. ``_native.decode_block_txs`` (csrc/txcodec.cpp): decode + canonical re-serialisation + txids +
+     signed-message digests + address strings + JSON columns + merkle root, threaded in C++;
+  2. one HBM UTXO ``lookup`` launch for every input: existence in ``unspent_outputs`` AND the spent
+     output's amount and address (the payload the table carries), so no SQL read is needed;
+  3. one batched point decompression for every key involved (signers and outputs), one batched
+     P-256 verify (sharded over ranks on a multi-GPU node) + the ASCII-hex retry pass;
+  4. fees, output validity and the merkle root as array arithmetic;
+  5. the ledger writes of ``_apply_block`` as a handful of ``executemany`` calls + one index
+     insert launch + one erase launch, inside the same single SQLite transaction.
+
+Scope: blocks whose txs are all REGULAR (no governance message type, only REGULAR outputs, 1-or-n
+signatures). Anything else, and ANY failed check, hands the block to the object path
+(``manager._create_block``), which then reproduces the reference's exact verdict, error message or
+exception. The fast path only ever answers "valid" itself, so it can cost time but not semantics;
+``tests/test_fastpath.py`` runs both paths over the same blocks and compares the whole ledger.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+from decimal import Decimal
+from time import perf_counter
+from typing import List, Optional
+
+import numpy as np
+
+from ..constants import MAX_BLOCK_SIZE_HEX, SMALLEST
+from ..models.transaction import Transaction
+from ..ops import p256 as op
+from ..ops.native import gpu_available, lib
+from ..utils import metrics
+from ..utils.codec import TransactionType, get_transaction_type_from_message
+from ..utils.logger import get_logger
+from .utxo import TAG_BY_TABLE
+
+logger = get_logger(__name__)
+THREADS = int(os.environ.get('UPOW_CODEC_THREADS', '0')) or max(1, min(16, os.cpu_count() or 1))
+ENABLED = os.environ.get('UPOW_FASTPATH', '1') != '0'
+timings: dict = {}
+last_path = None  # 'native' | 'object' for the last block (tests, metrics)
+AMOUNT_LIMIT = 1 << 52  # > max supply in smallest units; keeps per-tx int64 sums exact
+
+
+def _i32(d, k):
+    return np.frombuffer(d[k], dtype=np.int32)
+
+
+def decode(tx_hexes: List[str]) -> Optional[dict]:
+    """Native decode; None when the block needs the object path."""
+    if not ENABLED:
+        return None
+    d = lib().decode_block_txs(list(tx_hexes), THREADS)
+    if not d['all_fast']:
+        return None
+    msg_off, msg_len = _i32(d, 'msg_off'), _i32(d, 'msg_len')
+    for k in np.nonzero(msg_off >= 0)[0]:
+        h = d['hex'][k]
+        msg = bytes.fromhex(h[2 * msg_off[k]:2 * (msg_off[k] + msg_len[k])])
+        if get_transaction_type_from_message(msg) != TransactionType.REGULAR:
+            return None
+    return d
+
+
+async def create_block_from_hex(block_content: str, tx_hexes: List[str], error_list: list = None,
+                                last_block: dict = None) -> bool:
+    """``create_block(block_content, [Transaction.from_hex(h) for h in tx_hexes])``, natively when possible."""
+    global last_path
+    from . import manager
+    if error_list is None:
+        error_list = []
+    t0 = perf_counter()
+    dec = decode(tx_hexes) if tx_hexes else None
+    if dec is None:
+        last_path = 'object'
+        txs = [await Transaction.from_hex(h) for h in tx_hexes]
+        return await manager.create_block(block_content, txs, last_block, error_list)
+    async with manager.ledger_lock():
+        ok = await _create_block_fast(block_content, dec, error_list, last_block, t0)
+        last_path = 'native'
+        if ok is None:
+            last_path = 'object'
+            txs = [await Transaction.from_hex(h) for h in tx_hexes]
+            ok = await manager._create_block(block_content, txs, last_block, error_list)
+        manager._record_block_metrics(ok, perf_counter() - t0, len(tx_hexes), 'native' if last_path == 'native' else 'push')
+        return ok
+
+
+async def _create_block_fast(block_content: str, d: dict, error_list: list, last_block: Optional[dict],
+                             t0: float) -> Optional[bool]:
+    """True/False for a decided block; None = hand over to the object path."""
+    from . import manager, validate
+    from .database import Database
+    database: Database = Database.instance
+    manager.Manager.difficulty = None
+    if last_block is None or last_block['id'] % manager.BLOCKS_COUNT == 0:
+        difficulty, last_block = await manager.calculate_difficulty()
+    else:
+        difficulty, last_block = await manager.get_difficulty()
+    hdr = await manager.check_block_header(block_content, (difficulty, last_block), error_list)
+    if hdr is None:
+        return False
+    block_no, merkle_tree = hdr
+    logger.info(f'Creating block no. {block_no} (native path, {d["n"]} txs)')
+    if block_no in manager.double_spend_dict:
+        return None
+    n = int(d['n'])
+    if int(_i32(d, 'hex_len').sum()) > MAX_BLOCK_SIZE_HEX:
+        return None
+    if d['merkle'] != merkle_tree:
+        return None
+    t1 = perf_counter()
+
+    # ---- inputs: one lookup launch (existence in unspent_outputs + amount + address)
+    in_keys = np.frombuffer(d['in_keys'], dtype=np.uint8).reshape(-1, 40)
+    n_in = len(in_keys)
+    keyview = np.ascontiguousarray(in_keys[:, :36]).view(np.dtype((np.void, 36))).ravel()
+    if len(np.unique(keyview)) != n_in:
+        return None
+    tags, pay = database.utxo.lookup_records(in_keys)
+    if n_in and (np.any(tags != TAG_BY_TABLE['unspent_outputs']) or np.any(pay['len'] == 0)):
+        return None
+    in_amount = pay['amount'].astype(np.uint64)
+    out_amount = np.frombuffer(d['out_amount'], dtype=np.uint64)
+    if (n_in and in_amount.max() >= AMOUNT_LIMIT) or (len(out_amount) and out_amount.max() >= AMOUNT_LIMIT):
+        return None
+    t2 = perf_counter()
+
+    # ---- keys: decompress every distinct 33-byte key (signers + outputs) in one batch
+    in_sig = _i32(d, 'in_sig')
+    sig_ids, job_input = np.unique(in_sig, return_index=True)  # first input per distinct signature
+    out_len = np.frombuffer(d['out_len'], dtype=np.uint8)
+    out_addr = np.frombuffer(d['out_addr'], dtype=np.uint8).reshape(-1, 64)
+    # every spent output's key (the object path resolves each input's point, not only the signers)
+    all_addr = np.concatenate([pay['addr'], out_addr]) if len(out_addr) else np.ascontiguousarray(pay['addr'])
+    all_len = np.concatenate([pay['len'].astype(np.uint8), out_len])
+    xy = np.zeros((len(all_addr), 64), dtype=np.uint8)
+    ok = np.ones(len(all_addr), dtype=bool)
+    c33 = np.nonzero(all_len == 33)[0]
+    if len(c33):
+        comp = np.ascontiguousarray(all_addr[c33, :33])
+        uniq, inv = np.unique(comp.view(np.dtype((np.void, 33))).ravel(), return_inverse=True)
+        ubuf = np.ascontiguousarray(uniq).view(np.uint8)
+        dev = 'gpu' if (gpu_available() and len(uniq) >= op.GPU_MIN_BATCH) else 'cpu'
+        out, okb = lib().p256_decompress(ubuf, dev == 'gpu')
+        upts = np.frombuffer(out, dtype=np.uint8).reshape(-1, 64)
+        uok = np.frombuffer(okb, dtype=np.uint8).astype(bool)
+        xy[c33] = upts[inv]
+        ok[c33] = uok[inv]
+    c64 = np.nonzero(all_len == 64)[0]
+    if len(c64):
+        from ..utils.p256 import is_on_curve
+        for k in c64:
+            raw = bytes(all_addr[k])
+            xy[k] = all_addr[k]
+            ok[k] = is_on_curve(int.from_bytes(raw[:32], 'little'), int.from_bytes(raw[32:], 'little'))
+    n_jobs = len(job_input)
+    if not ok.all():  # a signer key or an output address is off-curve: the object path decides
+        return None
+    if np.any(out_amount == 0):
+        return None
+    t3 = perf_counter()
+
+    # ---- signatures: one batched verify (+ the reference's ASCII-hex retry for the failures)
+    sigs = np.frombuffer(d['sigs'], dtype=np.uint8).reshape(-1, 64)
+    digest = np.frombuffer(d['digest'], dtype=np.uint8).reshape(-1, 32)
+    in_tx = _i32(d, 'in_tx')
+    job_tx = in_tx[job_input]
+    recs = np.concatenate([xy[job_input], sigs[sig_ids], digest[job_tx]], axis=1)
+    status = validate._verify(np.ascontiguousarray(recs).tobytes(), None).copy() if n_jobs else np.zeros(0, np.uint8)
+    retry = np.nonzero(status == op.INVALID)[0]
+    if len(retry):
+        signed_len = _i32(d, 'signed_len')
+        rr = recs[retry].copy()
+        for m, j in enumerate(retry):
+            k = int(job_tx[j])
+            rr[m, 128:] = np.frombuffer(hashlib.sha256(d['hex'][k][:2 * signed_len[k]].encode()).digest(), np.uint8)
+        st2 = validate._verify(np.ascontiguousarray(rr).tobytes(), None)
+        status[retry] = np.where(st2 == op.VALID, op.VALID, status[retry])
+    if np.any(status != op.VALID):
+        return None
+    t4 = perf_counter()
+
+    # ---- fees (REGULAR txs: every output counts)
+    in_start, out_start = _i32(d, 'in_start'), _i32(d, 'out_start')
+    in_sum = np.add.reduceat(in_amount.astype(np.int64), in_start[:-1]) if n_in else np.zeros(n, np.int64)
+    out_sum = np.add.reduceat(out_amount.astype(np.int64), out_start[:-1])
+    fee = in_sum - out_sum
+    if np.any(fee < 0):
+        return None
+    fees_total = Decimal(int(fee.sum())) / SMALLEST
+    validate.timings.update({'decompress_s': t3 - t2, 'collect_s': 0.0, 'ecdsa_s': t4 - t3, 'rules_s': 0.0,
+                             'signatures': n_jobs, 'txs': n})
+    metrics.inc('upow_signatures_verified_total', n_jobs, help='P-256 signatures verified in block validation')
+    manager.last_block_timings.update({'utxo_s': t2 - t1, 'verify_s': t4 - t2, 'merkle_s': 0.0,
+                                       'total_s': t4 - t0, 'txs': n})
+
+    # ---- rows for the ledger writes
+    in_strs, in_json = lib().input_address_strings(np.ascontiguousarray(pay['addr']).tobytes(),
+                                                   pay['len'].astype(np.uint8).tobytes(), d['in_start'], 8)
+    hexes, hashes = d['hex'], d['tx_hash']
+    out_strs = d['out_addr_str']
+    fee_str = [_numeric6(int(f)) for f in fee]
+    raw_keys = d['in_keys']
+    spent = [(raw_keys[40 * k:40 * k + 32].hex(), int(raw_keys[40 * k + 32])) for k in range(n_in)]
+    out_tx = _i32(d, 'out_tx')
+    out_index = np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]
+    txid = np.frombuffer(d['txid'], dtype=np.uint8).reshape(-1, 32)
+
+    async def apply(block_hash, address, random, block_reward, content_time, coinbase_transaction):
+        try:
+            with database.transaction(foreign_keys=False):
+                await database.add_block(block_no, block_hash, block_content, address, random, difficulty,
+                                         block_reward + fees_total, content_time)
+                database.checkpoint('block')
+                await database.add_transaction(coinbase_transaction, block_hash)
+                rows = [(block_hash, hashes[k], hexes[k], in_json[k], d['out_addr_json'][k], d['out_amount_json'][k],
+                         fee_str[k]) for k in range(n)]
+                addr_rows = []
+                for k in range(n):
+                    for a in set(in_strs[in_start[k]:in_start[k + 1]]) | set(out_strs[out_start[k]:out_start[k + 1]]):
+                        addr_rows.append((a, hashes[k]))
+                database.insert_transaction_rows(rows, addr_rows)
+                database.checkpoint('transactions')
+                database.insert_regular_outputs(
+                    [(hashes[out_tx[o]], int(out_index[o]), out_strs[o], 0) for o in range(len(out_tx))],
+                    txid[out_tx], out_index, out_amount, out_addr, out_len)
+                await database.add_transaction_outputs([coinbase_transaction])
+                database.checkpoint('outputs')
+                await database.remove_pending_transactions_by_hash(list(hashes))
+                database.remove_spent_regular(spent, in_keys)
+                database._delete_outpoints('pending_spent_outputs', spent)
+                database.checkpoint('spent')
+        except Exception as e:
+            logger.error(f'Transaction of {block_no} has not been added in block {e}')
+            database._rebuild_utxo_index()
+            manager.Manager.difficulty = None
+            return False
+        return True
+
+    res = await manager._finalize_block(block_no, block_content, fees_total, n, apply, error_list, t0)
+    timings.update({'decode_to_checks_s': t1 - t0, 'apply_s': perf_counter() - t4})
+    return res
+
+
+def _numeric6(fee_smallest: int) -> str:
+    """``numeric(Decimal(fee) / 10**8, 6)`` for a non-negative fee: round half up to 6 decimals."""
+    q = (fee_smallest + 50) // 100
+    return f'{q // 1000000}.{q % 1000000:06d}'
+
+
+__all__ = ['create_block_from_hex', 'decode']

@@ -255,13 +255,9 @@ _GOV_SPEND = (TransactionType.INODE_DE_REGISTRATION, TransactionType.VOTE_AS_VAL
               TransactionType.REVOKE_AS_DELEGATE)
 
 
-async def check_block(block_content: str, transactions: List[Transaction], mining_info: tuple = None,
-                      error_list=None) -> bool:
-    """manager.py:422-647."""
-    from .validate import verify_block_transactions
-    if error_list is None:
-        error_list = []
-    t0 = perf_counter()
+async def check_block_header(block_content: str, mining_info: tuple, error_list: list):
+    """Header checks of manager.py:430-462 (PoW, previous hash, timestamp window).
+    Returns (block_no, merkle_tree) or None after recording the error."""
     if mining_info is None:
         mining_info = await calculate_difficulty()
     difficulty, last_block = mining_info
@@ -270,23 +266,37 @@ async def check_block(block_content: str, transactions: List[Transaction], minin
     if not await check_block_is_valid(block_content, mining_info):
         error_list.append('block not valid')
         logger.error('block not valid')
-        return False
+        return None
     content_time = int(content_time)
     if last_block != {} and previous_hash != last_block['hash']:
         error_list.append(error := 'Previous hash is not matched')
         logger.error(error)
-        return False
+        return None
     last_ts = last_block['timestamp'] if 'timestamp' in last_block else 0
     if last_ts > content_time or last_ts == content_time:
         error_list.append(error := 'timestamp younger than previous block')
         logger.error(error)
-        return False
+        return None
     current_timestamp = timestamp()
     if content_time > current_timestamp:
         error_list.append(error := f'timestamp in the future content_time: {content_time}, '
                                    f'current_timestamp {current_timestamp}')
         logger.error(error)
+        return None
+    return block_no, merkle_tree
+
+
+async def check_block(block_content: str, transactions: List[Transaction], mining_info: tuple = None,
+                      error_list=None) -> bool:
+    """manager.py:422-647."""
+    from .validate import verify_block_transactions
+    if error_list is None:
+        error_list = []
+    t0 = perf_counter()
+    hdr = await check_block_header(block_content, mining_info, error_list)
+    if hdr is None:
         return False
+    block_no, merkle_tree = hdr
     database: Database = Database.instance
     transactions = [tx for tx in transactions if isinstance(tx, Transaction)]
     if get_transactions_size(transactions) > MAX_BLOCK_SIZE_HEX:
@@ -435,6 +445,20 @@ async def _create_block(block_content: str, transactions: List[Transaction], las
     logger.info(f'Creating block no. {block_no}')
     if not await check_block(block_content, transactions, (difficulty, last_block), error_list=error_list):
         return False
+    fees = sum(t.fees for t in transactions)
+
+    async def apply(block_hash, address, random, block_reward, content_time, coinbase_transaction):
+        return await _apply_block(block_no, block_hash, block_content, address, random, difficulty, block_reward, fees,
+                                  content_time, coinbase_transaction, transactions)
+    return await _finalize_block(block_no, block_content, fees, len(transactions), apply, error_list,
+                                 create_start_time)
+
+
+async def _finalize_block(block_no: int, block_content: str, fees, n_txs: int, apply, error_list: list,
+                          create_start_time: float) -> bool:
+    """The part of manager.py:650-757 after ``check_block``: inode rewards, genesis-key rule, coinbase,
+    ledger writes (``apply``), logs, UTXO snapshot cadence and the emission-details record. Shared by
+    the object path (:func:`_create_block`) and the native block path (ledger/fastpath.py)."""
     database: Database = Database.instance
     block_hash = sha256(block_content)
     previous_hash, address, merkle_tree, content_time, content_difficulty, random = split_block_content(block_content)
@@ -449,16 +473,14 @@ async def _create_block(block_content: str, transactions: List[Transaction], las
             error_list.append(error := 'Emission detail is not formed. Hence you cannot mine currently.')
             logger.error(error)
             return False
-    fees = sum(t.fees for t in transactions)
     coinbase_transaction = CoinbaseTransaction(block_hash, address, miner_reward + fees)
     if inode_rewards:
         coinbase_transaction.outputs.extend([TransactionOutput(a, r) for a, r in inode_rewards.items()])
     if not all(o.verify() for o in coinbase_transaction.outputs):
         return False
-    if not await _apply_block(block_no, block_hash, block_content, address, random, difficulty, block_reward, fees,
-                              content_time, coinbase_transaction, transactions):
+    if not await apply(block_hash, address, random, block_reward, content_time, coinbase_transaction):
         return False
-    logger.info(f'Added {len(transactions)} transactions in block {block_no}. Reward: {block_reward}, Fees: {fees} '
+    logger.info(f'Added {n_txs} transactions in block {block_no}. Reward: {block_reward}, Fees: {fees} '
                 f'in {perf_counter() - create_start_time:.3f} seconds')
     if block_no % 10 == 0:
         logger.info(f'unspent_outputs_hash on block no. {block_no}: {await database.get_unspent_outputs_hash()}')

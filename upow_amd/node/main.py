@@ -31,6 +31,7 @@ from .. import config
 from ..constants import ENDIAN, GENESIS_PREV_HASH, MAX_SUPPLY, VERSION
 from ..ledger import manager as mgr
 from ..ledger.database import Database, UniqueViolationError
+from ..ledger.fastpath import create_block_from_hex
 from ..ledger.manager import (Manager, block_to_bytes, calculate_difficulty, clear_pending_transactions, create_block,
                               ledger_lock,
                               create_block_in_syncing_old, get_circulating_supply, get_difficulty,
@@ -407,23 +408,26 @@ async def push_block(request: Request, background_tasks: BackgroundTasks, block_
                                       'accepted'}
     if next_block_id > block_no:
         return {'ok': False, 'error': 'Too old block'}
-    final_transactions, hashes = [], []
+    # full tx hex and mempool hashes, in the reference's order (full txs first, main.py:587-600); the
+    # block then goes through the native block path (ledger/fastpath.py), which defers to the object
+    # path for anything beyond plain transfers
+    final_hexes, hashes = [], []
     for tx_hex in txs:
         if len(tx_hex) == 64:
             hashes.append(tx_hex)
         else:
-            final_transactions.append(await Transaction.from_hex(tx_hex))
+            final_hexes.append(tx_hex)
     if hashes:
-        pending_transactions = await db.get_pending_transactions_by_hash(hashes)
-        if len(pending_transactions) < len(hashes):
+        pending_hexes = await db.get_pending_transactions_hex_by_hash(hashes)
+        if len(pending_hexes) < len(hashes):
             if sender:
                 background_tasks.add_task(sync_blockchain, sender)
                 return {'ok': False, 'error': 'Transaction hash not found, had to sync according to sender node, '
                                               'block may have been accepted'}
             return {'ok': False, 'error': 'Transaction hash not found'}
-        final_transactions.extend(pending_transactions)
+        final_hexes.extend(pending_hexes)
     error_list = []
-    if not await create_block(block_content, final_transactions, error_list=error_list):
+    if not await create_block_from_hex(block_content, final_hexes, error_list=error_list):
         return {'ok': False, 'error': error_list[0]} if error_list else {'ok': False}
     block_hash = sha256(block_content)
     Manager.difficulty = None
@@ -432,7 +436,7 @@ async def push_block(request: Request, background_tasks: BackgroundTasks, block_
     if LAST_PENDING_TRANSACTIONS_CLEAN[0] < timestamp() - 600:
         LAST_PENDING_TRANSACTIONS_CLEAN[0] = timestamp()
         background_tasks.add_task(clear_pending_transactions, pending)
-    block_data = {'block_no': block_no, 'block_hash': block_hash, 'transactions_count': len(final_transactions),
+    block_data = {'block_no': block_no, 'block_hash': block_hash, 'transactions_count': len(final_hexes),
                   'timestamp': timestamp(), 'difficulty': difficulty, 'last_block': last_block,
                   'pending_transactions': pending[:10], 'pending_transactions_hashes': [sha256(t) for t in pending],
                   'merkle_root': get_transactions_merkle_tree(pending[:10])}
@@ -441,7 +445,7 @@ async def push_block(request: Request, background_tasks: BackgroundTasks, block_
         NodesManager.update_last_message(sender)
     background_tasks.add_task(propagate, 'push_block', {
         'block_content': block_content,
-        'txs': [tx.hex() for tx in final_transactions] if len(final_transactions) < 10 else txs,
+        'txs': [(await Transaction.from_hex(h)).hex() for h in final_hexes] if len(final_hexes) < 10 else txs,
         'block_no': block_no})
     return {'ok': True}
 
