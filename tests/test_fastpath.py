@@ -69,9 +69,9 @@ class Pair:
         return await devnet.mine_header(address_of(GENESIS), list(txs), ts=ts, device='cpu')
 
 
-async def _setup():
-    a = await Database.create(utxo_backend='host')
-    b = await Database.create(utxo_backend='host')
+async def _setup(backend='host'):
+    a = await Database.create(utxo_backend=backend)
+    b = await Database.create(utxo_backend=backend)
     p = Pair(a, b)
     base = 1_700_000_000
     for k in range(8):
@@ -85,9 +85,13 @@ def _signed(inputs, outputs, keys, message=None):
     return tx.sign(keys)
 
 
-def test_fast_path_matches_object_path():
+@pytest.mark.parametrize('backend', ['host', pytest.param('gpu', marks=pytest.mark.gpu)])
+def test_fast_path_matches_object_path(backend, request):
+    if backend == 'gpu':
+        request.getfixturevalue('gpu')
+
     async def go():
-        p, base = await _setup()
+        p, base = await _setup(backend)
         ts = base + 60 * 10
         p.use(p.a)
         txs = []

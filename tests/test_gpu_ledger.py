@@ -17,6 +17,7 @@ def test_verify_bench_pipeline_on_gpu(gpu, monkeypatch):
     args = argparse.Namespace(steps=1, warmup=1, txs=600)
     out = run_verify_bench(args, DistContext())
     assert out['config']['utxo_backend'] == 'gpu' and out['config']['device'] == 'gpu'
+    assert out['config']['block_path'] == 'native'
     assert out['value'] > 0
 
 
