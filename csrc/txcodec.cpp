@@ -38,7 +38,8 @@ namespace upow {
 enum TxFlag : uint8_t {
     TX_FAST = 0,      // fully decoded, regular outputs, 1-or-n signatures
     TX_GENERAL = 1,   // valid encoding the fast path does not handle
-    TX_MALFORMED = 2  // the Python parser has to see it (it raises or reads it leniently)
+    TX_MALFORMED = 2,  // the Python parser has to see it (it raises or reads it leniently)
+    TX_COINBASE = 3    // specifier 36 (sync pages carry the block's coinbase among its txs)
 };
 
 struct DecIn {
@@ -174,7 +175,7 @@ static void decode_one(const char* hx, size_t hlen, DecTx& t) {
     size_t mlen = 0;
     bool has_msg = false;
     if (spec == 36) {  // coinbase inside the tx list
-        t.flag = TX_GENERAL;
+        t.flag = TX_COINBASE;
         return;
     }
     if (spec == 1) {

@@ -172,3 +172,56 @@ def test_governance_block_takes_object_path():
         c = await p.mine([st], ts=base + 600)
         await p.push(c, [st], expect=True)
     asyncio.run(go())
+
+
+def test_sync_mode_matches_object_sync():
+    """Replaying a chain page (blocks + their coinbase txs, as /get_blocks serves them) through the
+    native sync path and through create_block_in_syncing_old gives identical ledgers."""
+    async def go():
+        p, base = await _setup()
+        ts = base + 60 * 10
+        p.use(p.a)
+        for r in range(2):
+            txs = []
+            for k in KEYS[:4]:
+                tx = await create_transaction(GENESIS, address_of(k), '0.75')
+                await p.a.add_pending_transaction(tx)
+                txs.append(tx)
+            p.use(p.b)
+            for t in txs:
+                await p.b.add_pending_transaction(t)
+            c = await p.mine(txs, ts=ts + 60 * r)
+            await p.push(c, txs, expect=True)
+        page = await p.a.get_blocks(1, 100)
+        src = await Database.create(utxo_backend='host')
+        dst = await Database.create(utxo_backend='host')
+        from upow_amd.models.transaction import CoinbaseTransaction
+        for db, native in ((src, False), (dst, True)):
+            Database.instance = db
+            last = {}
+            for info in page:
+                manager.Manager.difficulty = None
+                hexes = list(info['transactions'])
+                cb = None
+                for k, h in enumerate(hexes):
+                    t = await Transaction.from_hex(h, False)
+                    if isinstance(t, CoinbaseTransaction):
+                        cb = t
+                        del hexes[k]
+                        break
+                if native:
+                    ok = await fastpath.create_block_from_hex(info['block']['content'], hexes, last_block=last or None,
+                                                              coinbase=cb)
+                    if hexes:
+                        assert fastpath.last_path == 'native'
+                else:
+                    txs = [await Transaction.from_hex(h) for h in hexes]
+                    ok = await manager.create_block_in_syncing_old(info['block']['content'], txs, cb,
+                                                                   last or None)
+                assert ok
+                last = info['block']
+        da, dbb = _dump(src), _dump(dst)
+        for k in da:
+            assert da[k] == dbb[k], k
+        assert _dump(src)['blocks'] == _dump(p.a)['blocks']
+    asyncio.run(go())

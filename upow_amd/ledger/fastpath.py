@@ -68,31 +68,42 @@ def decode(tx_hexes: List[str]) -> Optional[dict]:
 
 
 async def create_block_from_hex(block_content: str, tx_hexes: List[str], error_list: list = None,
-                                last_block: dict = None) -> bool:
-    """``create_block(block_content, [Transaction.from_hex(h) for h in tx_hexes])``, natively when possible."""
+                                last_block: dict = None, coinbase=None) -> bool:
+    """``create_block(block_content, [Transaction.from_hex(h) for h in tx_hexes])``, natively when possible.
+
+    With ``coinbase`` (a CoinbaseTransaction) this is the sync variant ``create_block_in_syncing_old``
+    (manager.py:760-835), which trusts the supplied coinbase instead of rebuilding it."""
     global last_path
     from . import manager
     if error_list is None:
         error_list = []
     t0 = perf_counter()
+
+    async def object_path(locked: bool):
+        txs = [await Transaction.from_hex(h) for h in tx_hexes]
+        if coinbase is not None:
+            fn = manager._create_block_in_syncing_old if locked else manager.create_block_in_syncing_old
+            return await fn(block_content, txs, coinbase, last_block, error_list)
+        fn = manager._create_block if locked else manager.create_block
+        return await fn(block_content, txs, last_block, error_list)
+
     dec = decode(tx_hexes) if tx_hexes else None
     if dec is None:
         last_path = 'object'
-        txs = [await Transaction.from_hex(h) for h in tx_hexes]
-        return await manager.create_block(block_content, txs, last_block, error_list)
+        return await object_path(False)
     async with manager.ledger_lock():
-        ok = await _create_block_fast(block_content, dec, error_list, last_block, t0)
+        ok = await _create_block_fast(block_content, dec, error_list, last_block, t0, coinbase)
         last_path = 'native'
         if ok is None:
             last_path = 'object'
-            txs = [await Transaction.from_hex(h) for h in tx_hexes]
-            ok = await manager._create_block(block_content, txs, last_block, error_list)
-        manager._record_block_metrics(ok, perf_counter() - t0, len(tx_hexes), 'native' if last_path == 'native' else 'push')
+            ok = await object_path(True)
+        label = ('sync' if coinbase is not None else 'push') if last_path == 'object' else 'native'
+        manager._record_block_metrics(ok, perf_counter() - t0, len(tx_hexes), label)
         return ok
 
 
 async def _create_block_fast(block_content: str, d: dict, error_list: list, last_block: Optional[dict],
-                             t0: float) -> Optional[bool]:
+                             t0: float, coinbase=None) -> Optional[bool]:
     """True/False for a decided block; None = hand over to the object path."""
     from . import manager, validate
     from .database import Database
@@ -106,7 +117,7 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     if hdr is None:
         return False
     block_no, merkle_tree = hdr
-    logger.info(f'Creating block no. {block_no} (native path, {d["n"]} txs)')
+    logger.info(f'{"Syncing" if coinbase is not None else "Creating"} block no. {block_no} (native path, {d["n"]} txs)')
     if block_no in manager.double_spend_dict:
         return None
     n = int(d['n'])
@@ -243,7 +254,10 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
             return False
         return True
 
-    res = await manager._finalize_block(block_no, block_content, fees_total, n, apply, error_list, t0)
+    if coinbase is not None:
+        res = await manager._finalize_sync_block(block_no, block_content, fees_total, n, apply, coinbase, t0)
+    else:
+        res = await manager._finalize_block(block_no, block_content, fees_total, n, apply, error_list, t0)
     timings.update({'decode_to_checks_s': t1 - t0, 'apply_s': perf_counter() - t4})
     return res
 

@@ -535,16 +535,26 @@ async def _create_block_in_syncing_old(block_content: str, transactions: List[Tr
     logger.info(f'Syncing block no. {block_no}')
     if not await check_block(block_content, transactions, (difficulty, last_block), error_list=error_list):
         return False
+    fees = sum(t.fees for t in transactions)
+
+    async def apply(block_hash, address, random, block_reward, content_time, coinbase_transaction):
+        return await _apply_block(block_no, block_hash, block_content, address, random, difficulty, block_reward, fees,
+                                  content_time, coinbase_transaction, transactions)
+    return await _finalize_sync_block(block_no, block_content, fees, len(transactions), apply, cb_transaction,
+                                      create_start_time)
+
+
+async def _finalize_sync_block(block_no: int, block_content: str, fees, n_txs: int, apply,
+                               cb_transaction: Optional[CoinbaseTransaction], create_start_time: float) -> bool:
+    """Tail of manager.py:760-835 (trusted coinbase), shared with the native block path."""
     block_hash = sha256(block_content)
     previous_hash, address, merkle_tree, content_time, content_difficulty, random = split_block_content(block_content)
     block_reward = get_block_reward(block_no)
-    fees = sum(t.fees for t in transactions)
     if cb_transaction is None or not all(o.verify() for o in cb_transaction.outputs):
         return False
-    if not await _apply_block(block_no, block_hash, block_content, address, random, difficulty, block_reward, fees,
-                              content_time, cb_transaction, transactions):
+    if not await apply(block_hash, address, random, block_reward, content_time, cb_transaction):
         return False
-    logger.info(f'Added {len(transactions)} transactions in block {block_no}. Reward: {block_reward}, Fees: {fees} '
+    logger.info(f'Added {n_txs} transactions in block {block_no}. Reward: {block_reward}, Fees: {fees} '
                 f'in {perf_counter() - create_start_time:.3f} seconds')
     if block_no % 10 == 0:
         logger.info(f'unspent_outputs_hash on block no. {block_no}: '

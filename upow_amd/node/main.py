@@ -32,6 +32,7 @@ from ..constants import ENDIAN, GENESIS_PREV_HASH, MAX_SUPPLY, VERSION
 from ..ledger import manager as mgr
 from ..ledger.database import Database, UniqueViolationError
 from ..ledger.fastpath import create_block_from_hex
+from ..ops.native import lib
 from ..ledger.manager import (Manager, block_to_bytes, calculate_difficulty, clear_pending_transactions, create_block,
                               ledger_lock,
                               create_block_in_syncing_old, get_circulating_supply, get_difficulty,
@@ -117,19 +118,26 @@ async def create_blocks(blocks: list, error_list=None) -> bool:
     i = last_block['id'] + 1
     for block_info in blocks:
         block = block_info['block']
-        txs = [await Transaction.from_hex(tx) for tx in block_info['transactions']]
+        hexes = list(block_info['transactions'])
+        # the first coinbase among the txs is the trusted one (main.py:112-117); the rest go through
+        # the native block path (ledger/fastpath.py) in sync mode
+        flags = lib().decode_block_txs(hexes, 1)['flags'] if hexes else b''
         cb_tx = None
-        for tx in txs:
-            if isinstance(tx, CoinbaseTransaction):
-                txs.remove(tx)
-                cb_tx = tx
-                break
-        block['merkle_tree'] = get_transactions_merkle_tree([tx.hex() for tx in txs])
-        block_content = block.get('content') or block_to_bytes(last_block['hash'], block)
+        for k, f in enumerate(flags):
+            if f == 3:
+                cand = await Transaction.from_hex(hexes[k])
+                if isinstance(cand, CoinbaseTransaction):
+                    cb_tx = cand
+                    del hexes[k]
+                    break
+        block_content = block.get('content')
+        if not block_content:
+            txs = [await Transaction.from_hex(h) for h in hexes]
+            block['merkle_tree'] = get_transactions_merkle_tree([tx.hex() for tx in txs])
+            block_content = block_to_bytes(last_block['hash'], block)
         assert i == block['id']
-        if not await create_block_in_syncing_old(
-                block_content.hex() if isinstance(block_content, bytes) else block_content, txs, cb_tx, last_block,
-                error_list=error_list):
+        if not await create_block_from_hex(block_content.hex() if isinstance(block_content, bytes) else block_content,
+                                           hexes, error_list=error_list, last_block=last_block, coinbase=cb_tx):
             return False
         last_block = block
         i += 1
