@@ -202,6 +202,38 @@ PYBIND11_MODULE(_native, m) {
         { py::gil_scoped_release rel; o = utxo_dump(h, nullptr); }
         return py::bytes(reinterpret_cast<const char*>(o.data()), o.size());
     });
+    m.def("utxo_block_inputs", [recs_arg](int64_t h, py::buffer keys, py::bytes in_start, py::bytes out_amount,
+                                          py::bytes out_start, uint32_t want_tag) {
+        int64_t n_in; const uint8_t* kp = recs_arg(keys, n_in);
+        std::string is = in_start, oa = out_amount, os = out_start;
+        if (is.size() % 4 || is.size() < 4 || os.size() != is.size() || oa.size() % 8)
+            throw std::invalid_argument("bad segment arrays");
+        const int64_t n_tx = int64_t(is.size() / 4) - 1;
+        const int32_t* isp = reinterpret_cast<const int32_t*>(is.data());
+        const int32_t* osp = reinterpret_cast<const int32_t*>(os.data());
+        const int64_t n_out = int64_t(oa.size() / 8);
+        for (int64_t t = 0; t < n_tx; ++t)  // the kernels index with these: validate them on the host
+            if (isp[t] < 0 || isp[t + 1] < isp[t] || osp[t] < 0 || osp[t + 1] < osp[t])
+                throw std::invalid_argument("segment offsets must be non-decreasing");
+        if (isp[n_tx] != n_in || osp[n_tx] != n_out || isp[0] != 0 || osp[0] != 0)
+            throw std::invalid_argument("segment offsets do not cover the arrays");
+        BlockInputsResult r;
+        {
+            py::gil_scoped_release rel;
+            r = utxo_block_inputs(h, kp, n_in, isp, reinterpret_cast<const uint64_t*>(oa.data()), n_out, osp, n_tx,
+                                  want_tag);
+        }
+        auto b = [](const void* p, size_t n) { return py::bytes(static_cast<const char*>(p), n); };
+        return py::make_tuple(b(r.tags.data(), r.tags.size()), b(r.payload.data(), r.payload.size()),
+                              b(r.dup_of.data(), 4 * r.dup_of.size()), b(r.fee.data(), 8 * r.fee.size()),
+                              b(r.missing.data(), 4 * r.missing.size()), r.n_dup);
+    });
+    m.def("utxo_set_hash", [](int64_t h, uint32_t tag) {
+        std::vector<uint8_t> d;
+        uint64_t n = 0;
+        { py::gil_scoped_release rel; d = utxo_set_hash(h, tag, &n); }
+        return py::make_tuple(py::bytes(reinterpret_cast<const char*>(d.data()), d.size()), n);
+    });
     m.def("utxo_dump_payload", [](int64_t h) {
         std::vector<uint8_t> o, pay;
         { py::gil_scoped_release rel; o = utxo_dump(h, &pay); }

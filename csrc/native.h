@@ -56,6 +56,20 @@ std::vector<uint8_t> utxo_lookup(int64_t h, const uint8_t* recs, int64_t n, std:
 std::vector<uint8_t> utxo_erase(int64_t h, const uint8_t* recs, int64_t n);  // 1 if erased
 std::vector<uint8_t> utxo_dump(int64_t h, std::vector<uint8_t>* payload_out);
 
+// whole-block input pass: lookup (K7) + duplicate candidates (K10) + per-tx fees (K11) in one round trip
+struct BlockInputsResult {
+    std::vector<uint8_t> tags, payload;  // per input: table tag (0xff absent), 80-byte payload
+    std::vector<uint32_t> dup_of;        // per input: 1 + index of the earlier identical input, else 0
+    std::vector<int64_t> fee;            // per tx: sum(spent) - sum(outputs), smallest units
+    std::vector<uint32_t> missing;       // per tx: inputs not found with want_tag (or without payload)
+    uint32_t n_dup = 0;
+};
+BlockInputsResult utxo_block_inputs(int64_t h, const uint8_t* keys, int64_t n_in, const int32_t* in_start,
+                                    const uint64_t* out_amount, int64_t n_out, const int32_t* out_start,
+                                    int64_t n_tx, uint32_t want_tag);
+// K12: SHA-256 over (txid || index byte) of the entries with `tag`, sorted by (txid, index)
+std::vector<uint8_t> utxo_set_hash(int64_t h, uint32_t tag, uint64_t* count_out);
+
 // ---------------------------------------------------------------- base58
 std::string b58encode(const uint8_t* data, size_t n);
 std::vector<uint8_t> b58decode(const std::string& s);

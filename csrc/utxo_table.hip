@@ -17,6 +17,7 @@
 // inputs_addresses) without touching the SQL tables. Probing scans only the compact 48-byte key
 // slots; the payload line is read once, on a hit.
 #include <hip/hip_runtime.h>
+#include <hipcub/device/device_radix_sort.hpp>
 
 #include <cstring>
 #include <mutex>
@@ -26,6 +27,7 @@
 #include <vector>
 
 #include "native.h"
+#include "sha256_common.h"
 
 namespace upow {
 
@@ -367,6 +369,230 @@ std::vector<uint8_t> utxo_dump(int64_t h, std::vector<uint8_t>* payload_out) {
         if (n) uck(hipMemcpy(payload_out->data(), dp.p, payload_out->size(), hipMemcpyDeviceToHost), "d2h payload");
     }
     return out;
+}
+
+// ================================================================================================
+// Whole-block input pass (K7 + K10 + K11 in one round trip) and the sorted UTXO-set hash (K12).
+// ================================================================================================
+
+// K10: duplicate outpoints within a block. One 64-bit CAS per lane into a scratch table whose word
+// packs a 40-bit fingerprint of (txid, index) with the lane id of the first inserter; a lane that
+// meets its own fingerprint reports that lane (dup_of = winner + 1). The host confirms candidates
+// against the full 36-byte keys, so a fingerprint collision can never fail a valid block.
+__device__ __forceinline__ uint64_t outpoint_fp(const uint32_t k[8], uint32_t idx) {
+    uint64_t h = (uint64_t(k[0]) << 32 | k[1]) ^ (uint64_t(k[2]) << 17) ^ (uint64_t(k[3]) * 0x9E3779B97F4A7C15ull) ^
+                 (uint64_t(k[4]) << 7) ^ (uint64_t(k[5]) << 29) ^ k[6] ^ (uint64_t(k[7]) << 41) ^
+                 (uint64_t(idx) * 0xC2B2AE3D27D4EB4Full);
+    h ^= h >> 31;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 29;
+    return h;
+}
+
+__global__ __launch_bounds__(256) void block_dup_kernel(const UtxoKeyRec* __restrict__ recs, int64_t n,
+                                                        unsigned long long* __restrict__ scratch, uint32_t mask,
+                                                        uint32_t* __restrict__ dup_of) {
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t k[8];
+    load_key(recs[i], k);
+    const uint64_t fp = outpoint_fp(k, recs[i].index & 0xffu);
+    const unsigned long long mine = (fp & ~0xFFFFFFull) | (uint64_t(i) & 0xFFFFFFull);
+    const unsigned long long want = fp & ~0xFFFFFFull;
+    uint32_t s = uint32_t(fp) & mask;
+    uint32_t res = 0;
+    for (uint32_t probe = 0; probe <= mask; ++probe) {
+        const unsigned long long prev = atomicCAS(&scratch[s], 0ull, mine);
+        if (prev == 0ull) break;  // claimed: first occurrence
+        if ((prev & ~0xFFFFFFull) == want) {
+            res = uint32_t(prev & 0xFFFFFFull) + 1u;
+            break;
+        }
+        s = (s + 1) & mask;
+    }
+    dup_of[i] = res;
+}
+
+// K11: per-tx fee = sum(spent amounts) - sum(output amounts), int64 smallest units; missing[t] counts
+// inputs not found with the wanted tag.
+__global__ __launch_bounds__(256) void block_fee_kernel(const uint8_t* __restrict__ tags,
+                                                        const UtxoPayload* __restrict__ pay,
+                                                        const int32_t* __restrict__ in_start,
+                                                        const uint64_t* __restrict__ out_amount,
+                                                        const int32_t* __restrict__ out_start, int64_t n_tx,
+                                                        uint32_t want_tag, int64_t* __restrict__ fee,
+                                                        uint32_t* __restrict__ missing) {
+    const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= n_tx) return;
+    int64_t acc = 0;
+    uint32_t miss = 0;
+    for (int32_t k = in_start[t]; k < in_start[t + 1]; ++k) {
+        if (tags[k] != want_tag || pay[k].addr_len == 0) ++miss;
+        acc += int64_t(pay[k].amount);
+    }
+    for (int32_t k = out_start[t]; k < out_start[t + 1]; ++k) acc -= int64_t(out_amount[k]);
+    fee[t] = acc;
+    missing[t] = miss;
+}
+
+BlockInputsResult utxo_block_inputs(int64_t h, const uint8_t* keys, int64_t n_in, const int32_t* in_start,
+                                    const uint64_t* out_amount, int64_t n_out, const int32_t* out_start,
+                                    int64_t n_tx, uint32_t want_tag) {
+    std::lock_guard<std::mutex> lk(g_ut_mu);
+    UtxoTableDev& t = table(h);
+    BlockInputsResult r;
+    r.tags.assign(size_t(n_in), 0xff);
+    r.payload.assign(size_t(n_in) * sizeof(UtxoPayload), 0);
+    r.dup_of.assign(size_t(n_in), 0);
+    r.fee.assign(size_t(n_tx), 0);
+    r.missing.assign(size_t(n_tx), 0);
+    if (n_tx == 0) return r;
+    if (n_in >= (int64_t(1) << 24)) throw std::invalid_argument("too many inputs for one block pass");
+    uint32_t log2 = 8;
+    while ((int64_t(1) << log2) < 2 * n_in) ++log2;
+    const uint32_t scap = 1u << log2;
+    DevBuf<UtxoKeyRec> d_keys(n_in);
+    DevBuf<uint8_t> d_tags(n_in);
+    DevBuf<UtxoPayload> d_pay(n_in);
+    DevBuf<uint32_t> d_dup(n_in);
+    DevBuf<unsigned long long> d_scratch(scap);
+    DevBuf<int32_t> d_in_start(n_tx + 1), d_out_start(n_tx + 1);
+    DevBuf<uint64_t> d_out(n_out);
+    DevBuf<int64_t> d_fee(n_tx);
+    DevBuf<uint32_t> d_miss(n_tx);
+    if (n_in) uck(hipMemcpy(d_keys.p, keys, sizeof(UtxoKeyRec) * n_in, hipMemcpyHostToDevice), "h2d keys");
+    if (n_out) uck(hipMemcpy(d_out.p, out_amount, 8 * size_t(n_out), hipMemcpyHostToDevice), "h2d out");
+    uck(hipMemcpy(d_in_start.p, in_start, 4 * size_t(n_tx + 1), hipMemcpyHostToDevice), "h2d in_start");
+    uck(hipMemcpy(d_out_start.p, out_start, 4 * size_t(n_tx + 1), hipMemcpyHostToDevice), "h2d out_start");
+    uck(hipMemset(d_scratch.p, 0, sizeof(unsigned long long) * scap), "memset scratch");
+    if (n_in) {
+        const dim3 g(unsigned((n_in + 255) / 256));
+        hipLaunchKernelGGL(utxo_lookup_kernel, g, dim3(256), 0, 0, t.tab, t.pay, t.cap - 1, d_keys.p, n_in, d_tags.p,
+                           d_pay.p);
+        uck(hipGetLastError(), "utxo_lookup_kernel");
+        hipLaunchKernelGGL(block_dup_kernel, g, dim3(256), 0, 0, d_keys.p, n_in, d_scratch.p, scap - 1, d_dup.p);
+        uck(hipGetLastError(), "block_dup_kernel");
+    }
+    hipLaunchKernelGGL(block_fee_kernel, dim3(unsigned((n_tx + 255) / 256)), dim3(256), 0, 0, d_tags.p, d_pay.p,
+                       d_in_start.p, d_out.p, d_out_start.p, n_tx, want_tag, d_fee.p, d_miss.p);
+    uck(hipGetLastError(), "block_fee_kernel");
+    if (n_in) {
+        uck(hipMemcpy(r.tags.data(), d_tags.p, size_t(n_in), hipMemcpyDeviceToHost), "d2h tags");
+        uck(hipMemcpy(r.payload.data(), d_pay.p, r.payload.size(), hipMemcpyDeviceToHost), "d2h payload");
+        uck(hipMemcpy(r.dup_of.data(), d_dup.p, 4 * size_t(n_in), hipMemcpyDeviceToHost), "d2h dup");
+    }
+    uck(hipMemcpy(r.fee.data(), d_fee.p, 8 * size_t(n_tx), hipMemcpyDeviceToHost), "d2h fee");
+    uck(hipMemcpy(r.missing.data(), d_miss.p, 4 * size_t(n_tx), hipMemcpyDeviceToHost), "d2h missing");
+    // exact confirmation of duplicate candidates (full 36-byte key compare)
+    const UtxoKeyRec* kr = reinterpret_cast<const UtxoKeyRec*>(keys);
+    for (int64_t i = 0; i < n_in; ++i) {
+        if (!r.dup_of[size_t(i)]) continue;
+        const uint32_t w = r.dup_of[size_t(i)] - 1;
+        if (std::memcmp(kr[i].txid, kr[w].txid, 32) != 0 || (kr[i].index & 0xffu) != (kr[w].index & 0xffu))
+            r.dup_of[size_t(i)] = 0;  // fingerprint collision, not a duplicate
+        else
+            ++r.n_dup;
+    }
+    return r;
+}
+
+// K12: SHA-256 over (txid || index byte) of every entry with `tag`, sorted by (txid, index).
+// Stable LSD radix sort on the device (hipCUB): index, then the txid's four 64-bit big-endian words
+// from least to most significant; the message is gathered on the device and hashed on the host
+// (Merkle–Damgard is sequential).
+__global__ __launch_bounds__(256) void set_compact_kernel(const UtxoSlot* __restrict__ tab, uint32_t cap,
+                                                          uint32_t tag, UtxoKeyRec* __restrict__ out,
+                                                          uint32_t* __restrict__ count) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= cap) return;
+    const uint32_t m = tab[s].meta;
+    if ((m & 3u) != ST_FULL || ((m >> 16) & 0xffu) != tag) return;
+    const uint32_t o = atomicAdd(count, 1u);
+    UtxoKeyRec r;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        r.txid[4 * w] = uint8_t(tab[s].k[w]);
+        r.txid[4 * w + 1] = uint8_t(tab[s].k[w] >> 8);
+        r.txid[4 * w + 2] = uint8_t(tab[s].k[w] >> 16);
+        r.txid[4 * w + 3] = uint8_t(tab[s].k[w] >> 24);
+    }
+    r.index = (m >> 8) & 0xffu;
+    r.tag = tag;
+    out[o] = r;
+}
+
+// column c of the sort: 0 = index, 1..4 = big-endian txid word (4 - c), gathered through perm
+__global__ __launch_bounds__(256) void sort_column_kernel(const UtxoKeyRec* __restrict__ recs,
+                                                          const uint32_t* __restrict__ perm, uint32_t n, int c,
+                                                          uint64_t* __restrict__ col) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const UtxoKeyRec& r = recs[perm[i]];
+    if (c == 0) {
+        col[i] = r.index & 0xffu;
+        return;
+    }
+    const uint8_t* b = r.txid + 8 * (4 - c);
+    uint64_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v = (v << 8) | b[q];
+    col[i] = v;
+}
+
+__global__ __launch_bounds__(256) void iota_kernel(uint32_t* __restrict__ p, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = i;
+}
+
+__global__ __launch_bounds__(256) void set_message_kernel(const UtxoKeyRec* __restrict__ recs,
+                                                          const uint32_t* __restrict__ perm, uint32_t n,
+                                                          uint8_t* __restrict__ msg) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const UtxoKeyRec& r = recs[perm[i]];
+    uint8_t* o = msg + size_t(i) * 33;
+#pragma unroll
+    for (int q = 0; q < 32; ++q) o[q] = r.txid[q];
+    o[32] = uint8_t(r.index);
+}
+
+std::vector<uint8_t> utxo_set_hash(int64_t h, uint32_t tag, uint64_t* count_out) {
+    std::lock_guard<std::mutex> lk(g_ut_mu);
+    UtxoTableDev& t = table(h);
+    DevBuf<UtxoKeyRec> recs(t.cap);
+    uck(hipMemset(t.d_counter, 0, sizeof(uint32_t)), "memset");
+    hipLaunchKernelGGL(set_compact_kernel, dim3((t.cap + 255) / 256), dim3(256), 0, 0, t.tab, t.cap, tag, recs.p,
+                       t.d_counter);
+    uck(hipGetLastError(), "set_compact_kernel");
+    uint32_t n = 0;
+    uck(hipMemcpy(&n, t.d_counter, sizeof(uint32_t), hipMemcpyDeviceToHost), "d2h n");
+    if (count_out) *count_out = n;
+    std::vector<uint8_t> msg(size_t(n) * 33);
+    if (n) {
+        DevBuf<uint32_t> perm_a(n), perm_b(n);
+        DevBuf<uint64_t> col_a(n), col_b(n);
+        const dim3 g((n + 255) / 256);
+        hipLaunchKernelGGL(iota_kernel, g, dim3(256), 0, 0, perm_a.p, n);
+        size_t temp_bytes = 0;
+        uck(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, col_a.p, col_b.p, perm_a.p, perm_b.p, n),
+            "radix sort sizing");
+        DevBuf<uint8_t> temp(temp_bytes);
+        for (int c = 0; c <= 4; ++c) {  // least significant column first; radix sort is stable
+            hipLaunchKernelGGL(sort_column_kernel, g, dim3(256), 0, 0, recs.p, perm_a.p, n, c, col_a.p);
+            uck(hipGetLastError(), "sort_column_kernel");
+            uck(hipcub::DeviceRadixSort::SortPairs(temp.p, temp_bytes, col_a.p, col_b.p, perm_a.p, perm_b.p, n,
+                                                   0, c == 0 ? 8 : 64),
+                "radix sort");
+            std::swap(perm_a.p, perm_b.p);
+        }
+        DevBuf<uint8_t> d_msg(size_t(n) * 33);
+        hipLaunchKernelGGL(set_message_kernel, g, dim3(256), 0, 0, recs.p, perm_a.p, n, d_msg.p);
+        uck(hipGetLastError(), "set_message_kernel");
+        uck(hipMemcpy(msg.data(), d_msg.p, msg.size(), hipMemcpyDeviceToHost), "d2h message");
+    }
+    std::vector<uint8_t> digest(32);
+    host_sha256(msg.data(), msg.size(), digest.data());
+    return digest;
 }
 
 }  // namespace upow

@@ -72,3 +72,49 @@ def test_gpu_backend_matches_host(gpu):
     assert (idx.probe(keys[::97]) == 1).all()
     t, p = idx.lookup(keys[::97])  # payloads survive the device rehash
     assert (t == 1).all() and [int(a) for a in p['amount']] == amounts[::97]
+
+
+def _block_inputs_case(idx, seed):
+    rng = random.Random(seed)
+    keys = _keys(4000, seed)
+    amounts = [rng.randrange(1, 1 << 40) for _ in keys]
+    addrs = [bytes([42]) + rng.randbytes(32) for _ in keys]
+    idx.insert(keys[:3000], 0, make_payload(amounts[:3000], addrs[:3000]))
+    idx.insert(keys[3000:3500], 3, make_payload(amounts[3000:3500], addrs[3000:3500]))
+    # a block: 700 txs of 1-3 inputs drawn from live, wrong-table and unknown outpoints, plus duplicates
+    spend = keys[:1500] + keys[3000:3010] + keys[3600:3610] + keys[5:9]
+    rng.shuffle(spend)
+    in_start = [0]
+    while in_start[-1] < len(spend):
+        in_start.append(min(len(spend), in_start[-1] + rng.randint(1, 3)))
+    n_tx = len(in_start) - 1
+    out_start = [0]
+    for _ in range(n_tx):
+        out_start.append(out_start[-1] + rng.randint(1, 2))
+    out_amount = np.array([rng.randrange(1, 1 << 38) for _ in range(out_start[-1])], dtype=np.uint64)
+    return pack_records(spend), np.array(in_start, np.int32), out_amount, np.array(out_start, np.int32)
+
+
+def test_block_inputs_host():
+    idx = UtxoIndex(backend='host')
+    recs, ins, outs, ost = _block_inputs_case(idx, 11)
+    tags, pay, dup_of, fee, missing, n_dup = idx.block_inputs(recs, ins, outs, ost, 0)
+    assert n_dup == 4 and int((dup_of > 0).sum()) == 4
+    assert int(missing.sum()) == 20 + 4 * 0  # 10 wrong-table + 10 unknown (duplicates of live keys are found)
+    amt = pay['amount'].astype(np.int64)
+    for t in range(len(ins) - 1):
+        assert fee[t] == amt[ins[t]:ins[t + 1]].sum() - outs[ost[t]:ost[t + 1]].astype(np.int64).sum()
+
+
+@pytest.mark.gpu
+def test_block_inputs_and_set_hash_gpu_match_host(gpu):
+    h, g = UtxoIndex(backend='host'), UtxoIndex(backend='gpu')
+    ch = _block_inputs_case(h, 13)
+    cg = _block_inputs_case(g, 13)
+    rh, rg = h.block_inputs(*ch, 0), g.block_inputs(*cg, 0)
+    for k in (0, 1, 3, 4):  # tags, payloads, fees, missing: identical
+        assert np.array_equal(np.asarray(rh[k]).view(np.uint8), np.asarray(rg[k]).view(np.uint8)), k
+    # duplicates: which copy is flagged depends on lane order on the GPU; the count does not
+    assert rh[5] == rg[5] == int((rg[2] > 0).sum()) == 4
+    for tag in (0, 3, 5):
+        assert h.set_hash(tag) == g.set_hash(tag)

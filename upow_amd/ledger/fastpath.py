@@ -127,17 +127,17 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         return None
     t1 = perf_counter()
 
-    # ---- inputs: one lookup launch (existence in unspent_outputs + amount + address)
+    # ---- inputs: one device pass = lookup (existence in unspent_outputs + amount + address),
+    #      duplicate detection and per-tx fees (csrc/utxo_table.hip utxo_block_inputs)
     in_keys = np.frombuffer(d['in_keys'], dtype=np.uint8).reshape(-1, 40)
     n_in = len(in_keys)
-    keyview = np.ascontiguousarray(in_keys[:, :36]).view(np.dtype((np.void, 36))).ravel()
-    if len(np.unique(keyview)) != n_in:
-        return None
-    tags, pay = database.utxo.lookup_records(in_keys)
-    if n_in and (np.any(tags != TAG_BY_TABLE['unspent_outputs']) or np.any(pay['len'] == 0)):
-        return None
-    in_amount = pay['amount'].astype(np.uint64)
+    in_start, out_start = _i32(d, 'in_start'), _i32(d, 'out_start')
     out_amount = np.frombuffer(d['out_amount'], dtype=np.uint64)
+    tags, pay, dup_of, fee, missing, n_dup = database.utxo.block_inputs(
+        in_keys, in_start, out_amount, out_start, TAG_BY_TABLE['unspent_outputs'])
+    if n_dup or np.any(missing):
+        return None
+    in_amount = pay['amount']
     if (n_in and in_amount.max() >= AMOUNT_LIMIT) or (len(out_amount) and out_amount.max() >= AMOUNT_LIMIT):
         return None
     t2 = perf_counter()
@@ -197,11 +197,7 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         return None
     t4 = perf_counter()
 
-    # ---- fees (REGULAR txs: every output counts)
-    in_start, out_start = _i32(d, 'in_start'), _i32(d, 'out_start')
-    in_sum = np.add.reduceat(in_amount.astype(np.int64), in_start[:-1]) if n_in else np.zeros(n, np.int64)
-    out_sum = np.add.reduceat(out_amount.astype(np.int64), out_start[:-1])
-    fee = in_sum - out_sum
+    # ---- fees (REGULAR txs: every output counts; computed by the device pass above)
     if np.any(fee < 0):
         return None
     fees_total = Decimal(int(fee.sum())) / SMALLEST

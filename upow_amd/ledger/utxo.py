@@ -315,10 +315,49 @@ class UtxoIndex:
             keys = [(bytes(recs[n, :32]).hex(), int(idx[n])) for n in range(len(recs))]
             self.be.reset(keys, [int(t) for t in tags], payload)
 
+    def block_inputs(self, in_keys: np.ndarray, in_start: np.ndarray, out_amount: np.ndarray,
+                     out_start: np.ndarray, want_tag: int = 0):
+        """One pass over a block's inputs: K7 lookup (tag + payload), K10 duplicate detection and K11
+        per-tx fees. GPU backend: one H2D/D2H round trip and three kernels (csrc/utxo_table.hip).
+
+        Returns (tags u8[n_in], payload[n_in], dup_of u32[n_in] (1 + earlier duplicate, else 0),
+        fee i64[n_tx], missing u32[n_tx], n_dup)."""
+        in_start = np.ascontiguousarray(in_start, dtype=np.int32)
+        out_start = np.ascontiguousarray(out_start, dtype=np.int32)
+        out_amount = np.ascontiguousarray(out_amount, dtype=np.uint64)
+        if isinstance(self.be, _GpuBackend):
+            t, p, d, f, m, nd = self.be.L.utxo_block_inputs(self.be.h, np.ascontiguousarray(in_keys),
+                                                            in_start.tobytes(), out_amount.tobytes(),
+                                                            out_start.tobytes(), want_tag)
+            return (np.frombuffer(t, np.uint8), np.frombuffer(p, PAYLOAD_DTYPE), np.frombuffer(d, np.uint32),
+                    np.frombuffer(f, np.int64), np.frombuffer(m, np.uint32), int(nd))
+        tags, pay = self.lookup_records(in_keys)
+        n_in = len(in_keys)
+        dup_of = np.zeros(n_in, dtype=np.uint32)
+        first = {}
+        for i in range(n_in):
+            k = bytes(in_keys[i, :33])
+            if k in first:
+                dup_of[i] = first[k] + 1
+            else:
+                first[k] = i
+        bad = ((tags != want_tag) | (pay['len'] == 0)).astype(np.uint32)
+        n_tx = len(in_start) - 1
+        amt = pay['amount'].astype(np.int64)
+        ins = np.array([amt[in_start[t]:in_start[t + 1]].sum() for t in range(n_tx)], dtype=np.int64)
+        outs = np.array([out_amount[out_start[t]:out_start[t + 1]].astype(np.int64).sum() for t in range(n_tx)],
+                        dtype=np.int64)
+        miss = np.array([bad[in_start[t]:in_start[t + 1]].sum() for t in range(n_tx)], dtype=np.uint32)
+        return tags, pay, dup_of, ins - outs, miss, int((dup_of > 0).sum())
+
     def set_hash(self, tag: int = 0) -> str:
         """K12 from the index: SHA-256 over (txid || index byte) of table ``tag`` sorted by (txid, index)
-        — byte-identical to ``Database.get_unspent_outputs_hash`` (reference database.py:827-830)."""
+        — byte-identical to ``Database.get_unspent_outputs_hash`` (reference database.py:827-830).
+        GPU backend: compaction + stable LSD radix sort + message gather on the device."""
         import hashlib
+        if isinstance(self.be, _GpuBackend):
+            digest, _ = self.be.L.utxo_set_hash(self.be.h, tag)
+            return digest.hex()
         recs = self.records()
         recs = recs[recs[:, 36:40].copy().view(np.uint32).ravel() == tag]
         payload = np.concatenate([recs[:, :32], recs[:, 32:33]], axis=1)  # index byte (the reference's bytes([i]))
