@@ -61,7 +61,9 @@ class Pair:
         for k in da:
             assert da[k] == dbb[k], k
         self.use(self.a)
-        assert await self.a.get_unspent_outputs_hash() == await self.b.get_unspent_outputs_hash()
+        h = self.a.sql_unspent_outputs_hash()
+        assert h == self.b.sql_unspent_outputs_hash() == await self.a.get_unspent_outputs_hash() \
+            == await self.b.get_unspent_outputs_hash()
         return ra, ea
 
     async def mine(self, txs=(), ts=None):

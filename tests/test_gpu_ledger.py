@@ -39,7 +39,7 @@ def test_gpu_index_snapshot_roundtrip(gpu, tmp_path, monkeypatch):
             await devnet.mine_block(addr, ts=1_700_000_000 + 60 * b)
         tx = await create_transaction(0x4242, address_of(0x99), '7')
         await devnet.mine_block(addr, [tx], ts=1_700_000_000 + 600)
-        assert db.utxo.set_hash() == await db.get_unspent_outputs_hash()
+        assert db.utxo.set_hash() == db.sql_unspent_outputs_hash() == await db.get_unspent_outputs_hash()
         snapshot.save(db)
         n = len(db.utxo)
         db.close()

@@ -874,7 +874,15 @@ class Database:
         return self.utxo.filter(outputs, TAG_BY_TABLE['validators_ballot'])
 
     async def get_unspent_outputs_hash(self) -> str:
-        """database.py:827-830: SHA256 over (tx_hash bytes || index byte) sorted by (tx_hash, index)."""
+        """database.py:827-830: SHA256 over (tx_hash bytes || index byte) sorted by (tx_hash, index).
+
+        With the HBM index this is K12 on the device (compaction + radix sort + gather, host hash
+        tail); ``UPOW_UTXO_HASH_SQL=1`` forces the SQL ORDER BY form."""
+        if self.utxo.backend_name == 'gpu' and os.environ.get('UPOW_UTXO_HASH_SQL', '0') != '1':
+            return self.utxo.set_hash(TAG_BY_TABLE['unspent_outputs'])
+        return self.sql_unspent_outputs_hash()
+
+    def sql_unspent_outputs_hash(self) -> str:
         rows = self._q('SELECT tx_hash, "index" FROM unspent_outputs ORDER BY tx_hash, "index"')
         return sha256(''.join(r[0] + bytes([r[1]]).hex() for r in rows))
 
