@@ -319,25 +319,29 @@ UPOW_HD fe sc_reduce(const fe& a) {
     const uint32_t br = raw_sub(d, a, fe_const_n());
     return fe_select(br == 0, d, a);
 }
-// a^(n-2) in the Montgomery domain (a_m = a*R): returns a^-1 * R
+// a^(n-2) in the Montgomery domain (a_m = a*R): returns a^-1 * R.
+// n-2 = ffffffff 00000000 ffffffff ffffffff | bce6faad a7179e84 f3b9cac2 fc63254f. The high half is
+// runs of ones (addition chain through a^(2^32-1)); the low half is scanned bit by bit with the bit
+// taken from a constant word, so the branch is wave-uniform and nothing is indexed dynamically
+// (a windowed table in a local array would live in scratch memory on the GPU).
+UPOW_HD fe sc_sqr_n_mont(fe a, int n) {
+    for (int i = 0; i < n; ++i) a = sc_mont_mul(a, a);
+    return a;
+}
 UPOW_HD fe sc_inv_mont(const fe& a_m) {
-    // n-2 = ffffffff 00000000 ffffffff ffffffff bce6faad a7179e84 f3b9cac2 fc63254f
-    const fe n2{{0xfc63254fu, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu, 0xffffffffu, 0xffffffffu, 0x00000000u,
-                 0xffffffffu}};
-    // 4-bit fixed window
-    fe tbl[16];
-    tbl[0] = fe{P256_RN};
-    tbl[1] = a_m;
-    for (int i = 2; i < 16; ++i) tbl[i] = sc_mont_mul(tbl[i - 1], a_m);
-    fe r = fe{P256_RN};
-    for (int w = 63; w >= 0; --w) {
-        if (w != 63) {
-            r = sc_mont_mul(r, r); r = sc_mont_mul(r, r); r = sc_mont_mul(r, r); r = sc_mont_mul(r, r);
-        }
-        const uint32_t nib = (n2.v[w >> 3] >> ((w & 7) * 4)) & 0xfu;
-        r = sc_mont_mul(r, tbl[nib]);
+    const fe x2 = sc_mont_mul(sc_mont_mul(a_m, a_m), a_m);     // 2^2-1
+    const fe x4 = sc_mont_mul(sc_sqr_n_mont(x2, 2), x2);       // 2^4-1
+    const fe x8 = sc_mont_mul(sc_sqr_n_mont(x4, 4), x4);       // 2^8-1
+    const fe x16 = sc_mont_mul(sc_sqr_n_mont(x8, 8), x8);      // 2^16-1
+    const fe x32 = sc_mont_mul(sc_sqr_n_mont(x16, 16), x16);   // 2^32-1
+    fe t = sc_mont_mul(sc_sqr_n_mont(x32, 64), x32);           // ffffffff 00000000 ffffffff
+    t = sc_mont_mul(sc_sqr_n_mont(t, 32), x32);                // ... ffffffff
+    for (int k = 0; k < 128; ++k) {
+        const uint32_t word = k < 32 ? 0xbce6faadu : k < 64 ? 0xa7179e84u : k < 96 ? 0xf3b9cac2u : 0xfc63254fu;
+        t = sc_mont_mul(t, t);
+        if ((word >> (31 - (k & 31))) & 1u) t = sc_mont_mul(t, a_m);
     }
-    return r;
+    return t;
 }
 
 // ------------------------------------------------------------------------------------------------
