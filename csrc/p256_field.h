@@ -55,45 +55,33 @@ UPOW_HD bool fe_eq(const fe& a, const fe& b) {
     for (int i = 0; i < 8; ++i) t |= a.v[i] ^ b.v[i];
     return t == 0;
 }
-// a >= b (unsigned 256-bit)
+// a >= b (unsigned 256-bit): no final borrow of a - b
 UPOW_HD bool fe_geq(const fe& a, const fe& b) {
-    // compute a - b and look at the final borrow
-    uint64_t borrow = 0;
+    unsigned c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint64_t d = uint64_t(a.v[i]) - b.v[i] - borrow;
-        borrow = (d >> 63) & 1;
-    }
-    return borrow == 0;
+    for (int i = 0; i < 8; ++i) (void)__builtin_subc(a.v[i], b.v[i], c, &c);
+    return c == 0;
 }
-// r = a + b, returns carry
+// r = a + b, returns carry. Carry builtins map onto v_add_co_u32 / v_addc_co_u32 chains on gfx950
+// (the uint64 formulation compiles to 64-bit shift-adds plus register moves: ~4x the instructions).
 UPOW_HD uint32_t raw_add(fe& r, const fe& a, const fe& b) {
-    uint64_t c = 0;
+    unsigned c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        c += uint64_t(a.v[i]) + b.v[i];
-        r.v[i] = uint32_t(c);
-        c >>= 32;
-    }
-    return uint32_t(c);
+    for (int i = 0; i < 8; ++i) r.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+    return c;
 }
 // r = a - b, returns borrow
 UPOW_HD uint32_t raw_sub(fe& r, const fe& a, const fe& b) {
-    uint64_t borrow = 0;
+    unsigned c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint64_t d = uint64_t(a.v[i]) - b.v[i] - borrow;
-        r.v[i] = uint32_t(d);
-        borrow = (d >> 63) & 1;
-    }
-    return uint32_t(borrow);
+    for (int i = 0; i < 8; ++i) r.v[i] = __builtin_subc(a.v[i], b.v[i], c, &c);
+    return c;
 }
 // r = cond ? a : b  (branch-free select)
 UPOW_HD fe fe_select(bool cond, const fe& a, const fe& b) {
     fe r;
-    const uint32_t m = cond ? 0xffffffffu : 0u;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) r.v[i] = (a.v[i] & m) | (b.v[i] & ~m);
+    for (int i = 0; i < 8; ++i) r.v[i] = cond ? a.v[i] : b.v[i];
     return r;
 }
 
@@ -169,51 +157,90 @@ UPOW_HD void sqr_512(uint32_t c[16], const fe& a) {
     }
 }
 
-// NIST fast reduction of a 512-bit value mod p.
+// NIST fast reduction of a 512-bit value mod p (FIPS 186-4 D.2.3):
+//   c mod p = s1 + 2 s2 + 2 s3 + s4 + s5 - s6 - s7 - s8 - s9 (mod p)
+// evaluated with 32-bit add/sub-with-carry chains (v_add_co/v_addc on gfx950; int64 limbs cost
+// 64-bit shift-adds plus sign-extension moves), then the signed overflow T in [-4, 6] is folded with
+// 2^256 == K = 2^224 - 2^192 - 2^96 + 1 (mod p) and the result brought into [0, p) branch-free.
+#define UPOW_ACC(OP, S)                                                     \
+    {                                                                       \
+        unsigned cy_ = 0;                                                   \
+        _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) r[i_] = OP(r[i_], S[i_], cy_, &cy_); \
+        top = (OP(top, 0u, cy_, &cy_));                                     \
+    }
 UPOW_HD fe fe_reduce(const uint32_t c[16]) {
-    const int64_t c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3], c4 = c[4], c5 = c[5], c6 = c[6], c7 = c[7];
-    const int64_t c8 = c[8], c9 = c[9], c10 = c[10], c11 = c[11], c12 = c[12], c13 = c[13], c14 = c[14],
-                  c15 = c[15];
-    int64_t t[8];
-    t[0] = c0 + c8 + c9 - c11 - c12 - c13 - c14;
-    t[1] = c1 + c9 + c10 - c12 - c13 - c14 - c15;
-    t[2] = c2 + c10 + c11 - c13 - c14 - c15;
-    t[3] = c3 + 2 * c11 + 2 * c12 + c13 - c15 - c8 - c9;
-    t[4] = c4 + 2 * c12 + 2 * c13 + c14 - c9 - c10;
-    t[5] = c5 + 2 * c13 + 2 * c14 + c15 - c10 - c11;
-    t[6] = c6 + 3 * c14 + 2 * c15 + c13 - c8 - c9;
-    t[7] = c7 + 3 * c15 + c8 - c10 - c11 - c12 - c13;
-    fe r;
-    int64_t carry = 0;
+    const uint32_t z = 0;
+    const uint32_t s1[8] = {c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]};
+    const uint32_t s2[8] = {z, z, z, c[11], c[12], c[13], c[14], c[15]};
+    const uint32_t s3[8] = {z, z, z, c[12], c[13], c[14], c[15], z};
+    const uint32_t s4[8] = {c[8], c[9], c[10], z, z, z, c[14], c[15]};
+    const uint32_t s5[8] = {c[9], c[10], c[11], c[13], c[14], c[15], c[13], c[8]};
+    const uint32_t s6[8] = {c[11], c[12], c[13], z, z, z, c[8], c[10]};
+    const uint32_t s7[8] = {c[12], c[13], c[14], c[15], z, z, c[9], c[11]};
+    const uint32_t s8[8] = {c[13], c[14], c[15], c[8], c[9], c[10], z, c[12]};
+    const uint32_t s9[8] = {c[14], c[15], z, c[9], c[10], c[11], z, c[13]};
+    uint32_t r[8];
+    uint32_t top = 0;  // signed 9th limb (two's complement)
+    {
+        unsigned cy = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int64_t v = t[i] + carry;
-        r.v[i] = uint32_t(v);
-        carry = v >> 32;  // arithmetic shift
+        for (int i = 0; i < 8; ++i) r[i] = __builtin_addc(s2[i], s3[i], cy, &cy);
+        top = cy;
+        cy = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = __builtin_addc(r[i], r[i], cy, &cy);
+        top = 2 * top + cy;
     }
-    // fold carry * 2^256 == carry * (2^224 - 2^192 - 2^96 + 1) (mod p), twice
+    UPOW_ACC(__builtin_addc, s1)
+    UPOW_ACC(__builtin_addc, s4)
+    UPOW_ACC(__builtin_addc, s5)
+    UPOW_ACC(__builtin_subc, s6)
+    UPOW_ACC(__builtin_subc, s7)
+    UPOW_ACC(__builtin_subc, s8)
+    UPOW_ACC(__builtin_subc, s9)
+    // W = r + T*K with T = (int32)top: add T at limb 0, subtract at limbs 3 and 6, add at limb 7;
+    // every addend is sign-extended to the 9th limb h
+    const uint32_t t = top;
+    const uint32_t sx = uint32_t(int32_t(t) >> 31);
+    uint32_t h = 0;
+    {
+        unsigned cy = 0;
+        r[0] = __builtin_addc(r[0], t, cy, &cy);
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-        int64_t u[8];
+        for (int i = 1; i < 8; ++i) r[i] = __builtin_addc(r[i], sx, cy, &cy);
+        h = __builtin_addc(h, sx, cy, &cy);
+        cy = 0;
+        r[3] = __builtin_subc(r[3], t, cy, &cy);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) u[i] = int64_t(r.v[i]);
-        u[0] += carry;
-        u[3] -= carry;
-        u[6] -= carry;
-        u[7] += carry;
-        carry = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int64_t v = u[i] + carry;
-            r.v[i] = uint32_t(v);
-            carry = v >> 32;
-        }
+        for (int i = 4; i < 8; ++i) r[i] = __builtin_subc(r[i], sx, cy, &cy);
+        h = __builtin_subc(h, sx, cy, &cy);
+        cy = 0;
+        r[6] = __builtin_subc(r[6], t, cy, &cy);
+        r[7] = __builtin_subc(r[7], sx, cy, &cy);
+        h = __builtin_subc(h, sx, cy, &cy);
+        cy = 0;
+        r[7] = __builtin_addc(r[7], t, cy, &cy);
+        h = __builtin_addc(h, sx, cy, &cy);
     }
-    // now 0 <= r < 2^256 < 2p
-    fe t2;
-    const uint32_t br = raw_sub(t2, r, fe_const_p());
-    return fe_select(br == 0, t2, r);
+    // W = r + h*2^256 with h in {-1, 0, 1}:
+    //   h = 1  -> r + K            (< p, no carry)
+    //   h = -1 -> r - K = r + p - 2^256
+    //   h = 0  -> r - p = r + K - 2^256 when r >= p (i.e. when r + K carries), else r
+    const fe K{{1u, 0u, 0u, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xfffffffeu, 0u}};
+    const fe P{P256_P};
+    fe rk, rp, rr;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rr.v[i] = r[i];
+    const uint32_t ck = raw_add(rk, rr, K);
+    raw_add(rp, rr, P);
+    const bool hneg = h == 0xffffffffu;
+    const bool use_k = h == 1u || (h == 0u && ck);
+    fe o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o.v[i] = hneg ? rp.v[i] : (use_k ? rk.v[i] : rr.v[i]);
+    return o;
 }
+#undef UPOW_ACC
 
 UPOW_HD fe fe_mul(const fe& a, const fe& b) {
     uint32_t c[16];
