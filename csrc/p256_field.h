@@ -103,57 +103,53 @@ UPOW_HD fe fe_sub(const fe& a, const fe& b) {
 }
 UPOW_HD fe fe_neg(const fe& a) { return fe_sub(fe_zero(), a); }
 
-// 512-bit schoolbook product, operand scanning: each partial product a_i*b_j + r + carry fits in
-// 64 bits ((2^32-1)^2 + 2(2^32-1) = 2^64 - 1).
+// 512-bit schoolbook product, one row per limb of a: t = a_i*b_j + c[i+j] is one v_mad_u64_u32
+// with a zero-extended 32-bit addend (never overflows 64 bits); the row's high words are chained in
+// with a single add-with-carry per product. (Writing the step as a 64-bit sum of three terms makes
+// the compiler emit 64-bit shift-adds and ~2 register moves per product instead.)
 UPOW_HD void mul_512(uint32_t c[16], const fe& a, const fe& b) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) c[i] = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        uint64_t carry = 0;
+        unsigned cy = 0;
+        uint32_t prev = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const uint64_t t = uint64_t(a.v[i]) * b.v[j] + c[i + j] + carry;
-            c[i + j] = uint32_t(t);
-            carry = t >> 32;
+            const uint64_t t = uint64_t(a.v[i]) * b.v[j] + c[i + j];
+            c[i + j] = __builtin_addc(uint32_t(t), prev, cy, &cy);
+            prev = uint32_t(t >> 32);
         }
-        c[i + 8] = uint32_t(carry);
+        c[i + 8] = prev + cy;  // cannot overflow: the row sum is < 2^(32(i+9))
     }
 }
 
-// squaring: off-diagonal products once, doubled, plus the diagonal.
+// squaring: off-diagonal rows once (28 products), double with funnel shifts, add the 8 squares.
 UPOW_HD void sqr_512(uint32_t c[16], const fe& a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) c[i] = 0;
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
-        uint64_t carry = 0;
+        unsigned cy = 0;
+        uint32_t prev = 0;
 #pragma unroll
         for (int j = i + 1; j < 8; ++j) {
-            const uint64_t t = uint64_t(a.v[i]) * a.v[j] + c[i + j] + carry;
-            c[i + j] = uint32_t(t);
-            carry = t >> 32;
+            const uint64_t t = uint64_t(a.v[i]) * a.v[j] + c[i + j];
+            c[i + j] = __builtin_addc(uint32_t(t), prev, cy, &cy);
+            prev = uint32_t(t >> 32);
         }
-        c[i + 8] = uint32_t(carry);
+        c[i + 8] = prev + cy;
     }
-    // double
-    uint32_t top = 0;
+    c[15] = c[14] >> 31;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const uint32_t nt = c[i] >> 31;
-        c[i] = (c[i] << 1) | top;
-        top = nt;
-    }
-    // add diagonal
-    uint64_t carry = 0;
+    for (int k = 14; k > 0; --k) c[k] = (c[k] << 1) | (c[k - 1] >> 31);
+    c[0] = c[0] << 1;
+    unsigned cy = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const uint64_t sq = uint64_t(a.v[i]) * a.v[i];
-        uint64_t t = uint64_t(c[2 * i]) + uint32_t(sq) + carry;
-        c[2 * i] = uint32_t(t);
-        t = uint64_t(c[2 * i + 1]) + uint32_t(sq >> 32) + (t >> 32);
-        c[2 * i + 1] = uint32_t(t);
-        carry = t >> 32;
+        c[2 * i] = __builtin_addc(c[2 * i], uint32_t(sq), cy, &cy);
+        c[2 * i + 1] = __builtin_addc(c[2 * i + 1], uint32_t(sq >> 32), cy, &cy);
     }
 }
 
