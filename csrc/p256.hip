@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -153,7 +154,8 @@ static uint8_t verify_one_host(const VerifyItem& it, const aff* gtab) {
 // ------------------------------------------------------------------------------------------------
 // device kernels
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void p256_verify_kernel(const VerifyItem* __restrict__ items, int64_t n,
+template <int MIN_WAVES>
+__global__ __launch_bounds__(64, MIN_WAVES) void p256_verify_kernel(const VerifyItem* __restrict__ items, int64_t n,
                                                           const aff* __restrict__ gtab, jac* __restrict__ scratch,
                                                           uint8_t* __restrict__ status) {
     const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -259,7 +261,12 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
     hck(hipMemcpy(d_items, items, sizeof(VerifyItem) * n, hipMemcpyHostToDevice), "h2d items");
     const int block = 64;
     const int grid = int((n + block - 1) / block);
-    hipLaunchKernelGGL(p256_verify_kernel, dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch, d_st);
+    // UPOW_P256_VARIANT=1: force 4 waves/SIMD (128 VGPRs, some spills) instead of the compiler's 3
+    const char* var = std::getenv("UPOW_P256_VARIANT");
+    if (var && var[0] == '1')
+        hipLaunchKernelGGL(p256_verify_kernel<4>, dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch, d_st);
+    else
+        hipLaunchKernelGGL(p256_verify_kernel<1>, dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch, d_st);
     hck(hipGetLastError(), "p256_verify_kernel launch");
     hck(hipMemcpy(st.data(), d_st, size_t(n), hipMemcpyDeviceToHost), "d2h status");
     (void)hipFree(d_items); (void)hipFree(d_scratch); (void)hipFree(d_st);

@@ -21,6 +21,19 @@ for i in range(8300):
     recs.append(op.record(pubs[i % 64], op.sign(msg, keys[i % 64]), hashlib.sha256(msg).digest()))
 base = b''.join(recs)
 out = {}
+import os
+for var in ('0', '1'):
+    os.environ['UPOW_P256_VARIANT'] = var
+    buf = base * 16
+    op.verify_records(buf[:160 * 512], device='gpu')
+    t = time.perf_counter()
+    st = op.verify_records(buf, device='gpu')
+    out[f'variant{var}_gpu_{8300 * 16}'] = round(8300 * 16 / (time.perf_counter() - t), 1)
+    assert (st == 1).all()
+    t = time.perf_counter()
+    st = op.verify_records(base, device='gpu')
+    out[f'variant{var}_gpu_8300'] = round(8300 / (time.perf_counter() - t), 1)
+os.environ['UPOW_P256_VARIANT'] = '0'
 for n in (8300, 8300 * 4, 8300 * 16):
     buf = base * (n // 8300)
     op.verify_records(buf[:160 * 512], device='gpu')

@@ -57,6 +57,8 @@ class Pair:
         assert ea == eb
         if expect is not None:
             assert ra == expect, ea
+        self.a.index_addresses()
+        self.b.index_addresses()
         da, dbb = _dump(self.a), _dump(self.b)
         for k in da:
             assert da[k] == dbb[k], k

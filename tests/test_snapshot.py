@@ -83,3 +83,22 @@ def test_concurrent_blocks_at_same_height_serialised(tmp_path):
         assert await db.get_next_block_id() == 5
         db.close()
     asyncio.run(go())
+
+
+def test_lazy_address_index_follows_rollback(tmp_path):
+    async def go():
+        db = await _chain(tmp_path / 'a.sqlite3', blocks=3)
+        dest = address_of(0x77)
+        assert len(await db.get_address_transactions(dest)) == 1  # catch-up happens on query
+        assert db._address_index_height() == 4
+        tx = await create_transaction(KEY, dest, '0.5')
+        await devnet.mine_block(address_of(KEY), [tx], ts=1_700_000_000 + 60 * 8, device='cpu')
+        assert db._address_index_height() == 4  # not indexed on the apply path
+        assert len(await db.get_address_transactions(dest)) == 2 and db._address_index_height() == 5
+        await db.remove_blocks(5)
+        assert db._address_index_height() == 4
+        assert len(await db.get_address_transactions(dest)) == 1
+        n = db._q1('SELECT COUNT(*) FROM address_transactions')[0]
+        assert db.index_addresses() == 0 and db._q1('SELECT COUNT(*) FROM address_transactions')[0] == n
+        db.close()
+    asyncio.run(go())

@@ -80,6 +80,10 @@ CREATE TABLE IF NOT EXISTS address_transactions (
     address TEXT NOT NULL,
     tx_hash TEXT NOT NULL REFERENCES transactions(tx_hash) ON DELETE CASCADE
 );
+CREATE TABLE IF NOT EXISTS address_index_state (
+    k TEXT PRIMARY KEY,
+    height INTEGER NOT NULL
+);
 """
 for _t in OUTPUT_TABLES[1:]:
     SCHEMA += f"""
@@ -365,14 +369,17 @@ class Database:
         with self.transaction():
             self.conn.execute('DELETE FROM transactions')
             self.conn.execute('DELETE FROM blocks')
+            self.conn.execute("UPDATE address_index_state SET height = 0 WHERE k = 'height'")
         self._rebuild_utxo_index()
 
     async def delete_block(self, id: int):
         self._x('DELETE FROM blocks WHERE id = ?', (id,))
+        self._address_index_rollback()
         self._rebuild_utxo_index()
 
     async def delete_blocks(self, offset: int):
         self._x('DELETE FROM blocks WHERE id > ?', (offset,))
+        self._address_index_rollback()
         self._rebuild_utxo_index()
 
     async def remove_blocks(self, block_no: int):
@@ -388,6 +395,7 @@ class Database:
             if isinstance(tx, Transaction):
                 outputs_to_be_restored.extend([(i.tx_hash, i.index) for i in tx.inputs if i.tx_hash not in hashes])
         self._x('DELETE FROM blocks WHERE id >= ?', (block_no,))
+        self._address_index_rollback()
         await self.add_unspent_outputs(outputs_to_be_restored)
         self._rebuild_utxo_index()
 
@@ -464,20 +472,50 @@ class Database:
         rows = [await self._tx_row(t, block_hash) for t in transactions]
         self.insert_transaction_rows(rows)
 
-    def insert_transaction_rows(self, rows: List[tuple], addr_rows: Optional[List[tuple]] = None):
-        if addr_rows is None:
-            addr_rows = []
-            for r in rows:
-                tx_hash = r[1]
-                addrs = set(_arr(r[3])) | set(_arr(r[4]))
-                addr_rows.extend((a, tx_hash) for a in addrs)
+    def insert_transaction_rows(self, rows: List[tuple]):
+        """Confirmed tx rows. The per-address index (``address_transactions``) is maintained lazily by
+        :meth:`index_addresses` — off the block-apply critical path."""
         try:
             with self.transaction():
                 self.conn.executemany('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, '
                                       'outputs_addresses, outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)', rows)
-                self.conn.executemany('INSERT INTO address_transactions (address, tx_hash) VALUES (?, ?)', addr_rows)
         except sqlite3.IntegrityError as e:
             raise UniqueViolationError(str(e)) from e
+
+    # ---------------------------------------------------------------- lazy address index
+    def _address_index_height(self) -> int:
+        row = self._q1("SELECT height FROM address_index_state WHERE k = 'height'")
+        if row is not None:
+            return int(row[0])
+        # ledgers written before the watermark existed indexed every tx eagerly
+        has_rows = self._q1('SELECT 1 FROM address_transactions LIMIT 1') is not None
+        h = self._tip_id() if has_rows else 0
+        self._x("INSERT OR REPLACE INTO address_index_state (k, height) VALUES ('height', ?)", (h,))
+        return h
+
+    def index_addresses(self) -> int:
+        """Bring ``address_transactions`` up to the tip: one INSERT … SELECT over json_each of the
+        inputs/outputs address columns of every tx in blocks above the watermark (all in SQLite's C
+        code). Returns the number of blocks indexed."""
+        with self.transaction():
+            wm = self._address_index_height()
+            tip = self._tip_id()
+            if tip <= wm:
+                return 0
+            self.conn.execute(
+                'INSERT INTO address_transactions (address, tx_hash) '
+                'SELECT j.value, t.tx_hash FROM transactions t JOIN blocks b ON b.hash = t.block_hash, '
+                'json_each(t.inputs_addresses) j WHERE b.id > ? AND b.id <= ? '
+                'UNION '
+                'SELECT j.value, t.tx_hash FROM transactions t JOIN blocks b ON b.hash = t.block_hash, '
+                'json_each(t.outputs_addresses) j WHERE b.id > ? AND b.id <= ?', (wm, tip, wm, tip))
+            self.conn.execute("UPDATE address_index_state SET height = ? WHERE k = 'height'", (tip,))
+        return tip - wm
+
+    def _address_index_rollback(self):
+        """After blocks were deleted (their address rows cascade away), pull the watermark down."""
+        tip = self._tip_id()
+        self._x("UPDATE address_index_state SET height = MIN(height, ?) WHERE k = 'height'", (tip,))
 
     async def add_block(self, id: int, block_hash: str, block_content: str, address: str, random: int,
                         difficulty: Decimal, reward: Decimal, timestamp: Union[datetime, int]):
@@ -932,6 +970,7 @@ class Database:
 
     async def get_address_transactions(self, address: str, check_pending_txs: bool = False,
                                        check_signatures: bool = False, limit: int = 50, offset: int = 0):
+        self.index_addresses()
         forms = self._forms(address)
         ph = ','.join('?' * len(forms))
         rows = self._q(f'SELECT DISTINCT transactions.tx_hex, blocks.id AS block_no, transactions.rowid AS rid '

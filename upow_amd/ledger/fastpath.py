@@ -228,11 +228,7 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
                 await database.add_transaction(coinbase_transaction, block_hash)
                 rows = [(block_hash, hashes[k], hexes[k], in_json[k], d['out_addr_json'][k], d['out_amount_json'][k],
                          fee_str[k]) for k in range(n)]
-                addr_rows = []
-                for k in range(n):
-                    for a in set(in_strs[in_start[k]:in_start[k + 1]]) | set(out_strs[out_start[k]:out_start[k + 1]]):
-                        addr_rows.append((a, hashes[k]))
-                database.insert_transaction_rows(rows, addr_rows)
+                database.insert_transaction_rows(rows)
                 database.checkpoint('transactions')
                 database.insert_regular_outputs(
                     [(hashes[out_tx[o]], int(out_index[o]), out_strs[o], 0) for o in range(len(out_tx))],

@@ -10,6 +10,8 @@ Run: ``python -m upow_amd.node --host 0.0.0.0 --port 3006`` (uvicorn).
 """
 from __future__ import annotations
 
+import asyncio
+
 import json
 import os
 import random
@@ -64,9 +66,11 @@ BANNED_SENDERS = ['DgQKikeDqS2Fzue23KuA36L4eJSFh649zA9jJ6zwbzUMp']  # main.py:42
 @asynccontextmanager
 async def lifespan(app: FastAPI):
     await startup()
+    indexer = asyncio.create_task(_address_indexer())
     try:
         yield
     finally:
+        indexer.cancel()
         await shutdown_websocket_manager()
         if db is not None and db.path != ':memory:' and os.environ.get('UPOW_SNAPSHOT', '1') != '0':
             try:  # checkpoint the UTXO index so the next start skips the SQL rebuild (ledger/snapshot.py)
@@ -74,6 +78,17 @@ async def lifespan(app: FastAPI):
                 snapshot.save(db)
             except Exception as e:
                 logger.error(f'UTXO snapshot on shutdown failed: {e}')
+
+
+async def _address_indexer(period: float = 30.0):
+    """Keep the lazily built per-address tx index near the tip (queries also catch it up on demand)."""
+    while True:
+        await asyncio.sleep(period)
+        try:
+            if db is not None:
+                db.index_addresses()
+        except Exception as e:
+            logger.error(f'address indexer: {e}')
 
 
 async def startup():
