@@ -341,13 +341,15 @@ class UtxoIndex:
                 dup_of[i] = first[k] + 1
             else:
                 first[k] = i
-        bad = ((tags != want_tag) | (pay['len'] == 0)).astype(np.uint32)
-        n_tx = len(in_start) - 1
+        bad = ((tags != want_tag) | (pay['len'] == 0)).astype(np.int64)
         amt = pay['amount'].astype(np.int64)
-        ins = np.array([amt[in_start[t]:in_start[t + 1]].sum() for t in range(n_tx)], dtype=np.int64)
-        outs = np.array([out_amount[out_start[t]:out_start[t + 1]].astype(np.int64).sum() for t in range(n_tx)],
-                        dtype=np.int64)
-        miss = np.array([bad[in_start[t]:in_start[t + 1]].sum() for t in range(n_tx)], dtype=np.uint32)
+
+        def seg_sum(x, starts):  # per-tx sums over contiguous segments (empty segments -> 0)
+            cs = np.concatenate([[0], np.cumsum(x, dtype=np.int64)])
+            return cs[starts[1:]] - cs[starts[:-1]]
+        ins = seg_sum(amt, in_start)
+        outs = seg_sum(out_amount.astype(np.int64), out_start)
+        miss = seg_sum(bad, in_start).astype(np.uint32)
         return tags, pay, dup_of, ins - outs, miss, int((dup_of > 0).sum())
 
     def set_hash(self, tag: int = 0) -> str:
