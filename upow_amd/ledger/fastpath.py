@@ -210,13 +210,13 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     # ---- rows for the ledger writes
     in_strs, in_json = lib().input_address_strings(np.ascontiguousarray(pay['addr']).tobytes(),
                                                    pay['len'].astype(np.uint8).tobytes(), d['in_start'], 8)
+    L = lib()
     hexes, hashes = d['hex'], d['tx_hash']
-    out_strs = d['out_addr_str']
-    fee_str = [_numeric6(int(f)) for f in fee]
-    raw_keys = d['in_keys']
-    spent = [(raw_keys[40 * k:40 * k + 32].hex(), int(raw_keys[40 * k + 32])) for k in range(n_in)]
+    fee_str = L.fee_strings(np.ascontiguousarray(fee, dtype=np.int64).tobytes())
+    spent = L.outpoint_rows(d['in_keys'])
     out_tx = _i32(d, 'out_tx')
     out_index = np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]
+    out_rows = L.output_rows(hashes, d['out_tx'], d['out_start'], d['out_addr_str'])
     txid = np.frombuffer(d['txid'], dtype=np.uint8).reshape(-1, 32)
 
     async def apply(block_hash, address, random, block_reward, content_time, coinbase_transaction):
@@ -226,13 +226,11 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
                                          block_reward + fees_total, content_time)
                 database.checkpoint('block')
                 await database.add_transaction(coinbase_transaction, block_hash)
-                rows = [(block_hash, hashes[k], hexes[k], in_json[k], d['out_addr_json'][k], d['out_amount_json'][k],
-                         fee_str[k]) for k in range(n)]
+                rows = list(zip([block_hash] * n, hashes, hexes, in_json, d['out_addr_json'], d['out_amount_json'],
+                                fee_str))
                 database.insert_transaction_rows(rows)
                 database.checkpoint('transactions')
-                database.insert_regular_outputs(
-                    [(hashes[out_tx[o]], int(out_index[o]), out_strs[o], 0) for o in range(len(out_tx))],
-                    txid[out_tx], out_index, out_amount, out_addr, out_len)
+                database.insert_regular_outputs(out_rows, txid[out_tx], out_index, out_amount, out_addr, out_len)
                 await database.add_transaction_outputs([coinbase_transaction])
                 database.checkpoint('outputs')
                 await database.remove_pending_transactions_by_hash(list(hashes))
@@ -252,12 +250,6 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         res = await manager._finalize_block(block_no, block_content, fees_total, n, apply, error_list, t0)
     timings.update({'decode_to_checks_s': t1 - t0, 'apply_s': perf_counter() - t4})
     return res
-
-
-def _numeric6(fee_smallest: int) -> str:
-    """``numeric(Decimal(fee) / 10**8, 6)`` for a non-negative fee: round half up to 6 decimals."""
-    q = (fee_smallest + 50) // 100
-    return f'{q // 1000000}.{q % 1000000:06d}'
 
 
 __all__ = ['create_block_from_hex', 'decode']
