@@ -68,11 +68,34 @@ def decode(tx_hexes: List[str]) -> Optional[dict]:
 
 
 async def create_block_from_hex(block_content: str, tx_hexes: List[str], error_list: list = None,
-                                last_block: dict = None, coinbase=None) -> bool:
+                                last_block: dict = None, coinbase=None, mirror: bool = True) -> bool:
     """``create_block(block_content, [Transaction.from_hex(h) for h in tx_hexes])``, natively when possible.
 
     With ``coinbase`` (a CoinbaseTransaction) this is the sync variant ``create_block_in_syncing_old``
-    (manager.py:760-835), which trusts the supplied coinbase instead of rebuilding it."""
+    (manager.py:760-835), which trusts the supplied coinbase instead of rebuilding it.
+
+    On a multi-GPU cluster node (parallel/cluster.py) the leader first broadcasts the block to the
+    follower replicas (``mirror``); every rank validates it (signatures sharded across the GPUs) and
+    an all-reduce checks that all replicas reached the same verdict."""
+    from ..parallel import cluster
+    c = cluster.get()
+    if c is not None and c.leader and mirror and not c.replaying:
+        c.send('block', content=block_content, txs=list(tx_hexes),
+               cb=coinbase.hex() if coinbase is not None else None)
+    err = None
+    try:
+        ok = await _create_block_from_hex(block_content, tx_hexes, error_list, last_block, coinbase)
+    except Exception as e:  # every replica must still take part in the agreement below
+        ok, err = False, e
+    if c is not None and not c.replaying:
+        ok = c.agree(ok, 'block')
+    if err is not None and (c is None or c.leader):
+        raise err
+    return ok
+
+
+async def _create_block_from_hex(block_content: str, tx_hexes: List[str], error_list: list = None,
+                                 last_block: dict = None, coinbase=None) -> bool:
     global last_path
     from . import manager
     if error_list is None:

@@ -12,6 +12,8 @@ def main(argv=None):
     ap.add_argument('--db', default=None, help='SQLite ledger path')
     ap.add_argument('--core-url', default=None, help='bootstrap peer (empty string disables)')
     ap.add_argument('--log-level', default='info')
+    ap.add_argument('--cluster', action='store_true',
+                    help='multi-GPU node under torchrun: rank 0 serves the API, other ranks are HBM replicas')
     a = ap.parse_args(argv)
     if a.data:
         os.environ['UPOW_DATA_DIR'] = a.data
@@ -20,7 +22,35 @@ def main(argv=None):
     if a.core_url is not None:
         os.environ['UPOW_CORE_URL'] = a.core_url
     import uvicorn
+    if a.cluster and int(os.environ.get('WORLD_SIZE', '1')) > 1:
+        return _run_cluster(a)
     uvicorn.run('upow_amd.node.main:app', host=a.host, port=a.port, log_level=a.log_level)
+
+
+def _run_cluster(a):
+    """One process per GPU (parallel/cluster.py): rank 0 runs the node, the others replicate it."""
+    import asyncio
+
+    from ..ops.native import lib
+    from ..parallel import cluster
+    from ..parallel.dist import init_from_env, shutdown
+    lib()  # the extension binds to torch's HIP runtime before the process group exists
+    ctx = init_from_env()
+    c = cluster.init(ctx)
+    try:
+        if ctx.rank == 0:
+            import uvicorn
+            from . import main as node_main
+            uvicorn.run(node_main.app, host=a.host, port=a.port, log_level=a.log_level)
+        else:
+            from ..ledger.database import Database
+
+            async def follow():
+                db = await Database.create(path=':memory:')
+                await cluster.follower_main(c, db)
+            asyncio.run(follow())
+    finally:
+        shutdown(ctx)
 
 
 if __name__ == '__main__':

@@ -35,6 +35,7 @@ from ..ledger import manager as mgr
 from ..ledger.database import Database, UniqueViolationError
 from ..ledger.fastpath import create_block_from_hex
 from ..ops.native import lib
+from ..parallel import cluster
 from ..ledger.manager import (Manager, block_to_bytes, calculate_difficulty, clear_pending_transactions, create_block,
                               ledger_lock,
                               create_block_in_syncing_old, get_circulating_supply, get_difficulty,
@@ -71,6 +72,7 @@ async def lifespan(app: FastAPI):
         yield
     finally:
         indexer.cancel()
+        cluster.leader_quit()
         await shutdown_websocket_manager()
         if db is not None and db.path != ':memory:' and os.environ.get('UPOW_SNAPSHOT', '1') != '0':
             try:  # checkpoint the UTXO index so the next start skips the SQL rebuild (ledger/snapshot.py)
@@ -98,6 +100,8 @@ async def startup():
     ip_filter = IPManager()
     path = os.environ.get('UPOW_DATABASE_PATH') or config.data_path('ledger.sqlite3')
     db = await Database.create(path=path)
+    if cluster.get() is not None:  # multi-GPU node: bring the follower replicas to our tip
+        await cluster.leader_replay(db)
     await start_websocket_manager()
 
 
@@ -191,7 +195,7 @@ async def _sync_blockchain(node_url: str = None):
                     local_cache = local_blocks[:n]
                     local_cache.reverse()
                     async with ledger_lock():
-                        await db.remove_blocks(last_common_block + 1)
+                        await cluster.mirror_rollback(db, last_common_block + 1)
                     break
     limit = 1000
     while True:
@@ -219,7 +223,7 @@ async def _sync_blockchain(node_url: str = None):
             if local_cache is not None:
                 logger.info('sync failed, reverting back to previous chain')
                 async with ledger_lock():
-                    await db.delete_blocks(last_common_block)
+                    await cluster.mirror_delete(db, last_common_block)
                 await create_blocks(local_cache)
             return error[0] if error else e
 
@@ -335,6 +339,7 @@ async def verify_and_push_tx(tx: Transaction, request: Request, background_tasks
         if sender in BANNED_SENDERS:
             return JSONResponse(status_code=403, content={'ok': False, 'error': 'Access forbidden temporarily.'})
         if await db.add_pending_transaction(tx):
+            cluster.mirror_tx(tx.hex())
             if 'Sender-Node' in request.headers:
                 NodesManager.update_last_message(request.headers['Sender-Node'])
             background_tasks.add_task(propagate, 'push_tx', {'tx_hex': tx.hex()})
@@ -458,7 +463,7 @@ async def push_block(request: Request, background_tasks: BackgroundTasks, block_
     pending = sorted(await db.get_pending_transactions_limit(hex_only=True))
     if LAST_PENDING_TRANSACTIONS_CLEAN[0] < timestamp() - 600:
         LAST_PENDING_TRANSACTIONS_CLEAN[0] = timestamp()
-        background_tasks.add_task(clear_pending_transactions, pending)
+        background_tasks.add_task(cluster.mirror_gc, pending)
     block_data = {'block_no': block_no, 'block_hash': block_hash, 'transactions_count': len(final_hexes),
                   'timestamp': timestamp(), 'difficulty': difficulty, 'last_block': last_block,
                   'pending_transactions': pending[:10], 'pending_transactions_hashes': [sha256(t) for t in pending],
@@ -496,7 +501,7 @@ async def get_mining_info(request: Request, background_tasks: BackgroundTasks):
     pending = sorted(await db.get_pending_transactions_limit(hex_only=True))
     if LAST_PENDING_TRANSACTIONS_CLEAN[0] < timestamp() - 600:
         LAST_PENDING_TRANSACTIONS_CLEAN[0] = timestamp()
-        background_tasks.add_task(clear_pending_transactions, pending)
+        background_tasks.add_task(cluster.mirror_gc, pending)
     return {'ok': True, 'result': {
         'difficulty': difficulty, 'last_block': last_block, 'pending_transactions': pending[:10],
         'pending_transactions_hashes': [sha256(t) for t in pending],
@@ -609,6 +614,17 @@ async def add_node(request: Request, url: str, background_tasks: BackgroundTasks
 @app.get('/get_nodes')
 async def get_nodes():
     return {'ok': True, 'result': NodesManager.get_recent_nodes()[:100]}
+
+
+@app.get('/cluster_info')
+async def cluster_info():
+    """Multi-GPU node: every replica's height and UTXO-set hash (a collective). Not in the reference."""
+    c = cluster.get()
+    if c is None:
+        return {'ok': True, 'result': {'world': 1, 'replicas': [{'rank': 0, 'height': db._tip_id(),
+                                                                'utxo_hash': db.sql_unspent_outputs_hash()}]}}
+    c.send('status')
+    return {'ok': True, 'result': {'world': c.ctx.world, 'backend': c.ctx.backend, 'replicas': c.status(db)}}
 
 
 @app.get('/metrics')
