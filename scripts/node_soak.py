@@ -1,0 +1,210 @@
+"""Steady-state node + miner soak on one MI355X (BASELINE.json config 5, scaled to one GPU):
+a full node (REST, GPU UTXO set, native block path), the GPU miner CLI pointed at it, and a
+synthetic wallet pushing ~40 tx/s through /push_tx.
+
+    python scripts/node_soak.py [--rate 40] [--seconds 120] [--difficulty 9.5] [--out FILE]
+
+Prints one JSON line: confirmed tx/s, inclusion latency (push -> block) percentiles, block interval,
+node-side block apply latency (from /metrics) and the miner's reported hashrate. Data: synthetic
+(random keys; the miner's own coinbases are fanned out into ~5,000 spendable outputs first).
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import random
+import re
+import socket
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+from decimal import Decimal
+
+import httpx
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--rate', type=float, default=40.0)
+    ap.add_argument('--seconds', type=float, default=120.0)
+    ap.add_argument('--difficulty', default='9.5')
+    ap.add_argument('--out', default=None)
+    a = ap.parse_args()
+
+    from upow_amd.models.transaction import Transaction, TransactionInput, TransactionOutput
+    from upow_amd.ops import p256 as op
+    from upow_amd.ops.native import lib
+    from upow_amd.utils.codec import point_to_string
+    lib()
+    rng = random.Random(7)
+    key = rng.randrange(1, op.oracle.N)
+    pub = op.public_key(key)
+    addr = point_to_string(pub)
+    sinks = [point_to_string(op.public_key(rng.randrange(1, op.oracle.N))) for _ in range(64)]
+
+    data = tempfile.mkdtemp(prefix='soak', dir=os.path.join(ROOT, 'gpurun_out') if os.path.isdir(
+        os.path.join(ROOT, 'gpurun_out')) else None)
+    port = _port()
+    url = f'http://127.0.0.1:{port}'
+    env = dict(os.environ, UPOW_DATA_DIR=data, UPOW_CORE_URL='', UPOW_START_DIFFICULTY=a.difficulty,
+               UPOW_RATE_LIMIT='0', PYTHONPATH=ROOT, UPOW_LOG_LEVEL='WARNING', UPOW_SNAPSHOT='0')
+    node = subprocess.Popen([sys.executable, '-m', 'upow_amd.node', '--host', '127.0.0.1', '--port', str(port),
+                             '--log-level', 'warning'], env=env, cwd=ROOT, stdout=open(os.path.join(data, 'node.log'), 'w'),
+                            stderr=subprocess.STDOUT)
+    client = httpx.Client(timeout=30)
+    for _ in range(600):
+        try:
+            if client.get(url + '/get_nodes').status_code == 200:
+                break
+        except Exception:
+            time.sleep(0.2)
+    miner_log = open(os.path.join(data, 'miner.log'), 'w')
+    from upow_amd.ops.native import gpu_available
+    chunk = [] if gpu_available() else ['--chunk', '65536', '--device', 'cpu']
+    miner = subprocess.Popen([sys.executable, '-m', 'upow_amd.miner', addr, '1', url + '/', '--refresh', '10', *chunk],
+                             env=env, cwd=ROOT, stdout=miner_log, stderr=subprocess.STDOUT)
+    t_start = time.time()
+
+    def height():
+        return client.get(url + '/get_mining_info').json()['result']['last_block'].get('id', 0)
+
+    def wait_height(h, limit=600):
+        t = time.time()
+        while height() < h:
+            if time.time() - t > limit:
+                raise RuntimeError(f'no block {h} within {limit} s')
+            time.sleep(0.25)
+
+    def spendable():
+        r = client.get(url + '/get_address_info', params={'address': addr}).json()['result']
+        return [(o['tx_hash'], o['index'], Decimal(str(o['amount']))) for o in r['spendable_outputs']]
+
+    def push(tx):
+        r = client.post(url + '/push_tx', json={'tx_hex': tx.hex()}).json()
+        if not r.get('ok'):
+            raise RuntimeError(f'push_tx rejected: {r}')
+
+    def make_tx(h, i, amount, outs):
+        inp = TransactionInput(h, i, amount=amount, public_key=pub)
+        tx = Transaction([inp], [TransactionOutput(x, v) for x, v in outs])
+        return tx.sign([key])
+
+    # ---- fund: coinbase -> 25 outputs -> 25 x 200 outputs (5,000 spendable UTXOs)
+    wait_height(2)
+    cb = spendable()[0]
+    push(make_tx(cb[0], cb[1], cb[2], [(addr, Decimal('0.2399'))] * 25))
+    h0 = height()
+    wait_height(h0 + 2)
+    lvl1 = [u for u in spendable() if u[2] == Decimal('0.2399')]
+    for u in lvl1:
+        push(make_tx(u[0], u[1], u[2], [(addr, Decimal('0.00119'))] * 200))
+    h1 = height()
+    wait_height(h1 + 2)
+    pool = [u for u in spendable() if u[2] == Decimal('0.00119')]
+    setup_s = time.time() - t_start
+
+    # ---- steady state: one 1-in/1-out tx per pool UTXO at the target rate
+    pushed = {}
+    included = {}
+    blocks = []
+    stop = threading.Event()
+    h_start = height()
+
+    def watcher():
+        c = httpx.Client(timeout=30)
+        seen = h_start
+        while not stop.is_set():
+            try:
+                h = c.get(url + '/get_mining_info').json()['result']['last_block'].get('id', 0)
+            except Exception:
+                time.sleep(0.2)
+                continue
+            while seen < h:
+                seen += 1
+                b = c.get(url + '/get_block', params={'block': seen}).json()['result']
+                now = time.time()
+                blocks.append((seen, now, len(b['transactions'])))
+                for t in b['transactions']:
+                    th = hashlib.sha256(bytes.fromhex(t)).hexdigest()
+                    if th in pushed and th not in included:
+                        included[th] = now
+            time.sleep(0.2)
+
+    w = threading.Thread(target=watcher, daemon=True)
+    w.start()
+    t0 = time.time()
+    n = 0
+    errors = 0
+    while time.time() - t0 < a.seconds and n < len(pool):
+        target = t0 + n / a.rate
+        if time.time() < target:
+            time.sleep(target - time.time())
+        h, i, amount = pool[n]
+        tx = make_tx(h, i, amount, [(sinks[n % len(sinks)], amount - Decimal('0.00001'))])
+        try:
+            push(tx)
+            pushed[tx.hash()] = time.time()
+        except Exception:
+            errors += 1
+        n += 1
+    t_push_end = time.time()
+    # drain: wait until everything pushed is in a block (or 4 block intervals)
+    deadline = time.time() + 120
+    while len(included) < len(pushed) and time.time() < deadline:
+        time.sleep(0.5)
+    stop.set()
+    w.join(5)
+    metrics = client.get(url + '/metrics').text
+    miner.terminate()
+    node.terminate()
+    for p in (miner, node):
+        try:
+            p.wait(20)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    miner_log.close()
+    lat = sorted(included[h] - pushed[h] for h in included)
+    rates = [float(x) for x in re.findall(r'([0-9.]+) MH/s', open(os.path.join(data, 'miner.log')).read())]
+    apply = {}
+    for ln in metrics.splitlines():
+        m = re.match(r'upow_block_apply_seconds_(sum|count)\{path="(\w+)"\} (\S+)', ln)
+        if m:
+            apply.setdefault(m.group(2), {})[m.group(1)] = float(m.group(3))
+    steady_blocks = [b for b in blocks if b[1] <= t_push_end + 1]
+    intervals = [b2[1] - b1[1] for b1, b2 in zip(blocks, blocks[1:])]
+    q = lambda p: round(lat[min(len(lat) - 1, int(p * len(lat)))], 2) if lat else None
+    out = {
+        'metric': 'node_soak_confirmed_tx_per_s', 'value': round(len(included) / max(1e-9, t_push_end - t0), 2),
+        'unit': 'tx/s', 'target_rate': a.rate, 'pushed': len(pushed), 'push_errors': errors,
+        'confirmed': len(included), 'seconds': round(t_push_end - t0, 1),
+        'inclusion_latency_s': {'p50': q(0.5), 'p90': q(0.9), 'p99': q(0.99), 'max': round(lat[-1], 2) if lat else None},
+        'blocks': len(blocks), 'mean_block_interval_s': round(sum(intervals) / len(intervals), 2) if intervals else None,
+        'txs_per_block_max': max((b[2] for b in blocks), default=0),
+        'block_apply_ms_mean': {k: round(1000 * v['sum'] / v['count'], 2) for k, v in apply.items() if v.get('count')},
+        'miner_mhs_median': sorted(rates)[len(rates) // 2] if rates else None,
+        'difficulty': a.difficulty, 'setup_s': round(setup_s, 1), 'data': 'synthetic keys, miner coinbases fanned out',
+    }
+    line = json.dumps(out)
+    print(line, flush=True)
+    if a.out:
+        with open(a.out, 'w') as f:
+            f.write(line + '\n')
+
+
+if __name__ == '__main__':
+    main()

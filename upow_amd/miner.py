@@ -79,7 +79,10 @@ def main(argv=None):
             hashes = job['pending_transactions_hashes']
             merkle = miner_merkle_root(hashes)
             now = timestamp()
-            ts_min = min(now, last.get('timestamp', now - 60) + 1)
+            ts_min = last.get('timestamp', now - 60) + 1
+            if ts_min > now:  # the previous block is from this very second: a valid header needs a later one
+                time.sleep(ts_min - now)
+                now = timestamp()
             if ctx.is_main:
                 print(f"difficulty: {job['difficulty']}\nblock number: {last.get('id', 0)}\n"
                       f"Confirming {len(hashes)} transactions", flush=True)
