@@ -98,6 +98,51 @@ __device__ __forceinline__ uint32_t pow_h0(const PowJobDev& job, uint32_t v) {
     return job.mid[0] + a;
 }
 
+// Variant 2 (A/B evidence for the design note above): the same v2 search with the expanded message
+// schedule W16..W63 staged in LDS instead of VGPRs. Each lane owns a 16-word ring in LDS laid out
+// [word][lane] (consecutive lanes -> consecutive banks, conflict-free); every produced word is one
+// ds_write_b32 and each of its four consumers one ds_read_b32. `volatile` keeps the compiler from
+// forwarding the stores back into registers, so this really is the LDS-staged form.
+typedef __attribute__((address_space(3))) volatile uint32_t lds_u32;
+
+__device__ __forceinline__ uint32_t pow_h0_lds(const PowJobDev& job, uint32_t v, lds_u32* ring) {
+    const uint32_t tid = threadIdx.x;
+    // words 0..15 are job constants (SGPRs) or the nonce word; only W16..W63 live in LDS
+    auto W = [&](int i) -> uint32_t { return i < 16 ? (i == 10 ? v : job.w[i]) : ring[(i & 15) * 256 + tid]; };
+    uint32_t a = job.st[0], b = job.st[1], c = job.st[2], d = job.st[3];
+    uint32_t e = job.st[4], f = job.st[5], g = job.st[6], h = job.st[7];
+#pragma unroll
+    for (int i = 10; i < 64; ++i) {
+        uint32_t wi;
+        if (i < 16) {
+            wi = W(i);
+        } else {
+            wi = W(i - 16) + SSIG0(W(i - 15)) + W(i - 7) + SSIG1(W(i - 2));
+            ring[(i & 15) * 256 + tid] = wi;
+        }
+        uint32_t t1 = h + BSIG1(e) + CH(e, f, g) + dK[i] + wi;
+        uint32_t t2 = BSIG0(a) + MAJ(a, b, c);
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    return job.mid[0] + a;
+}
+
+__global__ __launch_bounds__(256, 1) void pow_search_lds_kernel(PowJobDev job, uint32_t v_base, uint32_t iters,
+                                                                uint32_t* __restrict__ out_count,
+                                                                uint32_t* __restrict__ out_words, uint32_t cap) {
+    __shared__ uint32_t ring[16 * 256];
+    const uint32_t nthreads = gridDim.x * blockDim.x;
+    uint32_t v = v_base + blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t it = 0; it < iters; ++it, v += nthreads) {
+        const uint32_t h0 = pow_h0_lds(job, v, (lds_u32*)ring);
+        const bool hit = ((h0 ^ job.tword) & job.tmask) == 0 && ((h0 >> job.frac_shift) & 0xfu) < job.frac_limit;
+        if (__builtin_expect(hit, 0)) {
+            const uint32_t slot = atomicAdd(out_count, 1u);
+            if (slot < cap) out_words[slot] = v;
+        }
+    }
+}
+
 template <int LAYOUT, int MIN_WAVES_PER_SIMD>
 __global__ __launch_bounds__(256, MIN_WAVES_PER_SIMD) void pow_search_kernel(PowJobDev job, uint32_t v_base, uint32_t iters,
                                                          uint32_t* __restrict__ out_count,
@@ -182,8 +227,9 @@ static int pow_resident_blocks(bool v2, int variant) {
     int dev = 0, cus = 0, per_cu = 0;
     hip_check(hipGetDevice(&dev), "hipGetDevice");
     hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "attr");
-    const void* fn = v2 ? (variant == 1 ? reinterpret_cast<const void*>(&pow_search_kernel<2, 8>)
-                                        : reinterpret_cast<const void*>(&pow_search_kernel<2, 1>))
+    const void* fn = v2 ? (variant == 1   ? reinterpret_cast<const void*>(&pow_search_kernel<2, 8>)
+                           : variant == 2 ? reinterpret_cast<const void*>(&pow_search_lds_kernel)
+                                          : reinterpret_cast<const void*>(&pow_search_kernel<2, 1>))
                         : reinterpret_cast<const void*>(&pow_search_kernel<1, 1>);
     hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0), "occupancy");
     hipFuncAttributes attr{};
@@ -235,7 +281,10 @@ PowResult pow_search_gpu(const PowJobHost& hj, uint64_t start, uint64_t count, i
             }
         }
         const uint32_t vb = uint32_t(start + done);
-        if (v2 && variant == 1)
+        if (v2 && variant == 2)
+            hipLaunchKernelGGL(pow_search_lds_kernel, dim3(gb), dim3(block), 0, 0, job, vb, iters, buf.d_count,
+                               buf.d_words, cap);
+        else if (v2 && variant == 1)
             hipLaunchKernelGGL((pow_search_kernel<2, 8>), dim3(gb), dim3(block), 0, 0, job, vb, iters,
                                buf.d_count, buf.d_words, cap);
         else if (v2)
