@@ -28,6 +28,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "thread_pool.h"
 #include "native.h"
 #include "sha256_common.h"
 
@@ -57,6 +58,7 @@ struct DecTx {
     uint8_t flag = TX_MALFORMED;
     uint8_t version = 0;
     bool canonical = false;
+    bool upper_hex = false;  // the input used A-F digits (the stored hex must be re-rendered)
     int32_t msg_off = -1, msg_len = 0;  // into canon bytes
     int32_t signed_len = 0;             // hex(False) byte length (a prefix of canon)
     std::vector<DecIn> ins;
@@ -77,6 +79,29 @@ static inline int hexval(char c) {
 }
 
 static const char kHex[] = "0123456789abcdef";
+
+// CPython objects for the (all-ASCII) strings the codec produces: PyUnicode_New(len, 127) + memcpy
+// is the cheapest constructor, and a PyList_New list is filled with PyList_SET_ITEM (steals the ref).
+static PyObject* ascii_str(const char* p, size_t n) {
+    PyObject* o = PyUnicode_New(Py_ssize_t(n), 127);
+    if (!o) throw py::error_already_set();
+    std::memcpy(PyUnicode_DATA(o), p, n);
+    return o;
+}
+
+static py::list new_list(size_t n) {
+    PyObject* l = PyList_New(Py_ssize_t(n));
+    if (!l) throw py::error_already_set();
+    return py::reinterpret_steal<py::list>(l);
+}
+
+static void hex32(const uint8_t* b, char* out) {
+    static const char hx[] = "0123456789abcdef";
+    for (int i = 0; i < 32; ++i) {
+        out[2 * i] = hx[b[i] >> 4];
+        out[2 * i + 1] = hx[b[i] & 15];
+    }
+}
 
 static std::string to_hex(const uint8_t* p, size_t n) {
     std::string s(2 * n, '0');
@@ -125,6 +150,7 @@ static void decode_one(const char* hx, size_t hlen, DecTx& t) {
     for (size_t i = 0; i < b.size(); ++i) {
         const int hi = hexval(hx[2 * i]), lo = hexval(hx[2 * i + 1]);
         if (hi < 0 || lo < 0) return;  // whitespace etc.: bytes.fromhex semantics are the parser's business
+        t.upper_hex |= (hx[2 * i] >= 'A' && hx[2 * i] <= 'F') | (hx[2 * i + 1] >= 'A' && hx[2 * i + 1] <= 'F');
         b[i] = uint8_t(hi << 4 | lo);
     }
     const size_t n = b.size();
@@ -294,17 +320,7 @@ static void decode_one(const char* hx, size_t hlen, DecTx& t) {
 
 template <typename F>
 static void parallel_for(int64_t n, int threads, F&& f) {
-    threads = int(std::max<int64_t>(1, std::min<int64_t>(threads, n)));
-    if (threads == 1) {
-        for (int64_t i = 0; i < n; ++i) f(i);
-        return;
-    }
-    std::vector<std::thread> pool;
-    for (int t = 0; t < threads; ++t)
-        pool.emplace_back([&, t] {
-            for (int64_t i = t; i < n; i += threads) f(i);
-        });
-    for (auto& th : pool) th.join();
+    HostPool::get().parallel_for(n, threads, std::forward<F>(f));
 }
 
 // merkle root: SHA-256 over the txids of the txs sorted by their canonical bytes (manager.py:365-378)
@@ -331,14 +347,25 @@ static py::bytes as_bytes(const std::vector<uint8_t>& v) {
 static py::dict decode_block_txs(py::list hexes, int threads) {
     const int64_t n = int64_t(hexes.size());
     const size_t N = static_cast<size_t>(n);
-    std::vector<std::string> src(N);
-    for (int64_t i = 0; i < n; ++i) src[size_t(i)] = hexes[size_t(i)].cast<std::string>();
+    // zero-copy views of the input hex strings (compact ASCII str objects expose their buffer; the
+    // list keeps them alive for the whole call)
+    std::vector<const char*> srcp(N);
+    std::vector<size_t> srcl(N);
+    for (size_t i = 0; i < N; ++i) {
+        PyObject* o = PyList_GET_ITEM(hexes.ptr(), Py_ssize_t(i));
+        if (!PyUnicode_Check(o)) throw py::type_error("transaction hex must be str");
+        Py_ssize_t sz = 0;
+        const char* p = PyUnicode_AsUTF8AndSize(o, &sz);
+        if (!p) throw py::error_already_set();
+        srcp[i] = p;
+        srcl[i] = size_t(sz);
+    }
     std::vector<DecTx> txs(N);
     const bool prof = std::getenv("UPOW_TXCODEC_PROFILE") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
     {
         py::gil_scoped_release rel;
-        parallel_for(n, threads, [&](int64_t i) { decode_one(src[size_t(i)].data(), src[size_t(i)].size(), txs[size_t(i)]); });
+        parallel_for(n, threads, [&](int64_t i) { decode_one(srcp[size_t(i)], srcl[size_t(i)], txs[size_t(i)]); });
     }
     auto t1 = std::chrono::steady_clock::now();
     py::dict d;
@@ -387,7 +414,8 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
         out_addr(NO * 64, 0), out_len(NO), out_type(NO);
     std::vector<int32_t> in_sig(NI), in_tx(NI), out_tx(NO);
     std::vector<uint64_t> out_amount(NO);
-    py::list canon_hex(N), tx_hash(N), out_addr_str(NO), out_addr_json(N), out_amount_json(N);
+    py::list canon_hex = new_list(N), tx_hash = new_list(N), out_addr_str = new_list(NO), out_addr_json = new_list(N),
+             out_amount_json = new_list(N);
     for (int64_t i = 0; i < n; ++i) {
         const DecTx& t = txs[size_t(i)];
         std::memcpy(&txid[32 * size_t(i)], t.txid, 32);
@@ -411,16 +439,23 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
             out_type[o] = t.outs[j].type;
             out_amount[o] = t.outs[j].amount;
             out_tx[o] = int32_t(i);
-            out_addr_str[o] = py::str(t.out_addr[j]);
+            PyList_SET_ITEM(out_addr_str.ptr(), Py_ssize_t(o), ascii_str(t.out_addr[j].data(), t.out_addr[j].size()));
         }
-        canon_hex[size_t(i)] = t.canonical && src[size_t(i)].size() == 2 * t.canon.size() &&
-                                       std::all_of(src[size_t(i)].begin(), src[size_t(i)].end(),
-                                                   [](char ch) { return !(ch >= 'A' && ch <= 'F'); })
-                                   ? py::object(hexes[size_t(i)])
-                                   : py::object(py::str(to_hex(t.canon.data(), t.canon.size())));
-        tx_hash[size_t(i)] = py::str(to_hex(t.txid, 32));
-        out_addr_json[size_t(i)] = py::str(t.out_addr_json);
-        out_amount_json[size_t(i)] = py::str(t.out_amount_json);
+        // the input string is reused when it already is the canonical lowercase hex of the tx
+        if (t.canonical && !t.upper_hex && srcl[size_t(i)] == 2 * t.canon.size()) {
+            PyObject* o = PyList_GET_ITEM(hexes.ptr(), Py_ssize_t(i));
+            Py_INCREF(o);
+            PyList_SET_ITEM(canon_hex.ptr(), Py_ssize_t(i), o);
+        } else {
+            const std::string h = to_hex(t.canon.data(), t.canon.size());
+            PyList_SET_ITEM(canon_hex.ptr(), Py_ssize_t(i), ascii_str(h.data(), h.size()));
+        }
+        char hx[64];
+        hex32(t.txid, hx);
+        PyList_SET_ITEM(tx_hash.ptr(), Py_ssize_t(i), ascii_str(hx, 64));
+        PyList_SET_ITEM(out_addr_json.ptr(), Py_ssize_t(i), ascii_str(t.out_addr_json.data(), t.out_addr_json.size()));
+        PyList_SET_ITEM(out_amount_json.ptr(), Py_ssize_t(i),
+                        ascii_str(t.out_amount_json.data(), t.out_amount_json.size()));
     }
     d["in_keys"] = as_bytes(in_keys);
     d["in_type"] = as_bytes(in_type);
@@ -481,8 +516,8 @@ static py::tuple input_address_strings(py::bytes addrs64, py::bytes lens, py::by
     }
     for (size_t i = 0; i < n_in; ++i)
         if (bad[i]) throw std::invalid_argument("input address payload missing");
-    py::list strs(n_in), json(n_tx);
-    for (size_t i = 0; i < n_in; ++i) strs[i] = py::str(out[i]);
+    py::list strs = new_list(n_in), json = new_list(n_tx);
+    for (size_t i = 0; i < n_in; ++i) PyList_SET_ITEM(strs.ptr(), Py_ssize_t(i), ascii_str(out[i].data(), out[i].size()));
     for (size_t t = 0; t < n_tx; ++t) {
         std::string j = "[";
         for (int32_t k = st[t]; k < st[t + 1]; ++k) {
@@ -492,7 +527,7 @@ static py::tuple input_address_strings(py::bytes addrs64, py::bytes lens, py::by
             j += '"';
         }
         j += ']';
-        json[t] = py::str(j);
+        PyList_SET_ITEM(json.ptr(), Py_ssize_t(t), ascii_str(j.data(), j.size()));
     }
     return py::make_tuple(strs, json);
 }
@@ -546,10 +581,56 @@ static py::list fee_strings(py::bytes fee_b) {
     return out;
 }
 
+// Distinct rows of an (n x width) byte matrix: (unique rows in first-seen order, inverse int32[n]).
+// Replaces np.unique over a void dtype (a full sort of opaque records) for the per-block public-key
+// set: open addressing keyed by the row's leading bytes after the prefix (P-256 x coordinates are
+// uniformly distributed, so they are a good hash as they are).
+static py::tuple unique_rows(py::buffer buf, int width) {
+    py::buffer_info bi = buf.request();
+    const size_t total = size_t(bi.size) * size_t(bi.itemsize);
+    if (width <= 0 || total % size_t(width)) throw std::invalid_argument("buffer is not n x width bytes");
+    const size_t n = total / size_t(width);
+    const uint8_t* d = static_cast<const uint8_t*>(bi.ptr);
+    size_t cap = 16;
+    while (cap < 2 * n) cap <<= 1;
+    std::vector<int32_t> slot(cap, -1);
+    std::vector<int32_t> inv(n), first;
+    first.reserve(n);
+    {
+        py::gil_scoped_release nogil;
+        for (size_t i = 0; i < n; ++i) {
+            const uint8_t* r = d + i * size_t(width);
+            uint64_t h = 1469598103934665603ull;
+            for (int k = 0; k < width; ++k) h = (h ^ r[k]) * 1099511628211ull;
+            size_t s = size_t(h) & (cap - 1);
+            for (;;) {
+                const int32_t u = slot[s];
+                if (u < 0) {
+                    slot[s] = int32_t(first.size());
+                    inv[i] = int32_t(first.size());
+                    first.push_back(int32_t(i));
+                    break;
+                }
+                if (std::memcmp(d + size_t(first[size_t(u)]) * size_t(width), r, size_t(width)) == 0) {
+                    inv[i] = u;
+                    break;
+                }
+                s = (s + 1) & (cap - 1);
+            }
+        }
+    }
+    std::string uniq(first.size() * size_t(width), '\0');
+    for (size_t u = 0; u < first.size(); ++u)
+        std::memcpy(&uniq[u * size_t(width)], d + size_t(first[u]) * size_t(width), size_t(width));
+    return py::make_tuple(py::bytes(uniq), py::bytes(reinterpret_cast<const char*>(inv.data()), inv.size() * 4));
+}
+
 void register_txcodec(py::module_& m) {
     m.def("outpoint_rows", &outpoint_rows);
     m.def("output_rows", &output_rows);
     m.def("fee_strings", &fee_strings);
+    m.def("unique_rows", &unique_rows, py::arg("buf"), py::arg("width"),
+          "(unique rows in first-seen order, inverse int32) of an n x width byte matrix");
     m.def("decode_block_txs", &decode_block_txs, py::arg("hexes"), py::arg("threads") = 8,
           "Decode, canonicalise and hash a block's transactions (see csrc/txcodec.cpp)");
     m.def("input_address_strings", &input_address_strings, py::arg("addrs64"), py::arg("lens"), py::arg("in_start"),

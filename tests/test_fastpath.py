@@ -89,13 +89,16 @@ def _signed(inputs, outputs, keys, message=None):
     return tx.sign(keys)
 
 
+@pytest.mark.parametrize('native_sql', [True, False], ids=['native-writer', 'executemany'])
 @pytest.mark.parametrize('backend', ['host', pytest.param('gpu', marks=pytest.mark.gpu)])
-def test_fast_path_matches_object_path(backend, request):
+def test_fast_path_matches_object_path(backend, native_sql, request):
     if backend == 'gpu':
         request.getfixturevalue('gpu')
 
     async def go():
         p, base = await _setup(backend)
+        assert p.b.native_sql  # csrc/ledger_sql.cpp drives the ledger's own connection
+        p.b.native_sql = native_sql
         ts = base + 60 * 10
         p.use(p.a)
         txs = []

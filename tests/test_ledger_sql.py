@@ -1,0 +1,73 @@
+"""Native bulk ledger writer (csrc/ledger_sql.cpp) — column binding, error mapping, transaction
+membership, and equality with the ``sqlite3.executemany`` fallback through the native block path."""
+import os
+import sqlite3
+
+import numpy as np
+import pytest
+
+from upow_amd.ledger.database import Database
+from upow_amd.ops.native import lib
+
+
+def test_probe_enabled_for_memory_and_file(tmp_path):
+    mem = Database(':memory:', utxo_backend='host')
+    assert mem.native_sql
+    f = Database(str(tmp_path / 'ledger.sqlite3'), utxo_backend='host')
+    assert f.native_sql
+    fn, _, autocommit = lib().sql_probe(f.conn)
+    assert os.path.realpath(fn) == os.path.realpath(str(tmp_path / 'ledger.sqlite3')) and autocommit == 1
+    mem.close()
+    f.close()
+
+
+def test_probe_respects_env(monkeypatch):
+    monkeypatch.setenv('UPOW_NATIVE_SQL', '0')
+    assert not Database(':memory:', utxo_backend='host').native_sql
+
+
+def test_column_kinds_and_order():
+    L = lib()
+    c = sqlite3.connect(':memory:', isolation_level=None)
+    c.execute('CREATE TABLE t (h TEXT UNIQUE, i INTEGER, g TEXT, k TEXT, z INTEGER, nul TEXT)')
+    raw = np.frombuffer(bytes(range(256)) * 2, dtype=np.uint8)[:40 * 4].copy()
+    words = ['w0', None, 'w2']
+    n = L.sql_executemany(c, 'INSERT INTO t VALUES (?, ?, ?, ?, ?, ?)',
+                          [('hex32', raw, 40, 0), np.array([7, 8, 9, 10], np.int64),
+                           ('gather', words, np.array([2, 0, 1, 2], np.int32)), 'const', 5, None], 4)
+    assert n == 4 and c.total_changes == 4
+    rows = c.execute('SELECT * FROM t ORDER BY rowid').fetchall()
+    assert rows[0] == (bytes(raw[:32]).hex(), 7, 'w2', 'const', 5, None)
+    assert rows[1][2] == 'w0' and rows[2][2] is None and rows[3][0] == bytes(raw[120:152]).hex()
+    # explicit row order: the last row first
+    c.execute('CREATE TABLE o (x INTEGER)')
+    L.sql_executemany(c, 'INSERT INTO o VALUES (?)', [np.array([10, 20, 30], np.int64)], 3,
+                      np.array([2, 0, 1], np.int64))
+    assert [r[0] for r in c.execute('SELECT x FROM o ORDER BY rowid')] == [30, 10, 20]
+    # deletes report their row changes; a missing key changes nothing
+    d = L.sql_executemany(c, 'DELETE FROM o WHERE x = ?', [np.array([10, 99, 30], np.int64)], 3)
+    assert d == 2
+    # UNIQUE violations surface as sqlite3.IntegrityError (callers map it to UniqueViolationError)
+    with pytest.raises(sqlite3.IntegrityError):
+        L.sql_executemany(c, 'INSERT INTO t (h) VALUES (?)', [('hex32', raw, 40, 0)], 1)
+    with pytest.raises(sqlite3.OperationalError):
+        L.sql_executemany(c, 'INSERT INTO missing VALUES (?)', [1], 1)
+    with pytest.raises(ValueError):
+        L.sql_executemany(c, 'INSERT INTO o VALUES (?)', [np.array([1], np.int64)], 2)
+    with pytest.raises(IndexError):
+        L.sql_executemany(c, 'INSERT INTO t (g) VALUES (?)', [('gather', words, np.array([3], np.int32))], 1)
+
+
+def test_native_writes_join_the_open_transaction():
+    db = Database(':memory:', utxo_backend='host')
+    assert db.native_sql
+    db.conn.execute('CREATE TABLE x (v INTEGER)')
+    with pytest.raises(RuntimeError):
+        with db.transaction():
+            db.bulk('INSERT INTO x VALUES (?)', [np.arange(5, dtype=np.int64)], 5)
+            assert db._q1('SELECT COUNT(*) FROM x')[0] == 5
+            raise RuntimeError('roll back')
+    assert db._q1('SELECT COUNT(*) FROM x')[0] == 0  # rolled back with the Python-side BEGIN
+    with db.transaction():
+        db.bulk('INSERT INTO x VALUES (?)', [np.arange(3, dtype=np.int64)], 3)
+    assert db._q1('SELECT COUNT(*) FROM x')[0] == 3

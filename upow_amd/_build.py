@@ -75,7 +75,7 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> Path:
         if verbose:
             print(f'[upow_amd._build] up to date: {TARGET.name}')
         return TARGET
-    cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', str(TARGET), *map(str, objs)]
+    cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', str(TARGET), *map(str, objs), '-ldl']
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f'link failed: {" ".join(cmd)}\n{r.stdout}\n{r.stderr}')

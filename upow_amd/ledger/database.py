@@ -185,6 +185,7 @@ class Database:
                 self.utxo_source = 'snapshot'
         if self.utxo_source == 'sql':
             self._rebuild_utxo_index()
+        self.native_sql = self._probe_native_sql()
 
     # ------------------------------------------------------------------ lifecycle
     @staticmethod
@@ -228,6 +229,39 @@ class Database:
     def _xm(self, sql: str, rows: Iterable):
         with self.lock:
             self.conn.executemany(sql, rows)
+
+    # ------------------------------------------------------------------ native bulk writes
+    def _probe_native_sql(self) -> bool:
+        """Can csrc/ledger_sql.cpp drive THIS connection's sqlite3 handle? Proven by a round trip on a
+        TEMP table: rows the native side inserts must be visible to (and counted by) the Python
+        connection. ``UPOW_NATIVE_SQL=0`` keeps every write on ``sqlite3.executemany``."""
+        if os.environ.get('UPOW_NATIVE_SQL', '1') == '0':
+            return False
+        try:
+            from ..ops.native import lib
+            L = lib()
+            with self.lock:
+                c = self.conn
+                c.execute('CREATE TEMP TABLE IF NOT EXISTS _native_probe (x INTEGER)')
+                c.execute('DELETE FROM _native_probe')
+                c.executemany('INSERT INTO _native_probe VALUES (?)', [(1,), (2,), (3,)])
+                fn, changes, _ = L.sql_probe(c)
+                want = '' if self.path == ':memory:' else os.path.realpath(self.path)
+                same = (fn == want or (fn and os.path.realpath(fn) == want)) and changes == c.total_changes
+                if same:
+                    n = L.sql_executemany(c, 'INSERT INTO _native_probe VALUES (?)', [np.array([4, 5], np.int64)], 2)
+                    same = n == 2 and c.execute('SELECT SUM(x) FROM _native_probe').fetchone()[0] == 15
+                c.execute('DROP TABLE _native_probe')
+            return bool(same)
+        except Exception as e:  # pragma: no cover - depends on the interpreter build
+            logger.warning(f'native ledger writer disabled: {e}')
+            return False
+
+    def bulk(self, sql: str, cols: list, n: int, order=None) -> int:
+        """Column-major executemany (see csrc/ledger_sql.cpp); returns the summed row changes."""
+        from ..ops.native import lib
+        with self.lock:
+            return lib().sql_executemany(self.conn, sql, cols, n, order)
 
     class _Tx:
         """Re-entrant SQL transaction: only the outermost level issues BEGIN/COMMIT/ROLLBACK, so a
@@ -353,7 +387,11 @@ class Database:
 
     async def remove_pending_transactions_by_hash(self, tx_hashes: List[str]):
         with self.lock:
-            self.conn.executemany('DELETE FROM pending_transactions WHERE tx_hash = ?', [(h,) for h in tx_hashes])
+            # only the hashes present in the (small) mempool: no index probe per confirmed tx
+            pending = {r[0] for r in self.conn.execute('SELECT tx_hash FROM pending_transactions')}
+            hit = [(h,) for h in tx_hashes if h in pending] if pending else []
+            if hit:
+                self.conn.executemany('DELETE FROM pending_transactions WHERE tx_hash = ?', hit)
 
     async def remove_pending_transactions(self):
         with self.transaction():
@@ -479,6 +517,21 @@ class Database:
             with self.transaction():
                 self.conn.executemany('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, '
                                       'outputs_addresses, outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)', rows)
+        except sqlite3.IntegrityError as e:
+            raise UniqueViolationError(str(e)) from e
+
+    def insert_transaction_columns(self, block_hash: str, hashes: list, hexes: list, inputs_addresses: list,
+                                   outputs_addresses: list, outputs_amounts: list, fees: list):
+        """``insert_transaction_rows`` from per-column lists (native block path)."""
+        n = len(hashes)
+        if not self.native_sql:
+            return self.insert_transaction_rows(list(zip([block_hash] * n, hashes, hexes, inputs_addresses,
+                                                          outputs_addresses, outputs_amounts, fees)))
+        try:
+            with self.transaction():
+                self.bulk('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, '
+                          'outputs_addresses, outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)',
+                          [block_hash, hashes, hexes, inputs_addresses, outputs_addresses, outputs_amounts, fees], n)
         except sqlite3.IntegrityError as e:
             raise UniqueViolationError(str(e)) from e
 
@@ -704,19 +757,26 @@ class Database:
             payload = await self._payload_from_ledger([(r[0], r[1]) for r in rows])
         self.utxo.insert([(r[0], r[1]) for r in rows], TAG_BY_TABLE['unspent_outputs'], payload)
 
-    def insert_regular_outputs(self, rows: List[tuple], txids: np.ndarray, indexes: np.ndarray, amounts: np.ndarray,
-                               addrs: np.ndarray, lens: np.ndarray) -> None:
-        """Native block path: REGULAR outputs as (tx_hash, index, address, is_stake) rows + one index
-        insert with their payloads (amount, normalised address bytes) — ``add_unspent_outputs`` in bulk."""
-        if not rows:
+    def insert_regular_outputs(self, tx_hashes: list, out_tx: np.ndarray, indexes: np.ndarray, out_addr_str: list,
+                               txids: np.ndarray, amounts: np.ndarray, addrs: np.ndarray, lens: np.ndarray) -> None:
+        """Native block path: REGULAR outputs as (tx_hash, index, address, is_stake=0) rows + one index
+        insert with their payloads (amount, normalised address bytes) — ``add_unspent_outputs`` in bulk.
+        Output ``o`` belongs to tx ``out_tx[o]`` (its hash ``tx_hashes[out_tx[o]]``, digest ``txids[o]``)."""
+        n = len(out_tx)
+        if not n:
             return
-        with self.lock:
-            self.conn.executemany('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) '
-                                  'VALUES (?, ?, ?, ?)', rows)
-        n = len(rows)
+        out_tx = np.ascontiguousarray(out_tx, dtype=np.int32)
+        indexes = np.ascontiguousarray(indexes, dtype=np.int64)
+        sql = 'INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) VALUES (?, ?, ?, ?)'
+        if self.native_sql:
+            self.bulk(sql, [('gather', list(tx_hashes), out_tx), indexes, list(out_addr_str), 0], n)
+        else:
+            with self.lock:
+                self.conn.executemany(sql, [(tx_hashes[t], int(i), a, 0)
+                                            for t, i, a in zip(out_tx.tolist(), indexes.tolist(), out_addr_str)])
         recs = np.zeros((n, 40), dtype=np.uint8)
         recs[:, :32] = txids
-        recs[:, 32:36] = np.asarray(indexes, dtype=np.uint32).reshape(n, 1).view(np.uint8)
+        recs[:, 32:36] = indexes.astype(np.uint32).reshape(n, 1).view(np.uint8)
         recs[:, 36:40] = np.full((n, 1), TAG_BY_TABLE['unspent_outputs'], dtype=np.uint32).view(np.uint8)
         pay = np.zeros(n, dtype=PAYLOAD_DTYPE)
         pay['amount'] = amounts
@@ -727,19 +787,46 @@ class Database:
         pay['addr'] = a
         self.utxo.insert_records(recs, pay)
 
-    def remove_spent_regular(self, inputs: List[Tuple[str, int]], in_keys: np.ndarray) -> bool:
-        """Native block path: ``remove_unspent_outputs`` for REGULAR spends (same partial-delete semantics)."""
-        if not inputs:
+    @staticmethod
+    def _key_order(in_keys: np.ndarray) -> np.ndarray:
+        """Row order sorted by the leading 8 bytes of the tx hash: B-tree locality for bulk deletes
+        (the set of deleted rows, and so the result, does not depend on the order)."""
+        return np.argsort(in_keys[:, :8].copy().view('>u8').ravel(), kind='stable').astype(np.int64)
+
+    def remove_spent_regular(self, in_keys: np.ndarray) -> bool:
+        """Native block path: ``remove_unspent_outputs`` for REGULAR spends (same partial-delete semantics).
+        ``in_keys``: n x 40 outpoint records (txid 32 B, index u32, tag u32)."""
+        n_in = len(in_keys)
+        if not n_in:
             return True
+        in_keys = np.ascontiguousarray(in_keys, dtype=np.uint8)
+        idx = in_keys[:, 32:36].copy().view(np.uint32).ravel().astype(np.int64)
+        sql = 'DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?'
         with self.transaction():
-            n = self.conn.executemany('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?', inputs).rowcount
+            if self.native_sql:
+                n = self.bulk(sql, [('hex32', in_keys, 40, 0), idx], n_in, self._key_order(in_keys))
+            else:
+                n = self.conn.executemany(sql, [(bytes(k[:32]).hex(), int(i)) for k, i in zip(in_keys, idx)]).rowcount
         recs = np.array(in_keys, dtype=np.uint8, copy=True)
-        recs[:, 36:40] = np.full((len(recs), 1), TAG_BY_TABLE['unspent_outputs'], dtype=np.uint32).view(np.uint8)
+        recs[:, 36:40] = np.full((n_in, 1), TAG_BY_TABLE['unspent_outputs'], dtype=np.uint32).view(np.uint8)
         self.utxo.erase_records(recs)
-        if n != len(inputs):
-            logger.error(f'Failed to delete all UTXOs: {n} of {len(inputs)} deleted')
+        if n != n_in:
+            logger.error(f'Failed to delete all UTXOs: {n} of {n_in} deleted')
             return False
         return True
+
+    def remove_pending_spent_keys(self, in_keys: np.ndarray) -> int:
+        """``DELETE FROM pending_spent_outputs`` for every spent outpoint of a block, restricted to the
+        outpoints that are actually in the (small) pending table instead of one index probe per input."""
+        with self.lock:
+            pending = self.conn.execute('SELECT tx_hash, "index" FROM pending_spent_outputs').fetchall()
+        if not pending or not len(in_keys):
+            return 0
+        have = {(r[0], r[1]) for r in pending}
+        keys = np.ascontiguousarray(in_keys, dtype=np.uint8)
+        idx = keys[:, 32:36].copy().view(np.uint32).ravel().tolist()
+        hit = [(h, i) for h, i in zip((bytes(k[:32]).hex() for k in keys), idx) if (h, i) in have]
+        return self._delete_outpoints('pending_spent_outputs', hit) if hit else 0
 
     async def _add_gov_outputs(self, table: str, outputs: List[tuple]):
         if not outputs:

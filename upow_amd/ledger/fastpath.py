@@ -178,9 +178,10 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     c33 = np.nonzero(all_len == 33)[0]
     if len(c33):
         comp = np.ascontiguousarray(all_addr[c33, :33])
-        uniq, inv = np.unique(comp.view(np.dtype((np.void, 33))).ravel(), return_inverse=True)
-        ubuf = np.ascontiguousarray(uniq).view(np.uint8)
-        dev = 'gpu' if (gpu_available() and len(uniq) >= op.GPU_MIN_BATCH) else 'cpu'
+        ubytes, inv_b = lib().unique_rows(comp, 33)
+        inv = np.frombuffer(inv_b, dtype=np.int32)
+        ubuf = np.frombuffer(ubytes, dtype=np.uint8)
+        dev = 'gpu' if (gpu_available() and len(ubuf) // 33 >= op.GPU_MIN_BATCH) else 'cpu'
         out, okb = lib().p256_decompress(ubuf, dev == 'gpu')
         upts = np.frombuffer(out, dtype=np.uint8).reshape(-1, 64)
         uok = np.frombuffer(okb, dtype=np.uint8).astype(bool)
@@ -230,41 +231,46 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     manager.last_block_timings.update({'utxo_s': t2 - t1, 'verify_s': t4 - t2, 'merkle_s': 0.0,
                                        'total_s': t4 - t0, 'txs': n})
 
-    # ---- rows for the ledger writes
+    # ---- columns for the ledger writes (bound natively by csrc/ledger_sql.cpp when available)
     in_strs, in_json = lib().input_address_strings(np.ascontiguousarray(pay['addr']).tobytes(),
                                                    pay['len'].astype(np.uint8).tobytes(), d['in_start'], 8)
     L = lib()
     hexes, hashes = d['hex'], d['tx_hash']
     fee_str = L.fee_strings(np.ascontiguousarray(fee, dtype=np.int64).tobytes())
-    spent = L.outpoint_rows(d['in_keys'])
     out_tx = _i32(d, 'out_tx')
     out_index = np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]
-    out_rows = L.output_rows(hashes, d['out_tx'], d['out_start'], d['out_addr_str'])
     txid = np.frombuffer(d['txid'], dtype=np.uint8).reshape(-1, 32)
 
     async def apply(block_hash, address, random, block_reward, content_time, coinbase_transaction):
+        ta = perf_counter()
         try:
             with database.transaction(foreign_keys=False):
                 await database.add_block(block_no, block_hash, block_content, address, random, difficulty,
                                          block_reward + fees_total, content_time)
                 database.checkpoint('block')
                 await database.add_transaction(coinbase_transaction, block_hash)
-                rows = list(zip([block_hash] * n, hashes, hexes, in_json, d['out_addr_json'], d['out_amount_json'],
-                                fee_str))
-                database.insert_transaction_rows(rows)
+                database.insert_transaction_columns(block_hash, hashes, hexes, in_json, d['out_addr_json'],
+                                                    d['out_amount_json'], fee_str)
                 database.checkpoint('transactions')
-                database.insert_regular_outputs(out_rows, txid[out_tx], out_index, out_amount, out_addr, out_len)
+                tb = perf_counter()
+                database.insert_regular_outputs(hashes, out_tx, out_index, d['out_addr_str'], txid[out_tx],
+                                                out_amount, out_addr, out_len)
                 await database.add_transaction_outputs([coinbase_transaction])
                 database.checkpoint('outputs')
+                tc = perf_counter()
                 await database.remove_pending_transactions_by_hash(list(hashes))
-                database.remove_spent_regular(spent, in_keys)
-                database._delete_outpoints('pending_spent_outputs', spent)
+                database.remove_spent_regular(in_keys)
+                td = perf_counter()
+                database.remove_pending_spent_keys(in_keys)
                 database.checkpoint('spent')
+                te = perf_counter()
         except Exception as e:
             logger.error(f'Transaction of {block_no} has not been added in block {e}')
             database._rebuild_utxo_index()
             manager.Manager.difficulty = None
             return False
+        timings.update({'apply_txrows_s': tb - ta, 'apply_outputs_s': tc - tb, 'apply_spent_s': td - tc,
+                        'apply_pending_s': te - td, 'commit_s': perf_counter() - te})
         return True
 
     if coinbase is not None:
