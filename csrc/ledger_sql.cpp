@@ -89,13 +89,15 @@ sqlite3* handle_of(py::handle conn) {
 
 // One bound column of a bulk statement.
 struct Col {
-    enum Kind { TEXT_LIST, GATHER, HEX32, INT64, CONST_TEXT, CONST_INT, NUL } kind = NUL;
+    enum Kind { TEXT_LIST, GATHER, HEX32, INT64, CONST_TEXT, CONST_INT, NUL, ARENA } kind = NUL;
     std::vector<const char*> ptr;  // TEXT_LIST / GATHER: UTF-8 views (nullptr = NULL)
     std::vector<int> len;
     const int32_t* idx = nullptr;  // GATHER
     int64_t idx_n = 0;
     const uint8_t* raw = nullptr;  // HEX32
     int64_t stride = 0, offset = 0, raw_n = 0;
+    const char* blob = nullptr;     // ARENA: concatenated text + offsets[n + 1]
+    const int64_t* aoff = nullptr;
     const int64_t* ival = nullptr;  // INT64
     int64_t ival_n = 0;
     std::string ctext;
@@ -125,6 +127,7 @@ void utf8_list(py::list lst, Col& c) {
 //   list[str|None]                   text per row
 //   ('gather', list[str], int32 buf)  text list[idx[row]]
 //   ('hex32', buf, stride, offset)    lowercase hex of the 32 bytes at row*stride+offset
+//   ('arena', blob, int64 offsets)    text blob[off[row]:off[row+1]] (csrc/txcodec.cpp text arenas)
 //   int64 numpy array                 integer per row
 //   str / int / None                  the same value for every row
 Col parse_col(py::handle spec, int64_t n) {
@@ -163,6 +166,17 @@ Col parse_col(py::handle spec, int64_t n) {
             c.offset = t[3].cast<int64_t>();
             if (n > 0 && ((n - 1) * c.stride + c.offset + 32 > c.raw_n || c.offset < 0 || c.stride < 0))
                 throw std::out_of_range("hex32 column out of range");
+        } else if (tag == "arena") {
+            c.kind = Col::ARENA;
+            py::buffer_info bb = t[1].cast<py::buffer>().request(), ob = t[2].cast<py::buffer>().request();
+            // offsets arrive as raw bytes (txcodec) or an int64 array: only the byte size is checked
+            if (ob.size * ob.itemsize != 8 * (n + 1)) throw std::invalid_argument("arena offsets must be int64[n + 1]");
+            c.blob = static_cast<const char*>(bb.ptr);
+            c.aoff = static_cast<const int64_t*>(ob.ptr);
+            const int64_t blen = bb.size * bb.itemsize;
+            for (int64_t i = 0; i < n; ++i)
+                if (c.aoff[i] < 0 || c.aoff[i + 1] < c.aoff[i] || c.aoff[i + 1] > blen)
+                    throw std::out_of_range("arena offsets");
         } else {
             throw std::invalid_argument("unknown column tag " + tag);
         }
@@ -236,6 +250,9 @@ int64_t executemany(py::object conn, const std::string& sql, py::sequence cols, 
                         else a.bind_null(st, p);
                         break;
                     }
+                    case Col::ARENA:
+                        a.bind_text(st, p, c.blob + c.aoff[r], int(c.aoff[r + 1] - c.aoff[r]), nullptr);
+                        break;
                     case Col::HEX32: {
                         if (hb >= 8) {
                             a.finalize(st);

@@ -343,6 +343,21 @@ static py::bytes as_bytes(const std::vector<uint8_t>& v) {
     return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
 }
 
+// Text arena: all strings of one column concatenated + int64 offsets[n+1]. The bulk ledger writer
+// (csrc/ledger_sql.cpp, column kind 'arena') binds slices of it, so the per-output strings never
+// become Python objects.
+struct Arena {
+    std::string blob;
+    std::vector<int64_t> off{0};
+    void add(const char* p, size_t n) {
+        blob.append(p, n);
+        off.push_back(int64_t(blob.size()));
+    }
+    py::tuple py() const {
+        return py::make_tuple(py::bytes(blob), py::bytes(reinterpret_cast<const char*>(off.data()), off.size() * 8));
+    }
+};
+
 // decode_block_txs(hexes, threads) -> dict (see module docstring of upow_amd/ledger/fastpath.py)
 static py::dict decode_block_txs(py::list hexes, int threads) {
     const int64_t n = int64_t(hexes.size());
@@ -414,8 +429,11 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
         out_addr(NO * 64, 0), out_len(NO), out_type(NO);
     std::vector<int32_t> in_sig(NI), in_tx(NI), out_tx(NO);
     std::vector<uint64_t> out_amount(NO);
-    py::list canon_hex = new_list(N), tx_hash = new_list(N), out_addr_str = new_list(NO), out_addr_json = new_list(N),
-             out_amount_json = new_list(N);
+    py::list canon_hex = new_list(N);
+    Arena addr_arena, addr_json_arena, amount_json_arena;
+    addr_arena.blob.reserve(NO * 45);
+    addr_json_arena.blob.reserve(N * 96);
+    amount_json_arena.blob.reserve(N * 24);
     for (int64_t i = 0; i < n; ++i) {
         const DecTx& t = txs[size_t(i)];
         std::memcpy(&txid[32 * size_t(i)], t.txid, 32);
@@ -439,23 +457,19 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
             out_type[o] = t.outs[j].type;
             out_amount[o] = t.outs[j].amount;
             out_tx[o] = int32_t(i);
-            PyList_SET_ITEM(out_addr_str.ptr(), Py_ssize_t(o), ascii_str(t.out_addr[j].data(), t.out_addr[j].size()));
+            addr_arena.add(t.out_addr[j].data(), t.out_addr[j].size());
         }
         // the input string is reused when it already is the canonical lowercase hex of the tx
         if (t.canonical && !t.upper_hex && srcl[size_t(i)] == 2 * t.canon.size()) {
-            PyObject* o = PyList_GET_ITEM(hexes.ptr(), Py_ssize_t(i));
-            Py_INCREF(o);
-            PyList_SET_ITEM(canon_hex.ptr(), Py_ssize_t(i), o);
+            PyObject* obj = PyList_GET_ITEM(hexes.ptr(), Py_ssize_t(i));
+            Py_INCREF(obj);
+            PyList_SET_ITEM(canon_hex.ptr(), Py_ssize_t(i), obj);
         } else {
             const std::string h = to_hex(t.canon.data(), t.canon.size());
             PyList_SET_ITEM(canon_hex.ptr(), Py_ssize_t(i), ascii_str(h.data(), h.size()));
         }
-        char hx[64];
-        hex32(t.txid, hx);
-        PyList_SET_ITEM(tx_hash.ptr(), Py_ssize_t(i), ascii_str(hx, 64));
-        PyList_SET_ITEM(out_addr_json.ptr(), Py_ssize_t(i), ascii_str(t.out_addr_json.data(), t.out_addr_json.size()));
-        PyList_SET_ITEM(out_amount_json.ptr(), Py_ssize_t(i),
-                        ascii_str(t.out_amount_json.data(), t.out_amount_json.size()));
+        addr_json_arena.add(t.out_addr_json.data(), t.out_addr_json.size());
+        amount_json_arena.add(t.out_amount_json.data(), t.out_amount_json.size());
     }
     d["in_keys"] = as_bytes(in_keys);
     d["in_type"] = as_bytes(in_type);
@@ -470,12 +484,17 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
     d["out_tx"] = i32(out_tx);
     d["out_amount"] = py::bytes(reinterpret_cast<const char*>(out_amount.data()), out_amount.size() * 8);
     d["hex"] = canon_hex;
-    d["tx_hash"] = tx_hash;
-    d["out_addr_str"] = out_addr_str;
-    d["out_addr_json"] = out_addr_json;
-    d["out_amount_json"] = out_amount_json;
+    d["out_addr_str"] = addr_arena.py();
+    d["out_addr_json"] = addr_json_arena.py();
+    d["out_amount_json"] = amount_json_arena.py();
     auto t2 = std::chrono::steady_clock::now();
     d["merkle"] = merkle_of(txs);
+    {
+        // ~8 heap blocks per tx were allocated by the pool's threads: release them there too (a
+        // serial free of ~10^5 blocks from foreign malloc arenas costs ~10 ms on the main thread)
+        py::gil_scoped_release rel;
+        parallel_for(n, threads, [&](int64_t i) { txs[size_t(i)] = DecTx(); });
+    }
     if (prof) {
         auto t3 = std::chrono::steady_clock::now();
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -487,7 +506,7 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
 
 // Canonical compressed address strings for spent outputs (database._input_address): 33-byte
 // addresses keep x with the normalised prefix, 64-byte ones take the parity of y. Returns the
-// per-input strings and, per tx, the inputs_addresses JSON column.
+// per-tx inputs_addresses JSON column as a text arena (blob, int64 offsets[n_tx + 1]).
 static py::tuple input_address_strings(py::bytes addrs64, py::bytes lens, py::bytes in_start_b, int threads) {
     std::string a = addrs64, l = lens, s = in_start_b;
     const size_t n_in = l.size();
@@ -516,10 +535,11 @@ static py::tuple input_address_strings(py::bytes addrs64, py::bytes lens, py::by
     }
     for (size_t i = 0; i < n_in; ++i)
         if (bad[i]) throw std::invalid_argument("input address payload missing");
-    py::list strs = new_list(n_in), json = new_list(n_tx);
-    for (size_t i = 0; i < n_in; ++i) PyList_SET_ITEM(strs.ptr(), Py_ssize_t(i), ascii_str(out[i].data(), out[i].size()));
+    Arena json;
+    json.blob.reserve(n_tx * 100);
+    std::string j;
     for (size_t t = 0; t < n_tx; ++t) {
-        std::string j = "[";
+        j.assign(1, '[');
         for (int32_t k = st[t]; k < st[t + 1]; ++k) {
             if (k > st[t]) j += ',';
             j += '"';
@@ -527,9 +547,9 @@ static py::tuple input_address_strings(py::bytes addrs64, py::bytes lens, py::by
             j += '"';
         }
         j += ']';
-        PyList_SET_ITEM(json.ptr(), Py_ssize_t(t), ascii_str(j.data(), j.size()));
+        json.add(j.data(), j.size());
     }
-    return py::make_tuple(strs, json);
+    return json.py();
 }
 
 // ---- row builders for the bulk ledger writes (ledger/fastpath.py): Python tuples built in C++

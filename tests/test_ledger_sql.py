@@ -39,6 +39,17 @@ def test_column_kinds_and_order():
     rows = c.execute('SELECT * FROM t ORDER BY rowid').fetchall()
     assert rows[0] == (bytes(raw[:32]).hex(), 7, 'w2', 'const', 5, None)
     assert rows[1][2] == 'w0' and rows[2][2] is None and rows[3][0] == bytes(raw[120:152]).hex()
+    # text arena (the codec's form): blob + int64 offsets, as bytes or as an array
+    c.execute('CREATE TABLE a (s TEXT)')
+    blob, off = b'alphabetagamma', np.array([0, 5, 9, 14], np.int64)
+    for offs in (off, off.tobytes()):
+        assert L.sql_executemany(c, 'INSERT INTO a VALUES (?)', [('arena', blob, offs)], 3) == 3
+    assert [r[0] for r in c.execute('SELECT s FROM a')] == ['alpha', 'beta', 'gamma'] * 2
+    from upow_amd.ledger.database import _expand_col, arena_list
+    assert arena_list((blob, off.tobytes())) == ['alpha', 'beta', 'gamma']
+    assert _expand_col(('hex32', raw, 40, 0), 2) == [bytes(raw[:32]).hex(), bytes(raw[40:72]).hex()]
+    with pytest.raises(IndexError):
+        L.sql_executemany(c, 'INSERT INTO a VALUES (?)', [('arena', blob, np.array([0, 5, 99], np.int64))], 2)
     # explicit row order: the last row first
     c.execute('CREATE TABLE o (x INTEGER)')
     L.sql_executemany(c, 'INSERT INTO o VALUES (?)', [np.array([10, 20, 30], np.int64)], 3,

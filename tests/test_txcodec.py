@@ -8,6 +8,8 @@ import numpy as np
 import pytest
 from hypothesis import HealthCheck, given, settings, strategies as st
 
+from upow_amd.ledger.database import arena_list
+
 from upow_amd.models.block import get_transactions_merkle_tree
 from upow_amd.models.transaction import Transaction, TransactionInput, TransactionOutput
 from upow_amd.utils.codec import OutputType, point_to_string
@@ -49,15 +51,17 @@ def _check_fast(d, hexes):
     in_start, out_start = i32('in_start'), i32('out_start')
     in_keys = np.frombuffer(d['in_keys'], dtype=np.uint8).reshape(-1, 40)
     out_amount = np.frombuffer(d['out_amount'], dtype=np.uint64)
+    out_addr_json, out_amount_json = arena_list(d['out_addr_json']), arena_list(d['out_amount_json'])
+    out_addr_str = arena_list(d['out_addr_str'])
     for k, h in enumerate(hexes):
         tx, _ = Transaction.parse(h)
         assert d['hex'][k] == tx.hex()
-        assert d['tx_hash'][k] == tx.hash()
+        assert d['txid'][32 * k:32 * k + 32].hex() == tx.hash()
         assert d['digest'][32 * k:32 * k + 32] == hashlib.sha256(bytes.fromhex(tx.hex(False))).digest()
         assert i32('signed_len')[k] * 2 == len(tx.hex(False))
-        assert d['out_addr_json'][k] == json.dumps([o.address for o in tx.outputs], separators=(',', ':'))
-        assert d['out_amount_json'][k] == json.dumps([int(o.amount * 10 ** 8) for o in tx.outputs], separators=(',', ':'))
-        assert d['out_addr_str'][out_start[k]:out_start[k + 1]] == [o.address for o in tx.outputs]
+        assert out_addr_json[k] == json.dumps([o.address for o in tx.outputs], separators=(',', ':'))
+        assert out_amount_json[k] == json.dumps([int(o.amount * 10 ** 8) for o in tx.outputs], separators=(',', ':'))
+        assert out_addr_str[out_start[k]:out_start[k + 1]] == [o.address for o in tx.outputs]
         assert [int(a) for a in out_amount[out_start[k]:out_start[k + 1]]] == [int(o.amount * 10 ** 8) for o in tx.outputs]
         for j, i in enumerate(tx.inputs):
             rec = in_keys[in_start[k] + j]
@@ -139,8 +143,8 @@ def test_input_address_strings(L):
         addrs += raw + bytes(64 - len(raw))
         lens.append(len(raw))
     starts = np.array([0, 2, 6], dtype=np.int32).tobytes()
-    strs, js = L.input_address_strings(bytes(addrs), bytes(lens), starts, 2)
-    assert strs == [point_to_string(p) for p in pts]
+    js = arena_list(L.input_address_strings(bytes(addrs), bytes(lens), starts, 2))
+    strs = [point_to_string(p) for p in pts]
     assert js == [json.dumps(strs[:2], separators=(',', ':')), json.dumps(strs[2:], separators=(',', ':'))]
 
 

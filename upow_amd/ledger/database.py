@@ -159,6 +159,34 @@ def _at(arr: list, index: int):
     return arr[index] if 0 <= index < len(arr) else None
 
 
+def _expand_col(spec, n: int) -> list:
+    """Python values of one bulk column spec (the ``sqlite3.executemany`` fallback of Database.bulk)."""
+    if isinstance(spec, list):
+        return spec
+    if isinstance(spec, tuple):
+        kind = spec[0]
+        if kind == 'gather':
+            return [spec[1][i] for i in np.asarray(spec[2]).tolist()]
+        if kind == 'hex32':
+            raw = np.frombuffer(spec[1], dtype=np.uint8)
+            stride, off = spec[2], spec[3]
+            return [bytes(raw[r * stride + off:r * stride + off + 32]).hex() for r in range(n)]
+        if kind == 'arena':
+            blob = bytes(spec[1]).decode()  # ASCII: byte offsets are character offsets
+            off = np.frombuffer(spec[2], dtype=np.int64).tolist()
+            return [blob[off[i]:off[i + 1]] for i in range(n)]
+        raise ValueError(f'unknown column kind {kind}')
+    if isinstance(spec, np.ndarray):
+        return spec.tolist()
+    return [spec] * n
+
+
+def arena_list(arena) -> List[str]:
+    """The strings of a (blob, int64 offsets) text arena from csrc/txcodec.cpp."""
+    blob, off = arena
+    return _expand_col(('arena', blob, off), len(off) // 8 - 1)
+
+
 class Database:
     """SQLite-backed ledger. ``Database.instance`` is the process singleton (as in the reference)."""
     instance: 'Database' = None
@@ -258,10 +286,21 @@ class Database:
             return False
 
     def bulk(self, sql: str, cols: list, n: int, order=None) -> int:
-        """Column-major executemany (see csrc/ledger_sql.cpp); returns the summed row changes."""
-        from ..ops.native import lib
+        """Column-major executemany; returns the summed row changes. Column specs as in
+        csrc/ledger_sql.cpp (text lists, int64 arrays, ('gather'|'hex32'|'arena', ...) views of the block
+        codec's buffers, or one constant). Without the native writer the same specs are expanded to
+        Python rows for ``sqlite3.executemany``."""
+        if n == 0:
+            return 0
+        if self.native_sql:
+            from ..ops.native import lib
+            with self.lock:
+                return lib().sql_executemany(self.conn, sql, cols, n, order)
+        rows = list(zip(*[_expand_col(c, n) for c in cols]))
+        if order is not None:
+            rows = [rows[i] for i in np.asarray(order).tolist()]
         with self.lock:
-            return lib().sql_executemany(self.conn, sql, cols, n, order)
+            return self.conn.executemany(sql, rows).rowcount
 
     class _Tx:
         """Re-entrant SQL transaction: only the outermost level issues BEGIN/COMMIT/ROLLBACK, so a
@@ -384,6 +423,20 @@ class Database:
 
     async def remove_pending_transaction(self, tx_hash: str):
         self._x('DELETE FROM pending_transactions WHERE tx_hash = ?', (tx_hash,))
+
+    def remove_pending_by_txids(self, txids: np.ndarray) -> int:
+        """``remove_pending_transactions_by_hash`` for a block given as n x 32 raw txids: hex strings
+        are only rendered when the mempool is non-empty."""
+        with self.lock:
+            if self.conn.execute('SELECT 1 FROM pending_transactions LIMIT 1').fetchone() is None:
+                return 0
+        hashes = [bytes(t).hex() for t in np.ascontiguousarray(txids, dtype=np.uint8).reshape(-1, 32)]
+        with self.lock:
+            pending = {r[0] for r in self.conn.execute('SELECT tx_hash FROM pending_transactions')}
+            hit = [(h,) for h in hashes if h in pending]
+            if hit:
+                self.conn.executemany('DELETE FROM pending_transactions WHERE tx_hash = ?', hit)
+        return len(hit)
 
     async def remove_pending_transactions_by_hash(self, tx_hashes: List[str]):
         with self.lock:
@@ -520,18 +573,14 @@ class Database:
         except sqlite3.IntegrityError as e:
             raise UniqueViolationError(str(e)) from e
 
-    def insert_transaction_columns(self, block_hash: str, hashes: list, hexes: list, inputs_addresses: list,
-                                   outputs_addresses: list, outputs_amounts: list, fees: list):
-        """``insert_transaction_rows`` from per-column lists (native block path)."""
-        n = len(hashes)
-        if not self.native_sql:
-            return self.insert_transaction_rows(list(zip([block_hash] * n, hashes, hexes, inputs_addresses,
-                                                          outputs_addresses, outputs_amounts, fees)))
+    def insert_transaction_columns(self, n: int, block_hash: str, tx_hash, tx_hex, inputs_addresses,
+                                   outputs_addresses, outputs_amounts, fees):
+        """``insert_transaction_rows`` from bulk column specs (native block path, see :meth:`bulk`)."""
         try:
             with self.transaction():
                 self.bulk('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, '
                           'outputs_addresses, outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)',
-                          [block_hash, hashes, hexes, inputs_addresses, outputs_addresses, outputs_amounts, fees], n)
+                          [block_hash, tx_hash, tx_hex, inputs_addresses, outputs_addresses, outputs_amounts, fees], n)
         except sqlite3.IntegrityError as e:
             raise UniqueViolationError(str(e)) from e
 
@@ -757,23 +806,18 @@ class Database:
             payload = await self._payload_from_ledger([(r[0], r[1]) for r in rows])
         self.utxo.insert([(r[0], r[1]) for r in rows], TAG_BY_TABLE['unspent_outputs'], payload)
 
-    def insert_regular_outputs(self, tx_hashes: list, out_tx: np.ndarray, indexes: np.ndarray, out_addr_str: list,
-                               txids: np.ndarray, amounts: np.ndarray, addrs: np.ndarray, lens: np.ndarray) -> None:
+    def insert_regular_outputs(self, indexes: np.ndarray, addresses, txids: np.ndarray, amounts: np.ndarray,
+                               addrs: np.ndarray, lens: np.ndarray) -> None:
         """Native block path: REGULAR outputs as (tx_hash, index, address, is_stake=0) rows + one index
         insert with their payloads (amount, normalised address bytes) — ``add_unspent_outputs`` in bulk.
-        Output ``o`` belongs to tx ``out_tx[o]`` (its hash ``tx_hashes[out_tx[o]]``, digest ``txids[o]``)."""
-        n = len(out_tx)
+        ``txids``: n x 32 creating-tx digests; ``addresses``: a bulk text column spec (see :meth:`bulk`)."""
+        n = len(indexes)
         if not n:
             return
-        out_tx = np.ascontiguousarray(out_tx, dtype=np.int32)
+        txids = np.ascontiguousarray(txids, dtype=np.uint8)
         indexes = np.ascontiguousarray(indexes, dtype=np.int64)
-        sql = 'INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) VALUES (?, ?, ?, ?)'
-        if self.native_sql:
-            self.bulk(sql, [('gather', list(tx_hashes), out_tx), indexes, list(out_addr_str), 0], n)
-        else:
-            with self.lock:
-                self.conn.executemany(sql, [(tx_hashes[t], int(i), a, 0)
-                                            for t, i, a in zip(out_tx.tolist(), indexes.tolist(), out_addr_str)])
+        self.bulk('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) VALUES (?, ?, ?, ?)',
+                  [('hex32', txids, 32, 0), indexes, addresses, 0], n)
         recs = np.zeros((n, 40), dtype=np.uint8)
         recs[:, :32] = txids
         recs[:, 32:36] = indexes.astype(np.uint32).reshape(n, 1).view(np.uint8)
@@ -801,12 +845,9 @@ class Database:
             return True
         in_keys = np.ascontiguousarray(in_keys, dtype=np.uint8)
         idx = in_keys[:, 32:36].copy().view(np.uint32).ravel().astype(np.int64)
-        sql = 'DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?'
         with self.transaction():
-            if self.native_sql:
-                n = self.bulk(sql, [('hex32', in_keys, 40, 0), idx], n_in, self._key_order(in_keys))
-            else:
-                n = self.conn.executemany(sql, [(bytes(k[:32]).hex(), int(i)) for k, i in zip(in_keys, idx)]).rowcount
+            n = self.bulk('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
+                          [('hex32', in_keys, 40, 0), idx], n_in, self._key_order(in_keys))
         recs = np.array(in_keys, dtype=np.uint8, copy=True)
         recs[:, 36:40] = np.full((n_in, 1), TAG_BY_TABLE['unspent_outputs'], dtype=np.uint32).view(np.uint8)
         self.utxo.erase_records(recs)

@@ -111,6 +111,7 @@ async def _create_block_from_hex(block_content: str, tx_hexes: List[str], error_
         return await fn(block_content, txs, last_block, error_list)
 
     dec = decode(tx_hexes) if tx_hexes else None
+    timings['decode_s'] = perf_counter() - t0
     if dec is None:
         last_path = 'object'
         return await object_path(False)
@@ -231,11 +232,11 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     manager.last_block_timings.update({'utxo_s': t2 - t1, 'verify_s': t4 - t2, 'merkle_s': 0.0,
                                        'total_s': t4 - t0, 'txs': n})
 
-    # ---- columns for the ledger writes (bound natively by csrc/ledger_sql.cpp when available)
-    in_strs, in_json = lib().input_address_strings(np.ascontiguousarray(pay['addr']).tobytes(),
-                                                   pay['len'].astype(np.uint8).tobytes(), d['in_start'], 8)
+    # ---- columns for the ledger writes: views of the codec's buffers, bound natively by
+    #      csrc/ledger_sql.cpp (tx hashes rendered from the raw digests, text arenas for the strings)
     L = lib()
-    hexes, hashes = d['hex'], d['tx_hash']
+    in_json = L.input_address_strings(np.ascontiguousarray(pay['addr']).tobytes(),
+                                      pay['len'].astype(np.uint8).tobytes(), d['in_start'], THREADS)
     fee_str = L.fee_strings(np.ascontiguousarray(fee, dtype=np.int64).tobytes())
     out_tx = _i32(d, 'out_tx')
     out_index = np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]
@@ -249,16 +250,17 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
                                          block_reward + fees_total, content_time)
                 database.checkpoint('block')
                 await database.add_transaction(coinbase_transaction, block_hash)
-                database.insert_transaction_columns(block_hash, hashes, hexes, in_json, d['out_addr_json'],
-                                                    d['out_amount_json'], fee_str)
+                database.insert_transaction_columns(n, block_hash, ('hex32', txid, 32, 0), d['hex'],
+                                                    ('arena', *in_json), ('arena', *d['out_addr_json']),
+                                                    ('arena', *d['out_amount_json']), fee_str)
                 database.checkpoint('transactions')
                 tb = perf_counter()
-                database.insert_regular_outputs(hashes, out_tx, out_index, d['out_addr_str'], txid[out_tx],
+                database.insert_regular_outputs(out_index, ('arena', *d['out_addr_str']), txid[out_tx],
                                                 out_amount, out_addr, out_len)
                 await database.add_transaction_outputs([coinbase_transaction])
                 database.checkpoint('outputs')
                 tc = perf_counter()
-                await database.remove_pending_transactions_by_hash(list(hashes))
+                database.remove_pending_by_txids(txid)
                 database.remove_spent_regular(in_keys)
                 td = perf_counter()
                 database.remove_pending_spent_keys(in_keys)
