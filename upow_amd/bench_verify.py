@@ -160,4 +160,9 @@ def run_verify_bench(args, ctx):
                    'seq_len': txs_per_block, 'parallelism': f'dp{ctx.world}', 'device': device,
                    'utxo_backend': utxo_backend, 'block_path': '+'.join(paths)},
         'stage_ms_avg': avg,
+        # the same run split by stage: validation alone (decode, HBM UTXO pass, decompression, ECDSA —
+        # everything before the ledger writes) and the signature kernel alone, per 2 MB block
+        'validate_tx_per_s': round(txs_per_block / max(1e-9, (avg.get('decode_to_checks_s', 0) + avg.get('utxo_s', 0)
+                                                             + avg.get('verify_s', 0)) / 1000), 1),
+        'ecdsa_sig_per_s': round(txs_per_block / max(1e-9, avg.get('ecdsa_s', 0) / 1000), 1),
     }

@@ -33,6 +33,7 @@ from .. import config
 from ..constants import ENDIAN, GENESIS_PREV_HASH, MAX_SUPPLY, VERSION
 from ..ledger import manager as mgr
 from ..ledger.database import Database, UniqueViolationError
+from ..ledger import fastpath
 from ..ledger.fastpath import create_block_from_hex
 from ..ops.native import lib
 from ..parallel import cluster
@@ -140,7 +141,7 @@ async def create_blocks(blocks: list, error_list=None) -> bool:
         hexes = list(block_info['transactions'])
         # the first coinbase among the txs is the trusted one (main.py:112-117); the rest go through
         # the native block path (ledger/fastpath.py) in sync mode
-        flags = lib().decode_block_txs(hexes, 1)['flags'] if hexes else b''
+        flags = lib().decode_block_txs(hexes, fastpath.THREADS)['flags'] if hexes else b''
         cb_tx = None
         for k, f in enumerate(flags):
             if f == 3:
