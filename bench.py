@@ -12,7 +12,8 @@ Weak scaling: per-GPU work (2^32 nonces/step) is fixed as N grows; ``value`` is 
 of all N GPUs. ``vs_baseline`` divides by BASELINE.md's 0.99 MH/s (the reference miner.py inner loop,
 one process, measured in the survey sandbox — the reference publishes no number).
 
-``--mode verify`` measures the second BASELINE metric instead (tx-verify/s on a synthetic 2 MB block).
+``--mode verify`` measures the second BASELINE metric instead (tx-verify/s on a synthetic 2 MB block);
+``--mode sync`` the chain-sync throughput of the same blocks replayed from a ``/get_blocks`` page.
 """
 from __future__ import annotations
 
@@ -106,7 +107,7 @@ def main(argv=None):
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--mode', choices=['mine', 'verify'], default='mine')
+    ap.add_argument('--mode', choices=['mine', 'verify', 'sync'], default='mine')
     ap.add_argument('--difficulty', default='6.3')
     ap.add_argument('--nonces', type=int, default=0, help='nonce words per rank per step (default 2^32)')
     ap.add_argument('--variant', type=int, default=int(os.environ.get('UPOW_POW_VARIANT', '0')))
@@ -120,7 +121,13 @@ def main(argv=None):
     from upow_amd.parallel.dist import init_from_env, shutdown
     ctx = init_from_env()
     try:
-        out = bench_mine(args, ctx) if args.mode == 'mine' else bench_verify(args, ctx)
+        if args.mode == 'mine':
+            out = bench_mine(args, ctx)
+        elif args.mode == 'verify':
+            out = bench_verify(args, ctx)
+        else:
+            from upow_amd.bench_verify import run_sync_bench
+            out = run_sync_bench(args, ctx)
         if ctx.is_main:
             print(json.dumps(out), flush=True)
     finally:

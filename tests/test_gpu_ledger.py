@@ -47,3 +47,34 @@ def test_gpu_index_snapshot_roundtrip(gpu, tmp_path, monkeypatch):
         assert db2.utxo_source == 'snapshot' and len(db2.utxo) == n and snapshot.verify(db2)['ok']
         db2.close()
     asyncio.run(go())
+
+
+@pytest.mark.gpu
+def test_sync_bench_pipeline_on_gpu(gpu, monkeypatch):
+    """Chain sync replay (node.main.create_blocks: decode-ahead thread + native block path) on the
+    HBM UTXO index: the replica reaches the source tip."""
+    from decimal import Decimal
+    from upow_amd import constants
+    from upow_amd.ledger import manager
+    monkeypatch.setattr(constants, 'START_DIFFICULTY', Decimal('4.0'))
+    monkeypatch.setattr(manager, 'START_DIFFICULTY', Decimal('4.0'))
+    from upow_amd.bench_verify import run_sync_bench
+    from upow_amd.parallel.dist import DistContext
+    out = run_sync_bench(argparse.Namespace(steps=2, warmup=1, txs=500), DistContext())
+    assert out['config']['utxo_backend'] == 'gpu' and out['config']['block_path'] == 'native'
+    assert out['value'] > 0
+
+
+def test_sync_bench_pipeline_host(monkeypatch):
+    """Same replay on the host backend (CPU container): exercises the pipelined create_blocks."""
+    from decimal import Decimal
+    from upow_amd import constants
+    from upow_amd.ledger import manager
+    from upow_amd.ops import native
+    monkeypatch.setattr(constants, 'START_DIFFICULTY', Decimal('2.0'))
+    monkeypatch.setattr(manager, 'START_DIFFICULTY', Decimal('2.0'))
+    monkeypatch.setattr(native, 'gpu_available', lambda: False)
+    from upow_amd.bench_verify import run_sync_bench
+    from upow_amd.parallel.dist import DistContext
+    out = run_sync_bench(argparse.Namespace(steps=3, warmup=1, txs=120), DistContext())
+    assert out['config']['block_path'] == 'native' and out['value'] > 0

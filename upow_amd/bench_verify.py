@@ -29,7 +29,8 @@ def _funding_tx(owner_addrs, amount: Decimal, rng):
     return Transaction([inp], [TransactionOutput(a, amount) for a in owner_addrs])
 
 
-async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None, device=None):
+async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None, device=None, base_ts=None,
+                 make_blocks: bool = True):
     from . import devnet
     from .ledger import manager
     from .ledger.database import Database
@@ -41,7 +42,7 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
     manager.Manager.difficulty = None
     keys = [rng.randrange(1, op.oracle.N) for _ in range(256)]
     addrs = [point_to_string(op.public_key(k)) for k in keys]
-    base_ts = int(time.time()) - 10_000
+    base_ts = base_ts if base_ts is not None else int(time.time()) - 10_000
     genesis_addr = addrs[0]
     await devnet.mine_block(genesis_addr, ts=base_ts, device=device)
     # funding block written straight into the ledger (trusted setup, not part of the measurement)
@@ -65,7 +66,7 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
     # spending blocks
     blocks = []
     j = 0
-    for b in range(n_blocks):
+    for b in range(n_blocks if make_blocks else 0):
         txs = []
         for _ in range(txs_per_block):
             (h1, i1), (h2, i2) = outpoints[2 * j], outpoints[2 * j + 1]
@@ -165,4 +166,76 @@ def run_verify_bench(args, ctx):
         'validate_tx_per_s': round(txs_per_block / max(1e-9, (avg.get('decode_to_checks_s', 0) + avg.get('utxo_s', 0)
                                                              + avg.get('verify_s', 0)) / 1000), 1),
         'ecdsa_sig_per_s': round(txs_per_block / max(1e-9, avg.get('ecdsa_s', 0) / 1000), 1),
+    }
+
+
+async def _run_sync(args, ctx, device, utxo_backend):
+    """Sync throughput: a source ledger applies ``steps + warmup`` full blocks through push_block; a
+    second ledger with the same genesis + funding then replays them the way a syncing node does
+    (``node.main.create_blocks`` over a ``/get_blocks`` page: trusted coinbase, native block path,
+    decode of block k+1 overlapped with the apply of block k). Only the replay is timed."""
+    from . import devnet
+    from .constants import START_DIFFICULTY
+    from .ledger import manager
+    from .ledger.database import Database
+    from .models.block import get_transactions_merkle_tree
+    from .ledger import fastpath
+    n_blocks = args.steps + args.warmup
+    base_ts = int(time.time()) - 10_000
+    seed = 4321 + ctx.rank
+    src, addr, blocks, _ = await _setup(n_blocks, args.txs, seed, utxo_backend, device, base_ts=base_ts)
+    prev = (await src.get_last_block())['hash']
+    for b, txs_hex in enumerate(blocks):
+        content = devnet.mine_header_raw(prev, addr, get_transactions_merkle_tree(txs_hex), base_ts + 10 + b,
+                                         START_DIFFICULTY, device=device)
+        errors = []
+        if not await fastpath.create_block_from_hex(content, txs_hex, error_list=errors):
+            raise RuntimeError(f'source block rejected: {errors}')
+        prev = hashlib.sha256(bytes.fromhex(content)).hexdigest()
+    page = await src.get_blocks(3, n_blocks)
+    assert len(page) == n_blocks and all(len(p['transactions']) == args.txs + 1 for p in page)
+    src.close()
+    dst, _, _, _ = await _setup(n_blocks, args.txs, seed, utxo_backend, device, base_ts=base_ts, make_blocks=False)
+    Database.instance = dst
+    manager.Manager.difficulty = None
+    from .node.main import create_blocks
+    if args.warmup:
+        if not await create_blocks(page[:args.warmup]):
+            raise RuntimeError('sync warmup rejected')
+    ctx.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    errors = []
+    if not await create_blocks(page[args.warmup:], errors):
+        raise RuntimeError(f'sync rejected: {errors}')
+    ctx.synchronize()
+    ctx.barrier()
+    wall = ctx.allreduce_max_f(time.perf_counter() - t0)
+    assert (await dst.get_last_block())['hash'] == page[-1]['block']['hash']
+    return args.steps * args.txs, wall, fastpath.last_path
+
+
+def run_sync_bench(args, ctx):
+    from .ops.native import gpu_available
+    device = 'gpu' if gpu_available() else 'cpu'
+    utxo_backend = 'gpu' if device == 'gpu' else 'host'
+    txs, wall, path = asyncio.run(_run_sync(args, ctx, device, utxo_backend))
+    total = ctx.allreduce_sum(txs)
+    return {
+        'metric': 'sync_tx_per_s',
+        'value': round(total / wall, 1),
+        'unit': 'tx/s',
+        'n_gpus': ctx.world if device == 'gpu' else 0,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(wall * 1000 / max(1, args.steps), 2),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'uint32',
+        'data': 'synthetic 2 MB blocks replayed from a /get_blocks page (coinbase included)',
+        'config': {'model': 'upow chain sync (node.main.create_blocks, trusted coinbase)',
+                   'global_batch': total // max(1, args.steps), 'seq_len': args.txs,
+                   'parallelism': f'dp{ctx.world}', 'device': device, 'utxo_backend': utxo_backend,
+                   'block_path': path},
     }

@@ -265,6 +265,12 @@ class Database:
         connection. ``UPOW_NATIVE_SQL=0`` keeps every write on ``sqlite3.executemany``."""
         if os.environ.get('UPOW_NATIVE_SQL', '1') == '0':
             return False
+        import platform
+        import sys
+        # the handle is read from pysqlite_Connection's first field: only for CPython builds whose
+        # layout is known (3.8-3.12 keep `sqlite3 *db` right after PyObject_HEAD)
+        if platform.python_implementation() != 'CPython' or not (3, 8) <= sys.version_info[:2] <= (3, 12):
+            return False
         try:
             from ..ops.native import lib
             L = lib()

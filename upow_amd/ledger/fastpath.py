@@ -68,8 +68,12 @@ def decode(tx_hexes: List[str]) -> Optional[dict]:
 
 
 async def create_block_from_hex(block_content: str, tx_hexes: List[str], error_list: list = None,
-                                last_block: dict = None, coinbase=None, mirror: bool = True) -> bool:
+                                last_block: dict = None, coinbase=None, mirror: bool = True,
+                                decoded: Optional[dict] = None) -> bool:
     """``create_block(block_content, [Transaction.from_hex(h) for h in tx_hexes])``, natively when possible.
+
+    ``decoded``: ``decode(tx_hexes)`` computed ahead of time (the sync pipeline decodes block k+1 on a
+    host thread while block k is applied); None means decode here.
 
     With ``coinbase`` (a CoinbaseTransaction) this is the sync variant ``create_block_in_syncing_old``
     (manager.py:760-835), which trusts the supplied coinbase instead of rebuilding it.
@@ -84,7 +88,7 @@ async def create_block_from_hex(block_content: str, tx_hexes: List[str], error_l
                cb=coinbase.hex() if coinbase is not None else None)
     err = None
     try:
-        ok = await _create_block_from_hex(block_content, tx_hexes, error_list, last_block, coinbase)
+        ok = await _create_block_from_hex(block_content, tx_hexes, error_list, last_block, coinbase, decoded)
     except Exception as e:  # every replica must still take part in the agreement below
         ok, err = False, e
     if c is not None and not c.replaying:
@@ -95,7 +99,7 @@ async def create_block_from_hex(block_content: str, tx_hexes: List[str], error_l
 
 
 async def _create_block_from_hex(block_content: str, tx_hexes: List[str], error_list: list = None,
-                                 last_block: dict = None, coinbase=None) -> bool:
+                                 last_block: dict = None, coinbase=None, decoded: Optional[dict] = None) -> bool:
     global last_path
     from . import manager
     if error_list is None:
@@ -110,7 +114,7 @@ async def _create_block_from_hex(block_content: str, tx_hexes: List[str], error_
         fn = manager._create_block if locked else manager.create_block
         return await fn(block_content, txs, last_block, error_list)
 
-    dec = decode(tx_hexes) if tx_hexes else None
+    dec = decoded if decoded is not None else (decode(tx_hexes) if tx_hexes else None)
     timings['decode_s'] = perf_counter() - t0
     if dec is None:
         last_path = 'object'

@@ -128,28 +128,55 @@ async def propagate(path: str, args: dict, ignore_url=None, nodes: list = None):
 
 
 # ---------------------------------------------------------------------------------------------- sync
+def _scan_sync_block(hexes: list):
+    """Host-thread half of a sync step (no ledger state involved): find the coinbase candidate
+    (txcodec flag 3 = specifier 36) and decode the remaining txs for the native block path."""
+    flags = lib().decode_block_txs(hexes, fastpath.THREADS)['flags'] if hexes else b''
+    k = next((i for i, f in enumerate(flags) if f == 3), None)
+    rest = hexes if k is None else hexes[:k] + hexes[k + 1:]
+    return k, (fastpath.decode(rest) if rest else None)
+
+
+_SYNC_DECODER = None
+
+
+def _sync_decoder():
+    global _SYNC_DECODER
+    if _SYNC_DECODER is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _SYNC_DECODER = ThreadPoolExecutor(max_workers=1, thread_name_prefix='upow-sync-decode')
+    return _SYNC_DECODER
+
+
 async def create_blocks(blocks: list, error_list=None) -> bool:
-    """main.py:97-150."""
+    """main.py:97-150, as a two-stage pipeline: while block k is validated and applied on the event
+    loop (GPU passes + ledger writes, GIL released in the native parts), block k+1 is already being
+    decoded on a host thread (``_scan_sync_block``: txids, canonical bytes, addresses, merkle)."""
     if error_list is None:
         error_list = []
     _, last_block = await calculate_difficulty()
     last_block['id'] = last_block['id'] if last_block != {} else 0
     last_block['hash'] = last_block['hash'] if 'hash' in last_block else GENESIS_PREV_HASH
     i = last_block['id'] + 1
-    for block_info in blocks:
+    loop = asyncio.get_running_loop()
+    pool = _sync_decoder()
+    hexes_of = [list(b['transactions']) for b in blocks]
+    ahead = loop.run_in_executor(pool, _scan_sync_block, hexes_of[0]) if blocks else None
+    for n, block_info in enumerate(blocks):
         block = block_info['block']
-        hexes = list(block_info['transactions'])
+        hexes = hexes_of[n]
+        cb_k, dec = await ahead
+        ahead = loop.run_in_executor(pool, _scan_sync_block, hexes_of[n + 1]) if n + 1 < len(blocks) else None
         # the first coinbase among the txs is the trusted one (main.py:112-117); the rest go through
         # the native block path (ledger/fastpath.py) in sync mode
-        flags = lib().decode_block_txs(hexes, fastpath.THREADS)['flags'] if hexes else b''
         cb_tx = None
-        for k, f in enumerate(flags):
-            if f == 3:
-                cand = await Transaction.from_hex(hexes[k])
-                if isinstance(cand, CoinbaseTransaction):
-                    cb_tx = cand
-                    del hexes[k]
-                    break
+        if cb_k is not None:
+            cand = await Transaction.from_hex(hexes[cb_k])
+            if isinstance(cand, CoinbaseTransaction):
+                cb_tx = cand
+                del hexes[cb_k]
+            else:
+                dec = None  # not what the scan assumed: decode inline below
         block_content = block.get('content')
         if not block_content:
             txs = [await Transaction.from_hex(h) for h in hexes]
@@ -157,7 +184,10 @@ async def create_blocks(blocks: list, error_list=None) -> bool:
             block_content = block_to_bytes(last_block['hash'], block)
         assert i == block['id']
         if not await create_block_from_hex(block_content.hex() if isinstance(block_content, bytes) else block_content,
-                                           hexes, error_list=error_list, last_block=last_block, coinbase=cb_tx):
+                                           hexes, error_list=error_list, last_block=last_block, coinbase=cb_tx,
+                                           decoded=dec):
+            if ahead is not None:
+                await ahead
             return False
         last_block = block
         i += 1
