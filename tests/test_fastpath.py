@@ -232,3 +232,39 @@ def test_sync_mode_matches_object_sync():
             assert da[k] == dbb[k], k
         assert _dump(src)['blocks'] == _dump(p.a)['blocks']
     asyncio.run(go())
+
+
+def test_ascii_hex_signature_fallback_matches():
+    """transaction_input.py:100-109: a signature over the ASCII hex string of ``hex(False)`` (legacy
+    wallets) verifies through the retry pass. Both paths must accept it, with one signature per tx
+    and with per-input signatures, and both must still reject a signature over neither form."""
+    from upow_amd.ops import p256 as op
+
+    async def go():
+        p, base = await _setup()
+        ts = base + 60 * 10
+        p.use(p.a)
+        txs = []
+        for k in KEYS[:2]:
+            tx = await create_transaction(GENESIS, address_of(k), '1.5')
+            msg = tx.hex(False).encode()  # the ASCII form, not bytes.fromhex
+            sig = op.sign(msg, GENESIS)
+            for i in tx.inputs:
+                i.signed = sig
+            assert await p.a.add_pending_transaction(tx)  # mempool admission takes the fallback too
+            txs.append(tx)
+        p.use(p.b)
+        for t in txs:
+            assert await p.b.add_pending_transaction(t)
+        c = await p.mine(txs, ts=ts)
+        await p.push(c, txs, expect=True)
+        assert fastpath.last_path == 'native'  # accepted by the native retry pass itself
+        # a signature over some other message fails both forms on both paths
+        p.use(p.a)
+        bad = await create_transaction(GENESIS, address_of(KEYS[3]), '1')
+        sig = op.sign(b'not the tx', GENESIS)
+        for i in bad.inputs:
+            i.signed = sig
+        c = await p.mine([bad], ts=ts + 60)
+        await p.push(c, [bad], expect=False)
+    asyncio.run(go())
