@@ -11,6 +11,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -55,6 +56,11 @@ public:
         done_cv_.notify_all();
         done_cv_.wait(lk, [&] { return active_ == 0; });
         body_ = nullptr;
+        if (error_) {  // first exception of any participant, rethrown on the calling thread
+            std::exception_ptr e = error_;
+            error_ = nullptr;
+            std::rethrow_exception(e);
+        }
     }
 
     ~HostPool() {
@@ -71,11 +77,17 @@ private:
     static constexpr int kMaxThreads = 32;
 
     void drain() {
-        for (;;) {
-            const int64_t b = next_.fetch_add(chunk_, std::memory_order_relaxed);
-            if (b >= n_) return;
-            const int64_t e = std::min(n_, b + chunk_);
-            for (int64_t i = b; i < e; ++i) (*body_)(i);
+        try {
+            for (;;) {
+                const int64_t b = next_.fetch_add(chunk_, std::memory_order_relaxed);
+                if (b >= n_) return;
+                const int64_t e = std::min(n_, b + chunk_);
+                for (int64_t i = b; i < e; ++i) (*body_)(i);
+            }
+        } catch (...) {
+            std::lock_guard<std::mutex> g(mu_);
+            if (!error_) error_ = std::current_exception();
+            next_.store(n_, std::memory_order_relaxed);  // the others stop at their next chunk
         }
     }
 
@@ -120,6 +132,7 @@ private:
     int active_ = 0, wanted_ = 0;
     uint64_t generation_ = 0;
     bool stop_ = false;
+    std::exception_ptr error_;
     pid_t pid_ = getpid();
 };
 

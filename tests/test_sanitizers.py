@@ -17,4 +17,5 @@ def test_host_code_clean_under_asan_ubsan():
     r = subprocess.run([os.path.join(ROOT, 'tools', 'sanitize_host.sh')], cwd=ROOT, capture_output=True, text=True,
                        timeout=1200)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    assert 'all checks passed' in r.stdout
+    assert 'host selftest: all checks passed' in r.stdout
+    assert 'pool selftest: all checks passed' in r.stdout  # ThreadSanitizer run of csrc/thread_pool.h

@@ -29,3 +29,8 @@ $CXX -fsanitize=address,undefined -pthread "$OUT"/host_selftest.o "$OUT"/p256.o 
   "$OUT"/base58.o -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib -o "$OUT/host_selftest"
 # leak checking off: the HIP runtime keeps process-lifetime allocations
 ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 "$OUT/host_selftest"
+# ThreadSanitizer on the host worker pool (csrc/thread_pool.h)
+if stale "$OUT/pool_selftest" tools/pool_selftest.cpp csrc/thread_pool.h; then
+  $CXX -O1 -g -std=c++17 -fsanitize=thread -pthread -Icsrc tools/pool_selftest.cpp -o "$OUT/pool_selftest"
+fi
+TSAN_OPTIONS=halt_on_error=1 "$OUT/pool_selftest"
