@@ -25,6 +25,7 @@
 #include <thread>
 #include <vector>
 
+#include "dev_pool.h"
 #include "native.h"
 #include "p256_field.h"
 #include "sha256_common.h"
@@ -252,12 +253,12 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
     std::vector<uint8_t> st(static_cast<size_t>(n));
     if (n == 0) return st;
     const aff* d_tab = device_g_table();
-    VerifyItem* d_items = nullptr;
-    jac* d_scratch = nullptr;
-    uint8_t* d_st = nullptr;
-    hck(hipMalloc(&d_items, sizeof(VerifyItem) * n), "hipMalloc items");
-    hck(hipMalloc(&d_scratch, sizeof(jac) * 16 * n), "hipMalloc scratch");
-    hck(hipMalloc(&d_st, size_t(n)), "hipMalloc status");
+    PooledBuf<VerifyItem> b_items{size_t(n)};
+    PooledBuf<jac> b_scratch(size_t(16) * size_t(n));
+    PooledBuf<uint8_t> b_st{size_t(n)};
+    VerifyItem* d_items = b_items.p;
+    jac* d_scratch = b_scratch.p;
+    uint8_t* d_st = b_st.p;
     hck(hipMemcpy(d_items, items, sizeof(VerifyItem) * n, hipMemcpyHostToDevice), "h2d items");
     const int block = 64;
     const int grid = int((n + block - 1) / block);
@@ -269,7 +270,6 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
         hipLaunchKernelGGL(p256_verify_kernel<1>, dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch, d_st);
     hck(hipGetLastError(), "p256_verify_kernel launch");
     hck(hipMemcpy(st.data(), d_st, size_t(n), hipMemcpyDeviceToHost), "d2h status");
-    (void)hipFree(d_items); (void)hipFree(d_scratch); (void)hipFree(d_st);
     return st;
 }
 
@@ -291,10 +291,8 @@ void p256_decompress_host(const uint8_t* in, int64_t n, uint8_t* out, uint8_t* o
 
 void p256_decompress_gpu(const uint8_t* in, int64_t n, uint8_t* out, uint8_t* ok) {
     if (n == 0) return;
-    uint8_t *d_in = nullptr, *d_out = nullptr, *d_ok = nullptr;
-    hck(hipMalloc(&d_in, 33 * size_t(n)), "hipMalloc in");
-    hck(hipMalloc(&d_out, 64 * size_t(n)), "hipMalloc out");
-    hck(hipMalloc(&d_ok, size_t(n)), "hipMalloc ok");
+    PooledBuf<uint8_t> b_in{33 * size_t(n)}, b_out{64 * size_t(n)}, b_ok{size_t(n)};
+    uint8_t *d_in = b_in.p, *d_out = b_out.p, *d_ok = b_ok.p;
     hck(hipMemcpy(d_in, in, 33 * size_t(n), hipMemcpyHostToDevice), "h2d in");
     const int block = 256;
     hipLaunchKernelGGL(p256_decompress_kernel, dim3(int((n + block - 1) / block)), dim3(block), 0, 0, d_in, n,
@@ -302,7 +300,6 @@ void p256_decompress_gpu(const uint8_t* in, int64_t n, uint8_t* out, uint8_t* ok
     hck(hipGetLastError(), "p256_decompress_kernel launch");
     hck(hipMemcpy(out, d_out, 64 * size_t(n), hipMemcpyDeviceToHost), "d2h out");
     hck(hipMemcpy(ok, d_ok, size_t(n), hipMemcpyDeviceToHost), "d2h ok");
-    (void)hipFree(d_in); (void)hipFree(d_out); (void)hipFree(d_ok);
 }
 
 bool p256_pubkey(const uint8_t d_be[32], uint8_t out_le[64]) {

@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "dev_pool.h"
 #include "native.h"
 #include "sha256_common.h"
 
@@ -120,13 +121,12 @@ std::vector<uint8_t> sha256_batch_gpu(const uint8_t* data, int64_t nbytes, const
     total += 4;
     std::vector<uint8_t> packed(size_t(total), 0);
     for (int64_t i = 0; i < n; ++i) std::memcpy(packed.data() + aoff[i], data + offsets[i], lens[i]);
-    uint8_t* d_data = nullptr;
-    int64_t* d_off = nullptr;
-    uint32_t *d_len = nullptr, *d_out = nullptr;
-    hchk(hipMalloc(&d_data, size_t(total)), "hipMalloc data");
-    hchk(hipMalloc(&d_off, sizeof(int64_t) * n), "hipMalloc off");
-    hchk(hipMalloc(&d_len, sizeof(uint32_t) * n), "hipMalloc len");
-    hchk(hipMalloc(&d_out, 32 * size_t(n)), "hipMalloc out");
+    PooledBuf<uint8_t> b_data{size_t(total)};
+    PooledBuf<int64_t> b_off{size_t(n)};
+    PooledBuf<uint32_t> b_len{size_t(n)}, b_out{size_t(n) * 8};
+    uint8_t* d_data = b_data.p;
+    int64_t* d_off = b_off.p;
+    uint32_t *d_len = b_len.p, *d_out = b_out.p;
     hchk(hipMemcpy(d_data, packed.data(), size_t(total), hipMemcpyHostToDevice), "h2d data");
     hchk(hipMemcpy(d_off, aoff.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice), "h2d off");
     hchk(hipMemcpy(d_len, lens.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice), "h2d len");
@@ -137,7 +137,6 @@ std::vector<uint8_t> sha256_batch_gpu(const uint8_t* data, int64_t nbytes, const
     hchk(hipGetLastError(), "sha256_varlen_kernel launch");
     std::vector<uint32_t> words(size_t(n) * 8);
     hchk(hipMemcpy(words.data(), d_out, 32 * size_t(n), hipMemcpyDeviceToHost), "d2h out");
-    (void)hipFree(d_data); (void)hipFree(d_off); (void)hipFree(d_len); (void)hipFree(d_out);
     for (size_t k = 0; k < words.size(); ++k) store_be32(out.data() + 4 * k, words[k]);
     return out;
 }

@@ -26,6 +26,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "dev_pool.h"
 #include "native.h"
 #include "sha256_common.h"
 
@@ -279,12 +280,9 @@ uint32_t utxo_capacity(int64_t h) {
     return table(h).cap;
 }
 
+// per-call scratch comes from the caching pool (csrc/dev_pool.h): no hipMalloc/hipFree per block
 template <typename T>
-struct DevBuf {
-    T* p = nullptr;
-    explicit DevBuf(size_t n) { uck(hipMalloc(&p, sizeof(T) * (n ? n : 1)), "hipMalloc"); }
-    ~DevBuf() { (void)hipFree(p); }
-};
+using DevBuf = PooledBuf<T>;
 
 uint32_t utxo_insert(int64_t h, const uint8_t* recs, int64_t n, const uint8_t* payload) {
     std::lock_guard<std::mutex> lk(g_ut_mu);
