@@ -113,6 +113,7 @@ def main(argv=None):
     ap.add_argument('--variant', type=int, default=int(os.environ.get('UPOW_POW_VARIANT', '0')))
     ap.add_argument('--txs', type=int, default=8300, help='verify mode: txs per block')
     ap.add_argument('--object-path', action='store_true', help='verify mode: Transaction-object path (A/B)')
+    ap.add_argument('--ledger', default=None, help='verify mode: directory for a file-backed (WAL) ledger')
     args = ap.parse_args(argv)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))

@@ -30,7 +30,7 @@ def _funding_tx(owner_addrs, amount: Decimal, rng):
 
 
 async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None, device=None, base_ts=None,
-                 make_blocks: bool = True):
+                 make_blocks: bool = True, ledger_path: str = None):
     from . import devnet
     from .ledger import manager
     from .ledger.database import Database
@@ -38,7 +38,7 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
     from .ops import p256 as op
     from .utils.codec import point_to_string
     rng = random.Random(seed)
-    db = await Database.create(utxo_backend=utxo_backend)
+    db = await Database.create(ledger_path, utxo_backend=utxo_backend)
     manager.Manager.difficulty = None
     keys = [rng.randrange(1, op.oracle.N) for _ in range(256)]
     addrs = [point_to_string(op.public_key(k)) for k in keys]
@@ -84,12 +84,26 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
     return db, genesis_addr, blocks, base_ts
 
 
+def _ledger_path(args, ctx):
+    """``--ledger DIR``: a file-backed ledger (WAL, synchronous=NORMAL — what a node runs with) in a
+    fresh per-rank directory; default is an in-memory SQLite ledger."""
+    base = getattr(args, 'ledger', None)
+    if not base:
+        return None
+    import os
+    import tempfile
+    os.makedirs(base, exist_ok=True)
+    os.environ.setdefault('UPOW_SNAPSHOT', '0')
+    return os.path.join(tempfile.mkdtemp(prefix=f'bench_r{ctx.rank}_', dir=base), 'ledger.sqlite3')
+
+
 async def _run(args, ctx, device, utxo_backend):
     from . import devnet
     from .ledger import fastpath, manager, validate
     from .models.transaction import Transaction
     n_blocks = args.steps + args.warmup
-    db, addr, blocks, base_ts = await _setup(n_blocks, args.txs, 1234 + ctx.rank, utxo_backend, device)
+    db, addr, blocks, base_ts = await _setup(n_blocks, args.txs, 1234 + ctx.rank, utxo_backend, device,
+                                             ledger_path=_ledger_path(args, ctx))
     # mine every header up front (untimed): block b+1's previous hash is sha256(header_b) and the
     # difficulty stays at START_DIFFICULTY below block 100
     from .constants import START_DIFFICULTY
@@ -159,7 +173,8 @@ def run_verify_bench(args, ctx):
         'data': 'synthetic 2 MB blocks: random P-256 keys, 2-in/2-out signed txs, funding UTXOs',
         'config': {'model': 'upow block validation + apply (push_block path)', 'global_batch': total // max(1, args.steps),
                    'seq_len': txs_per_block, 'parallelism': f'dp{ctx.world}', 'device': device,
-                   'utxo_backend': utxo_backend, 'block_path': '+'.join(paths)},
+                   'utxo_backend': utxo_backend, 'block_path': '+'.join(paths),
+                   'ledger': 'file (WAL)' if getattr(args, 'ledger', None) else 'memory'},
         'stage_ms_avg': avg,
         # the same run split by stage: validation alone (decode, HBM UTXO pass, decompression, ECDSA —
         # everything before the ledger writes) and the signature kernel alone, per 2 MB block
