@@ -81,6 +81,9 @@ const SqliteApi& api() {
 }
 
 sqlite3* handle_of(py::handle conn) {
+    // only ever reinterpret a real sqlite3.Connection (or a subclass of it)
+    static PyObject* conn_type = py::module_::import("sqlite3").attr("Connection").ptr();
+    if (PyObject_IsInstance(conn.ptr(), conn_type) != 1) throw py::type_error("expected a sqlite3.Connection");
     // CPython 3.10 Modules/_sqlite/connection.h: struct { PyObject_HEAD; sqlite3 *db; ... }
     sqlite3* db = *reinterpret_cast<sqlite3**>(reinterpret_cast<char*>(conn.ptr()) + sizeof(PyObject));
     if (!db) throw std::runtime_error("sqlite3 connection is closed");

@@ -67,6 +67,8 @@ def test_column_kinds_and_order():
         L.sql_executemany(c, 'INSERT INTO o VALUES (?)', [np.array([1], np.int64)], 2)
     with pytest.raises(IndexError):
         L.sql_executemany(c, 'INSERT INTO t (g) VALUES (?)', [('gather', words, np.array([3], np.int32))], 1)
+    with pytest.raises(TypeError):  # never reinterprets anything but a sqlite3.Connection
+        L.sql_executemany(object(), 'INSERT INTO o VALUES (?)', [1], 1)
 
 
 def test_native_writes_join_the_open_transaction():
