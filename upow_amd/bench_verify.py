@@ -93,7 +93,6 @@ def _ledger_path(args, ctx):
     import os
     import tempfile
     os.makedirs(base, exist_ok=True)
-    os.environ.setdefault('UPOW_SNAPSHOT', '0')
     return os.path.join(tempfile.mkdtemp(prefix=f'bench_r{ctx.rank}_', dir=base), 'ledger.sqlite3')
 
 

@@ -203,11 +203,16 @@ class Database:
             self.conn.execute('PRAGMA journal_mode = WAL')
             self.conn.execute('PRAGMA synchronous = NORMAL')
             # a 2 MB block rewrites ~10 MB of B-tree pages: keep the hot index levels in a large page
-            # cache (MI355X hosts have RAM to spare) and checkpoint the WAL every ~4 blocks instead of
-            # on every commit (SQLite's default is 1000 pages = 4 MB)
+            # cache (MI355X hosts have RAM to spare), and take WAL checkpoints (page copy-back + fsync)
+            # off the block-apply path: a background thread with its own connection runs PASSIVE
+            # checkpoints; the commit-time auto-checkpoint only remains as a 400 MB safety net
             cache_mb = int(os.environ.get('UPOW_SQLITE_CACHE_MB', '1024'))
             self.conn.execute(f'PRAGMA cache_size = -{cache_mb * 1024}')
-            self.conn.execute(f"PRAGMA wal_autocheckpoint = {int(os.environ.get('UPOW_WAL_AUTOCHECKPOINT', '10000'))}")
+            bg = os.environ.get('UPOW_WAL_CHECKPOINT_THREAD', '1') != '0'
+            auto = int(os.environ.get('UPOW_WAL_AUTOCHECKPOINT', '100000' if bg else '10000'))
+            self.conn.execute(f'PRAGMA wal_autocheckpoint = {auto}')
+            if bg:
+                self._start_checkpointer(float(os.environ.get('UPOW_WAL_CHECKPOINT_PERIOD', '0.5')))
         self.conn.executescript(SCHEMA)
         store_dir = os.path.dirname(path) if path != ':memory:' else None
         self.emission_details = JsonStore(os.path.join(store_dir, 'emission_details.json') if store_dir else None)
@@ -243,7 +248,36 @@ class Database:
         row = self._q1('SELECT MAX(id) FROM blocks')
         return int(row[0] or 0)
 
+    _ckpt_stop: Optional[threading.Event] = None
+    _ckpt_thread: Optional[threading.Thread] = None
+
+    def _start_checkpointer(self, period: float):
+        """WAL checkpoints on a daemon thread: ``PRAGMA wal_checkpoint(PASSIVE)`` copies committed frames
+        back into the database file without blocking the writer (the fsync happens here, not at the
+        block's COMMIT). sqlite3 releases the GIL while the checkpoint runs."""
+        self._ckpt_stop = threading.Event()
+        path = self.path
+
+        def run(stop: threading.Event):
+            conn = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
+            try:
+                while not stop.wait(period):
+                    try:
+                        conn.execute('PRAGMA wal_checkpoint(PASSIVE)').fetchall()
+                    except sqlite3.Error as e:  # busy/locked: try again next period
+                        logger.debug(f'WAL checkpoint skipped: {e}')
+            finally:
+                conn.close()
+
+        self._ckpt_thread = threading.Thread(target=run, args=(self._ckpt_stop,), name='upow-wal-checkpoint',
+                                             daemon=True)
+        self._ckpt_thread.start()
+
     def close(self):
+        if self._ckpt_stop is not None:
+            self._ckpt_stop.set()
+            self._ckpt_thread.join(timeout=10)
+            self._ckpt_stop = None
         with self.lock:
             self.conn.close()
 
