@@ -155,7 +155,36 @@ static uint8_t verify_one_host(const VerifyItem& it, const aff* gtab) {
 // ------------------------------------------------------------------------------------------------
 // device kernels
 // ------------------------------------------------------------------------------------------------
-template <int MIN_WAVES>
+// Per-lane window table {1..15}Q lives in global scratch. SOA = false: [lane][k] Jacobian entries
+// (each lane's 16 x 96 B contiguous; a table load gathers 64 scattered lines per dword). SOA = true:
+// dword-major [k][dword][lane], so the lanes of a wave that picked the same window digit read one
+// contiguous run per dword (at most 16 distinct runs per load instead of 64 lines).
+template <bool SOA>
+__device__ __forceinline__ void tab_store(jac* scratch, int64_t n, int64_t i, int k, const jac& p) {
+    if (SOA) {
+        uint32_t* s = reinterpret_cast<uint32_t*>(scratch);
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&p);
+#pragma unroll
+        for (int d = 0; d < 24; ++d) s[(int64_t(k) * 24 + d) * n + i] = src[d];
+    } else {
+        scratch[i * 16 + k] = p;
+    }
+}
+
+template <bool SOA>
+__device__ __forceinline__ jac tab_load(const jac* scratch, int64_t n, int64_t i, int k) {
+    if (SOA) {
+        jac p;
+        const uint32_t* s = reinterpret_cast<const uint32_t*>(scratch);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&p);
+#pragma unroll
+        for (int d = 0; d < 24; ++d) dst[d] = s[(int64_t(k) * 24 + d) * n + i];
+        return p;
+    }
+    return scratch[i * 16 + k];
+}
+
+template <int MIN_WAVES, bool SOA>
 __global__ __launch_bounds__(64, MIN_WAVES) void p256_verify_kernel(const VerifyItem* __restrict__ items, int64_t n,
                                                           const aff* __restrict__ gtab, jac* __restrict__ scratch,
                                                           uint8_t* __restrict__ status) {
@@ -166,18 +195,17 @@ __global__ __launch_bounds__(64, MIN_WAVES) void p256_verify_kernel(const Verify
     fe r, u1, u2;
     const uint8_t pro = verify_prologue(it, q, r, u1, u2);
     if (pro != 255) { status[i] = pro; return; }
-    jac* tbl = scratch + i * 16;
     jac t = jac_from_aff(q);
-    tbl[1] = t;
+    tab_store<SOA>(scratch, n, i, 1, t);
     for (int k = 2; k < 16; ++k) {
         t = jac_madd(t, q);
-        tbl[k] = t;
+        tab_store<SOA>(scratch, n, i, k, t);
     }
     jac acc = jac_inf();
     for (int w = 63; w >= 0; --w) {
         acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc);
         const uint32_t nib = fe_nibble(u2, w);
-        if (nib) acc = jac_add(acc, tbl[nib]);
+        if (nib) acc = jac_add(acc, tab_load<SOA>(scratch, n, i, int(nib)));
     }
     const jac R = jac_add(mul_g(u1, gtab), acc);
     status[i] = verify_epilogue(R, r);
@@ -262,12 +290,19 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
     hck(hipMemcpy(d_items, items, sizeof(VerifyItem) * n, hipMemcpyHostToDevice), "h2d items");
     const int block = 64;
     const int grid = int((n + block - 1) / block);
-    // UPOW_P256_VARIANT=1: force 4 waves/SIMD (128 VGPRs, some spills) instead of the compiler's 3
+    // UPOW_P256_VARIANT=1: force 4 waves/SIMD (128 VGPRs, some spills) instead of the compiler's 3;
+    // UPOW_P256_VARIANT=2: dword-major (SoA) window tables
     const char* var = std::getenv("UPOW_P256_VARIANT");
-    if (var && var[0] == '1')
-        hipLaunchKernelGGL(p256_verify_kernel<4>, dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch, d_st);
+    const char v = var ? var[0] : '0';
+    if (v == '1')
+        hipLaunchKernelGGL((p256_verify_kernel<4, false>), dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch,
+                           d_st);
+    else if (v == '2')
+        hipLaunchKernelGGL((p256_verify_kernel<1, true>), dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch,
+                           d_st);
     else
-        hipLaunchKernelGGL(p256_verify_kernel<1>, dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch, d_st);
+        hipLaunchKernelGGL((p256_verify_kernel<1, false>), dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch,
+                           d_st);
     hck(hipGetLastError(), "p256_verify_kernel launch");
     hck(hipMemcpy(st.data(), d_st, size_t(n), hipMemcpyDeviceToHost), "d2h status");
     return st;

@@ -22,7 +22,7 @@ for i in range(8300):
 base = b''.join(recs)
 out = {}
 import os
-for var in ('0', '1'):
+for var in ('0', '1', '2'):
     os.environ['UPOW_P256_VARIANT'] = var
     buf = base * 16
     op.verify_records(buf[:160 * 512], device='gpu')

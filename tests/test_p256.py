@@ -111,7 +111,9 @@ def test_decompress_host(native):
 
 
 @pytest.mark.gpu
-def test_gpu_batch_verify_matches_host(gpu):
+@pytest.mark.parametrize('variant', ['0', '1', '2'])  # default, 4 waves/SIMD, SoA window tables
+def test_gpu_batch_verify_matches_host(gpu, variant, monkeypatch):
+    monkeypatch.setenv('UPOW_P256_VARIANT', variant)
     recs, exp = _batch(700, 5)
     st_gpu = op.verify_records(recs, device='gpu')
     assert (st_gpu == exp).all()
