@@ -55,11 +55,26 @@ inline void host_compress_words(uint32_t st[8], const uint32_t w_in[16]) {
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
-inline void host_compress(uint32_t st[8], const uint8_t blk[64]) {
+// x86 SHA extensions (csrc/sha256_ni.cpp): used for every host block when the CPU has them
+bool sha256_ni_enabled();
+void sha256_ni_blocks(uint32_t st[8], const uint8_t* data, size_t nblocks);
+
+inline void host_compress_scalar(uint32_t st[8], const uint8_t blk[64]) {
     uint32_t w[16];
     for (int i = 0; i < 16; ++i) w[i] = load_be32(blk + 4 * i);
     host_compress_words(st, w);
 }
+
+inline void host_compress_blocks(uint32_t st[8], const uint8_t* p, size_t nblocks) {
+    static const bool ni = sha256_ni_enabled();
+    if (ni) {
+        sha256_ni_blocks(st, p, nblocks);
+        return;
+    }
+    for (size_t b = 0; b < nblocks; ++b) host_compress_scalar(st, p + 64 * b);
+}
+
+inline void host_compress(uint32_t st[8], const uint8_t blk[64]) { host_compress_blocks(st, blk, 1); }
 
 // Partial compression: run rounds [0, nrounds) of block `w` from state `st` (state NOT fed forward).
 // Used to precompute the nonce-independent rounds of the PoW tail block on the host.
@@ -90,18 +105,22 @@ struct HostSha256 {
             buflen += take; p += take; n -= take;
             if (buflen == 64) { host_compress(st, buf); buflen = 0; }
         }
-        while (n >= 64) { host_compress(st, p); p += 64; n -= 64; }
+        if (n >= 64) {
+            host_compress_blocks(st, p, n / 64);
+            p += n & ~size_t(63);
+            n &= 63;
+        }
         if (n) { std::memcpy(buf, p, n); buflen = n; }
     }
     void final(uint8_t out[32]) {
-        uint64_t bits = total * 8;
-        uint8_t pad = 0x80;
-        update(&pad, 1);
-        uint8_t z = 0;
-        while (buflen != 56) update(&z, 1);
-        uint8_t len[8];
-        for (int i = 0; i < 8; ++i) len[i] = uint8_t(bits >> (56 - 8 * i));
-        update(len, 8);
+        const uint64_t bits = total * 8;
+        uint8_t tail[128] = {0};  // one or two padding blocks
+        std::memcpy(tail, buf, buflen);
+        tail[buflen] = 0x80;
+        const size_t nb = buflen < 56 ? 1 : 2;
+        for (int i = 0; i < 8; ++i) tail[64 * nb - 1 - i] = uint8_t(bits >> (8 * i));
+        host_compress_blocks(st, tail, nb);
+        buflen = 0;
         for (int i = 0; i < 8; ++i) store_be32(out + 4 * i, st[i]);
     }
 };

@@ -57,6 +57,21 @@ static void test_sha256() {
         auto ref = sha(data.data() + off[i], size_t(off[i + 1] - off[i]));
         CHECK(std::memcmp(b.data() + 32 * i, ref.data(), 32) == 0);
     }
+    // SHA-NI block function == scalar rounds (multi-block runs from random states)
+    if (sha256_ni_enabled()) {
+        for (int t = 0; t < 200; ++t) {
+            const size_t nb = 1 + rng() % 5;
+            std::vector<uint8_t> blk(64 * nb);
+            for (auto& x : blk) x = uint8_t(rng());
+            uint32_t a[8], c[8];
+            for (int i = 0; i < 8; ++i) a[i] = c[i] = uint32_t(rng());
+            sha256_ni_blocks(a, blk.data(), nb);
+            for (size_t k = 0; k < nb; ++k) host_compress_scalar(c, blk.data() + 64 * k);
+            CHECK(std::memcmp(a, c, sizeof(a)) == 0);
+        }
+    } else {
+        std::printf("note: no SHA-NI on this CPU, scalar path only\n");
+    }
 }
 
 static void test_base58() {
