@@ -290,18 +290,20 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
     hck(hipMemcpy(d_items, items, sizeof(VerifyItem) * n, hipMemcpyHostToDevice), "h2d items");
     const int block = 64;
     const int grid = int((n + block - 1) / block);
-    // UPOW_P256_VARIANT=1: force 4 waves/SIMD (128 VGPRs, some spills) instead of the compiler's 3;
-    // UPOW_P256_VARIANT=2: dword-major (SoA) window tables
+    // Default (variant 1): __launch_bounds__(64, 4) -> 4 waves/SIMD at 128 VGPRs (a few spills), 7-9 %
+    // faster than the compiler's 142-VGPR / 3-wave choice (variant 0) in the A/B runs of
+    // scripts/p256_throughput.py (profiles/p256_variants_ab.txt). Variant 2: dword-major (SoA)
+    // window tables, slower (the gathers were not the bottleneck).
     const char* var = std::getenv("UPOW_P256_VARIANT");
-    const char v = var ? var[0] : '0';
-    if (v == '1')
-        hipLaunchKernelGGL((p256_verify_kernel<4, false>), dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch,
+    const char v = var ? var[0] : '1';
+    if (v == '0')
+        hipLaunchKernelGGL((p256_verify_kernel<1, false>), dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch,
                            d_st);
     else if (v == '2')
         hipLaunchKernelGGL((p256_verify_kernel<1, true>), dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch,
                            d_st);
     else
-        hipLaunchKernelGGL((p256_verify_kernel<1, false>), dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch,
+        hipLaunchKernelGGL((p256_verify_kernel<4, false>), dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch,
                            d_st);
     hck(hipGetLastError(), "p256_verify_kernel launch");
     hck(hipMemcpy(st.data(), d_st, size_t(n), hipMemcpyDeviceToHost), "d2h status");
