@@ -114,6 +114,8 @@ def main(argv=None):
     ap.add_argument('--txs', type=int, default=8300, help='verify mode: txs per block')
     ap.add_argument('--object-path', action='store_true', help='verify mode: Transaction-object path (A/B)')
     ap.add_argument('--ledger', default=None, help='verify mode: directory for a file-backed (WAL) ledger')
+    ap.add_argument('--from-mempool', action='store_true',
+                    help='verify mode: block txs are in the mempool and pushed as hashes (the miner path)')
     args = ap.parse_args(argv)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))

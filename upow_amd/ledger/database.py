@@ -471,18 +471,23 @@ class Database:
         self._x('DELETE FROM pending_transactions WHERE tx_hash = ?', (tx_hash,))
 
     def remove_pending_by_txids(self, txids: np.ndarray) -> int:
-        """``remove_pending_transactions_by_hash`` for a block given as n x 32 raw txids: hex strings
-        are only rendered when the mempool is non-empty."""
+        """``remove_pending_transactions_by_hash`` for a block given as n x 32 raw txids. Empty mempool:
+        nothing to do. A mempool much smaller than the block: delete only the hashes it holds. Otherwise
+        (the usual case for a mined block, whose txs came from the mempool) one native bulk delete."""
+        txids = np.ascontiguousarray(txids, dtype=np.uint8).reshape(-1, 32)
         with self.lock:
-            if self.conn.execute('SELECT 1 FROM pending_transactions LIMIT 1').fetchone() is None:
+            n_pending = self.conn.execute('SELECT COUNT(*) FROM pending_transactions').fetchone()[0]
+        if n_pending == 0 or not len(txids):
+            return 0
+        if 4 * n_pending < len(txids):
+            with self.lock:
+                pending = {r[0] for r in self.conn.execute('SELECT tx_hash FROM pending_transactions')}
+            keep = [k for k, t in enumerate(txids) if bytes(t).hex() in pending]
+            txids = txids[keep]
+            if not len(txids):
                 return 0
-        hashes = [bytes(t).hex() for t in np.ascontiguousarray(txids, dtype=np.uint8).reshape(-1, 32)]
-        with self.lock:
-            pending = {r[0] for r in self.conn.execute('SELECT tx_hash FROM pending_transactions')}
-            hit = [(h,) for h in hashes if h in pending]
-            if hit:
-                self.conn.executemany('DELETE FROM pending_transactions WHERE tx_hash = ?', hit)
-        return len(hit)
+        return self.bulk('DELETE FROM pending_transactions WHERE tx_hash = ?', [('hex32', txids, 32, 0)],
+                         len(txids), self._key_order(txids))
 
     async def remove_pending_transactions_by_hash(self, tx_hashes: List[str]):
         with self.lock:
@@ -730,7 +735,11 @@ class Database:
         if not hashes:
             return []
         want = set(hashes)
-        return [r['tx_hex'] for r in self._q('SELECT tx_hash, tx_hex FROM pending_transactions') if r['tx_hash'] in want]
+        with self.lock:
+            cur = self.conn.cursor()
+            cur.row_factory = None  # plain tuples: this scans the whole mempool
+            rows = cur.execute('SELECT tx_hash, tx_hex FROM pending_transactions').fetchall()
+        return [x for h, x in rows if h in want]
 
     async def get_transactions(self, tx_hashes: List[str]):
         infos = await self.get_transactions_info(tx_hashes)
@@ -903,17 +912,23 @@ class Database:
         return True
 
     def remove_pending_spent_keys(self, in_keys: np.ndarray) -> int:
-        """``DELETE FROM pending_spent_outputs`` for every spent outpoint of a block, restricted to the
-        outpoints that are actually in the (small) pending table instead of one index probe per input."""
+        """``DELETE FROM pending_spent_outputs`` for every spent outpoint of a block (n x 40 key records),
+        with the same three cases as :meth:`remove_pending_by_txids`."""
+        keys = np.ascontiguousarray(in_keys, dtype=np.uint8).reshape(-1, 40)
         with self.lock:
-            pending = self.conn.execute('SELECT tx_hash, "index" FROM pending_spent_outputs').fetchall()
-        if not pending or not len(in_keys):
+            n_pending = self.conn.execute('SELECT COUNT(*) FROM pending_spent_outputs').fetchone()[0]
+        if n_pending == 0 or not len(keys):
             return 0
-        have = {(r[0], r[1]) for r in pending}
-        keys = np.ascontiguousarray(in_keys, dtype=np.uint8)
-        idx = keys[:, 32:36].copy().view(np.uint32).ravel().tolist()
-        hit = [(h, i) for h, i in zip((bytes(k[:32]).hex() for k in keys), idx) if (h, i) in have]
-        return self._delete_outpoints('pending_spent_outputs', hit) if hit else 0
+        idx = keys[:, 32:36].copy().view(np.uint32).ravel().astype(np.int64)
+        if 4 * n_pending < len(keys):
+            with self.lock:
+                have = {(r[0], r[1]) for r in self.conn.execute('SELECT tx_hash, "index" FROM pending_spent_outputs')}
+            keep = [k for k in range(len(keys)) if (bytes(keys[k, :32]).hex(), int(idx[k])) in have]
+            keys, idx = keys[keep], idx[keep]
+            if not len(keys):
+                return 0
+        return self.bulk('DELETE FROM pending_spent_outputs WHERE tx_hash = ? AND "index" = ?',
+                         [('hex32', keys, 40, 0), idx], len(keys), self._key_order(keys))
 
     async def _add_gov_outputs(self, table: str, outputs: List[tuple]):
         if not outputs:
