@@ -325,15 +325,24 @@ static void parallel_for(int64_t n, int threads, F&& f) {
 
 // merkle root: SHA-256 over the txids of the txs sorted by their canonical bytes (manager.py:365-378)
 static std::string merkle_of(const std::vector<DecTx>& txs) {
-    std::vector<int> order(txs.size());
-    for (size_t i = 0; i < order.size(); ++i) order[i] = int(i);
-    std::sort(order.begin(), order.end(), [&](int a, int b) {
-        const auto& x = txs[size_t(a)].canon;
-        const auto& y = txs[size_t(b)].canon;
+    // sort by (big-endian 8-byte prefix, full bytes): canonical txs start with version, n_in and a
+    // random input txid, so the integer prefix decides almost every comparison without touching
+    // the tx bytes (zero padding of short txs is resolved by the full comparison on a tie)
+    std::vector<std::pair<uint64_t, int>> order(txs.size());
+    for (size_t i = 0; i < order.size(); ++i) {
+        const auto& c = txs[i].canon;
+        uint64_t key = 0;
+        for (size_t k = 0; k < 8; ++k) key = (key << 8) | (k < c.size() ? c[k] : 0u);
+        order[i] = {key, int(i)};
+    }
+    std::sort(order.begin(), order.end(), [&](const std::pair<uint64_t, int>& a, const std::pair<uint64_t, int>& b) {
+        if (a.first != b.first) return a.first < b.first;
+        const auto& x = txs[size_t(a.second)].canon;
+        const auto& y = txs[size_t(b.second)].canon;
         return std::lexicographical_compare(x.begin(), x.end(), y.begin(), y.end());
     });
     HostSha256 h;
-    for (int i : order) h.update(txs[size_t(i)].txid, 32);
+    for (const auto& o : order) h.update(txs[size_t(o.second)].txid, 32);
     uint8_t out[32];
     h.final(out);
     return to_hex(out, 32);
