@@ -138,10 +138,14 @@ async def _run(args, ctx, device, utxo_backend):
     paths = set()
     total_txs = 0
     from_mempool = getattr(args, 'from_mempool', False)
+    untimed = 0.0  # mempool admission of the next block's txs happens inside the wall-clock window
     for b, txs_hex in enumerate(blocks):
         if from_mempool:
+            ta = time.perf_counter()
             _admit_untimed(db, txs_hex)
             hashes = [hashlib.sha256(bytes.fromhex(h)).hexdigest() for h in txs_hex]  # the miner's request
+            if b > args.warmup:
+                untimed += time.perf_counter() - ta
         if b == args.warmup:
             ctx.barrier()
             ctx.synchronize()
@@ -172,7 +176,7 @@ async def _run(args, ctx, device, utxo_backend):
             paths.add('object' if args.object_path else fastpath.last_path)
     ctx.synchronize()
     ctx.barrier()
-    wall = time.perf_counter() - t_start
+    wall = time.perf_counter() - t_start - untimed
     wall = ctx.allreduce_max_f(wall)
     return total_txs, wall, stages, len(blocks[0]), sorted(paths)
 
