@@ -34,7 +34,7 @@ for var in ('0', '1', '2'):
     st = op.verify_records(base, device='gpu')
     out[f'variant{var}_gpu_8300'] = round(8300 / (time.perf_counter() - t), 1)
 os.environ['UPOW_P256_VARIANT'] = '1'  # the default
-for n in (8300, 8300 * 4, 8300 * 16):
+for n in (8300, 8300 * 4, 8300 * 16, 8300 * 64):  # 64 blocks = 8,300 waves: saturates the chip
     buf = base * (n // 8300)
     op.verify_records(buf[:160 * 512], device='gpu')
     t = time.perf_counter()
