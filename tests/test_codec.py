@@ -138,3 +138,26 @@ def test_tx_limits():
         Transaction([TransactionInput('00' * 32, 0)] * 256, [])
     with pytest.raises(AssertionError):
         TransactionOutput(point_to_string(o.get_public_key(5)), Decimal('0.000000001'))
+
+
+def test_tx_hex_memo_tracks_in_place_edits():
+    """Transaction.hex() is memoised; editing an output or input in place (same counts) must change
+    the serialisation and therefore the signed message and the txid."""
+    from decimal import Decimal
+
+    from upow_amd.models.transaction import Transaction, TransactionInput, TransactionOutput
+    from upow_amd.wallet.builders import address_of
+    tx = Transaction([TransactionInput('ab' * 32, 0)], [TransactionOutput(address_of(5), Decimal('1'))])
+    tx.inputs[0].signed = (7, 8)
+    msg1, full1 = tx.hex(False), tx.hex()
+    tx.outputs[0] = TransactionOutput(address_of(5), Decimal('2'))
+    assert tx.hex(False) != msg1 and tx.hex() != full1
+    msg2 = tx.hex(False)
+    tx.outputs[0].amount = Decimal('3')
+    assert tx.hex(False) != msg2
+    msg3 = tx.hex(False)
+    tx.inputs[0].index = 1
+    assert tx.hex(False) != msg3
+    tx.inputs[0].signed = (1, 2)
+    assert tx.hex(False) == tx.hex(False) and tx.hex().endswith(
+        (1).to_bytes(32, 'little').hex() + (2).to_bytes(32, 'little').hex())

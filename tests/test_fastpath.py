@@ -268,3 +268,77 @@ def test_ascii_hex_signature_fallback_matches():
         c = await p.mine([bad], ts=ts + 60)
         await p.push(c, [bad], expect=False)
     asyncio.run(go())
+
+
+@pytest.mark.parametrize('seed', [1, 2, 3])
+def test_random_blocks_differential(seed):
+    """Randomised blocks built from the live UTXO set, each carrying one randomly chosen fault (or
+    none): both paths must return the same verdict and error and leave identical ledgers (Pair.push
+    compares every table, the UTXO index with payloads and the UTXO-set hash)."""
+    rng = random.Random(seed)
+
+    async def go():
+        p, base = await _setup()
+        ts = base + 60 * 10
+        keys = [GENESIS] + KEYS
+        # fan the genesis coinbases out to the test keys first (several small outputs each)
+        p.use(p.a)
+        fan = []
+        for k in KEYS:
+            tx = await create_transaction(GENESIS, address_of(k), '0.7')
+            await p.a.add_pending_transaction(tx)
+            fan.append(tx)
+        c = await p.mine(fan, ts=ts)
+        await p.push(c, fan, expect=True)
+        accepted = 0
+        for r in range(8):
+            ts += 60
+            p.use(p.a)
+            owners = rng.sample(keys, 3)
+            txs, used = [], set()
+            for k in owners:
+                outs = [o for o in await p.a.get_spendable_outputs(address_of(k))
+                        if (o.tx_hash, o.index) not in used]
+                if not outs:
+                    continue
+                ins = outs[:rng.randint(1, min(3, len(outs)))]
+                used |= {(i.tx_hash, i.index) for i in ins}
+                total = sum(i.amount for i in ins)
+                pay = (total * Decimal(rng.randint(1, 9)) / 10).quantize(Decimal('0.00000001'))
+                outs_ = [TransactionOutput(address_of(rng.choice(keys)), pay)]
+                if total - pay > Decimal('0.01'):
+                    outs_.append(TransactionOutput(address_of(k), total - pay - Decimal('0.001')))
+                msg = rng.choice([None, None, b'memo %d' % r])
+                tx = Transaction(ins, outs_, msg)
+                tx.sign([k])
+                txs.append(tx)
+            if not txs:
+                continue
+            fault = rng.choice(['none', 'none', 'sig', 'dup_in_block', 'overspend', 'unknown_input', 'zero_out'])
+            victim = txs[0]
+            if fault == 'sig':
+                a_, b_ = victim.inputs[0].signed
+                for i in victim.inputs:
+                    i.signed = (a_, (b_ ^ 0x5) or 1)
+            elif fault == 'dup_in_block':
+                twin = Transaction([victim.inputs[0]], [TransactionOutput(address_of(GENESIS), Decimal('0.0001'))])
+                twin.sign([owners[0]] if owners else [GENESIS])
+                txs.append(twin)
+            elif fault == 'overspend':
+                victim.outputs[0] = TransactionOutput(victim.outputs[0].address, Decimal('1000000'))
+                victim.sign([o for o in owners])
+            elif fault == 'unknown_input':
+                ghost = Transaction([TransactionInput('cd' * 32, 1)], [TransactionOutput(address_of(GENESIS), Decimal('1'))])
+                ghost.inputs[0].signed = victim.inputs[0].signed
+                txs.append(ghost)
+            elif fault == 'zero_out':
+                victim.outputs.append(TransactionOutput(address_of(GENESIS), Decimal('0')))
+                victim.sign([o for o in owners])
+            hexes = [t.hex() for t in txs]
+            c = await p.mine(hexes, ts=ts)
+            ok, err = await p.push(c, hexes)
+            accepted += bool(ok)
+            if fault == 'none':
+                assert ok, err
+        assert accepted >= 1
+    asyncio.run(go())

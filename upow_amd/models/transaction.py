@@ -276,9 +276,13 @@ class Transaction:
     def hex(self, full: bool = True) -> str:
         """transaction.py:46-83 (``full=False`` is the signed message).
 
-        Memoised per (full, signature state): a block's txs are serialised several times on the
-        validation/apply path (txid, merkle, size check, storage)."""
-        fp = (full, len(self.inputs), len(self.outputs), self.message,
+        Memoised on a fingerprint of every serialised field (version, outpoints, outputs, message and,
+        for ``full``, the signatures): a block's txs are serialised several times on the
+        validation/apply path (txid, merkle, size check, storage), while a tx edited in place (an
+        output replaced or re-valued, then re-signed) must never be signed or hashed from stale bytes."""
+        fp = (full, self.version, self.message,
+              tuple((i.tx_hash, i.index, i.input_type) for i in self.inputs),
+              tuple((o.address_bytes, o.amount, o.transaction_type) for o in self.outputs),
               tuple(i.signed for i in self.inputs) if full else None)
         memo = self.__dict__.setdefault('_hex_memo', {})
         c = memo.get(full)
