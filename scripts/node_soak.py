@@ -44,6 +44,9 @@ def main():
     ap.add_argument('--seconds', type=float, default=120.0)
     ap.add_argument('--difficulty', default='9.5')
     ap.add_argument('--out', default=None)
+    ap.add_argument('--fanout1', type=int, default=25, help='coinbase -> N outputs')
+    ap.add_argument('--fanout2', type=int, default=200, help='each of those -> M outputs (pool = N*M UTXOs)')
+    ap.add_argument('--threads', type=int, default=1, help='concurrent /push_tx clients')
     a = ap.parse_args()
 
     from upow_amd.models.transaction import Transaction, TransactionInput, TransactionOutput
@@ -104,18 +107,20 @@ def main():
         tx = Transaction([inp], [TransactionOutput(x, v) for x, v in outs])
         return tx.sign([key])
 
-    # ---- fund: coinbase -> 25 outputs -> 25 x 200 outputs (5,000 spendable UTXOs)
+    # ---- fund: coinbase -> fanout1 outputs -> fanout1 x fanout2 outputs (the spendable pool)
     wait_height(2)
     cb = spendable()[0]
-    push(make_tx(cb[0], cb[1], cb[2], [(addr, Decimal('0.2399'))] * 25))
+    v1 = (cb[2] / a.fanout1 - Decimal('0.0001')).quantize(Decimal('0.00000001'))
+    push(make_tx(cb[0], cb[1], cb[2], [(addr, v1)] * a.fanout1))
     h0 = height()
     wait_height(h0 + 2)
-    lvl1 = [u for u in spendable() if u[2] == Decimal('0.2399')]
+    lvl1 = [u for u in spendable() if u[2] == v1]
+    v2 = (v1 / a.fanout2 - Decimal('0.00000100')).quantize(Decimal('0.00000001'))
     for u in lvl1:
-        push(make_tx(u[0], u[1], u[2], [(addr, Decimal('0.00119'))] * 200))
+        push(make_tx(u[0], u[1], u[2], [(addr, v2)] * a.fanout2))
     h1 = height()
     wait_height(h1 + 2)
-    pool = [u for u in spendable() if u[2] == Decimal('0.00119')]
+    pool = [u for u in spendable() if u[2] == v2]
     setup_s = time.time() - t_start
 
     # ---- steady state: one 1-in/1-out tx per pool UTXO at the target rate
@@ -147,21 +152,39 @@ def main():
 
     w = threading.Thread(target=watcher, daemon=True)
     w.start()
+    # pre-sign the whole pool (not part of the node's load)
+    fee = min(Decimal('0.00001'), v2 / 2)
+    signed = [make_tx(h, i, amount, [(sinks[k % len(sinks)], amount - fee)])
+              for k, (h, i, amount) in enumerate(pool[:int(a.rate * a.seconds) + 1])]
     t0 = time.time()
-    n = 0
-    errors = 0
-    while time.time() - t0 < a.seconds and n < len(pool):
-        target = t0 + n / a.rate
-        if time.time() < target:
-            time.sleep(target - time.time())
-        h, i, amount = pool[n]
-        tx = make_tx(h, i, amount, [(sinks[n % len(sinks)], amount - Decimal('0.00001'))])
-        try:
-            push(tx)
-            pushed[tx.hash()] = time.time()
-        except Exception:
-            errors += 1
-        n += 1
+    errors = [0]
+    lock = threading.Lock()
+
+    def pusher(tid):
+        c = httpx.Client(timeout=30)
+        for k in range(tid, len(signed), a.threads):
+            target = t0 + k / a.rate
+            if time.time() < target:
+                time.sleep(target - time.time())
+            if time.time() - t0 > a.seconds + 5:
+                break
+            tx = signed[k]
+            try:
+                r = c.post(url + '/push_tx', json={'tx_hex': tx.hex()}).json()
+                if not r.get('ok'):
+                    raise RuntimeError(r)
+                with lock:
+                    pushed[tx.hash()] = time.time()
+            except Exception:
+                with lock:
+                    errors[0] += 1
+
+    ps = [threading.Thread(target=pusher, args=(t,), daemon=True) for t in range(a.threads)]
+    for t in ps:
+        t.start()
+    for t in ps:
+        t.join()
+    n = len(pushed) + errors[0]
     t_push_end = time.time()
     # drain: wait until everything pushed is in a block (or 4 block intervals)
     deadline = time.time() + 120
@@ -190,7 +213,8 @@ def main():
     q = lambda p: round(lat[min(len(lat) - 1, int(p * len(lat)))], 2) if lat else None
     out = {
         'metric': 'node_soak_confirmed_tx_per_s', 'value': round(len(included) / max(1e-9, t_push_end - t0), 2),
-        'unit': 'tx/s', 'target_rate': a.rate, 'pushed': len(pushed), 'push_errors': errors,
+        'unit': 'tx/s', 'target_rate': a.rate, 'pushed': len(pushed), 'push_errors': errors[0],
+        'push_threads': a.threads, 'pool_utxos': len(pool),
         'confirmed': len(included), 'seconds': round(t_push_end - t0, 1),
         'inclusion_latency_s': {'p50': q(0.5), 'p90': q(0.9), 'p99': q(0.99), 'max': round(lat[-1], 2) if lat else None},
         'blocks': len(blocks), 'mean_block_interval_s': round(sum(intervals) / len(intervals), 2) if intervals else None,

@@ -15,6 +15,7 @@ Differences by design (MI355X build):
 from __future__ import annotations
 
 from decimal import Decimal
+from operator import attrgetter
 from io import BytesIO
 from typing import List, Optional, Tuple
 
@@ -46,6 +47,12 @@ def ecdsa_verify(sig: Tuple[int, int], msg, q: Point) -> bool:
     """fastecdsa.ecdsa.verify contract: raises p256.EcdsaError on bad key / r,s range."""
     from ..ops import p256 as op
     return op.verify(sig, msg, q)
+
+
+# C-level field getters for the hex() memo fingerprint (operator.attrgetter + map, no Python loop)
+_IN_KEY = attrgetter('tx_hash', 'index', 'input_type')
+_OUT_KEY = attrgetter('address_bytes', 'amount', 'transaction_type')
+_SIG_KEY = attrgetter('signed')
 
 
 class TransactionOutput:
@@ -280,10 +287,8 @@ class Transaction:
         for ``full``, the signatures): a block's txs are serialised several times on the
         validation/apply path (txid, merkle, size check, storage), while a tx edited in place (an
         output replaced or re-valued, then re-signed) must never be signed or hashed from stale bytes."""
-        fp = (full, self.version, self.message,
-              tuple((i.tx_hash, i.index, i.input_type) for i in self.inputs),
-              tuple((o.address_bytes, o.amount, o.transaction_type) for o in self.outputs),
-              tuple(i.signed for i in self.inputs) if full else None)
+        fp = (full, self.version, self.message, tuple(map(_IN_KEY, self.inputs)), tuple(map(_OUT_KEY, self.outputs)),
+              tuple(map(_SIG_KEY, self.inputs)) if full else None)
         memo = self.__dict__.setdefault('_hex_memo', {})
         c = memo.get(full)
         if c is not None and c[0] == fp:
