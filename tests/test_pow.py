@@ -91,3 +91,23 @@ def test_gpu_full_sweep_d63(gpu):
     assert 100 < len(r.nonces) < 320  # expectation 2^32 / 22.37M = 192
     for n in r.nonces[:20]:
         assert check_pow(job.header_with_nonce(n), prev, '6.3')
+
+
+def test_miner_tip_watcher_stops_stale_jobs():
+    """The miner drops a job once the node's tip moves (upow_amd/miner.py TipWatcher)."""
+    import time as _t
+
+    from upow_amd.miner import TipWatcher
+    tips = ['aa' * 32]
+    w = TipWatcher('http://node/', 0.01, fetch=lambda url: {'last_block': {'hash': tips[-1]}})
+    try:
+        deadline = _t.time() + 5
+        while w.tip is None and _t.time() < deadline:
+            _t.sleep(0.01)
+        assert not w.moved('aa' * 32)
+        tips.append('bb' * 32)
+        while not w.moved('aa' * 32) and _t.time() < deadline:
+            _t.sleep(0.01)
+        assert w.moved('aa' * 32) and not w.moved('bb' * 32)
+    finally:
+        w.close()

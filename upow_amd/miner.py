@@ -10,7 +10,11 @@ MI355X version:
   winner's header is agreed by all-reduce and broadcast, and rank 0 submits it;
 * ``workers`` is accepted for argv compatibility and ignored on GPUs (the kernel already runs one
   nonce per lane); on a CPU-only host it is the host-search thread count;
-* the job is refreshed every ``--refresh`` seconds (default 90, like the reference's window).
+* the job is refreshed every ``--refresh`` seconds (default 90, like the reference's window), and
+  earlier as soon as the node's tip moves: rank 0 polls ``/get_mining_info`` every ``--poll`` seconds
+  (default 3 s, inside the endpoint's 30/min limit) and the ranks agree to drop the stale job — one
+  GPU sweeps a timestamp's whole 2^32 nonces in ~0.12 s, so mining on an old tip for up to 90 s
+  would waste almost all of the work after a competing block arrives.
 """
 from __future__ import annotations
 
@@ -18,6 +22,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import httpx
@@ -30,6 +35,32 @@ from .utils.codec import timestamp
 def fetch_mining_info(node_url: str) -> dict:
     r = httpx.get(node_url + 'get_mining_info', timeout=5)
     return r.json()['result']
+
+
+class TipWatcher:
+    """Background poll of the node's tip (rank 0 only). ``moved(prev)`` is True once the node reports
+    a last block whose hash differs from the job's previous hash."""
+
+    def __init__(self, node_url: str, interval: float, fetch=fetch_mining_info):
+        self.node_url, self.interval, self.fetch = node_url, interval, fetch
+        self.tip = None
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, name='upow-tip-watch', daemon=True)
+        self._t.start()
+
+    def _run(self):
+        while not self._stop.wait(self.interval):
+            try:
+                self.tip = self.fetch(self.node_url)['last_block'].get('hash', GENESIS_PREV_HASH)
+            except Exception:
+                pass
+
+    def moved(self, prev: str) -> bool:
+        return self.tip is not None and self.tip != prev
+
+    def close(self):
+        self._stop.set()
+        self._t.join(timeout=5)
 
 
 def submit(node_url: str, header: bytes, hashes, block_no: int) -> dict:
@@ -45,6 +76,7 @@ def main(argv=None):
     ap.add_argument('node_url', nargs='?', default=None)
     ap.add_argument('--device', choices=['gpu', 'cpu'], default=None)
     ap.add_argument('--refresh', type=float, default=90.0)
+    ap.add_argument('--poll', type=float, default=3.0, help='tip poll period in seconds (0 = off)')
     ap.add_argument('--chunk', type=int, default=1 << 28)
     ap.add_argument('--extranonce', action='store_true',
                     help='also vary the (unchecked) header difficulty field once timestamps are exhausted')
@@ -61,6 +93,7 @@ def main(argv=None):
     device = a.device or ('gpu' if gpu_available() else 'cpu')
     kw = {} if device == 'gpu' else {'threads': max(1, a.workers)}
     accepted = 0
+    watcher = TipWatcher(node_url, a.poll) if (ctx.is_main and a.poll > 0) else None
     try:
         while True:
             job = None
@@ -89,7 +122,10 @@ def main(argv=None):
             miner = ClusterMiner(ctx, prev, a.address, merkle, job['difficulty'], ts_max=now, ts_min=ts_min,
                                  extranonce=a.extranonce, device=device, chunk=a.chunk, **kw)
             t0 = time.time()
-            header = miner.mine(should_stop=lambda: time.time() - t0 > a.refresh)
+            if watcher is not None:
+                watcher.tip = None  # only polls made during this job count
+            header = miner.mine(should_stop=lambda: time.time() - t0 > a.refresh or
+                                (watcher is not None and watcher.moved(prev)))
             dt = max(time.time() - t0, 1e-9)
             rate = ctx.allreduce_sum(miner.hashes) / dt
             if ctx.is_main:
@@ -109,6 +145,8 @@ def main(argv=None):
             if a.blocks and accepted >= a.blocks:
                 break
     finally:
+        if watcher is not None:
+            watcher.close()
         shutdown(ctx)
 
 
