@@ -562,6 +562,11 @@ class Database:
     async def get_need_propagate_transactions(self, last_propagation_delta: int = 600,
                                               limit: int = MAX_BLOCK_SIZE_HEX) -> List[str]:
         now = int(_utcnow().replace(tzinfo=timezone.utc).timestamp())
+        # the node's middleware asks this on EVERY request: only stale txs can be returned, so when no
+        # pending tx is older than the delta the answer is [] without ordering the whole mempool
+        if self._q1('SELECT 1 FROM pending_transactions WHERE propagation_time < ? LIMIT 1',
+                    (now - last_propagation_delta,)) is None:
+            return []
         return_txs, size = [], 0
         for r in self._pending_rows_ordered():
             tx_hex = r['tx_hex']

@@ -53,22 +53,47 @@ class NodesManager:
             NodesManager.async_client = httpx.AsyncClient(timeout=NodesManager.timeout, follow_redirects=True)
         return NodesManager.async_client
 
+    _stamp = None   # (mtime_ns, size, inode) of nodes.json as last read or written by this process
+    _written = None  # (nodes, last_messages) as last written by this process
+
+    @staticmethod
+    def _file_stamp():
+        try:
+            st = os.stat(NodesManager.path)
+            return st.st_mtime_ns, st.st_size, st.st_ino
+        except OSError:
+            return None
+
     @staticmethod
     def init(path: Optional[str] = None):
+        """(Re)load nodes.json. The node calls this on every request (as the reference does with
+        pickledb); the file is only re-read when it changed on disk since this process last read or
+        wrote it, so another process sharing the peer table is still seen at once."""
         if path is not None or NodesManager.path is None:
             NodesManager.path = path or config.data_path('nodes.json')
+            NodesManager._stamp = None
+        if NodesManager._stamp is not None and NodesManager.db is not None and \
+                NodesManager._file_stamp() == NodesManager._stamp:
+            return
         with _file_lock(NodesManager.path):
             NodesManager.db = JsonStore(NodesManager.path, auto_dump=False)
             core = NodesManager._core_url()
             NodesManager.nodes = NodesManager.db.get('nodes') or ([core] if core else [])
             NodesManager.last_messages = NodesManager.db.get('last_messages') or ({core: timestamp()} if core else {})
+            NodesManager._stamp = NodesManager._file_stamp()
 
     @staticmethod
     def sync():
+        """Write the peer table back, skipped when nothing changed since this process's last write."""
+        state = (list(NodesManager.nodes), dict(NodesManager.last_messages))
+        if state == NodesManager._written and NodesManager._file_stamp() == NodesManager._stamp:
+            return
         with _file_lock(NodesManager.path):
             NodesManager.db.set('nodes', NodesManager.nodes)
             NodesManager.db.set('last_messages', NodesManager.last_messages)
             NodesManager.db.dump()
+            NodesManager._stamp = NodesManager._file_stamp()
+            NodesManager._written = state
 
     @staticmethod
     async def request(url: str, method: str = 'GET', **kwargs):
