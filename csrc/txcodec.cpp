@@ -561,38 +561,9 @@ static py::tuple input_address_strings(py::bytes addrs64, py::bytes lens, py::by
     return json.py();
 }
 
-// ---- row builders for the bulk ledger writes (ledger/fastpath.py): Python tuples built in C++
+// ---- column helpers for the bulk ledger writes (ledger/fastpath.py)
 
 // (tx_hash hex, index) for 40-byte key records
-static py::list outpoint_rows(py::bytes keys_b) {
-    std::string k = keys_b;
-    if (k.size() % 40) throw std::invalid_argument("key records must be n x 40 bytes");
-    const size_t n = k.size() / 40;
-    py::list out(n);
-    for (size_t i = 0; i < n; ++i) {
-        const uint8_t* r = reinterpret_cast<const uint8_t*>(k.data()) + 40 * i;
-        out[i] = py::make_tuple(py::str(to_hex(r, 32)), int(r[32]));
-    }
-    return out;
-}
-
-// (tx_hash, index within tx, address string, is_stake=0) for every output
-static py::list output_rows(py::list tx_hashes, py::bytes out_tx_b, py::bytes out_start_b, py::list out_addr) {
-    std::string ot = out_tx_b, os = out_start_b;
-    const int32_t* tx = reinterpret_cast<const int32_t*>(ot.data());
-    const int32_t* st = reinterpret_cast<const int32_t*>(os.data());
-    const size_t n = ot.size() / 4;
-    if (out_addr.size() != n) throw std::invalid_argument("out_addr length");
-    py::list out(n);
-    py::int_ zero(0);
-    for (size_t o = 0; o < n; ++o) {
-        const int32_t t = tx[o];
-        if (t < 0 || size_t(t) >= tx_hashes.size()) throw std::out_of_range("out_tx");
-        out[o] = py::make_tuple(tx_hashes[size_t(t)], int(int32_t(o) - st[t]), out_addr[o], zero);
-    }
-    return out;
-}
-
 // numeric(Decimal(fee) / 10**8, 6): fee in smallest units rounded half up to 6 decimals
 static py::list fee_strings(py::bytes fee_b) {
     std::string f = fee_b;
@@ -655,8 +626,6 @@ static py::tuple unique_rows(py::buffer buf, int width) {
 }
 
 void register_txcodec(py::module_& m) {
-    m.def("outpoint_rows", &outpoint_rows);
-    m.def("output_rows", &output_rows);
     m.def("fee_strings", &fee_strings);
     m.def("unique_rows", &unique_rows, py::arg("buf"), py::arg("width"),
           "(unique rows in first-seen order, inverse int32) of an n x width byte matrix");
