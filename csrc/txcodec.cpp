@@ -563,7 +563,6 @@ static py::tuple input_address_strings(py::bytes addrs64, py::bytes lens, py::by
 
 // ---- column helpers for the bulk ledger writes (ledger/fastpath.py)
 
-// (tx_hash hex, index) for 40-byte key records
 // numeric(Decimal(fee) / 10**8, 6): fee in smallest units rounded half up to 6 decimals
 static py::list fee_strings(py::bytes fee_b) {
     std::string f = fee_b;
