@@ -229,10 +229,25 @@ async def _sync_blockchain(node_url: str = None):
                         await cluster.mirror_rollback(db, last_common_block + 1)
                     break
     limit = 1000
+    prefetch = None  # (offset, task): the next page, fetched over HTTP while this one is applied
+
+    def drop_prefetch():
+        nonlocal prefetch
+        if prefetch is not None:
+            prefetch[1].cancel()
+            prefetch[1].add_done_callback(lambda t: t.cancelled() or t.exception())
+            prefetch = None
+
     while True:
         i = await db.get_next_block_id()
         try:
-            blocks = await node_interface.get_blocks(i, limit)
+            if prefetch is not None and prefetch[0] == i:
+                task = prefetch[1]
+                prefetch = None
+                blocks = await task
+            else:
+                drop_prefetch()
+                blocks = await node_interface.get_blocks(i, limit)
         except Exception as e:
             logger.error(e)
             NodesManager.sync()
@@ -248,8 +263,11 @@ async def _sync_blockchain(node_url: str = None):
                         await propagate('push_block', {'block_content': last_block['content'], 'txs': txs_hashes,
                                                        'block_no': last_block['id']}, node_url)
                 return True
+            nxt = i + len(blocks)
+            prefetch = (nxt, asyncio.ensure_future(node_interface.get_blocks(nxt, limit)))
             assert await create_blocks(blocks, error_list=error)
         except Exception as e:
+            drop_prefetch()
             logger.error(error[0] if error else e)
             if local_cache is not None:
                 logger.info('sync failed, reverting back to previous chain')
