@@ -427,6 +427,16 @@ class Database:
         if not outputs:
             return []
         want = {(str(h), int(i)) for h, i in outputs}
+        if len(want) <= 32:
+            # a single tx's inputs (mempool admission): exact (tx_hash, index) probes on the outpoint
+            # index, instead of pulling every row of each funding tx (often hundreds) into Python
+            found = []
+            with self.lock:
+                for h, i in want:
+                    for r in self.conn.execute(f'SELECT rowid FROM {table} WHERE tx_hash = ? AND "index" = ?', (h, i)):
+                        found.append((r[0], (h, i)))
+            found.sort()
+            return [o for _, o in found]
         hashes = sorted({h for h, _ in want})
         out = []
         for k in range(0, len(hashes), 500):
