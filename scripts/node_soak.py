@@ -66,8 +66,9 @@ def main():
     url = f'http://127.0.0.1:{port}'
     env = dict(os.environ, UPOW_DATA_DIR=data, UPOW_CORE_URL='', UPOW_START_DIFFICULTY=a.difficulty,
                UPOW_RATE_LIMIT='0', PYTHONPATH=ROOT, UPOW_LOG_LEVEL='WARNING', UPOW_SNAPSHOT='0')
-    prof = ['-m', 'cProfile', '-o', os.path.join(data, 'node.prof')] if os.environ.get('UPOW_SOAK_PROFILE') == '1' else []
-    node = subprocess.Popen([sys.executable, *prof, '-m', 'upow_amd.node', '--host', '127.0.0.1', '--port', str(port),
+    if os.environ.get('UPOW_SOAK_PROFILE') == '1':
+        env['UPOW_PROFILE_OUT'] = os.path.join(data, 'node.prof')
+    node = subprocess.Popen([sys.executable, '-m', 'upow_amd.node', '--host', '127.0.0.1', '--port', str(port),
                              '--log-level', 'warning'], env=env, cwd=ROOT, stdout=open(os.path.join(data, 'node.log'), 'w'),
                             stderr=subprocess.STDOUT)
     client = httpx.Client(timeout=30)

@@ -24,6 +24,23 @@ def main(argv=None):
     import uvicorn
     if a.cluster and int(os.environ.get('WORLD_SIZE', '1')) > 1:
         return _run_cluster(a)
+    prof_out = os.environ.get('UPOW_PROFILE_OUT')  # cProfile of the serving process (load tests)
+    if prof_out:
+        import cProfile
+        import signal
+        import sys
+        prof = cProfile.Profile()
+
+        def dump(*_):
+            prof.disable()
+            prof.dump_stats(prof_out)
+            sys.exit(0)
+
+        # uvicorn re-raises the SIGTERM it caught once the graceful shutdown is done: dump there
+        signal.signal(signal.SIGTERM, dump)
+        prof.enable()
+        uvicorn.run('upow_amd.node.main:app', host=a.host, port=a.port, log_level=a.log_level)
+        dump()
     uvicorn.run('upow_amd.node.main:app', host=a.host, port=a.port, log_level=a.log_level)
 
 
