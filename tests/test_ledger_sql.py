@@ -84,3 +84,42 @@ def test_native_writes_join_the_open_transaction():
     with db.transaction():
         db.bulk('INSERT INTO x VALUES (?)', [np.arange(3, dtype=np.int64)], 3)
     assert db._q1('SELECT COUNT(*) FROM x')[0] == 3
+
+
+def test_small_outpoint_lookups_via_sql_match_index():
+    """GPU-backend nodes answer a single tx's outpoint lookups from SQLite (no device round trip);
+    the answer must equal the UTXO index's for every table, including absent and repeated keys."""
+    import asyncio
+    import random
+    from decimal import Decimal
+
+    from upow_amd import devnet
+    from upow_amd.ledger import manager
+    from upow_amd.ledger.database import OUTPUT_TABLES
+    from upow_amd.ledger.utxo import TAG_BY_TABLE
+    from upow_amd.wallet.builders import address_of
+
+    async def go():
+        db = await Database.create(utxo_backend='host')
+        manager.Manager.difficulty = None
+        manager.START_DIFFICULTY, saved = Decimal('1.0'), manager.START_DIFFICULTY
+        try:
+            for b in range(4):
+                await devnet.mine_block(address_of(0xABC), ts=1_700_000_000 + 60 * b, device='cpu')
+        finally:
+            manager.START_DIFFICULTY = saved
+        live = [(r[0], r[1]) for r in db._q('SELECT tx_hash, "index" FROM unspent_outputs')]
+        rng = random.Random(3)
+        for _ in range(40):
+            req = rng.sample(live, min(len(live), rng.randint(0, 3))) + [('ef' * 32, rng.randint(0, 3))]
+            req += req[:1]  # a repeated key
+            rng.shuffle(req)
+            for table in OUTPUT_TABLES:
+                want = db.utxo.filter(req, TAG_BY_TABLE[table])
+                db.utxo.backend_name = 'gpu'  # take the SQL branch
+                try:
+                    got = db._filter_outputs(table, req)
+                finally:
+                    db.utxo.backend_name = 'host'
+                assert got == want, (table, req)
+    asyncio.run(go())

@@ -1096,24 +1096,36 @@ class Database:
         logger.info(f'Successfully removed {len(inputs)} pending_spent_outputs in {perf_counter() - start:.3f} seconds')
         return True
 
-    # lookups (database.py:788-825); the HBM/host index answers these without SQL
+    # lookups (database.py:788-825): a block's outpoints go to the HBM/host index in one batch; a
+    # handful of them (one tx at /push_tx) on the GPU backend go to SQLite's outpoint index instead —
+    # a device round trip costs ~1 ms when the card is busy (a co-located miner keeps every CU
+    # occupied), an indexed probe ~5 us, and both hold the same set.
+    SMALL_LOOKUP = 16
+
+    def _filter_outputs(self, table: str, outputs):
+        if len(outputs) > self.SMALL_LOOKUP or self.utxo.backend_name != 'gpu':
+            return self.utxo.filter(outputs, TAG_BY_TABLE[table])
+        uniq = list(dict.fromkeys((h, int(i)) for h, i in outputs))
+        found = set(self._select_outpoints(table, uniq))
+        return [k for k in uniq if k in found]  # the index's answer order: unique, first seen
+
     async def get_unspent_outputs(self, outputs):
-        return self.utxo.filter(outputs, TAG_BY_TABLE['unspent_outputs'])
+        return self._filter_outputs('unspent_outputs', outputs)
 
     async def get_inode_outputs(self, outputs):
-        return self.utxo.filter(outputs, TAG_BY_TABLE['inode_registration_output'])
+        return self._filter_outputs('inode_registration_output', outputs)
 
     async def get_validator_voting_power_outputs(self, outputs):
-        return self.utxo.filter(outputs, TAG_BY_TABLE['validators_voting_power'])
+        return self._filter_outputs('validators_voting_power', outputs)
 
     async def get_delegates_voting_power_outputs(self, outputs):
-        return self.utxo.filter(outputs, TAG_BY_TABLE['delegates_voting_power'])
+        return self._filter_outputs('delegates_voting_power', outputs)
 
     async def get_inodes_ballot_outputs(self, outputs):
-        return self.utxo.filter(outputs, TAG_BY_TABLE['inodes_ballot'])
+        return self._filter_outputs('inodes_ballot', outputs)
 
     async def get_validators_ballot_outputs(self, outputs):
-        return self.utxo.filter(outputs, TAG_BY_TABLE['validators_ballot'])
+        return self._filter_outputs('validators_ballot', outputs)
 
     async def get_unspent_outputs_hash(self) -> str:
         """database.py:827-830: SHA256 over (tx_hash bytes || index byte) sorted by (tx_hash, index).
