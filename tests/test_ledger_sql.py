@@ -123,3 +123,27 @@ def test_small_outpoint_lookups_via_sql_match_index():
                     db.utxo.backend_name = 'host'
                 assert got == want, (table, req)
     asyncio.run(go())
+
+
+def test_block_trace_file(tmp_path, monkeypatch):
+    """UPOW_TRACE_FILE: one JSON line per validated block with the stage timings."""
+    import asyncio
+    import json
+    from decimal import Decimal
+
+    from upow_amd import devnet
+    from upow_amd.ledger import manager
+    from upow_amd.wallet.builders import address_of
+    trace = tmp_path / 'blocks.jsonl'
+    monkeypatch.setattr(manager, '_TRACE_PATH', str(trace))
+    monkeypatch.setattr(manager, 'START_DIFFICULTY', Decimal('1.0'))
+
+    async def go():
+        await Database.create(utxo_backend='host')
+        manager.Manager.difficulty = None
+        for b in range(3):
+            await devnet.mine_block(address_of(0x5EED), ts=1_700_000_000 + 60 * b, device='cpu')
+    asyncio.run(go())
+    recs = [json.loads(ln) for ln in trace.read_text().splitlines()]
+    assert len(recs) == 3 and all(r['ok'] for r in recs)
+    assert [r['height'] for r in recs] == [1, 2, 3] and all('ms' in r and 'stages_ms' in r for r in recs)

@@ -419,7 +419,31 @@ async def create_block(block_content: str, transactions: List[Transaction], last
         return ok
 
 
+_TRACE_PATH = os.environ.get('UPOW_TRACE_FILE')  # JSON-lines block trace (one record per block)
+
+
+def _trace_block(ok: bool, seconds: float, n_txs: int, path: str):
+    """Append one record per validated block: verdict, path, tip, and the per-stage wall times the
+    native path / batched validator recorded (decode, HBM UTXO pass, decompression, ECDSA, ledger
+    writes, commit). Off unless ``UPOW_TRACE_FILE`` is set."""
+    if not _TRACE_PATH:
+        return
+    import json
+    import time as _time
+    from . import fastpath, validate
+    stages = {k: round(v * 1000, 3) for k, v in {**last_block_timings, **validate.timings, **fastpath.timings}.items()
+              if k.endswith('_s') and isinstance(v, float)}
+    rec = {'t': round(_time.time(), 3), 'ok': ok, 'path': path, 'txs': n_txs, 'ms': round(seconds * 1000, 3),
+           'height': Database.instance._tip_id() if Database.instance else None, 'stages_ms': stages}
+    try:
+        with open(_TRACE_PATH, 'a') as f:
+            f.write(json.dumps(rec) + '\n')
+    except OSError as e:
+        logger.error(f'block trace write failed: {e}')
+
+
 def _record_block_metrics(ok: bool, seconds: float, n_txs: int, path: str):
+    _trace_block(ok, seconds, n_txs, path)
     if ok:
         metrics.inc('upow_blocks_applied_total', labels={'path': path}, help='blocks validated and applied')
         metrics.inc('upow_transactions_applied_total', n_txs, help='non-coinbase transactions applied')
