@@ -1,6 +1,8 @@
 // Base58 (Bitcoin alphabet) codec for the 33-byte compressed addresses (reference: the `base58`
 // package used by upow/helpers.py:171-188). Host C++; the node converts addresses for every output
 // it parses and every input it stores, so this sits on the block-apply path.
+#include <algorithm>
+#include <array>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -10,59 +12,99 @@ namespace upow {
 
 static const char* kB58 = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz";
 
+// Base conversion 2^32 -> 58^5 on 32-bit limbs: each input word is multiplied into the accumulated
+// number with one 64-bit carry chain, so a 33-byte address takes ~9 x 9 limb steps instead of the
+// ~33 x 45 digit steps of the schoolbook byte loop (the division is by a constant: a multiply-high).
 std::string b58encode(const uint8_t* data, size_t n) {
+    constexpr uint64_t kBase = 656356768ull;  // 58^5 < 2^32
     size_t zeros = 0;
     while (zeros < n && data[zeros] == 0) ++zeros;
-    // big-number base conversion 256 -> 58 (log(256)/log(58) ~ 1.366)
-    std::vector<uint8_t> digits((n - zeros) * 138 / 100 + 1, 0);
+    const size_t m = n - zeros;
+    // ceil(m * 8 / log2(58^5)) limbs, log2(58^5) ~ 29.29
+    std::vector<uint32_t> limbs(m * 8 / 29 + 2, 0);  // little-endian, base 58^5
     size_t len = 0;
-    for (size_t i = zeros; i < n; ++i) {
-        uint32_t carry = data[i];
-        size_t j = 0;
-        for (auto it = digits.rbegin(); (carry != 0 || j < len) && it != digits.rend(); ++it, ++j) {
-            carry += 256u * (*it);
-            *it = uint8_t(carry % 58);
-            carry /= 58;
+    const uint8_t* p = data + zeros;
+    size_t head = m % 4 ? m % 4 : 4;  // the first word takes the leading m mod 4 bytes
+    for (size_t i = 0; i < m;) {
+        const size_t take = i == 0 ? std::min(head, m) : 4;
+        uint64_t carry = 0;
+        for (size_t k = 0; k < take; ++k) carry = (carry << 8) | p[i + k];
+        const unsigned shift = unsigned(8 * take);
+        for (size_t j = 0; j < len; ++j) {
+            carry += uint64_t(limbs[j]) << shift;
+            limbs[j] = uint32_t(carry % kBase);
+            carry /= kBase;
         }
-        len = j;
+        while (carry) {
+            limbs[len++] = uint32_t(carry % kBase);
+            carry /= kBase;
+        }
+        i += take;
     }
-    auto it = digits.begin() + (digits.size() - len);
-    while (it != digits.end() && *it == 0) ++it;
     std::string out(zeros, '1');
-    for (; it != digits.end(); ++it) out.push_back(kB58[*it]);
+    char buf[5];
+    bool lead = true;
+    for (size_t j = len; j-- > 0;) {
+        uint32_t v = limbs[j];
+        for (int k = 4; k >= 0; --k) {
+            buf[k] = kB58[v % 58];
+            v /= 58;
+        }
+        for (int k = 0; k < 5; ++k) {
+            if (lead && buf[k] == '1') continue;  // leading zero digits of the top limb
+            lead = false;
+            out.push_back(buf[k]);
+        }
+    }
     return out;
 }
 
-std::vector<uint8_t> b58decode(const std::string& s_in) {
-    static int8_t map[256];
-    static bool init = false;
-    if (!init) {
-        for (int i = 0; i < 256; ++i) map[i] = -1;
-        for (int i = 0; i < 58; ++i) map[uint8_t(kB58[i])] = int8_t(i);
-        init = true;
-    }
-    std::string s = s_in;
-    while (!s.empty() && (s.back() == ' ' || s.back() == '\n' || s.back() == '\t' || s.back() == '\r')) s.pop_back();
+// The inverse conversion 58^5 -> 2^32: five digits at a time are folded into 32-bit limbs with one
+// 64-bit carry chain (58^5 < 2^30, so limb * 58^5 + carry stays below 2^62). The digit table is a
+// function-local static, so concurrent first calls from the host pool are race-free.
+std::vector<uint8_t> b58decode(const std::string& s) {
+    static const std::array<int8_t, 256> map = [] {
+        std::array<int8_t, 256> m{};
+        m.fill(-1);
+        for (int i = 0; i < 58; ++i) m[uint8_t(kB58[i])] = int8_t(i);
+        return m;
+    }();
+    size_t end = s.size();
+    while (end > 0 && (s[end - 1] == ' ' || s[end - 1] == '\n' || s[end - 1] == '\t' || s[end - 1] == '\r')) --end;
     size_t zeros = 0;
-    while (zeros < s.size() && s[zeros] == '1') ++zeros;
-    std::vector<uint8_t> b256((s.size() - zeros) * 733 / 1000 + 1, 0);
+    while (zeros < end && s[zeros] == '1') ++zeros;
+    const size_t m = end - zeros;
+    std::vector<uint32_t> limbs(m * 6 / 32 + 2, 0);  // log2(58) < 6 bits per digit; little-endian
     size_t len = 0;
-    for (size_t i = zeros; i < s.size(); ++i) {
-        int v = map[uint8_t(s[i])];
-        if (v < 0) throw std::invalid_argument(std::string("Invalid character '") + s[i] + "'");
-        uint32_t carry = uint32_t(v);
-        size_t j = 0;
-        for (auto it = b256.rbegin(); (carry != 0 || j < len) && it != b256.rend(); ++it, ++j) {
-            carry += 58u * (*it);
-            *it = uint8_t(carry & 0xff);
-            carry >>= 8;
+    for (size_t i = zeros; i < end;) {
+        const size_t take = i == zeros && m % 5 ? m % 5 : 5;
+        uint64_t carry = 0, mul = 1;
+        for (size_t k = 0; k < take; ++k) {
+            const int v = map[uint8_t(s[i + k])];
+            if (v < 0) throw std::invalid_argument(std::string("Invalid character '") + s[i + k] + "'");
+            carry = carry * 58 + uint64_t(v);
+            mul *= 58;
         }
-        len = j;
+        for (size_t j = 0; j < len; ++j) {
+            carry += uint64_t(limbs[j]) * mul;
+            limbs[j] = uint32_t(carry);
+            carry >>= 32;
+        }
+        while (carry) {
+            limbs[len++] = uint32_t(carry);
+            carry >>= 32;
+        }
+        i += take;
     }
-    auto it = b256.begin() + (b256.size() - len);
-    while (it != b256.end() && *it == 0) ++it;
     std::vector<uint8_t> out(zeros, 0);
-    out.insert(out.end(), it, b256.end());
+    out.reserve(zeros + 4 * len);
+    for (size_t j = len; j-- > 0;) {
+        for (int k = 3; k >= 0; --k) {
+            const uint8_t b = uint8_t(limbs[j] >> (8 * k));
+            if (b == 0 && j == len - 1 && out.size() == zeros) continue;  // leading zero bytes of the top limb
+            out.push_back(b);
+        }
+    }
     return out;
 }
 
