@@ -236,6 +236,18 @@ PYBIND11_MODULE(_native, m) {
         { py::gil_scoped_release rel; d = utxo_set_hash(h, tag, &n); }
         return py::make_tuple(py::bytes(reinterpret_cast<const char*>(d.data()), d.size()), n);
     });
+    m.def("utxo_address_scan", [](int64_t h, py::bytes addr, uint32_t tag_mask) {
+        std::string a = addr;
+        std::vector<uint8_t> o, pay;
+        uint64_t total = 0;
+        {
+            py::gil_scoped_release rel;
+            o = utxo_address_scan(h, reinterpret_cast<const uint8_t*>(a.data()), uint32_t(a.size()), tag_mask, pay,
+                                  &total);
+        }
+        return py::make_tuple(py::bytes(reinterpret_cast<const char*>(o.data()), o.size()),
+                              py::bytes(reinterpret_cast<const char*>(pay.data()), pay.size()), total);
+    });
     m.def("utxo_dump_payload", [](int64_t h) {
         std::vector<uint8_t> o, pay;
         { py::gil_scoped_release rel; o = utxo_dump(h, &pay); }

@@ -224,6 +224,57 @@ __global__ __launch_bounds__(256) void utxo_dump_kernel(const UtxoSlot* __restri
     if (pay_out) pay_out[o] = pay[s];
 }
 
+
+// K14: outputs owned by one address (reference `database.py:909-937,1138-1205`: balance / spendable
+// outputs by address). One lane per slot streams the key metas and, for live slots whose tag is in
+// `tag_mask`, the 80-byte payload line; the address is compared as four 16-byte vectors held in SGPRs
+// (the query is uniform). Matches are rare, so they are compacted with one atomic each; the amount sum
+// is a wave reduction + one 64-bit atomic per wave that found anything.
+__global__ __launch_bounds__(256) void utxo_address_scan_kernel(const UtxoSlot* __restrict__ tab,
+                                                                const UtxoPayload* __restrict__ pay, uint32_t cap,
+                                                                uint4 q0, uint4 q1, uint4 q2, uint4 q3, uint32_t qlen,
+                                                                uint32_t tag_mask, uint32_t max_out,
+                                                                UtxoKeyRec* __restrict__ out,
+                                                                UtxoPayload* __restrict__ pay_out,
+                                                                uint32_t* __restrict__ count,
+                                                                unsigned long long* __restrict__ total) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t amt = 0;
+    if (s < cap) {
+        const uint32_t m = tab[s].meta;
+        const uint32_t tag = (m >> 16) & 0xffu;
+        if ((m & 3u) == ST_FULL && tag < 32u && ((tag_mask >> tag) & 1u) && pay[s].addr_len == qlen) {
+            const uint4* a = reinterpret_cast<const uint4*>(pay[s].addr);
+            const uint4 a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
+            const uint32_t d = (a0.x ^ q0.x) | (a0.y ^ q0.y) | (a0.z ^ q0.z) | (a0.w ^ q0.w) | (a1.x ^ q1.x) |
+                               (a1.y ^ q1.y) | (a1.z ^ q1.z) | (a1.w ^ q1.w) | (a2.x ^ q2.x) | (a2.y ^ q2.y) |
+                               (a2.z ^ q2.z) | (a2.w ^ q2.w) | (a3.x ^ q3.x) | (a3.y ^ q3.y) | (a3.z ^ q3.z) |
+                               (a3.w ^ q3.w);
+            if (d == 0) {
+                amt = pay[s].amount;
+                const uint32_t o = atomicAdd(count, 1u);
+                if (o < max_out) {
+                    UtxoKeyRec r;
+#pragma unroll
+                    for (int w = 0; w < 8; ++w) {
+                        r.txid[4 * w] = uint8_t(tab[s].k[w]);
+                        r.txid[4 * w + 1] = uint8_t(tab[s].k[w] >> 8);
+                        r.txid[4 * w + 2] = uint8_t(tab[s].k[w] >> 16);
+                        r.txid[4 * w + 3] = uint8_t(tab[s].k[w] >> 24);
+                    }
+                    r.index = (m >> 8) & 0xffu;
+                    r.tag = tag;
+                    out[o] = r;
+                    pay_out[o] = pay[s];
+                }
+            }
+        }
+    }
+    // wave64 sum: amounts are < 2^63 in total (MAX_SUPPLY in smallest units fits in 2^51)
+    for (int off = 32; off > 0; off >>= 1) amt += __shfl_down(amt, off, 64);
+    if ((threadIdx.x & 63u) == 0 && amt) atomicAdd(total, static_cast<unsigned long long>(amt));
+}
+
 // ------------------------------------------------------------------------------------------------
 static void uck(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
@@ -347,6 +398,43 @@ std::vector<uint8_t> utxo_erase(int64_t h, const uint8_t* recs, int64_t n) {
     uck(hipGetLastError(), "utxo_erase_kernel");
     uck(hipMemcpy(out.data(), o.p, size_t(n), hipMemcpyDeviceToHost), "d2h erased");
     return out;
+}
+
+std::vector<uint8_t> utxo_address_scan(int64_t h, const uint8_t* addr, uint32_t len, uint32_t tag_mask,
+                                       std::vector<uint8_t>& payload_out, uint64_t* total_out) {
+    if (len > 64) throw std::invalid_argument("address is at most 64 bytes");
+    std::lock_guard<std::mutex> lk(g_ut_mu);
+    UtxoTableDev& t = table(h);
+    uint4 q[4];
+    std::memset(q, 0, sizeof(q));
+    std::memcpy(q, addr, len);  // payload addresses are zero-padded to 64 bytes
+    // first pass sizes the output; a second pass runs only if more matches than the guess came back
+    uint32_t cap_out = 4096, n = 0;
+    DevBuf<unsigned long long> dt(1);
+    for (int pass = 0; pass < 2; ++pass) {
+        DevBuf<UtxoKeyRec> d(cap_out);
+        DevBuf<UtxoPayload> dp(cap_out);
+        uck(hipMemset(t.d_counter, 0, sizeof(uint32_t)), "memset");
+        uck(hipMemset(dt.p, 0, sizeof(unsigned long long)), "memset");
+        hipLaunchKernelGGL(utxo_address_scan_kernel, dim3(int((t.cap + 255) / 256)), dim3(256), 0, 0, t.tab, t.pay,
+                           t.cap, q[0], q[1], q[2], q[3], len, tag_mask, cap_out, d.p, dp.p, t.d_counter, dt.p);
+        uck(hipGetLastError(), "utxo_address_scan_kernel");
+        uck(hipMemcpy(&n, t.d_counter, sizeof(uint32_t), hipMemcpyDeviceToHost), "d2h n");
+        if (n <= cap_out) {
+            unsigned long long tot = 0;
+            uck(hipMemcpy(&tot, dt.p, sizeof(tot), hipMemcpyDeviceToHost), "d2h total");
+            *total_out = tot;
+            std::vector<uint8_t> out(size_t(n) * sizeof(UtxoKeyRec));
+            payload_out.assign(size_t(n) * sizeof(UtxoPayload), 0);
+            if (n) {
+                uck(hipMemcpy(out.data(), d.p, out.size(), hipMemcpyDeviceToHost), "d2h recs");
+                uck(hipMemcpy(payload_out.data(), dp.p, payload_out.size(), hipMemcpyDeviceToHost), "d2h payload");
+            }
+            return out;
+        }
+        cap_out = n;
+    }
+    throw std::runtime_error("utxo_address_scan: table changed between passes");
 }
 
 std::vector<uint8_t> utxo_dump(int64_t h, std::vector<uint8_t>* payload_out) {

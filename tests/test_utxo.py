@@ -118,3 +118,58 @@ def test_block_inputs_and_set_hash_gpu_match_host(gpu):
     assert rh[5] == rg[5] == int((rg[2] > 0).sum()) == 4
     for tag in (0, 3, 5):
         assert h.set_hash(tag) == g.set_hash(tag)
+
+
+def _address_case(idx, seed):
+    """3000 outputs over 40 owners (33-byte and 64-byte addresses) in three tables, some spent."""
+    rng = random.Random(seed)
+    owners = [bytes([42 + (k & 1)]) + rng.randbytes(32) if k % 4 else rng.randbytes(64) for k in range(40)]
+    keys = _keys(3000, seed)
+    own = [rng.randrange(40) for _ in keys]
+    amounts = [rng.randrange(1, 1 << 44) for _ in keys]
+    tags = [rng.choice((0, 0, 0, 3, 5)) for _ in keys]
+    for t in (0, 3, 5):
+        sel = [k for k in range(3000) if tags[k] == t]
+        idx.insert([keys[k] for k in sel], t, make_payload([amounts[k] for k in sel], [owners[own[k]] for k in sel]))
+    idx.erase(keys[:300])
+    live = set(range(300, 3000))
+
+    def want(o, tagset):
+        ks = sorted((keys[k][0], keys[k][1]) for k in live if own[k] == o and tags[k] in tagset)
+        amt = {keys[k]: amounts[k] for k in live}
+        return ks, sum(amt[k] for k in ks)
+    return owners, want
+
+
+def _check_address_outputs(idx, owners, want):
+    for o in (0, 1, 2, 3, 17):
+        for tagset in ((0,), (0, 3, 5), (5,)):
+            recs, pay, total = idx.address_outputs(owners[o], tagset)
+            ks, amt = want(o, tagset)
+            got = [(bytes(r[:32]).hex(), int(r[32:36].copy().view(np.uint32)[0])) for r in recs]
+            assert got == ks and total == amt
+            assert all(bytes(p['addr'][:p['len']]) == owners[o] for p in pay)
+    # a 33-byte query never matches a 64-byte address that starts with the same bytes, and vice versa
+    assert len(idx.address_outputs(owners[0][:33], (0, 3, 5))[0]) == 0
+    assert idx.address_outputs(b'\x42' + bytes(32))[2] == 0
+
+
+def test_address_outputs_host():
+    idx = UtxoIndex(backend='host')
+    _check_address_outputs(idx, *_address_case(idx, 21))
+
+
+@pytest.mark.gpu
+def test_address_outputs_gpu_scan(gpu):
+    """K14 utxo_address_scan kernel vs a plain host filter; the device amount sum matches too, and a
+    result larger than the first-pass output buffer (4096) takes the resize pass."""
+    idx = UtxoIndex(backend='gpu')
+    owners, want = _address_case(idx, 21)
+    _check_address_outputs(idx, owners, want)
+    many = _keys(5000, 99)
+    a = bytes([43]) + bytes(range(32))
+    idx.insert(many, 0, make_payload([7] * len(many), [a] * len(many)))
+    raw, pay, total = gpu.utxo_address_scan(idx.be.h, a, 1)
+    assert len(raw) == 40 * 5000 and total == 7 * 5000
+    recs, _, tot = idx.address_outputs(a)
+    assert len(recs) == 5000 and tot == 35000

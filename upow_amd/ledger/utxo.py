@@ -118,6 +118,18 @@ class _HostBackend:
     def records(self) -> np.ndarray:
         return pack_records(list(self.d.keys()), list(self.d.values()))
 
+    def address_scan(self, addr: bytes, tag_mask: int):
+        hits = [k for k, t in self.d.items() if (tag_mask >> t) & 1 and self._addr(self.p.get(k)) == addr]
+        pay = np.frombuffer(b''.join(self.p[k] for k in hits), dtype=PAYLOAD_DTYPE)
+        return pack_records(hits, [self.d[k] for k in hits]), pay
+
+    @staticmethod
+    def _addr(raw: Optional[bytes]) -> bytes:
+        if not raw:
+            return b''
+        n = int.from_bytes(raw[8:12], 'little')
+        return raw[16:16 + n]
+
     def records_payload(self):
         keys = list(self.d.keys())
         pay = np.frombuffer(b''.join(self.p.get(k, bytes(80)) for k in keys), dtype=PAYLOAD_DTYPE)
@@ -210,6 +222,10 @@ class _GpuBackend:
     def records(self) -> np.ndarray:
         return np.frombuffer(self.L.utxo_dump(self.h), dtype=np.uint8).reshape(-1, 40)
 
+    def address_scan(self, addr: bytes, tag_mask: int):
+        raw, pay, _total = self.L.utxo_address_scan(self.h, addr, tag_mask)
+        return np.frombuffer(raw, dtype=np.uint8).reshape(-1, 40), np.frombuffer(pay, dtype=PAYLOAD_DTYPE)
+
     def records_payload(self):
         raw, pay = self.L.utxo_dump_payload(self.h)
         return np.frombuffer(raw, dtype=np.uint8).reshape(-1, 40), np.frombuffer(pay, dtype=PAYLOAD_DTYPE)
@@ -295,6 +311,19 @@ class UtxoIndex:
     def records(self) -> np.ndarray:
         """All live entries as 40-byte records, in canonical (txid, index) order."""
         return sort_records(np.ascontiguousarray(self.be.records()))
+
+    def address_outputs(self, addr: bytes, tags: Iterable[int] = (0,)):
+        """K14 (reference ``database.py:909-937,1138-1205``): the live outpoints whose payload address is
+        ``addr`` (raw 33/64 bytes, prefix normalised as stored) in the given tables, as (records, payloads)
+        in canonical (txid, index) order, plus their amount sum in smallest units. GPU backend: one
+        ``utxo_address_scan`` launch over the HBM table instead of an index walk."""
+        mask = 0
+        for t in tags:
+            mask |= 1 << int(t)
+        recs, pay = self.be.address_scan(bytes(addr), mask)
+        order = sort_order(np.ascontiguousarray(recs))
+        recs, pay = np.ascontiguousarray(recs[order]), np.ascontiguousarray(pay[order])
+        return recs, pay, int(pay['amount'].sum()) if len(pay) else 0
 
     def records_payload(self):
         """(records, payloads) of every live entry, in canonical (txid, index) order."""
