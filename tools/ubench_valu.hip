@@ -25,8 +25,13 @@ __global__ __launch_bounds__(256) void k(unsigned* out, unsigned seed, int iters
     if (OP == 7) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(x) : "v"(b), "v"(c)); \
     if (OP == 8) asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(x) : "v"(b)); \
     if (OP == 9) asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(x) : "v"(b), "v"(c)); \
-    if (OP == 10) asm volatile("v_mad_u64_u32 %0, s[0:1], %1, %2, %0" : "+v"(*(unsigned long long*)&x) : "v"(b), "v"(c) : "s0", "s1");
-            if (OP == 10) { STEP(a0) STEP(a2) STEP(a4) STEP(a6) }
+    if (OP == 10) asm volatile("v_mad_u64_u32 %0, s[0:1], %1, %2, %0" : "+v"(*(unsigned long long*)&x) : "v"(b), "v"(c) : "s0", "s1"); \
+    if (OP == 11) asm volatile("v_lshrrev_b64 %0, 7, %0" : "+v"(*(unsigned long long*)&x)); \
+    if (OP == 12) asm volatile("v_alignbyte_b32 %0, %0, %1, 3" : "+v"(x) : "v"(b)); \
+    if (OP == 13) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(x) : "v"(b), "v"(c)); \
+    if (OP == 14) asm volatile("v_pk_mov_b32 %0, %0, %0 op_sel:[1,0]" : "+v"(*(unsigned long long*)&x)); \
+    if (OP == 15) asm volatile("v_lshl_add_u32 %0, %0, 3, %1" : "+v"(x) : "v"(b));
+            if (OP == 10 || OP == 11 || OP == 14) { STEP(a0) STEP(a2) STEP(a4) STEP(a6) }
             else { STEP(a0) STEP(a1) STEP(a2) STEP(a3) STEP(a4) STEP(a5) STEP(a6) STEP(a7) }
         }
     }
@@ -47,7 +52,7 @@ double run(const char* name, int blocks_per_cu, int cus, unsigned* d, double ghz
     CHK(hipEventSynchronize(e1));
     float ms = 0;
     CHK(hipEventElapsedTime(&ms, e0, e1));
-    const double ops_per_lane = double(iters) * 16 * (OP == 10 ? 4 : 8);
+    const double ops_per_lane = double(iters) * 16 * ((OP == 10 || OP == 11 || OP == 14) ? 4 : 8);
     const double lane_ops = ops_per_lane * grid * 256.0;
     const double per_s = lane_ops / (ms * 1e-3);
     printf("%-16s blocks/CU=%d  %8.2f Tlane-op/s  = %6.1f lane-ops/clk/CU @%.2fGHz\n", name, blocks_per_cu,
@@ -73,6 +78,11 @@ int main() {
         run<7>("v_xad_u32", bpc, cus, d, ghz);
         run<9>("v_bfi_b32", bpc, cus, d, ghz);
         run<10>("v_mad_u64_u32", bpc, cus, d, ghz);
+        run<11>("v_lshrrev_b64", bpc, cus, d, ghz);
+        run<12>("v_alignbyte_b32", bpc, cus, d, ghz);
+        run<13>("v_perm_b32", bpc, cus, d, ghz);
+        run<14>("v_pk_mov_b32", bpc, cus, d, ghz);
+        run<15>("v_lshl_add_u32", bpc, cus, d, ghz);
     }
     return 0;
 }
