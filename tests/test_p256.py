@@ -128,3 +128,46 @@ def test_gpu_decompress(gpu):
         addrs.append(bytes([42 if q.y % 2 == 0 else 43]) + q.x.to_bytes(32, 'little'))
     addrs.append(bytes([43]) + (o.P - 1).to_bytes(32, 'little'))
     assert op.decompress(addrs, device='gpu') == op.decompress(addrs, device='cpu')
+
+
+def _high_x_batch(count: int, seed: int):
+    """Signatures whose R = u1*G + u2*Q has x(R) in [n, p), so r = x(R) - n: the kernels' inversion-free
+    x-check must also compare (r + n)*Z^2 against X. Such R are ~2^-130 rare for honest signers, so the
+    key is solved for instead: pick R, e, s; Q = u2^-1 * (R - u1*G). Each valid record is followed by
+    the same signature with r = x(R) (>= n: a range error) and with r + 1 (a plain mismatch)."""
+    rng = random.Random(seed)
+    recs, exp = [], []
+    x = o.N
+    while len(exp) < 3 * count:
+        x += rng.randrange(1, 1 << 20)
+        try:
+            y = o.x_to_y(x, rng.random() < 0.5)
+        except Exception:
+            continue
+        if not o.is_on_curve(x, y):
+            continue
+        r = x - o.N
+        s = rng.randrange(1, o.N)
+        e = rng.randbytes(32)
+        w = pow(s, -1, o.N)
+        u1 = int.from_bytes(e, 'big') * w % o.N
+        u2 = r * w % o.N
+        t = o._to_affine(o._jadd((x, y, 1), o._jmul(o.N - u1, (o.GX, o.GY, 1))))
+        q = o.Point(*o.scalar_mult(pow(u2, -1, o.N), *t))
+        assert o.verify_digest(r, s, int.from_bytes(e, 'big'), q.x, q.y)
+        recs += [op.record(q, (r, s), e), op.record(q, (x, s), e), op.record(q, (r + 1, s), e)]
+        exp += [1, 3, 0]
+    return b''.join(recs), np.array(exp, dtype=np.uint8)
+
+
+def test_high_x_r_plus_n_host(native):
+    recs, exp = _high_x_batch(8, 31)
+    assert (op.verify_records(recs, device='cpu', threads=2) == exp).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('variant', ['0', '1', '2'])
+def test_high_x_r_plus_n_gpu(gpu, variant, monkeypatch):
+    monkeypatch.setenv('UPOW_P256_VARIANT', variant)
+    recs, exp = _high_x_batch(40, 32)
+    assert (op.verify_records(recs, device='gpu') == exp).all()
