@@ -139,3 +139,47 @@ def test_block_apply_is_atomic_under_injected_failure(chain, stage):
         await devnet.mine_block(a, [tx], ts=base + 3)
         assert await chain.get_address_balance(b) == 1
     asyncio.run(go())
+
+
+@pytest.mark.parametrize('backend', ['host', pytest.param('gpu', marks=pytest.mark.gpu)])
+def test_rollback_restores_utxo_index(monkeypatch, backend, request):
+    """remove_blocks (reference database.py:146-169) on either index backend: the index after rolling
+    back block 4 (which spends block-3 outputs) equals the index at height 3 — keys, tags and payloads —
+    and the UTXO-set hash and balances follow; re-mining the block afterwards applies cleanly."""
+    if backend == 'gpu':
+        request.getfixturevalue('gpu')
+    monkeypatch.setattr(manager, 'START_DIFFICULTY', Decimal('1.5'))
+    manager.Manager.difficulty = None
+    manager.cache.clear()
+
+    async def go():
+        db = await Database.create(utxo_backend=backend)
+        try:
+            a = builders.address_of(KEY_A)
+            b = builders.address_of(KEY_B)
+            base = 1_700_000_000
+            await devnet.mine_block(a, ts=base + 1)
+            await devnet.mine_block(a, ts=base + 2)
+            tx = await builders.create_transaction(KEY_A, b, '2.5')
+            assert await db.add_pending_transaction(tx)
+            await devnet.mine_block(a, [tx], ts=base + 3)
+            recs3, pay3 = db.utxo.records_payload()
+            hash3, bal3 = await db.get_unspent_outputs_hash(), await db.get_address_balance(b)
+            tx2 = await builders.create_transaction(KEY_B, a, '1')
+            assert await db.add_pending_transaction(tx2)
+            await devnet.mine_block(a, [tx2], ts=base + 4)
+            assert await db.get_address_balance(b) == Decimal('1.5')
+            await db.remove_blocks(4)
+            manager.Manager.difficulty = None
+            assert await db.get_next_block_id() == 4
+            recs, pay = db.utxo.records_payload()
+            assert recs.tobytes() == recs3.tobytes() and pay.tobytes() == pay3.tobytes()
+            assert await db.get_unspent_outputs_hash() == hash3
+            assert await db.get_address_balance(b) == bal3 == Decimal('2.5')
+            tx3 = await builders.create_transaction(KEY_B, a, '0.5')
+            assert await db.add_pending_transaction(tx3)
+            await devnet.mine_block(a, [tx3], ts=base + 5)
+            assert await db.get_address_balance(b) == Decimal(2)
+        finally:
+            db.close()
+    asyncio.run(go())
