@@ -141,6 +141,32 @@ def test_block_apply_is_atomic_under_injected_failure(chain, stage):
     asyncio.run(go())
 
 
+def test_address_utxos_tool(chain, tmp_path, capsys):
+    """``python -m upow_amd.tools address-utxos``: the index's view of an address equals the SQL view
+    (spendable outputs and balance)."""
+    from upow_amd import tools
+
+    async def go():
+        a = builders.address_of(KEY_A)
+        b = builders.address_of(KEY_B)
+        base = 1_700_000_000
+        await devnet.mine_block(a, ts=base + 1)
+        await devnet.mine_block(a, ts=base + 2)
+        tx = await builders.create_transaction(KEY_A, b, '2.5')
+        assert await chain.add_pending_transaction(tx)
+        await devnet.mine_block(a, [tx], ts=base + 3)
+        for addr in (a, b):
+            res = await tools.address_utxos(addr, db=chain)
+            assert Decimal(res['total']) == await chain.get_address_balance(addr)
+            sql = sorted((i.tx_hash, i.index) for i in await chain.get_spendable_outputs(addr))
+            assert sorted((o['tx_hash'], o['index']) for o in res['outputs']) == sql
+            assert all(o['table'] == 'unspent_outputs' for o in res['outputs'])
+    asyncio.run(go())
+    with pytest.raises(SystemExit):
+        tools.main(['address-utxos'])
+    capsys.readouterr()
+
+
 @pytest.mark.parametrize('backend', ['host', pytest.param('gpu', marks=pytest.mark.gpu)])
 def test_rollback_restores_utxo_index(monkeypatch, backend, request):
     """remove_blocks (reference database.py:146-169) on either index backend: the index after rolling
