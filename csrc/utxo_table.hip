@@ -77,6 +77,11 @@ __device__ __forceinline__ bool key_eq(const UtxoSlot& s, const uint32_t k[8]) {
     return d == 0;
 }
 
+// Owner fingerprint kept in the key slot (pad[0]): address bytes 1..4 (after the 42/43 parity prefix of
+// a compressed key these are x-coordinate bytes, i.e. uniformly random), so the K14 address scan can
+// reject a slot from the 48-byte key line alone and touch the 80-byte payload line only on a likely hit.
+__device__ __forceinline__ uint32_t addr_fingerprint(const uint8_t* addr) { return ld_u32(addr + 1); }
+
 __global__ __launch_bounds__(256) void utxo_insert_kernel(UtxoSlot* __restrict__ tab, UtxoPayload* __restrict__ pay,
                                                           uint32_t mask, const UtxoKeyRec* __restrict__ recs,
                                                           const UtxoPayload* __restrict__ in_pay, int64_t n,
@@ -97,7 +102,9 @@ __global__ __launch_bounds__(256) void utxo_insert_kernel(UtxoSlot* __restrict__
                 for (int w = 0; w < 8; ++w) tab[s].k[w] = k[w];
                 if (in_pay) {
                     pay[s] = in_pay[i];
+                    tab[s].pad[0] = addr_fingerprint(in_pay[i].addr);
                 } else {
+                    tab[s].pad[0] = 0;
                     pay[s].amount = 0;
                     pay[s].addr_len = 0;
                 }
@@ -228,12 +235,13 @@ __global__ __launch_bounds__(256) void utxo_dump_kernel(const UtxoSlot* __restri
 // K14: outputs owned by one address (reference `database.py:909-937,1138-1205`: balance / spendable
 // outputs by address). One lane per slot streams the key metas and, for live slots whose tag is in
 // `tag_mask`, the 80-byte payload line; the address is compared as four 16-byte vectors held in SGPRs
-// (the query is uniform). Matches are rare, so they are compacted with one atomic each; the amount sum
+// (the query is uniform). The slot's owner fingerprint is checked first, so the payload line is read
+// only for likely hits. Matches are rare, so they are compacted with one atomic each; the amount sum
 // is a wave reduction + one 64-bit atomic per wave that found anything.
 __global__ __launch_bounds__(256) void utxo_address_scan_kernel(const UtxoSlot* __restrict__ tab,
                                                                 const UtxoPayload* __restrict__ pay, uint32_t cap,
                                                                 uint4 q0, uint4 q1, uint4 q2, uint4 q3, uint32_t qlen,
-                                                                uint32_t tag_mask, uint32_t max_out,
+                                                                uint32_t qfp, uint32_t tag_mask, uint32_t max_out,
                                                                 UtxoKeyRec* __restrict__ out,
                                                                 UtxoPayload* __restrict__ pay_out,
                                                                 uint32_t* __restrict__ count,
@@ -243,7 +251,8 @@ __global__ __launch_bounds__(256) void utxo_address_scan_kernel(const UtxoSlot* 
     if (s < cap) {
         const uint32_t m = tab[s].meta;
         const uint32_t tag = (m >> 16) & 0xffu;
-        if ((m & 3u) == ST_FULL && tag < 32u && ((tag_mask >> tag) & 1u) && pay[s].addr_len == qlen) {
+        if ((m & 3u) == ST_FULL && tag < 32u && ((tag_mask >> tag) & 1u) && tab[s].pad[0] == qfp &&
+            pay[s].addr_len == qlen) {
             const uint4* a = reinterpret_cast<const uint4*>(pay[s].addr);
             const uint4 a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
             const uint32_t d = (a0.x ^ q0.x) | (a0.y ^ q0.y) | (a0.z ^ q0.z) | (a0.w ^ q0.w) | (a1.x ^ q1.x) |
@@ -408,6 +417,8 @@ std::vector<uint8_t> utxo_address_scan(int64_t h, const uint8_t* addr, uint32_t 
     uint4 q[4];
     std::memset(q, 0, sizeof(q));
     std::memcpy(q, addr, len);  // payload addresses are zero-padded to 64 bytes
+    uint32_t qfp = 0;           // same bytes as addr_fingerprint() on the zero-padded query
+    std::memcpy(&qfp, reinterpret_cast<const uint8_t*>(q) + 1, 4);
     // first pass sizes the output; a second pass runs only if more matches than the guess came back
     uint32_t cap_out = 4096, n = 0;
     DevBuf<unsigned long long> dt(1);
@@ -417,7 +428,7 @@ std::vector<uint8_t> utxo_address_scan(int64_t h, const uint8_t* addr, uint32_t 
         uck(hipMemset(t.d_counter, 0, sizeof(uint32_t)), "memset");
         uck(hipMemset(dt.p, 0, sizeof(unsigned long long)), "memset");
         hipLaunchKernelGGL(utxo_address_scan_kernel, dim3(int((t.cap + 255) / 256)), dim3(256), 0, 0, t.tab, t.pay,
-                           t.cap, q[0], q[1], q[2], q[3], len, tag_mask, cap_out, d.p, dp.p, t.d_counter, dt.p);
+                           t.cap, q[0], q[1], q[2], q[3], len, qfp, tag_mask, cap_out, d.p, dp.p, t.d_counter, dt.p);
         uck(hipGetLastError(), "utxo_address_scan_kernel");
         uck(hipMemcpy(&n, t.d_counter, sizeof(uint32_t), hipMemcpyDeviceToHost), "d2h n");
         if (n <= cap_out) {
