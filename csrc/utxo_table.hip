@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/device/device_radix_sort.hpp>
 
+#include <cstddef>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -38,6 +39,7 @@ struct alignas(16) UtxoSlot {
     uint32_t pad[3];
 };
 static_assert(sizeof(UtxoSlot) == 48, "slot size");
+static_assert(offsetof(UtxoSlot, meta) == 32 && offsetof(UtxoSlot, pad) == 36, "meta + fingerprint are one aligned 16-byte word");
 
 enum : uint32_t { ST_EMPTY = 0, ST_FULL = 1, ST_TOMB = 2, ST_BUSY = 3 };
 
@@ -249,9 +251,11 @@ __global__ __launch_bounds__(256) void utxo_address_scan_kernel(const UtxoSlot* 
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t amt = 0;
     if (s < cap) {
-        const uint32_t m = tab[s].meta;
+        // meta and fingerprint in one 16-byte load (slot bytes 32..47, 16-byte aligned)
+        const uint4 mw = *reinterpret_cast<const uint4*>(&tab[s].meta);
+        const uint32_t m = mw.x;
         const uint32_t tag = (m >> 16) & 0xffu;
-        if ((m & 3u) == ST_FULL && tag < 32u && ((tag_mask >> tag) & 1u) && tab[s].pad[0] == qfp &&
+        if ((m & 3u) == ST_FULL && tag < 32u && ((tag_mask >> tag) & 1u) && mw.y == qfp &&
             pay[s].addr_len == qlen) {
             const uint4* a = reinterpret_cast<const uint4*>(pay[s].addr);
             const uint4 a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
