@@ -1,0 +1,66 @@
+# One parametrised GPU validation runner (replaces the per-lease gpu_roundN.sh scripts).
+#
+#   gpurun --timeout 1200 -- 'bash scripts/gpu_run.sh TAG [STEPS...]'
+#
+# STEPS (default: test smoke mine verify prof): any of
+#   test     pytest -m gpu (one process, per-test thread timeout)
+#   smoke    __graft_entry__.smoke()
+#   mine     bench.py (driver default: PoW MH/s + verify side metrics)
+#   verify   bench.py --mode verify --ledger <tmp dir> (file ledger, metric 2)
+#   verifymem bench.py --mode verify (in-memory ledger)
+#   prof     rocprofv3 --kernel-trace --stats over a short bench.py
+#   vprof    rocprofv3 --kernel-trace --stats over the verify bench
+#   py:<script.py>  any extra python script under scripts/ (args after a comma: py:x.py,--a,1)
+# Every GPU step has its own time limit and the chain stops at the first failure.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+TAG=${1:-run}
+shift || true
+STEPS=${*:-test smoke mine verify prof}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+for s in $STEPS; do
+  echo "== $TAG: $s ($(date +%T))"
+  case $s in
+    test)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
+      tail -3 "$OUT/pytest.log" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+        || { cat "$OUT/smoke.log"; exit 1; }
+      tail -1 "$OUT/smoke.log" ;;
+    mine)
+      timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
+        || { tail -20 "$OUT/bench.err"; exit 1; }
+      cat "$OUT/bench.json" ;;
+    verify)
+      rm -rf /tmp/upow_bench_ledger
+      timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger \
+        > "$OUT/verify_file.json" 2> "$OUT/verify_file.err" || { tail -20 "$OUT/verify_file.err"; exit 1; }
+      cat "$OUT/verify_file.json" ;;
+    verifymem)
+      timeout -k 10 600 python bench.py --mode verify > "$OUT/verify_mem.json" 2> "$OUT/verify_mem.err" \
+        || { tail -20 "$OUT/verify_mem.err"; exit 1; }
+      cat "$OUT/verify_mem.json" ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o pow --output-format csv \
+        -- python3 bench.py --steps 5 --warmup 1 > "$OUT/prof.log" 2>&1 || { tail -20 "$OUT/prof.log"; exit 1; }
+      echo prof-ok ;;
+    vprof)
+      rm -rf /tmp/upow_bench_ledger
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/vprof" -o verify --output-format csv \
+        -- python3 bench.py --mode verify --ledger /tmp/upow_bench_ledger --steps 3 --warmup 1 \
+        > "$OUT/vprof.log" 2>&1 || { tail -20 "$OUT/vprof.log"; exit 1; }
+      echo vprof-ok ;;
+    py:*)
+      spec=${s#py:}; script=${spec%%,*}; rest=""
+      [ "$spec" != "$script" ] && rest=${spec#*,} && rest=${rest//,/ }
+      timeout -k 10 600 python -u "scripts/$script" $rest > "$OUT/${script%.py}.out" 2>&1 \
+        || { tail -30 "$OUT/${script%.py}.out"; exit 1; }
+      tail -15 "$OUT/${script%.py}.out" ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "== $TAG done"

@@ -107,26 +107,56 @@ def test_rate_limit_and_ip_filter(node):
     assert r.status_code == 429 and r.json()['error'].startswith('Rate limit exceeded')
     r = client.get('/get_nodes//', follow_redirects=False)
     assert r.status_code in (302, 307)
-    main.ip_filter.block_endpoints = {'/get_nodes'}
-    main.ip_filter.last_update = 1e18
-    assert client.get('/get_nodes').status_code == 403
-    main.ip_filter.block_endpoints = set()
+    from upow_amd.node.access import AccessPolicy
+    main.access.install(AccessPolicy(blocked_paths=frozenset({'/get_nodes'})))
+    r = client.get('/get_nodes')
+    assert r.status_code == 403 and r.json() == {'ok': False, 'error': 'Access forbidden temporarily.'}
+    main.access.install(AccessPolicy.from_json({'blocklist': ['10.1.0.0/16']}))
+    r = client.get('/get_nodes', headers={'X-Forwarded-For': '10.1.2.3, 1.1.1.1'})
+    assert r.status_code == 403 and r.json()['error'] == 'Access forbidden.'
+    assert client.get('/get_nodes', headers={'X-Real-IP': '10.2.0.1'}).status_code == 200
+    main.access.install(AccessPolicy.from_json({'whitelist': ['9.9.9.9'], 'blocklist': ['9.9.9.9']}))
+    assert client.get('/get_nodes', headers={'X-Real-IP': '9.9.9.9'}).status_code == 200  # allow-list wins
+    assert client.get('/get_nodes', headers={'X-Real-IP': '8.8.8.8'}).status_code == 403
+    main.access.reload()  # back to the (empty) policy file
     assert client.get('/send_to_address', params={'to_address': 'x', 'amount': 1}).status_code == 403
 
 
 def test_websocket_protocol(node):
+    """/ws client contract on the node app: pong, the double success on subscribe, unsubscribe
+    (subscribed and not), a published block, and close after a refused verb."""
+    from starlette.websockets import WebSocketDisconnect
     client, main = node
     with client.websocket_connect('/ws') as ws:
         ws.send_json({'type': 'ping'})
-        assert ws.receive_json()['type'] == 'pong'
+        pong = ws.receive_json()
+        assert pong['type'] == 'pong' and 'timestamp' in pong
         ws.send_json({'type': 'subscribe_block'})
         m1, m2 = ws.receive_json(), ws.receive_json()
-        assert m1['type'] == 'success' and m1['data'] == {'channel': 'block'}
-        assert m2['message'] == 'Subscribed to block updates'
+        assert (m1['type'], m1['message'], m1['data']) == ('success', 'Subscribed to block', {'channel': 'block'})
+        assert (m2['message'], m2['data']) == ('Subscribed to block updates', {'type': 'block_subscription'})
+        ws.send_json({'type': 'unsubscribe_block'})
+        u1, u2 = ws.receive_json(), ws.receive_json()
+        assert (u1['message'], u1['data']) == ('Unsubscribed from block', {'channel': 'block'})
+        assert (u2['message'], u2['data']) == ('Unsubscribed from block updates', {'type': 'block_unsubscription'})
+        ws.send_json({'type': 'unsubscribe_block'})
+        e, u3 = ws.receive_json(), ws.receive_json()
+        assert (e['type'], e['error_code']) == ('error', 'NOT_SUBSCRIBED')
+        assert e['message'] == "Not subscribed to channel 'block'"
+        assert u3['type'] == 'success' and u3['data'] == {'type': 'block_unsubscription'}
+        ws.send_json({'type': 'subscribe_block'})
+        ws.receive_json(), ws.receive_json()
+        ws.send_json({'type': 'pong'})  # accepted silently
         from upow_amd.wallet.builders import address_of
         assert _mine(client, address_of(KEY_A), 1_700_000_001) == {'ok': True}
         ev = ws.receive_json()
-        assert ev['type'] == 'new_block' and ev['data']['block_no'] == 1
-        ws.send_json({'type': 'subscribe_transaction'})
+        assert ev['type'] == 'new_block' and ev['data']['block_no'] == 1 and 'timestamp' in ev
+        assert isinstance(ev['data']['difficulty'], float)  # Decimal goes out as a JSON number
+        ws.send_json({'type': 'subscribe_transaction'})  # not on the reference allow-list
         err = ws.receive_json()
         assert err['type'] == 'error' and err['error_code'] == 'INVALID_MESSAGE_TYPE'
+        assert err['message'] == "Message type 'subscribe_transaction' not allowed"
+        with pytest.raises(WebSocketDisconnect) as exc:
+            ws.receive_json()
+        assert exc.value.code == 1000
+    assert main.websocket_router is not None

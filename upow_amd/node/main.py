@@ -45,9 +45,9 @@ from ..models.transaction import CoinbaseTransaction, Transaction
 from ..utils import codec
 from ..utils.codec import sha256, timestamp
 from ..utils.logger import get_logger
-from ..websocket.endpoint import (broadcast_new_block, broadcast_new_transaction, shutdown_websocket_manager,
-                                  start_websocket_manager, websocket_router)
-from .ip_manager import IPManager
+from ..websocket.endpoint import (broadcast_new_block, broadcast_new_transaction, router as websocket_router,
+                                  shutdown_websocket_manager, start_websocket_manager)
+from .access import AccessControl
 from .nodes_manager import NodeInterface, NodesManager
 from .ratelimit import Limiter, RateLimitExceeded, get_remote_address, rate_limit_exceeded_handler
 from .utils import ip_is_local
@@ -59,7 +59,7 @@ db: Database = None
 started = False
 is_syncing = False
 self_url = None
-ip_filter: IPManager = None
+access: AccessControl = None
 transactions_cache = deque(maxlen=100)
 LAST_PENDING_TRANSACTIONS_CLEAN = [0]
 BANNED_SENDERS = ['DgQKikeDqS2Fzue23KuA36L4eJSFh649zA9jJ6zwbzUMp']  # main.py:426
@@ -96,9 +96,9 @@ async def _address_indexer(period: float = 30.0):
 
 async def startup():
     """main.py:246-257: open the ledger (UPOW_DATABASE_PATH, default <data dir>/ledger.sqlite3)."""
-    global db, ip_filter
+    global db, access
     NodesManager.init()
-    ip_filter = IPManager()
+    access = AccessControl()
     path = os.environ.get('UPOW_DATABASE_PATH') or config.data_path('ledger.sqlite3')
     db = await Database.create(path=path)
     if cluster.get() is not None:  # multi-GPU node: bring the follower replicas to our tip
@@ -299,63 +299,77 @@ async def propagate_old_transactions(propagate_txs):
         await propagate('push_tx', {'tx_hex': tx_hex})
 
 
-async def get_ip_address_from_header(request: Request):
-    xff = request.headers.get('x-forwarded-for', '')
-    visitor_ip = xff.split(',')[0].strip() if xff else request.headers.get('x-real-ip', None)
-    if not visitor_ip and request.client:
-        visitor_ip = request.client.host
-    return visitor_ip
+_SLASH_RUNS = re.compile('/+')
+
+
+def client_address(request: Request):
+    """Visitor address: first X-Forwarded-For hop, else X-Real-IP (both set by the NGINX front end the
+    reference documents, NGINX.md:46-58), else the socket peer."""
+    forwarded = request.headers.get('x-forwarded-for', '')
+    if forwarded:
+        return forwarded.split(',')[0].strip()
+    return request.headers.get('x-real-ip') or (request.client.host if request.client else None)
+
+
+def _deny(text: str) -> JSONResponse:
+    return JSONResponse(status_code=403, content={'ok': False, 'error': text})
+
+
+async def _join_network(request: Request, local: bool) -> None:
+    """First non-local request (reference main.py:327-361): pull the first known peer's peer list,
+    learn our public URL from the request, and announce it to our peers and theirs. Best effort."""
+    global started, self_url
+    known = NodesManager.get_recent_nodes()
+    if not known:
+        return
+    seed = known[0]
+    try:
+        listing = await NodesManager.request(f'{seed}/get_nodes')
+        known.extend(listing['result'])
+        NodesManager.sync()
+        if local:
+            return
+        started = True
+        self_url = str(request.base_url).strip('/')
+        for own in {self_url, self_url.replace('http://', 'https://')}:
+            while own in known:
+                known.remove(own)
+        NodesManager.sync()
+        await propagate('add_node', {'url': self_url})
+        await propagate('add_node', {'url': self_url}, nodes=await NodeInterface(seed).get_nodes())
+    except Exception:
+        pass
 
 
 @app.middleware('http')
-async def middleware(request: Request, call_next):
-    """main.py:286-372."""
-    global started, self_url
-    nodes = NodesManager.get_recent_nodes()
-    hostname = request.base_url.hostname
-    client_ip = await get_ip_address_from_header(request)
-    if not ip_filter.is_ip_allowed(client_ip):
-        return JSONResponse(status_code=403, content={'ok': False, 'error': 'Access forbidden.'})
-    normalized_path = re.sub('/+', '/', request.scope['path'])
-    if normalized_path != request.scope['path']:
-        return RedirectResponse(str(request.url).replace(request.scope['path'], normalized_path))
-    if ip_filter.is_endpoint_blocked(normalized_path):
-        return JSONResponse(status_code=403, content={'ok': False, 'error': 'Access forbidden temporarily.'})
-    if 'Sender-Node' in request.headers and request.headers['Sender-Node']:
-        NodesManager.add_node(request.headers['Sender-Node'])
-    local = ip_is_local(hostname) or hostname == 'localhost'
-    if normalized_path == '/send_to_address' and not local:
-        return JSONResponse(status_code=403, content={
-            'ok': False, 'error': 'Access forbidden. This endpoint can only be accessed from localhost.'})
-    if normalized_path != '/get_nodes' and (nodes and not started or local):
-        try:
-            if not started:
-                node_url = nodes[0]
-                j = await NodesManager.request(f'{node_url}/get_nodes')
-                nodes.extend(j['result'])
-                NodesManager.sync()
-                if not local:
-                    started = True
-                    self_url = str(request.base_url).strip('/')
-                    for candidate in (self_url, self_url.replace('http://', 'https://')):
-                        try:
-                            nodes.remove(candidate)
-                        except ValueError:
-                            pass
-                    NodesManager.sync()
-                    try:
-                        await propagate('add_node', {'url': self_url})
-                        cousin_nodes = await NodeInterface(node_url).get_nodes()
-                        await propagate('add_node', {'url': self_url}, nodes=cousin_nodes)
-                    except Exception:
-                        pass
-        except Exception:
-            pass
-    propagate_txs = await db.get_need_propagate_transactions()
+async def gatekeeper(request: Request, call_next):
+    """Per-request gates, in order: access policy on the client address, path canonicalisation
+    (redirect), blocked paths, Sender-Node peer learning, localhost-only /send_to_address, network
+    join on the first request, and re-propagation of mempool txs that were not gossiped for 10 min
+    (attached to the response as a background task)."""
+    policy = access.policy()
+    if not policy.admits(client_address(request)):
+        return _deny('Access forbidden.')
+    raw_path = request.scope['path']
+    path = _SLASH_RUNS.sub('/', raw_path)
+    if path != raw_path:
+        return RedirectResponse(str(request.url).replace(raw_path, path))
+    if policy.path_blocked(path):
+        return _deny('Access forbidden temporarily.')
+    sender = request.headers.get('Sender-Node')
+    if sender:
+        NodesManager.add_node(sender)
+    host = request.base_url.hostname
+    local = host == 'localhost' or ip_is_local(host)
+    if path == '/send_to_address' and not local:
+        return _deny('Access forbidden. This endpoint can only be accessed from localhost.')
+    if not started and path != '/get_nodes':
+        await _join_network(request, local)
+    stale = await db.get_need_propagate_transactions()
     response = await call_next(request)
     response.headers['Access-Control-Allow-Origin'] = '*'
-    if propagate_txs:
-        response.background = BackgroundTask(propagate_old_transactions, propagate_txs)
+    if stale:
+        response.background = BackgroundTask(propagate_old_transactions, stale)
     return response
 
 
