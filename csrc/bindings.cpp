@@ -13,7 +13,7 @@ using namespace upow;
 
 namespace upow {
 void register_txcodec(py::module_& m);  // txcodec.cpp
-void register_ledger_sql(py::module_& m);  // ledger_sql.cpp
+void register_ledger_writer(py::module_& m);  // ledger_writer.cpp
 }
 
 static PowJobHost make_job(py::bytes header, uint32_t tmask, uint32_t tword, uint32_t frac_shift,
@@ -48,7 +48,7 @@ static void packed_args(py::buffer data, py::buffer offsets, const uint8_t*& d, 
 PYBIND11_MODULE(_native, m) {
     m.doc() = "upow_amd native core: host C++ crypto + gfx950 HIP kernels";
     register_txcodec(m);
-    register_ledger_sql(m);
+    register_ledger_writer(m);
 
     m.def("sha256", [](py::bytes msg) {
         std::string s = msg;

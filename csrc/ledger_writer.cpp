@@ -1,0 +1,887 @@
+// Ledger journal + background SQL materialiser, on a SQLite connection this layer opens and owns.
+//
+// reference: the block-apply writes of upow/manager.py:706-730 → upow/database.py add_block 254-270,
+// add_transactions 236-252, add_transaction_outputs 524-580, remove_outputs 589-621,
+// remove_pending_transactions_by_hash — asyncpg statements against PostgreSQL, issued one by one on the
+// request path. Here a validated block's writes become ONE encoded batch of column-major bulk statements:
+//
+//   commit point   the batch is appended to an append-only journal file (CRC-framed record, write(2);
+//                  fdatasync per record or per materialiser group) — together with the HBM UTXO update
+//                  this is when the block is applied;
+//   materialise    a background thread applies queued batches to the schema.sql tables, several blocks
+//                  per SQLite transaction (group commit), and records the last applied journal sequence
+//                  number in `upow_journal_state` inside the same transaction;
+//   watermark      readers that need those tables wait until the applied sequence covers the last batch
+//                  that wrote them (Python: Database._settle);
+//   restart        journal records above the recorded sequence are re-applied before the ledger opens,
+//                  a torn tail record is cut off.
+//
+// Each record carries an opaque `meta` section (the block's undo data: created and spent outpoints with
+// their payloads) that rollback reads back (journal_meta) to undo the HBM table without a rebuild.
+//
+// libsqlite3 is resolved with dlopen from the copy the interpreter's _sqlite3 module already loaded.
+#include <dlfcn.h>
+#include <fcntl.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace upow {
+namespace {
+
+struct sqlite3;
+struct sqlite3_stmt;
+typedef void (*destructor_t)(void*);
+constexpr int SQLITE_OK = 0, SQLITE_ROW = 100, SQLITE_DONE = 101, SQLITE_CONSTRAINT = 19;
+constexpr int SQLITE_OPEN_READWRITE = 0x2, SQLITE_OPEN_CREATE = 0x4, SQLITE_OPEN_NOMUTEX = 0x8000,
+              SQLITE_OPEN_URI = 0x40;
+
+struct SqliteApi {
+    int (*open_v2)(const char*, sqlite3**, int, const char*) = nullptr;
+    int (*close_v2)(sqlite3*) = nullptr;
+    int (*exec)(sqlite3*, const char*, void*, void*, char**) = nullptr;
+    int (*busy_timeout)(sqlite3*, int) = nullptr;
+    int (*prepare_v2)(sqlite3*, const char*, int, sqlite3_stmt**, const char**) = nullptr;
+    int (*bind_text)(sqlite3_stmt*, int, const char*, int, destructor_t) = nullptr;
+    int (*bind_int64)(sqlite3_stmt*, int, long long) = nullptr;
+    int (*bind_null)(sqlite3_stmt*, int) = nullptr;
+    int (*step)(sqlite3_stmt*) = nullptr;
+    int (*reset)(sqlite3_stmt*) = nullptr;
+    int (*clear_bindings)(sqlite3_stmt*) = nullptr;
+    int (*finalize)(sqlite3_stmt*) = nullptr;
+    int (*changes)(sqlite3*) = nullptr;
+    long long (*column_int64)(sqlite3_stmt*, int) = nullptr;
+    const char* (*errmsg)(sqlite3*) = nullptr;
+    void (*free)(void*) = nullptr;
+    bool ok = false;
+};
+
+const SqliteApi& api() {
+    static SqliteApi a = [] {
+        SqliteApi s;
+        void* h = dlopen("libsqlite3.so.0", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("libsqlite3.so.0", RTLD_NOW);
+        if (!h) return s;
+        auto sym = [&](auto& fn, const char* name) { fn = reinterpret_cast<std::decay_t<decltype(fn)>>(dlsym(h, name)); };
+        sym(s.open_v2, "sqlite3_open_v2");
+        sym(s.close_v2, "sqlite3_close_v2");
+        sym(s.exec, "sqlite3_exec");
+        sym(s.busy_timeout, "sqlite3_busy_timeout");
+        sym(s.prepare_v2, "sqlite3_prepare_v2");
+        sym(s.bind_text, "sqlite3_bind_text");
+        sym(s.bind_int64, "sqlite3_bind_int64");
+        sym(s.bind_null, "sqlite3_bind_null");
+        sym(s.step, "sqlite3_step");
+        sym(s.reset, "sqlite3_reset");
+        sym(s.clear_bindings, "sqlite3_clear_bindings");
+        sym(s.finalize, "sqlite3_finalize");
+        sym(s.changes, "sqlite3_changes");
+        sym(s.column_int64, "sqlite3_column_int64");
+        sym(s.errmsg, "sqlite3_errmsg");
+        sym(s.free, "sqlite3_free");
+        s.ok = s.open_v2 && s.close_v2 && s.exec && s.busy_timeout && s.prepare_v2 && s.bind_text && s.bind_int64 &&
+               s.bind_null && s.step && s.reset && s.clear_bindings && s.finalize && s.changes && s.column_int64 &&
+               s.errmsg && s.free;
+        return s;
+    }();
+    if (!a.ok) throw std::runtime_error("libsqlite3.so.0 not available for the native ledger writer");
+    return a;
+}
+
+// ------------------------------------------------------------------------------------------ byte codec
+struct Out {
+    std::string b;
+    void raw(const void* p, size_t n) { b.append(static_cast<const char*>(p), n); }
+    void u8(uint8_t v) { raw(&v, 1); }
+    void u32(uint32_t v) { raw(&v, 4); }
+    void i64(int64_t v) { raw(&v, 8); }
+    void str(const std::string& s) {
+        u32(uint32_t(s.size()));
+        raw(s.data(), s.size());
+    }
+};
+
+struct In {
+    const char* p;
+    const char* e;
+    void need(size_t n) const {
+        if (size_t(e - p) < n) throw std::runtime_error("ledger batch truncated");
+    }
+    template <class T>
+    T get() {
+        need(sizeof(T));
+        T v;
+        std::memcpy(&v, p, sizeof(T));
+        p += sizeof(T);
+        return v;
+    }
+    const char* take(size_t n) {
+        need(n);
+        const char* r = p;
+        p += n;
+        return r;
+    }
+    std::string str() {
+        uint32_t n = get<uint32_t>();
+        return std::string(take(n), n);
+    }
+};
+
+// Column kinds of an encoded statement.
+enum ColKind : uint8_t { K_NULL = 0, K_CTEXT = 1, K_CINT = 2, K_INT64 = 3, K_HEX32 = 4, K_TEXT = 5 };
+
+// Encode one column spec (Python side) for n rows:
+//   list[str|None]                    text per row
+//   ('gather', list[str], int32 buf)   text list[idx[row]]
+//   ('hex32', buf, stride, offset)     lowercase hex of the 32 bytes at row*stride+offset
+//   ('arena', blob, int64 offsets)     text blob[off[row]:off[row+1]] (csrc/txcodec.cpp text arenas)
+//   int64 numpy array                  integer per row
+//   str / int / None                   the same value for every row
+void encode_text_rows(Out& o, int64_t n, const std::vector<const char*>& ptr, const std::vector<int64_t>& len,
+                      const int32_t* idx) {
+    // K_TEXT: u8 has_null, [u8 null[n]], i64 off[n+1], blob
+    std::vector<int64_t> off(size_t(n) + 1, 0);
+    std::vector<uint8_t> nul(size_t(n), 0);
+    bool any_null = false;
+    for (int64_t r = 0; r < n; ++r) {
+        const size_t g = idx ? size_t(idx[r]) : size_t(r);
+        nul[size_t(r)] = ptr[g] == nullptr;
+        any_null |= ptr[g] == nullptr;
+        off[size_t(r) + 1] = off[size_t(r)] + (ptr[g] ? len[g] : 0);
+    }
+    o.u8(K_TEXT);
+    o.u8(any_null);
+    if (any_null) o.raw(nul.data(), nul.size());
+    o.raw(off.data(), off.size() * 8);
+    for (int64_t r = 0; r < n; ++r) {
+        const size_t g = idx ? size_t(idx[r]) : size_t(r);
+        if (ptr[g]) o.raw(ptr[g], size_t(len[g]));
+    }
+}
+
+void utf8_list(py::list lst, std::vector<const char*>& ptr, std::vector<int64_t>& len) {
+    const size_t n = lst.size();
+    ptr.resize(n);
+    len.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+        PyObject* obj = PyList_GET_ITEM(lst.ptr(), i);
+        if (obj == Py_None) {
+            ptr[i] = nullptr;
+            len[i] = 0;
+            continue;
+        }
+        Py_ssize_t sz = 0;
+        const char* s = PyUnicode_AsUTF8AndSize(obj, &sz);
+        if (!s) throw py::error_already_set();
+        ptr[i] = s;
+        len[i] = sz;
+    }
+}
+
+void encode_col(Out& o, py::handle spec, int64_t n) {
+    if (spec.is_none()) {
+        o.u8(K_NULL);
+    } else if (py::isinstance<py::str>(spec)) {
+        o.u8(K_CTEXT);
+        o.str(spec.cast<std::string>());
+    } else if (py::isinstance<py::bool_>(spec) || py::isinstance<py::int_>(spec)) {
+        o.u8(K_CINT);
+        o.i64(spec.cast<long long>());
+    } else if (py::isinstance<py::list>(spec)) {
+        std::vector<const char*> ptr;
+        std::vector<int64_t> len;
+        utf8_list(spec.cast<py::list>(), ptr, len);
+        if (int64_t(ptr.size()) != n) throw std::invalid_argument("text column length != n");
+        encode_text_rows(o, n, ptr, len, nullptr);
+    } else if (py::isinstance<py::tuple>(spec)) {
+        py::tuple t = spec.cast<py::tuple>();
+        const std::string tag = t[0].cast<std::string>();
+        if (tag == "gather") {
+            std::vector<const char*> ptr;
+            std::vector<int64_t> len;
+            utf8_list(t[1].cast<py::list>(), ptr, len);
+            py::buffer_info bi = t[2].cast<py::buffer>().request();
+            if (bi.itemsize != 4) throw std::invalid_argument("gather index must be int32");
+            if (bi.size != n) throw std::invalid_argument("gather index length != n");
+            const int32_t* idx = static_cast<const int32_t*>(bi.ptr);
+            for (int64_t i = 0; i < n; ++i)
+                if (idx[i] < 0 || size_t(idx[i]) >= ptr.size()) throw std::out_of_range("gather index");
+            encode_text_rows(o, n, ptr, len, idx);
+        } else if (tag == "hex32") {
+            py::buffer_info bi = t[1].cast<py::buffer>().request();
+            const uint8_t* raw = static_cast<const uint8_t*>(bi.ptr);
+            const int64_t raw_n = bi.size * bi.itemsize, stride = t[2].cast<int64_t>(), offset = t[3].cast<int64_t>();
+            if (offset < 0 || stride < 0 || (n > 0 && (n - 1) * stride + offset + 32 > raw_n))
+                throw std::out_of_range("hex32 column out of range");
+            o.u8(K_HEX32);
+            for (int64_t r = 0; r < n; ++r) o.raw(raw + r * stride + offset, 32);
+        } else if (tag == "arena") {
+            py::buffer_info bb = t[1].cast<py::buffer>().request(), ob = t[2].cast<py::buffer>().request();
+            if (ob.size * ob.itemsize != 8 * (n + 1)) throw std::invalid_argument("arena offsets must be int64[n + 1]");
+            const char* blob = static_cast<const char*>(bb.ptr);
+            const int64_t* aoff = static_cast<const int64_t*>(ob.ptr);
+            const int64_t blen = bb.size * bb.itemsize;
+            for (int64_t i = 0; i < n; ++i)
+                if (aoff[i] < 0 || aoff[i + 1] < aoff[i] || aoff[i + 1] > blen) throw std::out_of_range("arena offsets");
+            o.u8(K_TEXT);
+            o.u8(0);
+            std::vector<int64_t> off(size_t(n) + 1);
+            for (int64_t i = 0; i <= n; ++i) off[size_t(i)] = aoff[i] - aoff[0];
+            o.raw(off.data(), off.size() * 8);
+            o.raw(blob + aoff[0], size_t(aoff[n] - aoff[0]));
+        } else {
+            throw std::invalid_argument("unknown column tag " + tag);
+        }
+    } else {
+        py::buffer_info bi = spec.cast<py::buffer>().request();
+        if (bi.itemsize != 8 || bi.format.find_first_of("qlQL") == std::string::npos)
+            throw std::invalid_argument("integer column must be int64");
+        if (bi.size != n) throw std::invalid_argument("int column length != n");
+        o.u8(K_INT64);
+        o.raw(bi.ptr, size_t(n) * 8);
+    }
+}
+
+// Statement encoding: str sql, u32 flags (1: guard sql, 2: expected change count), [str guard], [i64 expect],
+// i64 n, u32 n_cols, cols..., u8 has_order, [i64 order[n]].
+py::bytes encode_stmt(const std::string& sql, py::sequence cols, int64_t n, py::object order, py::object guard,
+                      py::object expect) {
+    if (n < 0) throw std::invalid_argument("n < 0");
+    Out o;
+    o.str(sql);
+    const uint32_t flags = (guard.is_none() ? 0u : 1u) | (expect.is_none() ? 0u : 2u);
+    o.u32(flags);
+    if (flags & 1) o.str(guard.cast<std::string>());
+    if (flags & 2) o.i64(expect.cast<int64_t>());
+    o.i64(n);
+    o.u32(uint32_t(cols.size()));
+    for (auto spec : cols) encode_col(o, spec, n);
+    if (order.is_none()) {
+        o.u8(0);
+    } else {
+        py::buffer_info bi = order.cast<py::buffer>().request();
+        if (bi.itemsize != 8 || bi.size != n) throw std::invalid_argument("order must be int64[n]");
+        const int64_t* ord = static_cast<const int64_t*>(bi.ptr);
+        for (int64_t i = 0; i < n; ++i)
+            if (ord[i] < 0 || ord[i] >= n) throw std::out_of_range("order");
+        o.u8(1);
+        o.raw(ord, size_t(n) * 8);
+    }
+    return py::bytes(o.b);
+}
+
+// Decoded view of one column inside a batch buffer.
+struct ColView {
+    uint8_t kind = K_NULL;
+    std::string ctext;
+    long long cint = 0;
+    const char* data = nullptr;  // INT64 / HEX32 rows, TEXT blob
+    const uint8_t* nul = nullptr;
+    const char* off = nullptr;  // TEXT offsets (i64[n+1], unaligned)
+};
+
+int64_t ld64(const char* p) {
+    int64_t v;
+    std::memcpy(&v, p, 8);
+    return v;
+}
+
+const char kHex[] = "0123456789abcdef";
+
+struct SqlError : std::runtime_error {
+    int rc;
+    SqlError(const std::string& m, int c) : std::runtime_error(m), rc(c) {}
+};
+
+// ------------------------------------------------------------------------------------------ journal
+constexpr uint32_t kMagic = 0x314a5055;  // "UPJ1"
+struct RecHeader {
+    uint32_t magic;
+    uint32_t crc;       // CRC-32C over seq, block_id, meta_len, payload_len and both sections
+    uint64_t seq;
+    int64_t block_id;   // -1: not a block
+    uint64_t meta_len;
+    uint64_t payload_len;
+};
+static_assert(sizeof(RecHeader) == 40, "journal record header layout");
+
+uint32_t crc32c_sw(uint32_t crc, const uint8_t* p, size_t n) {
+    static uint32_t table[8][256];
+    static bool init = [] {
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+            table[0][i] = c;
+        }
+        for (uint32_t i = 0; i < 256; ++i)
+            for (int t = 1; t < 8; ++t) table[t][i] = (table[t - 1][i] >> 8) ^ table[0][table[t - 1][i] & 0xff];
+        return true;
+    }();
+    (void)init;
+    crc = ~crc;
+    while (n >= 8) {
+        uint64_t v;
+        std::memcpy(&v, p, 8);
+        v ^= crc;
+        crc = table[7][v & 0xff] ^ table[6][(v >> 8) & 0xff] ^ table[5][(v >> 16) & 0xff] ^
+              table[4][(v >> 24) & 0xff] ^ table[3][(v >> 32) & 0xff] ^ table[2][(v >> 40) & 0xff] ^
+              table[1][(v >> 48) & 0xff] ^ table[0][v >> 56];
+        p += 8;
+        n -= 8;
+    }
+    while (n--) crc = (crc >> 8) ^ table[0][(crc ^ *p++) & 0xff];
+    return ~crc;
+}
+
+__attribute__((target("sse4.2"))) uint32_t crc32c_hw(uint32_t crc, const uint8_t* p, size_t n) {
+    uint64_t c = ~crc;
+    while (n >= 8) {
+        uint64_t v;
+        std::memcpy(&v, p, 8);
+        c = __builtin_ia32_crc32di(c, v);
+        p += 8;
+        n -= 8;
+    }
+    uint32_t c32 = uint32_t(c);
+    while (n--) c32 = __builtin_ia32_crc32qi(c32, *p++);
+    return ~c32;
+}
+
+uint32_t crc32c(uint32_t crc, const void* p, size_t n) {
+    static const bool hw = __builtin_cpu_supports("sse4.2");
+    return hw ? crc32c_hw(crc, static_cast<const uint8_t*>(p), n) : crc32c_sw(crc, static_cast<const uint8_t*>(p), n);
+}
+
+uint32_t record_crc(const RecHeader& h, const char* meta, const char* payload) {
+    uint32_t c = crc32c(0, &h.seq, sizeof(RecHeader) - 8);
+    c = crc32c(c, meta, h.meta_len);
+    return crc32c(c, payload, h.payload_len);
+}
+
+void write_all(int fd, const char* p, size_t n) {
+    while (n) {
+        ssize_t w = ::write(fd, p, n);
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            throw std::runtime_error(std::string("journal write failed: ") + strerror(errno));
+        }
+        p += w;
+        n -= size_t(w);
+    }
+}
+
+bool read_exact(int fd, char* p, size_t n, off_t at) {
+    while (n) {
+        ssize_t r = ::pread(fd, p, n, at);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) return false;
+        p += r;
+        n -= size_t(r);
+        at += r;
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------ writer
+struct Batch {
+    uint64_t seq;
+    std::shared_ptr<std::string> payload;  // u32 n_stmts + statements
+};
+
+enum SyncMode { SYNC_OFF = 0, SYNC_GROUP = 1, SYNC_COMMIT = 2 };
+
+class LedgerWriter {
+   public:
+    LedgerWriter(const std::string& db_path, const std::string& journal_path, int sync_mode, int64_t cache_mb,
+                 int group_max, int64_t journal_max_bytes)
+        : db_path_(db_path), journal_path_(journal_path), sync_(sync_mode), group_max_(std::max(1, group_max)),
+          journal_max_(journal_max_bytes) {
+        const SqliteApi& a = api();
+        int rc = a.open_v2(db_path.c_str(), &db_, SQLITE_OPEN_READWRITE | SQLITE_OPEN_CREATE | SQLITE_OPEN_NOMUTEX |
+                                                     SQLITE_OPEN_URI, nullptr);
+        if (rc != SQLITE_OK) {
+            std::string m = db_ ? a.errmsg(db_) : "open failed";
+            if (db_) a.close_v2(db_);
+            db_ = nullptr;
+            throw std::runtime_error("ledger writer: cannot open " + db_path + ": " + m);
+        }
+        a.busy_timeout(db_, 60000);
+        // the journal is the durability point: SQL commits never need to reach the disk on their own
+        exec("PRAGMA journal_mode = WAL");
+        exec("PRAGMA synchronous = OFF");
+        exec("PRAGMA foreign_keys = OFF");
+        exec("PRAGMA cache_size = -" + std::to_string(std::max<int64_t>(16, cache_mb) * 1024));
+        exec("PRAGMA wal_autocheckpoint = 0");
+        exec("CREATE TABLE IF NOT EXISTS upow_journal_state (k INTEGER PRIMARY KEY CHECK (k = 0), seq INTEGER NOT NULL)");
+        exec("INSERT OR IGNORE INTO upow_journal_state (k, seq) VALUES (0, 0)");
+        applied_ = uint64_t(query_int("SELECT seq FROM upow_journal_state WHERE k = 0"));
+        next_seq_ = applied_ + 1;
+        fd_ = ::open(journal_path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
+        if (fd_ < 0) throw std::runtime_error("ledger writer: cannot open journal " + journal_path + ": " + strerror(errno));
+        recover();
+        thread_ = std::thread([this] { run(); });
+    }
+
+    ~LedgerWriter() { close(); }
+
+    void close() {
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            if (closed_) return;
+            stop_ = true;
+        }
+        cv_.notify_all();
+        if (thread_.joinable()) thread_.join();
+        {
+            std::lock_guard<std::mutex> jl(jmu_);
+            if (fd_ >= 0) {
+                ::fdatasync(fd_);
+                ::close(fd_);
+                fd_ = -1;
+            }
+        }
+        for (auto& kv : stmts_) api().finalize(kv.second);
+        stmts_.clear();
+        if (db_) api().close_v2(db_);
+        db_ = nullptr;
+        std::lock_guard<std::mutex> lk(mu_);
+        closed_ = true;
+    }
+
+    // Commit point: append the record (and fdatasync in SYNC_COMMIT mode), queue it for the
+    // materialiser. Returns the record's sequence number.
+    uint64_t submit(const std::vector<std::string>& stmts, const std::string& meta, int64_t block_id) {
+        auto payload = std::make_shared<std::string>();
+        size_t total = 4;
+        for (auto& s : stmts) total += s.size();
+        payload->reserve(total);
+        uint32_t ns = uint32_t(stmts.size());
+        payload->append(reinterpret_cast<const char*>(&ns), 4);
+        for (auto& s : stmts) payload->append(s);
+        uint64_t seq;
+        {
+            std::lock_guard<std::mutex> jl(jmu_);
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (failed_) throw std::runtime_error("ledger writer stopped after an error: " + error_);
+                if (closed_ || stop_) throw std::runtime_error("ledger writer is closed");
+            }
+            seq = next_seq_++;
+            RecHeader h{kMagic, 0, seq, block_id, meta.size(), payload->size()};
+            h.crc = record_crc(h, meta.data(), payload->data());
+            const off_t at = journal_size_;
+            std::string head(reinterpret_cast<const char*>(&h), sizeof h);
+            write_all(fd_, head.data(), head.size());
+            write_all(fd_, meta.data(), meta.size());
+            write_all(fd_, payload->data(), payload->size());
+            if (sync_ == SYNC_COMMIT) ::fdatasync(fd_);
+            journal_size_ += off_t(sizeof h + meta.size() + payload->size());
+            if (block_id >= 0) meta_index_[block_id] = {at, seq};
+            bytes_written_ += sizeof h + meta.size() + payload->size();
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            queue_.push_back(Batch{seq, payload});
+            submitted_ = seq;
+        }
+        cv_.notify_all();
+        return seq;
+    }
+
+    // Fault injection (tests): hold queued batches back from SQL.
+    void set_paused(bool p) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            paused_ = p;
+        }
+        cv_.notify_all();
+    }
+
+    uint64_t applied() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return applied_;
+    }
+
+    // Block until every record with sequence <= seq is in the SQL tables (or the writer failed).
+    void wait(uint64_t seq, double timeout_s) {
+        std::unique_lock<std::mutex> lk(mu_);
+        auto pred = [&] { return applied_ >= seq || failed_; };
+        if (timeout_s > 0) {
+            if (!cv_done_.wait_for(lk, std::chrono::duration<double>(timeout_s), pred))
+                throw std::runtime_error("ledger writer: timed out waiting for the SQL materialiser");
+        } else {
+            cv_done_.wait(lk, pred);
+        }
+        if (failed_ && applied_ < seq) throw std::runtime_error("ledger writer failed: " + error_);
+    }
+
+    py::object journal_meta(int64_t block_id) {
+        std::lock_guard<std::mutex> jl(jmu_);
+        auto it = meta_index_.find(block_id);
+        if (it == meta_index_.end()) return py::none();
+        RecHeader h;
+        if (!read_exact(fd_, reinterpret_cast<char*>(&h), sizeof h, it->second.first) || h.magic != kMagic)
+            return py::none();
+        std::string meta(h.meta_len, '\0');
+        if (!read_exact(fd_, meta.data(), meta.size(), it->second.first + off_t(sizeof h))) return py::none();
+        return py::bytes(meta);
+    }
+
+    // Drop the undo index of blocks >= block_id (they were rolled back).
+    void forget_blocks_from(int64_t block_id) {
+        std::lock_guard<std::mutex> jl(jmu_);
+        meta_index_.erase(meta_index_.lower_bound(block_id), meta_index_.end());
+    }
+
+    py::dict stats() {
+        py::dict d;
+        std::lock_guard<std::mutex> jl(jmu_);
+        std::lock_guard<std::mutex> lk(mu_);
+        d["submitted"] = submitted_;
+        d["applied"] = applied_;
+        d["queued"] = queue_.size();
+        d["groups"] = groups_;
+        d["journal_bytes"] = int64_t(journal_size_);
+        d["bytes_written"] = bytes_written_;
+        d["apply_s"] = apply_ns_ / 1e9;
+        d["commit_s"] = commit_ns_ / 1e9;
+        d["sync_s"] = sync_ns_ / 1e9;
+        d["replayed"] = replayed_;
+        d["rotations"] = rotations_;
+        d["failed"] = failed_;
+        d["error"] = error_;
+        d["change_mismatches"] = mismatches_;
+        return d;
+    }
+
+   private:
+    void exec(const std::string& sql) {
+        char* err = nullptr;
+        int rc = api().exec(db_, sql.c_str(), nullptr, nullptr, &err);
+        if (rc != SQLITE_OK) {
+            std::string m = err ? err : api().errmsg(db_);
+            if (err) api().free(err);
+            throw SqlError("ledger writer: " + m + " [" + sql.substr(0, 120) + "]", rc);
+        }
+    }
+
+    int64_t query_int(const std::string& sql) {
+        const SqliteApi& a = api();
+        sqlite3_stmt* st = nullptr;
+        int rc = a.prepare_v2(db_, sql.c_str(), int(sql.size()), &st, nullptr);
+        if (rc != SQLITE_OK) throw SqlError(std::string("ledger writer: ") + a.errmsg(db_), rc);
+        int64_t v = 0;
+        rc = a.step(st);
+        if (rc == SQLITE_ROW) v = a.column_int64(st, 0);
+        a.finalize(st);
+        if (rc != SQLITE_ROW && rc != SQLITE_DONE) throw SqlError(std::string("ledger writer: ") + a.errmsg(db_), rc);
+        return v;
+    }
+
+    sqlite3_stmt* prepared(const std::string& sql) {
+        auto it = stmts_.find(sql);
+        if (it != stmts_.end()) return it->second;
+        sqlite3_stmt* st = nullptr;
+        int rc = api().prepare_v2(db_, sql.c_str(), int(sql.size()), &st, nullptr);
+        if (rc != SQLITE_OK) throw SqlError(std::string("ledger writer: ") + api().errmsg(db_) + " [" + sql + "]", rc);
+        if (stmts_.size() > 256) {
+            for (auto& kv : stmts_) api().finalize(kv.second);
+            stmts_.clear();
+        }
+        stmts_[sql] = st;
+        return st;
+    }
+
+    // Apply one encoded batch inside the open transaction.
+    void apply_batch(const std::string& payload) {
+        const SqliteApi& a = api();
+        In in{payload.data(), payload.data() + payload.size()};
+        const uint32_t ns = in.get<uint32_t>();
+        for (uint32_t s = 0; s < ns; ++s) {
+            const std::string sql = in.str();
+            const uint32_t flags = in.get<uint32_t>();
+            std::string guard;
+            int64_t expect = -1;
+            if (flags & 1) guard = in.str();
+            if (flags & 2) expect = in.get<int64_t>();
+            const int64_t n = in.get<int64_t>();
+            const uint32_t nc = in.get<uint32_t>();
+            std::vector<ColView> cols(nc);
+            for (auto& c : cols) {
+                c.kind = in.get<uint8_t>();
+                switch (c.kind) {
+                    case K_NULL: break;
+                    case K_CTEXT: c.ctext = in.str(); break;
+                    case K_CINT: c.cint = in.get<int64_t>(); break;
+                    case K_INT64: c.data = in.take(size_t(n) * 8); break;
+                    case K_HEX32: c.data = in.take(size_t(n) * 32); break;
+                    case K_TEXT: {
+                        const uint8_t has_null = in.get<uint8_t>();
+                        if (has_null) c.nul = reinterpret_cast<const uint8_t*>(in.take(size_t(n)));
+                        c.off = in.take(size_t(n + 1) * 8);
+                        const int64_t blen = ld64(c.off + 8 * n);
+                        c.data = in.take(size_t(blen));
+                        break;
+                    }
+                    default: throw std::runtime_error("ledger batch: bad column kind");
+                }
+            }
+            const char* order = nullptr;
+            if (in.get<uint8_t>()) order = in.take(size_t(n) * 8);
+            if (!guard.empty() && query_int(guard) == 0) continue;
+            sqlite3_stmt* st = prepared(sql);
+            int64_t changes = 0;
+            char hexbuf[8][64];
+            for (int64_t k = 0; k < n; ++k) {
+                const int64_t r = order ? ld64(order + 8 * k) : k;
+                int hb = 0;
+                for (uint32_t j = 0; j < nc; ++j) {
+                    const ColView& c = cols[j];
+                    const int p = int(j) + 1;
+                    switch (c.kind) {
+                        case K_NULL: a.bind_null(st, p); break;
+                        case K_CTEXT: a.bind_text(st, p, c.ctext.data(), int(c.ctext.size()), nullptr); break;
+                        case K_CINT: a.bind_int64(st, p, c.cint); break;
+                        case K_INT64: a.bind_int64(st, p, ld64(c.data + 8 * r)); break;
+                        case K_HEX32: {
+                            if (hb >= 8) throw std::runtime_error("at most 8 hex32 columns");
+                            char* out = hexbuf[hb++];
+                            const uint8_t* src = reinterpret_cast<const uint8_t*>(c.data) + 32 * r;
+                            for (int b = 0; b < 32; ++b) {
+                                out[2 * b] = kHex[src[b] >> 4];
+                                out[2 * b + 1] = kHex[src[b] & 15];
+                            }
+                            a.bind_text(st, p, out, 64, nullptr);
+                            break;
+                        }
+                        case K_TEXT: {
+                            if (c.nul && c.nul[r]) {
+                                a.bind_null(st, p);
+                            } else {
+                                const int64_t o0 = ld64(c.off + 8 * r), o1 = ld64(c.off + 8 * (r + 1));
+                                a.bind_text(st, p, c.data + o0, int(o1 - o0), nullptr);
+                            }
+                            break;
+                        }
+                    }
+                }
+                int rc = a.step(st);
+                if (rc != SQLITE_DONE && rc != SQLITE_ROW) {
+                    std::string m = a.errmsg(db_);
+                    a.reset(st);
+                    throw SqlError("ledger writer: " + m + " [" + sql.substr(0, 120) + "]", rc);
+                }
+                changes += a.changes(db_);
+                a.reset(st);
+            }
+            a.clear_bindings(st);
+            if (expect >= 0 && changes != expect) ++mismatches_;
+        }
+    }
+
+    // Start-up: re-apply every intact record above the recorded sequence, cut off a torn tail.
+    void recover() {
+        off_t at = 0;
+        const off_t end = ::lseek(fd_, 0, SEEK_END);
+        std::vector<std::pair<uint64_t, std::string>> redo;
+        uint64_t max_seq = applied_;
+        while (at + off_t(sizeof(RecHeader)) <= end) {
+            RecHeader h;
+            if (!read_exact(fd_, reinterpret_cast<char*>(&h), sizeof h, at) || h.magic != kMagic) break;
+            const off_t body = at + off_t(sizeof h);
+            if (h.meta_len > uint64_t(end) || h.payload_len > uint64_t(end) ||
+                body + off_t(h.meta_len + h.payload_len) > end)
+                break;
+            std::string meta(h.meta_len, '\0'), payload(h.payload_len, '\0');
+            if (!read_exact(fd_, meta.data(), meta.size(), body) ||
+                !read_exact(fd_, payload.data(), payload.size(), body + off_t(h.meta_len)))
+                break;
+            if (record_crc(h, meta.data(), payload.data()) != h.crc) break;
+            if (h.block_id >= 0) meta_index_[h.block_id] = {at, h.seq};
+            if (h.seq > applied_) redo.emplace_back(h.seq, std::move(payload));
+            max_seq = std::max<uint64_t>(max_seq, h.seq);
+            at = body + off_t(h.meta_len + h.payload_len);
+        }
+        if (at != end) {
+            if (::ftruncate(fd_, at) != 0) throw std::runtime_error("journal truncate failed");
+            ::fdatasync(fd_);
+        }
+        journal_size_ = at;
+        ::lseek(fd_, at, SEEK_SET);
+        next_seq_ = max_seq + 1;
+        if (!redo.empty()) {
+            exec("BEGIN IMMEDIATE");
+            try {
+                for (auto& r : redo) apply_batch(r.second);
+                exec("UPDATE upow_journal_state SET seq = " + std::to_string(redo.back().first) + " WHERE k = 0");
+                exec("COMMIT");
+            } catch (...) {
+                char* e = nullptr;
+                api().exec(db_, "ROLLBACK", nullptr, nullptr, &e);
+                if (e) api().free(e);
+                throw;
+            }
+            applied_ = redo.back().first;
+            replayed_ = int64_t(redo.size());
+        }
+        submitted_ = applied_;
+    }
+
+    void maybe_rotate() {
+        // all records are in SQL: make the SQL side durable, then start an empty journal
+        std::lock_guard<std::mutex> jl(jmu_);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (!queue_.empty() || applied_ != submitted_) return;
+        }
+        if (journal_max_ <= 0 || journal_size_ < journal_max_) return;
+        exec("PRAGMA synchronous = FULL");
+        exec("UPDATE upow_journal_state SET seq = seq WHERE k = 0");
+        exec("PRAGMA wal_checkpoint(PASSIVE)");
+        exec("PRAGMA synchronous = OFF");
+        if (::ftruncate(fd_, 0) != 0) throw std::runtime_error("journal truncate failed");
+        ::fdatasync(fd_);
+        ::lseek(fd_, 0, SEEK_SET);
+        journal_size_ = 0;
+        meta_index_.clear();
+        ++rotations_;
+    }
+
+    void run() {
+        for (;;) {
+            std::vector<Batch> group;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || (!queue_.empty() && !failed_ && !paused_); });
+                if (paused_ && !stop_) continue;
+                if (queue_.empty() || failed_) {
+                    if (stop_) return;
+                    continue;
+                }
+                while (!queue_.empty() && int(group.size()) < group_max_) {
+                    group.push_back(std::move(queue_.front()));
+                    queue_.pop_front();
+                }
+            }
+            auto t0 = std::chrono::steady_clock::now();
+            try {
+                if (sync_ == SYNC_GROUP) {
+                    std::lock_guard<std::mutex> jl(jmu_);
+                    ::fdatasync(fd_);
+                }
+                auto t1 = std::chrono::steady_clock::now();
+                exec("BEGIN IMMEDIATE");
+                try {
+                    for (auto& b : group) apply_batch(*b.payload);
+                    exec("UPDATE upow_journal_state SET seq = " + std::to_string(group.back().seq) + " WHERE k = 0");
+                } catch (...) {
+                    char* e = nullptr;
+                    api().exec(db_, "ROLLBACK", nullptr, nullptr, &e);
+                    if (e) api().free(e);
+                    throw;
+                }
+                auto t2 = std::chrono::steady_clock::now();
+                exec("COMMIT");
+                auto t3 = std::chrono::steady_clock::now();
+                {
+                    std::lock_guard<std::mutex> lk(mu_);
+                    applied_ = group.back().seq;
+                    ++groups_;
+                    sync_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+                    apply_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
+                    commit_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(t3 - t2).count();
+                }
+                cv_done_.notify_all();
+                maybe_rotate();
+            } catch (const std::exception& e) {
+                {
+                    std::lock_guard<std::mutex> lk(mu_);
+                    failed_ = true;
+                    error_ = e.what();
+                }
+                cv_done_.notify_all();
+            }
+        }
+    }
+
+    std::string db_path_, journal_path_;
+    int sync_;
+    int group_max_;
+    int64_t journal_max_;
+    sqlite3* db_ = nullptr;
+    std::unordered_map<std::string, sqlite3_stmt*> stmts_;  // materialiser thread only
+    int fd_ = -1;
+    off_t journal_size_ = 0;
+    std::map<int64_t, std::pair<off_t, uint64_t>> meta_index_;  // block id -> (record offset, seq)
+    std::mutex jmu_;  // journal file + meta index + next_seq_
+    uint64_t next_seq_ = 1;
+    int64_t bytes_written_ = 0;
+    std::mutex mu_;  // queue + watermark
+    std::condition_variable cv_, cv_done_;
+    std::deque<Batch> queue_;
+    uint64_t submitted_ = 0, applied_ = 0;
+    bool stop_ = false, closed_ = false, failed_ = false, paused_ = false;
+    std::string error_;
+    int64_t groups_ = 0, replayed_ = 0, rotations_ = 0, mismatches_ = 0;
+    int64_t apply_ns_ = 0, commit_ns_ = 0, sync_ns_ = 0;
+    std::thread thread_;
+};
+
+}  // namespace
+
+void register_ledger_writer(py::module_& m) {
+    m.def("ledger_encode_stmt", &encode_stmt, py::arg("sql"), py::arg("cols"), py::arg("n"),
+          py::arg("order") = py::none(), py::arg("guard") = py::none(), py::arg("expect") = py::none(),
+          "encode one column-major bulk statement for LedgerWriter.submit");
+    m.def("crc32c", [](py::buffer b) {
+        py::buffer_info bi = b.request();
+        return crc32c(0, bi.ptr, size_t(bi.size * bi.itemsize));
+    });
+    py::class_<LedgerWriter>(m, "LedgerWriter")
+        .def(py::init([](const std::string& db, const std::string& journal, int sync, int64_t cache_mb, int group_max,
+                         int64_t journal_max) {
+                 py::gil_scoped_release nogil;
+                 return new LedgerWriter(db, journal, sync, cache_mb, group_max, journal_max);
+             }),
+             py::arg("db_path"), py::arg("journal_path"), py::arg("sync_mode") = 1, py::arg("cache_mb") = 256,
+             py::arg("group_max") = 8, py::arg("journal_max_bytes") = int64_t(1) << 30)
+        .def("submit",
+             [](LedgerWriter& w, py::list stmts, py::bytes meta, int64_t block_id) {
+                 std::vector<std::string> s;
+                 s.reserve(stmts.size());
+                 for (auto x : stmts) s.push_back(x.cast<std::string>());
+                 std::string mt = meta;
+                 py::gil_scoped_release nogil;
+                 return w.submit(s, mt, block_id);
+             },
+             py::arg("stmts"), py::arg("meta") = py::bytes(""), py::arg("block_id") = -1)
+        .def("applied", &LedgerWriter::applied)
+        .def("set_paused", &LedgerWriter::set_paused)
+        .def("wait", &LedgerWriter::wait, py::arg("seq"), py::arg("timeout_s") = 0.0,
+             py::call_guard<py::gil_scoped_release>())
+        .def("journal_meta", &LedgerWriter::journal_meta)
+        .def("forget_blocks_from", &LedgerWriter::forget_blocks_from)
+        .def("stats", &LedgerWriter::stats)
+        .def("close", &LedgerWriter::close, py::call_guard<py::gil_scoped_release>());
+}
+
+}  // namespace upow

@@ -23,10 +23,13 @@ from upow_amd.constants import START_DIFFICULTY
 from upow_amd.ledger import fastpath
 from upow_amd.models.block import get_transactions_merkle_tree
 
-async def main(path, n_blocks, n_txs):
+async def main(path, n_blocks, n_txs, pause):
     db, addr, blocks, base_ts = await bench_verify._setup(n_blocks, n_txs, 99, 'host', 'cpu', ledger_path=path)
     prev = (await db.get_last_block())['hash']
     print('ready', (await db.get_last_block())['id'], flush=True)
+    if pause:  # committed to the journal, never materialised: the kill lands before SQL catch-up
+        db.flush()
+        db.writer.set_paused(True)
     for b, txs in enumerate(blocks):
         content = devnet.mine_header_raw(prev, addr, get_transactions_merkle_tree(txs), base_ts + 10 + b,
                                          START_DIFFICULTY, device='cpu')
@@ -36,15 +39,16 @@ async def main(path, n_blocks, n_txs):
         print('applied', b, flush=True)
     print('done', flush=True)
 
-asyncio.run(main(sys.argv[1], int(sys.argv[3]), int(sys.argv[4])))
+asyncio.run(main(sys.argv[1], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5] == 'pause'))
 '''
 
 
-def _run_and_kill(tmp_path, kill_after: int, delay: float) -> str:
+def _run_and_kill(tmp_path, kill_after: int, delay: float, pause: bool = False) -> str:
     path = str(tmp_path / 'ledger.sqlite3')
     env = dict(os.environ, UPOW_START_DIFFICULTY='1.5', UPOW_SNAPSHOT_EVERY='3', UPOW_DISABLE_GPU='1',
                UPOW_WAL_CHECKPOINT_PERIOD='0.05')
-    p = subprocess.Popen([sys.executable, '-c', WRITER, path, ROOT, str(BLOCKS), str(TXS)], env=env,
+    p = subprocess.Popen([sys.executable, '-c', WRITER, path, ROOT, str(BLOCKS), str(TXS),
+                          'pause' if pause else 'run'], env=env,
                          stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
     try:
         applied = -1
@@ -100,5 +104,39 @@ def test_sigkill_mid_chain_recovers_whole_blocks(tmp_path, kill_after, delay):
             return tip
         finally:
             db.close()
+
+    asyncio.run(check())
+
+
+def test_sigkill_between_journal_append_and_sql_catch_up(tmp_path):
+    """The materialiser is held back, so every block after the setup is only in the journal (and the
+    HBM/host index) when the process dies. Reopening must re-apply the journal to the tables: the tip
+    includes every block reported as applied, and the rebuilt index hashes like the SQL UTXO set."""
+    kill_after = 3
+    path = _run_and_kill(tmp_path, kill_after, 0.0, pause=True)
+    import asyncio
+
+    from upow_amd.ledger.database import Database
+
+    async def check():
+        db = Database(path, utxo_backend='host')
+        try:
+            assert db.writer.stats()['replayed'] >= kill_after + 1
+            tip = db._tip_id()
+            assert tip >= 2 + kill_after + 1
+            counts = db._q('SELECT b.id, COUNT(t.tx_hash) FROM blocks b LEFT JOIN transactions t '
+                           'ON t.block_hash = b.hash WHERE b.id > 2 GROUP BY b.id')
+            assert len(counts) == tip - 2 and all(c == TXS + 1 for _, c in counts), counts
+            assert db.utxo.set_hash() == db.sql_unspent_outputs_hash()
+            n_unspent = db._q1('SELECT COUNT(*) FROM unspent_outputs')[0]
+            assert n_unspent == 2 + BLOCKS * TXS * 2 + (tip - 2)
+        finally:
+            db.close()
+        # a second open finds nothing left to replay
+        db2 = Database(path, utxo_backend='host')
+        try:
+            assert db2.writer.stats()['replayed'] == 0 and db2._tip_id() == tip
+        finally:
+            db2.close()
 
     asyncio.run(check())

@@ -89,16 +89,19 @@ def _signed(inputs, outputs, keys, message=None):
     return tx.sign(keys)
 
 
-@pytest.mark.parametrize('native_sql', [True, False], ids=['native-writer', 'executemany'])
+@pytest.mark.parametrize('journal', [True, False], ids=['journal-writer', 'sync-executemany'])
 @pytest.mark.parametrize('backend', ['host', pytest.param('gpu', marks=pytest.mark.gpu)])
-def test_fast_path_matches_object_path(backend, native_sql, request):
+def test_fast_path_matches_object_path(backend, journal, request):
     if backend == 'gpu':
         request.getfixturevalue('gpu')
 
     async def go():
         p, base = await _setup(backend)
-        assert p.b.native_sql  # csrc/ledger_sql.cpp drives the ledger's own connection
-        p.b.native_sql = native_sql
+        assert p.b.writer is not None  # csrc/ledger_writer.cpp owns a connection of its own
+        if not journal:  # synchronous bulk writes on the Python connection (UPOW_LEDGER_WRITER=0)
+            p.b.flush()
+            p.b.writer.close()
+            p.b.writer = None
         ts = base + 60 * 10
         p.use(p.a)
         txs = []

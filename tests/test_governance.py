@@ -94,3 +94,111 @@ def test_governance_lifecycle(db):
         regular = set(await db.get_unspent_outputs(outs))
         assert regular  # governance outputs live in their own tables
     asyncio.run(go())
+
+
+GOV_QUERIES = ('get_active_inodes', 'get_inode_count', 'get_all_registered_inode', 'get_inode_ballot',
+               'get_validator_ballot')
+
+
+async def _gov_answers(db, people, check_pending):
+    """Every indexed governance query, for every address (reference: database.py:939-1436)."""
+    out = {}
+    cp = check_pending
+    out['active'] = await db.get_active_inodes(cp)
+    out['count'] = await db.get_inode_count(cp)
+    out['registered'] = await db.get_all_registered_inode(cp)
+    out['inode_ballot'] = await db.get_inode_ballot(0, 1000, cp)
+    out['validator_ballot'] = await db.get_validator_ballot(0, 1000, cp)
+    out['page'] = await db.get_validator_ballot(1, 2, cp)
+    out['multi'] = await db.get_multiple_address_stakes(set(people), cp)
+    for a in people:
+        row = out.setdefault(a, {})
+        row['stake'] = await db.get_address_stake(a, cp)
+        row['vstake'] = await db.get_validators_stake(a, cp)
+        row['ratio'] = await db.get_inode_vote_ratio_by_address(a, cp)
+        row['iballot'] = await db.get_inode_ballot_by_address(0, 1000, a, cp)
+        row['vballot'] = await db.get_validator_ballot_by_address(0, 1000, a, cp)
+        for fn in ('get_stake_outputs', 'get_inode_registration_outputs', 'get_validator_registration_outputs',
+                   'get_validators_voting_power', 'get_delegates_voting_power', 'get_validators_spent_votes',
+                   'get_delegates_spent_votes', 'get_delegates_all_power'):
+            row[fn] = [(i.tx_hash, i.index, i.amount) for i in await getattr(db, fn)(a, cp)]
+        for other in people:
+            row[('iin', other)] = [(i.tx_hash, i.index, i.amount)
+                                   for i in await db.get_inode_ballot_input_by_address(a, other, cp)]
+            row[('vin', other)] = [(i.tx_hash, i.index, i.amount)
+                                   for i in await db.get_validator_ballot_input_by_address(a, other, cp)]
+    return out
+
+
+async def _compare_index_with_sql(db, people):
+    for cp in (False, True):
+        fast = await _gov_answers(db, people, cp)
+        gov, db.gov = db.gov, None
+        try:
+            ref = await _gov_answers(db, people, cp)
+        finally:
+            db.gov = gov
+        for k in ref:
+            assert fast[k] == ref[k], (cp, k)
+    return fast
+
+
+def test_governance_index_matches_sql(db):
+    """The in-memory governance index (ledger/governance.py) answers every governance query exactly
+    like the SQL implementation, with and without the mempool overlay, through registrations, votes,
+    pending governance txs, revokes and a rollback."""
+    async def go():
+        A = B.address_of(KA)
+        inodes = [0x1100 + k for k in range(2)]
+        validators = [0x2200 + k for k in range(3)]
+        delegates = [0x3300 + k for k in range(5)]
+        people_keys = inodes + validators + delegates
+        people = [B.address_of(k) for k in people_keys]
+        ts = [1_700_000_000]
+
+        async def block(txs=()):
+            ts[0] += 60  # one block per target interval: the difficulty stays at the start value
+            return await devnet.mine_block(A, list(txs), ts=ts[0])
+
+        async def push_and_mine(*txs):
+            for t in txs:
+                assert await db.add_pending_transaction(t), t.transaction_type
+            await block(await db.get_pending_transactions_limit())
+
+        for _ in range(500):
+            await block()
+        # funding in three txs (at most 255 inputs each), each admitted before the next is built
+        for p in people[:len(inodes)]:
+            assert await db.add_pending_transaction(await B.create_transaction(KA, p, '1100'))
+        assert await db.add_pending_transaction(await B.create_transaction_to_send_multiple_wallet(
+            KA, people[len(inodes):], ['150'] * len(validators) + ['40'] * len(delegates)))
+        await block(await db.get_pending_transactions_limit())
+        await push_and_mine(*[await B.create_stake_transaction(k, '10' if k in delegates else '12')
+                              for k in people_keys])
+        await push_and_mine(*[await B.create_inode_registration_transaction(k) for k in inodes],
+                            *[await B.create_validator_registration_transaction(k) for k in validators])
+        votes = []
+        for j, k in enumerate(validators):
+            votes.append(await B.create_voting_transaction(k, 3 + j, B.address_of(inodes[j % 2])))
+        for j, k in enumerate(delegates):
+            votes.append(await B.create_voting_transaction(k, 2 + j % 4, B.address_of(validators[j % 3])))
+        await push_and_mine(*votes)
+        await _compare_index_with_sql(db, people)
+        active = await db.get_active_inodes()
+        assert sorted(a['wallet'] for a in active) == sorted(B.address_of(k) for k in inodes)
+        # pending governance state: a revoke and a second-round stake wait in the mempool
+        assert await db.add_pending_transaction(await B.create_revoke_transaction(delegates[0],
+                                                                                  B.address_of(validators[0])))
+        tip = (await db.get_last_block())['id']
+        await _compare_index_with_sql(db, people)
+        # revokes confirmed, then rolled back
+        await block(await db.get_pending_transactions_limit())
+        await _compare_index_with_sql(db, people)
+        await db.remove_blocks(tip + 1)
+        manager.Manager.difficulty = None
+        await _compare_index_with_sql(db, people)
+        # the index equals one rebuilt from the tables
+        rows = {t: dict(tab.rows) for t, tab in db.gov.tables.items()}
+        db.gov.rebuild()
+        assert rows == {t: dict(tab.rows) for t, tab in db.gov.tables.items()}
+    asyncio.run(go())

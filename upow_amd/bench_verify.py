@@ -174,11 +174,20 @@ async def _run(args, ctx, device, utxo_backend):
                            **{k: v for k, v in validate.timings.items() if k.endswith('_s')},
                            **({} if args.object_path else fastpath.timings)})
             paths.add('object' if args.object_path else fastpath.last_path)
+    # the timed region ends when the SQL tables hold every block (the journal is the commit point;
+    # the materialiser must have caught up too)
+    td = time.perf_counter()
+    db.flush()
+    drain = time.perf_counter() - td
     ctx.synchronize()
     ctx.barrier()
     wall = time.perf_counter() - t_start - untimed
     wall = ctx.allreduce_max_f(wall)
-    return total_txs, wall, stages, len(blocks[0]), sorted(paths)
+    writer = db.writer.stats() if db.writer is not None else None
+    if writer is not None:
+        writer = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in writer.items() if k != 'error'}
+    extra = {'drain_s': drain, 'writer': writer}
+    return total_txs, wall, stages, len(blocks[0]), sorted(paths), extra
 
 
 def run_verify_bench(args, ctx):
@@ -187,7 +196,7 @@ def run_verify_bench(args, ctx):
     utxo_backend = 'gpu' if device == 'gpu' else 'host'
     if not hasattr(args, 'object_path'):
         args.object_path = False
-    total_txs, wall, stages, txs_per_block, paths = asyncio.run(_run(args, ctx, device, utxo_backend))
+    total_txs, wall, stages, txs_per_block, paths, extra = asyncio.run(_run(args, ctx, device, utxo_backend))
     total = ctx.allreduce_sum(total_txs)
     tps = total / wall
     avg = {k: round(sum(s[k] for s in stages) / len(stages) * 1000, 2) for k in stages[0]
@@ -216,6 +225,11 @@ def run_verify_bench(args, ctx):
         'validate_tx_per_s': round(txs_per_block / max(1e-9, (avg.get('decode_to_checks_s', 0) + avg.get('utxo_s', 0)
                                                              + avg.get('verify_s', 0)) / 1000), 1),
         'ecdsa_sig_per_s': round(txs_per_block / max(1e-9, avg.get('ecdsa_s', 0) / 1000), 1),
+        # commit-point latency of one block (validation + journal append + HBM update), and the SQL
+        # materialiser's catch-up after the last block (inside the timed region)
+        'commit_latency_ms': avg.get('block_s'),
+        'final_drain_ms': round(extra['drain_s'] * 1000, 2),
+        'ledger_writer': extra['writer'],
     }
 
 

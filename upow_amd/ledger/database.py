@@ -14,8 +14,11 @@ from __future__ import annotations
 
 import json
 import os
+import re
 import sqlite3
+import struct
 import threading
+import weakref
 from collections import defaultdict
 from datetime import datetime, timedelta, timezone
 from decimal import ROUND_HALF_UP, Decimal
@@ -32,6 +35,7 @@ from ..utils.codec import (AddressFormat, OutputType, TransactionType, normalize
                            point_to_string, round_up_decimal, sha256, string_to_bytes, string_to_point)
 from ..utils.jsonstore import JsonStore
 from ..utils.logger import get_logger
+from .governance import GOV_TABLES, STAKE, GovernanceIndex
 from .utxo import PAYLOAD_DTYPE, TAG_BY_TABLE, UtxoIndex, make_payload
 
 logger = get_logger(__name__)
@@ -187,33 +191,119 @@ def arena_list(arena) -> List[str]:
     return _expand_col(('arena', blob, off), len(off) // 8 - 1)
 
 
+_TABLES = ('blocks', 'transactions', 'unspent_outputs', 'pending_transactions', 'pending_spent_outputs',
+           'address_transactions', 'address_index_state', *OUTPUT_TABLES[1:])
+_TABLE_RE = re.compile(r'\b(' + '|'.join(_TABLES) + r')\b')
+# tables whose rows reference transactions(tx_hash) / blocks(hash): a write to them must see the parents
+_FK_PARENTS = {t: ('transactions', 'blocks') for t in ('unspent_outputs', 'pending_spent_outputs',
+                                                       'address_transactions', *OUTPUT_TABLES[1:])}
+_FK_PARENTS['transactions'] = ('blocks',)
+_SQL_TABLES: Dict[Tuple[str, bool], Optional[frozenset]] = {}
+
+
+def _tables_of(sql: str, write: bool) -> Optional[frozenset]:
+    """Ledger tables a statement reads (or writes, with their FK parents); None = all of them
+    (a DELETE/UPDATE on blocks or transactions cascades through the output tables)."""
+    key = (sql, write)
+    hit = _SQL_TABLES.get(key, False)
+    if hit is not False:
+        return hit
+    names = set(_TABLE_RE.findall(sql))
+    res: Optional[frozenset]
+    head = sql.lstrip()[:6].upper()
+    if write and head in ('DELETE', 'UPDATE') and names & {'blocks', 'transactions'}:
+        res = None
+    else:
+        if write:
+            for t in list(names):
+                names.update(_FK_PARENTS.get(t, ()))
+        res = frozenset(names)
+    if len(_SQL_TABLES) > 4096:
+        _SQL_TABLES.clear()
+    _SQL_TABLES[key] = res
+    return res
+
+
+def _ephemeral_dir() -> str:
+    """A private directory on tmpfs for an in-memory ledger (``':memory:'``): the ledger's SQLite file
+    must be openable by two connections (Python's and the native writer's), which a SQLite
+    ``:memory:`` database is not."""
+    import tempfile
+    base = os.environ.get('UPOW_EPHEMERAL_DIR') or ('/dev/shm' if os.path.isdir('/dev/shm') and
+                                                     os.access('/dev/shm', os.W_OK) else None)
+    return tempfile.mkdtemp(prefix='upow_ledger_', dir=base)
+
+
+def _cleanup_ephemeral(state: dict):
+    w = state.get('writer')
+    if w is not None:
+        try:
+            w.close()
+        except Exception:
+            pass
+    c = state.get('conn')
+    if c is not None:
+        try:
+            c.close()
+        except Exception:
+            pass
+    d = state.get('dir')
+    if d:
+        import shutil
+        shutil.rmtree(d, ignore_errors=True)
+
+
 class Database:
-    """SQLite-backed ledger. ``Database.instance`` is the process singleton (as in the reference)."""
+    """SQLite-backed ledger. ``Database.instance`` is the process singleton (as in the reference).
+
+    Block applications of the native path are written through :class:`LedgerWriter`
+    (csrc/ledger_writer.cpp): a journal append is the commit point and a background thread on a
+    connection of its own materialises the tables. Every read through this class first waits until
+    the tables it names are materialised up to the last committed batch (:meth:`_settle`); writes
+    through the Python connection wait for the tables they write and their FK parents."""
     instance: 'Database' = None
     credentials: dict = {}
     is_indexed = True
 
     def __init__(self, path: str = ':memory:', utxo_backend: Optional[str] = None):
         self.path = path
-        self.conn = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
-        self.conn.row_factory = sqlite3.Row
+        self._eph = {}
+        if path == ':memory:':
+            self._eph['dir'] = _ephemeral_dir()
+            self.file = os.path.join(self._eph['dir'], 'ledger.sqlite3')
+            weakref.finalize(self, _cleanup_ephemeral, self._eph)
+        else:
+            self.file = path
+        self._conn = sqlite3.connect(self.file, check_same_thread=False, isolation_level=None, timeout=120)
+        self._eph['conn'] = self._conn if path == ':memory:' else None
+        self._conn.row_factory = sqlite3.Row
         self.lock = threading.RLock()
-        self.conn.execute('PRAGMA foreign_keys = ON')
-        if path != ':memory:':
-            self.conn.execute('PRAGMA journal_mode = WAL')
-            self.conn.execute('PRAGMA synchronous = NORMAL')
-            # a 2 MB block rewrites ~10 MB of B-tree pages: keep the hot index levels in a large page
-            # cache (MI355X hosts have RAM to spare), and take WAL checkpoints (page copy-back + fsync)
-            # off the block-apply path: a background thread with its own connection runs PASSIVE
-            # checkpoints; the commit-time auto-checkpoint only remains as a 400 MB safety net
-            cache_mb = int(os.environ.get('UPOW_SQLITE_CACHE_MB', '1024'))
-            self.conn.execute(f'PRAGMA cache_size = -{cache_mb * 1024}')
-            bg = os.environ.get('UPOW_WAL_CHECKPOINT_THREAD', '1') != '0'
-            auto = int(os.environ.get('UPOW_WAL_AUTOCHECKPOINT', '100000' if bg else '10000'))
-            self.conn.execute(f'PRAGMA wal_autocheckpoint = {auto}')
-            if bg:
-                self._start_checkpointer(float(os.environ.get('UPOW_WAL_CHECKPOINT_PERIOD', '0.5')))
-        self.conn.executescript(SCHEMA)
+        self.writer = None
+        self._submitted = 0
+        self._applied_seen = 0
+        self._table_seq: Dict[str, int] = {}
+        self._tip_cache: Optional[dict] = None
+        self._tip_gen = 0
+        self._genesis_cache: Optional[str] = None
+        self._pending_empty: Optional[bool] = None
+        self._mempool_ver = 0
+        self._conn.execute('PRAGMA foreign_keys = ON')
+        self._conn.execute('PRAGMA journal_mode = WAL')
+        self._conn.execute('PRAGMA synchronous = ' + ('OFF' if path == ':memory:' else 'NORMAL'))
+        # a 2 MB block rewrites ~10 MB of B-tree pages: keep the hot index levels in a large page
+        # cache (MI355X hosts have RAM to spare), and take WAL checkpoints (page copy-back + fsync)
+        # off the block-apply path: a background thread with its own connection runs PASSIVE
+        # checkpoints; the commit-time auto-checkpoint only remains as a 400 MB safety net
+        cache_mb = int(os.environ.get('UPOW_SQLITE_CACHE_MB', '1024' if path != ':memory:' else '256'))
+        self._conn.execute(f'PRAGMA cache_size = -{cache_mb * 1024}')
+        bg = os.environ.get('UPOW_WAL_CHECKPOINT_THREAD', '1') != '0'
+        auto = int(os.environ.get('UPOW_WAL_AUTOCHECKPOINT', '100000' if bg else '10000'))
+        self._conn.execute(f'PRAGMA wal_autocheckpoint = {auto}')
+        if bg:
+            self._start_checkpointer(float(os.environ.get('UPOW_WAL_CHECKPOINT_PERIOD', '0.5')))
+        self._conn.executescript(SCHEMA)
+        if os.environ.get('UPOW_LEDGER_WRITER', '1') != '0':
+            self._open_writer(cache_mb)
         store_dir = os.path.dirname(path) if path != ':memory:' else None
         self.emission_details = JsonStore(os.path.join(store_dir, 'emission_details.json') if store_dir else None)
         self.utxo = UtxoIndex(backend=utxo_backend)
@@ -224,7 +314,29 @@ class Database:
                 self.utxo_source = 'snapshot'
         if self.utxo_source == 'sql':
             self._rebuild_utxo_index()
-        self.native_sql = self._probe_native_sql()
+        self.gov: Optional[GovernanceIndex] = None
+        if os.environ.get('UPOW_GOV_INDEX', '1') != '0':
+            self.gov = GovernanceIndex(self)
+            self.gov.rebuild()
+
+    def _open_writer(self, cache_mb: int):
+        """The native writer owns its own connection to the same file. Opening it re-applies any
+        journal records that were committed but not yet materialised when the process stopped."""
+        from ..ops.native import lib
+        mode = {'off': 0, 'group': 1, 'commit': 2}[os.environ.get('UPOW_JOURNAL_SYNC', 'group')]
+        if self.path == ':memory:':
+            mode = 0
+        journal = os.environ.get('UPOW_JOURNAL_PATH') or os.path.join(os.path.dirname(os.path.abspath(self.file)),
+                                                                       os.path.basename(self.file) + '.journal')
+        self.writer = lib().LedgerWriter(self.file, journal, mode, cache_mb,
+                                         int(os.environ.get('UPOW_WRITER_GROUP', '8')),
+                                         int(os.environ.get('UPOW_JOURNAL_MAX_MB', '1024')) << 20)
+        self._eph['writer'] = self.writer if self.path == ':memory:' else None
+        self.journal_path = journal
+        st = self.writer.stats()
+        self._submitted = self._applied_seen = st['applied']
+        if st['replayed']:
+            logger.info(f'ledger journal: re-applied {st["replayed"]} committed batch(es) to the SQL tables')
 
     # ------------------------------------------------------------------ lifecycle
     @staticmethod
@@ -245,6 +357,9 @@ class Database:
         return Database.instance
 
     def _tip_id(self) -> int:
+        tip = self._tip_cache
+        if tip is not None:
+            return int(tip['id'])
         row = self._q1('SELECT MAX(id) FROM blocks')
         return int(row[0] or 0)
 
@@ -256,7 +371,7 @@ class Database:
         back into the database file without blocking the writer (the fsync happens here, not at the
         block's COMMIT). sqlite3 releases the GIL while the checkpoint runs."""
         self._ckpt_stop = threading.Event()
-        path = self.path
+        path = self.file
 
         def run(stop: threading.Event):
             conn = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
@@ -278,91 +393,130 @@ class Database:
             self._ckpt_stop.set()
             self._ckpt_thread.join(timeout=10)
             self._ckpt_stop = None
+        if self.writer is not None:
+            self.writer.close()  # drains the queue into SQL first
         with self.lock:
-            self.conn.close()
+            self._conn.close()
+        if self.path == ':memory:':
+            _cleanup_ephemeral(self._eph)
+
+    # ------------------------------------------------------------------ materialisation barrier
+    def _settle(self, tables: Optional[frozenset] = None):
+        """Wait until the SQL tables in ``tables`` (None: all) hold every batch committed to the
+        journal that writes them. No-op when the writer is idle or absent."""
+        if self.writer is None:
+            return
+        if tables is None:
+            target = self._submitted
+        else:
+            ts = self._table_seq
+            target = max((ts.get(t, 0) for t in tables), default=0)
+        if target <= self._applied_seen:
+            return
+        applied = self.writer.applied()
+        if applied < target:
+            self.writer.wait(target, float(os.environ.get('UPOW_WRITER_WAIT_TIMEOUT', '600')))
+            applied = max(applied, target)
+        if applied > self._applied_seen:
+            self._applied_seen = applied
+
+    def flush(self):
+        """Block until the SQL tables hold every committed block (tests, tools, shutdown)."""
+        self._settle(None)
+
+    @property
+    def conn(self) -> sqlite3.Connection:
+        """The Python connection, after the tables are fully materialised (direct callers may read or
+        write anything). Hot paths use :meth:`_q`/:meth:`_x`, which only wait for what they touch."""
+        self._settle(None)
+        self._invalidate_for(None)
+        return self._conn
+
+    def _invalidate_for(self, tables: Optional[frozenset]):
+        if tables is None or 'blocks' in tables:
+            self._tip_cache = None
+            self._genesis_cache = None
+            self._tip_gen += 1
+        if tables is None or 'pending_transactions' in tables or 'pending_spent_outputs' in tables:
+            self._pending_empty = None
+            self._mempool_ver += 1
+
+    def submit_batch(self, stmts: List[bytes], tables: Iterable[str], meta: bytes = b'', block_id: int = -1) -> int:
+        """Commit a batch of encoded statements (``lib().ledger_encode_stmt``) through the journal. The
+        Python lock keeps a batch from landing while a Python-side SQL transaction is open."""
+        with self.lock:
+            if self._tx_depth:
+                raise RuntimeError('ledger batch submitted inside an open SQL transaction')
+            seq = self.writer.submit(stmts, meta, block_id)
+            self._submitted = seq
+            for t in tables:
+                self._table_seq[t] = seq
+        return seq
 
     # ------------------------------------------------------------------ SQL helpers
     def _q(self, sql: str, args: Iterable = ()) -> List[sqlite3.Row]:
+        self._settle(_tables_of(sql, False))
         with self.lock:
-            return self.conn.execute(sql, tuple(args)).fetchall()
+            return self._conn.execute(sql, tuple(args)).fetchall()
 
     def _q1(self, sql: str, args: Iterable = ()):
+        self._settle(_tables_of(sql, False))
         with self.lock:
-            return self.conn.execute(sql, tuple(args)).fetchone()
+            return self._conn.execute(sql, tuple(args)).fetchone()
 
     def _x(self, sql: str, args: Iterable = ()):
+        t = _tables_of(sql, True)
+        self._settle(t)
         with self.lock:
-            return self.conn.execute(sql, tuple(args))
+            self._invalidate_for(t)
+            return self._conn.execute(sql, tuple(args))
 
     def _xm(self, sql: str, rows: Iterable):
+        t = _tables_of(sql, True)
+        self._settle(t)
         with self.lock:
-            self.conn.executemany(sql, rows)
+            self._invalidate_for(t)
+            return self._conn.executemany(sql, rows)
 
     # ------------------------------------------------------------------ native bulk writes
-    def _probe_native_sql(self) -> bool:
-        """Can csrc/ledger_sql.cpp drive THIS connection's sqlite3 handle? Proven by a round trip on a
-        TEMP table: rows the native side inserts must be visible to (and counted by) the Python
-        connection. ``UPOW_NATIVE_SQL=0`` keeps every write on ``sqlite3.executemany``."""
-        if os.environ.get('UPOW_NATIVE_SQL', '1') == '0':
-            return False
-        import platform
-        import sys
-        # the handle is read from pysqlite_Connection's first field: only for CPython builds whose
-        # layout is known (3.8-3.12 keep `sqlite3 *db` right after PyObject_HEAD)
-        if platform.python_implementation() != 'CPython' or not (3, 8) <= sys.version_info[:2] <= (3, 12):
-            return False
-        try:
-            from ..ops.native import lib
-            L = lib()
-            with self.lock:
-                c = self.conn
-                c.execute('CREATE TEMP TABLE IF NOT EXISTS _native_probe (x INTEGER)')
-                c.execute('DELETE FROM _native_probe')
-                c.executemany('INSERT INTO _native_probe VALUES (?)', [(1,), (2,), (3,)])
-                fn, changes, _ = L.sql_probe(c)
-                want = '' if self.path == ':memory:' else os.path.realpath(self.path)
-                same = (fn == want or (fn and os.path.realpath(fn) == want)) and changes == c.total_changes
-                if same:
-                    n = L.sql_executemany(c, 'INSERT INTO _native_probe VALUES (?)', [np.array([4, 5], np.int64)], 2)
-                    same = n == 2 and c.execute('SELECT SUM(x) FROM _native_probe').fetchone()[0] == 15
-                c.execute('DROP TABLE _native_probe')
-            return bool(same)
-        except Exception as e:  # pragma: no cover - depends on the interpreter build
-            logger.warning(f'native ledger writer disabled: {e}')
-            return False
+    @staticmethod
+    def encode(sql: str, cols: list, n: int, order=None, guard: Optional[str] = None,
+               expect: Optional[int] = None) -> bytes:
+        """One column-major bulk statement for :meth:`submit_batch`. Column specs as in
+        csrc/ledger_writer.cpp: text lists, int64 arrays, ('gather'|'hex32'|'arena', ...) views of the
+        block codec's buffers, or one constant for every row."""
+        from ..ops.native import lib
+        return lib().ledger_encode_stmt(sql, cols, n, order, guard, expect)
 
     def bulk(self, sql: str, cols: list, n: int, order=None) -> int:
-        """Column-major executemany; returns the summed row changes. Column specs as in
-        csrc/ledger_sql.cpp (text lists, int64 arrays, ('gather'|'hex32'|'arena', ...) views of the block
-        codec's buffers, or one constant). Without the native writer the same specs are expanded to
-        Python rows for ``sqlite3.executemany``."""
+        """Column-major executemany on the Python connection (synchronous); returns the row changes."""
         if n == 0:
             return 0
-        if self.native_sql:
-            from ..ops.native import lib
-            with self.lock:
-                return lib().sql_executemany(self.conn, sql, cols, n, order)
         rows = list(zip(*[_expand_col(c, n) for c in cols]))
         if order is not None:
             rows = [rows[i] for i in np.asarray(order).tolist()]
-        with self.lock:
-            return self.conn.executemany(sql, rows).rowcount
+        return self._xm(sql, rows).rowcount
 
     class _Tx:
         """Re-entrant SQL transaction: only the outermost level issues BEGIN/COMMIT/ROLLBACK, so a
-        whole block application (many helper calls) commits or rolls back as one unit."""
+        whole block application (many helper calls) commits or rolls back as one unit. The outermost
+        level first waits for the native writer to drain (it cannot take the write lock meanwhile)."""
 
         def __init__(self, db, foreign_keys: bool = True):
             self.db = db
             self.fk = foreign_keys
 
         def __enter__(self):
+            if self.db._tx_depth == 0:
+                self.db._settle(None)
             self.db.lock.acquire()
             if self.db._tx_depth == 0:
+                c = self.db._conn
                 if not self.fk:  # only settable outside a transaction
-                    self.db.conn.execute('PRAGMA foreign_keys = OFF')
-                self.db.conn.execute('BEGIN')
+                    c.execute('PRAGMA foreign_keys = OFF')
+                c.execute('BEGIN')
                 self.db._fk_off = not self.fk
+                self.db._invalidate_for(None)
             self.db._tx_depth += 1
             return self.db
 
@@ -370,9 +524,10 @@ class Database:
             try:
                 self.db._tx_depth -= 1
                 if self.db._tx_depth == 0:
-                    self.db.conn.execute('COMMIT' if et is None else 'ROLLBACK')
+                    self.db._conn.execute('COMMIT' if et is None else 'ROLLBACK')
+                    self.db._invalidate_for(None)
                     if self.db._fk_off:
-                        self.db.conn.execute('PRAGMA foreign_keys = ON')
+                        self.db._conn.execute('PRAGMA foreign_keys = ON')
                         self.db._fk_off = False
                 elif et is not None:
                     self.db._tx_failed = True
@@ -385,9 +540,7 @@ class Database:
     _fk_off = False
 
     def transaction(self, foreign_keys: bool = True):
-        """``foreign_keys=False``: skip FK enforcement for this (outermost) transaction — the native
-        block path, which only inserts rows whose parents it inserted in the same transaction and
-        deletes nothing that cascades."""
+        """``foreign_keys=False``: skip FK enforcement for this (outermost) transaction."""
         return Database._Tx(self, foreign_keys)
 
     # fault injection (tests): raise inside block application after the named stage
@@ -412,6 +565,8 @@ class Database:
                 amounts.append(r[2])
                 addrs.append(_addr_bytes(r[3]))
         self.utxo.reset(keys, tags, make_payload(amounts, addrs))
+        if getattr(self, 'gov', None) is not None:
+            self.gov.rebuild()
 
     async def _payload_from_ledger(self, outpoints: List[Tuple[str, int]]):
         infos = await self.get_transactions_info([h for h, _ in outpoints])
@@ -431,9 +586,10 @@ class Database:
             # a single tx's inputs (mempool admission): exact (tx_hash, index) probes on the outpoint
             # index, instead of pulling every row of each funding tx (often hundreds) into Python
             found = []
+            self._settle(frozenset((table,)))
             with self.lock:
                 for h, i in want:
-                    for r in self.conn.execute(f'SELECT rowid FROM {table} WHERE tx_hash = ? AND "index" = ?', (h, i)):
+                    for r in self._conn.execute(f'SELECT rowid FROM {table} WHERE tx_hash = ? AND "index" = ?', (h, i)):
                         found.append((r[0], (h, i)))
             found.sort()
             return [o for _, o in found]
@@ -449,9 +605,8 @@ class Database:
         return [o for _, o in out]
 
     def _delete_outpoints(self, table: str, inputs: List[Tuple[str, int]]) -> int:
-        with self.lock:
-            return self.conn.executemany(f'DELETE FROM {table} WHERE tx_hash = ? AND "index" = ?',
-                                         [(h, int(i)) for h, i in inputs]).rowcount
+        return self._xm(f'DELETE FROM {table} WHERE tx_hash = ? AND "index" = ?',
+                        [(h, int(i)) for h, i in inputs]).rowcount
 
     def _pending_spent_set(self) -> Set[Tuple[str, int]]:
         return {(r[0], r[1]) for r in self._q('SELECT tx_hash, "index" FROM pending_spent_outputs')}
@@ -485,13 +640,11 @@ class Database:
         nothing to do. A mempool much smaller than the block: delete only the hashes it holds. Otherwise
         (the usual case for a mined block, whose txs came from the mempool) one native bulk delete."""
         txids = np.ascontiguousarray(txids, dtype=np.uint8).reshape(-1, 32)
-        with self.lock:
-            n_pending = self.conn.execute('SELECT COUNT(*) FROM pending_transactions').fetchone()[0]
+        n_pending = self._q1('SELECT COUNT(*) FROM pending_transactions')[0]
         if n_pending == 0 or not len(txids):
             return 0
         if 4 * n_pending < len(txids):
-            with self.lock:
-                pending = {r[0] for r in self.conn.execute('SELECT tx_hash FROM pending_transactions')}
+            pending = {r[0] for r in self._q('SELECT tx_hash FROM pending_transactions')}
             keep = [k for k, t in enumerate(txids) if bytes(t).hex() in pending]
             txids = txids[keep]
             if not len(txids):
@@ -500,12 +653,11 @@ class Database:
                          len(txids), self._key_order(txids))
 
     async def remove_pending_transactions_by_hash(self, tx_hashes: List[str]):
-        with self.lock:
-            # only the hashes present in the (small) mempool: no index probe per confirmed tx
-            pending = {r[0] for r in self.conn.execute('SELECT tx_hash FROM pending_transactions')}
-            hit = [(h,) for h in tx_hashes if h in pending] if pending else []
-            if hit:
-                self.conn.executemany('DELETE FROM pending_transactions WHERE tx_hash = ?', hit)
+        # only the hashes present in the (small) mempool: no index probe per confirmed tx
+        pending = {r[0] for r in self._q('SELECT tx_hash FROM pending_transactions')}
+        hit = [(h,) for h in tx_hashes if h in pending] if pending else []
+        if hit:
+            self._xm('DELETE FROM pending_transactions WHERE tx_hash = ?', hit)
 
     async def remove_pending_transactions(self):
         with self.transaction():
@@ -535,7 +687,10 @@ class Database:
         self._rebuild_utxo_index()
 
     async def remove_blocks(self, block_no: int):
-        """database.py:146-169: roll back blocks >= block_no and restore the outputs they spent."""
+        """database.py:146-169: roll back blocks >= block_no and restore the outputs they spent. The UTXO
+        index is rolled back from the journal's undo records when every removed block has one, else
+        rebuilt from the tables."""
+        tip = self._tip_id()
         blocks_to_remove = await self.get_blocks(block_no, 500)
         transactions_to_remove, transactions_hashes = [], []
         for b in blocks_to_remove:
@@ -546,10 +701,18 @@ class Database:
         for tx in transactions_to_remove:
             if isinstance(tx, Transaction):
                 outputs_to_be_restored.extend([(i.tx_hash, i.index) for i in tx.inputs if i.tx_hash not in hashes])
+        undone = self._undo_blocks_in_index(block_no, tip)
         self._x('DELETE FROM blocks WHERE id >= ?', (block_no,))
         self._address_index_rollback()
-        await self.add_unspent_outputs(outputs_to_be_restored)
-        self._rebuild_utxo_index()
+        await self.add_unspent_outputs(outputs_to_be_restored, index=not undone)
+        if self.writer is not None:
+            self.writer.forget_blocks_from(block_no)
+        if not undone:
+            self._rebuild_utxo_index()
+        elif self.gov is not None:
+            self.gov.rebuild()
+        self.utxo_rollbacks = getattr(self, 'utxo_rollbacks', 0) + 1
+        self.last_rollback_undo = undone
 
     def _pending_rows_ordered(self):
         """``ORDER BY fees / LENGTH(tx_hex) DESC, LENGTH(tx_hex), tx_hex`` (database.py:173-174)."""
@@ -589,9 +752,7 @@ class Database:
 
     async def update_pending_transactions_propagation_time(self, txs_hash: List[str]):
         now = int(_utcnow().replace(tzinfo=timezone.utc).timestamp())
-        with self.lock:
-            self.conn.executemany('UPDATE pending_transactions SET propagation_time = ? WHERE tx_hash = ?',
-                                  [(now, h) for h in txs_hash])
+        self._xm('UPDATE pending_transactions SET propagation_time = ? WHERE tx_hash = ?', [(now, h) for h in txs_hash])
 
     async def get_next_block_average_fee(self):
         rows = sorted(self._q('SELECT LENGTH(tx_hex) AS size, fees FROM pending_transactions'),
@@ -634,8 +795,8 @@ class Database:
         :meth:`index_addresses` — off the block-apply critical path."""
         try:
             with self.transaction():
-                self.conn.executemany('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, '
-                                      'outputs_addresses, outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)', rows)
+                self._xm('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, '
+                         'outputs_addresses, outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)', rows)
         except sqlite3.IntegrityError as e:
             raise UniqueViolationError(str(e)) from e
 
@@ -750,8 +911,9 @@ class Database:
         if not hashes:
             return []
         want = set(hashes)
+        self._settle(frozenset(('pending_transactions',)))
         with self.lock:
-            cur = self.conn.cursor()
+            cur = self._conn.cursor()
             cur.row_factory = None  # plain tuples: this scans the whole mempool
             rows = cur.execute('SELECT tx_hash, tx_hex FROM pending_transactions').fetchall()
         return [x for h, x in rows if h in want]
@@ -792,12 +954,23 @@ class Database:
                 return await Transaction.from_hex(r['tx_hex'])
         return None
 
+    def _last_block_row(self) -> Optional[dict]:
+        """The tip row, from the chain-tip cache the native block path keeps (no wait for the SQL
+        materialiser) or from SQL."""
+        tip = self._tip_cache
+        if tip is None:
+            gen = self._tip_gen
+            tip = self._block_row(self._q1('SELECT * FROM blocks ORDER BY id DESC LIMIT 1'))
+            if gen == self._tip_gen:  # no block landed or was removed meanwhile
+                self._tip_cache = tip
+        return dict(tip) if tip is not None else None
+
     async def get_last_block(self) -> Optional[dict]:
-        return self._block_row(self._q1('SELECT * FROM blocks ORDER BY id DESC LIMIT 1'))
+        return self._last_block_row()
 
     async def get_next_block_id(self) -> int:
-        r = self._q1('SELECT id FROM blocks ORDER BY id DESC LIMIT 1')
-        return (r[0] if r is not None else 0) + 1
+        tip = self._last_block_row()
+        return (tip['id'] if tip is not None else 0) + 1
 
     async def get_block(self, block_hash: str) -> Optional[dict]:
         return self._block_row(self._q1('SELECT * FROM blocks WHERE hash = ?', (block_hash,)))
@@ -828,6 +1001,9 @@ class Database:
 
     async def get_block_by_id(self, block_id: int) -> Optional[dict]:
         # calculate_difficulty passes `id - BLOCKS_COUNT + 1` as a Decimal (manager.py:95-97)
+        tip = self._tip_cache
+        if tip is not None and tip['id'] == int(block_id):
+            return dict(tip)
         return self._block_row(self._q1('SELECT * FROM blocks WHERE id = ?', (int(block_id),)))
 
     async def get_block_transactions(self, block_hash: str, check_signatures: bool = True, hex_only: bool = False):
@@ -849,7 +1025,7 @@ class Database:
         return [{'hash': r['tx_hash'], 'is_coinbase': not _arr(r['inputs_addresses'])} for r in rows]
 
     # ------------------------------------------------------------------ outputs (database.py:439-580)
-    async def add_unspent_outputs(self, outputs: List[tuple]) -> None:
+    async def add_unspent_outputs(self, outputs: List[tuple], index: bool = True) -> None:
         if not outputs:
             return
         payload = None
@@ -869,88 +1045,180 @@ class Database:
             rows = [(o[0], o[1], o[2], None if o[3] is None else int(bool(o[3]))) for o in outputs]
             if len(outputs[0]) >= 5:  # (tx_hash, index, address, is_stake, amount in smallest units)
                 payload = make_payload([o[4] for o in outputs], [_addr_bytes(o[2]) for o in outputs])
-        with self.lock:
-            self.conn.executemany('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) '
-                                  'VALUES (?, ?, ?, ?)', rows)
+        self._xm('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) VALUES (?, ?, ?, ?)', rows)
+        if self.gov is not None:
+            self.gov.added(STAKE, [(r[0], r[1]) for r in rows if r[3] == 1])
+        if not index:
+            return
         if payload is None:
             payload = await self._payload_from_ledger([(r[0], r[1]) for r in rows])
         self.utxo.insert([(r[0], r[1]) for r in rows], TAG_BY_TABLE['unspent_outputs'], payload)
 
-    def insert_regular_outputs(self, indexes: np.ndarray, addresses, txids: np.ndarray, amounts: np.ndarray,
-                               addrs: np.ndarray, lens: np.ndarray) -> None:
-        """Native block path: REGULAR outputs as (tx_hash, index, address, is_stake=0) rows + one index
-        insert with their payloads (amount, normalised address bytes) — ``add_unspent_outputs`` in bulk.
-        ``txids``: n x 32 creating-tx digests; ``addresses``: a bulk text column spec (see :meth:`bulk`)."""
-        n = len(indexes)
-        if not n:
-            return
-        txids = np.ascontiguousarray(txids, dtype=np.uint8)
-        indexes = np.ascontiguousarray(indexes, dtype=np.int64)
-        self.bulk('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) VALUES (?, ?, ?, ?)',
-                  [('hex32', txids, 32, 0), indexes, addresses, 0], n)
-        recs = np.zeros((n, 40), dtype=np.uint8)
-        recs[:, :32] = txids
-        recs[:, 32:36] = indexes.astype(np.uint32).reshape(n, 1).view(np.uint8)
-        recs[:, 36:40] = np.full((n, 1), TAG_BY_TABLE['unspent_outputs'], dtype=np.uint32).view(np.uint8)
-        pay = np.zeros(n, dtype=PAYLOAD_DTYPE)
-        pay['amount'] = amounts
-        pay['len'] = lens
-        a = np.array(addrs, dtype=np.uint8, copy=True)
-        c33 = lens == 33
-        a[c33, 0] = np.where(a[c33, 0] == 43, 43, 42)  # bytes_to_string normalises the prefix
-        pay['addr'] = a
-        self.utxo.insert_records(recs, pay)
-
     @staticmethod
     def _key_order(in_keys: np.ndarray) -> np.ndarray:
-        """Row order sorted by the leading 8 bytes of the tx hash: B-tree locality for bulk deletes
-        (the set of deleted rows, and so the result, does not depend on the order)."""
+        """Row order sorted by the leading 8 bytes of the tx hash: B-tree locality for bulk writes
+        (the set of rows written, and so the result, does not depend on the order)."""
         return np.argsort(in_keys[:, :8].copy().view('>u8').ravel(), kind='stable').astype(np.int64)
 
-    def remove_spent_regular(self, in_keys: np.ndarray) -> bool:
-        """Native block path: ``remove_unspent_outputs`` for REGULAR spends (same partial-delete semantics).
-        ``in_keys``: n x 40 outpoint records (txid 32 B, index u32, tag u32)."""
-        n_in = len(in_keys)
-        if not n_in:
-            return True
-        in_keys = np.ascontiguousarray(in_keys, dtype=np.uint8)
-        idx = in_keys[:, 32:36].copy().view(np.uint32).ravel().astype(np.int64)
-        with self.transaction():
-            n = self.bulk('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
-                          [('hex32', in_keys, 40, 0), idx], n_in, self._key_order(in_keys))
-        recs = np.array(in_keys, dtype=np.uint8, copy=True)
-        recs[:, 36:40] = np.full((n_in, 1), TAG_BY_TABLE['unspent_outputs'], dtype=np.uint32).view(np.uint8)
-        self.utxo.erase_records(recs)
-        if n != n_in:
-            logger.error(f'Failed to delete all UTXOs: {n} of {n_in} deleted')
-            return False
-        return True
+    def _mempool_empty(self) -> bool:
+        """Are both mempool tables empty? Cached until a Python-side write touches them."""
+        if self._pending_empty is None:
+            self._pending_empty = self._q1('SELECT EXISTS(SELECT 1 FROM pending_transactions) OR '
+                                           'EXISTS(SELECT 1 FROM pending_spent_outputs)')[0] == 0
+        return self._pending_empty
 
-    def remove_pending_spent_keys(self, in_keys: np.ndarray) -> int:
-        """``DELETE FROM pending_spent_outputs`` for every spent outpoint of a block (n x 40 key records),
-        with the same three cases as :meth:`remove_pending_by_txids`."""
-        keys = np.ascontiguousarray(in_keys, dtype=np.uint8).reshape(-1, 40)
-        with self.lock:
-            n_pending = self.conn.execute('SELECT COUNT(*) FROM pending_spent_outputs').fetchone()[0]
-        if n_pending == 0 or not len(keys):
-            return 0
-        idx = keys[:, 32:36].copy().view(np.uint32).ravel().astype(np.int64)
-        if 4 * n_pending < len(keys):
-            with self.lock:
-                have = {(r[0], r[1]) for r in self.conn.execute('SELECT tx_hash, "index" FROM pending_spent_outputs')}
-            keep = [k for k in range(len(keys)) if (bytes(keys[k, :32]).hex(), int(idx[k])) in have]
-            keys, idx = keys[keep], idx[keep]
-            if not len(keys):
-                return 0
-        return self.bulk('DELETE FROM pending_spent_outputs WHERE tx_hash = ? AND "index" = ?',
-                         [('hex32', keys, 40, 0), idx], len(keys), self._key_order(keys))
+    def apply_native_block(self, block_row: dict, coinbase_row: tuple, coinbase_outputs: list, n: int,
+                           tx_cols: list, out_cols: tuple, in_keys: np.ndarray, spent_payload: np.ndarray) -> int:
+        """The ledger writes of one native-path block (reference manager.py:706-730: add_block,
+        add_transaction(coinbase), add_transactions, add_transaction_outputs, remove_pending_transactions,
+        remove_outputs, remove_pending_spent_outputs) as ONE journal batch, plus the HBM index update.
+
+        ``tx_cols``: bulk column specs of the n tx rows (tx_hash, tx_hex, inputs_addresses,
+        outputs_addresses, outputs_amounts, fees); ``out_cols``: (index int64, address text spec,
+        txids n x 32, amounts u64, raw addresses n x 64, address lengths) of the REGULAR outputs;
+        ``in_keys``: n x 40 spent outpoint records; ``spent_payload``: their index payloads (undo data).
+        Returns the journal sequence number (0 without the native writer: written synchronously)."""
+        out_index, out_addr_spec, out_txid, out_amount, out_addr, out_len = out_cols
+        n_out, n_in = len(out_index), len(in_keys)
+        tag_u = TAG_BY_TABLE['unspent_outputs']
+        # ---- index records: created outputs (block txs + coinbase) and spent inputs
+        recs = np.zeros((n_out, 40), dtype=np.uint8)
+        recs[:, :32] = out_txid
+        recs[:, 32:36] = out_index.astype(np.uint32).reshape(-1, 1).view(np.uint8)
+        recs[:, 36:40] = np.full((n_out, 1), tag_u, dtype=np.uint32).view(np.uint8)
+        pay = np.zeros(n_out, dtype=PAYLOAD_DTYPE)
+        pay['amount'] = out_amount
+        pay['len'] = out_len
+        a = np.array(out_addr, dtype=np.uint8, copy=True)
+        c33 = out_len == 33
+        a[c33, 0] = np.where(a[c33, 0] == 43, 43, 42)  # bytes_to_string normalises the prefix
+        pay['addr'] = a
+        from .utxo import pack_records
+        cb_keys = [(o[0], o[1]) for o in coinbase_outputs]
+        cb_recs = pack_records(cb_keys, tag_u)
+        cb_pay = make_payload([o[4] for o in coinbase_outputs], [_addr_bytes(o[2]) for o in coinbase_outputs])
+        in_keys = np.ascontiguousarray(in_keys, dtype=np.uint8).reshape(-1, 40)
+        spent = np.array(in_keys, dtype=np.uint8, copy=True)
+        spent[:, 36:40] = np.full((n_in, 1), tag_u, dtype=np.uint32).view(np.uint8)
+        in_idx = in_keys[:, 32:36].copy().view(np.uint32).ravel().astype(np.int64)
+        in_order = self._key_order(in_keys) if n_in else None
+
+        # ---- statements (schema.sql write set of one block)
+        b = block_row
+        stmts = [
+            ('INSERT INTO blocks (id, hash, content, address, random, difficulty, reward, timestamp) '
+             'VALUES (?, ?, ?, ?, ?, ?, ?, ?)',
+             [int(b['id']), b['hash'], b['content'], b['address'], int(b['random']), b['difficulty'], b['reward'],
+              int(b['timestamp'])], 1, None, None, None),
+            ('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, outputs_addresses, '
+             'outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)', list(coinbase_row), 1, None, None, None),
+        ]
+        self.checkpoint('block')
+        stmts.append(('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, outputs_addresses, '
+                      'outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)', [b['hash'], *tx_cols], n, None, None, None))
+        self.checkpoint('transactions')
+        ins_u = 'INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) VALUES (?, ?, ?, ?)'
+        if n_out:
+            stmts.append((ins_u, [('hex32', np.ascontiguousarray(out_txid), 32, 0),
+                                  np.ascontiguousarray(out_index, dtype=np.int64), out_addr_spec, 0],
+                          n_out, None, None, None))
+        if coinbase_outputs:
+            stmts.append((ins_u, [[o[0] for o in coinbase_outputs], np.array([o[1] for o in coinbase_outputs], np.int64),
+                                  [o[2] for o in coinbase_outputs],
+                                  [None if o[3] is None else str(int(bool(o[3]))) for o in coinbase_outputs]],
+                          len(coinbase_outputs), None, None, None))
+        self.checkpoint('outputs')
+        tables = {'blocks', 'transactions', 'unspent_outputs'}
+        mempool = n and not self._mempool_empty()
+        if mempool:
+            txids = np.ascontiguousarray(tx_cols[0][1], dtype=np.uint8).reshape(-1, 32)
+            stmts.append(('DELETE FROM pending_transactions WHERE tx_hash = ?', [('hex32', txids, 32, 0)], n,
+                          self._key_order(txids), 'SELECT EXISTS(SELECT 1 FROM pending_transactions)', None))
+        if n_in:
+            stmts.append(('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
+                          [('hex32', in_keys, 40, 0), in_idx], n_in, in_order, None, n_in))
+        if mempool and n_in:
+            stmts.append(('DELETE FROM pending_spent_outputs WHERE tx_hash = ? AND "index" = ?',
+                          [('hex32', in_keys, 40, 0), in_idx], n_in, in_order,
+                          'SELECT EXISTS(SELECT 1 FROM pending_spent_outputs)', None))
+            tables |= {'pending_transactions', 'pending_spent_outputs'}
+        self.checkpoint('spent')
+
+        seq = 0
+        if self.writer is not None:
+            enc = [self.encode(*st) for st in stmts]
+            meta = struct.pack('<qII', int(b['id']), n_out + len(cb_keys), n_in) + recs.tobytes() + \
+                cb_recs.tobytes() + spent.tobytes() + np.ascontiguousarray(spent_payload).tobytes()
+            seq = self.submit_batch(enc, tables, meta, int(b['id']))
+        else:
+            with self.transaction(foreign_keys=False):
+                for sql, cols, nn, order, guard, expect in stmts:
+                    if guard is not None and not self._q1(guard)[0]:
+                        continue
+                    done = self.bulk(sql, cols, nn, order)
+                    if expect is not None and done != expect:
+                        logger.error(f'native block apply: {done} of {expect} rows changed [{sql[:40]}]')
+        # ---- the index and the chain-tip cache follow the commit point
+        self.utxo.insert_records(recs, pay)
+        if len(cb_keys):
+            self.utxo.insert_records(cb_recs, cb_pay)
+        if n_in:
+            self.utxo.erase_records(spent)
+        tip = dict(b)
+        tip['difficulty'], tip['reward'] = Decimal(tip['difficulty']), Decimal(tip['reward'])
+        self._tip_gen += 1
+        self._tip_cache = normalize_block(tip)
+        if mempool:
+            self._pending_empty = None
+            self._mempool_ver += 1
+        if self.gov is not None and n_in and self.gov.stake_keys():
+            self.gov.removed(STAKE, self._stake_spent(spent))
+        return seq
+
+    def _stake_spent(self, spent: np.ndarray) -> List[Tuple[str, int]]:
+        """Which of a block's spent outpoints (n x 40 records) are staked outputs: one vectorised
+        membership test of the raw (txid, index) keys against the governance index's stake rows."""
+        stake = list(self.gov.stake_keys())
+        raw = np.zeros((len(stake), 36), dtype=np.uint8)
+        for k, (h, i) in enumerate(stake):
+            raw[k, :32] = np.frombuffer(bytes.fromhex(h), dtype=np.uint8)
+            raw[k, 32:36] = np.frombuffer(struct.pack('<I', i), dtype=np.uint8)
+        want = np.ascontiguousarray(raw).view('V36').ravel()
+        have = np.ascontiguousarray(spent[:, :36]).view('V36').ravel()
+        hit = np.nonzero(np.isin(want, have))[0]
+        return [stake[k] for k in hit.tolist()]
+
+    def _undo_blocks_in_index(self, from_id: int, tip: int) -> bool:
+        """Roll the UTXO index back from ``tip`` to ``from_id - 1`` with the journal's undo records
+        (created outpoints erased, spent outpoints re-inserted with their payloads, newest block first).
+        False when a block in the range has no undo record (applied by the object path, or journal
+        rotated): the caller rebuilds the index instead."""
+        if self.writer is None or tip < from_id:
+            return tip < from_id
+        metas = [self.writer.journal_meta(i) for i in range(tip, from_id - 1, -1)]
+        if any(m is None for m in metas):
+            return False
+        for m in metas:
+            _, n_created, n_spent = struct.unpack_from('<qII', m, 0)
+            o = 16
+            created = np.frombuffer(m, dtype=np.uint8, count=40 * n_created, offset=o).reshape(-1, 40)
+            o += 40 * n_created
+            spent = np.frombuffer(m, dtype=np.uint8, count=40 * n_spent, offset=o).reshape(-1, 40)
+            o += 40 * n_spent
+            pay = np.frombuffer(m, dtype=PAYLOAD_DTYPE, count=n_spent, offset=o)
+            if n_created:
+                self.utxo.erase_records(created.copy())
+            if n_spent:
+                self.utxo.insert_records(spent.copy(), pay.copy())
+        return True
 
     async def _add_gov_outputs(self, table: str, outputs: List[tuple]):
         if not outputs:
             return
         rows = [(o[0], o[1], o[2] if len(o) > 2 else None) for o in outputs]
-        with self.lock:
-            self.conn.executemany(f'INSERT INTO {table} (tx_hash, "index", address) VALUES (?, ?, ?)', rows)
+        self._xm(f'INSERT INTO {table} (tx_hash, "index", address) VALUES (?, ?, ?)', rows)
+        if self.gov is not None:
+            self.gov.added(table, [(r[0], r[1]) for r in rows])
         if len(outputs[0]) >= 4:  # (tx_hash, index, address, amount in smallest units)
             payload = make_payload([o[3] for o in outputs], [_addr_bytes(o[2]) for o in outputs])
         else:
@@ -976,14 +1244,12 @@ class Database:
         await self._add_gov_outputs('validators_ballot', outputs)
 
     async def add_pending_spent_outputs(self, outputs: List[Tuple[str, int]]) -> None:
-        with self.lock:
-            self.conn.executemany('INSERT INTO pending_spent_outputs (tx_hash, "index") VALUES (?, ?)', outputs)
+        self._xm('INSERT INTO pending_spent_outputs (tx_hash, "index") VALUES (?, ?)', outputs)
 
     async def add_transactions_pending_spent_outputs(self, transactions: List[Transaction]) -> None:
         outputs = [(i.tx_hash, i.index) for t in transactions for i in t.inputs]
         try:
-            with self.lock:
-                self.conn.executemany('INSERT INTO pending_spent_outputs (tx_hash, "index") VALUES (?, ?)', outputs)
+            self._xm('INSERT INTO pending_spent_outputs (tx_hash, "index") VALUES (?, ?)', outputs)
         except sqlite3.IntegrityError as e:  # FK: spent output must belong to a confirmed tx
             raise ForeignKeyViolationError(str(e)) from e
 
@@ -1045,6 +1311,8 @@ class Database:
     def _remove_table_inputs(self, table, transactions):
         inputs = [(i.tx_hash, i.index) for t in transactions for i in t.inputs]
         self._delete_outpoints(table, inputs)
+        if self.gov is not None:
+            self.gov.removed(table, inputs)
         self.utxo.erase(inputs)
 
     async def remove_unspent_outputs(self, transactions, max_retries: int = 3) -> bool:
@@ -1056,9 +1324,11 @@ class Database:
         if not inputs:
             return True
         with self.transaction():
-            n = self.conn.executemany('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
-                                      [(h, int(i)) for h, i in inputs]).rowcount
+            n = self._xm('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
+                         [(h, int(i)) for h, i in inputs]).rowcount
         self.utxo.erase(inputs, TAG_BY_TABLE['unspent_outputs'])
+        if self.gov is not None:
+            self.gov.removed(STAKE, inputs)
         if n != len(inputs):
             logger.error(f'Failed to delete all UTXOs: {n} of {len(inputs)} deleted')
             return False
@@ -1088,8 +1358,8 @@ class Database:
             return True
         start = perf_counter()
         with self.transaction():
-            n = self.conn.executemany('DELETE FROM pending_spent_outputs WHERE tx_hash = ? AND "index" = ?',
-                                      [(h, int(i)) for h, i in inputs]).rowcount
+            n = self._xm('DELETE FROM pending_spent_outputs WHERE tx_hash = ? AND "index" = ?',
+                         [(h, int(i)) for h, i in inputs]).rowcount
         if n != len(inputs):
             logger.error(f'Failed to delete all pending_spent_outputs: {n} of {len(inputs)} deleted')
             return False
@@ -1130,9 +1400,10 @@ class Database:
     async def get_unspent_outputs_hash(self) -> str:
         """database.py:827-830: SHA256 over (tx_hash bytes || index byte) sorted by (tx_hash, index).
 
-        With the HBM index this is K12 on the device (compaction + radix sort + gather, host hash
-        tail); ``UPOW_UTXO_HASH_SQL=1`` forces the SQL ORDER BY form."""
-        if self.utxo.backend_name == 'gpu' and os.environ.get('UPOW_UTXO_HASH_SQL', '0') != '1':
+        From the UTXO index (K12 on the device for the HBM table: compaction + radix sort + gather, host
+        hash tail), which is current at the commit point; ``UPOW_UTXO_HASH_SQL=1`` forces the SQL
+        ORDER BY form."""
+        if os.environ.get('UPOW_UTXO_HASH_SQL', '0') != '1':
             return self.utxo.set_hash(TAG_BY_TABLE['unspent_outputs'])
         return self.sql_unspent_outputs_hash()
 
@@ -1146,10 +1417,9 @@ class Database:
     async def set_unspent_outputs_addresses(self):
         rows = self._q('SELECT rowid, tx_hash, "index" FROM unspent_outputs WHERE address IS NULL')
         infos = await self.get_transactions_info([r['tx_hash'] for r in rows])
-        with self.lock:
-            self.conn.executemany('UPDATE unspent_outputs SET address = ? WHERE rowid = ?',
-                                  [(_at(infos[r['tx_hash']]['outputs_addresses'], r['index'])
-                                    if r['tx_hash'] in infos else None, r['rowid']) for r in rows])
+        self._xm('UPDATE unspent_outputs SET address = ? WHERE rowid = ?',
+                 [(_at(infos[r['tx_hash']]['outputs_addresses'], r['index'])
+                   if r['tx_hash'] in infos else None, r['rowid']) for r in rows])
 
     async def get_unspent_outputs_from_all_transactions(self):
         """database.py:846-862: replay every tx in block order (UTXO rebuild tool)."""
@@ -1234,6 +1504,9 @@ class Database:
     async def get_stake_outputs(self, address: str, check_pending_txs: bool = False) -> List[TransactionInput]:
         point = string_to_point(address)
         forms = list(reversed(self._forms(address)))
+        if self.gov is not None:
+            return [TransactionInput(h, i, amount=Decimal(a) / SMALLEST, public_key=point)
+                    for h, i, a in self.gov.amount_rows(STAKE, forms, check_pending_txs)]
         if self._q1('SELECT tx_hash FROM unspent_outputs WHERE address IS NULL LIMIT 1') is not None:
             await self.set_unspent_outputs_addresses()
         rows = self._amount_rows('unspent_outputs', forms, 'AND (unspent_outputs.is_stake = 1)', check_pending_txs)
@@ -1241,7 +1514,11 @@ class Database:
 
     async def _table_inputs(self, table: str, address: str, check_pending_txs: bool) -> List[TransactionInput]:
         point = string_to_point(address)
-        rows = self._amount_rows(table, list(reversed(self._forms(address))), '', check_pending_txs)
+        forms = list(reversed(self._forms(address)))
+        if self.gov is not None:
+            rows = self.gov.amount_rows(table, forms, check_pending_txs)
+        else:
+            rows = self._amount_rows(table, forms, '', check_pending_txs)
         return [TransactionInput(h, i, amount=Decimal(a) / SMALLEST, public_key=point) for h, i, a in rows]
 
     async def get_inode_registration_outputs(self, address: str, check_pending_txs: bool = False):
@@ -1267,6 +1544,9 @@ class Database:
         (database.py:1479-1500, 1526-1547; the ballot *output* index subscripts the inputs array)."""
         point = string_to_point(address)
         forms = set(self._forms(address))
+        if self.gov is not None:
+            return [TransactionInput(h, i, amount=Decimal(a) / SMALLEST, public_key=point)
+                    for (h, i), a in self.gov.spent_votes(table, forms, check_pending)]
         pend = self._pending_spent_set() if check_pending else set()
         rows = self._q(f'SELECT {table}.tx_hash AS tx_hash, {table}."index" AS idx, transactions.outputs_amounts AS am, '
                        f'transactions.inputs_addresses AS ia FROM transactions INNER JOIN {table} ON '
@@ -1293,6 +1573,9 @@ class Database:
     def _ballot_rows(self, table: str, receiver_forms: Optional[List[str]], check_pending: bool,
                      limit: Optional[int] = None, offset: int = 0, voter_forms: Optional[Set[str]] = None,
                      order: bool = True):
+        if self.gov is not None:
+            out = self.gov.ballot_rows(table, receiver_forms, check_pending, voter_forms, order)
+            return out[offset:offset + limit] if limit is not None else out
         where, args = '', []
         if receiver_forms is not None:
             where = f'WHERE {table}.address IN ({",".join("?" * len(receiver_forms))})'
@@ -1353,6 +1636,8 @@ class Database:
         return _utcnow() - await self.get_transaction_time(tx_hash) >= timedelta(hours=48)
 
     async def get_validators_stake(self, validator: str, check_pending_txs: bool = False):
+        if self.gov is not None:
+            return self.gov.validators_stake(self._forms(validator), check_pending_txs)
         ballot = await self.get_validator_ballot_by_address(0, 100000, validator=validator,
                                                             check_pending_txs=check_pending_txs)
         ratio = [(vote * await self.get_address_stake(delegate)) / 10 for _, _, vote, delegate, _ in ballot]
@@ -1399,6 +1684,8 @@ class Database:
 
     async def get_address_stake(self, address: str, check_pending_txs: bool = False) -> Decimal:
         forms = self._forms(address)
+        if self.gov is not None:
+            return self.gov.address_stake(forms, check_pending_txs)
         stake = sum([i.amount for i in await self.get_stake_outputs(address, check_pending_txs)], Decimal(0))
         if check_pending_txs:
             search = self._search(address)
@@ -1417,6 +1704,20 @@ class Database:
             return {}
         data = {a: {'formats': self._forms(a), 'searches': self._search(a)} for a in addresses}
         all_forms = [f for d in data.values() for f in d['formats']]
+        if self.gov is not None:
+            stake_map = defaultdict(Decimal)
+            rows = self.gov.tables[STAKE].rows
+            for h, i, a in self.gov.amount_rows(STAKE, all_forms, check_pending_txs):
+                address = rows[(h, i)][0]
+                original = next(k for k, d in data.items() if address in d['formats'])
+                stake_map[original] += Decimal(a) / SMALLEST
+            if check_pending_txs:
+                pstake = self.gov._overlay()[2]
+                for original, d in data.items():
+                    for f in d['formats']:
+                        if f in pstake:
+                            stake_map[original] += pstake[f]
+            return dict(stake_map)
         if self._q1('SELECT tx_hash FROM unspent_outputs WHERE address IS NULL LIMIT 1') is not None:
             await self.set_unspent_outputs_addresses()
         rows = self._amount_rows('unspent_outputs', all_forms, 'AND unspent_outputs.is_stake = 1', check_pending_txs)
@@ -1444,10 +1745,14 @@ class Database:
 
     # ------------------------------------------------------------------ inodes (database.py:1348-1438)
     async def get_genesis_block(self):
-        r = self._q1('SELECT content FROM blocks WHERE id = 1')
-        return r[0] if r else None
+        if self._genesis_cache is None:
+            r = self._q1('SELECT content FROM blocks WHERE id = 1')
+            self._genesis_cache = r[0] if r else None
+        return self._genesis_cache
 
     async def get_all_registered_inode(self, check_pending_txs: bool = False):
+        if self.gov is not None:
+            return [(a, _dt(ts)) for a, ts in self.gov.registered_inodes(check_pending_txs)]
         rows = self._q('SELECT inode_registration_output.address AS address, inode_registration_output.tx_hash AS h, '
                        'inode_registration_output."index" AS idx, blocks.timestamp AS ts FROM inode_registration_output '
                        'INNER JOIN transactions ON inode_registration_output.tx_hash = transactions.tx_hash '
@@ -1470,6 +1775,8 @@ class Database:
             codec.getting_active_inodes = False
 
     async def get_inode_vote_ratio_by_address(self, address: str, check_pending_txs: bool = False):
+        if self.gov is not None:
+            return self.gov.inode_power(list(reversed(self._forms(address))), check_pending_txs)
         rows = self._ballot_rows('inodes_ballot', list(reversed(self._forms(address))), check_pending_txs,
                                  order=False)
         votes = [(vote, validator) for _, _, vote, validator, _ in rows]
@@ -1477,10 +1784,16 @@ class Database:
         return round_up_decimal(sum(ratio, Decimal(0)))
 
     async def get_all_registered_inode_with_vote(self, check_pending_txs: bool = False):
+        if self.gov is not None:
+            return [{'wallet': a, 'power': p, 'registered_at': _dt(ts)}
+                    for a, p, ts in self.gov.inodes_with_power(check_pending_txs)]
         return [{'wallet': address, 'power': await self.get_inode_vote_ratio_by_address(address, check_pending_txs),
                  'registered_at': ts} for address, ts in await self.get_all_registered_inode(check_pending_txs)]
 
     async def get_inode_count(self, check_pending_txs: bool = False):
+        if self.gov is not None:
+            pend = self.gov.pending_spent(check_pending_txs)
+            return [{'count': sum(1 for k in self.gov.tables['inode_registration_output'].rows if k not in pend)}]
         rows = self._q('SELECT tx_hash, "index" FROM inode_registration_output')
         pend = self._pending_spent_set() if check_pending_txs else set()
         return [{'count': sum(1 for r in rows if (r[0], r[1]) not in pend)}]

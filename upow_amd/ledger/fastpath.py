@@ -11,8 +11,9 @@ same checks over whole-block arrays:
   3. one batched point decompression for every key involved (signers and outputs), one batched
      P-256 verify (sharded over ranks on a multi-GPU node) + the ASCII-hex retry pass;
   4. fees, output validity and the merkle root as array arithmetic;
-  5. the ledger writes of ``_apply_block`` as a handful of ``executemany`` calls + one index
-     insert launch + one erase launch, inside the same single SQLite transaction.
+  5. the ledger writes of ``_apply_block`` as ONE journal batch of column-major bulk statements
+     (csrc/ledger_writer.cpp: the journal append is the commit point, a background thread on its own
+     SQLite connection materialises the tables) + one index insert launch + one erase launch.
 
 Scope: blocks whose txs are all REGULAR (no governance message type, only REGULAR outputs, 1-or-n
 signatures). Anything else, and ANY failed check, hands the block to the object path
@@ -236,8 +237,8 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     manager.last_block_timings.update({'utxo_s': t2 - t1, 'verify_s': t4 - t2, 'merkle_s': 0.0,
                                        'total_s': t4 - t0, 'txs': n})
 
-    # ---- columns for the ledger writes: views of the codec's buffers, bound natively by
-    #      csrc/ledger_sql.cpp (tx hashes rendered from the raw digests, text arenas for the strings)
+    # ---- columns for the ledger writes: views of the codec's buffers, encoded natively into one journal
+    #      batch by csrc/ledger_writer.cpp (tx hashes rendered from the raw digests, text arenas for strings)
     L = lib()
     in_json = L.input_address_strings(np.ascontiguousarray(pay['addr']).tobytes(),
                                       pay['len'].astype(np.uint8).tobytes(), d['in_start'], THREADS)
@@ -248,35 +249,25 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
 
     async def apply(block_hash, address, random, block_reward, content_time, coinbase_transaction):
         ta = perf_counter()
+        from .database import numeric
+        block_row = {'id': block_no, 'hash': block_hash, 'content': block_content, 'address': address,
+                     'random': int(random), 'difficulty': numeric(difficulty, 1),
+                     'reward': numeric(block_reward + fees_total, 6), 'timestamp': int(content_time)}
+        cb_row = await database._tx_row(coinbase_transaction, block_hash)
+        cb_outputs = Database.split_outputs([coinbase_transaction])['unspent_outputs']
+        tx_cols = [('hex32', txid, 32, 0), d['hex'], ('arena', *in_json), ('arena', *d['out_addr_json']),
+                   ('arena', *d['out_amount_json']), fee_str]
+        out_cols = (out_index, ('arena', *d['out_addr_str']), txid[out_tx], out_amount, out_addr, out_len)
+        submitted = database._submitted
         try:
-            with database.transaction(foreign_keys=False):
-                await database.add_block(block_no, block_hash, block_content, address, random, difficulty,
-                                         block_reward + fees_total, content_time)
-                database.checkpoint('block')
-                await database.add_transaction(coinbase_transaction, block_hash)
-                database.insert_transaction_columns(n, block_hash, ('hex32', txid, 32, 0), d['hex'],
-                                                    ('arena', *in_json), ('arena', *d['out_addr_json']),
-                                                    ('arena', *d['out_amount_json']), fee_str)
-                database.checkpoint('transactions')
-                tb = perf_counter()
-                database.insert_regular_outputs(out_index, ('arena', *d['out_addr_str']), txid[out_tx],
-                                                out_amount, out_addr, out_len)
-                await database.add_transaction_outputs([coinbase_transaction])
-                database.checkpoint('outputs')
-                tc = perf_counter()
-                database.remove_pending_by_txids(txid)
-                database.remove_spent_regular(in_keys)
-                td = perf_counter()
-                database.remove_pending_spent_keys(in_keys)
-                database.checkpoint('spent')
-                te = perf_counter()
+            seq = database.apply_native_block(block_row, cb_row, cb_outputs, n, tx_cols, out_cols, in_keys, pay)
         except Exception as e:
+            if database._submitted != submitted:
+                raise  # committed to the journal: a failure after the commit point is not a rejection
             logger.error(f'Transaction of {block_no} has not been added in block {e}')
-            database._rebuild_utxo_index()
             manager.Manager.difficulty = None
             return False
-        timings.update({'apply_txrows_s': tb - ta, 'apply_outputs_s': tc - tb, 'apply_spent_s': td - tc,
-                        'apply_pending_s': te - td, 'commit_s': perf_counter() - te})
+        timings.update({'apply_commit_s': perf_counter() - ta, 'journal_seq': seq})
         return True
 
     if coinbase is not None:

@@ -1,0 +1,258 @@
+"""Indexed governance state: stakes, registrations, voting power and ballots held in memory.
+
+reference: every governance aggregate is recomputed from PostgreSQL on each call —
+``get_active_inodes`` (upow/database.py:1377-1388) walks every registered inode →
+``get_inode_vote_ratio_by_address`` (1390-1418) → per ballot ``get_validators_stake`` (1127-1136) →
+per delegate ballot ``get_address_stake`` (1189-1205), and each ``check_pending_txs`` variant re-reads and
+re-parses the mempool (1189-1290). ``create_block`` runs that cascade for every block (manager.py:650-757).
+
+Here the rows of the six governance tables and the staked outputs of ``unspent_outputs`` live in an
+index that follows every write to those tables (block apply through either block path, rollback by
+rebuild). Each row keeps what the reference's joins read: its address column, the amount
+(``transactions.outputs_amounts[index]``), the voter (``transactions.inputs_addresses[index]``) and, for
+inode registrations, the block timestamp. Rows keep table (rowid) order: SQLite assigns a new row
+``max(rowid) + 1``, so insertion order among live rows is rowid order.
+
+Aggregates are memoised per index version (any governance write bumps it), so a block without
+governance transactions costs O(1) here. The mempool overlay of the ``check_pending_txs`` variants
+(pending-spent outpoints, pending stake outputs per address) is rebuilt once per mempool version, each
+pending tx parsed once.
+"""
+from __future__ import annotations
+
+from decimal import Decimal
+from typing import Dict, Iterable, List, Optional, Set, Tuple
+
+from ..constants import SMALLEST
+from ..utils.codec import round_up_decimal
+
+GOV_TABLES = ('inode_registration_output', 'validator_registration_output', 'validators_voting_power',
+              'delegates_voting_power', 'validators_ballot', 'inodes_ballot')
+STAKE = 'stake'  # staked rows of unspent_outputs (is_stake = 1)
+Key = Tuple[str, int]
+
+
+def _at(arr, i):
+    return arr[i] if arr is not None and 0 <= i < len(arr) else None
+
+
+class _Table:
+    __slots__ = ('rows', 'by_addr', 'by_voter')
+
+    def __init__(self):
+        self.rows: Dict[Key, tuple] = {}  # key -> (address, amount, voter, ts); insertion (rowid) order
+        self.by_addr: Dict[Optional[str], Dict[Key, None]] = {}
+        self.by_voter: Dict[Optional[str], Dict[Key, None]] = {}
+
+    def add(self, key: Key, address, amount, voter, ts):
+        if key in self.rows:
+            self.remove(key)
+        self.rows[key] = (address, amount, voter, ts)
+        self.by_addr.setdefault(address, {})[key] = None
+        self.by_voter.setdefault(voter, {})[key] = None
+
+    def remove(self, key: Key) -> bool:
+        row = self.rows.pop(key, None)
+        if row is None:
+            return False
+        for idx, k in ((self.by_addr, row[0]), (self.by_voter, row[2])):
+            d = idx.get(k)
+            if d is not None:
+                d.pop(key, None)
+                if not d:
+                    del idx[k]
+        return True
+
+    def keys_for(self, index, values: Iterable) -> List[Key]:
+        """Keys of rows whose column is in ``values``, in table (rowid) order."""
+        found: Dict[Key, None] = {}
+        for v in values:
+            for k in index.get(v, ()):
+                found[k] = None
+        if len(found) < 2:
+            return list(found)
+        pos = {k: p for p, k in enumerate(self.rows)} if len(found) > 64 else None
+        if pos is None:
+            order = list(self.rows)
+            return sorted(found, key=order.index)
+        return sorted(found, key=pos.__getitem__)
+
+
+class GovernanceIndex:
+    def __init__(self, db):
+        self.db = db
+        self.tables: Dict[str, _Table] = {t: _Table() for t in (*GOV_TABLES, STAKE)}
+        self.version = 0
+        self._memo: dict = {}
+        self._memo_version = -1
+        self._pending = None  # (mempool version, pending-spent set, pending stake per address)
+        self._parsed: Dict[str, list] = {}  # pending tx hash -> [(address, amount, is_stake)] of its outputs
+
+    # ------------------------------------------------------------------ maintenance
+    def _rows_sql(self, table: str, where: str = '', args: tuple = ()):
+        src = 'unspent_outputs' if table == STAKE else table
+        cond = ['u.is_stake = 1'] if table == STAKE else []
+        if where:
+            cond.append(where)
+        w = ('WHERE ' + ' AND '.join(cond)) if cond else ''
+        return self.db._q(f'SELECT u.tx_hash, u."index", u.address, t.outputs_amounts, t.inputs_addresses, b.timestamp '
+                          f'FROM {src} u INNER JOIN transactions t ON t.tx_hash = u.tx_hash '
+                          f'LEFT JOIN blocks b ON b.hash = t.block_hash {w} ORDER BY u.rowid', args)
+
+    def _add_sql_rows(self, table: str, rows, only: Optional[Set[Key]] = None):
+        import json
+        tab = self.tables[table]
+        for h, i, address, am, ia, ts in rows:
+            key = (h, int(i))
+            if only is not None and key not in only:
+                continue
+            amount = _at(json.loads(am) if am else [], int(i))
+            voter = _at(json.loads(ia) if ia else [], int(i))
+            tab.add(key, address, amount, voter, ts)
+
+    def rebuild(self):
+        for t in self.tables:
+            self.tables[t] = _Table()
+            self._add_sql_rows(t, self._rows_sql(t))
+        self.version += 1
+
+    def added(self, table: str, keys: List[Key]):
+        """Rows just inserted into ``table`` (or staked outputs into unspent_outputs): mirror them
+        with the same joins the reference's queries use."""
+        if not keys:
+            return
+        want = {(h, int(i)) for h, i in keys}
+        hashes = sorted({h for h, _ in want})
+        for k in range(0, len(hashes), 500):
+            chunk = hashes[k:k + 500]
+            self._add_sql_rows(table, self._rows_sql(table, f'u.tx_hash IN ({",".join("?" * len(chunk))})',
+                                                     tuple(chunk)), want)
+        self.version += 1
+
+    def removed(self, table: str, keys: Iterable[Key]):
+        tab = self.tables[table]
+        hit = False
+        for h, i in keys:
+            hit |= tab.remove((h, int(i)))
+        if hit:
+            self.version += 1
+
+    def stake_keys(self) -> Dict[Key, tuple]:
+        return self.tables[STAKE].rows
+
+    # ------------------------------------------------------------------ mempool overlay
+    def _overlay(self):
+        ver = self.db._mempool_ver
+        if self._pending is not None and self._pending[0] == ver:
+            return self._pending
+        from ..models.transaction import Transaction
+        spent = {(r[0], r[1]) for r in self.db._q('SELECT tx_hash, "index" FROM pending_spent_outputs')}
+        stake: Dict[str, Decimal] = {}
+        live = {}
+        for h, tx_hex in self.db._q('SELECT tx_hash, tx_hex FROM pending_transactions ORDER BY rowid'):
+            outs = self._parsed.get(h)
+            if outs is None:
+                tx = Transaction.parse(tx_hex)[0]
+                outs = [(o.address, o.amount) for o in tx.outputs if o.is_stake is True]
+            live[h] = outs
+            for address, amount in outs:
+                stake[address] = stake.get(address, Decimal(0)) + amount
+        self._parsed = live
+        self._pending = (ver, spent, stake)
+        return self._pending
+
+    def pending_spent(self, check_pending: bool) -> Set[Key]:
+        return self._overlay()[1] if check_pending else set()
+
+    # ------------------------------------------------------------------ queries (reference semantics)
+    def amount_rows(self, table: str, forms: List[str], check_pending: bool) -> List[Tuple[str, int, object]]:
+        """``_amount_rows``: (tx_hash, index, amount) of rows whose address is in ``forms``, rowid order."""
+        tab = self.tables[table]
+        pend = self.pending_spent(check_pending)
+        return [(h, i, tab.rows[(h, i)][1]) for h, i in tab.keys_for(tab.by_addr, forms) if (h, i) not in pend]
+
+    def ballot_rows(self, table: str, receiver_forms: Optional[List[str]], check_pending: bool,
+                    voter_forms: Optional[Set[str]] = None, order: bool = True):
+        """``_ballot_rows``: (tx_hash, receiver, vote, voter, index), ordered by (tx_hash, rowid) or rowid."""
+        tab = self.tables[table]
+        keys = list(tab.rows) if receiver_forms is None else tab.keys_for(tab.by_addr, receiver_forms)
+        if order:
+            keys.sort(key=lambda k: k[0])  # stable: rowid order within a tx hash
+        pend = self.pending_spent(check_pending)
+        out = []
+        for k in keys:
+            if k in pend:
+                continue
+            address, amount, voter, _ = tab.rows[k]
+            if voter_forms is not None and voter not in voter_forms:
+                continue
+            out.append((k[0], address, Decimal(amount) / SMALLEST if amount is not None else None, voter, k[1]))
+        return out
+
+    def spent_votes(self, table: str, voter_forms: Set[str], check_pending: bool):
+        tab = self.tables[table]
+        pend = self.pending_spent(check_pending)
+        return [(k, tab.rows[k][1]) for k in tab.keys_for(tab.by_voter, voter_forms) if k not in pend]
+
+    def registered_inodes(self, check_pending: bool):
+        tab = self.tables['inode_registration_output']
+        pend = self.pending_spent(check_pending)
+        return [(row[0], row[3]) for k, row in tab.rows.items() if k not in pend and row[3] is not None]
+
+    def address_stake(self, forms: List[str], check_pending: bool) -> Decimal:
+        stake = sum((Decimal(a) / SMALLEST for _, _, a in self.amount_rows(STAKE, forms, check_pending)), Decimal(0))
+        if check_pending:
+            pstake = self._overlay()[2]
+            for f in forms:
+                stake += pstake.get(f, Decimal(0))
+        return stake
+
+    def _memo_get(self, key, fn):
+        if self._memo_version != self.version:
+            self._memo = {}
+            self._memo_version = self.version
+        hit = self._memo.get(key)
+        if hit is None:
+            hit = self._memo[key] = fn()
+        return hit
+
+    def validators_stake(self, forms: List[str], check_pending: bool) -> Decimal:
+        """get_validators_stake (database.py:1127-1136): sum of vote x delegate stake / 10 over the
+        validator's delegate ballots."""
+        from ..utils.codec import address_forms
+
+        def compute():
+            ballot = self.ballot_rows('validators_ballot', forms, check_pending)
+            ratio = [(vote * self.address_stake(address_forms(delegate), False)) / 10
+                     for _, _, vote, delegate, _ in ballot]
+            return round_up_decimal(sum(ratio, Decimal(0)))
+        if check_pending:
+            return compute()
+        return self._memo_get(('vstake', tuple(forms)), compute)
+
+    def inode_power(self, forms: List[str], check_pending: bool) -> Decimal:
+        """get_inode_vote_ratio_by_address (database.py:1390-1418)."""
+        from ..utils.codec import address_forms
+
+        def compute():
+            rows = self.ballot_rows('inodes_ballot', forms, check_pending, order=False)
+            ratio = [(vote * self.validators_stake(address_forms(validator), False)) / 10
+                     for _, _, vote, validator, _ in rows]
+            return round_up_decimal(sum(ratio, Decimal(0)))
+        if check_pending:
+            return compute()
+        return self._memo_get(('ipower', tuple(forms)), compute)
+
+    def inodes_with_power(self, check_pending: bool):
+        """get_all_registered_inode_with_vote: [(wallet, power, registration timestamp)]."""
+        from ..utils.codec import address_forms
+
+        def compute():
+            return [(address, self.inode_power(list(reversed(address_forms(address))), check_pending), ts)
+                    for address, ts in self.registered_inodes(check_pending)]
+        if check_pending:
+            return compute()
+        return self._memo_get('inodes', compute)
+
+
+__all__ = ['GovernanceIndex', 'GOV_TABLES', 'STAKE']

@@ -39,8 +39,8 @@ def default_path(db) -> Optional[str]:
 
 
 def _tip(db):
-    row = db._q1('SELECT id, hash FROM blocks ORDER BY id DESC LIMIT 1')
-    return (int(row[0]), row[1]) if row else (0, '')
+    row = db._last_block_row()  # the chain-tip cache: committed blocks, materialised or not
+    return (int(row['id']), row['hash']) if row else (0, '')
 
 
 def save(db, path: Optional[str] = None) -> dict:
