@@ -177,8 +177,9 @@ PYBIND11_MODULE(_native, m) {
             if (pi.size * pi.itemsize != n * 80) throw std::invalid_argument("payload must be n x 80 bytes");
             pp = static_cast<const uint8_t*>(pi.ptr);
         }
-        py::gil_scoped_release rel;
-        return utxo_insert(h, p, n, pp);
+        uint64_t r;
+        { py::gil_scoped_release rel; r = utxo_insert(h, p, n, pp); }
+        return py::make_tuple(uint32_t(r), uint32_t(r >> 32));  // (no free slot, duplicates skipped)
     }, py::arg("h"), py::arg("recs"), py::arg("payload") = py::none());
     m.def("utxo_lookup", [recs_arg](int64_t h, py::buffer recs) {
         int64_t n; const uint8_t* p = recs_arg(recs, n);
@@ -236,18 +237,18 @@ PYBIND11_MODULE(_native, m) {
         { py::gil_scoped_release rel; d = utxo_set_hash(h, tag, &n); }
         return py::make_tuple(py::bytes(reinterpret_cast<const char*>(d.data()), d.size()), n);
     });
-    m.def("utxo_address_scan", [](int64_t h, py::bytes addr, uint32_t tag_mask) {
+    m.def("utxo_address_scan", [](int64_t h, py::bytes addr, uint32_t tag_mask, uint32_t stake_sel) {
         std::string a = addr;
         std::vector<uint8_t> o, pay;
         uint64_t total = 0;
         {
             py::gil_scoped_release rel;
-            o = utxo_address_scan(h, reinterpret_cast<const uint8_t*>(a.data()), uint32_t(a.size()), tag_mask, pay,
-                                  &total);
+            o = utxo_address_scan(h, reinterpret_cast<const uint8_t*>(a.data()), uint32_t(a.size()), tag_mask,
+                                  stake_sel, pay, &total);
         }
         return py::make_tuple(py::bytes(reinterpret_cast<const char*>(o.data()), o.size()),
                               py::bytes(reinterpret_cast<const char*>(pay.data()), pay.size()), total);
-    });
+    }, py::arg("h"), py::arg("addr"), py::arg("tag_mask"), py::arg("stake_sel") = 0);
     m.def("utxo_dump_payload", [](int64_t h) {
         std::vector<uint8_t> o, pay;
         { py::gil_scoped_release rel; o = utxo_dump(h, &pay); }

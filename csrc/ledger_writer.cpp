@@ -570,6 +570,9 @@ class LedgerWriter {
         d["failed"] = failed_;
         d["error"] = error_;
         d["change_mismatches"] = mismatches_;
+        py::dict per;
+        for (auto& kv : stmt_stats_) per[py::str(kv.first)] = py::make_tuple(kv.second.first / 1e9, kv.second.second);
+        d["statements"] = per;
         return d;
     }
 
@@ -648,6 +651,7 @@ class LedgerWriter {
             const char* order = nullptr;
             if (in.get<uint8_t>()) order = in.take(size_t(n) * 8);
             if (!guard.empty() && query_int(guard) == 0) continue;
+            const auto ts0 = std::chrono::steady_clock::now();
             sqlite3_stmt* st = prepared(sql);
             int64_t changes = 0;
             char hexbuf[8][64];
@@ -695,6 +699,10 @@ class LedgerWriter {
             }
             a.clear_bindings(st);
             if (expect >= 0 && changes != expect) ++mismatches_;
+            std::lock_guard<std::mutex> lk(mu_);
+            auto& acc = stmt_stats_[sql.substr(0, 48)];
+            acc.first += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - ts0).count();
+            acc.second += n;
         }
     }
 
@@ -843,6 +851,7 @@ class LedgerWriter {
     std::string error_;
     int64_t groups_ = 0, replayed_ = 0, rotations_ = 0, mismatches_ = 0;
     int64_t apply_ns_ = 0, commit_ns_ = 0, sync_ns_ = 0;
+    std::map<std::string, std::pair<int64_t, int64_t>> stmt_stats_;  // sql prefix -> (ns, rows); materialiser thread
     std::thread thread_;
 };
 

@@ -50,14 +50,14 @@ int64_t utxo_create(uint32_t log2_cap);
 void utxo_destroy(int64_t h);
 uint32_t utxo_capacity(int64_t h);
 // payload records: 80 bytes {u64 amount, u32 address length, u32 pad, address[64]} (nullptr = zeros)
-uint32_t utxo_insert(int64_t h, const uint8_t* recs, int64_t n, const uint8_t* payload);  // #failed (full)
+uint64_t utxo_insert(int64_t h, const uint8_t* recs, int64_t n, const uint8_t* payload);  // #full | (#duplicates << 32)
 std::vector<uint8_t> utxo_probe(int64_t h, const uint8_t* recs, int64_t n);  // tag or 0xff
 std::vector<uint8_t> utxo_lookup(int64_t h, const uint8_t* recs, int64_t n, std::vector<uint8_t>& payload_out);
 std::vector<uint8_t> utxo_erase(int64_t h, const uint8_t* recs, int64_t n);  // 1 if erased
 std::vector<uint8_t> utxo_dump(int64_t h, std::vector<uint8_t>* payload_out);
 // K14: live outputs whose payload address equals addr[0:len] and whose tag is in tag_mask
 std::vector<uint8_t> utxo_address_scan(int64_t h, const uint8_t* addr, uint32_t len, uint32_t tag_mask,
-                                       std::vector<uint8_t>& payload_out, uint64_t* total_out);
+                                       uint32_t stake_sel, std::vector<uint8_t>& payload_out, uint64_t* total_out);
 
 // whole-block input pass: lookup (K7) + duplicate candidates (K10) + per-tx fees (K11) in one round trip
 struct BlockInputsResult {

@@ -53,9 +53,10 @@ static_assert(sizeof(UtxoKeyRec) == 40, "key record");
 struct alignas(16) UtxoPayload {  // 80 bytes
     uint64_t amount;
     uint32_t addr_len;
-    uint32_t pad;
+    uint32_t flags;  // bit 0: is_stake (unspent_outputs.is_stake = 1)
     uint8_t addr[64];
 };
+constexpr uint32_t PAY_STAKE = 1u;
 static_assert(sizeof(UtxoPayload) == 80, "payload");
 
 __device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) {
@@ -84,42 +85,56 @@ __device__ __forceinline__ bool key_eq(const UtxoSlot& s, const uint32_t k[8]) {
 // reject a slot from the 48-byte key line alone and touch the 80-byte payload line only on a likely hit.
 __device__ __forceinline__ uint32_t addr_fingerprint(const uint8_t* addr) { return ld_u32(addr + 1); }
 
+// Insert: walk the probe chain to its first EMPTY slot remembering the first reusable (EMPTY or
+// tombstone) slot; a live entry with the same outpoint already in the chain is a duplicate and is not
+// inserted again (counter[1]). The remembered slot is claimed with a CAS; a lane that loses the race
+// walks the chain again. counter[0] counts entries that found no slot (table full).
+// Lanes of one launch never insert the same outpoint twice (block validation rejects duplicate inputs,
+// hence duplicate txids), so the chain walk only has to see entries published by earlier launches.
 __global__ __launch_bounds__(256) void utxo_insert_kernel(UtxoSlot* __restrict__ tab, UtxoPayload* __restrict__ pay,
                                                           uint32_t mask, const UtxoKeyRec* __restrict__ recs,
                                                           const UtxoPayload* __restrict__ in_pay, int64_t n,
-                                                          uint32_t* __restrict__ failed) {
+                                                          uint32_t* __restrict__ counter) {
     const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t k[8];
     load_key(recs[i], k);
     const uint32_t idx = recs[i].index & 0xffu, tag = recs[i].tag & 0xffu;
-    uint32_t s = slot_hash(k, idx) & mask;
-    for (uint32_t probe = 0; probe <= mask; ++probe) {
-        uint32_t* mp = &tab[s].meta;
-        const uint32_t m = __hip_atomic_load(mp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t st = m & 3u;
-        if (st == ST_EMPTY || st == ST_TOMB) {
-            if (atomicCAS(mp, m, ST_BUSY) == m) {
-#pragma unroll
-                for (int w = 0; w < 8; ++w) tab[s].k[w] = k[w];
-                if (in_pay) {
-                    pay[s] = in_pay[i];
-                    tab[s].pad[0] = addr_fingerprint(in_pay[i].addr);
-                } else {
-                    tab[s].pad[0] = 0;
-                    pay[s].amount = 0;
-                    pay[s].addr_len = 0;
-                }
-                __threadfence();
-                atomicExch(mp, ST_FULL | (idx << 8) | (tag << 16));
+    const uint32_t home = slot_hash(k, idx) & mask;
+    for (int attempt = 0; attempt < 64; ++attempt) {
+        uint32_t s = home, free_slot = 0xffffffffu, free_meta = 0;
+        for (uint32_t probe = 0; probe <= mask; ++probe) {
+            const uint32_t m = __hip_atomic_load(&tab[s].meta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t st = m & 3u;
+            if (st == ST_FULL && ((m >> 8) & 0xffu) == idx && key_eq(tab[s], k)) {
+                atomicAdd(counter + 1, 1u);
                 return;
             }
-            --probe;  // lost the race for this slot: look at it again
-            continue;
+            if ((st == ST_EMPTY || st == ST_TOMB) && free_slot == 0xffffffffu) {
+                free_slot = s;
+                free_meta = m;
+            }
+            if (st == ST_EMPTY) break;
+            s = (s + 1) & mask;
         }
-        s = (s + 1) & mask;
+        if (free_slot == 0xffffffffu) break;
+        uint32_t* mp = &tab[free_slot].meta;
+        if (atomicCAS(mp, free_meta, ST_BUSY) != free_meta) continue;  // lost the race: walk again
+#pragma unroll
+        for (int w = 0; w < 8; ++w) tab[free_slot].k[w] = k[w];
+        if (in_pay) {
+            pay[free_slot] = in_pay[i];
+            tab[free_slot].pad[0] = addr_fingerprint(in_pay[i].addr);
+        } else {
+            UtxoPayload z{};
+            pay[free_slot] = z;
+            tab[free_slot].pad[0] = 0;
+        }
+        __threadfence();
+        atomicExch(mp, ST_FULL | (idx << 8) | (tag << 16));
+        return;
     }
-    atomicAdd(failed, 1u);
+    atomicAdd(counter, 1u);
 }
 
 // tags_out[i] = tag of the outpoint, 0xff when absent
@@ -243,7 +258,8 @@ __global__ __launch_bounds__(256) void utxo_dump_kernel(const UtxoSlot* __restri
 __global__ __launch_bounds__(256) void utxo_address_scan_kernel(const UtxoSlot* __restrict__ tab,
                                                                 const UtxoPayload* __restrict__ pay, uint32_t cap,
                                                                 uint4 q0, uint4 q1, uint4 q2, uint4 q3, uint32_t qlen,
-                                                                uint32_t qfp, uint32_t tag_mask, uint32_t max_out,
+                                                                uint32_t qfp, uint32_t tag_mask, uint32_t stake_sel,
+                                                                uint32_t max_out,
                                                                 UtxoKeyRec* __restrict__ out,
                                                                 UtxoPayload* __restrict__ pay_out,
                                                                 uint32_t* __restrict__ count,
@@ -255,8 +271,10 @@ __global__ __launch_bounds__(256) void utxo_address_scan_kernel(const UtxoSlot* 
         const uint4 mw = *reinterpret_cast<const uint4*>(&tab[s].meta);
         const uint32_t m = mw.x;
         const uint32_t tag = (m >> 16) & 0xffu;
+        // stake_sel: 0 any output, 1 only is_stake = 0 (spendable), 2 only is_stake = 1
+        const uint32_t stake = tag == 0u ? (pay[s].flags & PAY_STAKE) : 0u;
         if ((m & 3u) == ST_FULL && tag < 32u && ((tag_mask >> tag) & 1u) && mw.y == qfp &&
-            pay[s].addr_len == qlen) {
+            pay[s].addr_len == qlen && (stake_sel == 0u || (stake_sel == 1u) == (stake == 0u))) {
             const uint4* a = reinterpret_cast<const uint4*>(pay[s].addr);
             const uint4 a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
             const uint32_t d = (a0.x ^ q0.x) | (a0.y ^ q0.y) | (a0.z ^ q0.z) | (a0.w ^ q0.w) | (a1.x ^ q1.x) |
@@ -322,7 +340,8 @@ int64_t utxo_create(uint32_t log2_cap) {
     uck(hipMalloc(&t.tab, sizeof(UtxoSlot) * size_t(t.cap)), "hipMalloc utxo table");
     uck(hipMemset(t.tab, 0, sizeof(UtxoSlot) * size_t(t.cap)), "memset utxo table");
     uck(hipMalloc(&t.pay, sizeof(UtxoPayload) * size_t(t.cap)), "hipMalloc utxo payload");
-    uck(hipMalloc(&t.d_counter, sizeof(uint32_t)), "hipMalloc counter");
+    uck(hipMemset(t.pay, 0, sizeof(UtxoPayload) * size_t(t.cap)), "memset utxo payload");
+    uck(hipMalloc(&t.d_counter, 2 * sizeof(uint32_t)), "hipMalloc counter");
     std::lock_guard<std::mutex> lk(g_ut_mu);
     const int64_t h = g_next_handle++;
     g_tables[h] = t;
@@ -348,7 +367,7 @@ uint32_t utxo_capacity(int64_t h) {
 template <typename T>
 using DevBuf = PooledBuf<T>;
 
-uint32_t utxo_insert(int64_t h, const uint8_t* recs, int64_t n, const uint8_t* payload) {
+uint64_t utxo_insert(int64_t h, const uint8_t* recs, int64_t n, const uint8_t* payload) {
     std::lock_guard<std::mutex> lk(g_ut_mu);
     UtxoTableDev& t = table(h);
     if (n == 0) return 0;
@@ -356,13 +375,13 @@ uint32_t utxo_insert(int64_t h, const uint8_t* recs, int64_t n, const uint8_t* p
     uck(hipMemcpy(d.p, recs, sizeof(UtxoKeyRec) * n, hipMemcpyHostToDevice), "h2d recs");
     DevBuf<UtxoPayload> dp(payload ? n : 0);
     if (payload) uck(hipMemcpy(dp.p, payload, sizeof(UtxoPayload) * n, hipMemcpyHostToDevice), "h2d payload");
-    uck(hipMemset(t.d_counter, 0, sizeof(uint32_t)), "memset");
+    uck(hipMemset(t.d_counter, 0, 2 * sizeof(uint32_t)), "memset");
     hipLaunchKernelGGL(utxo_insert_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, 0, t.tab, t.pay, t.cap - 1, d.p,
                        payload ? dp.p : nullptr, n, t.d_counter);
     uck(hipGetLastError(), "utxo_insert_kernel");
-    uint32_t failed = 0;
-    uck(hipMemcpy(&failed, t.d_counter, sizeof(uint32_t), hipMemcpyDeviceToHost), "d2h failed");
-    return failed;
+    uint32_t c[2] = {0, 0};
+    uck(hipMemcpy(c, t.d_counter, sizeof c, hipMemcpyDeviceToHost), "d2h failed");
+    return uint64_t(c[0]) | (uint64_t(c[1]) << 32);  // (table full) | (duplicates << 32)
 }
 
 std::vector<uint8_t> utxo_lookup(int64_t h, const uint8_t* recs, int64_t n, std::vector<uint8_t>& payload_out) {
@@ -414,7 +433,7 @@ std::vector<uint8_t> utxo_erase(int64_t h, const uint8_t* recs, int64_t n) {
 }
 
 std::vector<uint8_t> utxo_address_scan(int64_t h, const uint8_t* addr, uint32_t len, uint32_t tag_mask,
-                                       std::vector<uint8_t>& payload_out, uint64_t* total_out) {
+                                       uint32_t stake_sel, std::vector<uint8_t>& payload_out, uint64_t* total_out) {
     if (len > 64) throw std::invalid_argument("address is at most 64 bytes");
     std::lock_guard<std::mutex> lk(g_ut_mu);
     UtxoTableDev& t = table(h);
@@ -432,7 +451,7 @@ std::vector<uint8_t> utxo_address_scan(int64_t h, const uint8_t* addr, uint32_t 
         uck(hipMemset(t.d_counter, 0, sizeof(uint32_t)), "memset");
         uck(hipMemset(dt.p, 0, sizeof(unsigned long long)), "memset");
         hipLaunchKernelGGL(utxo_address_scan_kernel, dim3(int((t.cap + 255) / 256)), dim3(256), 0, 0, t.tab, t.pay,
-                           t.cap, q[0], q[1], q[2], q[3], len, qfp, tag_mask, cap_out, d.p, dp.p, t.d_counter, dt.p);
+                           t.cap, q[0], q[1], q[2], q[3], len, qfp, tag_mask, stake_sel, cap_out, d.p, dp.p, t.d_counter, dt.p);
         uck(hipGetLastError(), "utxo_address_scan_kernel");
         uck(hipMemcpy(&n, t.d_counter, sizeof(uint32_t), hipMemcpyDeviceToHost), "d2h n");
         if (n <= cap_out) {

@@ -142,25 +142,42 @@ def test_block_apply_is_atomic_under_injected_failure(chain, stage):
 
 
 def test_address_utxos_tool(chain, tmp_path, capsys):
-    """``python -m upow_amd.tools address-utxos``: the index's view of an address equals the SQL view
-    (spendable outputs and balance)."""
+    """``python -m upow_amd.tools address-utxos``: the index's view of an address equals the SQL view —
+    spendable outputs and balance (get_address_balance, is_stake excluded), staked outputs, governance
+    tables — with outputs sent to both string forms of the same key."""
     from upow_amd import tools
+    from upow_amd.utils.codec import AddressFormat, string_to_point
 
     async def go():
         a = builders.address_of(KEY_A)
         b = builders.address_of(KEY_B)
+        b_full = point_to_string(string_to_point(b), AddressFormat.FULL_HEX)
         base = 1_700_000_000
-        await devnet.mine_block(a, ts=base + 1)
-        await devnet.mine_block(a, ts=base + 2)
+        for k in range(4):
+            await devnet.mine_block(a, ts=base + 1 + k)
         tx = await builders.create_transaction(KEY_A, b, '2.5')
         assert await chain.add_pending_transaction(tx)
-        await devnet.mine_block(a, [tx], ts=base + 3)
-        for addr in (a, b):
+        a_full = point_to_string(string_to_point(a), AddressFormat.FULL_HEX)
+        # a version-1 tx: every output in the full-hex (64-byte) form
+        tx2 = await builders.create_transaction(KEY_A, b_full, '1.25', send_back_address=a_full)
+        assert tx2.version == 1
+        assert await chain.add_pending_transaction(tx2)
+        await devnet.mine_block(a, [tx, tx2], ts=base + 10)
+        stx = await builders.create_stake_transaction(KEY_B, '1')  # a staked output + delegate voting power
+        assert await chain.add_pending_transaction(stx)
+        await devnet.mine_block(a, [stx], ts=base + 11)
+        for addr in (a, b, b_full, a_full):
             res = await tools.address_utxos(addr, db=chain)
-            assert Decimal(res['total']) == await chain.get_address_balance(addr)
+            assert Decimal(res['spendable']) == await chain.get_address_balance(addr)
+            assert Decimal(res['stake']) == await chain.get_address_stake(addr)
             sql = sorted((i.tx_hash, i.index) for i in await chain.get_spendable_outputs(addr))
-            assert sorted((o['tx_hash'], o['index']) for o in res['outputs']) == sql
-            assert all(o['table'] == 'unspent_outputs' for o in res['outputs'])
+            sql += sorted((i.tx_hash, i.index) for i in await chain.get_stake_outputs(addr))
+            sql += sorted((i.tx_hash, i.index) for i in await chain.get_delegates_voting_power(addr))
+            assert sorted((o['tx_hash'], o['index']) for o in res['outputs']) == sorted(sql)
+        res = await tools.address_utxos(b, db=chain)
+        assert sorted(o['amount'] for o in res['outputs'] if not o['is_stake'] and o['table'] == 'unspent_outputs') \
+            == ['1.25', '2.5'] or Decimal(res['spendable']) == Decimal('3.75') - 1
+        assert Decimal(res['stake']) == 1 and Decimal(res['tables']['delegates_voting_power']) == 10
     asyncio.run(go())
     with pytest.raises(SystemExit):
         tools.main(['address-utxos'])

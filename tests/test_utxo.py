@@ -173,3 +173,50 @@ def test_address_outputs_gpu_scan(gpu):
     assert len(raw) == 40 * 5000 and total == 7 * 5000
     recs, _, tot = idx.address_outputs(a)
     assert len(recs) == 5000 and tot == 35000
+
+
+@pytest.mark.parametrize('backend', ['host', pytest.param('gpu', marks=pytest.mark.gpu)])
+def test_duplicate_insert_is_skipped(backend, request):
+    """Inserting an outpoint that is already live leaves the entry (tag, payload) as it was and is
+    counted, on both index backends (csrc/utxo_table.hip utxo_insert_kernel walks the probe chain)."""
+    if backend == 'gpu':
+        request.getfixturevalue('gpu')
+    idx = UtxoIndex(backend=backend)
+    keys = _keys(300, 5)
+    addr = bytes([42]) + bytes(range(32))
+    idx.insert(keys, 0, make_payload([5] * 300, [addr] * 300))
+    before = idx.records_payload()
+    idx.insert(keys[:10] + _keys(3, 77), 3, make_payload([9] * 13, [addr] * 13))
+    assert idx.duplicates == 10 and len(idx) == 303
+    recs, pay = idx.records_payload()
+    tags, p = idx.lookup(keys[:10])
+    assert (tags == 0).all() and (p['amount'] == 5).all()
+
+
+@pytest.mark.gpu
+def test_scan_fingerprint_after_rehash_and_tombstone_reuse(gpu):
+    """The owner fingerprint lives in the key slot: it must be rewritten when the table grows (dump +
+    re-insert) and when an insert reuses a tombstoned slot; stake flags follow the payload."""
+    from upow_amd.ledger.utxo import STAKE_EXCLUDE, STAKE_ONLY, _GpuBackend
+    g = UtxoIndex(backend='gpu')
+    g.be = _GpuBackend(log2_cap=8)  # 128 entries before the first rehash
+    h = UtxoIndex(backend='host')
+    owners = [bytes([42 + (o & 1)]) + bytes([o] * 32) for o in range(4)]
+    rng = np.random.default_rng(3)
+    for round_ in range(6):
+        keys = _keys(200, 1000 + round_)
+        own = rng.integers(0, 4, len(keys))
+        stake = (rng.random(len(keys)) < 0.3).tolist()
+        pay = make_payload([int(a) for a in rng.integers(1, 10**6, len(keys))], [owners[o] for o in own], stake)
+        for idx in (g, h):
+            idx.insert(keys, 0, pay)
+        gone = keys[::3]
+        for idx in (g, h):
+            idx.erase(gone)
+            idx.insert(gone[:20], 0, make_payload([11] * 20, [owners[1]] * 20))  # lands in tombstones
+    assert g.be.log2 > 8
+    for o in owners:
+        for sel in (0, STAKE_EXCLUDE, STAKE_ONLY):
+            rg, pg, tg = g.address_outputs(o, (0,), sel)
+            rh, ph, th = h.address_outputs(o, (0,), sel)
+            assert rg.tobytes() == rh.tobytes() and pg.tobytes() == ph.tobytes() and tg == th

@@ -33,7 +33,7 @@ from ..models.transaction import CoinbaseTransaction, Transaction, TransactionIn
 from ..utils import codec
 from ..utils.codec import (AddressFormat, OutputType, TransactionType, normalize_block, point_to_bytes,
                            point_to_string, round_up_decimal, sha256, string_to_bytes, string_to_point)
-from ..utils.jsonstore import JsonStore
+from ..utils.logstore import LogStore
 from ..utils.logger import get_logger
 from .governance import GOV_TABLES, STAKE, GovernanceIndex
 from .utxo import PAYLOAD_DTYPE, TAG_BY_TABLE, UtxoIndex, make_payload
@@ -305,7 +305,9 @@ class Database:
         if os.environ.get('UPOW_LEDGER_WRITER', '1') != '0':
             self._open_writer(cache_mb)
         store_dir = os.path.dirname(path) if path != ':memory:' else None
-        self.emission_details = JsonStore(os.path.join(store_dir, 'emission_details.json') if store_dir else None)
+        # per-block inode emission records (reference: pickledb emission_details.json): an append-only log
+        self.emission_details = LogStore(os.path.join(store_dir, 'emission_details.jsonl') if store_dir else None,
+                                         legacy_json=os.path.join(store_dir, 'emission_details.json') if store_dir else None)
         self.utxo = UtxoIndex(backend=utxo_backend)
         self.utxo_source = 'sql'
         if path != ':memory:' and os.environ.get('UPOW_SNAPSHOT', '1') != '0':
@@ -395,6 +397,7 @@ class Database:
             self._ckpt_stop = None
         if self.writer is not None:
             self.writer.close()  # drains the queue into SQL first
+        self.emission_details.close()
         with self.lock:
             self._conn.close()
         if self.path == ':memory:':
@@ -553,29 +556,31 @@ class Database:
     def _rebuild_utxo_index(self):
         """Rebuild the HBM/host UTXO set from the output tables; each entry's payload (amount,
         address bytes) comes from its creating tx's JSON columns, read with SQLite's json_extract."""
-        keys, tags, amounts, addrs = [], [], [], []
+        keys, tags, amounts, addrs, stake = [], [], [], [], []
         for table in OUTPUT_TABLES:
             tag = TAG_BY_TABLE[table]
+            stake_col = 'u.is_stake' if table == 'unspent_outputs' else 'NULL'
             for r in self._q(f'SELECT u.tx_hash, u."index", '
                              f'json_extract(t.outputs_amounts, \'$[\' || u."index" || \']\'), '
-                             f'json_extract(t.outputs_addresses, \'$[\' || u."index" || \']\') '
+                             f'json_extract(t.outputs_addresses, \'$[\' || u."index" || \']\'), {stake_col} '
                              f'FROM {table} u LEFT JOIN transactions t ON t.tx_hash = u.tx_hash'):
                 keys.append((r[0], r[1]))
                 tags.append(tag)
                 amounts.append(r[2])
                 addrs.append(_addr_bytes(r[3]))
-        self.utxo.reset(keys, tags, make_payload(amounts, addrs))
+                stake.append(r[4] == 1)
+        self.utxo.reset(keys, tags, make_payload(amounts, addrs, stake))
         if getattr(self, 'gov', None) is not None:
             self.gov.rebuild()
 
-    async def _payload_from_ledger(self, outpoints: List[Tuple[str, int]]):
+    async def _payload_from_ledger(self, outpoints: List[Tuple[str, int]], stake=None):
         infos = await self.get_transactions_info([h for h, _ in outpoints])
         amounts, addrs = [], []
         for h, i in outpoints:
             info = infos.get(h)
             amounts.append(_at(info['outputs_amounts'], i) if info else None)
             addrs.append(_addr_bytes(_at(info['outputs_addresses'], i)) if info else None)
-        return make_payload(amounts, addrs)
+        return make_payload(amounts, addrs, stake)
 
     def _select_outpoints(self, table: str, outputs: List[Tuple[str, int]]) -> List[Tuple[str, int]]:
         """``SELECT tx_hash, index FROM <table> WHERE (tx_hash, index) = ANY($1)`` (rows in table order)."""
@@ -1044,14 +1049,15 @@ class Database:
         else:
             rows = [(o[0], o[1], o[2], None if o[3] is None else int(bool(o[3]))) for o in outputs]
             if len(outputs[0]) >= 5:  # (tx_hash, index, address, is_stake, amount in smallest units)
-                payload = make_payload([o[4] for o in outputs], [_addr_bytes(o[2]) for o in outputs])
+                payload = make_payload([o[4] for o in outputs], [_addr_bytes(o[2]) for o in outputs],
+                                       [r[3] == 1 for r in rows])
         self._xm('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) VALUES (?, ?, ?, ?)', rows)
         if self.gov is not None:
             self.gov.added(STAKE, [(r[0], r[1]) for r in rows if r[3] == 1])
         if not index:
             return
         if payload is None:
-            payload = await self._payload_from_ledger([(r[0], r[1]) for r in rows])
+            payload = await self._payload_from_ledger([(r[0], r[1]) for r in rows], [r[3] == 1 for r in rows])
         self.utxo.insert([(r[0], r[1]) for r in rows], TAG_BY_TABLE['unspent_outputs'], payload)
 
     @staticmethod
@@ -1096,7 +1102,8 @@ class Database:
         from .utxo import pack_records
         cb_keys = [(o[0], o[1]) for o in coinbase_outputs]
         cb_recs = pack_records(cb_keys, tag_u)
-        cb_pay = make_payload([o[4] for o in coinbase_outputs], [_addr_bytes(o[2]) for o in coinbase_outputs])
+        cb_pay = make_payload([o[4] for o in coinbase_outputs], [_addr_bytes(o[2]) for o in coinbase_outputs],
+                              [bool(o[3]) for o in coinbase_outputs])
         in_keys = np.ascontiguousarray(in_keys, dtype=np.uint8).reshape(-1, 40)
         spent = np.array(in_keys, dtype=np.uint8, copy=True)
         spent[:, 36:40] = np.full((n_in, 1), tag_u, dtype=np.uint32).view(np.uint8)

@@ -28,7 +28,7 @@ from ..utils.logger import get_logger
 from .utxo import PAYLOAD_DTYPE, TAG_BY_TABLE
 
 logger = get_logger(__name__)
-MAGIC, VERSION = 'upow-utxo-snapshot', 2
+MAGIC, VERSION = 'upow-utxo-snapshot', 3  # v3: payload flags (is_stake)
 FILE_NAME = 'utxo_snapshot.bin'
 
 

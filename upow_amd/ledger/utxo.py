@@ -31,17 +31,24 @@ TABLE_BY_TAG = {v: k for k, v in TAG_BY_TABLE.items()}
 MISSING = 0xFF
 
 # per-outpoint payload carried by the index (csrc/utxo_table.hip UtxoPayload): the spent output's
-# amount in smallest units and its raw address bytes (33 compressed / 64 uncompressed)
-PAYLOAD_DTYPE = np.dtype([('amount', '<u8'), ('len', '<u4'), ('pad', '<u4'), ('addr', 'u1', (64,))])
+# amount in smallest units, flags (bit 0: unspent_outputs.is_stake = 1) and its raw address bytes
+# (33 compressed / 64 uncompressed)
+PAYLOAD_DTYPE = np.dtype([('amount', '<u8'), ('len', '<u4'), ('flags', '<u4'), ('addr', 'u1', (64,))])
+FLAG_STAKE = 1
+STAKE_ANY, STAKE_EXCLUDE, STAKE_ONLY = 0, 1, 2  # address-scan selectors
 assert PAYLOAD_DTYPE.itemsize == 80
 
 
-def make_payload(amounts: Sequence[Optional[int]], addrs: Sequence[Optional[bytes]]) -> np.ndarray:
-    """Payload records; an unknown amount/address gives len 0 (consumers then fall back to SQL)."""
+def make_payload(amounts: Sequence[Optional[int]], addrs: Sequence[Optional[bytes]],
+                 stake: Optional[Sequence] = None) -> np.ndarray:
+    """Payload records; an unknown amount/address gives len 0 (consumers then fall back to SQL).
+    ``stake``: per-output is_stake values (truthy -> FLAG_STAKE)."""
     n = len(amounts)
     p = np.zeros(n, dtype=PAYLOAD_DTYPE)
     if n == 0:
         return p
+    if stake is not None:
+        p['flags'] = np.fromiter((FLAG_STAKE if s else 0 for s in stake), dtype=np.uint32, count=n)
     raw = np.zeros((n, 64), dtype=np.uint8)
     lens = np.zeros(n, dtype=np.uint32)
     amt = np.zeros(n, dtype=np.uint64)
@@ -88,12 +95,18 @@ class _HostBackend:
         self.d, self.p = {}, {}
         self.insert(keys, tags, payload)
 
-    def insert(self, keys, tags, payload=None):
+    def insert(self, keys, tags, payload=None) -> int:
+        """Returns the number of outpoints already present (left untouched, like the HBM table)."""
         raw = payload.tobytes() if payload is not None else None
+        dups = 0
         for n, ((h, i), t) in enumerate(zip(keys, tags)):
             k = (h, int(i))
+            if k in self.d:
+                dups += 1
+                continue
             self.d[k] = int(t)
             self.p[k] = raw[80 * n:80 * n + 80] if raw is not None else bytes(80)
+        return dups
 
     def probe(self, keys) -> np.ndarray:
         return np.array([self.d.get((h, int(i)), MISSING) for h, i in keys], dtype=np.uint8)
@@ -118,8 +131,14 @@ class _HostBackend:
     def records(self) -> np.ndarray:
         return pack_records(list(self.d.keys()), list(self.d.values()))
 
-    def address_scan(self, addr: bytes, tag_mask: int):
-        hits = [k for k, t in self.d.items() if (tag_mask >> t) & 1 and self._addr(self.p.get(k)) == addr]
+    def address_scan(self, addr: bytes, tag_mask: int, stake_sel: int = STAKE_ANY):
+        def stake_ok(k, t):
+            if stake_sel == STAKE_ANY:
+                return True
+            st = t == 0 and bool(int.from_bytes(self.p.get(k, bytes(80))[12:16], 'little') & FLAG_STAKE)
+            return st == (stake_sel == STAKE_ONLY)
+        hits = [k for k, t in self.d.items() if (tag_mask >> t) & 1 and self._addr(self.p.get(k)) == addr
+                and stake_ok(k, t)]
         pay = np.frombuffer(b''.join(self.p[k] for k in hits), dtype=PAYLOAD_DTYPE)
         return pack_records(hits, [self.d[k] for k in hits]), pay
 
@@ -167,7 +186,7 @@ class _GpuBackend:
         self.L.utxo_destroy(self.h)
         self.h = self.L.utxo_create(self.log2)
         if len(recs):
-            assert self.L.utxo_insert(self.h, np.ascontiguousarray(recs), pay) == 0
+            assert self.L.utxo_insert(self.h, np.ascontiguousarray(recs), pay) == (0, 0)
         self.count, self.tombs = len(recs), 0
 
     def reset(self, keys, tags, payload=None):
@@ -179,18 +198,19 @@ class _GpuBackend:
 
     def insert(self, keys, tags, payload=None):
         if not len(keys):
-            return
-        self.insert_records(pack_records(keys, list(tags)), payload)
+            return 0
+        return self.insert_records(pack_records(keys, list(tags)), payload)
 
     def insert_records(self, recs: np.ndarray, payload=None):
         if not len(recs):
             return
         self._ensure(len(recs))
         pay = None if payload is None else np.ascontiguousarray(payload).view(np.uint8)
-        failed = self.L.utxo_insert(self.h, np.ascontiguousarray(recs), pay)
+        failed, dups = self.L.utxo_insert(self.h, np.ascontiguousarray(recs), pay)
         if failed:
             raise RuntimeError(f'UTXO table insert failed for {failed} entries')
-        self.count += len(recs)
+        self.count += len(recs) - dups
+        return dups
 
     def lookup_records(self, recs: np.ndarray):
         tags, pay = self.L.utxo_lookup(self.h, np.ascontiguousarray(recs))
@@ -222,8 +242,8 @@ class _GpuBackend:
     def records(self) -> np.ndarray:
         return np.frombuffer(self.L.utxo_dump(self.h), dtype=np.uint8).reshape(-1, 40)
 
-    def address_scan(self, addr: bytes, tag_mask: int):
-        raw, pay, _total = self.L.utxo_address_scan(self.h, addr, tag_mask)
+    def address_scan(self, addr: bytes, tag_mask: int, stake_sel: int = STAKE_ANY):
+        raw, pay, _total = self.L.utxo_address_scan(self.h, addr, tag_mask, stake_sel)
         return np.frombuffer(raw, dtype=np.uint8).reshape(-1, 40), np.frombuffer(pay, dtype=PAYLOAD_DTYPE)
 
     def records_payload(self):
@@ -249,6 +269,13 @@ class UtxoIndex:
     def __init__(self, backend: Optional[str] = None):
         self.backend_name = backend or default_backend()
         self.be = _GpuBackend() if self.backend_name == 'gpu' else _HostBackend()
+        self.duplicates = 0  # inserts of an outpoint that was already live (skipped; a ledger bug if ever > 0)
+
+    def _dups(self, n: int):
+        if n:
+            self.duplicates += int(n)
+            import logging
+            logging.getLogger('upow').error(f'UTXO index: {n} insert(s) of an already live outpoint skipped')
 
     def reset(self, keys: Sequence[Outpoint], tags: Sequence[int], payload: Optional[np.ndarray] = None):
         self.be.reset(list(keys), list(tags), payload)
@@ -256,17 +283,17 @@ class UtxoIndex:
     def insert(self, keys: Sequence[Outpoint], tag, payload: Optional[np.ndarray] = None):
         keys = list(keys)
         tags = [tag] * len(keys) if isinstance(tag, int) else list(tag)
-        self.be.insert(keys, tags, payload)
+        self._dups(self.be.insert(keys, tags, payload))
 
     def insert_records(self, recs: np.ndarray, payload: Optional[np.ndarray] = None):
         """Insert packed 40-byte key records (tags inside) — the block fast path's form."""
         if isinstance(self.be, _GpuBackend):
-            self.be.insert_records(recs, payload)
+            self._dups(self.be.insert_records(recs, payload))
             return
         idx = recs[:, 32:36].copy().view(np.uint32).ravel()
         tags = recs[:, 36:40].copy().view(np.uint32).ravel()
         keys = [(bytes(recs[n, :32]).hex(), int(idx[n])) for n in range(len(recs))]
-        self.be.insert(keys, [int(t) for t in tags], payload)
+        self._dups(self.be.insert(keys, [int(t) for t in tags], payload))
 
     def lookup(self, keys: Sequence[Outpoint]):
         """(tags uint8[n], payload PAYLOAD_DTYPE[n]) for each outpoint (tag 0xff / len 0 when absent)."""
@@ -312,7 +339,7 @@ class UtxoIndex:
         """All live entries as 40-byte records, in canonical (txid, index) order."""
         return sort_records(np.ascontiguousarray(self.be.records()))
 
-    def address_outputs(self, addr: bytes, tags: Iterable[int] = (0,)):
+    def address_outputs(self, addr: bytes, tags: Iterable[int] = (0,), stake_sel: int = STAKE_ANY):
         """K14 (reference ``database.py:909-937,1138-1205``): the live outpoints whose payload address is
         ``addr`` (raw 33/64 bytes, prefix normalised as stored) in the given tables, as (records, payloads)
         in canonical (txid, index) order, plus their amount sum in smallest units. GPU backend: one
@@ -320,7 +347,7 @@ class UtxoIndex:
         mask = 0
         for t in tags:
             mask |= 1 << int(t)
-        recs, pay = self.be.address_scan(bytes(addr), mask)
+        recs, pay = self.be.address_scan(bytes(addr), mask, stake_sel)
         order = sort_order(np.ascontiguousarray(recs))
         recs, pay = np.ascontiguousarray(recs[order]), np.ascontiguousarray(pay[order])
         return recs, pay, int(pay['amount'].sum()) if len(pay) else 0

@@ -21,18 +21,37 @@ from .ledger.database import Database
 
 
 async def address_utxos(address: str, path: str = None, db: Database = None) -> dict:
-    from .ledger.database import _addr_bytes
-    from .ledger.utxo import TABLE_BY_TAG
+    """Live outputs owned by ``address`` in all seven output tables, from the UTXO index (K14; one
+    ``utxo_address_scan`` per address form on a GPU node). Both string forms of the key are matched
+    (compressed 33 B and full 64 B, like the reference's ``address = ANY(addresses)``). ``spendable`` is
+    the reference's ``get_address_balance`` (database.py:1138-1160: unspent_outputs rows with
+    is_stake NULL/0); ``stake`` and each governance table are summed separately."""
+    from .ledger.utxo import STAKE_ONLY, TABLE_BY_TAG
+    from .utils.codec import address_search_hex
     db = db or await Database.create(path=path)
-    raw = _addr_bytes(address)
-    if raw is None:
+    try:
+        forms = [bytes.fromhex(h) for h in address_search_hex(address)]
+    except Exception:
         raise SystemExit(f'not an address: {address}')
-    recs, pay, total = db.utxo.address_outputs(raw, TABLE_BY_TAG)
-    idx = recs[:, 32:36].copy().view('<u4').ravel()
-    tag = recs[:, 36:40].copy().view('<u4').ravel()
-    return {'address': address, 'backend': db.utxo.backend_name, 'total': str(Decimal(total) / SMALLEST),
-            'outputs': [{'tx_hash': bytes(recs[k, :32]).hex(), 'index': int(idx[k]), 'table': TABLE_BY_TAG[int(tag[k])],
-                         'amount': str(Decimal(int(pay['amount'][k])) / SMALLEST)} for k in range(len(recs))]}
+    outputs, sums = [], {'spendable': 0, 'stake': 0, **{t: 0 for t in TABLE_BY_TAG.values() if t != 'unspent_outputs'}}
+    for raw in forms:
+        recs, pay, _ = db.utxo.address_outputs(raw, TABLE_BY_TAG)
+        idx = recs[:, 32:36].copy().view('<u4').ravel()
+        tag = recs[:, 36:40].copy().view('<u4').ravel()
+        for k in range(len(recs)):
+            table = TABLE_BY_TAG[int(tag[k])]
+            stake = table == 'unspent_outputs' and bool(int(pay['flags'][k]) & 1)
+            amount = int(pay['amount'][k])
+            key = ('stake' if stake else 'spendable') if table == 'unspent_outputs' else table
+            sums[key] += amount
+            outputs.append({'tx_hash': bytes(recs[k, :32]).hex(), 'index': int(idx[k]), 'table': table,
+                            'is_stake': stake, 'amount': str(Decimal(amount) / SMALLEST), 'form': len(raw)})
+    outputs.sort(key=lambda o: (o['tx_hash'], o['index']))
+    return {'address': address, 'backend': db.utxo.backend_name,
+            'spendable': str(Decimal(sums.pop('spendable')) / SMALLEST), 'stake': str(Decimal(sums.pop('stake')) / SMALLEST),
+            'tables': {t: str(Decimal(v) / SMALLEST) for t, v in sums.items()},
+            'total': str(Decimal(sum(int(Decimal(o['amount']) * SMALLEST) for o in outputs)) / SMALLEST),
+            'outputs': outputs}
 
 
 async def rebuild_utxo(path: str = None):
