@@ -1,4 +1,4 @@
-// Ledger journal + background SQL materialiser, on a SQLite connection this layer opens and owns.
+// Ledger journal + background SQL materialisers, on SQLite connections this layer opens and owns.
 //
 // reference: the block-apply writes of upow/manager.py:706-730 → upow/database.py add_block 254-270,
 // add_transactions 236-252, add_transaction_outputs 524-580, remove_outputs 589-621,
@@ -8,9 +8,10 @@
 //   commit point   the batch is appended to an append-only journal file (CRC-framed record, write(2);
 //                  fdatasync per record or per materialiser group) — together with the HBM UTXO update
 //                  this is when the block is applied;
-//   materialise    a background thread applies queued batches to the schema.sql tables, several blocks
-//                  per SQLite transaction (group commit), and records the last applied journal sequence
-//                  number in `upow_journal_state` inside the same transaction;
+//   materialise    one background thread per database file (the UTXO table lives in a file of its own)
+//                  applies queued batches to the schema.sql tables, several blocks per SQLite transaction
+//                  (group commit), and records the last applied journal sequence number in that file's
+//                  `upow_journal_state` inside the same transaction;
 //   watermark      readers that need those tables wait until the applied sequence covers the last batch
 //                  that wrote them (Python: Database._settle);
 //   restart        journal records above the recorded sequence are re-applied before the ledger opens,
@@ -24,6 +25,7 @@
 #include <fcntl.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -72,6 +74,9 @@ struct SqliteApi {
     long long (*column_int64)(sqlite3_stmt*, int) = nullptr;
     const char* (*errmsg)(sqlite3*) = nullptr;
     void (*free)(void*) = nullptr;
+    int (*config)(int, ...) = nullptr;
+    int (*initialize)() = nullptr;
+    int (*shutdown)() = nullptr;
     bool ok = false;
 };
 
@@ -98,9 +103,12 @@ const SqliteApi& api() {
         sym(s.column_int64, "sqlite3_column_int64");
         sym(s.errmsg, "sqlite3_errmsg");
         sym(s.free, "sqlite3_free");
+        sym(s.config, "sqlite3_config");
+        sym(s.initialize, "sqlite3_initialize");
+        sym(s.shutdown, "sqlite3_shutdown");
         s.ok = s.open_v2 && s.close_v2 && s.exec && s.busy_timeout && s.prepare_v2 && s.bind_text && s.bind_int64 &&
                s.bind_null && s.step && s.reset && s.clear_bindings && s.finalize && s.changes && s.column_int64 &&
-               s.errmsg && s.free;
+               s.errmsg && s.free && s.config && s.initialize && s.shutdown;
         return s;
     }();
     if (!a.ok) throw std::runtime_error("libsqlite3.so.0 not available for the native ledger writer");
@@ -261,14 +269,16 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
     }
 }
 
-// Statement encoding: str sql, u32 flags (1: guard sql, 2: expected change count), [str guard], [i64 expect],
+// Statement encoding: str sql, u32 flags (1: guard sql, 2: expected change count, bits 8..15: target
+// database file), [str guard], [i64 expect],
 // i64 n, u32 n_cols, cols..., u8 has_order, [i64 order[n]].
 py::bytes encode_stmt(const std::string& sql, py::sequence cols, int64_t n, py::object order, py::object guard,
-                      py::object expect) {
+                      py::object expect, int shard) {
     if (n < 0) throw std::invalid_argument("n < 0");
+    if (shard < 0 || shard > 15) throw std::invalid_argument("shard must be in [0, 15]");
     Out o;
     o.str(sql);
-    const uint32_t flags = (guard.is_none() ? 0u : 1u) | (expect.is_none() ? 0u : 2u);
+    const uint32_t flags = (guard.is_none() ? 0u : 1u) | (expect.is_none() ? 0u : 2u) | (uint32_t(shard) << 8);
     o.u32(flags);
     if (flags & 1) o.str(guard.cast<std::string>());
     if (flags & 2) o.i64(expect.cast<int64_t>());
@@ -401,44 +411,56 @@ bool read_exact(int fd, char* p, size_t n, off_t at) {
     return true;
 }
 
+// The distribution's libsqlite3 is built with OMIT_LOOKASIDE (every small allocation goes to malloc) and
+// the default MEMSTATUS=1, which wraps each malloc/free in one process-wide mutex: two materialiser
+// threads on two files then serialise on that mutex. Allocation statistics can only be switched off before
+// the library is initialised, so this runs when the extension loads (before any connection exists):
+// returns the sqlite3_config result (0 = applied, 21 = library already initialised).
+int sqlite_disable_memstatus() {
+    const SqliteApi& a = api();
+    constexpr int SQLITE_CONFIG_MEMSTATUS = 9;
+    return a.config(SQLITE_CONFIG_MEMSTATUS, 0);
+}
+
 // ------------------------------------------------------------------------------------------ writer
+// One journal, several database files ("shards"): each statement names the file it writes (flags bits
+// 8..15) and every file has its own materialiser thread and connection, so the UTXO table and the
+// block/tx tables are brought up to date in parallel. Each file records the last journal sequence it
+// applied (upow_journal_state, updated in the same transaction as the rows).
+enum SyncMode { SYNC_OFF = 0, SYNC_GROUP = 1, SYNC_COMMIT = 2 };
+
 struct Batch {
     uint64_t seq;
     std::shared_ptr<std::string> payload;  // u32 n_stmts + statements
 };
 
-enum SyncMode { SYNC_OFF = 0, SYNC_GROUP = 1, SYNC_COMMIT = 2 };
+struct Shard {
+    std::string path;
+    sqlite3* db = nullptr;
+    std::unordered_map<std::string, sqlite3_stmt*> stmts;  // shard thread only
+    std::deque<Batch> queue;
+    uint64_t applied = 0;
+    int64_t groups = 0, replayed = 0, apply_ns = 0, commit_ns = 0, sync_ns = 0;
+    std::thread thread;
+};
 
 class LedgerWriter {
    public:
-    LedgerWriter(const std::string& db_path, const std::string& journal_path, int sync_mode, int64_t cache_mb,
-                 int group_max, int64_t journal_max_bytes)
-        : db_path_(db_path), journal_path_(journal_path), sync_(sync_mode), group_max_(std::max(1, group_max)),
+    LedgerWriter(const std::vector<std::string>& db_paths, const std::string& journal_path, int sync_mode,
+                 int64_t cache_mb, int group_max, int64_t journal_max_bytes)
+        : journal_path_(journal_path), sync_(sync_mode), group_max_(std::max(1, group_max)),
           journal_max_(journal_max_bytes) {
-        const SqliteApi& a = api();
-        int rc = a.open_v2(db_path.c_str(), &db_, SQLITE_OPEN_READWRITE | SQLITE_OPEN_CREATE | SQLITE_OPEN_NOMUTEX |
-                                                     SQLITE_OPEN_URI, nullptr);
-        if (rc != SQLITE_OK) {
-            std::string m = db_ ? a.errmsg(db_) : "open failed";
-            if (db_) a.close_v2(db_);
-            db_ = nullptr;
-            throw std::runtime_error("ledger writer: cannot open " + db_path + ": " + m);
+        if (db_paths.empty() || db_paths.size() > 16) throw std::invalid_argument("1..16 database files");
+        for (auto& p : db_paths) {
+            shards_.emplace_back(new Shard());
+            Shard& sh = *shards_.back();
+            sh.path = p;
+            open_shard(sh, cache_mb);
         }
-        a.busy_timeout(db_, 60000);
-        // the journal is the durability point: SQL commits never need to reach the disk on their own
-        exec("PRAGMA journal_mode = WAL");
-        exec("PRAGMA synchronous = OFF");
-        exec("PRAGMA foreign_keys = OFF");
-        exec("PRAGMA cache_size = -" + std::to_string(std::max<int64_t>(16, cache_mb) * 1024));
-        exec("PRAGMA wal_autocheckpoint = 0");
-        exec("CREATE TABLE IF NOT EXISTS upow_journal_state (k INTEGER PRIMARY KEY CHECK (k = 0), seq INTEGER NOT NULL)");
-        exec("INSERT OR IGNORE INTO upow_journal_state (k, seq) VALUES (0, 0)");
-        applied_ = uint64_t(query_int("SELECT seq FROM upow_journal_state WHERE k = 0"));
-        next_seq_ = applied_ + 1;
         fd_ = ::open(journal_path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
         if (fd_ < 0) throw std::runtime_error("ledger writer: cannot open journal " + journal_path + ": " + strerror(errno));
         recover();
-        thread_ = std::thread([this] { run(); });
+        for (size_t i = 0; i < shards_.size(); ++i) shards_[i]->thread = std::thread([this, i] { run(i); });
     }
 
     ~LedgerWriter() { close(); }
@@ -450,7 +472,8 @@ class LedgerWriter {
             stop_ = true;
         }
         cv_.notify_all();
-        if (thread_.joinable()) thread_.join();
+        for (auto& sh : shards_)
+            if (sh->thread.joinable()) sh->thread.join();
         {
             std::lock_guard<std::mutex> jl(jmu_);
             if (fd_ >= 0) {
@@ -459,24 +482,26 @@ class LedgerWriter {
                 fd_ = -1;
             }
         }
-        for (auto& kv : stmts_) api().finalize(kv.second);
-        stmts_.clear();
-        if (db_) api().close_v2(db_);
-        db_ = nullptr;
+        for (auto& sh : shards_) {
+            for (auto& kv : sh->stmts) api().finalize(kv.second);
+            sh->stmts.clear();
+            if (sh->db) api().close_v2(sh->db);
+            sh->db = nullptr;
+        }
         std::lock_guard<std::mutex> lk(mu_);
         closed_ = true;
     }
 
-    // Commit point: append the record (and fdatasync in SYNC_COMMIT mode), queue it for the
+    // Commit point: append the record (and fdatasync in SYNC_COMMIT mode), queue it for every
     // materialiser. Returns the record's sequence number.
     uint64_t submit(const std::vector<std::string>& stmts, const std::string& meta, int64_t block_id) {
         auto payload = std::make_shared<std::string>();
         size_t total = 4;
-        for (auto& s : stmts) total += s.size();
+        for (auto& st : stmts) total += st.size();
         payload->reserve(total);
         uint32_t ns = uint32_t(stmts.size());
         payload->append(reinterpret_cast<const char*>(&ns), 4);
-        for (auto& s : stmts) payload->append(s);
+        for (auto& st : stmts) payload->append(st);
         uint64_t seq;
         {
             std::lock_guard<std::mutex> jl(jmu_);
@@ -489,18 +514,17 @@ class LedgerWriter {
             RecHeader h{kMagic, 0, seq, block_id, meta.size(), payload->size()};
             h.crc = record_crc(h, meta.data(), payload->data());
             const off_t at = journal_size_;
-            std::string head(reinterpret_cast<const char*>(&h), sizeof h);
-            write_all(fd_, head.data(), head.size());
+            write_all(fd_, reinterpret_cast<const char*>(&h), sizeof h);
             write_all(fd_, meta.data(), meta.size());
             write_all(fd_, payload->data(), payload->size());
             if (sync_ == SYNC_COMMIT) ::fdatasync(fd_);
             journal_size_ += off_t(sizeof h + meta.size() + payload->size());
             if (block_id >= 0) meta_index_[block_id] = {at, seq};
-            bytes_written_ += sizeof h + meta.size() + payload->size();
+            bytes_written_ += int64_t(sizeof h + meta.size() + payload->size());
         }
         {
             std::lock_guard<std::mutex> lk(mu_);
-            queue_.push_back(Batch{seq, payload});
+            for (auto& sh : shards_) sh->queue.push_back(Batch{seq, payload});
             submitted_ = seq;
         }
         cv_.notify_all();
@@ -516,22 +540,22 @@ class LedgerWriter {
         cv_.notify_all();
     }
 
-    uint64_t applied() {
+    uint64_t applied(int shard) {
         std::lock_guard<std::mutex> lk(mu_);
-        return applied_;
+        return applied_locked(shard);
     }
 
-    // Block until every record with sequence <= seq is in the SQL tables (or the writer failed).
-    void wait(uint64_t seq, double timeout_s) {
+    // Block until every record with sequence <= seq is in the SQL tables of `shard` (-1: all files).
+    void wait(uint64_t seq, int shard, double timeout_s) {
         std::unique_lock<std::mutex> lk(mu_);
-        auto pred = [&] { return applied_ >= seq || failed_; };
+        auto pred = [&] { return applied_locked(shard) >= seq || failed_; };
         if (timeout_s > 0) {
             if (!cv_done_.wait_for(lk, std::chrono::duration<double>(timeout_s), pred))
                 throw std::runtime_error("ledger writer: timed out waiting for the SQL materialiser");
         } else {
             cv_done_.wait(lk, pred);
         }
-        if (failed_ && applied_ < seq) throw std::runtime_error("ledger writer failed: " + error_);
+        if (failed_ && applied_locked(shard) < seq) throw std::runtime_error("ledger writer failed: " + error_);
     }
 
     py::object journal_meta(int64_t block_id) {
@@ -557,66 +581,123 @@ class LedgerWriter {
         std::lock_guard<std::mutex> jl(jmu_);
         std::lock_guard<std::mutex> lk(mu_);
         d["submitted"] = submitted_;
-        d["applied"] = applied_;
-        d["queued"] = queue_.size();
-        d["groups"] = groups_;
+        d["applied"] = applied_locked(-1);
+        size_t queued = 0;
+        int64_t groups = 0, replayed = 0;
+        double apply_s = 0, commit_s = 0, sync_s = 0;
+        py::list per;
+        for (auto& sh : shards_) {
+            queued = std::max(queued, sh->queue.size());
+            groups += sh->groups;
+            replayed = std::max(replayed, sh->replayed);
+            apply_s = std::max(apply_s, sh->apply_ns / 1e9);
+            commit_s = std::max(commit_s, sh->commit_ns / 1e9);
+            sync_s = std::max(sync_s, sh->sync_ns / 1e9);
+            py::dict x;
+            x["applied"] = sh->applied;
+            x["groups"] = sh->groups;
+            x["apply_s"] = sh->apply_ns / 1e9;
+            x["commit_s"] = sh->commit_ns / 1e9;
+            x["replayed"] = sh->replayed;
+            per.append(x);
+        }
+        d["queued"] = queued;
+        d["groups"] = groups;
         d["journal_bytes"] = int64_t(journal_size_);
         d["bytes_written"] = bytes_written_;
-        d["apply_s"] = apply_ns_ / 1e9;
-        d["commit_s"] = commit_ns_ / 1e9;
-        d["sync_s"] = sync_ns_ / 1e9;
-        d["replayed"] = replayed_;
+        d["apply_s"] = apply_s;  // the slowest file
+        d["commit_s"] = commit_s;
+        d["sync_s"] = sync_s;
+        d["replayed"] = replayed;
         d["rotations"] = rotations_;
         d["failed"] = failed_;
         d["error"] = error_;
         d["change_mismatches"] = mismatches_;
-        py::dict per;
-        for (auto& kv : stmt_stats_) per[py::str(kv.first)] = py::make_tuple(kv.second.first / 1e9, kv.second.second);
-        d["statements"] = per;
+        d["shards"] = per;
+        py::dict st;
+        for (auto& kv : stmt_stats_) st[py::str(kv.first)] = py::make_tuple(kv.second.first / 1e9, kv.second.second);
+        d["statements"] = st;
         return d;
     }
 
    private:
-    void exec(const std::string& sql) {
-        char* err = nullptr;
-        int rc = api().exec(db_, sql.c_str(), nullptr, nullptr, &err);
+    uint64_t applied_locked(int shard) const {
+        if (shard >= 0) return shards_.at(size_t(shard))->applied;
+        uint64_t m = ~uint64_t(0);
+        for (auto& sh : shards_) m = std::min(m, sh->applied);
+        return m;
+    }
+
+    void open_shard(Shard& sh, int64_t cache_mb) {
+        const SqliteApi& a = api();
+        int rc = a.open_v2(sh.path.c_str(), &sh.db,
+                           SQLITE_OPEN_READWRITE | SQLITE_OPEN_CREATE | SQLITE_OPEN_NOMUTEX | SQLITE_OPEN_URI, nullptr);
         if (rc != SQLITE_OK) {
-            std::string m = err ? err : api().errmsg(db_);
+            std::string m = sh.db ? a.errmsg(sh.db) : "open failed";
+            if (sh.db) a.close_v2(sh.db);
+            sh.db = nullptr;
+            throw std::runtime_error("ledger writer: cannot open " + sh.path + ": " + m);
+        }
+        a.busy_timeout(sh.db, 60000);
+        // the journal is the durability point: SQL commits never need to reach the disk on their own
+        exec(sh.db, "PRAGMA journal_mode = WAL");
+        exec(sh.db, "PRAGMA synchronous = OFF");
+        exec(sh.db, "PRAGMA foreign_keys = OFF");
+        exec(sh.db, "PRAGMA secure_delete = OFF");  // the distribution build defaults to zero-filling freed cells
+        exec(sh.db, "PRAGMA cache_size = -" + std::to_string(std::max<int64_t>(16, cache_mb) * 1024));
+        exec(sh.db, "PRAGMA wal_autocheckpoint = 0");
+        exec(sh.db, "CREATE TABLE IF NOT EXISTS upow_journal_state (k INTEGER PRIMARY KEY CHECK (k = 0), seq INTEGER NOT NULL)");
+        exec(sh.db, "INSERT OR IGNORE INTO upow_journal_state (k, seq) VALUES (0, 0)");
+        sh.applied = uint64_t(query_int(sh.db, "SELECT seq FROM upow_journal_state WHERE k = 0"));
+    }
+
+    static void exec(sqlite3* db, const std::string& sql) {
+        char* err = nullptr;
+        int rc = api().exec(db, sql.c_str(), nullptr, nullptr, &err);
+        if (rc != SQLITE_OK) {
+            std::string m = err ? err : api().errmsg(db);
             if (err) api().free(err);
             throw SqlError("ledger writer: " + m + " [" + sql.substr(0, 120) + "]", rc);
         }
     }
 
-    int64_t query_int(const std::string& sql) {
+    static void rollback(sqlite3* db) {
+        char* e = nullptr;
+        api().exec(db, "ROLLBACK", nullptr, nullptr, &e);
+        if (e) api().free(e);
+    }
+
+    static int64_t query_int(sqlite3* db, const std::string& sql) {
         const SqliteApi& a = api();
         sqlite3_stmt* st = nullptr;
-        int rc = a.prepare_v2(db_, sql.c_str(), int(sql.size()), &st, nullptr);
-        if (rc != SQLITE_OK) throw SqlError(std::string("ledger writer: ") + a.errmsg(db_), rc);
+        int rc = a.prepare_v2(db, sql.c_str(), int(sql.size()), &st, nullptr);
+        if (rc != SQLITE_OK) throw SqlError(std::string("ledger writer: ") + a.errmsg(db), rc);
         int64_t v = 0;
         rc = a.step(st);
         if (rc == SQLITE_ROW) v = a.column_int64(st, 0);
         a.finalize(st);
-        if (rc != SQLITE_ROW && rc != SQLITE_DONE) throw SqlError(std::string("ledger writer: ") + a.errmsg(db_), rc);
+        if (rc != SQLITE_ROW && rc != SQLITE_DONE) throw SqlError(std::string("ledger writer: ") + a.errmsg(db), rc);
         return v;
     }
 
-    sqlite3_stmt* prepared(const std::string& sql) {
-        auto it = stmts_.find(sql);
-        if (it != stmts_.end()) return it->second;
+    static sqlite3_stmt* prepared(Shard& sh, const std::string& sql) {
+        auto it = sh.stmts.find(sql);
+        if (it != sh.stmts.end()) return it->second;
         sqlite3_stmt* st = nullptr;
-        int rc = api().prepare_v2(db_, sql.c_str(), int(sql.size()), &st, nullptr);
-        if (rc != SQLITE_OK) throw SqlError(std::string("ledger writer: ") + api().errmsg(db_) + " [" + sql + "]", rc);
-        if (stmts_.size() > 256) {
-            for (auto& kv : stmts_) api().finalize(kv.second);
-            stmts_.clear();
+        int rc = api().prepare_v2(sh.db, sql.c_str(), int(sql.size()), &st, nullptr);
+        if (rc != SQLITE_OK) throw SqlError(std::string("ledger writer: ") + api().errmsg(sh.db) + " [" + sql + "]", rc);
+        if (sh.stmts.size() > 256) {
+            for (auto& kv : sh.stmts) api().finalize(kv.second);
+            sh.stmts.clear();
         }
-        stmts_[sql] = st;
+        sh.stmts[sql] = st;
         return st;
     }
 
-    // Apply one encoded batch inside the open transaction.
-    void apply_batch(const std::string& payload) {
+    // Apply the statements of one encoded batch that belong to `shard`, inside its open transaction.
+    void apply_batch(size_t shard, const std::string& payload) {
         const SqliteApi& a = api();
+        Shard& sh = *shards_[shard];
         In in{payload.data(), payload.data() + payload.size()};
         const uint32_t ns = in.get<uint32_t>();
         for (uint32_t s = 0; s < ns; ++s) {
@@ -626,6 +707,7 @@ class LedgerWriter {
             int64_t expect = -1;
             if (flags & 1) guard = in.str();
             if (flags & 2) expect = in.get<int64_t>();
+            const size_t target = (flags >> 8) & 0xffu;
             const int64_t n = in.get<int64_t>();
             const uint32_t nc = in.get<uint32_t>();
             std::vector<ColView> cols(nc);
@@ -650,9 +732,11 @@ class LedgerWriter {
             }
             const char* order = nullptr;
             if (in.get<uint8_t>()) order = in.take(size_t(n) * 8);
-            if (!guard.empty() && query_int(guard) == 0) continue;
+            if (target >= shards_.size()) throw std::runtime_error("ledger batch: statement for an unknown file");
+            if (target != shard) continue;
+            if (!guard.empty() && query_int(sh.db, guard) == 0) continue;
             const auto ts0 = std::chrono::steady_clock::now();
-            sqlite3_stmt* st = prepared(sql);
+            sqlite3_stmt* st = prepared(sh, sql);
             int64_t changes = 0;
             char hexbuf[8][64];
             for (int64_t k = 0; k < n; ++k) {
@@ -690,28 +774,36 @@ class LedgerWriter {
                 }
                 int rc = a.step(st);
                 if (rc != SQLITE_DONE && rc != SQLITE_ROW) {
-                    std::string m = a.errmsg(db_);
+                    std::string m = a.errmsg(sh.db);
                     a.reset(st);
                     throw SqlError("ledger writer: " + m + " [" + sql.substr(0, 120) + "]", rc);
                 }
-                changes += a.changes(db_);
+                changes += a.changes(sh.db);
                 a.reset(st);
             }
             a.clear_bindings(st);
-            if (expect >= 0 && changes != expect) ++mismatches_;
+            const int64_t ns_used =
+                std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - ts0).count();
             std::lock_guard<std::mutex> lk(mu_);
+            if (expect >= 0 && changes != expect) ++mismatches_;
             auto& acc = stmt_stats_[sql.substr(0, 48)];
-            acc.first += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - ts0).count();
+            acc.first += ns_used;
             acc.second += n;
         }
     }
 
-    // Start-up: re-apply every intact record above the recorded sequence, cut off a torn tail.
+    // Start-up: re-apply, per file, every intact record above that file's recorded sequence; cut off a
+    // torn tail record.
     void recover() {
         off_t at = 0;
         const off_t end = ::lseek(fd_, 0, SEEK_END);
-        std::vector<std::pair<uint64_t, std::string>> redo;
-        uint64_t max_seq = applied_;
+        std::vector<std::pair<uint64_t, std::shared_ptr<std::string>>> records;
+        uint64_t max_seq = 0;
+        uint64_t min_applied = ~uint64_t(0);
+        for (auto& sh : shards_) {
+            max_seq = std::max(max_seq, sh->applied);
+            min_applied = std::min(min_applied, sh->applied);
+        }
         while (at + off_t(sizeof(RecHeader)) <= end) {
             RecHeader h;
             if (!read_exact(fd_, reinterpret_cast<char*>(&h), sizeof h, at) || h.magic != kMagic) break;
@@ -719,13 +811,14 @@ class LedgerWriter {
             if (h.meta_len > uint64_t(end) || h.payload_len > uint64_t(end) ||
                 body + off_t(h.meta_len + h.payload_len) > end)
                 break;
-            std::string meta(h.meta_len, '\0'), payload(h.payload_len, '\0');
+            std::string meta(h.meta_len, '\0');
+            auto payload = std::make_shared<std::string>(h.payload_len, '\0');
             if (!read_exact(fd_, meta.data(), meta.size(), body) ||
-                !read_exact(fd_, payload.data(), payload.size(), body + off_t(h.meta_len)))
+                !read_exact(fd_, payload->data(), payload->size(), body + off_t(h.meta_len)))
                 break;
-            if (record_crc(h, meta.data(), payload.data()) != h.crc) break;
+            if (record_crc(h, meta.data(), payload->data()) != h.crc) break;
             if (h.block_id >= 0) meta_index_[h.block_id] = {at, h.seq};
-            if (h.seq > applied_) redo.emplace_back(h.seq, std::move(payload));
+            if (h.seq > min_applied) records.emplace_back(h.seq, payload);
             max_seq = std::max<uint64_t>(max_seq, h.seq);
             at = body + off_t(h.meta_len + h.payload_len);
         }
@@ -736,36 +829,46 @@ class LedgerWriter {
         journal_size_ = at;
         ::lseek(fd_, at, SEEK_SET);
         next_seq_ = max_seq + 1;
-        if (!redo.empty()) {
-            exec("BEGIN IMMEDIATE");
+        for (size_t i = 0; i < shards_.size(); ++i) {
+            Shard& sh = *shards_[i];
+            uint64_t last = 0;
+            int64_t n = 0;
+            exec(sh.db, "BEGIN IMMEDIATE");
             try {
-                for (auto& r : redo) apply_batch(r.second);
-                exec("UPDATE upow_journal_state SET seq = " + std::to_string(redo.back().first) + " WHERE k = 0");
-                exec("COMMIT");
+                for (auto& r : records) {
+                    if (r.first <= sh.applied) continue;
+                    apply_batch(i, *r.second);
+                    last = r.first;
+                    ++n;
+                }
+                if (n) exec(sh.db, "UPDATE upow_journal_state SET seq = " + std::to_string(last) + " WHERE k = 0");
+                exec(sh.db, "COMMIT");
             } catch (...) {
-                char* e = nullptr;
-                api().exec(db_, "ROLLBACK", nullptr, nullptr, &e);
-                if (e) api().free(e);
+                rollback(sh.db);
                 throw;
             }
-            applied_ = redo.back().first;
-            replayed_ = int64_t(redo.size());
+            if (n) sh.applied = last;
+            sh.replayed = n;
         }
-        submitted_ = applied_;
+        submitted_ = applied_locked(-1);
+        for (auto& sh : shards_) submitted_ = std::max(submitted_, sh->applied);
     }
 
     void maybe_rotate() {
-        // all records are in SQL: make the SQL side durable, then start an empty journal
+        // every record is in every file: make the SQL side durable, then start an empty journal
         std::lock_guard<std::mutex> jl(jmu_);
         {
             std::lock_guard<std::mutex> lk(mu_);
-            if (!queue_.empty() || applied_ != submitted_) return;
+            for (auto& sh : shards_)
+                if (!sh->queue.empty() || sh->applied != submitted_) return;
         }
         if (journal_max_ <= 0 || journal_size_ < journal_max_) return;
-        exec("PRAGMA synchronous = FULL");
-        exec("UPDATE upow_journal_state SET seq = seq WHERE k = 0");
-        exec("PRAGMA wal_checkpoint(PASSIVE)");
-        exec("PRAGMA synchronous = OFF");
+        for (auto& sh : shards_) {
+            exec(sh->db, "PRAGMA synchronous = FULL");
+            exec(sh->db, "UPDATE upow_journal_state SET seq = seq WHERE k = 0");
+            exec(sh->db, "PRAGMA wal_checkpoint(PASSIVE)");
+            exec(sh->db, "PRAGMA synchronous = OFF");
+        }
         if (::ftruncate(fd_, 0) != 0) throw std::runtime_error("journal truncate failed");
         ::fdatasync(fd_);
         ::lseek(fd_, 0, SEEK_SET);
@@ -774,49 +877,48 @@ class LedgerWriter {
         ++rotations_;
     }
 
-    void run() {
+    void run(size_t i) {
+        Shard& sh = *shards_[i];
         for (;;) {
             std::vector<Batch> group;
             {
                 std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_ || (!queue_.empty() && !failed_ && !paused_); });
-                if (paused_ && !stop_) continue;
-                if (queue_.empty() || failed_) {
+                cv_.wait(lk, [&] { return stop_ || (!sh.queue.empty() && !failed_ && !paused_); });
+                if (sh.queue.empty() || failed_) {
                     if (stop_) return;
                     continue;
                 }
-                while (!queue_.empty() && int(group.size()) < group_max_) {
-                    group.push_back(std::move(queue_.front()));
-                    queue_.pop_front();
+                if (paused_ && !stop_) continue;
+                while (!sh.queue.empty() && int(group.size()) < group_max_) {
+                    group.push_back(std::move(sh.queue.front()));
+                    sh.queue.pop_front();
                 }
             }
             auto t0 = std::chrono::steady_clock::now();
             try {
-                if (sync_ == SYNC_GROUP) {
+                if (sync_ == SYNC_GROUP && i == 0) {
                     std::lock_guard<std::mutex> jl(jmu_);
                     ::fdatasync(fd_);
                 }
                 auto t1 = std::chrono::steady_clock::now();
-                exec("BEGIN IMMEDIATE");
+                exec(sh.db, "BEGIN IMMEDIATE");
                 try {
-                    for (auto& b : group) apply_batch(*b.payload);
-                    exec("UPDATE upow_journal_state SET seq = " + std::to_string(group.back().seq) + " WHERE k = 0");
+                    for (auto& b : group) apply_batch(i, *b.payload);
+                    exec(sh.db, "UPDATE upow_journal_state SET seq = " + std::to_string(group.back().seq) + " WHERE k = 0");
                 } catch (...) {
-                    char* e = nullptr;
-                    api().exec(db_, "ROLLBACK", nullptr, nullptr, &e);
-                    if (e) api().free(e);
+                    rollback(sh.db);
                     throw;
                 }
                 auto t2 = std::chrono::steady_clock::now();
-                exec("COMMIT");
+                exec(sh.db, "COMMIT");
                 auto t3 = std::chrono::steady_clock::now();
                 {
                     std::lock_guard<std::mutex> lk(mu_);
-                    applied_ = group.back().seq;
-                    ++groups_;
-                    sync_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
-                    apply_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
-                    commit_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(t3 - t2).count();
+                    sh.applied = group.back().seq;
+                    ++sh.groups;
+                    sh.sync_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+                    sh.apply_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
+                    sh.commit_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(t3 - t2).count();
                 }
                 cv_done_.notify_all();
                 maybe_rotate();
@@ -824,68 +926,67 @@ class LedgerWriter {
                 {
                     std::lock_guard<std::mutex> lk(mu_);
                     failed_ = true;
-                    error_ = e.what();
+                    error_ = sh.path + ": " + e.what();
                 }
                 cv_done_.notify_all();
+                cv_.notify_all();
             }
         }
     }
 
-    std::string db_path_, journal_path_;
+    std::string journal_path_;
     int sync_;
     int group_max_;
     int64_t journal_max_;
-    sqlite3* db_ = nullptr;
-    std::unordered_map<std::string, sqlite3_stmt*> stmts_;  // materialiser thread only
+    std::vector<std::unique_ptr<Shard>> shards_;
     int fd_ = -1;
     off_t journal_size_ = 0;
     std::map<int64_t, std::pair<off_t, uint64_t>> meta_index_;  // block id -> (record offset, seq)
     std::mutex jmu_;  // journal file + meta index + next_seq_
     uint64_t next_seq_ = 1;
     int64_t bytes_written_ = 0;
-    std::mutex mu_;  // queue + watermark
+    std::mutex mu_;  // queues + watermarks + statistics
     std::condition_variable cv_, cv_done_;
-    std::deque<Batch> queue_;
-    uint64_t submitted_ = 0, applied_ = 0;
+    uint64_t submitted_ = 0;
     bool stop_ = false, closed_ = false, failed_ = false, paused_ = false;
     std::string error_;
-    int64_t groups_ = 0, replayed_ = 0, rotations_ = 0, mismatches_ = 0;
-    int64_t apply_ns_ = 0, commit_ns_ = 0, sync_ns_ = 0;
-    std::map<std::string, std::pair<int64_t, int64_t>> stmt_stats_;  // sql prefix -> (ns, rows); materialiser thread
-    std::thread thread_;
+    int64_t rotations_ = 0, mismatches_ = 0;
+    std::map<std::string, std::pair<int64_t, int64_t>> stmt_stats_;  // sql prefix -> (ns, rows)
 };
 
 }  // namespace
 
 void register_ledger_writer(py::module_& m) {
+    static const int memstatus_rc = sqlite_disable_memstatus();
+    m.attr("sqlite_memstatus_config_rc") = memstatus_rc;
     m.def("ledger_encode_stmt", &encode_stmt, py::arg("sql"), py::arg("cols"), py::arg("n"),
           py::arg("order") = py::none(), py::arg("guard") = py::none(), py::arg("expect") = py::none(),
-          "encode one column-major bulk statement for LedgerWriter.submit");
+          py::arg("shard") = 0, "encode one column-major bulk statement for LedgerWriter.submit");
     m.def("crc32c", [](py::buffer b) {
         py::buffer_info bi = b.request();
         return crc32c(0, bi.ptr, size_t(bi.size * bi.itemsize));
     });
     py::class_<LedgerWriter>(m, "LedgerWriter")
-        .def(py::init([](const std::string& db, const std::string& journal, int sync, int64_t cache_mb, int group_max,
-                         int64_t journal_max) {
+        .def(py::init([](std::vector<std::string> dbs, const std::string& journal, int sync, int64_t cache_mb,
+                         int group_max, int64_t journal_max) {
                  py::gil_scoped_release nogil;
-                 return new LedgerWriter(db, journal, sync, cache_mb, group_max, journal_max);
+                 return new LedgerWriter(dbs, journal, sync, cache_mb, group_max, journal_max);
              }),
-             py::arg("db_path"), py::arg("journal_path"), py::arg("sync_mode") = 1, py::arg("cache_mb") = 256,
+             py::arg("db_paths"), py::arg("journal_path"), py::arg("sync_mode") = 1, py::arg("cache_mb") = 256,
              py::arg("group_max") = 8, py::arg("journal_max_bytes") = int64_t(1) << 30)
         .def("submit",
              [](LedgerWriter& w, py::list stmts, py::bytes meta, int64_t block_id) {
-                 std::vector<std::string> s;
-                 s.reserve(stmts.size());
-                 for (auto x : stmts) s.push_back(x.cast<std::string>());
+                 std::vector<std::string> v;
+                 v.reserve(stmts.size());
+                 for (auto x : stmts) v.push_back(x.cast<std::string>());
                  std::string mt = meta;
                  py::gil_scoped_release nogil;
-                 return w.submit(s, mt, block_id);
+                 return w.submit(v, mt, block_id);
              },
              py::arg("stmts"), py::arg("meta") = py::bytes(""), py::arg("block_id") = -1)
-        .def("applied", &LedgerWriter::applied)
+        .def("applied", &LedgerWriter::applied, py::arg("shard") = -1)
         .def("set_paused", &LedgerWriter::set_paused)
-        .def("wait", &LedgerWriter::wait, py::arg("seq"), py::arg("timeout_s") = 0.0,
+        .def("wait", &LedgerWriter::wait, py::arg("seq"), py::arg("shard") = -1, py::arg("timeout_s") = 0.0,
              py::call_guard<py::gil_scoped_release>())
         .def("journal_meta", &LedgerWriter::journal_meta)
         .def("forget_blocks_from", &LedgerWriter::forget_blocks_from)

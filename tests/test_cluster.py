@@ -55,7 +55,8 @@ def test_cluster_node_replicates_and_shards(tmp_path, monkeypatch):
     (tmp_path / 'n').mkdir()
     _prefill(tmp_path / 'n' / 'ledger.sqlite3', 4)
     import shutil
-    shutil.copy(tmp_path / 'n' / 'ledger.sqlite3', tmp_path / 'wallet.sqlite3')  # the test's own view
+    from upow_amd.ledger.database import copy_ledger
+    copy_ledger(tmp_path / 'n' / 'ledger.sqlite3', tmp_path / 'wallet.sqlite3')  # the test's own view
     port, mport = _port(), _port()
     env = dict(os.environ, UPOW_DATA_DIR=str(tmp_path / 'n'), UPOW_CORE_URL='', UPOW_START_DIFFICULTY='1.0',
                UPOW_UTXO_BACKEND='host', UPOW_DISABLE_GPU='1', UPOW_RATE_LIMIT='0', PYTHONPATH=ROOT,

@@ -45,7 +45,8 @@ def test_fork_rollback_and_resync(tmp_path, monkeypatch):
     (tmp_path / 'b').mkdir()
     a_db, b_db = tmp_path / 'a' / 'ledger.sqlite3', tmp_path / 'b' / 'ledger.sqlite3'
     _build_chain(a_db, COMMON, 0x61, start)
-    shutil.copy(a_db, b_db)
+    from upow_amd.ledger.database import copy_ledger
+    copy_ledger(a_db, b_db)
     tip_a = _build_chain(a_db, A_EXTRA, 0x61, start)     # branch A: 523 blocks
     tip_b = _build_chain(b_db, B_EXTRA, 0x61, start + 7)  # branch B: 526 blocks (same genesis miner, other timestamps)
     assert tip_a['id'] == COMMON + A_EXTRA and tip_b['id'] == COMMON + B_EXTRA and tip_a['hash'] != tip_b['hash']

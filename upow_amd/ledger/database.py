@@ -63,12 +63,6 @@ CREATE TABLE IF NOT EXISTS transactions (
     outputs_amounts TEXT,
     fees TEXT NOT NULL
 );
-CREATE TABLE IF NOT EXISTS unspent_outputs (
-    tx_hash TEXT REFERENCES transactions(tx_hash) ON DELETE CASCADE,
-    "index" INTEGER NOT NULL,
-    address TEXT NULL,
-    is_stake INTEGER
-);
 CREATE TABLE IF NOT EXISTS pending_transactions (
     tx_hash TEXT UNIQUE,
     tx_hex TEXT,
@@ -97,9 +91,7 @@ CREATE TABLE IF NOT EXISTS {_t} (
     address TEXT NULL
 );"""
 SCHEMA += """
-CREATE INDEX IF NOT EXISTS tx_hash_idx ON unspent_outputs (tx_hash, "index");
 CREATE INDEX IF NOT EXISTS block_hash_idx ON transactions (block_hash);
-CREATE INDEX IF NOT EXISTS unspent_address_idx ON unspent_outputs (address);
 CREATE INDEX IF NOT EXISTS pending_spent_idx ON pending_spent_outputs (tx_hash, "index");
 CREATE INDEX IF NOT EXISTS address_transactions_idx ON address_transactions (address);
 CREATE INDEX IF NOT EXISTS address_transactions_tx_idx ON address_transactions (tx_hash);
@@ -107,6 +99,37 @@ CREATE INDEX IF NOT EXISTS address_transactions_tx_idx ON address_transactions (
 for _t in OUTPUT_TABLES[1:]:
     SCHEMA += f'CREATE INDEX IF NOT EXISTS {_t}_outpoint_idx ON {_t} (tx_hash, "index");\n'
     SCHEMA += f'CREATE INDEX IF NOT EXISTS {_t}_address_idx ON {_t} (address);\n'
+
+
+# The UTXO table lives in a database file of its own (``<ledger>-utxo``, attached as ``utxo``): the native
+# writer materialises it on its own thread in parallel with the block/tx tables. SQLite cannot declare a
+# foreign key across files, so the reference's ``tx_hash REFERENCES transactions(tx_hash) ON DELETE
+# CASCADE`` (schema.sql) is kept as a TEMP trigger on the Python connection (see Database.__init__).
+UTXO_SCHEMA = """
+CREATE TABLE IF NOT EXISTS utxo.unspent_outputs (
+    tx_hash TEXT,
+    "index" INTEGER NOT NULL,
+    address TEXT NULL,
+    is_stake INTEGER
+);
+CREATE INDEX IF NOT EXISTS utxo.tx_hash_idx ON unspent_outputs (tx_hash, "index");
+"""
+UTXO_CASCADE = ("CREATE TEMP TRIGGER IF NOT EXISTS upow_unspent_cascade AFTER DELETE ON main.transactions "
+                "BEGIN DELETE FROM unspent_outputs WHERE tx_hash = OLD.tx_hash; END")
+SHARD_OF_TABLE = {'unspent_outputs': 1}  # every other table is in the main file (shard 0)
+
+
+def ledger_files(path: str) -> List[str]:
+    """Every file of a (closed) file ledger: the main database, the UTXO database and the journal."""
+    return [path, path + '-utxo', path + '.journal']
+
+
+def copy_ledger(src: str, dst: str):
+    """Copy a closed file ledger (all of its files) to ``dst``."""
+    import shutil
+    for s, d in zip(ledger_files(str(src)), ledger_files(str(dst))):
+        if os.path.exists(s):
+            shutil.copy(s, d)
 
 
 def numeric(value, scale: int) -> str:
@@ -280,7 +303,7 @@ class Database:
         self.lock = threading.RLock()
         self.writer = None
         self._submitted = 0
-        self._applied_seen = 0
+        self._applied_seen: Dict[int, int] = {}  # shard (-1: all) -> applied sequence already observed
         self._table_seq: Dict[str, int] = {}
         self._tip_cache: Optional[dict] = None
         self._tip_gen = 0
@@ -302,6 +325,14 @@ class Database:
         if bg:
             self._start_checkpointer(float(os.environ.get('UPOW_WAL_CHECKPOINT_PERIOD', '0.5')))
         self._conn.executescript(SCHEMA)
+        self.utxo_file = self.file + '-utxo'
+        self._conn.execute('ATTACH DATABASE ? AS utxo', (self.utxo_file,))
+        self._conn.execute('PRAGMA utxo.journal_mode = WAL')
+        self._conn.execute('PRAGMA utxo.synchronous = ' + ('OFF' if path == ':memory:' else 'NORMAL'))
+        self._conn.execute(f'PRAGMA utxo.cache_size = -{cache_mb * 1024}')
+        self._conn.executescript(UTXO_SCHEMA)
+        self._migrate_single_file_utxo()
+        self._conn.execute(UTXO_CASCADE)
         if os.environ.get('UPOW_LEDGER_WRITER', '1') != '0':
             self._open_writer(cache_mb)
         store_dir = os.path.dirname(path) if path != ':memory:' else None
@@ -316,10 +347,24 @@ class Database:
                 self.utxo_source = 'snapshot'
         if self.utxo_source == 'sql':
             self._rebuild_utxo_index()
+        # spendable-output / balance queries answered by the UTXO index (K14) instead of SQL
+        self.address_queries_from_index = os.environ.get('UPOW_ADDRESS_SQL', '0') != '1'
         self.gov: Optional[GovernanceIndex] = None
         if os.environ.get('UPOW_GOV_INDEX', '1') != '0':
             self.gov = GovernanceIndex(self)
             self.gov.rebuild()
+
+    def _migrate_single_file_utxo(self):
+        """Ledgers written before the UTXO table got its own file keep ``unspent_outputs`` in the main
+        file: move the rows once (unqualified names would otherwise resolve to the main copy)."""
+        c = self._conn
+        if c.execute("SELECT 1 FROM main.sqlite_master WHERE type = 'table' AND name = 'unspent_outputs'").fetchone():
+            c.execute('BEGIN')
+            c.execute('INSERT INTO utxo.unspent_outputs (tx_hash, "index", address, is_stake) '
+                      'SELECT tx_hash, "index", address, is_stake FROM main.unspent_outputs ORDER BY rowid')
+            c.execute('DROP TABLE main.unspent_outputs')
+            c.execute('COMMIT')
+            logger.info('ledger: moved unspent_outputs into its own database file')
 
     def _open_writer(self, cache_mb: int):
         """The native writer owns its own connection to the same file. Opening it re-applies any
@@ -330,13 +375,14 @@ class Database:
             mode = 0
         journal = os.environ.get('UPOW_JOURNAL_PATH') or os.path.join(os.path.dirname(os.path.abspath(self.file)),
                                                                        os.path.basename(self.file) + '.journal')
-        self.writer = lib().LedgerWriter(self.file, journal, mode, cache_mb,
+        self.writer = lib().LedgerWriter([self.file, self.utxo_file], journal, mode, cache_mb,
                                          int(os.environ.get('UPOW_WRITER_GROUP', '8')),
                                          int(os.environ.get('UPOW_JOURNAL_MAX_MB', '1024')) << 20)
         self._eph['writer'] = self.writer if self.path == ':memory:' else None
         self.journal_path = journal
         st = self.writer.stats()
-        self._submitted = self._applied_seen = st['applied']
+        self._submitted = st['submitted']
+        self._applied_seen = {-1: st['applied']}
         if st['replayed']:
             logger.info(f'ledger journal: re-applied {st["replayed"]} committed batch(es) to the SQL tables')
 
@@ -377,6 +423,7 @@ class Database:
 
         def run(stop: threading.Event):
             conn = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
+            conn.execute('ATTACH DATABASE ? AS utxo', (path + '-utxo',))
             try:
                 while not stop.wait(period):
                     try:
@@ -410,18 +457,24 @@ class Database:
         if self.writer is None:
             return
         if tables is None:
-            target = self._submitted
+            waits = {-1: self._submitted}
         else:
             ts = self._table_seq
-            target = max((ts.get(t, 0) for t in tables), default=0)
-        if target <= self._applied_seen:
-            return
-        applied = self.writer.applied()
-        if applied < target:
-            self.writer.wait(target, float(os.environ.get('UPOW_WRITER_WAIT_TIMEOUT', '600')))
-            applied = max(applied, target)
-        if applied > self._applied_seen:
-            self._applied_seen = applied
+            waits = {}
+            for t in tables:
+                seq = ts.get(t, 0)
+                sh = SHARD_OF_TABLE.get(t, 0)
+                if seq > waits.get(sh, 0):
+                    waits[sh] = seq
+        seen = self._applied_seen
+        for sh, target in waits.items():
+            if target <= seen.get(sh, 0) or target <= seen.get(-1, 0):
+                continue
+            applied = self.writer.applied(sh)
+            if applied < target:
+                self.writer.wait(target, sh, float(os.environ.get('UPOW_WRITER_WAIT_TIMEOUT', '600')))
+                applied = target
+            seen[sh] = max(seen.get(sh, 0), applied)
 
     def flush(self):
         """Block until the SQL tables hold every committed block (tests, tools, shutdown)."""
@@ -489,7 +542,9 @@ class Database:
         csrc/ledger_writer.cpp: text lists, int64 arrays, ('gather'|'hex32'|'arena', ...) views of the
         block codec's buffers, or one constant for every row."""
         from ..ops.native import lib
-        return lib().ledger_encode_stmt(sql, cols, n, order, guard, expect)
+        tables = _tables_of(sql, False) or frozenset()
+        shard = max((SHARD_OF_TABLE.get(t, 0) for t in tables), default=0)
+        return lib().ledger_encode_stmt(sql, cols, n, order, guard, expect, shard)
 
     def bulk(self, sql: str, cols: list, n: int, order=None) -> int:
         """Column-major executemany on the Python connection (synchronous); returns the row changes."""
@@ -1498,8 +1553,31 @@ class Database:
             out.append((r['tx_hash'], r['idx'], _at(_arr(r['am']), r['idx'])))
         return out
 
+    def _index_address_rows(self, address: str, stake_sel: int, check_pending: bool) -> List[Tuple[str, int, int]]:
+        """(tx_hash, index, amount) of the live ``unspent_outputs`` entries owned by ``address`` (either byte
+        form), from the UTXO index (K14: one HBM scan per form on a GPU node, an owner map on the host)
+        in canonical (tx_hash, index) order. The reference's ``address = ANY($1)`` over unspent_outputs
+        (database.py:909-937) has no defined row order; the index answers at the commit point, without
+        waiting for the SQL materialiser and without an address B-tree to maintain per block."""
+        pend = (self.gov.pending_spent(True) if self.gov is not None else self._pending_spent_set()) \
+            if check_pending else set()
+        out = []
+        for h in codec.address_search_hex(address):
+            recs, pay, _ = self.utxo.address_outputs(bytes.fromhex(h), (TAG_BY_TABLE['unspent_outputs'],), stake_sel)
+            idx = recs[:, 32:36].copy().view('<u4').ravel()
+            for k in range(len(recs)):
+                key = (bytes(recs[k, :32]).hex(), int(idx[k]))
+                if key not in pend:
+                    out.append((key[0], key[1], int(pay['amount'][k])))
+        out.sort(key=lambda r: (r[0], r[1]))
+        return out
+
     async def get_spendable_outputs(self, address: str, check_pending_txs: bool = False) -> List[TransactionInput]:
         point = string_to_point(address)
+        if self.address_queries_from_index:
+            from .utxo import STAKE_EXCLUDE
+            return [TransactionInput(h, i, amount=Decimal(a) / SMALLEST, public_key=point)
+                    for h, i, a in self._index_address_rows(address, STAKE_EXCLUDE, check_pending_txs)]
         forms = list(reversed(self._forms(address)))
         if self._q1('SELECT tx_hash FROM unspent_outputs WHERE address IS NULL LIMIT 1') is not None:
             await self.set_unspent_outputs_addresses()
@@ -1809,12 +1887,26 @@ class Database:
         point = string_to_point(address)
         forms = self._forms(address)
         ph = ','.join('?' * len(forms))
-        rows = self._q(f'SELECT unspent_outputs.tx_hash AS h, unspent_outputs."index" AS idx, transactions.outputs_amounts AS am '
-                       f'FROM unspent_outputs INNER JOIN transactions ON (transactions.tx_hash = unspent_outputs.tx_hash) '
-                       f'INNER JOIN blocks ON (blocks.hash = transactions.block_hash) WHERE unspent_outputs.address IN ({ph}) '
-                       f'AND blocks.id >= ? ORDER BY unspent_outputs.rowid', (*forms, block_no))
-        unspent = [TransactionInput(r['h'], r['idx'], amount=Decimal(_at(_arr(r['am']), r['idx'])) / SMALLEST,
-                                    public_key=point) for r in rows]
+        if self.address_queries_from_index:
+            from .utxo import STAKE_ANY
+            hits = self._index_address_rows(address, STAKE_ANY, False)
+            recent = set()
+            hashes = sorted({h for h, _, _ in hits})
+            for k in range(0, len(hashes), 500):
+                chunk = hashes[k:k + 500]
+                recent.update(r[0] for r in self._q(
+                    f'SELECT t.tx_hash FROM transactions t INNER JOIN blocks b ON b.hash = t.block_hash '
+                    f'WHERE t.tx_hash IN ({",".join("?" * len(chunk))}) AND b.id >= ?', (*chunk, block_no)))
+            unspent = [TransactionInput(h, i, amount=Decimal(a) / SMALLEST, public_key=point)
+                       for h, i, a in hits if h in recent]
+        else:
+            rows = self._q(f'SELECT unspent_outputs.tx_hash AS h, unspent_outputs."index" AS idx, '
+                           f'transactions.outputs_amounts AS am FROM unspent_outputs INNER JOIN transactions ON '
+                           f'(transactions.tx_hash = unspent_outputs.tx_hash) INNER JOIN blocks ON '
+                           f'(blocks.hash = transactions.block_hash) WHERE unspent_outputs.address IN ({ph}) '
+                           f'AND blocks.id >= ? ORDER BY unspent_outputs.rowid', (*forms, block_no))
+            unspent = [TransactionInput(r['h'], r['idx'], amount=Decimal(_at(_arr(r['am']), r['idx'])) / SMALLEST,
+                                        public_key=point) for r in rows]
         srows = self._q('SELECT transactions.tx_hex AS tx_hex, transactions.inputs_addresses AS ia FROM transactions '
                         'INNER JOIN blocks ON (transactions.block_hash = blocks.hash) WHERE blocks.id >= ? '
                         'ORDER BY transactions.rowid', (block_no,))

@@ -90,9 +90,10 @@ class _HostBackend:
     def __init__(self):
         self.d: Dict[Outpoint, int] = {}
         self.p: Dict[Outpoint, bytes] = {}  # raw 80-byte payloads
+        self.by_addr: Dict[bytes, Dict[Outpoint, None]] = {}  # owner address bytes -> outpoints (K14 on the host)
 
     def reset(self, keys, tags, payload=None):
-        self.d, self.p = {}, {}
+        self.d, self.p, self.by_addr = {}, {}, {}
         self.insert(keys, tags, payload)
 
     def insert(self, keys, tags, payload=None) -> int:
@@ -105,7 +106,10 @@ class _HostBackend:
                 dups += 1
                 continue
             self.d[k] = int(t)
-            self.p[k] = raw[80 * n:80 * n + 80] if raw is not None else bytes(80)
+            p = self.p[k] = raw[80 * n:80 * n + 80] if raw is not None else bytes(80)
+            a = self._addr(p)
+            if a:
+                self.by_addr.setdefault(a, {})[k] = None
         return dups
 
     def probe(self, keys) -> np.ndarray:
@@ -124,7 +128,12 @@ class _HostBackend:
             t = self.d.get(k)
             if t is not None and (tag is None or t == tag):
                 del self.d[k]
-                self.p.pop(k, None)
+                a = self._addr(self.p.pop(k, None))
+                owned = self.by_addr.get(a)
+                if owned is not None:
+                    owned.pop(k, None)
+                    if not owned:
+                        del self.by_addr[a]
                 out[n] = 1
         return out
 
@@ -137,8 +146,7 @@ class _HostBackend:
                 return True
             st = t == 0 and bool(int.from_bytes(self.p.get(k, bytes(80))[12:16], 'little') & FLAG_STAKE)
             return st == (stake_sel == STAKE_ONLY)
-        hits = [k for k, t in self.d.items() if (tag_mask >> t) & 1 and self._addr(self.p.get(k)) == addr
-                and stake_ok(k, t)]
+        hits = [k for k in self.by_addr.get(bytes(addr), ()) if (tag_mask >> self.d[k]) & 1 and stake_ok(k, self.d[k])]
         pay = np.frombuffer(b''.join(self.p[k] for k in hits), dtype=PAYLOAD_DTYPE)
         return pack_records(hits, [self.d[k] for k in hits]), pay
 
