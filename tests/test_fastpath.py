@@ -135,9 +135,13 @@ def test_fast_path_matches_object_path(backend, journal, request):
     asyncio.run(go())
 
 
-def test_rejections_match():
+@pytest.mark.parametrize('backend', ['host', pytest.param('gpu', marks=pytest.mark.gpu)])
+def test_rejections_match(backend, request):
+    if backend == 'gpu':
+        request.getfixturevalue('gpu')
+
     async def go():
-        p, base = await _setup()
+        p, base = await _setup(backend)
         ts = base + 60 * 10
         p.use(p.a)
         good = await create_transaction(GENESIS, address_of(KEYS[0]), '3')
@@ -273,15 +277,20 @@ def test_ascii_hex_signature_fallback_matches():
     asyncio.run(go())
 
 
-@pytest.mark.parametrize('seed', [1, 2, 3])
-def test_random_blocks_differential(seed):
+@pytest.mark.parametrize('seed,backend', [(1, 'host'), (2, 'host'), (3, 'host'),
+                                          pytest.param(4, 'gpu', marks=pytest.mark.gpu),
+                                          pytest.param(5, 'gpu', marks=pytest.mark.gpu)])
+def test_random_blocks_differential(seed, backend, request):
     """Randomised blocks built from the live UTXO set, each carrying one randomly chosen fault (or
     none): both paths must return the same verdict and error and leave identical ledgers (Pair.push
-    compares every table, the UTXO index with payloads and the UTXO-set hash)."""
+    compares every table, the UTXO index with payloads and the UTXO-set hash). The gpu cases run both
+    ledgers on the HBM table and the gfx950 verify/decompress kernels."""
+    if backend == 'gpu':
+        request.getfixturevalue('gpu')
     rng = random.Random(seed)
 
     async def go():
-        p, base = await _setup()
+        p, base = await _setup(backend)
         ts = base + 60 * 10
         keys = [GENESIS] + KEYS
         # fan the genesis coinbases out to the test keys first (several small outputs each)
