@@ -160,3 +160,50 @@ def test_websocket_protocol(node):
             ws.receive_json()
         assert exc.value.code == 1000
     assert main.websocket_router is not None
+
+
+@pytest.mark.parametrize('ledger_thread', ['1', '0'])
+def test_block_apply_does_not_block_the_http_loop(tmp_path, monkeypatch, ledger_thread):
+    """While a block is validated/applied (here: held for 1.2 s on the ledger thread), other requests
+    are served by the HTTP loop (ledger/worker.py). With UPOW_LEDGER_THREAD=0 the same request waits
+    for the block — the reference's behaviour (main.py:521-652 on the single asyncio loop)."""
+    import threading
+    import time
+    monkeypatch.setenv('UPOW_LEDGER_THREAD', ledger_thread)
+    monkeypatch.setenv('UPOW_DATA_DIR', str(tmp_path))
+    monkeypatch.setenv('UPOW_CORE_URL', '')
+    monkeypatch.setenv('UPOW_DATABASE_PATH', str(tmp_path / 'ledger.sqlite3'))
+    monkeypatch.setenv('UPOW_UTXO_BACKEND', 'host')
+    from upow_amd.ledger import fastpath, manager
+    monkeypatch.setattr(manager, 'START_DIFFICULTY', Decimal('1.5'))
+    manager.Manager.difficulty = None
+    from upow_amd.node import main
+    from upow_amd.node.nodes_manager import NodesManager
+    from upow_amd.wallet.builders import address_of
+    NodesManager.path = None
+    main.limiter.reset()
+    inner = fastpath._create_block_from_hex
+    ledger_threads = []
+
+    async def slow(*a, **kw):
+        ledger_threads.append(threading.current_thread().name)
+        time.sleep(1.2)  # a long block: blocks whichever event loop runs it
+        return await inner(*a, **kw)
+    monkeypatch.setattr(fastpath, '_create_block_from_hex', slow)
+    from starlette.testclient import TestClient
+    with TestClient(main.app, base_url='http://testserver') as client:
+        result = {}
+        t = threading.Thread(target=lambda: result.setdefault('block', _mine(client, address_of(KEY_A), 1_700_000_001)))
+        t.start()
+        while not ledger_threads:
+            time.sleep(0.01)
+        t0 = time.perf_counter()
+        assert client.get('/get_nodes').json()['ok']
+        latency = time.perf_counter() - t0
+        t.join()
+        assert result['block'] == {'ok': True}
+    main.db.close()
+    if ledger_thread == '1':
+        assert ledger_threads == ['upow-ledger'] and latency < 0.6, latency
+    else:
+        assert ledger_threads != ['upow-ledger'] and latency > 0.5, latency

@@ -565,10 +565,13 @@ class Database:
             self.fk = foreign_keys
 
         def __enter__(self):
-            if self.db._tx_depth == 0:
-                self.db._settle(None)
             self.db.lock.acquire()
             if self.db._tx_depth == 0:
+                try:  # no SQL transaction is open on this connection: safe to wait for the writer
+                    self.db._settle(None)
+                except BaseException:
+                    self.db.lock.release()
+                    raise
                 c = self.db._conn
                 if not self.fk:  # only settable outside a transaction
                     c.execute('PRAGMA foreign_keys = OFF')

@@ -20,6 +20,8 @@ pending tx parsed once.
 """
 from __future__ import annotations
 
+import functools
+import threading
 from decimal import Decimal
 from typing import Dict, Iterable, List, Optional, Set, Tuple
 
@@ -78,9 +80,19 @@ class _Table:
         return sorted(found, key=pos.__getitem__)
 
 
+def _locked(fn):
+    """Serialise index access: block application (ledger thread) and API queries (HTTP loop) share it."""
+    @functools.wraps(fn)
+    def wrapper(self, *args, **kwargs):
+        with self.lock:
+            return fn(self, *args, **kwargs)
+    return wrapper
+
+
 class GovernanceIndex:
     def __init__(self, db):
         self.db = db
+        self.lock = threading.RLock()
         self.tables: Dict[str, _Table] = {t: _Table() for t in (*GOV_TABLES, STAKE)}
         self.version = 0
         self._memo: dict = {}
@@ -110,12 +122,14 @@ class GovernanceIndex:
             voter = _at(json.loads(ia) if ia else [], int(i))
             tab.add(key, address, amount, voter, ts)
 
+    @_locked
     def rebuild(self):
         for t in self.tables:
             self.tables[t] = _Table()
             self._add_sql_rows(t, self._rows_sql(t))
         self.version += 1
 
+    @_locked
     def added(self, table: str, keys: List[Key]):
         """Rows just inserted into ``table`` (or staked outputs into unspent_outputs): mirror them
         with the same joins the reference's queries use."""
@@ -129,6 +143,7 @@ class GovernanceIndex:
                                                      tuple(chunk)), want)
         self.version += 1
 
+    @_locked
     def removed(self, table: str, keys: Iterable[Key]):
         tab = self.tables[table]
         hit = False
@@ -137,10 +152,12 @@ class GovernanceIndex:
         if hit:
             self.version += 1
 
+    @_locked
     def stake_keys(self) -> Dict[Key, tuple]:
-        return self.tables[STAKE].rows
+        return dict(self.tables[STAKE].rows)
 
     # ------------------------------------------------------------------ mempool overlay
+    @_locked
     def _overlay(self):
         ver = self.db._mempool_ver
         if self._pending is not None and self._pending[0] == ver:
@@ -161,16 +178,19 @@ class GovernanceIndex:
         self._pending = (ver, spent, stake)
         return self._pending
 
+    @_locked
     def pending_spent(self, check_pending: bool) -> Set[Key]:
         return self._overlay()[1] if check_pending else set()
 
     # ------------------------------------------------------------------ queries (reference semantics)
+    @_locked
     def amount_rows(self, table: str, forms: List[str], check_pending: bool) -> List[Tuple[str, int, object]]:
         """``_amount_rows``: (tx_hash, index, amount) of rows whose address is in ``forms``, rowid order."""
         tab = self.tables[table]
         pend = self.pending_spent(check_pending)
         return [(h, i, tab.rows[(h, i)][1]) for h, i in tab.keys_for(tab.by_addr, forms) if (h, i) not in pend]
 
+    @_locked
     def ballot_rows(self, table: str, receiver_forms: Optional[List[str]], check_pending: bool,
                     voter_forms: Optional[Set[str]] = None, order: bool = True):
         """``_ballot_rows``: (tx_hash, receiver, vote, voter, index), ordered by (tx_hash, rowid) or rowid."""
@@ -189,16 +209,19 @@ class GovernanceIndex:
             out.append((k[0], address, Decimal(amount) / SMALLEST if amount is not None else None, voter, k[1]))
         return out
 
+    @_locked
     def spent_votes(self, table: str, voter_forms: Set[str], check_pending: bool):
         tab = self.tables[table]
         pend = self.pending_spent(check_pending)
         return [(k, tab.rows[k][1]) for k in tab.keys_for(tab.by_voter, voter_forms) if k not in pend]
 
+    @_locked
     def registered_inodes(self, check_pending: bool):
         tab = self.tables['inode_registration_output']
         pend = self.pending_spent(check_pending)
         return [(row[0], row[3]) for k, row in tab.rows.items() if k not in pend and row[3] is not None]
 
+    @_locked
     def address_stake(self, forms: List[str], check_pending: bool) -> Decimal:
         stake = sum((Decimal(a) / SMALLEST for _, _, a in self.amount_rows(STAKE, forms, check_pending)), Decimal(0))
         if check_pending:
@@ -216,6 +239,7 @@ class GovernanceIndex:
             hit = self._memo[key] = fn()
         return hit
 
+    @_locked
     def validators_stake(self, forms: List[str], check_pending: bool) -> Decimal:
         """get_validators_stake (database.py:1127-1136): sum of vote x delegate stake / 10 over the
         validator's delegate ballots."""
@@ -230,6 +254,7 @@ class GovernanceIndex:
             return compute()
         return self._memo_get(('vstake', tuple(forms)), compute)
 
+    @_locked
     def inode_power(self, forms: List[str], check_pending: bool) -> Decimal:
         """get_inode_vote_ratio_by_address (database.py:1390-1418)."""
         from ..utils.codec import address_forms
@@ -243,6 +268,7 @@ class GovernanceIndex:
             return compute()
         return self._memo_get(('ipower', tuple(forms)), compute)
 
+    @_locked
     def inodes_with_power(self, check_pending: bool):
         """get_all_registered_inode_with_vote: [(wallet, power, registration timestamp)]."""
         from ..utils.codec import address_forms

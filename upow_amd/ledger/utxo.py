@@ -273,8 +273,21 @@ def default_backend() -> str:
         return 'host'
 
 
+def _locked(fn):
+    """One index, two threads (ledger worker + HTTP loop): every backend operation under one lock."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapper(self, *args, **kwargs):
+        with self.lock:
+            return fn(self, *args, **kwargs)
+    return wrapper
+
+
 class UtxoIndex:
     def __init__(self, backend: Optional[str] = None):
+        import threading
+        self.lock = threading.RLock()
         self.backend_name = backend or default_backend()
         self.be = _GpuBackend() if self.backend_name == 'gpu' else _HostBackend()
         self.duplicates = 0  # inserts of an outpoint that was already live (skipped; a ledger bug if ever > 0)
@@ -285,14 +298,17 @@ class UtxoIndex:
             import logging
             logging.getLogger('upow').error(f'UTXO index: {n} insert(s) of an already live outpoint skipped')
 
+    @_locked
     def reset(self, keys: Sequence[Outpoint], tags: Sequence[int], payload: Optional[np.ndarray] = None):
         self.be.reset(list(keys), list(tags), payload)
 
+    @_locked
     def insert(self, keys: Sequence[Outpoint], tag, payload: Optional[np.ndarray] = None):
         keys = list(keys)
         tags = [tag] * len(keys) if isinstance(tag, int) else list(tag)
         self._dups(self.be.insert(keys, tags, payload))
 
+    @_locked
     def insert_records(self, recs: np.ndarray, payload: Optional[np.ndarray] = None):
         """Insert packed 40-byte key records (tags inside) — the block fast path's form."""
         if isinstance(self.be, _GpuBackend):
@@ -303,16 +319,19 @@ class UtxoIndex:
         keys = [(bytes(recs[n, :32]).hex(), int(idx[n])) for n in range(len(recs))]
         self._dups(self.be.insert(keys, [int(t) for t in tags], payload))
 
+    @_locked
     def lookup(self, keys: Sequence[Outpoint]):
         """(tags uint8[n], payload PAYLOAD_DTYPE[n]) for each outpoint (tag 0xff / len 0 when absent)."""
         return self.be.lookup(list(keys))
 
+    @_locked
     def lookup_records(self, recs: np.ndarray):
         if isinstance(self.be, _GpuBackend):
             return self.be.lookup_records(recs)
         idx = recs[:, 32:36].copy().view(np.uint32).ravel()
         return self.be.lookup([(bytes(recs[n, :32]).hex(), int(idx[n])) for n in range(len(recs))])
 
+    @_locked
     def erase_records(self, recs: np.ndarray) -> np.ndarray:
         if isinstance(self.be, _GpuBackend):
             if not len(recs):
@@ -329,12 +348,15 @@ class UtxoIndex:
         return self.be.erase([(bytes(recs[n, :32]).hex(), int(idx[n])) for n in range(len(recs))],
                              None if tag == MISSING else tag)
 
+    @_locked
     def probe(self, keys: Sequence[Outpoint]) -> np.ndarray:
         return self.be.probe(list(keys))
 
+    @_locked
     def erase(self, keys: Sequence[Outpoint], tag: Optional[int] = None) -> np.ndarray:
         return self.be.erase(list(keys), tag)
 
+    @_locked
     def filter(self, outputs: Iterable[Outpoint], tag: int) -> List[Outpoint]:
         """Outpoints of ``outputs`` present in table ``tag`` (unique, in first-seen order)."""
         uniq = list(dict.fromkeys((h, int(i)) for h, i in outputs))
@@ -343,10 +365,12 @@ class UtxoIndex:
         t = self.probe(uniq)
         return [k for k, v in zip(uniq, t) if v == tag]
 
+    @_locked
     def records(self) -> np.ndarray:
         """All live entries as 40-byte records, in canonical (txid, index) order."""
         return sort_records(np.ascontiguousarray(self.be.records()))
 
+    @_locked
     def address_outputs(self, addr: bytes, tags: Iterable[int] = (0,), stake_sel: int = STAKE_ANY):
         """K14 (reference ``database.py:909-937,1138-1205``): the live outpoints whose payload address is
         ``addr`` (raw 33/64 bytes, prefix normalised as stored) in the given tables, as (records, payloads)
@@ -360,12 +384,14 @@ class UtxoIndex:
         recs, pay = np.ascontiguousarray(recs[order]), np.ascontiguousarray(pay[order])
         return recs, pay, int(pay['amount'].sum()) if len(pay) else 0
 
+    @_locked
     def records_payload(self):
         """(records, payloads) of every live entry, in canonical (txid, index) order."""
         recs, pay = self.be.records_payload()
         order = sort_order(np.ascontiguousarray(recs))
         return np.ascontiguousarray(recs[order]), np.ascontiguousarray(pay[order])
 
+    @_locked
     def reset_records(self, recs: np.ndarray, payload: Optional[np.ndarray] = None):
         """Replace the whole index with packed records (snapshot restore: one H2D copy + insert launch)."""
         recs = np.ascontiguousarray(recs, dtype=np.uint8).reshape(-1, 40)
@@ -379,6 +405,7 @@ class UtxoIndex:
             keys = [(bytes(recs[n, :32]).hex(), int(idx[n])) for n in range(len(recs))]
             self.be.reset(keys, [int(t) for t in tags], payload)
 
+    @_locked
     def block_inputs(self, in_keys: np.ndarray, in_start: np.ndarray, out_amount: np.ndarray,
                      out_start: np.ndarray, want_tag: int = 0):
         """One pass over a block's inputs: K7 lookup (tag + payload), K10 duplicate detection and K11
@@ -416,6 +443,7 @@ class UtxoIndex:
         miss = seg_sum(bad, in_start).astype(np.uint32)
         return tags, pay, dup_of, ins - outs, miss, int((dup_of > 0).sum())
 
+    @_locked
     def set_hash(self, tag: int = 0) -> str:
         """K12 from the index: SHA-256 over (txid || index byte) of table ``tag`` sorted by (txid, index)
         — byte-identical to ``Database.get_unspent_outputs_hash`` (reference database.py:827-830).

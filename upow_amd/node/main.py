@@ -35,6 +35,8 @@ from ..ledger import manager as mgr
 from ..ledger.database import Database, UniqueViolationError
 from ..ledger import fastpath
 from ..ledger.fastpath import create_block_from_hex
+from ..ledger import worker as ledger_worker
+from ..ledger.worker import on_ledger
 from ..ops.native import lib
 from ..parallel import cluster
 from ..ledger.manager import (Manager, block_to_bytes, calculate_difficulty, clear_pending_transactions, create_block,
@@ -73,6 +75,7 @@ async def lifespan(app: FastAPI):
         yield
     finally:
         indexer.cancel()
+        ledger_worker.stop()
         cluster.leader_quit()
         await shutdown_websocket_manager()
         if db is not None and db.path != ':memory:' and os.environ.get('UPOW_SNAPSHOT', '1') != '0':
@@ -103,6 +106,8 @@ async def startup():
     db = await Database.create(path=path)
     if cluster.get() is not None:  # multi-GPU node: bring the follower replicas to our tip
         await cluster.leader_replay(db)
+    # block validation/apply (and every cluster collective) from here on runs on the ledger thread
+    ledger_worker.start()
     await start_websocket_manager()
 
 
@@ -194,6 +199,20 @@ async def create_blocks(blocks: list, error_list=None) -> bool:
     return True
 
 
+async def _locked(fn, *args):
+    """``fn(*args)`` under the ledger lock (called on the ledger thread, where the lock lives)."""
+    async with ledger_lock():
+        return await fn(*args)
+
+
+async def _on_ledger_sync(fn, *args):
+    """A synchronous cluster call made from the ledger thread: every collective of a multi-GPU node is
+    issued by that one thread, so ranks see them in one order."""
+    async def call():
+        return fn(*args)
+    return await on_ledger(call)
+
+
 async def _sync_blockchain(node_url: str = None):
     """main.py:153-227: pull pages of 1000 blocks; on a fork (height > 500) roll back to the last
     common block among the last 500 and re-apply; on failure restore the cached local chain."""
@@ -225,8 +244,7 @@ async def _sync_blockchain(node_url: str = None):
                     last_common_block = local_block['block']['id']
                     local_cache = local_blocks[:n]
                     local_cache.reverse()
-                    async with ledger_lock():
-                        await cluster.mirror_rollback(db, last_common_block + 1)
+                    await on_ledger(_locked, cluster.mirror_rollback, db, last_common_block + 1)
                     break
     limit = 1000
     prefetch = None  # (offset, task): the next page, fetched over HTTP while this one is applied
@@ -265,15 +283,14 @@ async def _sync_blockchain(node_url: str = None):
                 return True
             nxt = i + len(blocks)
             prefetch = (nxt, asyncio.ensure_future(node_interface.get_blocks(nxt, limit)))
-            assert await create_blocks(blocks, error_list=error)
+            assert await on_ledger(create_blocks, blocks, error_list=error)
         except Exception as e:
             drop_prefetch()
             logger.error(error[0] if error else e)
             if local_cache is not None:
                 logger.info('sync failed, reverting back to previous chain')
-                async with ledger_lock():
-                    await cluster.mirror_delete(db, last_common_block)
-                await create_blocks(local_cache)
+                await on_ledger(_locked, cluster.mirror_delete, db, last_common_block)
+                await on_ledger(create_blocks, local_cache)
             return error[0] if error else e
 
 
@@ -402,7 +419,8 @@ async def verify_and_push_tx(tx: Transaction, request: Request, background_tasks
         if sender in BANNED_SENDERS:
             return JSONResponse(status_code=403, content={'ok': False, 'error': 'Access forbidden temporarily.'})
         if await db.add_pending_transaction(tx):
-            cluster.mirror_tx(tx.hex())
+            if cluster.get() is not None:
+                await _on_ledger_sync(cluster.mirror_tx, tx.hex())
             if 'Sender-Node' in request.headers:
                 NodesManager.update_last_message(request.headers['Sender-Node'])
             background_tasks.add_task(propagate, 'push_tx', {'tx_hex': tx.hex()})
@@ -518,7 +536,7 @@ async def push_block(request: Request, background_tasks: BackgroundTasks, block_
             return {'ok': False, 'error': 'Transaction hash not found'}
         final_hexes.extend(pending_hexes)
     error_list = []
-    if not await create_block_from_hex(block_content, final_hexes, error_list=error_list):
+    if not await on_ledger(create_block_from_hex, block_content, final_hexes, error_list=error_list):
         return {'ok': False, 'error': error_list[0]} if error_list else {'ok': False}
     block_hash = sha256(block_content)
     Manager.difficulty = None
@@ -526,7 +544,7 @@ async def push_block(request: Request, background_tasks: BackgroundTasks, block_
     pending = sorted(await db.get_pending_transactions_limit(hex_only=True))
     if LAST_PENDING_TRANSACTIONS_CLEAN[0] < timestamp() - 600:
         LAST_PENDING_TRANSACTIONS_CLEAN[0] = timestamp()
-        background_tasks.add_task(cluster.mirror_gc, pending)
+        background_tasks.add_task(on_ledger, cluster.mirror_gc, pending)
     block_data = {'block_no': block_no, 'block_hash': block_hash, 'transactions_count': len(final_hexes),
                   'timestamp': timestamp(), 'difficulty': difficulty, 'last_block': last_block,
                   'pending_transactions': pending[:10], 'pending_transactions_hashes': [sha256(t) for t in pending],
@@ -564,7 +582,7 @@ async def get_mining_info(request: Request, background_tasks: BackgroundTasks):
     pending = sorted(await db.get_pending_transactions_limit(hex_only=True))
     if LAST_PENDING_TRANSACTIONS_CLEAN[0] < timestamp() - 600:
         LAST_PENDING_TRANSACTIONS_CLEAN[0] = timestamp()
-        background_tasks.add_task(cluster.mirror_gc, pending)
+        background_tasks.add_task(on_ledger, cluster.mirror_gc, pending)
     return {'ok': True, 'result': {
         'difficulty': difficulty, 'last_block': last_block, 'pending_transactions': pending[:10],
         'pending_transactions_hashes': [sha256(t) for t in pending],
