@@ -60,11 +60,22 @@ double run(const char* name, int blocks_per_cu, int cus, unsigned* d, double ghz
     return per_s;
 }
 
-int main() {
+int main(int argc, char** argv) {
     int cus = 0;
     CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     unsigned* d;
     CHK(hipMalloc(&d, sizeof(unsigned) * cus * 8 * 256));
+    if (argc > 1 && argv[1][0] == 'c') {
+        // PMC calibration: ONE launch with a known VALU count (16 x 8 v_add_u32 per loop iteration plus
+        // the loop's own VALU overhead, see the ISA), to read rocprofv3's SQ_INSTS_VALU / SQ_WAVES scale
+        // against (docs/PERF.md §1).
+        const int grid = cus * 4, iters = 1000;
+        hipLaunchKernelGGL(k<0>, dim3(grid), dim3(256), 0, 0, d, 1u, iters);
+        CHK(hipDeviceSynchronize());
+        printf("calib: waves=%d  v_add_u32 per wave=%d  (expected SQ_INSTS_VALU >= %.4e, SQ_WAVES = %d)\n",
+               grid * 4, iters * 128, double(grid) * 4 * iters * 128, grid * 4);
+        return 0;
+    }
     const double ghz = 2.1;
     for (int bpc : {4, 8}) {
         run<0>("v_add_u32", bpc, cus, d, ghz);
