@@ -12,8 +12,12 @@ Weak scaling: per-GPU work (2^32 nonces/step) is fixed as N grows; ``value`` is 
 of all N GPUs. ``vs_baseline`` divides by BASELINE.md's 0.99 MH/s (the reference miner.py inner loop,
 one process, measured in the survey sandbox — the reference publishes no number).
 
-``--mode verify`` measures the second BASELINE metric instead (tx-verify/s on a synthetic 2 MB block);
-``--mode sync`` the chain-sync throughput of the same blocks replayed from a ``/get_blocks`` page.
+The default (mine) run then also measures the second BASELINE metric in the same process on every
+rank — tx-verify/s over 2 MB blocks (8,300 signed txs each) through the native push_block path into a
+file-backed ledger — and reports it as extra keys (``verify_tx_per_s`` aggregated over ranks,
+``ecdsa_sig_per_s``, per-block commit latency); ``--verify-steps 0`` skips it.
+``--mode verify`` runs that measurement alone (default 10 blocks); ``--mode sync`` the chain-sync
+throughput of the same blocks replayed from a ``/get_blocks`` page.
 """
 from __future__ import annotations
 
@@ -102,6 +106,28 @@ def bench_verify(args, ctx):
     return run_verify_bench(args, ctx)
 
 
+def _verify_side_metrics(args, ctx) -> dict:
+    """BASELINE metric 2 next to the hashrate: ``steps`` timed 2 MB blocks (+1 warmup) through the
+    native push_block path on this rank's GPU, file-backed ledger in a temporary directory."""
+    import shutil
+    import tempfile
+    from upow_amd.bench_verify import run_verify_bench
+    tmp = tempfile.mkdtemp(prefix='upow_bench_verify_')
+    try:
+        v = argparse.Namespace(**{**vars(args), 'steps': args.verify_steps, 'warmup': 1, 'ledger': tmp,
+                                  'object_path': False, 'from_mempool': False})
+        r = run_verify_bench(v, ctx)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return {'verify_tx_per_s': r['value'], 'verify_ms_per_block': r['ms_per_step'],
+            'verify_commit_latency_ms': r['commit_latency_ms'], 'validate_tx_per_s': r['validate_tx_per_s'],
+            'ecdsa_sig_per_s': r['ecdsa_sig_per_s'],
+            'verify_config': {'metric': r['metric'], 'unit': r['unit'], 'steps': args.verify_steps, 'warmup': 1,
+                              'txs_per_block': r['config']['seq_len'], 'ledger': r['config']['ledger'],
+                              'block_path': r['config']['block_path'], 'scaling': 'weak',
+                              'data': r['data']}}
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -116,6 +142,8 @@ def main(argv=None):
     ap.add_argument('--ledger', default=None, help='verify mode: directory for a file-backed (WAL) ledger')
     ap.add_argument('--from-mempool', action='store_true',
                     help='verify mode: block txs are in the mempool and pushed as hashes (the miner path)')
+    ap.add_argument('--verify-steps', type=int, default=4,
+                    help='mine mode: timed 2 MB blocks of the tx-verify side measurement (0: skip; GPU only)')
     args = ap.parse_args(argv)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -126,6 +154,8 @@ def main(argv=None):
     try:
         if args.mode == 'mine':
             out = bench_mine(args, ctx)
+            if args.verify_steps > 0 and out['config']['device'] == 'gpu':
+                out.update(_verify_side_metrics(args, ctx))
         elif args.mode == 'verify':
             out = bench_verify(args, ctx)
         else:
