@@ -4,8 +4,9 @@
 // hipMalloc + hipFree per call cost ~0.1-0.3 ms each, and hipFree synchronises the device. One 2 MB
 // block makes a dozen such calls, and the ECDSA launch itself takes only ~3 ms. Buffers here are
 // rounded up to a power-of-two size class and parked on a per-device free list when released, so
-// the steady state makes no driver allocations at all. Reuse is safe because every native launch
-// and copy goes to the null stream: a later call's H2D copy into a recycled buffer is ordered after
+// the steady state makes no driver allocations at all. Reuse is safe because every node-side launch
+// and copy goes to the device's node stream (csrc/streams.h) and each call synchronises that stream
+// before its buffers are released: a later call's H2D copy into a recycled buffer is ordered after
 // the earlier kernels that used it. Memory is never returned to the driver; the high-water mark is
 // bounded by the largest batch (a few tens of MB per device).
 #pragma once

@@ -27,6 +27,7 @@
 
 #include "dev_pool.h"
 #include "native.h"
+#include "streams.h"
 #include "p256_field.h"
 #include "sha256_common.h"
 
@@ -250,7 +251,8 @@ static const aff* device_g_table() {
     if (!t.d_tab) {
         const auto& h = g_table();
         hck(hipMalloc(&t.d_tab, sizeof(aff) * h.size()), "hipMalloc gtab");
-        hck(hipMemcpy(t.d_tab, h.data(), sizeof(aff) * h.size(), hipMemcpyHostToDevice), "h2d gtab");
+        node_h2d(t.d_tab, h.data(), sizeof(aff) * h.size(), "h2d gtab");
+        node_sync("gtab upload");
         t.device = dev;
     }
     return t.d_tab;
@@ -287,7 +289,7 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
     VerifyItem* d_items = b_items.p;
     jac* d_scratch = b_scratch.p;
     uint8_t* d_st = b_st.p;
-    hck(hipMemcpy(d_items, items, sizeof(VerifyItem) * n, hipMemcpyHostToDevice), "h2d items");
+    node_h2d(d_items, items, sizeof(VerifyItem) * n, "h2d items");
     const int block = 64;
     const int grid = int((n + block - 1) / block);
     // Default (variant 1): __launch_bounds__(64, 4) -> 4 waves/SIMD at 128 VGPRs (a few spills), 7-9 %
@@ -297,16 +299,16 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
     const char* var = std::getenv("UPOW_P256_VARIANT");
     const char v = var ? var[0] : '1';
     if (v == '0')
-        hipLaunchKernelGGL((p256_verify_kernel<1, false>), dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch,
+        hipLaunchKernelGGL((p256_verify_kernel<1, false>), dim3(grid), dim3(block), 0, node_stream(), d_items, n, d_tab, d_scratch,
                            d_st);
     else if (v == '2')
-        hipLaunchKernelGGL((p256_verify_kernel<1, true>), dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch,
+        hipLaunchKernelGGL((p256_verify_kernel<1, true>), dim3(grid), dim3(block), 0, node_stream(), d_items, n, d_tab, d_scratch,
                            d_st);
     else
-        hipLaunchKernelGGL((p256_verify_kernel<4, false>), dim3(grid), dim3(block), 0, 0, d_items, n, d_tab, d_scratch,
+        hipLaunchKernelGGL((p256_verify_kernel<4, false>), dim3(grid), dim3(block), 0, node_stream(), d_items, n, d_tab, d_scratch,
                            d_st);
     hck(hipGetLastError(), "p256_verify_kernel launch");
-    hck(hipMemcpy(st.data(), d_st, size_t(n), hipMemcpyDeviceToHost), "d2h status");
+    node_d2h(st.data(), d_st, size_t(n), "d2h status");
     return st;
 }
 
@@ -330,13 +332,13 @@ void p256_decompress_gpu(const uint8_t* in, int64_t n, uint8_t* out, uint8_t* ok
     if (n == 0) return;
     PooledBuf<uint8_t> b_in{33 * size_t(n)}, b_out{64 * size_t(n)}, b_ok{size_t(n)};
     uint8_t *d_in = b_in.p, *d_out = b_out.p, *d_ok = b_ok.p;
-    hck(hipMemcpy(d_in, in, 33 * size_t(n), hipMemcpyHostToDevice), "h2d in");
+    node_h2d(d_in, in, 33 * size_t(n), "h2d in");
     const int block = 256;
-    hipLaunchKernelGGL(p256_decompress_kernel, dim3(int((n + block - 1) / block)), dim3(block), 0, 0, d_in, n,
+    hipLaunchKernelGGL(p256_decompress_kernel, dim3(int((n + block - 1) / block)), dim3(block), 0, node_stream(), d_in, n,
                        d_out, d_ok);
     hck(hipGetLastError(), "p256_decompress_kernel launch");
-    hck(hipMemcpy(out, d_out, 64 * size_t(n), hipMemcpyDeviceToHost), "d2h out");
-    hck(hipMemcpy(ok, d_ok, size_t(n), hipMemcpyDeviceToHost), "d2h ok");
+    node_d2h(out, d_out, 64 * size_t(n), "d2h out");
+    node_d2h(ok, d_ok, size_t(n), "d2h ok");
 }
 
 bool p256_pubkey(const uint8_t d_be[32], uint8_t out_le[64]) {

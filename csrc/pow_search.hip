@@ -30,6 +30,7 @@
 #include <string>
 
 #include "native.h"
+#include "streams.h"
 #include "sha256_common.h"
 
 namespace upow {
@@ -258,11 +259,18 @@ PowResult pow_search_gpu(const PowJobHost& hj, uint64_t start, uint64_t count, i
     PowJobDev job = make_pow_job(hj);
     const bool v2 = hj.header.size() == 108;
     PowDeviceBuffers& buf = pow_buffers(cap);
-    hip_check(hipMemsetAsync(buf.d_count, 0, sizeof(uint32_t), 0), "memset");
+    hipStream_t st = miner_stream();  // least priority: node kernels go first (csrc/streams.h)
+    hip_check(hipMemsetAsync(buf.d_count, 0, sizeof(uint32_t), st), "memset");
     const uint32_t block = 256;
     if (grid_blocks <= 0) grid_blocks = pow_resident_blocks(v2, variant);
     const uint64_t per_launch_threads = uint64_t(grid_blocks) * block;
-    if (chunk_iters == 0) chunk_iters = uint32_t(std::max<uint64_t>(1, (uint64_t(1) << 28) / per_launch_threads));
+    if (chunk_iters == 0) {
+        // nonces per dispatch: 2^28 (~7.6 ms on MI355X) by default; a miner sharing the GPU with a node
+        // sets UPOW_POW_DISPATCH_LOG2 lower so a queued node kernel waits at most one short dispatch
+        int lg = 28;
+        if (const char* e = std::getenv("UPOW_POW_DISPATCH_LOG2")) lg = std::max(16, std::min(32, std::atoi(e)));
+        chunk_iters = uint32_t(std::max<uint64_t>(1, (uint64_t(1) << lg) / per_launch_threads));
+    }
     uint64_t done = 0;
     while (done < count) {
         const uint64_t left = count - done;
@@ -282,30 +290,34 @@ PowResult pow_search_gpu(const PowJobHost& hj, uint64_t start, uint64_t count, i
         }
         const uint32_t vb = uint32_t(start + done);
         if (v2 && variant == 2)
-            hipLaunchKernelGGL(pow_search_lds_kernel, dim3(gb), dim3(block), 0, 0, job, vb, iters, buf.d_count,
+            hipLaunchKernelGGL(pow_search_lds_kernel, dim3(gb), dim3(block), 0, st, job, vb, iters, buf.d_count,
                                buf.d_words, cap);
         else if (v2 && variant == 1)
-            hipLaunchKernelGGL((pow_search_kernel<2, 8>), dim3(gb), dim3(block), 0, 0, job, vb, iters,
+            hipLaunchKernelGGL((pow_search_kernel<2, 8>), dim3(gb), dim3(block), 0, st, job, vb, iters,
                                buf.d_count, buf.d_words, cap);
         else if (v2)
-            hipLaunchKernelGGL((pow_search_kernel<2, 1>), dim3(gb), dim3(block), 0, 0, job, vb, iters,
+            hipLaunchKernelGGL((pow_search_kernel<2, 1>), dim3(gb), dim3(block), 0, st, job, vb, iters,
                                buf.d_count, buf.d_words, cap);
         else
-            hipLaunchKernelGGL((pow_search_kernel<1, 1>), dim3(gb), dim3(block), 0, 0, job, vb, iters,
+            hipLaunchKernelGGL((pow_search_kernel<1, 1>), dim3(gb), dim3(block), 0, st, job, vb, iters,
                                buf.d_count, buf.d_words, cap);
         hip_check(hipGetLastError(), "pow_search_kernel launch");
         done += uint64_t(iters) * gb * block;
     }
     uint32_t n = 0;
-    hip_check(hipMemcpy(&n, buf.d_count, sizeof(uint32_t), hipMemcpyDeviceToHost), "copy count");
+    hip_check(hipMemcpyAsync(&n, buf.d_count, sizeof(uint32_t), hipMemcpyDeviceToHost, st), "copy count");
+    hip_check(hipStreamSynchronize(st), "miner stream sync");
     PowResult r;
     r.searched = done;
     r.total_hits = n;
     const uint32_t stored = n < cap ? n : cap;
     r.words.resize(stored);
     if (stored)
-        hip_check(hipMemcpy(r.words.data(), buf.d_words, sizeof(uint32_t) * stored, hipMemcpyDeviceToHost),
+    {
+        hip_check(hipMemcpyAsync(r.words.data(), buf.d_words, sizeof(uint32_t) * stored, hipMemcpyDeviceToHost, st),
                   "copy words");
+        hip_check(hipStreamSynchronize(st), "miner stream sync");
+    }
     // any ragged remainder (< 256 nonces) is searched on the host so the requested range is exact
     if (done < count) {
         for (uint64_t k = done; k < count; ++k) {

@@ -17,6 +17,7 @@
 
 #include "dev_pool.h"
 #include "native.h"
+#include "streams.h"
 #include "sha256_common.h"
 
 namespace upow {
@@ -127,16 +128,16 @@ std::vector<uint8_t> sha256_batch_gpu(const uint8_t* data, int64_t nbytes, const
     uint8_t* d_data = b_data.p;
     int64_t* d_off = b_off.p;
     uint32_t *d_len = b_len.p, *d_out = b_out.p;
-    hchk(hipMemcpy(d_data, packed.data(), size_t(total), hipMemcpyHostToDevice), "h2d data");
-    hchk(hipMemcpy(d_off, aoff.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice), "h2d off");
-    hchk(hipMemcpy(d_len, lens.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice), "h2d len");
+    node_h2d(d_data, packed.data(), size_t(total), "h2d data");
+    node_h2d(d_off, aoff.data(), sizeof(int64_t) * n, "h2d off");
+    node_h2d(d_len, lens.data(), sizeof(uint32_t) * n, "h2d len");
     const int block = 256;
     const int grid = int((n + block - 1) / block);
-    hipLaunchKernelGGL(sha256_varlen_kernel, dim3(grid), dim3(block), 0, 0,
+    hipLaunchKernelGGL(sha256_varlen_kernel, dim3(grid), dim3(block), 0, node_stream(),
                        reinterpret_cast<const uint32_t*>(d_data), d_off, d_len, n, d_out);
     hchk(hipGetLastError(), "sha256_varlen_kernel launch");
     std::vector<uint32_t> words(size_t(n) * 8);
-    hchk(hipMemcpy(words.data(), d_out, 32 * size_t(n), hipMemcpyDeviceToHost), "d2h out");
+    node_d2h(words.data(), d_out, 32 * size_t(n), "d2h out");
     for (size_t k = 0; k < words.size(); ++k) store_be32(out.data() + 4 * k, words[k]);
     return out;
 }

@@ -1,0 +1,73 @@
+// HIP streams for sharing one MI355X between the node and a co-located miner.
+//
+// Every node-side launch (block verify, decompression, batched SHA-256, the UTXO table passes) goes to
+// a per-device NON-BLOCKING stream created at the device's greatest priority; the PoW search goes to a
+// stream at the least priority. The command processor then dispatches a waiting node kernel's
+// workgroups ahead of the miner's as soon as CUs free up (there is no preemption: the miner's dispatch
+// length, UPOW_POW_DISPATCH_LOG2, bounds the wait). Host copies are stream-ordered; a D2H copy is
+// followed by a sync of the same stream only, never of the whole device.
+// UPOW_NODE_STREAM_PRIORITY=normal puts the node stream at the default priority (A/B).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+
+namespace upow {
+
+inline void stream_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+enum class StreamRole { Node = 0, Miner = 1 };
+
+inline hipStream_t role_stream(StreamRole role) {
+    constexpr int kMaxDev = 64;
+    static std::mutex mu;
+    static hipStream_t streams[2][kMaxDev] = {};
+    int dev = 0;
+    stream_check(hipGetDevice(&dev), "hipGetDevice");
+    if (dev < 0 || dev >= kMaxDev) throw std::runtime_error("device ordinal out of range");
+    const int r = int(role);
+    std::lock_guard<std::mutex> g(mu);
+    if (!streams[r][dev]) {
+        int least = 0, greatest = 0;
+        stream_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+        int prio = role == StreamRole::Node ? greatest : least;
+        if (role == StreamRole::Node) {
+            const char* e = std::getenv("UPOW_NODE_STREAM_PRIORITY");
+            if (e && std::strcmp(e, "normal") == 0) prio = 0;
+        }
+        stream_check(hipStreamCreateWithPriority(&streams[r][dev], hipStreamNonBlocking, prio),
+                     "hipStreamCreateWithPriority");
+    }
+    return streams[r][dev];
+}
+
+inline hipStream_t node_stream() { return role_stream(StreamRole::Node); }
+inline hipStream_t miner_stream() { return role_stream(StreamRole::Miner); }
+
+inline void node_h2d(void* dst, const void* src, size_t n, const char* what = "h2d") {
+    if (n) stream_check(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, node_stream()), what);
+}
+
+// D2H into (pageable) host memory; returns after the data has landed
+inline void node_d2h(void* dst, const void* src, size_t n, const char* what = "d2h") {
+    if (!n) return;
+    stream_check(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, node_stream()), what);
+    stream_check(hipStreamSynchronize(node_stream()), what);
+}
+
+inline void node_memset(void* dst, int v, size_t n, const char* what = "memset") {
+    if (n) stream_check(hipMemsetAsync(dst, v, n, node_stream()), what);
+}
+
+inline void node_sync(const char* what = "node stream sync") {
+    stream_check(hipStreamSynchronize(node_stream()), what);
+}
+
+}  // namespace upow

@@ -29,6 +29,7 @@
 
 #include "dev_pool.h"
 #include "native.h"
+#include "streams.h"
 #include "sha256_common.h"
 
 namespace upow {
@@ -338,9 +339,10 @@ int64_t utxo_create(uint32_t log2_cap) {
     uck(hipGetDevice(&t.device), "hipGetDevice");
     t.cap = 1u << log2_cap;
     uck(hipMalloc(&t.tab, sizeof(UtxoSlot) * size_t(t.cap)), "hipMalloc utxo table");
-    uck(hipMemset(t.tab, 0, sizeof(UtxoSlot) * size_t(t.cap)), "memset utxo table");
+    node_memset(t.tab, 0, sizeof(UtxoSlot) * size_t(t.cap), "memset utxo table");
     uck(hipMalloc(&t.pay, sizeof(UtxoPayload) * size_t(t.cap)), "hipMalloc utxo payload");
-    uck(hipMemset(t.pay, 0, sizeof(UtxoPayload) * size_t(t.cap)), "memset utxo payload");
+    node_memset(t.pay, 0, sizeof(UtxoPayload) * size_t(t.cap), "memset utxo payload");
+    node_sync("utxo_create");
     uck(hipMalloc(&t.d_counter, 2 * sizeof(uint32_t)), "hipMalloc counter");
     std::lock_guard<std::mutex> lk(g_ut_mu);
     const int64_t h = g_next_handle++;
@@ -372,15 +374,15 @@ uint64_t utxo_insert(int64_t h, const uint8_t* recs, int64_t n, const uint8_t* p
     UtxoTableDev& t = table(h);
     if (n == 0) return 0;
     DevBuf<UtxoKeyRec> d(n);
-    uck(hipMemcpy(d.p, recs, sizeof(UtxoKeyRec) * n, hipMemcpyHostToDevice), "h2d recs");
+    node_h2d(d.p, recs, sizeof(UtxoKeyRec) * n, "h2d recs");
     DevBuf<UtxoPayload> dp(payload ? n : 0);
-    if (payload) uck(hipMemcpy(dp.p, payload, sizeof(UtxoPayload) * n, hipMemcpyHostToDevice), "h2d payload");
-    uck(hipMemset(t.d_counter, 0, 2 * sizeof(uint32_t)), "memset");
-    hipLaunchKernelGGL(utxo_insert_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, 0, t.tab, t.pay, t.cap - 1, d.p,
+    if (payload) node_h2d(dp.p, payload, sizeof(UtxoPayload) * n, "h2d payload");
+    node_memset(t.d_counter, 0, 2 * sizeof(uint32_t), "memset");
+    hipLaunchKernelGGL(utxo_insert_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, node_stream(), t.tab, t.pay, t.cap - 1, d.p,
                        payload ? dp.p : nullptr, n, t.d_counter);
     uck(hipGetLastError(), "utxo_insert_kernel");
     uint32_t c[2] = {0, 0};
-    uck(hipMemcpy(c, t.d_counter, sizeof c, hipMemcpyDeviceToHost), "d2h failed");
+    node_d2h(c, t.d_counter, sizeof c, "d2h failed");
     return uint64_t(c[0]) | (uint64_t(c[1]) << 32);  // (table full) | (duplicates << 32)
 }
 
@@ -393,12 +395,12 @@ std::vector<uint8_t> utxo_lookup(int64_t h, const uint8_t* recs, int64_t n, std:
     DevBuf<UtxoKeyRec> d(n);
     DevBuf<uint8_t> o(n);
     DevBuf<UtxoPayload> po(n);
-    uck(hipMemcpy(d.p, recs, sizeof(UtxoKeyRec) * n, hipMemcpyHostToDevice), "h2d recs");
-    hipLaunchKernelGGL(utxo_lookup_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, 0, t.tab, t.pay, t.cap - 1, d.p, n,
+    node_h2d(d.p, recs, sizeof(UtxoKeyRec) * n, "h2d recs");
+    hipLaunchKernelGGL(utxo_lookup_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, node_stream(), t.tab, t.pay, t.cap - 1, d.p, n,
                        o.p, po.p);
     uck(hipGetLastError(), "utxo_lookup_kernel");
-    uck(hipMemcpy(out.data(), o.p, size_t(n), hipMemcpyDeviceToHost), "d2h tags");
-    uck(hipMemcpy(payload_out.data(), po.p, payload_out.size(), hipMemcpyDeviceToHost), "d2h payload");
+    node_d2h(out.data(), o.p, size_t(n), "d2h tags");
+    node_d2h(payload_out.data(), po.p, payload_out.size(), "d2h payload");
     return out;
 }
 
@@ -409,10 +411,10 @@ std::vector<uint8_t> utxo_probe(int64_t h, const uint8_t* recs, int64_t n) {
     if (n == 0) return out;
     DevBuf<UtxoKeyRec> d(n);
     DevBuf<uint8_t> o(n);
-    uck(hipMemcpy(d.p, recs, sizeof(UtxoKeyRec) * n, hipMemcpyHostToDevice), "h2d recs");
-    hipLaunchKernelGGL(utxo_probe_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, 0, t.tab, t.cap - 1, d.p, n, o.p);
+    node_h2d(d.p, recs, sizeof(UtxoKeyRec) * n, "h2d recs");
+    hipLaunchKernelGGL(utxo_probe_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, node_stream(), t.tab, t.cap - 1, d.p, n, o.p);
     uck(hipGetLastError(), "utxo_probe_kernel");
-    uck(hipMemcpy(out.data(), o.p, size_t(n), hipMemcpyDeviceToHost), "d2h tags");
+    node_d2h(out.data(), o.p, size_t(n), "d2h tags");
     return out;
 }
 
@@ -423,12 +425,12 @@ std::vector<uint8_t> utxo_erase(int64_t h, const uint8_t* recs, int64_t n) {
     if (n == 0) return out;
     DevBuf<UtxoKeyRec> d(n);
     DevBuf<uint8_t> o(n);
-    uck(hipMemcpy(d.p, recs, sizeof(UtxoKeyRec) * n, hipMemcpyHostToDevice), "h2d recs");
-    uck(hipMemset(t.d_counter, 0, sizeof(uint32_t)), "memset");
-    hipLaunchKernelGGL(utxo_erase_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, 0, t.tab, t.cap - 1, d.p, n, o.p,
+    node_h2d(d.p, recs, sizeof(UtxoKeyRec) * n, "h2d recs");
+    node_memset(t.d_counter, 0, sizeof(uint32_t), "memset");
+    hipLaunchKernelGGL(utxo_erase_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, node_stream(), t.tab, t.cap - 1, d.p, n, o.p,
                        t.d_counter);
     uck(hipGetLastError(), "utxo_erase_kernel");
-    uck(hipMemcpy(out.data(), o.p, size_t(n), hipMemcpyDeviceToHost), "d2h erased");
+    node_d2h(out.data(), o.p, size_t(n), "d2h erased");
     return out;
 }
 
@@ -448,21 +450,21 @@ std::vector<uint8_t> utxo_address_scan(int64_t h, const uint8_t* addr, uint32_t 
     for (int pass = 0; pass < 2; ++pass) {
         DevBuf<UtxoKeyRec> d(cap_out);
         DevBuf<UtxoPayload> dp(cap_out);
-        uck(hipMemset(t.d_counter, 0, sizeof(uint32_t)), "memset");
-        uck(hipMemset(dt.p, 0, sizeof(unsigned long long)), "memset");
-        hipLaunchKernelGGL(utxo_address_scan_kernel, dim3(int((t.cap + 255) / 256)), dim3(256), 0, 0, t.tab, t.pay,
+        node_memset(t.d_counter, 0, sizeof(uint32_t), "memset");
+        node_memset(dt.p, 0, sizeof(unsigned long long), "memset");
+        hipLaunchKernelGGL(utxo_address_scan_kernel, dim3(int((t.cap + 255) / 256)), dim3(256), 0, node_stream(), t.tab, t.pay,
                            t.cap, q[0], q[1], q[2], q[3], len, qfp, tag_mask, stake_sel, cap_out, d.p, dp.p, t.d_counter, dt.p);
         uck(hipGetLastError(), "utxo_address_scan_kernel");
-        uck(hipMemcpy(&n, t.d_counter, sizeof(uint32_t), hipMemcpyDeviceToHost), "d2h n");
+        node_d2h(&n, t.d_counter, sizeof(uint32_t), "d2h n");
         if (n <= cap_out) {
             unsigned long long tot = 0;
-            uck(hipMemcpy(&tot, dt.p, sizeof(tot), hipMemcpyDeviceToHost), "d2h total");
+            node_d2h(&tot, dt.p, sizeof(tot), "d2h total");
             *total_out = tot;
             std::vector<uint8_t> out(size_t(n) * sizeof(UtxoKeyRec));
             payload_out.assign(size_t(n) * sizeof(UtxoPayload), 0);
             if (n) {
-                uck(hipMemcpy(out.data(), d.p, out.size(), hipMemcpyDeviceToHost), "d2h recs");
-                uck(hipMemcpy(payload_out.data(), dp.p, payload_out.size(), hipMemcpyDeviceToHost), "d2h payload");
+                node_d2h(out.data(), d.p, out.size(), "d2h recs");
+                node_d2h(payload_out.data(), dp.p, payload_out.size(), "d2h payload");
             }
             return out;
         }
@@ -476,17 +478,17 @@ std::vector<uint8_t> utxo_dump(int64_t h, std::vector<uint8_t>* payload_out) {
     UtxoTableDev& t = table(h);
     DevBuf<UtxoKeyRec> d(t.cap);
     DevBuf<UtxoPayload> dp(payload_out ? t.cap : 0);
-    uck(hipMemset(t.d_counter, 0, sizeof(uint32_t)), "memset");
-    hipLaunchKernelGGL(utxo_dump_kernel, dim3(int((t.cap + 255) / 256)), dim3(256), 0, 0, t.tab, t.pay, t.cap, d.p,
+    node_memset(t.d_counter, 0, sizeof(uint32_t), "memset");
+    hipLaunchKernelGGL(utxo_dump_kernel, dim3(int((t.cap + 255) / 256)), dim3(256), 0, node_stream(), t.tab, t.pay, t.cap, d.p,
                        payload_out ? dp.p : nullptr, t.d_counter);
     uck(hipGetLastError(), "utxo_dump_kernel");
     uint32_t n = 0;
-    uck(hipMemcpy(&n, t.d_counter, sizeof(uint32_t), hipMemcpyDeviceToHost), "d2h n");
+    node_d2h(&n, t.d_counter, sizeof(uint32_t), "d2h n");
     std::vector<uint8_t> out(size_t(n) * sizeof(UtxoKeyRec));
-    if (n) uck(hipMemcpy(out.data(), d.p, out.size(), hipMemcpyDeviceToHost), "d2h dump");
+    if (n) node_d2h(out.data(), d.p, out.size(), "d2h dump");
     if (payload_out) {
         payload_out->assign(size_t(n) * sizeof(UtxoPayload), 0);
-        if (n) uck(hipMemcpy(payload_out->data(), dp.p, payload_out->size(), hipMemcpyDeviceToHost), "d2h payload");
+        if (n) node_d2h(payload_out->data(), dp.p, payload_out->size(), "d2h payload");
     }
     return out;
 }
@@ -580,29 +582,29 @@ BlockInputsResult utxo_block_inputs(int64_t h, const uint8_t* keys, int64_t n_in
     DevBuf<uint64_t> d_out(n_out);
     DevBuf<int64_t> d_fee(n_tx);
     DevBuf<uint32_t> d_miss(n_tx);
-    if (n_in) uck(hipMemcpy(d_keys.p, keys, sizeof(UtxoKeyRec) * n_in, hipMemcpyHostToDevice), "h2d keys");
-    if (n_out) uck(hipMemcpy(d_out.p, out_amount, 8 * size_t(n_out), hipMemcpyHostToDevice), "h2d out");
-    uck(hipMemcpy(d_in_start.p, in_start, 4 * size_t(n_tx + 1), hipMemcpyHostToDevice), "h2d in_start");
-    uck(hipMemcpy(d_out_start.p, out_start, 4 * size_t(n_tx + 1), hipMemcpyHostToDevice), "h2d out_start");
-    uck(hipMemset(d_scratch.p, 0, sizeof(unsigned long long) * scap), "memset scratch");
+    if (n_in) node_h2d(d_keys.p, keys, sizeof(UtxoKeyRec) * n_in, "h2d keys");
+    if (n_out) node_h2d(d_out.p, out_amount, 8 * size_t(n_out), "h2d out");
+    node_h2d(d_in_start.p, in_start, 4 * size_t(n_tx + 1), "h2d in_start");
+    node_h2d(d_out_start.p, out_start, 4 * size_t(n_tx + 1), "h2d out_start");
+    node_memset(d_scratch.p, 0, sizeof(unsigned long long) * scap, "memset scratch");
     if (n_in) {
         const dim3 g(unsigned((n_in + 255) / 256));
-        hipLaunchKernelGGL(utxo_lookup_kernel, g, dim3(256), 0, 0, t.tab, t.pay, t.cap - 1, d_keys.p, n_in, d_tags.p,
+        hipLaunchKernelGGL(utxo_lookup_kernel, g, dim3(256), 0, node_stream(), t.tab, t.pay, t.cap - 1, d_keys.p, n_in, d_tags.p,
                            d_pay.p);
         uck(hipGetLastError(), "utxo_lookup_kernel");
-        hipLaunchKernelGGL(block_dup_kernel, g, dim3(256), 0, 0, d_keys.p, n_in, d_scratch.p, scap - 1, d_dup.p);
+        hipLaunchKernelGGL(block_dup_kernel, g, dim3(256), 0, node_stream(), d_keys.p, n_in, d_scratch.p, scap - 1, d_dup.p);
         uck(hipGetLastError(), "block_dup_kernel");
     }
-    hipLaunchKernelGGL(block_fee_kernel, dim3(unsigned((n_tx + 255) / 256)), dim3(256), 0, 0, d_tags.p, d_pay.p,
+    hipLaunchKernelGGL(block_fee_kernel, dim3(unsigned((n_tx + 255) / 256)), dim3(256), 0, node_stream(), d_tags.p, d_pay.p,
                        d_in_start.p, d_out.p, d_out_start.p, n_tx, want_tag, d_fee.p, d_miss.p);
     uck(hipGetLastError(), "block_fee_kernel");
     if (n_in) {
-        uck(hipMemcpy(r.tags.data(), d_tags.p, size_t(n_in), hipMemcpyDeviceToHost), "d2h tags");
-        uck(hipMemcpy(r.payload.data(), d_pay.p, r.payload.size(), hipMemcpyDeviceToHost), "d2h payload");
-        uck(hipMemcpy(r.dup_of.data(), d_dup.p, 4 * size_t(n_in), hipMemcpyDeviceToHost), "d2h dup");
+        node_d2h(r.tags.data(), d_tags.p, size_t(n_in), "d2h tags");
+        node_d2h(r.payload.data(), d_pay.p, r.payload.size(), "d2h payload");
+        node_d2h(r.dup_of.data(), d_dup.p, 4 * size_t(n_in), "d2h dup");
     }
-    uck(hipMemcpy(r.fee.data(), d_fee.p, 8 * size_t(n_tx), hipMemcpyDeviceToHost), "d2h fee");
-    uck(hipMemcpy(r.missing.data(), d_miss.p, 4 * size_t(n_tx), hipMemcpyDeviceToHost), "d2h missing");
+    node_d2h(r.fee.data(), d_fee.p, 8 * size_t(n_tx), "d2h fee");
+    node_d2h(r.missing.data(), d_miss.p, 4 * size_t(n_tx), "d2h missing");
     // exact confirmation of duplicate candidates (full 36-byte key compare)
     const UtxoKeyRec* kr = reinterpret_cast<const UtxoKeyRec*>(keys);
     for (int64_t i = 0; i < n_in; ++i) {
@@ -680,35 +682,36 @@ std::vector<uint8_t> utxo_set_hash(int64_t h, uint32_t tag, uint64_t* count_out)
     std::lock_guard<std::mutex> lk(g_ut_mu);
     UtxoTableDev& t = table(h);
     DevBuf<UtxoKeyRec> recs(t.cap);
-    uck(hipMemset(t.d_counter, 0, sizeof(uint32_t)), "memset");
-    hipLaunchKernelGGL(set_compact_kernel, dim3((t.cap + 255) / 256), dim3(256), 0, 0, t.tab, t.cap, tag, recs.p,
+    node_memset(t.d_counter, 0, sizeof(uint32_t), "memset");
+    hipLaunchKernelGGL(set_compact_kernel, dim3((t.cap + 255) / 256), dim3(256), 0, node_stream(), t.tab, t.cap, tag, recs.p,
                        t.d_counter);
     uck(hipGetLastError(), "set_compact_kernel");
     uint32_t n = 0;
-    uck(hipMemcpy(&n, t.d_counter, sizeof(uint32_t), hipMemcpyDeviceToHost), "d2h n");
+    node_d2h(&n, t.d_counter, sizeof(uint32_t), "d2h n");
     if (count_out) *count_out = n;
     std::vector<uint8_t> msg(size_t(n) * 33);
     if (n) {
         DevBuf<uint32_t> perm_a(n), perm_b(n);
         DevBuf<uint64_t> col_a(n), col_b(n);
         const dim3 g((n + 255) / 256);
-        hipLaunchKernelGGL(iota_kernel, g, dim3(256), 0, 0, perm_a.p, n);
+        hipLaunchKernelGGL(iota_kernel, g, dim3(256), 0, node_stream(), perm_a.p, n);
         size_t temp_bytes = 0;
-        uck(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, col_a.p, col_b.p, perm_a.p, perm_b.p, n),
+        uck(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, col_a.p, col_b.p, perm_a.p, perm_b.p, n, 0, 64,
+                                               node_stream()),
             "radix sort sizing");
         DevBuf<uint8_t> temp(temp_bytes);
         for (int c = 0; c <= 4; ++c) {  // least significant column first; radix sort is stable
-            hipLaunchKernelGGL(sort_column_kernel, g, dim3(256), 0, 0, recs.p, perm_a.p, n, c, col_a.p);
+            hipLaunchKernelGGL(sort_column_kernel, g, dim3(256), 0, node_stream(), recs.p, perm_a.p, n, c, col_a.p);
             uck(hipGetLastError(), "sort_column_kernel");
             uck(hipcub::DeviceRadixSort::SortPairs(temp.p, temp_bytes, col_a.p, col_b.p, perm_a.p, perm_b.p, n,
-                                                   0, c == 0 ? 8 : 64),
+                                                   0, c == 0 ? 8 : 64, node_stream()),
                 "radix sort");
             std::swap(perm_a.p, perm_b.p);
         }
         DevBuf<uint8_t> d_msg(size_t(n) * 33);
-        hipLaunchKernelGGL(set_message_kernel, g, dim3(256), 0, 0, recs.p, perm_a.p, n, d_msg.p);
+        hipLaunchKernelGGL(set_message_kernel, g, dim3(256), 0, node_stream(), recs.p, perm_a.p, n, d_msg.p);
         uck(hipGetLastError(), "set_message_kernel");
-        uck(hipMemcpy(msg.data(), d_msg.p, msg.size(), hipMemcpyDeviceToHost), "d2h message");
+        node_d2h(msg.data(), d_msg.p, msg.size(), "d2h message");
     }
     std::vector<uint8_t> digest(32);
     host_sha256(msg.data(), msg.size(), digest.data());

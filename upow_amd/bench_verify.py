@@ -150,6 +150,7 @@ async def _run(args, ctx, device, utxo_backend):
             ctx.barrier()
             ctx.synchronize()
             t_start = time.perf_counter()
+            unix_start = time.time()
         t0 = time.perf_counter()
         errors = []
         if from_mempool:
@@ -186,7 +187,7 @@ async def _run(args, ctx, device, utxo_backend):
     writer = db.writer.stats() if db.writer is not None else None
     if writer is not None:
         writer = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in writer.items() if k != 'error'}
-    extra = {'drain_s': drain, 'writer': writer}
+    extra = {'drain_s': drain, 'writer': writer, 'window_unix': [unix_start, time.time()]}
     return total_txs, wall, stages, len(blocks[0]), sorted(paths), extra
 
 
@@ -230,6 +231,7 @@ def run_verify_bench(args, ctx):
         'commit_latency_ms': avg.get('block_s'),
         'final_drain_ms': round(extra['drain_s'] * 1000, 2),
         'ledger_writer': extra['writer'],
+        'window_unix': extra['window_unix'],
     }
 
 
