@@ -1,4 +1,5 @@
-"""Multi-process (gloo, world_size 2) tests of the nonce-space data parallelism and collectives.
+"""Multi-process (gloo, world_size 2 and 4) tests of the nonce-space data parallelism, the collectives,
+sharded verification and the multi-GPU node's replica op stream.
 
 The same code runs over RCCL on MI355X ranks; here every rank uses the host C++ search."""
 import hashlib
@@ -29,6 +30,9 @@ def _worker(rank, world, port, q):
         # collectives
         assert ctx.allreduce_min(10 + rank) == 10
         assert ctx.allreduce_sum(1) == world
+        # fused per-chunk agreement of ClusterMiner: element-wise MIN in one collective
+        assert ctx.allreduce_min_vec([rank if rank % 2 else world, 0 if rank == world - 1 else 1, 1]) == \
+            [1 if world > 1 else world, 0, 1]
         assert ctx.broadcast_bytes(b'x' * 300 if rank == 1 else None, src=1, max_len=0) == b'x' * 300
         got = ctx.all_gather_bytes(bytes([rank]) * (rank + 1))
         assert got == [bytes([r]) * (r + 1) for r in range(world)]
@@ -58,17 +62,23 @@ def _worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
-def test_dp_miner_gloo_world2():
+def _spawn(target, world, *args):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=target, args=(r, world, port, *args, q)) for r in range(world)]
     for p in procs:
         p.start()
-    results = dict(q.get(timeout=240) for _ in procs)
+    results = dict(q.get(timeout=300) for _ in procs)
     for p in procs:
         p.join(60)
-    assert results == {0: 'ok', 1: 'ok'}, results
+    return results
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_dp_miner_gloo(world):
+    results = _spawn(_worker, world)
+    assert results == {r: 'ok' for r in range(world)}, results
 
 
 def test_shard_bounds_partition():
@@ -156,14 +166,79 @@ def _replica_worker(rank, world, port, tmp, q):
         q.put((rank, traceback.format_exc()))
 
 
-def test_sharded_verify_and_replicated_ledger_gloo_world2(tmp_path):
-    ctx = mp.get_context('spawn')
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_replica_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    results = dict(q.get(timeout=240) for _ in procs)
-    for p in procs:
-        p.join(60)
-    assert results == {0: 'ok', 1: 'ok'}, results
+@pytest.mark.parametrize('world', [2, 4])
+def test_sharded_verify_and_replicated_ledger_gloo(tmp_path, world):
+    results = _spawn(_replica_worker, world, str(tmp_path))
+    assert results == {r: 'ok' for r in range(world)}, results
+
+
+def _cluster_worker(rank, world, port, tmp, q):
+    """The multi-GPU node's op stream (parallel/cluster.py): the leader applies blocks (each broadcast as a
+    binary frame, signatures sharded over the ranks, verdict agreed), admits mempool txs, rolls a block
+    back and re-applies it; every follower replica must end at the same height and UTXO-set hash."""
+    os.environ.update({'RANK': str(rank), 'WORLD_SIZE': str(world), 'LOCAL_RANK': str(rank),
+                       'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port), 'UPOW_DISABLE_GPU': '1',
+                       'UPOW_START_DIFFICULTY': '1.0', 'UPOW_CORE_URL': ''})
+    try:
+        import asyncio
+
+        from upow_amd import devnet
+        from upow_amd.ledger import fastpath, validate
+        from upow_amd.ledger.database import Database
+        from upow_amd.parallel import cluster
+        from upow_amd.parallel.dist import init_from_env, shutdown
+        from upow_amd.wallet.builders import address_of, create_transaction
+
+        ctx = init_from_env(backend='gloo', want_gpu=False)
+        c = cluster.init(ctx)
+
+        async def go():
+            db = await Database.create(path=os.path.join(tmp, f'c{rank}.sqlite3'), utxo_backend='host')
+            if rank != 0:
+                await cluster.follower_main(c, db)
+                res = (db._tip_id(), await db.get_unspent_outputs_hash())
+                db.close()
+                return res
+            key = 0x71
+            addr = address_of(key)
+            base = 1_700_000_000
+            await cluster.leader_replay(db)
+            assert validate._dist_ctx is ctx
+            for b in range(5):
+                content = await devnet.mine_header(addr, [], ts=base + 60 * b, device='cpu')
+                assert await fastpath.create_block_from_hex(content, [])
+            txs = []
+            for j in range(4):
+                tx = await create_transaction(key, address_of(0x200 + j), '1.25')
+                assert await db.add_pending_transaction(tx)
+                cluster.mirror_tx(tx.hex())
+                txs.append(tx)
+            content = await devnet.mine_header(addr, txs, ts=base + 60 * 5, device='cpu')
+            assert await fastpath.create_block_from_hex(content, [t.hex() for t in txs])
+            assert fastpath.last_path == 'native'
+            c.send('status')
+            st = c.status(db)
+            assert len({(x['height'], x['utxo_hash']) for x in st}) == 1 and st[0]['height'] == 6, st
+            await cluster.mirror_rollback(db, 6)
+            c.send('status')
+            st = c.status(db)
+            assert len({(x['height'], x['utxo_hash']) for x in st}) == 1 and st[0]['height'] == 5, st
+            assert await fastpath.create_block_from_hex(content, [t.hex() for t in txs])
+            res = (db._tip_id(), await db.get_unspent_outputs_hash())
+            cluster.leader_quit()
+            db.close()
+            return res
+
+        res = asyncio.run(go())
+        hs = ctx.all_gather_bytes(repr(res).encode())
+        assert len(set(hs)) == 1 and res[0] == 6, hs
+        shutdown(ctx)
+        q.put((rank, 'ok'))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_cluster_op_stream_replicas_and_rollback_gloo_world4(tmp_path):
+    results = _spawn(_cluster_worker, 4, str(tmp_path))
+    assert results == {r: 'ok' for r in range(4)}, results

@@ -85,8 +85,8 @@ async def create_block_from_hex(block_content: str, tx_hexes: List[str], error_l
     from ..parallel import cluster
     c = cluster.get()
     if c is not None and c.leader and mirror and not c.replaying:
-        c.send('block', content=block_content, txs=list(tx_hexes),
-               cb=coinbase.hex() if coinbase is not None else None)
+        from ..parallel.cluster import pack_txs
+        c.send('block', pack_txs(tx_hexes), content=block_content, cb=coinbase.hex() if coinbase is not None else None)
     err = None
     try:
         ok = await _create_block_from_hex(block_content, tx_hexes, error_list, last_block, coinbase, decoded)

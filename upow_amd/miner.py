@@ -81,7 +81,12 @@ def main(argv=None):
     ap.add_argument('--extranonce', action='store_true',
                     help='also vary the (unchecked) header difficulty field once timestamps are exhausted')
     ap.add_argument('--blocks', type=int, default=0, help='stop after this many accepted blocks (0 = forever)')
+    ap.add_argument('--dispatch-log2', type=int, default=int(os.environ.get('UPOW_POW_DISPATCH_LOG2', '24')),
+                    help='nonces per GPU dispatch (log2). 24 (~0.5 ms) lets a node sharing the GPU run its block '
+                         'kernels between dispatches at a ~1%% hashrate cost; 28 for a dedicated GPU '
+                         '(docs/PERF.md §3)')
     a = ap.parse_args(argv)
+    os.environ['UPOW_POW_DISPATCH_LOG2'] = str(a.dispatch_log2)
     from . import config
     node_url = (a.node_url or os.environ.get('UPOW_MINING_NODE_URL') or 'http://localhost:3006/').strip('/') + '/'
 

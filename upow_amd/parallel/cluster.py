@@ -48,12 +48,20 @@ class Cluster:
         return self.ctx.rank == 0
 
     # ------------------------------------------------------------------ op stream
-    def send(self, op: str, **kw):
+    # One frame per op: u32 header length, a small JSON header, then a binary payload (a block's txs
+    # travel as raw bytes, half the size of hex and no JSON string escaping): two broadcasts per op
+    # (length, then frame) over RCCL.
+    def send(self, op: str, payload: bytes = b'', **kw):
         assert self.leader
-        self.ctx.broadcast_bytes(json.dumps({'op': op, **kw}, separators=(',', ':')).encode(), src=0, max_len=0)
+        head = json.dumps({'op': op, **kw}, separators=(',', ':')).encode()
+        self.ctx.broadcast_bytes(len(head).to_bytes(4, 'little') + head + payload, src=0, max_len=0)
 
     def recv(self) -> dict:
-        return json.loads(self.ctx.broadcast_bytes(None, src=0, max_len=0).decode())
+        raw = self.ctx.broadcast_bytes(None, src=0, max_len=0)
+        n = int.from_bytes(raw[:4], 'little')
+        msg = json.loads(raw[4:4 + n].decode())
+        msg['_payload'] = raw[4 + n:]
+        return msg
 
     def agree(self, ok: bool, what: str) -> bool:
         n = self.ctx.allreduce_sum(1 if ok else 0)
@@ -66,6 +74,28 @@ class Cluster:
         mine = json.dumps({'rank': self.ctx.rank, 'height': db._tip_id(),
                            'utxo_hash': db.sql_unspent_outputs_hash(), 'utxo_entries': len(db.utxo)}).encode()
         return [json.loads(b.decode()) for b in self.ctx.all_gather_bytes(mine)]
+
+
+def pack_txs(tx_hexes) -> bytes:
+    """Raw tx bytes of a block: u32 count, then u32 length + bytes per tx."""
+    parts = [len(tx_hexes).to_bytes(4, 'little')]
+    for h in tx_hexes:
+        raw = bytes.fromhex(h)
+        parts.append(len(raw).to_bytes(4, 'little'))
+        parts.append(raw)
+    return b''.join(parts)
+
+
+def unpack_txs(buf: bytes) -> List[str]:
+    n = int.from_bytes(buf[:4], 'little')
+    out, o = [], 4
+    for _ in range(n):
+        k = int.from_bytes(buf[o:o + 4], 'little')
+        out.append(buf[o + 4:o + 4 + k].hex())
+        o += 4 + k
+    if o != len(buf):
+        raise ValueError('cluster frame: trailing bytes after the tx list')
+    return out
 
 
 def init(ctx: DistContext) -> Optional[Cluster]:
@@ -127,7 +157,7 @@ async def leader_replay(db):
         if not page:
             break
         for info in page:
-            c.send('replay_block', content=info['block']['content'], txs=list(info['transactions']))
+            c.send('replay_block', pack_txs(info['transactions']), content=info['block']['content'])
             offset = info['block']['id'] + 1
     for r in db._q('SELECT tx_hex FROM pending_transactions ORDER BY rowid'):
         c.send('tx', h=r['tx_hex'])
@@ -182,7 +212,7 @@ async def follower_main(c: Cluster, db):
             await db.delete_blockchain()
             last_block = None
         elif op == 'replay_block':
-            hexes, cb = await _split_coinbase(msg['txs'])
+            hexes, cb = await _split_coinbase(unpack_txs(msg['_payload']))
             ok = await fastpath.create_block_from_hex(msg['content'], hexes, coinbase=cb, last_block=last_block,
                                                       mirror=False)
             if not ok:
@@ -197,7 +227,7 @@ async def follower_main(c: Cluster, db):
             if msg.get('cb'):
                 cb = await Transaction.from_hex(msg['cb'])
             # difficulty/last block come from this replica's own ledger (identical to the leader's)
-            await fastpath.create_block_from_hex(msg['content'], msg['txs'], coinbase=cb, mirror=False)
+            await fastpath.create_block_from_hex(msg['content'], unpack_txs(msg['_payload']), coinbase=cb, mirror=False)
         elif op == 'tx':
             try:
                 await db.add_pending_transaction(await Transaction.from_hex(msg['h']))

@@ -46,6 +46,15 @@ class DistContext:
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return int(t.item())
 
+    def allreduce_min_vec(self, values) -> list:
+        """Element-wise MIN of a short int vector: several per-step agreements in ONE collective."""
+        if not self.is_distributed:
+            return [int(v) for v in values]
+        import torch.distributed as dist
+        t = self._t(list(values))
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return [int(x) for x in t.tolist()]
+
     def allreduce_max_f(self, v: float) -> float:
         if not self.is_distributed:
             return float(v)

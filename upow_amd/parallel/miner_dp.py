@@ -130,16 +130,17 @@ class ClusterMiner:
                     self.hashes += n
                     pos += n
                 local = job.header_with_nonce(nonces[0]) if nonces else None
-                winner = ctx.allreduce_min(ctx.rank if local is not None else ctx.world)
+                # one fused all-reduce(MIN) per chunk: [lowest finder rank | world, any rank asked to
+                # stop -> 0, every rank's slice exhausted -> 1]
+                winner, keep_going, all_done = ctx.allreduce_min_vec(
+                    [ctx.rank if local is not None else ctx.world, 0 if should_stop() else 1, 1 if pos >= hi else 0])
                 if winner < ctx.world:
                     header = ctx.broadcast_bytes(local if ctx.rank == winner else None, src=winner)
                     if not self.target.check_hex(hashlib.sha256(header).hexdigest()):
                         raise RuntimeError('broadcast header failed the PoW re-check')
                     return header
-                stop = ctx.allreduce_min(0 if should_stop() else 1) == 0
-                done = ctx.allreduce_min(1 if pos >= hi else 0) == 1
-                if stop:
+                if keep_going == 0:
                     return None
-                if done:
+                if all_done == 1:
                     break
         return None
