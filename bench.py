@@ -115,7 +115,7 @@ def _verify_side_metrics(args, ctx) -> dict:
     tmp = tempfile.mkdtemp(prefix='upow_bench_verify_')
     try:
         v = argparse.Namespace(**{**vars(args), 'steps': args.verify_steps, 'warmup': 1, 'ledger': tmp,
-                                  'object_path': False, 'from_mempool': False})
+                                  'object_path': False, 'from_mempool': False, 'governance': False})
         r = run_verify_bench(v, ctx)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
@@ -142,6 +142,8 @@ def main(argv=None):
     ap.add_argument('--ledger', default=None, help='verify mode: directory for a file-backed (WAL) ledger')
     ap.add_argument('--from-mempool', action='store_true',
                     help='verify mode: block txs are in the mempool and pushed as hashes (the miner path)')
+    ap.add_argument('--governance', action='store_true',
+                    help='verify mode: seed 12 inodes, 200 validators, 5,000 delegates with ballots before the blocks')
     ap.add_argument('--verify-steps', type=int, default=4,
                     help='mine mode: timed 2 MB blocks of the tx-verify side measurement (0: skip; GPU only)')
     args = ap.parse_args(argv)

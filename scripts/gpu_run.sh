@@ -8,6 +8,8 @@
 #   mine     bench.py (driver default: PoW MH/s + verify side metrics)
 #   verify   bench.py --mode verify --ledger <tmp dir> (file ledger, metric 2)
 #   verifymem bench.py --mode verify (in-memory ledger)
+#   verifygov bench.py --mode verify --governance (file ledger; 12 inodes, 200 validators, 5,000 delegates)
+#   coloc    scripts/colocated.py (node + miner sharing the GPU)
 #   prof     rocprofv3 --kernel-trace --stats over a short bench.py
 #   vprof    rocprofv3 --kernel-trace --stats over the verify bench
 #   py:<script.py>  any extra python script under scripts/ (args after a comma: py:x.py,--a,1)
@@ -40,6 +42,15 @@ for s in $STEPS; do
       timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger \
         > "$OUT/verify_file.json" 2> "$OUT/verify_file.err" || { tail -20 "$OUT/verify_file.err"; exit 1; }
       cat "$OUT/verify_file.json" ;;
+    verifygov)
+      rm -rf /tmp/upow_bench_ledger
+      timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger --governance \
+        > "$OUT/verify_gov.json" 2> "$OUT/verify_gov.err" || { tail -20 "$OUT/verify_gov.err"; exit 1; }
+      cat "$OUT/verify_gov.json" ;;
+    coloc)
+      timeout -k 10 300 python scripts/colocated.py --dispatch-log2 24 --prio high --out "$OUT/coloc.json" \
+        > "$OUT/coloc.log" 2>&1 || { tail -20 "$OUT/coloc.log"; exit 1; }
+      cat "$OUT/coloc.json" ;;
     verifymem)
       timeout -k 10 600 python bench.py --mode verify > "$OUT/verify_mem.json" 2> "$OUT/verify_mem.err" \
         || { tail -20 "$OUT/verify_mem.err"; exit 1; }

@@ -21,6 +21,7 @@ def main():
     assert ctx.is_distributed, 'set UPOW_FORCE_DIST=1 or run with >1 rank'
     assert ctx.allreduce_min(5 + ctx.rank) == 5
     assert ctx.allreduce_sum(2) == 2 * ctx.world
+    assert ctx.allreduce_min_vec([ctx.rank, 1, 0]) == [0, 1, 0]  # ClusterMiner's fused per-chunk agreement
     assert ctx.broadcast_bytes(b'h' * 108 if ctx.rank == 0 else None, src=0) == b'h' * 108
     big = bytes(range(256)) * 9000  # ~2.3 MB block-sized payload
     assert ctx.broadcast_bytes(big if ctx.rank == 0 else None, src=0, max_len=0) == big
@@ -40,6 +41,15 @@ def main():
                                                                                      range(1, ctx.world)]
     b, t = verify_dp.broadcast_block(ctx, 'ff' * 108 if ctx.rank == 0 else None, ['aa', 'bb'] if ctx.rank == 0 else None)
     assert b == 'ff' * 108 and t == ['aa', 'bb']
+    # the multi-GPU node's op frame (parallel/cluster.py): JSON header + raw tx bytes, over RCCL
+    from upow_amd.parallel import cluster
+    c = cluster.Cluster(ctx)
+    txs = [bytes([k]) * (100 + k) for k in range(50)]
+    if ctx.rank == 0:
+        c.send('block', cluster.pack_txs([t.hex() for t in txs]), content='ee' * 108)
+    msg = c.recv() if ctx.rank != 0 else None
+    if ctx.rank != 0:
+        assert msg['op'] == 'block' and cluster.unpack_txs(msg['_payload']) == [t.hex() for t in txs]
     ctx.barrier()
     if ctx.rank == 0:
         print(json.dumps({'rccl_selfcheck': 'ok', 'world': ctx.world, 'backend': ctx.backend}))

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import asyncio
 import hashlib
+import json
 import random
 import time
 from decimal import Decimal
@@ -30,7 +31,7 @@ def _funding_tx(owner_addrs, amount: Decimal, rng):
 
 
 async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None, device=None, base_ts=None,
-                 make_blocks: bool = True, ledger_path: str = None):
+                 make_blocks: bool = True, ledger_path: str = None, governance: bool = False):
     from . import devnet
     from .ledger import manager
     from .ledger.database import Database
@@ -62,6 +63,8 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
                      __import__('json').dumps([int(o.amount * SMALLEST) for o in t.outputs]), '0.000000'))
     db.insert_transaction_rows(rows)
     await db.add_transaction_outputs(funding + [cb])
+    if governance:
+        _seed_governance(db, rng, block_hash)
     outpoints = [(t.hash(), i) for t in funding for i in range(len(t.outputs))]
     # spending blocks
     blocks = []
@@ -103,6 +106,85 @@ def _admit_untimed(db, txs_hex):
         db.conn.executemany('INSERT INTO pending_spent_outputs (tx_hash, "index") VALUES (?, ?)', spent)
 
 
+def _seed_governance(db, rng, block_hash: str, n_inodes: int = 12, n_validators: int = 200,
+                     n_delegates: int = 5000):
+    """Trusted setup of a governance-heavy chain state inside the funding block (written straight into the
+    ledger like the funding outputs; not part of the measurement): every validator and delegate has a
+    staked output, validators and inodes are registered, each delegate votes for one validator and each
+    validator for two inodes. Row layout as the reference's output tables (database.py:524-580): a
+    ballot carries the vote in ``outputs_amounts[index]`` and the voter in ``inputs_addresses[index]`` of
+    its tx. Returns the inode addresses."""
+    import json
+    from .ops import p256 as op
+    from .utils.codec import point_to_string
+    keys = [rng.randrange(1, op.oracle.N) for _ in range(n_inodes + n_validators + n_delegates)]
+    addrs = [point_to_string(op.public_key(k)) for k in keys]
+    inodes = addrs[:n_inodes]
+    validators = addrs[n_inodes:n_inodes + n_validators]
+    delegates = addrs[n_inodes + n_validators:]
+    tx_rows = []
+    tables = {t: [] for t in ('unspent_outputs', 'inode_registration_output', 'validator_registration_output',
+                              'validators_ballot', 'inodes_ballot')}
+
+    def tx(voter, receiver, amount):
+        h = rng.randbytes(32).hex()
+        tx_rows.append((block_hash, h, rng.randbytes(120).hex(), json.dumps([voter]), json.dumps([receiver]),
+                        json.dumps([amount]), '0.000000'))
+        return h
+    for a in validators + delegates:  # staked outputs (unspent_outputs.is_stake = 1)
+        tables['unspent_outputs'].append((tx(a, a, 10 * SMALLEST), 0, a, 1))
+    for a in inodes:
+        tables['inode_registration_output'].append((tx(a, a, 1000 * SMALLEST), 0, a))
+    for a in validators:
+        tables['validator_registration_output'].append((tx(a, a, 100 * SMALLEST), 0, a))
+        for _ in range(2):
+            target = inodes[rng.randrange(n_inodes)]
+            tables['inodes_ballot'].append((tx(a, target, rng.randint(1, 5) * SMALLEST), 0, target))
+    for a in delegates:
+        target = validators[rng.randrange(n_validators)]
+        tables['validators_ballot'].append((tx(a, target, rng.randint(1, 10) * SMALLEST), 0, target))
+    db.insert_transaction_rows(tx_rows)
+    db._xm('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) VALUES (?, ?, ?, ?)',
+           tables.pop('unspent_outputs'))
+    for t, rows in tables.items():
+        db._xm(f'INSERT INTO {t} (tx_hash, "index", address) VALUES (?, ?, ?)', rows)
+    db._rebuild_utxo_index()  # index + governance index from the tables
+    return inodes
+
+
+async def _governance_probe(db) -> dict:
+    """get_active_inodes on the seeded chain: the first (index build of the aggregates) and the
+    per-block steady-state call (memoised until a governance write), and the SQL cascade's cost for
+    one validator's stake (database.py:1127-1136 + 1189-1205, the per-ballot N+1) for comparison."""
+    t0 = time.perf_counter()
+    first = await db.get_active_inodes()
+    t1 = time.perf_counter()
+    n = 200
+    for _ in range(n):
+        await db.get_active_inodes()
+    t2 = time.perf_counter()
+    db.gov.version += 1  # force one full recomputation of the aggregates
+    await db.get_active_inodes()
+    t3 = time.perf_counter()
+    validator = db.gov.ballot_rows('inodes_ballot', None, False)[0][3]
+    gov, db.gov = db.gov, None
+    try:
+        t4 = time.perf_counter()
+        sql_stake = await db.get_validators_stake(validator)
+        t5 = time.perf_counter()
+    finally:
+        db.gov = gov
+    idx_stake = await db.get_validators_stake(validator)
+    t = db.gov.tables
+    return {'inodes': len(t['inode_registration_output'].rows), 'validators': len(t['validator_registration_output'].rows),
+            'delegates_ballots': len(t['validators_ballot'].rows), 'inode_ballots': len(t['inodes_ballot'].rows),
+            'stake_rows': len(t['stake'].rows), 'active_inodes': len(first),
+            'get_active_inodes_first_ms': round((t1 - t0) * 1e3, 3),
+            'get_active_inodes_per_block_ms': round((t2 - t1) * 1e3 / n, 4),
+            'get_active_inodes_recompute_ms': round((t3 - t2) * 1e3, 3),
+            'one_validator_stake_sql_ms': round((t5 - t4) * 1e3, 2), 'stake_matches_sql': sql_stake == idx_stake}
+
+
 def _ledger_path(args, ctx):
     """``--ledger DIR``: a file-backed ledger (WAL, synchronous=NORMAL — what a node runs with) in a
     fresh per-rank directory; default is an in-memory SQLite ledger."""
@@ -120,8 +202,10 @@ async def _run(args, ctx, device, utxo_backend):
     from .ledger import fastpath, manager, validate
     from .models.transaction import Transaction
     n_blocks = args.steps + args.warmup
+    gov = getattr(args, 'governance', False)
     db, addr, blocks, base_ts = await _setup(n_blocks, args.txs, 1234 + ctx.rank, utxo_backend, device,
-                                             ledger_path=_ledger_path(args, ctx))
+                                             ledger_path=_ledger_path(args, ctx), governance=gov)
+    gov_probe = await _governance_probe(db) if gov else None
     # mine every header up front (untimed): block b+1's previous hash is sha256(header_b) and the
     # difficulty stays at START_DIFFICULTY below block 100
     from .constants import START_DIFFICULTY
@@ -187,7 +271,12 @@ async def _run(args, ctx, device, utxo_backend):
     writer = db.writer.stats() if db.writer is not None else None
     if writer is not None:
         writer = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in writer.items() if k != 'error'}
-    extra = {'drain_s': drain, 'writer': writer, 'window_unix': [unix_start, time.time()]}
+    extra = {'drain_s': drain, 'writer': writer, 'window_unix': [unix_start, time.time()], 'governance': gov_probe}
+    if gov_probe is not None:
+        gov_probe['active_inodes_after'] = len(await db.get_active_inodes())
+        gov_probe['coinbase_outputs_last_block'] = len(json.loads(
+            db._q1('SELECT outputs_addresses FROM transactions WHERE tx_hex LIKE ? LIMIT 1',
+                   ('%' + (await db.get_last_block())['hash'] + '%',))[0]))
     return total_txs, wall, stages, len(blocks[0]), sorted(paths), extra
 
 
@@ -198,6 +287,10 @@ def run_verify_bench(args, ctx):
     if not hasattr(args, 'object_path'):
         args.object_path = False
     total_txs, wall, stages, txs_per_block, paths, extra = asyncio.run(_run(args, ctx, device, utxo_backend))
+    if getattr(args, 'governance', False):
+        args_cfg = 'governance: 12 inodes, 200 validators, 5000 delegates'
+    else:
+        args_cfg = None
     total = ctx.allreduce_sum(total_txs)
     tps = total / wall
     avg = {k: round(sum(s[k] for s in stages) / len(stages) * 1000, 2) for k in stages[0]
@@ -219,7 +312,8 @@ def run_verify_bench(args, ctx):
                    'seq_len': txs_per_block, 'parallelism': f'dp{ctx.world}', 'device': device,
                    'utxo_backend': utxo_backend, 'block_path': '+'.join(paths),
                    'ledger': 'file (WAL)' if getattr(args, 'ledger', None) else 'memory',
-                   'txs_from': 'mempool (hashes)' if getattr(args, 'from_mempool', False) else 'block body (hex)'},
+                   'txs_from': 'mempool (hashes)' if getattr(args, 'from_mempool', False) else 'block body (hex)',
+                   **({'chain_state': args_cfg} if args_cfg else {})},
         'stage_ms_avg': avg,
         # the same run split by stage: validation alone (decode, HBM UTXO pass, decompression, ECDSA —
         # everything before the ledger writes) and the signature kernel alone, per 2 MB block
@@ -232,6 +326,7 @@ def run_verify_bench(args, ctx):
         'final_drain_ms': round(extra['drain_s'] * 1000, 2),
         'ledger_writer': extra['writer'],
         'window_unix': extra['window_unix'],
+        **({'governance': extra['governance']} if extra['governance'] else {}),
     }
 
 

@@ -1236,19 +1236,18 @@ class Database:
         if mempool:
             self._pending_empty = None
             self._mempool_ver += 1
-        if self.gov is not None and n_in and self.gov.stake_keys():
-            self.gov.removed(STAKE, self._stake_spent(spent))
+        if self.gov is not None and n_in:
+            hit = self._stake_spent(spent)
+            if hit:
+                self.gov.removed(STAKE, hit)
         return seq
 
     def _stake_spent(self, spent: np.ndarray) -> List[Tuple[str, int]]:
         """Which of a block's spent outpoints (n x 40 records) are staked outputs: one vectorised
         membership test of the raw (txid, index) keys against the governance index's stake rows."""
-        stake = list(self.gov.stake_keys())
-        raw = np.zeros((len(stake), 36), dtype=np.uint8)
-        for k, (h, i) in enumerate(stake):
-            raw[k, :32] = np.frombuffer(bytes.fromhex(h), dtype=np.uint8)
-            raw[k, 32:36] = np.frombuffer(struct.pack('<I', i), dtype=np.uint8)
-        want = np.ascontiguousarray(raw).view('V36').ravel()
+        stake, want = self.gov.stake_raw()
+        if not stake:
+            return []
         have = np.ascontiguousarray(spent[:, :36]).view('V36').ravel()
         hit = np.nonzero(np.isin(want, have))[0]
         return [stake[k] for k in hit.tolist()]

@@ -34,22 +34,41 @@ STAKE = 'stake'  # staked rows of unspent_outputs (is_stake = 1)
 Key = Tuple[str, int]
 
 
+_FORMS: Dict[str, List[str]] = {}
+
+
+def _forms(address: str) -> List[str]:
+    """Both string forms of an address (codec.address_forms: a point decompression + two encodings),
+    memoised: an aggregate recomputation asks for every voter's forms."""
+    hit = _FORMS.get(address)
+    if hit is None:
+        from ..utils.codec import address_forms
+        if len(_FORMS) > (1 << 20):
+            _FORMS.clear()
+        hit = _FORMS[address] = address_forms(address)
+    return hit
+
+
 def _at(arr, i):
     return arr[i] if arr is not None and 0 <= i < len(arr) else None
 
 
 class _Table:
-    __slots__ = ('rows', 'by_addr', 'by_voter')
+    __slots__ = ('rows', 'seq', 'by_addr', 'by_voter', 'next_seq')
 
     def __init__(self):
         self.rows: Dict[Key, tuple] = {}  # key -> (address, amount, voter, ts); insertion (rowid) order
+        self.seq: Dict[Key, int] = {}  # key -> insertion sequence (sort key for rowid order)
         self.by_addr: Dict[Optional[str], Dict[Key, None]] = {}
         self.by_voter: Dict[Optional[str], Dict[Key, None]] = {}
+        self.next_seq = 0
 
     def add(self, key: Key, address, amount, voter, ts):
         if key in self.rows:
             self.remove(key)
         self.rows[key] = (address, amount, voter, ts)
+        self.seq[key] = self.next_seq
+        self.next_seq += 1
         self.by_addr.setdefault(address, {})[key] = None
         self.by_voter.setdefault(voter, {})[key] = None
 
@@ -57,6 +76,7 @@ class _Table:
         row = self.rows.pop(key, None)
         if row is None:
             return False
+        del self.seq[key]
         for idx, k in ((self.by_addr, row[0]), (self.by_voter, row[2])):
             d = idx.get(k)
             if d is not None:
@@ -73,11 +93,7 @@ class _Table:
                 found[k] = None
         if len(found) < 2:
             return list(found)
-        pos = {k: p for p, k in enumerate(self.rows)} if len(found) > 64 else None
-        if pos is None:
-            order = list(self.rows)
-            return sorted(found, key=order.index)
-        return sorted(found, key=pos.__getitem__)
+        return sorted(found, key=self.seq.__getitem__)
 
 
 def _locked(fn):
@@ -155,6 +171,20 @@ class GovernanceIndex:
     @_locked
     def stake_keys(self) -> Dict[Key, tuple]:
         return dict(self.tables[STAKE].rows)
+
+    @_locked
+    def stake_raw(self):
+        """(keys, n x 36 raw (txid || u32 index) array) of the staked outputs, memoised per version: the
+        native block path tests a block's spent outpoints against it with one vectorised isin."""
+        def build():
+            import numpy as np
+            keys = list(self.tables[STAKE].rows)
+            raw = np.zeros((len(keys), 36), dtype=np.uint8)
+            for k, (h, i) in enumerate(keys):
+                raw[k, :32] = np.frombuffer(bytes.fromhex(h), dtype=np.uint8)
+                raw[k, 32:36] = np.frombuffer(int(i).to_bytes(4, 'little'), dtype=np.uint8)
+            return keys, np.ascontiguousarray(raw).view('V36').ravel()
+        return self._memo_get('stake_raw', build)
 
     # ------------------------------------------------------------------ mempool overlay
     @_locked
@@ -243,11 +273,9 @@ class GovernanceIndex:
     def validators_stake(self, forms: List[str], check_pending: bool) -> Decimal:
         """get_validators_stake (database.py:1127-1136): sum of vote x delegate stake / 10 over the
         validator's delegate ballots."""
-        from ..utils.codec import address_forms
-
         def compute():
             ballot = self.ballot_rows('validators_ballot', forms, check_pending)
-            ratio = [(vote * self.address_stake(address_forms(delegate), False)) / 10
+            ratio = [(vote * self.address_stake(_forms(delegate), False)) / 10
                      for _, _, vote, delegate, _ in ballot]
             return round_up_decimal(sum(ratio, Decimal(0)))
         if check_pending:
@@ -257,11 +285,9 @@ class GovernanceIndex:
     @_locked
     def inode_power(self, forms: List[str], check_pending: bool) -> Decimal:
         """get_inode_vote_ratio_by_address (database.py:1390-1418)."""
-        from ..utils.codec import address_forms
-
         def compute():
             rows = self.ballot_rows('inodes_ballot', forms, check_pending, order=False)
-            ratio = [(vote * self.validators_stake(address_forms(validator), False)) / 10
+            ratio = [(vote * self.validators_stake(_forms(validator), False)) / 10
                      for _, _, vote, validator, _ in rows]
             return round_up_decimal(sum(ratio, Decimal(0)))
         if check_pending:
@@ -271,10 +297,8 @@ class GovernanceIndex:
     @_locked
     def inodes_with_power(self, check_pending: bool):
         """get_all_registered_inode_with_vote: [(wallet, power, registration timestamp)]."""
-        from ..utils.codec import address_forms
-
         def compute():
-            return [(address, self.inode_power(list(reversed(address_forms(address))), check_pending), ts)
+            return [(address, self.inode_power(list(reversed(_forms(address))), check_pending), ts)
                     for address, ts in self.registered_inodes(check_pending)]
         if check_pending:
             return compute()
