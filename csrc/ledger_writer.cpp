@@ -34,7 +34,6 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
-#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -737,32 +736,15 @@ class LedgerWriter {
             if (target != shard) continue;
             if (!guard.empty() && query_int(sh.db, guard) == 0) continue;
             const auto ts0 = std::chrono::steady_clock::now();
-            // INSERTs bind kMultiRows rows per step through a multi-row VALUES statement: the table and
-            // index cursors are opened once per step instead of once per row
-            constexpr int kMultiRows = 64;
-            sqlite3_stmt* st1 = prepared(sh, sql);
-            sqlite3_stmt* stk = nullptr;
-            static const bool multirow = [] {
-                const char* e = std::getenv("UPOW_WRITER_MULTIROW");
-                return !(e && e[0] == '0');
-            }();
-            if (multirow && n >= kMultiRows && sql.compare(0, 6, "INSERT") == 0) {
-                const size_t v = sql.rfind("VALUES");
-                if (v != std::string::npos) {
-                    const std::string tuple = sql.substr(v + 6);
-                    std::string multi = sql;
-                    multi.reserve(sql.size() + (tuple.size() + 1) * kMultiRows);
-                    for (int q = 1; q < kMultiRows; ++q) multi += "," + tuple;
-                    stk = prepared(sh, multi);
-                }
-            }
+            sqlite3_stmt* st = prepared(sh, sql);
             int64_t changes = 0;
-            std::vector<char> hexbufs(size_t(kMultiRows) * 8 * 64);
-            auto bind_row = [&](sqlite3_stmt* st, int64_t r, int base, char* hexrow) {
+            char hexbuf[8][64];
+            for (int64_t k = 0; k < n; ++k) {
+                const int64_t r = order ? ld64(order + 8 * k) : k;
                 int hb = 0;
                 for (uint32_t j = 0; j < nc; ++j) {
                     const ColView& c = cols[j];
-                    const int p = base + int(j) + 1;
+                    const int p = int(j) + 1;
                     switch (c.kind) {
                         case K_NULL: a.bind_null(st, p); break;
                         case K_CTEXT: a.bind_text(st, p, c.ctext.data(), int(c.ctext.size()), nullptr); break;
@@ -770,7 +752,7 @@ class LedgerWriter {
                         case K_INT64: a.bind_int64(st, p, ld64(c.data + 8 * r)); break;
                         case K_HEX32: {
                             if (hb >= 8) throw std::runtime_error("at most 8 hex32 columns");
-                            char* out = hexrow + 64 * hb++;
+                            char* out = hexbuf[hb++];
                             const uint8_t* src = reinterpret_cast<const uint8_t*>(c.data) + 32 * r;
                             for (int b = 0; b < 32; ++b) {
                                 out[2 * b] = kHex[src[b] >> 4];
@@ -790,16 +772,6 @@ class LedgerWriter {
                         }
                     }
                 }
-            };
-            sqlite3_stmt* st = st1;
-            for (int64_t k = 0; k < n;) {
-                const bool multi = stk != nullptr && n - k >= kMultiRows;
-                st = multi ? stk : st1;
-                const int rows = multi ? kMultiRows : 1;
-                for (int q = 0; q < rows; ++q) {
-                    const int64_t r = order ? ld64(order + 8 * (k + q)) : k + q;
-                    bind_row(st, r, q * int(nc), hexbufs.data() + size_t(q) * 8 * 64);
-                }
                 int rc = a.step(st);
                 if (rc != SQLITE_DONE && rc != SQLITE_ROW) {
                     std::string m = a.errmsg(sh.db);
@@ -808,10 +780,7 @@ class LedgerWriter {
                 }
                 changes += a.changes(sh.db);
                 a.reset(st);
-                k += rows;
             }
-            if (stk) a.clear_bindings(stk);
-            st = st1;
             a.clear_bindings(st);
             const int64_t ns_used =
                 std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - ts0).count();
