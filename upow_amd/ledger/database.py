@@ -1252,6 +1252,133 @@ class Database:
         hit = np.nonzero(np.isin(want, have))[0]
         return [stake[k] for k in hit.tolist()]
 
+    # spend order and insert order of the object path's writes (manager._apply_block → remove_outputs,
+    # add_transaction_outputs): kept so SQL row order (rowid) is the same on both write paths
+    _GOV_INSERT_ORDER = ('inode_registration_output', 'validators_voting_power', 'delegates_voting_power',
+                         'validator_registration_output', 'inodes_ballot', 'validators_ballot')
+    _SPEND_ORDER = ('inode_registration_output', 'unspent_outputs', 'validators_voting_power',
+                    'delegates_voting_power', 'inodes_ballot', 'validators_ballot')
+
+    async def apply_object_block(self, block_row: dict, coinbase, transactions) -> int:
+        """The object path's block writes (manager._apply_block; reference manager.py:706-730) as ONE journal
+        batch — every table, governance ones included — plus the UTXO-index, governance-index and
+        chain-tip updates from the same in-memory data, so a block with governance transactions commits
+        like a native-path block (and carries undo records for rollback)."""
+        b = block_row
+        txs = [coinbase] + list(transactions)
+        rows = [await self._tx_row(t, b['hash']) for t in txs]  # coinbase row first, as add_transaction did
+        tx_sql = ('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, outputs_addresses, '
+                  'outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)')
+        stmts = [('INSERT INTO blocks (id, hash, content, address, random, difficulty, reward, timestamp) '
+                  'VALUES (?, ?, ?, ?, ?, ?, ?, ?)',
+                  [int(b['id']), b['hash'], b['content'], b['address'], int(b['random']), b['difficulty'], b['reward'],
+                   int(b['timestamp'])], 1, None, None, None)]
+        self.checkpoint('block')
+        stmts.append((tx_sql, [list(col) for col in zip(*rows)], len(rows), None, None, None))
+        self.checkpoint('transactions')
+        outs = self.split_outputs(list(transactions) + [coinbase])
+        created = []  # (table, key, payload fields) for the indexes
+        u = outs['unspent_outputs']
+        if u:
+            stmts.append(('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) VALUES (?, ?, ?, ?)',
+                          [[o[0] for o in u], np.array([o[1] for o in u], np.int64), [o[2] for o in u],
+                           [None if o[3] is None else str(int(bool(o[3]))) for o in u]], len(u), None, None, None))
+        for table in self._GOV_INSERT_ORDER:
+            g = outs[table]
+            if g:
+                stmts.append((f'INSERT INTO {table} (tx_hash, "index", address) VALUES (?, ?, ?)',
+                              [[o[0] for o in g], np.array([o[1] for o in g], np.int64), [o[2] for o in g]],
+                              len(g), None, None, None))
+        self.checkpoint('outputs')
+        tables = {'blocks', 'transactions', 'unspent_outputs', *self._GOV_INSERT_ORDER}
+        spends = defaultdict(list)
+        for t in transactions:
+            spends[self.spend_table(t.transaction_type)].extend((i.tx_hash, int(i.index)) for i in t.inputs)
+        mempool = bool(transactions) and not self._mempool_empty()
+        if mempool:
+            hashes = [t.hash() for t in transactions]
+            stmts.append(('DELETE FROM pending_transactions WHERE tx_hash = ?', [hashes], len(hashes), None,
+                          'SELECT EXISTS(SELECT 1 FROM pending_transactions)', None))
+        for table in self._SPEND_ORDER:
+            keys = spends.get(table)
+            if keys:
+                stmts.append((f'DELETE FROM {table} WHERE tx_hash = ? AND "index" = ?',
+                              [[h for h, _ in keys], np.array([i for _, i in keys], np.int64)], len(keys), None,
+                              None, len(keys)))
+        all_in = [k for t in transactions for k in ((i.tx_hash, int(i.index)) for i in t.inputs)]
+        if mempool and all_in:
+            stmts.append(('DELETE FROM pending_spent_outputs WHERE tx_hash = ? AND "index" = ?',
+                          [[h for h, _ in all_in], np.array([i for _, i in all_in], np.int64)], len(all_in), None,
+                          'SELECT EXISTS(SELECT 1 FROM pending_spent_outputs)', None))
+            tables |= {'pending_transactions', 'pending_spent_outputs'}
+        self.checkpoint('spent')
+
+        # ---- index records: created outputs (per table) and spent outpoints with their current payloads
+        from .utxo import pack_records
+        ins_recs, ins_pay = [], []
+        if u:
+            ins_recs.append(pack_records([(o[0], o[1]) for o in u], TAG_BY_TABLE['unspent_outputs']))
+            ins_pay.append(make_payload([o[4] for o in u], [_addr_bytes(o[2]) for o in u], [o[3] for o in u]))
+        for table in self._GOV_INSERT_ORDER:
+            g = outs[table]
+            if g:
+                ins_recs.append(pack_records([(o[0], o[1]) for o in g], TAG_BY_TABLE[table]))
+                ins_pay.append(make_payload([o[3] for o in g], [_addr_bytes(o[2]) for o in g]))
+        created_recs = np.concatenate(ins_recs) if ins_recs else np.zeros((0, 40), np.uint8)
+        created_pay = np.concatenate(ins_pay) if ins_pay else np.zeros(0, PAYLOAD_DTYPE)
+        sp_recs, sp_pay = [], []
+        for table in self._SPEND_ORDER:
+            keys = spends.get(table)
+            if keys:
+                tags, pay = self.utxo.lookup(keys)
+                present = tags == TAG_BY_TABLE[table]
+                keys = [k for k, ok in zip(keys, present) if ok]
+                if keys:
+                    sp_recs.append(pack_records(keys, TAG_BY_TABLE[table]))
+                    sp_pay.append(np.ascontiguousarray(pay[present]))
+        spent_recs = np.concatenate(sp_recs) if sp_recs else np.zeros((0, 40), np.uint8)
+        spent_pay = np.concatenate(sp_pay) if sp_pay else np.zeros(0, PAYLOAD_DTYPE)
+
+        enc = [self.encode(*st) for st in stmts]
+        meta = struct.pack('<qII', int(b['id']), len(created_recs), len(spent_recs)) + created_recs.tobytes() + \
+            spent_recs.tobytes() + spent_pay.tobytes()
+        seq = self.submit_batch(enc, tables, meta, int(b['id']))
+        # ---- the indexes and the chain-tip cache follow the commit point
+        if len(spent_recs):
+            self.utxo.erase_records(spent_recs)
+        if len(created_recs):
+            self.utxo.insert_records(created_recs, created_pay)
+        if self.gov is not None:
+            self._gov_apply_block(rows, outs, spends, int(b['timestamp']))
+        tip = dict(b)
+        tip['difficulty'], tip['reward'] = Decimal(tip['difficulty']), Decimal(tip['reward'])
+        self._tip_gen += 1
+        self._tip_cache = normalize_block(tip)
+        if mempool:
+            self._pending_empty = None
+            self._mempool_ver += 1
+        return seq
+
+    def _gov_apply_block(self, rows, outs, spends, block_ts: int):
+        """Governance-index update for one object-path block from its own rows: what GovernanceIndex.added
+        would read back through the SQL joins (address; amount = outputs_amounts[index]; voter =
+        inputs_addresses[index]; the block's timestamp)."""
+        ia = {r[1]: _arr(r[3]) for r in rows}
+        am = {r[1]: _arr(r[5]) for r in rows}
+        g = self.gov
+        with g.lock:
+            for table in self._SPEND_ORDER:
+                keys = spends.get(table)
+                if keys:
+                    g.removed(STAKE if table == 'unspent_outputs' else table, keys)
+            for o in outs['unspent_outputs']:
+                if o[3] is True or o[3] == 1:
+                    g.tables[STAKE].add((o[0], o[1]), o[2], _at(am[o[0]], o[1]), _at(ia[o[0]], o[1]), block_ts)
+            for table in self._GOV_INSERT_ORDER:
+                for o in outs[table]:
+                    g.tables[table].add((o[0], o[1]), o[2], _at(am[o[0]], o[1]), _at(ia[o[0]], o[1]), block_ts)
+            g.version += 1
+
     def _undo_blocks_in_index(self, from_id: int, tip: int) -> bool:
         """Roll the UTXO index back from ``tip`` to ``from_id - 1`` with the journal's undo records
         (created outpoints erased, spent outpoints re-inserted with their payloads, newest block first).

@@ -41,7 +41,17 @@ from ..utils.logger import get_logger
 from .utxo import TAG_BY_TABLE
 
 logger = get_logger(__name__)
-THREADS = int(os.environ.get('UPOW_CODEC_THREADS', '0')) or max(1, min(16, os.cpu_count() or 1))
+def _codec_threads() -> int:
+    """Host threads for the block codec: the CPUs this process may run on (affinity, not the machine
+    total), capped at 16, minus two for the ledger's materialiser threads that run concurrently."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    return max(1, min(16, avail) - 2)
+
+
+THREADS = int(os.environ.get('UPOW_CODEC_THREADS', '0')) or _codec_threads()
 ENABLED = os.environ.get('UPOW_FASTPATH', '1') != '0'
 timings: dict = {}
 last_path = None  # 'native' | 'object' for the last block (tests, metrics)

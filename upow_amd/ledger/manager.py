@@ -370,6 +370,26 @@ async def _apply_block(block_no, block_hash, block_content, address, random, dif
     SQLite transaction: a failure at any stage leaves the ledger and the UTXO index untouched (the
     reference deletes the half-written block instead, manager.py:718-723)."""
     database: Database = Database.instance
+    if database.writer is not None and block_no not in double_spend_dict:
+        # through the ledger journal like the native path (commit point + background materialisers);
+        # blocks of the double-spend exception table keep the synchronous path below, whose partial
+        # deletes and uniqueness errors are decided by SQL
+        from .database import numeric
+        if isinstance(content_time, datetime):
+            content_time = int(content_time.timestamp())
+        row = {'id': block_no, 'hash': block_hash, 'content': block_content, 'address': address, 'random': int(random),
+               'difficulty': numeric(difficulty, 1), 'reward': numeric(block_reward + fees, 6),
+               'timestamp': int(content_time)}
+        submitted = database._submitted
+        try:
+            await database.apply_object_block(row, coinbase_transaction, transactions)
+        except Exception as e:
+            if database._submitted != submitted:
+                raise  # committed to the journal: a failure after the commit point is not a rejection
+            logger.error(f'Transaction of {block_no} has not been added in block {e}')
+            Manager.difficulty = None
+            return False
+        return True
     try:
         with database.transaction():
             await database.add_block(block_no, block_hash, block_content, address, random, difficulty,
