@@ -44,17 +44,18 @@ def run(tid):
             time.sleep(target - time.time())
         if time.time() - t0 > seconds + 5:
             break
+        ts = time.time()
         try:
             ok = c.post(url + '/push_tx', json={'tx_hex': hx}).json().get('ok')
         except Exception:
             ok = False
         with lock:
-            res.append((k, time.time(), 1 if ok else 0))
+            res.append((k, time.time(), 1 if ok else 0, ts))
 ts = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
 [t.start() for t in ts]
 [t.join() for t in ts]
 with open(src + '.out', 'w') as f:
-    f.write(''.join(f'{k} {tp} {ok}\n' for k, tp, ok in res))
+    f.write(''.join(f'{k} {tp} {ok} {ts}\n' for k, tp, ok, ts in res))
 '''
 
 
@@ -93,8 +94,10 @@ def main():
         os.path.join(ROOT, 'gpurun_out')) else None)
     port = _port()
     url = f'http://127.0.0.1:{port}'
+    trace = os.path.join(data, 'blocks.jsonl')  # per-block apply windows (UPOW_TRACE_FILE)
     env = dict(os.environ, UPOW_DATA_DIR=data, UPOW_CORE_URL='', UPOW_START_DIFFICULTY=a.difficulty,
-               UPOW_RATE_LIMIT='0', PYTHONPATH=ROOT, UPOW_LOG_LEVEL='WARNING', UPOW_SNAPSHOT='0')
+               UPOW_RATE_LIMIT='0', PYTHONPATH=ROOT, UPOW_LOG_LEVEL='WARNING', UPOW_SNAPSHOT='0',
+               UPOW_TRACE_FILE=trace)
     if os.environ.get('UPOW_SOAK_PROFILE') == '1':
         env['UPOW_PROFILE_OUT'] = os.path.join(data, 'node.prof')
     node = subprocess.Popen([sys.executable, '-m', 'upow_amd.node', '--host', '127.0.0.1', '--port', str(port),
@@ -190,6 +193,7 @@ def main():
     t0 = time.time()
     errors = [0]
     lock = threading.Lock()
+    req = []  # (request start, request end) of every /push_tx
 
     def pusher(tid):
         c = httpx.Client(timeout=30)
@@ -200,8 +204,11 @@ def main():
             if time.time() - t0 > a.seconds + 5:
                 break
             tx = signed[k]
+            ts = time.time()
             try:
                 r = c.post(url + '/push_tx', json={'tx_hex': tx.hex()}).json()
+                with lock:
+                    req.append((ts, time.time()))
                 if not r.get('ok'):
                     raise RuntimeError(r)
                 with lock:
@@ -232,7 +239,8 @@ def main():
         for proc, out in kids:
             proc.wait()
             for ln in open(out):
-                k, tp, ok = ln.split()
+                k, tp, ok, ts = ln.split()
+                req.append((float(ts), float(tp)))
                 if ok == '1':
                     pushed[hashes[int(k)]] = float(tp)
                 else:
@@ -263,6 +271,20 @@ def main():
         if m:
             apply.setdefault(m.group(2), {})[m.group(1)] = float(m.group(3))
     steady_blocks = [b for b in blocks if b[1] <= t_push_end + 1]
+    # /push_tx request latency, overall and for requests that overlapped a block application
+    windows = []
+    if os.path.exists(trace):
+        for ln in open(trace):
+            r = json.loads(ln)
+            if r.get('ok') and r.get('txs', 0) > 0:
+                windows.append((r['t'] - r['ms'] / 1000.0, r['t']))
+    windows.sort()
+
+    def overlaps(a0, a1):
+        return any(w0 < a1 and a0 < w1 for w0, w1 in windows)
+    req_lat = sorted((b - a) * 1000 for a, b in req)
+    req_lat_blk = sorted((b - a) * 1000 for a, b in req if overlaps(a, b))
+    pq = lambda v, p: round(v[min(len(v) - 1, int(p * len(v)))], 2) if v else None
     intervals = [b2[1] - b1[1] for b1, b2 in zip(blocks, blocks[1:])]
     q = lambda p: round(lat[min(len(lat) - 1, int(p * len(lat)))], 2) if lat else None
     out = {
@@ -275,6 +297,11 @@ def main():
         'txs_per_block_max': max((b[2] for b in blocks), default=0),
         'block_apply_ms_mean': {k: round(1000 * v['sum'] / v['count'], 2) for k, v in apply.items() if v.get('count')},
         'miner_mhs_median': sorted(rates)[len(rates) // 2] if rates else None,
+        'push_tx_latency_ms': {'p50': pq(req_lat, 0.5), 'p99': pq(req_lat, 0.99), 'n': len(req_lat)},
+        'push_tx_latency_during_block_apply_ms': {'p50': pq(req_lat_blk, 0.5), 'p99': pq(req_lat_blk, 0.99),
+                                                  'n': len(req_lat_blk)},
+        'block_apply_windows': len(windows),
+        'block_apply_ms_max': round(max((w1 - w0) * 1000 for w0, w1 in windows), 1) if windows else None,
         'difficulty': a.difficulty, 'setup_s': round(setup_s, 1), 'data': 'synthetic keys, miner coinbases fanned out',
     }
     line = json.dumps(out)
