@@ -90,8 +90,7 @@ def main():
     addr = point_to_string(pub)
     sinks = [point_to_string(op.public_key(rng.randrange(1, op.oracle.N))) for _ in range(64)]
 
-    data = tempfile.mkdtemp(prefix='soak', dir=os.path.join(ROOT, 'gpurun_out') if os.path.isdir(
-        os.path.join(ROOT, 'gpurun_out')) else None)
+    data = tempfile.mkdtemp(prefix='soak')  # ledger files stay out of gpurun_out/ (size cap on the copy back)
     port = _port()
     url = f'http://127.0.0.1:{port}'
     trace = os.path.join(data, 'blocks.jsonl')  # per-block apply windows (UPOW_TRACE_FILE)
