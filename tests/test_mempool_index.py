@@ -1,0 +1,131 @@
+"""Host mempool index (ledger/mempool.py): journaled /push_tx admission against the SQL-only path.
+
+Two ledgers take the same admissions and blocks — one with the index (admission journals its rows, the
+checks read host memory), one with ``mempool_index = False`` (the reference's SQL INSERT/SELECT path,
+upow/database.py:93-115, 832-838) — and must give the same verdicts and the same mempool tables."""
+import asyncio
+from datetime import timedelta
+from decimal import Decimal
+
+import pytest
+
+from upow_amd import devnet
+from upow_amd.ledger import database as dbmod
+from upow_amd.ledger import fastpath, manager
+from upow_amd.ledger.database import Database, UniqueViolationError
+from upow_amd.models.transaction import Transaction, TransactionInput, TransactionOutput
+from upow_amd.wallet.builders import address_of, create_transaction
+
+GENESIS = 0xA11CE
+KEYS = [0x5EED + k for k in range(4)]
+
+
+@pytest.fixture(autouse=True)
+def _low_difficulty(monkeypatch):
+    monkeypatch.setattr(manager, 'START_DIFFICULTY', Decimal('1.0'))
+
+
+def _use(db):
+    Database.instance = db
+    manager.Manager.difficulty = None
+
+
+def _pending(db):
+    db.flush()
+    return (sorted(tuple(r) for r in db._q('SELECT tx_hash, tx_hex, inputs_addresses, fees FROM pending_transactions')),
+            sorted(tuple(r) for r in db._q('SELECT tx_hash, "index" FROM pending_spent_outputs')))
+
+
+async def _chain(blocks=6):
+    a = await Database.create()
+    b = await Database.create()
+    b.mempool_index = False
+    base = 1_700_000_000
+    for k in range(blocks):
+        for db in (a, b):
+            _use(db)
+            c = await devnet.mine_header(address_of(GENESIS), [], ts=base + 60 * k, device='cpu')
+            assert await fastpath.create_block_from_hex(c, [])
+    return a, b, base + 60 * blocks
+
+
+async def _admit_both(a, b, tx):
+    out = []
+    for db in (a, b):
+        _use(db)
+        try:
+            out.append(await db.add_pending_transaction(tx))
+        except UniqueViolationError:
+            out.append('dup')
+    assert out[0] == out[1], out
+    return out[0]
+
+
+def test_admission_matches_sql_path():
+    async def go():
+        a, b, ts = await _chain()
+        assert a.writer is not None and b.writer is not None
+        _use(a)
+        txs = []
+        for k in KEYS:  # each built after the previous one is pending: spendable outputs skip its inputs
+            _use(a)
+            txs.append(await create_transaction(GENESIS, address_of(k), '1.5'))
+            assert await _admit_both(a, b, txs[-1]) is True
+        assert a._mp is not None and len(a._mp.txs) == len(txs)
+        assert await _admit_both(a, b, txs[0]) is False  # its own inputs are pending-spent (reference order)
+        # same inputs, different outputs: a double spend against the mempool
+        ins = [TransactionInput(i.tx_hash, i.index, amount=i.amount, public_key=i.public_key) for i in txs[1].inputs]
+        ds = Transaction(ins, [TransactionOutput(address_of(KEYS[0]), Decimal('0.5'))])
+        ds.sign([GENESIS])
+        assert await _admit_both(a, b, ds) is False
+        assert _pending(a) == _pending(b)
+        assert await a.get_pending_spent_outputs([(i.tx_hash, i.index) for i in txs[2].inputs]) == \
+            await b.get_pending_spent_outputs([(i.tx_hash, i.index) for i in txs[2].inputs])
+        # a block confirming two of them: both leave the index and the tables
+        for db in (a, b):
+            _use(db)
+            c = await devnet.mine_header(address_of(GENESIS), txs[:2], ts=ts, device='cpu')
+            assert await fastpath.create_block_from_hex(c, [t.hex() for t in txs[:2]])
+        assert len(a._mp.txs) == 2
+        assert _pending(a) == _pending(b)
+        assert len(_pending(a)[0]) == 2
+        reloads = a.mempool_reloads
+        _use(a)
+        assert await a.get_need_propagate_transactions() == []
+        assert a.mempool_reloads == reloads  # blocks and admissions keep the index: no SQL reload
+    asyncio.run(go())
+
+
+def test_block_after_empty_decision_deletes_late_admission():
+    """A tx admitted after a block found the mempool empty, and confirmed by that block: the block's
+    batch carries no mempool deletes, so the confirm step journals a follow-up delete."""
+    async def go():
+        a, _, _ = await _chain(4)
+        _use(a)
+        tx = await create_transaction(GENESIS, address_of(KEYS[0]), '1')
+        assert await a.add_pending_transaction(tx)
+        a._mempool_confirm(False, hashes=[tx.hash()], inputs=[(i.tx_hash, i.index) for i in tx.inputs])
+        assert a._mp.empty()
+        assert _pending(a) == ([], [])
+    asyncio.run(go())
+
+
+def test_stale_propagation_and_python_write_invalidate(monkeypatch):
+    async def go():
+        a, _, _ = await _chain(4)
+        _use(a)
+        tx = await create_transaction(GENESIS, address_of(KEYS[1]), '1')
+        assert await a.add_pending_transaction(tx)
+        assert await a.get_need_propagate_transactions() == []
+        real = dbmod._utcnow
+        monkeypatch.setattr(dbmod, '_utcnow', lambda: real() + timedelta(seconds=700))
+        assert await a.get_need_propagate_transactions() == [tx.hex()]
+        await a.update_pending_transactions_propagation_time([tx.hash()])  # Python-side write: index dropped
+        assert a._mp is None
+        assert await a.get_need_propagate_transactions() == []
+        assert a._mp is not None and a._mp.has_tx(tx.hash())
+        await a.remove_pending_transaction(tx.hash())
+        assert a._mp is None
+        assert await a.get_pending_spent_outputs([(i.tx_hash, i.index) for i in tx.inputs]) == \
+            [(i.tx_hash, i.index) for i in tx.inputs]  # the spent rows stay (reference behaviour)
+    asyncio.run(go())

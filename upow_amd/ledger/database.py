@@ -36,6 +36,7 @@ from ..utils.codec import (AddressFormat, OutputType, TransactionType, normalize
 from ..utils.logstore import LogStore
 from ..utils.logger import get_logger
 from .governance import GOV_TABLES, STAKE, GovernanceIndex
+from .mempool import MempoolIndex
 from .utxo import PAYLOAD_DTYPE, TAG_BY_TABLE, UtxoIndex, make_payload
 
 logger = get_logger(__name__)
@@ -310,6 +311,9 @@ class Database:
         self._genesis_cache: Optional[str] = None
         self._pending_empty: Optional[bool] = None
         self._mempool_ver = 0
+        self._mp: Optional[MempoolIndex] = None  # ledger/mempool.py; None: (re)load from SQL on next use
+        self.mempool_reloads = 0
+        self.mempool_index = os.environ.get('UPOW_MEMPOOL_INDEX', '1') != '0'
         self._conn.execute('PRAGMA foreign_keys = ON')
         self._conn.execute('PRAGMA journal_mode = WAL')
         self._conn.execute('PRAGMA synchronous = ' + ('OFF' if path == ':memory:' else 'NORMAL'))
@@ -476,6 +480,35 @@ class Database:
                 applied = target
             seen[sh] = max(seen.get(sh, 0), applied)
 
+    def _fresh(self, table: str) -> bool:
+        """Does ``table`` already hold every journaled batch that writes it? (never waits)"""
+        if self.writer is None:
+            return True
+        seq = self._table_seq.get(table, 0)
+        sh = SHARD_OF_TABLE.get(table, 0)
+        seen = self._applied_seen
+        if seq <= seen.get(sh, 0) or seq <= seen.get(-1, 0):
+            return True
+        applied = self.writer.applied(sh)
+        if applied >= seq:
+            seen[sh] = max(seen.get(sh, 0), applied)
+            return True
+        return False
+
+    def lagging(self) -> bool:
+        """Is any journaled batch not yet in SQL? (never waits)"""
+        if self.writer is None:
+            return False
+        target = self._submitted
+        return target > self._applied_seen.get(-1, 0) and self.writer.applied(-1) < target
+
+    async def asettle(self, tables: Optional[frozenset] = None):
+        """:meth:`_settle` for an event loop: the wait runs on an executor thread (the native wait
+        releases the GIL), so one request waiting for the materialiser does not stall the others."""
+        if self.lagging():
+            import asyncio
+            await asyncio.get_running_loop().run_in_executor(None, self._settle, tables)
+
     def flush(self):
         """Block until the SQL tables hold every committed block (tests, tools, shutdown)."""
         self._settle(None)
@@ -496,6 +529,7 @@ class Database:
         if tables is None or 'pending_transactions' in tables or 'pending_spent_outputs' in tables:
             self._pending_empty = None
             self._mempool_ver += 1
+            self._mp = None
 
     def submit_batch(self, stmts: List[bytes], tables: Iterable[str], meta: bytes = b'', block_id: int = -1) -> int:
         """Commit a batch of encoded statements (``lib().ledger_encode_stmt``) through the journal. The
@@ -671,6 +705,51 @@ class Database:
         return self._xm(f'DELETE FROM {table} WHERE tx_hash = ? AND "index" = ?',
                         [(h, int(i)) for h, i in inputs]).rowcount
 
+    _PENDING = frozenset(('pending_transactions', 'pending_spent_outputs'))
+
+    def _mempool(self) -> Optional[MempoolIndex]:
+        """The host mempool index (ledger/mempool.py), loaded from SQL when dropped; None without the
+        journal writer (SQL is then always current) or with ``UPOW_MEMPOOL_INDEX=0``."""
+        if self.writer is None or not self.mempool_index:
+            return None
+        mp = self._mp
+        if mp is None:
+            self._settle(self._PENDING)
+            with self.lock:
+                mp = MempoolIndex(self._conn.execute('SELECT tx_hash, propagation_time FROM pending_transactions'),
+                                  self._conn.execute('SELECT tx_hash, "index" FROM pending_spent_outputs'))
+                self._mp = mp
+            self.mempool_reloads += 1
+        return mp
+
+    def _mempool_confirm(self, mempool_deleted: bool, txids=None, in_keys=None, hashes=None, inputs=None):
+        """A committed block's txs and inputs leave the mempool index. A tx of the block admitted after
+        the block found the mempool empty (its batch then carries no mempool deletes) is deleted from
+        the tables by a follow-up batch, journaled after the admission's own INSERTs."""
+        mp = self._mp
+        if mp is None:
+            return
+        if txids is not None:
+            hit_tx, hit_in = mp.confirm_raw(txids, in_keys)
+        else:
+            hit_tx, hit_in = mp.confirm(hashes or [], inputs or [])
+        if not (hit_tx or hit_in):
+            return
+        self._pending_empty = None
+        self._mempool_ver += 1
+        if mempool_deleted:
+            return
+        stmts = []
+        if hit_tx:
+            stmts.append(self.encode('DELETE FROM pending_transactions WHERE tx_hash = ?', [[h.hex() for h in hit_tx]],
+                                     len(hit_tx)))
+        if hit_in:
+            stmts.append(self.encode('DELETE FROM pending_spent_outputs WHERE tx_hash = ? AND "index" = ?',
+                                     [[k[:32].hex() for k in hit_in],
+                                      np.array([int.from_bytes(k[32:36], 'little') for k in hit_in], np.int64)],
+                                     len(hit_in)))
+        self.submit_batch(stmts, self._PENDING)
+
     def _pending_spent_set(self) -> Set[Tuple[str, int]]:
         return {(r[0], r[1]) for r in self._q('SELECT tx_hash, "index" FROM pending_spent_outputs')}
 
@@ -685,6 +764,9 @@ class Database:
             logger.error('Error in adding transaction.')
             return False
         inputs_addresses = [await _input_address(i) for i in transaction.inputs]
+        mp = self._mempool() if verify else None
+        if mp is not None:
+            return self._admit(mp, transaction, tx_hex, inputs_addresses)
         try:
             self._x('INSERT INTO pending_transactions (tx_hash, tx_hex, inputs_addresses, fees, propagation_time) '
                     'VALUES (?, ?, ?, ?, ?)',
@@ -693,6 +775,32 @@ class Database:
         except sqlite3.IntegrityError as e:
             raise UniqueViolationError(str(e)) from e
         await self.add_transactions_pending_spent_outputs([transaction])
+        return True
+
+    def _admit(self, mp: MempoolIndex, transaction: Transaction, tx_hex: str, inputs_addresses: list) -> bool:
+        """Journaled admission of a verified tx: reserve it in the mempool index, then commit its
+        pending_transactions and pending_spent_outputs rows as one batch (both under the index lock,
+        so a block that later finds the tx in the index knows its rows are already journaled)."""
+        tx_hash = sha256(tx_hex)
+        ptime = int(_utcnow().replace(tzinfo=timezone.utc).timestamp())
+        inputs = [(i.tx_hash, int(i.index)) for i in transaction.inputs]
+        with mp.lock:
+            why = mp.try_add(tx_hash, ptime, inputs)
+            if why == 'duplicate':
+                raise UniqueViolationError(f'UNIQUE constraint failed: pending_transactions.tx_hash ({tx_hash})')
+            if why is not None:
+                logger.error(f'Double spending in pending {tx_hash}')
+                return False
+            stmts = [self.encode('INSERT INTO pending_transactions (tx_hash, tx_hex, inputs_addresses, fees, '
+                                 'propagation_time) VALUES (?, ?, ?, ?, ?)',
+                                 [tx_hash, tx_hex, _j(inputs_addresses), numeric(transaction.fees, 6), ptime], 1)]
+            if inputs:
+                stmts.append(self.encode('INSERT INTO pending_spent_outputs (tx_hash, "index") VALUES (?, ?)',
+                                         [[h for h, _ in inputs], np.array([i for _, i in inputs], np.int64)],
+                                         len(inputs)))
+            self.submit_batch(stmts, self._PENDING)
+        self._pending_empty = False
+        self._mempool_ver += 1
         return True
 
     async def remove_pending_transaction(self, tx_hash: str):
@@ -799,7 +907,11 @@ class Database:
                                               limit: int = MAX_BLOCK_SIZE_HEX) -> List[str]:
         now = int(_utcnow().replace(tzinfo=timezone.utc).timestamp())
         # the node's middleware asks this on EVERY request: only stale txs can be returned, so when no
-        # pending tx is older than the delta the answer is [] without ordering the whole mempool
+        # pending tx is older than the delta the answer is [] without ordering the whole mempool (from
+        # the mempool index when there is one: no SQL at all)
+        mp = self._mempool()
+        if mp is not None and not mp.maybe_stale(now, last_propagation_delta):
+            return []
         if self._q1('SELECT 1 FROM pending_transactions WHERE propagation_time < ? LIMIT 1',
                     (now - last_propagation_delta,)) is None:
             return []
@@ -932,8 +1044,17 @@ class Database:
         d['reward'] = Decimal(d['reward'])
         return normalize_block(d)
 
+    def _q1_present(self, sql: str, args: tuple):
+        """``_q1`` for rows that never change once written (a confirmed tx by hash): a row already in
+        SQL is the answer, so the materialiser is only waited for when the row is not there yet. (Rows
+        leave ``transactions`` only through rollback, which runs on the Python connection after a full
+        settle.)"""
+        with self.lock:
+            r = self._conn.execute(sql, args).fetchone()
+        return r if r is not None else self._q1(sql, args)
+
     async def get_transaction(self, tx_hash: str, check_signatures: bool = True):
-        res = self._q1('SELECT tx_hex, block_hash FROM transactions WHERE tx_hash = ?', (tx_hash,))
+        res = self._q1_present('SELECT tx_hex, block_hash FROM transactions WHERE tx_hash = ?', (tx_hash,))
         if res is None:
             return None
         tx = await Transaction.from_hex(res['tx_hex'], check_signatures)
@@ -950,12 +1071,20 @@ class Database:
         return d
 
     async def get_transaction_info(self, tx_hash: str) -> Optional[dict]:
-        res = self._q1('SELECT * FROM transactions WHERE tx_hash = ?', (tx_hash,))
+        res = self._q1_present('SELECT * FROM transactions WHERE tx_hash = ?', (tx_hash,))
         return self._info_row(res) if res is not None else None
 
     async def get_transactions_info(self, tx_hashes: List[str]) -> Dict[str, dict]:
         out = {}
         hashes = list(dict.fromkeys(tx_hashes))
+        if len(hashes) <= 32:  # a pushed tx's funding txs: as _q1_present, without a settle when all are in
+            with self.lock:
+                for r in self._conn.execute(f'SELECT * FROM transactions WHERE tx_hash IN '
+                                            f'({",".join("?" * len(hashes))})', hashes):
+                    out[r['tx_hash']] = self._info_row(r)
+            if len(out) == len(hashes):
+                return out
+            hashes = [h for h in hashes if h not in out]
         for k in range(0, len(hashes), 500):
             chunk = hashes[k:k + 500]
             for r in self._q(f'SELECT * FROM transactions WHERE tx_hash IN ({",".join("?" * len(chunk))})', chunk):
@@ -1126,6 +1255,9 @@ class Database:
 
     def _mempool_empty(self) -> bool:
         """Are both mempool tables empty? Cached until a Python-side write touches them."""
+        mp = self._mp
+        if mp is not None:
+            return mp.empty()
         if self._pending_empty is None:
             self._pending_empty = self._q1('SELECT EXISTS(SELECT 1 FROM pending_transactions) OR '
                                            'EXISTS(SELECT 1 FROM pending_spent_outputs)')[0] == 0
@@ -1236,6 +1368,8 @@ class Database:
         if mempool:
             self._pending_empty = None
             self._mempool_ver += 1
+        if n:
+            self._mempool_confirm(bool(mempool), txids=np.asarray(tx_cols[0][1]).reshape(-1, 32), in_keys=in_keys)
         if self.gov is not None and n_in:
             hit = self._stake_spent(spent)
             if hit:
@@ -1357,6 +1491,8 @@ class Database:
         if mempool:
             self._pending_empty = None
             self._mempool_ver += 1
+        if transactions:
+            self._mempool_confirm(mempool, hashes=[t.hash() for t in transactions], inputs=all_in)
         return seq
 
     def _gov_apply_block(self, rows, outs, spends, block_ts: int):
@@ -1560,11 +1696,13 @@ class Database:
     # lookups (database.py:788-825): a block's outpoints go to the HBM/host index in one batch; a
     # handful of them (one tx at /push_tx) on the GPU backend go to SQLite's outpoint index instead —
     # a device round trip costs ~1 ms when the card is busy (a co-located miner keeps every CU
-    # occupied), an indexed probe ~5 us, and both hold the same set.
+    # occupied), an indexed probe ~5 us, and both hold the same set once the table is materialised.
+    # While the materialiser is still writing a just-committed block into the table, the index
+    # (current at the commit point) answers: waiting for the table would cost tens of ms.
     SMALL_LOOKUP = 16
 
     def _filter_outputs(self, table: str, outputs):
-        if len(outputs) > self.SMALL_LOOKUP or self.utxo.backend_name != 'gpu':
+        if len(outputs) > self.SMALL_LOOKUP or self.utxo.backend_name != 'gpu' or not self._fresh(table):
             return self.utxo.filter(outputs, TAG_BY_TABLE[table])
         uniq = list(dict.fromkeys((h, int(i)) for h, i in outputs))
         found = set(self._select_outpoints(table, uniq))
@@ -1603,6 +1741,9 @@ class Database:
         return sha256(''.join(r[0] + bytes([r[1]]).hex() for r in rows))
 
     async def get_pending_spent_outputs(self, outputs):
+        mp = self._mempool()
+        if mp is not None:
+            return mp.spent_of(outputs)
         return self._select_outpoints('pending_spent_outputs', outputs)
 
     async def set_unspent_outputs_addresses(self):

@@ -1,0 +1,105 @@
+"""Host-memory index of the mempool tables, so ``/push_tx`` admission never waits for SQL.
+
+reference: ``add_pending_transaction`` (upow/database.py:93-115) INSERTs into ``pending_transactions``
+and ``pending_spent_outputs``, and ``verify_pending`` asks ``get_pending_spent_outputs``
+(database.py:832-838) whether an input is already spent by a mempool tx; ``create_block`` deletes the
+confirmed txs and their inputs from both tables (manager.py:717-730). Here block writes reach SQLite
+through the journal's background materialiser (csrc/ledger_writer.cpp), so a SQL read of a mempool table
+right after a block has to wait for that block's rows to land (tens of ms for a full block). This index
+holds what admission needs — the pending tx hashes (with their propagation time) and the outpoints they
+spend — and follows every writer of the two tables:
+
+* admission adds the tx here and journals its two INSERTs as one small batch (no FK wait: the inputs were
+  just found unspent, so their txs are confirmed);
+* a block removes its txs and inputs here when it commits (native and object paths);
+* any other Python-side write to a mempool table drops the index; the next use re-reads it from SQL.
+
+Keys are raw bytes: 32-byte tx hashes, 36-byte outpoints (txid || index u32 LE), the layout of the
+block codec's input records, so a block's removal is a slice of its arrays, not a hex round trip.
+"""
+from __future__ import annotations
+
+import threading
+from typing import Dict, Iterable, List, Optional, Set, Tuple
+
+import numpy as np
+
+
+def outpoint_key(tx_hash: str, index: int) -> bytes:
+    return bytes.fromhex(tx_hash) + int(index).to_bytes(4, 'little')
+
+
+def _rows_raw(arr: np.ndarray, width: int) -> List[bytes]:
+    """The leading ``width`` bytes of each row of an n x k uint8 array, as bytes objects."""
+    a = np.ascontiguousarray(np.asarray(arr, dtype=np.uint8)[:, :width])
+    buf = a.tobytes()
+    return [buf[k:k + width] for k in range(0, len(buf), width)]
+
+
+class MempoolIndex:
+    def __init__(self, tx_rows: Iterable[Tuple[str, int]], spent_rows: Iterable[Tuple[str, int]]):
+        self.lock = threading.Lock()
+        self.txs: Dict[bytes, int] = {bytes.fromhex(h): int(t) for h, t in tx_rows}
+        self.spent: Set[bytes] = {outpoint_key(h, i) for h, i in spent_rows}
+        self.min_ptime: Optional[int] = min(self.txs.values()) if self.txs else None
+
+    def empty(self) -> bool:
+        return not self.txs and not self.spent
+
+    def has_tx(self, tx_hash: str) -> bool:
+        return bytes.fromhex(tx_hash) in self.txs
+
+    def spent_of(self, outputs: Iterable[Tuple[str, int]]) -> List[Tuple[str, int]]:
+        """The outpoints among ``outputs`` that a mempool tx already spends (unique, first seen)."""
+        seen = dict.fromkeys((h, int(i)) for h, i in outputs)
+        return [o for o in seen if outpoint_key(*o) in self.spent]
+
+    def try_add(self, tx_hash: str, ptime: int, inputs: List[Tuple[str, int]]) -> Optional[str]:
+        """Reserve a tx and its inputs (caller holds ``lock``); returns why it cannot be added, or None."""
+        h = bytes.fromhex(tx_hash)
+        if h in self.txs:
+            return 'duplicate'
+        keys = [outpoint_key(a, i) for a, i in inputs]
+        if any(k in self.spent for k in keys):
+            return 'double spend'
+        self.txs[h] = int(ptime)
+        self.spent.update(keys)
+        if self.min_ptime is None or ptime < self.min_ptime:
+            self.min_ptime = int(ptime)
+        return None
+
+    def _confirm(self, tx_keys: List[bytes], in_keys: List[bytes]) -> Tuple[List[bytes], List[bytes]]:
+        with self.lock:
+            hit_tx = []
+            if self.txs:
+                pop = self.txs.pop
+                hit_tx = [k for k in tx_keys if pop(k, None) is not None]
+            hit_in = []
+            if self.spent and in_keys:
+                s = self.spent
+                hit_in = [k for k in in_keys if k in s]
+                s.difference_update(hit_in)
+            if not self.txs:
+                self.min_ptime = None
+            return hit_tx, hit_in
+
+    def confirm_raw(self, txids: np.ndarray, in_keys: np.ndarray) -> Tuple[List[bytes], List[bytes]]:
+        """A committed block's txs (n x 32) and spent outpoints (n x >=36 records) leave the mempool;
+        returns the raw tx hashes and outpoints that were in it."""
+        return self._confirm(_rows_raw(txids, 32) if len(txids) else [],
+                             _rows_raw(in_keys, 36) if len(in_keys) else [])
+
+    def confirm(self, tx_hashes: List[str], inputs: List[Tuple[str, int]]) -> Tuple[List[bytes], List[bytes]]:
+        return self._confirm([bytes.fromhex(h) for h in tx_hashes], [outpoint_key(h, i) for h, i in inputs])
+
+    def maybe_stale(self, now: int, delta: int) -> bool:
+        """Could a pending tx be older than ``delta`` seconds? ``min_ptime`` only moves down between
+        recomputes, so False is exact and True is re-checked against the current entries."""
+        with self.lock:
+            if self.min_ptime is None or now - self.min_ptime <= delta:
+                return False
+            self.min_ptime = min(self.txs.values()) if self.txs else None
+            return self.min_ptime is not None and now - self.min_ptime > delta
+
+
+__all__ = ['MempoolIndex', 'outpoint_key']
