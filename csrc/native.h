@@ -38,6 +38,10 @@ std::vector<uint8_t> sha256_batch_gpu(const uint8_t* data, int64_t nbytes, const
 // verify items: 160-byte records {qx LE, qy LE, r LE, s LE, e = SHA-256 digest BE}
 // status: 1 valid, 0 invalid, 2 key off-curve, 3 r/s out of range
 std::vector<uint8_t> p256_verify_host(const uint8_t* items, int64_t n, int threads);
+// one 160-byte VerifyItem on 64-bit limbs (csrc/p256_host.cpp); status as p256_verify_host
+uint8_t p256_verify_one_host64(const uint8_t* item);
+// p256.hip's fixed-base table: 32 x 256 affine points, each x[8] y[8] little-endian u32 words
+const void* p256_g_table_host();
 std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n);
 void p256_decompress_host(const uint8_t* in33, int64_t n, uint8_t* out64, uint8_t* ok);
 void p256_decompress_gpu(const uint8_t* in33, int64_t n, uint8_t* out64, uint8_t* ok);

@@ -82,6 +82,8 @@ static const std::vector<aff>& g_table() {
     return g_tab;
 }
 
+const void* p256_g_table_host() { return g_table().data(); }
+
 UPOW_HD jac mul_g(const fe& k, const aff* tab) {
     jac acc = jac_inf();
     for (int j = 0; j < kGWin; ++j) {
@@ -265,9 +267,17 @@ std::vector<uint8_t> p256_verify_host(const uint8_t* items, int64_t n, int threa
     std::vector<uint8_t> st(static_cast<size_t>(n));
     const aff* tab = g_table().data();
     const VerifyItem* it = reinterpret_cast<const VerifyItem*>(items);
+    static const bool legacy = [] {
+        const char* v = std::getenv("UPOW_P256_HOST32");
+        return v && v[0] == '1';
+    }();
     threads = int(std::max<int64_t>(1, std::min<int64_t>(threads, n)));
     auto work = [&](int t) {
-        for (int64_t i = t; i < n; i += threads) st[i] = verify_one_host(it[i], tab);
+        if (legacy)  // UPOW_P256_HOST32=1: the 32-bit-limb field code the GPU kernel uses
+            for (int64_t i = t; i < n; i += threads) st[i] = verify_one_host(it[i], tab);
+        else
+            for (int64_t i = t; i < n; i += threads)
+                st[i] = p256_verify_one_host64(reinterpret_cast<const uint8_t*>(&it[i]));
     };
     if (threads <= 1) {
         work(0);

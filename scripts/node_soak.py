@@ -115,6 +115,13 @@ def main():
     miner = subprocess.Popen([sys.executable, '-m', 'upow_amd.miner', addr, '1', url + '/', '--refresh', '10', *chunk],
                              env=env, cwd=ROOT, stdout=miner_log, stderr=subprocess.STDOUT)
     t_start = time.time()
+    phase = ['setup']
+
+    def heartbeat():  # progress on stdout: a quiet minute-long setup must not look like a hang
+        while node.poll() is None:
+            time.sleep(15)
+            print(f'[soak] {time.time() - t_start:.0f}s phase={phase[0]}', flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
 
     def height():
         return client.get(url + '/get_mining_info').json()['result']['last_block'].get('id', 0)
@@ -190,6 +197,7 @@ def main():
     signed = [make_tx(h, i, amount, [(sinks[k % len(sinks)], amount - fee)])
               for k, (h, i, amount) in enumerate(pool[:int(a.rate * a.seconds) + 1])]
     t0 = time.time()
+    phase[0] = 'push'
     errors = [0]
     lock = threading.Lock()
     req = []  # (request start, request end) of every /push_tx
@@ -246,6 +254,7 @@ def main():
                     errors[0] += 1
     n = len(pushed) + errors[0]
     t_push_end = time.time()
+    phase[0] = 'drain'
     # drain: wait until everything pushed is in a block (or 4 block intervals)
     deadline = time.time() + 120
     while sum(h in included for h in list(pushed)) < len(pushed) and time.time() < deadline:

@@ -1,8 +1,10 @@
 """K14 utxo_address_scan throughput on one MI355X: fill the HBM UTXO table to ~45 % load with random
 outpoints owned by 1 000 addresses, then time address queries (one full-table scan each).
 
-Bytes per scan = capacity x 48 B key slots (meta words; the 80 B payload line is read only for
-live slots whose tag matches), so the figure of merit is slots/s and the effective HBM rate."""
+The figure of merit is slots/s. ``logical_key_GB_per_s`` = capacity x 48 B key slots per scan time: the
+bytes a scan is DEFINED over, not the bytes it moves — the kernel reads only each slot's meta words (the
+80 B payload line only for live slots whose tag matches), so the HBM traffic is lower; take that from
+rocprofv3 ``--pmc FETCH_SIZE`` on this script, not from this figure."""
 import json
 import os
 import sys
@@ -12,7 +14,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from upow_amd.ledger.utxo import PAYLOAD_DTYPE, UtxoIndex  # noqa: E402
+from upow_amd.ledger.utxo import PAYLOAD_DTYPE, STAKE_ANY, UtxoIndex  # noqa: E402
 
 
 def main(n=int(os.environ.get('N', 7_500_000)), queries=50):
@@ -34,16 +36,16 @@ def main(n=int(os.environ.get('N', 7_500_000)), queries=50):
         done += m
     L, h = idx.be.L, idx.be.h
     cap = L.utxo_capacity(h)
-    L.utxo_address_scan(h, bytes(owners[0, :33]), 1)  # warm
+    L.utxo_address_scan(h, bytes(owners[0, :33]), 1, STAKE_ANY)  # warm
     t = time.perf_counter()
     hits = 0
     for q in range(queries):
-        raw, _, _ = L.utxo_address_scan(h, bytes(owners[q % 1000, :33]), 1)
+        raw, _, _ = L.utxo_address_scan(h, bytes(owners[q % 1000, :33]), 1, STAKE_ANY)
         hits += len(raw) // 40
     dt = (time.perf_counter() - t) / queries
     print(json.dumps({'live': len(idx), 'capacity': cap, 'ms_per_query': round(dt * 1e3, 3),
                       'slots_per_s': round(cap / dt / 1e9, 2), 'unit': 'G slots/s',
-                      'key_GB_per_s': round(cap * 48 / dt / 1e9, 1), 'avg_hits': hits / queries}))
+                      'logical_key_GB_per_s': round(cap * 48 / dt / 1e9, 1), 'avg_hits': hits / queries}))
 
 
 if __name__ == '__main__':

@@ -99,6 +99,38 @@ def test_mining_flow_and_queries(node):
     assert series['upow_blocks_rejected_total{path="push"}'] >= 1
 
 
+def test_push_tx_direct_path_matches_routed(node, monkeypatch):
+    """POST /push_tx with a JSON body bypasses the framework router (node/main.py _push_tx_direct): the
+    responses, status codes and error envelopes must be the routed endpoint's."""
+    client, main = node
+    from upow_amd.wallet.builders import address_of
+    a, b = address_of(KEY_A), address_of(KEY_B)
+    for k in range(1, 3):
+        assert _mine(client, a, 1_700_000_000 + k) == {'ok': True}
+    from starlette.testclient import TestClient
+    raw = TestClient(main.app, base_url='http://testserver', raise_server_exceptions=False)  # 500s as responses
+    cases = [{'tx_hex': 'zz'}, {'tx_hex': '00' * 40}, {'tx_hex': 'ab', 'extra': 1}]
+    got = {}
+    for fast in (True, False):
+        monkeypatch.setattr(main, '_PUSH_FAST', fast)
+        got[fast] = [(r.status_code, r.json()) for r in (raw.post('/push_tx', json=c) for c in cases)]
+        got[fast].append((lambda r: (r.status_code, r.headers['access-control-allow-origin']))(
+            raw.post('/push_tx', content=b'{not json', headers={'content-type': 'application/json'})))
+    assert got[True] == got[False]
+    assert got[True][0][0] == 500 and got[True][0][1]['ok'] is False
+
+    async def mk():
+        from upow_amd.wallet.builders import create_transaction
+        return await create_transaction(KEY_A, b, '0.5')
+    tx = asyncio.run(mk())
+    monkeypatch.setattr(main, '_PUSH_FAST', True)
+    r = client.post('/push_tx', json={'tx_hex': tx.hex()})
+    assert r.status_code == 200 and r.json() == {'ok': True, 'result': 'Transaction has been accepted', 'tx_hash': tx.hash()}
+    assert r.headers['access-control-allow-origin'] == '*'
+    monkeypatch.setattr(main, '_PUSH_FAST', False)
+    assert client.post('/push_tx', json={'tx_hex': tx.hex()}).json() == {'ok': False, 'error': 'Transaction just added'}
+
+
 def test_rate_limit_and_ip_filter(node):
     client, main = node
     for _ in range(3):

@@ -19,14 +19,14 @@ HDRS="csrc/native.h csrc/sha256_common.h csrc/p256_field.h"
 if stale "$OUT/p256.o" csrc/p256.hip $HDRS; then
   /opt/rocm/bin/hipcc --offload-arch=gfx950 $CFLAGS $SAN_HOST -c csrc/p256.hip -o "$OUT/p256.o"
 fi
-for f in csrc/sha256_host.cpp csrc/sha256_ni.cpp csrc/base58.cpp tools/host_selftest.cpp; do
+for f in csrc/sha256_host.cpp csrc/sha256_ni.cpp csrc/base58.cpp csrc/p256_host.cpp tools/host_selftest.cpp; do
   o="$OUT/$(basename "${f%.cpp}").o"
   if stale "$o" "$f" $HDRS; then
     $CXX $CFLAGS -fsanitize=address,undefined -fno-sanitize-recover=undefined -pthread -c "$f" -o "$o"
   fi
 done
 $CXX -fsanitize=address,undefined -pthread "$OUT"/host_selftest.o "$OUT"/p256.o "$OUT"/sha256_host.o \
-  "$OUT"/sha256_ni.o "$OUT"/base58.o -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib -o "$OUT/host_selftest"
+  "$OUT"/sha256_ni.o "$OUT"/base58.o "$OUT"/p256_host.o -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib -o "$OUT/host_selftest"
 # leak checking off: the HIP runtime keeps process-lifetime allocations
 ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 "$OUT/host_selftest"
 # ThreadSanitizer on the host worker pool (csrc/thread_pool.h)

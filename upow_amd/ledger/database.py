@@ -791,7 +791,8 @@ class Database:
             if why is not None:
                 logger.error(f'Double spending in pending {tx_hash}')
                 return False
-            stmts = [self.encode('INSERT INTO pending_transactions (tx_hash, tx_hex, inputs_addresses, fees, '
+            # OR IGNORE: a statement error would stop the materialiser; the index already refused duplicates
+            stmts = [self.encode('INSERT OR IGNORE INTO pending_transactions (tx_hash, tx_hex, inputs_addresses, fees, '
                                  'propagation_time) VALUES (?, ?, ?, ?, ?)',
                                  [tx_hash, tx_hex, _j(inputs_addresses), numeric(transaction.fees, 6), ptime], 1)]
             if inputs:

@@ -78,6 +78,10 @@ def start() -> Optional[LedgerWorker]:
     global _worker
     with _lock:
         if _worker is None and enabled():
+            # the GIL changes hands every switch interval when both threads run Python: at CPython's
+            # 5 ms default a request arriving during a block's Python stages waits up to 5 ms per turn
+            import sys
+            sys.setswitchinterval(float(os.environ.get('UPOW_SWITCH_INTERVAL_MS', '1')) / 1000.0)
             _worker = LedgerWorker()
             logger.info('ledger worker thread started')
         return _worker

@@ -49,6 +49,12 @@ def ecdsa_verify(sig: Tuple[int, int], msg, q: Point) -> bool:
     return op.verify(sig, msg, q)
 
 
+async def ecdsa_verify_async(sig: Tuple[int, int], msg, q: Point) -> bool:
+    """:func:`ecdsa_verify`, batched across concurrent /push_tx requests (ops/p256.py verify_async)."""
+    from ..ops import p256 as op
+    return await op.verify_async(sig, msg, q)
+
+
 # C-level field getters for the hex() memo fingerprint (operator.attrgetter + map, no Python loop)
 _IN_KEY = attrgetter('tx_hash', 'index', 'input_type')
 _OUT_KEY = attrgetter('address_bytes', 'amount', 'transaction_type')
@@ -189,16 +195,16 @@ class TransactionInput:
         except AssertionError:
             return False
         # raw bytes first, then the ASCII-hex string (transaction_input.py:107-109)
-        return ecdsa_verify(self.signed, bytes.fromhex(input_tx), public_key) or \
-            ecdsa_verify(self.signed, input_tx, public_key)
+        return await ecdsa_verify_async(self.signed, bytes.fromhex(input_tx), public_key) or \
+            await ecdsa_verify_async(self.signed, input_tx, public_key)
 
     async def verify_revoke_tx(self, input_tx: str) -> bool:
         try:
             public_key = await self.get_voter_public_key()
         except AssertionError:
             return False
-        return ecdsa_verify(self.signed, bytes.fromhex(input_tx), public_key) or \
-            ecdsa_verify(self.signed, input_tx, public_key)
+        return await ecdsa_verify_async(self.signed, bytes.fromhex(input_tx), public_key) or \
+            await ecdsa_verify_async(self.signed, input_tx, public_key)
 
     @property
     def as_dict(self):
