@@ -290,6 +290,21 @@ def main():
 
     def overlaps(a0, a1):
         return any(w0 < a1 and a0 < w1 for w0, w1 in windows)
+    # where the HTTP loop stalled (node's UPOW_TRACE_FILE.lag) and what the block path spent its time on
+    stalls = []
+    if os.path.exists(trace + '.lag'):
+        for ln in open(trace + '.lag'):
+            r = json.loads(ln)
+            if t0 <= r['t'] <= t_push_end:
+                stalls.append((r['t'] - r['ms'] / 1000.0, r['t'], r['ms']))
+    in_blk = [s for s in stalls if overlaps(s[0], s[1])]
+    stages = {}
+    if os.path.exists(trace):
+        for ln in open(trace):
+            r = json.loads(ln)
+            if r.get('ok') and r.get('txs', 0) > 0:
+                for k, v in r.get('stages_ms', {}).items():
+                    stages.setdefault(k, []).append(v)
     req_lat = sorted((b - a) * 1000 for a, b in req)
     req_lat_blk = sorted((b - a) * 1000 for a, b in req if overlaps(a, b))
     pq = lambda v, p: round(v[min(len(v) - 1, int(p * len(v)))], 2) if v else None
@@ -310,6 +325,11 @@ def main():
                                                   'n': len(req_lat_blk)},
         'block_apply_windows': len(windows),
         'block_apply_ms_max': round(max((w1 - w0) * 1000 for w0, w1 in windows), 1) if windows else None,
+        'loop_stalls_over_2ms': {'n': len(stalls), 'total_ms': round(sum(s[2] for s in stalls), 1),
+                                 'max_ms': round(max((s[2] for s in stalls), default=0), 1),
+                                 'n_during_block_apply': len(in_blk),
+                                 'total_ms_during_block_apply': round(sum(s[2] for s in in_blk), 1)},
+        'block_stage_ms_mean': {k: round(sum(v) / len(v), 2) for k, v in sorted(stages.items())},
         'difficulty': a.difficulty, 'setup_s': round(setup_s, 1), 'data': 'synthetic keys, miner coinbases fanned out',
     }
     line = json.dumps(out)

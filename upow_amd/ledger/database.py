@@ -1002,6 +1002,8 @@ class Database:
         """Bring ``address_transactions`` up to the tip: one INSERT … SELECT over json_each of the
         inputs/outputs address columns of every tx in blocks above the watermark (all in SQLite's C
         code). Returns the number of blocks indexed."""
+        if self._address_index_height() >= self._tip_id():
+            return 0  # kept current by the block batches: no write transaction (it would drop the caches)
         with self.transaction():
             wm = self._address_index_height()
             tip = self._tip_id()
@@ -1016,6 +1018,24 @@ class Database:
                 'json_each(t.outputs_addresses) j WHERE b.id > ? AND b.id <= ?', (wm, tip, wm, tip))
             self.conn.execute("UPDATE address_index_state SET height = ? WHERE k = 'height'", (tip,))
         return tip - wm
+
+    # the per-address index of one block, inside the block's own journal batch (materialiser thread):
+    # only when the watermark stands at the previous block, so a lagging index is left to the catch-up
+    # above (rows are a set: ``get_address_transactions`` orders by block and tx rowid)
+    _ADDR_BLOCK_SQL = (
+        'INSERT INTO address_transactions (address, tx_hash) '
+        "SELECT j.value, t.tx_hash FROM transactions t, json_each(t.inputs_addresses) j WHERE t.block_hash = ?1 "
+        "AND EXISTS (SELECT 1 FROM address_index_state WHERE k = 'height' AND height = ?2) "
+        'UNION '
+        "SELECT j.value, t.tx_hash FROM transactions t, json_each(t.outputs_addresses) j WHERE t.block_hash = ?1 "
+        "AND EXISTS (SELECT 1 FROM address_index_state WHERE k = 'height' AND height = ?2)")
+    _ADDR_BLOCK_WM = "UPDATE address_index_state SET height = ?2 + 1 WHERE k = 'height' AND height = ?2 AND ?1 IS NOT NULL"
+
+    def _address_index_stmts(self, block_hash: str, block_id: int) -> list:
+        if os.environ.get('UPOW_ADDRESS_INDEX_INLINE', '1') == '0':
+            return []
+        return [(self._ADDR_BLOCK_SQL, [block_hash, block_id - 1], 1, None, None, None),
+                (self._ADDR_BLOCK_WM, [block_hash, block_id - 1], 1, None, None, None)]
 
     def _address_index_rollback(self):
         """After blocks were deleted (their address rows cascade away), pull the watermark down."""
@@ -1341,6 +1361,8 @@ class Database:
                           'SELECT EXISTS(SELECT 1 FROM pending_spent_outputs)', None))
             tables |= {'pending_transactions', 'pending_spent_outputs'}
         self.checkpoint('spent')
+        stmts.extend(self._address_index_stmts(b['hash'], int(b['id'])))
+        tables |= {'address_transactions', 'address_index_state'}
 
         seq = 0
         if self.writer is not None:
@@ -1447,6 +1469,8 @@ class Database:
                           'SELECT EXISTS(SELECT 1 FROM pending_spent_outputs)', None))
             tables |= {'pending_transactions', 'pending_spent_outputs'}
         self.checkpoint('spent')
+        stmts.extend(self._address_index_stmts(b['hash'], int(b['id'])))
+        tables |= {'address_transactions', 'address_index_state'}
 
         # ---- index records: created outputs (per table) and spent outpoints with their current payloads
         from .utxo import pack_records

@@ -72,10 +72,13 @@ BANNED_SENDERS = ['DgQKikeDqS2Fzue23KuA36L4eJSFh649zA9jJ6zwbzUMp']  # main.py:42
 async def lifespan(app: FastAPI):
     await startup()
     indexer = asyncio.create_task(_address_indexer())
+    lag = asyncio.create_task(_loop_lag_monitor()) if os.environ.get('UPOW_TRACE_FILE') else None
     try:
         yield
     finally:
         indexer.cancel()
+        if lag is not None:
+            lag.cancel()
         ledger_worker.stop()
         cluster.leader_quit()
         await shutdown_websocket_manager()
@@ -87,12 +90,30 @@ async def lifespan(app: FastAPI):
                 logger.error(f'UTXO snapshot on shutdown failed: {e}')
 
 
+async def _loop_lag_monitor(tick: float = 0.001, report_ms: float = 2.0):
+    """With ``UPOW_TRACE_FILE``: how late the HTTP event loop runs a 1 ms timer, one JSON line per stall
+    over ``report_ms`` (``<trace>.lag``: wall time at the end of the stall and its length), so a soak can
+    tell which stalls overlap block application and which do not."""
+    import time as _time
+    path = os.environ['UPOW_TRACE_FILE'] + '.lag'
+    loop = asyncio.get_running_loop()
+    with open(path, 'a') as f:
+        while True:
+            t0 = loop.time()
+            await asyncio.sleep(tick)
+            late = (loop.time() - t0 - tick) * 1000.0
+            if late > report_ms:
+                f.write(json.dumps({'t': round(_time.time(), 4), 'ms': round(late, 2)}) + '\n')
+                f.flush()
+
+
 async def _address_indexer(period: float = 30.0):
     """Keep the lazily built per-address tx index near the tip (queries also catch it up on demand)."""
     while True:
         await asyncio.sleep(period)
         try:
             if db is not None:
+                await db.asettle()  # block batches keep the index current; this only catches up a lag
                 db.index_addresses()
         except Exception as e:
             logger.error(f'address indexer: {e}')
