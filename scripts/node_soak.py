@@ -174,21 +174,24 @@ def main():
         c = httpx.Client(timeout=30)
         seen = h_start
         while not stop.is_set():
+            # probe the next height with /get_block (an indexed lookup), not /get_mining_info: the
+            # monitor must not load the node with a mempool-wide template build five times a second
             try:
-                h = c.get(url + '/get_mining_info').json()['result']['last_block'].get('id', 0)
+                r = c.get(url + '/get_block', params={'block': seen + 1}).json()
             except Exception:
                 time.sleep(0.2)
                 continue
-            while seen < h:
-                seen += 1
-                b = c.get(url + '/get_block', params={'block': seen}).json()['result']
-                now = time.time()
-                blocks.append((seen, now, len(b['transactions'])))
-                for t in b['transactions']:
-                    th = hashlib.sha256(bytes.fromhex(t)).hexdigest()
-                    if th not in included:
-                        included[th] = now  # every block tx; matched against the pushed set at the end
-            time.sleep(0.2)
+            if not r.get('ok'):
+                time.sleep(0.2)
+                continue
+            seen += 1
+            b = r['result']
+            now = time.time()
+            blocks.append((seen, now, len(b['transactions'])))
+            for t in b['transactions']:
+                th = hashlib.sha256(bytes.fromhex(t)).hexdigest()
+                if th not in included:
+                    included[th] = now  # every block tx; matched against the pushed set at the end
 
     w = threading.Thread(target=watcher, daemon=True)
     w.start()

@@ -716,7 +716,8 @@ class Database:
         if mp is None:
             self._settle(self._PENDING)
             with self.lock:
-                mp = MempoolIndex(self._conn.execute('SELECT tx_hash, propagation_time FROM pending_transactions'),
+                mp = MempoolIndex(self._conn.execute('SELECT tx_hash, propagation_time, tx_hex, fees '
+                                                     'FROM pending_transactions'),
                                   self._conn.execute('SELECT tx_hash, "index" FROM pending_spent_outputs'))
                 self._mp = mp
             self.mempool_reloads += 1
@@ -784,8 +785,9 @@ class Database:
         tx_hash = sha256(tx_hex)
         ptime = int(_utcnow().replace(tzinfo=timezone.utc).timestamp())
         inputs = [(i.tx_hash, int(i.index)) for i in transaction.inputs]
+        fees = numeric(transaction.fees, 6)
         with mp.lock:
-            why = mp.try_add(tx_hash, ptime, inputs)
+            why = mp.try_add(tx_hash, ptime, inputs, tx_hex, fees)
             if why == 'duplicate':
                 raise UniqueViolationError(f'UNIQUE constraint failed: pending_transactions.tx_hash ({tx_hash})')
             if why is not None:
@@ -794,7 +796,7 @@ class Database:
             # OR IGNORE: a statement error would stop the materialiser; the index already refused duplicates
             stmts = [self.encode('INSERT OR IGNORE INTO pending_transactions (tx_hash, tx_hex, inputs_addresses, fees, '
                                  'propagation_time) VALUES (?, ?, ?, ?, ?)',
-                                 [tx_hash, tx_hex, _j(inputs_addresses), numeric(transaction.fees, 6), ptime], 1)]
+                                 [tx_hash, tx_hex, _j(inputs_addresses), fees, ptime], 1)]
             if inputs:
                 stmts.append(self.encode('INSERT INTO pending_spent_outputs (tx_hash, "index") VALUES (?, ?)',
                                          [[h for h, _ in inputs], np.array([i for _, i in inputs], np.int64)],
@@ -893,13 +895,17 @@ class Database:
 
     async def get_pending_transactions_limit(self, limit: int = MAX_BLOCK_SIZE_HEX, hex_only: bool = False,
                                              check_signatures: bool = True) -> List[Union[Transaction, str]]:
-        return_txs, size = [], 0
-        for r in self._pending_rows_ordered():
-            tx = r['tx_hex']
-            if size + len(tx) > limit:
-                break
-            return_txs.append(tx)
-            size += len(tx)
+        mp = self._mempool()
+        if mp is not None:
+            return_txs = mp.ordered_hex(limit)
+        else:
+            return_txs, size = [], 0
+            for r in self._pending_rows_ordered():
+                tx = r['tx_hex']
+                if size + len(tx) > limit:
+                    break
+                return_txs.append(tx)
+                size += len(tx)
         if hex_only:
             return return_txs
         return [await Transaction.from_hex(t, check_signatures) for t in return_txs]

@@ -16,10 +16,15 @@ spend — and follows every writer of the two tables:
 
 Keys are raw bytes: 32-byte tx hashes, 36-byte outpoints (txid || index u32 LE), the layout of the
 block codec's input records, so a block's removal is a slice of its arrays, not a hex round trip.
+
+Each pending tx also keeps its block-template sort key — ``ORDER BY fees / LENGTH(tx_hex) DESC,
+LENGTH(tx_hex), tx_hex`` (reference database.py:173-174) — so ``/get_mining_info`` orders the mempool
+with one C-level sort of precomputed tuples instead of re-reading and re-keying every row from SQL.
 """
 from __future__ import annotations
 
 import threading
+from decimal import Decimal
 from typing import Dict, Iterable, List, Optional, Set, Tuple
 
 import numpy as np
@@ -36,10 +41,20 @@ def _rows_raw(arr: np.ndarray, width: int) -> List[bytes]:
     return [buf[k:k + width] for k in range(0, len(buf), width)]
 
 
+def order_key(tx_hex: str, fees) -> tuple:
+    return (-(Decimal(fees) / len(tx_hex)), len(tx_hex), tx_hex)
+
+
 class MempoolIndex:
-    def __init__(self, tx_rows: Iterable[Tuple[str, int]], spent_rows: Iterable[Tuple[str, int]]):
+    def __init__(self, tx_rows: Iterable[Tuple[str, int, str, str]], spent_rows: Iterable[Tuple[str, int]]):
+        """``tx_rows``: (tx_hash, propagation_time, tx_hex, fees) of pending_transactions."""
         self.lock = threading.Lock()
-        self.txs: Dict[bytes, int] = {bytes.fromhex(h): int(t) for h, t in tx_rows}
+        self.txs: Dict[bytes, int] = {}  # tx hash -> propagation time
+        self.keys: Dict[bytes, tuple] = {}  # tx hash -> order_key
+        for h, t, hx, fees in tx_rows:
+            k = bytes.fromhex(h)
+            self.txs[k] = int(t)
+            self.keys[k] = order_key(hx, fees)
         self.spent: Set[bytes] = {outpoint_key(h, i) for h, i in spent_rows}
         self.min_ptime: Optional[int] = min(self.txs.values()) if self.txs else None
 
@@ -54,7 +69,19 @@ class MempoolIndex:
         seen = dict.fromkeys((h, int(i)) for h, i in outputs)
         return [o for o in seen if outpoint_key(*o) in self.spent]
 
-    def try_add(self, tx_hash: str, ptime: int, inputs: List[Tuple[str, int]]) -> Optional[str]:
+    def ordered_hex(self, limit: int) -> List[str]:
+        """Pending tx hex in block-template order, up to ``limit`` hex characters in total."""
+        with self.lock:
+            keys = sorted(self.keys.values())
+        out, size = [], 0
+        for k in keys:
+            if size + k[1] > limit:
+                break
+            out.append(k[2])
+            size += k[1]
+        return out
+
+    def try_add(self, tx_hash: str, ptime: int, inputs: List[Tuple[str, int]], tx_hex: str, fees) -> Optional[str]:
         """Reserve a tx and its inputs (caller holds ``lock``); returns why it cannot be added, or None."""
         h = bytes.fromhex(tx_hash)
         if h in self.txs:
@@ -63,6 +90,7 @@ class MempoolIndex:
         if any(k in self.spent for k in keys):
             return 'double spend'
         self.txs[h] = int(ptime)
+        self.keys[h] = order_key(tx_hex, fees)
         self.spent.update(keys)
         if self.min_ptime is None or ptime < self.min_ptime:
             self.min_ptime = int(ptime)
@@ -74,6 +102,8 @@ class MempoolIndex:
             if self.txs:
                 pop = self.txs.pop
                 hit_tx = [k for k in tx_keys if pop(k, None) is not None]
+                for k in hit_tx:
+                    del self.keys[k]
             hit_in = []
             if self.spent and in_keys:
                 s = self.spent
