@@ -301,6 +301,14 @@ def main():
             if t0 <= r['t'] <= t_push_end:
                 stalls.append((r['t'] - r['ms'] / 1000.0, r['t'], r['ms']))
     in_blk = [s for s in stalls if overlaps(s[0], s[1])]
+    stack_counts = {}
+    if os.path.exists(trace + '.stacks'):
+        for ln in open(trace + '.stacks'):
+            r = json.loads(ln)
+            if t0 <= r['t'] <= t_push_end:
+                key = ' < '.join(reversed(r['stack'][-3:]))
+                stack_counts[key] = stack_counts.get(key, 0) + 1
+    top_stacks = sorted(stack_counts.items(), key=lambda kv: -kv[1])[:12]
     stages = {}
     if os.path.exists(trace):
         for ln in open(trace):
@@ -332,6 +340,7 @@ def main():
                                  'max_ms': round(max((s[2] for s in stalls), default=0), 1),
                                  'n_during_block_apply': len(in_blk),
                                  'total_ms_during_block_apply': round(sum(s[2] for s in in_blk), 1)},
+        'loop_stall_samples_2ms': dict(top_stacks),
         'block_stage_ms_mean': {k: round(sum(v) / len(v), 2) for k, v in sorted(stages.items())},
         'difficulty': a.difficulty, 'setup_s': round(setup_s, 1), 'data': 'synthetic keys, miner coinbases fanned out',
     }

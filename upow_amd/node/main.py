@@ -16,6 +16,7 @@ import json
 import os
 import random
 import re
+import sys
 from asyncio import gather
 from collections import defaultdict, deque
 from contextlib import asynccontextmanager
@@ -94,17 +95,40 @@ async def _loop_lag_monitor(tick: float = 0.001, report_ms: float = 2.0):
     """With ``UPOW_TRACE_FILE``: how late the HTTP event loop runs a 1 ms timer, one JSON line per stall
     over ``report_ms`` (``<trace>.lag``: wall time at the end of the stall and its length), so a soak can
     tell which stalls overlap block application and which do not."""
+    import threading
     import time as _time
+    import traceback
     path = os.environ['UPOW_TRACE_FILE'] + '.lag'
     loop = asyncio.get_running_loop()
-    with open(path, 'a') as f:
-        while True:
-            t0 = loop.time()
-            await asyncio.sleep(tick)
-            late = (loop.time() - t0 - tick) * 1000.0
-            if late > report_ms:
-                f.write(json.dumps({'t': round(_time.time(), 4), 'ms': round(late, 2)}) + '\n')
-                f.flush()
+    beat = [_time.perf_counter()]
+    loop_tid = threading.get_ident()
+    stop = threading.Event()
+
+    def watchdog():
+        # while the loop is stalled past 5 ms, sample what the loop thread is executing (innermost
+        # frames) every 2 ms: the .stacks file names the code that holds the event loop
+        with open(os.environ['UPOW_TRACE_FILE'] + '.stacks', 'a') as out:
+            while not stop.wait(0.002):
+                if _time.perf_counter() - beat[0] > 0.005:
+                    fr = sys._current_frames().get(loop_tid)
+                    if fr is not None:
+                        st = traceback.extract_stack(fr)[-6:]
+                        out.write(json.dumps({'t': round(_time.time(), 4),
+                                              'stack': [f'{os.path.basename(x.filename)}:{x.lineno}:{x.name}' for x in st]}) + '\n')
+    threading.Thread(target=watchdog, name='upow-loop-watchdog', daemon=True).start()
+    try:
+        with open(path, 'a') as f:
+            while True:
+                t0 = loop.time()
+                beat[0] = _time.perf_counter()
+                await asyncio.sleep(tick)
+                beat[0] = _time.perf_counter()
+                late = (loop.time() - t0 - tick) * 1000.0
+                if late > report_ms:
+                    f.write(json.dumps({'t': round(_time.time(), 4), 'ms': round(late, 2)}) + '\n')
+                    f.flush()
+    finally:
+        stop.set()
 
 
 async def _address_indexer(period: float = 30.0):
