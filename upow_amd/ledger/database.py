@@ -19,7 +19,7 @@ import sqlite3
 import struct
 import threading
 import weakref
-from collections import defaultdict
+from collections import OrderedDict, defaultdict
 from datetime import datetime, timedelta, timezone
 from decimal import ROUND_HALF_UP, Decimal
 from statistics import mean
@@ -313,6 +313,9 @@ class Database:
         self._mempool_ver = 0
         self._mp: Optional[MempoolIndex] = None  # ledger/mempool.py; None: (re)load from SQL on next use
         self.mempool_reloads = 0
+        # parsed rows of confirmed txs by hash (immutable until a rollback, which clears it): a funding
+        # tx with hundreds of outputs is spent by many pushed txs, each would re-read and re-parse it
+        self._info_cache: 'OrderedDict[str, dict]' = OrderedDict()
         self.mempool_index = os.environ.get('UPOW_MEMPOOL_INDEX', '1') != '0'
         self._conn.execute('PRAGMA foreign_keys = ON')
         self._conn.execute('PRAGMA journal_mode = WAL')
@@ -522,6 +525,8 @@ class Database:
         return self._conn
 
     def _invalidate_for(self, tables: Optional[frozenset]):
+        if tables is None or 'blocks' in tables or 'transactions' in tables:
+            self._info_cache.clear()
         if tables is None or 'blocks' in tables:
             self._tip_cache = None
             self._genesis_cache = None
@@ -1097,18 +1102,43 @@ class Database:
         d['fees'] = Decimal(d['fees'])
         return d
 
+    INFO_CACHE = 8192
+
+    def _cache_info(self, h: str, info: dict):
+        c = self._info_cache
+        c[h] = info
+        if len(c) > self.INFO_CACHE:
+            c.popitem(last=False)
+
     async def get_transaction_info(self, tx_hash: str) -> Optional[dict]:
+        hit = self._info_cache.get(tx_hash)
+        if hit is not None:
+            return hit
         res = self._q1_present('SELECT * FROM transactions WHERE tx_hash = ?', (tx_hash,))
-        return self._info_row(res) if res is not None else None
+        if res is None:
+            return None
+        info = self._info_row(res)
+        self._cache_info(tx_hash, info)
+        return info
 
     async def get_transactions_info(self, tx_hashes: List[str]) -> Dict[str, dict]:
         out = {}
         hashes = list(dict.fromkeys(tx_hashes))
         if len(hashes) <= 32:  # a pushed tx's funding txs: as _q1_present, without a settle when all are in
-            with self.lock:
-                for r in self._conn.execute(f'SELECT * FROM transactions WHERE tx_hash IN '
-                                            f'({",".join("?" * len(hashes))})', hashes):
-                    out[r['tx_hash']] = self._info_row(r)
+            cache = self._info_cache
+            miss = []
+            for h in hashes:
+                hit = cache.get(h)
+                if hit is not None:
+                    out[h] = hit
+                else:
+                    miss.append(h)
+            if miss:
+                with self.lock:
+                    for r in self._conn.execute(f'SELECT * FROM transactions WHERE tx_hash IN '
+                                                f'({",".join("?" * len(miss))})', miss):
+                        info = out[r['tx_hash']] = self._info_row(r)
+                        self._cache_info(r['tx_hash'], info)
             if len(out) == len(hashes):
                 return out
             hashes = [h for h in hashes if h not in out]

@@ -9,6 +9,7 @@ from __future__ import annotations
 import fcntl
 import json
 import os
+import time
 from contextlib import contextmanager
 from random import sample
 from typing import List, Optional
@@ -56,19 +57,29 @@ class NodesManager:
     _stamp = None   # (mtime_ns, size, inode) of nodes.json as last read or written by this process
     _written = None  # (nodes, last_messages) as last written by this process
 
+    _stat_at = 0.0  # monotonic time of the last stat
+    _stat_val = None
+    STAT_PERIOD = 0.5  # seconds a stat result is reused (every /push_tx gossips through get_nodes)
+
     @staticmethod
-    def _file_stamp():
+    def _file_stamp(fresh: bool = False):
+        now = time.monotonic()
+        if not fresh and now - NodesManager._stat_at < NodesManager.STAT_PERIOD:
+            return NodesManager._stat_val
         try:
             st = os.stat(NodesManager.path)
-            return st.st_mtime_ns, st.st_size, st.st_ino
+            val = st.st_mtime_ns, st.st_size, st.st_ino
         except OSError:
-            return None
+            val = None
+        NodesManager._stat_at, NodesManager._stat_val = now, val
+        return val
 
     @staticmethod
     def init(path: Optional[str] = None):
         """(Re)load nodes.json. The node calls this on every request (as the reference does with
         pickledb); the file is only re-read when it changed on disk since this process last read or
-        wrote it, so another process sharing the peer table is still seen at once."""
+        wrote it (checked at most every ``STAT_PERIOD``), so another process sharing the peer table is
+        seen within half a second."""
         if path is not None or NodesManager.path is None:
             NodesManager.path = path or config.data_path('nodes.json')
             NodesManager._stamp = None
@@ -80,7 +91,7 @@ class NodesManager:
             core = NodesManager._core_url()
             NodesManager.nodes = NodesManager.db.get('nodes') or ([core] if core else [])
             NodesManager.last_messages = NodesManager.db.get('last_messages') or ({core: timestamp()} if core else {})
-            NodesManager._stamp = NodesManager._file_stamp()
+            NodesManager._stamp = NodesManager._file_stamp(fresh=True)
 
     @staticmethod
     def sync():
@@ -92,7 +103,7 @@ class NodesManager:
             NodesManager.db.set('nodes', NodesManager.nodes)
             NodesManager.db.set('last_messages', NodesManager.last_messages)
             NodesManager.db.dump()
-            NodesManager._stamp = NodesManager._file_stamp()
+            NodesManager._stamp = NodesManager._file_stamp(fresh=True)
             NodesManager._written = state
 
     @staticmethod
