@@ -219,6 +219,9 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
         std::vector<int64_t> len;
         utf8_list(spec.cast<py::list>(), ptr, len);
         if (int64_t(ptr.size()) != n) throw std::invalid_argument("text column length != n");
+        // the row copies run without the GIL (the caller's list keeps every str alive): a block's
+        // columns are megabytes, and the HTTP event loop thread must not wait for them
+        py::gil_scoped_release nogil;
         encode_text_rows(o, n, ptr, len, nullptr);
     } else if (py::isinstance<py::tuple>(spec)) {
         py::tuple t = spec.cast<py::tuple>();
@@ -233,6 +236,7 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
             const int32_t* idx = static_cast<const int32_t*>(bi.ptr);
             for (int64_t i = 0; i < n; ++i)
                 if (idx[i] < 0 || size_t(idx[i]) >= ptr.size()) throw std::out_of_range("gather index");
+            py::gil_scoped_release nogil;
             encode_text_rows(o, n, ptr, len, idx);
         } else if (tag == "hex32") {
             py::buffer_info bi = t[1].cast<py::buffer>().request();
@@ -241,6 +245,8 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
             if (offset < 0 || stride < 0 || (n > 0 && (n - 1) * stride + offset + 32 > raw_n))
                 throw std::out_of_range("hex32 column out of range");
             o.u8(K_HEX32);
+            py::gil_scoped_release nogil;
+            o.b.reserve(o.b.size() + size_t(n) * 32);
             for (int64_t r = 0; r < n; ++r) o.raw(raw + r * stride + offset, 32);
         } else if (tag == "arena") {
             py::buffer_info bb = t[1].cast<py::buffer>().request(), ob = t[2].cast<py::buffer>().request();
@@ -252,6 +258,7 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
                 if (aoff[i] < 0 || aoff[i + 1] < aoff[i] || aoff[i + 1] > blen) throw std::out_of_range("arena offsets");
             o.u8(K_TEXT);
             o.u8(0);
+            py::gil_scoped_release nogil;
             std::vector<int64_t> off(size_t(n) + 1);
             for (int64_t i = 0; i <= n; ++i) off[size_t(i)] = aoff[i] - aoff[0];
             o.raw(off.data(), off.size() * 8);
@@ -265,6 +272,7 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
             throw std::invalid_argument("integer column must be int64");
         if (bi.size != n) throw std::invalid_argument("int column length != n");
         o.u8(K_INT64);
+        py::gil_scoped_release nogil;
         o.raw(bi.ptr, size_t(n) * 8);
     }
 }
@@ -494,14 +502,19 @@ class LedgerWriter {
 
     // Commit point: append the record (and fdatasync in SYNC_COMMIT mode), queue it for every
     // materialiser. Returns the record's sequence number.
-    uint64_t submit(const std::vector<std::string>& stmts, const std::string& meta, int64_t block_id) {
+    struct Span {
+        const char* p;
+        size_t n;
+    };
+
+    uint64_t submit(const std::vector<Span>& stmts, const std::string& meta, int64_t block_id) {
         auto payload = std::make_shared<std::string>();
         size_t total = 4;
-        for (auto& st : stmts) total += st.size();
+        for (auto& st : stmts) total += st.n;
         payload->reserve(total);
         uint32_t ns = uint32_t(stmts.size());
         payload->append(reinterpret_cast<const char*>(&ns), 4);
-        for (auto& st : stmts) payload->append(st);
+        for (auto& st : stmts) payload->append(st.p, st.n);
         uint64_t seq;
         {
             std::lock_guard<std::mutex> jl(jmu_);
@@ -976,12 +989,18 @@ void register_ledger_writer(py::module_& m) {
              py::arg("group_max") = 8, py::arg("journal_max_bytes") = int64_t(1) << 30)
         .def("submit",
              [](LedgerWriter& w, py::list stmts, py::bytes meta, int64_t block_id) {
-                 std::vector<std::string> v;
+                 // only pointers are taken under the GIL (the list and the meta object keep the bytes
+                 // alive); the megabytes of a block batch are copied into the record without it
+                 std::vector<LedgerWriter::Span> v;
                  v.reserve(stmts.size());
-                 for (auto x : stmts) v.push_back(x.cast<std::string>());
-                 std::string mt = meta;
+                 for (auto x : stmts) {
+                     if (!PyBytes_Check(x.ptr())) throw std::invalid_argument("statements must be bytes");
+                     v.push_back({PyBytes_AS_STRING(x.ptr()), size_t(PyBytes_GET_SIZE(x.ptr()))});
+                 }
+                 const char* mp = PyBytes_AS_STRING(meta.ptr());
+                 const size_t mn = size_t(PyBytes_GET_SIZE(meta.ptr()));
                  py::gil_scoped_release nogil;
-                 return w.submit(v, mt, block_id);
+                 return w.submit(v, std::string(mp, mn), block_id);
              },
              py::arg("stmts"), py::arg("meta") = py::bytes(""), py::arg("block_id") = -1)
         .def("applied", &LedgerWriter::applied, py::arg("shard") = -1)

@@ -1403,8 +1403,9 @@ class Database:
         seq = 0
         if self.writer is not None:
             enc = [self.encode(*st) for st in stmts]
-            meta = struct.pack('<qII', int(b['id']), n_out + len(cb_keys), n_in) + recs.tobytes() + \
-                cb_recs.tobytes() + spent.tobytes() + np.ascontiguousarray(spent_payload).tobytes()
+            meta = b''.join((struct.pack('<qII', int(b['id']), n_out + len(cb_keys), n_in), memoryview(recs),
+                             memoryview(np.ascontiguousarray(cb_recs)), memoryview(spent),
+                             memoryview(np.ascontiguousarray(spent_payload)).cast('B')))
             seq = self.submit_batch(enc, tables, meta, int(b['id']))
         else:
             with self.transaction(foreign_keys=False):
