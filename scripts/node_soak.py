@@ -309,6 +309,12 @@ def main():
                 key = ' < '.join(reversed(r['stack'][-3:]))
                 stack_counts[key] = stack_counts.get(key, 0) + 1
     top_stacks = sorted(stack_counts.items(), key=lambda kv: -kv[1])[:12]
+    gcs = []
+    if os.path.exists(trace + '.gc'):
+        for ln in open(trace + '.gc'):
+            r = json.loads(ln)
+            if t0 <= r['t'] <= t_push_end:
+                gcs.append(r)
     stages = {}
     if os.path.exists(trace):
         for ln in open(trace):
@@ -341,6 +347,9 @@ def main():
                                  'n_during_block_apply': len(in_blk),
                                  'total_ms_during_block_apply': round(sum(s[2] for s in in_blk), 1)},
         'loop_stall_samples_2ms': dict(top_stacks),
+        'gc_over_2ms': {'n': len(gcs), 'total_ms': round(sum(g['ms'] for g in gcs), 1),
+                        'max_ms': round(max((g['ms'] for g in gcs), default=0), 1),
+                        'gen2': sum(1 for g in gcs if g.get('gen') == 2)},
         'block_stage_ms_mean': {k: round(sum(v) / len(v), 2) for k, v in sorted(stages.items())},
         'difficulty': a.difficulty, 'setup_s': round(setup_s, 1), 'data': 'synthetic keys, miner coinbases fanned out',
     }

@@ -116,6 +116,20 @@ async def _loop_lag_monitor(tick: float = 0.001, report_ms: float = 2.0):
                         out.write(json.dumps({'t': round(_time.time(), 4),
                                               'stack': [f'{os.path.basename(x.filename)}:{x.lineno}:{x.name}' for x in st]}) + '\n')
     threading.Thread(target=watchdog, name='upow-loop-watchdog', daemon=True).start()
+    import gc
+    gc_t0 = {}
+    gc_out = open(os.environ['UPOW_TRACE_FILE'] + '.gc', 'a')
+
+    def on_gc(phase, info):  # collections over 2 ms (they hold the GIL on whichever thread allocated)
+        if phase == 'start':
+            gc_t0['t'] = _time.perf_counter()
+        elif 't' in gc_t0:
+            ms = (_time.perf_counter() - gc_t0.pop('t')) * 1000.0
+            if ms > 2.0:
+                gc_out.write(json.dumps({'t': round(_time.time(), 4), 'gen': info.get('generation'),
+                                         'ms': round(ms, 2)}) + '\n')
+                gc_out.flush()
+    gc.callbacks.append(on_gc)
     try:
         with open(path, 'a') as f:
             while True:
@@ -129,6 +143,8 @@ async def _loop_lag_monitor(tick: float = 0.001, report_ms: float = 2.0):
                     f.flush()
     finally:
         stop.set()
+        gc.callbacks.remove(on_gc)
+        gc_out.close()
 
 
 async def _address_indexer(period: float = 30.0):
@@ -154,6 +170,11 @@ async def startup():
         await cluster.leader_replay(db)
     # block validation/apply (and every cluster collective) from here on runs on the ledger thread
     ledger_worker.start()
+    # what exists now (ledger caches, indexes, modules) lives for the process: keep it out of the
+    # cyclic collector's full passes, which run on whichever thread allocates and hold the GIL
+    import gc
+    gc.collect()
+    gc.freeze()
     await start_websocket_manager()
 
 
