@@ -313,6 +313,7 @@ class Database:
         self._mempool_ver = 0
         self._mp: Optional[MempoolIndex] = None  # ledger/mempool.py; None: (re)load from SQL on next use
         self.mempool_reloads = 0
+        self._seq_lock = threading.Lock()  # journal submission + per-table sequence bookkeeping
         # parsed rows of confirmed txs by hash (immutable until a rollback, which clears it): a funding
         # tx with hundreds of outputs is spent by many pushed txs, each would re-read and re-parse it
         self._info_cache: 'OrderedDict[str, dict]' = OrderedDict()
@@ -463,6 +464,10 @@ class Database:
         journal that writes them. No-op when the writer is idle or absent."""
         if self.writer is None:
             return
+        if self._tx_depth and self._tx_owner == threading.get_ident():
+            # inside this thread's open SQL transaction: a batch journaled since BEGIN cannot be
+            # materialised before COMMIT (it needs the write lock), so waiting would deadlock
+            return
         if tables is None:
             waits = {-1: self._submitted}
         else:
@@ -537,15 +542,22 @@ class Database:
             self._mp = None
 
     def submit_batch(self, stmts: List[bytes], tables: Iterable[str], meta: bytes = b'', block_id: int = -1) -> int:
-        """Commit a batch of encoded statements (``lib().ledger_encode_stmt``) through the journal. The
-        Python lock keeps a batch from landing while a Python-side SQL transaction is open."""
-        with self.lock:
-            if self._tx_depth:
-                raise RuntimeError('ledger batch submitted inside an open SQL transaction')
+        """Commit a batch of encoded statements (``lib().ledger_encode_stmt``) through the journal.
+
+        Does not take the connection lock: a block's batch is megabytes, and the /push_tx path must not
+        queue behind its journal write. A batch journaled while another thread has a Python-side SQL
+        transaction open is materialised after that transaction commits (the materialiser needs the
+        write lock), which is the order the two would have had if the batch had waited; the
+        transaction's own reads do not wait for it (see :meth:`_settle`)."""
+        if self._tx_depth and self._tx_owner == threading.get_ident():
+            raise RuntimeError('ledger batch submitted inside an open SQL transaction')
+        with self._seq_lock:
             seq = self.writer.submit(stmts, meta, block_id)
-            self._submitted = seq
+            if seq > self._submitted:
+                self._submitted = seq
             for t in tables:
-                self._table_seq[t] = seq
+                if seq > self._table_seq.get(t, 0):
+                    self._table_seq[t] = seq
         return seq
 
     # ------------------------------------------------------------------ SQL helpers
@@ -615,6 +627,7 @@ class Database:
                 if not self.fk:  # only settable outside a transaction
                     c.execute('PRAGMA foreign_keys = OFF')
                 c.execute('BEGIN')
+                self.db._tx_owner = threading.get_ident()
                 self.db._fk_off = not self.fk
                 self.db._invalidate_for(None)
             self.db._tx_depth += 1
@@ -636,6 +649,7 @@ class Database:
             return False
 
     _tx_depth = 0
+    _tx_owner = None
     _tx_failed = False
     _fk_off = False
 
