@@ -129,3 +129,21 @@ def test_stale_propagation_and_python_write_invalidate(monkeypatch):
         assert await a.get_pending_spent_outputs([(i.tx_hash, i.index) for i in tx.inputs]) == \
             [(i.tx_hash, i.index) for i in tx.inputs]  # the spent rows stay (reference behaviour)
     asyncio.run(go())
+
+
+def test_template_and_hash_lookup_match_sql_path():
+    async def go():
+        a, b, _ = await _chain(6)
+        txs = []
+        for k in KEYS:
+            _use(a)
+            txs.append(await create_transaction(GENESIS, address_of(k), str(1 + k % 3)))
+            assert await _admit_both(a, b, txs[-1]) is True
+        ha, xa = a.pending_template()
+        hb, xb = b.pending_template()
+        assert (ha, xa) == (hb, xb) and xa == [t.hash() for t in map(lambda h: next(x for x in txs if x.hex() == h), ha)]
+        assert await a.get_pending_transactions_limit(hex_only=True) == await b.get_pending_transactions_limit(hex_only=True)
+        want = [txs[2].hash(), txs[0].hash(), '00' * 32, 'zz']
+        assert await a.get_pending_transactions_hex_by_hash(want) == await b.get_pending_transactions_hex_by_hash(want[:3])
+        assert await a.get_pending_transactions_hex_by_hash([txs[1].hash()]) == [txs[1].hex()]
+    asyncio.run(go())

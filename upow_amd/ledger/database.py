@@ -929,6 +929,23 @@ class Database:
             return return_txs
         return [await Transaction.from_hex(t, check_signatures) for t in return_txs]
 
+    def pending_template(self, limit: int = MAX_BLOCK_SIZE_HEX) -> Tuple[List[str], List[str]]:
+        """(tx hex, tx hash) lists of ``get_pending_transactions_limit(hex_only=True)``; the hashes come
+        from the mempool index when there is one instead of being recomputed per call."""
+        mp = self._mempool()
+        if mp is not None:
+            rows = mp.ordered(limit)
+            return [hx for hx, _ in rows], [h.hex() for _, h in rows]
+        hexes = []
+        size = 0
+        for r in self._pending_rows_ordered():
+            tx = r['tx_hex']
+            if size + len(tx) > limit:
+                break
+            hexes.append(tx)
+            size += len(tx)
+        return hexes, [sha256(t) for t in hexes]
+
     async def get_need_propagate_transactions(self, last_propagation_delta: int = 600,
                                               limit: int = MAX_BLOCK_SIZE_HEX) -> List[str]:
         now = int(_utcnow().replace(tzinfo=timezone.utc).timestamp())
@@ -1173,6 +1190,9 @@ class Database:
         """tx hex of the pending txs among ``hashes``, in mempool (table) order like database.py:297-301."""
         if not hashes:
             return []
+        mp = self._mempool()
+        if mp is not None:
+            return mp.hex_in_order(hashes)
         want = set(hashes)
         self._settle(frozenset(('pending_transactions',)))
         with self.lock:

@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import threading
 from decimal import Decimal
+from operator import itemgetter
 from typing import Dict, Iterable, List, Optional, Set, Tuple
 
 import numpy as np
@@ -39,6 +40,9 @@ def _rows_raw(arr: np.ndarray, width: int) -> List[bytes]:
     a = np.ascontiguousarray(np.asarray(arr, dtype=np.uint8)[:, :width])
     buf = a.tobytes()
     return [buf[k:k + width] for k in range(0, len(buf), width)]
+
+
+_second = itemgetter(1)
 
 
 def order_key(tx_hex: str, fees) -> tuple:
@@ -69,17 +73,35 @@ class MempoolIndex:
         seen = dict.fromkeys((h, int(i)) for h, i in outputs)
         return [o for o in seen if outpoint_key(*o) in self.spent]
 
-    def ordered_hex(self, limit: int) -> List[str]:
-        """Pending tx hex in block-template order, up to ``limit`` hex characters in total."""
+    def ordered(self, limit: int) -> List[Tuple[str, bytes]]:
+        """(tx hex, raw tx hash) of the pending txs in block-template order, up to ``limit`` hex
+        characters in total."""
         with self.lock:
-            keys = sorted(self.keys.values())
+            items = sorted(self.keys.items(), key=_second)
         out, size = [], 0
-        for k in keys:
+        for h, k in items:
             if size + k[1] > limit:
                 break
-            out.append(k[2])
+            out.append((k[2], h))
             size += k[1]
         return out
+
+    def hex_in_order(self, tx_hashes: Iterable[str]) -> List[str]:
+        """tx hex of the pending txs among ``tx_hashes``, in admission (table row) order."""
+        want = set()
+        for h in tx_hashes:
+            try:
+                want.add(bytes.fromhex(h))
+            except ValueError:
+                continue
+        with self.lock:
+            if len(want) == 1:
+                k = self.keys.get(next(iter(want)))
+                return [k[2]] if k is not None else []
+            return [k[2] for h, k in self.keys.items() if h in want]
+
+    def ordered_hex(self, limit: int) -> List[str]:
+        return [hx for hx, _ in self.ordered(limit)]
 
     def try_add(self, tx_hash: str, ptime: int, inputs: List[Tuple[str, int]], tx_hex: str, fees) -> Optional[str]:
         """Reserve a tx and its inputs (caller holds ``lock``); returns why it cannot be added, or None."""

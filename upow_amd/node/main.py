@@ -24,6 +24,7 @@ from decimal import Decimal
 from typing import Annotated, Union
 
 from fastapi import Body, FastAPI, Header, Query
+from fastapi.encoders import jsonable_encoder
 from fastapi.responses import PlainTextResponse, RedirectResponse
 from starlette.background import BackgroundTasks
 from starlette.middleware.cors import CORSMiddleware
@@ -740,14 +741,19 @@ async def get_mining_info(request: Request, background_tasks: BackgroundTasks):
     """main.py:675-695."""
     Manager.difficulty = None
     difficulty, last_block = await get_difficulty()
-    pending = sorted(await db.get_pending_transactions_limit(hex_only=True))
+    hexes, hashes = db.pending_template()
+    order = sorted(range(len(hexes)), key=hexes.__getitem__)  # the reference sorts the hex strings
+    pending = [hexes[k] for k in order]
     if LAST_PENDING_TRANSACTIONS_CLEAN[0] < timestamp() - 600:
         LAST_PENDING_TRANSACTIONS_CLEAN[0] = timestamp()
         background_tasks.add_task(on_ledger, cluster.mirror_gc, pending)
-    return {'ok': True, 'result': {
-        'difficulty': difficulty, 'last_block': last_block, 'pending_transactions': pending[:10],
-        'pending_transactions_hashes': [sha256(t) for t in pending],
-        'merkle_root': get_transactions_merkle_tree(pending[:10])}}
+    # the framework's generic encoder walks every element of the 10k-entry hash list; only the small
+    # fields need it (Decimal difficulty, block dict)
+    head = jsonable_encoder({'difficulty': difficulty, 'last_block': last_block})
+    return JSONResponse({'ok': True, 'result': {
+        'difficulty': head['difficulty'], 'last_block': head['last_block'], 'pending_transactions': pending[:10],
+        'pending_transactions_hashes': [hashes[k] for k in order],
+        'merkle_root': get_transactions_merkle_tree(pending[:10])}})
 
 
 @app.get('/get_validators_info')
