@@ -361,6 +361,9 @@ class Database:
         if os.environ.get('UPOW_GOV_INDEX', '1') != '0':
             self.gov = GovernanceIndex(self)
             self.gov.rebuild()
+        # the address-index watermark row must exist before the first block: the per-block statements
+        # of the journal batches only advance an existing watermark
+        self._address_index_height()
 
     def _migrate_single_file_utxo(self):
         """Ledgers written before the UTXO table got its own file keep ``unspent_outputs`` in the main
@@ -611,9 +614,10 @@ class Database:
         whole block application (many helper calls) commits or rolls back as one unit. The outermost
         level first waits for the native writer to drain (it cannot take the write lock meanwhile)."""
 
-        def __init__(self, db, foreign_keys: bool = True):
+        def __init__(self, db, foreign_keys: bool = True, invalidate: bool = True):
             self.db = db
             self.fk = foreign_keys
+            self.inv = invalidate
 
         def __enter__(self):
             self.db.lock.acquire()
@@ -629,7 +633,9 @@ class Database:
                 c.execute('BEGIN')
                 self.db._tx_owner = threading.get_ident()
                 self.db._fk_off = not self.fk
-                self.db._invalidate_for(None)
+                self.db._tx_inv = self.inv
+                if self.inv:
+                    self.db._invalidate_for(None)
             self.db._tx_depth += 1
             return self.db
 
@@ -638,7 +644,8 @@ class Database:
                 self.db._tx_depth -= 1
                 if self.db._tx_depth == 0:
                     self.db._conn.execute('COMMIT' if et is None else 'ROLLBACK')
-                    self.db._invalidate_for(None)
+                    if self.db._tx_inv:
+                        self.db._invalidate_for(None)
                     if self.db._fk_off:
                         self.db._conn.execute('PRAGMA foreign_keys = ON')
                         self.db._fk_off = False
@@ -650,12 +657,15 @@ class Database:
 
     _tx_depth = 0
     _tx_owner = None
+    _tx_inv = True
     _tx_failed = False
     _fk_off = False
 
-    def transaction(self, foreign_keys: bool = True):
-        """``foreign_keys=False``: skip FK enforcement for this (outermost) transaction."""
-        return Database._Tx(self, foreign_keys)
+    def transaction(self, foreign_keys: bool = True, invalidate: bool = True):
+        """``foreign_keys=False``: skip FK enforcement for this (outermost) transaction.
+        ``invalidate=False``: the caller writes only through ``_x``/``_xm`` (which invalidate per table)
+        or invalidates what it wrote itself; the host caches are not dropped wholesale."""
+        return Database._Tx(self, foreign_keys, invalidate)
 
     # fault injection (tests): raise inside block application after the named stage
     fail_after_stage: Optional[str] = None
@@ -1045,21 +1055,23 @@ class Database:
         inputs/outputs address columns of every tx in blocks above the watermark (all in SQLite's C
         code). Returns the number of blocks indexed."""
         if self._address_index_height() >= self._tip_id():
-            return 0  # kept current by the block batches: no write transaction (it would drop the caches)
-        with self.transaction():
+            return 0  # kept current by the block batches: no write transaction
+        # the transaction only writes the two address tables: invalidate those, not every cache (a
+        # blanket invalidation would drop the mempool and tip caches the /push_tx path runs on)
+        with self.transaction(invalidate=False):
             wm = self._address_index_height()
             tip = self._tip_id()
             if tip <= wm:
                 return 0
-            self.conn.execute(
+            self._conn.execute(
                 'INSERT INTO address_transactions (address, tx_hash) '
                 'SELECT j.value, t.tx_hash FROM transactions t JOIN blocks b ON b.hash = t.block_hash, '
                 'json_each(t.inputs_addresses) j WHERE b.id > ? AND b.id <= ? '
                 'UNION '
                 'SELECT j.value, t.tx_hash FROM transactions t JOIN blocks b ON b.hash = t.block_hash, '
                 'json_each(t.outputs_addresses) j WHERE b.id > ? AND b.id <= ?', (wm, tip, wm, tip))
-            self.conn.execute("UPDATE address_index_state SET height = ? WHERE k = 'height'", (tip,))
-        return tip - wm
+            self._conn.execute("UPDATE address_index_state SET height = ? WHERE k = 'height'", (tip,))
+        return tip - wm  # (address tables feed no host cache: nothing to invalidate)
 
     # the per-address index of one block, inside the block's own journal batch (materialiser thread):
     # only when the watermark stands at the previous block, so a lagging index is left to the catch-up
