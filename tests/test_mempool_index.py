@@ -147,3 +147,55 @@ def test_template_and_hash_lookup_match_sql_path():
         assert await a.get_pending_transactions_hex_by_hash(want) == await b.get_pending_transactions_hex_by_hash(want[:3])
         assert await a.get_pending_transactions_hex_by_hash([txs[1].hash()]) == [txs[1].hex()]
     asyncio.run(go())
+
+
+def test_coalescer_batches_concurrent_submissions():
+    from upow_amd.utils import coalesce
+    calls = []
+
+    def fn(items):
+        calls.append(list(items))
+        return [x * 2 for x in items]
+
+    async def go():
+        c = coalesce.coalescer('test-double', fn)
+        res = await asyncio.gather(*[c.submit(k) for k in range(10)])
+        assert res == [2 * k for k in range(10)]
+        assert sum(len(b) for b in calls) == 10 and len(calls) <= 2  # first item alone at most, rest together
+    asyncio.run(go())
+
+
+@pytest.mark.gpu
+def test_admission_context_uses_batched_hbm_probe(gpu):
+    """With the admission context set (as the node's /push_tx handler does), outpoint checks and
+    signatures go through the coalescers: same verdicts as the synchronous path."""
+    from upow_amd.utils import coalesce
+
+    async def go():
+        a = await Database.create(utxo_backend='gpu')
+        b = await Database.create(utxo_backend='host')
+        base = 1_700_000_000
+        for k in range(4):
+            for db in (a, b):
+                _use(db)
+                c = await devnet.mine_header(address_of(GENESIS), [], ts=base + 60 * k, device='cpu')
+                assert await fastpath.create_block_from_hex(c, [])
+        txs = []
+        for k in KEYS[:3]:
+            _use(a)
+            txs.append(await create_transaction(GENESIS, address_of(k), '1'))
+
+        async def admit(db, tx):
+            coalesce.ADMISSION.set(True)
+            _use(db)
+            return await db.add_pending_transaction(tx)
+        for tx in txs:
+            assert await asyncio.create_task(admit(a, tx)) is True
+            assert await asyncio.create_task(admit(b, tx)) is True
+        ins = [TransactionInput(i.tx_hash, i.index + 7, amount=i.amount, public_key=i.public_key) for i in txs[0].inputs]
+        bad = Transaction(ins, [TransactionOutput(address_of(KEYS[0]), Decimal('0.5'))])
+        bad.sign([GENESIS])
+        assert await asyncio.create_task(admit(a, bad)) is False  # outpoint not in the HBM index
+        assert coalesce.stats().get('utxo-probe', {}).get('items', 0) >= 4
+        assert _pending(a) == _pending(b)
+    asyncio.run(go())

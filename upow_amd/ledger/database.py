@@ -33,6 +33,7 @@ from ..models.transaction import CoinbaseTransaction, Transaction, TransactionIn
 from ..utils import codec
 from ..utils.codec import (AddressFormat, OutputType, TransactionType, normalize_block, point_to_bytes,
                            point_to_string, round_up_decimal, sha256, string_to_bytes, string_to_point)
+from ..utils import coalesce
 from ..utils.logstore import LogStore
 from ..utils.logger import get_logger
 from .governance import GOV_TABLES, STAKE, GovernanceIndex
@@ -137,6 +138,21 @@ def numeric(value, scale: int) -> str:
     """PostgreSQL NUMERIC(p, scale) storage: round half away from zero to ``scale`` digits."""
     q = Decimal(1).scaleb(-scale)
     return str(Decimal(value).quantize(q, rounding=ROUND_HALF_UP))
+
+
+def _probe_batch(items: list) -> list:
+    """Coalesced admission probes: items are (database, tag, outpoints); one index lookup per (database,
+    tag) over the union, each item gets the set of its outpoints that are present."""
+    groups: Dict[tuple, tuple] = {}
+    for k, (db, tag, keys) in enumerate(items):
+        groups.setdefault((id(db), tag), (db, tag, []))[2].append(k)
+    res: list = [None] * len(items)
+    for db, tag, idxs in groups.values():
+        allkeys = list(dict.fromkeys(key for k in idxs for key in items[k][2]))
+        found = set(db.utxo.filter(allkeys, tag))
+        for k in idxs:
+            res[k] = found
+    return res
 
 
 def _utcnow() -> datetime:
@@ -1816,23 +1832,34 @@ class Database:
         found = set(self._select_outpoints(table, uniq))
         return [k for k in uniq if k in found]  # the index's answer order: unique, first seen
 
+    async def _outputs(self, table: str, outputs):
+        """``_filter_outputs``; a /push_tx admission on the GPU backend instead joins the event loop's
+        batched HBM-index probe (utils/coalesce.py): one device round trip for the concurrent requests,
+        on an executor thread, so the event loop neither blocks on the device nor on SQLite."""
+        if (coalesce.ADMISSION.get() and self.utxo.backend_name == 'gpu' and len(outputs) <= self.SMALL_LOOKUP
+                and os.environ.get('UPOW_ADMISSION_HBM_PROBE', '1') != '0'):
+            uniq = list(dict.fromkeys((h, int(i)) for h, i in outputs))
+            found = await coalesce.coalescer('utxo-probe', _probe_batch).submit((self, TAG_BY_TABLE[table], uniq))
+            return [k for k in uniq if k in found]
+        return self._filter_outputs(table, outputs)
+
     async def get_unspent_outputs(self, outputs):
-        return self._filter_outputs('unspent_outputs', outputs)
+        return await self._outputs('unspent_outputs', outputs)
 
     async def get_inode_outputs(self, outputs):
-        return self._filter_outputs('inode_registration_output', outputs)
+        return await self._outputs('inode_registration_output', outputs)
 
     async def get_validator_voting_power_outputs(self, outputs):
-        return self._filter_outputs('validators_voting_power', outputs)
+        return await self._outputs('validators_voting_power', outputs)
 
     async def get_delegates_voting_power_outputs(self, outputs):
-        return self._filter_outputs('delegates_voting_power', outputs)
+        return await self._outputs('delegates_voting_power', outputs)
 
     async def get_inodes_ballot_outputs(self, outputs):
-        return self._filter_outputs('inodes_ballot', outputs)
+        return await self._outputs('inodes_ballot', outputs)
 
     async def get_validators_ballot_outputs(self, outputs):
-        return self._filter_outputs('validators_ballot', outputs)
+        return await self._outputs('validators_ballot', outputs)
 
     async def get_unspent_outputs_hash(self) -> str:
         """database.py:827-830: SHA256 over (tx_hash bytes || index byte) sorted by (tx_hash, index).

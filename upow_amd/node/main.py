@@ -40,7 +40,7 @@ from ..ledger.fastpath import create_block_from_hex
 from ..ledger import worker as ledger_worker
 from ..ledger.worker import on_ledger
 from ..ops.native import lib
-from ..ops import p256 as p256_ops
+from ..utils import coalesce
 from ..parallel import cluster
 from ..ledger.manager import (Manager, block_to_bytes, calculate_difficulty, clear_pending_transactions, create_block,
                               ledger_lock,
@@ -571,8 +571,8 @@ async def root(request: Request):
 async def verify_and_push_tx(tx: Transaction, request: Request, background_tasks: BackgroundTasks):
     """main.py:417-458."""
     tx_hash = tx.hash()
-    if _ADMISSION_BATCH:  # signature checks of concurrent requests share one verify launch (ops/p256.py)
-        p256_ops.BATCH_ADMISSION.set(True)
+    if _ADMISSION_BATCH:  # checks of concurrent requests are batched off the loop (utils/coalesce.py)
+        coalesce.ADMISSION.set(True)
     if tx_hash in transactions_cache:
         logger.error(error_msg := 'Transaction just added')
         return {'ok': False, 'error': error_msg}

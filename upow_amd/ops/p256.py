@@ -7,16 +7,13 @@ is the SHA-256 digest of the signed message (big-endian, as hashed). Status code
 """
 from __future__ import annotations
 
-import asyncio
-import contextvars
 import hashlib
 import os
-import threading
-import weakref
 from typing import Iterable, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
+from ..utils import coalesce
 from ..utils import p256 as oracle
 from ..utils.p256 import EcdsaError, Point
 from .native import gpu_available, lib
@@ -77,86 +74,27 @@ def verify(sig: Tuple[int, int], msg: Union[str, bytes], q: Point) -> bool:
 
 # ---------------------------------------------------------------------------------------------- admission
 # reference: every /push_tx verifies its signatures one at a time on the node's event loop
-# (transaction_input.py:100-109 via fastecdsa). Here concurrent /push_tx handlers of one event loop hand
-# their single-signature checks to a coalescer: whatever arrives while a batch is being verified forms
-# the next batch, verified on an executor thread (the native call releases the GIL) on the GPU when the
-# batch is large enough to beat a round trip, else on host threads. The event loop never runs an
-# ECDSA verify itself, and under load one launch serves many requests.
-BATCH_ADMISSION = contextvars.ContextVar('upow_p256_batch_admission', default=False)
+# (transaction_input.py:100-109 via fastecdsa). Inside an admission context (utils/coalesce.py) the
+# checks of concurrent requests are verified together on an executor thread: on the GPU when the batch is
+# large enough to beat a round trip, else on host threads. The event loop never runs an ECDSA verify.
 ADMISSION_GPU_MIN = int(os.environ.get('UPOW_ADMISSION_GPU_MIN', '32'))
-_coalescers: 'weakref.WeakKeyDictionary' = weakref.WeakKeyDictionary()
-_pool_lock = threading.Lock()
-_pool = None
 
 
-def _executor():
-    global _pool
-    with _pool_lock:
-        if _pool is None:
-            from concurrent.futures import ThreadPoolExecutor
-            _pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix='upow-p256-admit')
-        return _pool
-
-
-def _verify_batch(buf: bytes, n: int) -> bytes:
+def _verify_batch(recs: List[bytes]) -> bytes:
+    n = len(recs)
     gpu = gpu_available() and n >= ADMISSION_GPU_MIN
-    return lib().p256_verify(np.frombuffer(buf, dtype=np.uint8), gpu, max(1, min(n, 8)))
-
-
-class _Coalescer:
-    def __init__(self, loop):
-        self.loop = loop
-        self.pending = []
-        self.running = False
-        self.batches = 0
-        self.items = 0
-
-    def submit(self, rec: bytes):
-        fut = self.loop.create_future()
-        self.pending.append((rec, fut))
-        if not self.running:
-            self.running = True
-            self.loop.create_task(self._drain())
-        return fut
-
-    async def _drain(self):
-        try:
-            while self.pending:
-                batch, self.pending = self.pending, []
-                try:
-                    st = await self.loop.run_in_executor(_executor(), _verify_batch,
-                                                         b''.join(r for r, _ in batch), len(batch))
-                except Exception as e:  # noqa: BLE001 - handed to every waiter
-                    for _, f in batch:
-                        if not f.done():
-                            f.set_exception(e)
-                    continue
-                self.batches += 1
-                self.items += len(batch)
-                for (_, f), v in zip(batch, st):
-                    if not f.done():
-                        f.set_result(v)
-        finally:
-            self.running = False
-
-
-def coalescer_stats() -> dict:
-    return {'batches': sum(c.batches for c in _coalescers.values()), 'items': sum(c.items for c in _coalescers.values())}
+    return lib().p256_verify(np.frombuffer(b''.join(recs), dtype=np.uint8), gpu, max(1, min(n, 8)))
 
 
 async def verify_async(sig: Tuple[int, int], msg: Union[str, bytes], q: Point) -> bool:
-    """:func:`verify` (same result, same exceptions); inside a ``BATCH_ADMISSION`` context it goes through
-    the event loop's coalescer instead of running on the loop."""
-    if not BATCH_ADMISSION.get():
+    """:func:`verify` (same result, same exceptions); inside an admission context it goes through the
+    event loop's signature coalescer instead of running on the loop."""
+    if not coalesce.ADMISSION.get():
         return verify(sig, msg, q)
     r, s = sig
     if r >= 1 << 256 or s >= 1 << 256 or r < 0 or s < 0:
         raise EcdsaError('Invalid Signature: r/s out of range')
-    loop = asyncio.get_running_loop()
-    c = _coalescers.get(loop)
-    if c is None:
-        c = _coalescers[loop] = _Coalescer(loop)
-    st = await c.submit(record(q, sig, hashlib.sha256(_msg(msg)).digest()))
+    st = await coalesce.coalescer('p256-admit', _verify_batch).submit(record(q, sig, hashlib.sha256(_msg(msg)).digest()))
     if st == BAD_KEY:
         raise EcdsaError('Invalid public key, point is not on curve P256')
     if st == BAD_RANGE:
@@ -183,4 +121,4 @@ def decompress(addresses33: Sequence[bytes], device: Optional[str] = None):
     return res
 
 
-__all__ = ['public_key', 'sign', 'verify', 'verify_async', 'BATCH_ADMISSION', 'verify_records', 'decompress', 'record', 'EcdsaError', 'oracle']
+__all__ = ['public_key', 'sign', 'verify', 'verify_async', 'verify_records', 'decompress', 'record', 'EcdsaError', 'oracle']
