@@ -180,18 +180,16 @@ def test_admission_context_uses_batched_hbm_probe(gpu):
                 _use(db)
                 c = await devnet.mine_header(address_of(GENESIS), [], ts=base + 60 * k, device='cpu')
                 assert await fastpath.create_block_from_hex(c, [])
-        txs = []
-        for k in KEYS[:3]:
-            _use(a)
-            txs.append(await create_transaction(GENESIS, address_of(k), '1'))
-
         async def admit(db, tx):
             coalesce.ADMISSION.set(True)
             _use(db)
             return await db.add_pending_transaction(tx)
-        for tx in txs:
-            assert await asyncio.create_task(admit(a, tx)) is True
-            assert await asyncio.create_task(admit(b, tx)) is True
+        txs = []
+        for k in KEYS[:3]:  # each built after the previous one is pending on `a`
+            _use(a)
+            txs.append(await create_transaction(GENESIS, address_of(k), '1'))
+            assert await asyncio.create_task(admit(a, txs[-1])) is True
+            assert await asyncio.create_task(admit(b, txs[-1])) is True
         ins = [TransactionInput(i.tx_hash, i.index + 7, amount=i.amount, public_key=i.public_key) for i in txs[0].inputs]
         bad = Transaction(ins, [TransactionOutput(address_of(KEYS[0]), Decimal('0.5'))])
         bad.sign([GENESIS])
