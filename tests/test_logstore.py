@@ -1,6 +1,7 @@
 """Append-only emission-details store (utils/logstore.py) — reference: the pickledb file rewritten whole
 on every per-block ``set`` (upow/database.py:22, manager.py:741-756)."""
 import json
+import os
 import time
 
 from upow_amd.utils.logstore import LogStore
@@ -50,3 +51,14 @@ def test_torn_tail_legacy_migration_and_compaction(tmp_path):
     assert st.get('3') == [2999]
     st.close()
     assert sum(1 for _ in open(path)) <= 1030
+
+
+def test_file_log_goes_through_listener_thread(tmp_path):
+    """Node/miner entry points turn file logging on (reference: logs/app.log always); records are
+    written by a listener thread into <data dir>/logs/app.log."""
+    import subprocess
+    import sys
+    code = "from upow_amd.utils.logger import get_logger; get_logger().info('hello from the node')"
+    env = dict(os.environ, UPOW_FILE_LOG='1', UPOW_DATA_DIR=str(tmp_path), UPOW_LOG_DIR='')
+    subprocess.run([sys.executable, '-c', code], env=env, check=True, cwd=os.path.dirname(os.path.dirname(__file__)))
+    assert 'hello from the node' in (tmp_path / 'logs' / 'app.log').read_text()

@@ -86,6 +86,7 @@ def main(argv=None):
                          'kernels between dispatches at a ~1%% hashrate cost; 28 for a dedicated GPU '
                          '(docs/PERF.md §3)')
     a = ap.parse_args(argv)
+    os.environ.setdefault('UPOW_FILE_LOG', '1')  # reference: logs/app.log always (my_logger.py:17-53)
     os.environ['UPOW_POW_DISPATCH_LOG2'] = str(a.dispatch_log2)
     from . import config
     node_url = (a.node_url or os.environ.get('UPOW_MINING_NODE_URL') or 'http://localhost:3006/').strip('/') + '/'

@@ -21,6 +21,7 @@ def main(argv=None):
         os.environ['UPOW_DATABASE_PATH'] = a.db
     if a.core_url is not None:
         os.environ['UPOW_CORE_URL'] = a.core_url
+    os.environ.setdefault('UPOW_FILE_LOG', '1')  # reference: logs/app.log always (my_logger.py:17-53)
     import uvicorn
     if a.cluster and int(os.environ.get('WORLD_SIZE', '1')) > 1:
         return _run_cluster(a)

@@ -1,9 +1,10 @@
 """Logging (reference: upow/my_logger.py:8-53, upow/helpers.py:20,24-28).
 
-One process-wide ``'upow'`` logger: rotating file ``logs/app.log`` (5 MB x 100, DEBUG) plus console
-(INFO; WARNING with ``--nologs``). The file handler is only attached when ``UPOW_LOG_DIR`` (default
-``logs``) is writable, so library use (tests, benches) does not litter the working directory unless
-``UPOW_FILE_LOG=1``.
+One process-wide ``'upow'`` logger: rotating file ``app.log`` (5 MB x 100, DEBUG) plus console
+(INFO; WARNING with ``--nologs``). The node and miner entry points turn the file on by default
+(``UPOW_FILE_LOG=1``, as the reference always writes ``logs/app.log``); library use (tests, benches)
+leaves it off unless asked. The directory is ``UPOW_LOG_DIR``, else ``<UPOW_DATA_DIR>/logs``, else
+``./logs``.
 """
 from __future__ import annotations
 
@@ -33,15 +34,25 @@ def _configure():
     console.setFormatter(fmt)
     logger.addHandler(console)
     if os.environ.get('UPOW_FILE_LOG', '0') == '1':
-        log_dir = os.environ.get('UPOW_LOG_DIR', 'logs')
+        data = os.environ.get('UPOW_DATA_DIR')
+        log_dir = os.environ.get('UPOW_LOG_DIR') or (os.path.join(data, 'logs') if data else 'logs')
         try:
             os.makedirs(log_dir, exist_ok=True)
             fh = RotatingFileHandler(os.path.join(log_dir, 'app.log'), maxBytes=5 * 1024 * 1024, backupCount=100)
-            fh.setLevel(logging.DEBUG)
-            fh.setFormatter(fmt)
-            logger.addHandler(fh)
         except OSError:
-            pass
+            return
+        fh.setLevel(logging.DEBUG)
+        fh.setFormatter(fmt)
+        # formatting and file I/O on a listener thread: /push_tx logs several lines per request, and the
+        # event loop should only pay for queueing the record
+        import atexit
+        import queue
+        from logging.handlers import QueueHandler, QueueListener
+        q: queue.SimpleQueue = queue.SimpleQueue()
+        listener = QueueListener(q, fh, respect_handler_level=True)
+        listener.start()
+        atexit.register(listener.stop)
+        logger.addHandler(QueueHandler(q))
 
 
 def get_logger(name: str = 'upow') -> logging.Logger:
