@@ -281,12 +281,16 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
 // database file), [str guard], [i64 expect],
 // i64 n, u32 n_cols, cols..., u8 has_order, [i64 order[n]].
 py::bytes encode_stmt(const std::string& sql, py::sequence cols, int64_t n, py::object order, py::object guard,
-                      py::object expect, int shard) {
+                      py::object expect, int shard, int route) {
     if (n < 0) throw std::invalid_argument("n < 0");
     if (shard < 0 || shard > 15) throw std::invalid_argument("shard must be in [0, 15]");
+    if (route < 0 || route > 8 || shard + route > 16) throw std::invalid_argument("route must be in [0, 8]");
     Out o;
     o.str(sql);
-    const uint32_t flags = (guard.is_none() ? 0u : 1u) | (expect.is_none() ? 0u : 2u) | (uint32_t(shard) << 8);
+    // route > 1: the rows are spread over files shard .. shard+route-1 by the first byte of column 0
+    // (a tx hash), each file's materialiser applying only its own rows
+    const uint32_t flags = (guard.is_none() ? 0u : 1u) | (expect.is_none() ? 0u : 2u) | (uint32_t(shard) << 8) |
+                           (route > 1 ? (4u | (uint32_t(route) << 16)) : 0u);
     o.u32(flags);
     if (flags & 1) o.str(guard.cast<std::string>());
     if (flags & 2) o.i64(expect.cast<int64_t>());
@@ -321,6 +325,25 @@ int64_t ld64(const char* p) {
     int64_t v;
     std::memcpy(&v, p, 8);
     return v;
+}
+
+uint32_t hex_nibble(char c) {
+    if (c >= '0' && c <= '9') return uint32_t(c - '0');
+    if (c >= 'a' && c <= 'f') return uint32_t(c - 'a' + 10);
+    if (c >= 'A' && c <= 'F') return uint32_t(c - 'A' + 10);
+    return 0;
+}
+
+// First byte of row r's tx hash in column c (raw hex32 rows, or hex text): the routing key of a
+// statement spread over several files.
+uint32_t route_byte(const ColView& c, int64_t r) {
+    if (c.kind == K_HEX32) return uint8_t(c.data[32 * r]);
+    if (c.kind == K_TEXT && !(c.nul && c.nul[r])) {
+        const int64_t o0 = ld64(c.off + 8 * r), o1 = ld64(c.off + 8 * (r + 1));
+        if (o1 - o0 >= 2) return (hex_nibble(c.data[o0]) << 4) | hex_nibble(c.data[o0 + 1]);
+    }
+    if (c.kind == K_CTEXT && c.ctext.size() >= 2) return (hex_nibble(c.ctext[0]) << 4) | hex_nibble(c.ctext[1]);
+    return 0;
 }
 
 const char kHex[] = "0123456789abcdef";
@@ -745,15 +768,30 @@ class LedgerWriter {
             }
             const char* order = nullptr;
             if (in.get<uint8_t>()) order = in.take(size_t(n) * 8);
-            if (target >= shards_.size()) throw std::runtime_error("ledger batch: statement for an unknown file");
-            if (target != shard) continue;
+            const size_t route = (flags & 4) ? ((flags >> 16) & 0xffu) : 1;
+            if (target + route > shards_.size()) throw std::runtime_error("ledger batch: statement for an unknown file");
+            if (shard < target || shard >= target + route) continue;
             if (!guard.empty() && query_int(sh.db, guard) == 0) continue;
+            // routed statement: which rows belong to this file (first byte of the column-0 tx hash)
+            std::vector<uint8_t> mine;
+            if (route > 1) {
+                if (nc == 0) throw std::runtime_error("ledger batch: routed statement without columns");
+                mine.assign(size_t(n), 0);
+                int64_t cnt = 0;
+                for (int64_t r = 0; r < n; ++r) {
+                    const uint32_t b = route_byte(cols[0], r);
+                    mine[size_t(r)] = uint8_t((b * route) >> 8) == uint8_t(shard - target);
+                    cnt += mine[size_t(r)];
+                }
+                if (expect == n) expect = cnt;  // "every row changes" holds per file
+            }
             const auto ts0 = std::chrono::steady_clock::now();
             sqlite3_stmt* st = prepared(sh, sql);
             int64_t changes = 0;
             char hexbuf[8][64];
             for (int64_t k = 0; k < n; ++k) {
                 const int64_t r = order ? ld64(order + 8 * k) : k;
+                if (!mine.empty() && !mine[size_t(r)]) continue;
                 int hb = 0;
                 for (uint32_t j = 0; j < nc; ++j) {
                     const ColView& c = cols[j];
@@ -974,7 +1012,7 @@ void register_ledger_writer(py::module_& m) {
     m.attr("sqlite_memstatus_config_rc") = memstatus_rc;
     m.def("ledger_encode_stmt", &encode_stmt, py::arg("sql"), py::arg("cols"), py::arg("n"),
           py::arg("order") = py::none(), py::arg("guard") = py::none(), py::arg("expect") = py::none(),
-          py::arg("shard") = 0, "encode one column-major bulk statement for LedgerWriter.submit");
+          py::arg("shard") = 0, py::arg("route") = 1, "encode one column-major bulk statement for LedgerWriter.submit");
     m.def("crc32c", [](py::buffer b) {
         py::buffer_info bi = b.request();
         return crc32c(0, bi.ptr, size_t(bi.size * bi.itemsize));

@@ -140,3 +140,47 @@ def test_sigkill_between_journal_append_and_sql_catch_up(tmp_path):
             db2.close()
 
     asyncio.run(check())
+
+
+def test_single_utxo_file_ledger_is_split_on_open(tmp_path):
+    """A ledger written with one UTXO file (before the 00-7f / 80-ff split) opens with the rows of the
+    high half moved to the second file (row ids kept), the same UTXO set and K12 hash, and keeps
+    applying blocks."""
+    import asyncio
+    import sqlite3
+    sys.path.insert(0, ROOT)
+    from upow_amd import bench_verify
+    from upow_amd.ledger.database import Database
+
+    path = str(tmp_path / 'ledger.sqlite3')
+
+    async def build():
+        db, *_ = await bench_verify._setup(2, 40, 7, 'host', 'cpu', ledger_path=path)
+        rows = sorted(tuple(r) for r in db._q('SELECT rowid, tx_hash, "index", address, is_stake FROM unspent_outputs'))
+        h = db.sql_unspent_outputs_hash()
+        db.close()
+        return rows, h
+    rows, h = asyncio.run(build())
+    assert any(r[1] >= '8' for r in rows) and any(r[1] < '8' for r in rows)
+    # fold the second file back into the first: the layout of a ledger from before the split
+    c = sqlite3.connect(path + '-utxo', isolation_level=None)
+    c.execute('ATTACH DATABASE ? AS hi', (path + '-utxo2',))
+    c.execute('INSERT INTO unspent_outputs (rowid, tx_hash, "index", address, is_stake) '
+              'SELECT rowid, tx_hash, "index", address, is_stake FROM hi.unspent_outputs')
+    c.execute('DETACH DATABASE hi')
+    c.close()
+    for sfx in ('', '-wal', '-shm'):
+        if os.path.exists(path + '-utxo2' + sfx):
+            os.remove(path + '-utxo2' + sfx)
+
+    async def reopen():
+        db = await Database.create(path=path, utxo_backend='host')
+        got = sorted(tuple(r) for r in db._q('SELECT rowid, tx_hash, "index", address, is_stake FROM unspent_outputs'))
+        hi = db._q1("SELECT COUNT(*) FROM utxo.unspent_outputs WHERE tx_hash >= '8'")[0]
+        lo2 = db._q1("SELECT COUNT(*) FROM utxo2.unspent_outputs WHERE tx_hash < '8'")[0]
+        ok = got == rows and hi == 0 and lo2 == 0 and db.sql_unspent_outputs_hash() == h == db.utxo.set_hash()
+        nxt = db._utxo_next_rowid
+        db.close()
+        return ok, nxt
+    ok, nxt = asyncio.run(reopen())
+    assert ok and nxt == max(r[0] for r in rows) + 1

@@ -103,27 +103,54 @@ for _t in OUTPUT_TABLES[1:]:
     SCHEMA += f'CREATE INDEX IF NOT EXISTS {_t}_address_idx ON {_t} (address);\n'
 
 
-# The UTXO table lives in a database file of its own (``<ledger>-utxo``, attached as ``utxo``): the native
-# writer materialises it on its own thread in parallel with the block/tx tables. SQLite cannot declare a
-# foreign key across files, so the reference's ``tx_hash REFERENCES transactions(tx_hash) ON DELETE
-# CASCADE`` (schema.sql) is kept as a TEMP trigger on the Python connection (see Database.__init__).
-UTXO_SCHEMA = """
-CREATE TABLE IF NOT EXISTS utxo.unspent_outputs (
+# The UTXO table is split over two database files of its own by the first byte of the tx hash
+# (``<ledger>-utxo``: 00-7f, attached as ``utxo``; ``<ledger>-utxo2``: 80-ff, attached as ``utxo2``): a
+# block rewrites ~33k UTXO rows, the largest share of its SQL, and each file has a native materialiser
+# thread of its own (csrc/ledger_writer.cpp routes a statement's rows by that byte).
+#
+# * Row ids come from one ledger-wide counter (explicit ``rowid`` on every insert), so ``rowid`` order
+#   over both files is insertion order, as in the single table of schema.sql.
+# * On the Python connection ``unspent_outputs`` is a TEMP view over both files for reads; Python-side
+#   writes are routed by :meth:`Database._utxo_exec` (a trigger body cannot name an attached table).
+# * SQLite cannot declare a foreign key across files: the reference's ``tx_hash REFERENCES
+#   transactions(tx_hash) ON DELETE CASCADE`` is applied by the block-deleting methods themselves.
+UTXO_SCHEMAS = ('utxo', 'utxo2')
+UTXO_SUFFIXES = ('-utxo', '-utxo2')
+
+
+def utxo_schema(schema: str = 'utxo') -> str:
+    return f"""
+CREATE TABLE IF NOT EXISTS {schema}.unspent_outputs (
     tx_hash TEXT,
     "index" INTEGER NOT NULL,
     address TEXT NULL,
     is_stake INTEGER
 );
-CREATE INDEX IF NOT EXISTS utxo.tx_hash_idx ON unspent_outputs (tx_hash, "index");
+CREATE INDEX IF NOT EXISTS {schema}.tx_hash_idx ON unspent_outputs (tx_hash, "index");
 """
-UTXO_CASCADE = ("CREATE TEMP TRIGGER IF NOT EXISTS upow_unspent_cascade AFTER DELETE ON main.transactions "
-                "BEGIN DELETE FROM unspent_outputs WHERE tx_hash = OLD.tx_hash; END")
-SHARD_OF_TABLE = {'unspent_outputs': 1}  # every other table is in the main file (shard 0)
+
+
+UTXO_SCHEMA = utxo_schema('utxo')
+UTXO_VIEW = """
+CREATE TEMP VIEW IF NOT EXISTS unspent_outputs AS
+    SELECT rowid AS rowid, tx_hash, "index", address, is_stake FROM utxo.unspent_outputs
+    UNION ALL
+    SELECT rowid AS rowid, tx_hash, "index", address, is_stake FROM utxo2.unspent_outputs;
+"""
+# table -> the writer files (shards) holding it; every other table is in the main file (shard 0). A table
+# on several files is written by routed statements: (first file, number of files).
+SHARD_OF_TABLE = {'unspent_outputs': (1, 2)}
+ROUTED_TABLES = {'unspent_outputs': (1, 2)}
+
+
+def utxo_file_of(tx_hash: str) -> int:
+    """0 for ``utxo`` (hash 00-7f), 1 for ``utxo2`` (80-ff) — the writer's routing (first byte * 2 >> 8)."""
+    return 0 if tx_hash[:1] < '8' else 1
 
 
 def ledger_files(path: str) -> List[str]:
-    """Every file of a (closed) file ledger: the main database, the UTXO database and the journal."""
-    return [path, path + '-utxo', path + '.journal']
+    """Every file of a (closed) file ledger: the main database, the two UTXO databases and the journal."""
+    return [path] + [path + sfx for sfx in UTXO_SUFFIXES] + [path + '.journal']
 
 
 def copy_ledger(src: str, dst: str):
@@ -349,16 +376,24 @@ class Database:
         if bg:
             self._start_checkpointer(float(os.environ.get('UPOW_WAL_CHECKPOINT_PERIOD', '0.5')))
         self._conn.executescript(SCHEMA)
-        self.utxo_file = self.file + '-utxo'
-        self._conn.execute('ATTACH DATABASE ? AS utxo', (self.utxo_file,))
-        self._conn.execute('PRAGMA utxo.journal_mode = WAL')
-        self._conn.execute('PRAGMA utxo.synchronous = ' + ('OFF' if path == ':memory:' else 'NORMAL'))
-        self._conn.execute(f'PRAGMA utxo.cache_size = -{cache_mb * 1024}')
-        self._conn.executescript(UTXO_SCHEMA)
+        self.utxo_files = [self.file + sfx for sfx in UTXO_SUFFIXES]
+        self.utxo_file = self.utxo_files[0]
+        fresh2 = not os.path.exists(self.utxo_files[1])
+        for schema, f in zip(UTXO_SCHEMAS, self.utxo_files):
+            self._conn.execute(f'ATTACH DATABASE ? AS {schema}', (f,))
+            self._conn.execute(f'PRAGMA {schema}.journal_mode = WAL')
+            self._conn.execute(f'PRAGMA {schema}.synchronous = ' + ('OFF' if path == ':memory:' else 'NORMAL'))
+            self._conn.execute(f'PRAGMA {schema}.cache_size = -{cache_mb * 1024}')
+            self._conn.executescript(utxo_schema(schema))
         self._migrate_single_file_utxo()
-        self._conn.execute(UTXO_CASCADE)
+        if fresh2:
+            self._migrate_utxo_split()
+        self._conn.executescript(UTXO_VIEW)
         if os.environ.get('UPOW_LEDGER_WRITER', '1') != '0':
             self._open_writer(cache_mb)
+        # next UTXO row id: one counter over both files (row id order = insertion order, as in one table)
+        self._utxo_next_rowid = 1 + max(self._conn.execute(f'SELECT COALESCE(MAX(rowid), 0) FROM {s}.unspent_outputs')
+                                        .fetchone()[0] for s in UTXO_SCHEMAS)
         store_dir = os.path.dirname(path) if path != ':memory:' else None
         # per-block inode emission records (reference: pickledb emission_details.json): an append-only log
         self.emission_details = LogStore(os.path.join(store_dir, 'emission_details.jsonl') if store_dir else None,
@@ -387,11 +422,30 @@ class Database:
         c = self._conn
         if c.execute("SELECT 1 FROM main.sqlite_master WHERE type = 'table' AND name = 'unspent_outputs'").fetchone():
             c.execute('BEGIN')
-            c.execute('INSERT INTO utxo.unspent_outputs (tx_hash, "index", address, is_stake) '
-                      'SELECT tx_hash, "index", address, is_stake FROM main.unspent_outputs ORDER BY rowid')
+            c.execute('INSERT INTO utxo.unspent_outputs (rowid, tx_hash, "index", address, is_stake) '
+                      'SELECT rowid, tx_hash, "index", address, is_stake FROM main.unspent_outputs ORDER BY rowid')
             c.execute('DROP TABLE main.unspent_outputs')
             c.execute('COMMIT')
             logger.info('ledger: moved unspent_outputs into its own database file')
+
+    def _migrate_utxo_split(self):
+        """Ledgers written with one UTXO file: move the rows of hashes 80-ff (with their row ids) into
+        the second file, whose journal watermark starts where the first file's stands."""
+        c = self._conn
+        move = c.execute("SELECT 1 FROM utxo.unspent_outputs WHERE tx_hash >= '8' LIMIT 1").fetchone() is not None
+        c.execute('BEGIN')
+        if move:
+            c.execute('INSERT INTO utxo2.unspent_outputs (rowid, tx_hash, "index", address, is_stake) '
+                      "SELECT rowid, tx_hash, \"index\", address, is_stake FROM utxo.unspent_outputs "
+                      "WHERE tx_hash >= '8' ORDER BY rowid")
+            c.execute("DELETE FROM utxo.unspent_outputs WHERE tx_hash >= '8'")
+        if c.execute("SELECT 1 FROM utxo.sqlite_master WHERE type = 'table' AND name = 'upow_journal_state'").fetchone():
+            c.execute('CREATE TABLE IF NOT EXISTS utxo2.upow_journal_state (k INTEGER PRIMARY KEY CHECK (k = 0), '
+                      'seq INTEGER NOT NULL)')
+            c.execute('INSERT OR REPLACE INTO utxo2.upow_journal_state (k, seq) SELECT k, seq FROM utxo.upow_journal_state')
+        c.execute('COMMIT')
+        if move:
+            logger.info('ledger: split unspent_outputs over two database files')
 
     def _open_writer(self, cache_mb: int):
         """The native writer owns its own connection to the same file. Opening it re-applies any
@@ -402,7 +456,7 @@ class Database:
             mode = 0
         journal = os.environ.get('UPOW_JOURNAL_PATH') or os.path.join(os.path.dirname(os.path.abspath(self.file)),
                                                                        os.path.basename(self.file) + '.journal')
-        self.writer = lib().LedgerWriter([self.file, self.utxo_file], journal, mode, cache_mb,
+        self.writer = lib().LedgerWriter([self.file, *self.utxo_files], journal, mode, cache_mb,
                                          int(os.environ.get('UPOW_WRITER_GROUP', '8')),
                                          int(os.environ.get('UPOW_JOURNAL_MAX_MB', '1024')) << 20)
         self._eph['writer'] = self.writer if self.path == ':memory:' else None
@@ -450,7 +504,8 @@ class Database:
 
         def run(stop: threading.Event):
             conn = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
-            conn.execute('ATTACH DATABASE ? AS utxo', (path + '-utxo',))
+            for schema, sfx in zip(UTXO_SCHEMAS, UTXO_SUFFIXES):
+                conn.execute(f'ATTACH DATABASE ? AS {schema}', (path + sfx,))
             try:
                 while not stop.wait(period):
                     try:
@@ -494,9 +549,9 @@ class Database:
             waits = {}
             for t in tables:
                 seq = ts.get(t, 0)
-                sh = SHARD_OF_TABLE.get(t, 0)
-                if seq > waits.get(sh, 0):
-                    waits[sh] = seq
+                for sh in SHARD_OF_TABLE.get(t, (0,)):
+                    if seq > waits.get(sh, 0):
+                        waits[sh] = seq
         seen = self._applied_seen
         for sh, target in waits.items():
             if target <= seen.get(sh, 0) or target <= seen.get(-1, 0):
@@ -512,15 +567,17 @@ class Database:
         if self.writer is None:
             return True
         seq = self._table_seq.get(table, 0)
-        sh = SHARD_OF_TABLE.get(table, 0)
         seen = self._applied_seen
-        if seq <= seen.get(sh, 0) or seq <= seen.get(-1, 0):
+        if seq <= seen.get(-1, 0):
             return True
-        applied = self.writer.applied(sh)
-        if applied >= seq:
+        for sh in SHARD_OF_TABLE.get(table, (0,)):
+            if seq <= seen.get(sh, 0):
+                continue
+            applied = self.writer.applied(sh)
+            if applied < seq:
+                return False
             seen[sh] = max(seen.get(sh, 0), applied)
-            return True
-        return False
+        return True
 
     def lagging(self) -> bool:
         """Is any journaled batch not yet in SQL? (never waits)"""
@@ -595,6 +652,8 @@ class Database:
         self._settle(t)
         with self.lock:
             self._invalidate_for(t)
+            if t and 'unspent_outputs' in t:
+                return self._utxo_exec(sql, [tuple(args)])
             return self._conn.execute(sql, tuple(args))
 
     def _xm(self, sql: str, rows: Iterable):
@@ -602,7 +661,63 @@ class Database:
         self._settle(t)
         with self.lock:
             self._invalidate_for(t)
+            if t and 'unspent_outputs' in t:
+                return self._utxo_exec(sql, list(rows))
             return self._conn.executemany(sql, rows)
+
+    class _Changed:
+        def __init__(self, n: int):
+            self.rowcount = n
+
+    _UTXO_INSERT = re.compile(r'^\s*INSERT\s+(OR\s+\w+\s+)?INTO\s+unspent_outputs\s*\(([^)]*)\)\s*VALUES', re.I)
+    _UTXO_TARGET = re.compile(r'^(\s*(?:DELETE\s+FROM|UPDATE))\s+unspent_outputs\b', re.I)
+
+    def _utxo_rowids(self, n: int) -> int:
+        """First of ``n`` consecutive row ids from the ledger-wide UTXO counter."""
+        with self._seq_lock:
+            base = self._utxo_next_rowid
+            self._utxo_next_rowid += n
+        return base
+
+    def _utxo_exec(self, sql: str, rows: list) -> '_Changed':
+        """A Python-side write to ``unspent_outputs`` (caller holds the lock, tables settled), routed to
+        the file(s) holding the rows: INSERTs by tx hash with row ids from the ledger-wide counter,
+        ``DELETE ... WHERE tx_hash = ? ...`` by tx hash, anything else on both files."""
+        c = self._conn
+        m = self._UTXO_INSERT.match(sql)
+        if m:
+            cols = [x.strip().strip('"') for x in m.group(2).split(',')]
+            h = cols.index('tx_hash')
+            values = sql[m.end():]
+            if 'rowid' not in cols:
+                base = self._utxo_rowids(len(rows))
+                rows = [(*r, base + k) for k, r in enumerate(rows)]
+                values = values.replace(')', ', ?)', 1)
+                cols.append('rowid')
+            head = f'INSERT {m.group(1) or ""}INTO %s.unspent_outputs ({", ".join(chr(34) + x + chr(34) if x == "index" else x for x in cols)}) VALUES'
+            n = 0
+            for f, schema in enumerate(UTXO_SCHEMAS):
+                part = [r for r in rows if utxo_file_of(r[h]) == f]
+                if part:
+                    n += c.executemany(head % schema + values, part).rowcount
+            return self._Changed(n)
+        m = self._UTXO_TARGET.match(sql)
+        if not m:
+            raise RuntimeError(f'unroutable write to unspent_outputs: {sql[:80]}')
+        by_hash = re.search(r'\bWHERE\s+tx_hash\s*=\s*\?', sql, re.I) is not None
+        n = 0
+        for f, schema in enumerate(UTXO_SCHEMAS):
+            part = [r for r in rows if utxo_file_of(r[0]) == f] if by_hash else rows
+            if part:
+                q = m.group(1) + f' {schema}.unspent_outputs' + sql[m.end():]
+                n += c.executemany(q, part).rowcount if part != [()] else c.execute(q).rowcount
+        return self._Changed(n)
+
+    def _utxo_cascade(self, tx_hashes: Iterable[str]):
+        """``ON DELETE CASCADE`` from transactions to unspent_outputs (schema.sql) for deleted txs."""
+        hs = [(h,) for h in tx_hashes]
+        if hs:
+            self._xm('DELETE FROM unspent_outputs WHERE tx_hash = ?', hs)
 
     # ------------------------------------------------------------------ native bulk writes
     @staticmethod
@@ -613,7 +728,11 @@ class Database:
         block codec's buffers, or one constant for every row."""
         from ..ops.native import lib
         tables = _tables_of(sql, False) or frozenset()
-        shard = max((SHARD_OF_TABLE.get(t, 0) for t in tables), default=0)
+        for t in tables:
+            if t in ROUTED_TABLES:  # rows spread over the table's files by tx hash (column 0)
+                first, count = ROUTED_TABLES[t]
+                return lib().ledger_encode_stmt(sql, cols, n, order, guard, expect, first, count)
+        shard = max((max(SHARD_OF_TABLE.get(t, (0,))) for t in tables), default=0)
         return lib().ledger_encode_stmt(sql, cols, n, order, guard, expect, shard)
 
     def bulk(self, sql: str, cols: list, n: int, order=None) -> int:
@@ -891,17 +1010,27 @@ class Database:
     async def delete_blockchain(self):
         with self.transaction():
             self.conn.execute('DELETE FROM transactions')
+            for schema in UTXO_SCHEMAS:  # the cascade to unspent_outputs (every row belongs to a tx)
+                self._conn.execute(f'DELETE FROM {schema}.unspent_outputs')
             self.conn.execute('DELETE FROM blocks')
             self.conn.execute("UPDATE address_index_state SET height = 0 WHERE k = 'height'")
         self._rebuild_utxo_index()
 
+    def _block_tx_hashes(self, where: str, args: tuple) -> List[str]:
+        return [r[0] for r in self._q(f'SELECT t.tx_hash FROM transactions t JOIN blocks b ON b.hash = t.block_hash '
+                                      f'WHERE {where}', args)]
+
     async def delete_block(self, id: int):
+        gone = self._block_tx_hashes('b.id = ?', (id,))
         self._x('DELETE FROM blocks WHERE id = ?', (id,))
+        self._utxo_cascade(gone)
         self._address_index_rollback()
         self._rebuild_utxo_index()
 
     async def delete_blocks(self, offset: int):
+        gone = self._block_tx_hashes('b.id > ?', (offset,))
         self._x('DELETE FROM blocks WHERE id > ?', (offset,))
+        self._utxo_cascade(gone)
         self._address_index_rollback()
         self._rebuild_utxo_index()
 
@@ -921,7 +1050,9 @@ class Database:
             if isinstance(tx, Transaction):
                 outputs_to_be_restored.extend([(i.tx_hash, i.index) for i in tx.inputs if i.tx_hash not in hashes])
         undone = self._undo_blocks_in_index(block_no, tip)
+        gone = self._block_tx_hashes('b.id >= ?', (block_no,))
         self._x('DELETE FROM blocks WHERE id >= ?', (block_no,))
+        self._utxo_cascade(gone)
         self._address_index_rollback()
         await self.add_unspent_outputs(outputs_to_be_restored, index=not undone)
         if self.writer is not None:
@@ -1433,15 +1564,20 @@ class Database:
         stmts.append(('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, outputs_addresses, '
                       'outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)', [b['hash'], *tx_cols], n, None, None, None))
         self.checkpoint('transactions')
-        ins_u = 'INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) VALUES (?, ?, ?, ?)'
+        # explicit row ids from the ledger-wide counter: the rows land in two files (see UTXO_SCHEMAS)
+        ins_u = 'INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake, rowid) VALUES (?, ?, ?, ?, ?)'
         if n_out:
+            base = self._utxo_rowids(n_out)
             stmts.append((ins_u, [('hex32', np.ascontiguousarray(out_txid), 32, 0),
-                                  np.ascontiguousarray(out_index, dtype=np.int64), out_addr_spec, 0],
+                                  np.ascontiguousarray(out_index, dtype=np.int64), out_addr_spec, 0,
+                                  np.arange(base, base + n_out, dtype=np.int64)],
                           n_out, None, None, None))
         if coinbase_outputs:
+            base = self._utxo_rowids(len(coinbase_outputs))
             stmts.append((ins_u, [[o[0] for o in coinbase_outputs], np.array([o[1] for o in coinbase_outputs], np.int64),
                                   [o[2] for o in coinbase_outputs],
-                                  [None if o[3] is None else str(int(bool(o[3]))) for o in coinbase_outputs]],
+                                  [None if o[3] is None else str(int(bool(o[3]))) for o in coinbase_outputs],
+                                  np.arange(base, base + len(coinbase_outputs), dtype=np.int64)],
                           len(coinbase_outputs), None, None, None))
         self.checkpoint('outputs')
         tables = {'blocks', 'transactions', 'unspent_outputs'}
@@ -1536,9 +1672,11 @@ class Database:
         created = []  # (table, key, payload fields) for the indexes
         u = outs['unspent_outputs']
         if u:
-            stmts.append(('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) VALUES (?, ?, ?, ?)',
+            base = self._utxo_rowids(len(u))
+            stmts.append(('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake, rowid) VALUES (?, ?, ?, ?, ?)',
                           [[o[0] for o in u], np.array([o[1] for o in u], np.int64), [o[2] for o in u],
-                           [None if o[3] is None else str(int(bool(o[3]))) for o in u]], len(u), None, None, None))
+                           [None if o[3] is None else str(int(bool(o[3]))) for o in u],
+                           np.arange(base, base + len(u), dtype=np.int64)], len(u), None, None, None))
         for table in self._GOV_INSERT_ORDER:
             g = outs[table]
             if g:

@@ -58,7 +58,7 @@ async def rebuild_utxo(path: str = None):
     db = await Database.create(path=path)
     outputs = await db.get_unspent_outputs_from_all_transactions()
     with db.transaction():
-        db.conn.execute('DELETE FROM unspent_outputs')
+        db._x('DELETE FROM unspent_outputs')
     await db.add_unspent_outputs(sorted(outputs))
     await db.set_unspent_outputs_addresses()
     db._rebuild_utxo_index()
