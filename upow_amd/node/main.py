@@ -703,13 +703,15 @@ async def push_block(request: Request, background_tasks: BackgroundTasks, block_
     block_hash = sha256(block_content)
     Manager.difficulty = None
     difficulty, last_block = await get_difficulty()
-    pending = sorted(await db.get_pending_transactions_limit(hex_only=True))
+    hexes, hashes_p = db.pending_template()  # the next template, from the mempool index's keys and hashes
+    order = sorted(range(len(hexes)), key=hexes.__getitem__)
+    pending = [hexes[k] for k in order]
     if LAST_PENDING_TRANSACTIONS_CLEAN[0] < timestamp() - 600:
         LAST_PENDING_TRANSACTIONS_CLEAN[0] = timestamp()
         background_tasks.add_task(on_ledger, cluster.mirror_gc, pending)
     block_data = {'block_no': block_no, 'block_hash': block_hash, 'transactions_count': len(final_hexes),
                   'timestamp': timestamp(), 'difficulty': difficulty, 'last_block': last_block,
-                  'pending_transactions': pending[:10], 'pending_transactions_hashes': [sha256(t) for t in pending],
+                  'pending_transactions': pending[:10], 'pending_transactions_hashes': [hashes_p[k] for k in order],
                   'merkle_root': get_transactions_merkle_tree(pending[:10])}
     background_tasks.add_task(broadcast_new_block, block_data)
     if sender:
