@@ -915,6 +915,17 @@ async def get_block(request: Request, block: str, full_transactions: bool = Fals
     block_hash, block_info = await _resolve_block(block)
     if not block_info:
         return {'ok': False, 'error': 'Block not found'}
+    if not full_transactions:
+        # a full block is ~8k hex strings (4 MB of JSON): they need no escaping, so the list is joined
+        # into the document directly instead of walked by the generic encoder on the event loop
+        txs = await db.get_block_transactions(block_hash, hex_only=True)
+        if all(t.isalnum() for t in txs):
+            mark = '"@@upow-txs@@"'
+            head = json.dumps(jsonable_encoder({'ok': True, 'result': {
+                'block': block_info, 'transactions': '@@upow-txs@@', 'full_transactions': None}}),
+                ensure_ascii=False, allow_nan=False, separators=(',', ':'))
+            body = head.replace(mark, '[' + ','.join(f'"{t}"' for t in txs) + ']', 1)
+            return Response(content=body, media_type='application/json')
     return {'ok': True, 'result': {
         'block': block_info,
         'transactions': await db.get_block_transactions(block_hash, hex_only=True) if not full_transactions else None,
