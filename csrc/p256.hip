@@ -23,6 +23,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "dev_pool.h"
@@ -117,7 +118,7 @@ UPOW_HD uint8_t verify_prologue(const VerifyItem& it, aff& q, fe& r, fe& u1, fe&
     if (fe_is_zero(s) || (fe_geq(s, n) && !fe_eq(s, n))) return 3;
     if (fe_eq(s, n)) return 0;  // s has no inverse mod n
     const fe e = sc_reduce(fe_from_be(it.e));
-    const fe w_m = sc_inv_mont(sc_to_mont(s));  // s^-1 * R
+    const fe w_m = sc_inv_bgcd_mont(s);         // s^-1 * R
     u1 = sc_mont_mul(e, w_m);                   // e * s^-1
     u2 = sc_mont_mul(sc_reduce(r), w_m);        // r * s^-1
     return 255;                                 // continue
@@ -156,6 +157,222 @@ static uint8_t verify_one_host(const VerifyItem& it, const aff* gtab) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// four lanes per signature (latency path for one block)
+// ------------------------------------------------------------------------------------------------
+// One 2 MB block is ~8,300 signatures = 130 waves at one signature per lane: 130 of the chip's 1,024
+// SIMDs are busy and the launch takes as long as one wave's serial chain (~3 ms). A wave64 VALU op
+// costs its four passes whatever the exec mask (profiles/p256_latency_ab.txt: 16 signatures per wave
+// run no faster than 64), so the only way to cut that latency is to split each signature's chain over
+// more lanes. Here a lane quad (4k .. 4k+3) owns one signature: all four lanes keep the whole point
+// state (redundantly) and the field products of the point formulas are scheduled in "steps" of up to
+// four independent products, one per lane; DPP quad_perm broadcasts hand every lane the others'
+// results (8 v_mov_dpp per product). Adds/subs stay redundant: they are cheap next to a 256x256-bit
+// product. Points are in XYZZ coordinates (x = X/ZZ, y = Y/ZZZ), whose formulas are shallow:
+//   doubling (a = -3, dbl-2008-s-1)            9 products, depth 3  -> 3 steps
+//   addition (add-2008-s)                      14 products, depth 4 -> 4 steps
+// (Jacobian doubling is 8 products but depth 4: 4 steps however many lanes.) A 4-bit window (4
+// doublings + 1 addition) is 16 steps instead of 48 serial products. The window table k*Q (k = 1..15)
+// is built the same way (3 + 13 x 4 steps). u1*G (32 fixed-base byte windows) splits by quarters:
+// each lane accumulates 8 windows on its own (Jacobian mixed adds), converts to XYZZ, and the four
+// partial points are broadcast and added. s^-1 runs redundantly on all four lanes (binary Euclid).
+// Waves go four to a workgroup so they land on four different SIMDs of a CU (single-wave workgroups
+// double up on one SIMD once there are more waves than CUs: profiles/p256_latency_ab.txt).
+//
+// The schedule is written once over a policy type: QuadDev broadcasts through DPP on the GPU;
+// QuadHost (one host thread) computes every product of a step itself, which lets the CPU tests check
+// the formulas and the step schedule bit for bit against the reference verifier.
+struct xz { fe x, y, zz, zzz; };  // XYZZ point; zz == 0 <=> infinity
+static_assert(sizeof(xz) == 128, "xz layout");
+
+struct QuadHost {
+    UPOW_HD void mul4(const fe& a0, const fe& b0, const fe& a1, const fe& b1, const fe& a2, const fe& b2,
+                      const fe& a3, const fe& b3, fe& r0, fe& r1, fe& r2, fe& r3) const {
+        const fe m0 = fe_mul(a0, b0), m1 = fe_mul(a1, b1), m2 = fe_mul(a2, b2), m3 = fe_mul(a3, b3);
+        r0 = m0;
+        r1 = m1;
+        r2 = m2;
+        r3 = m3;
+    }
+};
+
+template <int K>
+__device__ __forceinline__ fe fe_quad_bcast(const fe& a) {  // every lane of the quad gets lane K's value
+    fe r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = uint32_t(__builtin_amdgcn_mov_dpp(int(a.v[i]), K * 0x55, 0xF, 0xF, true));
+    return r;
+}
+struct QuadDev {
+    bool is1, is2, is3;  // this lane's role in its quad (lane & 3)
+    __device__ __forceinline__ fe pick(const fe& a0, const fe& a1, const fe& a2, const fe& a3) const {
+        fe r;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            uint32_t t = a0.v[i];
+            t = is1 ? a1.v[i] : t;
+            t = is2 ? a2.v[i] : t;
+            r.v[i] = is3 ? a3.v[i] : t;
+        }
+        return r;
+    }
+    __device__ __forceinline__ void mul4(const fe& a0, const fe& b0, const fe& a1, const fe& b1, const fe& a2,
+                                         const fe& b2, const fe& a3, const fe& b3, fe& r0, fe& r1, fe& r2,
+                                         fe& r3) const {
+        const fe m = fe_mul(pick(a0, a1, a2, a3), pick(b0, b1, b2, b3));
+        r0 = fe_quad_bcast<0>(m);
+        r1 = fe_quad_bcast<1>(m);
+        r2 = fe_quad_bcast<2>(m);
+        r3 = fe_quad_bcast<3>(m);
+    }
+};
+
+// fewer products per step: the spare lanes repeat the last product (its broadcast is dead code)
+template <class P>
+UPOW_HD void mul3(const P& pp, const fe& a0, const fe& b0, const fe& a1, const fe& b1, const fe& a2, const fe& b2,
+                  fe& r0, fe& r1, fe& r2) {
+    fe d;
+    pp.mul4(a0, b0, a1, b1, a2, b2, a2, b2, r0, r1, r2, d);
+}
+template <class P>
+UPOW_HD void mul2(const P& pp, const fe& a0, const fe& b0, const fe& a1, const fe& b1, fe& r0, fe& r1) {
+    fe d0, d1;
+    pp.mul4(a0, b0, a1, b1, a1, b1, a1, b1, r0, r1, d0, d1);
+}
+template <class P>
+UPOW_HD void mul1(const P& pp, const fe& a0, const fe& b0, fe& r0) {
+    fe d0, d1, d2;
+    pp.mul4(a0, b0, a0, b0, a0, b0, a0, b0, r0, d0, d1, d2);
+}
+
+UPOW_HD fe fe_x3(const fe& a) { return fe_add(fe_add(a, a), a); }
+
+// dbl-2008-s-1 with a = -3: M = 3 X^2 - 3 ZZ^2 = 3 (X - ZZ)(X + ZZ). Infinity (ZZ = 0) stays infinity.
+template <class P>
+UPOW_HD void dbl4(const P& pp, xz& p) {
+    const fe u = fe_add(p.y, p.y);
+    fe v, m0;
+    mul2(pp, u, u, fe_sub(p.x, p.zz), fe_add(p.x, p.zz), v, m0);
+    const fe m = fe_x3(m0);
+    fe w, s, mm, zz3;
+    pp.mul4(u, v, p.x, v, m, m, v, p.zz, w, s, mm, zz3);
+    const fe x3 = fe_sub(mm, fe_add(s, s));
+    fe ya, wy, zzz3;
+    mul3(pp, m, fe_sub(s, x3), w, p.y, w, p.zzz, ya, wy, zzz3);
+    p.x = x3;
+    p.y = fe_sub(ya, wy);
+    p.zz = zz3;
+    p.zzz = zzz3;
+}
+
+// add-2008-s with the reference verifier's special cases (infinity, P == Q, P == -Q)
+template <class P>
+UPOW_HD void add4(const P& pp, xz& p, const xz& q) {
+    if (fe_is_zero(q.zz)) return;
+    if (fe_is_zero(p.zz)) { p = q; return; }
+    fe u1, u2, s1, s2;
+    pp.mul4(p.x, q.zz, q.x, p.zz, p.y, q.zzz, q.y, p.zzz, u1, u2, s1, s2);
+    const fe ph = fe_sub(u2, u1), r = fe_sub(s2, s1);
+    if (fe_is_zero(ph)) {
+        if (fe_is_zero(r)) dbl4(pp, p);
+        else p.zz = p.zzz = fe_zero();
+        return;
+    }
+    fe pp2, rr, zz12, zzz12;
+    pp.mul4(ph, ph, r, r, p.zz, q.zz, p.zzz, q.zzz, pp2, rr, zz12, zzz12);
+    fe ppp, qq, zz3;
+    mul3(pp, ph, pp2, u1, pp2, zz12, pp2, ppp, qq, zz3);
+    const fe x3 = fe_sub(fe_sub(rr, ppp), fe_add(qq, qq));
+    fe ya, s1p, zzz3;
+    mul3(pp, r, fe_sub(qq, x3), s1, ppp, zzz12, ppp, ya, s1p, zzz3);
+    p.x = x3;
+    p.y = fe_sub(ya, s1p);
+    p.zz = zz3;
+    p.zzz = zzz3;
+}
+
+// u1*G over the byte windows [8*quarter, 8*quarter + 8) (one lane's share), Jacobian mixed adds
+UPOW_HD jac mul_g_quarter(const fe& k, const aff* tab, int quarter) {
+    jac acc = jac_inf();
+    uint32_t lo = k.v[0], hi = k.v[1];  // this quarter's 64 bits, consumed a byte at a time
+#pragma unroll
+    for (int l = 1; l < 4; ++l) {
+        lo = quarter == l ? k.v[2 * l] : lo;
+        hi = quarter == l ? k.v[2 * l + 1] : hi;
+    }
+    const aff* t = tab + quarter * 8 * kGEnt;
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t b = lo & 0xffu;
+        lo = (lo >> 8) | (hi << 24);
+        hi >>= 8;
+        if (b) acc = jac_madd(acc, t[j * kGEnt + b]);
+    }
+    return acc;
+}
+
+// Jacobian (X, Y, Z) -> XYZZ (X, Y, Z^2, Z^3): the same affine point, one lane on its own
+UPOW_HD xz jac_to_xz(const jac& p) {
+    const fe zz = fe_sqr(p.z);
+    return xz{p.x, p.y, zz, fe_mul(zz, p.z)};
+}
+
+// Shared verify body. `tab` holds this signature's 16 window entries (global scratch on the GPU, a
+// local array on the host); `gpart(K)` yields quarter K of u1*G in XYZZ form (on the GPU: lane K's own
+// quarter, broadcast). On the GPU every lane of the quad stores the (identical)
+// entries, so each later table read is of the lane's own store.
+template <class P, class GPart>
+UPOW_HD uint8_t verify_quad_core(const P& pp, const aff& q, const fe& r, const fe& u2, xz* tab, GPart gpart) {
+    const fe one = fe_one();
+    const xz t1{q.x, q.y, one, one};
+    xz t = t1;
+    tab[1] = t;
+    dbl4(pp, t);
+    tab[2] = t;
+    for (int k = 3; k < 16; ++k) {
+        add4(pp, t, t1);
+        tab[k] = t;
+    }
+    // u2*Q: 64 fixed 4-bit windows from the top; the entry is loaded before the window's doublings
+    xz acc{one, one, fe_zero(), fe_zero()};
+    fe k2 = u2;  // windows taken from the top nibble, then shifted out (no dynamic register indexing)
+    for (int w = 63; w >= 0; --w) {
+        const uint32_t nib = k2.v[7] >> 28;
+#pragma unroll
+        for (int l = 7; l > 0; --l) k2.v[l] = (k2.v[l] << 4) | (k2.v[l - 1] >> 28);
+        k2.v[0] <<= 4;
+        xz e;
+        if (nib) e = tab[nib];
+        if (w != 63) {
+            dbl4(pp, acc);
+            dbl4(pp, acc);
+            dbl4(pp, acc);
+            dbl4(pp, acc);
+        }
+        if (nib) add4(pp, acc, e);
+    }
+    // + u1*G, added a quarter at a time
+    add4(pp, acc, gpart(std::integral_constant<int, 0>{}));
+    add4(pp, acc, gpart(std::integral_constant<int, 1>{}));
+    add4(pp, acc, gpart(std::integral_constant<int, 2>{}));
+    add4(pp, acc, gpart(std::integral_constant<int, 3>{}));
+    // x(R) == r  <=>  X == r ZZ (and (r + n) ZZ when r + n < p)
+    if (fe_is_zero(acc.zz)) return 0;
+    if (fe_eq(fe_mul(r, acc.zz), acc.x)) return 1;
+    fe rn;
+    const uint32_t c = raw_add(rn, r, fe_const_n());
+    if (!c && !fe_geq(rn, fe_const_p()) && fe_eq(fe_mul(rn, acc.zz), acc.x)) return 1;
+    return 0;
+}
+
+static uint8_t verify_one_host_quad(const VerifyItem& it, const aff* gtab) {
+    aff q;
+    fe r, u1, u2;
+    const uint8_t pro = verify_prologue(it, q, r, u1, u2);
+    if (pro != 255) return pro;
+    xz tab[16];
+    return verify_quad_core(QuadHost{}, q, r, u2, tab, [&](auto K) { return jac_to_xz(mul_g_quarter(u1, gtab, K)); });
+}
+
+// ------------------------------------------------------------------------------------------------
 // device kernels
 // ------------------------------------------------------------------------------------------------
 // Per-lane window table {1..15}Q lives in global scratch. SOA = false: [lane][k] Jacobian entries
@@ -187,12 +404,15 @@ __device__ __forceinline__ jac tab_load(const jac* scratch, int64_t n, int64_t i
     return scratch[i * 16 + k];
 }
 
-template <int MIN_WAVES, bool SOA>
-__global__ __launch_bounds__(64, MIN_WAVES) void p256_verify_kernel(const VerifyItem* __restrict__ items, int64_t n,
+template <int MIN_WAVES, bool SOA, int WPB = 1>
+__global__ __launch_bounds__(64 * WPB, MIN_WAVES) void p256_verify_kernel(const VerifyItem* __restrict__ items, int64_t n,
                                                           const aff* __restrict__ gtab, jac* __restrict__ scratch,
-                                                          uint8_t* __restrict__ status) {
-    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+                                                          uint8_t* __restrict__ status, int spw) {
+    // spw = signatures per 64-lane wave (lanes >= spw idle; A/B of partially filled waves);
+    // WPB = waves per workgroup (a workgroup's waves are spread over the CU's SIMDs)
+    const int lane = int(threadIdx.x) & 63;
+    const int64_t i = (int64_t(blockIdx.x) * WPB + (threadIdx.x >> 6)) * spw + lane;
+    if (lane >= spw || i >= n) return;
     const VerifyItem it = items[i];
     aff q;
     fe r, u1, u2;
@@ -212,6 +432,33 @@ __global__ __launch_bounds__(64, MIN_WAVES) void p256_verify_kernel(const Verify
     }
     const jac R = jac_add(mul_g(u1, gtab), acc);
     status[i] = verify_epilogue(R, r);
+}
+
+// Four lanes per signature, four waves per workgroup (16 signatures per wave). Exits are quad-uniform.
+static constexpr int64_t kQuadMaxBatch = 32 * 1024;  // 2,048 waves of 16 signatures: two per SIMD
+__global__ __launch_bounds__(256, 1) void p256_verify_quad_kernel(const VerifyItem* __restrict__ items, int64_t n,
+                                                                   const aff* __restrict__ gtab,
+                                                                   xz* __restrict__ scratch,
+                                                                   uint8_t* __restrict__ status) {
+    const int lane = int(threadIdx.x) & 63;
+    const int64_t i = (int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 16 + (lane >> 2);
+    if (i >= n) return;
+    const int role = lane & 3;
+    const QuadDev pp{role == 1, role == 2, role == 3};
+    const VerifyItem it = items[i];
+    aff q;
+    fe r, u1, u2;
+    const uint8_t pro = verify_prologue(it, q, r, u1, u2);
+    if (pro != 255) {
+        if (role == 0) status[i] = pro;
+        return;
+    }
+    const xz mine = jac_to_xz(mul_g_quarter(u1, gtab, role));  // this lane's quarter of u1*G
+    const uint8_t st = verify_quad_core(pp, q, r, u2, scratch + i * 16, [&](auto K) {
+        constexpr int k = decltype(K)::value;
+        return xz{fe_quad_bcast<k>(mine.x), fe_quad_bcast<k>(mine.y), fe_quad_bcast<k>(mine.zz), fe_quad_bcast<k>(mine.zzz)};
+    });
+    if (role == 0) status[i] = st;
 }
 
 // item: 33-byte compressed address [spec | x LE]; out: x LE | y LE (64 B) and ok flag
@@ -267,14 +514,17 @@ std::vector<uint8_t> p256_verify_host(const uint8_t* items, int64_t n, int threa
     std::vector<uint8_t> st(static_cast<size_t>(n));
     const aff* tab = g_table().data();
     const VerifyItem* it = reinterpret_cast<const VerifyItem*>(items);
-    static const bool legacy = [] {
-        const char* v = std::getenv("UPOW_P256_HOST32");
-        return v && v[0] == '1';
-    }();
+    // UPOW_P256_HOST32 (read per call): '1' = the 32-bit-limb single-lane code the one-lane GPU kernels
+    // run; 'quad' = the four-lane step schedule of the quad kernel played by one host thread (CPU tests
+    // of both GPU code paths); unset = the 64-bit-limb host verifier.
+    const char* h32 = std::getenv("UPOW_P256_HOST32");
+    const int mode = !h32 ? 0 : (std::strcmp(h32, "quad") == 0 ? 2 : (h32[0] == '1' ? 1 : 0));
     threads = int(std::max<int64_t>(1, std::min<int64_t>(threads, n)));
     auto work = [&](int t) {
-        if (legacy)  // UPOW_P256_HOST32=1: the 32-bit-limb field code the GPU kernel uses
+        if (mode == 1)
             for (int64_t i = t; i < n; i += threads) st[i] = verify_one_host(it[i], tab);
+        else if (mode == 2)
+            for (int64_t i = t; i < n; i += threads) st[i] = verify_one_host_quad(it[i], tab);
         else
             for (int64_t i = t; i < n; i += threads)
                 st[i] = p256_verify_one_host64(reinterpret_cast<const uint8_t*>(&it[i]));
@@ -294,29 +544,49 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
     if (n == 0) return st;
     const aff* d_tab = device_g_table();
     PooledBuf<VerifyItem> b_items{size_t(n)};
-    PooledBuf<jac> b_scratch(size_t(16) * size_t(n));
     PooledBuf<uint8_t> b_st{size_t(n)};
     VerifyItem* d_items = b_items.p;
-    jac* d_scratch = b_scratch.p;
     uint8_t* d_st = b_st.p;
     node_h2d(d_items, items, sizeof(VerifyItem) * n, "h2d items");
+    // Variant (UPOW_P256_VARIANT, read per call): unset/'a' = auto, '4' = four lanes per signature,
+    // '0'..'3' = one lane per signature (below). Auto takes the quad kernel up to 32k signatures
+    // (2,048 waves, two per SIMD): there it cuts the latency of block-sized batches; past that the
+    // chip is full either way and one lane per signature does half the total work.
+    const char* var = std::getenv("UPOW_P256_VARIANT");
+    char v = var && var[0] ? var[0] : 'a';
+    if (v == 'a') v = n <= kQuadMaxBatch ? '4' : '1';
+    if (v == '4') {
+        PooledBuf<xz> b_tab(size_t(16) * size_t(n));
+        const int64_t waves = (n + 15) / 16;
+        hipLaunchKernelGGL(p256_verify_quad_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, node_stream(), d_items, n,
+                           d_tab, b_tab.p, d_st);
+        hck(hipGetLastError(), "p256_verify_quad_kernel launch");
+        node_d2h(st.data(), d_st, size_t(n), "d2h status");
+        return st;
+    }
+    PooledBuf<jac> b_scratch(size_t(16) * size_t(n));
+    jac* d_scratch = b_scratch.p;
     const int block = 64;
-    const int grid = int((n + block - 1) / block);
-    // Default (variant 1): __launch_bounds__(64, 4) -> 4 waves/SIMD at 128 VGPRs (a few spills), 7-9 %
-    // faster than the compiler's 142-VGPR / 3-wave choice (variant 0) in the A/B runs of
+    const char* spw_env = std::getenv("UPOW_P256_SPW");
+    int spw = spw_env ? std::atoi(spw_env) : 64;
+    if (spw < 1 || spw > 64) spw = 64;
+    const int grid = int((n + spw - 1) / spw);
+    // Variant 1 (the one-lane default): __launch_bounds__(64, 4) -> 4 waves/SIMD at 128 VGPRs (a few
+    // spills), 7-9 % faster than the compiler's 142-VGPR / 3-wave choice (variant 0) in the A/B runs of
     // scripts/p256_throughput.py (profiles/p256_variants_ab.txt). Variant 2: dword-major (SoA)
     // window tables, slower (the gathers were not the bottleneck).
-    const char* var = std::getenv("UPOW_P256_VARIANT");
-    const char v = var ? var[0] : '1';
     if (v == '0')
         hipLaunchKernelGGL((p256_verify_kernel<1, false>), dim3(grid), dim3(block), 0, node_stream(), d_items, n, d_tab, d_scratch,
-                           d_st);
+                           d_st, spw);
     else if (v == '2')
         hipLaunchKernelGGL((p256_verify_kernel<1, true>), dim3(grid), dim3(block), 0, node_stream(), d_items, n, d_tab, d_scratch,
-                           d_st);
+                           d_st, spw);
+    else if (v == '3')  // 4 waves per workgroup
+        hipLaunchKernelGGL((p256_verify_kernel<4, false, 4>), dim3((grid + 3) / 4), dim3(256), 0, node_stream(), d_items, n, d_tab,
+                           d_scratch, d_st, spw);
     else
         hipLaunchKernelGGL((p256_verify_kernel<4, false>), dim3(grid), dim3(block), 0, node_stream(), d_items, n, d_tab, d_scratch,
-                           d_st);
+                           d_st, spw);
     hck(hipGetLastError(), "p256_verify_kernel launch");
     node_d2h(st.data(), d_st, size_t(n), "d2h status");
     return st;

@@ -367,6 +367,49 @@ UPOW_HD fe sc_inv_mont(const fe& a_m) {
     return t;
 }
 
+// a^-1 * R mod n (the Montgomery form of the inverse, ready for sc_mont_mul) for a in [1, n), by the
+// binary extended Euclid: u = x*a, v = y*a (mod n) hold throughout; every pass makes u even (subtracting
+// the smaller of u, v from the larger when u is odd) and halves u and x, so log2(u*v) drops by at least
+// one bit per pass and u reaches 0 after at most 512 passes (~360 for random a), leaving v = gcd = 1 and
+// y = a^-1 (times R, which x starts at). Variable time, which is fine for verification (public data);
+// the GPU wave runs until its slowest lane is done (~385 passes). Each pass is ~170 full-rate VALU ops
+// with no multiplies: about a third of the VALU issue slots of the Fermat chain a^(n-2) (sc_inv_mont,
+// ~300 Montgomery products of 128 quarter-rate v_mad_u64_u32 each), which sign() still uses.
+UPOW_HD fe sc_inv_bgcd_mont(const fe& a) {
+    const fe n = fe_const_n();
+    fe u = a, v = n, x{P256_RN}, y = fe_zero();
+    while (!fe_is_zero(u)) {
+        const bool odd = u.v[0] & 1u;
+        fe d1, d2, dx, t;
+        const bool lt = raw_sub(d1, u, v) != 0;  // u < v
+        raw_sub(d2, v, u);
+        const uint32_t bx = raw_sub(dx, x, y);   // x - y mod n
+        raw_add(t, dx, n);
+        dx = fe_select(bx != 0, t, dx);
+        fe ndx;                                   // y - x mod n = n - (x - y) unless zero
+        raw_sub(ndx, n, dx);
+        ndx = fe_select(fe_is_zero(dx), dx, ndx);
+        const bool sw = odd && lt;
+        const fe nu = fe_select(odd, fe_select(lt, d2, d1), u);
+        const fe nx = fe_select(odd, fe_select(lt, ndx, dx), x);
+        v = fe_select(sw, u, v);
+        y = fe_select(sw, x, y);
+        // u = nu / 2 (nu is even); x = nx / 2 mod n
+#pragma unroll
+        for (int i = 0; i < 7; ++i) u.v[i] = (nu.v[i] >> 1) | (nu.v[i + 1] << 31);
+        u.v[7] = nu.v[7] >> 1;
+        const uint32_t mask = 0u - (nx.v[0] & 1u);
+        fe nm, xs;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) nm.v[i] = n.v[i] & mask;
+        const uint32_t c = raw_add(xs, nx, nm);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) x.v[i] = (xs.v[i] >> 1) | (xs.v[i + 1] << 31);
+        x.v[7] = (xs.v[7] >> 1) | (c << 31);
+    }
+    return y;
+}
+
 // ------------------------------------------------------------------------------------------------
 // points
 // ------------------------------------------------------------------------------------------------

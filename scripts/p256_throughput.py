@@ -22,7 +22,7 @@ for i in range(8300):
 base = b''.join(recs)
 out = {}
 import os
-for var in ('0', '1', '2'):
+for var in ('0', '1', '2', '4'):
     os.environ['UPOW_P256_VARIANT'] = var
     buf = base * 16
     op.verify_records(buf[:160 * 512], device='gpu')
@@ -33,7 +33,7 @@ for var in ('0', '1', '2'):
     t = time.perf_counter()
     st = op.verify_records(base, device='gpu')
     out[f'variant{var}_gpu_8300'] = round(8300 / (time.perf_counter() - t), 1)
-os.environ['UPOW_P256_VARIANT'] = '1'  # the default
+os.environ['UPOW_P256_VARIANT'] = 'a'  # the default: pair kernel up to 32k signatures, then one lane
 for n in (8300, 8300 * 4, 8300 * 16, 8300 * 64):  # 64 blocks = 8,300 waves: saturates the chip
     buf = base * (n // 8300)
     op.verify_records(buf[:160 * 512], device='gpu')

@@ -110,13 +110,46 @@ def test_decompress_host(native):
     assert op.decompress(addrs, device='cpu') == want
 
 
+def _chosen_s_batch():
+    """Valid signatures for chosen s (edge values of the binary-Euclid s^-1): pick k, R = kG, e, s and
+    solve for the key d = (s k - e) / r, so each record verifies; every one is followed by a copy with
+    s + 1 (or s - 1 at the top), which must not."""
+    rng = random.Random(41)
+    svals = [1, 2, 3, 5, o.N - 1, o.N - 2, (o.N + 1) // 2, 1 << 255, (1 << 128) + 1, 0xffffffff]
+    svals += [rng.randrange(1, o.N) for _ in range(6)]
+    recs, exp = [], []
+    for s in svals:
+        k = rng.randrange(1, o.N)
+        r = o.get_public_key(k).x % o.N
+        e = rng.randbytes(32)
+        d = (s * k - int.from_bytes(e, 'big')) * pow(r, -1, o.N) % o.N
+        q = o.get_public_key(d)
+        assert o.verify_digest(r, s, int.from_bytes(e, 'big'), q.x, q.y)
+        s2 = s + 1 if s + 1 < o.N else s - 1
+        recs += [op.record(q, (r, s), e), op.record(q, (r, s2), e)]
+        exp += [1, 0]
+    return b''.join(recs), np.array(exp, dtype=np.uint8)
+
+
+@pytest.mark.parametrize('mode', ['1', 'quad'])  # one-lane 32-bit GPU code; four-lane step schedule
+def test_host_gpu_code_paths(native, mode, monkeypatch):
+    """The GPU kernels' field/point code run on the host: the one-lane 32-bit path and the quad
+    kernel's four-product step schedule in XYZZ coordinates (QuadHost), both with the binary-Euclid
+    s^-1."""
+    monkeypatch.setenv('UPOW_P256_HOST32', mode)
+    for recs, exp in (_batch(140, 5), _high_x_batch(4, 33), _chosen_s_batch()):
+        assert (op.verify_records(recs, device='cpu', threads=4) == exp).all()
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize('variant', ['0', '1', '2'])  # default, 4 waves/SIMD, SoA window tables
+@pytest.mark.parametrize('variant', ['0', '1', '2', '4', 'a'])  # 3 waves/SIMD, 4 waves/SIMD, SoA tables, quad, auto
 def test_gpu_batch_verify_matches_host(gpu, variant, monkeypatch):
     monkeypatch.setenv('UPOW_P256_VARIANT', variant)
     recs, exp = _batch(700, 5)
     st_gpu = op.verify_records(recs, device='gpu')
     assert (st_gpu == exp).all()
+    recs, exp = _chosen_s_batch()
+    assert (op.verify_records(recs, device='gpu') == exp).all()
 
 
 @pytest.mark.gpu
@@ -166,7 +199,7 @@ def test_high_x_r_plus_n_host(native):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('variant', ['0', '1', '2'])
+@pytest.mark.parametrize('variant', ['0', '1', '2', '4'])
 def test_high_x_r_plus_n_gpu(gpu, variant, monkeypatch):
     monkeypatch.setenv('UPOW_P256_VARIANT', variant)
     recs, exp = _high_x_batch(40, 32)
