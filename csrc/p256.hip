@@ -4,14 +4,14 @@
 // signature at a time from upow/upow_transactions/transaction_input.py:84-120,
 // upow/upow_transactions/transaction.py:148-180,484-497 and upow/helpers.py:58-62,135-144.
 //
-// GPU design (gfx950, one signature per lane):
+// GPU design (gfx950): batches up to 32k signatures (a block) take four lanes per signature (the quad
+// kernel, see "four lanes per signature" below); larger batches one signature per lane:
 //  * u1*G uses a fixed-base byte-window table T[j][b] = b*256^j*G (32 x 255 affine points, 522 KB,
 //    L2/Infinity-Cache resident) -> 32 mixed additions and no doublings;
-//  * u2*Q uses a 4-bit fixed window over a per-lane table {1..15}Q kept in global scratch
-//    ([lane][k] 96-byte Jacobian entries) because 1.4 KB per lane does not fit LDS at useful
-//    occupancy -> 256 doublings + 64 additions;
+//  * u2*Q uses a 4-bit fixed window over a per-signature table {1..15}Q kept in global scratch
+//    (1.4-2 KB per signature does not fit LDS at useful occupancy) -> 256 doublings + 64 additions;
 //  * no field inversion: x(R) == r is tested as X == r*Z^2 (and (r+n)*Z^2 when r+n < p);
-//  * s^-1 mod n by a Montgomery-domain fixed-window exponentiation;
+//  * s^-1 mod n by a binary extended Euclid (p256_field.h sc_inv_bgcd_mont);
 //  * status per item: 1 valid, 0 invalid, 2 public key not on curve, 3 r/s out of [1, n]
 //    (fastecdsa raises for 2/3; the Python layer turns them into EcdsaError).
 #include <hip/hip_runtime.h>
