@@ -16,6 +16,7 @@ from __future__ import annotations
 import asyncio
 import hashlib
 import json
+import os
 import random
 import time
 from decimal import Decimal
@@ -221,6 +222,10 @@ async def _run(args, ctx, device, utxo_backend):
     stages = []
     paths = set()
     total_txs = 0
+    prof = None
+    if os.environ.get('UPOW_BENCH_PROFILE'):
+        import cProfile
+        prof = cProfile.Profile()
     from_mempool = getattr(args, 'from_mempool', False)
     untimed = 0.0  # mempool admission of the next block's txs happens inside the wall-clock window
     for b, txs_hex in enumerate(blocks):
@@ -233,6 +238,8 @@ async def _run(args, ctx, device, utxo_backend):
         if b == args.warmup:
             ctx.barrier()
             ctx.synchronize()
+            if prof is not None:
+                prof.enable()
             t_start = time.perf_counter()
             unix_start = time.time()
         t0 = time.perf_counter()
@@ -267,6 +274,16 @@ async def _run(args, ctx, device, utxo_backend):
     ctx.synchronize()
     ctx.barrier()
     wall = time.perf_counter() - t_start - untimed
+    if prof is not None:  # UPOW_BENCH_PROFILE=PATH: cProfile of the timed blocks only (text report)
+        import io
+        import pstats
+        prof.disable()
+        out = io.StringIO()
+        st = pstats.Stats(prof, stream=out)
+        st.sort_stats('cumulative').print_stats(70)
+        st.sort_stats('tottime').print_stats(40)
+        with open(os.environ['UPOW_BENCH_PROFILE'], 'w') as f:
+            f.write(out.getvalue())
     wall = ctx.allreduce_max_f(wall)
     writer = db.writer.stats() if db.writer is not None else None
     if writer is not None:
