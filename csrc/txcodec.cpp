@@ -434,42 +434,80 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
     if (!all_fast) return d;  // the caller takes the general path; skip building the rest
 
     const size_t NI = static_cast<size_t>(n_in), NO = static_cast<size_t>(n_out), NS = static_cast<size_t>(n_sig);
+    // The merkle root (a sort of the canonical bytes, then one SHA-256 over the txids) runs on its own
+    // thread while the pool fills the flat columns below: both only read `txs`.
+    std::string merkle;
+    std::thread merkle_thread([&] { merkle = merkle_of(txs); });
+    struct Joiner {  // an exception below must not destroy a joinable thread
+        std::thread& t;
+        ~Joiner() {
+            if (t.joinable()) t.join();
+        }
+    } merkle_joiner{merkle_thread};
     std::vector<uint8_t> in_keys(NI * 40, 0), in_type(NI), sigs(NS * 64), txid(N * 32), digest(N * 32),
         out_addr(NO * 64, 0), out_len(NO), out_type(NO);
     std::vector<int32_t> in_sig(NI), in_tx(NI), out_tx(NO);
     std::vector<uint64_t> out_amount(NO);
-    py::list canon_hex = new_list(N);
+    // text arenas: per-row string sizes -> offsets (serial, cheap), then every row copies its own
+    // strings into place in parallel
     Arena addr_arena, addr_json_arena, amount_json_arena;
-    addr_arena.blob.reserve(NO * 45);
-    addr_json_arena.blob.reserve(N * 96);
-    amount_json_arena.blob.reserve(N * 24);
-    for (int64_t i = 0; i < n; ++i) {
-        const DecTx& t = txs[size_t(i)];
-        std::memcpy(&txid[32 * size_t(i)], t.txid, 32);
-        std::memcpy(&digest[32 * size_t(i)], t.digest, 32);
-        size_t k = size_t(in_start[size_t(i)]);
-        for (const DecIn& in : t.ins) {
-            std::memcpy(&in_keys[40 * k], in.txid, 32);
-            const uint32_t idx = in.index, tag = 0xffu;
-            std::memcpy(&in_keys[40 * k + 32], &idx, 4);
-            std::memcpy(&in_keys[40 * k + 36], &tag, 4);
-            in_type[k] = in.type;
-            in_sig[k] = sig_start[size_t(i)] + in.sig;
-            in_tx[k] = int32_t(i);
-            ++k;
+    addr_arena.off.resize(NO + 1);
+    addr_json_arena.off.resize(N + 1);
+    amount_json_arena.off.resize(N + 1);
+    addr_arena.off[0] = addr_json_arena.off[0] = amount_json_arena.off[0] = 0;
+    for (size_t i = 0; i < N; ++i) {
+        const DecTx& t = txs[i];
+        size_t o = size_t(out_start[i]);
+        for (const std::string& a : t.out_addr) {
+            addr_arena.off[o + 1] = addr_arena.off[o] + int64_t(a.size());
+            ++o;
         }
-        std::memcpy(&sigs[64 * size_t(sig_start[size_t(i)])], t.sigs.data(), t.sigs.size());
-        size_t o = size_t(out_start[size_t(i)]);
-        for (size_t j = 0; j < t.outs.size(); ++j, ++o) {
-            std::memcpy(&out_addr[64 * o], t.outs[j].addr, t.outs[j].len);
-            out_len[o] = t.outs[j].len;
-            out_type[o] = t.outs[j].type;
-            out_amount[o] = t.outs[j].amount;
-            out_tx[o] = int32_t(i);
-            addr_arena.add(t.out_addr[j].data(), t.out_addr[j].size());
-        }
-        // the input string is reused when it already is the canonical lowercase hex of the tx
-        if (t.canonical && !t.upper_hex && srcl[size_t(i)] == 2 * t.canon.size()) {
+        addr_json_arena.off[i + 1] = addr_json_arena.off[i] + int64_t(t.out_addr_json.size());
+        amount_json_arena.off[i + 1] = amount_json_arena.off[i] + int64_t(t.out_amount_json.size());
+    }
+    addr_arena.blob.resize(size_t(addr_arena.off[NO]));
+    addr_json_arena.blob.resize(size_t(addr_json_arena.off[N]));
+    amount_json_arena.blob.resize(size_t(amount_json_arena.off[N]));
+    {
+        py::gil_scoped_release rel;
+        parallel_for(n, threads, [&](int64_t ii) {
+            const size_t i = size_t(ii);
+            const DecTx& t = txs[i];
+            std::memcpy(&txid[32 * i], t.txid, 32);
+            std::memcpy(&digest[32 * i], t.digest, 32);
+            size_t k = size_t(in_start[i]);
+            for (const DecIn& in : t.ins) {
+                std::memcpy(&in_keys[40 * k], in.txid, 32);
+                const uint32_t idx = in.index, tag = 0xffu;
+                std::memcpy(&in_keys[40 * k + 32], &idx, 4);
+                std::memcpy(&in_keys[40 * k + 36], &tag, 4);
+                in_type[k] = in.type;
+                in_sig[k] = sig_start[i] + in.sig;
+                in_tx[k] = int32_t(i);
+                ++k;
+            }
+            if (!t.sigs.empty()) std::memcpy(&sigs[64 * size_t(sig_start[i])], t.sigs.data(), t.sigs.size());
+            size_t o = size_t(out_start[i]);
+            for (size_t j = 0; j < t.outs.size(); ++j, ++o) {
+                std::memcpy(&out_addr[64 * o], t.outs[j].addr, t.outs[j].len);
+                out_len[o] = t.outs[j].len;
+                out_type[o] = t.outs[j].type;
+                out_amount[o] = t.outs[j].amount;
+                out_tx[o] = int32_t(i);
+                std::memcpy(&addr_arena.blob[size_t(addr_arena.off[o])], t.out_addr[j].data(), t.out_addr[j].size());
+            }
+            std::memcpy(&addr_json_arena.blob[size_t(addr_json_arena.off[i])], t.out_addr_json.data(),
+                        t.out_addr_json.size());
+            std::memcpy(&amount_json_arena.blob[size_t(amount_json_arena.off[i])], t.out_amount_json.data(),
+                        t.out_amount_json.size());
+        });
+    }
+    // the stored hex column: the input string is reused when it already is the canonical lowercase
+    // hex of the tx (Python objects: with the GIL, on this thread)
+    py::list canon_hex = new_list(N);
+    for (size_t i = 0; i < N; ++i) {
+        const DecTx& t = txs[i];
+        if (t.canonical && !t.upper_hex && srcl[i] == 2 * t.canon.size()) {
             PyObject* obj = PyList_GET_ITEM(hexes.ptr(), Py_ssize_t(i));
             Py_INCREF(obj);
             PyList_SET_ITEM(canon_hex.ptr(), Py_ssize_t(i), obj);
@@ -477,8 +515,6 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
             const std::string h = to_hex(t.canon.data(), t.canon.size());
             PyList_SET_ITEM(canon_hex.ptr(), Py_ssize_t(i), ascii_str(h.data(), h.size()));
         }
-        addr_json_arena.add(t.out_addr_json.data(), t.out_addr_json.size());
-        amount_json_arena.add(t.out_amount_json.data(), t.out_amount_json.size());
     }
     d["in_keys"] = as_bytes(in_keys);
     d["in_type"] = as_bytes(in_type);
@@ -497,7 +533,11 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
     d["out_addr_json"] = addr_json_arena.py();
     d["out_amount_json"] = amount_json_arena.py();
     auto t2 = std::chrono::steady_clock::now();
-    d["merkle"] = merkle_of(txs);
+    {
+        py::gil_scoped_release rel;
+        merkle_thread.join();
+    }
+    d["merkle"] = merkle;
     {
         // ~8 heap blocks per tx were allocated by the pool's threads: release them there too (a
         // serial free of ~10^5 blocks from foreign malloc arenas costs ~10 ms on the main thread)
@@ -507,8 +547,8 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
     if (prof) {
         auto t3 = std::chrono::steady_clock::now();
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        std::fprintf(stderr, "[txcodec] decode %.2f ms, python objects %.2f ms, merkle %.2f ms\n", ms(t0, t1),
-                     ms(t1, t2), ms(t2, t3));
+        std::fprintf(stderr, "[txcodec] decode %.2f ms, columns + python objects %.2f ms, merkle wait + free %.2f ms\n",
+                     ms(t0, t1), ms(t1, t2), ms(t2, t3));
     }
     return d;
 }
