@@ -107,14 +107,14 @@ def bench_verify(args, ctx):
 
 
 def _verify_side_metrics(args, ctx) -> dict:
-    """BASELINE metric 2 next to the hashrate: ``steps`` timed 2 MB blocks (+1 warmup) through the
+    """BASELINE metric 2 next to the hashrate: ``--verify-steps`` timed 2 MB blocks (+2 warmup) through the
     native push_block path on this rank's GPU, file-backed ledger in a temporary directory."""
     import shutil
     import tempfile
     from upow_amd.bench_verify import run_verify_bench
     tmp = tempfile.mkdtemp(prefix='upow_bench_verify_')
     try:
-        v = argparse.Namespace(**{**vars(args), 'steps': args.verify_steps, 'warmup': 1, 'ledger': tmp,
+        v = argparse.Namespace(**{**vars(args), 'steps': args.verify_steps, 'warmup': 2, 'ledger': tmp,
                                   'object_path': False, 'from_mempool': False, 'governance': False})
         r = run_verify_bench(v, ctx)
     finally:
@@ -122,7 +122,7 @@ def _verify_side_metrics(args, ctx) -> dict:
     return {'verify_tx_per_s': r['value'], 'verify_ms_per_block': r['ms_per_step'],
             'verify_commit_latency_ms': r['commit_latency_ms'], 'validate_tx_per_s': r['validate_tx_per_s'],
             'ecdsa_sig_per_s': r['ecdsa_sig_per_s'],
-            'verify_config': {'metric': r['metric'], 'unit': r['unit'], 'steps': args.verify_steps, 'warmup': 1,
+            'verify_config': {'metric': r['metric'], 'unit': r['unit'], 'steps': args.verify_steps, 'warmup': 2,
                               'txs_per_block': r['config']['seq_len'], 'ledger': r['config']['ledger'],
                               'block_path': r['config']['block_path'], 'scaling': 'weak',
                               'data': r['data']}}
@@ -144,7 +144,7 @@ def main(argv=None):
                     help='verify mode: block txs are in the mempool and pushed as hashes (the miner path)')
     ap.add_argument('--governance', action='store_true',
                     help='verify mode: seed 12 inodes, 200 validators, 5,000 delegates with ballots before the blocks')
-    ap.add_argument('--verify-steps', type=int, default=4,
+    ap.add_argument('--verify-steps', type=int, default=10,
                     help='mine mode: timed 2 MB blocks of the tx-verify side measurement (0: skip; GPU only)')
     args = ap.parse_args(argv)
 

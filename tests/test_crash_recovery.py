@@ -178,9 +178,10 @@ def test_single_utxo_file_ledger_is_split_on_open(tmp_path):
         got = sorted(tuple(r) for r in db._q('SELECT rowid, tx_hash, "index", address, is_stake FROM unspent_outputs'))
         hi = db._q1("SELECT COUNT(*) FROM utxo.unspent_outputs WHERE tx_hash >= '8'")[0]
         lo2 = db._q1("SELECT COUNT(*) FROM utxo2.unspent_outputs WHERE tx_hash < '8'")[0]
-        ok = got == rows and hi == 0 and lo2 == 0 and db.sql_unspent_outputs_hash() == h == db.utxo.set_hash()
+        ok = (got == rows, hi, lo2, db.sql_unspent_outputs_hash() == h, h == db.utxo.set_hash())
         nxt = db._utxo_next_rowid
         db.close()
-        return ok, nxt
-    ok, nxt = asyncio.run(reopen())
-    assert ok and nxt == max(r[0] for r in rows) + 1
+        return ok, nxt, len(got)
+    ok, nxt, n_got = asyncio.run(reopen())
+    assert ok == (True, 0, 0, True, True), (ok, n_got, len(rows))
+    assert nxt == max(r[0] for r in rows) + 1
