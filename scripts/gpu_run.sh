@@ -9,6 +9,7 @@
 #   verify   bench.py --mode verify --ledger <tmp dir> (file ledger, metric 2)
 #   verifymem bench.py --mode verify (in-memory ledger)
 #   verifygov bench.py --mode verify --governance (file ledger; 12 inodes, 200 validators, 5,000 delegates)
+#   sync     bench.py --mode sync (chain-sync replay of a /get_blocks page, decode-ahead pipeline)
 #   coloc    scripts/colocated.py (node + miner sharing the GPU)
 #   prof     rocprofv3 --kernel-trace --stats over a short bench.py
 #   vprof    rocprofv3 --kernel-trace --stats over the verify bench
@@ -47,6 +48,10 @@ for s in $STEPS; do
       timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger --governance \
         > "$OUT/verify_gov.json" 2> "$OUT/verify_gov.err" || { tail -20 "$OUT/verify_gov.err"; exit 1; }
       cat "$OUT/verify_gov.json" ;;
+    sync)
+      timeout -k 10 600 python bench.py --mode sync > "$OUT/sync.json" 2> "$OUT/sync.err" \
+        || { tail -20 "$OUT/sync.err"; exit 1; }
+      cat "$OUT/sync.json" ;;
     coloc)
       timeout -k 10 300 python scripts/colocated.py --dispatch-log2 24 --prio high --out "$OUT/coloc.json" \
         > "$OUT/coloc.log" 2>&1 || { tail -20 "$OUT/coloc.log"; exit 1; }

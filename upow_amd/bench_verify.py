@@ -370,7 +370,11 @@ async def _run_sync(args, ctx, device, utxo_backend):
         if not await fastpath.create_block_from_hex(content, txs_hex, error_list=errors):
             raise RuntimeError(f'source block rejected: {errors}')
         prev = hashlib.sha256(bytes.fromhex(content)).hexdigest()
-    page = await src.get_blocks(3, n_blocks)
+    page = []  # /get_blocks caps a response at 8 x the max block hex (database.get_blocks): several pages
+    while len(page) < n_blocks:
+        part = await src.get_blocks(3 + len(page), n_blocks - len(page))
+        assert part, 'source ledger returned an empty page'
+        page += part
     assert len(page) == n_blocks and all(len(p['transactions']) == args.txs + 1 for p in page)
     src.close()
     dst, _, _, _ = await _setup(n_blocks, args.txs, seed, utxo_backend, device, base_ts=base_ts, make_blocks=False)
@@ -386,6 +390,7 @@ async def _run_sync(args, ctx, device, utxo_backend):
     errors = []
     if not await create_blocks(page[args.warmup:], errors):
         raise RuntimeError(f'sync rejected: {errors}')
+    dst.flush()  # the SQL tables hold every block (the journal is the commit point)
     ctx.synchronize()
     ctx.barrier()
     wall = ctx.allreduce_max_f(time.perf_counter() - t0)
