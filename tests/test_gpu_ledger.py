@@ -76,5 +76,9 @@ def test_sync_bench_pipeline_host(monkeypatch):
     monkeypatch.setattr(native, 'gpu_available', lambda: False)
     from upow_amd.bench_verify import run_sync_bench
     from upow_amd.parallel.dist import DistContext
+    # a /get_blocks page is capped at 8 x MAX_BLOCK_SIZE_HEX: shrink the cap so the replay needs
+    # several pages, as 10 full 2 MB blocks do
+    from upow_amd.ledger import database
+    monkeypatch.setattr(database, 'MAX_BLOCK_SIZE_HEX', 120 * 560 // 8)
     out = run_sync_bench(argparse.Namespace(steps=3, warmup=1, txs=120), DistContext())
     assert out['config']['block_path'] == 'native' and out['value'] > 0
