@@ -664,10 +664,111 @@ static py::tuple unique_rows(py::buffer buf, int width) {
     return py::make_tuple(py::bytes(uniq), py::bytes(reinterpret_cast<const char*>(inv.data()), inv.size() * 4));
 }
 
+// The key + record stage of the native block path (ledger/fastpath.py) in one call: every 33-byte
+// address of the block (spent outputs' owners and new outputs) is deduplicated, the distinct keys are
+// decompressed in one batch (GPU when there are at least `gpu_min` of them), and the 160-byte verify
+// records [x | y | r | s | digest] of the signature jobs are assembled from the signers' points.
+// Returns (1, records) when every key is a curve point, (0, b"") when one is not, and (-1, b"") when an
+// address is not in the 33-byte form (64-byte keys: the caller's general path checks those).
+static py::tuple block_signer_records(py::buffer pay_addr_b, py::buffer pay_len_b, py::buffer out_addr_b,
+                                      py::buffer out_len_b, py::buffer job_input_b, py::buffer sigs_b,
+                                      py::buffer sig_ids_b, py::buffer digest_b, py::buffer job_tx_b, int64_t gpu_min) {
+    auto view = [](py::buffer& b, size_t elem, const char* what) {
+        py::buffer_info bi = b.request();
+        const size_t total = size_t(bi.size) * size_t(bi.itemsize);
+        if (total % elem) throw std::invalid_argument(std::string(what) + ": size is not a multiple of its row");
+        return std::make_pair(static_cast<const uint8_t*>(bi.ptr), total / elem);
+    };
+    const auto [pay_addr, n_in] = view(pay_addr_b, 64, "pay_addr");
+    const auto [pay_len, n_in2] = view(pay_len_b, 1, "pay_len");
+    const auto [out_addr, n_out] = view(out_addr_b, 64, "out_addr");
+    const auto [out_len, n_out2] = view(out_len_b, 1, "out_len");
+    const auto [job_input_p, n_jobs] = view(job_input_b, 8, "job_input");
+    const auto [sigs, n_sig] = view(sigs_b, 64, "sigs");
+    const auto [sig_ids_p, n_jobs2] = view(sig_ids_b, 8, "sig_ids");
+    const auto [digest, n_tx] = view(digest_b, 32, "digest");
+    const auto [job_tx_p, n_jobs3] = view(job_tx_b, 8, "job_tx");
+    if (n_in != n_in2 || n_out != n_out2 || n_jobs != n_jobs2 || n_jobs != n_jobs3)
+        throw std::invalid_argument("block_signer_records: column lengths differ");
+    const int64_t* job_input = reinterpret_cast<const int64_t*>(job_input_p);
+    const int64_t* sig_ids = reinterpret_cast<const int64_t*>(sig_ids_p);
+    const int64_t* job_tx = reinterpret_cast<const int64_t*>(job_tx_p);
+    for (size_t i = 0; i < n_in; ++i)
+        if (pay_len[i] != 33) return py::make_tuple(-1, py::bytes());
+    for (size_t i = 0; i < n_out; ++i)
+        if (out_len[i] != 33) return py::make_tuple(-1, py::bytes());
+    for (size_t j = 0; j < n_jobs; ++j)
+        if (job_input[j] < 0 || size_t(job_input[j]) >= n_in || sig_ids[j] < 0 || size_t(sig_ids[j]) >= n_sig ||
+            job_tx[j] < 0 || size_t(job_tx[j]) >= n_tx)
+            throw std::invalid_argument("block_signer_records: job index out of range");
+    std::vector<uint8_t> uniq;     // U x 33 distinct keys
+    std::vector<int32_t> pay_uid(n_in);
+    std::vector<uint8_t> xy, okb;  // U x 64, U
+    std::string recs(n_jobs * 160, '\0');
+    bool all_ok = true;
+    {
+        py::gil_scoped_release nogil;
+        const size_t n = n_in + n_out;
+        size_t cap = 16;
+        while (cap < 2 * n) cap <<= 1;
+        std::vector<int32_t> slot(cap, -1);
+        std::vector<const uint8_t*> first;
+        auto key_of = [&](size_t i) { return i < n_in ? pay_addr + 64 * i : out_addr + 64 * (i - n_in); };
+        for (size_t i = 0; i < n; ++i) {
+            const uint8_t* r = key_of(i);
+            uint64_t w[4];
+            std::memcpy(w, r + 1, 32);
+            uint64_t h = (w[0] * 0x9E3779B97F4A7C15ull) ^ (w[1] * 0xC2B2AE3D27D4EB4Full) ^
+                         (w[2] * 0x165667B19E3779F9ull) ^ (w[3] * 0x27D4EB2F165667C5ull) ^ r[0];
+            h ^= h >> 29;
+            size_t sl = size_t(h) & (cap - 1);
+            int32_t uid;
+            for (;;) {
+                const int32_t u = slot[sl];
+                if (u < 0) {
+                    uid = int32_t(first.size());
+                    slot[sl] = uid;
+                    first.push_back(r);
+                    break;
+                }
+                if (std::memcmp(first[size_t(u)], r, 33) == 0) {
+                    uid = u;
+                    break;
+                }
+                sl = (sl + 1) & (cap - 1);
+            }
+            if (i < n_in) pay_uid[i] = uid;
+        }
+        const size_t U = first.size();
+        uniq.resize(U * 33);
+        for (size_t u = 0; u < U; ++u) std::memcpy(&uniq[33 * u], first[u], 33);
+        xy.resize(U * 64);
+        okb.resize(U);
+        if (U) {
+            if (int64_t(U) >= gpu_min) p256_decompress_gpu(uniq.data(), int64_t(U), xy.data(), okb.data());
+            else p256_decompress_host(uniq.data(), int64_t(U), xy.data(), okb.data());
+        }
+        for (size_t u = 0; u < U; ++u) all_ok &= okb[u] != 0;
+        if (all_ok) {
+            for (size_t j = 0; j < n_jobs; ++j) {
+                char* rec = &recs[160 * j];
+                std::memcpy(rec, &xy[64 * size_t(pay_uid[size_t(job_input[j])])], 64);
+                std::memcpy(rec + 64, sigs + 64 * size_t(sig_ids[j]), 64);
+                std::memcpy(rec + 128, digest + 32 * size_t(job_tx[j]), 32);
+            }
+        }
+    }
+    if (!all_ok) return py::make_tuple(0, py::bytes());
+    return py::make_tuple(1, py::bytes(recs));
+}
+
 void register_txcodec(py::module_& m) {
     m.def("fee_strings", &fee_strings);
     m.def("unique_rows", &unique_rows, py::arg("buf"), py::arg("width"),
           "(unique rows in first-seen order, inverse int32) of an n x width byte matrix");
+    m.def("block_signer_records", &block_signer_records, py::arg("pay_addr"), py::arg("pay_len"), py::arg("out_addr"),
+          py::arg("out_len"), py::arg("job_input"), py::arg("sigs"), py::arg("sig_ids"), py::arg("digest"),
+          py::arg("job_tx"), py::arg("gpu_min"));
     m.def("decode_block_txs", &decode_block_txs, py::arg("hexes"), py::arg("threads") = 8,
           "Decode, canonicalise and hash a block's transactions (see csrc/txcodec.cpp)");
     m.def("input_address_strings", &input_address_strings, py::arg("addrs64"), py::arg("lens"), py::arg("in_start"),

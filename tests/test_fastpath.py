@@ -84,6 +84,15 @@ async def _setup(backend='host'):
     return p, base
 
 
+def _off_curve_x() -> int:
+    """Smallest x >= 5 with no curve point (x^3 - 3x + b is not a square mod p)."""
+    from upow_amd.utils import p256 as o
+    x = 5
+    while o.is_on_curve(x, o.x_to_y(x, False)):
+        x += 1
+    return x
+
+
 def _signed(inputs, outputs, keys, message=None):
     tx = Transaction(inputs, outputs, message)
     return tx.sign(keys)
@@ -132,6 +141,7 @@ def test_fast_path_matches_object_path(backend, journal, request):
         c2 = await p.mine(txs2, ts=ts + 60)
         await p.push(c2, txs2, expect=True)
         assert fastpath.last_path == 'native'
+        assert fastpath.last_path == 'native'
     asyncio.run(go())
 
 
@@ -162,7 +172,13 @@ def test_rejections_match(backend, request):
         # unknown input
         ghost = Transaction([TransactionInput('ab' * 32, 0)], [TransactionOutput(address_of(KEYS[1]), Decimal('1'))])
         ghost.inputs[0].signed = good.inputs[0].signed
-        for bad in ([good, dup], [forged], [greedy], [ghost]):
+        # output to a 33-byte address whose x is not on the curve
+        from upow_amd.utils import p256 as o
+        from upow_amd.utils.codec import bytes_to_string
+        x = _off_curve_x()
+        off = bytes_to_string(bytes([42]) + x.to_bytes(32, 'little'))
+        offc = await create_transaction(GENESIS, off, '1')
+        for bad in ([good, dup], [forged], [greedy], [ghost], [offc]):
             c = await p.mine(bad, ts=ts)
             res, err = await p.push(c, bad, expect=False)
             assert fastpath.last_path == 'object' and err
@@ -175,6 +191,54 @@ def test_rejections_match(backend, request):
         await p.push(c, [good], expect=True)
         assert fastpath.last_path == 'native'
     asyncio.run(go())
+
+
+def test_signer_records_native_matches_general():
+    """csrc/txcodec.cpp block_signer_records (dedup + batched decompression + record assembly) against
+    the numpy path that blocks with 64-byte addresses take: same 160-byte records; an off-curve key makes
+    both refuse."""
+    from upow_amd.ledger.utxo import PAYLOAD_DTYPE
+    from upow_amd.ops.native import lib
+    from upow_amd.utils import p256 as o
+    rng = random.Random(7)
+    pts = [o.get_public_key(rng.randrange(1, o.N)) for _ in range(12)]
+    comp = [bytes([43 if q.y & 1 else 42]) + q.x.to_bytes(32, 'little') for q in pts]
+    n_in, n_out, n_tx = 40, 30, 20
+    pay = np.zeros(n_in, dtype=PAYLOAD_DTYPE)
+    for i in range(n_in):
+        pay['addr'][i, :33] = np.frombuffer(comp[rng.randrange(12)], np.uint8)
+    pay['len'] = 33
+    out_addr = np.zeros((n_out, 64), np.uint8)
+    for i in range(n_out):
+        out_addr[i, :33] = np.frombuffer(comp[rng.randrange(12)], np.uint8)
+    out_len = np.full(n_out, 33, np.uint8)
+    sigs = np.frombuffer(rng.randbytes(64 * 25), np.uint8).reshape(-1, 64)
+    digest = np.frombuffer(rng.randbytes(32 * n_tx), np.uint8).reshape(-1, 32)
+    job_input = np.array(sorted(rng.sample(range(n_in), 25)), np.int64)
+    sig_ids = np.arange(25, dtype=np.int64)
+    job_tx = np.array([rng.randrange(n_tx) for _ in range(25)], np.int64)
+    args = (job_input, sigs, sig_ids, digest, job_tx)
+    for gpu_min in (1 << 62,):  # host decompression (the GPU variant runs in the block tests)
+        st, native = lib().block_signer_records(np.ascontiguousarray(pay['addr']), pay['len'].astype(np.uint8),
+                                                out_addr, out_len, *args, gpu_min)
+        general = fastpath._signer_records_general(pay, out_addr, out_len, *args, gpu_min)
+        assert st == 1 and native == general
+        want = comp[0]  # spot check: the first job's signer point
+        rec = np.frombuffer(native, np.uint8).reshape(-1, 160)[0]
+        signer = bytes(pay['addr'][job_input[0], :33])
+        q = pts[comp.index(signer)]
+        assert bytes(rec[:64]) == q.x.to_bytes(32, 'little') + q.y.to_bytes(32, 'little') and want
+        bad = out_addr.copy()
+        x = _off_curve_x()
+        bad[3, 1:33] = np.frombuffer(x.to_bytes(32, 'little'), np.uint8)
+        st, _ = lib().block_signer_records(np.ascontiguousarray(pay['addr']), pay['len'].astype(np.uint8),
+                                           bad, out_len, *args, gpu_min)
+        assert st == 0 and fastpath._signer_records_general(pay, bad, out_len, *args, gpu_min) is None
+        full = out_len.copy()
+        full[5] = 64
+        st, _ = lib().block_signer_records(np.ascontiguousarray(pay['addr']), pay['len'].astype(np.uint8),
+                                           out_addr, full, *args, gpu_min)
+        assert st == -1
 
 
 def test_governance_block_takes_object_path():

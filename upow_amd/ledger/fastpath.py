@@ -78,6 +78,34 @@ def decode(tx_hexes: List[str]) -> Optional[dict]:
     return d
 
 
+def _signer_records_general(pay, out_addr, out_len, job_input, sigs, sig_ids, digest, job_tx, gpu_min):
+    """Verify records when the block has 64-byte (version-1) addresses: 33-byte keys decompressed in one
+    batch, 64-byte ones checked on the curve; None when any key is invalid."""
+    all_addr = np.concatenate([pay['addr'], out_addr]) if len(out_addr) else np.ascontiguousarray(pay['addr'])
+    all_len = np.concatenate([pay['len'].astype(np.uint8), out_len])
+    xy = np.zeros((len(all_addr), 64), dtype=np.uint8)
+    ok = np.ones(len(all_addr), dtype=bool)
+    c33 = np.nonzero(all_len == 33)[0]
+    if len(c33):
+        comp = np.ascontiguousarray(all_addr[c33, :33])
+        ubytes, inv_b = lib().unique_rows(comp, 33)
+        inv = np.frombuffer(inv_b, dtype=np.int32)
+        ubuf = np.frombuffer(ubytes, dtype=np.uint8)
+        out, okb = lib().p256_decompress(ubuf, len(ubuf) // 33 >= gpu_min)
+        xy[c33] = np.frombuffer(out, dtype=np.uint8).reshape(-1, 64)[inv]
+        ok[c33] = np.frombuffer(okb, dtype=np.uint8).astype(bool)[inv]
+    c64 = np.nonzero(all_len == 64)[0]
+    if len(c64):
+        from ..utils.p256 import is_on_curve
+        for k in c64:
+            raw = bytes(all_addr[k])
+            xy[k] = all_addr[k]
+            ok[k] = is_on_curve(int.from_bytes(raw[:32], 'little'), int.from_bytes(raw[32:], 'little'))
+    if not ok.all():
+        return None
+    return np.ascontiguousarray(np.concatenate([xy[job_input], sigs[sig_ids], digest[job_tx]], axis=1)).tobytes()
+
+
 async def create_block_from_hex(block_content: str, tx_hexes: List[str], error_list: list = None,
                                 last_block: dict = None, coinbase=None, mirror: bool = True,
                                 decoded: Optional[dict] = None) -> bool:
@@ -181,49 +209,35 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         return None
     t2 = perf_counter()
 
-    # ---- keys: decompress every distinct 33-byte key (signers + outputs) in one batch
+    # ---- keys + verify records: every distinct 33-byte key (signers + outputs) decompressed in one
+    #      batch, then the 160-byte records of the signature jobs, in one native call
+    #      (csrc/txcodec.cpp block_signer_records); blocks with 64-byte addresses take the numpy path
     in_sig = _i32(d, 'in_sig')
     sig_ids, job_input = np.unique(in_sig, return_index=True)  # first input per distinct signature
     out_len = np.frombuffer(d['out_len'], dtype=np.uint8)
     out_addr = np.frombuffer(d['out_addr'], dtype=np.uint8).reshape(-1, 64)
-    # every spent output's key (the object path resolves each input's point, not only the signers)
-    all_addr = np.concatenate([pay['addr'], out_addr]) if len(out_addr) else np.ascontiguousarray(pay['addr'])
-    all_len = np.concatenate([pay['len'].astype(np.uint8), out_len])
-    xy = np.zeros((len(all_addr), 64), dtype=np.uint8)
-    ok = np.ones(len(all_addr), dtype=bool)
-    c33 = np.nonzero(all_len == 33)[0]
-    if len(c33):
-        comp = np.ascontiguousarray(all_addr[c33, :33])
-        ubytes, inv_b = lib().unique_rows(comp, 33)
-        inv = np.frombuffer(inv_b, dtype=np.int32)
-        ubuf = np.frombuffer(ubytes, dtype=np.uint8)
-        dev = 'gpu' if (gpu_available() and len(ubuf) // 33 >= op.GPU_MIN_BATCH) else 'cpu'
-        out, okb = lib().p256_decompress(ubuf, dev == 'gpu')
-        upts = np.frombuffer(out, dtype=np.uint8).reshape(-1, 64)
-        uok = np.frombuffer(okb, dtype=np.uint8).astype(bool)
-        xy[c33] = upts[inv]
-        ok[c33] = uok[inv]
-    c64 = np.nonzero(all_len == 64)[0]
-    if len(c64):
-        from ..utils.p256 import is_on_curve
-        for k in c64:
-            raw = bytes(all_addr[k])
-            xy[k] = all_addr[k]
-            ok[k] = is_on_curve(int.from_bytes(raw[:32], 'little'), int.from_bytes(raw[32:], 'little'))
+    sigs = np.frombuffer(d['sigs'], dtype=np.uint8).reshape(-1, 64)
+    digest = np.frombuffer(d['digest'], dtype=np.uint8).reshape(-1, 32)
+    in_tx = _i32(d, 'in_tx')
+    job_tx = in_tx[job_input]
     n_jobs = len(job_input)
-    if not ok.all():  # a signer key or an output address is off-curve: the object path decides
+    gpu_min = op.GPU_MIN_BATCH if gpu_available() else 1 << 62
+    kst, rec_bytes = lib().block_signer_records(
+        np.ascontiguousarray(pay['addr']), pay['len'].astype(np.uint8), out_addr, out_len,
+        job_input.astype(np.int64), sigs, sig_ids.astype(np.int64), digest, job_tx.astype(np.int64), gpu_min)
+    if kst == 0:  # a signer key or an output address is off-curve: the object path decides
         return None
+    if kst < 0:
+        rec_bytes = _signer_records_general(pay, out_addr, out_len, job_input, sigs, sig_ids, digest, job_tx, gpu_min)
+        if rec_bytes is None:
+            return None
+    recs = np.frombuffer(rec_bytes, dtype=np.uint8).reshape(-1, 160)
     if np.any(out_amount == 0):
         return None
     t3 = perf_counter()
 
     # ---- signatures: one batched verify (+ the reference's ASCII-hex retry for the failures)
-    sigs = np.frombuffer(d['sigs'], dtype=np.uint8).reshape(-1, 64)
-    digest = np.frombuffer(d['digest'], dtype=np.uint8).reshape(-1, 32)
-    in_tx = _i32(d, 'in_tx')
-    job_tx = in_tx[job_input]
-    recs = np.concatenate([xy[job_input], sigs[sig_ids], digest[job_tx]], axis=1)
-    status = validate._verify(np.ascontiguousarray(recs).tobytes(), None).copy() if n_jobs else np.zeros(0, np.uint8)
+    status = validate._verify(rec_bytes, None).copy() if n_jobs else np.zeros(0, np.uint8)
     retry = np.nonzero(status == op.INVALID)[0]
     if len(retry):
         signed_len = _i32(d, 'signed_len')
