@@ -363,11 +363,12 @@ class Database:
         self.mempool_index = os.environ.get('UPOW_MEMPOOL_INDEX', '1') != '0'
         self._conn.execute('PRAGMA foreign_keys = ON')
         # B-tree page size of a NEW ledger file (fixed once the file exists in WAL mode). A block inserts
-        # ~8.3k wide transaction rows and ~33k UTXO rows and deletes as many: on 32 KB pages the
-        # materialiser threads do that in ~60 % of the time they need on SQLite's default 4 KB pages
-        # (fewer page splits and B-tree levels; profiles/r2/sqlite_page_size_ab.txt: file-ledger verify
-        # 182-241k -> 378k tx/s). Point reads fetch one 32 KB page, a non-issue from the page cache.
-        page = int(os.environ.get('UPOW_SQLITE_PAGE_SIZE', '32768'))
+        # ~8.3k wide transaction rows and ~33k UTXO rows and deletes as many. Larger pages mean fewer
+        # splits and levels (a fresh ledger materialises 1.5x faster on 32 KB pages than on 4 KB:
+        # profiles/r2/sqlite_page_size_ab.txt), but once an index is far larger than one block's
+        # inserts every insert dirties its own leaf, and large pages then write more WAL and lose
+        # (profiles/r2/sqlite_page_scale_cpu.txt, 2 M rows). 8 KB beats 4 KB at both ends.
+        page = int(os.environ.get('UPOW_SQLITE_PAGE_SIZE', '8192'))
         self._conn.execute(f'PRAGMA page_size = {page}')
         self._conn.execute('PRAGMA journal_mode = WAL')
         self._conn.execute('PRAGMA synchronous = ' + ('OFF' if path == ':memory:' else 'NORMAL'))
