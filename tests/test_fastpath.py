@@ -418,3 +418,23 @@ def test_random_blocks_differential(seed, backend, request):
                 assert ok, err
         assert accepted >= 1
     asyncio.run(go())
+
+
+def test_block_trace_file(tmp_path, monkeypatch):
+    """UPOW_TRACE_FILE: one JSON line per validated block with verdict, path, height and stage times."""
+    import json
+    trace = tmp_path / 'blocks.jsonl'
+    monkeypatch.setattr(manager, '_TRACE_PATH', str(trace))
+
+    async def go():
+        p, base = await _setup()
+        p.use(p.a)
+        tx = await create_transaction(GENESIS, address_of(KEYS[0]), '1')
+        c = await p.mine([tx], ts=base + 60 * 10)
+        await p.push(c, [tx], expect=True)
+    asyncio.run(go())
+    recs = [json.loads(line) for line in trace.read_text().splitlines()]
+    assert recs and all(r['ok'] for r in recs)
+    last = recs[-1]
+    assert last['path'] == 'native' and last['txs'] == 1 and last['height'] == 9
+    assert {'decode_s', 'ecdsa_s', 'apply_commit_s'} <= set(last['stages_ms'])
