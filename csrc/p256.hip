@@ -171,8 +171,9 @@ static uint8_t verify_one_host(const VerifyItem& it, const aff* gtab) {
 //   doubling (a = -3, dbl-2008-s-1)            9 products, depth 3  -> 3 steps
 //   addition (add-2008-s)                      14 products, depth 4 -> 4 steps
 // (Jacobian doubling is 8 products but depth 4: 4 steps however many lanes.) A 4-bit window (4
-// doublings + 1 addition) is 16 steps instead of 48 serial products. The window table k*Q (k = 1..15)
-// is built the same way (3 + 13 x 4 steps). u1*G (32 fixed-base byte windows) splits by quarters:
+// doublings + 1 addition) is 16 steps instead of 48 serial products; with signed 5-bit windows
+// (Booth recoding: 52 windows of 5 doublings + 1 addition) u2*Q is 51 x 15 + 52 x 4 = 973 steps. The
+// window table k*Q (k = 1..16) is built the same way (3 + 14 x 4 steps). u1*G (32 fixed-base byte windows) splits by quarters:
 // each lane accumulates 8 windows on its own (Jacobian mixed adds), converts to XYZZ, and the four
 // partial points are broadcast and added. s^-1 runs redundantly on all four lanes (binary Euclid).
 // Waves go four to a workgroup so they land on four different SIMDs of a CU (single-wave workgroups
@@ -315,7 +316,7 @@ UPOW_HD xz jac_to_xz(const jac& p) {
     return xz{p.x, p.y, zz, fe_mul(zz, p.z)};
 }
 
-// Shared verify body. `tab` holds this signature's 16 window entries (global scratch on the GPU, a
+// Shared verify body. `tab` holds this signature's 16 window entries 1Q..16Q (global scratch on the GPU, a
 // local array on the host); `gpart(K)` yields quarter K of u1*G in XYZZ form (on the GPU: lane K's own
 // quarter, broadcast). On the GPU every lane of the quad stores the (identical)
 // entries, so each later table read is of the lane's own store.
@@ -324,30 +325,42 @@ UPOW_HD uint8_t verify_quad_core(const P& pp, const aff& q, const fe& r, const f
     const fe one = fe_one();
     const xz t1{q.x, q.y, one, one};
     xz t = t1;
-    tab[1] = t;
+    tab[0] = t;  // tab[k - 1] = k*Q, k = 1..16
     dbl4(pp, t);
-    tab[2] = t;
-    for (int k = 3; k < 16; ++k) {
+    tab[1] = t;
+    for (int k = 3; k <= 16; ++k) {
         add4(pp, t, t1);
-        tab[k] = t;
+        tab[k - 1] = t;
     }
-    // u2*Q: 64 fixed 4-bit windows from the top; the entry is loaded before the window's doublings
+    // u2*Q: 52 signed 5-bit windows (Booth recoding, digits in [-16, 16]) from the top, so 52
+    // additions instead of the 64 of unsigned 4-bit windows; a negative digit adds the entry with -Y.
+    // Window i's digit comes from bits [5i+4 .. 5i-1] of u2 (bit -1 = 0); they are kept at the top of
+    // a 288-bit shift register s = u2 << 28 and shifted out five at a time (no dynamic register indexing).
     xz acc{one, one, fe_zero(), fe_zero()};
-    fe k2 = u2;  // windows taken from the top nibble, then shifted out (no dynamic register indexing)
-    for (int w = 63; w >= 0; --w) {
-        const uint32_t nib = k2.v[7] >> 28;
+    uint32_t s9[9];
+    s9[0] = u2.v[0] << 28;
 #pragma unroll
-        for (int l = 7; l > 0; --l) k2.v[l] = (k2.v[l] << 4) | (k2.v[l - 1] >> 28);
-        k2.v[0] <<= 4;
+    for (int l = 1; l < 8; ++l) s9[l] = (u2.v[l] << 28) | (u2.v[l - 1] >> 4);
+    s9[8] = u2.v[7] >> 4;
+    for (int w = 51; w >= 0; --w) {
+        const uint32_t v = s9[8] >> 26;  // six bits: window w and the bit below it
+#pragma unroll
+        for (int l = 8; l > 0; --l) s9[l] = (s9[l] << 5) | (s9[l - 1] >> 27);
+        s9[0] <<= 5;
+        const int d = int((v >> 1) & 15u) + int(v & 1u) - 16 * int(v >> 5);
         xz e;
-        if (nib) e = tab[nib];
-        if (w != 63) {
+        if (d) {
+            e = tab[(d < 0 ? -d : d) - 1];
+            if (d < 0) e.y = fe_neg(e.y);
+        }
+        if (w != 51) {
+            dbl4(pp, acc);
             dbl4(pp, acc);
             dbl4(pp, acc);
             dbl4(pp, acc);
             dbl4(pp, acc);
         }
-        if (nib) add4(pp, acc, e);
+        if (d) add4(pp, acc, e);
     }
     // + u1*G, added a quarter at a time
     add4(pp, acc, gpart(std::integral_constant<int, 0>{}));
