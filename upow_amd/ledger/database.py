@@ -633,11 +633,16 @@ class Database:
         queue behind its journal write. A batch journaled while another thread has a Python-side SQL
         transaction open is materialised after that transaction commits (the materialiser needs the
         write lock), which is the order the two would have had if the batch had waited; the
-        transaction's own reads do not wait for it (see :meth:`_settle`)."""
+        transaction's own reads do not wait for it (see :meth:`_settle`).
+
+        The native submit orders records itself (its journal mutex assigns the sequence numbers); the
+        sequence lock here only guards the per-table bookkeeping, which takes maxima and so does not
+        care in which order concurrent submitters get there. A /push_tx admission therefore waits at
+        most for the journal write of a concurrent block, not for its payload assembly too."""
         if self._tx_depth and self._tx_owner == threading.get_ident():
             raise RuntimeError('ledger batch submitted inside an open SQL transaction')
+        seq = self.writer.submit(stmts, meta, block_id)
         with self._seq_lock:
-            seq = self.writer.submit(stmts, meta, block_id)
             if seq > self._submitted:
                 self._submitted = seq
             for t in tables:
