@@ -8,8 +8,9 @@
 // kernel, see "four lanes per signature" below); larger batches one signature per lane:
 //  * u1*G uses a fixed-base byte-window table T[j][b] = b*256^j*G (32 x 255 affine points, 522 KB,
 //    L2/Infinity-Cache resident) -> 32 mixed additions and no doublings;
-//  * u2*Q uses a 4-bit fixed window over a per-signature table {1..15}Q kept in global scratch
-//    (1.4-2 KB per signature does not fit LDS at useful occupancy) -> 256 doublings + 64 additions;
+//  * u2*Q uses signed 5-bit windows (BoothW5) over a per-signature table {1..16}Q kept in global
+//    scratch (1.5-2 KB per signature does not fit LDS at useful occupancy) -> 255 doublings + 52
+//    additions (unsigned 4-bit windows: 252 + 64);
 //  * no field inversion: x(R) == r is tested as X == r*Z^2 (and (r+n)*Z^2 when r+n < p);
 //  * s^-1 mod n by a binary extended Euclid (p256_field.h sc_inv_bgcd_mont);
 //  * status per item: 1 valid, 0 invalid, 2 public key not on curve, 3 r/s out of [1, n]
@@ -137,20 +138,48 @@ UPOW_HD uint8_t verify_epilogue(const jac& R, const fe& r) {
     return 0;
 }
 
+// Signed 5-bit windows of a scalar k < 2^256 (Booth recoding): 52 digits in [-16, 16], top first, with
+// k = sum d_i 32^i. Digit i comes from bits [5i+4 .. 5i-1] of k (bit -1 = 0): d = b0 + b1 + 2 b2 + 4 b3
+// + 8 b4 - 16 b5 of those six bits. They are read from the top of a 288-bit shift register s = k << 28
+// and shifted out five at a time (no dynamic register indexing on the GPU).
+struct BoothW5 {
+    uint32_t s9[9];
+    UPOW_HD explicit BoothW5(const fe& k) {
+        s9[0] = k.v[0] << 28;
+#pragma unroll
+        for (int l = 1; l < 8; ++l) s9[l] = (k.v[l] << 28) | (k.v[l - 1] >> 4);
+        s9[8] = k.v[7] >> 4;
+    }
+    UPOW_HD int next() {
+        const uint32_t v = s9[8] >> 26;
+#pragma unroll
+        for (int l = 8; l > 0; --l) s9[l] = (s9[l] << 5) | (s9[l - 1] >> 27);
+        s9[0] <<= 5;
+        return int((v >> 1) & 15u) + int(v & 1u) - 16 * int(v >> 5);
+    }
+};
+static constexpr int kBoothWindows = 52;
+
 static uint8_t verify_one_host(const VerifyItem& it, const aff* gtab) {
     aff q;
     fe r, u1, u2;
     const uint8_t pro = verify_prologue(it, q, r, u1, u2);
     if (pro != 255) return pro;
-    jac tbl[16];
+    jac tbl[17];  // k*Q, k = 1..16 (signed 5-bit windows)
     tbl[0] = jac_inf();
     tbl[1] = jac_from_aff(q);
-    for (int k = 2; k < 16; ++k) tbl[k] = jac_madd(tbl[k - 1], q);
+    for (int k = 2; k <= 16; ++k) tbl[k] = jac_madd(tbl[k - 1], q);
     jac acc = jac_inf();
-    for (int w = 63; w >= 0; --w) {
-        if (!jac_is_inf(acc)) { acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); }
-        const uint32_t nib = fe_nibble(u2, w);
-        if (nib) acc = jac_add(acc, tbl[nib]);
+    BoothW5 bw(u2);
+    for (int w = kBoothWindows - 1; w >= 0; --w) {
+        if (!jac_is_inf(acc))
+            for (int k = 0; k < 5; ++k) acc = jac_dbl(acc);
+        const int d = bw.next();
+        if (d) {
+            jac e = tbl[d < 0 ? -d : d];
+            if (d < 0) e.y = fe_neg(e.y);
+            acc = jac_add(acc, e);
+        }
     }
     const jac R = jac_add(mul_g(u1, gtab), acc);
     return verify_epilogue(R, r);
@@ -332,28 +361,18 @@ UPOW_HD uint8_t verify_quad_core(const P& pp, const aff& q, const fe& r, const f
         add4(pp, t, t1);
         tab[k - 1] = t;
     }
-    // u2*Q: 52 signed 5-bit windows (Booth recoding, digits in [-16, 16]) from the top, so 52
-    // additions instead of the 64 of unsigned 4-bit windows; a negative digit adds the entry with -Y.
-    // Window i's digit comes from bits [5i+4 .. 5i-1] of u2 (bit -1 = 0); they are kept at the top of
-    // a 288-bit shift register s = u2 << 28 and shifted out five at a time (no dynamic register indexing).
+    // u2*Q: 52 signed 5-bit windows (BoothW5) from the top, so 52 additions instead of the 64 of
+    // unsigned 4-bit windows; a negative digit adds the entry with -Y
     xz acc{one, one, fe_zero(), fe_zero()};
-    uint32_t s9[9];
-    s9[0] = u2.v[0] << 28;
-#pragma unroll
-    for (int l = 1; l < 8; ++l) s9[l] = (u2.v[l] << 28) | (u2.v[l - 1] >> 4);
-    s9[8] = u2.v[7] >> 4;
-    for (int w = 51; w >= 0; --w) {
-        const uint32_t v = s9[8] >> 26;  // six bits: window w and the bit below it
-#pragma unroll
-        for (int l = 8; l > 0; --l) s9[l] = (s9[l] << 5) | (s9[l - 1] >> 27);
-        s9[0] <<= 5;
-        const int d = int((v >> 1) & 15u) + int(v & 1u) - 16 * int(v >> 5);
+    BoothW5 bw(u2);
+    for (int w = kBoothWindows - 1; w >= 0; --w) {
+        const int d = bw.next();
         xz e;
         if (d) {
             e = tab[(d < 0 ? -d : d) - 1];
             if (d < 0) e.y = fe_neg(e.y);
         }
-        if (w != 51) {
+        if (w != kBoothWindows - 1) {
             dbl4(pp, acc);
             dbl4(pp, acc);
             dbl4(pp, acc);
@@ -431,17 +450,22 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void p256_verify_kernel(const 
     fe r, u1, u2;
     const uint8_t pro = verify_prologue(it, q, r, u1, u2);
     if (pro != 255) { status[i] = pro; return; }
-    jac t = jac_from_aff(q);
-    tab_store<SOA>(scratch, n, i, 1, t);
-    for (int k = 2; k < 16; ++k) {
+    jac t = jac_from_aff(q);  // entry k - 1 = k*Q, k = 1..16 (signed 5-bit windows)
+    tab_store<SOA>(scratch, n, i, 0, t);
+    for (int k = 2; k <= 16; ++k) {
         t = jac_madd(t, q);
-        tab_store<SOA>(scratch, n, i, k, t);
+        tab_store<SOA>(scratch, n, i, k - 1, t);
     }
     jac acc = jac_inf();
-    for (int w = 63; w >= 0; --w) {
-        acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc);
-        const uint32_t nib = fe_nibble(u2, w);
-        if (nib) acc = jac_add(acc, tab_load<SOA>(scratch, n, i, int(nib)));
+    BoothW5 bw(u2);
+    for (int w = kBoothWindows - 1; w >= 0; --w) {
+        acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc);
+        const int d = bw.next();
+        if (d) {
+            jac e = tab_load<SOA>(scratch, n, i, (d < 0 ? -d : d) - 1);
+            if (d < 0) e.y = fe_neg(e.y);
+            acc = jac_add(acc, e);
+        }
     }
     const jac R = jac_add(mul_g(u1, gtab), acc);
     status[i] = verify_epilogue(R, r);
