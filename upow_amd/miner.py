@@ -81,10 +81,10 @@ def main(argv=None):
     ap.add_argument('--extranonce', action='store_true',
                     help='also vary the (unchecked) header difficulty field once timestamps are exhausted')
     ap.add_argument('--blocks', type=int, default=0, help='stop after this many accepted blocks (0 = forever)')
-    ap.add_argument('--dispatch-log2', type=int, default=int(os.environ.get('UPOW_POW_DISPATCH_LOG2', '24')),
-                    help='nonces per GPU dispatch (log2). 24 (~0.5 ms) lets a node sharing the GPU run its block '
-                         'kernels between dispatches at a ~1%% hashrate cost; 28 for a dedicated GPU '
-                         '(docs/PERF.md §3)')
+    ap.add_argument('--dispatch-log2', type=int, default=int(os.environ.get('UPOW_POW_DISPATCH_LOG2', '23')),
+                    help='nonces per GPU dispatch (log2). 23 (~0.25 ms) lets a node sharing the GPU run its block '
+                         'kernels between dispatches (its GPU stages ~1.2x their idle time) at a ~2%% hashrate '
+                         'cost; 28 for a dedicated GPU (docs/PERF.md §3)')
     a = ap.parse_args(argv)
     os.environ.setdefault('UPOW_FILE_LOG', '1')  # reference: logs/app.log always (my_logger.py:17-53)
     os.environ['UPOW_POW_DISPATCH_LOG2'] = str(a.dispatch_log2)
