@@ -8,7 +8,9 @@ mkdir -p "$OUT"
 SAN_HOST="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined"
 CXX=/opt/rocm/llvm/bin/clang++
 CFLAGS="-O1 -g -fno-omit-frame-pointer -std=c++17 -I/opt/rocm/include"
-# HIP translation unit (host side instrumented; device code is compiled normally for gfx950)
+# HIP translation unit: device code at -O3 as in the build; host side instrumented, at -O0
+# with line tables: the force-inlined 256-bit field code of the four-lane emulation takes ~10 minutes
+# to optimise under ASan + UBSan instrumentation, ~1 minute unoptimised
 stale() {  # $1 = object, rest = inputs: rebuild when any input is newer
   local o=$1; shift
   [ ! -f "$o" ] && return 0
@@ -17,7 +19,8 @@ stale() {  # $1 = object, rest = inputs: rebuild when any input is newer
 }
 HDRS="csrc/native.h csrc/sha256_common.h csrc/p256_field.h"
 if stale "$OUT/p256.o" csrc/p256.hip $HDRS; then
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 $CFLAGS $SAN_HOST -c csrc/p256.hip -o "$OUT/p256.o"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -Xarch_host -O0 -g1 -std=c++17 -I/opt/rocm/include $SAN_HOST \
+    -c csrc/p256.hip -o "$OUT/p256.o"
 fi
 for f in csrc/sha256_host.cpp csrc/sha256_ni.cpp csrc/base58.cpp csrc/p256_host.cpp tools/host_selftest.cpp; do
   o="$OUT/$(basename "${f%.cpp}").o"
