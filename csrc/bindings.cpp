@@ -106,6 +106,8 @@ PYBIND11_MODULE(_native, m) {
        py::arg("start"), py::arg("count"), py::arg("grid_blocks") = 0, py::arg("chunk_iters") = 0,
        py::arg("cap") = 1 << 16, py::arg("variant") = 0);
 
+    m.def("set_node_device", [](int dev) { set_node_device_native(dev); }, py::arg("device"),
+          "pin node-side GPU work (verify, decompress, batched SHA-256) to this device from every thread");
     m.def("pow_kernel_info", [](int variant) {
         PowKernelInfo k = pow_kernel_info(variant);
         return py::dict(py::arg("cus") = k.cus, py::arg("blocks_per_cu") = k.blocks_per_cu,

@@ -579,6 +579,7 @@ std::vector<uint8_t> p256_verify_host(const uint8_t* items, int64_t n, int threa
 std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
     std::vector<uint8_t> st(static_cast<size_t>(n));
     if (n == 0) return st;
+    node_device_enter();
     const aff* d_tab = device_g_table();
     PooledBuf<VerifyItem> b_items{size_t(n)};
     PooledBuf<uint8_t> b_st{size_t(n)};
@@ -645,8 +646,11 @@ void p256_decompress_host(const uint8_t* in, int64_t n, uint8_t* out, uint8_t* o
     }
 }
 
+void set_node_device_native(int dev) { set_node_device(dev); }
+
 void p256_decompress_gpu(const uint8_t* in, int64_t n, uint8_t* out, uint8_t* ok) {
     if (n == 0) return;
+    node_device_enter();
     PooledBuf<uint8_t> b_in{33 * size_t(n)}, b_out{64 * size_t(n)}, b_ok{size_t(n)};
     uint8_t *d_in = b_in.p, *d_out = b_out.p, *d_ok = b_ok.p;
     node_h2d(d_in, in, 33 * size_t(n), "h2d in");

@@ -107,6 +107,7 @@ static void hchk(hipError_t e, const char* what) {
 }
 
 std::vector<uint8_t> sha256_batch_gpu(const uint8_t* data, int64_t nbytes, const int64_t* offsets, int64_t n) {
+    node_device_enter();
     (void)nbytes;
     std::vector<uint8_t> out(size_t(n) * 32);
     if (n == 0) return out;

@@ -11,6 +11,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -21,6 +22,23 @@ namespace upow {
 
 inline void stream_check(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// The GPU a process's node-side work belongs to (-1: whatever the calling thread has current). A
+// multi-GPU rank sets it once (``set_node_device``), so GPU calls made from its ledger worker thread
+// and executor threads, which start on device 0, still land on the rank's own GPU.
+inline std::atomic<int>& node_device_ref() {
+    static std::atomic<int> dev{-1};
+    return dev;
+}
+inline void set_node_device(int dev) { node_device_ref().store(dev); }
+// Called at the top of every node-side GPU entry point, before any allocation or launch.
+inline void node_device_enter() {
+    const int want = node_device_ref().load();
+    if (want < 0) return;
+    int cur = 0;
+    stream_check(hipGetDevice(&cur), "hipGetDevice");
+    if (cur != want) stream_check(hipSetDevice(want), "hipSetDevice");
 }
 
 enum class StreamRole { Node = 0, Miner = 1 };

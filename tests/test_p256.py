@@ -204,3 +204,21 @@ def test_high_x_r_plus_n_gpu(gpu, variant, monkeypatch):
     monkeypatch.setenv('UPOW_P256_VARIANT', variant)
     recs, exp = _high_x_batch(40, 32)
     assert (op.verify_records(recs, device='gpu') == exp).all()
+
+
+@pytest.mark.gpu
+def test_node_device_pin_from_worker_thread(gpu):
+    """set_node_device pins node-side GPU calls made from other threads (a cluster rank's ledger worker
+    and executor threads start on device 0) to the rank's device."""
+    import threading
+    from upow_amd.ops.native import lib
+    lib().set_node_device(0)
+    try:
+        recs, exp = _batch(100, 9)
+        out = {}
+        t = threading.Thread(target=lambda: out.update(st=op.verify_records(recs, device='gpu')))
+        t.start()
+        t.join()
+        assert (out['st'] == exp).all()
+    finally:
+        lib().set_node_device(-1)

@@ -144,6 +144,11 @@ def init_from_env(backend: Optional[str] = None, want_gpu: bool = True) -> DistC
                 ctx.device = f'cuda:{torch.cuda.current_device()}'
         except Exception:
             gpu = False
+        if gpu:
+            # node-side native GPU calls from any thread of this rank (ledger worker, executors) go to
+            # the rank's GPU, not to the device 0 a fresh thread starts on
+            from ..ops.native import lib
+            lib().set_node_device(int(ctx.device.split(':')[1]))
     force = os.environ.get('UPOW_FORCE_DIST', '0') == '1' and 'MASTER_PORT' in os.environ
     if world > 1 or force:
         ctx.forced = world == 1
