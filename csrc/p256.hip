@@ -197,7 +197,7 @@ static uint8_t verify_one_host(const VerifyItem& it, const aff* gtab) {
 // four independent products, one per lane; DPP quad_perm broadcasts hand every lane the others'
 // results (8 v_mov_dpp per product). Adds/subs stay redundant: they are cheap next to a 256x256-bit
 // product. Points are in XYZZ coordinates (x = X/ZZ, y = Y/ZZZ), whose formulas are shallow:
-//   doubling (a = -3, dbl-2008-s-1)            9 products, depth 3  -> 3 steps
+//   doubling (a = -3, dbl-2008-s-1)            9 products, depth 3  -> 3 steps (the first all squares)
 //   addition (add-2008-s)                      14 products, depth 4 -> 4 steps
 // (Jacobian doubling is 8 products but depth 4: 4 steps however many lanes.) A 4-bit window (4
 // doublings + 1 addition) is 16 steps instead of 48 serial products; with signed 5-bit windows
@@ -215,6 +215,13 @@ struct xz { fe x, y, zz, zzz; };  // XYZZ point; zz == 0 <=> infinity
 static_assert(sizeof(xz) == 128, "xz layout");
 
 struct QuadHost {
+    UPOW_HD void sqr4(const fe& a0, const fe& a1, const fe& a2, const fe& a3, fe& r0, fe& r1, fe& r2, fe& r3) const {
+        const fe m0 = fe_sqr(a0), m1 = fe_sqr(a1), m2 = fe_sqr(a2), m3 = fe_sqr(a3);
+        r0 = m0;
+        r1 = m1;
+        r2 = m2;
+        r3 = m3;
+    }
     UPOW_HD void mul4(const fe& a0, const fe& b0, const fe& a1, const fe& b1, const fe& a2, const fe& b2,
                       const fe& a3, const fe& b3, fe& r0, fe& r1, fe& r2, fe& r3) const {
         const fe m0 = fe_mul(a0, b0), m1 = fe_mul(a1, b1), m2 = fe_mul(a2, b2), m3 = fe_mul(a3, b3);
@@ -244,6 +251,15 @@ struct QuadDev {
             r.v[i] = is3 ? a3.v[i] : t;
         }
         return r;
+    }
+    // a step whose four products are all squares: the squaring row code (36 partial products, not 64)
+    __device__ __forceinline__ void sqr4(const fe& a0, const fe& a1, const fe& a2, const fe& a3, fe& r0, fe& r1, fe& r2,
+                                         fe& r3) const {
+        const fe m = fe_sqr(pick(a0, a1, a2, a3));
+        r0 = fe_quad_bcast<0>(m);
+        r1 = fe_quad_bcast<1>(m);
+        r2 = fe_quad_bcast<2>(m);
+        r3 = fe_quad_bcast<3>(m);
     }
     __device__ __forceinline__ void mul4(const fe& a0, const fe& b0, const fe& a1, const fe& b1, const fe& a2,
                                          const fe& b2, const fe& a3, const fe& b3, fe& r0, fe& r1, fe& r2,
@@ -276,13 +292,14 @@ UPOW_HD void mul1(const P& pp, const fe& a0, const fe& b0, fe& r0) {
 
 UPOW_HD fe fe_x3(const fe& a) { return fe_add(fe_add(a, a), a); }
 
-// dbl-2008-s-1 with a = -3: M = 3 X^2 - 3 ZZ^2 = 3 (X - ZZ)(X + ZZ). Infinity (ZZ = 0) stays infinity.
+// dbl-2008-s-1 with a = -3: M = 3 X^2 - 3 ZZ^2. The first step is three squarings (U^2, X^2, ZZ^2),
+// issued with the squaring code. Infinity (ZZ = 0) stays infinity.
 template <class P>
 UPOW_HD void dbl4(const P& pp, xz& p) {
     const fe u = fe_add(p.y, p.y);
-    fe v, m0;
-    mul2(pp, u, u, fe_sub(p.x, p.zz), fe_add(p.x, p.zz), v, m0);
-    const fe m = fe_x3(m0);
+    fe v, xx, zz2, unused;
+    pp.sqr4(u, p.x, p.zz, p.zz, v, xx, zz2, unused);
+    const fe m = fe_x3(fe_sub(xx, zz2));
     fe w, s, mm, zz3;
     pp.mul4(u, v, p.x, v, m, m, v, p.zz, w, s, mm, zz3);
     const fe x3 = fe_sub(mm, fe_add(s, s));
