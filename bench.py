@@ -78,6 +78,7 @@ def bench_mine(args, ctx):
         'value': round(mhs, 3),
         'unit': 'MH/s',
         'n_gpus': ctx.world if device == 'gpu' else 0,
+        'world': ctx.world,
         'steps': args.steps,
         'warmup': args.warmup,
         'ms_per_step': round(dt * 1000 / max(1, args.steps), 3),
@@ -102,8 +103,9 @@ def bench_mine(args, ctx):
 
 
 def bench_verify(args, ctx):
-    from upow_amd.bench_verify import run_verify_bench
-    return run_verify_bench(args, ctx)
+    from upow_amd.bench_verify import run_cluster_verify_bench, run_verify_bench
+    # N ranks validate ONE chain as a cluster node (replicas + sharded ECDSA), not N private chains
+    return run_cluster_verify_bench(args, ctx) if ctx.is_distributed else run_verify_bench(args, ctx)
 
 
 def _verify_side_metrics(args, ctx) -> dict:
@@ -111,12 +113,12 @@ def _verify_side_metrics(args, ctx) -> dict:
     native push_block path on this rank's GPU, file-backed ledger in a temporary directory."""
     import shutil
     import tempfile
-    from upow_amd.bench_verify import run_verify_bench
+    from upow_amd.bench_verify import run_cluster_verify_bench, run_verify_bench
     tmp = tempfile.mkdtemp(prefix='upow_bench_verify_')
     try:
         v = argparse.Namespace(**{**vars(args), 'steps': args.verify_steps, 'warmup': 2, 'ledger': tmp,
                                   'object_path': False, 'from_mempool': False, 'governance': False})
-        r = run_verify_bench(v, ctx)
+        r = run_cluster_verify_bench(v, ctx) if ctx.is_distributed else run_verify_bench(v, ctx)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     return {'verify_tx_per_s': r['value'], 'verify_ms_per_block': r['ms_per_step'],
@@ -124,11 +126,33 @@ def _verify_side_metrics(args, ctx) -> dict:
             'ecdsa_sig_per_s': r['ecdsa_sig_per_s'],
             'verify_config': {'metric': r['metric'], 'unit': r['unit'], 'steps': args.verify_steps, 'warmup': 2,
                               'txs_per_block': r['config']['seq_len'], 'ledger': r['config']['ledger'],
-                              'block_path': r['config']['block_path'], 'scaling': 'weak',
-                              'data': r['data']}}
+                              'block_path': r['config']['block_path'], 'scaling': r['scaling'],
+                              'layout': r['config']['parallelism'], 'data': r['data']}}
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _launch_ranks(n: int, argv) -> int:
+    """``python bench.py --gpus N`` without a torchrun environment: start ``torch.distributed.run`` with N
+    ranks (one per GPU, 127.0.0.1 rendezvous) as a CHILD process — this process has not touched the GPU
+    (no HIP call, no ``torch.cuda`` query), so nothing is exec'd from a GPU-initialised process. The
+    children inherit stdout: rank 0's JSON line is the only thing printed there."""
+    import subprocess
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')  # dmabuf IPC (RCCL across processes on this host)
+    env.setdefault('OMP_NUM_THREADS', '1')
+    return subprocess.call(cmd, env=env)
 
 
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
@@ -147,6 +171,16 @@ def main(argv=None):
     ap.add_argument('--verify-steps', type=int, default=10,
                     help='mine mode: timed 2 MB blocks of the tx-verify side measurement (0: skip; GPU only)')
     args = ap.parse_args(argv)
+
+    # rank launch: the driver either starts N ranks itself (torchrun sets WORLD_SIZE) or runs
+    # ``bench.py --gpus N`` plainly, in which case this process becomes the launcher of N ranks
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        sys.exit(_launch_ranks(args.gpus, argv))
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world != args.gpus:
+        print(json.dumps({'error': f'--gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a '
+                                   f'{world}-rank number as {args.gpus} GPUs'}), file=sys.stderr, flush=True)
+        sys.exit(2)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from upow_amd.ops.native import lib

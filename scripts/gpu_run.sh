@@ -52,6 +52,19 @@ for s in $STEPS; do
       timeout -k 10 600 python bench.py --mode sync > "$OUT/sync.json" 2> "$OUT/sync.err" \
         || { tail -20 "$OUT/sync.err"; exit 1; }
       cat "$OUT/sync.json" ;;
+    cluster)
+      # one chain on a cluster node through the RCCL path, forced single rank (the 1-GPU box)
+      rm -rf /tmp/upow_bench_ledger
+      UPOW_FORCE_DIST=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --mode verify --ledger /tmp/upow_bench_ledger \
+        > "$OUT/verify_cluster.json" 2> "$OUT/verify_cluster.err" || { tail -20 "$OUT/verify_cluster.err"; exit 1; }
+      grep '^{' "$OUT/verify_cluster.json" ;;
+    launch)
+      # the driver's plain command with an explicit --gpus 1 (no launcher hop) and the torchrun form
+      timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+        --master-port 29534 bench.py --gpus 1 --steps 5 --warmup 1 --verify-steps 2 \
+        > "$OUT/bench_torchrun1.json" 2> "$OUT/bench_torchrun1.err" || { tail -20 "$OUT/bench_torchrun1.err"; exit 1; }
+      grep '^{' "$OUT/bench_torchrun1.json" ;;
     coloc)
       timeout -k 10 300 python scripts/colocated.py --dispatch-log2 24 --prio high --out "$OUT/coloc.json" \
         > "$OUT/coloc.log" 2>&1 || { tail -20 "$OUT/coloc.log"; exit 1; }

@@ -347,6 +347,120 @@ def run_verify_bench(args, ctx):
     }
 
 
+async def _run_cluster(args, ctx, device, utxo_backend):
+    """ONE chain on a G-rank cluster node (parallel/cluster.py): every rank holds a replica built from the
+    same seed; rank 0 (the leader) pushes each block through ``fastpath.create_block_from_hex``, which
+    broadcasts it to the followers as a cluster ``block`` op; every rank validates it with the signature
+    batch sharded across the GPUs (validate.set_dist_context), applies it to its own ledger + HBM index,
+    and an all-reduce checks that all replicas agree. The timed region is the leader's block loop plus
+    every replica's SQL drain; the reported tx/s is the CHAIN's (not a sum over ranks)."""
+    from . import devnet
+    from .constants import START_DIFFICULTY
+    from .ledger import fastpath, manager, validate
+    from .models.block import get_transactions_merkle_tree
+    from .parallel import cluster
+    from .parallel.cluster import unpack_txs
+    n_blocks = args.steps + args.warmup
+    base_ts = ctx.allreduce_min(int(time.time()) - 10_000)
+    db, addr, blocks, _ = await _setup(n_blocks, args.txs, 1234, utxo_backend, device, base_ts=base_ts,
+                                       make_blocks=ctx.rank == 0, ledger_path=_ledger_path(args, ctx))
+    c = cluster.init(ctx)
+    st = c.status(db)
+    if any((s['height'], s['utxo_hash']) != (st[0]['height'], st[0]['utxo_hash']) for s in st):
+        raise RuntimeError(f'cluster bench: replicas differ after setup: {st}')
+    validate.set_dist_context(ctx)
+    headers = []
+    if c.leader:
+        prev = (await db.get_last_block())['hash']
+        for b, txs_hex in enumerate(blocks):
+            content = devnet.mine_header_raw(prev, addr, get_transactions_merkle_tree(txs_hex), base_ts + 10 + b,
+                                             START_DIFFICULTY, device=device)
+            headers.append(content)
+            prev = hashlib.sha256(bytes.fromhex(content)).hexdigest()
+    stages = []
+    total_txs = 0
+    try:
+        for b in range(n_blocks):
+            if b == args.warmup:
+                ctx.barrier()
+                ctx.synchronize()
+                t_start = time.perf_counter()
+            t0 = time.perf_counter()
+            errors = []
+            if c.leader:
+                ok = await fastpath.create_block_from_hex(headers[b], blocks[b], error_list=errors)
+                n_tx = len(blocks[b])
+            else:
+                msg = c.recv()
+                assert msg['op'] == 'block', msg['op']
+                txs = unpack_txs(msg['_payload'])
+                ok = await fastpath.create_block_from_hex(msg['content'], txs, error_list=errors, mirror=False)
+                n_tx = len(txs)
+            if not ok:
+                raise RuntimeError(f'cluster bench: block {b} rejected on rank {ctx.rank}: {errors}')
+            if b >= args.warmup:
+                total_txs += n_tx
+                stages.append({'block_s': time.perf_counter() - t0, **manager.last_block_timings,
+                               **{k: v for k, v in validate.timings.items() if k.endswith('_s')},
+                               **fastpath.timings})
+        db.flush()
+        ctx.synchronize()
+        ctx.barrier()
+        wall = ctx.allreduce_max_f(time.perf_counter() - t_start)
+        st = c.status(db)
+        agree = all((s['height'], s['utxo_hash']) == (st[0]['height'], st[0]['utxo_hash']) for s in st)
+        if not agree:
+            raise RuntimeError(f'cluster bench: replicas diverged: {st}')
+    finally:
+        validate.set_dist_context(None)
+        cluster.init(type(ctx)())  # a world-1 context: no cluster
+    writer = db.writer.stats() if db.writer is not None else None
+    if writer is not None:
+        writer = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in writer.items() if k != 'error'}
+    return total_txs, wall, stages, args.txs, [fastpath.last_path], {
+        'drain_s': 0.0, 'writer': writer, 'window_unix': None, 'governance': None,
+        'replicas': [{'rank': s['rank'], 'height': s['height'], 'utxo_hash': s['utxo_hash']} for s in st]}
+
+
+def run_cluster_verify_bench(args, ctx):
+    """tx-verify/s of ONE chain on the cluster node (all ranks; the same numbers on every rank)."""
+    from .ops.native import gpu_available
+    device = 'gpu' if gpu_available() else 'cpu'
+    utxo_backend = 'gpu' if device == 'gpu' else 'host'
+    total_txs, wall, stages, txs_per_block, paths, extra = asyncio.run(_run_cluster(args, ctx, device, utxo_backend))
+    avg = {k: round(sum(s[k] for s in stages) / len(stages) * 1000, 2) for k in stages[0]
+           if isinstance(stages[0][k], float)}
+    return {
+        'metric': 'block_tx_verify_per_s',
+        'value': round(total_txs / wall, 1),
+        'unit': 'tx/s',
+        'n_gpus': ctx.world if device == 'gpu' else 0,
+        'world': ctx.world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(wall * 1000 / max(1, args.steps), 2),
+        'higher_is_better': True,
+        'scaling': 'strong',
+        'vs_baseline': None,
+        'dtype': 'uint32',
+        'data': 'synthetic 2 MB blocks: random P-256 keys, 2-in/2-out signed txs, funding UTXOs',
+        'config': {'model': 'upow cluster node: one chain, G replicas, sharded ECDSA (push_block path)',
+                   'global_batch': txs_per_block, 'seq_len': txs_per_block, 'parallelism': f'replica{ctx.world}+sigshard',
+                   'device': device, 'utxo_backend': utxo_backend, 'block_path': '+'.join(p for p in paths if p),
+                   'ledger': 'file (WAL)' if getattr(args, 'ledger', None) else 'memory',
+                   'txs_from': 'block body (hex)'},
+        'stage_ms_avg': avg,
+        'validate_tx_per_s': round(txs_per_block / max(1e-9, (avg.get('decode_to_checks_s', 0) + avg.get('utxo_s', 0)
+                                                             + avg.get('verify_s', 0)) / 1000), 1),
+        'ecdsa_sig_per_s': round(txs_per_block / max(1e-9, avg.get('ecdsa_s', 0) / 1000), 1),
+        'commit_latency_ms': avg.get('block_s'),
+        'final_drain_ms': 0.0,
+        'ledger_writer': extra['writer'],
+        'window_unix': extra['window_unix'],
+        'replicas': extra['replicas'],
+    }
+
+
 async def _run_sync(args, ctx, device, utxo_backend):
     """Sync throughput: a source ledger applies ``steps + warmup`` full blocks through push_block; a
     second ledger with the same genesis + funding then replays them the way a syncing node does

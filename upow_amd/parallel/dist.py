@@ -55,6 +55,15 @@ class DistContext:
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return [int(x) for x in t.tolist()]
 
+    def allreduce_sum_vec(self, values) -> list:
+        """Element-wise SUM of a short int vector in ONE collective."""
+        if not self.is_distributed:
+            return [int(v) for v in values]
+        import torch.distributed as dist
+        t = self._t(list(values))
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return [int(x) for x in t.tolist()]
+
     def allreduce_max_f(self, v: float) -> float:
         if not self.is_distributed:
             return float(v)

@@ -61,8 +61,15 @@ class DataParallelMiner:
         if self.next_word >= NONCE_SPACE:
             self.roll()
         ctx = self.ctx
-        winner = ctx.allreduce_min(ctx.rank if local_header is not None else ctx.world)
-        global_hits = ctx.allreduce_sum(len(res.nonces))
+        # ONE all-reduce(SUM) per step: a found-flag slot per rank (the lowest set slot is the winner)
+        # followed by this rank's solution count
+        vec = [0] * (ctx.world + 1)
+        if local_header is not None:
+            vec[ctx.rank] = 1
+        vec[ctx.world] = len(res.nonces)
+        red = ctx.allreduce_sum_vec(vec)
+        winner = next((r for r in range(ctx.world) if red[r]), ctx.world)
+        global_hits = red[ctx.world]
         header = None
         if winner < ctx.world:
             header = ctx.broadcast_bytes(local_header if ctx.rank == winner else None, src=winner)
