@@ -17,8 +17,25 @@
 //   restart        journal records above the recorded sequence are re-applied before the ledger opens,
 //                  a torn tail record is cut off.
 //
-// Each record carries an opaque `meta` section (the block's undo data: created and spent outpoints with
-// their payloads) that rollback reads back (journal_meta) to undo the HBM table without a rebuild.
+// Concurrency of the commit point: a submitter reserves its sequence number and file offset under the
+// journal mutex and writes its record with pwrite(2) OUTSIDE it, so a /push_tx admission never waits
+// behind a block's 10 MB append; records are handed to the materialisers strictly in sequence order once
+// every lower record is written (publication).
+//
+// Durability (sync modes): off; group (the materialisers fdatasync before applying, so no SQL file is
+// ever ahead of the durable journal prefix); block (group + every BLOCK record is fdatasync'd before
+// submit returns, i.e. before push_block answers and gossips); commit (every record).
+//
+// Undo data (a block's created and spent outpoints with their payloads) goes to an undo log of its own
+// (segment files next to the journal) that journal rotation does not touch; it keeps the last `undo_keep`
+// blocks so rollback over the reference's 500-block fork window never needs an index rebuild.
+//
+// Backpressure: a block submit waits while any materialiser has more than `max_queue_bytes` queued, so a
+// sync that validates faster than SQLite materialises cannot grow memory without bound.
+//
+// Integrity: a statement whose expected change count is not met (a DELETE of spent outputs that did not
+// find every row: the HBM index and SQL disagree) stops the writer; SQLITE_BUSY/LOCKED on a group is
+// retried with backoff instead.
 //
 // libsqlite3 is resolved with dlopen from the copy the interpreter's _sqlite3 module already loaded.
 #include <dlfcn.h>
@@ -26,6 +43,7 @@
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#include <dirent.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -53,7 +71,8 @@ namespace {
 struct sqlite3;
 struct sqlite3_stmt;
 typedef void (*destructor_t)(void*);
-constexpr int SQLITE_OK = 0, SQLITE_ROW = 100, SQLITE_DONE = 101, SQLITE_CONSTRAINT = 19;
+constexpr int SQLITE_OK = 0, SQLITE_BUSY = 5, SQLITE_LOCKED = 6, SQLITE_ROW = 100, SQLITE_DONE = 101,
+              SQLITE_CONSTRAINT = 19;
 constexpr int SQLITE_OPEN_READWRITE = 0x2, SQLITE_OPEN_CREATE = 0x4, SQLITE_OPEN_NOMUTEX = 0x8000,
               SQLITE_OPEN_URI = 0x40;
 
@@ -353,6 +372,11 @@ struct SqlError : std::runtime_error {
     SqlError(const std::string& m, int c) : std::runtime_error(m), rc(c) {}
 };
 
+// A statement changed a different number of rows than its batch declared (ledger/index divergence).
+struct MismatchError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
 // ------------------------------------------------------------------------------------------ journal
 constexpr uint32_t kMagic = 0x314a5055;  // "UPJ1"
 struct RecHeader {
@@ -418,14 +442,15 @@ uint32_t record_crc(const RecHeader& h, const char* meta, const char* payload) {
     return crc32c(c, payload, h.payload_len);
 }
 
-void write_all(int fd, const char* p, size_t n) {
+void pwrite_all(int fd, const char* p, size_t n, off_t at) {
     while (n) {
-        ssize_t w = ::write(fd, p, n);
+        ssize_t w = ::pwrite(fd, p, n, at);
         if (w < 0) {
             if (errno == EINTR) continue;
             throw std::runtime_error(std::string("journal write failed: ") + strerror(errno));
         }
         p += w;
+        at += w;
         n -= size_t(w);
     }
 }
@@ -453,16 +478,196 @@ int sqlite_disable_memstatus() {
     return a.config(SQLITE_CONFIG_MEMSTATUS, 0);
 }
 
+// ------------------------------------------------------------------------------------------ undo log
+// A block's undo data lives in segment files `<prefix>.<n>` (n = 0, 1, ...), each holding up to
+// `seg_blocks` records: {magic, crc, block_id, len} + body. A negative block_id is a tombstone ("forget
+// blocks >= -(block_id + 1)", written on rollback so a restart does not resurrect rolled-back blocks).
+// Whole segments whose newest block is older than the retention window are unlinked: no compaction copy.
+constexpr uint32_t kUndoMagic = 0x31445055;  // "UPD1"
+struct UndoHeader {
+    uint32_t magic;
+    uint32_t crc;  // CRC-32C over block_id, len and the body
+    int64_t block_id;
+    uint64_t len;
+};
+static_assert(sizeof(UndoHeader) == 24, "undo record header layout");
+
+class UndoLog {
+   public:
+    UndoLog(std::string prefix, int64_t keep, int64_t seg_blocks)
+        : prefix_(std::move(prefix)), keep_(std::max<int64_t>(1, keep)), seg_blocks_(std::max<int64_t>(1, seg_blocks)) {}
+
+    ~UndoLog() {
+        for (auto& kv : segs_)
+            if (kv.second.fd >= 0) ::close(kv.second.fd);
+    }
+
+    void open() {
+        std::lock_guard<std::mutex> lk(mu_);
+        const size_t slash = prefix_.rfind('/');
+        const std::string dir = slash == std::string::npos ? "." : prefix_.substr(0, slash);
+        const std::string base = (slash == std::string::npos ? prefix_ : prefix_.substr(slash + 1)) + ".";
+        std::vector<int64_t> found;
+        if (DIR* d = ::opendir(dir.c_str())) {
+            while (dirent* e = ::readdir(d)) {
+                const std::string name = e->d_name;
+                if (name.size() <= base.size() || name.compare(0, base.size(), base) != 0) continue;
+                const std::string num = name.substr(base.size());
+                if (num.find_first_not_of("0123456789") != std::string::npos) continue;
+                found.push_back(std::stoll(num));
+            }
+            ::closedir(d);
+        }
+        std::sort(found.begin(), found.end());
+        for (int64_t no : found) {
+            Seg& sg = segs_[no];
+            sg.fd = ::open(path(no).c_str(), O_RDWR | O_CLOEXEC);
+            if (sg.fd < 0) throw std::runtime_error("undo log: cannot open " + path(no) + ": " + strerror(errno));
+            scan(no, sg, no == found.back());
+        }
+        if (segs_.empty()) new_segment(0);
+    }
+
+    void put(int64_t block_id, const std::string& body) {
+        std::lock_guard<std::mutex> lk(mu_);
+        append(block_id, body);
+        index_max_ = std::max(index_max_, block_id);
+        prune();
+    }
+
+    void forget_from(int64_t block_id) {
+        std::lock_guard<std::mutex> lk(mu_);
+        index_.erase(index_.lower_bound(block_id), index_.end());
+        append(-(block_id + 1), std::string());
+        index_max_ = index_.empty() ? -1 : index_.rbegin()->first;
+    }
+
+    bool get(int64_t block_id, std::string& out) {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = index_.find(block_id);
+        if (it == index_.end()) return false;
+        auto sg = segs_.find(it->second.first);
+        if (sg == segs_.end()) return false;
+        UndoHeader h;
+        if (!read_exact(sg->second.fd, reinterpret_cast<char*>(&h), sizeof h, it->second.second) ||
+            h.magic != kUndoMagic || h.block_id != block_id)
+            return false;
+        out.assign(h.len, '\0');
+        if (!read_exact(sg->second.fd, out.data(), out.size(), it->second.second + off_t(sizeof h))) return false;
+        return crc(h, out.data()) == h.crc;
+    }
+
+    void fill_stats(py::dict& d) {
+        std::lock_guard<std::mutex> lk(mu_);
+        int64_t bytes = 0;
+        for (auto& kv : segs_) bytes += kv.second.size;
+        d["undo_segments"] = int64_t(segs_.size());
+        d["undo_blocks"] = int64_t(index_.size());
+        d["undo_bytes"] = bytes;
+        d["undo_first_block"] = index_.empty() ? int64_t(-1) : index_.begin()->first;
+        d["undo_pruned_segments"] = pruned_;
+    }
+
+   private:
+    struct Seg {
+        int fd = -1;
+        off_t size = 0;
+        int64_t records = 0;
+        int64_t max_block = -1;
+    };
+
+    std::string path(int64_t no) const { return prefix_ + "." + std::to_string(no); }
+
+    static uint32_t crc(const UndoHeader& h, const char* body) {
+        uint32_t c = crc32c(0, &h.block_id, sizeof(UndoHeader) - 8);
+        return crc32c(c, body, h.len);
+    }
+
+    void new_segment(int64_t no) {
+        Seg& sg = segs_[no];
+        sg.fd = ::open(path(no).c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
+        if (sg.fd < 0) throw std::runtime_error("undo log: cannot create " + path(no) + ": " + strerror(errno));
+    }
+
+    void scan(int64_t no, Seg& sg, bool last) {
+        const off_t end = ::lseek(sg.fd, 0, SEEK_END);
+        off_t at = 0;
+        while (at + off_t(sizeof(UndoHeader)) <= end) {
+            UndoHeader h;
+            if (!read_exact(sg.fd, reinterpret_cast<char*>(&h), sizeof h, at) || h.magic != kUndoMagic) break;
+            if (h.len > uint64_t(end) || at + off_t(sizeof h + h.len) > end) break;
+            std::string body(h.len, '\0');
+            if (!read_exact(sg.fd, body.data(), body.size(), at + off_t(sizeof h)) || crc(h, body.data()) != h.crc) break;
+            if (h.block_id >= 0) {
+                index_[h.block_id] = {no, at};
+                sg.max_block = std::max(sg.max_block, h.block_id);
+            } else {
+                index_.erase(index_.lower_bound(-(h.block_id + 1)), index_.end());
+            }
+            ++sg.records;
+            at += off_t(sizeof h + h.len);
+        }
+        if (at != end && last && ::ftruncate(sg.fd, at) != 0) throw std::runtime_error("undo log truncate failed");
+        sg.size = at;
+        index_max_ = index_.empty() ? -1 : index_.rbegin()->first;
+    }
+
+    void append(int64_t block_id, const std::string& body) {
+        auto cur = std::prev(segs_.end());
+        if (cur->second.records >= seg_blocks_) {
+            new_segment(cur->first + 1);
+            cur = std::prev(segs_.end());
+        }
+        Seg& sg = cur->second;
+        UndoHeader h{kUndoMagic, 0, block_id, body.size()};
+        h.crc = crc(h, body.data());
+        pwrite_all(sg.fd, reinterpret_cast<const char*>(&h), sizeof h, sg.size);
+        pwrite_all(sg.fd, body.data(), body.size(), sg.size + off_t(sizeof h));
+        if (block_id >= 0) {
+            index_[block_id] = {cur->first, sg.size};
+            sg.max_block = std::max(sg.max_block, block_id);
+        }
+        sg.size += off_t(sizeof h + body.size());
+        ++sg.records;
+    }
+
+    void prune() {
+        // unlink whole segments (never the current one) whose newest block is outside the window
+        const int64_t floor_id = index_max_ - keep_;
+        for (auto it = segs_.begin(); it != segs_.end() && std::next(it) != segs_.end();) {
+            if (it->second.max_block >= floor_id) {
+                ++it;
+                continue;
+            }
+            for (auto ix = index_.begin(); ix != index_.end();)
+                ix = ix->second.first == it->first ? index_.erase(ix) : std::next(ix);
+            ::close(it->second.fd);
+            ::unlink(path(it->first).c_str());
+            ++pruned_;
+            it = segs_.erase(it);
+        }
+    }
+
+    std::string prefix_;
+    int64_t keep_, seg_blocks_;
+    std::mutex mu_;
+    std::map<int64_t, Seg> segs_;
+    std::map<int64_t, std::pair<int64_t, off_t>> index_;  // block id -> (segment, offset)
+    int64_t index_max_ = -1;
+    int64_t pruned_ = 0;
+};
+
 // ------------------------------------------------------------------------------------------ writer
 // One journal, several database files ("shards"): each statement names the file it writes (flags bits
 // 8..15) and every file has its own materialiser thread and connection, so the UTXO table and the
 // block/tx tables are brought up to date in parallel. Each file records the last journal sequence it
 // applied (upow_journal_state, updated in the same transaction as the rows).
-enum SyncMode { SYNC_OFF = 0, SYNC_GROUP = 1, SYNC_COMMIT = 2 };
+enum SyncMode { SYNC_OFF = 0, SYNC_GROUP = 1, SYNC_COMMIT = 2, SYNC_BLOCK = 3 };
 
 struct Batch {
     uint64_t seq;
     std::shared_ptr<std::string> payload;  // u32 n_stmts + statements
+    off_t end = 0;                         // journal offset just past the record
 };
 
 struct Shard {
@@ -470,6 +675,7 @@ struct Shard {
     sqlite3* db = nullptr;
     std::unordered_map<std::string, sqlite3_stmt*> stmts;  // shard thread only
     std::deque<Batch> queue;
+    size_t queued_bytes = 0;
     uint64_t applied = 0;
     int64_t groups = 0, replayed = 0, apply_ns = 0, commit_ns = 0, sync_ns = 0;
     std::thread thread;
@@ -478,10 +684,13 @@ struct Shard {
 class LedgerWriter {
    public:
     LedgerWriter(const std::vector<std::string>& db_paths, const std::string& journal_path, int sync_mode,
-                 int64_t cache_mb, int group_max, int64_t journal_max_bytes)
+                 int64_t cache_mb, int group_max, int64_t journal_max_bytes, int64_t undo_keep,
+                 int64_t max_queue_bytes, double throttle_timeout_s, int busy_timeout_ms)
         : journal_path_(journal_path), sync_(sync_mode), group_max_(std::max(1, group_max)),
-          journal_max_(journal_max_bytes) {
+          journal_max_(journal_max_bytes), max_queue_bytes_(max_queue_bytes), throttle_timeout_s_(throttle_timeout_s),
+          busy_timeout_ms_(std::max(1, busy_timeout_ms)), undo_(journal_path + ".undo", undo_keep, 64) {
         if (db_paths.empty() || db_paths.size() > 16) throw std::invalid_argument("1..16 database files");
+        if (sync_ < SYNC_OFF || sync_ > SYNC_BLOCK) throw std::invalid_argument("sync mode must be 0..3");
         for (auto& p : db_paths) {
             shards_.emplace_back(new Shard());
             Shard& sh = *shards_.back();
@@ -490,6 +699,7 @@ class LedgerWriter {
         }
         fd_ = ::open(journal_path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
         if (fd_ < 0) throw std::runtime_error("ledger writer: cannot open journal " + journal_path + ": " + strerror(errno));
+        undo_.open();
         recover();
         for (size_t i = 0; i < shards_.size(); ++i) shards_[i]->thread = std::thread([this, i] { run(i); });
     }
@@ -503,6 +713,7 @@ class LedgerWriter {
             stop_ = true;
         }
         cv_.notify_all();
+        cv_done_.notify_all();
         for (auto& sh : shards_)
             if (sh->thread.joinable()) sh->thread.join();
         {
@@ -523,13 +734,13 @@ class LedgerWriter {
         closed_ = true;
     }
 
-    // Commit point: append the record (and fdatasync in SYNC_COMMIT mode), queue it for every
-    // materialiser. Returns the record's sequence number.
     struct Span {
         const char* p;
         size_t n;
     };
 
+    // Commit point: reserve (seq, offset), write the record outside the journal mutex, publish it to the
+    // materialisers in sequence order, make it durable as the sync mode asks. Returns the sequence number.
     uint64_t submit(const std::vector<Span>& stmts, const std::string& meta, int64_t block_id) {
         auto payload = std::make_shared<std::string>();
         size_t total = 4;
@@ -538,7 +749,10 @@ class LedgerWriter {
         uint32_t ns = uint32_t(stmts.size());
         payload->append(reinterpret_cast<const char*>(&ns), 4);
         for (auto& st : stmts) payload->append(st.p, st.n);
+        if (block_id >= 0) throttle();
+        const size_t rec = sizeof(RecHeader) + payload->size();
         uint64_t seq;
+        off_t at;
         {
             std::lock_guard<std::mutex> jl(jmu_);
             {
@@ -547,23 +761,38 @@ class LedgerWriter {
                 if (closed_ || stop_) throw std::runtime_error("ledger writer is closed");
             }
             seq = next_seq_++;
-            RecHeader h{kMagic, 0, seq, block_id, meta.size(), payload->size()};
-            h.crc = record_crc(h, meta.data(), payload->data());
-            const off_t at = journal_size_;
-            write_all(fd_, reinterpret_cast<const char*>(&h), sizeof h);
-            write_all(fd_, meta.data(), meta.size());
-            write_all(fd_, payload->data(), payload->size());
-            if (sync_ == SYNC_COMMIT) ::fdatasync(fd_);
-            journal_size_ += off_t(sizeof h + meta.size() + payload->size());
-            if (block_id >= 0) meta_index_[block_id] = {at, seq};
-            bytes_written_ += int64_t(sizeof h + meta.size() + payload->size());
+            at = journal_size_;
+            journal_size_ += off_t(rec);
+            bytes_written_ += int64_t(rec);
+            ++inflight_;
+        }
+        RecHeader h{kMagic, 0, seq, block_id, 0, payload->size()};
+        h.crc = record_crc(h, nullptr, payload->data());
+        std::string werr;
+        try {
+            pwrite_all(fd_, reinterpret_cast<const char*>(&h), sizeof h, at);
+            pwrite_all(fd_, payload->data(), payload->size(), at + off_t(sizeof h));
+        } catch (const std::exception& e) {
+            werr = e.what();
+        }
+        {
+            std::lock_guard<std::mutex> jl(jmu_);
+            --inflight_;
         }
         {
             std::lock_guard<std::mutex> lk(mu_);
-            for (auto& sh : shards_) sh->queue.push_back(Batch{seq, payload});
-            submitted_ = seq;
+            if (!werr.empty() && !failed_) {
+                failed_ = true;
+                error_ = werr;
+            }
+            written_.emplace(seq, Batch{seq, payload, at + off_t(rec)});
+            publish_locked();
         }
         cv_.notify_all();
+        cv_done_.notify_all();
+        if (!werr.empty()) throw std::runtime_error(werr);
+        if (sync_ == SYNC_COMMIT || (sync_ == SYNC_BLOCK && block_id >= 0)) make_durable(seq);
+        if (block_id >= 0 && !meta.empty()) undo_.put(block_id, meta);
         return seq;
     }
 
@@ -574,6 +803,7 @@ class LedgerWriter {
             paused_ = p;
         }
         cv_.notify_all();
+        cv_done_.notify_all();
     }
 
     uint64_t applied(int shard) {
@@ -594,65 +824,78 @@ class LedgerWriter {
         if (failed_ && applied_locked(shard) < seq) throw std::runtime_error("ledger writer failed: " + error_);
     }
 
-    py::object journal_meta(int64_t block_id) {
-        std::lock_guard<std::mutex> jl(jmu_);
-        auto it = meta_index_.find(block_id);
-        if (it == meta_index_.end()) return py::none();
-        RecHeader h;
-        if (!read_exact(fd_, reinterpret_cast<char*>(&h), sizeof h, it->second.first) || h.magic != kMagic)
-            return py::none();
-        std::string meta(h.meta_len, '\0');
-        if (!read_exact(fd_, meta.data(), meta.size(), it->second.first + off_t(sizeof h))) return py::none();
-        return py::bytes(meta);
+    // Every record with sequence <= seq durable on disk (fdatasync'd journal prefix).
+    void durable(uint64_t seq) {
+        if (sync_ == SYNC_OFF) return;
+        make_durable(seq);
     }
 
-    // Drop the undo index of blocks >= block_id (they were rolled back).
-    void forget_blocks_from(int64_t block_id) {
-        std::lock_guard<std::mutex> jl(jmu_);
-        meta_index_.erase(meta_index_.lower_bound(block_id), meta_index_.end());
+    py::object journal_meta(int64_t block_id) {
+        std::string out;
+        if (!undo_.get(block_id, out)) return py::none();
+        return py::bytes(out);
     }
+
+    // Drop the undo data of blocks >= block_id (they were rolled back).
+    void forget_blocks_from(int64_t block_id) { undo_.forget_from(block_id); }
 
     py::dict stats() {
         py::dict d;
-        std::lock_guard<std::mutex> jl(jmu_);
-        std::lock_guard<std::mutex> lk(mu_);
-        d["submitted"] = submitted_;
-        d["applied"] = applied_locked(-1);
-        size_t queued = 0;
-        int64_t groups = 0, replayed = 0;
-        double apply_s = 0, commit_s = 0, sync_s = 0;
-        py::list per;
-        for (auto& sh : shards_) {
-            queued = std::max(queued, sh->queue.size());
-            groups += sh->groups;
-            replayed = std::max(replayed, sh->replayed);
-            apply_s = std::max(apply_s, sh->apply_ns / 1e9);
-            commit_s = std::max(commit_s, sh->commit_ns / 1e9);
-            sync_s = std::max(sync_s, sh->sync_ns / 1e9);
-            py::dict x;
-            x["applied"] = sh->applied;
-            x["groups"] = sh->groups;
-            x["apply_s"] = sh->apply_ns / 1e9;
-            x["commit_s"] = sh->commit_ns / 1e9;
-            x["replayed"] = sh->replayed;
-            per.append(x);
+        {
+            std::lock_guard<std::mutex> jl(jmu_);
+            std::lock_guard<std::mutex> lk(mu_);
+            d["submitted"] = submitted_;
+            d["applied"] = applied_locked(-1);
+            size_t queued = 0, qbytes = 0;
+            int64_t groups = 0, replayed = 0;
+            double apply_s = 0, commit_s = 0, sync_s = 0;
+            py::list per;
+            for (auto& sh : shards_) {
+                queued = std::max(queued, sh->queue.size());
+                qbytes = std::max(qbytes, sh->queued_bytes);
+                groups += sh->groups;
+                replayed = std::max(replayed, sh->replayed);
+                apply_s = std::max(apply_s, sh->apply_ns / 1e9);
+                commit_s = std::max(commit_s, sh->commit_ns / 1e9);
+                sync_s = std::max(sync_s, sh->sync_ns / 1e9);
+                py::dict x;
+                x["applied"] = sh->applied;
+                x["groups"] = sh->groups;
+                x["apply_s"] = sh->apply_ns / 1e9;
+                x["commit_s"] = sh->commit_ns / 1e9;
+                x["replayed"] = sh->replayed;
+                x["queued"] = sh->queue.size();
+                x["queued_bytes"] = sh->queued_bytes;
+                per.append(x);
+            }
+            d["queued"] = queued;
+            d["queued_bytes"] = qbytes;
+            d["max_queue_bytes"] = max_queue_bytes_;
+            d["throttle_waits"] = throttle_waits_;
+            d["throttle_s"] = throttle_ns_ / 1e9;
+            d["busy_retries"] = busy_retries_;
+            d["groups"] = groups;
+            d["journal_bytes"] = int64_t(journal_size_);
+            d["bytes_written"] = bytes_written_;
+            d["apply_s"] = apply_s;  // the slowest file
+            d["commit_s"] = commit_s;
+            d["sync_s"] = sync_s;
+            d["replayed"] = replayed;
+            d["rotations"] = rotations_;
+            d["failed"] = failed_;
+            d["error"] = error_;
+            d["change_mismatches"] = mismatches_;
+            d["sync_mode"] = sync_;
+            d["synced"] = synced_.load();
+            d["synced_bytes"] = synced_bytes_.load();
+            d["fdatasyncs"] = syncs_.load();
+            d["fdatasync_s"] = sync_total_ns_.load() / 1e9;
+            d["shards"] = per;
+            py::dict st;
+            for (auto& kv : stmt_stats_) st[py::str(kv.first)] = py::make_tuple(kv.second.first / 1e9, kv.second.second);
+            d["statements"] = st;
         }
-        d["queued"] = queued;
-        d["groups"] = groups;
-        d["journal_bytes"] = int64_t(journal_size_);
-        d["bytes_written"] = bytes_written_;
-        d["apply_s"] = apply_s;  // the slowest file
-        d["commit_s"] = commit_s;
-        d["sync_s"] = sync_s;
-        d["replayed"] = replayed;
-        d["rotations"] = rotations_;
-        d["failed"] = failed_;
-        d["error"] = error_;
-        d["change_mismatches"] = mismatches_;
-        d["shards"] = per;
-        py::dict st;
-        for (auto& kv : stmt_stats_) st[py::str(kv.first)] = py::make_tuple(kv.second.first / 1e9, kv.second.second);
-        d["statements"] = st;
+        undo_.fill_stats(d);
         return d;
     }
 
@@ -662,6 +905,68 @@ class LedgerWriter {
         uint64_t m = ~uint64_t(0);
         for (auto& sh : shards_) m = std::min(m, sh->applied);
         return m;
+    }
+
+    // caller holds mu_: queue every written record that continues the published prefix
+    void publish_locked() {
+        while (!written_.empty() && written_.begin()->first == next_pub_) {
+            Batch b = std::move(written_.begin()->second);
+            written_.erase(written_.begin());
+            for (auto& sh : shards_) {
+                sh->queue.push_back(b);
+                sh->queued_bytes += b.payload->size();
+            }
+            submitted_ = b.seq;
+            pub_end_ = b.end;
+            ++next_pub_;
+        }
+    }
+
+    size_t max_queued_bytes_locked() const {
+        size_t m = 0;
+        for (auto& sh : shards_) m = std::max(m, sh->queued_bytes);
+        return m;
+    }
+
+    void throttle() {
+        if (max_queue_bytes_ <= 0) return;
+        std::unique_lock<std::mutex> lk(mu_);
+        auto ok = [&] { return max_queued_bytes_locked() < size_t(max_queue_bytes_) || failed_ || stop_ || paused_; };
+        if (ok()) return;
+        const auto t0 = std::chrono::steady_clock::now();
+        ++throttle_waits_;
+        cv_done_.wait_for(lk, std::chrono::duration<double>(throttle_timeout_s_), ok);
+        throttle_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    }
+
+    void make_durable(uint64_t seq) {
+        {
+            // the record and every lower one written (published), so one sync covers a contiguous prefix
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_done_.wait(lk, [&] { return next_pub_ > seq || failed_ || stop_; });
+        }
+        ensure_synced(seq);
+    }
+
+    void ensure_synced(uint64_t seq) {
+        if (synced_.load() >= seq) return;
+        std::lock_guard<std::mutex> sl(sync_mu_);
+        if (synced_.load() >= seq) return;
+        uint64_t upto;
+        off_t upto_end;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            upto = next_pub_ - 1;
+            upto_end = pub_end_;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        ::fdatasync(fd_);
+        sync_total_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        ++syncs_;
+        if (upto > synced_.load()) {
+            synced_.store(upto);
+            synced_bytes_.store(int64_t(upto_end));
+        }
     }
 
     void open_shard(Shard& sh, int64_t cache_mb) {
@@ -674,7 +979,9 @@ class LedgerWriter {
             sh.db = nullptr;
             throw std::runtime_error("ledger writer: cannot open " + sh.path + ": " + m);
         }
-        a.busy_timeout(sh.db, 60000);
+        // short per-attempt wait: a group that still finds the file locked is retried (run()), so a long
+        // Python-side transaction delays materialisation but never stops the writer
+        a.busy_timeout(sh.db, busy_timeout_ms_);
         // the journal is the durability point: SQL commits never need to reach the disk on their own
         exec(sh.db, "PRAGMA journal_mode = WAL");
         exec(sh.db, "PRAGMA synchronous = OFF");
@@ -731,7 +1038,7 @@ class LedgerWriter {
     }
 
     // Apply the statements of one encoded batch that belong to `shard`, inside its open transaction.
-    void apply_batch(size_t shard, const std::string& payload) {
+    void apply_batch(size_t shard, const std::string& payload, bool strict) {
         const SqliteApi& a = api();
         Shard& sh = *shards_[shard];
         In in{payload.data(), payload.data() + payload.size()};
@@ -836,10 +1143,17 @@ class LedgerWriter {
             const int64_t ns_used =
                 std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - ts0).count();
             std::lock_guard<std::mutex> lk(mu_);
-            if (expect >= 0 && changes != expect) ++mismatches_;
             auto& acc = stmt_stats_[sql.substr(0, 48)];
             acc.first += ns_used;
             acc.second += n;
+            if (expect >= 0 && changes != expect) {
+                ++mismatches_;
+                // the journaled block said every one of these rows exists (validated against the HBM
+                // index): SQL and the index have diverged. Stop before materialising anything further.
+                if (strict)
+                    throw MismatchError("ledger writer: " + std::to_string(changes) + " of " + std::to_string(expect) +
+                                        " rows changed [" + sql.substr(0, 120) + "]");
+            }
         }
     }
 
@@ -868,7 +1182,6 @@ class LedgerWriter {
                 !read_exact(fd_, payload->data(), payload->size(), body + off_t(h.meta_len)))
                 break;
             if (record_crc(h, meta.data(), payload->data()) != h.crc) break;
-            if (h.block_id >= 0) meta_index_[h.block_id] = {at, h.seq};
             if (h.seq > min_applied) records.emplace_back(h.seq, payload);
             max_seq = std::max<uint64_t>(max_seq, h.seq);
             at = body + off_t(h.meta_len + h.payload_len);
@@ -880,6 +1193,10 @@ class LedgerWriter {
         journal_size_ = at;
         ::lseek(fd_, at, SEEK_SET);
         next_seq_ = max_seq + 1;
+        next_pub_ = next_seq_;
+        pub_end_ = at;
+        synced_.store(max_seq);
+        synced_bytes_.store(int64_t(at));
         for (size_t i = 0; i < shards_.size(); ++i) {
             Shard& sh = *shards_[i];
             uint64_t last = 0;
@@ -888,7 +1205,7 @@ class LedgerWriter {
             try {
                 for (auto& r : records) {
                     if (r.first <= sh.applied) continue;
-                    apply_batch(i, *r.second);
+                    apply_batch(i, *r.second, false);
                     last = r.first;
                     ++n;
                 }
@@ -908,8 +1225,10 @@ class LedgerWriter {
     void maybe_rotate() {
         // every record is in every file: make the SQL side durable, then start an empty journal
         std::lock_guard<std::mutex> jl(jmu_);
+        if (inflight_ != 0) return;  // a reserved record is still being written
         {
             std::lock_guard<std::mutex> lk(mu_);
+            if (!written_.empty()) return;
             for (auto& sh : shards_)
                 if (!sh->queue.empty() || sh->applied != submitted_) return;
         }
@@ -924,8 +1243,12 @@ class LedgerWriter {
         ::fdatasync(fd_);
         ::lseek(fd_, 0, SEEK_SET);
         journal_size_ = 0;
-        meta_index_.clear();
-        ++rotations_;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            pub_end_ = 0;
+        }
+        synced_bytes_.store(0);
+        ++rotations_;  // the undo log is separate: rollback keeps working across rotations
     }
 
     void run(size_t i) {
@@ -947,25 +1270,44 @@ class LedgerWriter {
             }
             auto t0 = std::chrono::steady_clock::now();
             try {
-                // every record of the group was fully written before it was queued, so a sync started
-                // now covers them; it runs without jmu_, so submit() (a /push_tx admission, the next
-                // block) never waits behind the disk flush
-                if (sync_ == SYNC_GROUP && i == 0) ::fdatasync(fd_);
+                // no SQL file may get ahead of the durable journal prefix: every materialiser makes sure the
+                // group's records are synced (one fdatasync serves all files; free when already synced)
+                if (sync_ != SYNC_OFF) ensure_synced(group.back().seq);
                 auto t1 = std::chrono::steady_clock::now();
-                exec(sh.db, "BEGIN IMMEDIATE");
-                try {
-                    for (auto& b : group) apply_batch(i, *b.payload);
-                    exec(sh.db, "UPDATE upow_journal_state SET seq = " + std::to_string(group.back().seq) + " WHERE k = 0");
-                } catch (...) {
-                    rollback(sh.db);
-                    throw;
+                std::chrono::steady_clock::time_point t2;
+                for (int attempt = 0;; ++attempt) {
+                    try {
+                        exec(sh.db, "BEGIN IMMEDIATE");
+                        try {
+                            for (auto& b : group) apply_batch(i, *b.payload, true);
+                            exec(sh.db, "UPDATE upow_journal_state SET seq = " + std::to_string(group.back().seq) +
+                                            " WHERE k = 0");
+                            t2 = std::chrono::steady_clock::now();
+                            exec(sh.db, "COMMIT");
+                        } catch (...) {
+                            rollback(sh.db);
+                            throw;
+                        }
+                        break;
+                    } catch (const SqlError& e) {
+                        // another connection holds the file's write lock (a long Python-side transaction):
+                        // back off and retry the whole group instead of stopping the ledger
+                        const int rc = e.rc & 0xff;
+                        bool stopping;
+                        {
+                            std::lock_guard<std::mutex> lk(mu_);
+                            stopping = stop_;
+                            if (rc == SQLITE_BUSY || rc == SQLITE_LOCKED) ++busy_retries_;
+                        }
+                        if ((rc != SQLITE_BUSY && rc != SQLITE_LOCKED) || stopping) throw;
+                        std::this_thread::sleep_for(std::chrono::milliseconds(std::min(1000, 5 << std::min(attempt, 8))));
+                    }
                 }
-                auto t2 = std::chrono::steady_clock::now();
-                exec(sh.db, "COMMIT");
                 auto t3 = std::chrono::steady_clock::now();
                 {
                     std::lock_guard<std::mutex> lk(mu_);
                     sh.applied = group.back().seq;
+                    for (auto& b : group) sh.queued_bytes -= b.payload->size();
                     ++sh.groups;
                     sh.sync_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
                     sh.apply_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
@@ -990,18 +1332,29 @@ class LedgerWriter {
     int group_max_;
     int64_t journal_max_;
     std::vector<std::unique_ptr<Shard>> shards_;
+    int64_t max_queue_bytes_;
+    double throttle_timeout_s_;
+    int busy_timeout_ms_;
+    UndoLog undo_;
     int fd_ = -1;
     off_t journal_size_ = 0;
-    std::map<int64_t, std::pair<off_t, uint64_t>> meta_index_;  // block id -> (record offset, seq)
-    std::mutex jmu_;  // journal file + meta index + next_seq_
+    std::mutex jmu_;  // reservations: next_seq_, journal_size_, inflight_
     uint64_t next_seq_ = 1;
+    int64_t inflight_ = 0;  // reserved records not yet written
     int64_t bytes_written_ = 0;
-    std::mutex mu_;  // queues + watermarks + statistics
+    std::mutex mu_;  // publication, queues, watermarks, statistics
     std::condition_variable cv_, cv_done_;
-    uint64_t submitted_ = 0;
+    std::map<uint64_t, Batch> written_;  // written but not yet published (a lower record still in flight)
+    uint64_t next_pub_ = 1;
+    off_t pub_end_ = 0;       // journal offset past the last published record
+    uint64_t submitted_ = 0;  // last published sequence
     bool stop_ = false, closed_ = false, failed_ = false, paused_ = false;
     std::string error_;
-    int64_t rotations_ = 0, mismatches_ = 0;
+    int64_t rotations_ = 0, mismatches_ = 0, busy_retries_ = 0, throttle_waits_ = 0, throttle_ns_ = 0;
+    std::mutex sync_mu_;
+    std::atomic<uint64_t> synced_{0};
+    std::atomic<int64_t> synced_bytes_{0};
+    std::atomic<int64_t> syncs_{0}, sync_total_ns_{0};
     std::map<std::string, std::pair<int64_t, int64_t>> stmt_stats_;  // sql prefix -> (ns, rows)
 };
 
@@ -1019,12 +1372,16 @@ void register_ledger_writer(py::module_& m) {
     });
     py::class_<LedgerWriter>(m, "LedgerWriter")
         .def(py::init([](std::vector<std::string> dbs, const std::string& journal, int sync, int64_t cache_mb,
-                         int group_max, int64_t journal_max) {
+                         int group_max, int64_t journal_max, int64_t undo_keep, int64_t max_queue_bytes,
+                         double throttle_timeout_s, int busy_timeout_ms) {
                  py::gil_scoped_release nogil;
-                 return new LedgerWriter(dbs, journal, sync, cache_mb, group_max, journal_max);
+                 return new LedgerWriter(dbs, journal, sync, cache_mb, group_max, journal_max, undo_keep,
+                                         max_queue_bytes, throttle_timeout_s, busy_timeout_ms);
              }),
              py::arg("db_paths"), py::arg("journal_path"), py::arg("sync_mode") = 1, py::arg("cache_mb") = 256,
-             py::arg("group_max") = 8, py::arg("journal_max_bytes") = int64_t(1) << 30)
+             py::arg("group_max") = 8, py::arg("journal_max_bytes") = int64_t(1) << 30, py::arg("undo_keep") = 600,
+             py::arg("max_queue_bytes") = int64_t(512) << 20, py::arg("throttle_timeout_s") = 300.0,
+             py::arg("busy_timeout_ms") = 5000)
         .def("submit",
              [](LedgerWriter& w, py::list stmts, py::bytes meta, int64_t block_id) {
                  // only pointers are taken under the GIL (the list and the meta object keep the bytes
@@ -1045,6 +1402,7 @@ void register_ledger_writer(py::module_& m) {
         .def("set_paused", &LedgerWriter::set_paused)
         .def("wait", &LedgerWriter::wait, py::arg("seq"), py::arg("shard") = -1, py::arg("timeout_s") = 0.0,
              py::call_guard<py::gil_scoped_release>())
+        .def("durable", &LedgerWriter::durable, py::arg("seq"), py::call_guard<py::gil_scoped_release>())
         .def("journal_meta", &LedgerWriter::journal_meta)
         .def("forget_blocks_from", &LedgerWriter::forget_blocks_from)
         .def("stats", &LedgerWriter::stats)

@@ -38,7 +38,7 @@ from ..utils.logstore import LogStore
 from ..utils.logger import get_logger
 from .governance import GOV_TABLES, STAKE, GovernanceIndex
 from .mempool import MempoolIndex
-from .utxo import PAYLOAD_DTYPE, TAG_BY_TABLE, UtxoIndex, make_payload
+from .utxo import FLAG_STAKE, PAYLOAD_DTYPE, TAG_BY_TABLE, UtxoIndex, make_payload
 
 logger = get_logger(__name__)
 
@@ -460,14 +460,24 @@ class Database:
         """The native writer owns its own connection to the same file. Opening it re-applies any
         journal records that were committed but not yet materialised when the process stopped."""
         from ..ops.native import lib
-        mode = {'off': 0, 'group': 1, 'commit': 2}[os.environ.get('UPOW_JOURNAL_SYNC', 'group')]
+        # durability: 'block' (default) fdatasyncs every block record before push_block answers and gossips;
+        # mempool admissions are synced by the materialisers' group sync (a lost admission is a lost mempool
+        # entry, never a lost block). 'group' syncs only there; 'commit' syncs every record; 'off' never.
+        mode = {'off': 0, 'group': 1, 'commit': 2, 'block': 3}[os.environ.get('UPOW_JOURNAL_SYNC', 'block')]
         if self.path == ':memory:':
             mode = 0
         journal = os.environ.get('UPOW_JOURNAL_PATH') or os.path.join(os.path.dirname(os.path.abspath(self.file)),
                                                                        os.path.basename(self.file) + '.journal')
         self.writer = lib().LedgerWriter([self.file, *self.utxo_files], journal, mode, cache_mb,
                                          int(os.environ.get('UPOW_WRITER_GROUP', '8')),
-                                         int(os.environ.get('UPOW_JOURNAL_MAX_MB', '1024')) << 20)
+                                         int(os.environ.get('UPOW_JOURNAL_MAX_MB', '1024')) << 20,
+                                         # undo data of the last N blocks survives journal rotation: a
+                                         # rollback over the reference's 500-block fork window never rebuilds
+                                         int(os.environ.get('UPOW_UNDO_KEEP', '600')),
+                                         # a block submit waits while a materialiser lags by more than this
+                                         int(os.environ.get('UPOW_WRITER_MAX_QUEUE_MB', '512')) << 20,
+                                         float(os.environ.get('UPOW_WRITER_THROTTLE_TIMEOUT', '300')),
+                                         int(os.environ.get('UPOW_WRITER_BUSY_MS', '5000')))
         self._eph['writer'] = self.writer if self.path == ':memory:' else None
         self.journal_path = journal
         st = self.writer.stats()
@@ -601,6 +611,23 @@ class Database:
         if self.lagging():
             import asyncio
             await asyncio.get_running_loop().run_in_executor(None, self._settle, tables)
+
+    def publish_writer_metrics(self):
+        """Journal/materialiser state as gauges for GET /metrics: a stopped writer (row-count mismatch = the
+        HBM index and SQL diverged, or an I/O error) must be visible to monitoring, not only in the log."""
+        if self.writer is None:
+            return
+        from ..utils import metrics
+        st = self.writer.stats()
+        g = metrics.set_gauge
+        g('upow_ledger_writer_failed', int(bool(st['failed'])), help='1 when the ledger writer stopped after an error')
+        g('upow_ledger_row_mismatches', st['change_mismatches'], help='statements whose row count differed from the block')
+        g('upow_ledger_journal_lag', st['submitted'] - st['applied'], help='journal records not yet in SQL')
+        g('upow_ledger_queued_bytes', st['queued_bytes'], help='bytes queued for the slowest materialiser')
+        g('upow_ledger_throttle_seconds', st['throttle_s'], help='time block submits waited on a lagging materialiser')
+        g('upow_ledger_busy_retries', st['busy_retries'], help='materialiser groups retried after SQLITE_BUSY')
+        g('upow_ledger_journal_synced', st['synced'], help='last journal sequence made durable (fdatasync)')
+        g('upow_ledger_undo_blocks', st['undo_blocks'], help='blocks with undo data retained for rollback')
 
     def flush(self):
         """Block until the SQL tables hold every committed block (tests, tools, shutdown)."""
@@ -901,32 +928,36 @@ class Database:
             self.mempool_reloads += 1
         return mp
 
-    def _mempool_confirm(self, mempool_deleted: bool, txids=None, in_keys=None, hashes=None, inputs=None):
-        """A committed block's txs and inputs leave the mempool index. A tx of the block admitted after
-        the block found the mempool empty (its batch then carries no mempool deletes) is deleted from
-        the tables by a follow-up batch, journaled after the admission's own INSERTs."""
+    def _mempool_confirm(self, mempool_deleted: bool, txids=None, in_keys=None, hashes=None, inputs=None,
+                         block_seq: int = 0):
+        """A committed block's txs and inputs leave the mempool index. The block's own batch deletes them
+        from the tables only if it carried the mempool DELETEs and the tx's INSERTs were journaled before
+        it; a tx of the block whose admission batch came after the block's (admitted on the HTTP loop while
+        the block was being applied) is deleted by a follow-up batch, journaled after those INSERTs."""
         mp = self._mp
         if mp is None:
             return
         if txids is not None:
-            hit_tx, hit_in = mp.confirm_raw(txids, in_keys)
+            hit_tx, hit_in, late_tx, late_in = mp.confirm_raw(txids, in_keys, block_seq)
         else:
-            hit_tx, hit_in = mp.confirm(hashes or [], inputs or [])
+            hit_tx, hit_in, late_tx, late_in = mp.confirm(hashes or [], inputs or [], block_seq)
         if not (hit_tx or hit_in):
             return
         self._pending_empty = None
         self._mempool_ver += 1
-        if mempool_deleted:
+        if not mempool_deleted:
+            late_tx, late_in = hit_tx, hit_in
+        if not (late_tx or late_in):
             return
         stmts = []
-        if hit_tx:
-            stmts.append(self.encode('DELETE FROM pending_transactions WHERE tx_hash = ?', [[h.hex() for h in hit_tx]],
-                                     len(hit_tx)))
-        if hit_in:
+        if late_tx:
+            stmts.append(self.encode('DELETE FROM pending_transactions WHERE tx_hash = ?',
+                                     [[h.hex() for h in late_tx]], len(late_tx)))
+        if late_in:
             stmts.append(self.encode('DELETE FROM pending_spent_outputs WHERE tx_hash = ? AND "index" = ?',
-                                     [[k[:32].hex() for k in hit_in],
-                                      np.array([int.from_bytes(k[32:36], 'little') for k in hit_in], np.int64)],
-                                     len(hit_in)))
+                                     [[k[:32].hex() for k in late_in],
+                                      np.array([int.from_bytes(k[32:36], 'little') for k in late_in], np.int64)],
+                                     len(late_in)))
         self.submit_batch(stmts, self._PENDING)
 
     def _pending_spent_set(self) -> Set[Tuple[str, int]]:
@@ -979,7 +1010,8 @@ class Database:
                 stmts.append(self.encode('INSERT INTO pending_spent_outputs (tx_hash, "index") VALUES (?, ?)',
                                          [[h for h, _ in inputs], np.array([i for _, i in inputs], np.int64)],
                                          len(inputs)))
-            self.submit_batch(stmts, self._PENDING)
+            seq = self.submit_batch(stmts, self._PENDING)
+            mp.set_seq(tx_hash, inputs, seq)
         self._pending_empty = False
         self._mempool_ver += 1
         return True
@@ -1063,7 +1095,8 @@ class Database:
         for tx in transactions_to_remove:
             if isinstance(tx, Transaction):
                 outputs_to_be_restored.extend([(i.tx_hash, i.index) for i in tx.inputs if i.tx_hash not in hashes])
-        undone = self._undo_blocks_in_index(block_no, tip)
+        created = self._undo_blocks_in_index(block_no, tip)
+        undone = created is not None
         gone = self._block_tx_hashes('b.id >= ?', (block_no,))
         self._x('DELETE FROM blocks WHERE id >= ?', (block_no,))
         self._utxo_cascade(gone)
@@ -1074,7 +1107,12 @@ class Database:
         if not undone:
             self._rebuild_utxo_index()
         elif self.gov is not None:
-            self.gov.rebuild()
+            # governance rows of the removed blocks' txs go with them (FK cascade); restored outpoints
+            # return as plain unstaked UTXOs, so no governance row comes back: removing is the whole undo
+            with self.gov.lock:
+                for t in self.gov.tables:
+                    self.gov.removed(t, created)
+                self.gov.version += 1
         self.utxo_rollbacks = getattr(self, 'utxo_rollbacks', 0) + 1
         self.last_rollback_undo = undone
 
@@ -1615,7 +1653,8 @@ class Database:
         seq = 0
         if self.writer is not None:
             enc = [self.encode(*st) for st in stmts]
-            meta = b''.join((struct.pack('<qII', int(b['id']), n_out + len(cb_keys), n_in), memoryview(recs),
+            meta = b''.join((bytes.fromhex(b['hash']), struct.pack('<qII', int(b['id']), n_out + len(cb_keys), n_in),
+                             memoryview(recs),
                              memoryview(np.ascontiguousarray(cb_recs)), memoryview(spent),
                              memoryview(np.ascontiguousarray(spent_payload)).cast('B')))
             seq = self.submit_batch(enc, tables, meta, int(b['id']))
@@ -1641,7 +1680,8 @@ class Database:
             self._pending_empty = None
             self._mempool_ver += 1
         if n:
-            self._mempool_confirm(bool(mempool), txids=np.asarray(tx_cols[0][1]).reshape(-1, 32), in_keys=in_keys)
+            self._mempool_confirm(bool(mempool), txids=np.asarray(tx_cols[0][1]).reshape(-1, 32), in_keys=in_keys,
+                                  block_seq=seq)
         if self.gov is not None and n_in:
             hit = self._stake_spent(spent)
             if hit:
@@ -1750,8 +1790,8 @@ class Database:
         spent_pay = np.concatenate(sp_pay) if sp_pay else np.zeros(0, PAYLOAD_DTYPE)
 
         enc = [self.encode(*st) for st in stmts]
-        meta = struct.pack('<qII', int(b['id']), len(created_recs), len(spent_recs)) + created_recs.tobytes() + \
-            spent_recs.tobytes() + spent_pay.tobytes()
+        meta = bytes.fromhex(b['hash']) + struct.pack('<qII', int(b['id']), len(created_recs), len(spent_recs)) + \
+            created_recs.tobytes() + spent_recs.tobytes() + spent_pay.tobytes()
         seq = self.submit_batch(enc, tables, meta, int(b['id']))
         # ---- the indexes and the chain-tip cache follow the commit point
         if len(spent_recs):
@@ -1768,7 +1808,7 @@ class Database:
             self._pending_empty = None
             self._mempool_ver += 1
         if transactions:
-            self._mempool_confirm(mempool, hashes=[t.hash() for t in transactions], inputs=all_in)
+            self._mempool_confirm(mempool, hashes=[t.hash() for t in transactions], inputs=all_in, block_seq=seq)
         return seq
 
     def _gov_apply_block(self, rows, outs, spends, block_ts: int):
@@ -1791,29 +1831,52 @@ class Database:
                     g.tables[table].add((o[0], o[1]), o[2], _at(am[o[0]], o[1]), _at(ia[o[0]], o[1]), block_ts)
             g.version += 1
 
-    def _undo_blocks_in_index(self, from_id: int, tip: int) -> bool:
-        """Roll the UTXO index back from ``tip`` to ``from_id - 1`` with the journal's undo records
-        (created outpoints erased, spent outpoints re-inserted with their payloads, newest block first).
-        False when a block in the range has no undo record (applied by the object path, or journal
-        rotated): the caller rebuilds the index instead."""
+    def _undo_blocks_in_index(self, from_id: int, tip: int):
+        """Roll the UTXO index back from ``tip`` to ``from_id - 1`` with the undo log's records (created
+        outpoints erased, spent outpoints re-inserted, newest block first). Returns the created outpoints
+        (for the governance index), or None when a block in the range has no undo record or its record
+        belongs to another block with that id (applied before a rollback whose tombstone was lost): the
+        caller rebuilds the index instead.
+
+        Spent outpoints come back the way ``remove_blocks`` restores them in SQL (reference
+        database.py:146-169 → add_unspent_outputs): as ``unspent_outputs`` rows with ``is_stake`` NULL,
+        whatever table they were spent from — so the index stays record-for-record equal to a rebuild."""
         if self.writer is None or tip < from_id:
-            return tip < from_id
-        metas = [self.writer.journal_meta(i) for i in range(tip, from_id - 1, -1)]
-        if any(m is None for m in metas):
-            return False
+            return [] if tip < from_id else None
+        hashes = {int(r[0]): r[1] for r in self._q('SELECT id, hash FROM blocks WHERE id >= ? AND id <= ?',
+                                                  (from_id, tip))}
+        metas = []
+        for i in range(tip, from_id - 1, -1):
+            m = self.writer.journal_meta(i)
+            if m is None or len(m) < 48 or hashes.get(i) is None or m[:32] != bytes.fromhex(hashes[i]):
+                return None
+            metas.append(m)
+        tag_u = TAG_BY_TABLE['unspent_outputs']
+        created_all = []
         for m in metas:
-            _, n_created, n_spent = struct.unpack_from('<qII', m, 0)
-            o = 16
+            _, n_created, n_spent = struct.unpack_from('<qII', m, 32)
+            o = 48
             created = np.frombuffer(m, dtype=np.uint8, count=40 * n_created, offset=o).reshape(-1, 40)
             o += 40 * n_created
             spent = np.frombuffer(m, dtype=np.uint8, count=40 * n_spent, offset=o).reshape(-1, 40)
             o += 40 * n_spent
             pay = np.frombuffer(m, dtype=PAYLOAD_DTYPE, count=n_spent, offset=o)
             if n_created:
-                self.utxo.erase_records(created.copy())
+                rec = created.copy()
+                rec[:, 36:40] = np.full((n_created, 1), 0xFF, dtype=np.uint32).view(np.uint8)  # any table
+                self.utxo.erase_records(rec)
+                created_all.append(created)
             if n_spent:
-                self.utxo.insert_records(spent.copy(), pay.copy())
-        return True
+                rec = spent.copy()
+                rec[:, 36:40] = np.full((n_spent, 1), tag_u, dtype=np.uint32).view(np.uint8)
+                p = pay.copy()
+                p['flags'] &= np.uint32(~FLAG_STAKE & 0xFFFFFFFF)
+                self.utxo.insert_records(rec, p)
+        keys = []
+        for c in created_all:
+            idx = c[:, 32:36].copy().view(np.uint32).ravel()
+            keys.extend(zip((bytes(r).hex() for r in c[:, :32]), idx.tolist()))
+        return keys
 
     async def _add_gov_outputs(self, table: str, outputs: List[tuple]):
         if not outputs:

@@ -59,6 +59,11 @@ class MempoolIndex:
             self.txs[k] = int(t)
             self.keys[k] = order_key(hx, fees)
         self.spent: Set[bytes] = {outpoint_key(h, i) for h, i in spent_rows}
+        # journal sequence of each admission's INSERT batch (rows loaded from SQL: 0, already materialised).
+        # A block confirming a tx whose admission was journaled AFTER the block's own batch cannot rely on
+        # that batch's DELETEs (they ran before the INSERTs): it needs a follow-up delete.
+        self.seq: Dict[bytes, int] = {}
+        self.spent_seq: Dict[bytes, int] = {}
         self.min_ptime: Optional[int] = min(self.txs.values()) if self.txs else None
 
     def empty(self) -> bool:
@@ -117,7 +122,15 @@ class MempoolIndex:
             self.min_ptime = int(ptime)
         return None
 
-    def _confirm(self, tx_keys: List[bytes], in_keys: List[bytes]) -> Tuple[List[bytes], List[bytes]]:
+    def set_seq(self, tx_hash: str, inputs: List[Tuple[str, int]], seq: int):
+        """Record the journal sequence of an admission's batch (caller holds ``lock``)."""
+        self.seq[bytes.fromhex(tx_hash)] = int(seq)
+        for a, i in inputs:
+            self.spent_seq[outpoint_key(a, i)] = int(seq)
+
+    def _confirm(self, tx_keys: List[bytes], in_keys: List[bytes], after: Optional[int] = None):
+        """Remove confirmed txs and outpoints; returns (hit_tx, hit_in, late_tx, late_in) where the late
+        lists hold the hits whose admission was journaled after sequence ``after``."""
         with self.lock:
             hit_tx = []
             if self.txs:
@@ -129,18 +142,25 @@ class MempoolIndex:
             if self.spent and in_keys:
                 hit_in = list(self.spent.intersection(in_keys))
                 self.spent.difference_update(hit_in)
+            late_tx, late_in = [], []
+            if hit_tx:
+                sq = self.seq.pop
+                late_tx = [k for k in hit_tx if sq(k, 0) > (after or 0)] if after is not None else []
+            if hit_in:
+                sq = self.spent_seq.pop
+                late_in = [k for k in hit_in if sq(k, 0) > (after or 0)] if after is not None else []
             if not self.txs:
                 self.min_ptime = None
-            return hit_tx, hit_in
+            return hit_tx, hit_in, late_tx, late_in
 
-    def confirm_raw(self, txids: np.ndarray, in_keys: np.ndarray) -> Tuple[List[bytes], List[bytes]]:
+    def confirm_raw(self, txids: np.ndarray, in_keys: np.ndarray, after: Optional[int] = None):
         """A committed block's txs (n x 32) and spent outpoints (n x >=36 records) leave the mempool;
-        returns the raw tx hashes and outpoints that were in it."""
+        returns the raw tx hashes and outpoints that were in it (and those admitted after ``after``)."""
         return self._confirm(_rows_raw(txids, 32) if len(txids) else [],
-                             _rows_raw(in_keys, 36) if len(in_keys) else [])
+                             _rows_raw(in_keys, 36) if len(in_keys) else [], after)
 
-    def confirm(self, tx_hashes: List[str], inputs: List[Tuple[str, int]]) -> Tuple[List[bytes], List[bytes]]:
-        return self._confirm([bytes.fromhex(h) for h in tx_hashes], [outpoint_key(h, i) for h, i in inputs])
+    def confirm(self, tx_hashes: List[str], inputs: List[Tuple[str, int]], after: Optional[int] = None):
+        return self._confirm([bytes.fromhex(h) for h in tx_hashes], [outpoint_key(h, i) for h, i in inputs], after)
 
     def maybe_stale(self, now: int, delta: int) -> bool:
         """Could a pending tx be older than ``delta`` seconds? ``min_ptime`` only moves down between

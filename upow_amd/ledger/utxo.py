@@ -344,9 +344,13 @@ class UtxoIndex:
         if not len(recs):
             return np.zeros(0, dtype=np.uint8)
         idx = recs[:, 32:36].copy().view(np.uint32).ravel()
-        tag = int(recs[0, 36:40].copy().view(np.uint32)[0])  # one tag filter per batch
-        return self.be.erase([(bytes(recs[n, :32]).hex(), int(idx[n])) for n in range(len(recs))],
-                             None if tag == MISSING else tag)
+        tags = recs[:, 36:40].copy().view(np.uint32).ravel()
+        keys = [(bytes(recs[n, :32]).hex(), int(idx[n])) for n in range(len(recs))]
+        out = np.zeros(len(recs), dtype=np.uint8)
+        for tag in np.unique(tags).tolist():  # per-record tag filter, like the HBM erase kernel
+            sel = np.nonzero(tags == tag)[0]
+            out[sel] = self.be.erase([keys[k] for k in sel.tolist()], None if tag == MISSING else int(tag))
+        return out
 
     @_locked
     def probe(self, keys: Sequence[Outpoint]) -> np.ndarray:

@@ -884,6 +884,7 @@ async def metrics_endpoint():
     metrics.set_gauge('upow_mempool_size', db._q1('SELECT COUNT(*) FROM pending_transactions')[0],
                       help='pending transactions')
     metrics.set_gauge('upow_chain_height', db._tip_id(), help='id of the last applied block')
+    db.publish_writer_metrics()
     return PlainTextResponse(metrics.prometheus_text(), media_type='text/plain; version=0.0.4')
 
 
