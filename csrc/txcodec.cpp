@@ -11,9 +11,11 @@
 //       -> txid = SHA-256(canonical bytes), signed-message digest = SHA-256(hex(False) bytes)
 //       -> address strings (base58 / hex), outputs JSON columns, merkle root
 //
-// A tx the fast path does not cover (coinbase specifier, grouped signatures that need ledger public
-// keys, amounts wider than 64 bits, governance output types, malformed encodings, ...) is flagged;
-// the caller then runs the general Python path for the whole block, which reproduces the
+// Governance transactions decode like any other: their output types and the tx type carried in the
+// message (helpers.py:97-112, ASCII digits) come out as columns, and the block path checks their rules
+// in batch (upow_amd/ledger/govcheck.py). A tx the fast path does not cover (coinbase specifier,
+// grouped signatures that need ledger public keys, amounts wider than 64 bits, malformed encodings, ...)
+// is flagged; the caller then runs the general Python path for the whole block, which reproduces the
 // reference's exact behaviour and error messages.
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -60,6 +62,7 @@ struct DecTx {
     bool canonical = false;
     bool upper_hex = false;  // the input used A-F digits (the stored hex must be re-rendered)
     int32_t msg_off = -1, msg_len = 0;  // into canon bytes
+    uint8_t tx_type = 0;                // TransactionType from the message; kTypeAsk: Python decides
     int32_t signed_len = 0;             // hex(False) byte length (a prefix of canon)
     std::vector<DecIn> ins;
     std::vector<DecOut> outs;
@@ -143,6 +146,46 @@ static bool hex_ambiguous(const std::string& s) {
     return true;
 }
 
+constexpr uint8_t kTypeAsk = 255;
+
+// get_transaction_type_from_message (helpers.py:97-112): int(message.decode()) looked up among the
+// TransactionType values 4-9, REGULAR otherwise. Decided here for the unambiguous encodings: all ASCII
+// digits (leading zeros allowed), or ASCII without any digit (int() fails). A message that is not valid
+// UTF-8 is rendered as hex first, whose integer value is never 4-9 (a byte >= 0x80 contributes an 8x/9x
+// digit pair or an a-f digit). Anything else (signs, whitespace, underscores, non-ASCII digits...) is left
+// to Python's int().
+static uint8_t message_tx_type(const uint8_t* m, size_t n) {
+    bool ascii = true, digits = n > 0, any_digit = false;
+    for (size_t i = 0; i < n; ++i) {
+        ascii &= m[i] < 0x80;
+        const bool d = m[i] >= '0' && m[i] <= '9';
+        digits &= d;
+        any_digit |= d;
+    }
+    if (!ascii) {
+        // valid UTF-8 with non-ASCII characters may hold Unicode digits: ask Python
+        size_t i = 0;
+        while (i < n) {
+            const uint8_t c = m[i];
+            const int len = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
+            if (!len || i + size_t(len) > n) return 0;  // invalid UTF-8 -> hex rendering -> REGULAR
+            for (int k = 1; k < len; ++k)
+                if ((m[i + size_t(k)] >> 6) != 2) return 0;
+            i += size_t(len);
+        }
+        return kTypeAsk;
+    }
+    if (digits) {
+        uint32_t v = 0;
+        for (size_t i = 0; i < n; ++i) {
+            v = v * 10 + uint32_t(m[i] - '0');
+            if (v > 1000) return 0;
+        }
+        return (v >= 4 && v <= 9) ? uint8_t(v) : 0;
+    }
+    return any_digit ? kTypeAsk : 0;
+}
+
 static void decode_one(const char* hx, size_t hlen, DecTx& t) {
     t = DecTx();
     if (hlen % 2) return;
@@ -193,7 +236,6 @@ static void decode_one(const char* hx, size_t hlen, DecTx& t) {
         p += size_t(amount_len);
         o.type = b[p++];
         if (o.type > 9 || o.type == 4) return;  // OutputType(..) raises (values 0-3, 5-9)
-        if (o.type != 0) general = true;         // governance / stake outputs: general path
     }
     if (!need(1)) return;
     const uint8_t spec = b[p++];
@@ -213,6 +255,7 @@ static void decode_one(const char* hx, size_t hlen, DecTx& t) {
         msg = &b[p];
         p += mlen;
         has_msg = true;
+        t.tx_type = message_tx_type(msg, mlen);
     } else if (spec != 0) {
         return;  // AssertionError in the parser
     }
@@ -393,7 +436,7 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
     }
     auto t1 = std::chrono::steady_clock::now();
     py::dict d;
-    std::vector<uint8_t> flags(N), version(N);
+    std::vector<uint8_t> flags(N), version(N), tx_type(N);
     std::vector<int32_t> in_start(N + 1), out_start(N + 1), sig_start(N + 1), signed_len(N), msg_off(N), msg_len(N),
         hex_len(N);
     int64_t n_in = 0, n_out = 0, n_sig = 0;
@@ -403,6 +446,7 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
         flags[size_t(i)] = t.flag;
         all_fast &= t.flag == TX_FAST;
         version[size_t(i)] = t.version;
+        tx_type[size_t(i)] = t.tx_type;
         in_start[size_t(i)] = int32_t(n_in);
         out_start[size_t(i)] = int32_t(n_out);
         sig_start[size_t(i)] = int32_t(n_sig);
@@ -424,6 +468,7 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
     d["all_fast"] = all_fast;
     d["flags"] = as_bytes(flags);
     d["version"] = as_bytes(version);
+    d["tx_type"] = as_bytes(tx_type);
     d["in_start"] = i32(in_start);
     d["out_start"] = i32(out_start);
     d["sig_start"] = i32(sig_start);

@@ -241,14 +241,17 @@ def test_signer_records_native_matches_general():
         assert st == -1
 
 
-def test_governance_block_takes_object_path():
+def test_stake_block_takes_native_path():
+    """A stake tx (STAKE + DELEGATE_VOTING_POWER outputs) decodes natively and its block applies on the
+    native path with the object path's ledger (tests/test_fastpath_governance.py has the full lifecycle)."""
     async def go():
         p, base = await _setup()
         p.use(p.a)
         st = await create_stake_transaction(GENESIS, '1')
-        assert fastpath.decode([st.hex()]) is None
+        assert fastpath.decode([st.hex()]) is not None
         c = await p.mine([st], ts=base + 600)
         await p.push(c, [st], expect=True)
+        assert fastpath.last_path == 'native'
     asyncio.run(go())
 
 

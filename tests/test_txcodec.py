@@ -107,12 +107,39 @@ def test_general_and_malformed_flags(L):
     gov.inputs[0].signed = (1, 2)
     grouped = _tx(rng, n_in=3, one_sig=False)
     gh = grouped.hex()[:-128]  # 2 signatures for 3 inputs -> assignment by public key
-    cases = {'coinbase': coinbase_like, 'stake output': gov.hex(), 'grouped sigs': gh,
+    cases = {'coinbase': coinbase_like, 'grouped sigs': gh,
              'odd hex': 'abc', 'bad char': 'zz' + _tx(rng).hex()[2:], 'version 4': '04' + _tx(rng).hex()[2:],
              'truncated': _tx(rng).hex()[:100]}
     d = L.decode_block_txs(list(cases.values()), 2)
     assert not d['all_fast']
     assert all(f != 0 for f in d['flags']), dict(zip(cases, d['flags']))
+    # governance outputs decode natively: the output-type column carries them
+    d = L.decode_block_txs([gov.hex()], 1)
+    assert d['all_fast'] and list(d['out_type']) == [int(OutputType.STAKE)] and list(d['tx_type']) == [0]
+
+
+_MESSAGES = [b'5', b'05', b'0005', b'4', b'9', b'10', b'3', b'0', b'', b' 5', b'5 ', b'+5', b'-5', b'5_0', b'1_0',
+             '\u0665'.encode(), '\uff15'.encode(), b'\xff5', b'\x80\x05', b'abc', b'hello 7', b'7\n', b'\t6',
+             b'99999999999999999999', b'00000000000000000007', b'\xc3\xa9', b'\xe2\x80', b'8']
+
+
+@settings(max_examples=200, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(st.one_of(st.sampled_from(_MESSAGES), st.binary(min_size=0, max_size=6),
+                 st.text(alphabet='0123456789 +-_\u0665\u0e55a', max_size=5).map(lambda t: t.encode())))
+def test_message_tx_type_matches_python(native, msg):
+    """The codec's tx type (helpers.py:97-112 get_transaction_type_from_message) equals Python's whenever it
+    decides (255 = left to Python's int())."""
+    from upow_amd.utils.codec import get_transaction_type_from_message
+    rng = random.Random(len(msg))
+    tx = _tx(rng, n_in=1, n_out=1, one_sig=True)
+    tx.message = msg
+    tx.transaction_type = get_transaction_type_from_message(msg)
+    h = tx.hex()
+    d = native.decode_block_txs([h], 1)
+    assert d['all_fast']
+    t = d['tx_type'][0]
+    if t != 255:
+        assert t == int(get_transaction_type_from_message(msg)), (msg, t)
 
 
 @settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.too_slow])

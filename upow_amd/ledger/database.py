@@ -268,6 +268,26 @@ _FK_PARENTS['transactions'] = ('blocks',)
 _SQL_TABLES: Dict[Tuple[str, bool], Optional[frozenset]] = {}
 
 
+def _arena_reader(spec):
+    """Row accessor of an ('arena', blob, int64 offsets) text column: row o -> str."""
+    _, blob, off = spec
+    off = np.frombuffer(off, dtype=np.int64) if isinstance(off, (bytes, bytearray)) else np.asarray(off, np.int64)
+    mv = memoryview(blob)
+    return lambda o: str(mv[int(off[o]):int(off[o + 1])], 'ascii')
+
+
+def _arena_subset(spec, sel: np.ndarray):
+    """('arena', blob, int64 offsets[n + 1]) restricted to the rows ``sel`` (vectorised byte gather)."""
+    _, blob, off = spec
+    off = np.frombuffer(off, dtype=np.int64) if isinstance(off, (bytes, bytearray)) else np.asarray(off, np.int64)
+    data = np.frombuffer(blob, dtype=np.uint8)
+    starts, lens = off[sel], off[sel + 1] - off[sel]
+    new_off = np.zeros(len(sel) + 1, dtype=np.int64)
+    np.cumsum(lens, out=new_off[1:])
+    idx = np.repeat(starts - new_off[:-1], lens) + np.arange(int(new_off[-1]), dtype=np.int64)
+    return ('arena', data[idx].tobytes(), new_off)
+
+
 def _tables_of(sql: str, write: bool) -> Optional[frozenset]:
     """Ledger tables a statement reads (or writes, with their FK parents); None = all of them
     (a DELETE/UPDATE on blocks or transactions cascades through the output tables)."""
@@ -1566,7 +1586,8 @@ class Database:
         return self._pending_empty
 
     def apply_native_block(self, block_row: dict, coinbase_row: tuple, coinbase_outputs: list, n: int,
-                           tx_cols: list, out_cols: tuple, in_keys: np.ndarray, spent_payload: np.ndarray) -> int:
+                           tx_cols: list, out_cols: tuple, in_keys: np.ndarray, spent_payload: np.ndarray,
+                           gov: Optional[dict] = None) -> int:
         """The ledger writes of one native-path block (reference manager.py:706-730: add_block,
         add_transaction(coinbase), add_transactions, add_transaction_outputs, remove_pending_transactions,
         remove_outputs, remove_pending_spent_outputs) as ONE journal batch, plus the HBM index update.
@@ -1575,18 +1596,26 @@ class Database:
         outputs_addresses, outputs_amounts, fees); ``out_cols``: (index int64, address text spec,
         txids n x 32, amounts u64, raw addresses n x 64, address lengths) of the REGULAR outputs;
         ``in_keys``: n x 40 spent outpoint records; ``spent_payload``: their index payloads (undo data).
+        ``gov`` (blocks with governance txs, ledger/govcheck.py): per-output ``out_tag``/``out_type``, per-input
+        ``in_tag`` (the table each input is spent from), ``out_tx``, ``gov_tx`` and the inputs_addresses arena:
+        outputs land in their tables (stake flag from the output type), spends leave theirs, and the
+        governance index follows from these columns — the object path's write set (apply_object_block) in
+        the same statement order, so both paths leave identical tables.
         Returns the journal sequence number (0 without the native writer: written synchronously)."""
         out_index, out_addr_spec, out_txid, out_amount, out_addr, out_len = out_cols
         n_out, n_in = len(out_index), len(in_keys)
         tag_u = TAG_BY_TABLE['unspent_outputs']
+        out_tag = gov['out_tag'] if gov is not None else np.full(n_out, tag_u, dtype=np.uint32)
         # ---- index records: created outputs (block txs + coinbase) and spent inputs
         recs = np.zeros((n_out, 40), dtype=np.uint8)
         recs[:, :32] = out_txid
         recs[:, 32:36] = out_index.astype(np.uint32).reshape(-1, 1).view(np.uint8)
-        recs[:, 36:40] = np.full((n_out, 1), tag_u, dtype=np.uint32).view(np.uint8)
+        recs[:, 36:40] = np.ascontiguousarray(out_tag, dtype=np.uint32).reshape(-1, 1).view(np.uint8)
         pay = np.zeros(n_out, dtype=PAYLOAD_DTYPE)
         pay['amount'] = out_amount
         pay['len'] = out_len
+        if gov is not None:
+            pay['flags'] = np.where(gov['out_type'] == int(OutputType.STAKE), FLAG_STAKE, 0).astype(np.uint32)
         a = np.array(out_addr, dtype=np.uint8, copy=True)
         c33 = out_len == 33
         a[c33, 0] = np.where(a[c33, 0] == 43, 43, 42)  # bytes_to_string normalises the prefix
@@ -1598,7 +1627,8 @@ class Database:
                               [bool(o[3]) for o in coinbase_outputs])
         in_keys = np.ascontiguousarray(in_keys, dtype=np.uint8).reshape(-1, 40)
         spent = np.array(in_keys, dtype=np.uint8, copy=True)
-        spent[:, 36:40] = np.full((n_in, 1), tag_u, dtype=np.uint32).view(np.uint8)
+        in_tag = gov['in_tag'].astype(np.uint32) if gov is not None else np.full(n_in, tag_u, dtype=np.uint32)
+        spent[:, 36:40] = np.ascontiguousarray(in_tag).reshape(-1, 1).view(np.uint8)
         in_idx = in_keys[:, 32:36].copy().view(np.uint32).ravel().astype(np.int64)
         in_order = self._key_order(in_keys) if n_in else None
 
@@ -1618,12 +1648,23 @@ class Database:
         self.checkpoint('transactions')
         # explicit row ids from the ledger-wide counter: the rows land in two files (see UTXO_SCHEMAS)
         ins_u = 'INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake, rowid) VALUES (?, ?, ?, ?, ?)'
-        if n_out:
-            base = self._utxo_rowids(n_out)
-            stmts.append((ins_u, [('hex32', np.ascontiguousarray(out_txid), 32, 0),
-                                  np.ascontiguousarray(out_index, dtype=np.int64), out_addr_spec, 0,
-                                  np.arange(base, base + n_out, dtype=np.int64)],
-                          n_out, None, None, None))
+        if gov is None:
+            if n_out:
+                base = self._utxo_rowids(n_out)
+                stmts.append((ins_u, [('hex32', np.ascontiguousarray(out_txid), 32, 0),
+                                      np.ascontiguousarray(out_index, dtype=np.int64), out_addr_spec, 0,
+                                      np.arange(base, base + n_out, dtype=np.int64)],
+                              n_out, None, None, None))
+        else:
+            sel = np.nonzero(out_tag == tag_u)[0]
+            if len(sel):
+                base = self._utxo_rowids(len(sel))
+                stake = (gov['out_type'][sel] == int(OutputType.STAKE)).astype(np.int64)
+                stmts.append((ins_u, [('hex32', np.ascontiguousarray(out_txid[sel]), 32, 0),
+                                      np.ascontiguousarray(out_index[sel], dtype=np.int64),
+                                      _arena_subset(out_addr_spec, sel), stake,
+                                      np.arange(base, base + len(sel), dtype=np.int64)],
+                              len(sel), None, None, None))
         if coinbase_outputs:
             base = self._utxo_rowids(len(coinbase_outputs))
             stmts.append((ins_u, [[o[0] for o in coinbase_outputs], np.array([o[1] for o in coinbase_outputs], np.int64),
@@ -1631,16 +1672,52 @@ class Database:
                                   [None if o[3] is None else str(int(bool(o[3]))) for o in coinbase_outputs],
                                   np.arange(base, base + len(coinbase_outputs), dtype=np.int64)],
                           len(coinbase_outputs), None, None, None))
-        self.checkpoint('outputs')
         tables = {'blocks', 'transactions', 'unspent_outputs'}
+        gov_created, gov_spent = {}, {}
+        if gov is not None:
+            addr_at = _arena_reader(out_addr_spec)
+            for table in self._GOV_INSERT_ORDER:
+                sel = np.nonzero(out_tag == TAG_BY_TABLE[table])[0]
+                if len(sel):
+                    rows = [(bytes(out_txid[o]).hex(), int(out_index[o]), addr_at(o)) for o in sel.tolist()]
+                    gov_created[table] = (sel, rows)
+                    stmts.append((f'INSERT INTO {table} (tx_hash, "index", address) VALUES (?, ?, ?)',
+                                  [[r[0] for r in rows], np.array([r[1] for r in rows], np.int64), [r[2] for r in rows]],
+                                  len(rows), None, None, None))
+                    tables.add(table)
+            for table in self._SPEND_ORDER:
+                if table == 'unspent_outputs':
+                    continue
+                sel = np.nonzero(in_tag == TAG_BY_TABLE[table])[0]
+                if len(sel):
+                    gov_spent[table] = [(bytes(in_keys[j, :32]).hex(), int(in_idx[j])) for j in sel.tolist()]
+                    tables.add(table)
+        self.checkpoint('outputs')
         mempool = n and not self._mempool_empty()
         if mempool:
             txids = np.ascontiguousarray(tx_cols[0][1], dtype=np.uint8).reshape(-1, 32)
             stmts.append(('DELETE FROM pending_transactions WHERE tx_hash = ?', [('hex32', txids, 32, 0)], n,
                           self._key_order(txids), 'SELECT EXISTS(SELECT 1 FROM pending_transactions)', None))
-        if n_in:
+
+        def spend_stmt(table):
+            keys = gov_spent[table]
+            stmts.append((f'DELETE FROM {table} WHERE tx_hash = ? AND "index" = ?',
+                          [[h for h, _ in keys], np.array([i for _, i in keys], np.int64)], len(keys), None, None,
+                          len(keys)))
+        if 'inode_registration_output' in gov_spent:
+            spend_stmt('inode_registration_output')
+        sel_u = np.nonzero(in_tag == tag_u)[0] if gov is not None else None
+        if gov is None and n_in:
             stmts.append(('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
                           [('hex32', in_keys, 40, 0), in_idx], n_in, in_order, None, n_in))
+        elif gov is not None and len(sel_u):
+            ku = np.ascontiguousarray(in_keys[sel_u])
+            stmts.append(('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
+                          [('hex32', ku, 40, 0), np.ascontiguousarray(in_idx[sel_u])], len(sel_u),
+                          self._key_order(ku), None, len(sel_u)))
+        for table in self._SPEND_ORDER[2:]:
+            if table in gov_spent:
+                spend_stmt(table)
         if mempool and n_in:
             stmts.append(('DELETE FROM pending_spent_outputs WHERE tx_hash = ? AND "index" = ?',
                           [('hex32', in_keys, 40, 0), in_idx], n_in, in_order,
@@ -1686,7 +1763,43 @@ class Database:
             hit = self._stake_spent(spent)
             if hit:
                 self.gov.removed(STAKE, hit)
+        if self.gov is not None and gov is not None:
+            self._gov_apply_native(gov, gov_created, gov_spent, out_txid, out_index, out_amount, out_addr_spec,
+                                   int(b['timestamp']))
         return seq
+
+    def _gov_apply_native(self, gov: dict, created: dict, spent: dict, out_txid, out_index, out_amount, out_addr_spec,
+                          block_ts: int):
+        """Governance-index update of a native-path block from its own columns (no SQL read-back): the rows
+        GovernanceIndex.added would read through the reference's joins — address, amount
+        (outputs_amounts[index]), voter (inputs_addresses[index], the reference's subscript) and the block
+        timestamp — for the created governance/stake outputs; spent governance rows leave their tables."""
+        g = self.gov
+        ia_blob, ia_off = gov['in_json']
+        ia_off = np.frombuffer(ia_off, dtype=np.int64) if isinstance(ia_off, (bytes, bytearray)) else ia_off
+        ia_cache = {}
+        out_tx = gov['out_tx']
+
+        def voter(o):
+            k = int(out_tx[o])
+            lst = ia_cache.get(k)
+            if lst is None:
+                lst = ia_cache[k] = json.loads(bytes(ia_blob[int(ia_off[k]):int(ia_off[k + 1])]))
+            return _at(lst, int(out_index[o]))
+        stake_sel = np.nonzero(gov['out_type'] == int(OutputType.STAKE))[0]
+        addr_at = _arena_reader(out_addr_spec)
+        with g.lock:
+            for table, keys in spent.items():
+                g.removed(table, keys)
+            for o in stake_sel.tolist():
+                g.tables[STAKE].add((bytes(out_txid[o]).hex(), int(out_index[o])), addr_at(o), int(out_amount[o]),
+                                    voter(o), block_ts)
+            for table in self._GOV_INSERT_ORDER:
+                if table in created:
+                    sel, rows = created[table]
+                    for o, r in zip(sel.tolist(), rows):
+                        g.tables[table].add((r[0], r[1]), r[2], int(out_amount[o]), voter(o), block_ts)
+            g.version += 1
 
     def _stake_spent(self, spent: np.ndarray) -> List[Tuple[str, int]]:
         """Which of a block's spent outpoints (n x 40 records) are staked outputs: one vectorised

@@ -15,10 +15,13 @@ same checks over whole-block arrays:
      (csrc/ledger_writer.cpp: the journal append is the commit point, a background thread on its own
      SQLite connection materialises the tables) + one index insert launch + one erase launch.
 
-Scope: blocks whose txs are all REGULAR (no governance message type, only REGULAR outputs, 1-or-n
-signatures). Anything else, and ANY failed check, hands the block to the object path
-(``manager._create_block``), which then reproduces the reference's exact verdict, error message or
-exception. The fast path only ever answers "valid" itself, so it can cost time but not semantics;
+Scope: every tx type. Governance transactions (stake/unstake outputs, inode and validator registration,
+votes, revokes) ride the same arrays: each input is looked up in the table its tx type spends from, their
+rules run in batch against the governance index (ledger/govcheck.py), revokes are verified against the
+voter's key, and their outputs and spends are journaled into the governance tables in the same batch.
+Txs whose signatures must be grouped by ledger public keys, and ANY failed check, hand the block to the
+object path (``manager._create_block``), which then reproduces the reference's exact verdict, error
+message or exception. The fast path only ever answers "valid" itself, so it can cost time but not semantics;
 ``tests/test_fastpath.py`` runs both paths over the same blocks and compares the whole ledger.
 """
 from __future__ import annotations
@@ -38,6 +41,7 @@ from ..ops.native import gpu_available, lib
 from ..utils import metrics
 from ..utils.codec import TransactionType, get_transaction_type_from_message
 from ..utils.logger import get_logger
+from .govcheck import BlockGovernance
 from .utxo import TAG_BY_TABLE
 
 logger = get_logger(__name__)
@@ -69,12 +73,16 @@ def decode(tx_hexes: List[str]) -> Optional[dict]:
     d = lib().decode_block_txs(list(tx_hexes), THREADS)
     if not d['all_fast']:
         return None
-    msg_off, msg_len = _i32(d, 'msg_off'), _i32(d, 'msg_len')
-    for k in np.nonzero(msg_off >= 0)[0]:
-        h = d['hex'][k]
-        msg = bytes.fromhex(h[2 * msg_off[k]:2 * (msg_off[k] + msg_len[k])])
-        if get_transaction_type_from_message(msg) != TransactionType.REGULAR:
-            return None
+    # tx types from the messages: decided natively except for encodings only Python's int() can judge
+    tx_type = np.frombuffer(d['tx_type'], dtype=np.uint8).copy()
+    ask = np.nonzero(tx_type == 255)[0]
+    if len(ask):
+        msg_off, msg_len = _i32(d, 'msg_off'), _i32(d, 'msg_len')
+        for k in ask.tolist():
+            h = d['hex'][k]
+            msg = bytes.fromhex(h[2 * msg_off[k]:2 * (msg_off[k] + msg_len[k])])
+            tx_type[k] = int(get_transaction_type_from_message(msg))
+    d['_tx_type'] = tx_type
     return d
 
 
@@ -200,35 +208,63 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     n_in = len(in_keys)
     in_start, out_start = _i32(d, 'in_start'), _i32(d, 'out_start')
     out_amount = np.frombuffer(d['out_amount'], dtype=np.uint64)
+    in_tx, out_tx = _i32(d, 'in_tx'), _i32(d, 'out_tx')
+    out_type = np.frombuffer(d['out_type'], dtype=np.uint8)
+    bg = BlockGovernance(d['_tx_type'], out_type, out_tx, out_start, in_tx)
     tags, pay, dup_of, fee, missing, n_dup = database.utxo.block_inputs(
         in_keys, in_start, out_amount, out_start, TAG_BY_TABLE['unspent_outputs'])
-    if n_dup or np.any(missing):
+    if n_dup:
+        return None
+    in_tag = None
+    if bg.any:
+        # each input must be live in the table its tx type spends from (manager.py:531-543)
+        in_tag = bg.spend_tags(TAG_BY_TABLE)
+        bad = (tags != in_tag) | (pay['len'] == 0)
+        if bad.any():
+            return None
+        fee = bg.fee_adjust(fee, out_amount)
+    elif np.any(missing):
         return None
     in_amount = pay['amount']
     if (n_in and in_amount.max() >= AMOUNT_LIMIT) or (len(out_amount) and out_amount.max() >= AMOUNT_LIMIT):
         return None
     t2 = perf_counter()
 
+    txid = np.frombuffer(d['txid'], dtype=np.uint8).reshape(-1, 32)
+    out_len = np.frombuffer(d['out_len'], dtype=np.uint8)
+    out_addr = np.frombuffer(d['out_addr'], dtype=np.uint8).reshape(-1, 64)
+    sig_pay = pay
+    if bg.any:
+        # governance rules against the pre-block state (ledger/govcheck.py); revokes are signed by voters
+        gres = await bg.check(database, in_start, out_amount, out_addr, out_len, in_keys, pay, txid)
+        if gres is None:
+            return None
+        if gres['signers']:
+            sig_pay = pay.copy()
+            for j, raw in gres['signers'].items():
+                sig_pay['addr'][j] = 0
+                sig_pay['addr'][j, :len(raw)] = np.frombuffer(raw, dtype=np.uint8)
+                sig_pay['len'][j] = len(raw)
+    t_gov = perf_counter()
+
     # ---- keys + verify records: every distinct 33-byte key (signers + outputs) decompressed in one
     #      batch, then the 160-byte records of the signature jobs, in one native call
     #      (csrc/txcodec.cpp block_signer_records); blocks with 64-byte addresses take the numpy path
     in_sig = _i32(d, 'in_sig')
     sig_ids, job_input = np.unique(in_sig, return_index=True)  # first input per distinct signature
-    out_len = np.frombuffer(d['out_len'], dtype=np.uint8)
-    out_addr = np.frombuffer(d['out_addr'], dtype=np.uint8).reshape(-1, 64)
     sigs = np.frombuffer(d['sigs'], dtype=np.uint8).reshape(-1, 64)
     digest = np.frombuffer(d['digest'], dtype=np.uint8).reshape(-1, 32)
-    in_tx = _i32(d, 'in_tx')
     job_tx = in_tx[job_input]
     n_jobs = len(job_input)
     gpu_min = op.GPU_MIN_BATCH if gpu_available() else 1 << 62
     kst, rec_bytes = lib().block_signer_records(
-        np.ascontiguousarray(pay['addr']), pay['len'].astype(np.uint8), out_addr, out_len,
+        np.ascontiguousarray(sig_pay['addr']), sig_pay['len'].astype(np.uint8), out_addr, out_len,
         job_input.astype(np.int64), sigs, sig_ids.astype(np.int64), digest, job_tx.astype(np.int64), gpu_min)
     if kst == 0:  # a signer key or an output address is off-curve: the object path decides
         return None
     if kst < 0:
-        rec_bytes = _signer_records_general(pay, out_addr, out_len, job_input, sigs, sig_ids, digest, job_tx, gpu_min)
+        rec_bytes = _signer_records_general(sig_pay, out_addr, out_len, job_input, sigs, sig_ids, digest, job_tx,
+                                            gpu_min)
         if rec_bytes is None:
             return None
     recs = np.frombuffer(rec_bytes, dtype=np.uint8).reshape(-1, 160)
@@ -251,12 +287,12 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         return None
     t4 = perf_counter()
 
-    # ---- fees (REGULAR txs: every output counts; computed by the device pass above)
+    # ---- fees (REGULAR txs; voting-power outputs excluded, governance txs carry none)
     if np.any(fee < 0):
         return None
     fees_total = Decimal(int(fee.sum())) / SMALLEST
-    validate.timings.update({'decompress_s': t3 - t2, 'collect_s': 0.0, 'ecdsa_s': t4 - t3, 'rules_s': 0.0,
-                             'signatures': n_jobs, 'txs': n})
+    validate.timings.update({'decompress_s': t3 - t_gov, 'collect_s': 0.0, 'ecdsa_s': t4 - t3,
+                             'rules_s': t_gov - t2, 'signatures': n_jobs, 'txs': n})
     metrics.inc('upow_signatures_verified_total', n_jobs, help='P-256 signatures verified in block validation')
     manager.last_block_timings.update({'utxo_s': t2 - t1, 'verify_s': t4 - t2, 'merkle_s': 0.0,
                                        'total_s': t4 - t0, 'txs': n})
@@ -267,9 +303,11 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     in_json = L.input_address_strings(np.ascontiguousarray(pay['addr']).tobytes(),
                                       pay['len'].astype(np.uint8).tobytes(), d['in_start'], THREADS)
     fee_str = L.fee_strings(np.ascontiguousarray(fee, dtype=np.int64).tobytes())
-    out_tx = _i32(d, 'out_tx')
     out_index = np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]
-    txid = np.frombuffer(d['txid'], dtype=np.uint8).reshape(-1, 32)
+    gov_cols = None
+    if bg.any:
+        gov_cols = {'out_tag': bg.output_tags(TAG_BY_TABLE), 'out_type': out_type, 'in_tag': in_tag,
+                    'gov_tx': bg.gov, 'out_tx': out_tx, 'in_json': in_json}
 
     async def apply(block_hash, address, random, block_reward, content_time, coinbase_transaction):
         ta = perf_counter()
@@ -284,7 +322,8 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         out_cols = (out_index, ('arena', *d['out_addr_str']), txid[out_tx], out_amount, out_addr, out_len)
         submitted = database._submitted
         try:
-            seq = database.apply_native_block(block_row, cb_row, cb_outputs, n, tx_cols, out_cols, in_keys, pay)
+            seq = database.apply_native_block(block_row, cb_row, cb_outputs, n, tx_cols, out_cols, in_keys, pay,
+                                              gov=gov_cols)
         except Exception as e:
             if database._submitted != submitted:
                 raise  # committed to the journal: a failure after the commit point is not a rejection

@@ -53,14 +53,50 @@ def _at(arr, i):
     return arr[i] if arr is not None and 0 <= i < len(arr) else None
 
 
+def point_key(raw: bytes) -> Optional[bytes]:
+    """The point an address denotes, as its normalised 33-byte compressed encoding — without a square
+    root: a 33-byte address keeps x with prefix 43 (odd y) or 42, a 64-byte one (x LE || y LE) takes the
+    parity of y. Two address strings are in each other's ``address_forms`` exactly when their keys match."""
+    if len(raw) == 33:
+        return bytes([43 if raw[0] == 43 else 42]) + bytes(raw[1:])
+    if len(raw) == 64:
+        return bytes([43 if raw[32] & 1 else 42]) + bytes(raw[:32])
+    return None
+
+
+_PT: Dict[str, Optional[bytes]] = {}
+
+
+def point_key_of(address: Optional[str]) -> Optional[bytes]:
+    """point_key of an address string (string_to_bytes semantics: hex first, then base58), memoised."""
+    if address is None:
+        return None
+    hit = _PT.get(address, b'')
+    if hit != b'':
+        return hit
+    from ..utils.codec import string_to_bytes
+    try:
+        hit = point_key(string_to_bytes(address))
+    except Exception:
+        hit = None
+    if len(_PT) > (1 << 20):
+        _PT.clear()
+    _PT[address] = hit
+    return hit
+
+
 class _Table:
-    __slots__ = ('rows', 'seq', 'by_addr', 'by_voter', 'next_seq')
+    __slots__ = ('rows', 'seq', 'by_addr', 'by_voter', 'by_pt', 'by_voter_pt', 'next_seq')
 
     def __init__(self):
         self.rows: Dict[Key, tuple] = {}  # key -> (address, amount, voter, ts); insertion (rowid) order
         self.seq: Dict[Key, int] = {}  # key -> insertion sequence (sort key for rowid order)
         self.by_addr: Dict[Optional[str], Dict[Key, None]] = {}
         self.by_voter: Dict[Optional[str], Dict[Key, None]] = {}
+        # by the point the address denotes (both string forms at once): the native block path's
+        # governance checks ask "is this key registered / staked / voting" with raw address bytes
+        self.by_pt: Dict[Optional[bytes], Dict[Key, None]] = {}
+        self.by_voter_pt: Dict[Optional[bytes], Dict[Key, None]] = {}
         self.next_seq = 0
 
     def add(self, key: Key, address, amount, voter, ts):
@@ -71,13 +107,16 @@ class _Table:
         self.next_seq += 1
         self.by_addr.setdefault(address, {})[key] = None
         self.by_voter.setdefault(voter, {})[key] = None
+        self.by_pt.setdefault(point_key_of(address), {})[key] = None
+        self.by_voter_pt.setdefault(point_key_of(voter), {})[key] = None
 
     def remove(self, key: Key) -> bool:
         row = self.rows.pop(key, None)
         if row is None:
             return False
         del self.seq[key]
-        for idx, k in ((self.by_addr, row[0]), (self.by_voter, row[2])):
+        for idx, k in ((self.by_addr, row[0]), (self.by_voter, row[2]), (self.by_pt, point_key_of(row[0])),
+                       (self.by_voter_pt, point_key_of(row[2]))):
             d = idx.get(k)
             if d is not None:
                 d.pop(key, None)
@@ -193,20 +232,40 @@ class GovernanceIndex:
         if self._pending is not None and self._pending[0] == ver:
             return self._pending
         from ..models.transaction import Transaction
+        from ..utils.codec import TransactionType
         spent = {(r[0], r[1]) for r in self.db._q('SELECT tx_hash, "index" FROM pending_spent_outputs')}
         stake: Dict[str, Decimal] = {}
         live = {}
+        votes = 0  # pending VOTE_AS_DELEGATE txs (the unstake rule consults them, transaction.py:474-477)
         for h, tx_hex in self.db._q('SELECT tx_hash, tx_hex FROM pending_transactions ORDER BY rowid'):
-            outs = self._parsed.get(h)
-            if outs is None:
+            hit = self._parsed.get(h)
+            if hit is None:
                 tx = Transaction.parse(tx_hex)[0]
-                outs = [(o.address, o.amount) for o in tx.outputs if o.is_stake is True]
-            live[h] = outs
-            for address, amount in outs:
+                hit = ([(o.address, o.amount) for o in tx.outputs if o.is_stake is True],
+                       getattr(tx, 'transaction_type', None) == TransactionType.VOTE_AS_DELEGATE)
+            live[h] = hit
+            votes += hit[1]
+            for address, amount in hit[0]:
                 stake[address] = stake.get(address, Decimal(0)) + amount
         self._parsed = live
-        self._pending = (ver, spent, stake)
+        self._pending = (ver, spent, stake, votes)
         return self._pending
+
+    @_locked
+    def pending_vote_as_delegate(self) -> int:
+        return self._overlay()[3]
+
+    @_locked
+    def has_point(self, table: str, pt: Optional[bytes], check_pending: bool, voter: bool = False) -> bool:
+        """Is there a live row of ``table`` whose address (``voter``: voter) denotes point ``pt``?"""
+        tab = self.tables[table]
+        keys = (tab.by_voter_pt if voter else tab.by_pt).get(pt)
+        if not keys:
+            return False
+        if not check_pending:
+            return True
+        pend = self.pending_spent(True)
+        return any(k not in pend for k in keys)
 
     @_locked
     def pending_spent(self, check_pending: bool) -> Set[Key]:
