@@ -117,7 +117,8 @@ def _verify_side_metrics(args, ctx) -> dict:
     tmp = tempfile.mkdtemp(prefix='upow_bench_verify_')
     try:
         v = argparse.Namespace(**{**vars(args), 'steps': args.verify_steps, 'warmup': 2, 'ledger': tmp,
-                                  'object_path': False, 'from_mempool': False, 'governance': False})
+                                  'object_path': False, 'from_mempool': False, 'governance': False,
+                                  'governance_txs': 0.0})
         r = run_cluster_verify_bench(v, ctx) if ctx.is_distributed else run_verify_bench(v, ctx)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
@@ -168,9 +169,13 @@ def main(argv=None):
                     help='verify mode: block txs are in the mempool and pushed as hashes (the miner path)')
     ap.add_argument('--governance', action='store_true',
                     help='verify mode: seed 12 inodes, 200 validators, 5,000 delegates with ballots before the blocks')
+    ap.add_argument('--governance-txs', default='0',
+                    help="verify mode: fraction of each block's txs that are governance txs, e.g. 5%% or 0.05")
     ap.add_argument('--verify-steps', type=int, default=10,
                     help='mine mode: timed 2 MB blocks of the tx-verify side measurement (0: skip; GPU only)')
     args = ap.parse_args(argv)
+    g = str(args.governance_txs).strip()
+    args.governance_txs = float(g[:-1]) / 100 if g.endswith('%') else float(g)
 
     # rank launch: the driver either starts N ranks itself (torchrun sets WORLD_SIZE) or runs
     # ``bench.py --gpus N`` plainly, in which case this process becomes the launcher of N ranks

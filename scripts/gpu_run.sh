@@ -9,6 +9,9 @@
 #   verify   bench.py --mode verify --ledger <tmp dir> (file ledger, metric 2)
 #   verifymem bench.py --mode verify (in-memory ledger)
 #   verifygov bench.py --mode verify --governance (file ledger; 12 inodes, 200 validators, 5,000 delegates)
+#   verifygov5 bench.py --mode verify --governance-txs 5% (file ledger; 5 % of every block's txs are governance txs)
+#   cluster  forced single-rank RCCL cluster node, one chain (bench.py --mode verify under torchrun)
+#   launch   bench.py --gpus 1 under torchrun (the driver's multi-rank entry form)
 #   sync     bench.py --mode sync (chain-sync replay of a /get_blocks page, decode-ahead pipeline)
 #   coloc    scripts/colocated.py (node + miner sharing the GPU)
 #   prof     rocprofv3 --kernel-trace --stats over a short bench.py
@@ -43,6 +46,11 @@ for s in $STEPS; do
       timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger \
         > "$OUT/verify_file.json" 2> "$OUT/verify_file.err" || { tail -20 "$OUT/verify_file.err"; exit 1; }
       cat "$OUT/verify_file.json" ;;
+    verifygov5)
+      rm -rf /tmp/upow_bench_ledger
+      timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger --governance-txs 5% \
+        > "$OUT/verify_gov5.json" 2> "$OUT/verify_gov5.err" || { tail -20 "$OUT/verify_gov5.err"; exit 1; }
+      cat "$OUT/verify_gov5.json" ;;
     verifygov)
       rm -rf /tmp/upow_bench_ledger
       timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger --governance \

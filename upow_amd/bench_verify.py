@@ -32,7 +32,10 @@ def _funding_tx(owner_addrs, amount: Decimal, rng):
 
 
 async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None, device=None, base_ts=None,
-                 make_blocks: bool = True, ledger_path: str = None, governance: bool = False):
+                 make_blocks: bool = True, ledger_path: str = None, governance: bool = False, gov_txs: float = 0.0):
+    """``gov_txs`` > 0: that fraction of every block's txs are governance txs (70 % delegate votes, 10 %
+    validator votes, 20 % delegate revokes of seeded ballots, signed by the voters) on a seeded governance
+    state; the chain starts four days back so the seeded ballots are past the 48 h revoke window."""
     from . import devnet
     from .ledger import manager
     from .ledger.database import Database
@@ -44,7 +47,11 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
     manager.Manager.difficulty = None
     keys = [rng.randrange(1, op.oracle.N) for _ in range(256)]
     addrs = [point_to_string(op.public_key(k)) for k in keys]
-    base_ts = base_ts if base_ts is not None else int(time.time()) - 10_000
+    n_gov = int(round(gov_txs * txs_per_block)) if gov_txs > 0 else 0
+    n_dv, n_vv = int(n_gov * 0.7), int(n_gov * 0.1)
+    n_rv = n_gov - n_dv - n_vv
+    if base_ts is None:
+        base_ts = int(time.time()) - (4 * 86_400 if n_gov else 10_000)
     genesis_addr = addrs[0]
     await devnet.mine_block(genesis_addr, ts=base_ts, device=device)
     # funding block written straight into the ledger (trusted setup, not part of the measurement)
@@ -64,15 +71,21 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
                      __import__('json').dumps([int(o.amount * SMALLEST) for o in t.outputs]), '0.000000'))
     db.insert_transaction_rows(rows)
     await db.add_transaction_outputs(funding + [cb])
-    if governance:
-        _seed_governance(db, rng, block_hash)
+    seeded = None
+    if governance or n_gov:
+        blocks_n = n_blocks if make_blocks else 0
+        seeded = _seed_governance(db, rng, block_hash, n_validators=max(200, blocks_n * n_vv + 1),
+                                  n_delegates=max(5000, blocks_n * (n_dv + n_rv) + 1))
     outpoints = [(t.hash(), i) for t in funding for i in range(len(t.outputs))]
     # spending blocks
     blocks = []
     j = 0
+    gov_next = {'d': 0, 'v': 0}
     for b in range(n_blocks if make_blocks else 0):
         txs = []
-        for _ in range(txs_per_block):
+        if n_gov:
+            txs.extend(_governance_txs(seeded, gov_next, n_dv, n_vv, n_rv, rng))
+        for _ in range(txs_per_block - len(txs)):
             (h1, i1), (h2, i2) = outpoints[2 * j], outpoints[2 * j + 1]
             owner = owners[2 * j]
             j += 1
@@ -84,8 +97,52 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
             tx = Transaction(ins, outs)
             tx.sign([keys[owner]])
             txs.append(tx.hex())
+        if n_gov:
+            rng.shuffle(txs)
         blocks.append(txs)
     return db, genesis_addr, blocks, base_ts
+
+
+def _governance_txs(seeded, nxt, n_dv, n_vv, n_rv, rng):
+    """One block's governance txs (wallet/builders.py shapes): delegate votes spending a seeded delegate
+    voting-power output, validator votes spending a validator voting-power output, and delegate revokes of
+    seeded ballots; every delegate/validator is used once per run."""
+    from .models.transaction import Transaction, TransactionInput, TransactionOutput
+    from .ops import p256 as op
+    from .utils.codec import OutputType as O, TransactionType as T
+    from .wallet.builders import type_message
+    out = []
+
+    def tx(key, inputs, outputs, t):
+        ins = [TransactionInput(h, i) for h, i in inputs]
+        pub = op.public_key(key)
+        for i in ins:
+            i.public_key = pub
+        return Transaction(ins, outputs, type_message(t)).sign([key]).hex()
+    for _ in range(n_dv):
+        d = seeded['delegates'][nxt['d']]
+        nxt['d'] += 1
+        v = rng.randint(1, 10)
+        target = seeded['validators'][rng.randrange(len(seeded['validators']))]['addr']
+        outs = [TransactionOutput(target, Decimal(v), O.VOTE_AS_DELEGATE)]
+        if v < 10:
+            outs.append(TransactionOutput(d['addr'], Decimal(10 - v), O.DELEGATE_VOTING_POWER))
+        out.append(tx(d['key'], [d['dvp']], outs, T.VOTE_AS_DELEGATE))
+    for _ in range(n_vv):
+        val = seeded['validators'][nxt['v']]
+        nxt['v'] += 1
+        v = rng.randint(1, 10)
+        target = seeded['inodes'][rng.randrange(len(seeded['inodes']))]
+        outs = [TransactionOutput(target, Decimal(v), O.VOTE_AS_VALIDATOR)]
+        if v < 10:
+            outs.append(TransactionOutput(val['addr'], Decimal(10 - v), O.VALIDATOR_VOTING_POWER))
+        out.append(tx(val['key'], [val['vvp']], outs, T.VOTE_AS_VALIDATOR))
+    for _ in range(n_rv):
+        d = seeded['delegates'][nxt['d']]
+        nxt['d'] += 1
+        out.append(tx(d['key'], [d['ballot']], [TransactionOutput(d['addr'], Decimal(d['vote']), O.DELEGATE_VOTING_POWER)],
+                      T.REVOKE_AS_DELEGATE))
+    return out
 
 
 def _admit_untimed(db, txs_hex):
@@ -111,10 +168,10 @@ def _seed_governance(db, rng, block_hash: str, n_inodes: int = 12, n_validators:
                      n_delegates: int = 5000):
     """Trusted setup of a governance-heavy chain state inside the funding block (written straight into the
     ledger like the funding outputs; not part of the measurement): every validator and delegate has a
-    staked output, validators and inodes are registered, each delegate votes for one validator and each
-    validator for two inodes. Row layout as the reference's output tables (database.py:524-580): a
-    ballot carries the vote in ``outputs_amounts[index]`` and the voter in ``inputs_addresses[index]`` of
-    its tx. Returns the inode addresses."""
+    staked output and a voting-power output, validators and inodes are registered, each delegate votes for
+    one validator and each validator for two inodes. Row layout as the reference's output tables
+    (database.py:524-580): a ballot carries the vote in ``outputs_amounts[index]`` and the voter in
+    ``inputs_addresses[index]`` of its tx. Returns the keys and outpoints per role."""
     import json
     from .ops import p256 as op
     from .utils.codec import point_to_string
@@ -125,32 +182,43 @@ def _seed_governance(db, rng, block_hash: str, n_inodes: int = 12, n_validators:
     delegates = addrs[n_inodes + n_validators:]
     tx_rows = []
     tables = {t: [] for t in ('unspent_outputs', 'inode_registration_output', 'validator_registration_output',
-                              'validators_ballot', 'inodes_ballot')}
+                              'validators_voting_power', 'delegates_voting_power', 'validators_ballot',
+                              'inodes_ballot')}
 
     def tx(voter, receiver, amount):
         h = rng.randbytes(32).hex()
         tx_rows.append((block_hash, h, rng.randbytes(120).hex(), json.dumps([voter]), json.dumps([receiver]),
                         json.dumps([amount]), '0.000000'))
         return h
+    out = {'inodes': inodes, 'validators': [], 'delegates': []}
     for a in validators + delegates:  # staked outputs (unspent_outputs.is_stake = 1)
         tables['unspent_outputs'].append((tx(a, a, 10 * SMALLEST), 0, a, 1))
     for a in inodes:
         tables['inode_registration_output'].append((tx(a, a, 1000 * SMALLEST), 0, a))
-    for a in validators:
+    for k, a in enumerate(validators):
         tables['validator_registration_output'].append((tx(a, a, 100 * SMALLEST), 0, a))
+        vvp = tx(a, a, 10 * SMALLEST)
+        tables['validators_voting_power'].append((vvp, 0, a))
+        out['validators'].append({'key': keys[n_inodes + k], 'addr': a, 'vvp': (vvp, 0)})
         for _ in range(2):
             target = inodes[rng.randrange(n_inodes)]
             tables['inodes_ballot'].append((tx(a, target, rng.randint(1, 5) * SMALLEST), 0, target))
-    for a in delegates:
+    for k, a in enumerate(delegates):
+        dvp = tx(a, a, 10 * SMALLEST)
+        tables['delegates_voting_power'].append((dvp, 0, a))
         target = validators[rng.randrange(n_validators)]
-        tables['validators_ballot'].append((tx(a, target, rng.randint(1, 10) * SMALLEST), 0, target))
+        vote = rng.randint(1, 10)
+        ballot = tx(a, target, vote * SMALLEST)
+        tables['validators_ballot'].append((ballot, 0, target))
+        out['delegates'].append({'key': keys[n_inodes + n_validators + k], 'addr': a, 'dvp': (dvp, 0),
+                                 'ballot': (ballot, 0), 'vote': vote})
     db.insert_transaction_rows(tx_rows)
     db._xm('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) VALUES (?, ?, ?, ?)',
            tables.pop('unspent_outputs'))
     for t, rows in tables.items():
         db._xm(f'INSERT INTO {t} (tx_hash, "index", address) VALUES (?, ?, ?)', rows)
     db._rebuild_utxo_index()  # index + governance index from the tables
-    return inodes
+    return out
 
 
 async def _governance_probe(db) -> dict:
@@ -204,8 +272,9 @@ async def _run(args, ctx, device, utxo_backend):
     from .models.transaction import Transaction
     n_blocks = args.steps + args.warmup
     gov = getattr(args, 'governance', False)
+    gov_txs = float(getattr(args, 'governance_txs', 0.0) or 0.0)
     db, addr, blocks, base_ts = await _setup(n_blocks, args.txs, 1234 + ctx.rank, utxo_backend, device,
-                                             ledger_path=_ledger_path(args, ctx), governance=gov)
+                                             ledger_path=_ledger_path(args, ctx), governance=gov, gov_txs=gov_txs)
     gov_probe = await _governance_probe(db) if gov else None
     # mine every header up front (untimed): block b+1's previous hash is sha256(header_b) and the
     # difficulty stays at START_DIFFICULTY below block 100
@@ -304,7 +373,12 @@ def run_verify_bench(args, ctx):
     if not hasattr(args, 'object_path'):
         args.object_path = False
     total_txs, wall, stages, txs_per_block, paths, extra = asyncio.run(_run(args, ctx, device, utxo_backend))
-    if getattr(args, 'governance', False):
+    gov_txs = float(getattr(args, 'governance_txs', 0.0) or 0.0)
+    if gov_txs:
+        args_cfg = (f'governance txs: {gov_txs:.0%} of every block (70% delegate votes, 10% validator votes, '
+                    f'20% delegate revokes) on a seeded state (12 inodes, validators, delegates with stakes, '
+                    f'voting power and ballots)')
+    elif getattr(args, 'governance', False):
         args_cfg = 'governance: 12 inodes, 200 validators, 5000 delegates'
     else:
         args_cfg = None

@@ -1760,7 +1760,7 @@ class Database:
             self._mempool_confirm(bool(mempool), txids=np.asarray(tx_cols[0][1]).reshape(-1, 32), in_keys=in_keys,
                                   block_seq=seq)
         if self.gov is not None and n_in:
-            hit = self._stake_spent(spent)
+            hit = self._stake_spent(spent, spent_payload)
             if hit:
                 self.gov.removed(STAKE, hit)
         if self.gov is not None and gov is not None:
@@ -1801,15 +1801,14 @@ class Database:
                         g.tables[table].add((r[0], r[1]), r[2], int(out_amount[o]), voter(o), block_ts)
             g.version += 1
 
-    def _stake_spent(self, spent: np.ndarray) -> List[Tuple[str, int]]:
-        """Which of a block's spent outpoints (n x 40 records) are staked outputs: one vectorised
-        membership test of the raw (txid, index) keys against the governance index's stake rows."""
-        stake, want = self.gov.stake_raw()
-        if not stake:
+    def _stake_spent(self, spent: np.ndarray, spent_payload: np.ndarray) -> List[Tuple[str, int]]:
+        """Which of a block's spent outpoints (n x 40 records) are staked outputs: the stake flag their index
+        payloads carry (FLAG_STAKE, set from unspent_outputs.is_stake), one vectorised test."""
+        hit = np.nonzero(np.asarray(spent_payload['flags']) & FLAG_STAKE)[0]
+        if not len(hit):
             return []
-        have = np.ascontiguousarray(spent[:, :36]).view('V36').ravel()
-        hit = np.nonzero(np.isin(want, have))[0]
-        return [stake[k] for k in hit.tolist()]
+        idx = spent[hit, 32:36].copy().view(np.uint32).ravel()
+        return [(bytes(spent[k, :32]).hex(), int(i)) for k, i in zip(hit.tolist(), idx.tolist())]
 
     # spend order and insert order of the object path's writes (manager._apply_block → remove_outputs,
     # add_transaction_outputs): kept so SQL row order (rowid) is the same on both write paths

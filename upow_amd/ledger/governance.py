@@ -86,9 +86,11 @@ def point_key_of(address: Optional[str]) -> Optional[bytes]:
 
 
 class _Table:
-    __slots__ = ('rows', 'seq', 'by_addr', 'by_voter', 'by_pt', 'by_voter_pt', 'next_seq')
+    __slots__ = ('rows', 'seq', 'by_addr', 'by_voter', 'by_pt', 'by_voter_pt', 'next_seq', 'name', 'changed')
 
-    def __init__(self):
+    def __init__(self, name: str = '', changed=None):
+        self.name = name
+        self.changed = changed  # callback(table, address point, voter point) on every add/remove
         self.rows: Dict[Key, tuple] = {}  # key -> (address, amount, voter, ts); insertion (rowid) order
         self.seq: Dict[Key, int] = {}  # key -> insertion sequence (sort key for rowid order)
         self.by_addr: Dict[Optional[str], Dict[Key, None]] = {}
@@ -107,14 +109,19 @@ class _Table:
         self.next_seq += 1
         self.by_addr.setdefault(address, {})[key] = None
         self.by_voter.setdefault(voter, {})[key] = None
-        self.by_pt.setdefault(point_key_of(address), {})[key] = None
-        self.by_voter_pt.setdefault(point_key_of(voter), {})[key] = None
+        pa, pv = point_key_of(address), point_key_of(voter)
+        self.by_pt.setdefault(pa, {})[key] = None
+        self.by_voter_pt.setdefault(pv, {})[key] = None
+        if self.changed is not None:
+            self.changed(self.name, pa, pv)
 
     def remove(self, key: Key) -> bool:
         row = self.rows.pop(key, None)
         if row is None:
             return False
         del self.seq[key]
+        if self.changed is not None:
+            self.changed(self.name, point_key_of(row[0]), point_key_of(row[2]))
         for idx, k in ((self.by_addr, row[0]), (self.by_voter, row[2]), (self.by_pt, point_key_of(row[0])),
                        (self.by_voter_pt, point_key_of(row[2]))):
             d = idx.get(k)
@@ -148,8 +155,15 @@ class GovernanceIndex:
     def __init__(self, db):
         self.db = db
         self.lock = threading.RLock()
-        self.tables: Dict[str, _Table] = {t: _Table() for t in (*GOV_TABLES, STAKE)}
+        self.tables: Dict[str, _Table] = {t: _Table(t, self._changed) for t in (*GOV_TABLES, STAKE)}
         self.version = 0
+        # the emission cascade (get_active_inodes -> inode power -> validator stake -> delegate stake) cached
+        # per point and invalidated along its dependencies, so a block that touches a few ballots or stakes
+        # recomputes only what depends on them instead of the whole N+1 cascade
+        self._astake: Dict[Optional[bytes], Decimal] = {}
+        self._vstake: Dict[Optional[bytes], Decimal] = {}
+        self._ipower: Dict[Optional[bytes], Decimal] = {}
+        self._dirty = {STAKE: set(), 'validators_ballot': set(), 'inodes_ballot': set()}
         self._memo: dict = {}
         self._memo_version = -1
         self._pending = None  # (mempool version, pending-spent set, pending stake per address)
@@ -177,11 +191,45 @@ class GovernanceIndex:
             voter = _at(json.loads(ia) if ia else [], int(i))
             tab.add(key, address, amount, voter, ts)
 
+    def _changed(self, table: str, addr_pt, voter_pt):
+        d = self._dirty.get(table)
+        if d is not None:
+            d.add(addr_pt)
+
+    def _resolve(self):
+        """Drop the cached aggregates that depend on changed rows: a delegate's stake feeds the stake of
+        every validator it voted for, which feeds the power of every inode that validator voted for."""
+        dirty = self._dirty
+        if not (dirty[STAKE] or dirty['validators_ballot'] or dirty['inodes_ballot']):
+            return
+        vb, ib = self.tables['validators_ballot'], self.tables['inodes_ballot']
+        for pt in dirty[STAKE]:
+            self._astake.pop(pt, None)
+            for k in vb.by_voter_pt.get(pt, ()):
+                dirty['validators_ballot'].add(point_key_of(vb.rows[k][0]))
+        for pt in dirty['validators_ballot']:
+            self._vstake.pop(pt, None)
+            for k in ib.by_voter_pt.get(pt, ()):
+                dirty['inodes_ballot'].add(point_key_of(ib.rows[k][0]))
+        for pt in dirty['inodes_ballot']:
+            self._ipower.pop(pt, None)
+        for d in dirty.values():
+            d.clear()
+
+    def _clear_aggregates(self):
+        self._astake.clear()
+        self._vstake.clear()
+        self._ipower.clear()
+        for d in self._dirty.values():
+            d.clear()
+
     @_locked
     def rebuild(self):
         for t in self.tables:
-            self.tables[t] = _Table()
+            self.tables[t] = _Table(t, None)
             self._add_sql_rows(t, self._rows_sql(t))
+            self.tables[t].changed = self._changed
+        self._clear_aggregates()
         self.version += 1
 
     @_locked
@@ -312,11 +360,18 @@ class GovernanceIndex:
 
     @_locked
     def address_stake(self, forms: List[str], check_pending: bool) -> Decimal:
+        if not check_pending:
+            pt = point_key_of(forms[0]) if forms else None
+            self._resolve()
+            hit = self._astake.get(pt)
+            if hit is None:
+                hit = self._astake[pt] = sum((Decimal(a) / SMALLEST for _, _, a in self.amount_rows(STAKE, forms, False)),
+                                             Decimal(0))
+            return hit
         stake = sum((Decimal(a) / SMALLEST for _, _, a in self.amount_rows(STAKE, forms, check_pending)), Decimal(0))
-        if check_pending:
-            pstake = self._overlay()[2]
-            for f in forms:
-                stake += pstake.get(f, Decimal(0))
+        pstake = self._overlay()[2]
+        for f in forms:
+            stake += pstake.get(f, Decimal(0))
         return stake
 
     def _memo_get(self, key, fn):
@@ -339,7 +394,12 @@ class GovernanceIndex:
             return round_up_decimal(sum(ratio, Decimal(0)))
         if check_pending:
             return compute()
-        return self._memo_get(('vstake', tuple(forms)), compute)
+        pt = point_key_of(forms[0]) if forms else None
+        self._resolve()
+        hit = self._vstake.get(pt)
+        if hit is None:
+            hit = self._vstake[pt] = compute()
+        return hit
 
     @_locked
     def inode_power(self, forms: List[str], check_pending: bool) -> Decimal:
@@ -351,7 +411,12 @@ class GovernanceIndex:
             return round_up_decimal(sum(ratio, Decimal(0)))
         if check_pending:
             return compute()
-        return self._memo_get(('ipower', tuple(forms)), compute)
+        pt = point_key_of(forms[0]) if forms else None
+        self._resolve()
+        hit = self._ipower.get(pt)
+        if hit is None:
+            hit = self._ipower[pt] = compute()
+        return hit
 
     @_locked
     def inodes_with_power(self, check_pending: bool):
