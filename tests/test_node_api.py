@@ -20,8 +20,8 @@ def node(tmp_path, monkeypatch):
     monkeypatch.setattr(manager, 'START_DIFFICULTY', Decimal('1.5'))
     manager.Manager.difficulty = None
     from upow_amd.node import main
-    from upow_amd.node.nodes_manager import NodesManager
-    NodesManager.path = None
+    from upow_amd.node import peers
+    peers.reset()
     main.limiter.reset()
     main.transactions_cache.clear()
     from starlette.testclient import TestClient
@@ -210,9 +210,9 @@ def test_block_apply_does_not_block_the_http_loop(tmp_path, monkeypatch, ledger_
     monkeypatch.setattr(manager, 'START_DIFFICULTY', Decimal('1.5'))
     manager.Manager.difficulty = None
     from upow_amd.node import main
-    from upow_amd.node.nodes_manager import NodesManager
+    from upow_amd.node import peers
     from upow_amd.wallet.builders import address_of
-    NodesManager.path = None
+    peers.reset()
     main.limiter.reset()
     inner = fastpath._create_block_from_hex
     ledger_threads = []

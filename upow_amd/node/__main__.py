@@ -8,7 +8,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--host', default='0.0.0.0')
     ap.add_argument('--port', type=int, default=3006)
-    ap.add_argument('--data', default=None, help='data directory (ledger, nodes.json, ip_config.json)')
+    ap.add_argument('--data', default=None, help='data directory (ledger, peers.json, ip_config.json)')
     ap.add_argument('--db', default=None, help='SQLite ledger path')
     ap.add_argument('--core-url', default=None, help='bootstrap peer (empty string disables)')
     ap.add_argument('--log-level', default='info')

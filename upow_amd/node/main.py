@@ -53,7 +53,8 @@ from ..utils.logger import get_logger
 from ..websocket.endpoint import (broadcast_new_block, broadcast_new_transaction, router as websocket_router,
                                   shutdown_websocket_manager, start_websocket_manager)
 from .access import AccessControl
-from .nodes_manager import NodeInterface, NodesManager
+from . import peers
+from .peers import PeerClient
 from .ratelimit import Limiter, RateLimitExceeded, get_remote_address, rate_limit_exceeded_handler
 from .utils import ip_is_local
 
@@ -83,6 +84,7 @@ async def lifespan(app: FastAPI):
             lag.cancel()
         ledger_worker.stop()
         cluster.leader_quit()
+        peers.book().flush()
         await shutdown_websocket_manager()
         if db is not None and db.path != ':memory:' and os.environ.get('UPOW_SNAPSHOT', '1') != '0':
             try:  # checkpoint the UTXO index so the next start skips the SQL rebuild (ledger/snapshot.py)
@@ -163,7 +165,7 @@ async def _address_indexer(period: float = 30.0):
 async def startup():
     """main.py:246-257: open the ledger (UPOW_DATABASE_PATH, default <data dir>/ledger.sqlite3)."""
     global db, access
-    NodesManager.init()
+    peers.book()
     access = AccessControl()
     path = os.environ.get('UPOW_DATABASE_PATH') or config.data_path('ledger.sqlite3')
     db = await Database.create(path=path)
@@ -189,14 +191,14 @@ app.include_router(websocket_router)
 # ---------------------------------------------------------------------------------------------- gossip
 async def propagate(path: str, args: dict, ignore_url=None, nodes: list = None):
     """main.py:79-94: fan out to <=10 recent + <=10 never-heard-from peers."""
-    self_node = NodeInterface(self_url or '')
-    ignore_node = NodeInterface(ignore_url or '')
+    self_node = PeerClient(self_url or '')
+    ignore_node = PeerClient(ignore_url or '')
     aws = []
-    for node_url in nodes or NodesManager.get_propagate_nodes():
-        ni = NodeInterface(node_url)
-        if ni.base_url == self_node.base_url or ni.base_url == ignore_node.base_url:
+    for node_url in nodes or peers.book().gossip_urls():
+        ni = PeerClient(node_url)
+        if ni.host == self_node.host or ni.host == ignore_node.host:
             continue
-        aws.append(ni.request(path, args, self_node.url))
+        aws.append(ni.call(path, args, self_node.url))
     await gather(*aws, return_exceptions=True)
 
 
@@ -287,7 +289,7 @@ async def _sync_blockchain(node_url: str = None):
     logger.info('sync blockchain')
     error = []
     if not node_url:
-        nodes = NodesManager.get_recent_nodes()
+        nodes = peers.book().recent_urls()
         if not nodes:
             logger.error(msg := 'No nodes found.')
             return msg
@@ -295,14 +297,14 @@ async def _sync_blockchain(node_url: str = None):
     node_url = node_url.strip('/')
     _, last_block = await calculate_difficulty()
     starting_from = i = await db.get_next_block_id()
-    node_interface = NodeInterface(node_url)
+    node_interface = PeerClient(node_url)
     local_cache = None
     last_common_block = None
     if last_block != {} and last_block['id'] > 500:
-        remote_last_block = (await node_interface.get_block(i - 1))['block']
+        remote_last_block = (await node_interface.block(i - 1))['block']
         if remote_last_block['hash'] != last_block['hash']:
             offset, limit = i - 500, 500
-            remote_blocks = await node_interface.get_blocks(offset, limit)
+            remote_blocks = await node_interface.blocks(offset, limit)
             local_blocks = await db.get_blocks(offset, limit)
             local_blocks = local_blocks[:len(remote_blocks)]
             local_blocks.reverse()
@@ -333,24 +335,24 @@ async def _sync_blockchain(node_url: str = None):
                 blocks = await task
             else:
                 drop_prefetch()
-                blocks = await node_interface.get_blocks(i, limit)
+                blocks = await node_interface.blocks(i, limit)
         except Exception as e:
             logger.error(e)
-            NodesManager.sync()
+            peers.book().flush()
             break
         try:
             _, last_block = await calculate_difficulty()
             if not blocks:
                 logger.info('syncing complete')
                 if last_block['id'] > starting_from:
-                    NodesManager.update_last_message(node_url)
+                    peers.book().seen(node_url)
                     if timestamp() - last_block['timestamp'] < 86400:
                         txs_hashes = await db.get_block_transaction_hashes(last_block['hash'])
                         await propagate('push_block', {'block_content': last_block['content'], 'txs': txs_hashes,
                                                        'block_no': last_block['id']}, node_url)
                 return True
             nxt = i + len(blocks)
-            prefetch = (nxt, asyncio.ensure_future(node_interface.get_blocks(nxt, limit)))
+            prefetch = (nxt, asyncio.ensure_future(node_interface.blocks(nxt, limit)))
             assert await on_ledger(create_blocks, blocks, error_list=error)
         except Exception as e:
             drop_prefetch()
@@ -404,24 +406,19 @@ async def _join_network(request: Request, local: bool) -> None:
     """First non-local request (reference main.py:327-361): pull the first known peer's peer list,
     learn our public URL from the request, and announce it to our peers and theirs. Best effort."""
     global started, self_url
-    known = NodesManager.get_recent_nodes()
+    known = peers.book().recent_urls()
     if not known:
         return
     seed = known[0]
     try:
-        listing = await NodesManager.request(f'{seed}/get_nodes')
+        listing = await peers.fetch_json(f'{seed}/get_nodes')
         known.extend(listing['result'])
-        NodesManager.sync()
         if local:
             return
         started = True
         self_url = str(request.base_url).strip('/')
-        for own in {self_url, self_url.replace('http://', 'https://')}:
-            while own in known:
-                known.remove(own)
-        NodesManager.sync()
         await propagate('add_node', {'url': self_url})
-        await propagate('add_node', {'url': self_url}, nodes=await NodeInterface(seed).get_nodes())
+        await propagate('add_node', {'url': self_url}, nodes=await PeerClient(seed).peers())
     except Exception:
         pass
 
@@ -466,7 +463,7 @@ class Gatekeeper:
             return
         sender = request.headers.get('Sender-Node')
         if sender:
-            NodesManager.add_node(sender)
+            peers.book().add(sender)
         host = request.base_url.hostname
         local = host == 'localhost' or ip_is_local(host)
         if path == '/send_to_address' and not local:
@@ -584,7 +581,7 @@ async def verify_and_push_tx(tx: Transaction, request: Request, background_tasks
             if cluster.get() is not None:
                 await _on_ledger_sync(cluster.mirror_tx, tx.hex())
             if 'Sender-Node' in request.headers:
-                NodesManager.update_last_message(request.headers['Sender-Node'])
+                peers.book().seen(request.headers['Sender-Node'])
             background_tasks.add_task(propagate, 'push_tx', {'tx_hex': tx.hex()})
             tx_data = {'tx_hash': tx_hash, 'from': await tx.inputs[0].get_address() if tx.inputs else None,
                        'to': [o.address for o in tx.outputs], 'amount': sum(o.amount for o in tx.outputs),
@@ -715,7 +712,7 @@ async def push_block(request: Request, background_tasks: BackgroundTasks, block_
                   'merkle_root': get_transactions_merkle_tree(pending[:10])}
     background_tasks.add_task(broadcast_new_block, block_data)
     if sender:
-        NodesManager.update_last_message(sender)
+        peers.book().seen(sender)
     background_tasks.add_task(propagate, 'push_block', {
         'block_content': block_content,
         'txs': [(await Transaction.from_hex(h)).hex() for h in final_hexes] if len(final_hexes) < 10 else txs,
@@ -846,16 +843,16 @@ async def get_address_transactions(request: Request, address: str, page: int = Q
 @app.get('/add_node')
 @limiter.limit('10/minute')
 async def add_node(request: Request, url: str, background_tasks: BackgroundTasks):
-    nodes = NodesManager.get_nodes()
+    nodes = peers.book().urls()
     url = url.strip('/')
     if url == self_url:
         return {'ok': False, 'error': 'Recursively adding node'}
     if url in nodes:
         return {'ok': False, 'error': 'Node already present'}
     try:
-        assert await NodesManager.is_node_working(url)
+        assert await peers.is_alive(url)
         background_tasks.add_task(propagate, 'add_node', {'url': url}, url)
-        NodesManager.add_node(url)
+        peers.book().add(url)
         return {'ok': True, 'result': 'Node added'}
     except Exception:
         return {'ok': False, 'error': 'Could not add node'}
@@ -863,7 +860,7 @@ async def add_node(request: Request, url: str, background_tasks: BackgroundTasks
 
 @app.get('/get_nodes')
 async def get_nodes():
-    return {'ok': True, 'result': NodesManager.get_recent_nodes()[:100]}
+    return {'ok': True, 'result': peers.book().recent_urls()[:100]}
 
 
 @app.get('/cluster_info')
