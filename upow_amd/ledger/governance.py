@@ -22,7 +22,7 @@ from __future__ import annotations
 
 import functools
 import threading
-from decimal import Decimal
+from decimal import Context, Decimal, DivisionByZero, Inexact, InvalidOperation, Overflow, Rounded
 from typing import Dict, Iterable, List, Optional, Set, Tuple
 
 from ..constants import SMALLEST
@@ -113,7 +113,7 @@ class _Table:
         self.by_pt.setdefault(pa, {})[key] = None
         self.by_voter_pt.setdefault(pv, {})[key] = None
         if self.changed is not None:
-            self.changed(self.name, pa, pv)
+            self.changed(self.name, key, self.rows[key], 1)
 
     def remove(self, key: Key) -> bool:
         row = self.rows.pop(key, None)
@@ -121,7 +121,7 @@ class _Table:
             return False
         del self.seq[key]
         if self.changed is not None:
-            self.changed(self.name, point_key_of(row[0]), point_key_of(row[2]))
+            self.changed(self.name, key, row, -1)
         for idx, k in ((self.by_addr, row[0]), (self.by_voter, row[2]), (self.by_pt, point_key_of(row[0])),
                        (self.by_voter_pt, point_key_of(row[2]))):
             d = idx.get(k)
@@ -151,19 +151,200 @@ def _locked(fn):
     return wrapper
 
 
+_EXACT = Context(prec=28, traps=[Inexact, Rounded, InvalidOperation, DivisionByZero, Overflow])
+
+
+class _ExactSum:
+    """``sum(terms, Decimal(0))`` maintained under additions and removals of terms. Exact decimal arithmetic
+    (any rounding trips the trap and marks the sum unusable, so the caller recomputes sequentially); the
+    result carries the exponent a sequential sum from ``Decimal(0)`` would have — min(0, term exponents) —
+    so value AND representation match the reference's left-to-right sum."""
+    __slots__ = ('value', 'exps', 'ok')
+
+    def __init__(self):
+        self.value = Decimal(0)
+        self.exps: Dict[int, int] = {}
+        self.ok = True
+
+    def update(self, term, sign: int):
+        if not self.ok:
+            return
+        try:
+            self.value = _EXACT.add(self.value, term) if sign > 0 else _EXACT.subtract(self.value, term)
+            e = term.as_tuple().exponent
+        except Exception:
+            self.ok = False
+            return
+        n = self.exps.get(e, 0) + sign
+        if n:
+            self.exps[e] = n
+        else:
+            del self.exps[e]
+
+    def result(self) -> Optional[Decimal]:
+        if not self.ok:
+            return None
+        if not self.exps:
+            return Decimal(0)
+        try:
+            return _EXACT.quantize(self.value, Decimal(1).scaleb(min(0, min(self.exps))))
+        except Exception:
+            return None
+
+
+class _Cascade:
+    """The emission aggregates of get_active_inodes (database.py:1377-1426) as running sums:
+
+      stake(D)       = sum over D's staked outputs of amount / SMALLEST                 (1189-1205)
+      vstake(V)      = round_up(sum over ballots to V of vote * stake(voter) / 10)     (1127-1136)
+      ipower(I)      = round_up(sum over ballots to I of vote * vstake(voter) / 10)    (1390-1418)
+
+    keyed by the point an address denotes. A row change updates its own term and propagates only along
+    its dependents (a stake change re-terms that delegate's ballots; a changed validator stake re-terms
+    that validator's inode ballots). Each term is computed with the reference's expression, so values are
+    bit-identical to the sequential recomputation; an entity whose sum cannot be kept exactly (or whose
+    rows lack a vote or voter) answers None and the caller recomputes it the reference's way."""
+
+    def __init__(self, gov: 'GovernanceIndex'):
+        self.gov = gov
+        self.build()
+
+    def build(self):
+        self.astake: Dict[Optional[bytes], _ExactSum] = {}
+        self.vsum: Dict[Optional[bytes], _ExactSum] = {}
+        self.isum: Dict[Optional[bytes], _ExactSum] = {}
+        self.vterm: Dict[Key, tuple] = {}   # validators_ballot key -> (receiver pt, term)
+        self.iterm: Dict[Key, tuple] = {}   # inodes_ballot key -> (receiver pt, term)
+        self.vval: Dict[Optional[bytes], Decimal] = {}
+        self.bad_v, self.bad_i = set(), set()
+        self.pending_v: Set[Optional[bytes]] = set()  # validators whose stake may have changed (propagated lazily)
+        t = self.gov.tables
+        for k, row in t[STAKE].rows.items():
+            self._stake_row(row, 1, propagate=False)
+        for k, row in t['validators_ballot'].rows.items():
+            self._vballot(k, row, 1, propagate=False)
+        self.vval = {}
+        for k, row in t['inodes_ballot'].rows.items():
+            self._iballot(k, row, 1)
+
+    # ---- results
+    def stake(self, pt) -> Optional[Decimal]:
+        s = self.astake.get(pt)
+        return Decimal(0) if s is None else s.result()
+
+    def validator_stake(self, pt) -> Optional[Decimal]:
+        if self.pending_v:
+            self._flush()
+        return self._vstake(pt)
+
+    def _vstake(self, pt) -> Optional[Decimal]:
+        if pt in self.bad_v:
+            return None
+        hit = self.vval.get(pt)
+        if hit is None:
+            s = self.vsum.get(pt)
+            r = Decimal(0) if s is None else s.result()
+            if r is None:
+                return None
+            hit = self.vval[pt] = round_up_decimal(r)
+        return hit
+
+    def inode_power(self, pt) -> Optional[Decimal]:
+        if self.pending_v:
+            self._flush()
+        if pt in self.bad_i:
+            return None
+        s = self.isum.get(pt)
+        r = Decimal(0) if s is None else s.result()
+        return None if r is None else round_up_decimal(r)
+
+    # ---- terms
+    @staticmethod
+    def _vote(row):
+        return Decimal(row[1]) / SMALLEST if row[1] is not None else None
+
+    def _vballot(self, key, row, sign, propagate=True):
+        recv = point_key_of(row[0])
+        if sign > 0:
+            vote, voter = self._vote(row), point_key_of(row[2])
+            st = self.stake(voter) if voter is not None else None
+            if vote is None or st is None:
+                self.bad_v.add(recv)
+                term = None
+            else:
+                term = (vote * st) / 10
+                self.vsum.setdefault(recv, _ExactSum()).update(term, 1)
+            self.vterm[key] = (recv, term)
+        else:
+            recv, term = self.vterm.pop(key, (recv, None))
+            if term is not None:
+                self.vsum.setdefault(recv, _ExactSum()).update(term, -1)
+        if propagate:
+            self._validator_changed(recv)
+
+    def _iballot(self, key, row, sign):
+        recv = point_key_of(row[0])
+        if sign > 0:
+            vote, voter = self._vote(row), point_key_of(row[2])
+            vs = self._vstake(voter) if voter is not None else None
+            if vote is None or vs is None:
+                self.bad_i.add(recv)
+                term = None
+            else:
+                term = (vote * vs) / 10
+                self.isum.setdefault(recv, _ExactSum()).update(term, 1)
+            self.iterm[key] = (recv, term)
+        else:
+            recv, term = self.iterm.pop(key, (recv, None))
+            if term is not None:
+                self.isum.setdefault(recv, _ExactSum()).update(term, -1)
+
+    def _stake_row(self, row, sign, propagate=True):
+        pt = point_key_of(row[0])
+        if row[1] is None:
+            self.astake.setdefault(pt, _ExactSum()).ok = False
+        else:
+            self.astake.setdefault(pt, _ExactSum()).update(Decimal(row[1]) / SMALLEST, sign)
+        if propagate:  # re-term every ballot this delegate cast
+            vb = self.gov.tables['validators_ballot']
+            for k in list(vb.by_voter_pt.get(pt, ())):
+                row_k = vb.rows[k]
+                self._vballot(k, row_k, -1, propagate=False)
+                self._vballot(k, row_k, 1, propagate=True)
+
+    def _validator_changed(self, pt):
+        self.pending_v.add(pt)
+        self.vval.pop(pt, None)
+
+    def _flush(self):
+        """Re-term the inode ballots of every validator whose stake may have changed since the last query
+        (once per validator however many of its ballots or delegates changed in between)."""
+        ib = self.gov.tables['inodes_ballot']
+        while self.pending_v:
+            pt = self.pending_v.pop()
+            for k in list(ib.by_voter_pt.get(pt, ())):
+                row_k = ib.rows[k]
+                self._iballot(k, row_k, -1)
+                self._iballot(k, row_k, 1)
+
+    def row_changed(self, table: str, key: Key, row: tuple, sign: int):
+        if table == STAKE:
+            self._stake_row(row, sign)
+        elif table == 'validators_ballot':
+            self._vballot(key, row, sign)
+        elif table == 'inodes_ballot':
+            self._iballot(key, row, sign)
+
+
 class GovernanceIndex:
     def __init__(self, db):
         self.db = db
         self.lock = threading.RLock()
         self.tables: Dict[str, _Table] = {t: _Table(t, self._changed) for t in (*GOV_TABLES, STAKE)}
         self.version = 0
-        # the emission cascade (get_active_inodes -> inode power -> validator stake -> delegate stake) cached
-        # per point and invalidated along its dependencies, so a block that touches a few ballots or stakes
-        # recomputes only what depends on them instead of the whole N+1 cascade
-        self._astake: Dict[Optional[bytes], Decimal] = {}
-        self._vstake: Dict[Optional[bytes], Decimal] = {}
-        self._ipower: Dict[Optional[bytes], Decimal] = {}
-        self._dirty = {STAKE: set(), 'validators_ballot': set(), 'inodes_ballot': set()}
+        # the emission cascade (get_active_inodes -> inode power -> validator stake -> delegate stake) kept
+        # as exact running sums that follow every row change (_Cascade), so a block costs O(its changes)
+        self.cascade = _Cascade(self)
         self._memo: dict = {}
         self._memo_version = -1
         self._pending = None  # (mempool version, pending-spent set, pending stake per address)
@@ -191,37 +372,8 @@ class GovernanceIndex:
             voter = _at(json.loads(ia) if ia else [], int(i))
             tab.add(key, address, amount, voter, ts)
 
-    def _changed(self, table: str, addr_pt, voter_pt):
-        d = self._dirty.get(table)
-        if d is not None:
-            d.add(addr_pt)
-
-    def _resolve(self):
-        """Drop the cached aggregates that depend on changed rows: a delegate's stake feeds the stake of
-        every validator it voted for, which feeds the power of every inode that validator voted for."""
-        dirty = self._dirty
-        if not (dirty[STAKE] or dirty['validators_ballot'] or dirty['inodes_ballot']):
-            return
-        vb, ib = self.tables['validators_ballot'], self.tables['inodes_ballot']
-        for pt in dirty[STAKE]:
-            self._astake.pop(pt, None)
-            for k in vb.by_voter_pt.get(pt, ()):
-                dirty['validators_ballot'].add(point_key_of(vb.rows[k][0]))
-        for pt in dirty['validators_ballot']:
-            self._vstake.pop(pt, None)
-            for k in ib.by_voter_pt.get(pt, ()):
-                dirty['inodes_ballot'].add(point_key_of(ib.rows[k][0]))
-        for pt in dirty['inodes_ballot']:
-            self._ipower.pop(pt, None)
-        for d in dirty.values():
-            d.clear()
-
-    def _clear_aggregates(self):
-        self._astake.clear()
-        self._vstake.clear()
-        self._ipower.clear()
-        for d in self._dirty.values():
-            d.clear()
+    def _changed(self, table: str, key: Key, row: tuple, sign: int):
+        self.cascade.row_changed(table, key, row, sign)
 
     @_locked
     def rebuild(self):
@@ -229,7 +381,7 @@ class GovernanceIndex:
             self.tables[t] = _Table(t, None)
             self._add_sql_rows(t, self._rows_sql(t))
             self.tables[t].changed = self._changed
-        self._clear_aggregates()
+        self.cascade.build()
         self.version += 1
 
     @_locked
@@ -361,17 +513,14 @@ class GovernanceIndex:
     @_locked
     def address_stake(self, forms: List[str], check_pending: bool) -> Decimal:
         if not check_pending:
-            pt = point_key_of(forms[0]) if forms else None
-            self._resolve()
-            hit = self._astake.get(pt)
-            if hit is None:
-                hit = self._astake[pt] = sum((Decimal(a) / SMALLEST for _, _, a in self.amount_rows(STAKE, forms, False)),
-                                             Decimal(0))
-            return hit
+            hit = self.cascade.stake(point_key_of(forms[0]) if forms else None)
+            if hit is not None:
+                return hit
         stake = sum((Decimal(a) / SMALLEST for _, _, a in self.amount_rows(STAKE, forms, check_pending)), Decimal(0))
-        pstake = self._overlay()[2]
-        for f in forms:
-            stake += pstake.get(f, Decimal(0))
+        if check_pending:
+            pstake = self._overlay()[2]
+            for f in forms:
+                stake += pstake.get(f, Decimal(0))
         return stake
 
     def _memo_get(self, key, fn):
@@ -394,12 +543,8 @@ class GovernanceIndex:
             return round_up_decimal(sum(ratio, Decimal(0)))
         if check_pending:
             return compute()
-        pt = point_key_of(forms[0]) if forms else None
-        self._resolve()
-        hit = self._vstake.get(pt)
-        if hit is None:
-            hit = self._vstake[pt] = compute()
-        return hit
+        hit = self.cascade.validator_stake(point_key_of(forms[0]) if forms else None)
+        return hit if hit is not None else compute()
 
     @_locked
     def inode_power(self, forms: List[str], check_pending: bool) -> Decimal:
@@ -411,12 +556,8 @@ class GovernanceIndex:
             return round_up_decimal(sum(ratio, Decimal(0)))
         if check_pending:
             return compute()
-        pt = point_key_of(forms[0]) if forms else None
-        self._resolve()
-        hit = self._ipower.get(pt)
-        if hit is None:
-            hit = self._ipower[pt] = compute()
-        return hit
+        hit = self.cascade.inode_power(point_key_of(forms[0]) if forms else None)
+        return hit if hit is not None else compute()
 
     @_locked
     def inodes_with_power(self, check_pending: bool):
