@@ -1764,8 +1764,10 @@ class Database:
             if hit:
                 self.gov.removed(STAKE, hit)
         if self.gov is not None and gov is not None:
+            tg = perf_counter()
             self._gov_apply_native(gov, gov_created, gov_spent, out_txid, out_index, out_amount, out_addr_spec,
                                    int(b['timestamp']))
+            self.last_gov_index_s = perf_counter() - tg
         return seq
 
     def _gov_apply_native(self, gov: dict, created: dict, spent: dict, out_txid, out_index, out_amount, out_addr_spec,

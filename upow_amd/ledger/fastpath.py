@@ -330,7 +330,8 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
             logger.error(f'Transaction of {block_no} has not been added in block {e}')
             manager.Manager.difficulty = None
             return False
-        timings.update({'apply_commit_s': perf_counter() - ta, 'journal_seq': seq})
+        timings.update({'apply_commit_s': perf_counter() - ta, 'journal_seq': seq,
+                        'gov_index_s': getattr(database, 'last_gov_index_s', 0.0) if gov_cols is not None else 0.0})
         return True
 
     if coinbase is not None:

@@ -114,30 +114,36 @@ class BlockGovernance:
         def ssum(t):
             return _seg(np.where(ot == t, amt, 0), starts)
 
-        def scount(t):
-            return _seg((ot == t).astype(np.int64), starts)
-
         def last_of(t):  # index of the last output of type t per tx (the reference's ``receiver``), -1 if none
             return np.maximum.reduceat(np.where(ot == t, np.arange(len(ot)), -1), starts[:-1])
-        gov_k = np.nonzero(self.gov)[0].tolist()
+        gov_idx = np.nonzero(self.gov)[0]
+        gov_k = gov_idx.tolist()
         tt = self.tx_type.tolist()
-        has = {t: (scount(t) > 0).tolist() for t in (O.STAKE, O.UN_STAKE, O.INODE_REGISTRATION)}
+        cnt = {t: _seg((ot == t).astype(np.int64), starts) for t in (O.STAKE, O.UN_STAKE, O.INODE_REGISTRATION,
+                                                                    O.VALIDATOR_VOTING_POWER)}
+        has = {t: (cnt[t] > 0).tolist() for t in (O.STAKE, O.UN_STAKE, O.INODE_REGISTRATION)}
         sums = {t: ssum(t).tolist() for t in (O.DELEGATE_VOTING_POWER, O.VALIDATOR_REGISTRATION, O.INODE_REGISTRATION,
                                               O.VOTE_AS_VALIDATOR, O.VOTE_AS_DELEGATE)}
-        n_vvp = scount(O.VALIDATOR_VOTING_POWER).tolist()
+        n_vvp = cnt[O.VALIDATOR_VOTING_POWER].tolist()
         last_vvp = last_of(O.VALIDATOR_VOTING_POWER).tolist()
         recv = {O.VOTE_AS_VALIDATOR: last_of(O.VOTE_AS_VALIDATOR).tolist(),
                 O.VOTE_AS_DELEGATE: last_of(O.VOTE_AS_DELEGATE).tolist()}
         ins = in_start.tolist()
-        p_addr, p_len = pay['addr'], pay['len'].tolist()
-
-        def addr_raw(j):  # spent output owner (get_address) of input j
-            return bytes(p_addr[j, :p_len[j]])
+        # point keys of every governance tx's input-0 owner, vectorised: [43 if odd y else 42] || x
+        j0 = in_start[gov_idx]
+        pa, pl = pay['addr'][j0], pay['len'][j0]
+        pts = np.empty((len(j0), 33), dtype=np.uint8)
+        pts[:, 1:] = np.where((pl == 33)[:, None], pa[:, 1:33], pa[:, :32])
+        odd = np.where(pl == 33, pa[:, 0] == 43, (pa[:, 32] & 1) == 1)
+        pts[:, 0] = np.where(odd, 43, 42)
+        if np.any((pl != 33) & (pl != 64)):
+            return None
+        pt_of = dict(zip(gov_k, pts.view('V33').ravel().tolist()))
+        p_addr, p_len = pay['addr'], pay['len']
 
         def out_pt(o):
             return point_key(bytes(out_addr[o, :out_len[o]]))
 
-        has_point = g.has_point
         memo = {}
 
         async def active(cp: bool):
@@ -145,98 +151,107 @@ class BlockGovernance:
                 memo[cp] = await db.get_active_inodes(cp)
             return memo[cp]
 
-        def staked(pt):
-            return has_point(STAKE, pt, False)
+        with g.lock:
+            pend = g.pending_spent(True)
+            T_ = g.tables
+            stake_pt, inode_pt, valid_pt = T_[STAKE].by_pt, T_[INODE_T].by_pt, T_[VALIDATOR_T].by_pt
+            dvp_pt, vb_voter = T_[DVP_T].by_pt, T_[VBALLOT_T].by_voter_pt
 
-        def inode_reg(pt, cp=True):
-            return has_point(INODE_T, pt, cp)
+            def live(index, pt, cp):
+                keys = index.get(pt)
+                if not keys:
+                    return False
+                return not cp or not pend or any(k not in pend for k in keys)
 
-        def validator_reg(pt, cp=True):
-            return has_point(VALIDATOR_T, pt, cp)
-
-        def delegate_power(pt):  # get_delegates_all_power: voting power outputs + cast delegate ballots
-            return has_point(DVP_T, pt, False) or has_point(VBALLOT_T, pt, False, voter=True)
-
-        now = None
-        signers = {}
-        for k in gov_k:
-            t = tt[k]
-            j0 = ins[k]
-            raw0 = addr_raw(j0)
-            pt0 = point_key(raw0)
-            if pt0 is None:
-                return None
-            # stake (transaction.py:434-465)
-            if has[O.STAKE][k]:
-                if staked(pt0) and not codec.is_blockchain_syncing:
-                    return None
-                if codec.bytes_to_string(raw0) in g._overlay()[2]:
-                    return None  # a pending stake tx of this address: the reference's tx_hash quirk decides
-                power = sums[O.DELEGATE_VOTING_POWER][k]
-                if power > 0:
-                    if power != 10 * S or delegate_power(pt0):
+            def delegate_power(pt):  # get_delegates_all_power: voting power outputs + cast delegate ballots
+                return live(dvp_pt, pt, False) or live(vb_voter, pt, False)
+            signers = {}
+            now = None
+            for k in gov_k:
+                t = tt[k]
+                pt0 = pt_of[k]
+                # stake (transaction.py:434-465)
+                if has[O.STAKE][k]:
+                    if live(stake_pt, pt0, False) and not codec.is_blockchain_syncing:
                         return None
-                elif not delegate_power(pt0):
-                    return None
-            # unstake (transaction.py:467-479)
-            if has[O.UN_STAKE][k]:
-                if has_point(VBALLOT_T, pt0, False, voter=True) and bytes(txid[k]).hex() != UNSTAKE_EXCEPTION:
-                    return None
-                if g.pending_vote_as_delegate():
-                    return None
-            if t == T.VALIDATOR_REGISTRATION:  # transaction.py:371-398
-                if not staked(pt0) or validator_reg(pt0) or inode_reg(pt0):
-                    return None
-                if sums[O.VALIDATOR_REGISTRATION][k] != 100 * S or n_vvp[k] != 1 or amt[last_vvp[k]] != 10 * S:
-                    return None
-            if t in _REVOKES:  # transaction.py:400-432: signed by the voter of each ballot input
-                table = IBALLOT_T if t == T.REVOKE_AS_VALIDATOR else VBALLOT_T
-                rows = g.tables[table].rows
-                valid = False
-                for j in range(ins[k], ins[k + 1]):
-                    key = (bytes(in_keys[j, :32]).hex(), int.from_bytes(bytes(in_keys[j, 32:36]), 'little'))
-                    row = rows.get(key)
-                    if row is None or key[1] != 0 or row[2] is None or row[3] is None:
-                        return None  # voter = inputs_addresses[0] of the ballot tx = the row's voter iff index 0
-                    vraw = codec.string_to_bytes(row[2])
-                    if len(vraw) not in (33, 64):
+                    j0k = ins[k]
+                    if codec.bytes_to_string(bytes(p_addr[j0k, :p_len[j0k]])) in g._overlay()[2]:
+                        return None  # a pending stake tx of this address: the reference's tx_hash quirk decides
+                    power = sums[O.DELEGATE_VOTING_POWER][k]
+                    if power > 0:
+                        if power != 10 * S or delegate_power(pt0):
+                            return None
+                    elif not delegate_power(pt0):
                         return None
-                    signers[j] = vraw
-                    if now is None:
-                        from .database import _dt, _utcnow
-                        now = _utcnow()
-                    valid |= now - _dt(row[3]) >= timedelta(hours=48)
-                voter_pt = point_key(signers[ins[k]])
-                if t == T.REVOKE_AS_VALIDATOR and not validator_reg(voter_pt):
-                    return None
-                if not staked(voter_pt) or not valid:
-                    return None
-            if t == T.INODE_DE_REGISTRATION:  # transaction.py:240-256
-                address = codec.bytes_to_string(raw0)
-                if not has_point(INODE_T, pt0, False):
-                    return None
-                if any(e.get('wallet') == address for e in await active(False)):
-                    return None
-            if has[O.INODE_REGISTRATION][k]:  # transaction.py:318-352
-                address = codec.bytes_to_string(raw0)
-                if sums[O.INODE_REGISTRATION][k] != 1000 * S or not staked(pt0) or inode_reg(pt0) or validator_reg(pt0):
-                    return None
-                if len(await active(True)) >= MAX_INODES:
-                    return None
-                if any(e.get('wallet') == address for e in await active(False)):
-                    return None
-            if t == T.VOTE_AS_VALIDATOR:  # transaction.py:258-290
-                v = sums[O.VOTE_AS_VALIDATOR][k]
-                if v > 10 * S or v <= 0 or inode_reg(pt0) or not validator_reg(pt0):
-                    return None
-                if not inode_reg(out_pt(recv[O.VOTE_AS_VALIDATOR][k])):
-                    return None
-            if t == T.VOTE_AS_DELEGATE:  # transaction.py:292-316 (block validation: stake without mempool)
-                v = sums[O.VOTE_AS_DELEGATE][k]
-                if v > 10 * S or v <= 0 or inode_reg(pt0) or not staked(pt0):
-                    return None
-                if not validator_reg(out_pt(recv[O.VOTE_AS_DELEGATE][k])):
-                    return None
+                # unstake (transaction.py:467-479)
+                if has[O.UN_STAKE][k]:
+                    if live(vb_voter, pt0, False) and bytes(txid[k]).hex() != UNSTAKE_EXCEPTION:
+                        return None
+                    if g.pending_vote_as_delegate():
+                        return None
+                if t == 0:
+                    if has[O.INODE_REGISTRATION][k]:
+                        pass  # checked below
+                    else:
+                        continue
+                if t == T.VOTE_AS_DELEGATE:  # transaction.py:292-316 (block validation: stake without mempool)
+                    v = sums[O.VOTE_AS_DELEGATE][k]
+                    if v > 10 * S or v <= 0 or live(inode_pt, pt0, True) or not live(stake_pt, pt0, False):
+                        return None
+                    if not live(valid_pt, out_pt(recv[O.VOTE_AS_DELEGATE][k]), True):
+                        return None
+                    continue
+                if t == T.VOTE_AS_VALIDATOR:  # transaction.py:258-290
+                    v = sums[O.VOTE_AS_VALIDATOR][k]
+                    if v > 10 * S or v <= 0 or live(inode_pt, pt0, True) or not live(valid_pt, pt0, True):
+                        return None
+                    if not live(inode_pt, out_pt(recv[O.VOTE_AS_VALIDATOR][k]), True):
+                        return None
+                    continue
+                if t == T.VALIDATOR_REGISTRATION:  # transaction.py:371-398
+                    if not live(stake_pt, pt0, False) or live(valid_pt, pt0, True) or live(inode_pt, pt0, True):
+                        return None
+                    if sums[O.VALIDATOR_REGISTRATION][k] != 100 * S or n_vvp[k] != 1 or amt[last_vvp[k]] != 10 * S:
+                        return None
+                if t in _REVOKES:  # transaction.py:400-432: signed by the voter of each ballot input
+                    table = IBALLOT_T if t == T.REVOKE_AS_VALIDATOR else VBALLOT_T
+                    rows = T_[table].rows
+                    valid = False
+                    for j in range(ins[k], ins[k + 1]):
+                        key = (bytes(in_keys[j, :32]).hex(), int.from_bytes(bytes(in_keys[j, 32:36]), 'little'))
+                        row = rows.get(key)
+                        if row is None or key[1] != 0 or row[2] is None or row[3] is None:
+                            return None  # voter = inputs_addresses[0] of the ballot tx = the row's voter iff index 0
+                        vraw = codec.string_to_bytes(row[2])
+                        if len(vraw) not in (33, 64):
+                            return None
+                        signers[j] = vraw
+                        if now is None:
+                            from .database import _dt, _utcnow
+                            now = _utcnow()
+                        valid = valid or now - _dt(row[3]) >= timedelta(hours=48)
+                    voter_pt = point_key(signers[ins[k]])
+                    if t == T.REVOKE_AS_VALIDATOR and not live(valid_pt, voter_pt, True):
+                        return None
+                    if not live(stake_pt, voter_pt, False) or not valid:
+                        return None
+                if t == T.INODE_DE_REGISTRATION:  # transaction.py:240-256
+                    j0k = ins[k]
+                    address = codec.bytes_to_string(bytes(p_addr[j0k, :p_len[j0k]]))
+                    if not live(inode_pt, pt0, False):
+                        return None
+                    if any(e.get('wallet') == address for e in await active(False)):
+                        return None
+                if has[O.INODE_REGISTRATION][k]:  # transaction.py:318-352
+                    j0k = ins[k]
+                    address = codec.bytes_to_string(bytes(p_addr[j0k, :p_len[j0k]]))
+                    if sums[O.INODE_REGISTRATION][k] != 1000 * S or not live(stake_pt, pt0, False) or \
+                            live(inode_pt, pt0, True) or live(valid_pt, pt0, True):
+                        return None
+                    if len(await active(True)) >= MAX_INODES:
+                        return None
+                    if any(e.get('wallet') == address for e in await active(False)):
+                        return None
         return {'signers': signers}
 
 

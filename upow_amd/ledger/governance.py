@@ -159,14 +159,16 @@ class _ExactSum:
     (any rounding trips the trap and marks the sum unusable, so the caller recomputes sequentially); the
     result carries the exponent a sequential sum from ``Decimal(0)`` would have — min(0, term exponents) —
     so value AND representation match the reference's left-to-right sum."""
-    __slots__ = ('value', 'exps', 'ok')
+    __slots__ = ('value', 'exps', 'ok', 'cached')
 
     def __init__(self):
         self.value = Decimal(0)
         self.exps: Dict[int, int] = {}
         self.ok = True
+        self.cached = None
 
     def update(self, term, sign: int):
+        self.cached = None
         if not self.ok:
             return
         try:
@@ -184,12 +186,15 @@ class _ExactSum:
     def result(self) -> Optional[Decimal]:
         if not self.ok:
             return None
+        if self.cached is not None:
+            return self.cached
         if not self.exps:
             return Decimal(0)
         try:
-            return _EXACT.quantize(self.value, Decimal(1).scaleb(min(0, min(self.exps))))
+            self.cached = _EXACT.quantize(self.value, Decimal(1).scaleb(min(0, min(self.exps))))
         except Exception:
             return None
+        return self.cached
 
 
 class _Cascade:

@@ -506,7 +506,9 @@ async def _finalize_block(block_no: int, block_content: str, fees, n_txs: int, a
     database: Database = Database.instance
     block_hash = sha256(block_content)
     previous_hash, address, merkle_tree, content_time, content_difficulty, random = split_block_content(block_content)
+    ta = perf_counter()
     active_inodes = await database.get_active_inodes()
+    last_block_timings['active_inodes_s'] = perf_counter() - ta
     await update_active_inodes_cache_with_data(active_inodes)
     block_reward = get_block_reward(block_no)
     miner_reward, inode_rewards = get_inode_rewards(block_reward, active_inodes, block_no=block_no)
