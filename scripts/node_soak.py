@@ -40,8 +40,9 @@ def run(tid):
     for j in range(tid, len(jobs), threads):
         k, hx = int(jobs[j][0]), jobs[j][1]
         target = t0 + k / rate
-        if time.time() < target:
-            time.sleep(target - time.time())
+        delay = target - time.time()  # one clock read: the check and the sleep must agree
+        if delay > 0:
+            time.sleep(delay)
         if time.time() - t0 > seconds + 5:
             break
         ts = time.time()

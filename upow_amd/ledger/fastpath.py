@@ -131,7 +131,8 @@ async def create_block_from_hex(block_content: str, tx_hexes: List[str], error_l
     from ..parallel import cluster
     c = cluster.get()
     if c is not None and c.leader and mirror and not c.replaying:
-        from ..parallel.cluster import pack_txs
+        from ..parallel.cluster import flush_txs, pack_txs
+        flush_txs()  # the followers' mempools first: block rules consult pending txs
         c.send('block', pack_txs(tx_hexes), content=block_content, cb=coinbase.hex() if coinbase is not None else None)
     err = None
     try:

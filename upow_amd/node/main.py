@@ -579,7 +579,7 @@ async def verify_and_push_tx(tx: Transaction, request: Request, background_tasks
             return JSONResponse(status_code=403, content={'ok': False, 'error': 'Access forbidden temporarily.'})
         if await db.add_pending_transaction(tx):
             if cluster.get() is not None:
-                await _on_ledger_sync(cluster.mirror_tx, tx.hex())
+                cluster.mirror_tx(tx.hex())  # queued; the ledger thread ships the batch
             if 'Sender-Node' in request.headers:
                 peers.book().seen(request.headers['Sender-Node'])
             background_tasks.add_task(propagate, 'push_tx', {'tx_hex': tx.hex()})

@@ -9,7 +9,11 @@ starts G ranks:
   mutation the leader makes, in the same order, from an op stream the leader broadcasts over RCCL:
 
       block     a block to validate+apply (push or sync form, tx hex + optional coinbase)
-      tx        a tx admitted to the mempool (governance rules consult pending txs)
+      txs       the txs admitted to the leader's mempool since the last op (governance rules consult
+                pending txs): /push_tx only appends to an outbox; the ledger thread ships the outbox as
+                ONE op every ``UPOW_CLUSTER_TX_FLUSH_MS`` and always right before any other op, so a
+                follower's mempool holds everything the leader's held when a block is applied
+      tx        one mempool tx (start-up replay)
       gc        mempool garbage collection
       rollback  / delete   fork handling (remove_blocks / delete_blocks)
       status    all-gather of (height, UTXO-set hash) — replica audit (GET /cluster_info)
@@ -28,6 +32,8 @@ collectives block the leader's event loop for their (sub-millisecond) duration.
 from __future__ import annotations
 
 import json
+import os
+import threading
 from typing import List, Optional
 
 from ..utils.logger import get_logger
@@ -114,10 +120,58 @@ def active_leader() -> Optional[Cluster]:
 
 
 # ---------------------------------------------------------------------------------------------- leader hooks
+_outbox: List[str] = []
+_outbox_lock = threading.Lock()
+_flush_scheduled = False
+FLUSH_S = float(os.environ.get('UPOW_CLUSTER_TX_FLUSH_MS', '20')) / 1000.0
+
+
 def mirror_tx(tx_hex: str):
+    """A tx admitted by the leader (any thread): queued for the next 'txs' op, never waits for a collective."""
+    global _flush_scheduled
     c = active_leader()
-    if c is not None:
-        c.send('tx', h=tx_hex)
+    if c is None:
+        return
+    with _outbox_lock:
+        _outbox.append(tx_hex)
+        if _flush_scheduled:
+            return
+        _flush_scheduled = True
+    _schedule_flush()
+
+
+def _schedule_flush():
+    """Flush the outbox on the thread that issues every other collective (the ledger thread), after the
+    flush interval: one broadcast pair per interval however many txs arrived."""
+    import asyncio
+    from ..ledger import worker
+    w = worker.get()
+    if w is not None:
+        w.loop.call_soon_threadsafe(lambda: w.loop.call_later(FLUSH_S, _timed_flush))
+        return
+    try:
+        asyncio.get_running_loop().call_later(FLUSH_S, _timed_flush)
+    except RuntimeError:  # no loop (tests, tools): ship now
+        _timed_flush()
+
+
+def _timed_flush():
+    global _flush_scheduled
+    with _outbox_lock:
+        _flush_scheduled = False
+    flush_txs()
+
+
+def flush_txs() -> int:
+    """Ship the queued mempool txs to the followers as one 'txs' op (ledger thread / op-issuing thread)."""
+    c = active_leader()
+    with _outbox_lock:
+        hexes = list(_outbox)
+        _outbox.clear()
+    if c is None or not hexes:
+        return 0
+    c.send('txs', pack_txs(hexes))
+    return len(hexes)
 
 
 async def mirror_gc(pending):
@@ -125,6 +179,7 @@ async def mirror_gc(pending):
     from ..ledger.manager import clear_pending_transactions
     c = active_leader()
     if c is not None:
+        flush_txs()
         c.send('gc', pending=list(pending) if pending is not None else None)
     return await clear_pending_transactions(pending)
 
@@ -132,6 +187,7 @@ async def mirror_gc(pending):
 async def mirror_rollback(db, block_no: int):
     c = active_leader()
     if c is not None:
+        flush_txs()
         c.send('rollback', n=int(block_no))
     await db.remove_blocks(block_no)
 
@@ -139,6 +195,7 @@ async def mirror_rollback(db, block_no: int):
 async def mirror_delete(db, offset: int):
     c = active_leader()
     if c is not None:
+        flush_txs()
         c.send('delete', n=int(offset))
     await db.delete_blocks(offset)
 
@@ -159,8 +216,9 @@ async def leader_replay(db):
         for info in page:
             c.send('replay_block', pack_txs(info['transactions']), content=info['block']['content'])
             offset = info['block']['id'] + 1
-    for r in db._q('SELECT tx_hex FROM pending_transactions ORDER BY rowid'):
-        c.send('tx', h=r['tx_hex'])
+    pending = [r['tx_hex'] for r in db._q('SELECT tx_hex FROM pending_transactions ORDER BY rowid')]
+    if pending:
+        c.send('txs', pack_txs(pending))
     c.send('replay_end')
     st = c.status(db)
     bad = [s for s in st if (s['height'], s['utxo_hash']) != (st[0]['height'], st[0]['utxo_hash'])]
@@ -174,6 +232,7 @@ def leader_quit():
     c = _cluster
     if c is not None and c.leader:
         try:
+            flush_txs()
             c.send('quit')
         except Exception as e:  # pragma: no cover - process group already gone
             logger.error(f'cluster quit: {e}')
@@ -233,6 +292,12 @@ async def follower_main(c: Cluster, db):
                 await db.add_pending_transaction(await Transaction.from_hex(msg['h']))
             except Exception as e:
                 logger.error(f'cluster follower: mempool insert failed: {e}')
+        elif op == 'txs':
+            for h in unpack_txs(msg['_payload']):
+                try:
+                    await db.add_pending_transaction(await Transaction.from_hex(h))
+                except Exception as e:
+                    logger.error(f'cluster follower: mempool insert failed: {e}')
         elif op == 'gc':
             await clear_pending_transactions(msg.get('pending'))
         elif op == 'rollback':
@@ -246,5 +311,5 @@ async def follower_main(c: Cluster, db):
     logger.info(f'cluster follower rank {c.ctx.rank} stopped at height {db._tip_id()}')
 
 
-__all__ = ['Cluster', 'init', 'get', 'mirror_tx', 'mirror_gc', 'mirror_rollback', 'mirror_delete', 'leader_replay',
+__all__ = ['Cluster', 'init', 'get', 'mirror_tx', 'flush_txs', 'mirror_gc', 'mirror_rollback', 'mirror_delete', 'leader_replay',
            'leader_quit', 'follower_main']
