@@ -118,7 +118,7 @@ def _verify_side_metrics(args, ctx) -> dict:
     try:
         v = argparse.Namespace(**{**vars(args), 'steps': args.verify_steps, 'warmup': 2, 'ledger': tmp,
                                   'object_path': False, 'from_mempool': False, 'governance': False,
-                                  'governance_txs': 0.0})
+                                  'governance_txs': 0.0, 'age_txs': 0})
         r = run_cluster_verify_bench(v, ctx) if ctx.is_distributed else run_verify_bench(v, ctx)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
@@ -171,6 +171,8 @@ def main(argv=None):
                     help='verify mode: seed 12 inodes, 200 validators, 5,000 delegates with ballots before the blocks')
     ap.add_argument('--governance-txs', default='0',
                     help="verify mode: fraction of each block's txs that are governance txs, e.g. 5%% or 0.05")
+    ap.add_argument('--age-txs', type=int, default=0,
+                    help='verify/sync modes: first age the ledger with N confirmed txs (2N UTXO rows), e.g. 2500000')
     ap.add_argument('--verify-steps', type=int, default=10,
                     help='mine mode: timed 2 MB blocks of the tx-verify side measurement (0: skip; GPU only)')
     args = ap.parse_args(argv)

@@ -10,6 +10,8 @@
 #   verifymem bench.py --mode verify (in-memory ledger)
 #   verifygov bench.py --mode verify --governance (file ledger; 12 inodes, 200 validators, 5,000 delegates)
 #   verifygov5 bench.py --mode verify --governance-txs 5% (file ledger; 5 % of every block's txs are governance txs)
+#   verifyaged bench.py --mode verify on a ledger aged to 2.5 M txs / 5 M UTXOs (20 blocks, SQL catch-up timed)
+#   syncaged   bench.py --mode sync: 1,000 blocks replayed into the aged ledger
 #   cluster  forced single-rank RCCL cluster node, one chain (bench.py --mode verify under torchrun)
 #   launch   bench.py --gpus 1 under torchrun (the driver's multi-rank entry form)
 #   sync     bench.py --mode sync (chain-sync replay of a /get_blocks page, decode-ahead pipeline)
@@ -51,6 +53,20 @@ for s in $STEPS; do
       timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger --governance-txs 5% \
         > "$OUT/verify_gov5.json" 2> "$OUT/verify_gov5.err" || { tail -20 "$OUT/verify_gov5.err"; exit 1; }
       cat "$OUT/verify_gov5.json" ;;
+    verifyaged)
+      # chain scale: the ledger first aged to 2.5 M tx rows / 5 M UTXO rows, then 2 MB blocks incl. SQL catch-up
+      rm -rf /tmp/upow_bench_ledger
+      timeout -k 10 900 python -u bench.py --mode verify --ledger /tmp/upow_bench_ledger --age-txs 2500000 \
+        --steps 20 --warmup 2 > "$OUT/verify_aged.json" 2> "$OUT/verify_aged.err" \
+        || { tail -20 "$OUT/verify_aged.err"; exit 1; }
+      cat "$OUT/verify_aged.json" ;;
+    syncaged)
+      # a 1,000-block sync (200 txs each) into the aged ledger, decode-ahead pipeline
+      rm -rf /tmp/upow_bench_ledger
+      timeout -k 10 900 python -u bench.py --mode sync --ledger /tmp/upow_bench_ledger --age-txs 2500000 \
+        --steps 1000 --warmup 5 --txs 200 > "$OUT/sync_aged.json" 2> "$OUT/sync_aged.err" \
+        || { tail -20 "$OUT/sync_aged.err"; exit 1; }
+      cat "$OUT/sync_aged.json" ;;
     verifygov)
       rm -rf /tmp/upow_bench_ledger
       timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger --governance \

@@ -32,7 +32,8 @@ def _funding_tx(owner_addrs, amount: Decimal, rng):
 
 
 async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None, device=None, base_ts=None,
-                 make_blocks: bool = True, ledger_path: str = None, governance: bool = False, gov_txs: float = 0.0):
+                 make_blocks: bool = True, ledger_path: str = None, governance: bool = False, gov_txs: float = 0.0,
+                 age_txs: int = 0, aging: dict = None):
     """``gov_txs`` > 0: that fraction of every block's txs are governance txs (70 % delegate votes, 10 %
     validator votes, 20 % delegate revokes of seeded ballots, signed by the voters) on a seeded governance
     state; the chain starts four days back so the seeded ballots are past the 48 h revoke window."""
@@ -54,6 +55,10 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
         base_ts = int(time.time()) - (4 * 86_400 if n_gov else 10_000)
     genesis_addr = addrs[0]
     await devnet.mine_block(genesis_addr, ts=base_ts, device=device)
+    if age_txs:
+        info = age_ledger(db, age_txs, random.Random(seed ^ 0xA6ED))  # own stream: funding stays seed-identical
+        if aging is not None:
+            aging.update(info)
     # funding block written straight into the ledger (trusted setup, not part of the measurement)
     n_out = n_blocks * txs_per_block * 2
     owners = [(i // 2) % 256 for i in range(n_out)]  # outputs 2j and 2j+1 share an owner
@@ -143,6 +148,68 @@ def _governance_txs(seeded, nxt, n_dv, n_vv, n_rv, rng):
         out.append(tx(d['key'], [d['ballot']], [TransactionOutput(d['addr'], Decimal(d['vote']), O.DELEGATE_VOTING_POWER)],
                       T.REVOKE_AS_DELEGATE))
     return out
+
+
+def age_ledger(db, n_txs: int, rng, chunk: int = 250_000) -> dict:
+    """Trusted bulk aging (untimed setup): ``n_txs`` synthetic confirmed transactions attached to the genesis
+    block, each with two unspent outputs owned by a pool of 1,024 addresses — ``n_txs`` transaction rows and
+    ``2 * n_txs`` UTXO rows in the SQL tables (both UTXO files) and in the UTXO index, the size a long-running
+    mainnet node's ledger has. Rows go through sqlite's executemany in large transactions; the index is
+    loaded in one batch from the same arrays (no SQL read-back)."""
+    import numpy as np
+    from .ledger.utxo import PAYLOAD_DTYPE, TAG_BY_TABLE
+    from .ops import p256 as op
+    from .utils.codec import point_to_string, string_to_bytes
+    t0 = time.perf_counter()
+    genesis = db._q1('SELECT hash FROM blocks WHERE id = 1')[0]
+    pool = [point_to_string(op.public_key(rng.randrange(1, op.oracle.N))) for _ in range(1024)]
+    pool_raw = [string_to_bytes(a) for a in pool]
+    nrng = np.random.default_rng(rng.randrange(1 << 32))
+    recs_all, pay_all = [], []
+    done = 0
+    while done < n_txs:
+        n = min(chunk, n_txs - done)
+        hashes = nrng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+        hexes = [bytes(h).hex() for h in hashes]
+        owners = nrng.integers(0, len(pool), size=(n, 2))
+        amounts = nrng.integers(1, 10 ** 10, size=(n, 2))
+        body = nrng.integers(0, 256, size=(n, 110), dtype=np.uint8)
+        tx_rows, u_rows = [], []
+        for k in range(n):
+            a0, a1 = pool[owners[k, 0]], pool[owners[k, 1]]
+            x0, x1 = int(amounts[k, 0]), int(amounts[k, 1])
+            tx_rows.append((genesis, hexes[k], bytes(body[k]).hex(), '[]', f'["{a0}","{a1}"]', f'[{x0},{x1}]',
+                            '0.000000'))
+            u_rows.append((hexes[k], 0, a0, None))
+            u_rows.append((hexes[k], 1, a1, None))
+        with db.transaction(foreign_keys=False, invalidate=False):
+            db._conn.executemany('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, '
+                                 'outputs_addresses, outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)', tx_rows)
+            db._utxo_exec('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) VALUES (?, ?, ?, ?)',
+                          u_rows)
+        recs = np.zeros((2 * n, 40), dtype=np.uint8)
+        recs[:, :32] = np.repeat(hashes, 2, axis=0)
+        recs[:, 32:36] = np.tile(np.array([[0, 0, 0, 0], [1, 0, 0, 0]], np.uint8), (n, 1))
+        recs[:, 36:40] = np.frombuffer(np.uint32(TAG_BY_TABLE['unspent_outputs']).tobytes(), np.uint8)
+        pay = np.zeros(2 * n, dtype=PAYLOAD_DTYPE)
+        pay['amount'] = amounts.reshape(-1).astype(np.uint64)
+        own = owners.reshape(-1)
+        raw = np.zeros((len(pool), 64), np.uint8)
+        lens = np.zeros(len(pool), np.uint32)
+        for i, r in enumerate(pool_raw):
+            raw[i, :len(r)] = np.frombuffer(r, np.uint8)
+            lens[i] = len(r)
+        pay['addr'] = raw[own]
+        pay['len'] = lens[own]
+        recs_all.append(recs)
+        pay_all.append(pay)
+        done += n
+    t1 = time.perf_counter()
+    live, live_pay = db.utxo.records_payload()
+    db.utxo.reset_records(np.concatenate([live] + recs_all), np.concatenate([live_pay] + pay_all))
+    db._info_cache.clear()
+    return {'aged_txs': n_txs, 'aged_utxos': 2 * n_txs, 'sql_insert_s': round(t1 - t0, 1),
+            'index_load_s': round(time.perf_counter() - t1, 1), 'utxo_index_entries': len(db.utxo)}
 
 
 def _admit_untimed(db, txs_hex):
@@ -273,8 +340,12 @@ async def _run(args, ctx, device, utxo_backend):
     n_blocks = args.steps + args.warmup
     gov = getattr(args, 'governance', False)
     gov_txs = float(getattr(args, 'governance_txs', 0.0) or 0.0)
+    aging = {}
     db, addr, blocks, base_ts = await _setup(n_blocks, args.txs, 1234 + ctx.rank, utxo_backend, device,
-                                             ledger_path=_ledger_path(args, ctx), governance=gov, gov_txs=gov_txs)
+                                             ledger_path=_ledger_path(args, ctx), governance=gov, gov_txs=gov_txs,
+                                             age_txs=int(getattr(args, 'age_txs', 0) or 0), aging=aging)
+    if aging:
+        db.flush()
     gov_probe = await _governance_probe(db) if gov else None
     # mine every header up front (untimed): block b+1's previous hash is sha256(header_b) and the
     # difficulty stays at START_DIFFICULTY below block 100
@@ -296,6 +367,7 @@ async def _run(args, ctx, device, utxo_backend):
         import cProfile
         prof = cProfile.Profile()
     from_mempool = getattr(args, 'from_mempool', False)
+    queue_trace = []  # (journal records not yet in SQL, bytes queued) after each timed block
     untimed = 0.0  # mempool admission of the next block's txs happens inside the wall-clock window
     for b, txs_hex in enumerate(blocks):
         if from_mempool:
@@ -330,6 +402,9 @@ async def _run(args, ctx, device, utxo_backend):
         t2 = time.perf_counter()
         if b >= args.warmup:
             total_txs += len(txs_hex)
+            if db.writer is not None:
+                wst = db.writer.stats()
+                queue_trace.append((wst['submitted'] - wst['applied'], wst['queued_bytes']))
             stages.append({'block_s': t2 - t0, **({'resolve_s': t_resolve} if from_mempool else {}),
                            **manager.last_block_timings,
                            **{k: v for k, v in validate.timings.items() if k.endswith('_s')},
@@ -357,7 +432,8 @@ async def _run(args, ctx, device, utxo_backend):
     writer = db.writer.stats() if db.writer is not None else None
     if writer is not None:
         writer = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in writer.items() if k != 'error'}
-    extra = {'drain_s': drain, 'writer': writer, 'window_unix': [unix_start, time.time()], 'governance': gov_probe}
+    extra = {'drain_s': drain, 'writer': writer, 'window_unix': [unix_start, time.time()], 'governance': gov_probe,
+             'aging': aging or None, 'queue_trace': queue_trace}
     if gov_probe is not None:
         gov_probe['active_inodes_after'] = len(await db.get_active_inodes())
         gov_probe['coinbase_outputs_last_block'] = len(json.loads(
@@ -418,6 +494,7 @@ def run_verify_bench(args, ctx):
         'ledger_writer': extra['writer'],
         'window_unix': extra['window_unix'],
         **({'governance': extra['governance']} if extra['governance'] else {}),
+        **({'aged_ledger': extra['aging'], 'writer_lag_after_block': extra['queue_trace']} if extra['aging'] else {}),
     }
 
 
@@ -547,13 +624,17 @@ async def _run_sync(args, ctx, device, utxo_backend):
     from .models.block import get_transactions_merkle_tree
     from .ledger import fastpath
     n_blocks = args.steps + args.warmup
-    base_ts = int(time.time()) - 10_000
+    # one block per target interval (60 s, manager.py:26): long chains keep the start difficulty at every
+    # 100-block retarget, as a real chain at equilibrium does
+    base_ts = int(time.time()) - 60 * (n_blocks + 10) - 1_000
     seed = 4321 + ctx.rank
     src, addr, blocks, _ = await _setup(n_blocks, args.txs, seed, utxo_backend, device, base_ts=base_ts)
     prev = (await src.get_last_block())['hash']
     for b, txs_hex in enumerate(blocks):
-        content = devnet.mine_header_raw(prev, addr, get_transactions_merkle_tree(txs_hex), base_ts + 10 + b,
-                                         START_DIFFICULTY, device=device)
+        manager.Manager.difficulty = None
+        difficulty, _ = await manager.calculate_difficulty()
+        content = devnet.mine_header_raw(prev, addr, get_transactions_merkle_tree(txs_hex), base_ts + 60 * (b + 1),
+                                         difficulty, device=device)
         errors = []
         if not await fastpath.create_block_from_hex(content, txs_hex, error_list=errors):
             raise RuntimeError(f'source block rejected: {errors}')
@@ -565,7 +646,11 @@ async def _run_sync(args, ctx, device, utxo_backend):
         page += part
     assert len(page) == n_blocks and all(len(p['transactions']) == args.txs + 1 for p in page)
     src.close()
-    dst, _, _, _ = await _setup(n_blocks, args.txs, seed, utxo_backend, device, base_ts=base_ts, make_blocks=False)
+    aging = {}
+    dst, _, _, _ = await _setup(n_blocks, args.txs, seed, utxo_backend, device, base_ts=base_ts, make_blocks=False,
+                                ledger_path=_ledger_path(args, ctx), age_txs=int(getattr(args, 'age_txs', 0) or 0),
+                                aging=aging)
+    dst.flush()
     Database.instance = dst
     manager.Manager.difficulty = None
     from .node.main import create_blocks
@@ -583,14 +668,17 @@ async def _run_sync(args, ctx, device, utxo_backend):
     ctx.barrier()
     wall = ctx.allreduce_max_f(time.perf_counter() - t0)
     assert (await dst.get_last_block())['hash'] == page[-1]['block']['hash']
-    return args.steps * args.txs, wall, fastpath.last_path
+    writer = dst.writer.stats() if dst.writer is not None else {}
+    return args.steps * args.txs, wall, fastpath.last_path, {
+        'aged_ledger': aging or None, 'journal_rotations': writer.get('rotations'),
+        'writer_throttle_s': writer.get('throttle_s'), 'undo_blocks': writer.get('undo_blocks')}
 
 
 def run_sync_bench(args, ctx):
     from .ops.native import gpu_available
     device = 'gpu' if gpu_available() else 'cpu'
     utxo_backend = 'gpu' if device == 'gpu' else 'host'
-    txs, wall, path = asyncio.run(_run_sync(args, ctx, device, utxo_backend))
+    txs, wall, path, extra = asyncio.run(_run_sync(args, ctx, device, utxo_backend))
     total = ctx.allreduce_sum(txs)
     return {
         'metric': 'sync_tx_per_s',
@@ -608,5 +696,6 @@ def run_sync_bench(args, ctx):
         'config': {'model': 'upow chain sync (node.main.create_blocks, trusted coinbase)',
                    'global_batch': total // max(1, args.steps), 'seq_len': args.txs,
                    'parallelism': f'dp{ctx.world}', 'device': device, 'utxo_backend': utxo_backend,
-                   'block_path': path},
+                   'block_path': path, 'ledger': 'file (WAL)' if getattr(args, 'ledger', None) else 'memory'},
+        **{k: v for k, v in extra.items() if v is not None},
     }
