@@ -420,6 +420,10 @@ class Database:
         self._conn.executescript(UTXO_VIEW)
         if os.environ.get('UPOW_LEDGER_WRITER', '1') != '0':
             self._open_writer(cache_mb)
+            if fresh2:
+                # journal records written under the one-file layout were just replayed into the first UTXO
+                # file only (they carry no routing): move their 80-ff rows across like the migration did
+                self._resplit_utxo()
         # next UTXO row id: one counter over both files (row id order = insertion order, as in one table)
         self._utxo_next_rowid = 1 + max(self._conn.execute(f'SELECT COALESCE(MAX(rowid), 0) FROM {s}.unspent_outputs')
                                         .fetchone()[0] for s in UTXO_SCHEMAS)
@@ -456,6 +460,18 @@ class Database:
             c.execute('DROP TABLE main.unspent_outputs')
             c.execute('COMMIT')
             logger.info('ledger: moved unspent_outputs into its own database file')
+
+    def _resplit_utxo(self):
+        c = self._conn
+        if c.execute("SELECT 1 FROM utxo.unspent_outputs WHERE tx_hash >= '8' LIMIT 1").fetchone() is None:
+            return
+        c.execute('BEGIN')
+        c.execute('INSERT INTO utxo2.unspent_outputs (rowid, tx_hash, "index", address, is_stake) '
+                  "SELECT rowid, tx_hash, \"index\", address, is_stake FROM utxo.unspent_outputs "
+                  "WHERE tx_hash >= '8' ORDER BY rowid")
+        c.execute("DELETE FROM utxo.unspent_outputs WHERE tx_hash >= '8'")
+        c.execute('COMMIT')
+        logger.info('ledger: moved replayed one-file-layout UTXO rows into the second file')
 
     def _migrate_utxo_split(self):
         """Ledgers written with one UTXO file: move the rows of hashes 80-ff (with their row ids) into
