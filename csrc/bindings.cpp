@@ -14,6 +14,7 @@ using namespace upow;
 namespace upow {
 void register_txcodec(py::module_& m);  // txcodec.cpp
 void register_ledger_writer(py::module_& m);  // ledger_writer.cpp
+void register_gov_index(py::module_& m);  // gov_index.cpp
 }
 
 static PowJobHost make_job(py::bytes header, uint32_t tmask, uint32_t tword, uint32_t frac_shift,
@@ -49,6 +50,7 @@ PYBIND11_MODULE(_native, m) {
     m.doc() = "upow_amd native core: host C++ crypto + gfx950 HIP kernels";
     register_txcodec(m);
     register_ledger_writer(m);
+    register_gov_index(m);
 
     m.def("sha256", [](py::bytes msg) {
         std::string s = msg;

@@ -312,9 +312,9 @@ async def _governance_probe(db) -> dict:
         db.gov = gov
     idx_stake = await db.get_validators_stake(validator)
     t = db.gov.tables
-    return {'inodes': len(t['inode_registration_output'].rows), 'validators': len(t['validator_registration_output'].rows),
-            'delegates_ballots': len(t['validators_ballot'].rows), 'inode_ballots': len(t['inodes_ballot'].rows),
-            'stake_rows': len(t['stake'].rows), 'active_inodes': len(first),
+    return {'inodes': len(t['inode_registration_output']), 'validators': len(t['validator_registration_output']),
+            'delegates_ballots': len(t['validators_ballot']), 'inode_ballots': len(t['inodes_ballot']),
+            'stake_rows': len(t['stake']), 'active_inodes': len(first),
             'get_active_inodes_first_ms': round((t1 - t0) * 1e3, 3),
             'get_active_inodes_per_block_ms': round((t2 - t1) * 1e3 / n, 4),
             'get_active_inodes_recompute_ms': round((t3 - t2) * 1e3, 3),

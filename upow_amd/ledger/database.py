@@ -37,6 +37,8 @@ from ..utils import coalesce
 from ..utils.logstore import LogStore
 from ..utils.logger import get_logger
 from .governance import GOV_TABLES, STAKE, GovernanceIndex
+from .governance import TID as GOV_TID
+from .governance import _row_args as _gov_row
 from .mempool import MempoolIndex
 from .utxo import FLAG_STAKE, PAYLOAD_DTYPE, TAG_BY_TABLE, UtxoIndex, make_payload
 
@@ -1689,24 +1691,23 @@ class Database:
                                   np.arange(base, base + len(coinbase_outputs), dtype=np.int64)],
                           len(coinbase_outputs), None, None, None))
         tables = {'blocks', 'transactions', 'unspent_outputs'}
-        gov_created, gov_spent = {}, {}
+        gov_spent = {}
         if gov is not None:
-            addr_at = _arena_reader(out_addr_spec)
             for table in self._GOV_INSERT_ORDER:
                 sel = np.nonzero(out_tag == TAG_BY_TABLE[table])[0]
                 if len(sel):
-                    rows = [(bytes(out_txid[o]).hex(), int(out_index[o]), addr_at(o)) for o in sel.tolist()]
-                    gov_created[table] = (sel, rows)
                     stmts.append((f'INSERT INTO {table} (tx_hash, "index", address) VALUES (?, ?, ?)',
-                                  [[r[0] for r in rows], np.array([r[1] for r in rows], np.int64), [r[2] for r in rows]],
-                                  len(rows), None, None, None))
+                                  [('hex32', np.ascontiguousarray(out_txid[sel]), 32, 0),
+                                   np.ascontiguousarray(out_index[sel], dtype=np.int64),
+                                   _arena_subset(out_addr_spec, sel)],
+                                  len(sel), None, None, None))
                     tables.add(table)
             for table in self._SPEND_ORDER:
                 if table == 'unspent_outputs':
                     continue
                 sel = np.nonzero(in_tag == TAG_BY_TABLE[table])[0]
                 if len(sel):
-                    gov_spent[table] = [(bytes(in_keys[j, :32]).hex(), int(in_idx[j])) for j in sel.tolist()]
+                    gov_spent[table] = sel
                     tables.add(table)
         self.checkpoint('outputs')
         mempool = n and not self._mempool_empty()
@@ -1716,10 +1717,10 @@ class Database:
                           self._key_order(txids), 'SELECT EXISTS(SELECT 1 FROM pending_transactions)', None))
 
         def spend_stmt(table):
-            keys = gov_spent[table]
+            sel = gov_spent[table]
+            ks = np.ascontiguousarray(in_keys[sel])
             stmts.append((f'DELETE FROM {table} WHERE tx_hash = ? AND "index" = ?',
-                          [[h for h, _ in keys], np.array([i for _, i in keys], np.int64)], len(keys), None, None,
-                          len(keys)))
+                          [('hex32', ks, 40, 0), np.ascontiguousarray(in_idx[sel])], len(sel), None, None, len(sel)))
         if 'inode_registration_output' in gov_spent:
             spend_stmt('inode_registration_output')
         sel_u = np.nonzero(in_tag == tag_u)[0] if gov is not None else None
@@ -1775,49 +1776,26 @@ class Database:
         if n:
             self._mempool_confirm(bool(mempool), txids=np.asarray(tx_cols[0][1]).reshape(-1, 32), in_keys=in_keys,
                                   block_seq=seq)
-        if self.gov is not None and n_in:
+        if self.gov is not None and gov is not None:
+            tg = perf_counter()
+            _, blob, off = out_addr_spec
+            off = np.frombuffer(off, dtype=np.int64) if isinstance(off, (bytes, bytearray)) else np.asarray(off, np.int64)
+            with self.gov.lock:
+                # governance/stake outputs in, governance and staked spends out (csrc/gov_index.cpp apply_block)
+                self.gov.store.apply_block(
+                    np.ascontiguousarray(gov['out_type'], dtype=np.uint8), np.ascontiguousarray(tx_cols[0][1]),
+                    np.ascontiguousarray(gov['out_tx'], dtype=np.int32), np.ascontiguousarray(gov['out_start'], np.int32),
+                    np.ascontiguousarray(out_amount, dtype=np.uint64), np.ascontiguousarray(out_addr, dtype=np.uint8),
+                    np.ascontiguousarray(out_len, dtype=np.uint8), bytes(blob), np.ascontiguousarray(off),
+                    np.ascontiguousarray(gov['in_start'], np.int32), np.ascontiguousarray(spent_payload).view(np.uint8),
+                    in_keys, np.ascontiguousarray(gov['in_tag'], dtype=np.uint8), n, int(b['timestamp']))
+                self.gov.version += 1
+            self.last_gov_index_s = perf_counter() - tg
+        elif self.gov is not None and n_in:
             hit = self._stake_spent(spent, spent_payload)
             if hit:
                 self.gov.removed(STAKE, hit)
-        if self.gov is not None and gov is not None:
-            tg = perf_counter()
-            self._gov_apply_native(gov, gov_created, gov_spent, out_txid, out_index, out_amount, out_addr_spec,
-                                   int(b['timestamp']))
-            self.last_gov_index_s = perf_counter() - tg
         return seq
-
-    def _gov_apply_native(self, gov: dict, created: dict, spent: dict, out_txid, out_index, out_amount, out_addr_spec,
-                          block_ts: int):
-        """Governance-index update of a native-path block from its own columns (no SQL read-back): the rows
-        GovernanceIndex.added would read through the reference's joins — address, amount
-        (outputs_amounts[index]), voter (inputs_addresses[index], the reference's subscript) and the block
-        timestamp — for the created governance/stake outputs; spent governance rows leave their tables."""
-        g = self.gov
-        ia_blob, ia_off = gov['in_json']
-        ia_off = np.frombuffer(ia_off, dtype=np.int64) if isinstance(ia_off, (bytes, bytearray)) else ia_off
-        ia_cache = {}
-        out_tx = gov['out_tx']
-
-        def voter(o):
-            k = int(out_tx[o])
-            lst = ia_cache.get(k)
-            if lst is None:
-                lst = ia_cache[k] = json.loads(bytes(ia_blob[int(ia_off[k]):int(ia_off[k + 1])]))
-            return _at(lst, int(out_index[o]))
-        stake_sel = np.nonzero(gov['out_type'] == int(OutputType.STAKE))[0]
-        addr_at = _arena_reader(out_addr_spec)
-        with g.lock:
-            for table, keys in spent.items():
-                g.removed(table, keys)
-            for o in stake_sel.tolist():
-                g.tables[STAKE].add((bytes(out_txid[o]).hex(), int(out_index[o])), addr_at(o), int(out_amount[o]),
-                                    voter(o), block_ts)
-            for table in self._GOV_INSERT_ORDER:
-                if table in created:
-                    sel, rows = created[table]
-                    for o, r in zip(sel.tolist(), rows):
-                        g.tables[table].add((r[0], r[1]), r[2], int(out_amount[o]), voter(o), block_ts)
-            g.version += 1
 
     def _stake_spent(self, spent: np.ndarray, spent_payload: np.ndarray) -> List[Tuple[str, int]]:
         """Which of a block's spent outpoints (n x 40 records) are staked outputs: the stake flag their index
@@ -1953,12 +1931,12 @@ class Database:
                 keys = spends.get(table)
                 if keys:
                     g.removed(STAKE if table == 'unspent_outputs' else table, keys)
-            for o in outs['unspent_outputs']:
-                if o[3] is True or o[3] == 1:
-                    g.tables[STAKE].add((o[0], o[1]), o[2], _at(am[o[0]], o[1]), _at(ia[o[0]], o[1]), block_ts)
-            for table in self._GOV_INSERT_ORDER:
-                for o in outs[table]:
-                    g.tables[table].add((o[0], o[1]), o[2], _at(am[o[0]], o[1]), _at(ia[o[0]], o[1]), block_ts)
+            for table in (STAKE, *self._GOV_INSERT_ORDER):
+                src = outs['unspent_outputs'] if table == STAKE else outs[table]
+                batch = [_gov_row((o[0], o[1]), o[2], _at(am[o[0]], o[1]), _at(ia[o[0]], o[1]), block_ts)
+                         for o in src if table != STAKE or o[3] is True or o[3] == 1]
+                if batch:
+                    g.store.add_rows(GOV_TID[table], batch)
             g.version += 1
 
     def _undo_blocks_in_index(self, from_id: int, tip: int):
@@ -2541,9 +2519,7 @@ class Database:
         all_forms = [f for d in data.values() for f in d['formats']]
         if self.gov is not None:
             stake_map = defaultdict(Decimal)
-            rows = self.gov.tables[STAKE].rows
-            for h, i, a in self.gov.amount_rows(STAKE, all_forms, check_pending_txs):
-                address = rows[(h, i)][0]
+            for h, i, a, address in self.gov.address_rows(STAKE, all_forms, check_pending_txs):
                 original = next(k for k, d in data.items() if address in d['formats'])
                 stake_map[original] += Decimal(a) / SMALLEST
             if check_pending_txs:
@@ -2627,8 +2603,7 @@ class Database:
 
     async def get_inode_count(self, check_pending_txs: bool = False):
         if self.gov is not None:
-            pend = self.gov.pending_spent(check_pending_txs)
-            return [{'count': sum(1 for k in self.gov.tables['inode_registration_output'].rows if k not in pend)}]
+            return [{'count': self.gov.inode_count(check_pending_txs)}]
         rows = self._q('SELECT tx_hash, "index" FROM inode_registration_output')
         pend = self._pending_spent_set() if check_pending_txs else set()
         return [{'count': sum(1 for r in rows if (r[0], r[1]) not in pend)}]

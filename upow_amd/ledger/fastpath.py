@@ -308,7 +308,7 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     gov_cols = None
     if bg.any:
         gov_cols = {'out_tag': bg.output_tags(TAG_BY_TABLE), 'out_type': out_type, 'in_tag': in_tag,
-                    'gov_tx': bg.gov, 'out_tx': out_tx, 'in_json': in_json}
+                    'gov_tx': bg.gov, 'out_tx': out_tx, 'out_start': out_start, 'in_start': in_start}
 
     async def apply(block_hash, address, random, block_reward, content_time, coinbase_transaction):
         ta = perf_counter()
