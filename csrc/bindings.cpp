@@ -1,4 +1,5 @@
 // pybind11 module `upow_amd._native`: the MI355X-native core (host C++ + gfx950 HIP kernels).
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -240,6 +241,13 @@ PYBIND11_MODULE(_native, m) {
         uint64_t n = 0;
         { py::gil_scoped_release rel; d = utxo_set_hash(h, tag, &n); }
         return py::make_tuple(py::bytes(reinterpret_cast<const char*>(d.data()), d.size()), n);
+    });
+    m.def("utxo_set_message", [](int64_t h, uint32_t tag) {
+        auto* v = new std::vector<uint8_t>();
+        uint64_t n = 0;
+        { py::gil_scoped_release rel; *v = utxo_set_message(h, tag, &n); }
+        py::capsule own(v, [](void* p) { delete static_cast<std::vector<uint8_t>*>(p); });
+        return py::array_t<uint8_t>({py::ssize_t(v->size())}, {py::ssize_t(1)}, v->data(), own);
     });
     m.def("utxo_address_scan", [](int64_t h, py::bytes addr, uint32_t tag_mask, uint32_t stake_sel) {
         std::string a = addr;

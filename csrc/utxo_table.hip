@@ -678,7 +678,7 @@ __global__ __launch_bounds__(256) void set_message_kernel(const UtxoKeyRec* __re
     o[32] = uint8_t(r.index);
 }
 
-std::vector<uint8_t> utxo_set_hash(int64_t h, uint32_t tag, uint64_t* count_out) {
+std::vector<uint8_t> utxo_set_message(int64_t h, uint32_t tag, uint64_t* count_out) {
     std::lock_guard<std::mutex> lk(g_ut_mu);
     UtxoTableDev& t = table(h);
     DevBuf<UtxoKeyRec> recs(t.cap);
@@ -713,6 +713,12 @@ std::vector<uint8_t> utxo_set_hash(int64_t h, uint32_t tag, uint64_t* count_out)
         uck(hipGetLastError(), "set_message_kernel");
         node_d2h(msg.data(), d_msg.p, msg.size(), "d2h message");
     }
+    return msg;
+}
+
+// the sequential SHA-256 tail runs without the table lock: block application is not held up by it
+std::vector<uint8_t> utxo_set_hash(int64_t h, uint32_t tag, uint64_t* count_out) {
+    const std::vector<uint8_t> msg = utxo_set_message(h, tag, count_out);
     std::vector<uint8_t> digest(32);
     host_sha256(msg.data(), msg.size(), digest.data());
     return digest;

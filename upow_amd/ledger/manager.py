@@ -529,7 +529,7 @@ async def _finalize_block(block_no: int, block_content: str, fees, n_txs: int, a
     logger.info(f'Added {n_txs} transactions in block {block_no}. Reward: {block_reward}, Fees: {fees} '
                 f'in {perf_counter() - create_start_time:.3f} seconds')
     if block_no % 10 == 0:
-        logger.info(f'unspent_outputs_hash on block no. {block_no}: {await database.get_unspent_outputs_hash()}')
+        await _log_utxo_hash(database, block_no)
     _maybe_snapshot(database, block_no)
     Manager.difficulty = None
     try:
@@ -539,6 +539,31 @@ async def _finalize_block(block_no: int, block_content: str, fees, n_txs: int, a
     except Exception as e:
         logger.error(f'Error in creating block: {block_no} {str(e)}')
     return True
+
+
+_K12_POOL = None
+
+
+async def _log_utxo_hash(database, block_no: int):
+    """The K12 log line every 10 blocks (reference manager.py:740-741, 833-834). Computed only when the line
+    is emitted. The sorted outpoint message is taken at this block (under the index lock, on the device);
+    the sequential SHA-256 over it (165 MB at 5 M UTXOs) runs on a worker thread, so the next block does
+    not wait for it."""
+    global _K12_POOL
+    import logging
+    if not logger.isEnabledFor(logging.INFO):
+        return
+    if os.environ.get('UPOW_UTXO_HASH_SQL', '0') == '1':
+        logger.info(f'unspent_outputs_hash on block no. {block_no}: {await database.get_unspent_outputs_hash()}')
+        return
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+    from .utxo import TAG_BY_TABLE
+    msg = database.utxo.set_message(TAG_BY_TABLE['unspent_outputs'])
+    if _K12_POOL is None:
+        _K12_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix='upow-k12')
+    _K12_POOL.submit(lambda: logger.info(f'unspent_outputs_hash on block no. {block_no}: '
+                                         f'{hashlib.sha256(msg).hexdigest()}'))
 
 
 SNAPSHOT_EVERY = int(os.environ.get('UPOW_SNAPSHOT_EVERY', '1000'))
@@ -603,8 +628,7 @@ async def _finalize_sync_block(block_no: int, block_content: str, fees, n_txs: i
     logger.info(f'Added {n_txs} transactions in block {block_no}. Reward: {block_reward}, Fees: {fees} '
                 f'in {perf_counter() - create_start_time:.3f} seconds')
     if block_no % 10 == 0:
-        logger.info(f'unspent_outputs_hash on block no. {block_no}: '
-                    f'{await Database.instance.get_unspent_outputs_hash()}')
+        await _log_utxo_hash(Database.instance, block_no)
     _maybe_snapshot(Database.instance, block_no)
     Manager.difficulty = None
     return True

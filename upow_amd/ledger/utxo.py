@@ -448,18 +448,22 @@ class UtxoIndex:
         return tags, pay, dup_of, ins - outs, miss, int((dup_of > 0).sum())
 
     @_locked
-    def set_hash(self, tag: int = 0) -> str:
-        """K12 from the index: SHA-256 over (txid || index byte) of table ``tag`` sorted by (txid, index)
-        — byte-identical to ``Database.get_unspent_outputs_hash`` (reference database.py:827-830).
+    def set_message(self, tag: int = 0) -> np.ndarray:
+        """K12's message: (txid || index byte) of every outpoint of table ``tag`` sorted by (txid, index).
         GPU backend: compaction + stable LSD radix sort + message gather on the device."""
-        import hashlib
         if isinstance(self.be, _GpuBackend):
-            digest, _ = self.be.L.utxo_set_hash(self.be.h, tag)
-            return digest.hex()
+            return self.be.L.utxo_set_message(self.be.h, tag)
         recs = self.records()
         recs = recs[recs[:, 36:40].copy().view(np.uint32).ravel() == tag]
-        payload = np.concatenate([recs[:, :32], recs[:, 32:33]], axis=1)  # index byte (the reference's bytes([i]))
-        return hashlib.sha256(payload.tobytes()).hexdigest()
+        # records() is in canonical (txid, index) order; index byte = the reference's bytes([i])
+        return np.ascontiguousarray(np.concatenate([recs[:, :32], recs[:, 32:33]], axis=1)).ravel()
+
+    def set_hash(self, tag: int = 0) -> str:
+        """K12 from the index: SHA-256 over :meth:`set_message` — byte-identical to
+        ``Database.get_unspent_outputs_hash`` (reference database.py:827-830). The sequential hash tail
+        runs outside the index lock (hashlib releases the GIL), so block application is not held up by it."""
+        import hashlib
+        return hashlib.sha256(self.set_message(tag)).hexdigest()
 
     def __len__(self):
         return len(self.be)
