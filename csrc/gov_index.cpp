@@ -587,10 +587,12 @@ class GovStore {
     }
 
     // ---- block apply (native path): governance/stake outputs in, governance spends out
+    // ``in_str``/``in_off``: each input's owner as the tx row's inputs_addresses column holds it (compressed
+    // base58 of the spent output's address; txcodec input_address_strings(per_input=True))
     py::dict apply_block(py::buffer out_type_b, py::buffer txid_b, py::buffer out_tx_b, py::buffer out_start_b,
                          py::buffer out_amount_b, py::buffer out_addr_b, py::buffer out_len_b, py::bytes addr_blob,
                          py::buffer addr_off_b, py::buffer in_start_b, py::buffer pay_b, py::buffer in_keys_b,
-                         py::buffer in_tag_b, int64_t n, int64_t block_ts) {
+                         py::buffer in_tag_b, py::bytes in_str, py::buffer in_off_b, int64_t n, int64_t block_ts) {
         const int32_t* os = buf<int32_t>(out_start_b, size_t(n) + 1, "out_start");
         const int32_t* is = buf<int32_t>(in_start_b, size_t(n) + 1, "in_start");
         const int64_t n_out = os[n], n_in = is[n];
@@ -604,13 +606,18 @@ class GovStore {
         const uint8_t* pay = buf<uint8_t>(pay_b, size_t(n_in) * 80, "payload");
         const uint8_t* ik = buf<uint8_t>(in_keys_b, size_t(n_in) * 40, "in_keys");
         const uint8_t* itag = buf<uint8_t>(in_tag_b, size_t(n_in), "in_tag");
-        std::string blob = addr_blob;
+        const int64_t* ioff = buf<int64_t>(in_off_b, size_t(n_in) + 1, "input string offsets");
+        const std::string blob = addr_blob, istr = in_str;
+        if (ioff[n_in] > int64_t(istr.size())) throw std::invalid_argument("input strings: offsets past the blob");
         // spends leave their tables (UTXO tags: 0 unspent_outputs -> staked rows, 1..6 governance tables)
         static const int kTagTid[7] = {STAKE, INODE, VALIDATOR, VVP, DVP, VBALLOT, IBALLOT};
         int64_t removed = 0, added = 0;
         for (int64_t j = 0; j < n_in; ++j) {
             const int tag = itag[j];
             if (tag > 6) continue;
+            uint32_t flags;
+            std::memcpy(&flags, pay + 80 * j + 12, 4);
+            if (tag == 0 && !(flags & 1)) continue;  // an unstaked output: not in the stake table
             uint32_t idx;
             std::memcpy(&idx, ik + 40 * j + 32, 4);
             removed += erase(kTagTid[tag], key_of(ik + 40 * j, idx));
@@ -638,7 +645,7 @@ class GovStore {
                 Pt vp;
                 if (point_key(pay + 80 * j + 16, len, vp)) {
                     row.vpt = vp;
-                    row.voter = b58_of_pt(vp);
+                    row.voter.assign(istr.data() + ioff[j], size_t(ioff[j + 1] - ioff[j]));
                     row.f |= HAS_VOTER;
                 }
             }

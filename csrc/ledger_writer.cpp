@@ -224,6 +224,16 @@ void utf8_list(py::list lst, std::vector<const char*>& ptr, std::vector<int64_t>
     }
 }
 
+// a row selection int64[n] (non-negative; the caller checks the upper bound against its column)
+const int64_t* row_selection(py::handle h, int64_t n) {
+    py::buffer_info bi = h.cast<py::buffer>().request();
+    if (bi.itemsize != 8 || bi.size != n) throw std::invalid_argument("row selection must be int64[n]");
+    const int64_t* sel = static_cast<const int64_t*>(bi.ptr);
+    for (int64_t r = 0; r < n; ++r)
+        if (sel[r] < 0) throw std::out_of_range("row selection");
+    return sel;
+}
+
 void encode_col(Out& o, py::handle spec, int64_t n) {
     if (spec.is_none()) {
         o.u8(K_NULL);
@@ -258,30 +268,51 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
             py::gil_scoped_release nogil;
             encode_text_rows(o, n, ptr, len, idx);
         } else if (tag == "hex32") {
+            // ('hex32', raw, stride, offset[, sel int64[n]]): 32 raw bytes per row, optionally rows sel of raw
             py::buffer_info bi = t[1].cast<py::buffer>().request();
             const uint8_t* raw = static_cast<const uint8_t*>(bi.ptr);
             const int64_t raw_n = bi.size * bi.itemsize, stride = t[2].cast<int64_t>(), offset = t[3].cast<int64_t>();
-            if (offset < 0 || stride < 0 || (n > 0 && (n - 1) * stride + offset + 32 > raw_n))
+            const int64_t* sel = t.size() > 4 ? row_selection(t[4], n) : nullptr;
+            int64_t top = n - 1;
+            if (sel) {
+                top = -1;
+                for (int64_t r = 0; r < n; ++r) top = std::max(top, sel[r]);
+            }
+            if (offset < 0 || stride < 0 || (n > 0 && top * stride + offset + 32 > raw_n))
                 throw std::out_of_range("hex32 column out of range");
             o.u8(K_HEX32);
             py::gil_scoped_release nogil;
             o.b.reserve(o.b.size() + size_t(n) * 32);
-            for (int64_t r = 0; r < n; ++r) o.raw(raw + r * stride + offset, 32);
+            for (int64_t r = 0; r < n; ++r) o.raw(raw + (sel ? sel[r] : r) * stride + offset, 32);
         } else if (tag == "arena") {
+            // ('arena', blob, offsets int64[N + 1][, sel int64[n]]): text rows, optionally rows sel of the arena
             py::buffer_info bb = t[1].cast<py::buffer>().request(), ob = t[2].cast<py::buffer>().request();
-            if (ob.size * ob.itemsize != 8 * (n + 1)) throw std::invalid_argument("arena offsets must be int64[n + 1]");
+            const int64_t* sel = t.size() > 3 ? row_selection(t[3], n) : nullptr;
+            const int64_t rows = ob.size * ob.itemsize / 8 - 1;
+            if (sel ? rows < 0 || ob.size * ob.itemsize % 8 : ob.size * ob.itemsize != 8 * (n + 1))
+                throw std::invalid_argument("arena offsets must be int64[n + 1]");
             const char* blob = static_cast<const char*>(bb.ptr);
             const int64_t* aoff = static_cast<const int64_t*>(ob.ptr);
             const int64_t blen = bb.size * bb.itemsize;
-            for (int64_t i = 0; i < n; ++i)
+            for (int64_t i = 0; i < (sel ? rows : n); ++i)
                 if (aoff[i] < 0 || aoff[i + 1] < aoff[i] || aoff[i + 1] > blen) throw std::out_of_range("arena offsets");
+            if (sel)
+                for (int64_t r = 0; r < n; ++r)
+                    if (sel[r] >= rows) throw std::out_of_range("arena row selection");
             o.u8(K_TEXT);
             o.u8(0);
             py::gil_scoped_release nogil;
             std::vector<int64_t> off(size_t(n) + 1);
-            for (int64_t i = 0; i <= n; ++i) off[size_t(i)] = aoff[i] - aoff[0];
-            o.raw(off.data(), off.size() * 8);
-            o.raw(blob + aoff[0], size_t(aoff[n] - aoff[0]));
+            if (!sel) {
+                for (int64_t i = 0; i <= n; ++i) off[size_t(i)] = aoff[i] - aoff[0];
+                o.raw(off.data(), off.size() * 8);
+                o.raw(blob + aoff[0], size_t(aoff[n] - aoff[0]));
+            } else {
+                for (int64_t r = 0; r < n; ++r) off[size_t(r) + 1] = off[size_t(r)] + aoff[sel[r] + 1] - aoff[sel[r]];
+                o.raw(off.data(), off.size() * 8);
+                o.b.reserve(o.b.size() + size_t(off[size_t(n)]));
+                for (int64_t r = 0; r < n; ++r) o.raw(blob + aoff[sel[r]], size_t(aoff[sel[r] + 1] - aoff[sel[r]]));
+            }
         } else {
             throw std::invalid_argument("unknown column tag " + tag);
         }

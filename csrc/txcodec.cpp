@@ -601,7 +601,8 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
 // Canonical compressed address strings for spent outputs (database._input_address): 33-byte
 // addresses keep x with the normalised prefix, 64-byte ones take the parity of y. Returns the
 // per-tx inputs_addresses JSON column as a text arena (blob, int64 offsets[n_tx + 1]).
-static py::tuple input_address_strings(py::bytes addrs64, py::bytes lens, py::bytes in_start_b, int threads) {
+static py::tuple input_address_strings(py::bytes addrs64, py::bytes lens, py::bytes in_start_b, int threads,
+                                       bool per_input) {
     std::string a = addrs64, l = lens, s = in_start_b;
     const size_t n_in = l.size();
     const size_t n_tx = s.size() / 4 - 1;
@@ -643,7 +644,13 @@ static py::tuple input_address_strings(py::bytes addrs64, py::bytes lens, py::by
         j += ']';
         json.add(j.data(), j.size());
     }
-    return json.py();
+    if (!per_input) return json.py();
+    // also each input's string on its own (the governance store's ballot voters)
+    Arena each;
+    each.blob.reserve(n_in * 45);
+    for (size_t i = 0; i < n_in; ++i) each.add(out[i].data(), out[i].size());
+    py::tuple jt = json.py(), et = each.py();
+    return py::make_tuple(jt[0], jt[1], et[0], et[1]);
 }
 
 // ---- column helpers for the bulk ledger writes (ledger/fastpath.py)
@@ -817,7 +824,7 @@ void register_txcodec(py::module_& m) {
     m.def("decode_block_txs", &decode_block_txs, py::arg("hexes"), py::arg("threads") = 8,
           "Decode, canonicalise and hash a block's transactions (see csrc/txcodec.cpp)");
     m.def("input_address_strings", &input_address_strings, py::arg("addrs64"), py::arg("lens"), py::arg("in_start"),
-          py::arg("threads") = 8);
+          py::arg("threads") = 8, py::arg("per_input") = false);
 }
 
 }  // namespace upow

@@ -240,14 +240,16 @@ def _expand_col(spec, n: int) -> list:
         kind = spec[0]
         if kind == 'gather':
             return [spec[1][i] for i in np.asarray(spec[2]).tolist()]
-        if kind == 'hex32':
+        if kind == 'hex32':  # optional 5th element: the rows to take
             raw = np.frombuffer(spec[1], dtype=np.uint8)
             stride, off = spec[2], spec[3]
-            return [bytes(raw[r * stride + off:r * stride + off + 32]).hex() for r in range(n)]
-        if kind == 'arena':
+            rows = np.asarray(spec[4]).tolist() if len(spec) > 4 else range(n)
+            return [bytes(raw[r * stride + off:r * stride + off + 32]).hex() for r in rows]
+        if kind == 'arena':  # optional 4th element: the rows to take
             blob = bytes(spec[1]).decode()  # ASCII: byte offsets are character offsets
             off = np.frombuffer(spec[2], dtype=np.int64).tolist()
-            return [blob[off[i]:off[i + 1]] for i in range(n)]
+            rows = np.asarray(spec[3]).tolist() if len(spec) > 3 else range(n)
+            return [blob[off[i]:off[i + 1]] for i in rows]
         raise ValueError(f'unknown column kind {kind}')
     if isinstance(spec, np.ndarray):
         return spec.tolist()
@@ -268,26 +270,6 @@ _FK_PARENTS = {t: ('transactions', 'blocks') for t in ('unspent_outputs', 'pendi
                                                        'address_transactions', *OUTPUT_TABLES[1:])}
 _FK_PARENTS['transactions'] = ('blocks',)
 _SQL_TABLES: Dict[Tuple[str, bool], Optional[frozenset]] = {}
-
-
-def _arena_reader(spec):
-    """Row accessor of an ('arena', blob, int64 offsets) text column: row o -> str."""
-    _, blob, off = spec
-    off = np.frombuffer(off, dtype=np.int64) if isinstance(off, (bytes, bytearray)) else np.asarray(off, np.int64)
-    mv = memoryview(blob)
-    return lambda o: str(mv[int(off[o]):int(off[o + 1])], 'ascii')
-
-
-def _arena_subset(spec, sel: np.ndarray):
-    """('arena', blob, int64 offsets[n + 1]) restricted to the rows ``sel`` (vectorised byte gather)."""
-    _, blob, off = spec
-    off = np.frombuffer(off, dtype=np.int64) if isinstance(off, (bytes, bytearray)) else np.asarray(off, np.int64)
-    data = np.frombuffer(blob, dtype=np.uint8)
-    starts, lens = off[sel], off[sel + 1] - off[sel]
-    new_off = np.zeros(len(sel) + 1, dtype=np.int64)
-    np.cumsum(lens, out=new_off[1:])
-    idx = np.repeat(starts - new_off[:-1], lens) + np.arange(int(new_off[-1]), dtype=np.int64)
-    return ('arena', data[idx].tobytes(), new_off)
 
 
 def _tables_of(sql: str, write: bool) -> Optional[frozenset]:
@@ -1620,6 +1602,7 @@ class Database:
         governance index follows from these columns — the object path's write set (apply_object_block) in
         the same statement order, so both paths leave identical tables.
         Returns the journal sequence number (0 without the native writer: written synchronously)."""
+        ts = [perf_counter()]  # stage clock: records, statements, encode, journal, index, mempool, governance
         out_index, out_addr_spec, out_txid, out_amount, out_addr, out_len = out_cols
         n_out, n_in = len(out_index), len(in_keys)
         tag_u = TAG_BY_TABLE['unspent_outputs']
@@ -1649,6 +1632,10 @@ class Database:
         spent[:, 36:40] = np.ascontiguousarray(in_tag).reshape(-1, 1).view(np.uint8)
         in_idx = in_keys[:, 32:36].copy().view(np.uint32).ravel().astype(np.int64)
         in_order = self._key_order(in_keys) if n_in else None
+        if gov is not None and n_in:
+            in_order_rank = np.empty(n_in, dtype=np.int64)  # position of each input in the key order
+            in_order_rank[in_order] = np.arange(n_in, dtype=np.int64)
+        ts.append(perf_counter())
 
         # ---- statements (schema.sql write set of one block)
         b = block_row
@@ -1674,13 +1661,13 @@ class Database:
                                       np.arange(base, base + n_out, dtype=np.int64)],
                               n_out, None, None, None))
         else:
+            out_txid_c = np.ascontiguousarray(out_txid)
             sel = np.nonzero(out_tag == tag_u)[0]
             if len(sel):
                 base = self._utxo_rowids(len(sel))
                 stake = (gov['out_type'][sel] == int(OutputType.STAKE)).astype(np.int64)
-                stmts.append((ins_u, [('hex32', np.ascontiguousarray(out_txid[sel]), 32, 0),
-                                      np.ascontiguousarray(out_index[sel], dtype=np.int64),
-                                      _arena_subset(out_addr_spec, sel), stake,
+                stmts.append((ins_u, [('hex32', out_txid_c, 32, 0, sel), np.ascontiguousarray(out_index[sel], dtype=np.int64),
+                                      (*out_addr_spec, sel), stake,
                                       np.arange(base, base + len(sel), dtype=np.int64)],
                               len(sel), None, None, None))
         if coinbase_outputs:
@@ -1697,9 +1684,8 @@ class Database:
                 sel = np.nonzero(out_tag == TAG_BY_TABLE[table])[0]
                 if len(sel):
                     stmts.append((f'INSERT INTO {table} (tx_hash, "index", address) VALUES (?, ?, ?)',
-                                  [('hex32', np.ascontiguousarray(out_txid[sel]), 32, 0),
-                                   np.ascontiguousarray(out_index[sel], dtype=np.int64),
-                                   _arena_subset(out_addr_spec, sel)],
+                                  [('hex32', out_txid_c, 32, 0, sel), np.ascontiguousarray(out_index[sel], dtype=np.int64),
+                                   (*out_addr_spec, sel)],
                                   len(sel), None, None, None))
                     tables.add(table)
             for table in self._SPEND_ORDER:
@@ -1718,9 +1704,9 @@ class Database:
 
         def spend_stmt(table):
             sel = gov_spent[table]
-            ks = np.ascontiguousarray(in_keys[sel])
             stmts.append((f'DELETE FROM {table} WHERE tx_hash = ? AND "index" = ?',
-                          [('hex32', ks, 40, 0), np.ascontiguousarray(in_idx[sel])], len(sel), None, None, len(sel)))
+                          [('hex32', in_keys, 40, 0, sel), np.ascontiguousarray(in_idx[sel])], len(sel), None, None,
+                          len(sel)))
         if 'inode_registration_output' in gov_spent:
             spend_stmt('inode_registration_output')
         sel_u = np.nonzero(in_tag == tag_u)[0] if gov is not None else None
@@ -1728,10 +1714,9 @@ class Database:
             stmts.append(('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
                           [('hex32', in_keys, 40, 0), in_idx], n_in, in_order, None, n_in))
         elif gov is not None and len(sel_u):
-            ku = np.ascontiguousarray(in_keys[sel_u])
             stmts.append(('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
-                          [('hex32', ku, 40, 0), np.ascontiguousarray(in_idx[sel_u])], len(sel_u),
-                          self._key_order(ku), None, len(sel_u)))
+                          [('hex32', in_keys, 40, 0, sel_u), np.ascontiguousarray(in_idx[sel_u])], len(sel_u),
+                          np.argsort(in_order_rank[sel_u], kind='stable').astype(np.int64), None, len(sel_u)))
         for table in self._SPEND_ORDER[2:]:
             if table in gov_spent:
                 spend_stmt(table)
@@ -1745,14 +1730,17 @@ class Database:
         tables |= {'address_transactions', 'address_index_state'}
 
         seq = 0
+        ts.append(perf_counter())
         if self.writer is not None:
             enc = [self.encode(*st) for st in stmts]
+            ts.append(perf_counter())
             meta = b''.join((bytes.fromhex(b['hash']), struct.pack('<qII', int(b['id']), n_out + len(cb_keys), n_in),
                              memoryview(recs),
                              memoryview(np.ascontiguousarray(cb_recs)), memoryview(spent),
                              memoryview(np.ascontiguousarray(spent_payload)).cast('B')))
             seq = self.submit_batch(enc, tables, meta, int(b['id']))
         else:
+            ts.append(perf_counter())
             with self.transaction(foreign_keys=False):
                 for sql, cols, nn, order, guard, expect in stmts:
                     if guard is not None and not self._q1(guard)[0]:
@@ -1761,11 +1749,13 @@ class Database:
                     if expect is not None and done != expect:
                         logger.error(f'native block apply: {done} of {expect} rows changed [{sql[:40]}]')
         # ---- the index and the chain-tip cache follow the commit point
+        ts.append(perf_counter())
         self.utxo.insert_records(recs, pay)
         if len(cb_keys):
             self.utxo.insert_records(cb_recs, cb_pay)
         if n_in:
             self.utxo.erase_records(spent)
+        ts.append(perf_counter())
         tip = dict(b)
         tip['difficulty'], tip['reward'] = Decimal(tip['difficulty']), Decimal(tip['reward'])
         self._tip_gen += 1
@@ -1776,6 +1766,7 @@ class Database:
         if n:
             self._mempool_confirm(bool(mempool), txids=np.asarray(tx_cols[0][1]).reshape(-1, 32), in_keys=in_keys,
                                   block_seq=seq)
+        ts.append(perf_counter())
         if self.gov is not None and gov is not None:
             tg = perf_counter()
             _, blob, off = out_addr_spec
@@ -1788,13 +1779,17 @@ class Database:
                     np.ascontiguousarray(out_amount, dtype=np.uint64), np.ascontiguousarray(out_addr, dtype=np.uint8),
                     np.ascontiguousarray(out_len, dtype=np.uint8), bytes(blob), np.ascontiguousarray(off),
                     np.ascontiguousarray(gov['in_start'], np.int32), np.ascontiguousarray(spent_payload).view(np.uint8),
-                    in_keys, np.ascontiguousarray(gov['in_tag'], dtype=np.uint8), n, int(b['timestamp']))
+                    in_keys, np.ascontiguousarray(gov['in_tag'], dtype=np.uint8), gov['in_str'][0],
+                    np.frombuffer(gov['in_str'][1], dtype=np.int64), n, int(b['timestamp']))
                 self.gov.version += 1
             self.last_gov_index_s = perf_counter() - tg
         elif self.gov is not None and n_in:
             hit = self._stake_spent(spent, spent_payload)
             if hit:
                 self.gov.removed(STAKE, hit)
+        ts.append(perf_counter())
+        self.last_apply_stages = dict(zip(('ap_records_s', 'ap_stmts_s', 'ap_encode_s', 'ap_journal_s', 'ap_index_s',
+                                           'ap_mempool_s', 'ap_gov_s'), np.diff(ts).tolist()))
         return seq
 
     def _stake_spent(self, spent: np.ndarray, spent_payload: np.ndarray) -> List[Tuple[str, int]]:

@@ -301,14 +301,16 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     # ---- columns for the ledger writes: views of the codec's buffers, encoded natively into one journal
     #      batch by csrc/ledger_writer.cpp (tx hashes rendered from the raw digests, text arenas for strings)
     L = lib()
-    in_json = L.input_address_strings(np.ascontiguousarray(pay['addr']).tobytes(),
-                                      pay['len'].astype(np.uint8).tobytes(), d['in_start'], THREADS)
+    in_str = L.input_address_strings(np.ascontiguousarray(pay['addr']).tobytes(), pay['len'].astype(np.uint8).tobytes(),
+                                     d['in_start'], THREADS, bg.any)
+    in_json = in_str[:2]
     fee_str = L.fee_strings(np.ascontiguousarray(fee, dtype=np.int64).tobytes())
     out_index = np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]
     gov_cols = None
     if bg.any:
         gov_cols = {'out_tag': bg.output_tags(TAG_BY_TABLE), 'out_type': out_type, 'in_tag': in_tag,
-                    'gov_tx': bg.gov, 'out_tx': out_tx, 'out_start': out_start, 'in_start': in_start}
+                    'gov_tx': bg.gov, 'out_tx': out_tx, 'out_start': out_start, 'in_start': in_start,
+                    'in_str': in_str[2:]}
 
     async def apply(block_hash, address, random, block_reward, content_time, coinbase_transaction):
         ta = perf_counter()
@@ -331,6 +333,7 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
             logger.error(f'Transaction of {block_no} has not been added in block {e}')
             manager.Manager.difficulty = None
             return False
+        timings.update(getattr(database, 'last_apply_stages', {}))
         timings.update({'apply_commit_s': perf_counter() - ta, 'journal_seq': seq,
                         'gov_index_s': getattr(database, 'last_gov_index_s', 0.0) if gov_cols is not None else 0.0})
         return True
