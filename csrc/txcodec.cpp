@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -653,6 +654,44 @@ static py::tuple input_address_strings(py::bytes addrs64, py::bytes lens, py::by
     return py::make_tuple(jt[0], jt[1], et[0], et[1]);
 }
 
+// address_transactions rows of a block's txs: every distinct address among each tx's input owners and
+// output addresses (the set the reference's json_each(inputs_addresses) UNION json_each(outputs_addresses)
+// yields per tx). Inputs: per-input and per-output string arenas with their tx segment starts. Returns
+// (address arena blob, int64 offsets, int64 tx index per row).
+static py::tuple address_pairs(py::bytes in_blob, py::bytes in_off_b, py::bytes in_start_b, py::bytes out_blob,
+                               py::bytes out_off_b, py::bytes out_start_b) {
+    const std::string ib = in_blob, io = in_off_b, is = in_start_b, ob = out_blob, oo = out_off_b, os = out_start_b;
+    const int64_t* ioff = reinterpret_cast<const int64_t*>(io.data());
+    const int64_t* ooff = reinterpret_cast<const int64_t*>(oo.data());
+    const int32_t* ist = reinterpret_cast<const int32_t*>(is.data());
+    const int32_t* ost = reinterpret_cast<const int32_t*>(os.data());
+    const size_t n = is.size() / 4 - 1;
+    if (os.size() / 4 - 1 != n) throw std::invalid_argument("address_pairs: tx counts differ");
+    const size_t n_in = io.size() / 8 - 1, n_out = oo.size() / 8 - 1;
+    if (size_t(ist[n]) > n_in || size_t(ost[n]) > n_out) throw std::invalid_argument("address_pairs: short arenas");
+    if (ioff[n_in] > int64_t(ib.size()) || ooff[n_out] > int64_t(ob.size()))
+        throw std::invalid_argument("address_pairs: offsets past the blob");
+    Arena out;
+    std::vector<int64_t> tx;
+    std::vector<std::string_view> seen;
+    out.blob.reserve(ib.size() + ob.size());
+    for (size_t k = 0; k < n; ++k) {
+        seen.clear();
+        auto take = [&](const std::string& blob, const int64_t* off, int64_t j) {
+            std::string_view v(blob.data() + off[j], size_t(off[j + 1] - off[j]));
+            for (auto& w : seen)
+                if (w == v) return;
+            seen.push_back(v);
+            out.add(v.data(), v.size());
+            tx.push_back(int64_t(k));
+        };
+        for (int64_t j = ist[k]; j < ist[k + 1]; ++j) take(ib, ioff, j);
+        for (int64_t o = ost[k]; o < ost[k + 1]; ++o) take(ob, ooff, o);
+    }
+    py::tuple a = out.py();
+    return py::make_tuple(a[0], a[1], py::bytes(reinterpret_cast<const char*>(tx.data()), tx.size() * 8));
+}
+
 // ---- column helpers for the bulk ledger writes (ledger/fastpath.py)
 
 // numeric(Decimal(fee) / 10**8, 6): fee in smallest units rounded half up to 6 decimals
@@ -823,6 +862,8 @@ void register_txcodec(py::module_& m) {
           py::arg("job_tx"), py::arg("gpu_min"));
     m.def("decode_block_txs", &decode_block_txs, py::arg("hexes"), py::arg("threads") = 8,
           "Decode, canonicalise and hash a block's transactions (see csrc/txcodec.cpp)");
+    m.def("address_pairs", &address_pairs, py::arg("in_blob"), py::arg("in_off"), py::arg("in_start"),
+          py::arg("out_blob"), py::arg("out_off"), py::arg("out_start"));
     m.def("input_address_strings", &input_address_strings, py::arg("addrs64"), py::arg("lens"), py::arg("in_start"),
           py::arg("threads") = 8, py::arg("per_input") = false);
 }

@@ -18,6 +18,7 @@
 #   coloc    scripts/colocated.py (node + miner sharing the GPU)
 #   prof     rocprofv3 --kernel-trace --stats over a short bench.py
 #   vprof    rocprofv3 --kernel-trace --stats over the verify bench
+#   soak3    three node soaks at 1,200 tx/s (scripts/node_soak.py)
 #   py:<script.py>  any extra python script under scripts/ (args after a comma: py:x.py,--a,1)
 # Every GPU step has its own time limit and the chain stops at the first failure.
 set -o pipefail
@@ -107,6 +108,14 @@ for s in $STEPS; do
         -- python3 bench.py --mode verify --ledger /tmp/upow_bench_ledger --steps 3 --warmup 1 \
         > "$OUT/vprof.log" 2>&1 || { tail -20 "$OUT/vprof.log"; exit 1; }
       echo vprof-ok ;;
+    soak3)
+      # three consecutive node soaks at 1,200 tx/s (node + GPU miner CLI + 4 x 8 pushing clients)
+      for i in 1 2 3; do
+        timeout -k 10 420 python -u scripts/node_soak.py --rate 1200 --seconds 45 --difficulty 9 --procs 4 --threads 8 \
+          --fanout1 255 --fanout2 220 --out "$OUT/soak_$i.json" > "$OUT/soak_$i.log" 2>&1 \
+          || { tail -30 "$OUT/soak_$i.log"; exit 1; }
+        tail -1 "$OUT/soak_$i.log" | cut -c1-600
+      done ;;
     py:*)
       spec=${s#py:}; script=${spec%%,*}; rest=""
       [ "$spec" != "$script" ] && rest=${spec#*,} && rest=${rest//,/ }

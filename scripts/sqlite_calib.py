@@ -21,7 +21,7 @@ import time  # noqa: E402
 
 import numpy as np  # noqa: E402
 
-from upow_amd.ledger.database import SCHEMA, UTXO_SCHEMA  # noqa: E402
+from upow_amd.ledger.database import SCHEMA, tx_schema, utxo_schema  # noqa: E402
 from upow_amd.ops.native import lib  # noqa: E402
 
 
@@ -40,7 +40,7 @@ def main():
                     help='UTXO rows split over this many files by the first txid byte (A/B for a wider split)')
     a = ap.parse_args()
     L = lib()
-    utxo_ddl = UTXO_SCHEMA
+    utxo_ddl = utxo_schema('utxo')
     if a.without_rowid:
         utxo_ddl = ('CREATE TABLE IF NOT EXISTS utxo.unspent_outputs (tx_hash TEXT, "index" INTEGER NOT NULL, '
                     'address TEXT NULL, is_stake INTEGER, PRIMARY KEY (tx_hash, "index")) WITHOUT ROWID;')
@@ -48,7 +48,7 @@ def main():
     path = os.path.join(d, 'ledger.sqlite3')
     c = sqlite3.connect(path, isolation_level=None)
     c.execute('PRAGMA journal_mode = WAL')
-    c.executescript(SCHEMA)
+    c.executescript(SCHEMA + tx_schema('main', legacy=True))
     c.execute('ATTACH DATABASE ? AS utxo', (path + '-utxo',))
     c.execute('PRAGMA utxo.journal_mode = WAL')
     c.executescript(utxo_ddl)

@@ -142,10 +142,12 @@ def test_sigkill_between_journal_append_and_sql_catch_up(tmp_path):
     asyncio.run(check())
 
 
-def test_single_utxo_file_ledger_is_split_on_open(tmp_path):
+def test_single_utxo_file_ledger_is_split_on_open(tmp_path, monkeypatch):
     """A ledger written with one UTXO file (before the 00-7f / 80-ff split) opens with the rows of the
     high half moved to the second file (row ids kept), the same UTXO set and K12 hash, and keeps
-    applying blocks."""
+    applying blocks. (Built in the layout of that era: transactions in the main file, two UTXO files.)"""
+    monkeypatch.setenv('UPOW_UTXO_FILES', '2')
+    monkeypatch.setenv('UPOW_TX_FILES', '0')
     import asyncio
     import sqlite3
     sys.path.insert(0, ROOT)

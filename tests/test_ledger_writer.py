@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 from upow_amd import devnet
+from upow_amd.ops.native import lib
 from upow_amd.ledger import manager
 from upow_amd.ledger.database import UTXO_SUFFIXES, Database, ledger_files
 from upow_amd.wallet import builders
@@ -54,8 +55,8 @@ def test_undo_log_retention_restart_and_tombstone(tmp_path):
 def test_undo_survives_journal_rotation(tmp_path):
     w, dbs = _writer(tmp_path, journal_max_bytes=4096)
     blob = b'x' * 2048
-    w.submit([Database.encode('CREATE TABLE IF NOT EXISTS t (x TEXT)', [], 1)], b'', -1)
-    stmt = Database.encode('INSERT INTO t (x) VALUES (?)', [['y' * 2048]], 1)
+    w.submit([lib().ledger_encode_stmt('CREATE TABLE IF NOT EXISTS t (x TEXT)', [], 1)], b'', -1)
+    stmt = lib().ledger_encode_stmt('INSERT INTO t (x) VALUES (?)', [['y' * 2048]], 1)
     for i in range(1, 40):
         w.submit([stmt], _meta(i) + blob, i)
         w.wait(w.stats()['submitted'], -1, 30.0)
@@ -89,12 +90,12 @@ def test_row_count_mismatch_stops_writer(tmp_path):
 
 def test_busy_file_is_retried_and_block_submit_is_throttled(tmp_path):
     w, dbs = _writer(tmp_path, max_queue_bytes=4096, throttle_timeout_s=0.4, busy_timeout_ms=20)
-    stmt = Database.encode('CREATE TABLE IF NOT EXISTS t (x TEXT)', [], 1)
+    stmt = lib().ledger_encode_stmt('CREATE TABLE IF NOT EXISTS t (x TEXT)', [], 1)
     w.submit([stmt], b'', -1)
     w.wait(w.stats()['submitted'], -1, 30.0)
     blocker = sqlite3.connect(dbs[0], isolation_level=None, timeout=1)
     blocker.execute('BEGIN IMMEDIATE')  # holds the write lock: the materialiser of file 0 gets SQLITE_BUSY
-    ins = Database.encode('INSERT INTO t (x) VALUES (?)', [['y' * 3000]], 1)
+    ins = lib().ledger_encode_stmt('INSERT INTO t (x) VALUES (?)', [['y' * 3000]], 1)
     w.submit([ins], b'', -1)
     w.submit([ins], b'', -1)
     t0 = time.time()
@@ -145,7 +146,9 @@ def test_journal_cut_at_synced_offset_reopens_consistent(tmp_path, monkeypatch):
         st = db.writer.stats()
         assert st['sync_mode'] == 3 and st['synced_bytes'] < st['journal_bytes']
         # the crash: copy the files as they are on disk now, cutting the journal at the synced offset
-        for s_, d_ in zip(ledger_files(str(src / 'ledger.sqlite3')), ledger_files(str(dst / 'ledger.sqlite3'))):
+        s0, d0 = str(src / 'ledger.sqlite3'), str(dst / 'ledger.sqlite3')
+        for s_ in ledger_files(s0):
+            d_ = d0 + s_[len(s0):]
             for sfx in ('', '-wal'):
                 if os.path.exists(s_ + sfx):
                     shutil.copy(s_ + sfx, d_ + sfx)

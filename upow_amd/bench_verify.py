@@ -183,10 +183,14 @@ def age_ledger(db, n_txs: int, rng, chunk: int = 250_000) -> dict:
             u_rows.append((hexes[k], 0, a0, None))
             u_rows.append((hexes[k], 1, a1, None))
         with db.transaction(foreign_keys=False, invalidate=False):
-            db._conn.executemany('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, '
-                                 'outputs_addresses, outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)', tx_rows)
-            db._utxo_exec('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) VALUES (?, ?, ?, ?)',
-                          u_rows)
+            ins_tx = ('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, outputs_addresses, '
+                      'outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)')
+            if db._split_target(ins_tx):
+                db._routed_exec('transactions', ins_tx, tx_rows)
+            else:
+                db._conn.executemany(ins_tx, tx_rows)
+            db._routed_exec('unspent_outputs', 'INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake) '
+                            'VALUES (?, ?, ?, ?)', u_rows)
         recs = np.zeros((2 * n, 40), dtype=np.uint8)
         recs[:, :32] = np.repeat(hashes, 2, axis=0)
         recs[:, 32:36] = np.tile(np.array([[0, 0, 0, 0], [1, 0, 0, 0]], np.uint8), (n, 1))

@@ -36,7 +36,7 @@ from ..utils.codec import (AddressFormat, OutputType, TransactionType, normalize
 from ..utils import coalesce
 from ..utils.logstore import LogStore
 from ..utils.logger import get_logger
-from .governance import GOV_TABLES, STAKE, GovernanceIndex
+from .governance import STAKE, GovernanceIndex
 from .governance import TID as GOV_TID
 from .governance import _row_args as _gov_row
 from .mempool import MempoolIndex
@@ -57,15 +57,6 @@ CREATE TABLE IF NOT EXISTS blocks (
     difficulty TEXT NOT NULL,
     reward TEXT NOT NULL,
     timestamp INTEGER
-);
-CREATE TABLE IF NOT EXISTS transactions (
-    block_hash TEXT NOT NULL REFERENCES blocks(hash) ON DELETE CASCADE,
-    tx_hash TEXT UNIQUE,
-    tx_hex TEXT,
-    inputs_addresses TEXT,
-    outputs_addresses TEXT,
-    outputs_amounts TEXT,
-    fees TEXT NOT NULL
 );
 CREATE TABLE IF NOT EXISTS pending_transactions (
     tx_hash TEXT UNIQUE,
@@ -95,7 +86,6 @@ CREATE TABLE IF NOT EXISTS {_t} (
     address TEXT NULL
 );"""
 SCHEMA += """
-CREATE INDEX IF NOT EXISTS block_hash_idx ON transactions (block_hash);
 CREATE INDEX IF NOT EXISTS pending_spent_idx ON pending_spent_outputs (tx_hash, "index");
 CREATE INDEX IF NOT EXISTS address_transactions_idx ON address_transactions (address);
 CREATE INDEX IF NOT EXISTS address_transactions_tx_idx ON address_transactions (tx_hash);
@@ -105,19 +95,67 @@ for _t in OUTPUT_TABLES[1:]:
     SCHEMA += f'CREATE INDEX IF NOT EXISTS {_t}_address_idx ON {_t} (address);\n'
 
 
-# The UTXO table is split over two database files of its own by the first byte of the tx hash
-# (``<ledger>-utxo``: 00-7f, attached as ``utxo``; ``<ledger>-utxo2``: 80-ff, attached as ``utxo2``): a
-# block rewrites ~33k UTXO rows, the largest share of its SQL, and each file has a native materialiser
-# thread of its own (csrc/ledger_writer.cpp routes a statement's rows by that byte).
+# Row-heavy tables live in database files of their own, each table split over several files by the first
+# byte of the tx hash (file k of n holds the hashes whose first byte b has b * n >> 8 == k). A 2 MB block
+# inserts ~8.3k transaction rows and ~33k UTXO rows and deletes as many; once a ledger holds millions of
+# rows every one of them is a random B-tree update, and each file has a native materialiser thread of its
+# own (csrc/ledger_writer.cpp routes a statement's rows by that byte), so the files apply in parallel.
 #
-# * Row ids come from one ledger-wide counter (explicit ``rowid`` on every insert), so ``rowid`` order
-#   over both files is insertion order, as in the single table of schema.sql.
-# * On the Python connection ``unspent_outputs`` is a TEMP view over both files for reads; Python-side
-#   writes are routed by :meth:`Database._utxo_exec` (a trigger body cannot name an attached table).
-# * SQLite cannot declare a foreign key across files: the reference's ``tx_hash REFERENCES
-#   transactions(tx_hash) ON DELETE CASCADE`` is applied by the block-deleting methods themselves.
-UTXO_SCHEMAS = ('utxo', 'utxo2')
-UTXO_SUFFIXES = ('-utxo', '-utxo2')
+#   ``<ledger>-utxo``, ``-utxo2``, ...  ``unspent_outputs``, attached as ``utxo``, ``utxo2``, ...
+#   ``<ledger>-tx``, ``-tx2``, ...      ``transactions``, attached as ``tx``, ``tx2``, ...
+#
+# * Row ids come from one ledger-wide counter per table (explicit ``rowid`` on every insert), so
+#   ``rowid`` order over the files is insertion order, as in the single tables of schema.sql.
+# * On the Python connection each split table is a TEMP view over its files for reads; Python-side
+#   writes are routed by :meth:`Database._routed_exec` (a trigger body cannot name an attached table).
+# * SQLite cannot declare a foreign key across files: the reference's ``ON DELETE CASCADE`` clauses that
+#   point at a split table (or from it at ``blocks``) are applied by the block-deleting methods themselves.
+# * The layout of a ledger is recorded in its main file (``upow_layout``) when it is created. Ledgers from
+#   before the transactions split keep ``transactions`` in the main file (one "file", no view) and two
+#   UTXO files.
+UTXO_FILES_DEFAULT = 4
+TX_FILES_DEFAULT = 4
+ROUTED = ('unspent_outputs', 'transactions')
+
+
+def _names(kind: str, n: int) -> Tuple[List[str], List[str]]:
+    """(schema names, file suffixes) of the ``n`` files of ``kind`` ('utxo' | 'tx')."""
+    schemas = [kind if k == 0 else f'{kind}{k + 1}' for k in range(n)]
+    return schemas, ['-' + sch for sch in schemas]
+
+
+# the two-file UTXO layout of earlier ledgers (still what ``_migrate_utxo_split`` produces)
+UTXO_SCHEMAS, UTXO_SUFFIXES = _names('utxo', 2)
+
+
+def file_of(tx_hash: str, n: int) -> int:
+    """Which of ``n`` files holds ``tx_hash``: the writer's routing (first byte * n >> 8; non-hex -> 0)."""
+    try:
+        return (int(tx_hash[:2], 16) * n) >> 8 if n > 1 else 0
+    except (ValueError, TypeError):
+        return 0
+
+
+TX_COLUMNS = 'block_hash, tx_hash, tx_hex, inputs_addresses, outputs_addresses, outputs_amounts, fees'
+UTXO_COLUMNS = 'tx_hash, "index", address, is_stake'
+
+
+def tx_schema(schema: str, legacy: bool = False) -> str:
+    """``transactions`` (schema.sql) in one of its files; ``legacy``: the main-file table of a ledger from
+    before the split, with the reference's cascade from ``blocks``."""
+    parent = ' REFERENCES blocks(hash) ON DELETE CASCADE' if legacy else ''
+    return f"""
+CREATE TABLE IF NOT EXISTS {schema}.transactions (
+    block_hash TEXT NOT NULL{parent},
+    tx_hash TEXT UNIQUE,
+    tx_hex TEXT,
+    inputs_addresses TEXT,
+    outputs_addresses TEXT,
+    outputs_amounts TEXT,
+    fees TEXT NOT NULL
+);
+CREATE INDEX IF NOT EXISTS {schema}.block_hash_idx ON transactions (block_hash);
+"""
 
 
 def utxo_schema(schema: str = 'utxo') -> str:
@@ -132,35 +170,35 @@ CREATE INDEX IF NOT EXISTS {schema}.tx_hash_idx ON unspent_outputs (tx_hash, "in
 """
 
 
-UTXO_SCHEMA = utxo_schema('utxo')
-UTXO_VIEW = """
-CREATE TEMP VIEW IF NOT EXISTS unspent_outputs AS
-    SELECT rowid AS rowid, tx_hash, "index", address, is_stake FROM utxo.unspent_outputs
-    UNION ALL
-    SELECT rowid AS rowid, tx_hash, "index", address, is_stake FROM utxo2.unspent_outputs;
-"""
-# table -> the writer files (shards) holding it; every other table is in the main file (shard 0). A table
-# on several files is written by routed statements: (first file, number of files).
-SHARD_OF_TABLE = {'unspent_outputs': (1, 2)}
-ROUTED_TABLES = {'unspent_outputs': (1, 2)}
+def split_view(table: str, schemas: List[str]) -> str:
+    """The TEMP view that reads a split table over its files (``rowid``: the ledger-wide row id)."""
+    if table == 'unspent_outputs':
+        arms = [f'SELECT rowid AS rowid, {UTXO_COLUMNS} FROM {sch}.unspent_outputs' for sch in schemas]
+    else:
+        arms = [f'SELECT {TX_COLUMNS}, rowid AS rowid FROM {sch}.transactions' for sch in schemas]
+    return f'CREATE TEMP VIEW IF NOT EXISTS {table} AS\n    ' + '\n    UNION ALL\n    '.join(arms) + ';\n'
 
 
 def utxo_file_of(tx_hash: str) -> int:
-    """0 for ``utxo`` (hash 00-7f), 1 for ``utxo2`` (80-ff) — the writer's routing (first byte * 2 >> 8)."""
-    return 0 if tx_hash[:1] < '8' else 1
+    """0 for ``utxo`` (hash 00-7f), 1 for ``utxo2`` (80-ff) in the two-file layout."""
+    return file_of(tx_hash, 2)
 
 
 def ledger_files(path: str) -> List[str]:
-    """Every file of a (closed) file ledger: the main database, the two UTXO databases and the journal."""
-    return [path] + [path + sfx for sfx in UTXO_SUFFIXES] + [path + '.journal']
+    """Every file of a (closed) file ledger: the main database, its table files and the journal."""
+    import glob
+    parts = sorted(glob.glob(glob.escape(path) + '-utxo*') + glob.glob(glob.escape(path) + '-tx*'))
+    parts = [f for f in parts if not f.endswith(('-wal', '-shm', '-journal'))]
+    return [path] + parts + [path + '.journal']
 
 
 def copy_ledger(src: str, dst: str):
     """Copy a closed file ledger (all of its files) to ``dst``."""
     import shutil
-    for s, d in zip(ledger_files(str(src)), ledger_files(str(dst))):
-        if os.path.exists(s):
-            shutil.copy(s, d)
+    src, dst = str(src), str(dst)
+    for f in ledger_files(src):
+        if os.path.exists(f):
+            shutil.copy(f, dst + f[len(src):])
 
 
 def numeric(value, scale: int) -> str:
@@ -348,6 +386,9 @@ class Database:
         self._conn = sqlite3.connect(self.file, check_same_thread=False, isolation_level=None, timeout=120)
         self._eph['conn'] = self._conn if path == ':memory:' else None
         self._conn.row_factory = sqlite3.Row
+        if os.environ.get('UPOW_SQL_TRACE'):  # every statement of the Python connection (query-plan audits)
+            trace = open(os.environ['UPOW_SQL_TRACE'], 'a')
+            self._conn.set_trace_callback(lambda q: trace.write(q.replace('\n', ' ') + '\n'))
         self.lock = threading.RLock()
         self.writer = None
         self._submitted = 0
@@ -385,32 +426,52 @@ class Database:
         bg = os.environ.get('UPOW_WAL_CHECKPOINT_THREAD', '1') != '0'
         auto = int(os.environ.get('UPOW_WAL_AUTOCHECKPOINT', '100000' if bg else '10000'))
         self._conn.execute(f'PRAGMA wal_autocheckpoint = {auto}')
-        if bg:
-            self._start_checkpointer(float(os.environ.get('UPOW_WAL_CHECKPOINT_PERIOD', '0.5')))
+        n_utxo, n_tx = self._layout()
         self._conn.executescript(SCHEMA)
-        self.utxo_files = [self.file + sfx for sfx in UTXO_SUFFIXES]
+        self.utxo_schemas, sfx = _names('utxo', n_utxo)
+        self.utxo_files = [self.file + x for x in sfx]
         self.utxo_file = self.utxo_files[0]
-        fresh2 = not os.path.exists(self.utxo_files[1])
-        for schema, f in zip(UTXO_SCHEMAS, self.utxo_files):
+        # n_tx == 0: a ledger from before the transactions split keeps the table in its main file
+        self.tx_schemas, sfx = _names('tx', n_tx)
+        self.tx_files = [self.file + x for x in sfx]
+        fresh2 = n_utxo == 2 and not os.path.exists(self.utxo_files[1])
+        for schema, f in [*zip(self.utxo_schemas, self.utxo_files), *zip(self.tx_schemas, self.tx_files)]:
             self._conn.execute(f'ATTACH DATABASE ? AS {schema}', (f,))
             self._conn.execute(f'PRAGMA {schema}.page_size = {page}')
             self._conn.execute(f'PRAGMA {schema}.journal_mode = WAL')
             self._conn.execute(f'PRAGMA {schema}.synchronous = ' + ('OFF' if path == ':memory:' else 'NORMAL'))
             self._conn.execute(f'PRAGMA {schema}.cache_size = -{cache_mb * 1024}')
-            self._conn.executescript(utxo_schema(schema))
+            self._conn.executescript(utxo_schema(schema) if schema.startswith('utxo') else tx_schema(schema))
+        if not n_tx:
+            self._conn.executescript(tx_schema('main', legacy=True))
+        else:
+            # the reference's cascades into and out of the split table are applied by the deleting methods
+            self._conn.execute('PRAGMA foreign_keys = OFF')
+        self._fk = not n_tx
         self._migrate_single_file_utxo()
         if fresh2:
             self._migrate_utxo_split()
-        self._conn.executescript(UTXO_VIEW)
+        self._conn.executescript(split_view('unspent_outputs', self.utxo_schemas))
+        if n_tx:
+            self._conn.executescript(split_view('transactions', self.tx_schemas))
+        # table -> writer files holding it (main file = 0); routed tables: (first file, number of files)
+        self._routed = {'unspent_outputs': (1, n_utxo)}
+        if n_tx:
+            self._routed['transactions'] = (1 + n_utxo, n_tx)
+        self._shard_of = {t: tuple(range(a, a + k)) for t, (a, k) in self._routed.items()}
+        if bg:
+            self._start_checkpointer(float(os.environ.get('UPOW_WAL_CHECKPOINT_PERIOD', '0.5')))
         if os.environ.get('UPOW_LEDGER_WRITER', '1') != '0':
             self._open_writer(cache_mb)
             if fresh2:
                 # journal records written under the one-file layout were just replayed into the first UTXO
                 # file only (they carry no routing): move their 80-ff rows across like the migration did
                 self._resplit_utxo()
-        # next UTXO row id: one counter over both files (row id order = insertion order, as in one table)
+        # next row ids: one counter per split table over its files (row id order = insertion order)
         self._utxo_next_rowid = 1 + max(self._conn.execute(f'SELECT COALESCE(MAX(rowid), 0) FROM {s}.unspent_outputs')
-                                        .fetchone()[0] for s in UTXO_SCHEMAS)
+                                        .fetchone()[0] for s in self.utxo_schemas)
+        self._tx_next_rowid = 1 + max(self._conn.execute(f'SELECT COALESCE(MAX(rowid), 0) FROM {s}.transactions')
+                                      .fetchone()[0] for s in (self.tx_schemas or ['main']))
         store_dir = os.path.dirname(path) if path != ':memory:' else None
         # per-block inode emission records (reference: pickledb emission_details.json): an append-only log
         self.emission_details = LogStore(os.path.join(store_dir, 'emission_details.jsonl') if store_dir else None,
@@ -432,6 +493,25 @@ class Database:
         # the address-index watermark row must exist before the first block: the per-block statements
         # of the journal batches only advance an existing watermark
         self._address_index_height()
+
+    def _layout(self) -> Tuple[int, int]:
+        """(UTXO files, transaction files; 0 = in the main file) of this ledger, recorded at creation."""
+        c = self._conn
+        c.execute('CREATE TABLE IF NOT EXISTS upow_layout (k TEXT PRIMARY KEY, v INTEGER NOT NULL)')
+        got = {r[0]: int(r[1]) for r in c.execute('SELECT k, v FROM upow_layout')}
+        if 'utxo_files' in got and 'tx_files' in got:
+            return got['utxo_files'], got['tx_files']
+        legacy = c.execute("SELECT 1 FROM main.sqlite_master WHERE type = 'table' AND name = 'blocks'").fetchone()
+        if legacy:
+            n_utxo, n_tx = 2, 0
+        else:
+            n_utxo = int(os.environ.get('UPOW_UTXO_FILES', str(UTXO_FILES_DEFAULT)))
+            n_tx = int(os.environ.get('UPOW_TX_FILES', str(TX_FILES_DEFAULT)))
+            if not (2 <= n_utxo <= 8 and 0 <= n_tx <= 8):
+                raise ValueError('UPOW_UTXO_FILES must be in 2..8 and UPOW_TX_FILES in 0..8')
+        c.executemany('INSERT OR REPLACE INTO upow_layout (k, v) VALUES (?, ?)',
+                      [('utxo_files', n_utxo), ('tx_files', n_tx)])
+        return n_utxo, n_tx
 
     def _migrate_single_file_utxo(self):
         """Ledgers written before the UTXO table got its own file keep ``unspent_outputs`` in the main
@@ -488,7 +568,7 @@ class Database:
             mode = 0
         journal = os.environ.get('UPOW_JOURNAL_PATH') or os.path.join(os.path.dirname(os.path.abspath(self.file)),
                                                                        os.path.basename(self.file) + '.journal')
-        self.writer = lib().LedgerWriter([self.file, *self.utxo_files], journal, mode, cache_mb,
+        self.writer = lib().LedgerWriter([self.file, *self.utxo_files, *self.tx_files], journal, mode, cache_mb,
                                          int(os.environ.get('UPOW_WRITER_GROUP', '8')),
                                          int(os.environ.get('UPOW_JOURNAL_MAX_MB', '1024')) << 20,
                                          # undo data of the last N blocks survives journal rotation: a
@@ -540,11 +620,12 @@ class Database:
         block's COMMIT). sqlite3 releases the GIL while the checkpoint runs."""
         self._ckpt_stop = threading.Event()
         path = self.file
+        files = [*zip(self.utxo_schemas, self.utxo_files), *zip(self.tx_schemas, self.tx_files)]
 
         def run(stop: threading.Event):
             conn = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
-            for schema, sfx in zip(UTXO_SCHEMAS, UTXO_SUFFIXES):
-                conn.execute(f'ATTACH DATABASE ? AS {schema}', (path + sfx,))
+            for schema, f in files:
+                conn.execute(f'ATTACH DATABASE ? AS {schema}', (f,))
             try:
                 while not stop.wait(period):
                     try:
@@ -588,7 +669,7 @@ class Database:
             waits = {}
             for t in tables:
                 seq = ts.get(t, 0)
-                for sh in SHARD_OF_TABLE.get(t, (0,)):
+                for sh in self._shard_of.get(t, (0,)):
                     if seq > waits.get(sh, 0):
                         waits[sh] = seq
         seen = self._applied_seen
@@ -609,7 +690,7 @@ class Database:
         seen = self._applied_seen
         if seq <= seen.get(-1, 0):
             return True
-        for sh in SHARD_OF_TABLE.get(table, (0,)):
+        for sh in self._shard_of.get(table, (0,)):
             if seq <= seen.get(sh, 0):
                 continue
             applied = self.writer.applied(sh)
@@ -713,8 +794,9 @@ class Database:
         self._settle(t)
         with self.lock:
             self._invalidate_for(t)
-            if t and 'unspent_outputs' in t:
-                return self._utxo_exec(sql, [tuple(args)])
+            split = self._split_target(sql)
+            if split is not None:
+                return self._routed_exec(split, sql, [tuple(args)])
             return self._conn.execute(sql, tuple(args))
 
     def _xm(self, sql: str, rows: Iterable):
@@ -722,16 +804,27 @@ class Database:
         self._settle(t)
         with self.lock:
             self._invalidate_for(t)
-            if t and 'unspent_outputs' in t:
-                return self._utxo_exec(sql, list(rows))
+            split = self._split_target(sql)
+            if split is not None:
+                return self._routed_exec(split, sql, list(rows))
             return self._conn.executemany(sql, rows)
 
     class _Changed:
         def __init__(self, n: int):
             self.rowcount = n
 
-    _UTXO_INSERT = re.compile(r'^\s*INSERT\s+(OR\s+\w+\s+)?INTO\s+unspent_outputs\s*\(([^)]*)\)\s*VALUES', re.I)
-    _UTXO_TARGET = re.compile(r'^(\s*(?:DELETE\s+FROM|UPDATE))\s+unspent_outputs\b', re.I)
+    _SPLIT_INSERT = re.compile(r'^\s*INSERT\s+(OR\s+\w+\s+)?INTO\s+(unspent_outputs|transactions)\s*\(([^)]*)\)\s*VALUES',
+                               re.I)
+    _SPLIT_TARGET = re.compile(r'^(\s*(?:DELETE\s+FROM|UPDATE))\s+(unspent_outputs|transactions)\b', re.I)
+
+    def _split_target(self, sql: str) -> Optional[str]:
+        """The split table a write statement targets (None: an ordinary table, or ``transactions`` of a
+        ledger that keeps it in the main file)."""
+        m = self._SPLIT_INSERT.match(sql) or self._SPLIT_TARGET.match(sql)
+        if m is None:
+            return None
+        t = m.group(2).lower()
+        return t if t in self._routed else None
 
     def _utxo_rowids(self, n: int) -> int:
         """First of ``n`` consecutive row ids from the ledger-wide UTXO counter."""
@@ -740,37 +833,49 @@ class Database:
             self._utxo_next_rowid += n
         return base
 
-    def _utxo_exec(self, sql: str, rows: list) -> '_Changed':
-        """A Python-side write to ``unspent_outputs`` (caller holds the lock, tables settled), routed to
-        the file(s) holding the rows: INSERTs by tx hash with row ids from the ledger-wide counter,
-        ``DELETE ... WHERE tx_hash = ? ...`` by tx hash, anything else on both files."""
+    def _tx_rowids(self, n: int) -> int:
+        """First of ``n`` consecutive row ids from the ledger-wide transactions counter."""
+        with self._seq_lock:
+            base = self._tx_next_rowid
+            self._tx_next_rowid += n
+        return base
+
+    # the journaled tx-row insert: tx hash in column 0 (a split table's routing key), explicit row id
+    _TX_INSERT = ('INSERT INTO transactions (tx_hash, block_hash, tx_hex, inputs_addresses, outputs_addresses, '
+                  'outputs_amounts, fees, rowid) VALUES (?, ?, ?, ?, ?, ?, ?, ?)')
+
+    def _routed_exec(self, table: str, sql: str, rows: list) -> '_Changed':
+        """A Python-side write to a split table (caller holds the lock, tables settled), routed to the
+        file(s) holding the rows: INSERTs by tx hash with row ids from the table's ledger-wide counter,
+        ``DELETE ... WHERE tx_hash = ? ...`` by tx hash, anything else on every file."""
         c = self._conn
-        m = self._UTXO_INSERT.match(sql)
+        schemas = self.utxo_schemas if table == 'unspent_outputs' else self.tx_schemas
+        nf = len(schemas)
+        m = self._SPLIT_INSERT.match(sql)
         if m:
-            cols = [x.strip().strip('"') for x in m.group(2).split(',')]
+            cols = [x.strip().strip('"') for x in m.group(3).split(',')]
             h = cols.index('tx_hash')
             values = sql[m.end():]
             if 'rowid' not in cols:
-                base = self._utxo_rowids(len(rows))
+                base = (self._utxo_rowids if table == 'unspent_outputs' else self._tx_rowids)(len(rows))
                 rows = [(*r, base + k) for k, r in enumerate(rows)]
                 values = values.replace(')', ', ?)', 1)
                 cols.append('rowid')
-            head = f'INSERT {m.group(1) or ""}INTO %s.unspent_outputs ({", ".join(chr(34) + x + chr(34) if x == "index" else x for x in cols)}) VALUES'
+            names = ', '.join(chr(34) + x + chr(34) if x == 'index' else x for x in cols)
+            head = f'INSERT {m.group(1) or ""}INTO %s.{table} ({names}) VALUES'
             n = 0
-            for f, schema in enumerate(UTXO_SCHEMAS):
-                part = [r for r in rows if utxo_file_of(r[h]) == f]
+            for f, schema in enumerate(schemas):
+                part = [r for r in rows if file_of(r[h], nf) == f]
                 if part:
                     n += c.executemany(head % schema + values, part).rowcount
             return self._Changed(n)
-        m = self._UTXO_TARGET.match(sql)
-        if not m:
-            raise RuntimeError(f'unroutable write to unspent_outputs: {sql[:80]}')
+        m = self._SPLIT_TARGET.match(sql)
         by_hash = re.search(r'\bWHERE\s+tx_hash\s*=\s*\?', sql, re.I) is not None
         n = 0
-        for f, schema in enumerate(UTXO_SCHEMAS):
-            part = [r for r in rows if utxo_file_of(r[0]) == f] if by_hash else rows
+        for f, schema in enumerate(schemas):
+            part = [r for r in rows if file_of(r[0], nf) == f] if by_hash else rows
             if part:
-                q = m.group(1) + f' {schema}.unspent_outputs' + sql[m.end():]
+                q = m.group(1) + f' {schema}.{table}' + sql[m.end():]
                 n += c.executemany(q, part).rowcount if part != [()] else c.execute(q).rowcount
         return self._Changed(n)
 
@@ -781,20 +886,18 @@ class Database:
             self._xm('DELETE FROM unspent_outputs WHERE tx_hash = ?', hs)
 
     # ------------------------------------------------------------------ native bulk writes
-    @staticmethod
-    def encode(sql: str, cols: list, n: int, order=None, guard: Optional[str] = None,
+    def encode(self, sql: str, cols: list, n: int, order=None, guard: Optional[str] = None,
                expect: Optional[int] = None) -> bytes:
         """One column-major bulk statement for :meth:`submit_batch`. Column specs as in
         csrc/ledger_writer.cpp: text lists, int64 arrays, ('gather'|'hex32'|'arena', ...) views of the
-        block codec's buffers, or one constant for every row."""
+        block codec's buffers, or one constant for every row. A statement on a split table is spread over
+        its files by the tx hash in column 0."""
         from ..ops.native import lib
-        tables = _tables_of(sql, False) or frozenset()
-        for t in tables:
-            if t in ROUTED_TABLES:  # rows spread over the table's files by tx hash (column 0)
-                first, count = ROUTED_TABLES[t]
-                return lib().ledger_encode_stmt(sql, cols, n, order, guard, expect, first, count)
-        shard = max((max(SHARD_OF_TABLE.get(t, (0,))) for t in tables), default=0)
-        return lib().ledger_encode_stmt(sql, cols, n, order, guard, expect, shard)
+        split = self._split_target(sql)
+        if split is not None:
+            first, count = self._routed[split]
+            return lib().ledger_encode_stmt(sql, cols, n, order, guard, expect, first, count)
+        return lib().ledger_encode_stmt(sql, cols, n, order, guard, expect, 0)  # every other table: main file
 
     def bulk(self, sql: str, cols: list, n: int, order=None) -> int:
         """Column-major executemany on the Python connection (synchronous); returns the row changes."""
@@ -843,7 +946,8 @@ class Database:
                     if self.db._tx_inv:
                         self.db._invalidate_for(None)
                     if self.db._fk_off:
-                        self.db._conn.execute('PRAGMA foreign_keys = ON')
+                        if self.db._fk:
+                            self.db._conn.execute('PRAGMA foreign_keys = ON')
                         self.db._fk_off = False
                 elif et is not None:
                     self.db._tx_failed = True
@@ -870,17 +974,51 @@ class Database:
         if self.fail_after_stage == stage:
             raise RuntimeError(f'injected failure after {stage}')
 
+    @staticmethod
+    def _txq(col: str, key: str) -> str:
+        """Column ``col`` of the tx whose hash is the SQL expression ``key``, as a correlated lookup. Where
+        ``transactions`` is split over several files, SQLite materialises the whole view to join it, but a
+        correlated lookup is pushed into each file's tx-hash index (rows without their tx come back NULL,
+        which callers of an INNER JOIN form skip)."""
+        return f'(SELECT t_.{col} FROM transactions t_ WHERE t_.tx_hash = {key})'
+
+    def _tx_source_for_utxo(self, k: int) -> Optional[str]:
+        """The one transactions table holding the txs of every row of UTXO file ``k`` (same hash routing), or
+        None when its hash range spans several tx files."""
+        if not self.tx_schemas:
+            return 'main.transactions'
+        nu, nt = len(self.utxo_schemas), len(self.tx_schemas)
+        lo, hi = (k * 256 + nu - 1) // nu, ((k + 1) * 256 + nu - 1) // nu  # first bytes b with b * nu >> 8 == k
+        files = {file_of(f'{b:02x}', nt) for b in range(lo, hi)}
+        return f'{self.tx_schemas[files.pop()]}.transactions' if len(files) == 1 else None
+
     def _rebuild_utxo_index(self):
         """Rebuild the HBM/host UTXO set from the output tables; each entry's payload (amount,
         address bytes) comes from its creating tx's JSON columns, read with SQLite's json_extract."""
         keys, tags, amounts, addrs, stake = [], [], [], [], []
+        am = 'json_extract(t.outputs_amounts, \'$[\' || u."index" || \']\')'
+        ad = 'json_extract(t.outputs_addresses, \'$[\' || u."index" || \']\')'
+        queries = []
         for table in OUTPUT_TABLES:
+            if table != 'unspent_outputs':
+                queries.append((table, f'SELECT u.tx_hash, u."index", '
+                                       f'(SELECT {am} FROM transactions t WHERE t.tx_hash = u.tx_hash), '
+                                       f'(SELECT {ad} FROM transactions t WHERE t.tx_hash = u.tx_hash), NULL '
+                                       f'FROM {table} u'))
+                continue
+            for k, sch in enumerate(self.utxo_schemas):  # each UTXO file against the tx file of its hash range
+                src = self._tx_source_for_utxo(k)
+                if src is not None:
+                    queries.append((table, f'SELECT u.tx_hash, u."index", {am}, {ad}, u.is_stake '
+                                           f'FROM {sch}.unspent_outputs u LEFT JOIN {src} t ON t.tx_hash = u.tx_hash'))
+                else:
+                    queries.append((table, f'SELECT u.tx_hash, u."index", '
+                                           f'(SELECT {am} FROM transactions t WHERE t.tx_hash = u.tx_hash), '
+                                           f'(SELECT {ad} FROM transactions t WHERE t.tx_hash = u.tx_hash), u.is_stake '
+                                           f'FROM {sch}.unspent_outputs u'))
+        for table, sql in queries:
             tag = TAG_BY_TABLE[table]
-            stake_col = 'u.is_stake' if table == 'unspent_outputs' else 'NULL'
-            for r in self._q(f'SELECT u.tx_hash, u."index", '
-                             f'json_extract(t.outputs_amounts, \'$[\' || u."index" || \']\'), '
-                             f'json_extract(t.outputs_addresses, \'$[\' || u."index" || \']\'), {stake_col} '
-                             f'FROM {table} u LEFT JOIN transactions t ON t.tx_hash = u.tx_hash'):
+            for r in self._q(sql):
                 keys.append((r[0], r[1]))
                 tags.append(tag)
                 amounts.append(r[2])
@@ -1075,28 +1213,65 @@ class Database:
 
     async def delete_blockchain(self):
         with self.transaction():
-            self.conn.execute('DELETE FROM transactions')
-            for schema in UTXO_SCHEMAS:  # the cascade to unspent_outputs (every row belongs to a tx)
+            # the cascade from blocks and transactions (every split-table row belongs to a tx)
+            for schema in self.tx_schemas or ['main']:
+                self._conn.execute(f'DELETE FROM {schema}.transactions')
+            for schema in self.utxo_schemas:
                 self._conn.execute(f'DELETE FROM {schema}.unspent_outputs')
+            if self.tx_schemas:
+                for child in self._TX_CHILDREN:
+                    self._conn.execute(f'DELETE FROM {child}')
             self.conn.execute('DELETE FROM blocks')
             self.conn.execute("UPDATE address_index_state SET height = 0 WHERE k = 'height'")
         self._rebuild_utxo_index()
 
     def _block_tx_hashes(self, where: str, args: tuple) -> List[str]:
-        return [r[0] for r in self._q(f'SELECT t.tx_hash FROM transactions t JOIN blocks b ON b.hash = t.block_hash '
-                                      f'WHERE {where}', args)]
+        """Hashes of the txs of the blocks matching ``where`` (a condition on ``blocks``)."""
+        return self._txs_of_blocks([r[0] for r in self._q(f'SELECT hash FROM blocks WHERE {where}', args)], 'tx_hash')
+
+    def _txs_of_blocks(self, block_hashes: List[str], cols: str) -> list:
+        """``SELECT cols FROM transactions WHERE block_hash IN (...)`` with literal lists (pushed into each
+        file's block_hash index; an IN (subquery) is not), in row id order per chunk of blocks."""
+        out = []
+        single = ',' not in cols
+        for k in range(0, len(block_hashes), 200):
+            chunk = block_hashes[k:k + 200]
+            rows = self._q(f'SELECT {cols} FROM transactions WHERE block_hash IN ({",".join("?" * len(chunk))}) '
+                           f'ORDER BY rowid', chunk)
+            out.extend(r[0] for r in rows) if single else out.extend(rows)
+        return out
+
+    # tables whose rows belong to a tx (schema.sql: tx_hash REFERENCES transactions ON DELETE CASCADE)
+    _TX_CHILDREN = ('pending_spent_outputs', 'address_transactions', *OUTPUT_TABLES[1:])
+
+    def _delete_blocks(self, where: str, args: tuple) -> List[str]:
+        """``DELETE FROM blocks WHERE <where>`` with the reference's cascade: blocks -> transactions -> every
+        table keyed by their tx hash. A split layout has no foreign keys across its files, so the cascade
+        is applied here (one temp table of the deleted hashes); unspent_outputs always is. Returns the
+        deleted txs' hashes."""
+        gone = self._block_tx_hashes(where, args)
+        if self.tx_schemas and gone:
+            with self.transaction():
+                c = self._conn
+                c.execute('CREATE TEMP TABLE IF NOT EXISTS upow_gone (h TEXT PRIMARY KEY)')
+                c.execute('DELETE FROM temp.upow_gone')
+                c.executemany('INSERT OR IGNORE INTO temp.upow_gone (h) VALUES (?)', [(h,) for h in gone])
+                for child in self._TX_CHILDREN:
+                    c.execute(f'DELETE FROM main.{child} WHERE tx_hash IN (SELECT h FROM temp.upow_gone)')
+                for schema in self.tx_schemas:
+                    c.execute(f'DELETE FROM {schema}.transactions WHERE tx_hash IN (SELECT h FROM temp.upow_gone)')
+                c.execute('DELETE FROM temp.upow_gone')
+        self._x(f'DELETE FROM blocks WHERE {where}', args)
+        self._utxo_cascade(gone)
+        return gone
 
     async def delete_block(self, id: int):
-        gone = self._block_tx_hashes('b.id = ?', (id,))
-        self._x('DELETE FROM blocks WHERE id = ?', (id,))
-        self._utxo_cascade(gone)
+        self._delete_blocks('id = ?', (id,))
         self._address_index_rollback()
         self._rebuild_utxo_index()
 
     async def delete_blocks(self, offset: int):
-        gone = self._block_tx_hashes('b.id > ?', (offset,))
-        self._x('DELETE FROM blocks WHERE id > ?', (offset,))
-        self._utxo_cascade(gone)
+        self._delete_blocks('id > ?', (offset,))
         self._address_index_rollback()
         self._rebuild_utxo_index()
 
@@ -1117,9 +1292,7 @@ class Database:
                 outputs_to_be_restored.extend([(i.tx_hash, i.index) for i in tx.inputs if i.tx_hash not in hashes])
         created = self._undo_blocks_in_index(block_no, tip)
         undone = created is not None
-        gone = self._block_tx_hashes('b.id >= ?', (block_no,))
-        self._x('DELETE FROM blocks WHERE id >= ?', (block_no,))
-        self._utxo_cascade(gone)
+        self._delete_blocks('id >= ?', (block_no,))
         self._address_index_rollback()
         await self.add_unspent_outputs(outputs_to_be_restored, index=not undone)
         if self.writer is not None:
@@ -1217,7 +1390,8 @@ class Database:
         return int(sum(r['size'] for r in rows) / MAX_BLOCK_SIZE_HEX + 1)
 
     async def clear_duplicate_pending_transactions(self):
-        self._x('DELETE FROM pending_transactions WHERE tx_hash IN (SELECT tx_hash FROM transactions)')
+        self._x('DELETE FROM pending_transactions WHERE EXISTS '
+                '(SELECT 1 FROM transactions t WHERE t.tx_hash = pending_transactions.tx_hash)')
 
     # ------------------------------------------------------------------ blocks / txs (database.py:233-437)
     async def add_transaction(self, transaction, block_hash: str):
@@ -1282,33 +1456,50 @@ class Database:
             tip = self._tip_id()
             if tip <= wm:
                 return 0
-            self._conn.execute(
-                'INSERT INTO address_transactions (address, tx_hash) '
-                'SELECT j.value, t.tx_hash FROM transactions t JOIN blocks b ON b.hash = t.block_hash, '
-                'json_each(t.inputs_addresses) j WHERE b.id > ? AND b.id <= ? '
-                'UNION '
-                'SELECT j.value, t.tx_hash FROM transactions t JOIN blocks b ON b.hash = t.block_hash, '
-                'json_each(t.outputs_addresses) j WHERE b.id > ? AND b.id <= ?', (wm, tip, wm, tip))
+            hashes = [r[0] for r in self._conn.execute('SELECT hash FROM blocks WHERE id > ? AND id <= ?', (wm, tip))]
+            for k in range(0, len(hashes), 200):  # literal lists: pushed into each tx file's block_hash index
+                chunk = hashes[k:k + 200]
+                ph = ','.join('?' * len(chunk))
+                self._conn.execute(
+                    'INSERT INTO address_transactions (address, tx_hash) '
+                    f'SELECT j.value, t.tx_hash FROM transactions t, json_each(t.inputs_addresses) j '
+                    f'WHERE t.block_hash IN ({ph}) '
+                    'UNION '
+                    f'SELECT j.value, t.tx_hash FROM transactions t, json_each(t.outputs_addresses) j '
+                    f'WHERE t.block_hash IN ({ph})', (*chunk, *chunk))
             self._conn.execute("UPDATE address_index_state SET height = ? WHERE k = 'height'", (tip,))
         return tip - wm  # (address tables feed no host cache: nothing to invalidate)
 
     # the per-address index of one block, inside the block's own journal batch (materialiser thread):
     # only when the watermark stands at the previous block, so a lagging index is left to the catch-up
     # above (rows are a set: ``get_address_transactions`` orders by block and tx rowid)
-    _ADDR_BLOCK_SQL = (
-        'INSERT INTO address_transactions (address, tx_hash) '
-        "SELECT j.value, t.tx_hash FROM transactions t, json_each(t.inputs_addresses) j WHERE t.block_hash = ?1 "
-        "AND EXISTS (SELECT 1 FROM address_index_state WHERE k = 'height' AND height = ?2) "
-        'UNION '
-        "SELECT j.value, t.tx_hash FROM transactions t, json_each(t.outputs_addresses) j WHERE t.block_hash = ?1 "
-        "AND EXISTS (SELECT 1 FROM address_index_state WHERE k = 'height' AND height = ?2)")
+    _ADDR_ROWS = 'INSERT INTO address_transactions (address, tx_hash) VALUES (?, ?)'
     _ADDR_BLOCK_WM = "UPDATE address_index_state SET height = ?2 + 1 WHERE k = 'height' AND height = ?2 AND ?1 IS NOT NULL"
 
-    def _address_index_stmts(self, block_hash: str, block_id: int) -> list:
+    @staticmethod
+    def address_rows(tx_rows) -> Tuple[List[str], List[str]]:
+        """(addresses, tx hashes) of the address_transactions rows of tx rows (block_hash, tx_hash, tx_hex,
+        inputs_addresses, outputs_addresses, ...): each distinct address among a tx's inputs and outputs
+        (json_each(inputs_addresses) UNION json_each(outputs_addresses))."""
+        addrs, hashes = [], []
+        for r in tx_rows:
+            seen = dict.fromkeys(a for col in (r[3], r[4]) for a in (json.loads(col) if col else [])
+                                 if isinstance(a, str))
+            addrs.extend(seen)
+            hashes.extend([r[1]] * len(seen))
+        return addrs, hashes
+
+    def _address_index_stmts(self, block_hash: str, block_id: int, rows: list) -> list:
+        """The block's address_transactions rows (``rows``: (address column spec, tx hash column spec, n)
+        parts) and the watermark update, applied only while the index is caught up to the block before
+        (otherwise :meth:`index_addresses` catches it up lazily). Rows are a set: ``get_address_transactions``
+        orders by block and tx row id."""
         if os.environ.get('UPOW_ADDRESS_INDEX_INLINE', '1') == '0':
             return []
-        return [(self._ADDR_BLOCK_SQL, [block_hash, block_id - 1], 1, None, None, None),
-                (self._ADDR_BLOCK_WM, [block_hash, block_id - 1], 1, None, None, None)]
+        guard = f"SELECT EXISTS(SELECT 1 FROM address_index_state WHERE k = 'height' AND height = {int(block_id) - 1})"
+        out = [(self._ADDR_ROWS, [a, h], n, None, guard, None) for a, h, n in rows if n]
+        out.append((self._ADDR_BLOCK_WM, [block_hash, block_id - 1], 1, None, None, None))
+        return out
 
     def _address_index_rollback(self):
         """After blocks were deleted (their address rows cascade away), pull the watermark down."""
@@ -1494,10 +1685,7 @@ class Database:
         index = {b['hash']: [] for b in blocks}
         index_tx_hash = {b['hash']: [] for b in blocks}
         if blocks:
-            for t in self._q('SELECT transactions.tx_hex, transactions.tx_hash, transactions.block_hash FROM '
-                             'transactions INNER JOIN blocks ON blocks.hash = transactions.block_hash '
-                             'WHERE blocks.id >= ? AND blocks.id <= ? ORDER BY transactions.rowid',
-                             (blocks[0]['id'], blocks[-1]['id'])):
+            for t in self._txs_of_blocks([b['hash'] for b in blocks], 'tx_hex, tx_hash, block_hash'):
                 if t['block_hash'] in index:
                     index[t['block_hash']].append(t['tx_hex'])
                     index_tx_hash[t['block_hash']].append(t['tx_hash'])
@@ -1587,7 +1775,7 @@ class Database:
 
     def apply_native_block(self, block_row: dict, coinbase_row: tuple, coinbase_outputs: list, n: int,
                            tx_cols: list, out_cols: tuple, in_keys: np.ndarray, spent_payload: np.ndarray,
-                           gov: Optional[dict] = None) -> int:
+                           gov: Optional[dict] = None, addr_pairs: Optional[tuple] = None) -> int:
         """The ledger writes of one native-path block (reference manager.py:706-730: add_block,
         add_transaction(coinbase), add_transactions, add_transaction_outputs, remove_pending_transactions,
         remove_outputs, remove_pending_spent_outputs) as ONE journal batch, plus the HBM index update.
@@ -1639,19 +1827,19 @@ class Database:
 
         # ---- statements (schema.sql write set of one block)
         b = block_row
+        tx_base = self._tx_rowids(n + 1)  # the coinbase row first, then the block's txs (insertion order)
         stmts = [
             ('INSERT INTO blocks (id, hash, content, address, random, difficulty, reward, timestamp) '
              'VALUES (?, ?, ?, ?, ?, ?, ?, ?)',
              [int(b['id']), b['hash'], b['content'], b['address'], int(b['random']), b['difficulty'], b['reward'],
               int(b['timestamp'])], 1, None, None, None),
-            ('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, outputs_addresses, '
-             'outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)', list(coinbase_row), 1, None, None, None),
+            (self._TX_INSERT, [coinbase_row[1], coinbase_row[0], *coinbase_row[2:], tx_base], 1, None, None, None),
         ]
         self.checkpoint('block')
-        stmts.append(('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, outputs_addresses, '
-                      'outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)', [b['hash'], *tx_cols], n, None, None, None))
+        stmts.append((self._TX_INSERT, [tx_cols[0], b['hash'], *tx_cols[1:],
+                                        np.arange(tx_base + 1, tx_base + 1 + n, dtype=np.int64)], n, None, None, None))
         self.checkpoint('transactions')
-        # explicit row ids from the ledger-wide counter: the rows land in two files (see UTXO_SCHEMAS)
+        # explicit row ids from the ledger-wide counter: the rows land in several files (see UTXO_FILES_DEFAULT)
         ins_u = 'INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake, rowid) VALUES (?, ?, ?, ?, ?)'
         if gov is None:
             if n_out:
@@ -1726,7 +1914,14 @@ class Database:
                           'SELECT EXISTS(SELECT 1 FROM pending_spent_outputs)', None))
             tables |= {'pending_transactions', 'pending_spent_outputs'}
         self.checkpoint('spent')
-        stmts.extend(self._address_index_stmts(b['hash'], int(b['id'])))
+        # address index rows: the coinbase's, then the txs' (txcodec.address_pairs: blob, offsets, tx index)
+        ca, ch = self.address_rows([coinbase_row])
+        parts = [(ca, ch, len(ca))]
+        if addr_pairs is not None:
+            ab, ao, at = addr_pairs
+            parts.append((('arena', ab, ao), ('hex32', tx_cols[0][1], 32, 0, np.frombuffer(at, dtype=np.int64)),
+                          len(at) // 8))
+        stmts.extend(self._address_index_stmts(b['hash'], int(b['id']), parts))
         tables |= {'address_transactions', 'address_index_state'}
 
         seq = 0
@@ -1816,14 +2011,16 @@ class Database:
         b = block_row
         txs = [coinbase] + list(transactions)
         rows = [await self._tx_row(t, b['hash']) for t in txs]  # coinbase row first, as add_transaction did
-        tx_sql = ('INSERT INTO transactions (block_hash, tx_hash, tx_hex, inputs_addresses, outputs_addresses, '
-                  'outputs_amounts, fees) VALUES (?, ?, ?, ?, ?, ?, ?)')
+        tx_base = self._tx_rowids(len(rows))
         stmts = [('INSERT INTO blocks (id, hash, content, address, random, difficulty, reward, timestamp) '
                   'VALUES (?, ?, ?, ?, ?, ?, ?, ?)',
                   [int(b['id']), b['hash'], b['content'], b['address'], int(b['random']), b['difficulty'], b['reward'],
                    int(b['timestamp'])], 1, None, None, None)]
         self.checkpoint('block')
-        stmts.append((tx_sql, [list(col) for col in zip(*rows)], len(rows), None, None, None))
+        cols = [list(col) for col in zip(*rows)]
+        stmts.append((self._TX_INSERT, [cols[1], cols[0], *cols[2:],
+                                        np.arange(tx_base, tx_base + len(rows), dtype=np.int64)], len(rows), None, None,
+                      None))
         self.checkpoint('transactions')
         outs = self.split_outputs(list(transactions) + [coinbase])
         created = []  # (table, key, payload fields) for the indexes
@@ -1863,7 +2060,8 @@ class Database:
                           'SELECT EXISTS(SELECT 1 FROM pending_spent_outputs)', None))
             tables |= {'pending_transactions', 'pending_spent_outputs'}
         self.checkpoint('spent')
-        stmts.extend(self._address_index_stmts(b['hash'], int(b['id'])))
+        aa, ah = self.address_rows(rows)
+        stmts.extend(self._address_index_stmts(b['hash'], int(b['id']), [(aa, ah, len(aa))]))
         tables |= {'address_transactions', 'address_index_state'}
 
         # ---- index records: created outputs (per table) and spent outpoints with their current payloads
@@ -2209,14 +2407,10 @@ class Database:
     async def get_unspent_outputs_from_all_transactions(self):
         """database.py:846-862: replay every tx in block order (UTXO rebuild tool)."""
         outputs = set()
-        rows = self._q('SELECT tx_hex, blocks.id AS block_no FROM transactions INNER JOIN blocks ON '
-                       '(transactions.block_hash = blocks.hash) ORDER BY blocks.id ASC, transactions.rowid ASC')
-        last_block_no = 0
-        for r in rows:
-            if r['block_no'] != last_block_no:
-                last_block_no = r['block_no']
-            tx_hash = sha256(r['tx_hex'])
-            tx = await Transaction.from_hex(r['tx_hex'], check_signatures=False)
+        blocks = [r[0] for r in self._q('SELECT hash FROM blocks ORDER BY id ASC')]
+        for tx_hex in (h for b in blocks for h in self._txs_of_blocks([b], 'tx_hex')):
+            tx_hash = sha256(tx_hex)
+            tx = await Transaction.from_hex(tx_hex, check_signatures=False)
             if isinstance(tx, Transaction):
                 outputs = outputs.difference({(i.tx_hash, i.index) for i in tx.inputs})
             outputs.update({(tx_hash, index) for index in range(len(tx.outputs))})
@@ -2244,10 +2438,11 @@ class Database:
         self.index_addresses()
         forms = self._forms(address)
         ph = ','.join('?' * len(forms))
-        rows = self._q(f'SELECT DISTINCT transactions.tx_hex, blocks.id AS block_no, transactions.rowid AS rid '
-                       f'FROM address_transactions INNER JOIN transactions ON '
-                       f'(address_transactions.tx_hash = transactions.tx_hash) INNER JOIN blocks ON '
-                       f'(transactions.block_hash = blocks.hash) WHERE address_transactions.address IN ({ph}) '
+        key = 'a.tx_hash'
+        rows = self._q(f'SELECT tx_hex, block_no, rid FROM (SELECT DISTINCT a.tx_hash, {self._txq("tx_hex", key)} AS tx_hex, '
+                       f'{self._txq("rowid", key)} AS rid, (SELECT b.id FROM blocks b WHERE b.hash = '
+                       f'{self._txq("block_hash", key)}) AS block_no FROM address_transactions a '
+                       f'WHERE a.address IN ({ph})) WHERE tx_hex IS NOT NULL AND block_no IS NOT NULL '
                        f'ORDER BY block_no DESC, rid LIMIT ? OFFSET ?', (*forms, limit, offset))
         txs = [r['tx_hex'] for r in rows]
         if check_pending_txs:
@@ -2265,13 +2460,13 @@ class Database:
                      args: tuple = ()):
         """``SELECT t.tx_hash, index, transactions.outputs_amounts[index + 1] FROM t JOIN transactions``."""
         ph = ','.join('?' * len(forms))
-        rows = self._q(f'SELECT {table}.tx_hash AS tx_hash, {table}."index" AS idx, transactions.outputs_amounts AS am '
-                       f'FROM {table} INNER JOIN transactions ON (transactions.tx_hash = {table}.tx_hash) '
-                       f'WHERE {table}.address IN ({ph}) {where} ORDER BY {table}.rowid', (*forms, *args))
+        rows = self._q(f'SELECT {table}.tx_hash AS tx_hash, {table}."index" AS idx, '
+                       f'{self._txq("outputs_amounts", table + ".tx_hash")} AS am '
+                       f'FROM {table} WHERE {table}.address IN ({ph}) {where} ORDER BY {table}.rowid', (*forms, *args))
         pend = self._pending_spent_set() if check_pending else set()
         out = []
         for r in rows:
-            if (r['tx_hash'], r['idx']) in pend:
+            if r['am'] is None or (r['tx_hash'], r['idx']) in pend:  # (INNER JOIN transactions)
                 continue
             out.append((r['tx_hash'], r['idx'], _at(_arr(r['am']), r['idx'])))
         return out
@@ -2356,11 +2551,13 @@ class Database:
             return [TransactionInput(h, i, amount=Decimal(a) / SMALLEST, public_key=point)
                     for (h, i), a in self.gov.spent_votes(table, forms, check_pending)]
         pend = self._pending_spent_set() if check_pending else set()
-        rows = self._q(f'SELECT {table}.tx_hash AS tx_hash, {table}."index" AS idx, transactions.outputs_amounts AS am, '
-                       f'transactions.inputs_addresses AS ia FROM transactions INNER JOIN {table} ON '
-                       f'(transactions.tx_hash = {table}.tx_hash) ORDER BY {table}.rowid')
+        key = f'{table}.tx_hash'
+        rows = self._q(f'SELECT {table}.tx_hash AS tx_hash, {table}."index" AS idx, {self._txq("outputs_amounts", key)} AS am, '
+                       f'{self._txq("inputs_addresses", key)} AS ia FROM {table} ORDER BY {table}.rowid')
         out = []
         for r in rows:
+            if r['am'] is None:  # (INNER JOIN transactions)
+                continue
             if _at(_arr(r['ia']), r['idx']) in forms and (r['tx_hash'], r['idx']) not in pend:
                 out.append(TransactionInput(r['tx_hash'], r['idx'], amount=Decimal(_at(_arr(r['am']), r['idx'])) / SMALLEST,
                                             public_key=point))
@@ -2388,14 +2585,14 @@ class Database:
         if receiver_forms is not None:
             where = f'WHERE {table}.address IN ({",".join("?" * len(receiver_forms))})'
             args = list(receiver_forms)
+        key = f'{table}.tx_hash'
         rows = self._q(f'SELECT {table}.tx_hash AS tx_hash, {table}.address AS receiver, {table}."index" AS idx, '
-                       f'transactions.outputs_amounts AS am, transactions.inputs_addresses AS ia FROM {table} '
-                       f'INNER JOIN transactions ON (transactions.tx_hash = {table}.tx_hash) {where} '
-                       f'ORDER BY {(table + ".tx_hash, ") if order else ""}{table}.rowid', args)
+                       f'{self._txq("outputs_amounts", key)} AS am, {self._txq("inputs_addresses", key)} AS ia '
+                       f'FROM {table} {where} ORDER BY {(table + ".tx_hash, ") if order else ""}{table}.rowid', args)
         pend = self._pending_spent_set() if check_pending else set()
         out = []
         for r in rows:
-            if (r['tx_hash'], r['idx']) in pend:
+            if r['am'] is None or (r['tx_hash'], r['idx']) in pend:  # (INNER JOIN transactions)
                 continue
             voter = _at(_arr(r['ia']), r['idx'])
             if voter_forms is not None and voter not in voter_forms:
@@ -2435,8 +2632,8 @@ class Database:
         return self._ballot_rows('validators_ballot', self._forms(validator), check_pending_txs, limit, offset)
 
     async def get_transaction_time(self, tx_hash) -> datetime:
-        r = self._q1('SELECT blocks.timestamp FROM blocks INNER JOIN transactions ON '
-                     '(blocks.hash = transactions.block_hash) WHERE transactions.tx_hash = ?', (tx_hash,))
+        r = self._q1('SELECT timestamp FROM blocks WHERE hash = '
+                     '(SELECT block_hash FROM transactions WHERE tx_hash = ?)', (tx_hash,))
         assert r is not None
         return _dt(r[0])
 
@@ -2559,12 +2756,13 @@ class Database:
     async def get_all_registered_inode(self, check_pending_txs: bool = False):
         if self.gov is not None:
             return [(a, _dt(ts)) for a, ts in self.gov.registered_inodes(check_pending_txs)]
-        rows = self._q('SELECT inode_registration_output.address AS address, inode_registration_output.tx_hash AS h, '
-                       'inode_registration_output."index" AS idx, blocks.timestamp AS ts FROM inode_registration_output '
-                       'INNER JOIN transactions ON inode_registration_output.tx_hash = transactions.tx_hash '
-                       'INNER JOIN blocks ON transactions.block_hash = blocks.hash ORDER BY inode_registration_output.rowid')
+        t = 'inode_registration_output'
+        rows = self._q(f'SELECT {t}.address AS address, {t}.tx_hash AS h, {t}."index" AS idx, '
+                       f'(SELECT b.timestamp FROM blocks b WHERE b.hash = {self._txq("block_hash", t + ".tx_hash")}) AS ts '
+                       f'FROM {t} ORDER BY {t}.rowid')
         pend = self._pending_spent_set() if check_pending_txs else set()
-        return [(r['address'], _dt(r['ts'])) for r in rows if (r['h'], r['idx']) not in pend]
+        # (INNER JOIN transactions, blocks: rows without both have no timestamp)
+        return [(r['address'], _dt(r['ts'])) for r in rows if r['ts'] is not None and (r['h'], r['idx']) not in pend]
 
     async def get_active_inodes(self, check_pending_txs: bool = False):
         codec.getting_active_inodes = True
@@ -2615,31 +2813,30 @@ class Database:
             for k in range(0, len(hashes), 500):
                 chunk = hashes[k:k + 500]
                 recent.update(r[0] for r in self._q(
-                    f'SELECT t.tx_hash FROM transactions t INNER JOIN blocks b ON b.hash = t.block_hash '
-                    f'WHERE t.tx_hash IN ({",".join("?" * len(chunk))}) AND b.id >= ?', (*chunk, block_no)))
+                    f'SELECT t.tx_hash FROM transactions t WHERE t.tx_hash IN ({",".join("?" * len(chunk))}) '
+                    f'AND (SELECT b.id FROM blocks b WHERE b.hash = t.block_hash) >= ?', (*chunk, block_no)))
             unspent = [TransactionInput(h, i, amount=Decimal(a) / SMALLEST, public_key=point)
                        for h, i, a in hits if h in recent]
         else:
+            key = 'unspent_outputs.tx_hash'
             rows = self._q(f'SELECT unspent_outputs.tx_hash AS h, unspent_outputs."index" AS idx, '
-                           f'transactions.outputs_amounts AS am FROM unspent_outputs INNER JOIN transactions ON '
-                           f'(transactions.tx_hash = unspent_outputs.tx_hash) INNER JOIN blocks ON '
-                           f'(blocks.hash = transactions.block_hash) WHERE unspent_outputs.address IN ({ph}) '
-                           f'AND blocks.id >= ? ORDER BY unspent_outputs.rowid', (*forms, block_no))
+                           f'{self._txq("outputs_amounts", key)} AS am FROM unspent_outputs '
+                           f'WHERE unspent_outputs.address IN ({ph}) AND (SELECT b.id FROM blocks b WHERE b.hash = '
+                           f'{self._txq("block_hash", key)}) >= ? ORDER BY unspent_outputs.rowid', (*forms, block_no))
             unspent = [TransactionInput(r['h'], r['idx'], amount=Decimal(_at(_arr(r['am']), r['idx'])) / SMALLEST,
                                         public_key=point) for r in rows]
-        srows = self._q('SELECT transactions.tx_hex AS tx_hex, transactions.inputs_addresses AS ia FROM transactions '
-                        'INNER JOIN blocks ON (transactions.block_hash = blocks.hash) WHERE blocks.id >= ? '
-                        'ORDER BY transactions.rowid', (block_no,))
+        srows = self._txs_of_blocks([r[0] for r in self._q('SELECT hash FROM blocks WHERE id >= ?', (block_no,))],
+                                    'tx_hex, inputs_addresses AS ia')
         spending = [await Transaction.from_hex(r['tx_hex'], False) for r in srows if address in _arr(r['ia'])][:block_no]
         return unspent, [i for tx in spending for i in tx.inputs]
 
     async def get_nice_transaction(self, tx_hash: str, address: str = None):
         """database.py:1606-1654."""
         is_confirm = True
-        res = self._q1('SELECT transactions.tx_hex AS tx_hex, transactions.tx_hash AS tx_hash, transactions.block_hash '
-                       'AS block_hash, transactions.inputs_addresses AS inputs_addresses, blocks.id AS block_no, '
-                       'blocks.timestamp AS timestamp FROM transactions INNER JOIN blocks ON '
-                       '(transactions.block_hash = blocks.hash) WHERE tx_hash = ?', (tx_hash,))
+        res = self._q1('SELECT t.tx_hex AS tx_hex, t.tx_hash AS tx_hash, t.block_hash AS block_hash, '
+                       't.inputs_addresses AS inputs_addresses, b.id AS block_no, b.timestamp AS timestamp '
+                       'FROM (SELECT tx_hex, tx_hash, block_hash, inputs_addresses FROM transactions WHERE tx_hash = ?) t '
+                       'INNER JOIN blocks b ON t.block_hash = b.hash', (tx_hash,))
         if res is None:
             res = self._q1('SELECT tx_hex, tx_hash, inputs_addresses FROM pending_transactions WHERE tx_hash = ?',
                            (tx_hash,))

@@ -302,8 +302,10 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     #      batch by csrc/ledger_writer.cpp (tx hashes rendered from the raw digests, text arenas for strings)
     L = lib()
     in_str = L.input_address_strings(np.ascontiguousarray(pay['addr']).tobytes(), pay['len'].astype(np.uint8).tobytes(),
-                                     d['in_start'], THREADS, bg.any)
+                                     d['in_start'], THREADS, True)
     in_json = in_str[:2]
+    # the block's address_transactions rows (each tx's distinct input owners and output addresses)
+    addr_pairs = L.address_pairs(in_str[2], in_str[3], d['in_start'], *d['out_addr_str'], d['out_start'])
     fee_str = L.fee_strings(np.ascontiguousarray(fee, dtype=np.int64).tobytes())
     out_index = np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]
     gov_cols = None
@@ -326,7 +328,7 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         submitted = database._submitted
         try:
             seq = database.apply_native_block(block_row, cb_row, cb_outputs, n, tx_cols, out_cols, in_keys, pay,
-                                              gov=gov_cols)
+                                              gov=gov_cols, addr_pairs=addr_pairs)
         except Exception as e:
             if database._submitted != submitted:
                 raise  # committed to the journal: a failure after the commit point is not a rejection

@@ -23,7 +23,7 @@ from typing import Optional
 
 import numpy as np
 
-from ..constants import MAX_INODES, SMALLEST
+from ..constants import MAX_INODES
 from ..utils import codec
 from ..utils.codec import OutputType, TransactionType
 
@@ -43,7 +43,6 @@ OUTPUT_TABLE = {int(O.REGULAR): 'unspent_outputs', int(O.STAKE): 'unspent_output
                 int(O.VALIDATOR_VOTING_POWER): VVP_T, int(O.DELEGATE_VOTING_POWER): DVP_T,
                 int(O.VOTE_AS_VALIDATOR): IBALLOT_T, int(O.VOTE_AS_DELEGATE): VBALLOT_T}
 UNSTAKE_EXCEPTION = '8befeb253bc6eddd8501f5b27a02b195f5c06a51ccf788213cbedafe7cc49c53'  # transaction.py:472
-_REVOKES = (int(T.REVOKE_AS_VALIDATOR), int(T.REVOKE_AS_DELEGATE))
 
 
 def _seg(values: np.ndarray, starts: np.ndarray) -> np.ndarray:

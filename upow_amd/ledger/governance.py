@@ -157,9 +157,12 @@ class GovernanceIndex:
         if where:
             cond.append(where)
         w = ('WHERE ' + ' AND '.join(cond)) if cond else ''
-        return self.db._q(f'SELECT u.tx_hash, u."index", u.address, t.outputs_amounts, t.inputs_addresses, b.timestamp '
-                          f'FROM {src} u INNER JOIN transactions t ON t.tx_hash = u.tx_hash '
-                          f'LEFT JOIN blocks b ON b.hash = t.block_hash {w} ORDER BY u.rowid', args)
+        txq = self.db._txq  # correlated lookups: pushed into each file of a split transactions table
+        rows = self.db._q(f'SELECT u.tx_hash, u."index", u.address, {txq("outputs_amounts", "u.tx_hash")}, '
+                          f'{txq("inputs_addresses", "u.tx_hash")}, (SELECT b.timestamp FROM blocks b WHERE b.hash = '
+                          f'{txq("block_hash", "u.tx_hash")}), {txq("rowid", "u.tx_hash")} FROM {src} u {w} ORDER BY u.rowid',
+                          args)
+        return [r[:6] for r in rows if r[6] is not None]  # (INNER JOIN transactions)
 
     def _add_sql_rows(self, table: str, rows, only: Optional[Set[Key]] = None):
         import json
