@@ -74,6 +74,9 @@ struct Row {
     uint64_t seq = 0;
     Pt pt{}, vpt{};
     uint8_t f = 0;
+    uint8_t term = 0;  // ballots: 0 no term in its receiver's sum, 1 unknown (sum marked bad), 2 term_c/term_e
+    int8_t term_e = 0;
+    __int128 term_c = 0;
 };
 
 using KeySet = std::unordered_set<Key, KHash>;
@@ -100,41 +103,47 @@ i128 p10(int k) {
 inline i128 iabs(i128 x) { return x < 0 ? -x : x; }
 const int kPrec = 28;
 
+// division and remainder by a positive power of ten: 64-bit instructions when both fit (the common case
+// for amounts and votes), the 128-bit library routine otherwise
+inline bool small(i128 x) { return x >= INT64_MIN && x <= INT64_MAX; }
+inline i128 qdiv(i128 a, i128 m) { return small(a) && small(m) ? i128(int64_t(a) / int64_t(m)) : a / m; }
+inline i128 qmod(i128 a, i128 m) { return small(a) && small(m) ? i128(int64_t(a) % int64_t(m)) : a % m; }
+
 struct Dec {
     i128 c = 0;
     int e = 0;
 };
 inline bool fits(i128 c) { return iabs(c) < p10(kPrec); }
+// c * 10^k still within 28 digits (checked before multiplying: no 128-bit overflow)
+inline bool scale_fits(i128 c, int k) { return k >= 0 && k <= kPrec && iabs(c) < p10(kPrec - k); }
 
 // Decimal(amount) / SMALLEST (1e8): the exact quotient at the exponent closest to the ideal 0
 Dec from_amount(int64_t a) {
-    Dec d{i128(a), 0};
-    if (a == 0) return d;
+    if (a == 0) return Dec{0, 0};
+    int64_t c = a;
     int t = 0;
-    while (t < 8 && d.c % 10 == 0) {
-        d.c /= 10;
+    while (t < 8 && c % 10 == 0) {
+        c /= 10;
         ++t;
     }
-    d.e = -(8 - t);
-    return d;
+    return Dec{i128(c), -(8 - t)};
 }
 
 bool mul(const Dec& a, const Dec& b, Dec& out) {
-    const i128 x = iabs(a.c), y = iabs(b.c);
-    if (x && y > (p10(kPrec) - 1) / x) return false;  // more than 28 digits: Python would round
-    out = {a.c * b.c, a.e + b.e};
+    i128 c;
+    if (__builtin_mul_overflow(a.c, b.c, &c) || !fits(c)) return false;  // more than 28 digits: Python rounds
+    out = {c, a.e + b.e};
     return true;
 }
 
 // x / 10 (Decimal(10)): exact, at the ideal exponent x.e when the coefficient allows
-Dec div10(const Dec& a) { return a.c % 10 == 0 ? Dec{a.c / 10, a.e} : Dec{a.c, a.e - 1}; }
+Dec div10(const Dec& a) { return qmod(a.c, 10) == 0 ? Dec{qdiv(a.c, 10), a.e} : Dec{a.c, a.e - 1}; }
 
 bool add(const Dec& a, const Dec& b, int sign, Dec& out) {
     const int e = std::min(a.e, b.e);
     const int da = a.e - e, db = b.e - e;
-    if (da > kPrec || db > kPrec) return false;
+    if (!scale_fits(a.c, da) || !scale_fits(b.c, db)) return false;
     const i128 ac = a.c * p10(da), bc = b.c * p10(db);
-    if (!fits(ac) || !fits(bc)) return false;
     const i128 c = sign > 0 ? ac + bc : ac - bc;
     if (!fits(c)) return false;
     out = {c, e};
@@ -143,16 +152,14 @@ bool add(const Dec& a, const Dec& b, int sign, Dec& out) {
 
 bool quantize_exact(const Dec& a, int e, Dec& out) {
     if (e < a.e) {
-        if (e < a.e - kPrec) return false;
-        const i128 c = a.c * p10(a.e - e);
-        if (!fits(c)) return false;
-        out = {c, e};
+        if (!scale_fits(a.c, a.e - e)) return false;
+        out = {a.c * p10(a.e - e), e};
         return true;
     }
     if (e - a.e > 38) return false;
     const i128 m = p10(e - a.e);
-    if (a.c % m != 0) return false;
-    out = {a.c / m, e};
+    if (qmod(a.c, m) != 0) return false;
+    out = {qdiv(a.c, m), e};
     return true;
 }
 
@@ -162,8 +169,9 @@ Dec round_up(const Dec& d) {
     const int k = -8 - d.e;
     if (k > 38) return Dec{0, -8};
     const i128 m = p10(k);
-    if (d.c % m == 0) return d;
-    i128 q = d.c / m, r = d.c % m;
+    const i128 r = qmod(d.c, m);
+    if (r == 0) return d;
+    i128 q = qdiv(d.c, m);
     const i128 twice = 2 * iabs(r);
     if (twice > m || (twice == m && (q % 2 != 0))) q += d.c < 0 ? -1 : 1;
     return Dec{q, -8};
@@ -185,28 +193,26 @@ py::object dec_py(const Dec& d) {
 }
 
 struct XSum {  // sum(terms, Decimal(0)) under additions and removals, exact or not ok
+    static constexpr int kLo = -56, kN = 64;  // term exponents kept: [-56, 7]
     Dec v;
-    std::map<int, int> exps;
+    int32_t cnt[kN] = {};  // live terms per exponent (the result's exponent is min(0, smallest live one))
     bool ok = true;
     void update(const Dec& t, int sign) {
         if (!ok) return;
         Dec r;
-        if (!add(v, t, sign, r)) {
+        if (t.e < kLo || t.e >= kLo + kN || !add(v, t, sign, r)) {
             ok = false;
             return;
         }
         v = r;
-        int& n = exps[t.e];
-        n += sign;
-        if (n == 0) exps.erase(t.e);
+        cnt[t.e - kLo] += sign;
     }
     bool result(Dec& out) const {
         if (!ok) return false;
-        if (exps.empty()) {
-            out = Dec{0, 0};
-            return true;
-        }
-        return quantize_exact(v, std::min(0, exps.begin()->first), out);
+        for (int i = 0; i < kN; ++i)
+            if (cnt[i]) return quantize_exact(v, std::min(0, i + kLo), out);
+        out = Dec{0, 0};
+        return true;
     }
 };
 
@@ -301,8 +307,6 @@ class GovStore {
         astake_.clear();
         vsum_.clear();
         isum_.clear();
-        vterm_.clear();
-        iterm_.clear();
         vval_.clear();
         bad_v_.clear();
         bad_i_.clear();
@@ -429,17 +433,17 @@ class GovStore {
         astake_.clear();
         vsum_.clear();
         isum_.clear();
-        vterm_.clear();
-        iterm_.clear();
         vval_.clear();
         bad_v_.clear();
         bad_i_.clear();
         pending_v_.clear();
         live_ = false;
         for (auto& kv : tabs_[STAKE].rows) stake_row(kv.second, 1, false);
-        for (auto& kv : tabs_[VBALLOT].rows) vballot(kv.first, kv.second, 1, false);
+        for (auto* t : {&tabs_[VBALLOT], &tabs_[IBALLOT]})
+            for (auto& kv : t->rows) kv.second.term = 0;
+        for (auto& kv : tabs_[VBALLOT].rows) vballot(kv.second, 1, false);
         vval_.clear();
-        for (auto& kv : tabs_[IBALLOT].rows) iballot(kv.first, kv.second, 1);
+        for (auto& kv : tabs_[IBALLOT].rows) iballot(kv.second, 1);
         live_ = true;
     }
 
@@ -688,14 +692,14 @@ class GovStore {
         row.seq = t.next_seq++;
         auto& ref = t.rows.emplace(k, std::move(row)).first->second;
         index_add(t, k, ref);
-        if (live_) changed(tid, k, ref, 1);
+        if (live_) changed(tid, ref, 1);
     }
 
     int erase(int tid, const Key& k) {
         Table& t = tabs_.at(size_t(tid));
         auto it = t.rows.find(k);
         if (it == t.rows.end()) return 0;
-        if (live_) changed(tid, k, it->second, -1);
+        if (live_) changed(tid, it->second, -1);
         const Row& r = it->second;
         if (r.f & HAS_ADDR) index_del(t.by_addr, r.addr, k);
         if (r.f & HAS_VOTER) index_del(t.by_voter, r.voter, k);
@@ -729,27 +733,31 @@ class GovStore {
         return true;
     }
 
-    void vballot(const Key& k, const Row& row, int sign, bool propagate) {
-        Pt recv = row.pt;
+    // a ballot's term vote * stake(voter) / 10 enters (sign > 0) or leaves its receiver's sum; the term is
+    // kept on the row (the receiver is the row's own point, which never changes)
+    static void set_term(Row& row, bool ok, const Dec& t) {
+        row.term = ok ? 2 : 1;
+        row.term_c = t.c;
+        row.term_e = int8_t(t.e);
+    }
+
+    void vballot(Row& row, int sign, bool propagate) {
+        const Pt& recv = row.pt;
         if (sign > 0) {
-            Dec st, term, prod;
+            Dec st, prod;
             bool ok = (row.f & HAS_AMOUNT) && (row.f & HAS_VOTER) && row.vpt != kNoPt && stake(row.vpt, st) &&
                       mul(from_amount(row.amount), st, prod);
             if (!ok) {
                 bad_v_.insert(recv);
-                vterm_[k] = {recv, std::nullopt};
+                set_term(row, false, Dec{});
             } else {
-                term = div10(prod);
+                const Dec term = div10(prod);
                 vsum_[recv].update(term, 1);
-                vterm_[k] = {recv, term};
+                set_term(row, true, term);
             }
-        } else {
-            auto it = vterm_.find(k);
-            if (it != vterm_.end()) {
-                recv = it->second.first;
-                if (it->second.second) vsum_[recv].update(*it->second.second, -1);
-                vterm_.erase(it);
-            }
+        } else if (row.term) {
+            if (row.term == 2) vsum_[recv].update(Dec{row.term_c, row.term_e}, -1);
+            row.term = 0;
         }
         if (propagate) {
             pending_v_.insert(recv);
@@ -757,27 +765,23 @@ class GovStore {
         }
     }
 
-    void iballot(const Key& k, const Row& row, int sign) {
-        Pt recv = row.pt;
+    void iballot(Row& row, int sign) {
+        const Pt& recv = row.pt;
         if (sign > 0) {
             Dec vs, prod;
             bool ok = (row.f & HAS_AMOUNT) && (row.f & HAS_VOTER) && row.vpt != kNoPt && vstake(row.vpt, vs) &&
                       mul(from_amount(row.amount), vs, prod);
             if (!ok) {
                 bad_i_.insert(recv);
-                iterm_[k] = {recv, std::nullopt};
+                set_term(row, false, Dec{});
             } else {
-                Dec term = div10(prod);
+                const Dec term = div10(prod);
                 isum_[recv].update(term, 1);
-                iterm_[k] = {recv, term};
+                set_term(row, true, term);
             }
-        } else {
-            auto it = iterm_.find(k);
-            if (it != iterm_.end()) {
-                recv = it->second.first;
-                if (it->second.second) isum_[recv].update(*it->second.second, -1);
-                iterm_.erase(it);
-            }
+        } else if (row.term) {
+            if (row.term == 2) isum_[recv].update(Dec{row.term_c, row.term_e}, -1);
+            row.term = 0;
         }
     }
 
@@ -792,9 +796,9 @@ class GovStore {
             if (it == tabs_[VBALLOT].by_vpt.end()) return;
             std::vector<Key> ks(it->second.begin(), it->second.end());
             for (auto& k : ks) {
-                const Row& r = tabs_[VBALLOT].rows.at(k);
-                vballot(k, r, -1, false);
-                vballot(k, r, 1, true);
+                Row& r = tabs_[VBALLOT].rows.at(k);
+                vballot(r, -1, false);
+                vballot(r, 1, true);
             }
         }
     }
@@ -807,26 +811,25 @@ class GovStore {
             if (it == tabs_[IBALLOT].by_vpt.end()) continue;
             std::vector<Key> ks(it->second.begin(), it->second.end());
             for (auto& k : ks) {
-                const Row& r = tabs_[IBALLOT].rows.at(k);
-                iballot(k, r, -1);
-                iballot(k, r, 1);
+                Row& r = tabs_[IBALLOT].rows.at(k);
+                iballot(r, -1);
+                iballot(r, 1);
             }
         }
     }
 
-    void changed(int tid, const Key& k, const Row& row, int sign) {
+    void changed(int tid, Row& row, int sign) {
         if (tid == STAKE)
             stake_row(row, sign, true);
         else if (tid == VBALLOT)
-            vballot(k, row, sign, true);
+            vballot(row, sign, true);
         else if (tid == IBALLOT)
-            iballot(k, row, sign);
+            iballot(row, sign);
     }
 
     std::array<Table, NT> tabs_;
     bool live_ = false;
     std::unordered_map<Pt, XSum, PHash> astake_, vsum_, isum_;
-    std::unordered_map<Key, std::pair<Pt, std::optional<Dec>>, KHash> vterm_, iterm_;
     std::unordered_map<Pt, Dec, PHash> vval_;
     std::unordered_set<Pt, PHash> bad_v_, bad_i_, pending_v_;
 };
