@@ -44,7 +44,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 #include <dirent.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -1284,6 +1286,14 @@ class LedgerWriter {
 
     void run(size_t i) {
         Shard& sh = *shards_[i];
+        // materialising is background work: below the block path and the HTTP loop in the CPU share the
+        // process gets (GPU boxes run a node under a CPU quota far below the core count)
+        if (const char* nv = std::getenv("UPOW_WRITER_NICE")) {
+            const int n = std::atoi(nv);
+            if (n > 0) setpriority(PRIO_PROCESS, pid_t(syscall(SYS_gettid)), n);
+        } else {
+            setpriority(PRIO_PROCESS, pid_t(syscall(SYS_gettid)), 5);
+        }
         for (;;) {
             std::vector<Batch> group;
             {

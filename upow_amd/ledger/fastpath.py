@@ -45,14 +45,27 @@ from .govcheck import BlockGovernance
 from .utxo import TAG_BY_TABLE
 
 logger = get_logger(__name__)
-def _codec_threads() -> int:
-    """Host threads for the block codec: the CPUs this process may run on (affinity, not the machine
-    total), capped at 16, minus two for the ledger's materialiser threads that run concurrently."""
+def cpu_budget() -> int:
+    """CPUs this process can actually use: its affinity, capped by a cgroup CPU quota (a GPU box gives a
+    node 16 CPUs' worth of time on a 256-core host; threads beyond that are throttled, not parallel)."""
     try:
         avail = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         avail = os.cpu_count() or 1
-    return max(1, min(16, avail) - 2)
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            quota, period = f.read().split()[:2]
+        if quota != 'max':
+            avail = min(avail, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return avail
+
+
+def _codec_threads() -> int:
+    """Host threads for the block codec: the usable CPUs (cpu_budget), capped at 16, minus two for the
+    ledger's materialiser threads that run concurrently."""
+    return max(1, min(16, cpu_budget()) - 2)
 
 
 THREADS = int(os.environ.get('UPOW_CODEC_THREADS', '0')) or _codec_threads()
