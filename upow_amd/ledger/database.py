@@ -30,7 +30,7 @@ import numpy as np
 
 from ..constants import MAX_BLOCK_SIZE_HEX, SMALLEST
 from ..models.transaction import CoinbaseTransaction, Transaction, TransactionInput
-from ..utils import codec
+from ..utils import codec, roctx
 from ..utils.codec import (AddressFormat, OutputType, TransactionType, normalize_block, point_to_bytes,
                            point_to_string, round_up_decimal, sha256, string_to_bytes, string_to_point)
 from ..utils import coalesce
@@ -1791,6 +1791,15 @@ class Database:
         the same statement order, so both paths leave identical tables.
         Returns the journal sequence number (0 without the native writer: written synchronously)."""
         ts = [perf_counter()]  # stage clock: records, statements, encode, journal, index, mempool, governance
+        names = ('apply:records', 'apply:stmts', 'apply:encode', 'apply:journal', 'apply:index', 'apply:mempool',
+                 'apply:gov')
+        roctx.push(names[0])
+
+        def stamp():  # next stage (and its roctx range)
+            ts.append(perf_counter())
+            roctx.pop()
+            if len(ts) <= len(names):
+                roctx.push(names[len(ts) - 1])
         out_index, out_addr_spec, out_txid, out_amount, out_addr, out_len = out_cols
         n_out, n_in = len(out_index), len(in_keys)
         tag_u = TAG_BY_TABLE['unspent_outputs']
@@ -1823,7 +1832,7 @@ class Database:
         if gov is not None and n_in:
             in_order_rank = np.empty(n_in, dtype=np.int64)  # position of each input in the key order
             in_order_rank[in_order] = np.arange(n_in, dtype=np.int64)
-        ts.append(perf_counter())
+        stamp()
 
         # ---- statements (schema.sql write set of one block)
         b = block_row
@@ -1925,17 +1934,17 @@ class Database:
         tables |= {'address_transactions', 'address_index_state'}
 
         seq = 0
-        ts.append(perf_counter())
+        stamp()
         if self.writer is not None:
             enc = [self.encode(*st) for st in stmts]
-            ts.append(perf_counter())
+            stamp()
             meta = b''.join((bytes.fromhex(b['hash']), struct.pack('<qII', int(b['id']), n_out + len(cb_keys), n_in),
                              memoryview(recs),
                              memoryview(np.ascontiguousarray(cb_recs)), memoryview(spent),
                              memoryview(np.ascontiguousarray(spent_payload)).cast('B')))
             seq = self.submit_batch(enc, tables, meta, int(b['id']))
         else:
-            ts.append(perf_counter())
+            stamp()
             with self.transaction(foreign_keys=False):
                 for sql, cols, nn, order, guard, expect in stmts:
                     if guard is not None and not self._q1(guard)[0]:
@@ -1944,13 +1953,13 @@ class Database:
                     if expect is not None and done != expect:
                         logger.error(f'native block apply: {done} of {expect} rows changed [{sql[:40]}]')
         # ---- the index and the chain-tip cache follow the commit point
-        ts.append(perf_counter())
+        stamp()
         self.utxo.insert_records(recs, pay)
         if len(cb_keys):
             self.utxo.insert_records(cb_recs, cb_pay)
         if n_in:
             self.utxo.erase_records(spent)
-        ts.append(perf_counter())
+        stamp()
         tip = dict(b)
         tip['difficulty'], tip['reward'] = Decimal(tip['difficulty']), Decimal(tip['reward'])
         self._tip_gen += 1
@@ -1961,7 +1970,7 @@ class Database:
         if n:
             self._mempool_confirm(bool(mempool), txids=np.asarray(tx_cols[0][1]).reshape(-1, 32), in_keys=in_keys,
                                   block_seq=seq)
-        ts.append(perf_counter())
+        stamp()
         if self.gov is not None and gov is not None:
             tg = perf_counter()
             _, blob, off = out_addr_spec
@@ -1982,7 +1991,7 @@ class Database:
             hit = self._stake_spent(spent, spent_payload)
             if hit:
                 self.gov.removed(STAKE, hit)
-        ts.append(perf_counter())
+        stamp()
         self.last_apply_stages = dict(zip(('ap_records_s', 'ap_stmts_s', 'ap_encode_s', 'ap_journal_s', 'ap_index_s',
                                            'ap_mempool_s', 'ap_gov_s'), np.diff(ts).tolist()))
         return seq

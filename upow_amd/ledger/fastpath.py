@@ -38,7 +38,7 @@ from ..constants import MAX_BLOCK_SIZE_HEX, SMALLEST
 from ..models.transaction import Transaction
 from ..ops import p256 as op
 from ..ops.native import gpu_available, lib
-from ..utils import metrics
+from ..utils import metrics, roctx
 from ..utils.codec import TransactionType, get_transaction_type_from_message
 from ..utils.logger import get_logger
 from .govcheck import BlockGovernance
@@ -175,13 +175,19 @@ async def _create_block_from_hex(block_content: str, tx_hexes: List[str], error_
         fn = manager._create_block if locked else manager.create_block
         return await fn(block_content, txs, last_block, error_list)
 
+    roctx.push('block:decode')
     dec = decoded if decoded is not None else (decode(tx_hexes) if tx_hexes else None)
+    roctx.pop()
     timings['decode_s'] = perf_counter() - t0
     if dec is None:
         last_path = 'object'
         return await object_path(False)
     async with manager.ledger_lock():
-        ok = await _create_block_fast(block_content, dec, error_list, last_block, t0, coinbase)
+        d0 = roctx.depth()
+        try:
+            ok = await _create_block_fast(block_content, dec, error_list, last_block, t0, coinbase)
+        finally:
+            roctx.unwind(d0)
         last_path = 'native'
         if ok is None:
             last_path = 'object'
@@ -215,6 +221,7 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     if d['merkle'] != merkle_tree:
         return None
     t1 = perf_counter()
+    roctx.push('block:utxo_pass')
 
     # ---- inputs: one device pass = lookup (existence in unspent_outputs + amount + address),
     #      duplicate detection and per-tx fees (csrc/utxo_table.hip utxo_block_inputs)
@@ -243,6 +250,8 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     if (n_in and in_amount.max() >= AMOUNT_LIMIT) or (len(out_amount) and out_amount.max() >= AMOUNT_LIMIT):
         return None
     t2 = perf_counter()
+    roctx.pop()
+    roctx.push('block:gov_rules')
 
     txid = np.frombuffer(d['txid'], dtype=np.uint8).reshape(-1, 32)
     out_len = np.frombuffer(d['out_len'], dtype=np.uint8)
@@ -260,6 +269,8 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
                 sig_pay['addr'][j, :len(raw)] = np.frombuffer(raw, dtype=np.uint8)
                 sig_pay['len'][j] = len(raw)
     t_gov = perf_counter()
+    roctx.pop()
+    roctx.push('block:signer_records')
 
     # ---- keys + verify records: every distinct 33-byte key (signers + outputs) decompressed in one
     #      batch, then the 160-byte records of the signature jobs, in one native call
@@ -285,6 +296,8 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     if np.any(out_amount == 0):
         return None
     t3 = perf_counter()
+    roctx.pop()
+    roctx.push('block:ecdsa')
 
     # ---- signatures: one batched verify (+ the reference's ASCII-hex retry for the failures)
     status = validate._verify(rec_bytes, None).copy() if n_jobs else np.zeros(0, np.uint8)
@@ -300,6 +313,8 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     if np.any(status != op.VALID):
         return None
     t4 = perf_counter()
+    roctx.pop()
+    roctx.push('block:apply')
 
     # ---- fees (REGULAR txs; voting-power outputs excluded, governance txs carry none)
     if np.any(fee < 0):
