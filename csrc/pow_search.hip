@@ -265,9 +265,10 @@ PowResult pow_search_gpu(const PowJobHost& hj, uint64_t start, uint64_t count, i
     if (grid_blocks <= 0) grid_blocks = pow_resident_blocks(v2, variant);
     const uint64_t per_launch_threads = uint64_t(grid_blocks) * block;
     if (chunk_iters == 0) {
-        // nonces per dispatch: 2^28 (~7.6 ms on MI355X) by default; a miner sharing the GPU with a node
-        // sets UPOW_POW_DISPATCH_LOG2 lower so a queued node kernel waits at most one short dispatch
-        int lg = 28;
+        // nonces per dispatch: 2^28 (~7.6 ms on MI355X) for a dedicated miner; 2^23 (~0.25 ms) once this
+        // process also runs node kernels, so a queued node kernel waits at most one short dispatch (the miner
+        // CLI next to a node process uses 2^23 too); UPOW_POW_DISPATCH_LOG2 overrides both
+        int lg = node_stream_live().load() ? 23 : 28;
         if (const char* e = std::getenv("UPOW_POW_DISPATCH_LOG2")) lg = std::max(16, std::min(32, std::atoi(e)));
         chunk_iters = uint32_t(std::max<uint64_t>(1, (uint64_t(1) << lg) / per_launch_threads));
     }

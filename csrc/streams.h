@@ -43,6 +43,13 @@ inline void node_device_enter() {
 
 enum class StreamRole { Node = 0, Miner = 1 };
 
+// set once this process has issued node work (UTXO passes, ECDSA, ...): a miner in the same process then
+// keeps its dispatches short (csrc/pow_search.hip)
+inline std::atomic<bool>& node_stream_live() {
+    static std::atomic<bool> live{false};
+    return live;
+}
+
 inline hipStream_t role_stream(StreamRole role) {
     constexpr int kMaxDev = 64;
     static std::mutex mu;
@@ -62,6 +69,7 @@ inline hipStream_t role_stream(StreamRole role) {
         }
         stream_check(hipStreamCreateWithPriority(&streams[r][dev], hipStreamNonBlocking, prio),
                      "hipStreamCreateWithPriority");
+        if (role == StreamRole::Node) node_stream_live().store(true);
     }
     return streams[r][dev];
 }
