@@ -774,7 +774,9 @@ class LedgerWriter {
 
     // Commit point: reserve (seq, offset), write the record outside the journal mutex, publish it to the
     // materialisers in sequence order, make it durable as the sync mode asks. Returns the sequence number.
-    uint64_t submit(const std::vector<Span>& stmts, const std::string& meta, int64_t block_id) {
+    // ``sync`` false: the caller makes the record durable itself later (durable(seq)), overlapping the
+    // fdatasync with its own work
+    uint64_t submit(const std::vector<Span>& stmts, const std::string& meta, int64_t block_id, bool sync = true) {
         auto payload = std::make_shared<std::string>();
         size_t total = 4;
         for (auto& st : stmts) total += st.n;
@@ -824,7 +826,7 @@ class LedgerWriter {
         cv_.notify_all();
         cv_done_.notify_all();
         if (!werr.empty()) throw std::runtime_error(werr);
-        if (sync_ == SYNC_COMMIT || (sync_ == SYNC_BLOCK && block_id >= 0)) make_durable(seq);
+        if (sync && (sync_ == SYNC_COMMIT || (sync_ == SYNC_BLOCK && block_id >= 0))) make_durable(seq);
         if (block_id >= 0 && !meta.empty()) undo_.put(block_id, meta);
         return seq;
     }
@@ -1424,7 +1426,7 @@ void register_ledger_writer(py::module_& m) {
              py::arg("max_queue_bytes") = int64_t(512) << 20, py::arg("throttle_timeout_s") = 300.0,
              py::arg("busy_timeout_ms") = 5000)
         .def("submit",
-             [](LedgerWriter& w, py::list stmts, py::bytes meta, int64_t block_id) {
+             [](LedgerWriter& w, py::list stmts, py::bytes meta, int64_t block_id, bool sync) {
                  // only pointers are taken under the GIL (the list and the meta object keep the bytes
                  // alive); the megabytes of a block batch are copied into the record without it
                  std::vector<LedgerWriter::Span> v;
@@ -1436,9 +1438,9 @@ void register_ledger_writer(py::module_& m) {
                  const char* mp = PyBytes_AS_STRING(meta.ptr());
                  const size_t mn = size_t(PyBytes_GET_SIZE(meta.ptr()));
                  py::gil_scoped_release nogil;
-                 return w.submit(v, std::string(mp, mn), block_id);
+                 return w.submit(v, std::string(mp, mn), block_id, sync);
              },
-             py::arg("stmts"), py::arg("meta") = py::bytes(""), py::arg("block_id") = -1)
+             py::arg("stmts"), py::arg("meta") = py::bytes(""), py::arg("block_id") = -1, py::arg("sync") = true)
         .def("applied", &LedgerWriter::applied, py::arg("shard") = -1)
         .def("set_paused", &LedgerWriter::set_paused)
         .def("wait", &LedgerWriter::wait, py::arg("seq"), py::arg("shard") = -1, py::arg("timeout_s") = 0.0,

@@ -310,6 +310,18 @@ _FK_PARENTS['transactions'] = ('blocks',)
 _SQL_TABLES: Dict[Tuple[str, bool], Optional[frozenset]] = {}
 
 
+_SYNC_POOL = None
+
+
+def _sync_pool():
+    """One helper thread for deferred journal fdatasyncs (the native call releases the GIL)."""
+    global _SYNC_POOL
+    if _SYNC_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _SYNC_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix='upow-journal-sync')
+    return _SYNC_POOL
+
+
 def _tables_of(sql: str, write: bool) -> Optional[frozenset]:
     """Ledger tables a statement reads (or writes, with their FK parents); None = all of them
     (a DELETE/UPDATE on blocks or transactions cascades through the output tables)."""
@@ -754,7 +766,8 @@ class Database:
             self._mempool_ver += 1
             self._mp = None
 
-    def submit_batch(self, stmts: List[bytes], tables: Iterable[str], meta: bytes = b'', block_id: int = -1) -> int:
+    def submit_batch(self, stmts: List[bytes], tables: Iterable[str], meta: bytes = b'', block_id: int = -1,
+                     defer_sync: bool = False) -> int:
         """Commit a batch of encoded statements (``lib().ledger_encode_stmt``) through the journal.
 
         Does not take the connection lock: a block's batch is megabytes, and the /push_tx path must not
@@ -769,7 +782,13 @@ class Database:
         most for the journal write of a concurrent block, not for its payload assembly too."""
         if self._tx_depth and self._tx_owner == threading.get_ident():
             raise RuntimeError('ledger batch submitted inside an open SQL transaction')
-        seq = self.writer.submit(stmts, meta, block_id)
+        if defer_sync:
+            # the block's fdatasync runs on a helper thread while the caller updates its indexes; the block
+            # is not answered or gossiped before wait_durable() (UPOW_JOURNAL_SYNC=block semantics)
+            seq = self.writer.submit(stmts, meta, block_id, False)
+            self._durable_wait = _sync_pool().submit(self.writer.durable, seq)
+        else:
+            seq = self.writer.submit(stmts, meta, block_id)
         with self._seq_lock:
             if seq > self._submitted:
                 self._submitted = seq
@@ -777,6 +796,14 @@ class Database:
                 if seq > self._table_seq.get(t, 0):
                     self._table_seq[t] = seq
         return seq
+
+    _durable_wait = None
+
+    def wait_durable(self):
+        """Block until the last block record submitted with ``defer_sync`` is on disk (re-raises its error)."""
+        f, self._durable_wait = self._durable_wait, None
+        if f is not None:
+            f.result()
 
     # ------------------------------------------------------------------ SQL helpers
     def _q(self, sql: str, args: Iterable = ()) -> List[sqlite3.Row]:
@@ -1942,7 +1969,7 @@ class Database:
                              memoryview(recs),
                              memoryview(np.ascontiguousarray(cb_recs)), memoryview(spent),
                              memoryview(np.ascontiguousarray(spent_payload)).cast('B')))
-            seq = self.submit_batch(enc, tables, meta, int(b['id']))
+            seq = self.submit_batch(enc, tables, meta, int(b['id']), defer_sync=True)
         else:
             stamp()
             with self.transaction(foreign_keys=False):

@@ -188,6 +188,11 @@ async def _create_block_from_hex(block_content: str, tx_hexes: List[str], error_
             ok = await _create_block_fast(block_content, dec, error_list, last_block, t0, coinbase)
         finally:
             roctx.unwind(d0)
+            # the block record's fdatasync overlapped the index updates; it is durable before the block is
+            # answered or gossiped
+            from .database import Database
+            with roctx.stage('block:durable'):
+                Database.instance.wait_durable()
         last_path = 'native'
         if ok is None:
             last_path = 'object'
