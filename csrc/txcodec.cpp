@@ -21,10 +21,13 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <string_view>
 #include <thread>
@@ -71,8 +74,25 @@ struct DecTx {
     std::vector<uint8_t> canon;
     uint8_t txid[32];
     uint8_t digest[32];
-    std::vector<std::string> out_addr;  // bytes_to_string form
+    std::vector<std::string> out_addr;  // bytes_to_string form; the first outs.size() entries are live
     std::string out_addr_json, out_amount_json;
+    // back to the freshly-constructed state while keeping every buffer's capacity: a workspace's DecTx
+    // objects are reused block after block, so the steady state decodes without touching malloc
+    void reset() {
+        flag = TX_MALFORMED;
+        version = 0;
+        canonical = upper_hex = false;
+        msg_off = -1;
+        msg_len = 0;
+        tx_type = 0;
+        signed_len = 0;
+        ins.clear();
+        outs.clear();
+        sigs.clear();
+        canon.clear();
+        out_addr_json.clear();
+        out_amount_json.clear();
+    }
 };
 
 static inline int hexval(char c) {
@@ -116,26 +136,46 @@ static std::string to_hex(const uint8_t* p, size_t n) {
     return s;
 }
 
-// base58 of a 33-byte compressed address, memoised per thread (blocks pay the same few addresses
-// over and over: change outputs, exchanges, pools)
-static std::string b58_33(const uint8_t b[33]) {
-    thread_local std::unordered_map<std::string, std::string> cache;
-    std::string key(reinterpret_cast<const char*>(b), 33);
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
-    if (cache.size() > (1u << 16)) cache.clear();
-    std::string s = b58encode(b, 33);
-    cache.emplace(std::move(key), s);
-    return s;
+// base58 of a 33-byte compressed address, memoised per thread in a direct-mapped table (blocks pay the
+// same few addresses over and over: change outputs, exchanges, pools). Fixed-size slots: a lookup hashes
+// the key's x bytes (uniform for curve points) and never allocates.
+struct B58Slot {
+    uint8_t key[33];
+    uint8_t len = 0;  // 0 = empty
+    char s[46];
+};
+static void b58_33(const uint8_t b[33], std::string& out) {
+    constexpr size_t kSlots = 1u << 13;
+    thread_local std::vector<B58Slot> cache(kSlots);
+    uint64_t h;
+    std::memcpy(&h, b + 1, 8);
+    B58Slot& e = cache[size_t((h ^ b[0]) * 0x9E3779B97F4A7C15ull >> 51)];
+    if (e.len && std::memcmp(e.key, b, 33) == 0) {
+        out.assign(e.s, e.len);
+        return;
+    }
+    out = b58encode(b, 33);
+    if (out.size() <= sizeof(e.s)) {
+        std::memcpy(e.key, b, 33);
+        std::memcpy(e.s, out.data(), out.size());
+        e.len = uint8_t(out.size());
+    }
 }
 
 // bytes_to_string (codec.py): 64 B -> hex, 33 B -> base58 of normalised prefix || x
-static std::string addr_string(const uint8_t* a, int len) {
-    if (len == 64) return to_hex(a, 64);
+static void addr_string(const uint8_t* a, int len, std::string& out) {
+    if (len == 64) {
+        out.resize(128);
+        for (int i = 0; i < 64; ++i) {
+            out[size_t(2 * i)] = kHex[a[i] >> 4];
+            out[size_t(2 * i + 1)] = kHex[a[i] & 15];
+        }
+        return;
+    }
     uint8_t b[33];
     b[0] = a[0] == 43 ? 43 : 42;
     std::memcpy(b + 1, a + 1, 32);
-    return b58_33(b);
+    b58_33(b, out);
 }
 
 // True when string_to_bytes(s) would take the bytes.fromhex branch (an all-hex base58 string of even
@@ -187,15 +227,35 @@ static uint8_t message_tx_type(const uint8_t* m, size_t n) {
     return any_digit ? kTypeAsk : 0;
 }
 
+// Hex digit table: low nibble = value, 0x10 = upper-case A-F, 0x80 = not a hex digit. Random hex has no
+// predictable digit/letter pattern, so the branchy hexval() costs ~2 mispredicts per byte; the table
+// decodes a 214-byte tx in a few hundred cycles with all error checks folded into one OR at the end.
+static const std::array<uint8_t, 256> kHexTab = [] {
+    std::array<uint8_t, 256> t{};
+    t.fill(0x80);
+    for (int c = 0; c < 10; ++c) t[size_t('0' + c)] = uint8_t(c);
+    for (int c = 0; c < 6; ++c) {
+        t[size_t('a' + c)] = uint8_t(10 + c);
+        t[size_t('A' + c)] = uint8_t(0x10 | (10 + c));
+    }
+    return t;
+}();
+
 static void decode_one(const char* hx, size_t hlen, DecTx& t) {
-    t = DecTx();
+    t.reset();
     if (hlen % 2) return;
-    std::vector<uint8_t> b(hlen / 2);
-    for (size_t i = 0; i < b.size(); ++i) {
-        const int hi = hexval(hx[2 * i]), lo = hexval(hx[2 * i + 1]);
-        if (hi < 0 || lo < 0) return;  // whitespace etc.: bytes.fromhex semantics are the parser's business
-        t.upper_hex |= (hx[2 * i] >= 'A' && hx[2 * i] <= 'F') | (hx[2 * i + 1] >= 'A' && hx[2 * i + 1] <= 'F');
-        b[i] = uint8_t(hi << 4 | lo);
+    thread_local std::vector<uint8_t> b;  // per-thread scratch: no allocation per tx
+    b.resize(hlen / 2);
+    {
+        const uint8_t* h = reinterpret_cast<const uint8_t*>(hx);
+        uint8_t acc = 0;
+        for (size_t i = 0; i < b.size(); ++i) {
+            const uint8_t hi = kHexTab[h[2 * i]], lo = kHexTab[h[2 * i + 1]];
+            acc |= hi | lo;
+            b[i] = uint8_t(hi << 4 | (lo & 15));
+        }
+        if (acc & 0x80) return;  // whitespace etc.: bytes.fromhex semantics are the parser's business
+        t.upper_hex = (acc & 0x10) != 0;
     }
     const size_t n = b.size();
     size_t p = 0;
@@ -263,7 +323,8 @@ static void decode_one(const char* hx, size_t hlen, DecTx& t) {
     // signatures: 64-byte (r, s) pairs up to the end; a zero r or a ragged tail is parser territory
     if ((n - p) % 64) return;
     const size_t n_sig = (n - p) / 64;
-    std::vector<const uint8_t*> sig_ptr(n_sig);
+    thread_local std::vector<const uint8_t*> sig_ptr, in_sig;
+    sig_ptr.resize(n_sig);
     for (size_t k = 0; k < n_sig; ++k) {
         const uint8_t* s = &b[p + 64 * k];
         bool rz = true;
@@ -272,7 +333,7 @@ static void decode_one(const char* hx, size_t hlen, DecTx& t) {
         sig_ptr[k] = s;
     }
     // signature -> input assignment (transaction.py:566-590)
-    std::vector<const uint8_t*> in_sig(static_cast<size_t>(n_in));
+    in_sig.resize(static_cast<size_t>(n_in));
     if (n_sig == 1) {
         for (auto& s : in_sig) s = sig_ptr[0];
     } else if (n_sig == size_t(n_in)) {
@@ -341,11 +402,12 @@ static void decode_one(const char* hx, size_t hlen, DecTx& t) {
     host_sha256(c.data(), c.size(), t.txid);
     host_sha256(c.data(), size_t(t.signed_len), t.digest);
     // output address strings + JSON columns (database.add_transactions)
-    t.out_addr.reserve(t.outs.size());
+    if (t.out_addr.size() < t.outs.size()) t.out_addr.resize(t.outs.size());
     t.out_addr_json = "[";
     t.out_amount_json = "[";
     for (size_t k = 0; k < t.outs.size(); ++k) {
-        std::string s = addr_string(t.outs[k].addr, t.outs[k].len);
+        std::string& s = t.out_addr[k];
+        addr_string(t.outs[k].addr, t.outs[k].len, s);
         if (t.outs[k].len == 33 && hex_ambiguous(s)) general = true;
         if (k) {
             t.out_addr_json += ',';
@@ -354,8 +416,15 @@ static void decode_one(const char* hx, size_t hlen, DecTx& t) {
         t.out_addr_json += '"';
         t.out_addr_json += s;
         t.out_addr_json += '"';
-        t.out_amount_json += std::to_string(t.outs[k].amount);
-        t.out_addr.push_back(std::move(s));
+        char num[24];
+        char* e = num + sizeof(num);
+        char* q = e;
+        uint64_t v = t.outs[k].amount;
+        do {
+            *--q = char('0' + v % 10);
+            v /= 10;
+        } while (v);
+        t.out_amount_json.append(q, size_t(e - q));
     }
     t.out_addr_json += ']';
     t.out_amount_json += ']';
@@ -368,11 +437,11 @@ static void parallel_for(int64_t n, int threads, F&& f) {
 }
 
 // merkle root: SHA-256 over the txids of the txs sorted by their canonical bytes (manager.py:365-378)
-static std::string merkle_of(const std::vector<DecTx>& txs) {
+static std::string merkle_of(const std::vector<DecTx>& txs, size_t n) {
     // sort by (big-endian 8-byte prefix, full bytes): canonical txs start with version, n_in and a
     // random input txid, so the integer prefix decides almost every comparison without touching
     // the tx bytes (zero padding of short txs is resolved by the full comparison on a tie)
-    std::vector<std::pair<uint64_t, int>> order(txs.size());
+    std::vector<std::pair<uint64_t, int>> order(n);
     for (size_t i = 0; i < order.size(); ++i) {
         const auto& c = txs[i].canon;
         uint64_t key = 0;
@@ -411,6 +480,43 @@ struct Arena {
     }
 };
 
+// Decode workspaces: the per-tx DecTx objects (and all their buffers) outlive a call and are reused by
+// the next one, so a steady stream of blocks decodes without heap traffic. Concurrent callers (the
+// ledger thread and the sync pipeline's decode-ahead thread) each lease their own workspace.
+struct DecWorkspace {
+    std::vector<DecTx> txs;
+};
+class DecWorkspaceLease {
+public:
+    DecWorkspaceLease() {
+        std::lock_guard<std::mutex> g(mu());
+        if (!free_list().empty()) {
+            ws_ = std::move(free_list().back());
+            free_list().pop_back();
+        } else {
+            ws_ = std::make_unique<DecWorkspace>();
+        }
+    }
+    ~DecWorkspaceLease() {
+        // a workspace that grew for an unusually large call is dropped rather than pinned forever
+        if (ws_->txs.size() > (1u << 16)) return;
+        std::lock_guard<std::mutex> g(mu());
+        if (free_list().size() < 4) free_list().push_back(std::move(ws_));
+    }
+    DecWorkspace& get() { return *ws_; }
+
+private:
+    static std::mutex& mu() {
+        static std::mutex m;
+        return m;
+    }
+    static std::vector<std::unique_ptr<DecWorkspace>>& free_list() {
+        static auto* l = new std::vector<std::unique_ptr<DecWorkspace>>();  // never destroyed at exit
+        return *l;
+    }
+    std::unique_ptr<DecWorkspace> ws_;
+};
+
 // decode_block_txs(hexes, threads) -> dict (see module docstring of upow_amd/ledger/fastpath.py)
 static py::dict decode_block_txs(py::list hexes, int threads) {
     const int64_t n = int64_t(hexes.size());
@@ -428,7 +534,9 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
         srcp[i] = p;
         srcl[i] = size_t(sz);
     }
-    std::vector<DecTx> txs(N);
+    DecWorkspaceLease ws;
+    std::vector<DecTx>& txs = ws.get().txs;
+    if (txs.size() < N) txs.resize(N);
     const bool prof = std::getenv("UPOW_TXCODEC_PROFILE") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
     {
@@ -483,7 +591,7 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
     // The merkle root (a sort of the canonical bytes, then one SHA-256 over the txids) runs on its own
     // thread while the pool fills the flat columns below: both only read `txs`.
     std::string merkle;
-    std::thread merkle_thread([&] { merkle = merkle_of(txs); });
+    std::thread merkle_thread([&] { merkle = merkle_of(txs, N); });
     struct Joiner {  // an exception below must not destroy a joinable thread
         std::thread& t;
         ~Joiner() {
@@ -504,10 +612,8 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
     for (size_t i = 0; i < N; ++i) {
         const DecTx& t = txs[i];
         size_t o = size_t(out_start[i]);
-        for (const std::string& a : t.out_addr) {
-            addr_arena.off[o + 1] = addr_arena.off[o] + int64_t(a.size());
-            ++o;
-        }
+        for (size_t j = 0; j < t.outs.size(); ++j, ++o)
+            addr_arena.off[o + 1] = addr_arena.off[o] + int64_t(t.out_addr[j].size());
         addr_json_arena.off[i + 1] = addr_json_arena.off[i] + int64_t(t.out_addr_json.size());
         amount_json_arena.off[i + 1] = amount_json_arena.off[i] + int64_t(t.out_amount_json.size());
     }
@@ -550,6 +656,7 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
     }
     // the stored hex column: the input string is reused when it already is the canonical lowercase
     // hex of the tx (Python objects: with the GIL, on this thread)
+    auto tA = std::chrono::steady_clock::now();
     py::list canon_hex = new_list(N);
     for (size_t i = 0; i < N; ++i) {
         const DecTx& t = txs[i];
@@ -562,6 +669,7 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
             PyList_SET_ITEM(canon_hex.ptr(), Py_ssize_t(i), ascii_str(h.data(), h.size()));
         }
     }
+    auto tB = std::chrono::steady_clock::now();
     d["in_keys"] = as_bytes(in_keys);
     d["in_type"] = as_bytes(in_type);
     d["in_sig"] = i32(in_sig);
@@ -584,16 +692,11 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
         merkle_thread.join();
     }
     d["merkle"] = merkle;
-    {
-        // ~8 heap blocks per tx were allocated by the pool's threads: release them there too (a
-        // serial free of ~10^5 blocks from foreign malloc arenas costs ~10 ms on the main thread)
-        py::gil_scoped_release rel;
-        parallel_for(n, threads, [&](int64_t i) { txs[size_t(i)] = DecTx(); });
-    }
     if (prof) {
         auto t3 = std::chrono::steady_clock::now();
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        std::fprintf(stderr, "[txcodec] decode %.2f ms, columns + python objects %.2f ms, merkle wait + free %.2f ms\n",
+        std::fprintf(stderr, "[txcodec] fill %.2f canonhex %.2f bytes %.2f\n", ms(t1,tA), ms(tA,tB), ms(tB,t2));
+        std::fprintf(stderr, "[txcodec] decode %.2f ms, columns + python objects %.2f ms, merkle wait %.2f ms\n",
                      ms(t0, t1), ms(t1, t2), ms(t2, t3));
     }
     return d;
@@ -626,7 +729,7 @@ static py::tuple input_address_strings(py::bytes addrs64, py::bytes lens, py::by
                 bad[size_t(i)] = 1;
                 return;
             }
-            out[size_t(i)] = b58_33(c);
+            b58_33(c, out[size_t(i)]);
         });
     }
     for (size_t i = 0; i < n_in; ++i)
