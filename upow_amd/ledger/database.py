@@ -310,18 +310,6 @@ _FK_PARENTS['transactions'] = ('blocks',)
 _SQL_TABLES: Dict[Tuple[str, bool], Optional[frozenset]] = {}
 
 
-_SYNC_POOL = None
-
-
-def _sync_pool():
-    """One helper thread for deferred journal fdatasyncs (the native call releases the GIL)."""
-    global _SYNC_POOL
-    if _SYNC_POOL is None:
-        from concurrent.futures import ThreadPoolExecutor
-        _SYNC_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix='upow-journal-sync')
-    return _SYNC_POOL
-
-
 def _tables_of(sql: str, write: bool) -> Optional[frozenset]:
     """Ledger tables a statement reads (or writes, with their FK parents); None = all of them
     (a DELETE/UPDATE on blocks or transactions cascades through the output tables)."""
@@ -783,10 +771,11 @@ class Database:
         if self._tx_depth and self._tx_owner == threading.get_ident():
             raise RuntimeError('ledger batch submitted inside an open SQL transaction')
         if defer_sync:
-            # the block's fdatasync runs on a helper thread while the caller updates its indexes; the block
-            # is not answered or gossiped before wait_durable() (UPOW_JOURNAL_SYNC=block semantics)
+            # the writer's journal I/O thread checksums, writes and fdatasyncs the block record (and stores
+            # its undo data) while the caller updates its indexes; the sequence number is fixed here. The
+            # block is not answered or gossiped before wait_durable() (UPOW_JOURNAL_SYNC=block semantics).
             seq = self.writer.submit(stmts, meta, block_id, False)
-            self._durable_wait = _sync_pool().submit(self.writer.durable, seq)
+            self._durable_seq = seq
         else:
             seq = self.writer.submit(stmts, meta, block_id)
         with self._seq_lock:
@@ -797,13 +786,14 @@ class Database:
                     self._table_seq[t] = seq
         return seq
 
-    _durable_wait = None
+    _durable_seq = 0
 
     def wait_durable(self):
-        """Block until the last block record submitted with ``defer_sync`` is on disk (re-raises its error)."""
-        f, self._durable_wait = self._durable_wait, None
-        if f is not None:
-            f.result()
+        """Block until the last block record submitted with ``defer_sync`` is written and on disk (raises when
+        the writer failed on it: a journal write error after the commit point stops the ledger)."""
+        seq, self._durable_seq = self._durable_seq, 0
+        if seq and self.writer is not None:
+            self.writer.durable(seq)
 
     # ------------------------------------------------------------------ SQL helpers
     def _q(self, sql: str, args: Iterable = ()) -> List[sqlite3.Row]:
