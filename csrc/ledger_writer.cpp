@@ -178,13 +178,15 @@ struct In {
 };
 
 // Column kinds of an encoded statement.
-enum ColKind : uint8_t { K_NULL = 0, K_CTEXT = 1, K_CINT = 2, K_INT64 = 3, K_HEX32 = 4, K_TEXT = 5 };
+enum ColKind : uint8_t { K_NULL = 0, K_CTEXT = 1, K_CINT = 2, K_INT64 = 3, K_HEX32 = 4, K_TEXT = 5, K_HEXTEXT = 6 };
 
 // Encode one column spec (Python side) for n rows:
 //   list[str|None]                    text per row
 //   ('gather', list[str], int32 buf)   text list[idx[row]]
 //   ('hex32', buf, stride, offset)     lowercase hex of the 32 bytes at row*stride+offset
 //   ('arena', blob, int64 offsets)     text blob[off[row]:off[row+1]] (csrc/txcodec.cpp text arenas)
+//   ('hexarena', blob, int64 offsets)  lowercase hex of the bytes blob[off[row]:off[row+1]]: raw in the
+//                                      journal (half the size of the text), rendered when bound
 //   int64 numpy array                  integer per row
 //   str / int / None                   the same value for every row
 void encode_text_rows(Out& o, int64_t n, const std::vector<const char*>& ptr, const std::vector<int64_t>& len,
@@ -288,7 +290,7 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
             py::gil_scoped_release nogil;
             o.b.reserve(o.b.size() + size_t(n) * 32);
             for (int64_t r = 0; r < n; ++r) o.raw(raw + (sel ? sel[r] : r) * stride + offset, 32);
-        } else if (tag == "arena") {
+        } else if (tag == "arena" || tag == "hexarena") {
             // ('arena', blob, offsets int64[N + 1][, sel int64[n]]): text rows, optionally rows sel of the arena
             py::buffer_info bb = t[1].cast<py::buffer>().request(), ob = t[2].cast<py::buffer>().request();
             const int64_t* sel = t.size() > 3 ? row_selection(t[3], n) : nullptr;
@@ -303,8 +305,12 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
             if (sel)
                 for (int64_t r = 0; r < n; ++r)
                     if (sel[r] >= rows) throw std::out_of_range("arena row selection");
-            o.u8(K_TEXT);
-            o.u8(0);
+            if (tag == "arena") {
+                o.u8(K_TEXT);
+                o.u8(0);
+            } else {
+                o.u8(K_HEXTEXT);
+            }
             py::gil_scoped_release nogil;
             std::vector<int64_t> off(size_t(n) + 1);
             if (!sel) {
@@ -359,6 +365,11 @@ EncodedStmt encode_stmt(const std::string& sql, py::sequence cols, int64_t n, py
     for (auto spec : cols) encode_col(o, spec, n);
     if (order.is_none()) {
         o.u8(0);
+    } else if (py::isinstance<py::str>(order)) {
+        // "key": rows in the order of column 0's leading 8 bytes (big-endian, stable), B-tree locality for
+        // the writes; the materialiser sorts, so the block path does not
+        if (order.cast<std::string>() != "key") throw std::invalid_argument("order must be int64[n] or 'key'");
+        o.u8(2);
     } else {
         py::buffer_info bi = order.cast<py::buffer>().request();
         if (bi.itemsize != 8 || bi.size != n) throw std::invalid_argument("order must be int64[n]");
@@ -398,6 +409,10 @@ uint32_t hex_nibble(char c) {
 // statement spread over several files.
 uint32_t route_byte(const ColView& c, int64_t r) {
     if (c.kind == K_HEX32) return uint8_t(c.data[32 * r]);
+    if (c.kind == K_HEXTEXT) {
+        const int64_t o0 = ld64(c.off + 8 * r), o1 = ld64(c.off + 8 * (r + 1));
+        return o1 > o0 ? uint8_t(c.data[o0]) : 0u;
+    }
     if (c.kind == K_TEXT && !(c.nul && c.nul[r])) {
         const int64_t o0 = ld64(c.off + 8 * r), o1 = ld64(c.off + 8 * (r + 1));
         if (o1 - o0 >= 2) return (hex_nibble(c.data[o0]) << 4) | hex_nibble(c.data[o0 + 1]);
@@ -937,7 +952,8 @@ class LedgerWriter {
     }
 
     // checksum + write one reserved record, then publish it (in sequence order); returns the write error
-    std::string write_record(Batch& b, off_t at, int64_t block_id) {
+    // (`before_publish`: a helper thread joined after the write and before the record is published)
+    std::string write_record(Batch& b, off_t at, int64_t block_id, std::thread* before_publish = nullptr) {
         RecHeader h{kMagic, 0, b.seq, block_id, 0, b.size};
         h.crc = record_crc_parts(h, b.parts);
         std::string werr;
@@ -946,6 +962,7 @@ class LedgerWriter {
         } catch (const std::exception& e) {
             werr = e.what();
         }
+        if (before_publish && before_publish->joinable()) before_publish->join();
         {
             std::lock_guard<std::mutex> jl(jmu_);
             --inflight_;
@@ -985,12 +1002,19 @@ class LedgerWriter {
             }
             const uint64_t seq = job.batch.seq;
             std::string err;
-            try {
-                if (job.block_id >= 0 && !job.meta.empty()) undo_.put(job.block_id, job.meta);
-            } catch (const std::exception& e) {
-                err = e.what();
+            // the undo record (its own file) is written alongside the journal record; both finish before
+            // the block is published
+            std::thread undo;
+            if (job.block_id >= 0 && !job.meta.empty()) {
+                undo = std::thread([&] {
+                    try {
+                        undo_.put(job.block_id, job.meta);
+                    } catch (const std::exception& e) {
+                        err = e.what();
+                    }
+                });
             }
-            std::string werr = write_record(job.batch, job.at, job.block_id);
+            std::string werr = write_record(job.batch, job.at, job.block_id, &undo);
             if (werr.empty() && !err.empty()) {
                 std::lock_guard<std::mutex> lk(mu_);
                 if (!failed_) {
@@ -1296,8 +1320,9 @@ class LedgerWriter {
                     case K_CINT: c.cint = in.get<int64_t>(); break;
                     case K_INT64: c.data = in.take(size_t(n) * 8); break;
                     case K_HEX32: c.data = in.take(size_t(n) * 32); break;
-                    case K_TEXT: {
-                        const uint8_t has_null = in.get<uint8_t>();
+                    case K_TEXT:
+                    case K_HEXTEXT: {
+                        const uint8_t has_null = c.kind == K_TEXT ? in.get<uint8_t>() : 0;
                         if (has_null) c.nul = reinterpret_cast<const uint8_t*>(in.take(size_t(n)));
                         c.off = in.take(size_t(n + 1) * 8);
                         const int64_t blen = ld64(c.off + 8 * n);
@@ -1308,10 +1333,25 @@ class LedgerWriter {
                 }
             }
             const char* order = nullptr;
-            if (in.get<uint8_t>()) order = in.take(size_t(n) * 8);
+            const uint8_t order_kind = in.get<uint8_t>();
+            if (order_kind == 1) order = in.take(size_t(n) * 8);
             const size_t route = (flags & 4) ? ((flags >> 16) & 0xffu) : 1;
             if (target + route > shards_.size()) throw std::runtime_error("ledger batch: statement for an unknown file");
             if (shard < target || shard >= target + route) continue;
+            std::vector<int64_t> key_order;
+            if (order_kind == 2) {
+                if (nc == 0 || cols[0].kind != K_HEX32) throw std::runtime_error("ledger batch: key order needs hex32 column 0");
+                std::vector<std::pair<uint64_t, int64_t>> kv{static_cast<size_t>(n)};
+                for (int64_t r = 0; r < n; ++r) {
+                    uint64_t k = 0;
+                    for (int b = 0; b < 8; ++b) k = (k << 8) | uint8_t(cols[0].data[32 * r + b]);
+                    kv[size_t(r)] = {k, r};
+                }
+                std::sort(kv.begin(), kv.end());  // (key, row): equal keys keep row order
+                key_order.resize(size_t(n));
+                for (int64_t r = 0; r < n; ++r) key_order[size_t(r)] = kv[size_t(r)].second;
+                order = reinterpret_cast<const char*>(key_order.data());
+            }
             if (!guard.empty() && query_int(sh.db, guard) == 0) continue;
             // routed statement: which rows belong to this file (first byte of the column-0 tx hash)
             std::vector<uint8_t> mine;
@@ -1330,6 +1370,7 @@ class LedgerWriter {
             sqlite3_stmt* st = prepared(sh, sql);
             int64_t changes = 0;
             char hexbuf[8][64];
+            std::vector<std::string> hextext(nc);  // rendered K_HEXTEXT values (bound as static text)
             for (int64_t k = 0; k < n; ++k) {
                 const int64_t r = order ? ld64(order + 8 * k) : k;
                 if (!mine.empty() && !mine[size_t(r)]) continue;
@@ -1351,6 +1392,18 @@ class LedgerWriter {
                                 out[2 * b + 1] = kHex[src[b] & 15];
                             }
                             a.bind_text(st, p, out, 64, nullptr);
+                            break;
+                        }
+                        case K_HEXTEXT: {
+                            const int64_t o0 = ld64(c.off + 8 * r), o1 = ld64(c.off + 8 * (r + 1));
+                            std::string& h = hextext[j];
+                            h.resize(size_t(2 * (o1 - o0)));
+                            const uint8_t* src = reinterpret_cast<const uint8_t*>(c.data) + o0;
+                            for (int64_t b = 0; b < o1 - o0; ++b) {
+                                h[size_t(2 * b)] = kHex[src[b] >> 4];
+                                h[size_t(2 * b + 1)] = kHex[src[b] & 15];
+                            }
+                            a.bind_text(st, p, h.data(), int(h.size()), nullptr);
                             break;
                         }
                         case K_TEXT: {
@@ -1636,7 +1689,7 @@ void register_ledger_writer(py::module_& m) {
              py::arg("max_queue_bytes") = int64_t(512) << 20, py::arg("throttle_timeout_s") = 300.0,
              py::arg("busy_timeout_ms") = 5000)
         .def("submit",
-             [](LedgerWriter& w, py::list stmts, py::bytes meta, int64_t block_id, bool sync) {
+             [](LedgerWriter& w, py::list stmts, py::object meta, int64_t block_id, bool sync) {
                  // encoded statements are taken as they are (shared buffers); plain bytes are copied
                  std::vector<Part> v;
                  v.reserve(stmts.size());
@@ -1650,10 +1703,27 @@ void register_ledger_writer(py::module_& m) {
                          throw std::invalid_argument("statements must be encoded statements or bytes");
                      }
                  }
-                 const char* mp = PyBytes_AS_STRING(meta.ptr());
-                 const size_t mn = size_t(PyBytes_GET_SIZE(meta.ptr()));
+                 // meta (the block's undo data): bytes, or a list of buffers joined here in one copy
+                 std::vector<std::pair<const char*, size_t>> mparts;
+                 std::vector<py::buffer_info> keep;
+                 if (py::isinstance<py::list>(meta)) {
+                     for (auto x : meta.cast<py::list>()) {
+                         keep.push_back(x.cast<py::buffer>().request());
+                         mparts.emplace_back(static_cast<const char*>(keep.back().ptr),
+                                             size_t(keep.back().size * keep.back().itemsize));
+                     }
+                 } else {
+                     keep.push_back(meta.cast<py::buffer>().request());
+                     mparts.emplace_back(static_cast<const char*>(keep.back().ptr),
+                                         size_t(keep.back().size * keep.back().itemsize));
+                 }
                  py::gil_scoped_release nogil;
-                 return w.submit(std::move(v), std::string(mp, mn), block_id, sync);
+                 std::string m;
+                 size_t total = 0;
+                 for (auto& pr : mparts) total += pr.second;
+                 m.reserve(total);
+                 for (auto& pr : mparts) m.append(pr.first, pr.second);
+                 return w.submit(std::move(v), std::move(m), block_id, sync);
              },
              py::arg("stmts"), py::arg("meta") = py::bytes(""), py::arg("block_id") = -1, py::arg("sync") = true)
         .def("applied", &LedgerWriter::applied, py::arg("shard") = -1)

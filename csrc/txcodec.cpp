@@ -598,28 +598,62 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
             if (t.joinable()) t.join();
         }
     } merkle_joiner{merkle_thread};
-    std::vector<uint8_t> in_keys(NI * 40, 0), in_type(NI), sigs(NS * 64), txid(N * 32), digest(N * 32),
-        out_addr(NO * 64, 0), out_len(NO), out_type(NO);
-    std::vector<int32_t> in_sig(NI), in_tx(NI), out_tx(NO);
-    std::vector<uint64_t> out_amount(NO);
-    // text arenas: per-row string sizes -> offsets (serial, cheap), then every row copies its own
-    // strings into place in parallel
-    Arena addr_arena, addr_json_arena, amount_json_arena;
-    addr_arena.off.resize(NO + 1);
-    addr_json_arena.off.resize(N + 1);
-    amount_json_arena.off.resize(N + 1);
-    addr_arena.off[0] = addr_json_arena.off[0] = amount_json_arena.off[0] = 0;
+    // Every column is filled in place inside its final Python bytes object (allocated here, with the GIL;
+    // written by the pool without it): no staging vector and no copy on the way out.
+    auto pyb = [](size_t len, char*& p) {
+        PyObject* o = PyBytes_FromStringAndSize(nullptr, Py_ssize_t(len));
+        if (!o) throw py::error_already_set();
+        p = PyBytes_AS_STRING(o);
+        return py::reinterpret_steal<py::bytes>(o);
+    };
+    char *c_in_keys, *c_in_type, *c_sigs, *c_txid, *c_digest, *c_out_addr, *c_out_len, *c_out_type, *c_in_sig,
+        *c_in_tx, *c_out_tx, *c_sig_first, *c_out_amount;
+    d["in_keys"] = pyb(NI * 40, c_in_keys);
+    d["in_type"] = pyb(NI, c_in_type);
+    d["in_sig"] = pyb(NI * 4, c_in_sig);
+    d["sig_first_in"] = pyb(NS * 4, c_sig_first);
+    d["in_tx"] = pyb(NI * 4, c_in_tx);
+    d["sigs"] = pyb(NS * 64, c_sigs);
+    d["txid"] = pyb(N * 32, c_txid);
+    d["digest"] = pyb(N * 32, c_digest);
+    d["out_addr"] = pyb(NO * 64, c_out_addr);
+    d["out_len"] = pyb(NO, c_out_len);
+    d["out_type"] = pyb(NO, c_out_type);
+    d["out_tx"] = pyb(NO * 4, c_out_tx);
+    d["out_amount"] = pyb(NO * 8, c_out_amount);
+    uint8_t* in_keys = reinterpret_cast<uint8_t*>(c_in_keys);
+    uint8_t* in_type = reinterpret_cast<uint8_t*>(c_in_type);
+    uint8_t* sigs = reinterpret_cast<uint8_t*>(c_sigs);
+    uint8_t* txid = reinterpret_cast<uint8_t*>(c_txid);
+    uint8_t* digest = reinterpret_cast<uint8_t*>(c_digest);
+    uint8_t* out_addr = reinterpret_cast<uint8_t*>(c_out_addr);
+    uint8_t* out_len = reinterpret_cast<uint8_t*>(c_out_len);
+    uint8_t* out_type = reinterpret_cast<uint8_t*>(c_out_type);
+    int32_t* in_sig = reinterpret_cast<int32_t*>(c_in_sig);
+    int32_t* in_tx = reinterpret_cast<int32_t*>(c_in_tx);
+    int32_t* out_tx = reinterpret_cast<int32_t*>(c_out_tx);
+    int32_t* sig_first_in = reinterpret_cast<int32_t*>(c_sig_first);
+    uint64_t* out_amount = reinterpret_cast<uint64_t*>(c_out_amount);
+    // text arenas (offsets serial and cheap, blobs filled in parallel): output address strings, the two
+    // per-tx JSON columns, and the canonical tx bytes (the stored tx_hex column, hex-rendered by the writer)
+    std::vector<int64_t> addr_off(NO + 1), ajson_off(N + 1), mjson_off(N + 1), canon_off(N + 1);
+    addr_off[0] = ajson_off[0] = mjson_off[0] = canon_off[0] = 0;
     for (size_t i = 0; i < N; ++i) {
         const DecTx& t = txs[i];
         size_t o = size_t(out_start[i]);
-        for (size_t j = 0; j < t.outs.size(); ++j, ++o)
-            addr_arena.off[o + 1] = addr_arena.off[o] + int64_t(t.out_addr[j].size());
-        addr_json_arena.off[i + 1] = addr_json_arena.off[i] + int64_t(t.out_addr_json.size());
-        amount_json_arena.off[i + 1] = amount_json_arena.off[i] + int64_t(t.out_amount_json.size());
+        for (size_t j = 0; j < t.outs.size(); ++j, ++o) addr_off[o + 1] = addr_off[o] + int64_t(t.out_addr[j].size());
+        ajson_off[i + 1] = ajson_off[i] + int64_t(t.out_addr_json.size());
+        mjson_off[i + 1] = mjson_off[i] + int64_t(t.out_amount_json.size());
+        canon_off[i + 1] = canon_off[i] + int64_t(t.canon.size());
     }
-    addr_arena.blob.resize(size_t(addr_arena.off[NO]));
-    addr_json_arena.blob.resize(size_t(addr_json_arena.off[N]));
-    amount_json_arena.blob.resize(size_t(amount_json_arena.off[N]));
+    auto offs = [](const std::vector<int64_t>& v) {
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size() * 8);
+    };
+    char *addr_blob, *ajson_blob, *mjson_blob, *canon_blob;
+    d["out_addr_str"] = py::make_tuple(pyb(size_t(addr_off[NO]), addr_blob), offs(addr_off));
+    d["out_addr_json"] = py::make_tuple(pyb(size_t(ajson_off[N]), ajson_blob), offs(ajson_off));
+    d["out_amount_json"] = py::make_tuple(pyb(size_t(mjson_off[N]), mjson_blob), offs(mjson_off));
+    d["canon"] = py::make_tuple(pyb(size_t(canon_off[N]), canon_blob), offs(canon_off));
     {
         py::gil_scoped_release rel;
         parallel_for(n, threads, [&](int64_t ii) {
@@ -628,6 +662,7 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
             std::memcpy(&txid[32 * i], t.txid, 32);
             std::memcpy(&digest[32 * i], t.digest, 32);
             size_t k = size_t(in_start[i]);
+            int32_t k_new_sig = 0;
             for (const DecIn& in : t.ins) {
                 std::memcpy(&in_keys[40 * k], in.txid, 32);
                 const uint32_t idx = in.index, tag = 0xffu;
@@ -635,27 +670,33 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
                 std::memcpy(&in_keys[40 * k + 36], &tag, 4);
                 in_type[k] = in.type;
                 in_sig[k] = sig_start[i] + in.sig;
+                // signatures are numbered in order of first use within the tx: the first input that uses
+                // a signature is the one for which it is the next new number
+                if (in.sig == k_new_sig) {
+                    sig_first_in[size_t(sig_start[i] + in.sig)] = int32_t(k);
+                    ++k_new_sig;
+                }
                 in_tx[k] = int32_t(i);
                 ++k;
             }
             if (!t.sigs.empty()) std::memcpy(&sigs[64 * size_t(sig_start[i])], t.sigs.data(), t.sigs.size());
             size_t o = size_t(out_start[i]);
             for (size_t j = 0; j < t.outs.size(); ++j, ++o) {
+                std::memset(&out_addr[64 * o], 0, 64);
                 std::memcpy(&out_addr[64 * o], t.outs[j].addr, t.outs[j].len);
                 out_len[o] = t.outs[j].len;
                 out_type[o] = t.outs[j].type;
                 out_amount[o] = t.outs[j].amount;
                 out_tx[o] = int32_t(i);
-                std::memcpy(&addr_arena.blob[size_t(addr_arena.off[o])], t.out_addr[j].data(), t.out_addr[j].size());
+                std::memcpy(addr_blob + addr_off[o], t.out_addr[j].data(), t.out_addr[j].size());
             }
-            std::memcpy(&addr_json_arena.blob[size_t(addr_json_arena.off[i])], t.out_addr_json.data(),
-                        t.out_addr_json.size());
-            std::memcpy(&amount_json_arena.blob[size_t(amount_json_arena.off[i])], t.out_amount_json.data(),
-                        t.out_amount_json.size());
+            std::memcpy(ajson_blob + ajson_off[i], t.out_addr_json.data(), t.out_addr_json.size());
+            std::memcpy(mjson_blob + mjson_off[i], t.out_amount_json.data(), t.out_amount_json.size());
+            std::memcpy(canon_blob + canon_off[i], t.canon.data(), t.canon.size());
         });
     }
-    // the stored hex column: the input string is reused when it already is the canonical lowercase
-    // hex of the tx (Python objects: with the GIL, on this thread)
+    // the stored hex column as str objects (object-path parity, mempool and cluster mirroring): the input
+    // string is reused when it already is the canonical lowercase hex of the tx
     auto tA = std::chrono::steady_clock::now();
     py::list canon_hex = new_list(N);
     for (size_t i = 0; i < N; ++i) {
@@ -670,22 +711,7 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
         }
     }
     auto tB = std::chrono::steady_clock::now();
-    d["in_keys"] = as_bytes(in_keys);
-    d["in_type"] = as_bytes(in_type);
-    d["in_sig"] = i32(in_sig);
-    d["in_tx"] = i32(in_tx);
-    d["sigs"] = as_bytes(sigs);
-    d["txid"] = as_bytes(txid);
-    d["digest"] = as_bytes(digest);
-    d["out_addr"] = as_bytes(out_addr);
-    d["out_len"] = as_bytes(out_len);
-    d["out_type"] = as_bytes(out_type);
-    d["out_tx"] = i32(out_tx);
-    d["out_amount"] = py::bytes(reinterpret_cast<const char*>(out_amount.data()), out_amount.size() * 8);
     d["hex"] = canon_hex;
-    d["out_addr_str"] = addr_arena.py();
-    d["out_addr_json"] = addr_json_arena.py();
-    d["out_amount_json"] = amount_json_arena.py();
     auto t2 = std::chrono::steady_clock::now();
     {
         py::gil_scoped_release rel;
@@ -797,21 +823,34 @@ static py::tuple address_pairs(py::bytes in_blob, py::bytes in_off_b, py::bytes 
 
 // ---- column helpers for the bulk ledger writes (ledger/fastpath.py)
 
-// numeric(Decimal(fee) / 10**8, 6): fee in smallest units rounded half up to 6 decimals
-static py::list fee_strings(py::bytes fee_b) {
+// numeric(Decimal(fee) / 10**8, 6): fee in smallest units rounded half up to 6 decimals, as a text arena
+// (blob, int64 offsets[n + 1]) that the bulk ledger writer binds directly
+static py::tuple fee_strings(py::bytes fee_b) {
     std::string f = fee_b;
     const int64_t* v = reinterpret_cast<const int64_t*>(f.data());
     const size_t n = f.size() / 8;
-    py::list out(n);
-    char buf[48];
+    Arena out;
+    out.blob.reserve(n * 12);
+    out.off.reserve(n + 1);
     for (size_t i = 0; i < n; ++i) {
         if (v[i] < 0) throw std::invalid_argument("negative fee");
-        const int64_t q = (v[i] + 50) / 100;
-        std::snprintf(buf, sizeof(buf), "%lld.%06lld", static_cast<long long>(q / 1000000),
-                      static_cast<long long>(q % 1000000));
-        out[i] = py::str(buf);
+        const uint64_t q = uint64_t(v[i] + 50) / 100;
+        char buf[32];
+        char* e = buf + sizeof(buf);
+        char* p = e;
+        uint64_t frac = q % 1000000, whole = q / 1000000;
+        for (int k = 0; k < 6; ++k) {
+            *--p = char('0' + frac % 10);
+            frac /= 10;
+        }
+        *--p = '.';
+        do {
+            *--p = char('0' + whole % 10);
+            whole /= 10;
+        } while (whole);
+        out.add(p, size_t(e - p));
     }
-    return out;
+    return out.py();
 }
 
 // Distinct rows of an (n x width) byte matrix: (unique rows in first-seen order, inverse int32[n]).

@@ -28,7 +28,7 @@ def _rows(pattern: str):
 def _name(row: dict) -> str:
     for k in ('Message', 'Function', 'Name', 'Marker_Message'):
         v = row.get(k)
-        if v and (v.startswith('block:') or v.startswith('apply:')):
+        if v and v.startswith(('block:', 'apply:', 'finalize:')):
             return v
     return ''
 
@@ -61,7 +61,7 @@ def main():
             row['stages'][name] = {'host_ms': round((t1 - t0) / 1e6, 3), 'kernels': len(inside),
                                    'gpu_busy_ms': round(busy, 3)}
             per_stage[name].append(((t1 - t0) / 1e6, busy, len(inside)))
-            if not name.startswith('apply:'):
+            if name.startswith('block:'):
                 for k0, k1, kn in inside:
                     per_kernel[(name, kn)].append((k1 - k0) / 1e6)
         detail.append(row)

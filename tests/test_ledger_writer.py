@@ -211,3 +211,21 @@ def test_deferred_block_record_is_durable_and_replayed(tmp_path):
     w.close()
     rows = [r[0] for r in sqlite3.connect(dbs[0]).execute('SELECT x FROM t ORDER BY rowid')]
     assert rows == ['b' * 100_000, 'b' * 100_000, 'after']
+
+
+def test_hexarena_column_binds_lowercase_hex(tmp_path):
+    # ('hexarena', blob, offsets[, sel]): raw bytes in the journal, lowercase hex text in SQL
+    w, dbs = _writer(tmp_path)
+    w.submit([lib().ledger_encode_stmt('CREATE TABLE IF NOT EXISTS t (i INTEGER, h TEXT)', [], 1)], b'', -1)
+    rows = [b'', b'\x00\xff', bytes(range(200))]
+    blob = b''.join(rows)
+    off = np.cumsum([0] + [len(r) for r in rows]).astype(np.int64)
+    ins = 'INSERT INTO t (i, h) VALUES (?, ?)'
+    seq = w.submit([lib().ledger_encode_stmt(ins, [np.arange(3, dtype=np.int64), ('hexarena', blob, off.tobytes())], 3),
+                    lib().ledger_encode_stmt(ins, [np.array([7, 8], dtype=np.int64),
+                                                   ('hexarena', blob, off.tobytes(), np.array([2, 1], np.int64))], 2)],
+                   b'', -1)
+    w.wait(seq)
+    w.close()
+    got = sqlite3.connect(dbs[0]).execute('SELECT i, h FROM t ORDER BY rowid').fetchall()
+    assert got == [(0, ''), (1, '00ff'), (2, bytes(range(200)).hex()), (7, bytes(range(200)).hex()), (8, '00ff')]

@@ -180,7 +180,7 @@ def test_fee_strings_match_python(L):
     from upow_amd.ledger.database import numeric
     rng = random.Random(4)
     fees = [0, 1, 49, 50, 51, 149, 150, 10 ** 8, 123456789012345] + [rng.randrange(1 << 50) for _ in range(300)]
-    got = L.fee_strings(np.array(fees, dtype=np.int64).tobytes())
+    got = arena_list(L.fee_strings(np.array(fees, dtype=np.int64).tobytes()))
     assert got == [numeric(Decimal(f) / 10 ** 8, 6) for f in fees]
     # the other row columns of the bulk writes are bound natively from the codec's buffers: see
     # tests/test_ledger_sql.py (hex32 / arena / gather columns) and tests/test_fastpath.py

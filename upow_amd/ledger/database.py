@@ -288,6 +288,11 @@ def _expand_col(spec, n: int) -> list:
             off = np.frombuffer(spec[2], dtype=np.int64).tolist()
             rows = np.asarray(spec[3]).tolist() if len(spec) > 3 else range(n)
             return [blob[off[i]:off[i + 1]] for i in rows]
+        if kind == 'hexarena':  # raw bytes per row, stored as their lowercase hex
+            blob = bytes(spec[1])
+            off = np.frombuffer(spec[2], dtype=np.int64).tolist()
+            rows = np.asarray(spec[3]).tolist() if len(spec) > 3 else range(n)
+            return [blob[off[i]:off[i + 1]].hex() for i in rows]
         raise ValueError(f'unknown column kind {kind}')
     if isinstance(spec, np.ndarray):
         return spec.tolist()
@@ -921,6 +926,8 @@ class Database:
         if n == 0:
             return 0
         rows = list(zip(*[_expand_col(c, n) for c in cols]))
+        if isinstance(order, str):  # 'key': by the leading 8 bytes of the column-0 hashes
+            order = np.argsort(np.array([bytes.fromhex(r[0][:16]) for r in rows], dtype='S8'), kind='stable')
         if order is not None:
             rows = [rows[i] for i in np.asarray(order).tolist()]
         return self._xm(sql, rows).rowcount
@@ -1845,7 +1852,9 @@ class Database:
         in_tag = gov['in_tag'].astype(np.uint32) if gov is not None else np.full(n_in, tag_u, dtype=np.uint32)
         spent[:, 36:40] = np.ascontiguousarray(in_tag).reshape(-1, 1).view(np.uint8)
         in_idx = in_keys[:, 32:36].copy().view(np.uint32).ravel().astype(np.int64)
-        in_order = self._key_order(in_keys) if n_in else None
+        # the spends' key order (B-tree locality) is computed by the materialiser ('key'), except where
+        # governance selections need the ranks here
+        in_order = self._key_order(in_keys) if n_in and gov is not None else 'key'
         if gov is not None and n_in:
             in_order_rank = np.empty(n_in, dtype=np.int64)  # position of each input in the key order
             in_order_rank[in_order] = np.arange(n_in, dtype=np.int64)
@@ -1914,7 +1923,7 @@ class Database:
         if mempool:
             txids = np.ascontiguousarray(tx_cols[0][1], dtype=np.uint8).reshape(-1, 32)
             stmts.append(('DELETE FROM pending_transactions WHERE tx_hash = ?', [('hex32', txids, 32, 0)], n,
-                          self._key_order(txids), 'SELECT EXISTS(SELECT 1 FROM pending_transactions)', None))
+                          'key', 'SELECT EXISTS(SELECT 1 FROM pending_transactions)', None))
 
         def spend_stmt(table):
             sel = gov_spent[table]
@@ -1955,10 +1964,9 @@ class Database:
         if self.writer is not None:
             enc = [self.encode(*st) for st in stmts]
             stamp()
-            meta = b''.join((bytes.fromhex(b['hash']), struct.pack('<qII', int(b['id']), n_out + len(cb_keys), n_in),
-                             memoryview(recs),
-                             memoryview(np.ascontiguousarray(cb_recs)), memoryview(spent),
-                             memoryview(np.ascontiguousarray(spent_payload)).cast('B')))
+            # the undo record as parts: the writer joins them in one copy off the GIL
+            meta = [bytes.fromhex(b['hash']), struct.pack('<qII', int(b['id']), n_out + len(cb_keys), n_in), recs,
+                    np.ascontiguousarray(cb_recs), spent, np.ascontiguousarray(spent_payload).view(np.uint8)]
             seq = self.submit_batch(enc, tables, meta, int(b['id']), defer_sync=True)
         else:
             stamp()

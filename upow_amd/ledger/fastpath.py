@@ -280,8 +280,10 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     # ---- keys + verify records: every distinct 33-byte key (signers + outputs) decompressed in one
     #      batch, then the 160-byte records of the signature jobs, in one native call
     #      (csrc/txcodec.cpp block_signer_records); blocks with 64-byte addresses take the numpy path
-    in_sig = _i32(d, 'in_sig')
-    sig_ids, job_input = np.unique(in_sig, return_index=True)  # first input per distinct signature
+    # one job per distinct signature, checked with its first input's key (the codec numbers signatures in
+    # order of first use, so the first input of each is a column of its own)
+    job_input = _i32(d, 'sig_first_in').astype(np.int64)
+    sig_ids = np.arange(len(job_input), dtype=np.int64)
     sigs = np.frombuffer(d['sigs'], dtype=np.uint8).reshape(-1, 64)
     digest = np.frombuffer(d['digest'], dtype=np.uint8).reshape(-1, 32)
     job_tx = in_tx[job_input]
@@ -333,32 +335,36 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
 
     # ---- columns for the ledger writes: views of the codec's buffers, encoded natively into one journal
     #      batch by csrc/ledger_writer.cpp (tx hashes rendered from the raw digests, text arenas for strings)
+    roctx.push('apply:strings')
     L = lib()
     in_str = L.input_address_strings(np.ascontiguousarray(pay['addr']).tobytes(), pay['len'].astype(np.uint8).tobytes(),
                                      d['in_start'], THREADS, True)
     in_json = in_str[:2]
     # the block's address_transactions rows (each tx's distinct input owners and output addresses)
     addr_pairs = L.address_pairs(in_str[2], in_str[3], d['in_start'], *d['out_addr_str'], d['out_start'])
-    fee_str = L.fee_strings(np.ascontiguousarray(fee, dtype=np.int64).tobytes())
+    fee_str = ('arena', *L.fee_strings(np.ascontiguousarray(fee, dtype=np.int64).tobytes()))
     out_index = np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]
     gov_cols = None
     if bg.any:
         gov_cols = {'out_tag': bg.output_tags(TAG_BY_TABLE), 'out_type': out_type, 'in_tag': in_tag,
                     'gov_tx': bg.gov, 'out_tx': out_tx, 'out_start': out_start, 'in_start': in_start,
                     'in_str': in_str[2:]}
+    roctx.pop()
 
     async def apply(block_hash, address, random, block_reward, content_time, coinbase_transaction):
         ta = perf_counter()
+        roctx.push('apply:coinbase')
         from .database import numeric
         block_row = {'id': block_no, 'hash': block_hash, 'content': block_content, 'address': address,
                      'random': int(random), 'difficulty': numeric(difficulty, 1),
                      'reward': numeric(block_reward + fees_total, 6), 'timestamp': int(content_time)}
         cb_row = await database._tx_row(coinbase_transaction, block_hash)
         cb_outputs = Database.split_outputs([coinbase_transaction])['unspent_outputs']
-        tx_cols = [('hex32', txid, 32, 0), d['hex'], ('arena', *in_json), ('arena', *d['out_addr_json']),
+        tx_cols = [('hex32', txid, 32, 0), ('hexarena', *d['canon']), ('arena', *in_json), ('arena', *d['out_addr_json']),
                    ('arena', *d['out_amount_json']), fee_str]
         out_cols = (out_index, ('arena', *d['out_addr_str']), txid[out_tx], out_amount, out_addr, out_len)
         submitted = database._submitted
+        roctx.pop()
         try:
             seq = database.apply_native_block(block_row, cb_row, cb_outputs, n, tx_cols, out_cols, in_keys, pay,
                                               gov=gov_cols, addr_pairs=addr_pairs)

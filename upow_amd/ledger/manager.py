@@ -23,7 +23,7 @@ from ..constants import (BLOCK_TIME, BLOCKS_COUNT, LAST_BLOCK_FOR_GENESIS_KEY, M
 from ..models.block import (block_to_bytes, check_pow, get_transactions_merkle_tree,
                             get_transactions_merkle_tree_ordered, split_block_content)
 from ..models.transaction import CoinbaseTransaction, Transaction, TransactionOutput
-from ..utils import codec, metrics
+from ..utils import codec, metrics, roctx
 from ..utils.codec import TransactionType, round_up_decimal, round_up_decimal_new, sha256, timestamp
 from ..utils.logger import get_logger
 from .database import Database
@@ -504,6 +504,7 @@ async def _finalize_block(block_no: int, block_content: str, fees, n_txs: int, a
     ledger writes (``apply``), logs, UTXO snapshot cadence and the emission-details record. Shared by
     the object path (:func:`_create_block`) and the native block path (ledger/fastpath.py)."""
     database: Database = Database.instance
+    roctx.push('finalize:rewards')
     block_hash = sha256(block_content)
     previous_hash, address, merkle_tree, content_time, content_difficulty, random = split_block_content(block_content)
     ta = perf_counter()
@@ -523,9 +524,12 @@ async def _finalize_block(block_no: int, block_content: str, fees, n_txs: int, a
     if inode_rewards:
         coinbase_transaction.outputs.extend([TransactionOutput(a, r) for a, r in inode_rewards.items()])
     if not all(o.verify() for o in coinbase_transaction.outputs):
+        roctx.pop()
         return False
+    roctx.pop()
     if not await apply(block_hash, address, random, block_reward, content_time, coinbase_transaction):
         return False
+    roctx.push('finalize:post')
     logger.info(f'Added {n_txs} transactions in block {block_no}. Reward: {block_reward}, Fees: {fees} '
                 f'in {perf_counter() - create_start_time:.3f} seconds')
     if block_no % 10 == 0:
@@ -538,6 +542,7 @@ async def _finalize_block(block_no: int, block_content: str, fees, n_txs: int, a
         database.emission_details.set(str(block_no), details)
     except Exception as e:
         logger.error(f'Error in creating block: {block_no} {str(e)}')
+    roctx.pop()
     return True
 
 
