@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -728,97 +729,204 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
     return d;
 }
 
+// A new Python bytes object of `len` bytes to be filled in place (GIL held for the allocation only).
+static py::bytes new_pybytes(size_t len, char*& p) {
+    PyObject* o = PyBytes_FromStringAndSize(nullptr, Py_ssize_t(len));
+    if (!o) throw py::error_already_set();
+    p = PyBytes_AS_STRING(o);
+    return py::reinterpret_steal<py::bytes>(o);
+}
+
+template <class T>
+static const T* buf_view(const py::buffer_info& bi, size_t& count) {
+    const size_t total = size_t(bi.size) * size_t(bi.itemsize);
+    if (total % sizeof(T)) throw std::invalid_argument("buffer size is not a multiple of its element");
+    count = total / sizeof(T);
+    return static_cast<const T*>(bi.ptr);
+}
+
+// tx segment starts int32[n_tx + 1] over `n_items` rows: non-decreasing, from 0, ending at n_items
+static void check_starts(const int32_t* st, size_t n_tx, size_t n_items, const char* what) {
+    if (st[0] != 0 || size_t(st[n_tx]) != n_items) throw std::invalid_argument(std::string(what) + ": bad segment starts");
+    for (size_t t = 0; t < n_tx; ++t)
+        if (st[t + 1] < st[t]) throw std::invalid_argument(std::string(what) + ": segment starts decrease");
+}
+
 // Canonical compressed address strings for spent outputs (database._input_address): 33-byte
 // addresses keep x with the normalised prefix, 64-byte ones take the parity of y. Returns the
-// per-tx inputs_addresses JSON column as a text arena (blob, int64 offsets[n_tx + 1]).
-static py::tuple input_address_strings(py::bytes addrs64, py::bytes lens, py::bytes in_start_b, int threads,
+// per-tx inputs_addresses JSON column as a text arena (blob, int64 offsets[n_tx + 1]) and, with
+// `per_input`, each input's string as a second arena. Every pass is parallel over the pool and writes
+// straight into the result bytes; the strings live in fixed slots (no per-input allocation).
+static py::tuple input_address_strings(py::buffer addrs64, py::buffer lens, py::buffer in_start_b, int threads,
                                        bool per_input) {
-    std::string a = addrs64, l = lens, s = in_start_b;
-    const size_t n_in = l.size();
-    const size_t n_tx = s.size() / 4 - 1;
-    if (a.size() != 64 * n_in) throw std::invalid_argument("addrs64 must be 64 bytes per input");
-    const int32_t* st = reinterpret_cast<const int32_t*>(s.data());
-    std::vector<std::string> out(n_in);
-    std::vector<uint8_t> bad(n_in, 0);
+    const py::buffer_info abi = addrs64.request(), lbi = lens.request(), sbi = in_start_b.request();
+    size_t n_a = 0, n_in = 0, n_st = 0;
+    const uint8_t* a = buf_view<uint8_t>(abi, n_a);
+    const uint8_t* l = buf_view<uint8_t>(lbi, n_in);
+    const int32_t* st = buf_view<int32_t>(sbi, n_st);
+    if (n_st < 1) throw std::invalid_argument("in_start must have n_tx + 1 entries");
+    const size_t n_tx = n_st - 1;
+    if (n_a != 64 * n_in) throw std::invalid_argument("addrs64 must be 64 bytes per input");
+    check_starts(st, n_tx, n_in, "input_address_strings");
+    struct Slot {
+        char s[46];
+        uint8_t len;
+    };
+    std::vector<Slot> out(n_in);
+    std::atomic<bool> bad{false};
     {
         py::gil_scoped_release rel;
         parallel_for(int64_t(n_in), threads, [&](int64_t i) {
-            const uint8_t* p = reinterpret_cast<const uint8_t*>(a.data()) + 64 * size_t(i);
+            const uint8_t* p = a + 64 * size_t(i);
             uint8_t c[33];
-            if (uint8_t(l[size_t(i)]) == 33) {
+            if (l[size_t(i)] == 33) {
                 c[0] = p[0] == 43 ? 43 : 42;
                 std::memcpy(c + 1, p + 1, 32);
-            } else if (uint8_t(l[size_t(i)]) == 64) {
+            } else if (l[size_t(i)] == 64) {
                 c[0] = (p[32] & 1) ? 43 : 42;  // y little-endian: parity is bit 0 of byte 32
                 std::memcpy(c + 1, p, 32);
             } else {
-                bad[size_t(i)] = 1;
+                bad = true;
                 return;
             }
-            b58_33(c, out[size_t(i)]);
+            thread_local std::string scratch;
+            b58_33(c, scratch);
+            if (scratch.size() > sizeof(out[0].s)) {
+                bad = true;
+                return;
+            }
+            std::memcpy(out[size_t(i)].s, scratch.data(), scratch.size());
+            out[size_t(i)].len = uint8_t(scratch.size());
         });
     }
-    for (size_t i = 0; i < n_in; ++i)
-        if (bad[i]) throw std::invalid_argument("input address payload missing");
-    Arena json;
-    json.blob.reserve(n_tx * 100);
-    std::string j;
+    if (bad) throw std::invalid_argument("input address payload missing");
+    // JSON rows: ["a","b",...] -> 2 + sum(len + 2) + (k - 1) commas (2 for an empty list)
+    std::vector<int64_t> joff(n_tx + 1, 0);
     for (size_t t = 0; t < n_tx; ++t) {
-        j.assign(1, '[');
-        for (int32_t k = st[t]; k < st[t + 1]; ++k) {
-            if (k > st[t]) j += ',';
-            j += '"';
-            j += out[size_t(k)];
-            j += '"';
-        }
-        j += ']';
-        json.add(j.data(), j.size());
+        int64_t len = 2;
+        for (int32_t k = st[t]; k < st[t + 1]; ++k) len += out[size_t(k)].len + 2 + (k > st[t] ? 1 : 0);
+        joff[t + 1] = joff[t] + len;
     }
-    if (!per_input) return json.py();
-    // also each input's string on its own (the governance store's ballot voters)
-    Arena each;
-    each.blob.reserve(n_in * 45);
-    for (size_t i = 0; i < n_in; ++i) each.add(out[i].data(), out[i].size());
-    py::tuple jt = json.py(), et = each.py();
-    return py::make_tuple(jt[0], jt[1], et[0], et[1]);
+    char* jb;
+    py::bytes jblob = new_pybytes(size_t(joff[n_tx]), jb);
+    std::vector<int64_t> eoff;
+    char* eb = nullptr;
+    py::bytes eblob;
+    if (per_input) {
+        eoff.assign(n_in + 1, 0);
+        for (size_t i = 0; i < n_in; ++i) eoff[i + 1] = eoff[i] + out[i].len;
+        eblob = new_pybytes(size_t(eoff[n_in]), eb);
+    }
+    {
+        py::gil_scoped_release rel;
+        parallel_for(int64_t(n_tx), threads, [&](int64_t t) {
+            char* q = jb + joff[size_t(t)];
+            *q++ = '[';
+            for (int32_t k = st[t]; k < st[t + 1]; ++k) {
+                if (k > st[t]) *q++ = ',';
+                *q++ = '"';
+                std::memcpy(q, out[size_t(k)].s, out[size_t(k)].len);
+                q += out[size_t(k)].len;
+                *q++ = '"';
+            }
+            *q = ']';
+        });
+        if (per_input)
+            parallel_for(int64_t(n_in), threads, [&](int64_t i) {
+                std::memcpy(eb + eoff[size_t(i)], out[size_t(i)].s, out[size_t(i)].len);
+            });
+    }
+    auto offs = [](const std::vector<int64_t>& v) {
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size() * 8);
+    };
+    if (!per_input) return py::make_tuple(jblob, offs(joff));
+    return py::make_tuple(jblob, offs(joff), eblob, offs(eoff));
 }
 
 // address_transactions rows of a block's txs: every distinct address among each tx's input owners and
 // output addresses (the set the reference's json_each(inputs_addresses) UNION json_each(outputs_addresses)
 // yields per tx). Inputs: per-input and per-output string arenas with their tx segment starts. Returns
-// (address arena blob, int64 offsets, int64 tx index per row).
-static py::tuple address_pairs(py::bytes in_blob, py::bytes in_off_b, py::bytes in_start_b, py::bytes out_blob,
-                               py::bytes out_off_b, py::bytes out_start_b) {
-    const std::string ib = in_blob, io = in_off_b, is = in_start_b, ob = out_blob, oo = out_off_b, os = out_start_b;
-    const int64_t* ioff = reinterpret_cast<const int64_t*>(io.data());
-    const int64_t* ooff = reinterpret_cast<const int64_t*>(oo.data());
-    const int32_t* ist = reinterpret_cast<const int32_t*>(is.data());
-    const int32_t* ost = reinterpret_cast<const int32_t*>(os.data());
-    const size_t n = is.size() / 4 - 1;
-    if (os.size() / 4 - 1 != n) throw std::invalid_argument("address_pairs: tx counts differ");
-    const size_t n_in = io.size() / 8 - 1, n_out = oo.size() / 8 - 1;
-    if (size_t(ist[n]) > n_in || size_t(ost[n]) > n_out) throw std::invalid_argument("address_pairs: short arenas");
-    if (ioff[n_in] > int64_t(ib.size()) || ooff[n_out] > int64_t(ob.size()))
-        throw std::invalid_argument("address_pairs: offsets past the blob");
-    Arena out;
-    std::vector<int64_t> tx;
-    std::vector<std::string_view> seen;
-    out.blob.reserve(ib.size() + ob.size());
-    for (size_t k = 0; k < n; ++k) {
-        seen.clear();
-        auto take = [&](const std::string& blob, const int64_t* off, int64_t j) {
-            std::string_view v(blob.data() + off[j], size_t(off[j + 1] - off[j]));
-            for (auto& w : seen)
+// (address arena blob, int64 offsets, int64 tx index per row). Two parallel passes over the txs: count
+// (rows, bytes) per tx, then fill at the prefix-summed positions.
+static py::tuple address_pairs(py::buffer in_blob, py::buffer in_off_b, py::buffer in_start_b, py::buffer out_blob,
+                               py::buffer out_off_b, py::buffer out_start_b, int threads) {
+    const py::buffer_info ibi = in_blob.request(), iobi = in_off_b.request(), isbi = in_start_b.request(),
+                          obi = out_blob.request(), oobi = out_off_b.request(), osbi = out_start_b.request();
+    size_t ib_n, io_n, is_n, ob_n, oo_n, os_n;
+    const char* ib = buf_view<char>(ibi, ib_n);
+    const int64_t* ioff = buf_view<int64_t>(iobi, io_n);
+    const int32_t* ist = buf_view<int32_t>(isbi, is_n);
+    const char* ob = buf_view<char>(obi, ob_n);
+    const int64_t* ooff = buf_view<int64_t>(oobi, oo_n);
+    const int32_t* ost = buf_view<int32_t>(osbi, os_n);
+    if (is_n < 1 || os_n != is_n) throw std::invalid_argument("address_pairs: tx counts differ");
+    if (io_n < 1 || oo_n < 1) throw std::invalid_argument("address_pairs: empty offsets");
+    const size_t n = is_n - 1, n_in = io_n - 1, n_out = oo_n - 1;
+    check_starts(ist, n, n_in, "address_pairs inputs");
+    check_starts(ost, n, n_out, "address_pairs outputs");
+    auto check_off = [](const int64_t* off, size_t m, size_t blen) {
+        if (off[0] < 0) throw std::invalid_argument("address_pairs: negative offset");
+        for (size_t j = 0; j < m; ++j)
+            if (off[j + 1] < off[j]) throw std::invalid_argument("address_pairs: offsets decrease");
+        if (size_t(off[m]) > blen) throw std::invalid_argument("address_pairs: offsets past the blob");
+    };
+    check_off(ioff, n_in, ib_n);
+    check_off(ooff, n_out, ob_n);
+    // the distinct strings of tx k in first-seen order, as (blob, offset index) pairs
+    auto each_distinct = [&](size_t k, auto&& emit) {
+        std::string_view seen[64];
+        size_t n_seen = 0;
+        std::vector<std::string_view> more;  // txs with more than 64 distinct addresses (rare)
+        auto take = [&](std::string_view v) {
+            for (size_t q = 0; q < n_seen; ++q)
+                if (seen[q] == v) return;
+            for (auto& w : more)
                 if (w == v) return;
-            seen.push_back(v);
-            out.add(v.data(), v.size());
-            tx.push_back(int64_t(k));
+            if (n_seen < 64) seen[n_seen++] = v;
+            else more.push_back(v);
+            emit(v);
         };
-        for (int64_t j = ist[k]; j < ist[k + 1]; ++j) take(ib, ioff, j);
-        for (int64_t o = ost[k]; o < ost[k + 1]; ++o) take(ob, ooff, o);
+        for (int64_t j = ist[k]; j < ist[k + 1]; ++j) take(std::string_view(ib + ioff[j], size_t(ioff[j + 1] - ioff[j])));
+        for (int64_t o = ost[k]; o < ost[k + 1]; ++o) take(std::string_view(ob + ooff[o], size_t(ooff[o + 1] - ooff[o])));
+    };
+    std::vector<int64_t> rows(n + 1, 0), bytes(n + 1, 0);
+    {
+        py::gil_scoped_release rel;
+        parallel_for(int64_t(n), threads, [&](int64_t k) {
+            int64_t r = 0, b = 0;
+            each_distinct(size_t(k), [&](std::string_view v) {
+                ++r;
+                b += int64_t(v.size());
+            });
+            rows[size_t(k) + 1] = r;
+            bytes[size_t(k) + 1] = b;
+        });
     }
-    py::tuple a = out.py();
-    return py::make_tuple(a[0], a[1], py::bytes(reinterpret_cast<const char*>(tx.data()), tx.size() * 8));
+    for (size_t k = 0; k < n; ++k) {
+        rows[k + 1] += rows[k];
+        bytes[k + 1] += bytes[k];
+    }
+    const size_t R = size_t(rows[n]);
+    char *blob, *offp, *txp;
+    py::bytes blob_b = new_pybytes(size_t(bytes[n]), blob), off_b = new_pybytes((R + 1) * 8, offp),
+              tx_b = new_pybytes(R * 8, txp);
+    int64_t* off = reinterpret_cast<int64_t*>(offp);
+    int64_t* tx = reinterpret_cast<int64_t*>(txp);
+    off[0] = 0;
+    {
+        py::gil_scoped_release rel;
+        parallel_for(int64_t(n), threads, [&](int64_t k) {
+            int64_t r = rows[size_t(k)], b = bytes[size_t(k)];
+            each_distinct(size_t(k), [&](std::string_view v) {
+                std::memcpy(blob + b, v.data(), v.size());
+                b += int64_t(v.size());
+                off[r + 1] = b;
+                tx[r] = k;
+                ++r;
+            });
+        });
+    }
+    return py::make_tuple(blob_b, off_b, tx_b);
 }
 
 // ---- column helpers for the bulk ledger writes (ledger/fastpath.py)
@@ -1005,7 +1113,7 @@ void register_txcodec(py::module_& m) {
     m.def("decode_block_txs", &decode_block_txs, py::arg("hexes"), py::arg("threads") = 8,
           "Decode, canonicalise and hash a block's transactions (see csrc/txcodec.cpp)");
     m.def("address_pairs", &address_pairs, py::arg("in_blob"), py::arg("in_off"), py::arg("in_start"),
-          py::arg("out_blob"), py::arg("out_off"), py::arg("out_start"));
+          py::arg("out_blob"), py::arg("out_off"), py::arg("out_start"), py::arg("threads") = 8);
     m.def("input_address_strings", &input_address_strings, py::arg("addrs64"), py::arg("lens"), py::arg("in_start"),
           py::arg("threads") = 8, py::arg("per_input") = false);
 }

@@ -184,3 +184,24 @@ def test_fee_strings_match_python(L):
     assert got == [numeric(Decimal(f) / 10 ** 8, 6) for f in fees]
     # the other row columns of the bulk writes are bound natively from the codec's buffers: see
     # tests/test_ledger_sql.py (hex32 / arena / gather columns) and tests/test_fastpath.py
+
+
+def test_address_pairs_distinct_per_tx(L):
+    # each tx's distinct addresses, inputs first then outputs, in first-seen order (the address index rows)
+    rng = random.Random(11)
+    pool = [''.join(rng.choice('abcdefgh') for _ in range(rng.randrange(1, 50))) for _ in range(12)]
+    txs = [([rng.choice(pool) for _ in range(rng.randrange(0, 5))], [rng.choice(pool) for _ in range(rng.randrange(0, 90))])
+           for _ in range(300)]
+
+    def arena(strs):
+        off = np.cumsum([0] + [len(x) for x in strs]).astype(np.int64)
+        return ''.join(strs).encode(), off.tobytes()
+
+    ins = [a for t in txs for a in t[0]]
+    outs = [a for t in txs for a in t[1]]
+    ist = np.cumsum([0] + [len(t[0]) for t in txs]).astype(np.int32).tobytes()
+    ost = np.cumsum([0] + [len(t[1]) for t in txs]).astype(np.int32).tobytes()
+    blob, off, tx = L.address_pairs(*arena(ins), ist, *arena(outs), ost, 3)
+    got = list(zip(np.frombuffer(tx, np.int64).tolist(), arena_list((blob, off))))
+    want = [(k, a) for k, t in enumerate(txs) for a in dict.fromkeys(t[0] + t[1])]
+    assert got == want

@@ -337,11 +337,11 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     #      batch by csrc/ledger_writer.cpp (tx hashes rendered from the raw digests, text arenas for strings)
     roctx.push('apply:strings')
     L = lib()
-    in_str = L.input_address_strings(np.ascontiguousarray(pay['addr']).tobytes(), pay['len'].astype(np.uint8).tobytes(),
+    in_str = L.input_address_strings(np.ascontiguousarray(pay['addr']), np.ascontiguousarray(pay['len'], dtype=np.uint8),
                                      d['in_start'], THREADS, True)
     in_json = in_str[:2]
     # the block's address_transactions rows (each tx's distinct input owners and output addresses)
-    addr_pairs = L.address_pairs(in_str[2], in_str[3], d['in_start'], *d['out_addr_str'], d['out_start'])
+    addr_pairs = L.address_pairs(in_str[2], in_str[3], d['in_start'], *d['out_addr_str'], d['out_start'], THREADS)
     fee_str = ('arena', *L.fee_strings(np.ascontiguousarray(fee, dtype=np.int64).tobytes()))
     out_index = np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]
     gov_cols = None
