@@ -1022,7 +1022,10 @@ class LedgerWriter {
                     error_ = "undo log: " + err;
                 }
             }
-            if (werr.empty() && err.empty() && sync_ != SYNC_OFF) {
+            // block records: durable before durable(seq) returns (any mode but off); other deferred
+            // records only in commit mode (the materialisers' group sync covers them otherwise)
+            const bool want_sync = sync_ == SYNC_COMMIT || (sync_ != SYNC_OFF && job.block_id >= 0);
+            if (werr.empty() && err.empty() && want_sync) {
                 try {
                     make_durable(seq);
                 } catch (const std::exception&) {

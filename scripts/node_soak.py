@@ -60,6 +60,17 @@ with open(src + '.out', 'w') as f:
 '''
 
 
+def _cpu_stat() -> dict:
+    """The cgroup's CPU accounting (cgroup v2 cpu.stat): usage and CFS bandwidth throttling. A GPU box
+    runs the job under a CPU quota far below its core count; a throttled period freezes every thread of the
+    node (the HTTP loop included) until the next period, which reads as a loop stall of up to ~100 ms."""
+    try:
+        with open('/sys/fs/cgroup/cpu.stat') as f:
+            return {k: int(v) for k, v in (ln.split() for ln in f if ln.strip())}
+    except (OSError, ValueError):
+        return {}
+
+
 def _port():
     s = socket.socket()
     s.bind(('127.0.0.1', 0))
@@ -201,6 +212,7 @@ def main():
     signed = [make_tx(h, i, amount, [(sinks[k % len(sinks)], amount - fee)])
               for k, (h, i, amount) in enumerate(pool[:int(a.rate * a.seconds) + 1])]
     t0 = time.time()
+    cpu0 = _cpu_stat()
     phase[0] = 'push'
     errors = [0]
     lock = threading.Lock()
@@ -258,6 +270,7 @@ def main():
                     errors[0] += 1
     n = len(pushed) + errors[0]
     t_push_end = time.time()
+    cpu1 = _cpu_stat()
     phase[0] = 'drain'
     # drain: wait until everything pushed is in a block (or 4 block intervals)
     deadline = time.time() + 120
@@ -352,6 +365,13 @@ def main():
                         'max_ms': round(max((g['ms'] for g in gcs), default=0), 1),
                         'gen2': sum(1 for g in gcs if g.get('gen') == 2)},
         'block_stage_ms_mean': {k: round(sum(v) / len(v), 2) for k, v in sorted(stages.items())},
+        # the whole job's cgroup over the push window (node, miner and the pushing clients share it)
+        'cgroup_cpu': {'cpus_used_mean': round((cpu1.get('usage_usec', 0) - cpu0.get('usage_usec', 0)) / 1e6
+                                               / max(1e-9, t_push_end - t0), 2),
+                       'nr_periods': cpu1.get('nr_periods', 0) - cpu0.get('nr_periods', 0),
+                       'nr_throttled': cpu1.get('nr_throttled', 0) - cpu0.get('nr_throttled', 0),
+                       'throttled_ms': round((cpu1.get('throttled_usec', 0) - cpu0.get('throttled_usec', 0)) / 1e3, 1)}
+        if cpu0 and cpu1 else None,
         'difficulty': a.difficulty, 'setup_s': round(setup_s, 1), 'data': 'synthetic keys, miner coinbases fanned out',
     }
     line = json.dumps(out)

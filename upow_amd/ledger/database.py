@@ -571,6 +571,7 @@ class Database:
         mode = {'off': 0, 'group': 1, 'commit': 2, 'block': 3}[os.environ.get('UPOW_JOURNAL_SYNC', 'block')]
         if self.path == ':memory:':
             mode = 0
+        self._journal_sync_mode = mode
         journal = os.environ.get('UPOW_JOURNAL_PATH') or os.path.join(os.path.dirname(os.path.abspath(self.file)),
                                                                        os.path.basename(self.file) + '.journal')
         self.writer = lib().LedgerWriter([self.file, *self.utxo_files, *self.tx_files], journal, mode, cache_mb,
@@ -759,8 +760,10 @@ class Database:
             self._mempool_ver += 1
             self._mp = None
 
+    _journal_sync_mode = 0
+
     def submit_batch(self, stmts: List[bytes], tables: Iterable[str], meta: bytes = b'', block_id: int = -1,
-                     defer_sync: bool = False) -> int:
+                     defer_sync: bool = False, write_behind: bool = False) -> int:
         """Commit a batch of encoded statements (``lib().ledger_encode_stmt``) through the journal.
 
         Does not take the connection lock: a block's batch is megabytes, and the /push_tx path must not
@@ -781,6 +784,11 @@ class Database:
             # block is not answered or gossiped before wait_durable() (UPOW_JOURNAL_SYNC=block semantics).
             seq = self.writer.submit(stmts, meta, block_id, False)
             self._durable_seq = seq
+        elif write_behind and self._journal_sync_mode != 2:
+            # a mempool record (not synced on its own unless UPOW_JOURNAL_SYNC=commit): the sequence number
+            # is reserved here and the writer's I/O thread writes it, so the HTTP loop never waits behind a
+            # block record's multi-megabyte write on the same file
+            seq = self.writer.submit(stmts, meta, block_id, False)
         else:
             seq = self.writer.submit(stmts, meta, block_id)
         with self._seq_lock:
@@ -1140,7 +1148,7 @@ class Database:
                                      [[k[:32].hex() for k in late_in],
                                       np.array([int.from_bytes(k[32:36], 'little') for k in late_in], np.int64)],
                                      len(late_in)))
-        self.submit_batch(stmts, self._PENDING)
+        self.submit_batch(stmts, self._PENDING, write_behind=True)
 
     def _pending_spent_set(self) -> Set[Tuple[str, int]]:
         return {(r[0], r[1]) for r in self._q('SELECT tx_hash, "index" FROM pending_spent_outputs')}
@@ -1192,7 +1200,7 @@ class Database:
                 stmts.append(self.encode('INSERT INTO pending_spent_outputs (tx_hash, "index") VALUES (?, ?)',
                                          [[h for h, _ in inputs], np.array([i for _, i in inputs], np.int64)],
                                          len(inputs)))
-            seq = self.submit_batch(stmts, self._PENDING)
+            seq = self.submit_batch(stmts, self._PENDING, write_behind=True)
             mp.set_seq(tx_hash, inputs, seq)
         self._pending_empty = False
         self._mempool_ver += 1
