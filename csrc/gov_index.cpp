@@ -31,6 +31,7 @@
 #include <map>
 #include <optional>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -594,9 +595,9 @@ class GovStore {
     // ``in_str``/``in_off``: each input's owner as the tx row's inputs_addresses column holds it (compressed
     // base58 of the spent output's address; txcodec input_address_strings(per_input=True))
     py::dict apply_block(py::buffer out_type_b, py::buffer txid_b, py::buffer out_tx_b, py::buffer out_start_b,
-                         py::buffer out_amount_b, py::buffer out_addr_b, py::buffer out_len_b, py::bytes addr_blob,
+                         py::buffer out_amount_b, py::buffer out_addr_b, py::buffer out_len_b, py::buffer addr_blob,
                          py::buffer addr_off_b, py::buffer in_start_b, py::buffer pay_b, py::buffer in_keys_b,
-                         py::buffer in_tag_b, py::bytes in_str, py::buffer in_off_b, int64_t n, int64_t block_ts) {
+                         py::buffer in_tag_b, py::buffer in_str, py::buffer in_off_b, int64_t n, int64_t block_ts) {
         const int32_t* os = buf<int32_t>(out_start_b, size_t(n) + 1, "out_start");
         const int32_t* is = buf<int32_t>(in_start_b, size_t(n) + 1, "in_start");
         const int64_t n_out = os[n], n_in = is[n];
@@ -611,8 +612,14 @@ class GovStore {
         const uint8_t* ik = buf<uint8_t>(in_keys_b, size_t(n_in) * 40, "in_keys");
         const uint8_t* itag = buf<uint8_t>(in_tag_b, size_t(n_in), "in_tag");
         const int64_t* ioff = buf<int64_t>(in_off_b, size_t(n_in) + 1, "input string offsets");
-        const std::string blob = addr_blob, istr = in_str;
+        const py::buffer_info bbi = addr_blob.request(), sbi = in_str.request();
+        const std::string_view blob(static_cast<const char*>(bbi.ptr), size_t(bbi.size * bbi.itemsize));
+        const std::string_view istr(static_cast<const char*>(sbi.ptr), size_t(sbi.size * sbi.itemsize));
         if (ioff[n_in] > int64_t(istr.size())) throw std::invalid_argument("input strings: offsets past the blob");
+        if (n_out && aoff[n_out] > int64_t(blob.size())) throw std::invalid_argument("addresses: offsets past the blob");
+        // pure C++ from here (the caller holds the index lock; the buffers stay alive for the call)
+        std::optional<py::gil_scoped_release> nogil;
+        nogil.emplace();
         // spends leave their tables (UTXO tags: 0 unspent_outputs -> staked rows, 1..6 governance tables)
         static const int kTagTid[7] = {STAKE, INODE, VALIDATOR, VVP, DVP, VBALLOT, IBALLOT};
         int64_t removed = 0, added = 0;
@@ -656,6 +663,7 @@ class GovStore {
             insert(tid, key_of(txid + 32 * k, index), std::move(row));
             ++added;
         }
+        nogil.reset();
         py::dict d;
         d["removed"] = removed;
         d["added"] = added;

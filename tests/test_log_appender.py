@@ -1,0 +1,35 @@
+"""Native rotating app.log appender (csrc/log_appender.cpp) behind the node's file log handler."""
+import logging
+import os
+
+from upow_amd.ops.native import lib
+from upow_amd.utils.logger import NativeFileHandler
+
+
+def test_appender_rotates_between_records(tmp_path):
+    path = str(tmp_path / 'app.log')
+    app = lib().LogAppender(path, 1000, 3)
+    lines = [f'line {i:04d} ' + 'x' * 80 + '\n' for i in range(60)]  # 91 bytes each: ~10 lines per file
+    for ln in lines:
+        app.write(ln)
+    app.flush()
+    assert app.rotations >= 3
+    app.close()
+    files = [path + s for s in ('.3', '.2', '.1', '')]
+    kept = ''.join(open(f).read() for f in files if os.path.exists(f))
+    assert not os.path.exists(path + '.4')  # backups beyond the count are dropped
+    assert kept.endswith(''.join(lines[-5:]))  # newest records last, whole lines, in order
+    for f in files:
+        if os.path.exists(f):
+            data = open(f).read()
+            assert len(data) < 1000 + 91 and data.endswith('\n')
+
+
+def test_native_handler_format_matches_formatter(tmp_path):
+    fmt = logging.Formatter('%(asctime)s - %(filename)s - %(levelname)s - %(message)s')
+    h = NativeFileHandler(lib().LogAppender(str(tmp_path / 'a.log'), 1 << 20, 2), fmt)
+    rec = logging.LogRecord('upow', logging.INFO, '/x/manager.py', 10, 'Added %d transactions', (5,), None)
+    h.emit(rec)
+    h.flush()
+    h.close()
+    assert open(tmp_path / 'a.log').read() == fmt.format(rec) + '\n'

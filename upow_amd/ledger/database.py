@@ -2008,17 +2008,22 @@ class Database:
             tg = perf_counter()
             _, blob, off = out_addr_spec
             off = np.frombuffer(off, dtype=np.int64) if isinstance(off, (bytes, bytearray)) else np.asarray(off, np.int64)
-            with self.gov.lock:
-                # governance/stake outputs in, governance and staked spends out (csrc/gov_index.cpp apply_block)
-                self.gov.store.apply_block(
-                    np.ascontiguousarray(gov['out_type'], dtype=np.uint8), np.ascontiguousarray(tx_cols[0][1]),
+            # governance/stake outputs in, governance and staked spends out (csrc/gov_index.cpp apply_block),
+            # on the governance apply thread: the block is committed, and every reader of the index (the next
+            # block's rule check included) waits for this update through the index lock
+            args = (np.ascontiguousarray(gov['out_type'], dtype=np.uint8), np.ascontiguousarray(tx_cols[0][1]),
                     np.ascontiguousarray(gov['out_tx'], dtype=np.int32), np.ascontiguousarray(gov['out_start'], np.int32),
                     np.ascontiguousarray(out_amount, dtype=np.uint64), np.ascontiguousarray(out_addr, dtype=np.uint8),
-                    np.ascontiguousarray(out_len, dtype=np.uint8), bytes(blob), np.ascontiguousarray(off),
+                    np.ascontiguousarray(out_len, dtype=np.uint8), blob, np.ascontiguousarray(off),
                     np.ascontiguousarray(gov['in_start'], np.int32), np.ascontiguousarray(spent_payload).view(np.uint8),
                     in_keys, np.ascontiguousarray(gov['in_tag'], dtype=np.uint8), gov['in_str'][0],
                     np.frombuffer(gov['in_str'][1], dtype=np.int64), n, int(b['timestamp']))
-                self.gov.version += 1
+            g = self.gov
+
+            def gov_apply():
+                g.store.apply_block(*args)
+                g.version += 1
+            g.defer(gov_apply)
             self.last_gov_index_s = perf_counter() - tg
         elif self.gov is not None and n_in:
             hit = self._stake_spent(spent, spent_payload)

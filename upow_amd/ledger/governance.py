@@ -127,6 +127,40 @@ class _TableView:
         return self.gov.store.remove_keys(self.tid, _k36(key)) > 0
 
 
+class _GovLock:
+    """The index lock, aware of a deferred block apply (:meth:`GovernanceIndex.defer`): every acquirer
+    outside the apply thread first waits for the last block's apply to finish (re-raising its error), so
+    no reader ever sees the index between a block's commit and its governance update."""
+
+    def __init__(self):
+        self._lock = threading.RLock()
+        self.job = None  # Future of the last deferred apply
+        self.worker_ident = None
+
+    def settle(self):
+        job = self.job
+        if job is not None and threading.get_ident() != self.worker_ident:
+            job.result()
+
+    def acquire(self, blocking: bool = True, timeout: float = -1) -> bool:
+        self.settle()
+        return self._lock.acquire(blocking, timeout)
+
+    def release(self):
+        self._lock.release()
+
+    def __enter__(self):
+        self.acquire()
+        return self
+
+    def __exit__(self, *exc):
+        self._lock.release()
+        return False
+
+
+_APPLY_POOL = None
+
+
 def _locked(fn):
     """Serialise index access: block application (ledger thread) and API queries (HTTP loop) share it."""
     @functools.wraps(fn)
@@ -140,7 +174,7 @@ class GovernanceIndex:
     def __init__(self, db):
         from ..ops.native import lib
         self.db = db
-        self.lock = threading.RLock()
+        self.lock = _GovLock()
         self.store = lib().GovStore()
         self.tables: Dict[str, _TableView] = {t: _TableView(self, t) for t in (*GOV_TABLES, STAKE)}
         self.version = 0
@@ -149,6 +183,22 @@ class GovernanceIndex:
         self._pending = None  # (mempool version, pending-spent set, pending stake per address, pending votes)
         self._parsed: Dict[str, tuple] = {}  # pending tx hash -> (stake outputs, is a delegate vote)
         self._blob = None  # (overlay, pending-spent keys as 36-byte records)
+
+    def defer(self, fn):
+        """Run ``fn`` (a block's index update) on the governance apply thread, under the index lock. The
+        block path moves on at once (the next block's decode, UTXO pass and signatures do not read the
+        index); every later acquirer of the lock waits for it first."""
+        global _APPLY_POOL
+        from concurrent.futures import ThreadPoolExecutor
+        if _APPLY_POOL is None:
+            _APPLY_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix='upow-gov-apply')
+        self.lock.settle()  # one deferred apply at a time, in block order
+
+        def run():
+            self.lock.worker_ident = threading.get_ident()
+            with self.lock._lock:
+                fn()
+        self.lock.job = _APPLY_POOL.submit(run)
 
     # ------------------------------------------------------------------ maintenance
     def _rows_sql(self, table: str, where: str = '', args: tuple = ()):

@@ -113,11 +113,22 @@ async def _loop_lag_monitor(tick: float = 0.001, report_ms: float = 2.0):
         with open(os.environ['UPOW_TRACE_FILE'] + '.stacks', 'a') as out:
             while not stop.wait(0.002):
                 if _time.perf_counter() - beat[0] > 0.005:
-                    fr = sys._current_frames().get(loop_tid)
+                    frames = sys._current_frames()
+                    fr = frames.get(loop_tid)
                     if fr is not None:
                         st = traceback.extract_stack(fr)[-6:]
+                        # the other Python threads' innermost frames at the same instant: a loop thread
+                        # parked in an I/O call is usually waiting for the GIL that one of these holds
+                        names = {t.ident: t.name for t in threading.enumerate()}
+                        others = {}
+                        for tid, f in frames.items():
+                            if tid in (loop_tid, threading.get_ident()):
+                                continue
+                            others[names.get(tid, str(tid))] = \
+                                f'{os.path.basename(f.f_code.co_filename)}:{f.f_lineno}:{f.f_code.co_name}'
                         out.write(json.dumps({'t': round(_time.time(), 4),
-                                              'stack': [f'{os.path.basename(x.filename)}:{x.lineno}:{x.name}' for x in st]}) + '\n')
+                                              'stack': [f'{os.path.basename(x.filename)}:{x.lineno}:{x.name}' for x in st],
+                                              'others': others}) + '\n')
     threading.Thread(target=watchdog, name='upow-loop-watchdog', daemon=True).start()
     import gc
     gc_t0 = {}

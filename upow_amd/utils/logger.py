@@ -43,8 +43,12 @@ def _configure():
             return
         fh.setLevel(logging.DEBUG)
         fh.setFormatter(fmt)
-        # formatting and file I/O on a listener thread: /push_tx logs several lines per request, and the
-        # event loop should only pay for queueing the record
+        native = _native_handler(fh.baseFilename, fmt)
+        if native is not None:
+            fh.close()
+            logger.addHandler(native)
+            return
+        # no native library: formatting and file I/O on a listener thread
         import atexit
         import queue
         from logging.handlers import QueueHandler, QueueListener
@@ -53,6 +57,58 @@ def _configure():
         listener.start()
         atexit.register(listener.stop)
         logger.addHandler(QueueHandler(q))
+
+
+class NativeFileHandler(logging.Handler):
+    """The rotating app.log through csrc/log_appender.cpp: the record is rendered here in the format above
+    (the timestamp text cached per second) and handed to a C++ writer thread that batches, writes and
+    rotates. /push_tx logs a line per request; no Python thread has to format or write them, so the HTTP
+    loop does not lose the GIL to a logging thread at a four-digit tx rate."""
+
+    def __init__(self, appender, fmt: logging.Formatter):
+        super().__init__(logging.DEBUG)
+        self.app = appender
+        self.setFormatter(fmt)
+        self._sec = None
+        self._stamp = ''
+
+    def emit(self, record):
+        try:
+            if record.exc_info or record.exc_text or record.stack_info:
+                line = self.format(record)
+            else:
+                sec = int(record.created)
+                if sec != self._sec:
+                    import time
+                    self._sec, self._stamp = sec, time.strftime('%Y-%m-%d %H:%M:%S', time.localtime(sec))
+                line = (f'{self._stamp},{int(record.msecs):03d} - {record.filename} - {record.levelname} - '
+                        f'{record.getMessage()}')
+            self.app.write(line + '\n')
+        except Exception:
+            self.handleError(record)
+
+    def flush(self):
+        self.app.flush()
+
+    def close(self):
+        try:
+            self.app.close()
+        finally:
+            super().close()
+
+
+def _native_handler(path: str, fmt: logging.Formatter):
+    if os.environ.get('UPOW_NATIVE_LOG', '1') == '0':
+        return None
+    try:
+        from ..ops.native import lib
+        app = lib().LogAppender(path, 5 * 1024 * 1024, 100)
+    except Exception:
+        return None
+    import atexit
+    h = NativeFileHandler(app, fmt)
+    atexit.register(h.close)
+    return h
 
 
 def get_logger(name: str = 'upow') -> logging.Logger:
