@@ -316,13 +316,20 @@ def main():
                 stalls.append((r['t'] - r['ms'] / 1000.0, r['t'], r['ms']))
     in_blk = [s for s in stalls if overlaps(s[0], s[1])]
     stack_counts = {}
+    other_counts = {}  # what the node's other Python threads were executing during loop stalls
     if os.path.exists(trace + '.stacks'):
         for ln in open(trace + '.stacks'):
             r = json.loads(ln)
             if t0 <= r['t'] <= t_push_end:
                 key = ' < '.join(reversed(r['stack'][-3:]))
                 stack_counts[key] = stack_counts.get(key, 0) + 1
+                for name, where in r.get('others', {}).items():
+                    if any(w in where for w in ('wait', 'select', 'sleep', '_worker', 'get')):
+                        continue  # parked threads
+                    k2 = f'{name} @ {where}'
+                    other_counts[k2] = other_counts.get(k2, 0) + 1
     top_stacks = sorted(stack_counts.items(), key=lambda kv: -kv[1])[:12]
+    top_others = sorted(other_counts.items(), key=lambda kv: -kv[1])[:12]
     gcs = []
     if os.path.exists(trace + '.gc'):
         for ln in open(trace + '.gc'):
@@ -361,6 +368,7 @@ def main():
                                  'n_during_block_apply': len(in_blk),
                                  'total_ms_during_block_apply': round(sum(s[2] for s in in_blk), 1)},
         'loop_stall_samples_2ms': dict(top_stacks),
+        'loop_stall_other_threads': dict(top_others),
         'gc_over_2ms': {'n': len(gcs), 'total_ms': round(sum(g['ms'] for g in gcs), 1),
                         'max_ms': round(max((g['ms'] for g in gcs), default=0), 1),
                         'gen2': sum(1 for g in gcs if g.get('gen') == 2)},

@@ -37,10 +37,6 @@ def main():
     st = verify_dp.verify_records_dp(ctx, b''.join(recs), device=dev)
     assert list(st) == want
     assert verify_dp.verify_shard_first_failure(ctx, b''.join(recs), device=dev) == 5
-    assert verify_dp.gather_mempool(ctx, ['ab%d' % ctx.rank, 'cd']) == ['ab0', 'cd'] + ['ab%d' % r for r in
-                                                                                     range(1, ctx.world)]
-    b, t = verify_dp.broadcast_block(ctx, 'ff' * 108 if ctx.rank == 0 else None, ['aa', 'bb'] if ctx.rank == 0 else None)
-    assert b == 'ff' * 108 and t == ['aa', 'bb']
     # the multi-GPU node's op frame (parallel/cluster.py): JSON header + raw tx bytes, over RCCL
     from upow_amd.parallel import cluster
     c = cluster.Cluster(ctx)

@@ -121,8 +121,17 @@ def _replica_worker(rank, world, port, tmp, q):
         assert list(st) == [1] * 7 + [0, 1], list(st)
         assert verify_dp.verify_shard_first_failure(ctx, b''.join(recs)) == 7
         assert verify_dp.verify_shard_first_failure(ctx, b''.join(recs[:7])) == -1
-        # mempool all-gather
-        assert verify_dp.gather_mempool(ctx, ['aa', 'bb'] if rank == 0 else ['bb', 'cc']) == ['aa', 'bb', 'cc']
+        async def replicate(content, txs):
+            # the harness's replication: rank 0's block to every rank, each applies it with the
+            # signature batch sharded across the ranks, and all verdicts must agree
+            import json as js
+            from upow_amd.ledger import manager
+            raw = ctx.broadcast_bytes(js.dumps({'b': content, 't': txs or []}).encode() if rank == 0 else None,
+                                      src=0, max_len=0)
+            obj = js.loads(raw.decode())
+            ok = await manager.create_block(obj['b'], [await Transaction.from_hex(h) for h in obj['t']])
+            assert ctx.allreduce_sum(1 if ok else 0) in (0, ctx.world)
+            return ok
 
         async def go():
             db = await Database.create(path=os.path.join(tmp, f'r{rank}.sqlite3'), utxo_backend='host')
@@ -132,7 +141,7 @@ def _replica_worker(rank, world, port, tmp, q):
             base = 1_700_000_000
             for b in range(3):
                 content = await devnet.mine_header(addr, [], ts=base + 60 * b, device='cpu') if rank == 0 else None
-                assert await verify_dp.replicate_block(ctx, content, [])
+                assert await replicate(content, [])
             txs = []
             if rank == 0:
                 for j in range(3):
@@ -148,12 +157,12 @@ def _replica_worker(rank, world, port, tmp, q):
                 bad = txs[:-1] + [forged]
                 bad_hex = [t.hex() for t in bad]
                 content = await devnet.mine_header(addr, bad, ts=base + 60 * 3, device='cpu')
-            assert not await verify_dp.replicate_block(ctx, content if rank == 0 else None, bad_hex)
+            assert not await replicate(content if rank == 0 else None, bad_hex)
             good = None
             if rank == 0:
                 good = [t.hex() for t in txs]
                 content = await devnet.mine_header(addr, txs, ts=base + 60 * 3, device='cpu')
-            assert await verify_dp.replicate_block(ctx, content if rank == 0 else None, good)
+            assert await replicate(content if rank == 0 else None, good)
             h = await db.get_unspent_outputs_hash()
             hs = ctx.all_gather_bytes(h.encode())
             assert len(set(hs)) == 1 and (await db.get_next_block_id()) == 5
