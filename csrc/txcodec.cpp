@@ -29,6 +29,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <optional>
 #include <string>
 #include <string_view>
 #include <thread>
@@ -518,6 +519,26 @@ private:
     std::unique_ptr<DecWorkspace> ws_;
 };
 
+// The block's merkle root, computed on its own thread from the decode workspace, which the job holds
+// until the root has been taken: the caller checks it against the header when it needs the verdict
+// (after the UTXO pass and the signatures), not when the decode returns.
+struct MerkleJob {
+    std::optional<DecWorkspaceLease> lease;
+    std::thread th;
+    std::string root;
+    ~MerkleJob() {
+        if (th.joinable()) th.join();
+    }
+    std::string result() {
+        if (th.joinable()) {
+            py::gil_scoped_release rel;
+            th.join();
+        }
+        lease.reset();  // the workspace goes back to the pool
+        return root;
+    }
+};
+
 // decode_block_txs(hexes, threads) -> dict (see module docstring of upow_amd/ledger/fastpath.py)
 static py::dict decode_block_txs(py::list hexes, int threads) {
     const int64_t n = int64_t(hexes.size());
@@ -535,8 +556,9 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
         srcp[i] = p;
         srcl[i] = size_t(sz);
     }
-    DecWorkspaceLease ws;
-    std::vector<DecTx>& txs = ws.get().txs;
+    auto job = std::make_shared<MerkleJob>();
+    job->lease.emplace();
+    std::vector<DecTx>& txs = job->lease->get().txs;
     if (txs.size() < N) txs.resize(N);
     const bool prof = std::getenv("UPOW_TXCODEC_PROFILE") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
@@ -590,15 +612,12 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
 
     const size_t NI = static_cast<size_t>(n_in), NO = static_cast<size_t>(n_out), NS = static_cast<size_t>(n_sig);
     // The merkle root (a sort of the canonical bytes, then one SHA-256 over the txids) runs on its own
-    // thread while the pool fills the flat columns below: both only read `txs`.
-    std::string merkle;
-    std::thread merkle_thread([&] { merkle = merkle_of(txs, N); });
-    struct Joiner {  // an exception below must not destroy a joinable thread
-        std::thread& t;
-        ~Joiner() {
-            if (t.joinable()) t.join();
-        }
-    } merkle_joiner{merkle_thread};
+    // thread while the pool fills the flat columns below (both only read `txs`) and beyond: the job owns
+    // the thread and the workspace (an exception below joins it in the job's destructor).
+    {
+        MerkleJob* j = job.get();
+        j->th = std::thread([j, &txs, N] { j->root = merkle_of(txs, N); });
+    }
     // Every column is filled in place inside its final Python bytes object (allocated here, with the GIL;
     // written by the pool without it): no staging vector and no copy on the way out.
     auto pyb = [](size_t len, char*& p) {
@@ -714,17 +733,11 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
     auto tB = std::chrono::steady_clock::now();
     d["hex"] = canon_hex;
     auto t2 = std::chrono::steady_clock::now();
-    {
-        py::gil_scoped_release rel;
-        merkle_thread.join();
-    }
-    d["merkle"] = merkle;
+    d["merkle_job"] = job;
     if (prof) {
-        auto t3 = std::chrono::steady_clock::now();
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        std::fprintf(stderr, "[txcodec] fill %.2f canonhex %.2f bytes %.2f\n", ms(t1,tA), ms(tA,tB), ms(tB,t2));
-        std::fprintf(stderr, "[txcodec] decode %.2f ms, columns + python objects %.2f ms, merkle wait %.2f ms\n",
-                     ms(t0, t1), ms(t1, t2), ms(t2, t3));
+        std::fprintf(stderr, "[txcodec] decode %.2f ms, columns %.2f ms (fill %.2f, hex list %.2f)\n", ms(t0, t1),
+                     ms(t1, t2), ms(t1, tA), ms(tA, tB));
     }
     return d;
 }
@@ -1104,6 +1117,8 @@ static py::tuple block_signer_records(py::buffer pay_addr_b, py::buffer pay_len_
 }
 
 void register_txcodec(py::module_& m) {
+    py::class_<MerkleJob, std::shared_ptr<MerkleJob>>(m, "MerkleJob")
+        .def("result", &MerkleJob::result, "the block's merkle root (hex); waits for the merkle thread");
     m.def("fee_strings", &fee_strings);
     m.def("unique_rows", &unique_rows, py::arg("buf"), py::arg("width"),
           "(unique rows in first-seen order, inverse int32) of an n x width byte matrix");

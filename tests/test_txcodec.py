@@ -68,7 +68,7 @@ def _check_fast(d, hexes):
             assert bytes(rec[:32]).hex() == i.tx_hash and int(rec[32]) == i.index
             sig = d['sigs'][64 * i32('in_sig')[in_start[k] + j]:][:64]
             assert (int.from_bytes(sig[:32], 'little'), int.from_bytes(sig[32:], 'little')) == i.signed
-    assert d['merkle'] == get_transactions_merkle_tree([Transaction.parse(h)[0] for h in hexes])
+    assert d['merkle_job'].result() == get_transactions_merkle_tree([Transaction.parse(h)[0] for h in hexes])
 
 
 def test_decode_matches_python_model(L):

@@ -223,8 +223,6 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     n = int(d['n'])
     if int(_i32(d, 'hex_len').sum()) > MAX_BLOCK_SIZE_HEX:
         return None
-    if d['merkle'] != merkle_tree:
-        return None
     t1 = perf_counter()
     roctx.push('block:utxo_pass')
 
@@ -318,6 +316,9 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         st2 = validate._verify(np.ascontiguousarray(rr).tobytes(), None)
         status[retry] = np.where(st2 == op.VALID, op.VALID, status[retry])
     if np.any(status != op.VALID):
+        return None
+    # the merkle root was computed on the codec's thread while the stages above ran
+    if d['merkle_job'].result() != merkle_tree:
         return None
     t4 = perf_counter()
     roctx.pop()
