@@ -287,6 +287,16 @@ def main():
         except subprocess.TimeoutExpired:
             p.kill()
     miner_log.close()
+    prof = os.path.join(data, 'node.prof')
+    if a.out and os.path.exists(prof):  # UPOW_SOAK_PROFILE=1: the event-loop thread's cProfile, top entries
+        import io
+        import pstats
+        buf = io.StringIO()
+        st = pstats.Stats(prof, stream=buf)
+        st.sort_stats('tottime').print_stats(45)
+        st.sort_stats('cumulative').print_stats(45)
+        with open(os.path.splitext(a.out)[0] + '_loop_profile.txt', 'w') as f:
+            f.write(buf.getvalue())
     included = {h: included[h] for h in pushed if h in included}
     lat = sorted(included[h] - pushed[h] for h in included)
     rates = [float(x) for x in re.findall(r'([0-9.]+) MH/s', open(os.path.join(data, 'miner.log')).read())]
