@@ -89,7 +89,14 @@ def main():
     ap.add_argument('--fanout2', type=int, default=200, help='each of those -> M outputs (pool = N*M UTXOs)')
     ap.add_argument('--threads', type=int, default=1, help='concurrent /push_tx clients (per process)')
     ap.add_argument('--procs', type=int, default=1, help='client processes pushing txs')
+    ap.add_argument('--client-cpus', default=None,
+                    help="CPU list for the miner and the pushing clients (e.g. '16-47'), away from the node's")
     a = ap.parse_args()
+    client_pin = None
+    if a.client_cpus:
+        from upow_amd.node.__main__ import parse_cpus
+        cpus = set(parse_cpus(a.client_cpus)) & os.sched_getaffinity(0)
+        client_pin = (lambda: os.sched_setaffinity(0, cpus)) if cpus else None
 
     from upow_amd.models.transaction import Transaction, TransactionInput, TransactionOutput
     from upow_amd.ops import p256 as op
@@ -125,6 +132,7 @@ def main():
     from upow_amd.ops.native import gpu_available
     chunk = [] if gpu_available() else ['--chunk', '65536', '--device', 'cpu']
     miner = subprocess.Popen([sys.executable, '-m', 'upow_amd.miner', addr, '1', url + '/', '--refresh', '10', *chunk],
+                             preexec_fn=client_pin,
                              env=env, cwd=ROOT, stdout=miner_log, stderr=subprocess.STDOUT)
     t_start = time.time()
     phase = ['setup']
@@ -258,7 +266,8 @@ def main():
             with open(src, 'w') as f:
                 f.write('\n'.join(f'{k} {hexes[k]}' for k in range(pidx, len(hexes), a.procs)))
             kids.append((subprocess.Popen([sys.executable, '-c', _PUSHER, url, src, str(t0), str(a.rate),
-                                           str(a.seconds), str(a.threads)], env=env, cwd=ROOT), src + '.out'))
+                                           str(a.seconds), str(a.threads)], env=env, cwd=ROOT,
+                                          preexec_fn=client_pin), src + '.out'))
         for proc, out in kids:
             proc.wait()
             for ln in open(out):

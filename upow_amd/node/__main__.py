@@ -4,6 +4,43 @@ import argparse
 import os
 
 
+def parse_cpus(spec: str):
+    """'0-15,32,40-43' -> sorted CPU list."""
+    out = set()
+    for part in spec.split(','):
+        part = part.strip()
+        if not part:
+            continue
+        if '-' in part:
+            lo, hi = part.split('-', 1)
+            out.update(range(int(lo), int(hi) + 1))
+        else:
+            out.add(int(part))
+    return sorted(out)
+
+
+def pin_cpus(spec: str):
+    """Process CPU affinity before any thread starts (``UPOW_CPU_AFFINITY``): 'off' (default), an explicit
+    CPU list, or 'auto' = as many CPUs as the cgroup CPU quota grants, taken from the current affinity set.
+    A node whose quota is far below the host's core count otherwise spreads its threads over every core,
+    and CFS bandwidth control hands quota to each core in slices: a burst then exhausts the period's quota
+    and freezes every thread of the node (the HTTP loop included) until the next period."""
+    if not spec or spec == 'off':
+        return None
+    cur = sorted(os.sched_getaffinity(0))
+    if spec == 'auto':
+        from ..ledger.fastpath import cpu_budget
+        q = cpu_budget()
+        if q >= len(cur):
+            return None
+        want = cur[:q]
+    else:
+        want = [c for c in parse_cpus(spec) if c in set(cur)]
+    if want:
+        os.sched_setaffinity(0, want)
+    return want
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--host', default='0.0.0.0')
@@ -15,6 +52,7 @@ def main(argv=None):
     ap.add_argument('--cluster', action='store_true',
                     help='multi-GPU node under torchrun: rank 0 serves the API, other ranks are HBM replicas')
     a = ap.parse_args(argv)
+    pin_cpus(os.environ.get('UPOW_CPU_AFFINITY', 'off'))
     if a.data:
         os.environ['UPOW_DATA_DIR'] = a.data
     if a.db:
