@@ -79,9 +79,12 @@ def start() -> Optional[LedgerWorker]:
     with _lock:
         if _worker is None and enabled():
             # the GIL changes hands every switch interval when both threads run Python: at CPython's
-            # 5 ms default a request arriving during a block's Python stages waits up to 5 ms per turn
+            # 5 ms default a request arriving during a block's Python stages waits up to 5 ms per turn, and
+            # the HTTP loop gives the GIL away at every socket call (recv, send, epoll), so each request
+            # can pay that wait several times. 0.25 ms: soaks at 1,200 tx/s measured lower push latency
+            # during block apply than at 1 ms, with no slower block apply (docs/PERF.md §3)
             import sys
-            sys.setswitchinterval(float(os.environ.get('UPOW_SWITCH_INTERVAL_MS', '1')) / 1000.0)
+            sys.setswitchinterval(float(os.environ.get('UPOW_SWITCH_INTERVAL_MS', '0.25')) / 1000.0)
             _worker = LedgerWorker()
             logger.info('ledger worker thread started')
         return _worker
