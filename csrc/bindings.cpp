@@ -244,6 +244,16 @@ PYBIND11_MODULE(_native, m) {
         { py::gil_scoped_release rel; d = utxo_set_hash(h, tag, &n); }
         return py::make_tuple(py::bytes(reinterpret_cast<const char*>(d.data()), d.size()), n);
     });
+    m.def("utxo_k12_snapshot", [](int64_t h, uint32_t tag) {
+        py::gil_scoped_release rel;
+        return utxo_k12_snapshot(h, tag);
+    });
+    m.def("utxo_k12_digest", [](int64_t id) {
+        uint64_t n = 0;
+        std::vector<uint8_t> d;
+        { py::gil_scoped_release rel; d = utxo_k12_digest(id, &n); }
+        return py::make_tuple(py::bytes(reinterpret_cast<const char*>(d.data()), d.size()), n);
+    });
     m.def("utxo_set_message", [](int64_t h, uint32_t tag) {
         auto* v = new std::vector<uint8_t>();
         uint64_t n = 0;

@@ -80,6 +80,8 @@ BlockInputsResult utxo_block_inputs(int64_t h, const uint8_t* keys, int64_t n_in
 std::vector<uint8_t> utxo_set_hash(int64_t h, uint32_t tag, uint64_t* count_out);
 // the (txid || index byte) message of table `tag` sorted by (txid, index): K12 without its hash tail
 std::vector<uint8_t> utxo_set_message(int64_t h, uint32_t tag, uint64_t* count_out);
+int64_t utxo_k12_snapshot(int64_t h, uint32_t tag);
+std::vector<uint8_t> utxo_k12_digest(int64_t id, uint64_t* count_out);
 
 // ---------------------------------------------------------------- base58
 std::string b58encode(const uint8_t* data, size_t n);

@@ -41,7 +41,9 @@ inline void node_device_enter() {
     if (cur != want) stream_check(hipSetDevice(want), "hipSetDevice");
 }
 
-enum class StreamRole { Node = 0, Miner = 1 };
+// Aux: background node work that must not sit in front of a block's kernels on the node stream (the
+// K12 UTXO-set digest's sort and gather), at the least priority
+enum class StreamRole { Node = 0, Miner = 1, Aux = 2 };
 
 // set once this process has issued node work (UTXO passes, ECDSA, ...): a miner in the same process then
 // keeps its dispatches short (csrc/pow_search.hip)
@@ -53,7 +55,7 @@ inline std::atomic<bool>& node_stream_live() {
 inline hipStream_t role_stream(StreamRole role) {
     constexpr int kMaxDev = 64;
     static std::mutex mu;
-    static hipStream_t streams[2][kMaxDev] = {};
+    static hipStream_t streams[3][kMaxDev] = {};
     int dev = 0;
     stream_check(hipGetDevice(&dev), "hipGetDevice");
     if (dev < 0 || dev >= kMaxDev) throw std::runtime_error("device ordinal out of range");
@@ -76,6 +78,7 @@ inline hipStream_t role_stream(StreamRole role) {
 
 inline hipStream_t node_stream() { return role_stream(StreamRole::Node); }
 inline hipStream_t miner_stream() { return role_stream(StreamRole::Miner); }
+inline hipStream_t aux_stream() { return role_stream(StreamRole::Aux); }
 
 inline void node_h2d(void* dst, const void* src, size_t n, const char* what = "h2d") {
     if (n) stream_check(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, node_stream()), what);

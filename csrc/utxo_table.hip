@@ -19,8 +19,10 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/device/device_radix_sort.hpp>
 
+#include <algorithm>
 #include <cstddef>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -714,6 +716,120 @@ std::vector<uint8_t> utxo_set_message(int64_t h, uint32_t tag, uint64_t* count_o
         node_d2h(msg.data(), d_msg.p, msg.size(), "d2h message");
     }
     return msg;
+}
+
+// ---- K12 off the block path: the block thread takes a snapshot (one compaction launch on the node stream,
+// so it sees exactly this block's table; no host sync), a worker thread turns it into the digest (sort and
+// gather on the aux stream, chunked D2H into pinned buffers overlapped with the host SHA-256). The next
+// block's kernels never queue behind the sort, and the 33-byte-per-UTXO message never becomes one host
+// allocation (165 MB at 5 M UTXOs).
+struct K12Snap {
+    int device = 0;
+    uint32_t cap = 0;
+    PooledBuf<UtxoKeyRec> recs;
+    PooledBuf<uint32_t> count;
+    hipEvent_t ready = nullptr;
+    K12Snap(uint32_t c) : cap(c), recs(c), count(1) {}
+};
+static std::mutex g_k12_mu;
+static std::unordered_map<int64_t, std::unique_ptr<K12Snap>> g_k12;
+static int64_t g_k12_next = 1;
+
+int64_t utxo_k12_snapshot(int64_t h, uint32_t tag) {
+    std::unique_ptr<K12Snap> s;
+    {
+        std::lock_guard<std::mutex> lk(g_ut_mu);
+        UtxoTableDev& t = table(h);
+        s = std::make_unique<K12Snap>(t.cap);
+        s->device = t.device;
+        node_memset(s->count.p, 0, sizeof(uint32_t), "memset k12 count");
+        hipLaunchKernelGGL(set_compact_kernel, dim3((t.cap + 255) / 256), dim3(256), 0, node_stream(), t.tab, t.cap,
+                           tag, s->recs.p, s->count.p);
+        uck(hipGetLastError(), "set_compact_kernel");
+        uck(hipEventCreateWithFlags(&s->ready, hipEventDisableTiming), "hipEventCreate");
+        uck(hipEventRecord(s->ready, node_stream()), "hipEventRecord");
+    }
+    std::lock_guard<std::mutex> g(g_k12_mu);
+    const int64_t id = g_k12_next++;
+    g_k12[id] = std::move(s);
+    return id;
+}
+
+std::vector<uint8_t> utxo_k12_digest(int64_t id, uint64_t* count_out) {
+    std::unique_ptr<K12Snap> s;
+    {
+        std::lock_guard<std::mutex> g(g_k12_mu);
+        auto it = g_k12.find(id);
+        if (it == g_k12.end()) throw std::invalid_argument("bad K12 snapshot id");
+        s = std::move(it->second);
+        g_k12.erase(it);
+    }
+    uck(hipSetDevice(s->device), "hipSetDevice");
+    hipStream_t st = aux_stream();
+    uck(hipStreamWaitEvent(st, s->ready, 0), "hipStreamWaitEvent");
+    uint32_t n = 0;
+    uck(hipMemcpyAsync(&n, s->count.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st), "d2h k12 count");
+    uck(hipStreamSynchronize(st), "k12 count sync");
+    if (count_out) *count_out = n;
+    HostSha256 sha;
+    if (n) {
+        PooledBuf<uint32_t> perm_a(n), perm_b(n);
+        PooledBuf<uint64_t> col_a(n), col_b(n);
+        const dim3 g((n + 255) / 256);
+        hipLaunchKernelGGL(iota_kernel, g, dim3(256), 0, st, perm_a.p, n);
+        size_t temp_bytes = 0;
+        uck(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, col_a.p, col_b.p, perm_a.p, perm_b.p, n, 0, 64, st),
+            "radix sort sizing");
+        PooledBuf<uint8_t> temp(temp_bytes);
+        uint32_t* pa = perm_a.p;
+        uint32_t* pb = perm_b.p;
+        for (int c = 0; c <= 4; ++c) {  // least significant column first; radix sort is stable
+            hipLaunchKernelGGL(sort_column_kernel, g, dim3(256), 0, st, s->recs.p, pa, n, c, col_a.p);
+            uck(hipGetLastError(), "sort_column_kernel");
+            uck(hipcub::DeviceRadixSort::SortPairs(temp.p, temp_bytes, col_a.p, col_b.p, pa, pb, n, 0, c == 0 ? 8 : 64,
+                                                   st),
+                "radix sort");
+            std::swap(pa, pb);
+        }
+        PooledBuf<uint8_t> d_msg(size_t(n) * 33);
+        hipLaunchKernelGGL(set_message_kernel, g, dim3(256), 0, st, s->recs.p, pa, n, d_msg.p);
+        uck(hipGetLastError(), "set_message_kernel");
+        // two pinned staging buffers: chunk k+1 is copied while chunk k is hashed
+        constexpr size_t kChunk = size_t(16) << 20;
+        static uint8_t* pinned[2] = {nullptr, nullptr};
+        static std::mutex pin_mu;
+        std::lock_guard<std::mutex> pl(pin_mu);
+        for (auto& b : pinned)
+            if (!b) uck(hipHostMalloc(reinterpret_cast<void**>(&b), kChunk, hipHostMallocDefault), "hipHostMalloc");
+        hipEvent_t ev[2];
+        for (auto& e : ev) uck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        const size_t total = size_t(n) * 33;
+        auto issue = [&](size_t off, int b) {
+            const size_t len = std::min(kChunk, total - off);
+            uck(hipMemcpyAsync(pinned[b], d_msg.p + off, len, hipMemcpyDeviceToHost, st), "d2h k12 chunk");
+            uck(hipEventRecord(ev[b], st), "hipEventRecord");
+            return len;
+        };
+        size_t off = 0;
+        int b = 0;
+        size_t len = issue(0, 0);
+        while (len) {
+            uck(hipEventSynchronize(ev[b]), "k12 chunk sync");
+            const size_t next = off + len;
+            size_t next_len = 0;
+            if (next < total) next_len = issue(next, 1 - b);
+            sha.update(pinned[b], len);
+            off = next;
+            len = next_len;
+            b = 1 - b;
+        }
+        uck(hipStreamSynchronize(st), "k12 sync");  // the pooled buffers may be reused after this
+        for (auto& e : ev) (void)hipEventDestroy(e);
+    }
+    (void)hipEventDestroy(s->ready);
+    std::vector<uint8_t> digest(32);
+    sha.final(digest.data());
+    return digest;
 }
 
 // the sequential SHA-256 tail runs without the table lock: block application is not held up by it

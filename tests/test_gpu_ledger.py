@@ -40,6 +40,11 @@ def test_gpu_index_snapshot_roundtrip(gpu, tmp_path, monkeypatch):
         tx = await create_transaction(0x4242, address_of(0x99), '7')
         await devnet.mine_block(addr, [tx], ts=1_700_000_000 + 600)
         assert db.utxo.set_hash() == db.sql_unspent_outputs_hash() == await db.get_unspent_outputs_hash()
+        # K12 off the block path: the snapshot is this state even when the table changes before the digest
+        before = db.utxo.set_hash()
+        digest = db.utxo.k12_snapshot(0)
+        await devnet.mine_block(addr, ts=1_700_000_000 + 660)
+        assert digest() == before != db.utxo.set_hash()
         snapshot.save(db)
         n = len(db.utxo)
         db.close()

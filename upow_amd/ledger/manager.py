@@ -551,9 +551,9 @@ _K12_POOL = None
 
 async def _log_utxo_hash(database, block_no: int):
     """The K12 log line every 10 blocks (reference manager.py:740-741, 833-834). Computed only when the line
-    is emitted. The sorted outpoint message is taken at this block (under the index lock, on the device);
-    the sequential SHA-256 over it (165 MB at 5 M UTXOs) runs on a worker thread, so the next block does
-    not wait for it."""
+    is emitted. The block path only takes a snapshot of the UTXO set at this block (one compaction launch);
+    the sort, the message gather and the sequential SHA-256 over it (165 MB at 5 M UTXOs) run on a worker
+    thread and the GPU's aux stream, so the next block waits for none of it."""
     global _K12_POOL
     import logging
     if not logger.isEnabledFor(logging.INFO):
@@ -561,14 +561,12 @@ async def _log_utxo_hash(database, block_no: int):
     if os.environ.get('UPOW_UTXO_HASH_SQL', '0') == '1':
         logger.info(f'unspent_outputs_hash on block no. {block_no}: {await database.get_unspent_outputs_hash()}')
         return
-    import hashlib
     from concurrent.futures import ThreadPoolExecutor
     from .utxo import TAG_BY_TABLE
-    msg = database.utxo.set_message(TAG_BY_TABLE['unspent_outputs'])
+    digest = database.utxo.k12_snapshot(TAG_BY_TABLE['unspent_outputs'])
     if _K12_POOL is None:
         _K12_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix='upow-k12')
-    _K12_POOL.submit(lambda: logger.info(f'unspent_outputs_hash on block no. {block_no}: '
-                                         f'{hashlib.sha256(msg).hexdigest()}'))
+    _K12_POOL.submit(lambda: logger.info(f'unspent_outputs_hash on block no. {block_no}: {digest()}'))
 
 
 SNAPSHOT_EVERY = int(os.environ.get('UPOW_SNAPSHOT_EVERY', '1000'))

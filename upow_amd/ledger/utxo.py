@@ -458,6 +458,17 @@ class UtxoIndex:
         # records() is in canonical (txid, index) order; index byte = the reference's bytes([i])
         return np.ascontiguousarray(np.concatenate([recs[:, :32], recs[:, 32:33]], axis=1)).ravel()
 
+    def k12_snapshot(self, tag: int = 0):
+        """K12 at this block, computed later: returns a callable giving the hex digest (the same value
+        :meth:`set_hash` gives now). GPU backend: the snapshot is one compaction launch on the node stream;
+        the callable (meant for a worker thread) sorts, gathers and hashes on the aux stream."""
+        if isinstance(self.be, _GpuBackend):
+            L, sid = self.be.L, self.be.L.utxo_k12_snapshot(self.be.h, tag)
+            return lambda: L.utxo_k12_digest(sid)[0].hex()
+        msg = self.set_message(tag)
+        import hashlib
+        return lambda: hashlib.sha256(msg).hexdigest()
+
     def set_hash(self, tag: int = 0) -> str:
         """K12 from the index: SHA-256 over :meth:`set_message` — byte-identical to
         ``Database.get_unspent_outputs_hash`` (reference database.py:827-830). The sequential hash tail
