@@ -19,6 +19,7 @@
 #   prof     rocprofv3 --kernel-trace --stats over a short bench.py
 #   vprof    rocprofv3 --kernel-trace --stats over the verify bench
 #   tprof    rocprofv3 kernel + roctx marker trace of the verify bench, summarised by scripts/block_trace.py
+#   sprof    the same for the sync bench (200-tx blocks)
 #   soak3    three node soaks at 1,200 tx/s (scripts/node_soak.py)
 #   py:<script.py>  any extra python script under scripts/ (args after a comma: py:x.py,--a,1)
 # Every GPU step has its own time limit and the chain stops at the first failure.
@@ -116,6 +117,13 @@ for s in $STEPS; do
         --output-format csv -- python3 bench.py --mode verify --ledger /tmp/upow_bench_ledger --steps 8 --warmup 2 \
         > "$OUT/tprof.log" 2>&1 || { tail -20 "$OUT/tprof.log"; exit 1; }
       python scripts/block_trace.py "$OUT/tprof" --out "$OUT/block_trace.json" | head -60 ;;
+    sprof)
+      # the same timeline for the chain-sync replay (200-tx blocks through the decode-ahead pipeline)
+      rm -rf /tmp/upow_bench_ledger
+      UPOW_ROCTX=1 timeout -k 10 600 rocprofv3 --kernel-trace --marker-trace --stats -d "$OUT/sprof" -o sync \
+        --output-format csv -- python3 bench.py --mode sync --ledger /tmp/upow_bench_ledger --steps 300 --warmup 5 \
+        --txs 200 > "$OUT/sprof.log" 2>&1 || { tail -20 "$OUT/sprof.log"; exit 1; }
+      python scripts/block_trace.py "$OUT/sprof" --out "$OUT/sync_trace.json" | head -80 ;;
     soak3)
       # three consecutive node soaks at 1,200 tx/s (node + GPU miner CLI + 4 x 8 pushing clients)
       for i in 1 2 3; do
