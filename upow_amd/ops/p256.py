@@ -19,7 +19,10 @@ from ..utils.p256 import EcdsaError, Point
 from .native import gpu_available, lib
 
 VALID, INVALID, BAD_KEY, BAD_RANGE = 1, 0, 2, 3
-GPU_MIN_BATCH = int(os.environ.get('UPOW_P256_GPU_MIN_BATCH', '256'))
+# below this many signatures (or keys) a batch runs on host threads. The quad kernel's latency floor is
+# ~1.3 ms whatever the batch (one signature's double-scalar chain on four lanes); 16 host threads pass it
+# near 100 signatures on an MI355X box (a 200-tx sync block: 2.5 ms host vs 1.4 ms GPU, docs/PERF.md)
+GPU_MIN_BATCH = int(os.environ.get('UPOW_P256_GPU_MIN_BATCH', '64'))
 
 
 def _msg(m: Union[str, bytes]) -> bytes:
