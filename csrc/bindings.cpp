@@ -17,6 +17,7 @@ void register_txcodec(py::module_& m);  // txcodec.cpp
 void register_ledger_writer(py::module_& m);  // ledger_writer.cpp
 void register_gov_index(py::module_& m);  // gov_index.cpp
 void register_log_appender(py::module_& m);  // log_appender.cpp
+void register_http_wire(py::module_& m);  // http_wire.cpp
 }
 
 static PowJobHost make_job(py::bytes header, uint32_t tmask, uint32_t tword, uint32_t frac_shift,
@@ -54,6 +55,7 @@ PYBIND11_MODULE(_native, m) {
     register_ledger_writer(m);
     register_gov_index(m);
     register_log_appender(m);
+    register_http_wire(m);
 
     m.def("sha256", [](py::bytes msg) {
         std::string s = msg;

@@ -1,0 +1,177 @@
+"""The node's server protocol (node/http.py over csrc/http_wire.cpp) on a real socket: HTTP/1.1 framing,
+keep-alive, pipelining, chunked bodies both ways, Expect: 100-continue, bad requests, and WebSocket
+(handshake, text/binary, fragmentation, ping/pong, close) through the ASGI scopes."""
+import asyncio
+import base64
+import hashlib
+import os
+import socket
+import struct
+import threading
+import time
+
+import httpx
+import pytest
+import uvicorn
+from starlette.applications import Starlette
+from starlette.responses import JSONResponse, PlainTextResponse, StreamingResponse
+from starlette.routing import Route, WebSocketRoute
+
+from upow_amd.node.http import NodeHttpProtocol
+
+
+async def hello(request):
+    return JSONResponse({'ok': True, 'q': request.query_params.get('q'), 'path': request.url.path})
+
+
+async def echo(request):
+    body = await request.body()
+    return PlainTextResponse(body.decode(), headers={'x-len': str(len(body))})
+
+
+async def stream(request):
+    async def gen():
+        for k in range(3):
+            yield f'part{k};'.encode()
+    return StreamingResponse(gen())
+
+
+async def ws_echo(websocket):
+    await websocket.accept()
+    while True:
+        msg = await websocket.receive()
+        if msg['type'] == 'websocket.disconnect':
+            return
+        if msg.get('text') == 'bye':
+            await websocket.close(code=4000)
+            return
+        if msg.get('text') is not None:
+            await websocket.send_text('echo:' + msg['text'])
+        else:
+            await websocket.send_bytes(b'echo:' + msg['bytes'])
+
+
+app = Starlette(routes=[Route('/hello', hello), Route('/echo', echo, methods=['POST']), Route('/stream', stream),
+                        WebSocketRoute('/ws', ws_echo)])
+
+
+@pytest.fixture(scope='module')
+def server():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    cfg = uvicorn.Config(app, host='127.0.0.1', port=port, log_level='warning', http=NodeHttpProtocol,
+                         lifespan='off', timeout_keep_alive=5)
+    srv = uvicorn.Server(cfg)
+    t = threading.Thread(target=srv.run, daemon=True)
+    t.start()
+    for _ in range(200):
+        if srv.started:
+            break
+        time.sleep(0.02)
+    yield port
+    srv.should_exit = True
+    t.join(5)
+
+
+def _raw(port, data: bytes, timeout: float = 5.0) -> bytes:
+    """Send raw bytes and read until the server closes the connection (every caller's last request asks
+    for that, or is one the server must close on)."""
+    with socket.create_connection(('127.0.0.1', port), timeout=timeout) as c:
+        c.sendall(data)
+        out = b''
+        while True:
+            try:
+                chunk = c.recv(65536)
+            except socket.timeout:
+                break
+            if not chunk:
+                break
+            out += chunk
+        return out
+
+
+def test_keep_alive_requests_and_bodies(server):
+    with httpx.Client(base_url=f'http://127.0.0.1:{server}') as c:
+        for k in range(5):  # one pooled connection, several requests
+            r = c.get('/hello', params={'q': str(k)})
+            assert r.status_code == 200 and r.json() == {'ok': True, 'q': str(k), 'path': '/hello'}
+        body = os.urandom(300_000).hex()
+        r = c.post('/echo', content=body)
+        assert r.text == body and r.headers['x-len'] == str(len(body))
+        r = c.get('/stream')
+        assert r.text == 'part0;part1;part2;' and r.headers.get('transfer-encoding') == 'chunked'
+        assert c.get('/missing').status_code == 404
+        assert c.head('/hello').status_code in (200, 405)
+
+
+def test_pipelined_and_chunked_request(server):
+    req = (b'GET /hello?q=a HTTP/1.1\r\nHost: x\r\n\r\n'
+           b'POST /echo HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n4\r\nabcd\r\n3;ext=1\r\nefg\r\n0\r\n\r\n'
+           b'GET /hello?q=c HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n')
+    out = _raw(server, req)
+    parts = out.split(b'HTTP/1.1 ')[1:]
+    assert len(parts) == 3 and all(p.startswith(b'200') for p in parts)
+    assert b'"q":"a"' in parts[0] and parts[1].endswith(b'abcdefg') and b'"q":"c"' in parts[2]
+
+
+def test_expect_continue_and_bad_requests(server):
+    with socket.create_connection(('127.0.0.1', server), timeout=5) as c:
+        c.sendall(b'POST /echo HTTP/1.1\r\nHost: x\r\nContent-Length: 5\r\nExpect: 100-continue\r\n\r\n')
+        assert c.recv(100).startswith(b'HTTP/1.1 100 Continue')
+        c.sendall(b'hello')
+        got = b''
+        while not got.endswith(b'hello'):
+            chunk = c.recv(4096)
+            assert chunk
+            got += chunk
+        assert got.startswith(b'HTTP/1.1 200')
+    assert _raw(server, b'GARBAGE\r\n\r\n').startswith(b'HTTP/1.1 400')
+    assert _raw(server, b'GET /hello HTTP/1.1\r\nContent-Length: 1\r\nContent-Length: 2\r\n\r\n').startswith(
+        b'HTTP/1.1 400')
+    out = _raw(server, b'GET /hello HTTP/1.0\r\n\r\n')  # HTTP/1.0: closed after the response
+    assert out.startswith(b'HTTP/1.1 200') and b'connection: close' in out.lower()
+
+
+def _ws_frame(op: int, payload: bytes, fin: bool = True) -> bytes:
+    mask = os.urandom(4)
+    n = len(payload)
+    head = bytes([(0x80 if fin else 0) | op])
+    head += bytes([0x80 | n]) if n < 126 else (bytes([0x80 | 126]) + struct.pack('!H', n))
+    return head + mask + bytes(b ^ mask[i % 4] for i, b in enumerate(payload))
+
+
+def _ws_read(c) -> tuple:
+    h = c.recv(2)
+    op, n = h[0] & 15, h[1] & 127
+    if n == 126:
+        n = struct.unpack('!H', c.recv(2))[0]
+    data = b''
+    while len(data) < n:
+        data += c.recv(n - len(data))
+    return op, data
+
+
+def test_websocket_upgrade_echo_fragments_ping_close(server):
+    key = base64.b64encode(os.urandom(16))
+    with socket.create_connection(('127.0.0.1', server), timeout=5) as c:
+        c.sendall(b'GET /ws HTTP/1.1\r\nHost: x\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n'
+                  b'Sec-WebSocket-Key: ' + key + b'\r\nSec-WebSocket-Version: 13\r\n\r\n' + _ws_frame(1, b'early'))
+        resp = b''
+        while b'\r\n\r\n' not in resp:
+            resp += c.recv(1)
+        assert resp.startswith(b'HTTP/1.1 101')
+        accept = base64.b64encode(hashlib.sha1(key + b'258EAFA5-E914-47DA-95CA-C5AB0DC85B11').digest())
+        assert accept in resp
+        assert _ws_read(c) == (1, b'echo:early')  # a frame sent with the handshake is not lost
+        c.sendall(_ws_frame(1, 'héllo'.encode()))
+        assert _ws_read(c) == (1, 'echo:héllo'.encode())
+        c.sendall(_ws_frame(2, b'\x00\x01' * 200))
+        assert _ws_read(c) == (2, b'echo:' + b'\x00\x01' * 200)
+        c.sendall(_ws_frame(1, b'frag', fin=False) + _ws_frame(9, b'p') + _ws_frame(0, b'ment'))
+        assert _ws_read(c) == (10, b'p')  # the ping is answered between the fragments
+        assert _ws_read(c) == (1, b'echo:fragment')
+        c.sendall(_ws_frame(1, b'bye'))
+        op, data = _ws_read(c)
+        assert op == 8 and struct.unpack('!H', data[:2])[0] == 4000

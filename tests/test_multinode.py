@@ -1,6 +1,10 @@
-"""Two real node processes (uvicorn on 127.0.0.1) + the miner CLI: mining, gossip, sync."""
+"""Two real node processes (uvicorn on 127.0.0.1) + the miner CLI: mining, gossip, sync, and a WebSocket
+subscriber receiving the new block over a real socket."""
+import base64
+import json
 import os
 import socket
+import struct
 import subprocess
 import sys
 import time
@@ -43,6 +47,41 @@ def _start(tmp, name, port):
     raise RuntimeError('node did not start')
 
 
+def _ws_connect(url):
+    host, port = url.split('//')[1].split(':')
+    c = socket.create_connection((host, int(port)), timeout=30)
+    key = base64.b64encode(os.urandom(16))
+    c.sendall(b'GET /ws HTTP/1.1\r\nHost: x\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n'
+              b'Sec-WebSocket-Key: ' + key + b'\r\nSec-WebSocket-Version: 13\r\n\r\n')
+    head = b''
+    while b'\r\n\r\n' not in head:
+        head += c.recv(1)
+    assert head.startswith(b'HTTP/1.1 101'), head
+    return c
+
+
+def _ws_frame(payload: bytes) -> bytes:
+    mask = os.urandom(4)
+    n = len(payload)
+    head = bytes([0x81]) + (bytes([0x80 | n]) if n < 126 else bytes([0x80 | 126]) + struct.pack('!H', n))
+    return head + mask + bytes(b ^ mask[i % 4] for i, b in enumerate(payload))
+
+
+def _ws_read(c) -> str:
+    while True:  # text frames; server pings are skipped
+        h = c.recv(2)
+        op, n = h[0] & 15, h[1] & 127
+        if n == 126:
+            n = struct.unpack('!H', c.recv(2))[0]
+        elif n == 127:
+            n = struct.unpack('!Q', c.recv(8))[0]
+        data = b''
+        while len(data) < n:
+            data += c.recv(n - len(data))
+        if op == 1:
+            return data.decode()
+
+
 def _height(url):
     return httpx.get(url + '/get_mining_info', timeout=5).json()['result']['last_block'].get('id', 0)
 
@@ -78,6 +117,10 @@ def test_mine_gossip_and_sync(two_nodes):
     res = httpx.get(a + '/sync_blockchain', params={'node_url': b}, timeout=60).json()
     assert res == {'ok': True}, res
     assert _height(a) == 2
+    ws = _ws_connect(a)  # the node's /ws endpoint over a real socket (node/http.py serves the upgrade)
+    ws.sendall(_ws_frame(json.dumps({'type': 'subscribe_block'}).encode()))
+    assert json.loads(_ws_read(ws))['message'] == 'Subscribed to block'
+    assert json.loads(_ws_read(ws))['data'] == {'type': 'block_subscription'}
     ha = httpx.get(a + '/get_block', params={'block': 2}).json()['result']['block']['hash']
     hb = httpx.get(b + '/get_block', params={'block': 2}).json()['result']['block']['hash']
     assert ha == hb
@@ -93,4 +136,7 @@ def test_mine_gossip_and_sync(two_nodes):
             break
         time.sleep(0.1)
     assert _height(a) == 3 and _height(b) == 3
+    ev = json.loads(_ws_read(ws))  # node A published its new block to the subscriber
+    assert ev['type'] == 'new_block' and ev['data']['block_no'] == 3
+    ws.close()
     assert httpx.get(a + '/').json()['unspent_outputs_hash'] == httpx.get(b + '/').json()['unspent_outputs_hash']

@@ -41,6 +41,15 @@ def pin_cpus(spec: str):
     return want
 
 
+def server_protocol() -> dict:
+    """uvicorn keyword arguments for the node's HTTP/WebSocket protocol (``node/http.py``: native request
+    framing, WebSocket served in place); ``UPOW_NATIVE_HTTP=0`` keeps uvicorn's own h11 protocol."""
+    if os.environ.get('UPOW_NATIVE_HTTP', '1') == '0':
+        return {}
+    from .http import NodeHttpProtocol
+    return {'http': NodeHttpProtocol}
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--host', default='0.0.0.0')
@@ -78,9 +87,9 @@ def main(argv=None):
         # uvicorn re-raises the SIGTERM it caught once the graceful shutdown is done: dump there
         signal.signal(signal.SIGTERM, dump)
         prof.enable()
-        uvicorn.run('upow_amd.node.main:app', host=a.host, port=a.port, log_level=a.log_level)
+        uvicorn.run('upow_amd.node.main:app', host=a.host, port=a.port, log_level=a.log_level, **server_protocol())
         dump()
-    uvicorn.run('upow_amd.node.main:app', host=a.host, port=a.port, log_level=a.log_level)
+    uvicorn.run('upow_amd.node.main:app', host=a.host, port=a.port, log_level=a.log_level, **server_protocol())
 
 
 def _run_cluster(a):
@@ -97,7 +106,7 @@ def _run_cluster(a):
         if ctx.rank == 0:
             import uvicorn
             from . import main as node_main
-            uvicorn.run(node_main.app, host=a.host, port=a.port, log_level=a.log_level)
+            uvicorn.run(node_main.app, host=a.host, port=a.port, log_level=a.log_level, **server_protocol())
         else:
             from ..ledger.database import Database
 
