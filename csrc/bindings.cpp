@@ -18,6 +18,7 @@ void register_ledger_writer(py::module_& m);  // ledger_writer.cpp
 void register_gov_index(py::module_& m);  // gov_index.cpp
 void register_log_appender(py::module_& m);  // log_appender.cpp
 void register_http_wire(py::module_& m);  // http_wire.cpp
+void register_mempool_index(py::module_& m);  // mempool_index.cpp
 }
 
 static PowJobHost make_job(py::bytes header, uint32_t tmask, uint32_t tword, uint32_t frac_shift,
@@ -56,6 +57,7 @@ PYBIND11_MODULE(_native, m) {
     register_gov_index(m);
     register_log_appender(m);
     register_http_wire(m);
+    register_mempool_index(m);
 
     m.def("sha256", [](py::bytes msg) {
         std::string s = msg;

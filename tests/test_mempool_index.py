@@ -71,7 +71,7 @@ def test_admission_matches_sql_path():
             _use(a)
             txs.append(await create_transaction(GENESIS, address_of(k), '1.5'))
             assert await _admit_both(a, b, txs[-1]) is True
-        assert a._mp is not None and len(a._mp.txs) == len(txs)
+        assert a._mp is not None and len(a._mp) == len(txs)
         assert await _admit_both(a, b, txs[0]) is False  # its own inputs are pending-spent (reference order)
         # same inputs, different outputs: a double spend against the mempool
         ins = [TransactionInput(i.tx_hash, i.index, amount=i.amount, public_key=i.public_key) for i in txs[1].inputs]
@@ -86,7 +86,7 @@ def test_admission_matches_sql_path():
             _use(db)
             c = await devnet.mine_header(address_of(GENESIS), txs[:2], ts=ts, device='cpu')
             assert await fastpath.create_block_from_hex(c, [t.hex() for t in txs[:2]])
-        assert len(a._mp.txs) == 2
+        assert len(a._mp) == 2
         assert _pending(a) == _pending(b)
         assert len(_pending(a)[0]) == 2
         reloads = a.mempool_reloads
@@ -197,3 +197,42 @@ def test_admission_context_uses_batched_hbm_probe(gpu):
         assert coalesce.stats().get('utxo-probe', {}).get('items', 0) >= 4
         assert _pending(a) == _pending(b)
     asyncio.run(go())
+
+
+def test_native_index_template_order_and_confirm():
+    # the C++ index against the reference's ORDER BY fees / LENGTH(tx_hex) DESC, LENGTH(tx_hex), tx_hex
+    # (Decimal arithmetic), and a block's raw confirm with the late-admission split
+    import random
+    import numpy as np
+    from upow_amd.ledger.mempool import MempoolIndex, outpoint_key
+    rng = random.Random(3)
+    rows = []
+    for k in range(400):
+        hx = rng.randbytes(rng.choice([100, 120, 120, 200])).hex()
+        fee = Decimal(rng.choice([0, 1, 2, 3, 10, 25])) / 1000000
+        rows.append((rng.randbytes(32).hex(), 1_700_000_000 + k, hx, format(fee, 'f')))
+    mp = MempoolIndex(rows, [])
+    want = sorted(rows, key=lambda r: (-(Decimal(r[3]) / len(r[2])), len(r[2]), r[2]))
+    got = mp.ordered(10 ** 9)
+    assert [hx for hx, _ in got] == [r[2] for r in want]
+    assert [h.hex() for _, h in got] == [r[0] for r in want]
+    limit = sum(len(r[2]) for r in want[:37]) + 5
+    assert len(mp.ordered(limit)) == 37
+    assert mp.hex_in_order([rows[5][0], rows[2][0], 'zz', rows[2][0]]) == [rows[2][2], rows[5][2]]
+    # admissions: duplicate, double spend, sequence; confirm splits hits by the block's sequence
+    h1, h2 = rng.randbytes(32).hex(), rng.randbytes(32).hex()
+    op = (rng.randbytes(32).hex(), 3)
+    with mp.lock:
+        assert mp.try_add(h1, 5, [op], 'ab' * 60, '0.000010') is None
+        assert mp.try_add(h1, 5, [], 'ab' * 60, '0.000010') == 'duplicate'
+        assert mp.try_add(h2, 5, [op], 'cd' * 60, '0.000010') == 'double spend'
+        mp.set_seq(h1, [op], 9)
+    assert mp.spent_of([op, op, (op[0], 4)]) == [op]
+    txids = np.frombuffer(bytes.fromhex(h1) + bytes.fromhex(rows[0][0]), np.uint8).reshape(-1, 32)
+    keys = np.zeros((1, 40), np.uint8)
+    keys[0, :36] = np.frombuffer(outpoint_key(*op), np.uint8)
+    hit_tx, hit_in, late_tx, late_in = mp.confirm_raw(txids, keys, 7)
+    assert sorted(hit_tx) == sorted([bytes.fromhex(h1), bytes.fromhex(rows[0][0])])
+    assert hit_in == [outpoint_key(*op)] and late_tx == [bytes.fromhex(h1)] and late_in == [outpoint_key(*op)]
+    assert len(mp) == 399 and not mp.has_tx(h1) and mp.spent_of([op]) == []
+    assert mp.maybe_stale(1_700_000_000 + 10_000, 100) and not mp.maybe_stale(1_700_000_000, 10 ** 6)

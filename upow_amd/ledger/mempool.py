@@ -25,7 +25,6 @@ from __future__ import annotations
 
 import threading
 from decimal import Decimal
-from operator import itemgetter
 from typing import Dict, Iterable, List, Optional, Set, Tuple
 
 import numpy as np
@@ -35,141 +34,82 @@ def outpoint_key(tx_hash: str, index: int) -> bytes:
     return bytes.fromhex(tx_hash) + int(index).to_bytes(4, 'little')
 
 
-def _rows_raw(arr: np.ndarray, width: int) -> List[bytes]:
-    """The leading ``width`` bytes of each row of an n x k uint8 array, as bytes objects."""
-    a = np.ascontiguousarray(np.asarray(arr, dtype=np.uint8)[:, :width])
-    return a.view(f'V{width}').ravel().tolist()  # void scalars -> bytes, built in C
-
-
-_second = itemgetter(1)
-
-
-def order_key(tx_hex: str, fees) -> tuple:
-    return (-(Decimal(fees) / len(tx_hex)), len(tx_hex), tx_hex)
+def _fee_text(fees) -> str:
+    """The fee as plain decimal text (``numeric()`` strings pass through; a Decimal in exponent form is
+    expanded) for the native index's exact 1e-8-unit parse."""
+    return fees if isinstance(fees, str) else format(Decimal(fees), 'f')
 
 
 class MempoolIndex:
+    """The index in C++ (csrc/mempool_index.cpp ``MempoolIndexCore``): admissions are hash-map probes, and a
+    committed block's raw txid / outpoint arrays leave it in one call without the GIL. ``lock`` serialises
+    an admission's reserve + journal + sequence record against a block's confirm (ledger/database.py)."""
+
     def __init__(self, tx_rows: Iterable[Tuple[str, int, str, str]], spent_rows: Iterable[Tuple[str, int]]):
         """``tx_rows``: (tx_hash, propagation_time, tx_hex, fees) of pending_transactions."""
+        from ..ops.native import lib
         self.lock = threading.Lock()
-        self.txs: Dict[bytes, int] = {}  # tx hash -> propagation time
-        self.keys: Dict[bytes, tuple] = {}  # tx hash -> order_key
-        for h, t, hx, fees in tx_rows:
-            k = bytes.fromhex(h)
-            self.txs[k] = int(t)
-            self.keys[k] = order_key(hx, fees)
-        self.spent: Set[bytes] = {outpoint_key(h, i) for h, i in spent_rows}
-        # journal sequence of each admission's INSERT batch (rows loaded from SQL: 0, already materialised).
-        # A block confirming a tx whose admission was journaled AFTER the block's own batch cannot rely on
-        # that batch's DELETEs (they ran before the INSERTs): it needs a follow-up delete.
-        self.seq: Dict[bytes, int] = {}
-        self.spent_seq: Dict[bytes, int] = {}
-        self.min_ptime: Optional[int] = min(self.txs.values()) if self.txs else None
+        self.core = lib().MempoolIndexCore()
+        self.core.load([(h, int(t), hx, _fee_text(f)) for h, t, hx, f in tx_rows],
+                       [(h, int(i)) for h, i in spent_rows])
+
+    def __len__(self) -> int:
+        return len(self.core)
 
     def empty(self) -> bool:
-        return not self.txs and not self.spent
+        return self.core.empty()
 
     def has_tx(self, tx_hash: str) -> bool:
-        return bytes.fromhex(tx_hash) in self.txs
+        try:
+            return self.core.has_tx(tx_hash)
+        except ValueError:
+            return False
 
     def spent_of(self, outputs: Iterable[Tuple[str, int]]) -> List[Tuple[str, int]]:
         """The outpoints among ``outputs`` that a mempool tx already spends (unique, first seen)."""
-        seen = dict.fromkeys((h, int(i)) for h, i in outputs)
-        return [o for o in seen if outpoint_key(*o) in self.spent]
+        return self.core.spent_of([(h, int(i)) for h, i in outputs])
 
     def ordered(self, limit: int) -> List[Tuple[str, bytes]]:
         """(tx hex, raw tx hash) of the pending txs in block-template order, up to ``limit`` hex
         characters in total."""
         with self.lock:
-            items = sorted(self.keys.items(), key=_second)
-        out, size = [], 0
-        for h, k in items:
-            if size + k[1] > limit:
-                break
-            out.append((k[2], h))
-            size += k[1]
-        return out
+            return self.core.ordered(int(limit))
 
     def hex_in_order(self, tx_hashes: Iterable[str]) -> List[str]:
         """tx hex of the pending txs among ``tx_hashes``, in admission (table row) order."""
-        want = set()
-        for h in tx_hashes:
-            try:
-                want.add(bytes.fromhex(h))
-            except ValueError:
-                continue
         with self.lock:
-            if len(want) == 1:
-                k = self.keys.get(next(iter(want)))
-                return [k[2]] if k is not None else []
-            return [k[2] for h, k in self.keys.items() if h in want]
+            return self.core.hex_in_order(list(tx_hashes))
 
     def ordered_hex(self, limit: int) -> List[str]:
         return [hx for hx, _ in self.ordered(limit)]
 
     def try_add(self, tx_hash: str, ptime: int, inputs: List[Tuple[str, int]], tx_hex: str, fees) -> Optional[str]:
         """Reserve a tx and its inputs (caller holds ``lock``); returns why it cannot be added, or None."""
-        h = bytes.fromhex(tx_hash)
-        if h in self.txs:
-            return 'duplicate'
-        keys = [outpoint_key(a, i) for a, i in inputs]
-        if any(k in self.spent for k in keys):
-            return 'double spend'
-        self.txs[h] = int(ptime)
-        self.keys[h] = order_key(tx_hex, fees)
-        self.spent.update(keys)
-        if self.min_ptime is None or ptime < self.min_ptime:
-            self.min_ptime = int(ptime)
-        return None
+        return self.core.try_add(tx_hash, int(ptime), [(h, int(i)) for h, i in inputs], tx_hex, _fee_text(fees))
 
     def set_seq(self, tx_hash: str, inputs: List[Tuple[str, int]], seq: int):
         """Record the journal sequence of an admission's batch (caller holds ``lock``)."""
-        self.seq[bytes.fromhex(tx_hash)] = int(seq)
-        for a, i in inputs:
-            self.spent_seq[outpoint_key(a, i)] = int(seq)
-
-    def _confirm(self, tx_keys: List[bytes], in_keys: List[bytes], after: Optional[int] = None):
-        """Remove confirmed txs and outpoints; returns (hit_tx, hit_in, late_tx, late_in) where the late
-        lists hold the hits whose admission was journaled after sequence ``after``."""
-        with self.lock:
-            hit_tx = []
-            if self.txs:
-                pop = self.txs.pop
-                hit_tx = [k for k in tx_keys if pop(k, None) is not None]
-                for k in hit_tx:
-                    del self.keys[k]
-            hit_in = []
-            if self.spent and in_keys:
-                hit_in = list(self.spent.intersection(in_keys))
-                self.spent.difference_update(hit_in)
-            late_tx, late_in = [], []
-            if hit_tx:
-                sq = self.seq.pop
-                late_tx = [k for k in hit_tx if sq(k, 0) > (after or 0)] if after is not None else []
-            if hit_in:
-                sq = self.spent_seq.pop
-                late_in = [k for k in hit_in if sq(k, 0) > (after or 0)] if after is not None else []
-            if not self.txs:
-                self.min_ptime = None
-            return hit_tx, hit_in, late_tx, late_in
+        self.core.set_seq(tx_hash, [(h, int(i)) for h, i in inputs], int(seq))
 
     def confirm_raw(self, txids: np.ndarray, in_keys: np.ndarray, after: Optional[int] = None):
         """A committed block's txs (n x 32) and spent outpoints (n x >=36 records) leave the mempool;
         returns the raw tx hashes and outpoints that were in it (and those admitted after ``after``)."""
-        return self._confirm(_rows_raw(txids, 32) if len(txids) else [],
-                             _rows_raw(in_keys, 36) if len(in_keys) else [], after)
+        t = np.ascontiguousarray(np.asarray(txids, dtype=np.uint8).reshape(-1, 32))
+        k = np.asarray(in_keys, dtype=np.uint8)
+        k = np.ascontiguousarray(k.reshape(-1, k.shape[-1] if k.ndim == 2 and k.shape[0] else 40))
+        with self.lock:
+            return self.core.confirm_raw(t, k, after)
 
     def confirm(self, tx_hashes: List[str], inputs: List[Tuple[str, int]], after: Optional[int] = None):
-        return self._confirm([bytes.fromhex(h) for h in tx_hashes], [outpoint_key(h, i) for h, i in inputs], after)
+        t = np.frombuffer(b''.join(bytes.fromhex(h) for h in tx_hashes), dtype=np.uint8).reshape(-1, 32)
+        k = np.frombuffer(b''.join(outpoint_key(h, i) for h, i in inputs), dtype=np.uint8).reshape(-1, 36)
+        return self.confirm_raw(t, k, after)
 
     def maybe_stale(self, now: int, delta: int) -> bool:
-        """Could a pending tx be older than ``delta`` seconds? ``min_ptime`` only moves down between
-        recomputes, so False is exact and True is re-checked against the current entries."""
+        """Could a pending tx be older than ``delta`` seconds? The minimum propagation time only moves down
+        between recomputes, so False is exact and True is re-checked against the current entries."""
         with self.lock:
-            if self.min_ptime is None or now - self.min_ptime <= delta:
-                return False
-            self.min_ptime = min(self.txs.values()) if self.txs else None
-            return self.min_ptime is not None and now - self.min_ptime > delta
+            return self.core.maybe_stale(int(now), int(delta))
 
 
 __all__ = ['MempoolIndex', 'outpoint_key']
