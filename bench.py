@@ -198,7 +198,10 @@ def main(argv=None):
         if args.mode == 'mine':
             out = bench_mine(args, ctx)
             if args.verify_steps > 0 and out['config']['device'] == 'gpu':
-                out.update(_verify_side_metrics(args, ctx))
+                try:
+                    out.update(_verify_side_metrics(args, ctx))
+                except Exception as e:  # the headline number stands on its own; say why the extra is missing
+                    out['verify_error'] = f'{type(e).__name__}: {e}'[:300]
         elif args.mode == 'verify':
             out = bench_verify(args, ctx)
         else:
