@@ -1116,7 +1116,75 @@ static py::tuple block_signer_records(py::buffer pay_addr_b, py::buffer pay_len_
     return py::make_tuple(1, py::bytes(recs));
 }
 
+// HBM index records of a block's created outputs: 40-byte keys (txid | index u32 | table tag u32) and
+// 80-byte payloads (amount u64 | address length u32 | flags u32 | address, prefix normalised as
+// bytes_to_string does) in one pass, instead of a dozen numpy passes over the block's outputs.
+static py::tuple output_index_records(py::buffer txid_b, py::buffer index_b, py::buffer tag_b, py::buffer amount_b,
+                                      py::buffer addr_b, py::buffer len_b, py::buffer stake_b) {
+    const py::buffer_info ti = txid_b.request(), ii = index_b.request(), gi = tag_b.request(), ai = amount_b.request(),
+                          di = addr_b.request(), li = len_b.request(), si = stake_b.request();
+    size_t n_t, n_i, n_g, n_a, n_d, n_l, n_s;
+    const uint8_t* txid = buf_view<uint8_t>(ti, n_t);
+    const int64_t* idx = buf_view<int64_t>(ii, n_i);
+    const uint32_t* tag = buf_view<uint32_t>(gi, n_g);
+    const uint64_t* amount = buf_view<uint64_t>(ai, n_a);
+    const uint8_t* addr = buf_view<uint8_t>(di, n_d);
+    const uint8_t* len = buf_view<uint8_t>(li, n_l);
+    const uint8_t* stake = buf_view<uint8_t>(si, n_s);
+    const size_t n = n_i;
+    if (n_t != 32 * n || n_g != n || n_a != n || n_d != 64 * n || n_l != n || (n_s && n_s != n))
+        throw std::invalid_argument("output_index_records: column lengths differ");
+    char *rp, *pp;
+    py::bytes recs = new_pybytes(40 * n, rp), pay = new_pybytes(80 * n, pp);
+    {
+        py::gil_scoped_release rel;
+        for (size_t o = 0; o < n; ++o) {
+            uint8_t* r = reinterpret_cast<uint8_t*>(rp) + 40 * o;
+            std::memcpy(r, txid + 32 * o, 32);
+            const uint32_t ix = uint32_t(idx[o]);
+            std::memcpy(r + 32, &ix, 4);
+            std::memcpy(r + 36, &tag[o], 4);
+            uint8_t* q = reinterpret_cast<uint8_t*>(pp) + 80 * o;
+            std::memcpy(q, &amount[o], 8);
+            const uint32_t l = len[o], fl = (n_s && stake[o]) ? 1u : 0u;
+            std::memcpy(q + 8, &l, 4);
+            std::memcpy(q + 12, &fl, 4);
+            std::memcpy(q + 16, addr + 64 * o, 64);
+            if (l == 33) q[16] = q[16] == 43 ? 43 : 42;
+        }
+    }
+    return py::make_tuple(recs, pay);
+}
+
+// the block's spent outpoints as erase records (the codec's input keys with each input's table tag) and
+// their output indexes as int64
+static py::tuple spent_index_records(py::buffer keys_b, py::buffer tag_b) {
+    const py::buffer_info ki = keys_b.request(), gi = tag_b.request();
+    size_t n_k, n_g;
+    const uint8_t* keys = buf_view<uint8_t>(ki, n_k);
+    const uint32_t* tag = buf_view<uint32_t>(gi, n_g);
+    if (n_k != 40 * n_g) throw std::invalid_argument("spent_index_records: 40-byte keys, one tag per key");
+    char *sp, *ip;
+    py::bytes spent = new_pybytes(n_k, sp), idx = new_pybytes(8 * n_g, ip);
+    {
+        py::gil_scoped_release rel;
+        for (size_t j = 0; j < n_g; ++j) {
+            uint8_t* r = reinterpret_cast<uint8_t*>(sp) + 40 * j;
+            std::memcpy(r, keys + 40 * j, 36);
+            std::memcpy(r + 36, &tag[j], 4);
+            uint32_t ix;
+            std::memcpy(&ix, keys + 40 * j + 32, 4);
+            const int64_t v = ix;
+            std::memcpy(ip + 8 * j, &v, 8);
+        }
+    }
+    return py::make_tuple(spent, idx);
+}
+
 void register_txcodec(py::module_& m) {
+    m.def("output_index_records", &output_index_records, py::arg("txid"), py::arg("index"), py::arg("tag"),
+          py::arg("amount"), py::arg("addr"), py::arg("len"), py::arg("stake"));
+    m.def("spent_index_records", &spent_index_records, py::arg("keys"), py::arg("tag"));
     py::class_<MerkleJob, std::shared_ptr<MerkleJob>>(m, "MerkleJob")
         .def("result", &MerkleJob::result, "the block's merkle root (hex); waits for the merkle thread");
     m.def("fee_strings", &fee_strings);

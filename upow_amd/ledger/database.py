@@ -1837,35 +1837,28 @@ class Database:
         tag_u = TAG_BY_TABLE['unspent_outputs']
         out_tag = gov['out_tag'] if gov is not None else np.full(n_out, tag_u, dtype=np.uint32)
         # ---- index records: created outputs (block txs + coinbase) and spent inputs
-        recs = np.zeros((n_out, 40), dtype=np.uint8)
-        recs[:, :32] = out_txid
-        recs[:, 32:36] = out_index.astype(np.uint32).reshape(-1, 1).view(np.uint8)
-        recs[:, 36:40] = np.ascontiguousarray(out_tag, dtype=np.uint32).reshape(-1, 1).view(np.uint8)
-        pay = np.zeros(n_out, dtype=PAYLOAD_DTYPE)
-        pay['amount'] = out_amount
-        pay['len'] = out_len
-        if gov is not None:
-            pay['flags'] = np.where(gov['out_type'] == int(OutputType.STAKE), FLAG_STAKE, 0).astype(np.uint32)
-        a = np.array(out_addr, dtype=np.uint8, copy=True)
-        c33 = out_len == 33
-        a[c33, 0] = np.where(a[c33, 0] == 43, 43, 42)  # bytes_to_string normalises the prefix
-        pay['addr'] = a
+        from ..ops.native import lib
+        stake = (np.asarray(gov['out_type']) == int(OutputType.STAKE)).astype(np.uint8) if gov is not None \
+            else np.zeros(0, np.uint8)
+        rb, pb = lib().output_index_records(
+            np.ascontiguousarray(out_txid, dtype=np.uint8), np.ascontiguousarray(out_index, dtype=np.int64),
+            np.ascontiguousarray(out_tag, dtype=np.uint32), np.ascontiguousarray(out_amount, dtype=np.uint64),
+            np.ascontiguousarray(out_addr, dtype=np.uint8), np.ascontiguousarray(out_len, dtype=np.uint8), stake)
+        recs = np.frombuffer(rb, dtype=np.uint8).reshape(-1, 40)
+        pay = np.frombuffer(pb, dtype=PAYLOAD_DTYPE)
         from .utxo import pack_records
         cb_keys = [(o[0], o[1]) for o in coinbase_outputs]
         cb_recs = pack_records(cb_keys, tag_u)
         cb_pay = make_payload([o[4] for o in coinbase_outputs], [_addr_bytes(o[2]) for o in coinbase_outputs],
                               [bool(o[3]) for o in coinbase_outputs])
         in_keys = np.ascontiguousarray(in_keys, dtype=np.uint8).reshape(-1, 40)
-        spent = np.array(in_keys, dtype=np.uint8, copy=True)
         in_tag = gov['in_tag'].astype(np.uint32) if gov is not None else np.full(n_in, tag_u, dtype=np.uint32)
-        spent[:, 36:40] = np.ascontiguousarray(in_tag).reshape(-1, 1).view(np.uint8)
-        in_idx = in_keys[:, 32:36].copy().view(np.uint32).ravel().astype(np.int64)
-        # the spends' key order (B-tree locality) is computed by the materialiser ('key'), except where
-        # governance selections need the ranks here
-        in_order = self._key_order(in_keys) if n_in and gov is not None else 'key'
-        if gov is not None and n_in:
-            in_order_rank = np.empty(n_in, dtype=np.int64)  # position of each input in the key order
-            in_order_rank[in_order] = np.arange(n_in, dtype=np.int64)
+        sb, ib = lib().spent_index_records(in_keys, np.ascontiguousarray(in_tag, dtype=np.uint32))
+        spent = np.frombuffer(sb, dtype=np.uint8).reshape(-1, 40)
+        in_idx = np.frombuffer(ib, dtype=np.int64)
+        # the spends' key order (B-tree locality) is computed by the materialiser ('key': a stable sort of the
+        # statement's rows by the leading 8 bytes of column 0, so a row selection keeps the global key order)
+        in_order = 'key'
         stamp()
 
         # ---- statements (schema.sql write set of one block)
@@ -1947,7 +1940,7 @@ class Database:
         elif gov is not None and len(sel_u):
             stmts.append(('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
                           [('hex32', in_keys, 40, 0, sel_u), np.ascontiguousarray(in_idx[sel_u])], len(sel_u),
-                          np.argsort(in_order_rank[sel_u], kind='stable').astype(np.int64), None, len(sel_u)))
+                          'key', None, len(sel_u)))
         for table in self._SPEND_ORDER[2:]:
             if table in gov_spent:
                 spend_stmt(table)
@@ -2023,6 +2016,9 @@ class Database:
             def gov_apply():
                 g.store.apply_block(*args)
                 g.version += 1
+                # the next block's coinbase needs the active inodes of this state: their emission cascade
+                # (ballot terms, validator stakes) is evaluated here, off the block path, into the memo
+                g.inodes_with_power(False)
             g.defer(gov_apply)
             self.last_gov_index_s = perf_counter() - tg
         elif self.gov is not None and n_in:
