@@ -602,7 +602,8 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
     PooledBuf<uint8_t> b_st{size_t(n)};
     VerifyItem* d_items = b_items.p;
     uint8_t* d_st = b_st.p;
-    node_h2d(d_items, items, sizeof(VerifyItem) * n, "h2d items");
+    StagedIO io(sizeof(VerifyItem) * size_t(n) + size_t(n));
+    io.h2d(d_items, items, sizeof(VerifyItem) * size_t(n));
     // Variant (UPOW_P256_VARIANT, read per call): unset/'a' = auto, '4' = four lanes per signature,
     // '0'..'3' = one lane per signature (below). Auto takes the quad kernel up to 32k signatures
     // (2,048 waves, two per SIMD): there it cuts the latency of block-sized batches; past that the
@@ -616,7 +617,8 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
         hipLaunchKernelGGL(p256_verify_quad_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, node_stream(), d_items, n,
                            d_tab, b_tab.p, d_st);
         hck(hipGetLastError(), "p256_verify_quad_kernel launch");
-        node_d2h(st.data(), d_st, size_t(n), "d2h status");
+        io.d2h(st.data(), d_st, size_t(n));
+        io.finish("verify status");
         return st;
     }
     PooledBuf<jac> b_scratch(size_t(16) * size_t(n));
@@ -670,13 +672,15 @@ void p256_decompress_gpu(const uint8_t* in, int64_t n, uint8_t* out, uint8_t* ok
     node_device_enter();
     PooledBuf<uint8_t> b_in{33 * size_t(n)}, b_out{64 * size_t(n)}, b_ok{size_t(n)};
     uint8_t *d_in = b_in.p, *d_out = b_out.p, *d_ok = b_ok.p;
-    node_h2d(d_in, in, 33 * size_t(n), "h2d in");
+    StagedIO io(98 * size_t(n));
+    io.h2d(d_in, in, 33 * size_t(n));
     const int block = 256;
     hipLaunchKernelGGL(p256_decompress_kernel, dim3(int((n + block - 1) / block)), dim3(block), 0, node_stream(), d_in, n,
                        d_out, d_ok);
     hck(hipGetLastError(), "p256_decompress_kernel launch");
-    node_d2h(out, d_out, 64 * size_t(n), "d2h out");
-    node_d2h(ok, d_ok, size_t(n), "d2h ok");
+    io.d2h(out, d_out, 64 * size_t(n));
+    io.d2h(ok, d_ok, size_t(n));
+    io.finish("decompress");
 }
 
 bool p256_pubkey(const uint8_t d_be[32], uint8_t out_le[64]) {

@@ -99,4 +99,66 @@ inline void node_sync(const char* what = "node stream sync") {
     stream_check(hipStreamSynchronize(node_stream()), what);
 }
 
+// Pinned staging for one node-side call's transfers (per thread, grown on demand, never returned: the
+// HIP runtime may be gone when threads exit). A pageable hipMemcpyAsync is a staged, host-synchronous
+// copy, and every node_d2h above ends in its own stream sync; a block's UTXO pass made five of them. With
+// StagedIO the inputs are packed into pinned memory and DMA'd asynchronously, all outputs land in pinned
+// memory with ONE stream sync, then are unpacked. The buffer is reused only after that sync.
+struct NodeStageBuf {
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+};
+inline uint8_t* node_stage(size_t n) {
+    thread_local NodeStageBuf* b = new NodeStageBuf();
+    if (n > b->cap) {
+        if (b->p) (void)hipHostFree(b->p);  // the previous call on this thread synced its stream
+        size_t c = b->cap ? b->cap : (size_t(1) << 20);
+        while (c < n) c *= 2;
+        b->p = nullptr;
+        stream_check(hipHostMalloc(reinterpret_cast<void**>(&b->p), c, hipHostMallocDefault), "hipHostMalloc stage");
+        b->cap = c;
+    }
+    return b->p;
+}
+
+class StagedIO {
+public:
+    explicit StagedIO(size_t total) : base_(node_stage(total + 64 * 16)), cap_(total + 64 * 16) {}
+    void h2d(void* dst, const void* src, size_t n) {
+        if (!n) return;
+        uint8_t* at = take(n);
+        std::memcpy(at, src, n);
+        stream_check(hipMemcpyAsync(dst, at, n, hipMemcpyHostToDevice, node_stream()), "staged h2d");
+    }
+    void d2h(void* dst, const void* src, size_t n) {
+        if (!n) return;
+        uint8_t* at = take(n);
+        stream_check(hipMemcpyAsync(at, src, n, hipMemcpyDeviceToHost, node_stream()), "staged d2h");
+        outs_[n_out_++] = {dst, at, n};
+    }
+    // one sync for every transfer of the call, then the outputs are unpacked
+    void finish(const char* what = "staged sync") {
+        node_sync(what);
+        for (int i = 0; i < n_out_; ++i) std::memcpy(outs_[i].dst, outs_[i].at, outs_[i].n);
+        n_out_ = 0;
+    }
+
+private:
+    uint8_t* take(size_t n) {
+        const size_t a = (used_ + 63) & ~size_t(63);
+        if (a + n > cap_) throw std::runtime_error("StagedIO: transfer plan larger than declared");
+        used_ = a + n;
+        return base_ + a;
+    }
+    struct Out {
+        void* dst;
+        const uint8_t* at;
+        size_t n;
+    };
+    uint8_t* base_;
+    size_t cap_, used_ = 0;
+    Out outs_[16];
+    int n_out_ = 0;
+};
+
 }  // namespace upow

@@ -584,10 +584,12 @@ BlockInputsResult utxo_block_inputs(int64_t h, const uint8_t* keys, int64_t n_in
     DevBuf<uint64_t> d_out(n_out);
     DevBuf<int64_t> d_fee(n_tx);
     DevBuf<uint32_t> d_miss(n_tx);
-    if (n_in) node_h2d(d_keys.p, keys, sizeof(UtxoKeyRec) * n_in, "h2d keys");
-    if (n_out) node_h2d(d_out.p, out_amount, 8 * size_t(n_out), "h2d out");
-    node_h2d(d_in_start.p, in_start, 4 * size_t(n_tx + 1), "h2d in_start");
-    node_h2d(d_out_start.p, out_start, 4 * size_t(n_tx + 1), "h2d out_start");
+    StagedIO io(sizeof(UtxoKeyRec) * size_t(n_in) + 8 * size_t(n_out) + 8 * size_t(n_tx + 1) +
+                size_t(n_in) * (1 + sizeof(UtxoPayload) + 4) + 12 * size_t(n_tx));
+    io.h2d(d_keys.p, keys, sizeof(UtxoKeyRec) * size_t(n_in));
+    io.h2d(d_out.p, out_amount, 8 * size_t(n_out));
+    io.h2d(d_in_start.p, in_start, 4 * size_t(n_tx + 1));
+    io.h2d(d_out_start.p, out_start, 4 * size_t(n_tx + 1));
     node_memset(d_scratch.p, 0, sizeof(unsigned long long) * scap, "memset scratch");
     if (n_in) {
         const dim3 g(unsigned((n_in + 255) / 256));
@@ -601,12 +603,13 @@ BlockInputsResult utxo_block_inputs(int64_t h, const uint8_t* keys, int64_t n_in
                        d_in_start.p, d_out.p, d_out_start.p, n_tx, want_tag, d_fee.p, d_miss.p);
     uck(hipGetLastError(), "block_fee_kernel");
     if (n_in) {
-        node_d2h(r.tags.data(), d_tags.p, size_t(n_in), "d2h tags");
-        node_d2h(r.payload.data(), d_pay.p, r.payload.size(), "d2h payload");
-        node_d2h(r.dup_of.data(), d_dup.p, 4 * size_t(n_in), "d2h dup");
+        io.d2h(r.tags.data(), d_tags.p, size_t(n_in));
+        io.d2h(r.payload.data(), d_pay.p, r.payload.size());
+        io.d2h(r.dup_of.data(), d_dup.p, 4 * size_t(n_in));
     }
-    node_d2h(r.fee.data(), d_fee.p, 8 * size_t(n_tx), "d2h fee");
-    node_d2h(r.missing.data(), d_miss.p, 4 * size_t(n_tx), "d2h missing");
+    io.d2h(r.fee.data(), d_fee.p, 8 * size_t(n_tx));
+    io.d2h(r.missing.data(), d_miss.p, 4 * size_t(n_tx));
+    io.finish("block inputs");
     // exact confirmation of duplicate candidates (full 36-byte key compare)
     const UtxoKeyRec* kr = reinterpret_cast<const UtxoKeyRec*>(keys);
     for (int64_t i = 0; i < n_in; ++i) {
