@@ -1243,6 +1243,10 @@ class LedgerWriter {
         exec(sh.db, "PRAGMA foreign_keys = OFF");
         exec(sh.db, "PRAGMA secure_delete = OFF");  // the distribution build defaults to zero-filling freed cells
         exec(sh.db, "PRAGMA cache_size = -" + std::to_string(std::max<int64_t>(16, cache_mb) * 1024));
+        // memory-mapped reads (UPOW_SQLITE_MMAP_MB): B-tree pages a materialiser misses in its page cache
+        // are read from the mapping instead of copied out of the OS page cache
+        if (const char* mm = std::getenv("UPOW_SQLITE_MMAP_MB"))
+            exec(sh.db, "PRAGMA mmap_size = " + std::to_string(std::max<int64_t>(0, std::atoll(mm)) << 20));
         exec(sh.db, "PRAGMA wal_autocheckpoint = 0");
         exec(sh.db, "CREATE TABLE IF NOT EXISTS upow_journal_state (k INTEGER PRIMARY KEY CHECK (k = 0), seq INTEGER NOT NULL)");
         exec(sh.db, "INSERT OR IGNORE INTO upow_journal_state (k, seq) VALUES (0, 0)");
