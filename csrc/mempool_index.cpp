@@ -152,25 +152,37 @@ public:
 
     // (tx hex, raw hash) in block-template order, up to `limit` hex characters in total
     py::list ordered(int64_t limit) const {
-        std::vector<std::pair<const H32*, const Entry*>> v;
-        v.reserve(txs_.size());
-        for (auto& kv : txs_) v.emplace_back(&kv.first, &kv.second);
-        std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) {
-            const Entry& x = *a.second;
-            const Entry& y = *b.second;
-            const __int128 l = __int128(x.fee) * y.len, r = __int128(y.fee) * x.len;
-            if (l != r) return l > r;  // higher fee density first
-            if (x.len != y.len) return x.len < y.len;
-            return hex_less(x.hex, y.hex);
-        });
         py::list out;
-        int64_t size = 0;
-        for (auto& p : v) {
-            if (size + p.second->len > limit) break;
+        for (auto& p : select(limit))
             out.append(py::make_tuple(p.second->hex, py::bytes(reinterpret_cast<const char*>(p.first->data()), 32)));
-            size += p.second->len;
-        }
         return out;
+    }
+
+    // the mining template of /get_mining_info and the new-block event (reference main.py:675-695): the
+    // selected txs re-sorted by hex string; returns (first `head` hexes, all tx hashes as hex strs, the
+    // same hashes as one JSON array body `"h0","h1",...` for the response, count)
+    py::tuple mining_template(int64_t limit, int64_t head) const {
+        auto v = select(limit);
+        std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return hex_less(a.second->hex, b.second->hex); });
+        static const char* digits = "0123456789abcdef";
+        py::list first, hashes;
+        std::string frag;
+        frag.reserve(v.size() * 67);
+        char h[64];
+        for (size_t k = 0; k < v.size(); ++k) {
+            if (int64_t(k) < head) first.append(v[k].second->hex);
+            const uint8_t* d = v[k].first->data();
+            for (int j = 0; j < 32; ++j) {
+                h[2 * j] = digits[d[j] >> 4];
+                h[2 * j + 1] = digits[d[j] & 15];
+            }
+            hashes.append(py::str(h, 64));
+            if (k) frag.push_back(',');
+            frag.push_back('"');
+            frag.append(h, 64);
+            frag.push_back('"');
+        }
+        return py::make_tuple(first, hashes, py::bytes(frag), v.size());
     }
 
     // tx hex of the pending txs among `hashes` (hex strings; malformed ones ignored), in admission order
@@ -275,6 +287,29 @@ public:
     }
 
 private:
+    // block-template order: fee density (exact cross-multiplication), then length, then hex; cut at `limit`
+    std::vector<std::pair<const H32*, const Entry*>> select(int64_t limit) const {
+        std::vector<std::pair<const H32*, const Entry*>> v;
+        v.reserve(txs_.size());
+        for (auto& kv : txs_) v.emplace_back(&kv.first, &kv.second);
+        std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) {
+            const Entry& x = *a.second;
+            const Entry& y = *b.second;
+            const __int128 l = __int128(x.fee) * y.len, r = __int128(y.fee) * x.len;
+            if (l != r) return l > r;  // higher fee density first
+            if (x.len != y.len) return x.len < y.len;
+            return hex_less(x.hex, y.hex);
+        });
+        int64_t size = 0;
+        size_t n = 0;
+        for (; n < v.size(); ++n) {
+            if (size + v[n].second->len > limit) break;
+            size += v[n].second->len;
+        }
+        v.resize(n);
+        return v;
+    }
+
     static bool hex_less(const py::object& a, const py::object& b) {
         Py_ssize_t na = 0, nb = 0;
         const char* pa = PyUnicode_AsUTF8AndSize(a.ptr(), &na);
@@ -337,6 +372,7 @@ void register_mempool_index(py::module_& m) {
         .def("spent_of", &MempoolIndex::spent_of)
         .def("ordered", &MempoolIndex::ordered)
         .def("hex_in_order", &MempoolIndex::hex_in_order)
+        .def("mining_template", &MempoolIndex::mining_template)
         .def("try_add", &MempoolIndex::try_add)
         .def("set_seq", &MempoolIndex::set_seq)
         .def("confirm_raw", &MempoolIndex::confirm_raw, py::arg("txids"), py::arg("in_keys"), py::arg("after") = py::none())

@@ -4,6 +4,7 @@ Two ledgers take the same admissions and blocks — one with the index (admissio
 checks read host memory), one with ``mempool_index = False`` (the reference's SQL INSERT/SELECT path,
 upow/database.py:93-115, 832-838) — and must give the same verdicts and the same mempool tables."""
 import asyncio
+import json
 from datetime import timedelta
 from decimal import Decimal
 
@@ -13,6 +14,7 @@ from upow_amd import devnet
 from upow_amd.ledger import database as dbmod
 from upow_amd.ledger import fastpath, manager
 from upow_amd.ledger.database import Database, UniqueViolationError
+from upow_amd.utils.codec import sha256
 from upow_amd.models.transaction import Transaction, TransactionInput, TransactionOutput
 from upow_amd.wallet.builders import address_of, create_transaction
 
@@ -143,6 +145,13 @@ def test_template_and_hash_lookup_match_sql_path():
         hb, xb = b.pending_template()
         assert (ha, xa) == (hb, xb) and xa == [t.hash() for t in map(lambda h: next(x for x in txs if x.hex() == h), ha)]
         assert await a.get_pending_transactions_limit(hex_only=True) == await b.get_pending_transactions_limit(hex_only=True)
+        # /get_mining_info's template: native (index) vs Python (SQL) path, whole and cut by the hex limit
+        for limit in (10 ** 9, sum(len(h) for h in ha[:4])):
+            fa, sa, ja = a.mining_template(limit, 3)
+            fb, sb, jb = b.mining_template(limit, 3)
+            assert (fa, sa, ja) == (fb, sb, jb)
+            hexes = sorted(h for h in ha if sum(len(x) for x in ha[:ha.index(h) + 1]) <= limit)
+            assert fa == hexes[:3] and json.loads(b'[' + ja + b']') == sa == [sha256(h) for h in hexes]
         want = [txs[2].hash(), txs[0].hash(), '00' * 32, 'zz']
         assert await a.get_pending_transactions_hex_by_hash(want) == await b.get_pending_transactions_hex_by_hash(want[:3])
         assert await a.get_pending_transactions_hex_by_hash([txs[1].hash()]) == [txs[1].hex()]

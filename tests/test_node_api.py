@@ -239,3 +239,15 @@ def test_block_apply_does_not_block_the_http_loop(tmp_path, monkeypatch, ledger_
         assert ledger_threads == ['upow-ledger'] and latency < 0.6, latency
     else:
         assert ledger_threads != ['upow-ledger'] and latency > 0.5, latency
+
+
+def test_request_host_locality_matches_base_url_hostname():
+    """The gate's cached Host-header test gives ``request.base_url.hostname``'s answer."""
+    from starlette.requests import Request as StarletteRequest
+    from upow_amd.node.main import _scope_host_is_local
+    from upow_amd.node.utils import ip_is_local
+    for host in (b'localhost:3006', b'127.0.0.1', b'192.168.1.7:80', b'example.org', b'8.8.8.8:3006', b'[::1]:80', None):
+        scope = {'type': 'http', 'headers': [(b'host', host)] if host else [], 'server': ('10.0.0.5', 80),
+                 'scheme': 'http', 'path': '/', 'query_string': b'', 'root_path': ''}
+        name = StarletteRequest(scope).base_url.hostname
+        assert _scope_host_is_local(scope) == (name == 'localhost' or ip_is_local(name)), host

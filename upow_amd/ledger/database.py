@@ -1387,6 +1387,18 @@ class Database:
             return return_txs
         return [await Transaction.from_hex(t, check_signatures) for t in return_txs]
 
+    def mining_template(self, limit: int = MAX_BLOCK_SIZE_HEX, head: int = 10) -> Tuple[List[str], List[str], bytes]:
+        """The next block template as ``/get_mining_info`` publishes it (reference main.py:675-695: the
+        selected pending txs sorted by hex): (first ``head`` hexes, all tx hashes, those hashes as one JSON
+        array body without brackets). From the mempool index in one native call when there is one."""
+        mp = self._mempool()
+        if mp is not None:
+            return mp.mining_template(limit, head)
+        hexes, hashes = self.pending_template(limit)
+        order = sorted(range(len(hexes)), key=hexes.__getitem__)
+        ordered_hashes = [hashes[k] for k in order]
+        return [hexes[k] for k in order[:head]], ordered_hashes, ','.join(f'"{h}"' for h in ordered_hashes).encode()
+
     def pending_template(self, limit: int = MAX_BLOCK_SIZE_HEX) -> Tuple[List[str], List[str]]:
         """(tx hex, tx hash) lists of ``get_pending_transactions_limit(hex_only=True)``; the hashes come
         from the mempool index when there is one instead of being recomputed per call."""
@@ -1764,7 +1776,14 @@ class Database:
             return dict(tip)
         return self._block_row(self._q1('SELECT * FROM blocks WHERE id = ?', (int(block_id),)))
 
+    def block_tx_hexes(self, block_hash: str) -> List[str]:
+        """The block's tx hex strings in block order (synchronous: callable from a worker thread)."""
+        return [r[0] for r in self._q('SELECT tx_hex FROM transactions WHERE block_hash = ? ORDER BY rowid',
+                                      (block_hash,))]
+
     async def get_block_transactions(self, block_hash: str, check_signatures: bool = True, hex_only: bool = False):
+        if hex_only:
+            return self.block_tx_hexes(block_hash)
         rows = self._q('SELECT tx_hex FROM transactions WHERE block_hash = ? ORDER BY rowid', (block_hash,))
         return [r['tx_hex'] if hex_only else await Transaction.from_hex(r['tx_hex'], check_signatures) for r in rows]
 

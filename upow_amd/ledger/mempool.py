@@ -80,6 +80,13 @@ class MempoolIndex:
         with self.lock:
             return self.core.hex_in_order(list(tx_hashes))
 
+    def mining_template(self, limit: int, head: int):
+        """(first ``head`` hexes, tx hashes, the hashes as a JSON array body) of the txs ``ordered``
+        selects, re-sorted by hex string as ``/get_mining_info`` publishes them."""
+        with self.lock:
+            first, hashes, frag, _ = self.core.mining_template(int(limit), int(head))
+        return first, hashes, frag
+
     def ordered_hex(self, limit: int) -> List[str]:
         return [hx for hx, _ in self.ordered(limit)]
 

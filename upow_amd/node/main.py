@@ -17,11 +17,14 @@ import os
 import random
 import re
 import sys
+import time
 from asyncio import gather
-from collections import defaultdict, deque
+from collections import OrderedDict, defaultdict, deque
 from contextlib import asynccontextmanager
+from functools import lru_cache
 from decimal import Decimal
-from typing import Annotated, Union
+from typing import Annotated, Optional, Union
+from urllib.parse import urlsplit
 
 from fastapi import Body, FastAPI, Header, Query
 from fastapi.encoders import jsonable_encoder
@@ -403,10 +406,39 @@ _SLASH_RUNS = re.compile('/+')
 def client_address(request: Request):
     """Visitor address: first X-Forwarded-For hop, else X-Real-IP (both set by the NGINX front end the
     reference documents, NGINX.md:46-58), else the socket peer."""
-    forwarded = request.headers.get('x-forwarded-for', '')
+    return _scope_client(request.scope)
+
+
+def _scope_client(scope) -> Optional[str]:
+    forwarded = real = None
+    for k, v in scope['headers']:
+        if k == b'x-forwarded-for':
+            forwarded = forwarded or v
+        elif k == b'x-real-ip':
+            real = real or v
     if forwarded:
-        return forwarded.split(',')[0].strip()
-    return request.headers.get('x-real-ip') or (request.client.host if request.client else None)
+        return forwarded.decode('latin-1').split(',')[0].strip()
+    if real:
+        return real.decode('latin-1')
+    client = scope.get('client')
+    return client[0] if client else None
+
+
+@lru_cache(maxsize=1024)
+def _host_is_local(host_header: Optional[bytes], server_host: Optional[str]) -> bool:
+    """Whether the request's host (``request.base_url.hostname``: the Host header without port and
+    brackets, else the server address) is localhost or a private address. Cached per header value: the
+    ``ipaddress`` parse and network scan would otherwise run on every request."""
+    host = urlsplit('//' + host_header.decode('latin-1')).hostname if host_header else server_host
+    return host == 'localhost' or (host is not None and ip_is_local(host))
+
+
+def _scope_host_is_local(scope) -> bool:
+    for k, v in scope['headers']:
+        if k == b'host':
+            return _host_is_local(v, None)
+    server = scope.get('server')
+    return _host_is_local(None, server[0] if server else None)
 
 
 def _deny(text: str) -> JSONResponse:
@@ -438,6 +470,7 @@ async def _join_network(request: Request, local: bool) -> None:
 # (ledger/mempool.py) and block pushes run on the ledger thread, which waits where it reads
 _ADMISSION_BATCH = os.environ.get('UPOW_ADMISSION_BATCH', '1') != '0'
 _NO_SETTLE = frozenset(('/push_tx', '/push_block'))
+_STALE_CHECK_AT = [0.0]
 
 
 class Gatekeeper:
@@ -461,7 +494,7 @@ class Gatekeeper:
             return
         request = Request(scope)
         policy = access.policy()
-        if not policy.admits(client_address(request)):
+        if not policy.admits(_scope_client(scope)):
             await _deny('Access forbidden.')(scope, receive, send)
             return
         raw_path = scope['path']
@@ -475,14 +508,19 @@ class Gatekeeper:
         sender = request.headers.get('Sender-Node')
         if sender:
             peers.book().add(sender)
-        host = request.base_url.hostname
-        local = host == 'localhost' or ip_is_local(host)
+        local = _scope_host_is_local(scope)
         if path == '/send_to_address' and not local:
             await _deny('Access forbidden. This endpoint can only be accessed from localhost.')(scope, receive, send)
             return
         if not started and path != '/get_nodes':
             await _join_network(request, local)
-        stale = await db.get_need_propagate_transactions()
+        # the reference asks on every request; an answer is only possible for txs not gossiped for
+        # 10 min, so asking at most once a second changes nothing but the per-request cost
+        stale = None
+        now = time.monotonic()
+        if now >= _STALE_CHECK_AT[0]:
+            _STALE_CHECK_AT[0] = now + 1.0
+            stale = await db.get_need_propagate_transactions()
         if path not in _NO_SETTLE:
             await db.asettle()
 
@@ -711,16 +749,12 @@ async def push_block(request: Request, background_tasks: BackgroundTasks, block_
     block_hash = sha256(block_content)
     Manager.difficulty = None
     difficulty, last_block = await get_difficulty()
-    hexes, hashes_p = db.pending_template()  # the next template, from the mempool index's keys and hashes
-    order = sorted(range(len(hexes)), key=hexes.__getitem__)
-    pending = [hexes[k] for k in order]
-    if LAST_PENDING_TRANSACTIONS_CLEAN[0] < timestamp() - 600:
-        LAST_PENDING_TRANSACTIONS_CLEAN[0] = timestamp()
-        background_tasks.add_task(on_ledger, cluster.mirror_gc, pending)
+    first, hashes_p, _ = db.mining_template()  # the next template, from the mempool index in one call
+    _mirror_gc_when_due(background_tasks)
     block_data = {'block_no': block_no, 'block_hash': block_hash, 'transactions_count': len(final_hexes),
                   'timestamp': timestamp(), 'difficulty': difficulty, 'last_block': last_block,
-                  'pending_transactions': pending[:10], 'pending_transactions_hashes': [hashes_p[k] for k in order],
-                  'merkle_root': get_transactions_merkle_tree(pending[:10])}
+                  'pending_transactions': first, 'pending_transactions_hashes': hashes_p,
+                  'merkle_root': get_transactions_merkle_tree(first)}
     background_tasks.add_task(broadcast_new_block, block_data)
     if sender:
         peers.book().seen(sender)
@@ -745,25 +779,32 @@ async def sync(request: Request, node_url: str = None):
     return {'ok': resp}
 
 
+def _mirror_gc_when_due(background_tasks: BackgroundTasks) -> None:
+    """Every 10 min, drop cluster-mirrored mempool txs that left the template (reference main.py:686-688
+    cleans the pending table on the same cadence)."""
+    if LAST_PENDING_TRANSACTIONS_CLEAN[0] < timestamp() - 600:
+        LAST_PENDING_TRANSACTIONS_CLEAN[0] = timestamp()
+        background_tasks.add_task(on_ledger, cluster.mirror_gc, sorted(db.pending_template()[0]))
+
+
+_HASHES_MARK = '@@upow-hashes@@'
+
+
 @app.get('/get_mining_info')
 @limiter.limit('30/minute')
 async def get_mining_info(request: Request, background_tasks: BackgroundTasks):
-    """main.py:675-695."""
+    """main.py:675-695. The template comes from the mempool index in one native call (selection, hex
+    order, hash strings and their JSON array); only the small fields go through the generic encoder."""
     Manager.difficulty = None
     difficulty, last_block = await get_difficulty()
-    hexes, hashes = db.pending_template()
-    order = sorted(range(len(hexes)), key=hexes.__getitem__)  # the reference sorts the hex strings
-    pending = [hexes[k] for k in order]
-    if LAST_PENDING_TRANSACTIONS_CLEAN[0] < timestamp() - 600:
-        LAST_PENDING_TRANSACTIONS_CLEAN[0] = timestamp()
-        background_tasks.add_task(on_ledger, cluster.mirror_gc, pending)
-    # the framework's generic encoder walks every element of the 10k-entry hash list; only the small
-    # fields need it (Decimal difficulty, block dict)
-    head = jsonable_encoder({'difficulty': difficulty, 'last_block': last_block})
-    return JSONResponse({'ok': True, 'result': {
-        'difficulty': head['difficulty'], 'last_block': head['last_block'], 'pending_transactions': pending[:10],
-        'pending_transactions_hashes': [hashes[k] for k in order],
-        'merkle_root': get_transactions_merkle_tree(pending[:10])}})
+    first, _, hashes_json = db.mining_template()
+    _mirror_gc_when_due(background_tasks)
+    head = jsonable_encoder({'ok': True, 'result': {
+        'difficulty': difficulty, 'last_block': last_block, 'pending_transactions': first,
+        'pending_transactions_hashes': _HASHES_MARK, 'merkle_root': get_transactions_merkle_tree(first)}})
+    doc = json.dumps(head, ensure_ascii=False, allow_nan=False, separators=(',', ':')).encode()
+    body = doc.replace(f'"{_HASHES_MARK}"'.encode(), b'[' + hashes_json + b']', 1)
+    return Response(content=body, media_type='application/json')
 
 
 @app.get('/get_validators_info')
@@ -918,6 +959,28 @@ async def _resolve_block(block: str):
     return block, await db.get_block(block)
 
 
+_BLOCK_BODIES: 'OrderedDict[str, bytes]' = OrderedDict()
+_BLOCK_BODIES_KEEP = 8
+
+
+def _block_body(block_hash: str, block_info: dict):
+    """The ``/get_block`` document of a block (hex strings need no escaping: joined into the document
+    instead of walked by the generic encoder). A block's content never changes under its hash, so the
+    last few documents are kept: every peer and explorer asks for the new tip."""
+    txs = db.block_tx_hexes(block_hash)
+    if not all(t.isalnum() for t in txs):
+        return None
+    mark = '"@@upow-txs@@"'
+    head = json.dumps(jsonable_encoder({'ok': True, 'result': {
+        'block': block_info, 'transactions': '@@upow-txs@@', 'full_transactions': None}}),
+        ensure_ascii=False, allow_nan=False, separators=(',', ':'))
+    body = head.replace(mark, '["' + '","'.join(txs) + '"]' if txs else '[]', 1).encode()
+    _BLOCK_BODIES[block_hash] = body
+    while len(_BLOCK_BODIES) > _BLOCK_BODIES_KEEP:
+        _BLOCK_BODIES.popitem(last=False)
+    return body
+
+
 @app.get('/get_block')
 @limiter.limit('30/minute')
 async def get_block(request: Request, block: str, full_transactions: bool = False):
@@ -925,15 +988,12 @@ async def get_block(request: Request, block: str, full_transactions: bool = Fals
     if not block_info:
         return {'ok': False, 'error': 'Block not found'}
     if not full_transactions:
-        # a full block is ~8k hex strings (4 MB of JSON): they need no escaping, so the list is joined
-        # into the document directly instead of walked by the generic encoder on the event loop
-        txs = await db.get_block_transactions(block_hash, hex_only=True)
-        if all(t.isalnum() for t in txs):
-            mark = '"@@upow-txs@@"'
-            head = json.dumps(jsonable_encoder({'ok': True, 'result': {
-                'block': block_info, 'transactions': '@@upow-txs@@', 'full_transactions': None}}),
-                ensure_ascii=False, allow_nan=False, separators=(',', ':'))
-            body = head.replace(mark, '[' + ','.join(f'"{t}"' for t in txs) + ']', 1)
+        body = _BLOCK_BODIES.get(block_hash)
+        if body is None:
+            # a full block is ~8k hex strings (4 MB of JSON): read and joined on a worker thread (the
+            # read waits for the ledger's connection, which a block apply holds), never on the loop
+            body = await asyncio.to_thread(_block_body, block_hash, block_info)
+        if body is not None:
             return Response(content=body, media_type='application/json')
     return {'ok': True, 'result': {
         'block': block_info,
