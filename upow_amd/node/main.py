@@ -54,7 +54,7 @@ from ..utils import codec
 from ..utils.codec import sha256, timestamp
 from ..utils.logger import get_logger
 from ..websocket.endpoint import (broadcast_new_block, broadcast_new_transaction, router as websocket_router,
-                                  shutdown_websocket_manager, start_websocket_manager)
+                                  shutdown_websocket_manager, start_websocket_manager, transaction_listeners)
 from .access import AccessControl
 from . import peers
 from .peers import PeerClient
@@ -632,10 +632,11 @@ async def verify_and_push_tx(tx: Transaction, request: Request, background_tasks
             if 'Sender-Node' in request.headers:
                 peers.book().seen(request.headers['Sender-Node'])
             background_tasks.add_task(propagate, 'push_tx', {'tx_hex': tx.hex()})
-            tx_data = {'tx_hash': tx_hash, 'from': await tx.inputs[0].get_address() if tx.inputs else None,
-                       'to': [o.address for o in tx.outputs], 'amount': sum(o.amount for o in tx.outputs),
-                       'fees': tx.fees}
-            background_tasks.add_task(broadcast_new_transaction, tx_data)
+            if transaction_listeners():  # the event is only built for subscribed /ws sessions
+                tx_data = {'tx_hash': tx_hash, 'from': await tx.inputs[0].get_address() if tx.inputs else None,
+                           'to': [o.address for o in tx.outputs], 'amount': sum(o.amount for o in tx.outputs),
+                           'fees': tx.fees}
+                background_tasks.add_task(broadcast_new_transaction, tx_data)
             transactions_cache.append(tx_hash)
             logger.info(f'Transaction has been accepted: {tx_hash}')
             return {'ok': True, 'result': 'Transaction has been accepted', 'tx_hash': tx_hash}

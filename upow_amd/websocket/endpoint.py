@@ -23,6 +23,10 @@ async def broadcast_new_block(block_data: dict, background_tasks=None) -> int:
     return n
 
 
+def transaction_listeners() -> bool:
+    return hub.listening('transaction')
+
+
 async def broadcast_new_transaction(tx_data: dict, background_tasks=None) -> int:
     return hub.publish('transaction', 'new_transaction', tx_data)
 

@@ -76,6 +76,10 @@ class Hub:
         return True
 
     # ------------------------------------------------------------------ fan-out
+    def listening(self, channel: str) -> bool:
+        """Whether any session is subscribed to ``channel`` (callers skip building unsent events)."""
+        return bool(self.members.get(channel))
+
     def publish(self, channel: str, kind: str, data: Any) -> int:
         """Queue ``{"type": kind, "data": data}`` for every member of ``channel``; returns how many
         sessions accepted it. Never awaits a client."""
