@@ -10,6 +10,10 @@
 // parser returns whole frames, unmasked.
 #include <pybind11/pybind11.h>
 
+#include <sys/socket.h>
+
+#include <cerrno>
+
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -341,6 +345,21 @@ void register_http_wire(py::module_& m) {
         .def("need_continue", &HttpParser::need_continue)
         .def("ack_continue", &HttpParser::ack_continue)
         .def("rest", &HttpParser::rest);
+    // One non-blocking send WITH the GIL held: a response of a few hundred bytes is one syscall of
+    // microseconds, while socket.send() releases the GIL around it and the event loop then waits to get it
+    // back from whichever thread took it (a wake-up on a loaded host). Returns the bytes sent (0 when the
+    // socket buffer is full) or -errno; the caller hands any rest to the transport.
+    m.def("send_now", [](int fd, py::buffer data) -> int64_t {
+        py::buffer_info bi = data.request();
+        const size_t n = size_t(bi.size * bi.itemsize);
+        for (;;) {
+            const ssize_t w = ::send(fd, bi.ptr, n, MSG_DONTWAIT | MSG_NOSIGNAL);
+            if (w >= 0) return int64_t(w);
+            if (errno == EINTR) continue;
+            if (errno == EAGAIN || errno == EWOULDBLOCK) return 0;
+            return -int64_t(errno);
+        }
+    });
     py::class_<WsParser>(m, "WsParser")
         .def(py::init<int64_t>(), py::arg("max_payload") = int64_t(16) << 20)
         .def("feed", &WsParser::feed, "complete client frames: (fin, opcode, unmasked payload)");

@@ -61,6 +61,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <optional>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -240,6 +241,18 @@ const int64_t* row_selection(py::handle h, int64_t n) {
     return sel;
 }
 
+// Column copies of a block (megabytes, often on the encode pool's threads) run without the GIL so the
+// HTTP event loop thread never waits for them. A /push_tx admission encodes a row or two on the loop
+// thread itself: releasing there would hand the GIL to whichever thread is runnable (the ledger thread
+// during a block) and make the loop wait for it back, so small columns keep it.
+constexpr int64_t kNoGilRows = 256;
+struct NoGilIfLarge {
+    std::optional<py::gil_scoped_release> rel;
+    explicit NoGilIfLarge(int64_t rows) {
+        if (rows >= kNoGilRows) rel.emplace();
+    }
+};
+
 void encode_col(Out& o, py::handle spec, int64_t n) {
     if (spec.is_none()) {
         o.u8(K_NULL);
@@ -256,7 +269,7 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
         if (int64_t(ptr.size()) != n) throw std::invalid_argument("text column length != n");
         // the row copies run without the GIL (the caller's list keeps every str alive): a block's
         // columns are megabytes, and the HTTP event loop thread must not wait for them
-        py::gil_scoped_release nogil;
+        NoGilIfLarge nogil(n);
         encode_text_rows(o, n, ptr, len, nullptr);
     } else if (py::isinstance<py::tuple>(spec)) {
         py::tuple t = spec.cast<py::tuple>();
@@ -271,7 +284,7 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
             const int32_t* idx = static_cast<const int32_t*>(bi.ptr);
             for (int64_t i = 0; i < n; ++i)
                 if (idx[i] < 0 || size_t(idx[i]) >= ptr.size()) throw std::out_of_range("gather index");
-            py::gil_scoped_release nogil;
+            NoGilIfLarge nogil(n);
             encode_text_rows(o, n, ptr, len, idx);
         } else if (tag == "hex32") {
             // ('hex32', raw, stride, offset[, sel int64[n]]): 32 raw bytes per row, optionally rows sel of raw
@@ -287,7 +300,7 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
             if (offset < 0 || stride < 0 || (n > 0 && top * stride + offset + 32 > raw_n))
                 throw std::out_of_range("hex32 column out of range");
             o.u8(K_HEX32);
-            py::gil_scoped_release nogil;
+            NoGilIfLarge nogil(n);
             o.b.reserve(o.b.size() + size_t(n) * 32);
             for (int64_t r = 0; r < n; ++r) o.raw(raw + (sel ? sel[r] : r) * stride + offset, 32);
         } else if (tag == "arena" || tag == "hexarena") {
@@ -311,7 +324,7 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
             } else {
                 o.u8(K_HEXTEXT);
             }
-            py::gil_scoped_release nogil;
+            NoGilIfLarge nogil(n);
             std::vector<int64_t> off(size_t(n) + 1);
             if (!sel) {
                 for (int64_t i = 0; i <= n; ++i) off[size_t(i)] = aoff[i] - aoff[0];
@@ -332,7 +345,7 @@ void encode_col(Out& o, py::handle spec, int64_t n) {
             throw std::invalid_argument("integer column must be int64");
         if (bi.size != n) throw std::invalid_argument("int column length != n");
         o.u8(K_INT64);
-        py::gil_scoped_release nogil;
+        NoGilIfLarge nogil(n);
         o.raw(bi.ptr, size_t(n) * 8);
     }
 }
@@ -1724,10 +1737,14 @@ void register_ledger_writer(py::module_& m) {
                      mparts.emplace_back(static_cast<const char*>(keep.back().ptr),
                                          size_t(keep.back().size * keep.back().itemsize));
                  }
-                 py::gil_scoped_release nogil;
-                 std::string m;
                  size_t total = 0;
                  for (auto& pr : mparts) total += pr.second;
+                 // a write-behind mempool record only reserves a sequence number and queues: keep the GIL
+                 // (see NoGilIfLarge); a block record may wait for writer backpressure and a synced one
+                 // for its write, both without the GIL
+                 std::optional<py::gil_scoped_release> nogil;
+                 if (sync || block_id >= 0 || total >= (size_t(1) << 16)) nogil.emplace();
+                 std::string m;
                  m.reserve(total);
                  for (auto& pr : mparts) m.append(pr.first, pr.second);
                  return w.submit(std::move(v), std::move(m), block_id, sync);

@@ -36,6 +36,11 @@ async def stream(request):
     return StreamingResponse(gen())
 
 
+async def big(request):
+    n = int(request.query_params['n'])
+    return PlainTextResponse(bytes(range(97, 123)) * (n // 26) + b'z' * (n % 26))
+
+
 async def ws_echo(websocket):
     await websocket.accept()
     while True:
@@ -51,7 +56,7 @@ async def ws_echo(websocket):
             await websocket.send_bytes(b'echo:' + msg['bytes'])
 
 
-app = Starlette(routes=[Route('/hello', hello), Route('/echo', echo, methods=['POST']), Route('/stream', stream),
+app = Starlette(routes=[Route('/hello', hello), Route('/echo', echo, methods=['POST']), Route('/stream', stream), Route('/big', big),
                         WebSocketRoute('/ws', ws_echo)])
 
 
@@ -175,3 +180,26 @@ def test_websocket_upgrade_echo_fragments_ping_close(server):
         c.sendall(_ws_frame(1, b'bye'))
         op, data = _ws_read(c)
         assert op == 8 and struct.unpack('!H', data[:2])[0] == 4000
+
+
+def test_large_response_to_a_slow_reader_arrives_whole(server):
+    """A response larger than the socket buffer: the GIL-held direct send takes what fits and the
+    transport sends the rest in order, also with a second response pipelined behind it."""
+    n = 12 * 1024 * 1024
+    partial = NodeHttpProtocol.partial_sends
+    with socket.create_connection(('127.0.0.1', server), timeout=10) as c:
+        c.sendall(b'GET /big?n=%d HTTP/1.1\r\nhost: x\r\n\r\nGET /big?n=30 HTTP/1.1\r\nhost: x\r\nconnection: close\r\n\r\n' % n)
+        time.sleep(0.3)  # let the server fill the socket buffer first
+        out = bytearray()
+        while True:
+            chunk = c.recv(1 << 16)
+            if not chunk:
+                break
+            out += chunk
+    want = bytes(range(97, 123)) * (n // 26) + b'z' * (n % 26)
+    head, rest = bytes(out).split(b'\r\n\r\n', 1)
+    assert b'content-length: %d' % n in head.lower()
+    assert rest[:n] == want
+    head2, body2 = rest[n:].split(b'\r\n\r\n', 1)
+    assert head2.startswith(b'HTTP/1.1 200') and body2 == bytes(range(97, 123)) + b'zzzz'
+    assert NodeHttpProtocol.partial_sends > partial

@@ -1678,6 +1678,10 @@ class Database:
 
     async def get_pending_transactions_hex_by_hash(self, hashes: List[str]) -> List[str]:
         """tx hex of the pending txs among ``hashes``, in mempool (table) order like database.py:297-301."""
+        return self.pending_hex_by_hash(hashes)
+
+    def pending_hex_by_hash(self, hashes: List[str]) -> List[str]:
+        """Synchronous :meth:`get_pending_transactions_hex_by_hash` (callable from a worker thread)."""
         if not hashes:
             return []
         mp = self._mempool()

@@ -26,6 +26,7 @@ import base64
 import hashlib
 import http
 import logging
+import os
 import struct
 import urllib.parse
 from collections import deque
@@ -36,6 +37,7 @@ from uvicorn.protocols.utils import get_local_addr, get_remote_addr, is_ssl
 
 from ..ops.native import lib
 
+_SEND_NOW = os.environ.get('UPOW_HTTP_SEND_NOW', '1') != '0'
 _WS_GUID = b'258EAFA5-E914-47DA-95CA-C5AB0DC85B11'
 _STATUS = {}
 
@@ -177,7 +179,7 @@ class _Cycle:
             if body:
                 out.append(body)
         if out:
-            p.transport.write(out[0] if len(out) == 1 else b''.join(out))
+            p.write(out[0] if len(out) == 1 else b''.join(out))
         if not more:
             if not self.head and not self.chunked and self.remaining:
                 raise RuntimeError('Response content shorter than Content-Length')
@@ -378,8 +380,11 @@ class NodeHttpProtocol(asyncio.Protocol):
         self.queue: deque = deque()  # pipelined requests waiting for the current response
         self.ws: Optional[_WebSocket] = None
         self.ka_timer = None
+        self.fd = -1
 
     # -- asyncio.Protocol
+    partial_sends = 0  # direct sends the transport had to finish (tests)
+
     def connection_made(self, transport):
         self.connections.add(self)
         self.transport = transport
@@ -387,6 +392,22 @@ class NodeHttpProtocol(asyncio.Protocol):
         self.server = get_local_addr(transport)
         self.client = get_remote_addr(transport)
         self.scheme = 'https' if is_ssl(transport) else 'http'
+        sock = transport.get_extra_info('socket')
+        self.fd = sock.fileno() if sock is not None and self.scheme == 'http' and _SEND_NOW else -1
+
+    def write(self, data: bytes) -> None:
+        """A response's bytes: sent at once from the loop thread without releasing the GIL while the
+        transport has nothing queued (``send_now``), the rest (a full socket buffer, an error to report)
+        through the transport, which keeps the order and the flow control."""
+        t = self.transport
+        if self.fd >= 0 and not t.get_write_buffer_size() and not t.is_closing():
+            n = lib().send_now(self.fd, data)
+            if n == len(data):
+                return
+            NodeHttpProtocol.partial_sends += 1
+            if n > 0:
+                data = memoryview(data)[n:]
+        t.write(data)
 
     def connection_lost(self, exc):
         self.connections.discard(self)

@@ -736,7 +736,8 @@ async def push_block(request: Request, background_tasks: BackgroundTasks, block_
         else:
             final_hexes.append(tx_hex)
     if hashes:
-        pending_hexes = await db.get_pending_transactions_hex_by_hash(hashes)
+        # on a worker thread: the mempool index lock may be held by a block confirm on the ledger thread
+        pending_hexes = await asyncio.to_thread(db.pending_hex_by_hash, hashes)
         if len(pending_hexes) < len(hashes):
             if sender:
                 background_tasks.add_task(sync_blockchain, sender)
@@ -750,7 +751,9 @@ async def push_block(request: Request, background_tasks: BackgroundTasks, block_
     block_hash = sha256(block_content)
     Manager.difficulty = None
     difficulty, last_block = await get_difficulty()
-    first, hashes_p, _ = db.mining_template()  # the next template, from the mempool index in one call
+    # the next template, from the mempool index in one call, on a worker thread: the index lock may be held
+    # by the ledger thread confirming a block, and the event loop must not wait for it
+    first, hashes_p, _ = await asyncio.to_thread(db.mining_template)
     _mirror_gc_when_due(background_tasks)
     block_data = {'block_no': block_no, 'block_hash': block_hash, 'transactions_count': len(final_hexes),
                   'timestamp': timestamp(), 'difficulty': difficulty, 'last_block': last_block,
@@ -798,7 +801,7 @@ async def get_mining_info(request: Request, background_tasks: BackgroundTasks):
     order, hash strings and their JSON array); only the small fields go through the generic encoder."""
     Manager.difficulty = None
     difficulty, last_block = await get_difficulty()
-    first, _, hashes_json = db.mining_template()
+    first, _, hashes_json = await asyncio.to_thread(db.mining_template)  # off the loop: see push_block
     _mirror_gc_when_due(background_tasks)
     head = jsonable_encoder({'ok': True, 'result': {
         'difficulty': difficulty, 'last_block': last_block, 'pending_transactions': first,
