@@ -60,6 +60,16 @@ with open(src + '.out', 'w') as f:
 '''
 
 
+def _jsonl(path: str):
+    """The records of a JSON-lines trace file; a line cut short (the node was stopped mid-write) is skipped."""
+    with open(path) as f:
+        for ln in f:
+            try:
+                yield json.loads(ln)
+            except ValueError:
+                continue
+
+
 def _cpu_stat() -> dict:
     """The cgroup's CPU accounting (cgroup v2 cpu.stat): usage and CFS bandwidth throttling. A GPU box
     runs the job under a CPU quota far below its core count; a throttled period freezes every thread of the
@@ -318,8 +328,7 @@ def main():
     # /push_tx request latency, overall and for requests that overlapped a block application
     windows = []
     if os.path.exists(trace):
-        for ln in open(trace):
-            r = json.loads(ln)
+        for r in _jsonl(trace):
             if r.get('ok') and r.get('txs', 0) > 0:
                 windows.append((r['t'] - r['ms'] / 1000.0, r['t']))
     windows.sort()
@@ -329,16 +338,14 @@ def main():
     # where the HTTP loop stalled (node's UPOW_TRACE_FILE.lag) and what the block path spent its time on
     stalls = []
     if os.path.exists(trace + '.lag'):
-        for ln in open(trace + '.lag'):
-            r = json.loads(ln)
+        for r in _jsonl(trace + '.lag'):
             if t0 <= r['t'] <= t_push_end:
                 stalls.append((r['t'] - r['ms'] / 1000.0, r['t'], r['ms']))
     in_blk = [s for s in stalls if overlaps(s[0], s[1])]
     stack_counts = {}
     other_counts = {}  # what the node's other Python threads were executing during loop stalls
     if os.path.exists(trace + '.stacks'):
-        for ln in open(trace + '.stacks'):
-            r = json.loads(ln)
+        for r in _jsonl(trace + '.stacks'):
             if t0 <= r['t'] <= t_push_end:
                 key = ' < '.join(reversed(r['stack'][-3:]))
                 stack_counts[key] = stack_counts.get(key, 0) + 1
@@ -351,14 +358,12 @@ def main():
     top_others = sorted(other_counts.items(), key=lambda kv: -kv[1])[:12]
     gcs = []
     if os.path.exists(trace + '.gc'):
-        for ln in open(trace + '.gc'):
-            r = json.loads(ln)
+        for r in _jsonl(trace + '.gc'):
             if t0 <= r['t'] <= t_push_end:
                 gcs.append(r)
     stages = {}
     if os.path.exists(trace):
-        for ln in open(trace):
-            r = json.loads(ln)
+        for r in _jsonl(trace):
             if r.get('ok') and r.get('txs', 0) > 0:
                 for k, v in r.get('stages_ms', {}).items():
                     stages.setdefault(k, []).append(v)
