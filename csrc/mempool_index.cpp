@@ -109,6 +109,7 @@ struct Entry {
     uint64_t order = 0;  // admission order (the table's row order)
     int64_t fee = 0;     // 1e-8 units
     py::object hex;      // the tx hex str (kept as the object the caller gave: no copy out)
+    const char* hp = nullptr;  // its UTF-8 bytes (owned by `hex`): ordering reads them without the GIL
     int64_t len = 0;
 };
 
@@ -152,35 +153,48 @@ public:
 
     // (tx hex, raw hash) in block-template order, up to `limit` hex characters in total
     py::list ordered(int64_t limit) const {
+        std::vector<std::pair<const H32*, const Entry*>> v;
+        {
+            py::gil_scoped_release nogil;  // callers hold the index lock: no entry changes meanwhile
+            v = select(limit);
+        }
         py::list out;
-        for (auto& p : select(limit))
+        for (auto& p : v)
             out.append(py::make_tuple(p.second->hex, py::bytes(reinterpret_cast<const char*>(p.first->data()), 32)));
         return out;
     }
 
     // the mining template of /get_mining_info and the new-block event (reference main.py:675-695): the
     // selected txs re-sorted by hex string; returns (first `head` hexes, all tx hashes as hex strs, the
-    // same hashes as one JSON array body `"h0","h1",...` for the response, count)
+    // same hashes as one JSON array body `"h0","h1",...` for the response, count). Selection, sorts and
+    // text run without the GIL (the caller holds the index lock); only the result objects need it.
     py::tuple mining_template(int64_t limit, int64_t head) const {
-        auto v = select(limit);
-        std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return hex_less(a.second->hex, b.second->hex); });
-        static const char* digits = "0123456789abcdef";
+        std::vector<std::pair<const H32*, const Entry*>> v;
+        std::string frag, hx;
+        {
+            py::gil_scoped_release nogil;
+            v = select(limit);
+            std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return hex_less(*a.second, *b.second); });
+            static const char* digits = "0123456789abcdef";
+            hx.resize(v.size() * 64);
+            frag.reserve(v.size() * 67);
+            for (size_t k = 0; k < v.size(); ++k) {
+                const uint8_t* d = v[k].first->data();
+                char* h = &hx[k * 64];
+                for (int j = 0; j < 32; ++j) {
+                    h[2 * j] = digits[d[j] >> 4];
+                    h[2 * j + 1] = digits[d[j] & 15];
+                }
+                if (k) frag.push_back(',');
+                frag.push_back('"');
+                frag.append(h, 64);
+                frag.push_back('"');
+            }
+        }
         py::list first, hashes;
-        std::string frag;
-        frag.reserve(v.size() * 67);
-        char h[64];
         for (size_t k = 0; k < v.size(); ++k) {
             if (int64_t(k) < head) first.append(v[k].second->hex);
-            const uint8_t* d = v[k].first->data();
-            for (int j = 0; j < 32; ++j) {
-                h[2 * j] = digits[d[j] >> 4];
-                h[2 * j + 1] = digits[d[j] & 15];
-            }
-            hashes.append(py::str(h, 64));
-            if (k) frag.push_back(',');
-            frag.push_back('"');
-            frag.append(h, 64);
-            frag.push_back('"');
+            hashes.append(py::str(hx.data() + k * 64, 64));
         }
         return py::make_tuple(first, hashes, py::bytes(frag), v.size());
     }
@@ -298,7 +312,7 @@ private:
             const __int128 l = __int128(x.fee) * y.len, r = __int128(y.fee) * x.len;
             if (l != r) return l > r;  // higher fee density first
             if (x.len != y.len) return x.len < y.len;
-            return hex_less(x.hex, y.hex);
+            return hex_less(x, y);
         });
         int64_t size = 0;
         size_t n = 0;
@@ -310,13 +324,10 @@ private:
         return v;
     }
 
-    static bool hex_less(const py::object& a, const py::object& b) {
-        Py_ssize_t na = 0, nb = 0;
-        const char* pa = PyUnicode_AsUTF8AndSize(a.ptr(), &na);
-        const char* pb = PyUnicode_AsUTF8AndSize(b.ptr(), &nb);
-        if (!pa || !pb) return false;
-        const int c = std::memcmp(pa, pb, size_t(std::min(na, nb)));
-        return c < 0 || (c == 0 && na < nb);
+    // tx hex strings are ASCII: UTF-8 length == character length
+    static bool hex_less(const Entry& a, const Entry& b) {
+        const int c = std::memcmp(a.hp, b.hp, size_t(std::min(a.len, b.len)));
+        return c < 0 || (c == 0 && a.len < b.len);
     }
 
     void add_entry(const H32& h, int64_t ptime, py::object hex, const std::string& fees, int64_t seq) {
@@ -326,8 +337,9 @@ private:
         e.order = next_order_++;
         e.fee = fee_units(fees);
         Py_ssize_t n = 0;
-        if (!PyUnicode_Check(hex.ptr()) || !PyUnicode_AsUTF8AndSize(hex.ptr(), &n))
-            throw std::invalid_argument("tx hex must be str");
+        const char* hp = PyUnicode_Check(hex.ptr()) ? PyUnicode_AsUTF8AndSize(hex.ptr(), &n) : nullptr;
+        if (!hp) throw std::invalid_argument("tx hex must be str");
+        e.hp = hp;
         e.len = int64_t(PyUnicode_GET_LENGTH(hex.ptr()));
         e.hex = std::move(hex);
         txs_[h] = std::move(e);
