@@ -203,3 +203,16 @@ def test_large_response_to_a_slow_reader_arrives_whole(server):
     head2, body2 = rest[n:].split(b'\r\n\r\n', 1)
     assert head2.startswith(b'HTTP/1.1 200') and body2 == bytes(range(97, 123)) + b'zzzz'
     assert NodeHttpProtocol.partial_sends > partial
+
+
+def test_client_gone_before_the_response_leaves_the_server_serving(server):
+    """A client that closes (with a reset) before its response is written: the direct send fails, the
+    transport reports the error and drops the connection, and the server keeps answering others."""
+    for _ in range(3):
+        c = socket.create_connection(('127.0.0.1', server), timeout=5)
+        c.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack('ii', 1, 0))  # close = RST
+        c.sendall(b'GET /big?n=4000000 HTTP/1.1\r\nhost: x\r\n\r\n')
+        c.close()
+    time.sleep(0.2)
+    r = httpx.get(f'http://127.0.0.1:{server}/hello', params={'q': 'still'}, timeout=5)
+    assert r.status_code == 200 and r.json()['q'] == 'still'
