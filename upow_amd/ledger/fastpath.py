@@ -127,6 +127,21 @@ def _signer_records_general(pay, out_addr, out_len, job_input, sigs, sig_ids, di
     return np.ascontiguousarray(np.concatenate([xy[job_input], sigs[sig_ids], digest[job_tx]], axis=1)).tobytes()
 
 
+def _with_signers(pay: np.ndarray, signers: dict) -> np.ndarray:
+    """``pay`` with the address of each input in ``signers`` ({input index: address bytes}) replaced:
+    one scatter per address length instead of three numpy calls per input."""
+    out = pay.copy()
+    js = np.fromiter(signers.keys(), dtype=np.int64, count=len(signers))
+    raws = list(signers.values())
+    lens = np.fromiter(map(len, raws), dtype=np.int64, count=len(raws))
+    out['addr'][js] = 0
+    for n in np.unique(lens).tolist():
+        sel = np.nonzero(lens == n)[0]
+        out['addr'][js[sel], :n] = np.frombuffer(b''.join(raws[k] for k in sel.tolist()), dtype=np.uint8).reshape(-1, n)
+        out['len'][js[sel]] = n
+    return out
+
+
 async def create_block_from_hex(block_content: str, tx_hexes: List[str], error_list: list = None,
                                 last_block: dict = None, coinbase=None, mirror: bool = True,
                                 decoded: Optional[dict] = None) -> bool:
@@ -266,11 +281,7 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         if gres is None:
             return None
         if gres['signers']:
-            sig_pay = pay.copy()
-            for j, raw in gres['signers'].items():
-                sig_pay['addr'][j] = 0
-                sig_pay['addr'][j, :len(raw)] = np.frombuffer(raw, dtype=np.uint8)
-                sig_pay['len'][j] = len(raw)
+            sig_pay = _with_signers(pay, gres['signers'])
     t_gov = perf_counter()
     roctx.pop()
     roctx.push('block:signer_records')
