@@ -32,6 +32,12 @@ public:
         open_file();
         thread_ = std::thread([this] { run(); });
     }
+    // an already open descriptor (the process's stderr, dup'ed: its file offset is shared, so lines never
+    // overwrite what other code writes to fd 2); no rotation
+    explicit LogAppender(int fd) : max_bytes_(0), backups_(0), fd_(fd) {
+        if (fd_ < 0) throw std::runtime_error("log appender: bad descriptor");
+        thread_ = std::thread([this] { run(); });
+    }
     ~LogAppender() { close(); }
 
     void write(const char* p, size_t n) {
@@ -168,6 +174,7 @@ private:
 void register_log_appender(py::module_& m) {
     py::class_<LogAppender>(m, "LogAppender")
         .def(py::init<std::string, int64_t, int>(), py::arg("path"), py::arg("max_bytes"), py::arg("backups"))
+        .def(py::init<int>(), py::arg("fd"))
         .def("write",
              [](LogAppender& a, py::str s) {
                  Py_ssize_t n = 0;

@@ -33,3 +33,19 @@ def test_native_handler_format_matches_formatter(tmp_path):
     h.flush()
     h.close()
     assert open(tmp_path / 'a.log').read() == fmt.format(rec) + '\n'
+
+
+def test_descriptor_appender_shares_the_offset_with_direct_writes(tmp_path):
+    """The console appender writes through a dup of the descriptor: lines written directly to the
+    original fd before and after land after them, never over them."""
+    path = str(tmp_path / 'console.txt')
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)  # no O_APPEND, like a shell redirect
+    os.write(fd, b'first\n')
+    app = lib().LogAppender(os.dup(fd))
+    for i in range(100):
+        app.write(f'rec {i}\n')
+    app.flush()
+    os.write(fd, b'last\n')
+    app.close()
+    os.close(fd)
+    assert open(path).read() == 'first\n' + ''.join(f'rec {i}\n' for i in range(100)) + 'last\n'

@@ -47,6 +47,12 @@ def _configure():
         if native is not None:
             fh.close()
             logger.addHandler(native)
+            # the console too: a synchronous write + flush of stderr per INFO line releases the GIL on the
+            # HTTP loop thread at every /push_tx; the same writer thread batches them instead
+            native_console = _native_console(fmt, console.level)
+            if native_console is not None:
+                logger.removeHandler(console)
+                logger.addHandler(native_console)
             return
         # no native library: formatting and file I/O on a listener thread
         import atexit
@@ -107,6 +113,26 @@ def _native_handler(path: str, fmt: logging.Formatter):
         return None
     import atexit
     h = NativeFileHandler(app, fmt)
+    atexit.register(h.close)
+    return h
+
+
+def _native_console(fmt: logging.Formatter, level: int):
+    if os.environ.get('UPOW_NATIVE_LOG', '1') == '0' or os.environ.get('UPOW_NATIVE_CONSOLE', '1') == '0':
+        return None
+    try:
+        from ..ops.native import lib
+        fd = os.dup(sys.stderr.fileno())
+    except Exception:
+        return None
+    try:
+        app = lib().LogAppender(fd)
+    except Exception:
+        os.close(fd)
+        return None
+    import atexit
+    h = NativeFileHandler(app, fmt)
+    h.setLevel(level)
     atexit.register(h.close)
     return h
 
