@@ -108,9 +108,7 @@ def bench_verify(args, ctx):
     return run_cluster_verify_bench(args, ctx) if ctx.is_distributed else run_verify_bench(args, ctx)
 
 
-def _verify_side_metrics(args, ctx) -> dict:
-    """BASELINE metric 2 next to the hashrate: ``--verify-steps`` timed 2 MB blocks (+2 warmup) through the
-    native push_block path on this rank's GPU, file-backed ledger in a temporary directory."""
+def _verify_once(args, ctx, keys: str) -> dict:
     import shutil
     import tempfile
     from upow_amd.bench_verify import run_cluster_verify_bench, run_verify_bench
@@ -118,17 +116,30 @@ def _verify_side_metrics(args, ctx) -> dict:
     try:
         v = argparse.Namespace(**{**vars(args), 'steps': args.verify_steps, 'warmup': 2, 'ledger': tmp,
                                   'object_path': False, 'from_mempool': False, 'governance': False,
-                                  'governance_txs': 0.0, 'age_txs': 0})
-        r = run_cluster_verify_bench(v, ctx) if ctx.is_distributed else run_verify_bench(v, ctx)
+                                  'governance_txs': 0.0, 'age_txs': 0, 'keys': keys})
+        return run_cluster_verify_bench(v, ctx) if ctx.is_distributed else run_verify_bench(v, ctx)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    return {'verify_tx_per_s': r['value'], 'verify_ms_per_block': r['ms_per_step'],
-            'verify_commit_latency_ms': r['commit_latency_ms'], 'validate_tx_per_s': r['validate_tx_per_s'],
-            'ecdsa_sig_per_s': r['ecdsa_sig_per_s'],
-            'verify_config': {'metric': r['metric'], 'unit': r['unit'], 'steps': args.verify_steps, 'warmup': 2,
-                              'txs_per_block': r['config']['seq_len'], 'ledger': r['config']['ledger'],
-                              'block_path': r['config']['block_path'], 'scaling': r['scaling'],
-                              'layout': r['config']['parallelism'], 'data': r['data']}}
+
+
+def _verify_side_metrics(args, ctx) -> dict:
+    """BASELINE metric 2 next to the hashrate: ``--verify-steps`` timed 2 MB blocks (+2 warmup) through the
+    native push_block path on this rank's GPU, file-backed ledger in a temporary directory. The reported
+    number uses distinct keys (a fresh key pair per tx, fresh output addresses: BASELINE's random-keypair
+    data); the 256-key pool run follows as a labelled second number (``verify_pool256_*``)."""
+    r = _verify_once(args, ctx, 'distinct')
+    out = {'verify_tx_per_s': r['value'], 'verify_ms_per_block': r['ms_per_step'],
+           'verify_commit_latency_ms': r['commit_latency_ms'], 'validate_tx_per_s': r['validate_tx_per_s'],
+           'ecdsa_sig_per_s': r['ecdsa_sig_per_s'], 'verify_stage_ms_avg': r['stage_ms_avg'],
+           'verify_config': {'metric': r['metric'], 'unit': r['unit'], 'steps': args.verify_steps, 'warmup': 2,
+                             'txs_per_block': r['config']['seq_len'], 'ledger': r['config']['ledger'],
+                             'block_path': r['config']['block_path'], 'scaling': r['scaling'],
+                             'layout': r['config']['parallelism'], 'keys': 'distinct', 'data': r['data']}}
+    if args.verify_pool256:
+        p = _verify_once(args, ctx, 'pool256')
+        out.update({'verify_pool256_tx_per_s': p['value'], 'verify_pool256_ms_per_block': p['ms_per_step'],
+                    'verify_pool256_data': p['data']})
+    return out
 
 
 def _free_port() -> int:
@@ -173,6 +184,10 @@ def main(argv=None):
                     help="verify mode: fraction of each block's txs that are governance txs, e.g. 5%% or 0.05")
     ap.add_argument('--age-txs', type=int, default=0,
                     help='verify/sync modes: first age the ledger with N confirmed txs (2N UTXO rows), e.g. 2500000')
+    ap.add_argument('--keys', choices=['distinct', 'pool256'], default='distinct',
+                    help='verify/sync modes: a fresh key pair per tx (default) or a 256-key pool (cache-friendly)')
+    ap.add_argument('--verify-pool256', type=int, default=1,
+                    help='mine mode: also report the 256-key-pool verify number as a labelled second value')
     ap.add_argument('--verify-steps', type=int, default=10,
                     help='mine mode: timed 2 MB blocks of the tx-verify side measurement (0: skip; GPU only)')
     args = ap.parse_args(argv)

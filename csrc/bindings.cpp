@@ -8,6 +8,7 @@
 
 #include "native.h"
 #include "sha256_common.h"
+#include "thread_pool.h"
 
 namespace py = pybind11;
 using namespace upow;
@@ -168,6 +169,43 @@ PYBIND11_MODULE(_native, m) {
         return py::make_tuple(py::bytes(reinterpret_cast<const char*>(r), 32),
                               py::bytes(reinterpret_cast<const char*>(s), 32));
     });
+
+    // Batch forms for wallets and synthetic-chain setup (bench_verify distinct keys): n keys / n (key,
+    // digest) pairs on the host pool without the GIL. A key outside [1, n-1] leaves its 64 output bytes zero.
+    m.def("p256_pubkey_batch", [](py::bytes keys_be, int threads) -> py::bytes {
+        const std::string d = keys_be;
+        if (d.size() % 32) throw std::invalid_argument("keys must be n x 32 bytes big-endian");
+        const int64_t n = int64_t(d.size() / 32);
+        std::string out(size_t(n) * 64, '\0');
+        {
+            py::gil_scoped_release rel;
+            HostPool::get().parallel_for(n, threads, [&](int64_t i) {
+                uint8_t q[64];
+                if (p256_pubkey(reinterpret_cast<const uint8_t*>(d.data()) + 32 * i, q)) std::memcpy(&out[size_t(64 * i)], q, 64);
+            });
+        }
+        return py::bytes(out);
+    }, py::arg("keys_be"), py::arg("threads") = 8);
+
+    m.def("p256_sign_batch", [](py::bytes keys_be, py::bytes digests, int threads) -> py::bytes {
+        const std::string d = keys_be, h = digests;
+        if (d.size() % 32 || h.size() != d.size()) throw std::invalid_argument("need n x 32-byte keys and digests");
+        const int64_t n = int64_t(d.size() / 32);
+        std::string out(size_t(n) * 64, '\0');
+        {
+            py::gil_scoped_release rel;
+            HostPool::get().parallel_for(n, threads, [&](int64_t i) {
+                uint8_t r[32], s[32];
+                const auto* kp = reinterpret_cast<const uint8_t*>(d.data()) + 32 * i;
+                const auto* hp = reinterpret_cast<const uint8_t*>(h.data()) + 32 * i;
+                if (p256_sign(kp, hp, r, s)) {
+                    std::memcpy(&out[size_t(64 * i)], r, 32);
+                    std::memcpy(&out[size_t(64 * i + 32)], s, 32);
+                }
+            });
+        }
+        return py::bytes(out);
+    }, py::arg("keys_be"), py::arg("digests"), py::arg("threads") = 8);
 
     auto recs_arg = [](py::buffer b, int64_t& n) {
         py::buffer_info bi = b.request();

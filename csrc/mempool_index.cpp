@@ -8,6 +8,12 @@
 // row, dict pops, set differences), competing with the HTTP loop. Here the block's raw txid and outpoint
 // arrays are consumed as they are, without the GIL, and admissions are one hash-map probe per key.
 //
+// Locking: every method takes the index's own reader/writer lock, so a lookup on the HTTP loop (spent_of,
+// has_tx) can never walk a hash node that a block's confirm_raw, running GIL-free on the ledger thread, is
+// erasing. Rule that keeps it deadlock-free against the GIL: nobody blocks on the lock while holding the GIL
+// (a contended acquire first releases the GIL, see `Shared`/`Exclusive`), and the GIL-free sections
+// re-acquire the GIL only after dropping the lock.
+//
 // Template order: the reference divides ``fees`` (a NUMERIC with <= 8 decimals) by the hex length; two
 // distinct ratios of such values differ by far more than a 28-digit quotient resolves, so comparing
 // fee_a * len_b with fee_b * len_a exactly gives the same order (ties: length, then the hex string).
@@ -18,6 +24,9 @@
 #include <array>
 #include <cstdint>
 #include <cstring>
+#include <condition_variable>
+#include <mutex>
+#include <shared_mutex>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -103,6 +112,66 @@ int64_t fee_units(const std::string& s) {
     return neg ? -v : v;
 }
 
+// Writer-preferring reader/writer lock (std::shared_mutex is glibc's reader-preferring rwlock: a steady
+// stream of overlapping lookups could starve a block's confirm). A waiting writer stops new readers.
+class RwLock {
+public:
+    bool try_lock_shared() {
+        std::lock_guard<std::mutex> g(m_);
+        if (writer_ || waiting_) return false;
+        ++readers_;
+        return true;
+    }
+    void lock_shared() {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return !writer_ && !waiting_; });
+        ++readers_;
+    }
+    void unlock_shared() {
+        std::lock_guard<std::mutex> g(m_);
+        if (--readers_ == 0) cv_.notify_all();
+    }
+    bool try_lock() {
+        std::lock_guard<std::mutex> g(m_);
+        if (writer_ || readers_) return false;
+        writer_ = true;
+        return true;
+    }
+    void lock() {
+        std::unique_lock<std::mutex> g(m_);
+        ++waiting_;
+        cv_.wait(g, [&] { return !writer_ && readers_ == 0; });
+        --waiting_;
+        writer_ = true;
+    }
+    void unlock() {
+        std::lock_guard<std::mutex> g(m_);
+        writer_ = false;
+        cv_.notify_all();
+    }
+
+private:
+    std::mutex m_;
+    std::condition_variable cv_;
+    int readers_ = 0, waiting_ = 0;
+    bool writer_ = false;
+};
+
+// Acquire the index lock from a thread that holds the GIL: an uncontended acquire keeps the GIL; a
+// contended one waits with the GIL released (the holder may need the GIL to finish).
+template <class Lock>
+struct GilSafe {
+    Lock lk;
+    explicit GilSafe(RwLock& m) : lk(m, std::try_to_lock) {
+        if (!lk.owns_lock()) {
+            py::gil_scoped_release nogil;
+            lk.lock();
+        }
+    }
+};
+using Shared = GilSafe<std::shared_lock<RwLock>>;
+using Exclusive = GilSafe<std::unique_lock<RwLock>>;
+
 struct Entry {
     int64_t ptime = 0;
     int64_t seq = 0;    // journal sequence of the admission's batch (0: loaded from SQL)
@@ -122,6 +191,7 @@ public:
     }
 
     void load(py::list tx_rows, py::list spent_rows) {
+        Exclusive g(mu_);
         for (auto r : tx_rows) {
             py::tuple t = r.cast<py::tuple>();
             add_entry(h32_hex(t[0].cast<std::string>()), t[1].cast<int64_t>(), t[2], py::str(t[3]).cast<std::string>(), 0);
@@ -132,32 +202,55 @@ public:
         }
     }
 
-    bool empty() const { return txs_.empty() && spent_.empty(); }
-    size_t size() const { return txs_.size(); }
-    size_t spent_size() const { return spent_.size(); }
-    bool has_tx(const std::string& h) const { return txs_.count(h32_hex(h)) != 0; }
+    bool empty() const {
+        Shared g(mu_);
+        return txs_.empty() && spent_.empty();
+    }
+    size_t size() const {
+        Shared g(mu_);
+        return txs_.size();
+    }
+    size_t spent_size() const {
+        Shared g(mu_);
+        return spent_.size();
+    }
+    bool has_tx(const std::string& h) const {
+        const H32 k = h32_hex(h);
+        Shared g(mu_);
+        return txs_.count(k) != 0;
+    }
 
     py::list spent_of(py::iterable outputs) const {
-        py::list out;
+        // keys parsed first (Python objects, GIL), then one probe pass under the lock
+        std::vector<std::pair<py::object, int64_t>> items;
+        std::vector<Op36> keys;
         std::unordered_set<Op36, HHash> seen;
         for (auto o : outputs) {
             py::tuple t = o.cast<py::tuple>();
-            const std::string h = t[0].cast<std::string>();
             const int64_t i = t[1].cast<int64_t>();
-            const Op36 k = op_key(h, i);
+            const Op36 k = op_key(t[0].cast<std::string>(), i);
             if (!seen.insert(k).second) continue;
-            if (spent_.count(k)) out.append(py::make_tuple(h, i));
+            items.emplace_back(py::reinterpret_borrow<py::object>(t[0]), i);
+            keys.push_back(k);
         }
+        std::vector<char> hit(keys.size(), 0);
+        {
+            Shared g(mu_);
+            for (size_t j = 0; j < keys.size(); ++j) hit[j] = spent_.count(keys[j]) != 0;
+        }
+        py::list out;
+        for (size_t j = 0; j < keys.size(); ++j)
+            if (hit[j]) out.append(py::make_tuple(items[j].first, items[j].second));
         return out;
     }
 
     // (tx hex, raw hash) in block-template order, up to `limit` hex characters in total
     py::list ordered(int64_t limit) const {
         std::vector<std::pair<const H32*, const Entry*>> v;
-        {
-            py::gil_scoped_release nogil;  // callers hold the index lock: no entry changes meanwhile
-            v = select(limit);
-        }
+        py::gil_scoped_release nogil;
+        std::shared_lock<RwLock> g(mu_);  // held until the result is built: entries stay put
+        v = select(limit);
+        py::gil_scoped_acquire gil;
         py::list out;
         for (auto& p : v)
             out.append(py::make_tuple(p.second->hex, py::bytes(reinterpret_cast<const char*>(p.first->data()), 32)));
@@ -167,12 +260,13 @@ public:
     // the mining template of /get_mining_info and the new-block event (reference main.py:675-695): the
     // selected txs re-sorted by hex string; returns (first `head` hexes, all tx hashes as hex strs, the
     // same hashes as one JSON array body `"h0","h1",...` for the response, count). Selection, sorts and
-    // text run without the GIL (the caller holds the index lock); only the result objects need it.
+    // text run without the GIL under the shared lock; only the result objects need the GIL.
     py::tuple mining_template(int64_t limit, int64_t head) const {
         std::vector<std::pair<const H32*, const Entry*>> v;
         std::string frag, hx;
+        py::gil_scoped_release nogil;
+        std::shared_lock<RwLock> g(mu_);  // held until the result is built: entries stay put
         {
-            py::gil_scoped_release nogil;
             v = select(limit);
             std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return hex_less(*a.second, *b.second); });
             static const char* digits = "0123456789abcdef";
@@ -191,6 +285,7 @@ public:
                 frag.push_back('"');
             }
         }
+        py::gil_scoped_acquire gil;
         py::list first, hashes;
         for (size_t k = 0; k < v.size(); ++k) {
             if (int64_t(k) < head) first.append(v[k].second->hex);
@@ -202,6 +297,7 @@ public:
     // tx hex of the pending txs among `hashes` (hex strings; malformed ones ignored), in admission order
     py::list hex_in_order(py::iterable hashes) const {
         std::vector<const Entry*> hit;
+        std::vector<H32> keys;
         std::unordered_set<H32, HHash> seen;
         for (auto h : hashes) {
             H32 k;
@@ -210,7 +306,10 @@ public:
             } catch (const std::exception&) {
                 continue;
             }
-            if (!seen.insert(k).second) continue;
+            if (seen.insert(k).second) keys.push_back(k);
+        }
+        Shared g(mu_);
+        for (auto& k : keys) {
             auto it = txs_.find(k);
             if (it != txs_.end()) hit.push_back(&it->second);
         }
@@ -223,27 +322,33 @@ public:
     // reserve a tx and its inputs: None, 'duplicate' or 'double spend'
     py::object try_add(const std::string& tx_hash, int64_t ptime, py::list inputs, py::object tx_hex, py::object fees) {
         const H32 h = h32_hex(tx_hash);
-        if (txs_.count(h)) return py::str("duplicate");
         std::vector<Op36> keys;
         keys.reserve(inputs.size());
         for (auto in : inputs) {
             py::tuple t = in.cast<py::tuple>();
             keys.push_back(op_key(t[0].cast<std::string>(), t[1].cast<int64_t>()));
         }
+        const std::string fee_text = py::str(fees).cast<std::string>();
+        Exclusive g(mu_);
+        if (txs_.count(h)) return py::str("duplicate");
         for (auto& k : keys)
             if (spent_.count(k)) return py::str("double spend");
-        add_entry(h, ptime, tx_hex, py::str(fees).cast<std::string>(), 0);
+        add_entry(h, ptime, tx_hex, fee_text, 0);
         for (auto& k : keys) spent_.insert(k);
         return py::none();
     }
 
     void set_seq(const std::string& tx_hash, py::list inputs, int64_t seq) {
-        auto it = txs_.find(h32_hex(tx_hash));
-        if (it != txs_.end()) it->second.seq = seq;
+        const H32 h = h32_hex(tx_hash);
+        std::vector<Op36> keys;
         for (auto in : inputs) {
             py::tuple t = in.cast<py::tuple>();
-            spent_seq_[op_key(t[0].cast<std::string>(), t[1].cast<int64_t>())] = seq;
+            keys.push_back(op_key(t[0].cast<std::string>(), t[1].cast<int64_t>()));
         }
+        Exclusive g(mu_);
+        auto it = txs_.find(h);
+        if (it != txs_.end()) it->second.seq = seq;
+        for (auto& k : keys) spent_seq_[k] = seq;
     }
 
     // a committed block's txs (n x 32 raw) and spent outpoints (n x >= 36 records) leave the index; returns
@@ -264,6 +369,7 @@ public:
         std::vector<py::object> dropped;  // Python refs released with the GIL held
         {
             py::gil_scoped_release nogil;
+            std::unique_lock<RwLock> g(mu_);  // dropped before the GIL is taken back
             if (!txs_.empty()) {
                 for (size_t i = 0; i < nt; ++i) {
                     H32 k;
@@ -295,6 +401,7 @@ public:
     }
 
     bool maybe_stale(int64_t now, int64_t delta) {
+        Exclusive g(mu_);
         if (!min_ptime_valid_ || now - min_ptime_ <= delta) return false;
         recompute_min();
         return min_ptime_valid_ && now - min_ptime_ > delta;
@@ -363,6 +470,7 @@ private:
         return out;
     }
 
+    mutable RwLock mu_;
     std::unordered_map<H32, Entry, HHash> txs_;
     std::unordered_set<Op36, HHash> spent_;
     std::unordered_map<Op36, int64_t, HHash> spent_seq_;

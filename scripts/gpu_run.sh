@@ -7,6 +7,7 @@
 #   smoke    __graft_entry__.smoke()
 #   mine     bench.py (driver default: PoW MH/s + verify side metrics)
 #   verify   bench.py --mode verify --ledger <tmp dir> (file ledger, metric 2)
+#   verifypool bench.py --mode verify --keys pool256 (file ledger, 256-key pool: the cache-friendly variant)
 #   verifymem bench.py --mode verify (in-memory ledger)
 #   verifygov bench.py --mode verify --governance (file ledger; 12 inodes, 200 validators, 5,000 delegates)
 #   verifygov5 bench.py --mode verify --governance-txs 5% (file ledger; 5 % of every block's txs are governance txs)
@@ -51,6 +52,12 @@ for s in $STEPS; do
       timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger \
         > "$OUT/verify_file.json" 2> "$OUT/verify_file.err" || { tail -20 "$OUT/verify_file.err"; exit 1; }
       cat "$OUT/verify_file.json" ;;
+    verifypool)
+      # the cache-friendly variant: a 256-key pool signs every tx and owns every output
+      rm -rf /tmp/upow_bench_ledger
+      timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger --keys pool256 \
+        > "$OUT/verify_pool256.json" 2> "$OUT/verify_pool256.err" || { tail -20 "$OUT/verify_pool256.err"; exit 1; }
+      cat "$OUT/verify_pool256.json" ;;
     verifygov5)
       rm -rf /tmp/upow_bench_ledger
       timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger --governance-txs 5% \

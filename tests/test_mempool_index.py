@@ -245,3 +245,63 @@ def test_native_index_template_order_and_confirm():
     assert hit_in == [outpoint_key(*op)] and late_tx == [bytes.fromhex(h1)] and late_in == [outpoint_key(*op)]
     assert len(mp) == 399 and not mp.has_tx(h1) and mp.spent_of([op]) == []
     assert mp.maybe_stale(1_700_000_000 + 10_000, 100) and not mp.maybe_stale(1_700_000_000, 10 ** 6)
+
+
+def test_lookups_concurrent_with_confirm_are_safe():
+    """``spent_of``/``has_tx``/``len`` run on the HTTP loop while a block's ``confirm_raw``
+    erases entries GIL-free on the ledger thread. The core's own reader/writer lock serialises them: hammer
+    both sides from threads and check every lookup answer is one the index could have held."""
+    import os
+    import threading
+    import numpy as np
+    from upow_amd.ops.native import lib
+    core = lib().MempoolIndexCore()
+    core.load([], [])
+    rng = np.random.default_rng(7)
+    stop = threading.Event()
+    errors = []
+    rounds = 300
+
+    def writer():
+        try:
+            for r in range(rounds):
+                txids = rng.integers(0, 256, size=(64, 32), dtype=np.uint8)
+                keys = np.zeros((128, 40), np.uint8)
+                for j in range(64):
+                    h = bytes(txids[j]).hex()
+                    ins = [(os.urandom(32).hex(), 0), (os.urandom(32).hex(), 1)]
+                    assert core.try_add(h, r, ins, 'ab' * (100 + j), '0.001') is None
+                    for m, (ih, ii) in enumerate(ins):
+                        keys[2 * j + m, :32] = np.frombuffer(bytes.fromhex(ih), np.uint8)
+                        keys[2 * j + m, 32] = ii
+                    core.set_seq(h, ins, r)
+                probe.append((bytes(txids[0]).hex(), [(bytes(keys[0, :32]).hex(), 0)]))
+                hit_tx, hit_in, _, _ = core.confirm_raw(txids, keys, None)
+                assert len(hit_tx) == 64 and len(hit_in) == 128
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+        finally:
+            stop.set()
+
+    probe = [('00' * 32, [('00' * 32, 0)])]
+
+    def reader():
+        try:
+            while not stop.is_set():
+                h, ins = probe[-1]
+                assert core.has_tx(h) in (True, False)
+                assert len(core.spent_of(ins + [('11' * 32, 3)])) <= 1
+                assert 0 <= len(core) <= 64
+                core.ordered(10_000)
+                core.mining_template(10_000, 5)
+                core.hex_in_order([h])
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    ts = [threading.Thread(target=reader) for _ in range(3)] + [threading.Thread(target=writer)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert not errors, errors
+    assert len(core) == 0 and core.spent_count() == 0

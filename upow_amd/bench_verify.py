@@ -24,6 +24,43 @@ from decimal import Decimal
 from .constants import SMALLEST
 
 
+def batch_keys(n: int, rng, threads: int = 16):
+    """``n`` random P-256 private keys, their public points (x, y little-endian) and 33-byte compressed
+    addresses, computed in one native batch on host threads (csrc/bindings.cpp ``p256_pubkey_batch``)."""
+    from .ops.native import lib
+    from .utils.p256 import N
+    keys = [rng.randrange(1, N) for _ in range(n)]
+    pubs = lib().p256_pubkey_batch(b''.join(k.to_bytes(32, 'big') for k in keys), threads)
+    addr33 = []
+    for i in range(n):
+        q = pubs[64 * i:64 * i + 64]
+        addr33.append(bytes([43 if q[32] & 1 else 42]) + q[:32])
+    return keys, pubs, addr33
+
+
+def _amount_bytes(units: int) -> bytes:
+    n = (units.bit_length() + 7) // 8
+    return bytes([n]) + units.to_bytes(n, 'little')
+
+
+def signed_spend_txs(spends, keys, owner33, recip33, amount_out=(1_250_000_000, 749_000_000), threads: int = 16):
+    """Version-3 2-in/2-out regular txs, serialised and signed in bulk (the bytes ``Transaction.sign().hex()``
+    produces: reference transaction.py:46-83 layout, RFC 6979 signature over SHA-256 of the unsigned part,
+    one signature for both inputs). ``spends[j]`` = ((txid, index), (txid, index)) of tx ``j``, signed by
+    ``keys[j]``; output 0 pays ``recip33[j]``, output 1 returns change to ``owner33[j]``."""
+    from .ops.native import lib
+    a0, a1 = _amount_bytes(amount_out[0]) + b'\x00', _amount_bytes(amount_out[1]) + b'\x00'
+    unsigned, digests = [], []
+    for j, ((h1, i1), (h2, i2)) in enumerate(spends):
+        u = (b'\x03\x02' + bytes.fromhex(h1) + bytes([i1, 0]) + bytes.fromhex(h2) + bytes([i2, 0]) + b'\x02'
+             + recip33[j] + a0 + owner33[j] + a1)
+        unsigned.append(u)
+        digests.append(hashlib.sha256(u).digest())
+    sigs = lib().p256_sign_batch(b''.join(keys[j].to_bytes(32, 'big') for j in range(len(spends))), b''.join(digests),
+                                 threads)
+    return [(u + b'\x00' + sigs[64 * j:64 * j + 64]).hex() for j, u in enumerate(unsigned)]
+
+
 def _funding_tx(owner_addrs, amount: Decimal, rng):
     from .models.transaction import Transaction, TransactionInput, TransactionOutput
     inp = TransactionInput(rng.randbytes(32).hex(), 0)
@@ -33,10 +70,15 @@ def _funding_tx(owner_addrs, amount: Decimal, rng):
 
 async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None, device=None, base_ts=None,
                  make_blocks: bool = True, ledger_path: str = None, governance: bool = False, gov_txs: float = 0.0,
-                 age_txs: int = 0, aging: dict = None):
+                 age_txs: int = 0, aging: dict = None, distinct_keys: bool = False):
     """``gov_txs`` > 0: that fraction of every block's txs are governance txs (70 % delegate votes, 10 %
     validator votes, 20 % delegate revokes of seeded ballots, signed by the voters) on a seeded governance
-    state; the chain starts four days back so the seeded ballots are past the 48 h revoke window."""
+    state; the chain starts four days back so the seeded ballots are past the 48 h revoke window.
+
+    ``distinct_keys``: every plain tx slot gets its own fresh key pair (it owns the two funding outputs the
+    tx spends) and pays a fresh recipient address — a 2 MB block then has ~8,300 distinct signers and
+    ~16,600 distinct output addresses, as random-keypair traffic does. Default (False): a pool of 256 keys
+    signs every tx and receives every output (cache-friendly: key dedup and the base58 memo hit)."""
     from . import devnet
     from .ledger import manager
     from .ledger.database import Database
@@ -61,10 +103,21 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
             aging.update(info)
     # funding block written straight into the ledger (trusted setup, not part of the measurement)
     n_out = n_blocks * txs_per_block * 2
-    owners = [(i // 2) % 256 for i in range(n_out)]  # outputs 2j and 2j+1 share an owner
+    if distinct_keys:
+        # own streams, so the funding set is identical whether or not this rank builds the blocks
+        from .utils.codec import bytes_to_string
+        t_keys = time.perf_counter()
+        tx_keys, _, tx_owner33 = batch_keys(n_blocks * txs_per_block, random.Random(seed * 7919 + 17))
+        owner_addr = [bytes_to_string(a) for a in tx_owner33]
+        fund_addrs = [owner_addr[i // 2] for i in range(n_out)]  # tx slot j owns outputs 2j and 2j+1
+        if aging is not None:
+            aging['distinct_key_setup_s'] = round(time.perf_counter() - t_keys, 2)
+    else:
+        owners = [(i // 2) % 256 for i in range(n_out)]  # outputs 2j and 2j+1 share an owner
+        fund_addrs = [addrs[o] for o in owners]
     funding = []
     for k in range(0, n_out, 255):
-        funding.append(_funding_tx([addrs[o] for o in owners[k:k + 255]], Decimal(10), rng))
+        funding.append(_funding_tx(fund_addrs[k:k + 255], Decimal(10), rng))
     block_hash = rng.randbytes(32).hex()
     last = await db.get_last_block()
     await db.add_block(2, block_hash, last['content'], genesis_addr, 0, Decimal('6.0'), Decimal(6), base_ts + 1)
@@ -86,10 +139,23 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
     blocks = []
     j = 0
     gov_next = {'d': 0, 'v': 0}
+    if distinct_keys and make_blocks:
+        _, _, recip33 = batch_keys(n_blocks * txs_per_block, random.Random(seed * 7919 + 29))
     for b in range(n_blocks if make_blocks else 0):
         txs = []
         if n_gov:
             txs.extend(_governance_txs(seeded, gov_next, n_dv, n_vv, n_rv, rng))
+        if distinct_keys:
+            n_plain = txs_per_block - len(txs)
+            slots = range(j, j + n_plain)
+            txs.extend(signed_spend_txs([(outpoints[2 * s], outpoints[2 * s + 1]) for s in slots],
+                                        [tx_keys[s] for s in slots], [tx_owner33[s] for s in slots],
+                                        [recip33[s] for s in slots]))
+            j += n_plain
+            if n_gov:
+                rng.shuffle(txs)
+            blocks.append(txs)
+            continue
         for _ in range(txs_per_block - len(txs)):
             (h1, i1), (h2, i2) = outpoints[2 * j], outpoints[2 * j + 1]
             owner = owners[2 * j]
@@ -325,6 +391,18 @@ async def _governance_probe(db) -> dict:
             'one_validator_stake_sql_ms': round((t5 - t4) * 1e3, 2), 'stake_matches_sql': sql_stake == idx_stake}
 
 
+def _distinct(args) -> bool:
+    return getattr(args, 'keys', 'distinct') == 'distinct'
+
+
+def _data_label(args) -> str:
+    if _distinct(args):
+        return ('synthetic 2 MB blocks: a fresh random P-256 key pair per tx (~8,300 distinct signers) paying a '
+                'fresh address (~16,600 distinct output addresses per block), 2-in/2-out signed txs, funding UTXOs')
+    return ('synthetic 2 MB blocks: 256 random P-256 keys sign every tx and own every output (cache-friendly), '
+            '2-in/2-out signed txs, funding UTXOs')
+
+
 def _ledger_path(args, ctx):
     """``--ledger DIR``: a file-backed ledger (WAL, synchronous=NORMAL — what a node runs with) in a
     fresh per-rank directory; default is an in-memory SQLite ledger."""
@@ -347,7 +425,9 @@ async def _run(args, ctx, device, utxo_backend):
     aging = {}
     db, addr, blocks, base_ts = await _setup(n_blocks, args.txs, 1234 + ctx.rank, utxo_backend, device,
                                              ledger_path=_ledger_path(args, ctx), governance=gov, gov_txs=gov_txs,
-                                             age_txs=int(getattr(args, 'age_txs', 0) or 0), aging=aging)
+                                             age_txs=int(getattr(args, 'age_txs', 0) or 0), aging=aging,
+                                             distinct_keys=_distinct(args))
+    key_setup = aging.pop('distinct_key_setup_s', None)
     if aging:
         db.flush()
     gov_probe = await _governance_probe(db) if gov else None
@@ -437,7 +517,7 @@ async def _run(args, ctx, device, utxo_backend):
     if writer is not None:
         writer = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in writer.items() if k != 'error'}
     extra = {'drain_s': drain, 'writer': writer, 'window_unix': [unix_start, time.time()], 'governance': gov_probe,
-             'aging': aging or None, 'queue_trace': queue_trace}
+             'aging': aging or None, 'queue_trace': queue_trace, 'key_setup_s': key_setup}
     if gov_probe is not None:
         gov_probe['active_inodes_after'] = len(await db.get_active_inodes())
         gov_probe['coinbase_outputs_last_block'] = len(json.loads(
@@ -478,8 +558,8 @@ def run_verify_bench(args, ctx):
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': 'uint32',
-        'data': 'synthetic 2 MB blocks: random P-256 keys, 2-in/2-out signed txs, funding UTXOs',
-        'config': {'model': 'upow block validation + apply (push_block path)', 'global_batch': total // max(1, args.steps),
+        'data': _data_label(args),
+        'config': {'model': 'upow block validation + apply (push_block path)', 'keys': getattr(args, 'keys', 'distinct'), 'global_batch': total // max(1, args.steps),
                    'seq_len': txs_per_block, 'parallelism': f'dp{ctx.world}', 'device': device,
                    'utxo_backend': utxo_backend, 'block_path': '+'.join(paths),
                    'ledger': 'file (WAL)' if getattr(args, 'ledger', None) else 'memory',
@@ -497,6 +577,7 @@ def run_verify_bench(args, ctx):
         'final_drain_ms': round(extra['drain_s'] * 1000, 2),
         'ledger_writer': extra['writer'],
         'window_unix': extra['window_unix'],
+        **({'key_setup_s': extra['key_setup_s']} if extra.get('key_setup_s') is not None else {}),
         **({'governance': extra['governance']} if extra['governance'] else {}),
         **({'aged_ledger': extra['aging'], 'writer_lag_after_block': extra['queue_trace']} if extra['aging'] else {}),
     }
@@ -518,7 +599,8 @@ async def _run_cluster(args, ctx, device, utxo_backend):
     n_blocks = args.steps + args.warmup
     base_ts = ctx.allreduce_min(int(time.time()) - 10_000)
     db, addr, blocks, _ = await _setup(n_blocks, args.txs, 1234, utxo_backend, device, base_ts=base_ts,
-                                       make_blocks=ctx.rank == 0, ledger_path=_ledger_path(args, ctx))
+                                       make_blocks=ctx.rank == 0, ledger_path=_ledger_path(args, ctx),
+                                       distinct_keys=_distinct(args))
     c = cluster.init(ctx)
     st = c.status(db)
     if any((s['height'], s['utxo_hash']) != (st[0]['height'], st[0]['utxo_hash']) for s in st):
@@ -598,8 +680,9 @@ def run_cluster_verify_bench(args, ctx):
         'scaling': 'strong',
         'vs_baseline': None,
         'dtype': 'uint32',
-        'data': 'synthetic 2 MB blocks: random P-256 keys, 2-in/2-out signed txs, funding UTXOs',
+        'data': _data_label(args),
         'config': {'model': 'upow cluster node: one chain, G replicas, sharded ECDSA (push_block path)',
+                   'keys': getattr(args, 'keys', 'distinct'),
                    'global_batch': txs_per_block, 'seq_len': txs_per_block, 'parallelism': f'replica{ctx.world}+sigshard',
                    'device': device, 'utxo_backend': utxo_backend, 'block_path': '+'.join(p for p in paths if p),
                    'ledger': 'file (WAL)' if getattr(args, 'ledger', None) else 'memory',
@@ -632,7 +715,8 @@ async def _run_sync(args, ctx, device, utxo_backend):
     # 100-block retarget, as a real chain at equilibrium does
     base_ts = int(time.time()) - 60 * (n_blocks + 10) - 1_000
     seed = 4321 + ctx.rank
-    src, addr, blocks, _ = await _setup(n_blocks, args.txs, seed, utxo_backend, device, base_ts=base_ts)
+    src, addr, blocks, _ = await _setup(n_blocks, args.txs, seed, utxo_backend, device, base_ts=base_ts,
+                                        distinct_keys=_distinct(args))
     prev = (await src.get_last_block())['hash']
     for b, txs_hex in enumerate(blocks):
         manager.Manager.difficulty = None
@@ -653,7 +737,8 @@ async def _run_sync(args, ctx, device, utxo_backend):
     aging = {}
     dst, _, _, _ = await _setup(n_blocks, args.txs, seed, utxo_backend, device, base_ts=base_ts, make_blocks=False,
                                 ledger_path=_ledger_path(args, ctx), age_txs=int(getattr(args, 'age_txs', 0) or 0),
-                                aging=aging)
+                                aging=aging, distinct_keys=_distinct(args))
+    aging.pop('distinct_key_setup_s', None)
     dst.flush()
     Database.instance = dst
     manager.Manager.difficulty = None
