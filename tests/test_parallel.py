@@ -94,7 +94,8 @@ def test_shard_bounds_partition():
 def _replica_worker(rank, world, port, tmp, q):
     os.environ.update({'RANK': str(rank), 'WORLD_SIZE': str(world), 'LOCAL_RANK': str(rank),
                        'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port), 'UPOW_DISABLE_GPU': '1',
-                       'UPOW_START_DIFFICULTY': '1.0', 'UPOW_CORE_URL': ''})
+                       'UPOW_START_DIFFICULTY': '1.0', 'UPOW_CORE_URL': '',
+                       'UPOW_CLUSTER_SHARD_MIN': '1'})  # shard even tiny blocks: the sharded path is under test
     try:
         import asyncio
         import hashlib as hl
@@ -211,7 +212,7 @@ def _cluster_worker(rank, world, port, tmp, q):
             key = 0x71
             addr = address_of(key)
             base = 1_700_000_000
-            await cluster.leader_replay(db)
+            await cluster.leader_start(db)
             assert validate._dist_ctx is ctx
             for b in range(5):
                 content = await devnet.mine_header(addr, [], ts=base + 60 * b, device='cpu')
@@ -219,9 +220,12 @@ def _cluster_worker(rank, world, port, tmp, q):
             txs = []
             for j in range(4):
                 tx = await create_transaction(key, address_of(0x200 + j), '1.25')
-                assert await db.add_pending_transaction(tx)
-                cluster.mirror_tx(tx.hex())
+                assert await db.add_pending_transaction(tx)  # replicated through db.on_admit
                 txs.append(tx)
+            cluster.flush_txs()
+            c.send('status')
+            st = c.status(db)
+            assert {x['mempool'] for x in st} == {4}, st
             content = await devnet.mine_header(addr, txs, ts=base + 60 * 5, device='cpu')
             assert await fastpath.create_block_from_hex(content, [t.hex() for t in txs])
             assert fastpath.last_path == 'native'
@@ -234,7 +238,7 @@ def _cluster_worker(rank, world, port, tmp, q):
             assert len({(x['height'], x['utxo_hash']) for x in st}) == 1 and st[0]['height'] == 5, st
             assert await fastpath.create_block_from_hex(content, [t.hex() for t in txs])
             res = (db._tip_id(), await db.get_unspent_outputs_hash())
-            cluster.leader_quit()
+            await cluster.leader_quit()
             db.close()
             return res
 

@@ -408,6 +408,8 @@ class Database:
         self._genesis_cache: Optional[str] = None
         self._pending_empty: Optional[bool] = None
         self._mempool_ver = 0
+        self.on_admit = None  # cluster leader: row hook of every admission (parallel/cluster.py)
+        self.on_confirm = None  # cluster leader: hook of a block's mempool confirm, under the index lock
         self._mp: Optional[MempoolIndex] = None  # ledger/mempool.py; None: (re)load from SQL on next use
         self.mempool_reloads = 0
         self._seq_lock = threading.Lock()  # journal submission + per-table sequence bookkeeping
@@ -1150,11 +1152,20 @@ class Database:
         the block was being applied) is deleted by a follow-up batch, journaled after those INSERTs."""
         mp = self._mp
         if mp is None:
+            if self.on_confirm is not None:  # no index: the block's SQL deletes cover all its txs and inputs
+                if txids is not None:
+                    kk = np.asarray(in_keys, dtype=np.uint8)
+                    self.on_confirm([bytes(r) for r in np.asarray(txids, np.uint8).reshape(-1, 32)],
+                                    [bytes(r[:36]) for r in kk.reshape(-1, kk.shape[-1] if kk.ndim == 2 else 40)])
+                else:
+                    from .mempool import outpoint_key
+                    self.on_confirm([bytes.fromhex(h) for h in hashes or []],
+                                    [outpoint_key(h, i) for h, i in inputs or []])
             return
         if txids is not None:
-            hit_tx, hit_in, late_tx, late_in = mp.confirm_raw(txids, in_keys, block_seq)
+            hit_tx, hit_in, late_tx, late_in = mp.confirm_raw(txids, in_keys, block_seq, self.on_confirm)
         else:
-            hit_tx, hit_in, late_tx, late_in = mp.confirm(hashes or [], inputs or [], block_seq)
+            hit_tx, hit_in, late_tx, late_in = mp.confirm(hashes or [], inputs or [], block_seq, self.on_confirm)
         if not (hit_tx or hit_in):
             return
         self._pending_empty = None
@@ -1191,14 +1202,17 @@ class Database:
         mp = self._mempool() if verify else None
         if mp is not None:
             return self._admit(mp, transaction, tx_hex, inputs_addresses)
+        ptime = int(_utcnow().replace(tzinfo=timezone.utc).timestamp())
         try:
             self._x('INSERT INTO pending_transactions (tx_hash, tx_hex, inputs_addresses, fees, propagation_time) '
                     'VALUES (?, ?, ?, ?, ?)',
-                    (sha256(tx_hex), tx_hex, _j(inputs_addresses), numeric(transaction.fees, 6),
-                     int(_utcnow().replace(tzinfo=timezone.utc).timestamp())))
+                    (sha256(tx_hex), tx_hex, _j(inputs_addresses), numeric(transaction.fees, 6), ptime))
         except sqlite3.IntegrityError as e:
             raise UniqueViolationError(str(e)) from e
         await self.add_transactions_pending_spent_outputs([transaction])
+        if self.on_admit is not None:
+            self.on_admit([tx_hex, _j(inputs_addresses), numeric(transaction.fees, 6), ptime,
+                           [[i.tx_hash, int(i.index)] for i in transaction.inputs]])
         return True
 
     def _admit(self, mp: MempoolIndex, transaction: Transaction, tx_hex: str, inputs_addresses: list) -> bool:
@@ -1226,9 +1240,67 @@ class Database:
                                          len(inputs)))
             seq = self.submit_batch(stmts, self._PENDING, write_behind=True)
             mp.set_seq(tx_hash, inputs, seq)
+            if self.on_admit is not None:  # cluster leader: replicate the admitted row (under the index lock)
+                self.on_admit([tx_hex, _j(inputs_addresses), fees, ptime, [[h, i] for h, i in inputs]])
         self._pending_empty = False
         self._mempool_ver += 1
         return True
+
+    def admit_replicated(self, rows: List[list]) -> int:
+        """Insert mempool rows admitted (and verified) by the cluster leader: ``[tx_hex, inputs_addresses
+        JSON, fees, propagation_time, [[txid, index], ...]]`` each (parallel/cluster.py). No re-verification:
+        the rows reproduce the leader's tables and index exactly, as one index pass under the index lock and
+        one journal batch. Returns how many rows were inserted."""
+        if not rows:
+            return 0
+        mp = self._mempool()
+        if mp is None:
+            n = 0
+            for tx_hex, ia, fees, ptime, inputs in rows:
+                try:
+                    self._x('INSERT INTO pending_transactions (tx_hash, tx_hex, inputs_addresses, fees, '
+                            'propagation_time) VALUES (?, ?, ?, ?, ?)', (sha256(tx_hex), tx_hex, ia, fees, int(ptime)))
+                except sqlite3.IntegrityError:
+                    continue
+                if inputs:
+                    self._xm('INSERT INTO pending_spent_outputs (tx_hash, "index") VALUES (?, ?)',
+                             [(h, int(i)) for h, i in inputs])
+                n += 1
+            return n
+        acc = []
+        with mp.lock:
+            for tx_hex, ia, fees, ptime, inputs in rows:
+                h = sha256(tx_hex)
+                ins = [(a, int(b)) for a, b in inputs]
+                why = mp.try_add(h, int(ptime), ins, tx_hex, fees)
+                if why is not None:
+                    logger.error(f'cluster replica: leader mempool row {h} refused ({why})')
+                    continue
+                acc.append((h, tx_hex, ia, fees, int(ptime), ins))
+            if not acc:
+                return 0
+            stmts = [self.encode('INSERT OR IGNORE INTO pending_transactions (tx_hash, tx_hex, inputs_addresses, fees, '
+                                 'propagation_time) VALUES (?, ?, ?, ?, ?)',
+                                 [[a[0] for a in acc], [a[1] for a in acc], [a[2] for a in acc], [a[3] for a in acc],
+                                  np.array([a[4] for a in acc], np.int64)], len(acc))]
+            spent = [(h, i) for a in acc for h, i in a[5]]
+            if spent:
+                stmts.append(self.encode('INSERT INTO pending_spent_outputs (tx_hash, "index") VALUES (?, ?)',
+                                         [[h for h, _ in spent], np.array([i for _, i in spent], np.int64)], len(spent)))
+            seq = self.submit_batch(stmts, self._PENDING, write_behind=True)
+            for a in acc:
+                mp.set_seq(a[0], a[5], seq)
+        self._pending_empty = False
+        self._mempool_ver += 1
+        return len(acc)
+
+    def clear_mempool(self):
+        """Empty both mempool tables (a cluster replica about to take the leader's mempool)."""
+        self.flush()
+        self._x('DELETE FROM pending_spent_outputs')
+        self._x('DELETE FROM pending_transactions')
+        self._pending_empty = None
+        self._mempool_ver += 1
 
     async def remove_pending_transaction(self, tx_hash: str):
         self._x('DELETE FROM pending_transactions WHERE tx_hash = ?', (tx_hash,))

@@ -42,24 +42,10 @@ from ..utils import metrics, roctx
 from ..utils.codec import TransactionType, get_transaction_type_from_message
 from ..utils.logger import get_logger
 from .govcheck import BlockGovernance
+from ..utils.cpus import cpu_budget  # noqa: F401 (re-exported: node/__main__.py)
 from .utxo import TAG_BY_TABLE
 
 logger = get_logger(__name__)
-def cpu_budget() -> int:
-    """CPUs this process can actually use: its affinity, capped by a cgroup CPU quota (a GPU box gives a
-    node 16 CPUs' worth of time on a 256-core host; threads beyond that are throttled, not parallel)."""
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        avail = os.cpu_count() or 1
-    try:
-        with open('/sys/fs/cgroup/cpu.max') as f:
-            quota, period = f.read().split()[:2]
-        if quota != 'max':
-            avail = min(avail, max(1, int(quota) // int(period)))
-    except (OSError, ValueError):
-        pass
-    return avail
 
 
 def _codec_threads() -> int:

@@ -98,19 +98,23 @@ class MempoolIndex:
         """Record the journal sequence of an admission's batch (caller holds ``lock``)."""
         self.core.set_seq(tx_hash, [(h, int(i)) for h, i in inputs], int(seq))
 
-    def confirm_raw(self, txids: np.ndarray, in_keys: np.ndarray, after: Optional[int] = None):
+    def confirm_raw(self, txids: np.ndarray, in_keys: np.ndarray, after: Optional[int] = None, on_hits=None):
         """A committed block's txs (n x 32) and spent outpoints (n x >=36 records) leave the mempool;
-        returns the raw tx hashes and outpoints that were in it (and those admitted after ``after``)."""
+        returns the raw tx hashes and outpoints that were in it (and those admitted after ``after``).
+        ``on_hits(hit_tx, hit_in)`` runs under ``lock`` right after the removal (cluster replication)."""
         t = np.ascontiguousarray(np.asarray(txids, dtype=np.uint8).reshape(-1, 32))
         k = np.asarray(in_keys, dtype=np.uint8)
         k = np.ascontiguousarray(k.reshape(-1, k.shape[-1] if k.ndim == 2 and k.shape[0] else 40))
         with self.lock:
-            return self.core.confirm_raw(t, k, after)
+            res = self.core.confirm_raw(t, k, after)
+            if on_hits is not None and (res[0] or res[1]):
+                on_hits(res[0], res[1])
+            return res
 
-    def confirm(self, tx_hashes: List[str], inputs: List[Tuple[str, int]], after: Optional[int] = None):
+    def confirm(self, tx_hashes: List[str], inputs: List[Tuple[str, int]], after: Optional[int] = None, on_hits=None):
         t = np.frombuffer(b''.join(bytes.fromhex(h) for h in tx_hashes), dtype=np.uint8).reshape(-1, 32)
         k = np.frombuffer(b''.join(outpoint_key(h, i) for h, i in inputs), dtype=np.uint8).reshape(-1, 36)
-        return self.confirm_raw(t, k, after)
+        return self.confirm_raw(t, k, after, on_hits)
 
     def maybe_stale(self, now: int, delta: int) -> bool:
         """Could a pending tx be older than ``delta`` seconds? The minimum propagation time only moves down

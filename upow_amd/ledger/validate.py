@@ -16,6 +16,7 @@ Here, for a whole block:
 from __future__ import annotations
 
 import hashlib
+import os
 from time import perf_counter
 from typing import List, Optional
 
@@ -30,6 +31,12 @@ from ..utils.logger import get_logger
 logger = get_logger(__name__)
 timings: dict = {}
 _dist_ctx = None  # set on multi-GPU nodes: the signature batch is sharded across ranks (parallel/verify_dp.py)
+# sharding threshold: below this many signatures every replica verifies the whole batch itself. One GPU
+# verifies a 2 MB block's ~8,300 signatures in ~1.2 ms (the quad kernel's latency floor); splitting them
+# saves under a millisecond and costs an all-gather plus the host syncs around it, so the cluster path only
+# shards batches that fill more than a chip (initial-sync batches, mempool bursts). Every replica sees the
+# same batch size, so all of them take the same branch.
+SHARD_MIN = int(os.environ.get('UPOW_CLUSTER_SHARD_MIN', '32768'))
 
 
 def set_dist_context(ctx) -> None:
@@ -40,7 +47,7 @@ def set_dist_context(ctx) -> None:
 
 
 def _verify(recs: bytes, device):
-    if _dist_ctx is not None:
+    if _dist_ctx is not None and len(recs) // 160 >= SHARD_MIN:
         from ..parallel.verify_dp import verify_records_dp
         return verify_records_dp(_dist_ctx, recs, device=device)
     return op.verify_records(recs, device=device)

@@ -98,24 +98,53 @@ def _run_cluster(a):
 
     from ..ops.native import lib
     from ..parallel import cluster
-    from ..parallel.dist import init_from_env, shutdown
+    from ..parallel.dist import init_from_env, op_context, shutdown
     lib()  # the extension binds to torch's HIP runtime before the process group exists
     ctx = init_from_env()
-    c = cluster.init(ctx)
+    c = cluster.init(op_context(ctx), ctx)  # op traffic on a short-timeout group, start-up on the default one
     try:
         if ctx.rank == 0:
             import uvicorn
             from . import main as node_main
             uvicorn.run(node_main.app, host=a.host, port=a.port, log_level=a.log_level, **server_protocol())
         else:
-            from ..ledger.database import Database
-
-            async def follow():
-                db = await Database.create(path=':memory:')
-                await cluster.follower_main(c, db)
-            asyncio.run(follow())
+            asyncio.run(_follow(c))
     finally:
         shutdown(ctx)
+
+
+def follower_ledger_path(rank: int) -> str:
+    """A follower's durable replica: ``<data dir>/rank<N>/ledger.sqlite3`` with its own journal, undo
+    segments and UTXO snapshot (``UPOW_CLUSTER_FOLLOWER_DB=:memory:`` keeps the old ephemeral replica)."""
+    from .. import config
+    spec = os.environ.get('UPOW_CLUSTER_FOLLOWER_DB')
+    if spec:
+        return spec if spec == ':memory:' else spec.replace('{rank}', str(rank))
+    return config.data_path(f'rank{rank}', 'ledger.sqlite3')
+
+
+async def _follow(c):
+    import signal
+
+    from ..ledger.database import Database
+    from ..parallel import cluster
+    # a stop signal reaches every rank of the job at once: the follower keeps applying the op stream until
+    # the leader's graceful shutdown sends 'quit' (then it snapshots and closes its ledger); if the leader
+    # is gone instead, the op group's collective timeout ends this process (parallel/dist.py)
+    signal.signal(signal.SIGTERM, lambda *_: None)
+    signal.signal(signal.SIGINT, lambda *_: None)
+    db = await Database.create(path=follower_ledger_path(c.ctx.rank))
+    try:
+        await cluster.follower_main(c, db)
+    finally:
+        if db.path != ':memory:' and os.environ.get('UPOW_SNAPSHOT', '1') != '0':
+            try:  # the next start restores the index from here instead of rebuilding it from SQL
+                from ..ledger import snapshot
+                snapshot.save(db)
+            except Exception as e:
+                from ..utils.logger import get_logger
+                get_logger(__name__).error(f'follower UTXO snapshot failed: {e}')
+        db.close()
 
 
 if __name__ == '__main__':

@@ -85,8 +85,9 @@ async def lifespan(app: FastAPI):
         indexer.cancel()
         if lag is not None:
             lag.cancel()
+        if cluster.get() is not None:
+            await on_ledger(cluster.leader_quit)  # the collective owner tells the replicas to stop
         ledger_worker.stop()
-        cluster.leader_quit()
         peers.book().flush()
         await shutdown_websocket_manager()
         if db is not None and db.path != ':memory:' and os.environ.get('UPOW_SNAPSHOT', '1') != '0':
@@ -183,10 +184,10 @@ async def startup():
     access = AccessControl()
     path = os.environ.get('UPOW_DATABASE_PATH') or config.data_path('ledger.sqlite3')
     db = await Database.create(path=path)
-    if cluster.get() is not None:  # multi-GPU node: bring the follower replicas to our tip
-        await cluster.leader_replay(db)
-    # block validation/apply (and every cluster collective) from here on runs on the ledger thread
+    # block validation/apply and every cluster collective run on the ledger thread
     ledger_worker.start()
+    if cluster.get() is not None:  # multi-GPU node: the replicas get only what they lack (parallel/cluster.py)
+        await on_ledger(cluster.leader_start, db)
     # what exists now (ledger caches, indexes, modules) lives for the process: keep it out of the
     # cyclic collector's full passes, which run on whichever thread allocates and hold the GIL
     import gc
@@ -626,9 +627,7 @@ async def verify_and_push_tx(tx: Transaction, request: Request, background_tasks
         sender = await tx.inputs[0].get_address()
         if sender in BANNED_SENDERS:
             return JSONResponse(status_code=403, content={'ok': False, 'error': 'Access forbidden temporarily.'})
-        if await db.add_pending_transaction(tx):
-            if cluster.get() is not None:
-                cluster.mirror_tx(tx.hex())  # queued; the ledger thread ships the batch
+        if await db.add_pending_transaction(tx):  # a cluster leader queues the row for its replicas
             if 'Sender-Node' in request.headers:
                 peers.book().seen(request.headers['Sender-Node'])
             background_tasks.add_task(propagate, 'push_tx', {'tx_hex': tx.hex()})
@@ -920,14 +919,16 @@ async def get_nodes():
 
 
 @app.get('/cluster_info')
-async def cluster_info():
-    """Multi-GPU node: every replica's height and UTXO-set hash (a collective). Not in the reference."""
+async def cluster_info(deep: bool = False):
+    """Multi-GPU node: every replica's height, tip hash and UTXO-set hash (a collective, issued by the
+    ledger thread like every other one; the hash is the index's K12 digest, ``deep=true`` adds each SQL
+    replica's table hash). Not in the reference."""
     c = cluster.get()
+    replicas = await on_ledger(cluster.status_all, db, deep)
     if c is None:
-        return {'ok': True, 'result': {'world': 1, 'replicas': [{'rank': 0, 'height': db._tip_id(),
-                                                                'utxo_hash': db.sql_unspent_outputs_hash()}]}}
-    c.send('status')
-    return {'ok': True, 'result': {'world': c.ctx.world, 'backend': c.ctx.backend, 'replicas': c.status(db)}}
+        return {'ok': True, 'result': {'world': 1, 'replicas': replicas}}
+    return {'ok': True, 'result': {'world': c.ctx.world, 'backend': c.ctx.backend, 'replicas': replicas,
+                                   'last_resync': c.last_resync, 'ops_sent': c.ops_sent}}
 
 
 @app.get('/metrics')

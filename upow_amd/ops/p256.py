@@ -14,6 +14,7 @@ from typing import Iterable, List, Optional, Sequence, Tuple, Union
 import numpy as np
 
 from ..utils import coalesce
+from ..utils.cpus import cpu_budget
 from ..utils import p256 as oracle
 from ..utils.p256 import EcdsaError, Point
 from .native import gpu_available, lib
@@ -58,7 +59,7 @@ def verify_records(records: Union[bytes, bytearray, np.ndarray], device: Optiona
     n = buf.size // 160
     if device is None:
         device = 'gpu' if (gpu_available() and n >= GPU_MIN_BATCH) else 'cpu'
-    st = lib().p256_verify(buf, device == 'gpu', threads or max(1, min(os.cpu_count() or 1, 16)))
+    st = lib().p256_verify(buf, device == 'gpu', threads or max(1, min(cpu_budget(), 16)))
     return np.frombuffer(st, dtype=np.uint8)
 
 

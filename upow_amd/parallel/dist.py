@@ -6,12 +6,27 @@ mempool deltas), so there is no bucketing: each exchange is one
 default stream, and the messages ride the LL/LL128 protocols over the direct links.
 
 Tests use the same code with the ``gloo`` backend on CPU (world_size > 1 on one host).
+
+Failure model. A collective that one rank never joins (a replica that diverged onto another code path, a
+rank that died) must not hang the node forever:
+
+* every collective of a cluster node runs on ONE owner thread per process (``bind_owner``; the leader's
+  ledger thread, the follower's op loop). A call from any other thread raises before touching the
+  communicator, so two threads can never interleave their collective sequences;
+* the cluster's op traffic runs on a process group created with a timeout (``UPOW_DIST_TIMEOUT_S``, 60 s
+  by default; the leader's idle heartbeat keeps followers inside it), and a collective that fails or times
+  out ends the process loudly with a non-zero status (``UPOW_DIST_FATAL=0`` raises instead, for tests);
+* start-up (ledger open and replica resync) uses the default group with a long timeout
+  (``UPOW_DIST_INIT_TIMEOUT_S``, 1 h).
 """
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass
+import threading
+from dataclasses import dataclass, field
 from typing import Optional
+
+EXIT_COLLECTIVE_FAILED = 70
 
 
 @dataclass
@@ -24,6 +39,10 @@ class DistContext:
 
     comm_device: str = 'cpu'  # where collective tensors live: cuda:N for RCCL, cpu for gloo
     forced: bool = False  # run collectives even for world == 1 (exercises the RCCL path on one GPU)
+    group: object = None  # process group of the collectives (None: the default group)
+    owner: Optional[int] = None  # thread ident allowed to issue collectives (None: any thread)
+    fatal: bool = field(default_factory=lambda: os.environ.get('UPOW_DIST_FATAL', '1') != '0')
+    collectives: int = 0  # issued so far (tests, /cluster_info)
 
     @property
     def is_distributed(self) -> bool:
@@ -32,6 +51,38 @@ class DistContext:
     @property
     def is_main(self) -> bool:
         return self.rank == 0
+
+    # ---------------------------------------------------------------- ownership and failure
+    def bind_owner(self, ident: Optional[int] = None):
+        """From now on only thread ``ident`` (default: the calling thread) may issue collectives."""
+        self.owner = threading.get_ident() if ident is None else ident
+
+    def _enter(self, what: str):
+        if self.owner is not None and threading.get_ident() != self.owner:
+            raise RuntimeError(f'collective {what} issued from thread {threading.current_thread().name}, '
+                               f'not the owner thread: ranks would see interleaved collective sequences')
+        self.collectives += 1
+
+    def _failed(self, what: str, e: BaseException):
+        """A collective failed or timed out: the ranks' sequences no longer line up, so nothing later can
+        be trusted. Exit loudly (the launcher tears the other ranks down) unless UPOW_DIST_FATAL=0."""
+        msg = f'rank {self.rank}/{self.world}: collective {what} failed ({type(e).__name__}: {e})'
+        if not self.fatal:
+            raise RuntimeError(msg) from e
+        import sys
+        try:
+            from ..utils.logger import get_logger
+            get_logger(__name__).critical(msg)
+        finally:
+            print(msg, file=sys.stderr, flush=True)
+            os._exit(EXIT_COLLECTIVE_FAILED)
+
+    def _run(self, what: str, fn, *args, **kw):
+        self._enter(what)
+        try:
+            return fn(*args, group=self.group, **kw)
+        except Exception as e:
+            self._failed(what, e)
 
     # ---------------------------------------------------------------- collectives (thin wrappers)
     def _t(self, values, dtype=None):
@@ -43,7 +94,7 @@ class DistContext:
             return int(v)
         import torch.distributed as dist
         t = self._t([v])
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        self._run('all_reduce(min)', dist.all_reduce, t, op=dist.ReduceOp.MIN)
         return int(t.item())
 
     def allreduce_min_vec(self, values) -> list:
@@ -52,7 +103,7 @@ class DistContext:
             return [int(v) for v in values]
         import torch.distributed as dist
         t = self._t(list(values))
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        self._run('all_reduce(min vec)', dist.all_reduce, t, op=dist.ReduceOp.MIN)
         return [int(x) for x in t.tolist()]
 
     def allreduce_sum_vec(self, values) -> list:
@@ -61,7 +112,7 @@ class DistContext:
             return [int(v) for v in values]
         import torch.distributed as dist
         t = self._t(list(values))
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        self._run('all_reduce(sum vec)', dist.all_reduce, t, op=dist.ReduceOp.SUM)
         return [int(x) for x in t.tolist()]
 
     def allreduce_max_f(self, v: float) -> float:
@@ -70,7 +121,7 @@ class DistContext:
         import torch
         import torch.distributed as dist
         t = self._t([v], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        self._run('all_reduce(max)', dist.all_reduce, t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
     def allreduce_sum(self, v: int) -> int:
@@ -78,7 +129,7 @@ class DistContext:
             return int(v)
         import torch.distributed as dist
         t = self._t([v])
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        self._run('all_reduce(sum)', dist.all_reduce, t, op=dist.ReduceOp.SUM)
         return int(t.item())
 
     def broadcast_bytes(self, data: Optional[bytes], src: int, max_len: int = 256) -> bytes:
@@ -93,14 +144,14 @@ class DistContext:
         size = max_len
         if max_len <= 0:
             t = self._t([n_src])
-            dist.broadcast(t, src=src)
+            self._run('broadcast(len)', dist.broadcast, t, src=src)
             size = int(t.item())
         buf = torch.zeros(size + 4, dtype=torch.uint8, device=self.comm_device)
         if self.rank == src:
             assert data is not None and len(data) <= size, 'payload larger than max_len (use max_len=0)'
             payload = len(data).to_bytes(4, 'little') + data
             buf[:len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(self.comm_device)
-        dist.broadcast(buf, src=src)
+        self._run('broadcast(bytes)', dist.broadcast, buf, src=src)
         raw = bytes(buf.cpu().numpy().tobytes())
         n = int.from_bytes(raw[:4], 'little')
         return raw[4:4 + n]
@@ -113,13 +164,13 @@ class DistContext:
         import torch.distributed as dist
         n = self._t([len(data)])
         sizes = [torch.zeros_like(n) for _ in range(self.world)]
-        dist.all_gather(sizes, n)
+        self._run('all_gather(len)', dist.all_gather, sizes, n)
         mx = max(int(s.item()) for s in sizes)
         buf = torch.zeros(max(mx, 1), dtype=torch.uint8, device=self.comm_device)
         if data:
             buf[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(self.comm_device)
         outs = [torch.zeros_like(buf) for _ in range(self.world)]
-        dist.all_gather(outs, buf)
+        self._run('all_gather(bytes)', dist.all_gather, outs, buf)
         return [bytes(o.cpu().numpy().tobytes()[:int(s.item())]) for o, s in zip(outs, sizes)]
 
     def barrier(self):
@@ -127,9 +178,9 @@ class DistContext:
             import torch.distributed as dist
             if self.backend == 'nccl':
                 import torch
-                dist.barrier(device_ids=[torch.cuda.current_device()])
+                self._run('barrier', dist.barrier, device_ids=[torch.cuda.current_device()])
             else:
-                dist.barrier()
+                self._run('barrier', dist.barrier)
 
     def synchronize(self):
         if self.device.startswith('cuda'):
@@ -164,16 +215,36 @@ def init_from_env(backend: Optional[str] = None, want_gpu: bool = True) -> DistC
         import torch.distributed as dist
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         be = backend or ('nccl' if gpu else 'gloo')
+        from datetime import timedelta
+        init_timeout = timedelta(seconds=float(os.environ.get('UPOW_DIST_INIT_TIMEOUT_S', '3600')))
         if not dist.is_initialized():
             if be == 'nccl':
                 import torch
-                dist.init_process_group(be, rank=rank, world_size=world,
+                dist.init_process_group(be, rank=rank, world_size=world, timeout=init_timeout,
                                         device_id=torch.device(ctx.device))
             else:
-                dist.init_process_group(be, rank=rank, world_size=world)
+                dist.init_process_group(be, rank=rank, world_size=world, timeout=init_timeout)
         ctx.backend = be
         ctx.comm_device = ctx.device if be == 'nccl' else 'cpu'
     return ctx
+
+
+def op_context(ctx: DistContext) -> DistContext:
+    """A copy of ``ctx`` whose collectives run on a new process group with the short op timeout
+    (``UPOW_DIST_TIMEOUT_S``): the cluster's steady-state op traffic. Collective (every rank calls it)."""
+    if not ctx.is_distributed:
+        return ctx
+    import dataclasses
+    from datetime import timedelta
+
+    import torch.distributed as dist
+    t = timedelta(seconds=float(os.environ.get('UPOW_DIST_TIMEOUT_S', '60')))
+    ctx._enter('new_group')
+    try:
+        g = dist.new_group(ranks=list(range(ctx.world)), timeout=t, backend=ctx.backend)
+    except Exception as e:
+        ctx._failed('new_group', e)
+    return dataclasses.replace(ctx, group=g, collectives=0)
 
 
 def shutdown(ctx: DistContext):

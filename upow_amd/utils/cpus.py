@@ -1,0 +1,25 @@
+"""Host CPU budget of this process (thread-pool sizing for the codec, host verify and admission)."""
+import os
+
+
+def cpu_budget(per_rank: bool = True) -> int:
+    """CPUs this process can actually use: its affinity, capped by a cgroup CPU quota (a GPU box gives a
+    node 16 CPUs' worth of time on a 256-core host; threads beyond that are throttled, not parallel).
+    ``per_rank``: one share of it per local rank (``LOCAL_WORLD_SIZE`` under torchrun) when the ranks of a
+    node share one affinity set, so 8 ranks do not each size their host pools for the whole machine."""
+    try:
+        aff = os.sched_getaffinity(0)
+        avail = len(aff)
+    except (AttributeError, OSError):
+        aff, avail = None, os.cpu_count() or 1
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            quota, period = f.read().split()[:2]
+        if quota != 'max':
+            avail = min(avail, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    local = int(os.environ.get('LOCAL_WORLD_SIZE', '1') or 1)
+    if per_rank and local > 1 and (aff is None or len(aff) >= (os.cpu_count() or 1) // 2):
+        avail = max(1, avail // local)  # not pinned per rank: split the node's budget
+    return avail

@@ -38,7 +38,9 @@ def _configure():
         log_dir = os.environ.get('UPOW_LOG_DIR') or (os.path.join(data, 'logs') if data else 'logs')
         try:
             os.makedirs(log_dir, exist_ok=True)
-            fh = RotatingFileHandler(os.path.join(log_dir, 'app.log'), maxBytes=5 * 1024 * 1024, backupCount=100)
+            rank = int(os.environ.get('RANK', '0') or 0)  # cluster followers rotate files of their own
+            name = 'app.log' if rank == 0 else f'app.rank{rank}.log'
+            fh = RotatingFileHandler(os.path.join(log_dir, name), maxBytes=5 * 1024 * 1024, backupCount=100)
         except OSError:
             return
         fh.setLevel(logging.DEBUG)
