@@ -22,6 +22,8 @@
 #   tprof    rocprofv3 kernel + roctx marker trace of the verify bench, summarised by scripts/block_trace.py
 #   sprof    the same for the sync bench (200-tx blocks)
 #   soak3    three node soaks at 1,200 tx/s (scripts/node_soak.py)
+#   soakc1   cluster node + DP miner under torchrun, forced single-rank RCCL, 40 tx/s (node_soak.py --cluster 1)
+#   soakc1k  the same at 1,200 tx/s
 #   py:<script.py>  any extra python script under scripts/ (args after a comma: py:x.py,--a,1)
 # Every GPU step has its own time limit and the chain stops at the first failure.
 set -o pipefail
@@ -131,6 +133,18 @@ for s in $STEPS; do
         --output-format csv -- python3 bench.py --mode sync --ledger /tmp/upow_bench_ledger --steps 300 --warmup 5 \
         --txs 200 > "$OUT/sprof.log" 2>&1 || { tail -20 "$OUT/sprof.log"; exit 1; }
       python scripts/block_trace.py "$OUT/sprof" --out "$OUT/sync_trace.json" | head -80 ;;
+    soakc1)
+      # BASELINE config 5 launcher on the 1-GPU box: cluster node + DP miner under torchrun, forced
+      # single-rank RCCL (scripts/node_soak.py --cluster 1)
+      timeout -k 10 420 python -u scripts/node_soak.py --cluster 1 --rate 40 --seconds 45 --difficulty 9 \
+        --out "$OUT/soak_cluster1.json" > "$OUT/soak_cluster1.log" 2>&1 || { tail -30 "$OUT/soak_cluster1.log"; exit 1; }
+      tail -1 "$OUT/soak_cluster1.log" | cut -c1-900 ;;
+    soakc1k)
+      # the same at 1,200 tx/s
+      timeout -k 10 420 python -u scripts/node_soak.py --cluster 1 --rate 1200 --seconds 45 --difficulty 9 --procs 4 \
+        --threads 8 --fanout1 255 --fanout2 220 --out "$OUT/soak_cluster1_1200.json" > "$OUT/soak_cluster1_1200.log" 2>&1 \
+        || { tail -30 "$OUT/soak_cluster1_1200.log"; exit 1; }
+      tail -1 "$OUT/soak_cluster1_1200.log" | cut -c1-900 ;;
     soak3)
       # three consecutive node soaks at 1,200 tx/s (node + GPU miner CLI + 4 x 8 pushing clients)
       for i in 1 2 3; do

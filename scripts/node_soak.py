@@ -2,7 +2,14 @@
 a full node (REST, GPU UTXO set, native block path), the GPU miner CLI pointed at it, and a
 synthetic wallet pushing ~40 tx/s through /push_tx.
 
-    python scripts/node_soak.py [--rate 40] [--seconds 120] [--difficulty 9.5] [--out FILE]
+    python scripts/node_soak.py [--rate 40] [--seconds 120] [--difficulty 9.5] [--out FILE] [--cluster N]
+
+``--cluster N`` runs BASELINE config 5 as written: the multi-GPU node (``torchrun --nproc-per-node N -m
+upow_amd.node --cluster``: rank 0 serves, ranks 1..N-1 are replicas) and the data-parallel miner
+(``torchrun --nproc-per-node N -m upow_amd.miner``) co-located on the same N GPUs, both started as child
+processes of this script before it touches a GPU. N = 1 forces the single-rank RCCL path (UPOW_FORCE_DIST).
+The report adds per-rank MH/s and the replica agreement (``/cluster_info?deep=true``: height, tip, K12 UTXO
+hash and SQL UTXO hash of every replica).
 
 Prints one JSON line: confirmed tx/s, inclusion latency (push -> block) percentiles, block interval,
 node-side block apply latency (from /metrics) and the miner's reported hashrate. Data: synthetic
@@ -99,6 +106,8 @@ def main():
     ap.add_argument('--fanout2', type=int, default=200, help='each of those -> M outputs (pool = N*M UTXOs)')
     ap.add_argument('--threads', type=int, default=1, help='concurrent /push_tx clients (per process)')
     ap.add_argument('--procs', type=int, default=1, help='client processes pushing txs')
+    ap.add_argument('--cluster', type=int, default=0,
+                    help='N > 0: multi-GPU node + DP miner on N GPUs under torchrun (N = 1: forced single-rank RCCL)')
     ap.add_argument('--client-cpus', default=None,
                     help="CPU list for the miner and the pushing clients (e.g. '16-47'), away from the node's")
     a = ap.parse_args()
@@ -128,9 +137,15 @@ def main():
                UPOW_TRACE_FILE=trace)
     if os.environ.get('UPOW_SOAK_PROFILE') == '1':
         env['UPOW_PROFILE_OUT'] = os.path.join(data, 'node.prof')
-    node = subprocess.Popen([sys.executable, '-m', 'upow_amd.node', '--host', '127.0.0.1', '--port', str(port),
-                             '--log-level', 'warning'], env=env, cwd=ROOT, stdout=open(os.path.join(data, 'node.log'), 'w'),
-                            stderr=subprocess.STDOUT)
+    launch = []  # torchrun prefix of the node and the miner in --cluster mode
+    if a.cluster:
+        if a.cluster == 1:
+            env['UPOW_FORCE_DIST'] = '1'
+        launch = lambda: [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',  # noqa: E731
+                          f'--nproc-per-node={a.cluster}', '--master-addr', '127.0.0.1', '--master-port', str(_port())]
+    node_cmd = ([*launch(), '-m', 'upow_amd.node', '--cluster'] if a.cluster else [sys.executable, '-m', 'upow_amd.node'])
+    node = subprocess.Popen([*node_cmd, '--host', '127.0.0.1', '--port', str(port), '--log-level', 'warning'],
+                            env=env, cwd=ROOT, stdout=open(os.path.join(data, 'node.log'), 'w'), stderr=subprocess.STDOUT)
     client = httpx.Client(timeout=30)
     for _ in range(600):
         try:
@@ -141,7 +156,8 @@ def main():
     miner_log = open(os.path.join(data, 'miner.log'), 'w')
     from upow_amd.ops.native import gpu_available
     chunk = [] if gpu_available() else ['--chunk', '65536', '--device', 'cpu']
-    miner = subprocess.Popen([sys.executable, '-m', 'upow_amd.miner', addr, '1', url + '/', '--refresh', '10', *chunk],
+    miner_cmd = [*launch(), '-m', 'upow_amd.miner'] if a.cluster else [sys.executable, '-m', 'upow_amd.miner']
+    miner = subprocess.Popen([*miner_cmd, addr, '1', url + '/', '--refresh', '10', *chunk],
                              preexec_fn=client_pin,
                              env=env, cwd=ROOT, stdout=miner_log, stderr=subprocess.STDOUT)
     t_start = time.time()
@@ -298,6 +314,13 @@ def main():
     stop.set()
     w.join(5)
     metrics = client.get(url + '/metrics').text
+    replicas = None
+    if a.cluster:
+        ci = client.get(url + '/cluster_info', params={'deep': 'true'}, timeout=120).json()['result']
+        reps = ci['replicas']
+        replicas = {'world': ci['world'], 'backend': ci['backend'], 'last_resync': ci.get('last_resync'),
+                    'agree': len({(r['height'], r['tip_hash'], r['utxo_hash'], r.get('sql_utxo_hash')) for r in reps}) == 1,
+                    'replicas': reps}
     miner.terminate()
     node.terminate()
     for p in (miner, node):
@@ -318,7 +341,9 @@ def main():
             f.write(buf.getvalue())
     included = {h: included[h] for h in pushed if h in included}
     lat = sorted(included[h] - pushed[h] for h in included)
-    rates = [float(x) for x in re.findall(r'([0-9.]+) MH/s', open(os.path.join(data, 'miner.log')).read())]
+    miner_text = open(os.path.join(data, 'miner.log')).read()
+    rates = [float(x) for x in re.findall(r'([0-9.]+) MH/s \(', miner_text)]
+    per_rank = [json.loads(x) for x in re.findall(r'per-rank MH/s: (\[[^\]]*\])', miner_text)]
     apply = {}
     for ln in metrics.splitlines():
         m = re.match(r'upow_block_apply_seconds_(sum|count)\{path="(\w+)"\} (\S+)', ln)
@@ -406,6 +431,11 @@ def main():
         if cpu0 and cpu1 else None,
         'difficulty': a.difficulty, 'setup_s': round(setup_s, 1), 'data': 'synthetic keys, miner coinbases fanned out',
     }
+    if a.cluster:
+        out['cluster'] = {'gpus': a.cluster, 'node': 'torchrun -m upow_amd.node --cluster',
+                          'miner': 'torchrun -m upow_amd.miner (nonce-space DP)',
+                          'miner_per_rank_mhs_median': [sorted(col)[len(col) // 2] for col in zip(*per_rank)] if per_rank else None,
+                          **(replicas or {})}
     line = json.dumps(out)
     print(line, flush=True)
     if a.out:

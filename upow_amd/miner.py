@@ -133,9 +133,12 @@ def main(argv=None):
             header = miner.mine(should_stop=lambda: time.time() - t0 > a.refresh or
                                 (watcher is not None and watcher.moved(prev)))
             dt = max(time.time() - t0, 1e-9)
-            rate = ctx.allreduce_sum(miner.hashes) / dt
+            per_rank = [float(x) / dt for x in ctx.all_gather_bytes(str(miner.hashes).encode())]
+            rate = sum(per_rank)
             if ctx.is_main:
                 print(f'{rate / 1e6:.1f} MH/s ({ctx.world} x {device})', flush=True)
+                if ctx.world > 1 or ctx.forced:
+                    print('per-rank MH/s: ' + json.dumps([round(r / 1e6, 1) for r in per_rank]), flush=True)
                 if header is not None:
                     print(header.hex())
                     print(','.join(hashes))

@@ -70,8 +70,8 @@ def main(argv=None):
         os.environ['UPOW_CORE_URL'] = a.core_url
     os.environ.setdefault('UPOW_FILE_LOG', '1')  # reference: logs/app.log always (my_logger.py:17-53)
     import uvicorn
-    if a.cluster and int(os.environ.get('WORLD_SIZE', '1')) > 1:
-        return _run_cluster(a)
+    if a.cluster and (int(os.environ.get('WORLD_SIZE', '1')) > 1 or os.environ.get('UPOW_FORCE_DIST') == '1'):
+        return _run_cluster(a)  # UPOW_FORCE_DIST=1: a single-rank cluster (the op stream over RCCL on one GPU)
     prof_out = os.environ.get('UPOW_PROFILE_OUT')  # cProfile of the serving process (load tests)
     if prof_out:
         import cProfile
