@@ -12,6 +12,7 @@ import time
 
 import httpx
 import pytest
+from hypothesis import HealthCheck, given, settings, strategies as st
 import uvicorn
 from starlette.applications import Starlette
 from starlette.responses import JSONResponse, PlainTextResponse, StreamingResponse
@@ -216,3 +217,67 @@ def test_client_gone_before_the_response_leaves_the_server_serving(server):
     time.sleep(0.2)
     r = httpx.get(f'http://127.0.0.1:{server}/hello', params={'q': 'still'}, timeout=5)
     assert r.status_code == 200 and r.json()['q'] == 'still'
+
+
+_GOOD = [b'GET /hello?q=1 HTTP/1.1\r\nHost: x\r\n\r\n',
+         b'POST /echo HTTP/1.1\r\nHost: x\r\nContent-Length: 3\r\n\r\nabc',
+         b'POST /echo HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n2\r\nhi\r\n0\r\n\r\n',
+         b'GET /missing HTTP/1.1\r\n\r\n']
+_BAD = [b'GARBAGE\r\n\r\n', b'GET  HTTP/1.1\r\n\r\n', b'GET / HTTP/2.0\r\n\r\n', b'G\x00T / HTTP/1.1\r\n\r\n',
+        b'GET / HTTP/1.1\r\n folded: x\r\n\r\n', b'GET / HTTP/1.1\r\nBad Header: 1\r\n\r\n',
+        b'GET / HTTP/1.1\r\nX: a\x01b\r\n\r\n',
+        b'POST /echo HTTP/1.1\r\nContent-Length: -5\r\n\r\n', b'POST /echo HTTP/1.1\r\nContent-Length: 99999999999999999999\r\n\r\n',
+        b'POST /echo HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n-5\r\nhello\r\n0\r\n\r\n',
+        b'POST /echo HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\nfffffffffffffffffff\r\n',
+        b'POST /echo HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n3\r\nabcXY0\r\n\r\n',
+        b'POST /echo HTTP/1.1\r\nTransfer-Encoding: gzip\r\n\r\n',
+        b'POST /echo HTTP/1.1\r\nContent-Length: 1\r\nTransfer-Encoding: chunked\r\n\r\n',
+        b'GET / HTTP/1.1\r\n' + b'X-Long: ' + b'a' * 70000 + b'\r\n\r\n']
+
+
+@settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(st.lists(st.one_of(st.sampled_from(_GOOD), st.sampled_from(_BAD), st.binary(max_size=40)), min_size=1, max_size=5),
+       st.lists(st.integers(1, 50), min_size=1, max_size=8))
+def test_random_streams_get_400_or_close_never_a_crash(server, pieces, cuts):
+    """Pipelined mixes of valid requests, malformed request lines and headers, oversized / negative /
+    non-hex chunk sizes and random garbage, written in random segments: the server answers every complete
+    valid request before the first bad one, answers the bad one with a 400 (or closes), and stays up."""
+    data = b''.join(pieces)
+    with socket.create_connection(('127.0.0.1', server), timeout=3) as c:
+        at, k = 0, 0
+        try:  # the server may answer 400 and close while the rest is still being written
+            while at < len(data):
+                n = cuts[k % len(cuts)]
+                c.sendall(data[at:at + n])
+                at += n
+                k += 1
+            c.shutdown(socket.SHUT_WR)
+        except OSError:  # broken pipe, reset, or not connected any more
+            pass
+        out = b''
+        while True:
+            try:
+                chunk = c.recv(65536)
+            except OSError:
+                break
+            if not chunk:
+                break
+            out += chunk
+    statuses = [int(p[:3]) for p in out.split(b'HTTP/1.1 ')[1:] if p[:3].isdigit()]
+    assert all(s in (100, 200, 400, 404, 405, 413, 431) for s in statuses), (statuses, out[:300])
+    if pieces[0] in _BAD:
+        assert statuses[:1] in ([], [400], [413], [431]), (statuses, out[:300])
+    with httpx.Client(base_url=f'http://127.0.0.1:{server}', timeout=5) as h:  # the server is still serving
+        assert h.get('/hello').status_code == 200
+
+
+def test_ws_64bit_length_with_msb_set_is_a_protocol_error(native):
+    """RFC 6455 5.2: the most significant bit of a 64-bit payload length must be 0: the parser
+    answers 1002 instead of reading a negative length."""
+    p = native.WsParser(1 << 16)
+    with pytest.raises(ValueError) as e:
+        p.feed(b'\x81\xff' + b'\x80' + b'\x00' * 7 + b'\x01\x02\x03\x04')
+    assert e.value.args[1] == 1002
+    with pytest.raises(ValueError) as e:  # just over the limit: 1009, whatever the buffered bytes
+        native.WsParser(100).feed(b'\x82\xff' + (101).to_bytes(8, 'big') + b'\x00' * 4)
+    assert e.value.args[1] == 1009

@@ -1,7 +1,10 @@
-"""Host C++ under AddressSanitizer + UndefinedBehaviorSanitizer (tools/sanitize_host.sh).
+"""Host C++ under the sanitizers (tools/sanitize_host.sh): the host crypto self-test under ASan + UBSan and
+the host pool under TSan; libFuzzer + ASan + UBSan on the network parsers (tx decoder, HTTP/WebSocket
+framing); and the Python tests of every pybind11 module with the whole extension instrumented, under
+ASan + UBSan and (the threaded ones) TSan.
 
-The first build takes a few minutes (the HIP translation unit is compiled for gfx950 with an
-instrumented host side); later runs reuse the objects under build/sanitize."""
+The first run builds the instrumented objects and extensions (several minutes); later runs reuse them
+under build/sanitize and build/native-{asan,tsan}."""
 import os
 import shutil
 import subprocess
@@ -13,9 +16,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 @pytest.mark.slow
 @pytest.mark.skipif(shutil.which('/opt/rocm/bin/hipcc') is None, reason='no ROCm toolchain')
-def test_host_code_clean_under_asan_ubsan():
+def test_host_code_clean_under_sanitizers_and_fuzzing():
+    env = dict(os.environ, FUZZ_SECONDS=os.environ.get('FUZZ_SECONDS', '10'))
     r = subprocess.run([os.path.join(ROOT, 'tools', 'sanitize_host.sh')], cwd=ROOT, capture_output=True, text=True,
-                       timeout=1200)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    assert 'host selftest: all checks passed' in r.stdout
-    assert 'pool selftest: all checks passed' in r.stdout  # ThreadSanitizer run of csrc/thread_pool.h
+                       timeout=2400, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-4000:]
+    out = r.stdout
+    assert 'host selftest: all checks passed' in out
+    assert 'pool selftest: all checks passed' in out  # ThreadSanitizer run of csrc/thread_pool.h
+    assert 'fuzz http: Done' in out and 'fuzz txdecode: Done' in out
+    assert 'python tests under ASan + UBSan:' in out and 'python tests under TSan:' in out
+    assert 'sanitize_host: all stages passed' in out

@@ -205,3 +205,60 @@ def test_address_pairs_distinct_per_tx(L):
     got = list(zip(np.frombuffer(tx, np.int64).tolist(), arena_list((blob, off))))
     want = [(k, a) for k, t in enumerate(txs) for a in dict.fromkeys(t[0] + t[1])]
     assert got == want
+
+
+def _mutate(rng, raw: bytes, other: bytes) -> bytes:
+    """One structural mutation of a serialised tx: flip/overwrite a byte, insert or delete a run, truncate,
+    duplicate a range, bump a count byte, splice in a piece of another tx, or upper-case / odd-length hex."""
+    b = bytearray(raw)
+    op = rng.randrange(8)
+    if not b:
+        return bytes(other[:rng.randrange(len(other) + 1)])
+    i = rng.randrange(len(b))
+    if op == 0:
+        b[i] ^= 1 << rng.randrange(8)
+    elif op == 1:
+        b[i] = rng.choice([0, 1, 2, 3, 4, 10, 33, 36, 42, 43, 64, 127, 128, 254, 255])
+    elif op == 2:
+        b[i:i] = rng.randbytes(rng.randint(1, 70))
+    elif op == 3:
+        del b[i:i + rng.randint(1, 70)]
+    elif op == 4:
+        del b[i:]
+    elif op == 5:
+        j = rng.randrange(len(b))
+        b[i:i] = b[min(i, j):max(i, j)][:200]
+    elif op == 6:
+        for k in (1, 2 + 34 * raw[1] if len(raw) > 1 else 1):  # the input / output count bytes
+            if k < len(b):
+                b[k] = (b[k] + rng.choice([-1, 1, 2, 255])) % 256
+    else:
+        j = rng.randrange(len(other) + 1)
+        b[i:] = other[j:j + rng.randint(1, 200)]
+    return bytes(b)
+
+
+@settings(max_examples=400, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(st.integers(0, 10 ** 9), st.integers(1, 4))
+def test_mutated_txs_rejected_or_agree_with_python_parser(native, seed, n_mut):
+    """Structured mutations of valid txs of every shape (multi-input, one or n signatures, messages, v1
+    64-byte addresses): for every mutant the native codec either does not claim the fast path, or the
+    Python parser (reference transaction.py:520-592) accepts the same bytes and serialises, hashes and
+    splits them identically. A block holding a mutant among valid txs is all-fast only if the mutant is."""
+    rng = random.Random(seed)
+    shapes = [dict(), dict(version=1), dict(msg=b'hello'), dict(n_in=3, one_sig=False), dict(n_in=2, one_sig=True)]
+    a, b = (_tx(rng, **rng.choice(shapes)).hex() for _ in range(2))
+    raw = bytes.fromhex(a)
+    for _ in range(n_mut):
+        raw = _mutate(rng, raw, bytes.fromhex(b))
+    cands = [raw.hex()]
+    if rng.random() < 0.3:
+        cands.append(raw.hex().upper())
+    for cand in cands:
+        d = native.decode_block_txs([cand], 1)
+        if d['all_fast']:
+            _check_fast(d, [cand])
+        blk = native.decode_block_txs([b, cand, a], 2)
+        assert bool(blk['all_fast']) == bool(d['all_fast'])
+        if blk['all_fast']:
+            _check_fast(blk, [b, cand, a])

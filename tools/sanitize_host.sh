@@ -1,9 +1,27 @@
 #!/usr/bin/env bash
-# Build tools/host_selftest.cpp + the native library's host code with ASan + UBSan and run it
-# (CPU only: GPU sanitizers are not used). Usage: tools/sanitize_host.sh [outdir]
+# Host code under the sanitizers (CPU only: GPU sanitizers are not used on this pool).
+#
+#   tools/sanitize_host.sh [outdir]          (FUZZ_SECONDS=N per fuzz target, default 20)
+#
+# 1. tools/host_selftest.cpp + the host crypto (SHA-256, SHA-NI, base58, P-256) under ASan + UBSan;
+#    the host worker pool (csrc/thread_pool.h) under ThreadSanitizer.
+# 2. libFuzzer + ASan + UBSan on the parsers of untrusted network input: the tx decoder every pushed tx and
+#    every peer block goes through (csrc/txdecode.h, tools/fuzz/fuzz_txdecode.cpp) and the HTTP/1.1 +
+#    WebSocket framing of every request (csrc/http_wire.h, tools/fuzz/fuzz_http.cpp), seeded with valid
+#    txs / requests / frames (tools/fuzz/make_corpus.py). ASan's global redzones are off for these builds
+#    (-mllvm -asan-globals=0): the fuzzer runtime and the target register some header-defined globals
+#    twice, which ASan reports as an ODR violation before the first input.
+# 3. The whole native extension built instrumented (python -m upow_amd._build --variant asan|tsan) and
+#    loaded by an interpreter linked with the same runtime (tools/pysan.c, UPOW_NATIVE_SO): the Python
+#    tests of every pybind11 module run under ASan + UBSan (txcodec, http_wire, mempool_index,
+#    ledger_writer, gov_index, log_appender, the block path) and the threaded ones under TSan
+#    (mempool index lookups racing a GIL-free confirm, the journal writer's I/O and materialiser threads,
+#    the log appender's writer thread).
 set -euo pipefail
 cd "$(dirname "$0")/.."
+ROOT=$(pwd)
 OUT=${1:-build/sanitize}
+FUZZ_SECONDS=${FUZZ_SECONDS:-20}
 mkdir -p "$OUT"
 SAN_HOST="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined"
 CXX=/opt/rocm/llvm/bin/clang++
@@ -18,6 +36,7 @@ stale() {  # $1 = object, rest = inputs: rebuild when any input is newer
   return 1
 }
 HDRS="csrc/native.h csrc/sha256_common.h csrc/p256_field.h"
+echo "== [1] host selftest (ASan + UBSan) and host pool (TSan)"
 if stale "$OUT/p256.o" csrc/p256.hip $HDRS; then
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -Xarch_host -O0 -g1 -std=c++17 -I/opt/rocm/include $SAN_HOST \
     -c csrc/p256.hip -o "$OUT/p256.o"
@@ -37,3 +56,47 @@ if stale "$OUT/pool_selftest" tools/pool_selftest.cpp csrc/thread_pool.h; then
   $CXX -O1 -g -std=c++17 -fsanitize=thread -pthread -Icsrc tools/pool_selftest.cpp -o "$OUT/pool_selftest"
 fi
 TSAN_OPTIONS=halt_on_error=1 "$OUT/pool_selftest"
+
+echo "== [2] libFuzzer targets (ASan + UBSan), ${FUZZ_SECONDS} s each"
+FZ="-O1 -g -fno-omit-frame-pointer -std=c++17 -fsanitize=fuzzer,address,undefined -fno-sanitize-recover=undefined -mllvm -asan-globals=0 -I/opt/rocm/include"
+if stale "$OUT/fuzz_http" tools/fuzz/fuzz_http.cpp csrc/http_wire.h; then
+  $CXX $FZ tools/fuzz/fuzz_http.cpp -o "$OUT/fuzz_http"
+fi
+if stale "$OUT/fuzz_txdecode" tools/fuzz/fuzz_txdecode.cpp csrc/txdecode.h csrc/base58.cpp csrc/sha256_host.cpp $HDRS; then
+  $CXX $FZ tools/fuzz/fuzz_txdecode.cpp csrc/base58.cpp csrc/sha256_ni.cpp csrc/sha256_host.cpp -pthread -o "$OUT/fuzz_txdecode"
+fi
+UPOW_NO_TORCH=1 python3 tools/fuzz/make_corpus.py "$OUT/corpus" > /dev/null
+for t in http txdecode; do
+  seeds=$OUT/corpus/${t#txdecode}; [ "$t" = txdecode ] && seeds=$OUT/corpus/tx
+  mkdir -p "$OUT/work_$t"
+  (cd "$OUT" && ./fuzz_$t -max_total_time="$FUZZ_SECONDS" -print_final_stats=1 "work_$t" "$ROOT/$seeds" > "fuzz_$t.log" 2>&1) \
+    || { tail -40 "$OUT/fuzz_$t.log"; exit 1; }
+  echo "fuzz $t: $(grep -E '^Done [0-9]+ runs' "$OUT/fuzz_$t.log") (corpus $(ls "$OUT/work_$t" | wc -l) inputs, no crash)"
+done
+
+echo "== [3] the native extension instrumented, its Python tests under ASan + UBSan and TSan"
+python3 -m upow_amd._build --variant asan -j 8 > /dev/null
+python3 -m upow_amd._build --variant tsan -j 8 > /dev/null
+PYINC=$(python3 -c 'import sysconfig; print(sysconfig.get_paths()["include"])')
+for v in asan tsan; do
+  san=$([ $v = asan ] && echo "-fsanitize=address,undefined" || echo "-fsanitize=thread")
+  if stale "$OUT/pysan_$v" tools/pysan.c; then
+    $CXX -x c++ -O1 -g $san -I"$PYINC" tools/pysan.c -L/usr/lib/x86_64-linux-gnu -lpython3.10 -Wl,--no-as-needed -lstdc++ \
+      -o "$OUT/pysan_$v"
+  fi
+done
+EXT=$(python3 -c 'import sysconfig; print(sysconfig.get_config_var("EXT_SUFFIX"))')
+export UPOW_NO_TORCH=1 UPOW_DISABLE_GPU=1 PYTHONMALLOC=malloc
+UPOW_NATIVE_SO=$ROOT/build/native-asan/_native$EXT ASAN_OPTIONS=detect_leaks=0:detect_odr_violation=0:abort_on_error=1 \
+  UBSAN_OPTIONS=print_stacktrace=1 timeout -k 10 1500 "$OUT/pysan_asan" -m pytest -q -x -m "not gpu" -p no:cacheprovider \
+  tests/test_txcodec.py tests/test_http_server.py tests/test_mempool_index.py tests/test_ledger_writer.py \
+  tests/test_gov_cascade.py tests/test_log_appender.py tests/test_fastpath.py tests/test_fastpath_governance.py \
+  tests/test_rollback_undo.py tests/test_crash_recovery.py > "$OUT/pytest_asan.log" 2>&1 \
+  || { tail -60 "$OUT/pytest_asan.log"; exit 1; }
+echo "python tests under ASan + UBSan: $(tail -1 "$OUT/pytest_asan.log")"
+UPOW_NATIVE_SO=$ROOT/build/native-tsan/_native$EXT TSAN_OPTIONS=halt_on_error=1:report_signal_unsafe=0 \
+  timeout -k 10 900 "$OUT/pysan_tsan" -m pytest -q -x -m "not gpu" -p no:cacheprovider \
+  tests/test_mempool_index.py tests/test_ledger_writer.py tests/test_log_appender.py > "$OUT/pytest_tsan.log" 2>&1 \
+  || { tail -60 "$OUT/pytest_tsan.log"; exit 1; }
+echo "python tests under TSan: $(tail -1 "$OUT/pytest_tsan.log")"
+echo "sanitize_host: all stages passed"

@@ -46,51 +46,75 @@ def _flags_common():
     return ['-O3', '-std=c++17', '-fPIC', '-Wall', '-Wno-unused-function', f'-I{CSRC}']
 
 
-def _compile(src: Path, hdr_digest: str, force: bool) -> Path:
-    BUILD.mkdir(parents=True, exist_ok=True)
-    key = hashlib.sha256(src.read_bytes() + hdr_digest.encode() + ARCH.encode()).hexdigest()[:16]
-    obj = BUILD / f'{src.stem}.{key}.o'
+# Sanitizer variants (tools/sanitize_host.sh): the same sources, host code instrumented, linked into
+# build/native-<variant>/_native*.so and loaded by an instrumented embedded interpreter (tools/pysan.c)
+# through UPOW_NATIVE_SO. Device code keeps -O3; the HIP TUs' host side is instrumented at -O0 (the
+# force-inlined 256-bit field code takes ~10 min to optimise under instrumentation).
+SAN_FLAGS = {'asan': ['-fsanitize=address,undefined', '-fno-sanitize-recover=undefined'],
+             'tsan': ['-fsanitize=thread']}
+CLANGXX = '/opt/rocm/llvm/bin/clang++'
+
+
+def _build_dir(variant: str) -> Path:
+    return BUILD if variant == 'release' else ROOT / 'build' / f'native-{variant}'
+
+
+def _compile(src: Path, hdr_digest: str, force: bool, variant: str = 'release') -> Path:
+    out = _build_dir(variant)
+    out.mkdir(parents=True, exist_ok=True)
+    key = hashlib.sha256(src.read_bytes() + hdr_digest.encode() + ARCH.encode() + variant.encode()).hexdigest()[:16]
+    obj = out / f'{src.stem}.{key}.o'
     if obj.exists() and not force:
         return obj
+    san = SAN_FLAGS.get(variant)
     if src.suffix == '.hip':
-        cmd = [HIPCC, f'--offload-arch={ARCH}', *_flags_common(), '-c', str(src), '-o', str(obj)]
+        host = [] if san is None else ['-Xarch_host', '-O0', '-Xarch_host', '-g1',
+                                       *[x for f in san for x in ('-Xarch_host', f)]]
+        cmd = [HIPCC, f'--offload-arch={ARCH}', *_flags_common(), *host, '-c', str(src), '-o', str(obj)]
     else:
         # host-only translation units: plain C++ (no device pass)
-        cmd = [CXX, *_flags_common(), f'-I{_pybind_include()}', f'-I{sysconfig.get_paths()["include"]}',
-               '-fvisibility=hidden', '-c', str(src), '-o', str(obj)]
+        cxx, extra = (CXX, []) if san is None else (CLANGXX, ['-O1', '-g', '-fno-omit-frame-pointer', *san])
+        cmd = [cxx, *_flags_common(), *extra, f'-I{_pybind_include()}', f'-I{sysconfig.get_paths()["include"]}',
+               '-I/opt/rocm/include', '-fvisibility=hidden', '-c', str(src), '-o', str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f'compile failed: {" ".join(cmd)}\n{r.stdout}\n{r.stderr}')
     return obj
 
 
-def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> Path:
+def build(force: bool = False, jobs: int = 4, verbose: bool = True, variant: str = 'release') -> Path:
+    """Compile and link the extension; ``variant`` 'asan' / 'tsan' builds an instrumented copy under
+    build/native-<variant>/ (the in-tree release .so is untouched)."""
     srcs = sorted(CSRC.glob('*.hip')) + sorted(CSRC.glob('*.cpp'))
     hd = _headers_digest()
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hd, force), srcs))
+        objs = list(ex.map(lambda s: _compile(s, hd, force, variant), srcs))
+    target = TARGET if variant == 'release' else _build_dir(variant) / TARGET.name
     link_key = hashlib.sha256(''.join(o.name for o in objs).encode()).hexdigest()[:16]
-    stamp = BUILD / 'link.stamp'
-    if TARGET.exists() and stamp.exists() and stamp.read_text() == link_key and not force:
+    stamp = _build_dir(variant) / 'link.stamp'
+    if target.exists() and stamp.exists() and stamp.read_text() == link_key and not force:
         if verbose:
-            print(f'[upow_amd._build] up to date: {TARGET.name}')
-        return TARGET
-    cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', str(TARGET), *map(str, objs), '-ldl']
+            print(f'[upow_amd._build] up to date: {target.name}')
+        return target
+    TARGET_ = target
+    # instrumented variants leave the sanitizer runtime to the executable that loads them (tools/pysan.c)
+    cmd = [HIPCC, f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', str(TARGET_), *map(str, objs), '-ldl']
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f'link failed: {" ".join(cmd)}\n{r.stdout}\n{r.stderr}')
     stamp.write_text(link_key)
     if verbose:
-        print(f'[upow_amd._build] built {TARGET} from {len(objs)} objects')
-    return TARGET
+        print(f'[upow_amd._build] built {TARGET_} from {len(objs)} objects')
+    return TARGET_
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--force', action='store_true')
     ap.add_argument('-j', '--jobs', type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument('--variant', choices=['release', 'asan', 'tsan'], default='release')
     a = ap.parse_args(argv)
-    build(force=a.force, jobs=a.jobs)
+    build(force=a.force, jobs=a.jobs, variant=a.variant)
 
 
 if __name__ == '__main__':

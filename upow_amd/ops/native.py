@@ -40,6 +40,15 @@ def lib():
     with _lock:
         if _lib is None:
             _preload_torch_hip()
+            so = os.environ.get('UPOW_NATIVE_SO')  # an instrumented build (tools/sanitize_host.sh)
+            if so:
+                import importlib.util as ilu
+                import sys
+                spec = ilu.spec_from_file_location('upow_amd._native', so)
+                _lib = ilu.module_from_spec(spec)
+                spec.loader.exec_module(_lib)
+                sys.modules['upow_amd._native'] = _lib
+                return _lib
             try:
                 _lib = importlib.import_module('upow_amd._native')
             except ImportError as e:
