@@ -808,7 +808,95 @@ static py::tuple spent_index_records(py::buffer keys_b, py::buffer tag_b) {
     return py::make_tuple(spent, idx);
 }
 
+// Cluster op frames (upow_amd/parallel/cluster.py pack_txs / unpack_txs): a block's tx hex strings as raw
+// bytes, u32 count then u32 length + bytes per tx, hex-decoded on the host pool without the GIL; and back
+// to lower-case hex strings on the follower. A string that is not even-length hex raises ValueError.
+static py::bytes pack_tx_hexes(py::list hexes, int threads) {
+    const size_t n = hexes.size();
+    std::vector<const char*> ptr(n);
+    std::vector<size_t> len(n), off(n + 1);
+    off[0] = 4;
+    for (size_t i = 0; i < n; ++i) {
+        PyObject* o = hexes[i].ptr();
+        if (!PyUnicode_Check(o)) throw py::type_error("tx hex must be str");
+        Py_ssize_t k = 0;
+        ptr[i] = PyUnicode_AsUTF8AndSize(o, &k);
+        if (!ptr[i]) throw py::error_already_set();
+        if (k % 2) throw py::value_error("tx hex of odd length");
+        len[i] = size_t(k) / 2;
+        off[i + 1] = off[i] + 4 + len[i];
+    }
+    char* out = nullptr;
+    py::bytes res = new_pybytes(off[n], out);
+    const uint32_t cnt = uint32_t(n);
+    std::memcpy(out, &cnt, 4);
+    std::atomic<bool> bad{false};
+    {
+        py::gil_scoped_release nogil;  // the str objects stay alive: `hexes` holds them
+        parallel_for(int64_t(n), threads, [&](int64_t i) {
+            uint8_t* d = reinterpret_cast<uint8_t*>(out) + off[size_t(i)];
+            const uint32_t l = uint32_t(len[size_t(i)]);
+            std::memcpy(d, &l, 4);
+            const uint8_t* h = reinterpret_cast<const uint8_t*>(ptr[size_t(i)]);
+            uint8_t acc = 0;
+            for (size_t j = 0; j < l; ++j) {
+                const uint8_t hi = kHexTab[h[2 * j]], lo = kHexTab[h[2 * j + 1]];
+                acc |= hi | lo;
+                d[4 + j] = uint8_t(hi << 4 | (lo & 15));
+            }
+            if (acc & 0x80) bad.store(true, std::memory_order_relaxed);
+        });
+    }
+    if (bad.load()) throw py::value_error("tx hex holds a non-hex character");
+    return res;
+}
+
+static py::list unpack_tx_hexes(py::bytes frame, int threads) {
+    char* p = nullptr;
+    Py_ssize_t total = 0;
+    PyBytes_AsStringAndSize(frame.ptr(), &p, &total);
+    const size_t nb = size_t(total);
+    if (nb < 4) throw py::value_error("cluster frame: short tx list");
+    uint32_t cnt;
+    std::memcpy(&cnt, p, 4);
+    std::vector<size_t> off, len;
+    size_t at = 4;
+    for (uint32_t i = 0; i < cnt; ++i) {
+        if (nb - at < 4) throw py::value_error("cluster frame: truncated tx list");
+        uint32_t l;
+        std::memcpy(&l, p + at, 4);
+        if (nb - at - 4 < l) throw py::value_error("cluster frame: truncated tx");
+        off.push_back(at + 4);
+        len.push_back(l);
+        at += 4 + size_t(l);
+    }
+    if (at != nb) throw py::value_error("cluster frame: trailing bytes after the tx list");
+    py::list out = new_list(cnt);
+    std::vector<PyObject*> strs(cnt);
+    for (uint32_t i = 0; i < cnt; ++i) {
+        strs[i] = PyUnicode_New(Py_ssize_t(2 * len[i]), 127);
+        if (!strs[i]) throw py::error_already_set();
+        PyList_SET_ITEM(out.ptr(), Py_ssize_t(i), strs[i]);  // the list owns it from here
+    }
+    std::vector<char*> dst(cnt);
+    for (uint32_t i = 0; i < cnt; ++i) dst[i] = static_cast<char*>(PyUnicode_DATA(strs[i]));
+    {
+        py::gil_scoped_release nogil;
+        parallel_for(int64_t(cnt), threads, [&](int64_t i) {
+            const uint8_t* b = reinterpret_cast<const uint8_t*>(p) + off[size_t(i)];
+            char* h = dst[size_t(i)];
+            for (size_t j = 0; j < len[size_t(i)]; ++j) {
+                h[2 * j] = kHex[b[j] >> 4];
+                h[2 * j + 1] = kHex[b[j] & 15];
+            }
+        });
+    }
+    return out;
+}
+
 void register_txcodec(py::module_& m) {
+    m.def("pack_tx_hexes", &pack_tx_hexes, py::arg("hexes"), py::arg("threads") = 8);
+    m.def("unpack_tx_hexes", &unpack_tx_hexes, py::arg("frame"), py::arg("threads") = 8);
     m.def("output_index_records", &output_index_records, py::arg("txid"), py::arg("index"), py::arg("tag"),
           py::arg("amount"), py::arg("addr"), py::arg("len"), py::arg("stake"));
     m.def("spent_index_records", &spent_index_records, py::arg("keys"), py::arg("tag"));

@@ -126,25 +126,20 @@ def _mempool_size(db) -> int:
 
 
 def pack_txs(tx_hexes) -> bytes:
-    """Raw tx bytes of a block: u32 count, then u32 length + bytes per tx."""
-    parts = [len(tx_hexes).to_bytes(4, 'little')]
-    for h in tx_hexes:
-        raw = bytes.fromhex(h)
-        parts.append(len(raw).to_bytes(4, 'little'))
-        parts.append(raw)
-    return b''.join(parts)
+    """Raw tx bytes of a block: u32 count, then u32 length + bytes per tx (hex-decoded natively on the
+    host pool, csrc/txcodec.cpp ``pack_tx_hexes``)."""
+    from ..ops.native import lib
+    return lib().pack_tx_hexes(list(tx_hexes), _threads())
 
 
 def unpack_txs(buf: bytes) -> List[str]:
-    n = int.from_bytes(buf[:4], 'little')
-    out, o = [], 4
-    for _ in range(n):
-        k = int.from_bytes(buf[o:o + 4], 'little')
-        out.append(buf[o + 4:o + 4 + k].hex())
-        o += 4 + k
-    if o != len(buf):
-        raise ValueError('cluster frame: trailing bytes after the tx list')
-    return out
+    from ..ops.native import lib
+    return lib().unpack_tx_hexes(bytes(buf), _threads())
+
+
+def _threads() -> int:
+    from ..ledger.fastpath import THREADS
+    return THREADS
 
 
 def init(ctx: DistContext, init_ctx: Optional[DistContext] = None) -> Optional[Cluster]:
