@@ -116,7 +116,7 @@ def _verify_once(args, ctx, keys: str) -> dict:
     try:
         v = argparse.Namespace(**{**vars(args), 'steps': args.verify_steps, 'warmup': 2, 'ledger': tmp,
                                   'object_path': False, 'from_mempool': False, 'governance': False,
-                                  'governance_txs': 0.0, 'age_txs': 0, 'keys': keys})
+                                  'governance_txs': 0.0, 'age_txs': 0, 'keys': keys, 'grouped_txs': 0.0})
         return run_cluster_verify_bench(v, ctx) if ctx.is_distributed else run_verify_bench(v, ctx)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
@@ -182,6 +182,9 @@ def main(argv=None):
                     help='verify mode: seed 12 inodes, 200 validators, 5,000 delegates with ballots before the blocks')
     ap.add_argument('--governance-txs', default='0',
                     help="verify mode: fraction of each block's txs that are governance txs, e.g. 5%% or 0.05")
+    ap.add_argument('--grouped-txs', default='0',
+                    help="verify mode (distinct keys): fraction of each block's txs with 2 signatures over 4 inputs of "
+                         "two keys (signature grouping by owner key), e.g. 10%%")
     ap.add_argument('--age-txs', type=int, default=0,
                     help='verify/sync modes: first age the ledger with N confirmed txs (2N UTXO rows), e.g. 2500000')
     ap.add_argument('--keys', choices=['distinct', 'pool256'], default='distinct',
@@ -193,6 +196,8 @@ def main(argv=None):
     args = ap.parse_args(argv)
     g = str(args.governance_txs).strip()
     args.governance_txs = float(g[:-1]) / 100 if g.endswith('%') else float(g)
+    g = str(args.grouped_txs).strip()
+    args.grouped_txs = float(g[:-1]) / 100 if g.endswith('%') else float(g)
 
     # rank launch: the driver either starts N ranks itself (torchrun sets WORLD_SIZE) or runs
     # ``bench.py --gpus N`` plainly, in which case this process becomes the launcher of N ranks

@@ -195,7 +195,7 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
     }
     auto t1 = std::chrono::steady_clock::now();
     py::dict d;
-    std::vector<uint8_t> flags(N), version(N), tx_type(N);
+    std::vector<uint8_t> flags(N), version(N), tx_type(N), grouped(N);
     std::vector<int32_t> in_start(N + 1), out_start(N + 1), sig_start(N + 1), signed_len(N), msg_off(N), msg_len(N),
         hex_len(N);
     int64_t n_in = 0, n_out = 0, n_sig = 0;
@@ -206,6 +206,7 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
         all_fast &= t.flag == TX_FAST;
         version[size_t(i)] = t.version;
         tx_type[size_t(i)] = t.tx_type;
+        grouped[size_t(i)] = t.grouped;
         in_start[size_t(i)] = int32_t(n_in);
         out_start[size_t(i)] = int32_t(n_out);
         sig_start[size_t(i)] = int32_t(n_sig);
@@ -228,6 +229,7 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
     d["flags"] = as_bytes(flags);
     d["version"] = as_bytes(version);
     d["tx_type"] = as_bytes(tx_type);
+    d["grouped"] = as_bytes(grouped);  // per tx: signatures grouped by owner key (sig_first_in -1 until resolved)
     d["in_start"] = i32(in_start);
     d["out_start"] = i32(out_start);
     d["sig_start"] = i32(sig_start);
@@ -316,7 +318,7 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
                 std::memcpy(&in_keys[40 * k + 32], &idx, 4);
                 std::memcpy(&in_keys[40 * k + 36], &tag, 4);
                 in_type[k] = in.type;
-                in_sig[k] = sig_start[i] + in.sig;
+                in_sig[k] = in.sig < 0 ? -1 : sig_start[i] + in.sig;
                 // signatures are numbered in order of first use within the tx: the first input that uses
                 // a signature is the one for which it is the next new number
                 if (in.sig == k_new_sig) {
@@ -326,6 +328,8 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
                 in_tx[k] = int32_t(i);
                 ++k;
             }
+            if (t.grouped)
+                for (size_t g = 0; g < t.sigs.size() / 64; ++g) sig_first_in[size_t(sig_start[i]) + g] = -1;
             if (!t.sigs.empty()) std::memcpy(&sigs[64 * size_t(sig_start[i])], t.sigs.data(), t.sigs.size());
             size_t o = size_t(out_start[i]);
             for (size_t j = 0; j < t.outs.size(); ++j, ++o) {

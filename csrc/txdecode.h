@@ -39,6 +39,7 @@ struct DecTx {
     uint8_t version = 0;
     bool canonical = false;
     bool upper_hex = false;  // the input used A-F digits (the stored hex must be re-rendered)
+    bool grouped = false;    // 1 < k < n signatures: input i's signature is its owner key's group (ins[].sig = -1)
     int32_t msg_off = -1, msg_len = 0;  // into canon bytes
     uint8_t tx_type = 0;                // TransactionType from the message; kTypeAsk: Python decides
     int32_t signed_len = 0;             // hex(False) byte length (a prefix of canon)
@@ -55,7 +56,7 @@ struct DecTx {
     void reset() {
         flag = TX_MALFORMED;
         version = 0;
-        canonical = upper_hex = false;
+        canonical = upper_hex = grouped = false;
         msg_off = -1;
         msg_len = 0;
         tx_type = 0;
@@ -297,8 +298,19 @@ static void decode_one(const char* hx, size_t hlen, DecTx& t) {
         for (auto& s : in_sig) s = sig_ptr[0];
     } else if (n_sig == size_t(n_in)) {
         for (size_t k = 0; k < n_sig; ++k) in_sig[k] = sig_ptr[k];
+    } else if (n_sig > 1 && n_sig < size_t(n_in)) {
+        // grouped by the inputs' owner keys in order of first appearance, signature g for group g: the
+        // owners come from the UTXO pass (upow_amd/ledger/fastpath.py resolves the groups). Repeated
+        // signatures would shrink the canonical list: the Python parser takes those
+        for (size_t a = 0; a < n_sig; ++a)
+            for (size_t z = a + 1; z < n_sig; ++z)
+                if (std::memcmp(sig_ptr[a], sig_ptr[z], 64) == 0) {
+                    t.flag = TX_GENERAL;
+                    return;
+                }
+        t.grouped = true;
     } else {
-        t.flag = TX_GENERAL;  // grouped by public key: needs the ledger
+        t.flag = TX_GENERAL;  // more signatures than inputs, or none: the parser's exception / unsigned inputs
         return;
     }
     if (n_in == 0 || n_out == 0) general = true;
@@ -342,7 +354,14 @@ static void decode_one(const char* hx, size_t hlen, DecTx& t) {
     } else {
         c.push_back(0);
     }
-    for (size_t i = 0; i < size_t(n_in); ++i) {
+    if (t.grouped) {  // every signature once, in order (= order of first use once the groups are resolved)
+        for (size_t k = 0; k < n_sig; ++k) {
+            t.sigs.insert(t.sigs.end(), sig_ptr[k], sig_ptr[k] + 64);
+            c.insert(c.end(), sig_ptr[k], sig_ptr[k] + 64);
+        }
+        for (auto& in : t.ins) in.sig = -1;
+    }
+    for (size_t i = 0; i < (t.grouped ? size_t(0) : size_t(n_in)); ++i) {
         int found = -1;
         const size_t ns = t.sigs.size() / 64;
         for (size_t k = 0; k < ns; ++k)

@@ -8,6 +8,7 @@
 #   mine     bench.py (driver default: PoW MH/s + verify side metrics)
 #   verify   bench.py --mode verify --ledger <tmp dir> (file ledger, metric 2)
 #   verifypool bench.py --mode verify --keys pool256 (file ledger, 256-key pool: the cache-friendly variant)
+#   verifygrp bench.py --mode verify --grouped-txs 10% (grouped-signature txs on the native path)
 #   verifymem bench.py --mode verify (in-memory ledger)
 #   verifygov bench.py --mode verify --governance (file ledger; 12 inodes, 200 validators, 5,000 delegates)
 #   verifygov5 bench.py --mode verify --governance-txs 5% (file ledger; 5 % of every block's txs are governance txs)
@@ -60,6 +61,12 @@ for s in $STEPS; do
       timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger --keys pool256 \
         > "$OUT/verify_pool256.json" 2> "$OUT/verify_pool256.err" || { tail -20 "$OUT/verify_pool256.err"; exit 1; }
       cat "$OUT/verify_pool256.json" ;;
+    verifygrp)
+      # 10 % of every block's txs with grouped signatures (4 inputs of two keys, 2 signatures)
+      rm -rf /tmp/upow_bench_ledger
+      timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger --grouped-txs 10% \
+        > "$OUT/verify_grouped10.json" 2> "$OUT/verify_grouped10.err" || { tail -20 "$OUT/verify_grouped10.err"; exit 1; }
+      cat "$OUT/verify_grouped10.json" ;;
     verifygov5)
       rm -rf /tmp/upow_bench_ledger
       timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger --governance-txs 5% \

@@ -441,3 +441,58 @@ def test_block_trace_file(tmp_path, monkeypatch):
     last = recs[-1]
     assert last['path'] == 'native' and last['txs'] == 1 and last['height'] == 9
     assert {'decode_s', 'ecdsa_s', 'apply_commit_s'} <= set(last['stages_ms'])
+
+
+@pytest.mark.parametrize('backend', ['host', pytest.param('gpu', marks=pytest.mark.gpu)])
+def test_grouped_signature_txs_native_and_rejections(backend, request):
+    """1 < k < n signatures (reference transaction.py:578-590: inputs grouped by owner key in order of first
+    appearance, signature g for group g) on the native path: accepted blocks stay native and match the object
+    path; a swapped signature order is rejected identically; more signatures than owner groups raises the
+    parser's IndexError on both paths."""
+    if backend == 'gpu':
+        request.getfixturevalue('gpu')
+
+    async def go():
+        p, base = await _setup(backend)
+        ts = base + 60 * 10
+        p.use(p.a)
+        fund = []
+        from upow_amd.wallet.builders import create_transaction_to_send_multiple_wallet
+        for k in KEYS[:3]:  # three outputs per key
+            tx = await create_transaction_to_send_multiple_wallet(GENESIS, [address_of(k)] * 3, ['1.5'] * 3)
+            await p.a.add_pending_transaction(tx)
+            fund.append(tx)
+        c = await p.mine(fund, ts=ts)
+        await p.push(c, fund, expect=True)
+        p.use(p.a)
+        outs = {k: await p.a.get_spendable_outputs(address_of(k)) for k in KEYS[:3]}
+        k0, k1, k2 = KEYS[:3]
+
+        def grouped(ins, keys, amount):
+            tx = Transaction(ins, [TransactionOutput(address_of(GENESIS), Decimal(amount))])
+            return tx.sign(keys)
+        a = grouped([outs[k0][0], outs[k1][0], outs[k0][1]], [k0, k1], '4.4')  # groups k0, k1: 2 sigs, 3 inputs
+        b = grouped([outs[k1][1], outs[k2][0], outs[k2][1], outs[k1][2]], [k1, k2], '5.9')  # 2 sigs, 4 inputs
+        plain = grouped([outs[k2][2]], [k2], '1.4')
+        for t in (a, b):
+            raw = bytes.fromhex(t.hex())
+            assert len(raw) == len(bytes.fromhex(t.hex(False))) + 1 + 128  # two signatures on the wire
+        assert fastpath.decode([a.hex(), b.hex()]) is not None
+        # rejected: the two signatures swapped (group 0 gets group 1's signature)
+        h = a.hex()
+        swapped = h[:-256] + h[-128:] + h[-256:-128]
+        c_bad = await p.mine([swapped], ts=ts + 60)
+        ok, err = await p.push(c_bad, [swapped], expect=False)
+        assert fastpath.last_path == 'object'
+        # more signatures than owner groups: the parser's IndexError on both paths
+        three = bytes.fromhex(b.hex()) + bytes.fromhex(b.hex())[-64:]
+        p.use(p.b)
+        c3 = await p.mine([three.hex()], ts=ts + 60)
+        with pytest.raises(IndexError):
+            await Transaction.from_hex(three.hex())
+        with pytest.raises(IndexError):
+            await fastpath.create_block_from_hex(c3, [three.hex()])
+        c2 = await p.mine([a, b, plain], ts=ts + 60)
+        await p.push(c2, [a, b, plain], expect=True)
+        assert fastpath.last_path == 'native'
+    asyncio.run(go())

@@ -54,7 +54,8 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     check(t.msg_off < 0 || size_t(t.msg_off) + size_t(t.msg_len) <= cn);
     check(t.ins.size() <= 255 && t.outs.size() <= 255 && !t.ins.empty() && !t.outs.empty());
     check(t.sigs.size() % 64 == 0 && !t.sigs.empty());
-    for (auto& in : t.ins) check(in.sig >= 0 && size_t(in.sig) < t.sigs.size() / 64);
+    for (auto& in : t.ins) check(t.grouped ? in.sig == -1 : (in.sig >= 0 && size_t(in.sig) < t.sigs.size() / 64));
+    if (t.grouped) check(t.sigs.size() / 64 > 1 && t.sigs.size() / 64 < t.ins.size());
     for (size_t k = 0; k < t.outs.size(); ++k) check(t.outs[k].len == 33 || t.outs[k].len == 64);
     uint8_t d[32];
     host_sha256(t.canon.data(), cn, d);
@@ -66,13 +67,13 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     const std::string ch = to_hex(t.canon.data(), cn);
     decode_one(ch.data(), ch.size(), u);
     const size_t uniq = t.sigs.size() / 64;
-    if (uniq != 1 && uniq != t.ins.size()) {
+    if (!t.grouped && uniq != 1 && uniq != t.ins.size()) {
         // n signatures for n inputs with repeats: the canonical bytes keep each signature once
         // (transaction.py:76-81), and k < n signatures read back as the grouped-by-key form
         check(u.flag == TX_GENERAL);
         return 0;
     }
-    check(u.flag == TX_FAST && u.canonical && u.canon == t.canon);
+    check(u.flag == TX_FAST && u.canonical && u.canon == t.canon && u.grouped == t.grouped);
     check(std::memcmp(u.txid, t.txid, 32) == 0 && u.signed_len == t.signed_len && u.tx_type == t.tx_type);
     check(u.out_addr_json == t.out_addr_json && u.out_amount_json == t.out_amount_json);
     return 0;

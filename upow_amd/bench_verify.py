@@ -61,6 +61,25 @@ def signed_spend_txs(spends, keys, owner33, recip33, amount_out=(1_250_000_000, 
     return [(u + b'\x00' + sigs[64 * j:64 * j + 64]).hex() for j, u in enumerate(unsigned)]
 
 
+def signed_grouped_txs(spends, keys_a, keys_b, owner33, recip33, amount_out=(1_250_000_000, 749_000_000),
+                       threads: int = 16):
+    """Version-3 4-in/2-out txs spending two outputs of key A then two of key B, with TWO signatures: the
+    1 < k < n case whose signature -> input assignment groups the inputs by owner key (reference
+    transaction.py:578-590), as a wallet produces when it spends coins of several keys together."""
+    from .ops.native import lib
+    a0, a1 = _amount_bytes(amount_out[0]) + b'\x00', _amount_bytes(amount_out[1]) + b'\x00'
+    unsigned, digests = [], []
+    for j, ins in enumerate(spends):
+        u = b'\x03\x04' + b''.join(bytes.fromhex(h) + bytes([i, 0]) for h, i in ins) + b'\x02' + recip33[j] + a0 \
+            + owner33[j] + a1
+        unsigned.append(u)
+        digests.append(hashlib.sha256(u).digest())
+    dig = b''.join(digests)
+    sa = lib().p256_sign_batch(b''.join(k.to_bytes(32, 'big') for k in keys_a), dig, threads)
+    sb = lib().p256_sign_batch(b''.join(k.to_bytes(32, 'big') for k in keys_b), dig, threads)
+    return [(u + b'\x00' + sa[64 * j:64 * j + 64] + sb[64 * j:64 * j + 64]).hex() for j, u in enumerate(unsigned)]
+
+
 def _funding_tx(owner_addrs, amount: Decimal, rng):
     from .models.transaction import Transaction, TransactionInput, TransactionOutput
     inp = TransactionInput(rng.randbytes(32).hex(), 0)
@@ -70,7 +89,7 @@ def _funding_tx(owner_addrs, amount: Decimal, rng):
 
 async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None, device=None, base_ts=None,
                  make_blocks: bool = True, ledger_path: str = None, governance: bool = False, gov_txs: float = 0.0,
-                 age_txs: int = 0, aging: dict = None, distinct_keys: bool = False):
+                 age_txs: int = 0, aging: dict = None, distinct_keys: bool = False, grouped_txs: float = 0.0):
     """``gov_txs`` > 0: that fraction of every block's txs are governance txs (70 % delegate votes, 10 %
     validator votes, 20 % delegate revokes of seeded ballots, signed by the voters) on a seeded governance
     state; the chain starts four days back so the seeded ballots are past the 48 h revoke window.
@@ -102,12 +121,14 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
         if aging is not None:
             aging.update(info)
     # funding block written straight into the ledger (trusted setup, not part of the measurement)
-    n_out = n_blocks * txs_per_block * 2
+    # grouped txs (distinct keys only) spend two key slots each: size the funding for the extra slots
+    n_grp = int(round(grouped_txs * txs_per_block)) if (grouped_txs > 0 and distinct_keys) else 0
+    n_out = n_blocks * (txs_per_block + n_grp) * 2
     if distinct_keys:
         # own streams, so the funding set is identical whether or not this rank builds the blocks
         from .utils.codec import bytes_to_string
         t_keys = time.perf_counter()
-        tx_keys, _, tx_owner33 = batch_keys(n_blocks * txs_per_block, random.Random(seed * 7919 + 17))
+        tx_keys, _, tx_owner33 = batch_keys(n_out // 2, random.Random(seed * 7919 + 17))
         owner_addr = [bytes_to_string(a) for a in tx_owner33]
         fund_addrs = [owner_addr[i // 2] for i in range(n_out)]  # tx slot j owns outputs 2j and 2j+1
         if aging is not None:
@@ -140,19 +161,26 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
     j = 0
     gov_next = {'d': 0, 'v': 0}
     if distinct_keys and make_blocks:
-        _, _, recip33 = batch_keys(n_blocks * txs_per_block, random.Random(seed * 7919 + 29))
+        _, _, recip33 = batch_keys(n_out // 2, random.Random(seed * 7919 + 29))
     for b in range(n_blocks if make_blocks else 0):
         txs = []
         if n_gov:
             txs.extend(_governance_txs(seeded, gov_next, n_dv, n_vv, n_rv, rng))
         if distinct_keys:
-            n_plain = txs_per_block - len(txs)
+            n_plain = txs_per_block - len(txs) - n_grp
             slots = range(j, j + n_plain)
             txs.extend(signed_spend_txs([(outpoints[2 * s], outpoints[2 * s + 1]) for s in slots],
                                         [tx_keys[s] for s in slots], [tx_owner33[s] for s in slots],
                                         [recip33[s] for s in slots]))
             j += n_plain
-            if n_gov:
+            if n_grp:  # slot pairs (A, B): A's two outputs then B's, signed by A and B
+                pairs = [(j + 2 * q, j + 2 * q + 1) for q in range(n_grp)]
+                txs.extend(signed_grouped_txs(
+                    [[outpoints[2 * a], outpoints[2 * a + 1], outpoints[2 * b], outpoints[2 * b + 1]] for a, b in pairs],
+                    [tx_keys[a] for a, _ in pairs], [tx_keys[b] for _, b in pairs], [tx_owner33[a] for a, _ in pairs],
+                    [recip33[a] for a, _ in pairs]))
+                j += 2 * n_grp
+            if n_gov or n_grp:
                 rng.shuffle(txs)
             blocks.append(txs)
             continue
@@ -426,7 +454,8 @@ async def _run(args, ctx, device, utxo_backend):
     db, addr, blocks, base_ts = await _setup(n_blocks, args.txs, 1234 + ctx.rank, utxo_backend, device,
                                              ledger_path=_ledger_path(args, ctx), governance=gov, gov_txs=gov_txs,
                                              age_txs=int(getattr(args, 'age_txs', 0) or 0), aging=aging,
-                                             distinct_keys=_distinct(args))
+                                             distinct_keys=_distinct(args),
+                                             grouped_txs=float(getattr(args, 'grouped_txs', 0.0) or 0.0))
     key_setup = aging.pop('distinct_key_setup_s', None)
     if aging:
         db.flush()
@@ -540,6 +569,9 @@ def run_verify_bench(args, ctx):
                     f'voting power and ballots)')
     elif getattr(args, 'governance', False):
         args_cfg = 'governance: 12 inodes, 200 validators, 5000 delegates'
+    elif float(getattr(args, 'grouped_txs', 0.0) or 0.0):
+        args_cfg = (f'grouped-signature txs: {float(args.grouped_txs):.0%} of every block are 4-in txs of two keys '
+                    f'with two signatures (inputs grouped by owner key, reference transaction.py:578-590)')
     else:
         args_cfg = None
     total = ctx.allreduce_sum(total_txs)

@@ -19,9 +19,10 @@ Scope: every tx type. Governance transactions (stake/unstake outputs, inode and 
 votes, revokes) ride the same arrays: each input is looked up in the table its tx type spends from, their
 rules run in batch against the governance index (ledger/govcheck.py), revokes are verified against the
 voter's key, and their outputs and spends are journaled into the governance tables in the same batch.
-Txs whose signatures must be grouped by ledger public keys, and ANY failed check, hand the block to the
-object path (``manager._create_block``), which then reproduces the reference's exact verdict, error
-message or exception. The fast path only ever answers "valid" itself, so it can cost time but not semantics;
+Txs with 1 < k < n signatures take the native path too: their inputs are grouped by the owner keys the UTXO
+pass returns, in order of first appearance, and signature g verifies against group g's key
+(``_resolve_groups``). ANY failed check hands the block to the object path (``manager._create_block``),
+which then reproduces the reference's exact verdict, error message or exception. The fast path only ever answers "valid" itself, so it can cost time but not semantics;
 ``tests/test_fastpath.py`` runs both paths over the same blocks and compares the whole ledger.
 """
 from __future__ import annotations
@@ -111,6 +112,35 @@ def _signer_records_general(pay, out_addr, out_len, job_input, sigs, sig_ids, di
     if not ok.all():
         return None
     return np.ascontiguousarray(np.concatenate([xy[job_input], sigs[sig_ids], digest[job_tx]], axis=1)).tobytes()
+
+
+def _owner_key(addr: np.ndarray, n: int) -> bytes:
+    """The public key an input's owner address stands for, as the parser's grouping sees it
+    (``point_to_string(get_public_key())``): x plus the parity of y. A 33-byte address carries the parity
+    in its prefix (43 odd, anything else even), a 64-byte one in y's low byte."""
+    if n == 33:
+        return bytes(addr[1:33]) + (b'\x01' if addr[0] == 43 else b'\x00')
+    return bytes(addr[:32]) + bytes([addr[32] & 1])
+
+
+def _resolve_groups(grouped, job_input, pay, in_start, sig_start, tx_type):
+    """Signature -> input assignment of txs with 1 < k < n signatures (reference transaction.py:578-590):
+    the inputs grouped by owner key in order of first appearance, signature g for group g. The verify job of
+    signature g is group g's first input (the reference checks each (key, signature) pair once). None when
+    the group count is not the signature count (the parser raises, or leaves inputs unsigned) or the tx
+    type verifies against other keys (revokes are signed by voters): the object path decides those."""
+    job_input = job_input.copy()
+    for t in np.asarray(grouped).tolist():
+        if int(tx_type[t]) != 0:
+            return None
+        first = {}
+        for j in range(int(in_start[t]), int(in_start[t + 1])):
+            first.setdefault(_owner_key(pay['addr'][j], int(pay['len'][j])), j)
+        s0, s1 = int(sig_start[t]), int(sig_start[t + 1])
+        if len(first) != s1 - s0:
+            return None
+        job_input[s0:s1] = list(first.values())  # dicts keep insertion order: group g = g-th new key
+    return job_input
 
 
 def _with_signers(pay: np.ndarray, signers: dict) -> np.ndarray:
@@ -278,6 +308,11 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     # one job per distinct signature, checked with its first input's key (the codec numbers signatures in
     # order of first use, so the first input of each is a column of its own)
     job_input = _i32(d, 'sig_first_in').astype(np.int64)
+    grouped = np.nonzero(np.frombuffer(d['grouped'], dtype=np.uint8))[0] if 'grouped' in d else ()
+    if len(grouped):
+        job_input = _resolve_groups(grouped, job_input, sig_pay, in_start, _i32(d, 'sig_start'), d['_tx_type'])
+        if job_input is None:
+            return None
     sig_ids = np.arange(len(job_input), dtype=np.int64)
     sigs = np.frombuffer(d['sigs'], dtype=np.uint8).reshape(-1, 64)
     digest = np.frombuffer(d['digest'], dtype=np.uint8).reshape(-1, 32)
