@@ -105,14 +105,18 @@ def test_general_and_malformed_flags(L):
     gov = Transaction([TransactionInput(rng.randbytes(32).hex(), 0)],
                       [TransactionOutput(_addr(rng), Decimal(1), OutputType.STAKE)])
     gov.inputs[0].signed = (1, 2)
-    grouped = _tx(rng, n_in=3, one_sig=False)
-    gh = grouped.hex()[:-128]  # 2 signatures for 3 inputs -> assignment by public key
-    cases = {'coinbase': coinbase_like, 'grouped sigs': gh,
+    four = _tx(rng, n_in=3, one_sig=False)
+    gh = four.hex() + four.hex()[-128:]  # 4 signatures for 3 inputs: the parser's IndexError
+    cases = {'coinbase': coinbase_like, 'more sigs than inputs': gh,
              'odd hex': 'abc', 'bad char': 'zz' + _tx(rng).hex()[2:], 'version 4': '04' + _tx(rng).hex()[2:],
              'truncated': _tx(rng).hex()[:100]}
     d = L.decode_block_txs(list(cases.values()), 2)
     assert not d['all_fast']
     assert all(f != 0 for f in d['flags']), dict(zip(cases, d['flags']))
+    # 2 signatures for 3 inputs decode natively, grouped (assignment by owner key in the block path)
+    grouped = _tx(rng, n_in=3, one_sig=False).hex()[:-128]
+    d = L.decode_block_txs([grouped], 1)
+    assert d['all_fast'] and list(d['grouped']) == [1] and list(np.frombuffer(d['sig_first_in'], np.int32)) == [-1, -1]
     # governance outputs decode natively: the output-type column carries them
     d = L.decode_block_txs([gov.hex()], 1)
     assert d['all_fast'] and list(d['out_type']) == [int(OutputType.STAKE)] and list(d['tx_type']) == [0]
