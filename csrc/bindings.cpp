@@ -152,6 +152,21 @@ PYBIND11_MODULE(_native, m) {
                               py::bytes(reinterpret_cast<const char*>(ok.data()), ok.size()));
     }, py::arg("data"), py::arg("gpu") = false);
 
+    m.def("p256_on_curve", [](py::buffer in, bool gpu, int threads) {
+        py::buffer_info bi = in.request();
+        const int64_t nbytes = bi.size * bi.itemsize;
+        if (nbytes % 64) throw std::invalid_argument("input must be n x 64 bytes (x LE | y LE)");
+        const int64_t n = nbytes / 64;
+        std::string ok(static_cast<size_t>(n), '\0');
+        {
+            py::gil_scoped_release rel;
+            auto* o = reinterpret_cast<uint8_t*>(&ok[0]);
+            if (gpu) p256_on_curve_gpu(static_cast<const uint8_t*>(bi.ptr), n, o);
+            else p256_on_curve_host(static_cast<const uint8_t*>(bi.ptr), n, o, threads);
+        }
+        return py::bytes(ok);
+    }, py::arg("data"), py::arg("gpu") = false, py::arg("threads") = 8);
+
     m.def("p256_pubkey", [](py::bytes d_be) -> py::object {
         std::string d = d_be;
         if (d.size() != 32) throw std::invalid_argument("private key must be 32 bytes big-endian");

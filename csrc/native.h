@@ -45,6 +45,9 @@ const void* p256_g_table_host();
 std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n);
 void p256_decompress_host(const uint8_t* in33, int64_t n, uint8_t* out64, uint8_t* ok);
 void p256_decompress_gpu(const uint8_t* in33, int64_t n, uint8_t* out64, uint8_t* ok);
+// on-curve check of 64-byte (version-1) addresses x LE | y LE: ok[i] = 1 iff x, y < p and y^2 = x^3 - 3x + b
+void p256_on_curve_host(const uint8_t* xy64, int64_t n, uint8_t* ok, int threads);
+void p256_on_curve_gpu(const uint8_t* xy64, int64_t n, uint8_t* ok);
 // pin node-side GPU work of this process to one device (csrc/streams.h node_device_enter); -1 = unpinned
 void set_node_device_native(int dev);
 bool p256_pubkey(const uint8_t d_be[32], uint8_t out_le[64]);

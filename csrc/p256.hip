@@ -29,6 +29,7 @@
 
 #include "dev_pool.h"
 #include "native.h"
+#include "thread_pool.h"
 #include "streams.h"
 #include "p256_field.h"
 #include "sha256_common.h"
@@ -534,6 +535,19 @@ __global__ __launch_bounds__(256) void p256_decompress_kernel(const uint8_t* __r
     ok[i] = good ? 1 : 0;
 }
 
+// item: 64-byte full address x LE | y LE (transaction_output.py:25-26, is_point_on_curve per output)
+UPOW_HD uint8_t on_curve_64(const uint8_t* a) {
+    const aff q{fe_from_le(a), fe_from_le(a + 32)};
+    return !fe_geq(q.x, fe_const_p()) && !fe_geq(q.y, fe_const_p()) && aff_on_curve(q) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void p256_on_curve_kernel(const uint8_t* __restrict__ in, int64_t n,
+                                                             uint8_t* __restrict__ ok) {
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    ok[i] = on_curve_64(in + 64 * i);
+}
+
 static void hck(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -663,6 +677,24 @@ void p256_decompress_host(const uint8_t* in, int64_t n, uint8_t* out, uint8_t* o
         fe_to_le(y, out + 64 * i + 32);
         ok[i] = good ? 1 : 0;
     }
+}
+
+void p256_on_curve_host(const uint8_t* in, int64_t n, uint8_t* ok, int threads) {
+    HostPool::get().parallel_for(n, threads, [&](int64_t i) { ok[i] = on_curve_64(in + 64 * i); });
+}
+
+void p256_on_curve_gpu(const uint8_t* in, int64_t n, uint8_t* ok) {
+    if (n == 0) return;
+    node_device_enter();
+    PooledBuf<uint8_t> b_in{64 * size_t(n)}, b_ok{size_t(n)};
+    StagedIO io(65 * size_t(n));
+    io.h2d(b_in.p, in, 64 * size_t(n));
+    const int block = 256;
+    hipLaunchKernelGGL(p256_on_curve_kernel, dim3(int((n + block - 1) / block)), dim3(block), 0, node_stream(), b_in.p, n,
+                       b_ok.p);
+    hck(hipGetLastError(), "p256_on_curve_kernel launch");
+    io.d2h(ok, b_ok.p, size_t(n));
+    io.finish("on-curve");
 }
 
 void set_node_device_native(int dev) { set_node_device(dev); }

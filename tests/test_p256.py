@@ -222,3 +222,46 @@ def test_node_device_pin_from_worker_thread(gpu):
         assert (out['st'] == exp).all()
     finally:
         lib().set_node_device(-1)
+
+
+def test_on_curve_batch_matches_oracle(native):
+    """Native batch on-curve check of 64-byte addresses (csrc/p256.hip p256_on_curve, host pool) against the
+    pure-int oracle: valid points, y flipped to the other root, x or y >= p, off-curve noise."""
+    import random
+    from upow_amd.utils import p256 as o
+    rng = random.Random(17)
+    rows, want = [], []
+    for k in range(300):
+        pt = o.get_public_key(rng.randrange(1, o.N))
+        x, y = pt.x, pt.y
+        kind = k % 5
+        if kind == 1:
+            y = o.P - y
+        elif kind == 2:
+            y = (y + 1) % o.P
+        elif kind == 3:
+            x = x + o.P if x + o.P < 1 << 256 else x
+        elif kind == 4:
+            x, y = rng.randrange(1 << 256), rng.randrange(1 << 256)
+        rows.append(x.to_bytes(32, 'little') + y.to_bytes(32, 'little'))
+        want.append(1 if (x < o.P and y < o.P and o.is_on_curve(x, y)) else 0)
+    got = native.p256_on_curve(b''.join(rows), False, 4)
+    assert list(got) == want and sum(want) > 100
+
+
+@pytest.mark.gpu
+def test_on_curve_batch_gpu_matches_host(gpu):
+    import random
+    from upow_amd.utils import p256 as o
+    rng = random.Random(23)
+    pubs = gpu.p256_pubkey_batch(b''.join(rng.randrange(1, o.N).to_bytes(32, 'big') for _ in range(5000)), 8)
+    rows = []
+    for k in range(5000):
+        x, y = int.from_bytes(pubs[64 * k:64 * k + 32], 'little'), int.from_bytes(pubs[64 * k + 32:64 * k + 64], 'little')
+        if k % 3 == 0:
+            x, y = rng.randrange(1 << 256), rng.randrange(1 << 256)
+        elif k % 2 == 0:
+            y = o.P - y
+        rows.append(x.to_bytes(32, 'little') + y.to_bytes(32, 'little'))
+    buf = b''.join(rows)
+    assert gpu.p256_on_curve(buf, True) == gpu.p256_on_curve(buf, False, 8)

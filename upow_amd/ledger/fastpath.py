@@ -88,7 +88,8 @@ def decode(tx_hexes: List[str]) -> Optional[dict]:
 
 def _signer_records_general(pay, out_addr, out_len, job_input, sigs, sig_ids, digest, job_tx, gpu_min):
     """Verify records when the block has 64-byte (version-1) addresses: 33-byte keys decompressed in one
-    batch, 64-byte ones checked on the curve; None when any key is invalid."""
+    batch, 64-byte ones checked on the curve in one batch (csrc/p256.hip ``p256_on_curve``); None when any
+    key is invalid."""
     all_addr = np.concatenate([pay['addr'], out_addr]) if len(out_addr) else np.ascontiguousarray(pay['addr'])
     all_len = np.concatenate([pay['len'].astype(np.uint8), out_len])
     xy = np.zeros((len(all_addr), 64), dtype=np.uint8)
@@ -103,12 +104,11 @@ def _signer_records_general(pay, out_addr, out_len, job_input, sigs, sig_ids, di
         xy[c33] = np.frombuffer(out, dtype=np.uint8).reshape(-1, 64)[inv]
         ok[c33] = np.frombuffer(okb, dtype=np.uint8).astype(bool)[inv]
     c64 = np.nonzero(all_len == 64)[0]
-    if len(c64):
-        from ..utils.p256 import is_on_curve
-        for k in c64:
-            raw = bytes(all_addr[k])
-            xy[k] = all_addr[k]
-            ok[k] = is_on_curve(int.from_bytes(raw[:32], 'little'), int.from_bytes(raw[32:], 'little'))
+    if len(c64):  # 64-byte keys: one native on-curve batch (transaction_output.py:25-26 per output)
+        full = np.ascontiguousarray(all_addr[c64, :64])
+        xy[c64] = full
+        okb = lib().p256_on_curve(full, len(c64) >= gpu_min, THREADS)
+        ok[c64] = np.frombuffer(okb, dtype=np.uint8).astype(bool)
     if not ok.all():
         return None
     return np.ascontiguousarray(np.concatenate([xy[job_input], sigs[sig_ids], digest[job_tx]], axis=1)).tobytes()
