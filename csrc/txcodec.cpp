@@ -655,9 +655,13 @@ static py::tuple unique_rows(py::buffer buf, int width) {
 // records [x | y | r | s | digest] of the signature jobs are assembled from the signers' points.
 // Returns (1, records) when every key is a curve point, (0, b"") when one is not, and (-1, b"") when an
 // address is not in the 33-byte form (64-byte keys: the caller's general path checks those).
+// `over_idx` / `over_addr` (optional): inputs whose signer is not the spent output's owner (revokes are signed
+// by the voter, ledger/govcheck.py): input over_idx[k] takes the 64-byte address row over_addr[k] (+ its
+// length over_len[k]) instead of its pay row, without the caller copying the whole payload column.
 static py::tuple block_signer_records(py::buffer pay_addr_b, py::buffer pay_len_b, py::buffer out_addr_b,
                                       py::buffer out_len_b, py::buffer job_input_b, py::buffer sigs_b,
-                                      py::buffer sig_ids_b, py::buffer digest_b, py::buffer job_tx_b, int64_t gpu_min) {
+                                      py::buffer sig_ids_b, py::buffer digest_b, py::buffer job_tx_b, int64_t gpu_min,
+                                      py::object over_idx_o, py::object over_addr_o, py::object over_len_o) {
     auto view = [](py::buffer& b, size_t elem, const char* what) {
         py::buffer_info bi = b.request();
         const size_t total = size_t(bi.size) * size_t(bi.itemsize);
@@ -678,8 +682,24 @@ static py::tuple block_signer_records(py::buffer pay_addr_b, py::buffer pay_len_
     const int64_t* job_input = reinterpret_cast<const int64_t*>(job_input_p);
     const int64_t* sig_ids = reinterpret_cast<const int64_t*>(sig_ids_p);
     const int64_t* job_tx = reinterpret_cast<const int64_t*>(job_tx_p);
+    std::vector<const uint8_t*> over(n_in, nullptr);  // per input: its override row, if any
+    std::vector<uint8_t> over_len_of(n_in, 0);
+    if (!over_idx_o.is_none()) {
+        py::buffer oi_b = over_idx_o.cast<py::buffer>(), oa_b = over_addr_o.cast<py::buffer>(),
+                   ol_b = over_len_o.cast<py::buffer>();
+        const auto [oi_p, n_o] = view(oi_b, 8, "over_idx");
+        const auto [oa_p, n_o2] = view(oa_b, 64, "over_addr");
+        const auto [ol_p, n_o3] = view(ol_b, 1, "over_len");
+        if (n_o != n_o2 || n_o != n_o3) throw std::invalid_argument("block_signer_records: override lengths differ");
+        const int64_t* oi = reinterpret_cast<const int64_t*>(oi_p);
+        for (size_t k = 0; k < n_o; ++k) {
+            if (oi[k] < 0 || size_t(oi[k]) >= n_in) throw std::invalid_argument("block_signer_records: override index");
+            over[size_t(oi[k])] = oa_p + 64 * k;
+            over_len_of[size_t(oi[k])] = ol_p[k];
+        }
+    }
     for (size_t i = 0; i < n_in; ++i)
-        if (pay_len[i] != 33) return py::make_tuple(-1, py::bytes());
+        if ((over[i] ? over_len_of[i] : pay_len[i]) != 33) return py::make_tuple(-1, py::bytes());
     for (size_t i = 0; i < n_out; ++i)
         if (out_len[i] != 33) return py::make_tuple(-1, py::bytes());
     for (size_t j = 0; j < n_jobs; ++j)
@@ -698,7 +718,9 @@ static py::tuple block_signer_records(py::buffer pay_addr_b, py::buffer pay_len_
         while (cap < 2 * n) cap <<= 1;
         std::vector<int32_t> slot(cap, -1);
         std::vector<const uint8_t*> first;
-        auto key_of = [&](size_t i) { return i < n_in ? pay_addr + 64 * i : out_addr + 64 * (i - n_in); };
+        auto key_of = [&](size_t i) {
+            return i < n_in ? (over[i] ? over[i] : pay_addr + 64 * i) : out_addr + 64 * (i - n_in);
+        };
         for (size_t i = 0; i < n; ++i) {
             const uint8_t* r = key_of(i);
             uint64_t w[4];
@@ -911,7 +933,8 @@ void register_txcodec(py::module_& m) {
           "(unique rows in first-seen order, inverse int32) of an n x width byte matrix");
     m.def("block_signer_records", &block_signer_records, py::arg("pay_addr"), py::arg("pay_len"), py::arg("out_addr"),
           py::arg("out_len"), py::arg("job_input"), py::arg("sigs"), py::arg("sig_ids"), py::arg("digest"),
-          py::arg("job_tx"), py::arg("gpu_min"));
+          py::arg("job_tx"), py::arg("gpu_min"), py::arg("over_idx") = py::none(), py::arg("over_addr") = py::none(),
+          py::arg("over_len") = py::none());
     m.def("decode_block_txs", &decode_block_txs, py::arg("hexes"), py::arg("threads") = 8,
           "Decode, canonicalise and hash a block's transactions (see csrc/txcodec.cpp)");
     m.def("address_pairs", &address_pairs, py::arg("in_blob"), py::arg("in_off"), py::arg("in_start"),

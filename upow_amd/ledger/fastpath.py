@@ -290,14 +290,13 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     txid = np.frombuffer(d['txid'], dtype=np.uint8).reshape(-1, 32)
     out_len = np.frombuffer(d['out_len'], dtype=np.uint8)
     out_addr = np.frombuffer(d['out_addr'], dtype=np.uint8).reshape(-1, 64)
-    sig_pay = pay
+    signers = None
     if bg.any:
         # governance rules against the pre-block state (ledger/govcheck.py); revokes are signed by voters
         gres = await bg.check(database, in_start, out_amount, out_addr, out_len, in_keys, pay, txid)
         if gres is None:
             return None
-        if gres['signers']:
-            sig_pay = _with_signers(pay, gres['signers'])
+        signers = gres['signers'] or None
     t_gov = perf_counter()
     roctx.pop()
     roctx.push('block:signer_records')
@@ -310,7 +309,7 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     job_input = _i32(d, 'sig_first_in').astype(np.int64)
     grouped = np.nonzero(np.frombuffer(d['grouped'], dtype=np.uint8))[0] if 'grouped' in d else ()
     if len(grouped):
-        job_input = _resolve_groups(grouped, job_input, sig_pay, in_start, _i32(d, 'sig_start'), d['_tx_type'])
+        job_input = _resolve_groups(grouped, job_input, pay, in_start, _i32(d, 'sig_start'), d['_tx_type'])
         if job_input is None:
             return None
     sig_ids = np.arange(len(job_input), dtype=np.int64)
@@ -319,12 +318,21 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     job_tx = in_tx[job_input]
     n_jobs = len(job_input)
     gpu_min = op.GPU_MIN_BATCH if gpu_available() else 1 << 62
+    over = {}
+    if signers:  # the voters' keys replace the owners' for revoke inputs, passed as a short override list
+        raws = list(signers.values())
+        ov_addr = np.zeros((len(raws), 64), np.uint8)
+        for k, r in enumerate(raws):
+            ov_addr[k, :len(r)] = np.frombuffer(r, np.uint8)
+        over = {'over_idx': np.fromiter(signers.keys(), dtype=np.int64, count=len(signers)), 'over_addr': ov_addr,
+                'over_len': np.fromiter(map(len, raws), dtype=np.uint8, count=len(raws))}
     kst, rec_bytes = lib().block_signer_records(
-        np.ascontiguousarray(sig_pay['addr']), sig_pay['len'].astype(np.uint8), out_addr, out_len,
-        job_input.astype(np.int64), sigs, sig_ids.astype(np.int64), digest, job_tx.astype(np.int64), gpu_min)
+        np.ascontiguousarray(pay['addr']), pay['len'].astype(np.uint8), out_addr, out_len,
+        job_input.astype(np.int64), sigs, sig_ids.astype(np.int64), digest, job_tx.astype(np.int64), gpu_min, **over)
     if kst == 0:  # a signer key or an output address is off-curve: the object path decides
         return None
     if kst < 0:
+        sig_pay = _with_signers(pay, signers) if signers else pay
         rec_bytes = _signer_records_general(sig_pay, out_addr, out_len, job_input, sigs, sig_ids, digest, job_tx,
                                             gpu_min)
         if rec_bytes is None:
