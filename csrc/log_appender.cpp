@@ -6,11 +6,17 @@
 // HTTP event loop for the GIL. Here a record costs the caller one mutex-protected append of the finished
 // line; a C++ thread writes the buffered lines, and rotates the files (app.log -> app.log.1 -> ... ->
 // app.log.<backups>) when the next write would pass max_bytes, as RotatingFileHandler does.
+//
+// Bounded: at most `max_pending` bytes wait for the writer (a stalled stderr pipe or disk must not grow the
+// node's memory); past that, lines are dropped and counted, and the writer notes the count in the log once
+// it catches up. An urgent record (ERROR and above) is written before the call returns, so the last lines
+// before an abort are not left in the buffer.
 #include <pybind11/pybind11.h>
 
 #include <fcntl.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -40,23 +46,54 @@ public:
     }
     ~LogAppender() { close(); }
 
-    void write(const char* p, size_t n) {
+    // returns false when the line was dropped (buffer full)
+    bool write(const char* p, size_t n, bool urgent = false) {
         {
             std::lock_guard<std::mutex> g(mu_);
-            if (closed_) return;
+            if (closed_) return false;
+            if (!urgent && pending_.size() + n > max_pending_) {  // urgent records are never dropped
+                ++dropped_;
+                ++dropped_unreported_;
+                return false;
+            }
             pending_.append(p, n);
             ++records_;
         }
         // no wake-up: the writer thread drains every 20 ms (a flush or close wakes it at once)
+        return true;
+    }
+
+    // an urgent record: appended, then written before returning (the caller released the GIL); a writer
+    // stuck on a stalled pipe costs the caller at most 100 ms, never a hang
+    void write_sync(const std::string& line) {
+        if (write(line.data(), line.size(), true)) flush_for(100);
+    }
+
+    void set_max_pending(int64_t n) {
+        std::lock_guard<std::mutex> g(mu_);
+        max_pending_ = size_t(std::max<int64_t>(4096, n));
+    }
+
+    int64_t dropped() {
+        std::lock_guard<std::mutex> g(mu_);
+        return int64_t(dropped_);
     }
 
     // everything written so far is in the file (tests, shutdown)
-    void flush() {
+    void flush() { flush_for(-1); }
+
+    // flush, waiting at most `ms` milliseconds (< 0: until done); true when everything is written
+    bool flush_for(int64_t ms) {
         std::unique_lock<std::mutex> lk(mu_);
         const uint64_t want = records_;
         ++flush_req_;
         cv_.notify_one();
-        done_cv_.wait(lk, [&] { return written_records_ >= want || closed_; });
+        auto done = [&] { return written_records_ >= want || closed_; };
+        if (ms < 0) {
+            done_cv_.wait(lk, done);
+            return true;
+        }
+        return done_cv_.wait_for(lk, std::chrono::milliseconds(ms), done);
     }
 
     void close() {
@@ -132,7 +169,7 @@ private:
     void run() {
         std::string buf;
         for (;;) {
-            uint64_t taken;
+            uint64_t taken, lost = 0;
             {
                 std::unique_lock<std::mutex> lk(mu_);
                 // batch: wake on data, but give a burst ~20 ms to accumulate unless someone waits on a flush
@@ -140,6 +177,7 @@ private:
                 flush_seen_ = flush_req_;
                 buf.swap(pending_);
                 taken = records_;
+                std::swap(lost, dropped_unreported_);
                 if (buf.empty() && stop_) {
                     written_records_ = taken;
                     done_cv_.notify_all();
@@ -147,6 +185,10 @@ private:
                 }
             }
             if (!buf.empty()) drain(buf);
+            if (lost) {
+                const std::string note = "log appender: " + std::to_string(lost) + " line(s) dropped (buffer full)\n";
+                drain(note);
+            }
             buf.clear();
             {
                 std::lock_guard<std::mutex> g(mu_);
@@ -164,7 +206,8 @@ private:
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
     std::string pending_;
-    uint64_t records_ = 0, written_records_ = 0, flush_req_ = 0, flush_seen_ = 0;
+    size_t max_pending_ = size_t(8) << 20;
+    uint64_t records_ = 0, written_records_ = 0, flush_req_ = 0, flush_seen_ = 0, dropped_ = 0, dropped_unreported_ = 0;
     bool stop_ = false, closed_ = false;
     std::thread thread_;
 };
@@ -180,8 +223,16 @@ void register_log_appender(py::module_& m) {
                  Py_ssize_t n = 0;
                  const char* p = PyUnicode_AsUTF8AndSize(s.ptr(), &n);
                  if (!p) throw py::error_already_set();
-                 a.write(p, size_t(n));
+                 return a.write(p, size_t(n), false);
              })
+        .def("write_sync",
+             [](LogAppender& a, py::str s) {
+                 std::string line = s;
+                 py::gil_scoped_release nogil;
+                 a.write_sync(line);
+             })
+        .def("set_max_pending", &LogAppender::set_max_pending, py::arg("bytes"))
+        .def_property_readonly("dropped", &LogAppender::dropped)
         .def("flush", &LogAppender::flush, py::call_guard<py::gil_scoped_release>())
         .def("close", &LogAppender::close, py::call_guard<py::gil_scoped_release>())
         .def_property_readonly("rotations", &LogAppender::rotations);

@@ -49,3 +49,22 @@ def test_descriptor_appender_shares_the_offset_with_direct_writes(tmp_path):
     app.close()
     os.close(fd)
     assert open(path).read() == 'first\n' + ''.join(f'rec {i}\n' for i in range(100)) + 'last\n'
+
+
+def test_pending_bytes_are_bounded_and_drops_are_reported(tmp_path):
+    """the buffer in front of the writer is bounded; lines past it are dropped, counted, and the
+    count is written to the log once the writer catches up. ERROR lines are written before write_sync returns."""
+    from upow_amd.ops.native import lib
+    path = str(tmp_path / 'b.log')
+    app = lib().LogAppender(path, 1 << 30, 1)
+    app.set_max_pending(4096)
+    line = 'x' * 99 + '\n'
+    ok = [app.write(line) for _ in range(200)]  # 20 KB in one burst: the writer drains every 20 ms
+    assert not all(ok) and app.dropped == ok.count(False)
+    app.write_sync('ERROR line\n')
+    text = open(path).read()
+    assert text.endswith('ERROR line\n') or 'ERROR line\n' in text
+    app.flush()
+    app.close()
+    text = open(path).read()
+    assert f'{app.dropped} line(s) dropped' in text and text.count(line) == ok.count(True)

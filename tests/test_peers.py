@@ -79,3 +79,37 @@ def test_legacy_nodes_json_import_and_merge(tmp_path):
     other.flush()
     b._stat_at = 0
     assert set(b.urls()) == {'http://a', 'http://b', 'http://c', 'http://d'} and b.last_seen('http://b') > 0
+
+
+def test_flush_merges_other_process_additions_and_keeps_prunes(tmp_path, monkeypatch):
+    """two books on one peers.json (two node processes). A flush re-reads the file under the lock
+    and merges before writing, so the other book's additions survive; a peer this book pruned is not
+    resurrected by the merge."""
+    import json
+    from upow_amd.node import peers as pm
+    path = str(tmp_path / 'peers.json')
+    a, b = pm.PeerBook(path), pm.PeerBook(path)
+    a.add('http://a.example:3006')
+    a.flush()
+    b.add('http://b.example:3006')  # b has not looked at the file since a wrote it
+    b.flush()
+    a.add('http://c.example:3006')
+    a.flush()
+    urls = {r['url'] for r in json.load(open(path))['peers']}
+    assert {'http://a.example:3006', 'http://b.example:3006', 'http://c.example:3006'} <= urls, urls
+    # a prunes a long-silent peer that b still lists: the next merge of b's file must not bring it back
+    now = pm._now()
+    with a.lock:
+        a._peers['http://old.example:3006'] = pm.Peer('http://old.example:3006', 1, now - pm.PRUNE_AFTER - 10)
+        a._dirty = True
+    a.flush()
+    b._stat_at = 0.0
+    b.records()  # b picks the old peer up from the file
+    with a.lock:
+        old = a._peers.pop('http://old.example:3006')
+        a._pruned[old.url] = old.last_seen
+        a._dirty = True
+    b._dirty = True
+    b.flush()  # b's table still has it
+    a.flush()
+    assert 'http://old.example:3006' not in {r['url'] for r in json.load(open(path))['peers']}

@@ -32,7 +32,10 @@ from typing import Dict, Iterable, List, Optional
 import httpx
 
 from .. import config
+from ..utils.logger import get_logger
 from ..constants import MAX_BLOCK_SIZE_HEX
+
+logger = get_logger(__name__)
 
 ACTIVE_WINDOW = 7 * 86_400      # recent peers (nodes_manager.py:24)
 PRUNE_AFTER = 90 * 86_400       # silence after which a peer may be dropped (nodes_manager.py:25)
@@ -95,6 +98,10 @@ class PeerBook:
         self._flushed_at = 0.0
         self._stamp = None       # (mtime_ns, size, inode) of the file as this process last saw it
         self._stat_at = 0.0
+        self._pruned: Dict[str, int] = {}  # url -> last_seen when this process pruned it (merges skip it)
+        self._wake = threading.Event()
+        self._flush_mu = threading.Lock()
+        self._flusher: Optional[threading.Thread] = None
         self.load()
 
     # ---- persistence
@@ -140,6 +147,9 @@ class PeerBook:
 
     def _merge(self, records: Iterable[Peer]):
         for r in records:
+            gone = self._pruned.get(r.url)
+            if gone is not None and r.last_seen <= gone:
+                continue  # pruned here; only news of the peer (a later contact) brings it back
             mine = self._peers.get(r.url)
             if mine is None:
                 self._peers[r.url] = Peer(r.url, r.first_seen, r.last_seen)
@@ -160,25 +170,64 @@ class PeerBook:
             self._stamp = stamp
 
     def flush(self, force: bool = True):
+        """Write the table. Under an exclusive lock on ``<path>.lock`` (the reference's FileLock,
+        nodes_manager.py:28-43) the file is re-read and merged first — newest last_seen wins, this process's
+        prunes stay pruned — so peers another process added since our last look are kept."""
+        if not self.path:
+            return
+        with self._flush_mu:  # one flush of this book at a time: a flush returns once its data is on disk
+            self._flush(force)
+
+    def _flush(self, force: bool):
         with self.lock:
-            if not self._dirty or not self.path:
+            if not self._dirty:
                 return
             if not force and time.monotonic() - self._flushed_at < FLUSH_INTERVAL:
                 return
-            os.makedirs(os.path.dirname(os.path.abspath(self.path)), exist_ok=True)
-            tmp = f'{self.path}.{os.getpid()}.tmp'
-            with open(tmp, 'w') as f:
-                json.dump({'peers': [asdict(p) for p in self._peers.values()]}, f)
-                f.flush()
-                os.fsync(f.fileno())
-            os.replace(tmp, self.path)
-            self._stamp = self._file_stamp()
-            self._dirty = False
-            self._flushed_at = time.monotonic()
+        import fcntl
+        os.makedirs(os.path.dirname(os.path.abspath(self.path)), exist_ok=True)
+        with open(self.path + '.lock', 'a') as lk:
+            fcntl.flock(lk.fileno(), fcntl.LOCK_EX)
+            try:
+                disk = self._read()
+                with self.lock:
+                    self._merge(disk)
+                    rows = [asdict(p) for p in self._peers.values()]
+                    self._dirty = False
+                tmp = f'{self.path}.{os.getpid()}.tmp'
+                with open(tmp, 'w') as f:
+                    json.dump({'peers': rows}, f)
+                    f.flush()
+                    os.fsync(f.fileno())
+                os.replace(tmp, self.path)
+                with self.lock:
+                    self._stamp = self._file_stamp()
+                    self._flushed_at = time.monotonic()
+            finally:
+                fcntl.flock(lk.fileno(), fcntl.LOCK_UN)
 
     def _changed(self):
+        """Mark dirty; the write (file lock, re-read, fsync) happens on the book's flusher thread, never on
+        the caller's (the HTTP event loop)."""
         self._dirty = True
-        self.flush(force=False)
+        if not self.path:
+            return
+        if self._flusher is None or not self._flusher.is_alive():
+            self._flusher = threading.Thread(target=self._flush_loop, name='upow-peers-flush', daemon=True)
+            self._flusher.start()
+        self._wake.set()
+
+    def _flush_loop(self):
+        while True:
+            self._wake.wait()
+            self._wake.clear()
+            wait = FLUSH_INTERVAL - (time.monotonic() - self._flushed_at)
+            if wait > 0:
+                time.sleep(wait)
+            try:
+                self.flush(force=True)
+            except Exception as e:  # pragma: no cover - disk trouble: keep serving, retry on the next change
+                logger.error(f'peers flush failed: {e}')
 
     # ---- queries
     def records(self) -> List[Peer]:
@@ -215,6 +264,7 @@ class PeerBook:
             if len(peers) > MAX_PEERS or len(never_heard(peers)) > MAX_NEVER_HEARD:
                 for p in stale(peers, now):
                     del self._peers[p.url]
+                    self._pruned[p.url] = p.last_seen
                 self._dirty = True
             if len(self._peers) > MAX_PEERS:
                 self._changed()

@@ -91,7 +91,10 @@ class NativeFileHandler(logging.Handler):
                     self._sec, self._stamp = sec, time.strftime('%Y-%m-%d %H:%M:%S', time.localtime(sec))
                 line = (f'{self._stamp},{int(record.msecs):03d} - {record.filename} - {record.levelname} - '
                         f'{record.getMessage()}')
-            self.app.write(line + '\n')
+            if record.levelno >= logging.ERROR:  # written before returning: not lost if the process dies next
+                self.app.write_sync(line + '\n')
+            else:
+                self.app.write(line + '\n')
         except Exception:
             self.handleError(record)
 
