@@ -233,6 +233,29 @@ struct QuadHost {
     }
 };
 
+// the eight-lane kernel's pair-split product (OctDev below) on one host thread: both lanes' halves
+UPOW_HD fe mul_pair_host(const fe& a, const fe& b);
+
+struct OctHost {
+    UPOW_HD void sqr4(const fe& a0, const fe& a1, const fe& a2, const fe& a3, fe& r0, fe& r1, fe& r2, fe& r3) const {
+        const fe m0 = mul_pair_host(a0, a0), m1 = mul_pair_host(a1, a1), m2 = mul_pair_host(a2, a2),
+                 m3 = mul_pair_host(a3, a3);
+        r0 = m0;
+        r1 = m1;
+        r2 = m2;
+        r3 = m3;
+    }
+    UPOW_HD void mul4(const fe& a0, const fe& b0, const fe& a1, const fe& b1, const fe& a2, const fe& b2,
+                      const fe& a3, const fe& b3, fe& r0, fe& r1, fe& r2, fe& r3) const {
+        const fe m0 = mul_pair_host(a0, b0), m1 = mul_pair_host(a1, b1), m2 = mul_pair_host(a2, b2),
+                 m3 = mul_pair_host(a3, b3);
+        r0 = m0;
+        r1 = m1;
+        r2 = m2;
+        r3 = m3;
+    }
+};
+
 template <int K>
 __device__ __forceinline__ fe fe_quad_bcast(const fe& a) {  // every lane of the quad gets lane K's value
     fe r;
@@ -266,6 +289,100 @@ struct QuadDev {
                                          const fe& b2, const fe& a3, const fe& b3, fe& r0, fe& r1, fe& r2,
                                          fe& r3) const {
         const fe m = fe_mul(pick(a0, a1, a2, a3), pick(b0, b1, b2, b3));
+        r0 = fe_quad_bcast<0>(m);
+        r1 = fe_quad_bcast<1>(m);
+        r2 = fe_quad_bcast<2>(m);
+        r3 = fe_quad_bcast<3>(m);
+    }
+};
+
+// Eight lanes per signature (two quads, `hi` = the upper one): every product of a step is split over a lane
+// PAIR (k, k + 4). Each lane runs four of the eight schoolbook rows (32 v_mad_u64_u32 instead of 64: the
+// quarter-rate 64-bit multiply-adds are half of a step's time), the upper lane's 12-word partial sum
+// crosses to its partner with DPP row_shl:4, the lower lane adds it and reduces, and row_shr:4 hands the
+// reduced product back to the upper lane; quad_perm broadcasts then give all four products to every lane
+// of both quads. 8,300 signatures fill 1,038 waves, one per SIMD of the chip, where the quad kernel left
+// half of the SIMDs idle. `split_rows` / `combine_rows` are the arithmetic; the host test runs them on one
+// thread (both halves) against fe_mul.
+UPOW_HD void split_rows(uint32_t p[12], const fe& a, const fe& b, bool upper) {
+    uint32_t ar[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ar[i] = upper ? a.v[4 + i] : a.v[i];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) p[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        unsigned cy = 0;
+        uint32_t prev = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint64_t t = uint64_t(ar[i]) * b.v[j] + p[i + j];
+            p[i + j] = __builtin_addc(uint32_t(t), prev, cy, &cy);
+            prev = uint32_t(t >> 32);
+        }
+        p[i + 8] = prev + cy;
+    }
+}
+// lo: columns 0..11 of the lower rows; hi: columns 4..15 of the upper rows (hi[w] is column w + 4)
+UPOW_HD fe combine_rows(const uint32_t lo[12], const uint32_t hi[12]) {
+    uint32_t c[16];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) c[w] = lo[w];
+    unsigned cy = 0;
+#pragma unroll
+    for (int w = 4; w < 12; ++w) c[w] = __builtin_addc(lo[w], hi[w - 4], cy, &cy);
+#pragma unroll
+    for (int w = 12; w < 16; ++w) c[w] = __builtin_addc(0u, hi[w - 4], cy, &cy);
+    return fe_reduce(c);
+}
+
+UPOW_HD fe mul_pair_host(const fe& a, const fe& b) {
+    uint32_t lo[12], hi[12];
+    split_rows(lo, a, b, false);
+    split_rows(hi, a, b, true);
+    return combine_rows(lo, hi);
+}
+
+struct OctDev {
+    bool is1, is2, is3, hi;  // lane & 3, and whether the lane is in the octet's upper quad
+    __device__ __forceinline__ fe pick(const fe& a0, const fe& a1, const fe& a2, const fe& a3) const {
+        fe r;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            uint32_t t = a0.v[i];
+            t = is1 ? a1.v[i] : t;
+            t = is2 ? a2.v[i] : t;
+            r.v[i] = is3 ? a3.v[i] : t;
+        }
+        return r;
+    }
+    __device__ __forceinline__ fe mul_pair(const fe& a, const fe& b) const {
+        uint32_t p[12], q[12];
+        split_rows(p, a, b, hi);
+#pragma unroll
+        for (int w = 0; w < 12; ++w) q[w] = uint32_t(__builtin_amdgcn_mov_dpp(int(p[w]), 0x104, 0xF, 0xF, true));  // row_shl:4
+        const fe m = combine_rows(p, q);  // meaningful on the lower quad
+        fe r;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t from_lo = uint32_t(__builtin_amdgcn_mov_dpp(int(m.v[i]), 0x114, 0xF, 0xF, true));  // row_shr:4
+            r.v[i] = hi ? from_lo : m.v[i];
+        }
+        return r;
+    }
+    __device__ __forceinline__ void sqr4(const fe& a0, const fe& a1, const fe& a2, const fe& a3, fe& r0, fe& r1, fe& r2,
+                                         fe& r3) const {
+        const fe a = pick(a0, a1, a2, a3);
+        const fe m = mul_pair(a, a);
+        r0 = fe_quad_bcast<0>(m);
+        r1 = fe_quad_bcast<1>(m);
+        r2 = fe_quad_bcast<2>(m);
+        r3 = fe_quad_bcast<3>(m);
+    }
+    __device__ __forceinline__ void mul4(const fe& a0, const fe& b0, const fe& a1, const fe& b1, const fe& a2,
+                                         const fe& b2, const fe& a3, const fe& b3, fe& r0, fe& r1, fe& r2,
+                                         fe& r3) const {
+        const fe m = mul_pair(pick(a0, a1, a2, a3), pick(b0, b1, b2, b3));
         r0 = fe_quad_bcast<0>(m);
         r1 = fe_quad_bcast<1>(m);
         r2 = fe_quad_bcast<2>(m);
@@ -413,14 +530,16 @@ UPOW_HD uint8_t verify_quad_core(const P& pp, const aff& q, const fe& r, const f
     return 0;
 }
 
-static uint8_t verify_one_host_quad(const VerifyItem& it, const aff* gtab) {
+template <class P>
+static uint8_t verify_one_host_steps(const VerifyItem& it, const aff* gtab) {
     aff q;
     fe r, u1, u2;
     const uint8_t pro = verify_prologue(it, q, r, u1, u2);
     if (pro != 255) return pro;
     xz tab[16];
-    return verify_quad_core(QuadHost{}, q, r, u2, tab, [&](auto K) { return jac_to_xz(mul_g_quarter(u1, gtab, K)); });
+    return verify_quad_core(P{}, q, r, u2, tab, [&](auto K) { return jac_to_xz(mul_g_quarter(u1, gtab, K)); });
 }
+static uint8_t verify_one_host_quad(const VerifyItem& it, const aff* gtab) { return verify_one_host_steps<QuadHost>(it, gtab); }
 
 // ------------------------------------------------------------------------------------------------
 // device kernels
@@ -516,6 +635,35 @@ __global__ __launch_bounds__(256, 1) void p256_verify_quad_kernel(const VerifyIt
     if (role == 0) status[i] = st;
 }
 
+// Eight lanes per signature (OctDev), four waves per workgroup (8 signatures per wave). Exits are
+// octet-uniform. Both quads of an octet hold the same point state; the u1*G quarters are computed by each
+// quad (lane & 3) and broadcast within it.
+__global__ __launch_bounds__(256, 1) void p256_verify_oct_kernel(const VerifyItem* __restrict__ items, int64_t n,
+                                                                  const aff* __restrict__ gtab,
+                                                                  xz* __restrict__ scratch,
+                                                                  uint8_t* __restrict__ status) {
+    const int lane = int(threadIdx.x) & 63;
+    const int64_t i = (int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 8 + (lane >> 3);
+    if (i >= n) return;
+    const int role = lane & 3;
+    const bool upper = (lane & 4) != 0;
+    const OctDev pp{role == 1, role == 2, role == 3, upper};
+    const VerifyItem it = items[i];
+    aff q;
+    fe r, u1, u2;
+    const uint8_t pro = verify_prologue(it, q, r, u1, u2);
+    if (pro != 255) {
+        if (role == 0 && !upper) status[i] = pro;
+        return;
+    }
+    const xz mine = jac_to_xz(mul_g_quarter(u1, gtab, role));  // this lane's quarter of u1*G
+    const uint8_t st = verify_quad_core(pp, q, r, u2, scratch + i * 16, [&](auto K) {
+        constexpr int k = decltype(K)::value;
+        return xz{fe_quad_bcast<k>(mine.x), fe_quad_bcast<k>(mine.y), fe_quad_bcast<k>(mine.zz), fe_quad_bcast<k>(mine.zzz)};
+    });
+    if (role == 0 && !upper) status[i] = st;
+}
+
 // item: 33-byte compressed address [spec | x LE]; out: x LE | y LE (64 B) and ok flag
 __global__ __launch_bounds__(256) void p256_decompress_kernel(const uint8_t* __restrict__ in, int64_t n,
                                                                uint8_t* __restrict__ out, uint8_t* __restrict__ ok) {
@@ -584,15 +732,18 @@ std::vector<uint8_t> p256_verify_host(const uint8_t* items, int64_t n, int threa
     const VerifyItem* it = reinterpret_cast<const VerifyItem*>(items);
     // UPOW_P256_HOST32 (read per call): '1' = the 32-bit-limb single-lane code the one-lane GPU kernels
     // run; 'quad' = the four-lane step schedule of the quad kernel played by one host thread (CPU tests
-    // of both GPU code paths); unset = the 64-bit-limb host verifier.
+    // of both GPU code paths); 'oct' = the same schedule with the eight-lane kernel's pair-split products;
+    // unset = the 64-bit-limb host verifier.
     const char* h32 = std::getenv("UPOW_P256_HOST32");
-    const int mode = !h32 ? 0 : (std::strcmp(h32, "quad") == 0 ? 2 : (h32[0] == '1' ? 1 : 0));
+    const int mode = !h32 ? 0 : (std::strcmp(h32, "quad") == 0 ? 2 : std::strcmp(h32, "oct") == 0 ? 3 : (h32[0] == '1' ? 1 : 0));
     threads = int(std::max<int64_t>(1, std::min<int64_t>(threads, n)));
     auto work = [&](int t) {
         if (mode == 1)
             for (int64_t i = t; i < n; i += threads) st[i] = verify_one_host(it[i], tab);
         else if (mode == 2)
             for (int64_t i = t; i < n; i += threads) st[i] = verify_one_host_quad(it[i], tab);
+        else if (mode == 3)  // the eight-lane kernel's pair-split products
+            for (int64_t i = t; i < n; i += threads) st[i] = verify_one_host_steps<OctHost>(it[i], tab);
         else
             for (int64_t i = t; i < n; i += threads)
                 st[i] = p256_verify_one_host64(reinterpret_cast<const uint8_t*>(&it[i]));
@@ -625,6 +776,16 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
     const char* var = std::getenv("UPOW_P256_VARIANT");
     char v = var && var[0] ? var[0] : 'a';
     if (v == 'a') v = n <= kQuadMaxBatch ? '4' : '1';
+    if (v == '8') {
+        PooledBuf<xz> b_tab(size_t(16) * size_t(n));
+        const int64_t waves = (n + 7) / 8;
+        hipLaunchKernelGGL(p256_verify_oct_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, node_stream(), d_items, n,
+                           d_tab, b_tab.p, d_st);
+        hck(hipGetLastError(), "p256_verify_oct_kernel launch");
+        io.d2h(st.data(), d_st, size_t(n));
+        io.finish("verify status");
+        return st;
+    }
     if (v == '4') {
         PooledBuf<xz> b_tab(size_t(16) * size_t(n));
         const int64_t waves = (n + 15) / 16;

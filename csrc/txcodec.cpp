@@ -920,7 +920,80 @@ static py::list unpack_tx_hexes(py::bytes frame, int threads) {
     return out;
 }
 
+// Signature -> input assignment of grouped txs (1 < k < n signatures, reference transaction.py:578-590),
+// the block path's `_resolve_groups`: each listed tx's inputs grouped by owner key (x and the parity of y:
+// a 33-byte address's prefix 43 = odd, anything else even; a 64-byte address's y byte 0) in order of first
+// appearance; signature g's verify job is group g's first input. Returns the updated job_input column
+// (int64) or None when some tx's group count differs from its signature count or its tx type is not
+// REGULAR (the object path decides those).
+static py::object resolve_groups(py::buffer grouped_b, py::buffer in_start_b, py::buffer sig_start_b, py::buffer tx_type_b,
+                                 py::buffer pay_addr_b, py::buffer pay_len_b, py::buffer job_input_b) {
+    auto view = [](py::buffer& b) { return b.request(); };
+    const py::buffer_info gi = view(grouped_b), isi = view(in_start_b), ssi = view(sig_start_b), tti = view(tx_type_b),
+                          pai = view(pay_addr_b), pli = view(pay_len_b), jii = view(job_input_b);
+    if (gi.itemsize != 8 || isi.itemsize != 4 || ssi.itemsize != 4 || tti.itemsize != 1 || jii.itemsize != 8 ||
+        pli.itemsize != 1)
+        throw std::invalid_argument("resolve_groups: column types");
+    const size_t n_tx = size_t(tti.size), n_in = size_t(pli.size), n_jobs = size_t(jii.size);
+    if (size_t(isi.size) != n_tx + 1 || size_t(ssi.size) != n_tx + 1 || size_t(pai.size * pai.itemsize) != 64 * n_in)
+        throw std::invalid_argument("resolve_groups: column lengths");
+    const int64_t* grouped = static_cast<const int64_t*>(gi.ptr);
+    const int32_t* in_start = static_cast<const int32_t*>(isi.ptr);
+    const int32_t* sig_start = static_cast<const int32_t*>(ssi.ptr);
+    const uint8_t* tx_type = static_cast<const uint8_t*>(tti.ptr);
+    const uint8_t* pay_addr = static_cast<const uint8_t*>(pai.ptr);
+    const uint8_t* pay_len = static_cast<const uint8_t*>(pli.ptr);
+    std::vector<int64_t> jobs(static_cast<const int64_t*>(jii.ptr), static_cast<const int64_t*>(jii.ptr) + n_jobs);
+    bool ok = true;
+    {
+        py::gil_scoped_release nogil;
+        std::vector<std::array<uint8_t, 33>> keys;
+        std::vector<int64_t> first;
+        for (ssize_t g = 0; g < gi.size && ok; ++g) {
+            const int64_t t = grouped[g];
+            if (t < 0 || size_t(t) >= n_tx || tx_type[t] != 0) {
+                ok = false;
+                break;
+            }
+            keys.clear();
+            first.clear();
+            for (int32_t j = in_start[t]; j < in_start[t + 1]; ++j) {
+                if (j < 0 || size_t(j) >= n_in) throw std::invalid_argument("resolve_groups: input index");
+                const uint8_t* a = pay_addr + 64 * size_t(j);
+                std::array<uint8_t, 33> k;
+                if (pay_len[j] == 33) {
+                    std::memcpy(k.data(), a + 1, 32);
+                    k[32] = a[0] == 43 ? 1 : 0;
+                } else {
+                    std::memcpy(k.data(), a, 32);
+                    k[32] = a[32] & 1;
+                }
+                bool seen = false;
+                for (auto& q : keys)
+                    if (q == k) {
+                        seen = true;
+                        break;
+                    }
+                if (!seen) {
+                    keys.push_back(k);
+                    first.push_back(j);
+                }
+            }
+            const int32_t s0 = sig_start[t], s1 = sig_start[t + 1];
+            if (int64_t(first.size()) != int64_t(s1 - s0) || s0 < 0 || size_t(s1) > n_jobs) {
+                ok = false;
+                break;
+            }
+            for (int32_t q = s0; q < s1; ++q) jobs[size_t(q)] = first[size_t(q - s0)];
+        }
+    }
+    if (!ok) return py::none();
+    return py::bytes(reinterpret_cast<const char*>(jobs.data()), jobs.size() * 8);
+}
+
 void register_txcodec(py::module_& m) {
+    m.def("resolve_groups", &resolve_groups, py::arg("grouped"), py::arg("in_start"), py::arg("sig_start"),
+          py::arg("tx_type"), py::arg("pay_addr"), py::arg("pay_len"), py::arg("job_input"));
     m.def("pack_tx_hexes", &pack_tx_hexes, py::arg("hexes"), py::arg("threads") = 8);
     m.def("unpack_tx_hexes", &unpack_tx_hexes, py::arg("frame"), py::arg("threads") = 8);
     m.def("output_index_records", &output_index_records, py::arg("txid"), py::arg("index"), py::arg("tag"),

@@ -496,3 +496,33 @@ def test_grouped_signature_txs_native_and_rejections(backend, request):
         await p.push(c2, [a, b, plain], expect=True)
         assert fastpath.last_path == 'native'
     asyncio.run(go())
+
+
+def test_resolve_groups_native_matches_python():
+    """csrc/txcodec.cpp resolve_groups vs the Python assignment: random owner layouts (33- and 64-byte
+    addresses of the same points, repeated keys), matching and mismatching signature counts, governance types."""
+    from upow_amd.ledger.utxo import PAYLOAD_DTYPE
+    rng = random.Random(4)
+    for _ in range(200):
+        n_tx = rng.randint(1, 6)
+        keys = [rng.randbytes(32) for _ in range(4)]
+        in_start, sig_start, addrs, lens, tx_type = [0], [0], [], [], []
+        for t in range(n_tx):
+            n_in = rng.randint(3, 7)
+            for _ in range(n_in):
+                k, odd = rng.randrange(4), rng.randrange(2)
+                if rng.random() < 0.5:
+                    addrs.append(bytes([43 if odd else rng.choice([42, 44])]) + keys[k] + bytes(31)); lens.append(33)
+                else:
+                    addrs.append(keys[k] + bytes([odd]) + rng.randbytes(31)); lens.append(64)
+            in_start.append(in_start[-1] + n_in)
+            sig_start.append(sig_start[-1] + rng.randint(2, 4))
+            tx_type.append(0 if rng.random() < 0.9 else 6)
+        pay = np.zeros(len(addrs), dtype=PAYLOAD_DTYPE)
+        pay['addr'] = np.frombuffer(b''.join(addrs), np.uint8).reshape(-1, 64)
+        pay['len'] = lens
+        grouped = np.array(sorted(rng.sample(range(n_tx), rng.randint(1, n_tx))), np.int64)
+        job = np.full(sig_start[-1], -1, np.int64)
+        args = (grouped, job, pay, np.array(in_start, np.int32), np.array(sig_start, np.int32), np.array(tx_type, np.uint8))
+        a, b = fastpath._resolve_groups(*args), fastpath._resolve_groups_py(*args)
+        assert (a is None) == (b is None) and (a is None or (a == b).all())

@@ -131,7 +131,7 @@ def _chosen_s_batch():
     return b''.join(recs), np.array(exp, dtype=np.uint8)
 
 
-@pytest.mark.parametrize('mode', ['1', 'quad'])  # one-lane 32-bit GPU code; four-lane step schedule
+@pytest.mark.parametrize('mode', ['1', 'quad', 'oct'])  # one-lane 32-bit code; four-lane steps; pair-split products
 def test_host_gpu_code_paths(native, mode, monkeypatch):
     """The GPU kernels' field/point code run on the host: the one-lane 32-bit path and the quad
     kernel's four-product step schedule in XYZZ coordinates (QuadHost), both with the binary-Euclid
@@ -142,7 +142,7 @@ def test_host_gpu_code_paths(native, mode, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('variant', ['0', '1', '2', '4', 'a'])  # 3 waves/SIMD, 4 waves/SIMD, SoA tables, quad, auto
+@pytest.mark.parametrize('variant', ['0', '1', '2', '4', '8', 'a'])  # 3 / 4 waves/SIMD, SoA tables, quad, oct, auto
 def test_gpu_batch_verify_matches_host(gpu, variant, monkeypatch):
     monkeypatch.setenv('UPOW_P256_VARIANT', variant)
     recs, exp = _batch(700, 5)
@@ -199,7 +199,7 @@ def test_high_x_r_plus_n_host(native):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('variant', ['0', '1', '2', '4'])
+@pytest.mark.parametrize('variant', ['0', '1', '2', '4', '8'])
 def test_high_x_r_plus_n_gpu(gpu, variant, monkeypatch):
     monkeypatch.setenv('UPOW_P256_VARIANT', variant)
     recs, exp = _high_x_batch(40, 32)

@@ -129,6 +129,15 @@ def _resolve_groups(grouped, job_input, pay, in_start, sig_start, tx_type):
     signature g is group g's first input (the reference checks each (key, signature) pair once). None when
     the group count is not the signature count (the parser raises, or leaves inputs unsigned) or the tx
     type verifies against other keys (revokes are signed by voters): the object path decides those."""
+    out = lib().resolve_groups(np.ascontiguousarray(grouped, dtype=np.int64), np.ascontiguousarray(in_start, np.int32),
+                               np.ascontiguousarray(sig_start, np.int32), np.ascontiguousarray(tx_type, np.uint8),
+                               np.ascontiguousarray(pay['addr']), np.ascontiguousarray(pay['len'], dtype=np.uint8),
+                               np.ascontiguousarray(job_input, dtype=np.int64))  # csrc/txcodec.cpp
+    return None if out is None else np.frombuffer(out, dtype=np.int64)
+
+
+def _resolve_groups_py(grouped, job_input, pay, in_start, sig_start, tx_type):
+    """The same assignment in Python (the reference form the native one is tested against)."""
     job_input = job_input.copy()
     for t in np.asarray(grouped).tolist():
         if int(tx_type[t]) != 0:
