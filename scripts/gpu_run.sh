@@ -23,6 +23,8 @@
 #   tprof    rocprofv3 kernel + roctx marker trace of the verify bench, summarised by scripts/block_trace.py
 #   sprof    the same for the sync bench (200-tx blocks)
 #   soak3    three node soaks at 1,200 tx/s (scripts/node_soak.py)
+#   soak3pin the same, node pinned to CPUs 0-11 and miner + clients to 12-15 (inside the cgroup quota)
+#   p256ab   verify latency quad vs oct kernel: wall time, rocprofv3 kernel trace, SQ counters
 #   soakc1   cluster node + DP miner under torchrun, forced single-rank RCCL, 40 tx/s (node_soak.py --cluster 1)
 #   soakc1k  the same at 1,200 tx/s
 #   py:<script.py>  any extra python script under scripts/ (args after a comma: py:x.py,--a,1)
@@ -152,6 +154,27 @@ for s in $STEPS; do
         --threads 8 --fanout1 255 --fanout2 220 --out "$OUT/soak_cluster1_1200.json" > "$OUT/soak_cluster1_1200.log" 2>&1 \
         || { tail -30 "$OUT/soak_cluster1_1200.log"; exit 1; }
       tail -1 "$OUT/soak_cluster1_1200.log" | cut -c1-900 ;;
+    p256ab)
+      # single-block verify latency, quad (4 lanes/signature) vs oct (8 lanes/signature): wall time, kernel
+      # trace, and SQ counters for each kernel (own rocprofv3 pass, no other trace domains)
+      timeout -k 10 300 python -u scripts/p256_latency.py 4:64,8:64 > "$OUT/p256_latency.txt" 2>&1 \
+        || { tail -20 "$OUT/p256_latency.txt"; exit 1; }
+      tail -1 "$OUT/p256_latency.txt"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/p256kt" -o p256 --output-format csv \
+        -- python3 scripts/p256_latency.py 4:64,8:64 > "$OUT/p256kt.log" 2>&1 || { tail -20 "$OUT/p256kt.log"; exit 1; }
+      timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY \
+        SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_SALU -d "$OUT/p256pmc" -o pmc --output-format csv \
+        -- python3 scripts/p256_latency.py 4:64,8:64 > "$OUT/p256pmc.log" 2>&1 || { tail -20 "$OUT/p256pmc.log"; exit 1; }
+      echo p256ab-ok ;;
+    soak3pin)
+      # the same three soaks with the job pinned inside the cgroup's CPU quota: node on CPUs 0-11, miner and
+      # pushing clients on 12-15 (a burst over the quota's width throttles every thread of the node)
+      for i in 1 2 3; do
+        UPOW_CPU_AFFINITY=0-11 timeout -k 10 420 python -u scripts/node_soak.py --rate 1200 --seconds 45 --difficulty 9 \
+          --procs 4 --threads 8 --fanout1 255 --fanout2 220 --client-cpus 12-15 --out "$OUT/soakpin_$i.json" \
+          > "$OUT/soakpin_$i.log" 2>&1 || { tail -30 "$OUT/soakpin_$i.log"; exit 1; }
+        tail -1 "$OUT/soakpin_$i.log" | cut -c1-600
+      done ;;
     soak3)
       # three consecutive node soaks at 1,200 tx/s (node + GPU miner CLI + 4 x 8 pushing clients)
       for i in 1 2 3; do
