@@ -14,6 +14,7 @@
 #   verifygov5 bench.py --mode verify --governance-txs 5% (file ledger; 5 % of every block's txs are governance txs)
 #   verifyaged bench.py --mode verify on a ledger aged to 2.5 M txs / 5 M UTXOs (20 blocks, SQL catch-up timed)
 #   syncaged   bench.py --mode sync: 1,000 blocks replayed into the aged ledger
+#   verifyaged60 / verifyaged8  60 blocks on the aged ledger, 4+4 file split vs 8+8
 #   cluster  forced single-rank RCCL cluster node, one chain (bench.py --mode verify under torchrun)
 #   launch   bench.py --gpus 1 under torchrun (the driver's multi-rank entry form)
 #   sync     bench.py --mode sync (chain-sync replay of a /get_blocks page, decode-ahead pipeline)
@@ -25,6 +26,7 @@
 #   soak3    three node soaks at 1,200 tx/s (scripts/node_soak.py)
 #   soak3pin the same, node pinned to CPUs 0-11 and miner + clients to 12-15 (inside the cgroup quota)
 #   p256ab   verify latency quad vs oct kernel: wall time, rocprofv3 kernel trace, SQ counters
+#   p256n    kernel trace of quad vs oct at 1,024 / 4,096 / 8,192 / 8,300 signatures
 #   soakc1   cluster node + DP miner under torchrun, forced single-rank RCCL, 40 tx/s (node_soak.py --cluster 1)
 #   soakc1k  the same at 1,200 tx/s
 #   py:<script.py>  any extra python script under scripts/ (args after a comma: py:x.py,--a,1)
@@ -81,6 +83,20 @@ for s in $STEPS; do
         --steps 20 --warmup 2 > "$OUT/verify_aged.json" 2> "$OUT/verify_aged.err" \
         || { tail -20 "$OUT/verify_aged.err"; exit 1; }
       cat "$OUT/verify_aged.json" ;;
+    verifyaged8)
+      # the aged ledger with transactions and UTXOs split 8 ways each (UPOW_TX_FILES / UPOW_UTXO_FILES), 60 blocks
+      rm -rf /tmp/upow_bench_ledger
+      UPOW_UTXO_FILES=8 UPOW_TX_FILES=8 timeout -k 10 900 python -u bench.py --mode verify --ledger /tmp/upow_bench_ledger \
+        --age-txs 2500000 --steps 60 --warmup 2 > "$OUT/verify_aged8.json" 2> "$OUT/verify_aged8.err" \
+        || { tail -20 "$OUT/verify_aged8.err"; exit 1; }
+      cat "$OUT/verify_aged8.json" | cut -c1-400 ;;
+    verifyaged60)
+      # the aged ledger, default 4 + 4 split, 60 blocks (the A of verifyaged8)
+      rm -rf /tmp/upow_bench_ledger
+      timeout -k 10 900 python -u bench.py --mode verify --ledger /tmp/upow_bench_ledger \
+        --age-txs 2500000 --steps 60 --warmup 2 > "$OUT/verify_aged60.json" 2> "$OUT/verify_aged60.err" \
+        || { tail -20 "$OUT/verify_aged60.err"; exit 1; }
+      cat "$OUT/verify_aged60.json" | cut -c1-400 ;;
     syncaged)
       # a 1,000-block sync (200 txs each) into the aged ledger, decode-ahead pipeline
       rm -rf /tmp/upow_bench_ledger
@@ -166,6 +182,12 @@ for s in $STEPS; do
         SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_SALU -d "$OUT/p256pmc" -o pmc --output-format csv \
         -- python3 scripts/p256_latency.py 4:64,8:64 > "$OUT/p256pmc.log" 2>&1 || { tail -20 "$OUT/p256pmc.log"; exit 1; }
       echo p256ab-ok ;;
+    p256n)
+      # quad vs oct kernel time against the signature count (waves per SIMD: n/16 vs n/8 waves on 1,024 SIMDs)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/p256n" -o p256n --output-format csv \
+        -- python3 scripts/p256_latency.py 4:64:1024,8:64:1024,4:64:4096,8:64:4096,4:64:8192,8:64:8192,4:64,8:64 \
+        > "$OUT/p256n.log" 2>&1 || { tail -20 "$OUT/p256n.log"; exit 1; }
+      tail -1 "$OUT/p256n.log" ;;
     soak3pin)
       # the same three soaks with the job pinned inside the cgroup's CPU quota: node on CPUs 0-11, miner and
       # pushing clients on 12-15 (a burst over the quota's width throttles every thread of the node)
