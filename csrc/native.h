@@ -87,7 +87,10 @@ int64_t utxo_k12_snapshot(int64_t h, uint32_t tag);
 std::vector<uint8_t> utxo_k12_digest(int64_t id, uint64_t* count_out);
 
 // ---------------------------------------------------------------- base58
-std::string b58encode(const uint8_t* data, size_t n);
+std::string b58encode(const uint8_t* data, size_t n);  // n <= kB58MaxInput
+// allocation-free form: writes at most kB58MaxOutput characters to out, returns how many
+constexpr size_t kB58MaxInput = 64, kB58MaxOutput = 88;  // 64 bytes -> at most 88 digits
+size_t b58encode_to(const uint8_t* data, size_t n, char* out);
 std::vector<uint8_t> b58decode(const std::string& s);
 
 // ---------------------------------------------------------------- device info

@@ -114,11 +114,13 @@ static void b58_33(const uint8_t b[33], std::string& out) {
         out.assign(e.s, e.len);
         return;
     }
-    out = b58encode(b, 33);
-    if (out.size() <= sizeof(e.s)) {
+    char buf[kB58MaxOutput];
+    const size_t len = b58encode_to(b, 33, buf);
+    out.assign(buf, len);  // reuses the workspace string's buffer: no allocation per output
+    if (len <= sizeof(e.s)) {
         std::memcpy(e.key, b, 33);
-        std::memcpy(e.s, out.data(), out.size());
-        e.len = uint8_t(out.size());
+        std::memcpy(e.s, buf, len);
+        e.len = uint8_t(len);
     }
 }
 

@@ -14,7 +14,8 @@
 #   verifygov5 bench.py --mode verify --governance-txs 5% (file ledger; 5 % of every block's txs are governance txs)
 #   verifyaged bench.py --mode verify on a ledger aged to 2.5 M txs / 5 M UTXOs (20 blocks, SQL catch-up timed)
 #   syncaged   bench.py --mode sync: 1,000 blocks replayed into the aged ledger
-#   verifyaged60 / verifyaged8  60 blocks on the aged ledger, 4+4 file split vs 8+8
+#   verifyaged60 60 blocks on the aged ledger (writer lag after every block, final drain)
+#   aged:NAME:K=V,...  the same 60-block aged run with extra environment variables
 #   cluster  forced single-rank RCCL cluster node, one chain (bench.py --mode verify under torchrun)
 #   launch   bench.py --gpus 1 under torchrun (the driver's multi-rank entry form)
 #   sync     bench.py --mode sync (chain-sync replay of a /get_blocks page, decode-ahead pipeline)
@@ -83,13 +84,6 @@ for s in $STEPS; do
         --steps 20 --warmup 2 > "$OUT/verify_aged.json" 2> "$OUT/verify_aged.err" \
         || { tail -20 "$OUT/verify_aged.err"; exit 1; }
       cat "$OUT/verify_aged.json" ;;
-    verifyaged8)
-      # the aged ledger with transactions and UTXOs split 8 ways each (UPOW_TX_FILES / UPOW_UTXO_FILES), 60 blocks
-      rm -rf /tmp/upow_bench_ledger
-      UPOW_UTXO_FILES=8 UPOW_TX_FILES=8 timeout -k 10 900 python -u bench.py --mode verify --ledger /tmp/upow_bench_ledger \
-        --age-txs 2500000 --steps 60 --warmup 2 > "$OUT/verify_aged8.json" 2> "$OUT/verify_aged8.err" \
-        || { tail -20 "$OUT/verify_aged8.err"; exit 1; }
-      cat "$OUT/verify_aged8.json" | cut -c1-400 ;;
     verifyaged60)
       # the aged ledger, default 4 + 4 split, 60 blocks (the A of verifyaged8)
       rm -rf /tmp/upow_bench_ledger
@@ -97,6 +91,14 @@ for s in $STEPS; do
         --age-txs 2500000 --steps 60 --warmup 2 > "$OUT/verify_aged60.json" 2> "$OUT/verify_aged60.err" \
         || { tail -20 "$OUT/verify_aged60.err"; exit 1; }
       cat "$OUT/verify_aged60.json" | cut -c1-400 ;;
+    aged:*)
+      # aged:NAME:K=V,K=V  the 60-block aged-ledger run with extra environment (A/B of writer settings)
+      spec=${s#aged:}; name=${spec%%:*}; envs=${spec#*:}
+      rm -rf /tmp/upow_bench_ledger
+      env ${envs//,/ } timeout -k 10 900 python -u bench.py --mode verify --ledger /tmp/upow_bench_ledger \
+        --age-txs 2500000 --steps 60 --warmup 2 > "$OUT/verify_aged_$name.json" 2> "$OUT/verify_aged_$name.err" \
+        || { tail -20 "$OUT/verify_aged_$name.err"; exit 1; }
+      cut -c1-300 "$OUT/verify_aged_$name.json" ;;
     syncaged)
       # a 1,000-block sync (200 txs each) into the aged ledger, decode-ahead pipeline
       rm -rf /tmp/upow_bench_ledger

@@ -41,7 +41,7 @@ async def _grow(db, n_tx: int = 3):
     return a, b, block_txs
 
 
-@pytest.mark.parametrize('n_utxo,n_tx', [(4, 4), (2, 3), (2, 0)])
+@pytest.mark.parametrize('n_utxo,n_tx', [(4, 4), (5, 5), (2, 3), (2, 0)])
 def test_layouts_apply_read_and_roll_back(tmp_path, monkeypatch, n_utxo, n_tx):
     monkeypatch.setenv('UPOW_UTXO_FILES', str(n_utxo))
     monkeypatch.setenv('UPOW_TX_FILES', str(n_tx))
@@ -94,3 +94,11 @@ def test_layouts_apply_read_and_roll_back(tmp_path, monkeypatch, n_utxo, n_tx):
         c = sqlite3.connect(path)
         assert c.execute("SELECT COUNT(*) FROM sqlite_master WHERE name = 'transactions'").fetchone()[0] == 1
         c.close()
+
+
+def test_layout_beyond_sqlite_attach_limit_is_refused(tmp_path, monkeypatch):
+    # one ATTACH per split file; SQLite allows 10, so 8 + 8 must fail loudly at creation, not on ATTACH
+    monkeypatch.setenv('UPOW_UTXO_FILES', '8')
+    monkeypatch.setenv('UPOW_TX_FILES', '8')
+    with pytest.raises(ValueError, match='at most 10'):
+        asyncio.run(Database.create(path=str(tmp_path / 'ledger.sqlite3'), utxo_backend='host'))

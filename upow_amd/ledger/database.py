@@ -518,8 +518,10 @@ class Database:
         else:
             n_utxo = int(os.environ.get('UPOW_UTXO_FILES', str(UTXO_FILES_DEFAULT)))
             n_tx = int(os.environ.get('UPOW_TX_FILES', str(TX_FILES_DEFAULT)))
-            if not (2 <= n_utxo <= 8 and 0 <= n_tx <= 8):
-                raise ValueError('UPOW_UTXO_FILES must be in 2..8 and UPOW_TX_FILES in 0..8')
+            # every split file is one ATTACH of the Python connection: SQLite allows 10 by default
+            if not (2 <= n_utxo <= 8 and 0 <= n_tx <= 8 and n_utxo + n_tx <= 10):
+                raise ValueError('UPOW_UTXO_FILES must be in 2..8, UPOW_TX_FILES in 0..8, and their sum at most 10 '
+                                 '(SQLite attaches at most 10 files to a connection)')
         c.executemany('INSERT OR REPLACE INTO upow_layout (k, v) VALUES (?, ?)',
                       [('utxo_files', n_utxo), ('tx_files', n_tx)])
         return n_utxo, n_tx
