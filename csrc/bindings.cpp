@@ -78,6 +78,38 @@ PYBIND11_MODULE(_native, m) {
         return py::bytes(reinterpret_cast<const char*>(out.data()), out.size());
     }, py::arg("data"), py::arg("offsets"), py::arg("threads") = 1);
 
+    // SHA-256 of the first nchars[k] characters of hexes[idx[k]] (the ASCII text itself, not the bytes it
+    // encodes): the reference's second verify attempt hashes the signed prefix of the tx hex string
+    // (transaction_input.py:84-120). Zero-copy views of the str objects, hashed on the host pool.
+    m.def("sha256_hex_prefixes", [](py::list hexes, py::array_t<int64_t, py::array::c_style | py::array::forcecast> idx,
+                                   py::array_t<int64_t, py::array::c_style | py::array::forcecast> nchars, int threads) {
+        const int64_t n = int64_t(idx.size());
+        if (int64_t(nchars.size()) != n) throw py::value_error("sha256_hex_prefixes: idx and nchars differ in length");
+        const int64_t* ix = idx.data();
+        const int64_t* nc = nchars.data();
+        std::vector<const char*> src(static_cast<size_t>(n));
+        const int64_t n_hex = int64_t(hexes.size());
+        for (int64_t k = 0; k < n; ++k) {
+            if (ix[k] < 0 || ix[k] >= n_hex) throw py::index_error("sha256_hex_prefixes: tx index out of range");
+            PyObject* o = PyList_GET_ITEM(hexes.ptr(), Py_ssize_t(ix[k]));
+            if (!PyUnicode_Check(o)) throw py::type_error("transaction hex must be str");
+            Py_ssize_t sz = 0;
+            const char* p = PyUnicode_AsUTF8AndSize(o, &sz);
+            if (!p) throw py::error_already_set();
+            if (nc[k] < 0 || nc[k] > int64_t(sz)) throw py::value_error("sha256_hex_prefixes: prefix longer than the hex");
+            src[size_t(k)] = p;
+        }
+        std::string out(size_t(n) * 32, '\0');
+        {
+            py::gil_scoped_release rel;  // the list (and so every str) stays alive for the call
+            HostPool::get().parallel_for(n, threads, [&](int64_t k) {
+                host_sha256(reinterpret_cast<const uint8_t*>(src[size_t(k)]), size_t(nc[k]),
+                            reinterpret_cast<uint8_t*>(&out[size_t(k) * 32]));
+            });
+        }
+        return py::bytes(out);
+    }, py::arg("hexes"), py::arg("idx"), py::arg("nchars"), py::arg("threads") = 1);
+
     m.def("sha256_batch_gpu", [](py::buffer data, py::buffer offsets) {
         const uint8_t* d; const int64_t* o; int64_t n, nb;
         packed_args(data, offsets, d, o, n, nb);

@@ -266,3 +266,21 @@ def test_mutated_txs_rejected_or_agree_with_python_parser(native, seed, n_mut):
         assert bool(blk['all_fast']) == bool(d['all_fast'])
         if blk['all_fast']:
             _check_fast(blk, [b, cand, a])
+
+
+def test_sha256_hex_prefixes_matches_hashlib(L):
+    # the ASCII-hex retry's batch hash: SHA-256 of the first n characters of the selected hex strings
+    import hashlib
+    import random
+    rng = random.Random(7)
+    hexes = [rng.randbytes(rng.randrange(1, 300)).hex() for _ in range(200)]
+    idx = np.array([rng.randrange(len(hexes)) for _ in range(500)], np.int64)
+    nch = np.array([rng.randrange(len(hexes[i]) + 1) for i in idx], np.int64)
+    got = L.sha256_hex_prefixes(hexes, idx, nch, 4)
+    want = b''.join(hashlib.sha256(hexes[i][:c].encode()).digest() for i, c in zip(idx, nch))
+    assert got == want
+    assert L.sha256_hex_prefixes(hexes, np.zeros(0, np.int64), np.zeros(0, np.int64), 4) == b''
+    with pytest.raises(IndexError):
+        L.sha256_hex_prefixes(hexes, np.array([len(hexes)], np.int64), np.array([0], np.int64), 1)
+    with pytest.raises(ValueError):
+        L.sha256_hex_prefixes(hexes, np.array([0], np.int64), np.array([len(hexes[0]) + 1], np.int64), 1)

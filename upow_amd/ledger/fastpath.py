@@ -27,7 +27,6 @@ which then reproduces the reference's exact verdict, error message or exception.
 """
 from __future__ import annotations
 
-import hashlib
 import os
 from decimal import Decimal
 from time import perf_counter
@@ -359,9 +358,12 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     if len(retry):
         signed_len = _i32(d, 'signed_len')
         rr = recs[retry].copy()
-        for m, j in enumerate(retry):
-            k = int(job_tx[j])
-            rr[m, 128:] = np.frombuffer(hashlib.sha256(d['hex'][k][:2 * signed_len[k]].encode()).digest(), np.uint8)
+        txs_retry = job_tx[retry].astype(np.int64)
+        # one native batch (host pool) of SHA-256 over the signed prefix of each failing tx's hex text:
+        # a hostile block full of bad signatures costs one pass, not a Python loop per signature
+        rr[:, 128:] = np.frombuffer(lib().sha256_hex_prefixes(d['hex'], txs_retry,
+                                                              2 * signed_len[txs_retry].astype(np.int64), THREADS),
+                                    np.uint8).reshape(-1, 32)
         st2 = validate._verify(np.ascontiguousarray(rr).tobytes(), None)
         status[retry] = np.where(st2 == op.VALID, op.VALID, status[retry])
     if np.any(status != op.VALID):
