@@ -21,13 +21,12 @@ static const char* kB58 = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstu
 // decoder calls this for every output address on all host-pool threads, and a heap vector per call
 // (freed later by whichever thread reuses the workspace) serialised the pool on malloc arena locks:
 // the 8,300-tx decode ran no faster on 8 threads than on 1.
-size_t b58encode_to(const uint8_t* data, size_t n, char* out) {
+static size_t b58_core(const uint8_t* data, size_t n, uint32_t* limbs, char* out) {
     constexpr uint64_t kBase = 656356768ull;  // 58^5 < 2^32
     size_t zeros = 0;
     while (zeros < n && data[zeros] == 0) ++zeros;
     const size_t m = n - zeros;
-    // ceil(m * 8 / log2(58^5)) limbs, log2(58^5) ~ 29.29
-    uint32_t limbs[kB58MaxInput * 8 / 29 + 2];  // little-endian, base 58^5
+    // limbs: ceil(m * 8 / log2(58^5)) words, log2(58^5) ~ 29.29, little-endian, base 58^5
     size_t len = 0;
     const uint8_t* p = data + zeros;
     const size_t head = m % 4 ? m % 4 : 4;  // the first word takes the leading m mod 4 bytes
@@ -66,10 +65,22 @@ size_t b58encode_to(const uint8_t* data, size_t n, char* out) {
     return o;
 }
 
+size_t b58encode_to(const uint8_t* data, size_t n, char* out) {
+    if (n > kB58MaxInput) throw std::invalid_argument("b58encode_to: input longer than 64 bytes");
+    uint32_t limbs[kB58MaxInput * 8 / 29 + 2];
+    return b58_core(data, n, limbs, out);
+}
+
 std::string b58encode(const uint8_t* data, size_t n) {
-    if (n > kB58MaxInput) throw std::invalid_argument("b58encode: input longer than 64 bytes");
-    char buf[kB58MaxOutput];
-    return std::string(buf, b58encode_to(data, n, buf));
+    if (n <= kB58MaxInput) {
+        char buf[kB58MaxOutput];
+        return std::string(buf, b58encode_to(data, n, buf));
+    }
+    // any length (the Python binding): heap buffers, 138 digits per 100 bytes at most
+    std::vector<uint32_t> limbs(n * 8 / 29 + 2);
+    std::string out(n * 138 / 100 + 2, '\0');
+    out.resize(b58_core(data, n, limbs.data(), &out[0]));
+    return out;
 }
 
 // The inverse conversion 58^5 -> 2^32: five digits at a time are folded into 32-bit limbs with one

@@ -23,6 +23,7 @@
 #   prof     rocprofv3 --kernel-trace --stats over a short bench.py
 #   vprof    rocprofv3 --kernel-trace --stats over the verify bench
 #   tprof    rocprofv3 kernel + roctx marker trace of the verify bench, summarised by scripts/block_trace.py
+#   tprofgov the same with 5 % governance txs per block
 #   sprof    the same for the sync bench (200-tx blocks)
 #   soak3    three node soaks at 1,200 tx/s (scripts/node_soak.py)
 #   soak3pin the same, node pinned to CPUs 0-11 and miner + clients to 12-15 (inside the cgroup quota)
@@ -153,6 +154,13 @@ for s in $STEPS; do
         --output-format csv -- python3 bench.py --mode verify --ledger /tmp/upow_bench_ledger --steps 8 --warmup 2 \
         > "$OUT/tprof.log" 2>&1 || { tail -20 "$OUT/tprof.log"; exit 1; }
       python scripts/block_trace.py "$OUT/tprof" --out "$OUT/block_trace.json" | head -60 ;;
+    tprofgov)
+      # the same timeline with 5 % governance txs per block (stage-by-stage cost of the governance rules)
+      rm -rf /tmp/upow_bench_ledger
+      UPOW_ROCTX=1 timeout -k 10 600 rocprofv3 --kernel-trace --marker-trace --stats -d "$OUT/tprofgov" -o verify \
+        --output-format csv -- python3 bench.py --mode verify --ledger /tmp/upow_bench_ledger --steps 8 --warmup 2 \
+        --governance-txs 5% > "$OUT/tprofgov.log" 2>&1 || { tail -20 "$OUT/tprofgov.log"; exit 1; }
+      python scripts/block_trace.py "$OUT/tprofgov" --out "$OUT/block_trace_gov.json" | head -60 ;;
     sprof)
       # the same timeline for the chain-sync replay (200-tx blocks through the decode-ahead pipeline)
       rm -rf /tmp/upow_bench_ledger

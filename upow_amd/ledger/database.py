@@ -113,8 +113,8 @@ for _t in OUTPUT_TABLES[1:]:
 # * The layout of a ledger is recorded in its main file (``upow_layout``) when it is created. Ledgers from
 #   before the transactions split keep ``transactions`` in the main file (one "file", no view) and two
 #   UTXO files.
-UTXO_FILES_DEFAULT = 4
-TX_FILES_DEFAULT = 4
+UTXO_FILES_DEFAULT = 5
+TX_FILES_DEFAULT = 5
 ROUTED = ('unspent_outputs', 'transactions')
 
 
@@ -583,13 +583,18 @@ class Database:
         journal = os.environ.get('UPOW_JOURNAL_PATH') or os.path.join(os.path.dirname(os.path.abspath(self.file)),
                                                                        os.path.basename(self.file) + '.journal')
         self.writer = lib().LedgerWriter([self.file, *self.utxo_files, *self.tx_files], journal, mode, cache_mb,
-                                         int(os.environ.get('UPOW_WRITER_GROUP', '8')),
+                                         # records per materialiser transaction: a lagging materialiser takes
+                                         # up to this many per commit (an aged 5 M-row ledger: 32 vs 8 halves the
+                                         # commit time, profiles/r4/verify_aged_writer_ab_r4g.json)
+                                         int(os.environ.get('UPOW_WRITER_GROUP', '32')),
                                          int(os.environ.get('UPOW_JOURNAL_MAX_MB', '1024')) << 20,
                                          # undo data of the last N blocks survives journal rotation: a
                                          # rollback over the reference's 500-block fork window never rebuilds
                                          int(os.environ.get('UPOW_UNDO_KEEP', '600')),
-                                         # a block submit waits while a materialiser lags by more than this
-                                         int(os.environ.get('UPOW_WRITER_MAX_QUEUE_MB', '512')) << 20,
+                                         # a block submit waits while a materialiser lags by more than this: ~5
+                                         # blocks of 2 MB, so the SQL files trail the journal by a bounded, short
+                                         # drain (< 100 ms) instead of a backlog that grows through a long sync
+                                         int(os.environ.get('UPOW_WRITER_MAX_QUEUE_MB', '8')) << 20,
                                          float(os.environ.get('UPOW_WRITER_THROTTLE_TIMEOUT', '300')),
                                          int(os.environ.get('UPOW_WRITER_BUSY_MS', '5000')))
         self._eph['writer'] = self.writer if self.path == ':memory:' else None
