@@ -60,7 +60,7 @@ for s in $STEPS; do
       rm -rf /tmp/upow_bench_ledger
       timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger \
         > "$OUT/verify_file.json" 2> "$OUT/verify_file.err" || { tail -20 "$OUT/verify_file.err"; exit 1; }
-      cat "$OUT/verify_file.json" ;;
+      cat "$OUT/verify_file.json" | tee -a "$OUT/verify_runs.jsonl" | cut -c1-300 ;;
     verifypool)
       # the cache-friendly variant: a 256-key pool signs every tx and owns every output
       rm -rf /tmp/upow_bench_ledger
@@ -77,7 +77,7 @@ for s in $STEPS; do
       rm -rf /tmp/upow_bench_ledger
       timeout -k 10 600 python bench.py --mode verify --ledger /tmp/upow_bench_ledger --governance-txs 5% \
         > "$OUT/verify_gov5.json" 2> "$OUT/verify_gov5.err" || { tail -20 "$OUT/verify_gov5.err"; exit 1; }
-      cat "$OUT/verify_gov5.json" ;;
+      cat "$OUT/verify_gov5.json" | tee -a "$OUT/verify_runs.jsonl" | cut -c1-300 ;;
     verifyaged)
       # chain scale: the ledger first aged to 2.5 M tx rows / 5 M UTXO rows, then 2 MB blocks incl. SQL catch-up
       rm -rf /tmp/upow_bench_ledger

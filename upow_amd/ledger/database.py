@@ -591,10 +591,11 @@ class Database:
                                          # undo data of the last N blocks survives journal rotation: a
                                          # rollback over the reference's 500-block fork window never rebuilds
                                          int(os.environ.get('UPOW_UNDO_KEEP', '600')),
-                                         # a block submit waits while a materialiser lags by more than this: ~5
-                                         # blocks of 2 MB, so the SQL files trail the journal by a bounded, short
-                                         # drain (< 100 ms) instead of a backlog that grows through a long sync
-                                         int(os.environ.get('UPOW_WRITER_MAX_QUEUE_MB', '8')) << 20,
+                                         # a block submit waits while a materialiser's backlog exceeds this (a
+                                         # 2 MB block is one ~8 MB record in every materialiser's queue): the SQL
+                                         # files trail the journal by at most ~3 blocks, a short drain instead of a
+                                         # backlog that grows through a long sync (profiles/r4/verify_aged60_*)
+                                         int(os.environ.get('UPOW_WRITER_MAX_QUEUE_MB', '24')) << 20,
                                          float(os.environ.get('UPOW_WRITER_THROTTLE_TIMEOUT', '300')),
                                          int(os.environ.get('UPOW_WRITER_BUSY_MS', '5000')))
         self._eph['writer'] = self.writer if self.path == ':memory:' else None
