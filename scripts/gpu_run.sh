@@ -27,6 +27,7 @@
 #   sprof    the same for the sync bench (200-tx blocks)
 #   soak3    three node soaks at 1,200 tx/s (scripts/node_soak.py)
 #   soak3pin the same, node pinned to CPUs 0-11 and miner + clients to 12-15 (inside the cgroup quota)
+#   soakenv:NAME:K=V,...  one pinned soak with extra environment variables
 #   p256ab   verify latency quad vs oct kernel: wall time, rocprofv3 kernel trace, SQ counters
 #   p256n    kernel trace of quad vs oct at 1,024 / 4,096 / 8,192 / 8,300 signatures
 #   soakc1   cluster node + DP miner under torchrun, forced single-rank RCCL, 40 tx/s (node_soak.py --cluster 1)
@@ -207,6 +208,13 @@ for s in $STEPS; do
           > "$OUT/soakpin_$i.log" 2>&1 || { tail -30 "$OUT/soakpin_$i.log"; exit 1; }
         tail -1 "$OUT/soakpin_$i.log" | cut -c1-600
       done ;;
+    soakenv:*)
+      # soakenv:NAME:K=V,K=V  one pinned 1,200 tx/s soak with extra environment (A/B of node settings)
+      spec=${s#soakenv:}; name=${spec%%:*}; envs=${spec#*:}
+      env ${envs//,/ } UPOW_CPU_AFFINITY=0-11 timeout -k 10 420 python -u scripts/node_soak.py --rate 1200 --seconds 45 \
+        --difficulty 9 --procs 4 --threads 8 --fanout1 255 --fanout2 220 --client-cpus 12-15 \
+        --out "$OUT/soakenv_$name.json" > "$OUT/soakenv_$name.log" 2>&1 || { tail -30 "$OUT/soakenv_$name.log"; exit 1; }
+      tail -1 "$OUT/soakenv_$name.log" | cut -c1-400 ;;
     soak3)
       # three consecutive node soaks at 1,200 tx/s (node + GPU miner CLI + 4 x 8 pushing clients)
       for i in 1 2 3; do
