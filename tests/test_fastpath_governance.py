@@ -143,3 +143,42 @@ def test_governance_lifecycle_native_matches_object():
         # inode rewards reach the coinbase identically on both paths after all of this
         assert _dump(p.a)['transactions'] == _dump(p.b)['transactions']
     asyncio.run(go())
+
+
+def test_native_block_prep_matches_numpy():
+    """gov_block_mask / gov_block_inputs (csrc/gov_index.cpp) against the numpy forms of BlockGovernance."""
+    import numpy as np
+    from upow_amd.ledger.govcheck import BlockGovernance, SPEND_TABLE, _seg
+    from upow_amd.ledger.utxo import PAYLOAD_DTYPE, TAG_BY_TABLE
+    from upow_amd.utils.codec import OutputType as O
+    rng = np.random.default_rng(11)
+    for trial in range(20):
+        n = int(rng.integers(1, 300))
+        n_out_per = rng.integers(1, 4, n)
+        n_in_per = rng.integers(1, 4, n)
+        out_start = np.concatenate([[0], np.cumsum(n_out_per)]).astype(np.int32)
+        in_start = np.concatenate([[0], np.cumsum(n_in_per)]).astype(np.int32)
+        n_out, n_in = int(out_start[-1]), int(in_start[-1])
+        tx_type = np.where(rng.random(n) < 0.2, rng.choice([4, 5, 6, 7, 8, 9], n), 0).astype(np.uint8)
+        out_type = np.where(rng.random(n_out) < 0.1, rng.integers(0, 10, n_out), 0).astype(np.uint8)
+        out_tx = np.repeat(np.arange(n, dtype=np.int32), n_out_per)
+        in_tx = np.repeat(np.arange(n, dtype=np.int32), n_in_per)
+        out_amount = rng.integers(0, 1 << 40, n_out).astype(np.uint64)
+        fee = rng.integers(-(1 << 30), 1 << 30, n).astype(np.int64)
+        bg = BlockGovernance(tx_type, out_type, out_tx, out_start, in_tx)
+        has = np.zeros(n, bool)
+        has[np.unique(out_tx[out_type != 0])] = True
+        assert np.array_equal(bg.gov, (tx_type != 0) | has) and bg.any == bool(((tx_type != 0) | has).any())
+        want_tag = bg.spend_tags(TAG_BY_TABLE)
+        tags = want_tag.copy()
+        pay = np.zeros(n_in, PAYLOAD_DTYPE)
+        pay['len'] = 33
+        flip = trial % 3
+        if flip == 1:
+            tags[int(rng.integers(n_in))] ^= 1
+        elif flip == 2:
+            pay['len'][int(rng.integers(n_in))] = 0
+        in_tag, bad, f = bg.inputs(TAG_BY_TABLE, tags, pay, fee, out_amount)
+        assert np.array_equal(in_tag, want_tag)
+        assert bad == bool(((tags != want_tag) | (pay['len'] == 0)).any()) == (flip != 0)
+        assert np.array_equal(f, bg.fee_adjust(fee, out_amount))

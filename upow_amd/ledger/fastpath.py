@@ -280,12 +280,10 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         return None
     in_tag = None
     if bg.any:
-        # each input must be live in the table its tx type spends from (manager.py:531-543)
-        in_tag = bg.spend_tags(TAG_BY_TABLE)
-        bad = (tags != in_tag) | (pay['len'] == 0)
-        if bad.any():
+        # each input must be live in the table its tx type spends from (manager.py:531-543); fees per get_fees
+        in_tag, bad, fee = bg.inputs(TAG_BY_TABLE, tags, pay, fee, out_amount)
+        if bad:
             return None
-        fee = bg.fee_adjust(fee, out_amount)
     elif np.any(missing):
         return None
     in_amount = pay['amount']

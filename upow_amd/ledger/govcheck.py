@@ -56,18 +56,32 @@ class BlockGovernance:
 
     def __init__(self, tx_type: np.ndarray, out_type: np.ndarray, out_tx: np.ndarray, out_start: np.ndarray,
                  in_tx: np.ndarray):
+        from ..ops.native import lib
         self.n = len(tx_type)
-        self.tx_type = tx_type
-        self.out_type = out_type
-        self.out_tx = out_tx
-        self.out_start = out_start
-        self.in_tx = in_tx
-        gov_out = out_type != 0
-        has_gov_out = np.zeros(self.n, dtype=bool)
-        if gov_out.any():
-            has_gov_out[np.unique(out_tx[gov_out])] = True
-        self.gov = (tx_type != 0) | has_gov_out
-        self.any = bool(self.gov.any())
+        self.tx_type = np.ascontiguousarray(tx_type, dtype=np.uint8)
+        self.out_type = np.ascontiguousarray(out_type, dtype=np.uint8)
+        self.out_tx = np.ascontiguousarray(out_tx, dtype=np.int32)
+        self.out_start = np.ascontiguousarray(out_start, dtype=np.int32)
+        self.in_tx = np.ascontiguousarray(in_tx, dtype=np.int32)
+        # one native pass (csrc/gov_index.cpp gov_block_mask): a non-REGULAR tx type or any non-REGULAR output
+        gov, self.any = lib().gov_block_mask(self.tx_type, self.out_type, self.out_tx, self.n, len(self.out_type))
+        self.gov = np.frombuffer(gov, dtype=np.uint8).astype(bool)
+
+    def inputs(self, tag_by_table: dict, tags: np.ndarray, pay: np.ndarray, fee: np.ndarray, out_amount: np.ndarray):
+        """After the UTXO pass, in one native pass (gov_block_inputs): every input's expected tag
+        (:meth:`spend_tags`), whether any input is not live in its table or has no payload, and the fees of
+        :meth:`fee_adjust`. Returns (in_tag u8[n_in], bad, fee i64[n])."""
+        from ..ops.native import lib
+        lut = np.full(256, tag_by_table['unspent_outputs'], dtype=np.uint8)
+        for t, table in SPEND_TABLE.items():
+            lut[t] = tag_by_table[table]
+        tags = np.ascontiguousarray(tags, dtype=np.uint8)
+        in_tag, bad, f = lib().gov_block_inputs(self.tx_type, self.in_tx, tags, np.ascontiguousarray(pay).view(np.uint8), lut,
+                                               self.out_type, self.out_start,
+                                               np.ascontiguousarray(out_amount, dtype=np.uint64),
+                                               np.ascontiguousarray(fee, dtype=np.int64), self.n, len(tags),
+                                               len(self.out_type))
+        return np.frombuffer(in_tag, dtype=np.uint8), bool(bad), np.frombuffer(f, dtype=np.int64)
 
     def spend_tags(self, tag_by_table: dict) -> np.ndarray:
         """Expected UTXO-index tag of every input (the table its tx type spends from)."""
