@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include <cstring>
+#include <malloc.h>
 #include <stdexcept>
 
 #include "native.h"
@@ -59,6 +60,17 @@ PYBIND11_MODULE(_native, m) {
     register_log_appender(m);
     register_http_wire(m);
     register_mempool_index(m);
+
+    // glibc allocator thresholds (mallopt): every 2 MB block's columns are fresh multi-megabyte Python bytes;
+    // above the (dynamic) mmap threshold each one is a new mapping whose pages fault in on first write, and
+    // a trimmed heap top faults in again next block. A fixed threshold/trim size keeps those pages mapped and
+    // reused (utils/cpus.py tune_malloc, called by the node and bench entry points). Returns success.
+    m.def("malloc_tune", [](int64_t mmap_threshold, int64_t trim_threshold) {
+        bool ok = true;
+        if (mmap_threshold > 0) ok &= mallopt(M_MMAP_THRESHOLD, int(std::min<int64_t>(mmap_threshold, INT32_MAX))) == 1;
+        if (trim_threshold > 0) ok &= mallopt(M_TRIM_THRESHOLD, int(std::min<int64_t>(trim_threshold, INT32_MAX))) == 1;
+        return ok;
+    });
 
     m.def("sha256", [](py::bytes msg) {
         std::string s = msg;

@@ -62,6 +62,8 @@ def main(argv=None):
                     help='multi-GPU node under torchrun: rank 0 serves the API, other ranks are HBM replicas')
     a = ap.parse_args(argv)
     pin_cpus(os.environ.get('UPOW_CPU_AFFINITY', 'off'))
+    from ..utils.cpus import tune_malloc
+    tune_malloc()
     if a.data:
         os.environ['UPOW_DATA_DIR'] = a.data
     if a.db:

@@ -23,3 +23,15 @@ def cpu_budget(per_rank: bool = True) -> int:
     if per_rank and local > 1 and (aff is None or len(aff) >= (os.cpu_count() or 1) // 2):
         avail = max(1, avail // local)  # not pinned per rank: split the node's budget
     return avail
+
+
+def tune_malloc() -> bool:
+    """Fixed glibc allocator thresholds for a block-processing process (``UPOW_MALLOC_TUNE=0`` leaves the
+    defaults): 256 MB mmap threshold and 1 GB trim threshold, so the multi-megabyte column buffers every
+    2 MB block allocates are reused heap pages instead of fresh mappings faulted in again on each block
+    (csrc/bindings.cpp ``malloc_tune``). The process keeps its peak heap mapped: tens of MB for a node,
+    nothing next to a GPU host's RAM."""
+    if os.environ.get('UPOW_MALLOC_TUNE', '1') == '0':
+        return False
+    from ..ops.native import lib
+    return bool(lib().malloc_tune(256 << 20, 1 << 30))
