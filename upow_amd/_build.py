@@ -23,7 +23,9 @@ CSRC = ROOT / 'csrc'
 BUILD = ROOT / 'build' / 'native'
 PKG = ROOT / 'upow_amd'
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-CXX = os.environ.get('CXX', 'g++')
+# host-only C++: ROCm's clang++, the compiler hipcc drives for the device files (one toolchain; its code for
+# the codec's base58 and SHA paths is 10-30 % faster than g++ -O3 here)
+CXX = os.environ.get('CXX', '/opt/rocm/llvm/bin/clang++')
 ARCH = os.environ.get('UPOW_OFFLOAD_ARCH', 'gfx950')
 EXT_SUFFIX = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
 TARGET = PKG / f'_native{EXT_SUFFIX}'
@@ -62,7 +64,8 @@ def _build_dir(variant: str) -> Path:
 def _compile(src: Path, hdr_digest: str, force: bool, variant: str = 'release') -> Path:
     out = _build_dir(variant)
     out.mkdir(parents=True, exist_ok=True)
-    key = hashlib.sha256(src.read_bytes() + hdr_digest.encode() + ARCH.encode() + variant.encode()).hexdigest()[:16]
+    key = hashlib.sha256(src.read_bytes() + hdr_digest.encode() + ARCH.encode() + variant.encode()
+                         + (CXX.encode() if src.suffix != '.hip' else b'')).hexdigest()[:16]
     obj = out / f'{src.stem}.{key}.o'
     if obj.exists() and not force:
         return obj
