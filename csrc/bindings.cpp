@@ -100,10 +100,13 @@ PYBIND11_MODULE(_native, m) {
         const int64_t* ix = idx.data();
         const int64_t* nc = nchars.data();
         std::vector<const char*> src(static_cast<size_t>(n));
+        std::vector<py::object> keep;  // the str objects stay alive while the GIL is released, whatever the list does
+        keep.reserve(static_cast<size_t>(n));
         const int64_t n_hex = int64_t(hexes.size());
         for (int64_t k = 0; k < n; ++k) {
             if (ix[k] < 0 || ix[k] >= n_hex) throw py::index_error("sha256_hex_prefixes: tx index out of range");
             PyObject* o = PyList_GET_ITEM(hexes.ptr(), Py_ssize_t(ix[k]));
+            keep.push_back(py::reinterpret_borrow<py::object>(o));
             if (!PyUnicode_Check(o)) throw py::type_error("transaction hex must be str");
             Py_ssize_t sz = 0;
             const char* p = PyUnicode_AsUTF8AndSize(o, &sz);
@@ -113,7 +116,7 @@ PYBIND11_MODULE(_native, m) {
         }
         std::string out(size_t(n) * 32, '\0');
         {
-            py::gil_scoped_release rel;  // the list (and so every str) stays alive for the call
+            py::gil_scoped_release rel;
             HostPool::get().parallel_for(n, threads, [&](int64_t k) {
                 host_sha256(reinterpret_cast<const uint8_t*>(src[size_t(k)]), size_t(nc[k]),
                             reinterpret_cast<uint8_t*>(&out[size_t(k) * 32]));

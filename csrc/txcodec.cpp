@@ -170,12 +170,14 @@ struct MerkleJob {
 static py::dict decode_block_txs(py::list hexes, int threads) {
     const int64_t n = int64_t(hexes.size());
     const size_t N = static_cast<size_t>(n);
-    // zero-copy views of the input hex strings (compact ASCII str objects expose their buffer; the
-    // list keeps them alive for the whole call)
+    // zero-copy views of the input hex strings (compact ASCII str objects expose their buffer)
     std::vector<const char*> srcp(N);
     std::vector<size_t> srcl(N);
+    // a reference per str: the views stay valid while the GIL is released even if another thread edits the list
+    std::vector<py::object> keep(N);
     for (size_t i = 0; i < N; ++i) {
         PyObject* o = PyList_GET_ITEM(hexes.ptr(), Py_ssize_t(i));
+        keep[i] = py::reinterpret_borrow<py::object>(o);
         if (!PyUnicode_Check(o)) throw py::type_error("transaction hex must be str");
         Py_ssize_t sz = 0;
         const char* p = PyUnicode_AsUTF8AndSize(o, &sz);
