@@ -1986,9 +1986,6 @@ class Database:
         # the spends' key order (B-tree locality) is computed by the materialiser ('key': a stable sort of the
         # statement's rows by the leading 8 bytes of column 0, so a row selection keeps the global key order)
         in_order = 'key'
-        # inserts too: the rows carry explicit row ids, so only the index B-trees (tx_hash keys) see the
-        # order, and key order walks their leaves once instead of at random
-        ins_order = 'key' if os.environ.get('UPOW_SORTED_INSERTS', '1') != '0' else None
         stamp()
 
         # ---- statements (schema.sql write set of one block)
@@ -2003,7 +2000,7 @@ class Database:
         ]
         self.checkpoint('block')
         stmts.append((self._TX_INSERT, [tx_cols[0], b['hash'], *tx_cols[1:],
-                                        np.arange(tx_base + 1, tx_base + 1 + n, dtype=np.int64)], n, ins_order, None, None))
+                                        np.arange(tx_base + 1, tx_base + 1 + n, dtype=np.int64)], n, None, None, None))
         self.checkpoint('transactions')
         # explicit row ids from the ledger-wide counter: the rows land in several files (see UTXO_FILES_DEFAULT)
         ins_u = 'INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake, rowid) VALUES (?, ?, ?, ?, ?)'
@@ -2013,7 +2010,7 @@ class Database:
                 stmts.append((ins_u, [('hex32', np.ascontiguousarray(out_txid), 32, 0),
                                       np.ascontiguousarray(out_index, dtype=np.int64), out_addr_spec, 0,
                                       np.arange(base, base + n_out, dtype=np.int64)],
-                              n_out, ins_order, None, None))
+                              n_out, None, None, None))
         else:
             out_txid_c = np.ascontiguousarray(out_txid)
             sel = np.nonzero(out_tag == tag_u)[0]
@@ -2023,7 +2020,7 @@ class Database:
                 stmts.append((ins_u, [('hex32', out_txid_c, 32, 0, sel), np.ascontiguousarray(out_index[sel], dtype=np.int64),
                                       (*out_addr_spec, sel), stake,
                                       np.arange(base, base + len(sel), dtype=np.int64)],
-                              len(sel), ins_order, None, None))
+                              len(sel), None, None, None))
         if coinbase_outputs:
             base = self._utxo_rowids(len(coinbase_outputs))
             stmts.append((ins_u, [[o[0] for o in coinbase_outputs], np.array([o[1] for o in coinbase_outputs], np.int64),
