@@ -61,6 +61,18 @@ last_path = None  # 'native' | 'object' for the last block (tests, metrics)
 AMOUNT_LIMIT = 1 << 52  # > max supply in smallest units; keeps per-tx int64 sums exact
 
 
+_VERIFY_POOL = None
+
+
+def _verify_pool():
+    """One helper thread for the block's signature verify (overlapped with the apply strings)."""
+    global _VERIFY_POOL
+    if _VERIFY_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _VERIFY_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix='upow-block-verify')
+    return _VERIFY_POOL
+
+
 def _i32(d, k):
     return np.frombuffer(d[k], dtype=np.int32)
 
@@ -350,8 +362,40 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     roctx.pop()
     roctx.push('block:ecdsa')
 
-    # ---- signatures: one batched verify (+ the reference's ASCII-hex retry for the failures)
-    status = validate._verify(rec_bytes, None).copy() if n_jobs else np.zeros(0, np.uint8)
+    # ---- signatures: one batched verify (+ the reference's ASCII-hex retry for the failures). The verify
+    #      runs on a helper thread (the native call releases the GIL) while this thread renders the apply
+    #      columns' strings on the host pool below: the kernel's ~1.2 ms and the strings' ~1 ms overlap. A
+    #      verify sharded over a cluster's ranks issues collectives and stays on this, the owner, thread.
+    # fees first (REGULAR txs; voting-power outputs excluded, governance txs carry none): a negative fee hands
+    # the block to the object path before anything is rendered
+    if np.any(fee < 0):
+        return None
+    vfut = _verify_pool().submit(validate._verify, rec_bytes, None) \
+        if n_jobs and validate.overlappable(n_jobs) else None
+    try:
+        # ---- columns for the ledger writes: views of the codec's buffers, encoded natively into one journal
+        #      batch by csrc/ledger_writer.cpp (tx hashes rendered from the raw digests, text arenas for strings)
+        roctx.push('apply:strings')
+        ts0 = perf_counter()
+        L = lib()
+        in_str = L.input_address_strings(np.ascontiguousarray(pay['addr']),
+                                         np.ascontiguousarray(pay['len'], dtype=np.uint8), d['in_start'], THREADS, True)
+        in_json = in_str[:2]
+        # the block's address_transactions rows (each tx's distinct input owners and output addresses)
+        addr_pairs = L.address_pairs(in_str[2], in_str[3], d['in_start'], *d['out_addr_str'], d['out_start'], THREADS)
+        fee_str = ('arena', *L.fee_strings(np.ascontiguousarray(fee, dtype=np.int64).tobytes()))
+        out_index = np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]
+        gov_cols = None
+        if bg.any:
+            gov_cols = {'out_tag': bg.output_tags(TAG_BY_TABLE), 'out_type': out_type, 'in_tag': in_tag,
+                        'gov_tx': bg.gov, 'out_tx': out_tx, 'out_start': out_start, 'in_start': in_start,
+                        'in_str': in_str[2:]}
+        strings_s = perf_counter() - ts0
+        roctx.pop()
+    finally:
+        # the verify's verdict (and, on an exception above, its end: no launch outlives this block)
+        status = (vfut.result() if vfut is not None else
+                  validate._verify(rec_bytes, None) if n_jobs else np.zeros(0, np.uint8)).copy()
     retry = np.nonzero(status == op.INVALID)[0]
     if len(retry):
         signed_len = _i32(d, 'signed_len')
@@ -373,33 +417,12 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     roctx.pop()
     roctx.push('block:apply')
 
-    # ---- fees (REGULAR txs; voting-power outputs excluded, governance txs carry none)
-    if np.any(fee < 0):
-        return None
     fees_total = Decimal(int(fee.sum())) / SMALLEST
     validate.timings.update({'decompress_s': t3 - t_gov, 'collect_s': 0.0, 'ecdsa_s': t4 - t3,
-                             'rules_s': t_gov - t2, 'signatures': n_jobs, 'txs': n})
+                             'rules_s': t_gov - t2, 'strings_s': strings_s, 'signatures': n_jobs, 'txs': n})
     metrics.inc('upow_signatures_verified_total', n_jobs, help='P-256 signatures verified in block validation')
     manager.last_block_timings.update({'utxo_s': t2 - t1, 'verify_s': t4 - t2, 'merkle_s': 0.0,
                                        'total_s': t4 - t0, 'txs': n})
-
-    # ---- columns for the ledger writes: views of the codec's buffers, encoded natively into one journal
-    #      batch by csrc/ledger_writer.cpp (tx hashes rendered from the raw digests, text arenas for strings)
-    roctx.push('apply:strings')
-    L = lib()
-    in_str = L.input_address_strings(np.ascontiguousarray(pay['addr']), np.ascontiguousarray(pay['len'], dtype=np.uint8),
-                                     d['in_start'], THREADS, True)
-    in_json = in_str[:2]
-    # the block's address_transactions rows (each tx's distinct input owners and output addresses)
-    addr_pairs = L.address_pairs(in_str[2], in_str[3], d['in_start'], *d['out_addr_str'], d['out_start'], THREADS)
-    fee_str = ('arena', *L.fee_strings(np.ascontiguousarray(fee, dtype=np.int64).tobytes()))
-    out_index = np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]
-    gov_cols = None
-    if bg.any:
-        gov_cols = {'out_tag': bg.output_tags(TAG_BY_TABLE), 'out_type': out_type, 'in_tag': in_tag,
-                    'gov_tx': bg.gov, 'out_tx': out_tx, 'out_start': out_start, 'in_start': in_start,
-                    'in_str': in_str[2:]}
-    roctx.pop()
 
     async def apply(block_hash, address, random, block_reward, content_time, coinbase_transaction):
         ta = perf_counter()

@@ -46,6 +46,11 @@ def set_dist_context(ctx) -> None:
     _dist_ctx = ctx if (ctx is not None and ctx.is_distributed) else None
 
 
+def overlappable(n_sigs: int) -> bool:
+    """True when :func:`_verify` of ``n_sigs`` signatures issues no collective (any thread may run it)."""
+    return _dist_ctx is None or n_sigs < SHARD_MIN
+
+
 def _verify(recs: bytes, device):
     if _dist_ctx is not None and len(recs) // 160 >= SHARD_MIN:
         from ..parallel.verify_dp import verify_records_dp
