@@ -76,3 +76,44 @@ def test_full_size_distinct_key_block_both_paths(backend, request):
         a.close()
         b.close()
     asyncio.run(go())
+
+
+@pytest.mark.parametrize('backend', ['host', pytest.param('gpu', marks=pytest.mark.gpu)])
+def test_full_size_block_of_bad_signatures_rejected_natively(backend, request):
+    """A hostile 2 MB block: every one of its 8,300 txs carries a signature that verifies under neither message
+    form. The native path decides it (the object path's error: the first bad tx in block order) instead of
+    handing 8,300 txs to the per-tx Python re-validation; the object path agrees, and neither ledger moves."""
+    if backend == 'gpu':
+        request.getfixturevalue('gpu')
+    import time
+    from upow_amd.bench_verify import _setup
+    n = 8300
+    device = 'gpu' if backend == 'gpu' else 'cpu'
+
+    async def go():
+        a, addr, blocks, base_ts = await _setup(1, n, 4343, utxo_backend=backend, device=device, distinct_keys=True)
+        b, _, _, _ = await _setup(1, n, 4343, utxo_backend=backend, device=device, distinct_keys=True,
+                                  make_blocks=False, base_ts=base_ts)
+        # flip one bit of s in each tx's (only) signature: the last 64 bytes on the wire are (r, s)
+        hexes = []
+        for h in blocks[0]:
+            raw = bytearray.fromhex(h)
+            raw[-1] ^= 0x01
+            hexes.append(raw.hex())
+        _use(a)
+        content = await devnet.mine_header(addr, hexes, ts=base_ts + 10, device='cpu')
+        before = a.sql_unspent_outputs_hash()
+        ea = []
+        assert not await manager.create_block(content, [await Transaction.from_hex(h) for h in hexes], error_list=ea)
+        _use(b)
+        eb = []
+        t = time.perf_counter()
+        assert not await fastpath.create_block_from_hex(content, hexes, error_list=eb)
+        native_s = time.perf_counter() - t
+        assert fastpath.last_path == 'native'
+        assert ea == eb and len(eb) == 1 and eb[0].endswith('has been not verified'), (ea, eb)
+        assert a.sql_unspent_outputs_hash() == b.sql_unspent_outputs_hash() == before
+        assert native_s < 30, native_s
+        a.close()
+        b.close()
+    asyncio.run(go())

@@ -178,10 +178,26 @@ def test_rejections_match(backend, request):
         x = _off_curve_x()
         off = bytes_to_string(bytes([42]) + x.to_bytes(32, 'little'))
         offc = await create_transaction(GENESIS, off, '1')
-        for bad in ([good, dup], [forged], [greedy], [ghost], [offc]):
+        for bad in ([good, dup], [greedy], [ghost], [offc]):
             c = await p.mine(bad, ts=ts)
             res, err = await p.push(c, bad, expect=False)
             assert fastpath.last_path == 'object' and err
+        # plainly invalid signatures: decided on the native path with the object path's error (the first bad
+        # tx in block order), whatever else the block holds
+        spend = [o for o in await p.a.get_spendable_outputs(address_of(GENESIS))
+                 if (o.tx_hash, o.index) != (good.inputs[0].tx_hash, good.inputs[0].index)]
+        others = []
+        for k, inp in zip((2, 3, 4), spend):  # each from its own genesis output: no double spend in the block
+            t = Transaction([inp], [TransactionOutput(address_of(KEYS[k]), Decimal('0.5'))])
+            t.sign([GENESIS])
+            others.append(t)
+        forged2, _ = Transaction.parse(others[2].hex())
+        r2, s2 = forged2.inputs[0].signed
+        forged2.inputs[0].signed = (r2 ^ 0x1, s2)
+        for bad in ([forged], [others[0], forged, others[1], forged2], [others[0], forged2, others[1], forged]):
+            c = await p.mine(bad, ts=ts)
+            res, err = await p.push(c, bad, expect=False)
+            assert fastpath.last_path == 'native' and len(err) == 1 and 'has been not verified' in err[0], err
         # merkle mismatch: header committed to other txs
         c = await p.mine([good], ts=ts)
         other = await create_transaction(GENESIS, address_of(KEYS[2]), '1')
@@ -483,7 +499,7 @@ def test_grouped_signature_txs_native_and_rejections(backend, request):
         swapped = h[:-256] + h[-128:] + h[-256:-128]
         c_bad = await p.mine([swapped], ts=ts + 60)
         ok, err = await p.push(c_bad, [swapped], expect=False)
-        assert fastpath.last_path == 'object'
+        assert fastpath.last_path == 'native' and 'has been not verified' in err[0]  # same error on both paths
         # more signatures than owner groups: the parser's IndexError on both paths
         three = bytes.fromhex(b.hex()) + bytes.fromhex(b.hex())[-64:]
         p.use(p.b)

@@ -114,7 +114,7 @@ def test_governance_lifecycle_native_matches_object():
         rv = [await B.create_revoke_transaction(D1, A[V1]), await B.create_revoke_transaction(V2, A[I2])]
         forged, _ = Transaction.parse(rv[0].hex())
         forged.inputs[0].signed = Transaction.parse((await B.create_revoke_transaction(D2, A[V2])).hex())[0].inputs[0].signed
-        await _push(p, [forged], ts + 240, False, 'object')  # signature of another voter
+        await _push(p, [forged], ts + 240, False, 'native')  # signature of another voter: same error, native
         await _push(p, rv, ts + 300, True, 'native')
         # unstake (D1 released its vote) and inode de-registration (I2 lost its votes, registered long ago)
         p.use(p.a)

@@ -409,7 +409,17 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         st2 = validate._verify(np.ascontiguousarray(rr).tobytes(), None)
         status[retry] = np.where(st2 == op.VALID, op.VALID, status[retry])
     if np.any(status != op.VALID):
-        return None
+        bad = np.nonzero(status != op.VALID)[0]
+        if np.all(status[bad] == op.INVALID):
+            # plainly invalid signatures (under both message forms) with every other rule of every tx held:
+            # the object path stops at the first such tx in block order (manager.py create_block →
+            # verify_block_transactions) with this message. Deciding it here spares a hostile block full of
+            # bad signatures the per-tx Python re-validation.
+            k = int(job_tx[bad].min())
+            error_list.append(error := f'transaction {txid[k].tobytes().hex()} has been not verified')
+            logger.error(error)
+            return False
+        return None  # malformed keys or out-of-range scalars: the object path raises what the reference raises
     # the merkle root was computed on the codec's thread while the stages above ran
     if d['merkle_job'].result() != merkle_tree:
         return None
