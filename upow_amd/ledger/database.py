@@ -113,8 +113,8 @@ for _t in OUTPUT_TABLES[1:]:
 # * The layout of a ledger is recorded in its main file (``upow_layout``) when it is created. Ledgers from
 #   before the transactions split keep ``transactions`` in the main file (one "file", no view) and two
 #   UTXO files.
-UTXO_FILES_DEFAULT = 5
-TX_FILES_DEFAULT = 5
+UTXO_FILES_DEFAULT = 4
+TX_FILES_DEFAULT = 4
 ROUTED = ('unspent_outputs', 'transactions')
 
 
