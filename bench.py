@@ -219,7 +219,12 @@ def main(argv=None):
     try:
         if args.mode == 'mine':
             out = bench_mine(args, ctx)
-            if args.verify_steps > 0 and out['config']['device'] == 'gpu':
+            if ctx.world > 1:
+                # the multi-GPU runs report the hashrate scaling curve; the verify side metric is the 1-GPU
+                # config (BASELINE config 4), and a cluster verify here would put RCCL collectives of a second
+                # workload between the headline measurement and its one JSON line
+                out['verify_side_metrics'] = 'single-GPU runs (bench.py --mode verify --gpus N for the cluster)'
+            elif args.verify_steps > 0 and out['config']['device'] == 'gpu':
                 try:
                     out.update(_verify_side_metrics(args, ctx))
                 except Exception as e:  # the headline number stands on its own; say why the extra is missing
