@@ -9,7 +9,8 @@ same checks over whole-block arrays:
   2. one HBM UTXO ``lookup`` launch for every input: existence in ``unspent_outputs`` AND the spent
      output's amount and address (the payload the table carries), so no SQL read is needed;
   3. one batched point decompression for every key involved (signers and outputs), one batched
-     P-256 verify (sharded over ranks on a multi-GPU node) + the ASCII-hex retry pass;
+     P-256 verify (sharded over ranks on a multi-GPU node; otherwise on a helper thread while this thread
+     renders the apply columns' address strings) + the ASCII-hex retry pass;
   4. fees, output validity and the merkle root as array arithmetic;
   5. the ledger writes of ``_apply_block`` as ONE journal batch of column-major bulk statements
      (csrc/ledger_writer.cpp: the journal append is the commit point, a background thread on its own
@@ -22,8 +23,12 @@ voter's key, and their outputs and spends are journaled into the governance tabl
 Txs with 1 < k < n signatures take the native path too: their inputs are grouped by the owner keys the UTXO
 pass returns, in order of first appearance, and signature g verifies against group g's key
 (``_resolve_groups``). ANY failed check hands the block to the object path (``manager._create_block``),
-which then reproduces the reference's exact verdict, error message or exception. The fast path only ever answers "valid" itself, so it can cost time but not semantics;
-``tests/test_fastpath.py`` runs both paths over the same blocks and compares the whole ledger.
+which then reproduces the reference's exact verdict, error message or exception — with one exception: when
+every other rule of every tx held and the only failures are plainly invalid signatures (under both message
+forms), the verdict and message are already known (the object path stops at the first such tx in block
+order with "transaction <hash> has been not verified"), so the block is rejected here, and a hostile block of
+bad signatures costs one batched verify instead of a per-tx Python re-validation.
+``tests/test_fastpath.py`` runs both paths over the same blocks and compares the whole ledger and the errors.
 """
 from __future__ import annotations
 
