@@ -12,6 +12,7 @@ cites its reference line range) so the consensus and node layers read the same.
 """
 from __future__ import annotations
 
+import asyncio
 import json
 import os
 import re
@@ -113,6 +114,7 @@ for _t in OUTPUT_TABLES[1:]:
 # * The layout of a ledger is recorded in its main file (``upow_layout``) when it is created. Ledgers from
 #   before the transactions split keep ``transactions`` in the main file (one "file", no view) and two
 #   UTXO files.
+_SQL_READERS = None  # Database._off_loop
 UTXO_FILES_DEFAULT = 4
 TX_FILES_DEFAULT = 4
 ROUTED = ('unspent_outputs', 'transactions')
@@ -642,16 +644,24 @@ class Database:
         path = self.file
         files = [*zip(self.utxo_schemas, self.utxo_files), *zip(self.tx_schemas, self.tx_files)]
 
+        # one file per period, round-robin: a checkpoint of every attached file at once (11 WALs copied back
+        # and fsync'd in one statement) made readers of those files wait for ~200 ms at a time, among them
+        # the HTTP loop's push_tx lookups (profiles/r4/node_soak_checkpoint_ab_r4w.json)
+        schemas = ['main', *(sch for sch, _ in files)]
+
         def run(stop: threading.Event):
             conn = sqlite3.connect(path, check_same_thread=False, isolation_level=None)
             for schema, f in files:
                 conn.execute(f'ATTACH DATABASE ? AS {schema}', (f,))
+            k = 0
             try:
-                while not stop.wait(period):
+                while not stop.wait(period / len(schemas)):
+                    schema = schemas[k % len(schemas)]
+                    k += 1
                     try:
-                        conn.execute('PRAGMA wal_checkpoint(PASSIVE)').fetchall()
-                    except sqlite3.Error as e:  # busy/locked: try again next period
-                        logger.debug(f'WAL checkpoint skipped: {e}')
+                        conn.execute(f'PRAGMA {schema}.wal_checkpoint(PASSIVE)').fetchall()
+                    except sqlite3.Error as e:  # busy/locked: try again next round
+                        logger.debug(f'WAL checkpoint of {schema} skipped: {e}')
             finally:
                 conn.close()
 
@@ -1686,8 +1696,19 @@ class Database:
             r = self._conn.execute(sql, args).fetchone()
         return r if r is not None else self._q1(sql, args)
 
+    @staticmethod
+    async def _off_loop(fn, *args):
+        """Run a blocking SQL read on the SQL reader threads, not on the calling event loop: a read that
+        waits on the disk (or behind a WAL checkpoint of its file) then stalls no HTTP request."""
+        global _SQL_READERS
+        if _SQL_READERS is None:
+            from concurrent.futures import ThreadPoolExecutor
+            _SQL_READERS = ThreadPoolExecutor(max_workers=2, thread_name_prefix='upow-sql-read')
+        return await asyncio.get_running_loop().run_in_executor(_SQL_READERS, fn, *args)
+
     async def get_transaction(self, tx_hash: str, check_signatures: bool = True):
-        res = self._q1_present('SELECT tx_hex, block_hash FROM transactions WHERE tx_hash = ?', (tx_hash,))
+        res = await self._off_loop(self._q1_present, 'SELECT tx_hex, block_hash FROM transactions WHERE tx_hash = ?',
+                                   (tx_hash,))
         if res is None:
             return None
         tx = await Transaction.from_hex(res['tx_hex'], check_signatures)
@@ -1715,7 +1736,7 @@ class Database:
         hit = self._info_cache.get(tx_hash)
         if hit is not None:
             return hit
-        res = self._q1_present('SELECT * FROM transactions WHERE tx_hash = ?', (tx_hash,))
+        res = await self._off_loop(self._q1_present, 'SELECT * FROM transactions WHERE tx_hash = ?', (tx_hash,))
         if res is None:
             return None
         info = self._info_row(res)
@@ -1735,11 +1756,13 @@ class Database:
                 else:
                     miss.append(h)
             if miss:
-                with self.lock:
-                    for r in self._conn.execute(f'SELECT * FROM transactions WHERE tx_hash IN '
-                                                f'({",".join("?" * len(miss))})', miss):
-                        info = out[r['tx_hash']] = self._info_row(r)
-                        self._cache_info(r['tx_hash'], info)
+                def read(miss=miss):
+                    with self.lock:
+                        return self._conn.execute(f'SELECT * FROM transactions WHERE tx_hash IN '
+                                                  f'({",".join("?" * len(miss))})', miss).fetchall()
+                for r in await self._off_loop(read):
+                    info = out[r['tx_hash']] = self._info_row(r)
+                    self._cache_info(r['tx_hash'], info)
             if len(out) == len(hashes):
                 return out
             hashes = [h for h in hashes if h not in out]
