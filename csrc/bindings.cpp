@@ -18,6 +18,7 @@ namespace upow {
 void register_txcodec(py::module_& m);  // txcodec.cpp
 void register_ledger_writer(py::module_& m);  // ledger_writer.cpp
 void register_gov_index(py::module_& m);  // gov_index.cpp
+void register_stall_probe(py::module_& m);  // stall_probe.cpp
 void register_log_appender(py::module_& m);  // log_appender.cpp
 void register_http_wire(py::module_& m);  // http_wire.cpp
 void register_mempool_index(py::module_& m);  // mempool_index.cpp
@@ -57,6 +58,7 @@ PYBIND11_MODULE(_native, m) {
     register_txcodec(m);
     register_ledger_writer(m);
     register_gov_index(m);
+    register_stall_probe(m);
     register_log_appender(m);
     register_http_wire(m);
     register_mempool_index(m);

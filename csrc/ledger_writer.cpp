@@ -44,6 +44,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 #include <dirent.h>
+#include <pthread.h>
 #include <sys/resource.h>
 #include <sys/stat.h>
 #include <sys/syscall.h>
@@ -1004,6 +1005,7 @@ class LedgerWriter {
     // The journal I/O thread: deferred (block) records in submission order. The undo data is stored before
     // the record is published, so a published block always has its undo record; the fdatasync follows.
     void io_run() {
+        pthread_setname_np(pthread_self(), "upow-wr-io");
         for (;;) {
             IoJob job;
             {
@@ -1560,6 +1562,7 @@ class LedgerWriter {
 
     void run(size_t i) {
         Shard& sh = *shards_[i];
+        pthread_setname_np(pthread_self(), ("upow-wr-" + std::to_string(i)).c_str());
         // materialising is background work: below the block path and the HTTP loop in the CPU share the
         // process gets (GPU boxes run a node under a CPU quota far below the core count)
         if (const char* nv = std::getenv("UPOW_WRITER_NICE")) {

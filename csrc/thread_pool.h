@@ -7,6 +7,8 @@
 // neighbouring outputs, dynamic balance across uneven txs), and the calling thread works too.
 #pragma once
 
+#include <string>
+#include <pthread.h>
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -109,6 +111,7 @@ private:
     }
 
     void loop(int id, uint64_t seen) {
+        pthread_setname_np(pthread_self(), ("upow-pool-" + std::to_string(id)).c_str());
         for (;;) {
             {
                 std::unique_lock<std::mutex> lk(mu_);

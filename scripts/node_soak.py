@@ -379,6 +379,27 @@ def main():
                         continue  # parked threads
                     k2 = f'{name} @ {where}'
                     other_counts[k2] = other_counts.get(k2, 0) + 1
+    # the native probe's samples (csrc/stall_probe.cpp: every thread's kernel state while the loop is late,
+    # taken without the GIL): the loop thread's state / wait channel / syscall, and which threads ran (R)
+    # or waited on the disk (D) meanwhile, by Python thread name where the node recorded one
+    names = {}
+    if os.path.exists(trace + '.threads'):
+        with open(trace + '.threads') as tf:
+            names = json.load(tf)
+    loop_tid = str(names.get('_loop', ''))
+    nat_loop, nat_busy, nat_n = {}, {}, 0
+    if os.path.exists(trace + '.native'):
+        for r in _jsonl(trace + '.native'):
+            if not t0 <= r['t'] <= t_push_end:
+                continue
+            nat_n += 1
+            for tid, comm, state, wchan, sc in r['threads']:
+                if str(tid) == loop_tid:
+                    k = f'{state} {wchan or "-"} sys={sc}'
+                    nat_loop[k] = nat_loop.get(k, 0) + 1
+                elif state in ('R', 'D'):
+                    k = f'{names.get(str(tid), comm)} {state} {wchan or "-"} sys={sc}'
+                    nat_busy[k] = nat_busy.get(k, 0) + 1
     top_stacks = sorted(stack_counts.items(), key=lambda kv: -kv[1])[:12]
     top_others = sorted(other_counts.items(), key=lambda kv: -kv[1])[:12]
     gcs = []
@@ -418,6 +439,9 @@ def main():
                                  'total_ms_during_block_apply': round(sum(s[2] for s in in_blk), 1)},
         'loop_stall_samples_2ms': dict(top_stacks),
         'loop_stall_other_threads': dict(top_others),
+        'loop_stall_native': {'samples': nat_n,
+                              'loop_thread': dict(sorted(nat_loop.items(), key=lambda kv: -kv[1])[:8]),
+                              'running_or_disk': dict(sorted(nat_busy.items(), key=lambda kv: -kv[1])[:16])},
         'gc_over_2ms': {'n': len(gcs), 'total_ms': round(sum(g['ms'] for g in gcs), 1),
                         'max_ms': round(max((g['ms'] for g in gcs), default=0), 1),
                         'gen2': sum(1 for g in gcs if g.get('gen') == 2)},

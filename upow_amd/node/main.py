@@ -134,6 +134,21 @@ async def _loop_lag_monitor(tick: float = 0.001, report_ms: float = 2.0):
                                               'stack': [f'{os.path.basename(x.filename)}:{x.lineno}:{x.name}' for x in st],
                                               'others': others}) + '\n')
     threading.Thread(target=watchdog, name='upow-loop-watchdog', daemon=True).start()
+    # the native probe (csrc/stall_probe.cpp) samples every thread's kernel state while the loop is late,
+    # GIL or no GIL; <trace>.threads maps its tids to Python thread names
+    import numpy as np
+    hb = np.array([_time.perf_counter()])
+    probe = None
+    try:
+        from ..ops.native import lib
+        probe = lib().StallProbe(os.environ['UPOW_TRACE_FILE'] + '.native', hb, threading.get_native_id(), 10.0, 2000)
+    except (ImportError, AttributeError) as e:
+        logger.warning(f'native stall probe unavailable: {e}')
+
+    def dump_thread_names():
+        with open(os.environ['UPOW_TRACE_FILE'] + '.threads', 'w') as tf:
+            json.dump({'_loop': threading.get_native_id(),
+                       **{str(t.native_id): t.name for t in threading.enumerate() if t.native_id}}, tf)
     import gc
     gc_t0 = {}
     gc_out = open(os.environ['UPOW_TRACE_FILE'] + '.gc', 'a')
@@ -150,11 +165,15 @@ async def _loop_lag_monitor(tick: float = 0.001, report_ms: float = 2.0):
     gc.callbacks.append(on_gc)
     try:
         with open(path, 'a') as f:
+            n = 0
             while True:
                 t0 = loop.time()
-                beat[0] = _time.perf_counter()
+                beat[0] = hb[0] = _time.perf_counter()
                 await asyncio.sleep(tick)
-                beat[0] = _time.perf_counter()
+                beat[0] = hb[0] = _time.perf_counter()
+                n += 1
+                if n % 2000 == 1:
+                    dump_thread_names()
                 late = (loop.time() - t0 - tick) * 1000.0
                 if late > report_ms:
                     f.write(json.dumps({'t': round(_time.time(), 4), 'ms': round(late, 2)}) + '\n')
@@ -162,6 +181,8 @@ async def _loop_lag_monitor(tick: float = 0.001, report_ms: float = 2.0):
     finally:
         stop.set()
         gc.callbacks.remove(on_gc)
+        if probe is not None:
+            probe.stop()
         gc_out.close()
 
 
