@@ -7,7 +7,7 @@
 // CLOCK_MONOTONIC) and, while the heartbeat is older than `late_ms`, appends one JSON line per sample:
 // the wall time, how late the loop is, and for the loop thread plus every thread that is running (R) or in
 // uninterruptible sleep (D): tid, comm, state, kernel wait channel and current syscall number
-// (/proc/self/task/<tid>/{stat,wchan,syscall}). The node maps tids to Python thread names (<trace>.threads).
+// (/proc/<pid>/task/<tid>/{stat,wchan,syscall}). The node maps tids to Python thread names (<trace>.threads).
 #include <pybind11/pybind11.h>
 
 #include <dirent.h>
@@ -51,16 +51,24 @@ std::string json_escape(const std::string& s) {
 
 class StallProbe {
 public:
-    StallProbe(std::string path, py::buffer heartbeat, long loop_tid, double late_ms, int period_us)
-        : path_(std::move(path)), loop_tid_(loop_tid), late_s_(late_ms / 1000.0), period_us_(period_us) {
-        py::buffer_info bi = heartbeat.request(true);
-        if (bi.itemsize != 8 || bi.size < 1 || bi.format != py::format_descriptor<double>::format())
-            throw std::invalid_argument("heartbeat must be a writable float64 array of at least one element");
+    // heartbeat None: sample on every period (`pid`: another process, e.g. the node a soak script started --
+    // a process-wide freeze of the node then does not freeze its observer). Samples are kept in memory and
+    // written at stop(): a probe that wrote each one could itself wait in the kernel's dirty-page throttling,
+    // the very kind of stall it is there to see.
+    StallProbe(std::string path, py::object heartbeat, long loop_tid, double late_ms, int period_us, long pid)
+        : path_(std::move(path)), loop_tid_(loop_tid), late_s_(late_ms / 1000.0), period_us_(period_us),
+          task_dir_(pid > 0 ? "/proc/" + std::to_string(pid) + "/task" : std::string("/proc/self/task")) {
+        if (!heartbeat.is_none()) {
+            py::buffer_info bi = heartbeat.cast<py::buffer>().request(true);
+            if (bi.itemsize != 8 || bi.size < 1 || bi.format != py::format_descriptor<double>::format())
+                throw std::invalid_argument("heartbeat must be a writable float64 array of at least one element");
+            hb_owner_ = heartbeat;  // keeps the array alive while the probe reads it
+            hb_ = static_cast<volatile double*>(bi.ptr);
+        }
         if (period_us < 200 || late_ms <= 0) throw std::invalid_argument("period_us >= 200 and late_ms > 0");
-        hb_owner_ = heartbeat;  // keeps the array alive while the probe reads it
-        hb_ = static_cast<volatile double*>(bi.ptr);
         out_ = std::fopen(path_.c_str(), "a");
         if (!out_) throw std::runtime_error("stall probe: cannot open " + path_);
+        buf_.reserve(size_t(1) << 20);
         thread_ = std::thread([this] { run(); });
     }
     ~StallProbe() { stop(); }
@@ -68,7 +76,10 @@ public:
     void stop() {
         if (stop_.exchange(true)) return;
         if (thread_.joinable()) thread_.join();
-        if (out_) std::fclose(out_);
+        if (out_) {
+            std::fwrite(buf_.data(), 1, buf_.size(), out_);
+            std::fclose(out_);
+        }
         out_ = nullptr;
     }
     long samples() const { return samples_.load(); }
@@ -82,8 +93,8 @@ private:
             timespec ts{};
             clock_gettime(CLOCK_MONOTONIC, &ts);
             const double now = double(ts.tv_sec) + double(ts.tv_nsec) * 1e-9;
-            const double late = now - *hb_;
-            if (!(late > late_s_)) continue;
+            const double late = hb_ ? now - *hb_ : 0.0;
+            if (hb_ && !(late > late_s_)) continue;
             sample(late, self);
         }
     }
@@ -93,14 +104,14 @@ private:
         clock_gettime(CLOCK_REALTIME, &wall);
         std::string line = "{\"t\": " + std::to_string(double(wall.tv_sec) + double(wall.tv_nsec) * 1e-9) +
                            ", \"late_ms\": " + std::to_string(late * 1000.0) + ", \"threads\": [";
-        DIR* d = opendir("/proc/self/task");
+        DIR* d = opendir(task_dir_.c_str());
         if (!d) return;
         bool first = true;
         while (dirent* e = readdir(d)) {
             if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
             const long tid = std::atol(e->d_name);
             if (tid == self) continue;
-            const std::string base = std::string("/proc/self/task/") + e->d_name;
+            const std::string base = task_dir_ + "/" + e->d_name;
             const std::string stat = read_small(base + "/stat");
             // "tid (comm) S ...": comm may hold spaces or parentheses, the state follows the last ')'
             const size_t rp = stat.rfind(')');
@@ -119,15 +130,18 @@ private:
         }
         closedir(d);
         line += "]}\n";
-        std::fputs(line.c_str(), out_);
-        std::fflush(out_);
+        if (buf_.size() + line.size() > kMaxBuf) return;  // bounded: the first kMaxBuf bytes of samples
+        buf_ += line;
         ++samples_;
     }
 
+    static constexpr size_t kMaxBuf = size_t(64) << 20;
     std::string path_;
     long loop_tid_;
     double late_s_;
     int period_us_;
+    std::string task_dir_;
+    std::string buf_;
     py::object hb_owner_;
     volatile double* hb_ = nullptr;
     FILE* out_ = nullptr;
@@ -142,8 +156,8 @@ namespace upow {
 
 void register_stall_probe(py::module_& m) {
     py::class_<StallProbe>(m, "StallProbe")
-        .def(py::init<std::string, py::buffer, long, double, int>(), py::arg("path"), py::arg("heartbeat"),
-             py::arg("loop_tid"), py::arg("late_ms") = 10.0, py::arg("period_us") = 2000)
+        .def(py::init<std::string, py::object, long, double, int, long>(), py::arg("path"), py::arg("heartbeat"),
+             py::arg("loop_tid"), py::arg("late_ms") = 10.0, py::arg("period_us") = 2000, py::arg("pid") = 0)
         .def("stop", &StallProbe::stop, py::call_guard<py::gil_scoped_release>())
         .def("samples", &StallProbe::samples);
 }

@@ -153,6 +153,15 @@ def main():
                 break
         except Exception:
             time.sleep(0.2)
+    # an observer outside the node (csrc/stall_probe.cpp, sampling /proc/<node>/task every 2 ms): what each
+    # node thread was doing in the kernel during a loop stall, even one that freezes the whole node process
+    ext_probe = None
+    if not a.cluster:
+        try:
+            from upow_amd.ops.native import lib as _lib
+            ext_probe = _lib().StallProbe(trace + '.ext', None, node.pid, 10.0, 2000, node.pid)
+        except (ImportError, AttributeError) as e:
+            print(f'external stall probe unavailable: {e}', flush=True)
     miner_log = open(os.path.join(data, 'miner.log'), 'w')
     from upow_amd.ops.native import gpu_available
     chunk = [] if gpu_available() else ['--chunk', '65536', '--device', 'cpu']
@@ -305,6 +314,8 @@ def main():
                     errors[0] += 1
     n = len(pushed) + errors[0]
     t_push_end = time.time()
+    if ext_probe is not None:
+        ext_probe.stop()
     cpu1 = _cpu_stat()
     phase[0] = 'drain'
     # drain: wait until everything pushed is in a block (or 4 block intervals)
@@ -400,6 +411,19 @@ def main():
                 elif state in ('R', 'D'):
                     k = f'{names.get(str(tid), comm)} {state} {wchan or "-"} sys={sc}'
                     nat_busy[k] = nat_busy.get(k, 0) + 1
+    ext_loop, ext_busy, ext_n = {}, {}, 0
+    if os.path.exists(trace + '.ext'):
+        for r in _jsonl(trace + '.ext'):
+            if not any(s0 <= r['t'] <= s1 for s0, s1, _ in stalls if s1 - s0 > 0.02):
+                continue  # only the samples inside a loop stall over 20 ms
+            ext_n += 1
+            for tid, comm, state, wchan, sc in r['threads']:
+                if str(tid) == (loop_tid or str(node.pid)):
+                    k = f'{state} {wchan or "-"} sys={sc}'
+                    ext_loop[k] = ext_loop.get(k, 0) + 1
+                elif state in ('R', 'D'):
+                    k = f'{names.get(str(tid), comm)} {state} {wchan or "-"} sys={sc}'
+                    ext_busy[k] = ext_busy.get(k, 0) + 1
     top_stacks = sorted(stack_counts.items(), key=lambda kv: -kv[1])[:12]
     top_others = sorted(other_counts.items(), key=lambda kv: -kv[1])[:12]
     gcs = []
@@ -442,6 +466,9 @@ def main():
         'loop_stall_native': {'samples': nat_n,
                               'loop_thread': dict(sorted(nat_loop.items(), key=lambda kv: -kv[1])[:8]),
                               'running_or_disk': dict(sorted(nat_busy.items(), key=lambda kv: -kv[1])[:16])},
+        'loop_stall_external': {'samples_in_stalls_over_20ms': ext_n,
+                                'loop_thread': dict(sorted(ext_loop.items(), key=lambda kv: -kv[1])[:8]),
+                                'running_or_disk': dict(sorted(ext_busy.items(), key=lambda kv: -kv[1])[:16])},
         'gc_over_2ms': {'n': len(gcs), 'total_ms': round(sum(g['ms'] for g in gcs), 1),
                         'max_ms': round(max((g['ms'] for g in gcs), default=0), 1),
                         'gen2': sum(1 for g in gcs if g.get('gen') == 2)},
