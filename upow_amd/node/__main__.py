@@ -62,8 +62,9 @@ def main(argv=None):
                     help='multi-GPU node under torchrun: rank 0 serves the API, other ranks are HBM replicas')
     a = ap.parse_args(argv)
     pin_cpus(os.environ.get('UPOW_CPU_AFFINITY', 'off'))
-    from ..utils.cpus import tune_malloc
+    from ..utils.cpus import presize_fd_table, tune_malloc
     tune_malloc()
+    presize_fd_table()
     if a.data:
         os.environ['UPOW_DATA_DIR'] = a.data
     if a.db:

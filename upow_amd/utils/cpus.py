@@ -35,3 +35,38 @@ def tune_malloc() -> bool:
         return False
     from ..ops.native import lib
     return bool(lib().malloc_tune(256 << 20, 1 << 30))
+
+
+def presize_fd_table(n: int = 16384) -> int:
+    """Grow this process's file-descriptor table to ``n`` slots now, while it is cheap (``UPOW_FD_PRESIZE=0``
+    skips). The kernel grows the table by doubling when an open/accept needs a slot past its end, and in a
+    multithreaded process each growth waits for an RCU grace period before the old table can go; every
+    other thread opening a descriptor meanwhile waits too. A node crossing a size boundary mid-run (ledger
+    files x connections x WAL/shm files, plus sockets) froze its HTTP event loop in ``accept4`` for
+    150-200 ms at a time: soak probe samples showed the loop in ``__wait_rcu_gp`` and the other threads in
+    ``expand_files`` (profiles/r4/node_soak_fdtable_r4z.json). The soft RLIMIT_NOFILE is raised to ``n``
+    when the hard limit allows. Returns the table size reached (/proc/self/status FDSize), 0 if skipped."""
+    if os.environ.get('UPOW_FD_PRESIZE', '1') == '0':
+        return 0
+    import resource
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    if soft != resource.RLIM_INFINITY and soft < n and (hard == resource.RLIM_INFINITY or hard >= n):
+        resource.setrlimit(resource.RLIMIT_NOFILE, (n, hard))
+        soft = n
+    top = (n if soft == resource.RLIM_INFINITY else min(n, soft)) - 1
+    fd = os.open(os.devnull, os.O_RDONLY)
+    try:
+        if fd < top:
+            os.dup2(fd, top, inheritable=False)  # the table is sized to fit the highest descriptor
+            os.close(top)
+    finally:
+        os.close(fd)
+    try:
+        with open('/proc/self/status') as f:
+            for line in f:
+                if line.startswith('FDSize:'):
+                    return int(line.split()[1])
+    except OSError:
+        pass
+    return top + 1
+
