@@ -212,8 +212,9 @@ def main(argv=None):
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from upow_amd.ops.native import lib
     lib()  # loads torch's HIP runtime first, then the extension (fails loudly if not built)
-    from upow_amd.utils.cpus import tune_malloc
+    from upow_amd.utils.cpus import presize_fd_table, tune_malloc
     tune_malloc()  # as the node process does (upow_amd/node/__main__.py)
+    presize_fd_table()
     from upow_amd.parallel.dist import init_from_env, shutdown
     ctx = init_from_env()
     try:
