@@ -88,7 +88,7 @@ for s in $STEPS; do
         || { tail -20 "$OUT/verify_aged.err"; exit 1; }
       cat "$OUT/verify_aged.json" ;;
     verifyaged60)
-      # the aged ledger, default 4 + 4 split, 60 blocks (the A of verifyaged8)
+      # the aged ledger, default split, 60 blocks (the A of verifyaged8)
       rm -rf /tmp/upow_bench_ledger
       timeout -k 10 900 python -u bench.py --mode verify --ledger /tmp/upow_bench_ledger \
         --age-txs 2500000 --steps 60 --warmup 2 > "$OUT/verify_aged60.json" 2> "$OUT/verify_aged60.err" \

@@ -115,8 +115,10 @@ for _t in OUTPUT_TABLES[1:]:
 #   before the transactions split keep ``transactions`` in the main file (one "file", no view) and two
 #   UTXO files.
 _SQL_READERS = None  # Database._off_loop
-UTXO_FILES_DEFAULT = 4
-TX_FILES_DEFAULT = 4
+# 5 + 5 (eleven files with the main one; SQLite attaches at most ten): ~20 % faster materialisation of an
+# aged ledger than 4 + 4 (profiles/r4/verify_aged_writer_ab_r4g.json, verify_aged60_s55_r4x.json)
+UTXO_FILES_DEFAULT = 5
+TX_FILES_DEFAULT = 5
 ROUTED = ('unspent_outputs', 'transactions')
 
 
