@@ -352,6 +352,19 @@ def main():
             f.write(buf.getvalue())
     included = {h: included[h] for h in pushed if h in included}
     lat = sorted(included[h] - pushed[h] for h in included)
+    # the slowest 1 %: when they were pushed and when their block was seen (seconds from the push start),
+    # and the heights that carried them -- a tail from one late block differs from txs a template skipped
+    tail = sorted(included, key=lambda h: included[h] - pushed[h])[-max(1, len(included) // 100):] if included else []
+    h_of = {}
+    for ht, bt, _ in blocks:
+        h_of.setdefault(round(bt, 3), ht)
+    tail_info = {
+        'n': len(tail),
+        'pushed_s': [round(min(pushed[h] for h in tail) - t0, 2), round(max(pushed[h] for h in tail) - t0, 2)] if tail else None,
+        'seen_s': [round(min(included[h] for h in tail) - t0, 2), round(max(included[h] for h in tail) - t0, 2)] if tail else None,
+        'heights': sorted({h_of.get(round(included[h], 3)) for h in tail} - {None}),
+        'block_seen_s': [[ht, round(bt - t0, 2), n] for ht, bt, n in blocks],
+    }
     miner_text = open(os.path.join(data, 'miner.log')).read()
     rates = [float(x) for x in re.findall(r'([0-9.]+) MH/s \(', miner_text)]
     per_rank = [json.loads(x) for x in re.findall(r'per-rank MH/s: (\[[^\]]*\])', miner_text)]
@@ -448,6 +461,7 @@ def main():
         'push_threads': a.threads, 'push_procs': a.procs, 'pool_utxos': len(pool),
         'confirmed': len(included), 'seconds': round(t_push_end - t0, 1),
         'inclusion_latency_s': {'p50': q(0.5), 'p90': q(0.9), 'p99': q(0.99), 'max': round(lat[-1], 2) if lat else None},
+        'inclusion_tail_1pct': tail_info,
         'blocks': len(blocks), 'mean_block_interval_s': round(sum(intervals) / len(intervals), 2) if intervals else None,
         'txs_per_block_max': max((b[2] for b in blocks), default=0),
         'block_apply_ms_mean': {k: round(1000 * v['sum'] / v['count'], 2) for k, v in apply.items() if v.get('count')},
