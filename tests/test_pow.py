@@ -111,3 +111,44 @@ def test_miner_tip_watcher_stops_stale_jobs():
         assert w.moved('aa' * 32) and not w.moved('bb' * 32)
     finally:
         w.close()
+
+
+def test_miner_job_planner_never_resweeps_a_space():
+    """After a job sweeps its whole space without a block, the next job of the same template drops one more
+    trailing transaction (a fresh merkle root), then -- nothing left to drop -- starts above the last swept
+    timestamp (upow_amd/miner.py JobPlanner)."""
+    from upow_amd.miner import JobPlanner
+    job = lambda hs: {'last_block': {'hash': 'aa' * 32, 'timestamp': 100}, 'pending_transactions_hashes': list(hs)}
+    p = JobPlanner()
+    assert p.plan(job('xyz'), 105) == (list('xyz'), 101)
+    p.finished(True, 105)
+    assert p.plan(job('xyz'), 106) == (list('xy'), 101)  # new merkle root, full window
+    p.finished(False, 106)  # stopped (tip moved / refresh): the same set again
+    assert p.plan(job('xyz'), 107) == (list('xy'), 101)
+    p.finished(True, 107)
+    assert p.plan(job('xyz'), 107) == (list('x'), 101)
+    p.finished(True, 107)
+    assert p.plan(job('xyz'), 108) == ([], 101)
+    p.finished(True, 108)
+    assert p.plan(job('xyz'), 108) == ([], 109)  # only timestamps not yet swept
+    p.finished(True, 110)
+    assert p.plan(job('xyz'), 111) == ([], 111)
+    # a changed template (or tip) starts over with every transaction
+    assert p.plan(job('xyzw'), 111) == (list('xyzw'), 101)
+    p.finished(True, 111)
+    nxt = {'last_block': {'hash': 'bb' * 32, 'timestamp': 111}, 'pending_transactions_hashes': list('xyzw')}
+    assert p.plan(nxt, 112) == (list('xyzw'), 112)
+
+
+def test_cluster_miner_reports_stop_vs_exhausted():
+    from upow_amd.parallel.dist import init_from_env
+    from upow_amd.parallel.miner_dp import ClusterMiner
+    ctx = init_from_env(want_gpu=False)
+
+    class _Miss:  # a search that finds nothing
+        nonces = []
+    none = lambda job, pos, n, **kw: _Miss()
+    m = ClusterMiner(ctx, 'aa' * 32, 'Dn7ufYB2yFEYdkJ1GAqLKnXSB2ytGTB5f4YfBk5eHGx6X', 'cc' * 32, 6, ts_max=101, ts_min=100,
+                     chunk=1 << 31, search_fn=none)
+    assert m.mine() is None and not m.stopped  # swept both timestamps
+    assert m.mine(should_stop=lambda: True) is None and m.stopped

@@ -14,7 +14,14 @@ MI355X version:
   earlier as soon as the node's tip moves: rank 0 polls ``/get_mining_info`` every ``--poll`` seconds
   (default 3 s, inside the endpoint's 30/min limit) and the ranks agree to drop the stale job — one
   GPU sweeps a timestamp's whole 2^32 nonces in ~0.12 s, so mining on an old tip for up to 90 s
-  would waste almost all of the work after a competing block arrives.
+  would waste almost all of the work after a competing block arrives;
+* a job whose whole space was swept without a block (the header is fixed but for the timestamp, which
+  may not run ahead of the clock, and the nonce) is followed by a FRESH space, never the same one again
+  (:class:`JobPlanner`): the template minus its last transaction (a new merkle root; dropping a suffix
+  never separates a parent from a child that follows it), and once no transaction is left to drop, only
+  the timestamps not yet swept. With an unchanged mempool a re-fetched job used to re-sweep the
+  timestamps it had already failed on, leaving ~2^32 fresh nonces per wall second: at difficulty 9 the
+  last block of a soak took 13-40 s instead of ~2 s (profiles/r4/node_soak_inclusion_tail_r4ac.json).
 """
 from __future__ import annotations
 
@@ -63,6 +70,41 @@ class TipWatcher:
         self._t.join(timeout=5)
 
 
+class JobPlanner:
+    """Rank 0's choice of (transactions, lowest timestamp) for the next job, so that a job never repeats
+    a search space an earlier job of the same template swept in full."""
+
+    def __init__(self):
+        self.key = None
+        self.trim = 0  # trailing template transactions left out
+        self.swept_to = None  # highest timestamp swept with the current transaction set
+        self.exhausted = False
+        self.last_ts_max = None
+
+    def plan(self, job: dict, now: int):
+        last = job['last_block']
+        hashes = job['pending_transactions_hashes']
+        key = (last.get('hash', GENESIS_PREV_HASH), hash(tuple(hashes)))
+        if key != self.key:
+            self.key, self.trim, self.swept_to, self.exhausted = key, 0, None, False
+        elif self.exhausted:
+            if self.trim < len(hashes):
+                self.trim += 1  # a new merkle root: the whole timestamp window is fresh again
+                self.swept_to = None
+            else:
+                self.swept_to = self.last_ts_max  # nothing left to vary but the clock
+        self.exhausted = False
+        use = hashes[:len(hashes) - self.trim] if self.trim else hashes
+        ts_min = last.get('timestamp', now - 60) + 1
+        if self.swept_to is not None:
+            ts_min = max(ts_min, self.swept_to + 1)
+        return use, ts_min
+
+    def finished(self, exhausted: bool, ts_max: int):
+        """The job ended: ``exhausted`` = its whole space was swept (not stopped, no block found)."""
+        self.exhausted, self.last_ts_max = exhausted, ts_max
+
+
 def submit(node_url: str, header: bytes, hashes, block_no: int) -> dict:
     r = httpx.post(node_url + 'push_block', json={'block_content': header.hex(), 'txs': hashes, 'block_no': block_no},
                    timeout=20 + int((len(hashes) or 1) / 3))
@@ -100,6 +142,7 @@ def main(argv=None):
     kw = {} if device == 'gpu' else {'threads': max(1, a.workers)}
     accepted = 0
     watcher = TipWatcher(node_url, a.poll) if (ctx.is_main and a.poll > 0) else None
+    planner = JobPlanner()
     try:
         while True:
             job = None
@@ -110,6 +153,7 @@ def main(argv=None):
                     except Exception as e:
                         print(e, flush=True)
                         time.sleep(1)
+                job['pending_transactions_hashes'], job['_ts_min'] = planner.plan(job, timestamp())
             job = json.loads(ctx.broadcast_bytes(json.dumps(job).encode() if ctx.is_main else None, src=0,
                                                  max_len=0).decode())
             last = job['last_block']
@@ -118,8 +162,8 @@ def main(argv=None):
             hashes = job['pending_transactions_hashes']
             merkle = miner_merkle_root(hashes)
             now = timestamp()
-            ts_min = last.get('timestamp', now - 60) + 1
-            if ts_min > now:  # the previous block is from this very second: a valid header needs a later one
+            ts_min = job['_ts_min']
+            if ts_min > now:  # the previous block (or the last swept timestamp) is from this very second
                 time.sleep(ts_min - now)
                 now = timestamp()
             if ctx.is_main:
@@ -132,6 +176,7 @@ def main(argv=None):
                 watcher.tip = None  # only polls made during this job count
             header = miner.mine(should_stop=lambda: time.time() - t0 > a.refresh or
                                 (watcher is not None and watcher.moved(prev)))
+            planner.finished(header is None and not miner.stopped, now)
             dt = max(time.time() - t0, 1e-9)
             per_rank = [float(x) / dt for x in ctx.all_gather_bytes(str(miner.hashes).encode())]
             rate = sum(per_rank)

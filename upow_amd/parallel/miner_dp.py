@@ -110,6 +110,7 @@ class ClusterMiner:
         self.search_kw = search_kw
         self._hp = header_prefix_raw
         self.hashes = 0
+        self.stopped = False  # the last mine() ended on should_stop (not on a swept space or a block)
 
     def units(self):
         for ts in range(self.ts_max, self.ts_min - 1, -1):
@@ -122,6 +123,7 @@ class ClusterMiner:
 
     def mine(self, should_stop: Callable[[], bool] = lambda: False) -> Optional[bytes]:
         ctx = self.ctx
+        self.stopped = False
         slice_len = NONCE_SPACE // ctx.world
         lo = ctx.rank * slice_len
         hi = NONCE_SPACE if ctx.rank == ctx.world - 1 else lo + slice_len
@@ -147,6 +149,7 @@ class ClusterMiner:
                         raise RuntimeError('broadcast header failed the PoW re-check')
                     return header
                 if keep_going == 0:
+                    self.stopped = True
                     return None
                 if all_done == 1:
                     break
