@@ -114,27 +114,36 @@ def test_miner_tip_watcher_stops_stale_jobs():
 
 
 def test_miner_job_planner_never_resweeps_a_space():
-    """After a job sweeps its whole space without a block, the next job of the same template drops one more
-    trailing transaction (a fresh merkle root), then -- nothing left to drop -- starts above the last swept
-    timestamp (upow_amd/miner.py JobPlanner)."""
+    """After a job sweeps its whole space without a block, the next job of the same template only sweeps the
+    timestamps added since; once the tip is trim_after_s old it drops one more trailing transaction (a fresh
+    merkle root and a fresh window), and with nothing left to drop only new timestamps again
+    (upow_amd/miner.py JobPlanner)."""
     from upow_amd.miner import JobPlanner
     job = lambda hs: {'last_block': {'hash': 'aa' * 32, 'timestamp': 100}, 'pending_transactions_hashes': list(hs)}
-    p = JobPlanner()
-    assert p.plan(job('xyz'), 105) == (list('xyz'), 101)
-    p.finished(True, 105)
-    assert p.plan(job('xyz'), 106) == (list('xy'), 101)  # new merkle root, full window
-    p.finished(False, 106)  # stopped (tip moved / refresh): the same set again
-    assert p.plan(job('xyz'), 107) == (list('xy'), 101)
-    p.finished(True, 107)
-    assert p.plan(job('xyz'), 107) == (list('x'), 101)
-    p.finished(True, 107)
-    assert p.plan(job('xyz'), 108) == ([], 101)
+    p = JobPlanner(trim_after_s=8)
+    assert p.plan(job('xyz'), 101) == (list('xyz'), 101)
+    p.finished(True, 101)
+    assert p.plan(job('xyz'), 101) == (list('xyz'), 102)  # young tip: wait for a new timestamp
+    p.finished(True, 103)
+    assert p.plan(job('xyz'), 104) == (list('xyz'), 104)
+    p.finished(False, 104)  # stopped (tip moved / refresh): the same window again
+    assert p.plan(job('xyz'), 105) == (list('xyz'), 104)
     p.finished(True, 108)
-    assert p.plan(job('xyz'), 108) == ([], 109)  # only timestamps not yet swept
+    assert p.plan(job('xyzw'), 108) == (list('xyzw'), 101)  # a new template: the full window
+    p.finished(True, 108)
+    assert p.plan(job('xyzw'), 108) == (list('xyz'), 101)  # tip 8 s old: new merkle root, full window
+    p.finished(True, 108)
+    assert p.plan(job('xyzw'), 109) == (list('xy'), 101)
+    p.finished(True, 109)
+    assert p.plan(job('xyzw'), 109) == (list('xy'), 110)  # half held back: only timestamps not yet swept
     p.finished(True, 110)
-    assert p.plan(job('xyz'), 111) == ([], 111)
+    assert p.plan(job('xyzw'), 111) == (list('xy'), 111)
+    one = JobPlanner(trim_after_s=8)  # a one-transaction template is never mined empty
+    assert one.plan(job('x'), 120) == (['x'], 101)
+    one.finished(True, 120)
+    assert one.plan(job('x'), 120) == (['x'], 121)
     # a changed template (or tip) starts over with every transaction
-    assert p.plan(job('xyzw'), 111) == (list('xyzw'), 101)
+    assert p.plan(job('xyzwv'), 111) == (list('xyzwv'), 101)
     p.finished(True, 111)
     nxt = {'last_block': {'hash': 'bb' * 32, 'timestamp': 111}, 'pending_transactions_hashes': list('xyzw')}
     assert p.plan(nxt, 112) == (list('xyzw'), 112)

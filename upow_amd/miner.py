@@ -17,11 +17,14 @@ MI355X version:
   would waste almost all of the work after a competing block arrives;
 * a job whose whole space was swept without a block (the header is fixed but for the timestamp, which
   may not run ahead of the clock, and the nonce) is followed by a FRESH space, never the same one again
-  (:class:`JobPlanner`): the template minus its last transaction (a new merkle root; dropping a suffix
-  never separates a parent from a child that follows it), and once no transaction is left to drop, only
-  the timestamps not yet swept. With an unchanged mempool a re-fetched job used to re-sweep the
-  timestamps it had already failed on, leaving ~2^32 fresh nonces per wall second: at difficulty 9 the
-  last block of a soak took 13-40 s instead of ~2 s (profiles/r4/node_soak_inclusion_tail_r4ac.json).
+  (:class:`JobPlanner`): only the timestamps not yet swept, and once the tip is ``--trim-after`` seconds
+  old (default 8), the template minus its last transaction (the merkle root is over the sorted hash set,
+  so only a different SET gives a new root; the dropped transactions, at most half the template, wait
+  one block). With an unchanged
+  mempool a re-fetched job used to re-sweep the timestamps it had already failed on, leaving ~2^32 fresh
+  nonces per wall second: at difficulty 9 the last block of a soak took 13-40 s instead of ~2 s
+  (profiles/r4/node_soak_inclusion_tail_r4ac.json). Dropping at once instead would starve the newest
+  transaction: right after a block the window is one or two timestamps, which a GPU sweeps in 0.2 s.
 """
 from __future__ import annotations
 
@@ -74,7 +77,8 @@ class JobPlanner:
     """Rank 0's choice of (transactions, lowest timestamp) for the next job, so that a job never repeats
     a search space an earlier job of the same template swept in full."""
 
-    def __init__(self):
+    def __init__(self, trim_after_s: float = 8.0):
+        self.trim_after_s = trim_after_s
         self.key = None
         self.trim = 0  # trailing template transactions left out
         self.swept_to = None  # highest timestamp swept with the current transaction set
@@ -88,11 +92,13 @@ class JobPlanner:
         if key != self.key:
             self.key, self.trim, self.swept_to, self.exhausted = key, 0, None, False
         elif self.exhausted:
-            if self.trim < len(hashes):
+            old = now - last.get('timestamp', now) >= self.trim_after_s
+            # at most half the template is held back: a one-transaction template is never mined empty
+            if old and self.trim < len(hashes) // 2:
                 self.trim += 1  # a new merkle root: the whole timestamp window is fresh again
                 self.swept_to = None
             else:
-                self.swept_to = self.last_ts_max  # nothing left to vary but the clock
+                self.swept_to = self.last_ts_max  # only the timestamps the clock has added since
         self.exhausted = False
         use = hashes[:len(hashes) - self.trim] if self.trim else hashes
         ts_min = last.get('timestamp', now - 60) + 1
@@ -118,6 +124,8 @@ def main(argv=None):
     ap.add_argument('node_url', nargs='?', default=None)
     ap.add_argument('--device', choices=['gpu', 'cpu'], default=None)
     ap.add_argument('--refresh', type=float, default=90.0)
+    ap.add_argument('--trim-after', type=float, default=8.0,
+                    help='tip age (s) after which a swept-out template is retried without its last transaction')
     ap.add_argument('--poll', type=float, default=3.0, help='tip poll period in seconds (0 = off)')
     ap.add_argument('--chunk', type=int, default=1 << 28)
     ap.add_argument('--extranonce', action='store_true',
@@ -142,7 +150,7 @@ def main(argv=None):
     kw = {} if device == 'gpu' else {'threads': max(1, a.workers)}
     accepted = 0
     watcher = TipWatcher(node_url, a.poll) if (ctx.is_main and a.poll > 0) else None
-    planner = JobPlanner()
+    planner = JobPlanner(a.trim_after)
     try:
         while True:
             job = None
