@@ -46,6 +46,11 @@ async def main(args):
                                                      ledger_path=os.path.join(path, 'ledger.sqlite3'),
                                                      gov_txs=gov, distinct_keys=True)
             db.flush()
+            # the tx strings as a node holds them: parsed from one JSON body (/push_block, sync), i.e. allocated
+            # together. The generator's strings are scattered over its setup heap, and that alone made the
+            # native decode of the governance block ~10 % slower single-threaded (8 % of it gone after this
+            # round trip, on one pinned CPU; docs/ROUND4.md section 8)
+            blocks = [json.loads(json.dumps(b)) for b in blocks]
             last = await db.get_last_block()
             prev, headers = last['hash'], []
             for b, txs in enumerate(blocks):
