@@ -459,6 +459,9 @@ async def _run(args, ctx, device, utxo_backend):
     key_setup = aging.pop('distinct_key_setup_s', None)
     if aging:
         db.flush()
+    # (untimed) the tx strings as a node holds them: parsed from one JSON body (/push_block, sync), allocated
+    # together, not scattered over the generator's setup heap (scripts/gov_ab.py, docs/ROUND4.md section 8)
+    blocks = [json.loads(json.dumps(b)) for b in blocks]
     gov_probe = await _governance_probe(db) if gov else None
     # mine every header up front (untimed): block b+1's previous hash is sha256(header_b) and the
     # difficulty stays at START_DIFFICULTY below block 100
