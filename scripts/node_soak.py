@@ -156,11 +156,21 @@ def main():
     # an observer outside the node (csrc/stall_probe.cpp, sampling /proc/<node>/task every 2 ms): what each
     # node thread was doing in the kernel during a loop stall, even one that freezes the whole node process
     ext_probe = None
-    if not a.cluster:
+    node_pid = node.pid
+    if a.cluster:  # the serving rank is a torchrun child: its loop thread id (= its pid) is in <trace>.threads
+        node_pid = None
+        for _ in range(100):
+            try:
+                with open(trace + '.threads') as tf:
+                    node_pid = int(json.load(tf)['_loop'])
+                break
+            except (OSError, ValueError, KeyError):
+                time.sleep(0.1)
+    if node_pid is not None:
         try:
             from upow_amd.ops.native import lib as _lib
-            ext_probe = _lib().StallProbe(trace + '.ext', None, node.pid, 10.0, 2000, node.pid)
-        except (ImportError, AttributeError) as e:
+            ext_probe = _lib().StallProbe(trace + '.ext', None, node_pid, 10.0, 2000, node_pid)
+        except (ImportError, AttributeError, RuntimeError) as e:
             print(f'external stall probe unavailable: {e}', flush=True)
     miner_log = open(os.path.join(data, 'miner.log'), 'w')
     from upow_amd.ops.native import gpu_available
@@ -431,7 +441,7 @@ def main():
                 continue  # only the samples inside a loop stall over 20 ms
             ext_n += 1
             for tid, comm, state, wchan, sc in r['threads']:
-                if str(tid) == (loop_tid or str(node.pid)):
+                if str(tid) == (loop_tid or str(node_pid)):
                     k = f'{state} {wchan or "-"} sys={sc}'
                     ext_loop[k] = ext_loop.get(k, 0) + 1
                 elif state in ('R', 'D'):
