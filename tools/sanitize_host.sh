@@ -91,12 +91,13 @@ UPOW_NATIVE_SO=$ROOT/build/native-asan/_native$EXT ASAN_OPTIONS=detect_leaks=0:d
   UBSAN_OPTIONS=print_stacktrace=1 timeout -k 10 1500 "$OUT/pysan_asan" -m pytest -q -x -m "not gpu" -p no:cacheprovider \
   tests/test_txcodec.py tests/test_http_server.py tests/test_mempool_index.py tests/test_ledger_writer.py \
   tests/test_gov_cascade.py tests/test_log_appender.py tests/test_fastpath.py tests/test_fastpath_governance.py \
-  tests/test_rollback_undo.py tests/test_crash_recovery.py > "$OUT/pytest_asan.log" 2>&1 \
+  tests/test_rollback_undo.py tests/test_crash_recovery.py tests/test_process_tuning.py > "$OUT/pytest_asan.log" 2>&1 \
   || { tail -60 "$OUT/pytest_asan.log"; exit 1; }
 echo "python tests under ASan + UBSan: $(tail -1 "$OUT/pytest_asan.log")"
 UPOW_NATIVE_SO=$ROOT/build/native-tsan/_native$EXT TSAN_OPTIONS=halt_on_error=1:report_signal_unsafe=0 \
   timeout -k 10 900 "$OUT/pysan_tsan" -m pytest -q -x -m "not gpu" -p no:cacheprovider \
-  tests/test_mempool_index.py tests/test_ledger_writer.py tests/test_log_appender.py > "$OUT/pytest_tsan.log" 2>&1 \
+  tests/test_mempool_index.py tests/test_ledger_writer.py tests/test_log_appender.py tests/test_process_tuning.py \
+  > "$OUT/pytest_tsan.log" 2>&1 \
   || { tail -60 "$OUT/pytest_tsan.log"; exit 1; }
 echo "python tests under TSan: $(tail -1 "$OUT/pytest_tsan.log")"
 echo "sanitize_host: all stages passed"
