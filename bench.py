@@ -191,6 +191,8 @@ def main(argv=None):
                     help='verify/sync modes: a fresh key pair per tx (default) or a 256-key pool (cache-friendly)')
     ap.add_argument('--verify-pool256', type=int, default=1,
                     help='mine mode: also report the 256-key-pool verify number as a labelled second value')
+    ap.add_argument('--sync-path', choices=['page', 'block'], default='page',
+                    help='sync mode: page-batched (ledger/pagesync.py, default) or the per-block pipeline (A/B)')
     ap.add_argument('--verify-steps', type=int, default=10,
                     help='mine mode: timed 2 MB blocks of the tx-verify side measurement (0: skip; GPU only)')
     args = ap.parse_args(argv)
@@ -234,6 +236,8 @@ def main(argv=None):
             out = bench_verify(args, ctx)
         else:
             from upow_amd.bench_verify import run_sync_bench
+            from upow_amd.ledger import pagesync
+            pagesync.ENABLED = args.sync_path == 'page'
             out = run_sync_bench(args, ctx)
         if ctx.is_main:
             print(json.dumps(out), flush=True)

@@ -919,7 +919,10 @@ class LedgerWriter {
     // the journal I/O thread right after its reservation, which checksums it, writes it, stores the block's
     // undo data, publishes it and fdatasyncs it; durable(seq) waits for all of that. The sequence number
     // (the commit order) is fixed before submit returns either way.
-    uint64_t submit(std::vector<Part> stmts, std::string meta, int64_t block_id, bool sync = true) {
+    // ``group`` (deferred records only): the I/O thread does not fdatasync this block record on its own; the
+    // caller's later durable(seq) makes the whole prefix durable with one fdatasync (group commit of a sync
+    // page: a crash loses at most the page's unsynced tail, which the node fetches again).
+    uint64_t submit(std::vector<Part> stmts, std::string meta, int64_t block_id, bool sync = true, bool group = false) {
         Batch b;
         const uint32_t ns = uint32_t(stmts.size());
         b.parts.reserve(stmts.size() + 1);
@@ -950,7 +953,7 @@ class LedgerWriter {
                 const uint64_t seq = b.seq;
                 {
                     std::lock_guard<std::mutex> g(io_mu_);
-                    io_q_.push_back(IoJob{std::move(b), at, block_id, std::move(meta)});
+                    io_q_.push_back(IoJob{std::move(b), at, block_id, std::move(meta), group});
                     ++io_pending_;
                 }
                 io_cv_.notify_one();
@@ -1000,6 +1003,7 @@ class LedgerWriter {
         off_t at;
         int64_t block_id;
         std::string meta;
+        bool group = false;  // group commit: no per-record fdatasync (durable() syncs the prefix)
     };
 
     // The journal I/O thread: deferred (block) records in submission order. The undo data is stored before
@@ -1039,7 +1043,8 @@ class LedgerWriter {
             }
             // block records: durable before durable(seq) returns (any mode but off); other deferred
             // records only in commit mode (the materialisers' group sync covers them otherwise)
-            const bool want_sync = sync_ == SYNC_COMMIT || (sync_ != SYNC_OFF && job.block_id >= 0);
+            const bool want_sync = sync_ == SYNC_COMMIT || (sync_ != SYNC_OFF && job.block_id >= 0 && !job.group);
+            if (job.group) ++group_records_;
             if (werr.empty() && err.empty() && want_sync) {
                 try {
                     make_durable(seq);
@@ -1159,6 +1164,7 @@ class LedgerWriter {
             d["synced"] = synced_.load();
             d["synced_bytes"] = synced_bytes_.load();
             d["fdatasyncs"] = syncs_.load();
+            d["group_records"] = group_records_.load();
             d["fdatasync_s"] = sync_total_ns_.load() / 1e9;
             d["shards"] = per;
             py::dict st;
@@ -1672,7 +1678,7 @@ class LedgerWriter {
     std::mutex sync_mu_;
     std::atomic<uint64_t> synced_{0};
     std::atomic<int64_t> synced_bytes_{0};
-    std::atomic<int64_t> syncs_{0}, sync_total_ns_{0};
+    std::atomic<int64_t> syncs_{0}, sync_total_ns_{0}, group_records_{0};
     std::map<std::string, std::pair<int64_t, int64_t>> stmt_stats_;  // sql prefix -> (ns, rows)
     // journal I/O thread (deferred block records)
     std::mutex io_mu_;
@@ -1712,7 +1718,7 @@ void register_ledger_writer(py::module_& m) {
              py::arg("max_queue_bytes") = int64_t(512) << 20, py::arg("throttle_timeout_s") = 300.0,
              py::arg("busy_timeout_ms") = 5000)
         .def("submit",
-             [](LedgerWriter& w, py::list stmts, py::object meta, int64_t block_id, bool sync) {
+             [](LedgerWriter& w, py::list stmts, py::object meta, int64_t block_id, bool sync, bool group) {
                  // encoded statements are taken as they are (shared buffers); plain bytes are copied
                  std::vector<Part> v;
                  v.reserve(stmts.size());
@@ -1750,9 +1756,10 @@ void register_ledger_writer(py::module_& m) {
                  std::string m;
                  m.reserve(total);
                  for (auto& pr : mparts) m.append(pr.first, pr.second);
-                 return w.submit(std::move(v), std::move(m), block_id, sync);
+                 return w.submit(std::move(v), std::move(m), block_id, sync, group);
              },
-             py::arg("stmts"), py::arg("meta") = py::bytes(""), py::arg("block_id") = -1, py::arg("sync") = true)
+             py::arg("stmts"), py::arg("meta") = py::bytes(""), py::arg("block_id") = -1, py::arg("sync") = true,
+             py::arg("group") = false)
         .def("applied", &LedgerWriter::applied, py::arg("shard") = -1)
         .def("set_paused", &LedgerWriter::set_paused)
         .def("wait", &LedgerWriter::wait, py::arg("seq"), py::arg("shard") = -1, py::arg("timeout_s") = 0.0,

@@ -33,6 +33,7 @@
 #   p256n    kernel trace of quad vs oct at 1,024 / 4,096 / 8,192 / 8,300 signatures
 #   soakc1   cluster node + DP miner under torchrun, forced single-rank RCCL, 40 tx/s (node_soak.py --cluster 1)
 #   soakc1k  the same at 1,200 tx/s
+#   bench:NAME:--a,1,...  bench.py with extra arguments (output bench_NAME.json)
 #   py:<script.py>  any extra python script under scripts/ (args after a comma: py:x.py,--a,1)
 # Every GPU step has its own time limit and the chain stops at the first failure.
 set -o pipefail
@@ -231,6 +232,13 @@ for s in $STEPS; do
           || { tail -30 "$OUT/soak_$i.log"; exit 1; }
         tail -1 "$OUT/soak_$i.log" | cut -c1-600
       done ;;
+    bench:*)
+      # bench:NAME:--arg,value,...  one bench.py run with extra arguments (file ledger under /tmp)
+      spec=${s#bench:}; name=${spec%%:*}; rest=${spec#*:}; rest=${rest//,/ }
+      rm -rf /tmp/upow_bench_ledger
+      timeout -k 10 900 python -u bench.py $rest > "$OUT/bench_$name.json" 2> "$OUT/bench_$name.err" \
+        || { tail -30 "$OUT/bench_$name.err"; exit 1; }
+      cut -c1-600 "$OUT/bench_$name.json" ;;
     py:*)
       spec=${s#py:}; script=${spec%%,*}; rest=""
       [ "$spec" != "$script" ] && rest=${spec#*,} && rest=${rest//,/ }

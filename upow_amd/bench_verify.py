@@ -419,6 +419,18 @@ async def _governance_probe(db) -> dict:
             'one_validator_stake_sql_ms': round((t5 - t4) * 1e3, 2), 'stake_matches_sql': sql_stake == idx_stake}
 
 
+def _dump_profile(prof, path: str):
+    import io
+    import pstats
+    prof.disable()
+    out = io.StringIO()
+    st = pstats.Stats(prof, stream=out)
+    st.sort_stats('cumulative').print_stats(70)
+    st.sort_stats('tottime').print_stats(40)
+    with open(path, 'w') as f:
+        f.write(out.getvalue())
+
+
 def _distinct(args) -> bool:
     return getattr(args, 'keys', 'distinct') == 'distinct'
 
@@ -535,15 +547,7 @@ async def _run(args, ctx, device, utxo_backend):
     ctx.barrier()
     wall = time.perf_counter() - t_start - untimed
     if prof is not None:  # UPOW_BENCH_PROFILE=PATH: cProfile of the timed blocks only (text report)
-        import io
-        import pstats
-        prof.disable()
-        out = io.StringIO()
-        st = pstats.Stats(prof, stream=out)
-        st.sort_stats('cumulative').print_stats(70)
-        st.sort_stats('tottime').print_stats(40)
-        with open(os.environ['UPOW_BENCH_PROFILE'], 'w') as f:
-            f.write(out.getvalue())
+        _dump_profile(prof, os.environ['UPOW_BENCH_PROFILE'])
     wall = ctx.allreduce_max_f(wall)
     writer = db.writer.stats() if db.writer is not None else None
     if writer is not None:
@@ -783,6 +787,11 @@ async def _run_sync(args, ctx, device, utxo_backend):
             raise RuntimeError('sync warmup rejected')
     ctx.barrier()
     ctx.synchronize()
+    prof = None
+    if os.environ.get('UPOW_BENCH_PROFILE'):  # cProfile of the timed replay only (text report)
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     errors = []
     if not await create_blocks(page[args.warmup:], errors):
@@ -791,11 +800,19 @@ async def _run_sync(args, ctx, device, utxo_backend):
     ctx.synchronize()
     ctx.barrier()
     wall = ctx.allreduce_max_f(time.perf_counter() - t0)
+    if prof is not None:
+        _dump_profile(prof, os.environ['UPOW_BENCH_PROFILE'])
     assert (await dst.get_last_block())['hash'] == page[-1]['block']['hash']
     writer = dst.writer.stats() if dst.writer is not None else {}
+    from .ledger import pagesync
     return args.steps * args.txs, wall, fastpath.last_path, {
         'aged_ledger': aging or None, 'journal_rotations': writer.get('rotations'),
-        'writer_throttle_s': writer.get('throttle_s'), 'undo_blocks': writer.get('undo_blocks')}
+        'writer_throttle_s': writer.get('throttle_s'), 'undo_blocks': writer.get('undo_blocks'),
+        'sync_path': 'page' if pagesync.ENABLED else 'per-block',
+        'page': ({k: (round(v, 4) if isinstance(v, float) else v) for k, v in pagesync.stats.items()}
+                 if pagesync.ENABLED else None),
+        'journal_fdatasyncs': writer.get('fdatasyncs'), 'journal_group_records': writer.get('group_records'),
+        'utxo_deferred_flushes': dst.utxo.deferred_flushes}
 
 
 def run_sync_bench(args, ctx):

@@ -413,7 +413,7 @@ class Database:
         self._pending_empty: Optional[bool] = None
         self._mempool_ver = 0
         self.on_admit = None  # cluster leader: row hook of every admission (parallel/cluster.py)
-        self.on_confirm = None  # cluster leader: hook of a block's mempool confirm, under the index lock
+        self.on_confirm = None  # cluster leader: hook (index, hit txs, hit inputs) of a block's mempool confirm
         self._mp: Optional[MempoolIndex] = None  # ledger/mempool.py; None: (re)load from SQL on next use
         self.mempool_reloads = 0
         self._seq_lock = threading.Lock()  # journal submission + per-table sequence bookkeeping
@@ -808,7 +808,9 @@ class Database:
             # the writer's journal I/O thread checksums, writes and fdatasyncs the block record (and stores
             # its undo data) while the caller updates its indexes; the sequence number is fixed here. The
             # block is not answered or gossiped before wait_durable() (UPOW_JOURNAL_SYNC=block semantics).
-            seq = self.writer.submit(stmts, meta, block_id, False)
+            # Inside a group commit (a sync page, ledger/pagesync.py) the record is not synced on its own: the
+            # page's closing wait_durable() makes every block of the page durable with one fdatasync.
+            seq = self.writer.submit(stmts, meta, block_id, False, self.group_commit > 0)
             self._durable_seq = seq
         elif write_behind and self._journal_sync_mode != 2:
             # a mempool record (not synced on its own unless UPOW_JOURNAL_SYNC=commit): the sequence number
@@ -826,10 +828,15 @@ class Database:
         return seq
 
     _durable_seq = 0
+    utxo_defer = False  # True while a sync page applies plan-checked blocks (UtxoIndex.defer_block)
+    group_commit = 0  # > 0 while a sync page applies its blocks (ledger/pagesync.py): one fdatasync per page
 
-    def wait_durable(self):
+    def wait_durable(self, force: bool = False):
         """Block until the last block record submitted with ``defer_sync`` is written and on disk (raises when
-        the writer failed on it: a journal write error after the commit point stops the ledger)."""
+        the writer failed on it: a journal write error after the commit point stops the ledger). During a group
+        commit this is a no-op unless ``force``: the page's end makes the whole page durable at once."""
+        if self.group_commit > 0 and not force:
+            return
         seq, self._durable_seq = self._durable_seq, 0
         if seq and self.writer is not None:
             self.writer.durable(seq)
@@ -1175,11 +1182,11 @@ class Database:
             if self.on_confirm is not None:  # no index: the block's SQL deletes cover all its txs and inputs
                 if txids is not None:
                     kk = np.asarray(in_keys, dtype=np.uint8)
-                    self.on_confirm([bytes(r) for r in np.asarray(txids, np.uint8).reshape(-1, 32)],
+                    self.on_confirm(None, [bytes(r) for r in np.asarray(txids, np.uint8).reshape(-1, 32)],
                                     [bytes(r[:36]) for r in kk.reshape(-1, kk.shape[-1] if kk.ndim == 2 else 40)])
                 else:
                     from .mempool import outpoint_key
-                    self.on_confirm([bytes.fromhex(h) for h in hashes or []],
+                    self.on_confirm(None, [bytes.fromhex(h) for h in hashes or []],
                                     [outpoint_key(h, i) for h, i in inputs or []])
             return
         if txids is not None:
@@ -1232,7 +1239,7 @@ class Database:
         await self.add_transactions_pending_spent_outputs([transaction])
         if self.on_admit is not None:
             self.on_admit([tx_hex, _j(inputs_addresses), numeric(transaction.fees, 6), ptime,
-                           [[i.tx_hash, int(i.index)] for i in transaction.inputs]])
+                           [[i.tx_hash, int(i.index)] for i in transaction.inputs], sha256(tx_hex)])
         return True
 
     def _admit(self, mp: MempoolIndex, transaction: Transaction, tx_hex: str, inputs_addresses: list) -> bool:
@@ -1261,7 +1268,7 @@ class Database:
             seq = self.submit_batch(stmts, self._PENDING, write_behind=True)
             mp.set_seq(tx_hash, inputs, seq)
             if self.on_admit is not None:  # cluster leader: replicate the admitted row (under the index lock)
-                self.on_admit([tx_hex, _j(inputs_addresses), fees, ptime, [[h, i] for h, i in inputs]])
+                self.on_admit([tx_hex, _j(inputs_addresses), fees, ptime, [[h, i] for h, i in inputs], tx_hash])
         self._pending_empty = False
         self._mempool_ver += 1
         return True
@@ -2132,11 +2139,16 @@ class Database:
                         logger.error(f'native block apply: {done} of {expect} rows changed [{sql[:40]}]')
         # ---- the index and the chain-tip cache follow the commit point
         stamp()
-        self.utxo.insert_records(recs, pay)
-        if len(cb_keys):
-            self.utxo.insert_records(cb_recs, cb_pay)
-        if n_in:
-            self.utxo.erase_records(spent)
+        if self.utxo_defer:
+            # a sync page (ledger/pagesync.py): the page's index writes go to the device as one insert and one
+            # erase launch when the page ends (or before anything reads the index)
+            self.utxo.defer_block([(recs, pay), (cb_recs, cb_pay)], spent if n_in else spent[:0])
+        else:
+            self.utxo.insert_records(recs, pay)
+            if len(cb_keys):
+                self.utxo.insert_records(cb_recs, cb_pay)
+            if n_in:
+                self.utxo.erase_records(spent)
         stamp()
         tip = dict(b)
         tip['difficulty'], tip['reward'] = Decimal(tip['difficulty']), Decimal(tip['reward'])

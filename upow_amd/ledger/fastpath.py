@@ -82,11 +82,11 @@ def _i32(d, k):
     return np.frombuffer(d[k], dtype=np.int32)
 
 
-def decode(tx_hexes: List[str]) -> Optional[dict]:
+def decode(tx_hexes: List[str], threads: int = 0) -> Optional[dict]:
     """Native decode; None when the block needs the object path."""
     if not ENABLED:
         return None
-    d = lib().decode_block_txs(list(tx_hexes), THREADS)
+    d = lib().decode_block_txs(list(tx_hexes), threads or THREADS)
     if not d['all_fast']:
         return None
     # tx types from the messages: decided natively except for encodings only Python's int() can judge
@@ -185,18 +185,19 @@ def _with_signers(pay: np.ndarray, signers: dict) -> np.ndarray:
 
 async def create_block_from_hex(block_content: str, tx_hexes: List[str], error_list: list = None,
                                 last_block: dict = None, coinbase=None, mirror: bool = True,
-                                decoded: Optional[dict] = None) -> bool:
+                                decoded: Optional[dict] = None, page=None) -> bool:
     """``create_block(block_content, [Transaction.from_hex(h) for h in tx_hexes])``, natively when possible.
 
     ``decoded``: ``decode(tx_hexes)`` computed ahead of time (the sync pipeline decodes block k+1 on a
-    host thread while block k is applied); None means decode here.
+    host thread while block k is applied); None means decode here. ``page``: this block's share of a sync
+    page's plan (ledger/pagesync.py ``PageBlock``: UTXO pass and signature verdicts already resolved).
 
     With ``coinbase`` (a CoinbaseTransaction) this is the sync variant ``create_block_in_syncing_old``
     (manager.py:760-835), which trusts the supplied coinbase instead of rebuilding it.
 
     On a multi-GPU cluster node (parallel/cluster.py) the leader first broadcasts the block to the
-    follower replicas (``mirror``); every rank validates it (signatures sharded across the GPUs) and
-    an all-reduce checks that all replicas reached the same verdict."""
+    follower replicas (``mirror``); every rank validates it, and the replicas agree in one all-reduce
+    right BEFORE any of them commits it (``cluster.commit_gate``)."""
     from ..parallel import cluster
     c = cluster.get()
     if c is not None and c.leader and mirror and not c.replaying:
@@ -204,19 +205,22 @@ async def create_block_from_hex(block_content: str, tx_hexes: List[str], error_l
         flush_txs()  # the followers' mempools first: block rules consult pending txs
         c.send('block', pack_txs(tx_hexes), content=block_content, cb=coinbase.hex() if coinbase is not None else None)
     err = None
+    # agree before commit: every replica votes right before its ledger writes (manager._finalize_* →
+    # cluster.commit_gate) and writes only if all voted yes; a replica that rejects votes no at the end
+    gate, token = cluster.open_gate('block')
     try:
-        ok = await _create_block_from_hex(block_content, tx_hexes, error_list, last_block, coinbase, decoded)
-    except Exception as e:  # every replica must still take part in the agreement below
+        ok = await _create_block_from_hex(block_content, tx_hexes, error_list, last_block, coinbase, decoded, page)
+    except Exception as e:  # every replica must still take part in the agreement
         ok, err = False, e
-    if c is not None and not c.replaying:
-        ok = c.agree(ok, 'block')
+    ok = cluster.close_gate(gate, token, ok)
     if err is not None and (c is None or c.leader):
         raise err
     return ok
 
 
 async def _create_block_from_hex(block_content: str, tx_hexes: List[str], error_list: list = None,
-                                 last_block: dict = None, coinbase=None, decoded: Optional[dict] = None) -> bool:
+                                 last_block: dict = None, coinbase=None, decoded: Optional[dict] = None,
+                                 page=None) -> bool:
     global last_path
     from . import manager
     if error_list is None:
@@ -241,7 +245,7 @@ async def _create_block_from_hex(block_content: str, tx_hexes: List[str], error_
     async with manager.ledger_lock():
         d0 = roctx.depth()
         try:
-            ok = await _create_block_fast(block_content, dec, error_list, last_block, t0, coinbase)
+            ok = await _create_block_fast(block_content, dec, error_list, last_block, t0, coinbase, page)
         finally:
             roctx.unwind(d0)
             # the block record's fdatasync overlapped the index updates; it is durable before the block is
@@ -259,7 +263,7 @@ async def _create_block_from_hex(block_content: str, tx_hexes: List[str], error_
 
 
 async def _create_block_fast(block_content: str, d: dict, error_list: list, last_block: Optional[dict],
-                             t0: float, coinbase=None) -> Optional[bool]:
+                             t0: float, coinbase=None, page=None) -> Optional[bool]:
     """True/False for a decided block; None = hand over to the object path."""
     from . import manager, validate
     from .database import Database
@@ -291,8 +295,15 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     in_tx, out_tx = _i32(d, 'in_tx'), _i32(d, 'out_tx')
     out_type = np.frombuffer(d['out_type'], dtype=np.uint8)
     bg = BlockGovernance(d['_tx_type'], out_type, out_tx, out_start, in_tx)
-    tags, pay, dup_of, fee, missing, n_dup = database.utxo.block_inputs(
-        in_keys, in_start, out_amount, out_start, TAG_BY_TABLE['unspent_outputs'])
+    if page is not None:
+        # a sync page's plan (ledger/pagesync.py) already resolved this block's inputs against the pre-page
+        # index plus the outputs of the page's earlier blocks, and found them live, unique and plain
+        if bg.any:
+            return None
+        tags, pay, fee, missing, n_dup = page.tags, page.pay, page.fee.copy(), None, 0
+    else:
+        tags, pay, dup_of, fee, missing, n_dup = database.utxo.block_inputs(
+            in_keys, in_start, out_amount, out_start, TAG_BY_TABLE['unspent_outputs'])
     if n_dup:
         return None
     in_tag = None
@@ -301,7 +312,7 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         in_tag, bad, fee = bg.inputs(TAG_BY_TABLE, tags, pay, fee, out_amount)
         if bad:
             return None
-    elif np.any(missing):
+    elif missing is not None and np.any(missing):
         return None
     in_amount = pay['amount']
     if (n_in and in_amount.max() >= AMOUNT_LIMIT) or (len(out_amount) and out_amount.max() >= AMOUNT_LIMIT):
@@ -349,9 +360,16 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
             ov_addr[k, :len(r)] = np.frombuffer(r, np.uint8)
         over = {'over_idx': np.fromiter(signers.keys(), dtype=np.int64, count=len(signers)), 'over_addr': ov_addr,
                 'over_len': np.fromiter(map(len, raws), dtype=np.uint8, count=len(raws))}
-    kst, rec_bytes = lib().block_signer_records(
-        np.ascontiguousarray(pay['addr']), pay['len'].astype(np.uint8), out_addr, out_len,
-        job_input.astype(np.int64), sigs, sig_ids.astype(np.int64), digest, job_tx.astype(np.int64), gpu_min, **over)
+    pre_status = None
+    if page is not None and not signers and page.n_jobs == n_jobs:
+        # the page verified this block's signatures in its one batch, with these very keys (and checked every
+        # output address of the page on the curve)
+        kst, rec_bytes, pre_status = 1, page.recs, page.status
+    else:
+        kst, rec_bytes = lib().block_signer_records(
+            np.ascontiguousarray(pay['addr']), pay['len'].astype(np.uint8), out_addr, out_len,
+            job_input.astype(np.int64), sigs, sig_ids.astype(np.int64), digest, job_tx.astype(np.int64), gpu_min,
+            **over)
     if kst == 0:  # a signer key or an output address is off-curve: the object path decides
         return None
     if kst < 0:
@@ -376,7 +394,7 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     if np.any(fee < 0):
         return None
     vfut = _verify_pool().submit(validate._verify, rec_bytes, None) \
-        if n_jobs and validate.overlappable(n_jobs) else None
+        if n_jobs and pre_status is None and validate.overlappable(n_jobs) else None
     try:
         # ---- columns for the ledger writes: views of the codec's buffers, encoded natively into one journal
         #      batch by csrc/ledger_writer.cpp (tx hashes rendered from the raw digests, text arenas for strings)
@@ -397,10 +415,16 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
                         'in_str': in_str[2:]}
         strings_s = perf_counter() - ts0
         roctx.pop()
-    finally:
-        # the verify's verdict (and, on an exception above, its end: no launch outlives this block)
-        status = (vfut.result() if vfut is not None else
-                  validate._verify(rec_bytes, None) if n_jobs else np.zeros(0, np.uint8)).copy()
+    except BaseException:
+        # no launch outlives this block, but the first error is the one that propagates: a failure of the
+        # overlapped verify must not replace the apply-columns error being raised here
+        if vfut is not None:
+            from concurrent.futures import wait
+            wait([vfut])
+        raise
+    # the verify's verdict
+    status = (pre_status if pre_status is not None else vfut.result() if vfut is not None else
+              validate._verify(rec_bytes, None) if n_jobs else np.zeros(0, np.uint8)).copy()
     retry = np.nonzero(status == op.INVALID)[0]
     if len(retry):
         signed_len = _i32(d, 'signed_len')

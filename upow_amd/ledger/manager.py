@@ -527,6 +527,8 @@ async def _finalize_block(block_no: int, block_content: str, fees, n_txs: int, a
         roctx.pop()
         return False
     roctx.pop()
+    if not _commit_gate():
+        return False
     if not await apply(block_hash, address, random, block_reward, content_time, coinbase_transaction):
         return False
     roctx.push('finalize:post')
@@ -544,6 +546,13 @@ async def _finalize_block(block_no: int, block_content: str, fees, n_txs: int, a
         logger.error(f'Error in creating block: {block_no} {str(e)}')
     roctx.pop()
     return True
+
+
+def _commit_gate() -> bool:
+    """On a multi-GPU cluster node: every replica agrees to commit this block before any of them writes it
+    (parallel/cluster.py ``commit_gate``); always True on a single node."""
+    from ..parallel import cluster
+    return cluster.commit_gate()
 
 
 _K12_POOL = None
@@ -625,6 +634,8 @@ async def _finalize_sync_block(block_no: int, block_content: str, fees, n_txs: i
     previous_hash, address, merkle_tree, content_time, content_difficulty, random = split_block_content(block_content)
     block_reward = get_block_reward(block_no)
     if cb_transaction is None or not all(o.verify() for o in cb_transaction.outputs):
+        return False
+    if not _commit_gate():
         return False
     if not await apply(block_hash, address, random, block_reward, content_time, cb_transaction):
         return False

@@ -101,14 +101,14 @@ class MempoolIndex:
     def confirm_raw(self, txids: np.ndarray, in_keys: np.ndarray, after: Optional[int] = None, on_hits=None):
         """A committed block's txs (n x 32) and spent outpoints (n x >=36 records) leave the mempool;
         returns the raw tx hashes and outpoints that were in it (and those admitted after ``after``).
-        ``on_hits(hit_tx, hit_in)`` runs under ``lock`` right after the removal (cluster replication)."""
+        ``on_hits(index, hit_tx, hit_in)`` runs under ``lock`` right after the removal (cluster replication)."""
         t = np.ascontiguousarray(np.asarray(txids, dtype=np.uint8).reshape(-1, 32))
         k = np.asarray(in_keys, dtype=np.uint8)
         k = np.ascontiguousarray(k.reshape(-1, k.shape[-1] if k.ndim == 2 and k.shape[0] else 40))
         with self.lock:
             res = self.core.confirm_raw(t, k, after)
             if on_hits is not None and (res[0] or res[1]):
-                on_hits(res[0], res[1])
+                on_hits(self, res[0], res[1])
             return res
 
     def confirm(self, tx_hashes: List[str], inputs: List[Tuple[str, int]], after: Optional[int] = None, on_hits=None):

@@ -1,0 +1,413 @@
+"""Page-batched chain sync: a ``/get_blocks`` page validated as one batch, applied block by block.
+
+reference: ``create_blocks`` (upow/node/main.py:97-150) applies a page of up to 1,000 blocks one after
+another, each through ``create_block_in_syncing_old`` → ``check_block`` (upow/manager.py:422-647,
+760-835): every block pays its own UTXO round trips and verifies its signatures one at a time
+(manager.py:628-632). Mainnet blocks are small (1-200 txs), so on the GPU path of ``ledger/fastpath.py``
+each block would pay the verify kernel's ~1.2 ms latency floor for a handful of signatures, plus a device
+round trip per UTXO pass and per index update.
+
+Here a page is cut into chunks of ``CHUNK`` blocks (default 128). For each chunk:
+
+  1. decode (csrc/txcodec.cpp) — on a helper thread, while the previous chunk is being applied;
+  2. a *plan* over the whole chunk (:func:`build_plan`): ONE HBM lookup of every input of the chunk, then
+     each input is resolved either from that pre-chunk index or from the outputs of an earlier block of the
+     chunk (its payload computed exactly as the apply will insert it), checked unique across the chunk, and
+     every signature of every eligible block is verified in ONE batched launch (on a multi-GPU cluster node
+     each rank verifies a contiguous shard, then one all-gather of status bytes: ``parallel/verify_dp.py``).
+     Signature validity depends on the state only through the signer key, the address of the spent output,
+     which is immutable once created; the plan resolves it before any block of the chunk is applied;
+  3. the blocks are applied in order through the ordinary native path with the plan's UTXO pass and
+     verdicts (``fastpath.create_block_from_hex(page=...)``): header, difficulty, fees, merkle, coinbase and
+     the ledger writes are per block as before. The HBM index writes of the page are deferred
+     (``UtxoIndex.defer_block``) and reach the device as one insert and one erase launch;
+  4. durability is one journal fdatasync for the whole page (``Database.group_commit``): a crash loses at
+     most the unsynced tail of the page, and the node fetches it again after the restart (it resumes at its
+     last durable block, like any sync).
+
+A block the plan cannot vouch for — governance txs, an input it cannot resolve, a double spend, an
+off-curve key, an undecodable tx — takes the ordinary per-block path (``page=None``), which settles the
+deferred index writes first and reproduces the reference's verdict exactly. After a block whose effects the
+plan did not model (the object path), the rest of the chunk is planned again against the settled index.
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+from dataclasses import dataclass
+from time import perf_counter
+from typing import List, Optional
+
+import numpy as np
+
+from ..ops import p256 as op
+from ..ops.native import gpu_available, lib
+from ..utils.codec import OutputType, TransactionType
+from ..utils.logger import get_logger
+from .utxo import MISSING, PAYLOAD_DTYPE, TAG_BY_TABLE, make_payload, pack_records
+
+logger = get_logger(__name__)
+
+ENABLED = os.environ.get('UPOW_PAGE_SYNC', '1') != '0'
+CHUNK = max(1, int(os.environ.get('UPOW_SYNC_CHUNK', '128')))
+TAG_U = TAG_BY_TABLE['unspent_outputs']
+_REVOKE = (int(TransactionType.REVOKE_AS_VALIDATOR), int(TransactionType.REVOKE_AS_DELEGATE))
+_HASH_MUL = np.uint64(0x9E3779B97F4A7C15)
+stats: dict = {}  # last page: blocks by path, plans, signatures (bench, /metrics)
+
+
+@dataclass
+class PageBlock:
+    """One block's share of a chunk plan: its inputs' table tags and payloads (as the HBM UTXO pass would
+    return them at this block), per-tx fees, and its verify records with their precomputed statuses."""
+    tags: np.ndarray
+    pay: np.ndarray
+    fee: np.ndarray
+    n_jobs: int
+    recs: bytes
+    status: np.ndarray
+
+
+@dataclass
+class Item:
+    block: dict  # the /get_blocks entry's block row (id, hash, content, ...)
+    all_hexes: list  # every tx of the entry, coinbase included
+    hexes: list  # the txs without the trusted coinbase
+    cb_hex: Optional[str]  # the coinbase candidate's hex (flag 3), parsed on the ledger thread
+    dec: Optional[dict]  # fastpath.decode(hexes), None when the block needs the object path
+
+
+def _i32(d, k):
+    return np.frombuffer(d[k], dtype=np.int32)
+
+
+def _coinbase_index(hexes: List[str]) -> Optional[int]:
+    """The first tx the codec flags as a coinbase (specifier 36). A coinbase's specifier is its last byte, so
+    only txs whose hex ends in 24 are decoded to ask."""
+    L = lib()
+    for k, h in enumerate(hexes):
+        if h.endswith('24') and L.decode_block_txs([h], 1)['flags'][0] == 3:
+            return k
+    return None
+
+
+def prepare(info: dict) -> Item:
+    """Host-thread half of a block (no ledger state): split off the coinbase candidate, decode the rest,
+    and finish the merkle root now (the codec's workspace goes back to its pool)."""
+    from . import fastpath
+    hexes = list(info['transactions'])
+    k = _coinbase_index(hexes)
+    cb_hex = None
+    if k is not None:
+        cb_hex = hexes[k]
+        hexes = hexes[:k] + hexes[k + 1:]
+    dec = fastpath.decode(hexes, threads=1 if len(hexes) < 512 else fastpath.THREADS) if hexes else None
+    if dec is not None:
+        dec['merkle_job'].result()
+    return Item(info['block'], list(info['transactions']), hexes, cb_hex, dec)
+
+
+def _key64(keys36: np.ndarray) -> np.ndarray:
+    """A 64-bit hash of 36-byte outpoint keys (txid's first 8 bytes mixed with the index). Equal hashes are
+    always confirmed on the full key; a collision only makes a block take the ordinary path."""
+    k = np.ascontiguousarray(keys36[:, :32]).view('<u8')[:, 0]
+    idx = np.ascontiguousarray(keys36[:, 32:36]).view('<u4')[:, 0].astype(np.uint64)
+    with np.errstate(over='ignore'):
+        return k ^ (idx + np.uint64(1)) * _HASH_MUL
+
+
+def build_plan(db, items: List[Item], cbs: list, ctx=None) -> List[Optional[PageBlock]]:
+    """Plan a chunk (see the module docstring). ``cbs[k]``: block k's parsed CoinbaseTransaction (or None).
+    Returns one PageBlock per block, None for the blocks that take the ordinary path."""
+    from ..parallel.verify_dp import verify_records_dp
+    from .database import Database
+    from .govcheck import OUTPUT_TABLE
+    t0 = perf_counter()
+    n_items = len(items)
+    plan: List[Optional[PageBlock]] = [None] * n_items
+    cand = []
+    for k, it in enumerate(items):
+        d = it.dec
+        if d is None or cbs[k] is None:
+            continue
+        gov, anyg = lib().gov_block_mask(np.ascontiguousarray(d['_tx_type'], np.uint8),
+                                         np.frombuffer(d['out_type'], np.uint8), _i32(d, 'out_tx'), int(d['n']),
+                                         len(d['out_type']))
+        cand.append((k, bool(anyg)))
+    if not cand:
+        return plan
+    # ---- the chunk's inputs (block order) and outputs (block txs, then the coinbase), with payloads exactly as
+    #      the apply will insert them (output_index_records / make_payload)
+    in_keys, in_blk, out_keys, out_blk, out_tag, out_pay = [], [], [], [], [], []
+    tag_lut = np.full(256, MISSING, np.uint32)
+    for t, table in OUTPUT_TABLE.items():
+        tag_lut[t] = TAG_BY_TABLE[table]
+    for k, _ in cand:
+        d = items[k].dec
+        ik = np.frombuffer(d['in_keys'], np.uint8).reshape(-1, 40)
+        in_keys.append(ik)
+        in_blk.append(np.full(len(ik), k, np.int32))
+        out_tx, out_start = _i32(d, 'out_tx'), _i32(d, 'out_start')
+        txid = np.frombuffer(d['txid'], np.uint8).reshape(-1, 32)
+        otype = np.frombuffer(d['out_type'], np.uint8)
+        tags = tag_lut[otype]
+        rb, pb = lib().output_index_records(
+            np.ascontiguousarray(txid[out_tx]), (np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]),
+            np.ascontiguousarray(tags, np.uint32), np.frombuffer(d['out_amount'], np.uint64),
+            np.frombuffer(d['out_addr'], np.uint8), np.frombuffer(d['out_len'], np.uint8),
+            (otype == int(OutputType.STAKE)).astype(np.uint8))
+        out_keys.append(np.frombuffer(rb, np.uint8).reshape(-1, 40))
+        out_pay.append(np.frombuffer(pb, PAYLOAD_DTYPE))
+        out_tag.append(tags)
+        out_blk.append(np.full(len(out_tx), k, np.int32))
+        cbo = Database.split_outputs([cbs[k]])['unspent_outputs']
+        if cbo:
+            from .database import _addr_bytes
+            out_keys.append(pack_records([(o[0], o[1]) for o in cbo], TAG_U))
+            out_pay.append(make_payload([o[4] for o in cbo], [_addr_bytes(o[2]) for o in cbo], [bool(o[3]) for o in cbo]))
+            out_tag.append(np.full(len(cbo), TAG_U, np.uint32))
+            out_blk.append(np.full(len(cbo), k, np.int32))
+    IK = np.ascontiguousarray(np.concatenate(in_keys))
+    BI = np.concatenate(in_blk)
+    OK_ = np.ascontiguousarray(np.concatenate(out_keys))
+    OB = np.concatenate(out_blk)
+    OT = np.concatenate(out_tag)
+    OP = np.concatenate(out_pay)
+    ni = len(IK)
+    # ---- 1. the pre-chunk index: one lookup launch for every input
+    tags_h, pay_h = db.utxo.lookup_records(IK) if ni else (np.zeros(0, np.uint8), np.zeros(0, PAYLOAD_DTYPE))
+    tags = np.asarray(tags_h, np.uint32).copy()
+    pay = np.array(pay_h, dtype=PAYLOAD_DTYPE)
+    hit = (tags != MISSING) & (pay['len'] > 0)
+    bad = np.zeros(ni, bool)
+    # ---- 2. the rest from the chunk's own outputs, created by an EARLIER block
+    miss = np.nonzero(~hit)[0]
+    if len(miss) and len(OK_):
+        ok64 = _key64(OK_)
+        order = np.argsort(ok64, kind='stable')
+        s64 = ok64[order]
+        q = _key64(IK[miss])
+        lo = np.searchsorted(s64, q, 'left')
+        hi = np.searchsorted(s64, q, 'right')
+        one = (hi - lo) == 1
+        pos = order[np.minimum(lo, len(order) - 1)]
+        same = one & np.all(OK_[pos, :36] == IK[miss, :36], axis=1)
+        earlier = OB[pos] < BI[miss]
+        res = same & earlier
+        r = miss[res]
+        tags[r] = OT[pos[res]]
+        pay[r] = OP[pos[res]]
+        hit[r] = True
+        bad[miss[(hi - lo) > 1]] = True  # a hash collision among the outputs: no claim either way
+    # ---- 3. every outpoint spent once in the chunk (a second spend is a double spend at its block)
+    if ni > 1:
+        k64 = _key64(IK)
+        order = np.argsort(k64, kind='stable')  # stable: equal keys keep chunk order
+        s = k64[order]
+        eq = np.nonzero(s[1:] == s[:-1])[0]
+        if len(eq):
+            a, b = order[eq], order[eq + 1]
+            bad[a] |= True  # conservative: both sides of a repeated (or colliding) key take the ordinary path
+            bad[b] |= True
+    ok_in = hit & ~bad & (tags == TAG_U)
+    # ---- 4. eligible blocks: plain (no governance txs or outputs), every input resolved, live and unique
+    starts = {}
+    pos0 = 0
+    for k, _ in cand:
+        n_in = len(np.frombuffer(items[k].dec['in_keys'], np.uint8)) // 40
+        starts[k] = (pos0, pos0 + n_in)
+        pos0 += n_in
+    elig = [k for k, anyg in cand if not anyg and bool(np.all(ok_in[starts[k][0]:starts[k][1]]))]
+    if not elig:
+        _record(t0, len(cand), 0, 0)
+        return plan
+    # ---- 5. the eligible blocks' signature jobs, records and ONE verify
+    pa, pl, oa, ol, ji, sg, sid, dg, jt, per = [], [], [], [], [], [], [], [], [], []
+    in_base = tx_base = sig_base = job_base = 0
+    fees = {}
+    keep = []
+    for k in elig:
+        d = items[k].dec
+        a, b = starts[k]
+        bpay = pay[a:b]
+        in_start, out_start = _i32(d, 'in_start'), _i32(d, 'out_start')
+        job_input = _i32(d, 'sig_first_in').astype(np.int64)
+        grouped = np.nonzero(np.frombuffer(d['grouped'], dtype=np.uint8))[0] if 'grouped' in d else ()
+        if len(grouped):
+            from .fastpath import _resolve_groups
+            job_input = _resolve_groups(grouped, job_input, bpay, in_start, _i32(d, 'sig_start'), d['_tx_type'])
+            if job_input is None:
+                continue
+        n_tx = int(d['n'])
+        in_tx = _i32(d, 'in_tx')
+        amt_in = bpay['amount'].astype(np.int64)
+        amt_out = np.frombuffer(d['out_amount'], np.uint64).astype(np.int64)
+        cs_in = np.concatenate([[0], np.cumsum(amt_in)])
+        cs_out = np.concatenate([[0], np.cumsum(amt_out)])
+        fees[k] = (cs_in[in_start[1:]] - cs_in[in_start[:-1]]) - (cs_out[out_start[1:]] - cs_out[out_start[:-1]])
+        nj = len(job_input)
+        pa.append(np.ascontiguousarray(bpay['addr']))
+        pl.append(bpay['len'].astype(np.uint8))
+        oa.append(np.frombuffer(d['out_addr'], np.uint8).reshape(-1, 64))
+        ol.append(np.frombuffer(d['out_len'], np.uint8))
+        ji.append(in_base + job_input)
+        jt.append(tx_base + in_tx[job_input].astype(np.int64))
+        sg.append(np.frombuffer(d['sigs'], np.uint8).reshape(-1, 64))
+        sid.append(sig_base + np.arange(nj, dtype=np.int64))
+        dg.append(np.frombuffer(d['digest'], np.uint8).reshape(-1, 32))
+        per.append((k, job_base, job_base + nj, a, b))
+        keep.append(k)
+        in_base += b - a
+        tx_base += n_tx
+        sig_base += len(sg[-1])
+        job_base += nj
+    if not keep:
+        _record(t0, len(cand), 0, 0)
+        return plan
+    gpu_min = op.GPU_MIN_BATCH if gpu_available() else 1 << 62
+    kst, rec_bytes = lib().block_signer_records(
+        np.ascontiguousarray(np.concatenate(pa)), np.concatenate(pl), np.ascontiguousarray(np.concatenate(oa)),
+        np.concatenate(ol), np.concatenate(ji), np.ascontiguousarray(np.concatenate(sg)), np.concatenate(sid),
+        np.ascontiguousarray(np.concatenate(dg)), np.concatenate(jt), gpu_min)
+    n_jobs = job_base
+    if ctx is not None and ctx.is_distributed:
+        # every replica planned the same chunk from the same state; a difference would desynchronise the
+        # sharded verify below, so it is checked (one 16-byte all-reduce per chunk) before anything is shared
+        lo_hi = ctx.allreduce_min_vec([n_jobs * 4 + (kst + 1), -(n_jobs * 4 + (kst + 1))])
+        if lo_hi[0] != -lo_hi[1]:
+            raise RuntimeError(f'page plan differs across cluster replicas ({n_jobs} jobs, kst {kst} here)')
+    if kst != 1:  # an off-curve key or a 64-byte address among the chunk's keys: the ordinary path decides
+        _record(t0, len(cand), 0, n_jobs)
+        return plan
+    recs = np.frombuffer(rec_bytes, np.uint8).reshape(-1, 160)
+    tv = perf_counter()
+    if n_jobs == 0:
+        status = np.zeros(0, np.uint8)
+    elif ctx is not None and ctx.is_distributed:
+        status = verify_records_dp(ctx, recs.reshape(-1))
+    else:
+        status = op.verify_records(recs.reshape(-1))
+    verify_s = perf_counter() - tv
+    tags_u = np.full(ni, TAG_U, np.uint8)
+    for k, j0, j1, a, b in per:
+        plan[k] = PageBlock(tags=tags_u[a:b], pay=pay[a:b], fee=fees[k], n_jobs=j1 - j0,
+                            recs=recs[j0:j1].tobytes(), status=np.asarray(status[j0:j1], np.uint8))
+    _record(t0, len(cand), len(keep), n_jobs, verify_s)
+    return plan
+
+
+def _record(t0: float, cand: int, planned: int, sigs: int, verify_s: float = 0.0):
+    stats['plans'] = stats.get('plans', 0) + 1
+    stats['planned_blocks'] = stats.get('planned_blocks', 0) + planned
+    stats['candidate_blocks'] = stats.get('candidate_blocks', 0) + cand
+    stats['plan_signatures'] = stats.get('plan_signatures', 0) + sigs
+    stats['plan_s'] = stats.get('plan_s', 0.0) + (perf_counter() - t0)
+    stats['plan_verify_s'] = stats.get('plan_verify_s', 0.0) + verify_s
+
+
+_POOL = None
+
+
+def _pool():
+    global _POOL
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix='upow-page-decode')
+    return _POOL
+
+
+def _prepare_chunk(infos: List[dict]) -> List[Item]:
+    return [prepare(i) for i in infos]
+
+
+async def create_blocks(blocks: list, error_list: list = None, mirror: bool = True) -> bool:
+    """node/main.py ``create_blocks`` (reference main.py:97-150) for a whole page; see the module docstring.
+    On a cluster leader the page goes to the followers first as ONE 'page' op; every rank then runs this same
+    procedure (its chunk plans sharding the signatures over the GPUs, every block agreed before it commits)."""
+    from ..models.transaction import CoinbaseTransaction, Transaction
+    from ..models.block import block_to_bytes, get_transactions_merkle_tree
+    from ..parallel import cluster
+    from . import fastpath, manager
+    from .database import Database
+    from ..constants import GENESIS_PREV_HASH
+    if error_list is None:
+        error_list = []
+    c = cluster.get()
+    ctx = None
+    if c is not None and not c.replaying:
+        ctx = c.op_ctx
+        if c.leader and mirror:
+            cluster.flush_txs()
+            c.send_page(blocks)
+    db: Database = Database.instance
+    _, last_block = await manager.calculate_difficulty()
+    last_block['id'] = last_block['id'] if last_block != {} else 0
+    last_block['hash'] = last_block['hash'] if 'hash' in last_block else GENESIS_PREV_HASH
+    i = last_block['id'] + 1
+    loop = asyncio.get_running_loop()
+    pool = _pool()
+    chunks = [blocks[a:a + CHUNK] for a in range(0, len(blocks), CHUNK)]
+    ahead = loop.run_in_executor(pool, _prepare_chunk, chunks[0]) if chunks else None
+    page_stats = {'blocks': 0, 'page_path': 0, 'ordinary_path': 0, 'replans': 0}
+    db.group_commit += 1
+    db.utxo_defer = True
+    try:
+        for ci in range(len(chunks)):
+            items = await ahead
+            ahead = loop.run_in_executor(pool, _prepare_chunk, chunks[ci + 1]) if ci + 1 < len(chunks) else None
+            cbs = []
+            for it in items:
+                cb = None
+                if it.cb_hex is not None:
+                    cand = await Transaction.from_hex(it.cb_hex)
+                    if isinstance(cand, CoinbaseTransaction):
+                        cb = cand
+                    else:  # not what the scan assumed: the whole block goes through the ordinary decode
+                        it.hexes = list(it.all_hexes)
+                        it.dec = None
+                cbs.append(cb)
+            plan = build_plan(db, items, cbs, ctx)
+            k = 0
+            while k < len(items):
+                it = items[k]
+                block = it.block
+                block_content = block.get('content')
+                if not block_content:
+                    txs = [await Transaction.from_hex(h) for h in it.hexes]
+                    block['merkle_tree'] = get_transactions_merkle_tree([tx.hex() for tx in txs])
+                    block_content = block_to_bytes(last_block['hash'], block)
+                assert i == block['id'], (i, block['id'])
+                pb = plan[k]
+                if not await fastpath.create_block_from_hex(
+                        block_content.hex() if isinstance(block_content, bytes) else block_content, it.hexes,
+                        error_list=error_list, last_block=last_block, coinbase=cbs[k], mirror=False, decoded=it.dec,
+                        page=pb):
+                    return False
+                page_stats['blocks'] += 1
+                used = pb is not None and fastpath.last_path == 'native'
+                page_stats['page_path' if used else 'ordinary_path'] += 1
+                last_block = block
+                i += 1
+                k += 1
+                if not used and (it.dec is None or fastpath.last_path != 'native') and k < len(items):
+                    # the object path applied this block: its effects are not what the plan modelled, so the
+                    # rest of the chunk is planned again against the settled index
+                    page_stats['replans'] += 1
+                    rest = build_plan(db, items[k:], cbs[k:], ctx)
+                    plan = plan[:k] + rest
+        return True
+    finally:
+        if ahead is not None:  # a failed page: let the helper thread's decode finish before returning
+            try:
+                await ahead
+            except Exception:
+                pass
+        db.utxo_defer = False
+        db.group_commit -= 1
+        db.utxo.settle()
+        if db.group_commit == 0:
+            db.wait_durable(force=True)  # the page's one fdatasync
+        stats.update(page_stats)
+
+
+__all__ = ['ENABLED', 'CHUNK', 'PageBlock', 'build_plan', 'create_blocks', 'prepare', 'stats']

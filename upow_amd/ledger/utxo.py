@@ -13,6 +13,7 @@ index is rebuilt from them after a rollback.
 """
 from __future__ import annotations
 
+import functools
 import os
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
@@ -274,12 +275,13 @@ def default_backend() -> str:
 
 
 def _locked(fn):
-    """One index, two threads (ledger worker + HTTP loop): every backend operation under one lock."""
-    import functools
-
+    """Run under the index lock, after any deferred writes (:meth:`UtxoIndex.defer_block`) reached the
+    backend: every read and every direct write sees the index as the committed blocks left it."""
     @functools.wraps(fn)
     def wrapper(self, *args, **kwargs):
         with self.lock:
+            if self._pend_ins or self._pend_del:
+                self._apply_pending()
             return fn(self, *args, **kwargs)
     return wrapper
 
@@ -291,6 +293,41 @@ class UtxoIndex:
         self.backend_name = backend or default_backend()
         self.be = _GpuBackend() if self.backend_name == 'gpu' else _HostBackend()
         self.duplicates = 0  # inserts of an outpoint that was already live (skipped; a ledger bug if ever > 0)
+        # deferred writes of committed blocks (a sync page's blocks, ledger/pagesync.py): applied as ONE insert
+        # launch and ONE erase launch before anything else touches the index
+        self._pend_ins: List[Tuple[np.ndarray, Optional[np.ndarray]]] = []
+        self._pend_del: List[np.ndarray] = []
+        self.deferred_flushes = 0
+
+    def defer_block(self, ins: Sequence[Tuple[np.ndarray, Optional[np.ndarray]]], spent: np.ndarray):
+        """Record one committed block's index writes (created-output records + payloads, spent records)
+        without touching the backend. Applying every deferred insert, then every deferred erase, equals
+        applying the blocks in order: an outpoint is created at most once, spent at most once, and only
+        after its creation (the page plan checks both before a block takes this path)."""
+        with self.lock:
+            for recs, pay in ins:
+                if len(recs):
+                    self._pend_ins.append((recs, pay))
+            if len(spent):
+                self._pend_del.append(spent)
+
+    def settle(self):
+        """Apply the deferred writes now (no-op when there are none)."""
+        with self.lock:
+            if self._pend_ins or self._pend_del:
+                self._apply_pending()
+
+    def _apply_pending(self):
+        ins, dels = self._pend_ins, self._pend_del
+        self._pend_ins, self._pend_del = [], []
+        self.deferred_flushes += 1
+        if ins:
+            recs = np.ascontiguousarray(np.concatenate([r for r, _ in ins]))
+            pays = [p for _, p in ins]
+            pay = None if any(p is None for p in pays) else np.ascontiguousarray(np.concatenate(pays))
+            self._insert_records(recs, pay)
+        if dels:
+            self._erase_records(np.ascontiguousarray(np.concatenate(dels)))
 
     def _dups(self, n: int):
         if n:
@@ -311,6 +348,9 @@ class UtxoIndex:
     @_locked
     def insert_records(self, recs: np.ndarray, payload: Optional[np.ndarray] = None):
         """Insert packed 40-byte key records (tags inside) — the block fast path's form."""
+        self._insert_records(recs, payload)
+
+    def _insert_records(self, recs: np.ndarray, payload: Optional[np.ndarray] = None):
         if isinstance(self.be, _GpuBackend):
             self._dups(self.be.insert_records(recs, payload))
             return
@@ -333,6 +373,9 @@ class UtxoIndex:
 
     @_locked
     def erase_records(self, recs: np.ndarray) -> np.ndarray:
+        return self._erase_records(recs)
+
+    def _erase_records(self, recs: np.ndarray) -> np.ndarray:
         if isinstance(self.be, _GpuBackend):
             if not len(recs):
                 return np.zeros(0, dtype=np.uint8)
@@ -462,6 +505,7 @@ class UtxoIndex:
         """K12 at this block, computed later: returns a callable giving the hex digest (the same value
         :meth:`set_hash` gives now). GPU backend: the snapshot is one compaction launch on the node stream;
         the callable (meant for a worker thread) sorts, gathers and hashes on the aux stream."""
+        self.settle()
         if isinstance(self.be, _GpuBackend):
             L, sid = self.be.L, self.be.L.utxo_k12_snapshot(self.be.h, tag)
             return lambda: L.utxo_k12_digest(sid)[0].hex()
@@ -477,6 +521,7 @@ class UtxoIndex:
         return hashlib.sha256(self.set_message(tag)).hexdigest()
 
     def __len__(self):
+        self.settle()
         return len(self.be)
 
 

@@ -103,6 +103,11 @@ def _run_cluster(a):
     from ..parallel import cluster
     from ..parallel.dist import init_from_env, op_context, shutdown
     lib()  # the extension binds to torch's HIP runtime before the process group exists
+    # a replica's block submit may wait on its SQL materialisers (writer backpressure); that wait must stay well
+    # inside the op group's collective timeout, or a slow disk would end the whole cluster (parallel/dist.py)
+    op_timeout = float(os.environ.setdefault('UPOW_DIST_TIMEOUT_S', '120'))
+    throttle = float(os.environ.get('UPOW_WRITER_THROTTLE_TIMEOUT', '300'))
+    os.environ['UPOW_WRITER_THROTTLE_TIMEOUT'] = str(min(throttle, op_timeout / 4))
     ctx = init_from_env()
     c = cluster.init(op_context(ctx), ctx)  # op traffic on a short-timeout group, start-up on the default one
     try:

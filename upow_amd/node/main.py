@@ -38,7 +38,7 @@ from .. import config
 from ..constants import ENDIAN, GENESIS_PREV_HASH, MAX_SUPPLY, VERSION
 from ..ledger import manager as mgr
 from ..ledger.database import Database, UniqueViolationError
-from ..ledger import fastpath
+from ..ledger import fastpath, pagesync
 from ..ledger.fastpath import create_block_from_hex
 from ..ledger import worker as ledger_worker
 from ..ledger.worker import on_ledger
@@ -260,6 +260,15 @@ def _sync_decoder():
 
 
 async def create_blocks(blocks: list, error_list=None) -> bool:
+    """main.py:97-150 for a /get_blocks page: page-batched (ledger/pagesync.py: one UTXO lookup and one
+    signature batch per chunk of blocks, deferred index writes, one fdatasync per page), or per block with
+    ``UPOW_PAGE_SYNC=0``."""
+    if pagesync.ENABLED:
+        return await pagesync.create_blocks(blocks, error_list)
+    return await create_blocks_per_block(blocks, error_list)
+
+
+async def create_blocks_per_block(blocks: list, error_list=None) -> bool:
     """main.py:97-150, as a two-stage pipeline: while block k is validated and applied on the event
     loop (GPU passes + ledger writes, GIL released in the native parts), block k+1 is already being
     decoded on a host thread (``_scan_sync_block``: txids, canonical bytes, addresses, merkle)."""
@@ -949,7 +958,7 @@ async def cluster_info(deep: bool = False):
     if c is None:
         return {'ok': True, 'result': {'world': 1, 'replicas': replicas}}
     return {'ok': True, 'result': {'world': c.ctx.world, 'backend': c.ctx.backend, 'replicas': replicas,
-                                   'last_resync': c.last_resync, 'ops_sent': c.ops_sent}}
+                                   'last_resync': c.last_resync, 'ops_sent': c.ops_sent, 'op_stream': c.info()}}
 
 
 @app.get('/metrics')

@@ -17,11 +17,27 @@ starts G ranks:
                 reserved inputs) replicated as they were ADMITTED on the leader: followers insert them
                 without re-verifying (the leader already did), in one native index pass + one journal batch
       block     a block to validate + apply (push or sync form, tx hex + optional coinbase)
+      page      a sync page: every block row and tx of a /get_blocks page (ledger/pagesync.py)
       gc        mempool garbage collection
       rollback / delete   fork handling (remove_blocks / delete_blocks)
       status    all-gather of every replica's (height, tip hash, UTXO-set K12 hash from the index)
       ping      idle heartbeat (keeps followers inside the op group's collective timeout)
       quit
+
+Framing. An op is ONE fixed-capacity broadcast when it fits in 64 KB (everything but blocks and sync
+pages), two otherwise (``DistContext.broadcast_frame``); mempool rows travel packed in binary.
+
+Start-up resync runs on the long-timeout group (``init_ctx``): a replay of a long chain can outlast the op
+timeout, and every ``ACK_EVERY`` replayed blocks the leader and the followers meet in an all-reduce that
+also carries each follower's success, so no broadcast stays queued for long and a follower that cannot
+apply the leader's chain stops the resync instead of hanging it.
+
+Agree before commit. A block (push or sync form) is validated on every replica; right before its ledger
+writes each replica votes in one all-reduce (``commit_gate``, called by ``manager._finalize_*``), and
+writes only when every replica voted to. A replica that rejected the block votes no when it finishes. A
+split vote is a replica divergence: nothing was committed anywhere, and every rank exits with status 70
+(``DistContext._failed``); a relaunch resyncs the replicas from that common state. Rollbacks, chain
+deletions and mempool GC end in an all-gather of (height, tip hash, mempool size) that must agree.
 
 Ordering and threads. Every collective of a rank is issued by ONE thread (``DistContext.bind_owner``):
 the leader's ledger thread, the follower's op loop. ``/cluster_info`` and the idle heartbeat are routed
@@ -31,15 +47,19 @@ admitted on the leader while a block was being applied is edited in the outbox e
 mempool confirm edited the leader's index (its tx dropped if the block confirmed it, confirmed inputs
 stripped), so a follower that inserts it after that block ends in the leader's state.
 
-Verification. Each replica validates every block itself; an all-reduce then checks that all replicas
-reached the same verdict (a split raises: replica divergence). The signature batch is sharded across
-the ranks only from ``UPOW_CLUSTER_SHARD_MIN`` signatures up (ledger/validate.py): a 2 MB block (~8,300
-signatures) verifies in ~1.2 ms on one GPU, less than a sharded verify costs in collectives.
+Verification. Each replica validates every block itself. A single pushed block's signature batch is sharded
+across the ranks only from ``UPOW_CLUSTER_SHARD_MIN`` signatures up (ledger/validate.py): a 2 MB block
+(~8,300 signatures) verifies in ~1.2 ms on one GPU, less than a sharded verify costs in collectives. Chain
+sync sends a whole ``/get_blocks`` page as one 'page' op; every rank plans it in chunks (ledger/pagesync.py)
+whose signature batches — thousands to hundreds of thousands of signatures — ARE sharded: rank r verifies
+a contiguous shard, one all-gather of status bytes, then every replica applies the blocks in order.
 """
 from __future__ import annotations
 
+import contextvars
 import json
 import os
+import struct
 import threading
 import time
 from typing import List, Optional
@@ -52,16 +72,20 @@ logger = get_logger(__name__)
 _cluster: Optional['Cluster'] = None
 HEARTBEAT_S = float(os.environ.get('UPOW_CLUSTER_HEARTBEAT_S', '5'))
 FORK_WINDOW = 500  # remove_blocks' reach (reference database.py:146-169 pages of 500)
+ACK_EVERY = int(os.environ.get('UPOW_CLUSTER_REPLAY_ACK', '32'))  # resync: replayed blocks per acknowledgement
 
 
 class Cluster:
     def __init__(self, ctx: DistContext, init_ctx: Optional[DistContext] = None):
         self.ctx = ctx  # op traffic (short timeout group)
-        self.init_ctx = init_ctx or ctx  # start-up barrier (long timeout group)
+        self.init_ctx = init_ctx or ctx  # start-up barrier and resync (long timeout group)
+        self.op_ctx = self.ctx  # the group the op stream runs on right now (init_ctx during resync)
         self.replaying = False
         self.closed = False  # after 'quit': no op is sent again (the heartbeat stops)
         self.last_send = time.monotonic()
         self.ops_sent = 0
+        self.ops_received = 0
+        self.commits_agreed = 0
         self.last_resync: Optional[dict] = None
 
     @property
@@ -69,40 +93,139 @@ class Cluster:
         return self.ctx.rank == 0
 
     # ------------------------------------------------------------------ op stream
-    # One frame per op: u32 header length, a small JSON header, then a binary payload (a block's txs
-    # travel as raw bytes, half the size of hex and no JSON string escaping): two broadcasts per op
-    # (length, then frame) over RCCL, both from the owner thread.
+    # One frame per op: u32 header length, a small JSON header, then a binary payload (a block's txs travel as
+    # raw bytes, half the size of hex and no JSON escaping), in one fixed-capacity broadcast when it fits.
     def send(self, op: str, payload: bytes = b'', **kw):
         assert self.leader
-        head = json.dumps({'op': op, **kw}, separators=(',', ':')).encode()
-        self.ctx.broadcast_bytes(len(head).to_bytes(4, 'little') + head + payload, src=0, max_len=0)
+        head = json.dumps({'op': op, **kw}, separators=(',', ':'), default=str).encode()
+        self.op_ctx.broadcast_frame(len(head).to_bytes(4, 'little') + head + payload, src=0)
         self.last_send = time.monotonic()
         self.ops_sent += 1
 
     def recv(self) -> dict:
-        raw = self.ctx.broadcast_bytes(None, src=0, max_len=0)
+        raw = self.op_ctx.broadcast_frame(None, src=0)
         n = int.from_bytes(raw[:4], 'little')
         msg = json.loads(raw[4:4 + n].decode())
         msg['_payload'] = raw[4 + n:]
+        self.ops_received += 1
         return msg
 
+    def send_page(self, blocks: list):
+        """A /get_blocks page (block rows + every tx, coinbase included) as ONE 'page' op."""
+        rows = [b['block'] for b in blocks]
+        counts = [len(b['transactions']) for b in blocks]
+        self.send('page', pack_txs([h for b in blocks for h in b['transactions']]), rows=rows, counts=counts)
+
+    @staticmethod
+    def unpack_page(msg: dict) -> list:
+        hexes = unpack_txs(msg['_payload'])
+        out, at = [], 0
+        for row, n in zip(msg['rows'], msg['counts']):
+            out.append({'block': row, 'transactions': hexes[at:at + n]})
+            at += n
+        return out
+
     def agree(self, ok: bool, what: str) -> bool:
-        n = self.ctx.allreduce_sum(1 if ok else 0)
+        n = self.op_ctx.allreduce_sum(1 if ok else 0)
         if n not in (0, self.ctx.world):
-            raise RuntimeError(f'cluster replicas diverged on {what}: {n}/{self.ctx.world} accepted')
+            self.diverged(f'{what}: {n}/{self.ctx.world} accepted')
         return bool(ok)
+
+    def diverged(self, what: str):
+        """Replica divergence: every rank detects it in the same collective, nothing was committed past the
+        agreed state, and each rank exits (status 70; ``UPOW_DIST_FATAL=0`` raises instead)."""
+        self.ctx._failed('replica agreement', RuntimeError(f'cluster replicas diverged on {what}'))
+
+    def agree_state(self, db, what: str):
+        """After a rollback, a chain deletion or a mempool GC: every replica at the same (height, tip hash,
+        mempool size), checked in one fixed-size all-gather."""
+        tip = _tip_hash(db)
+        mine = struct.pack('<qq', db._tip_id(), _mempool_size(db)) + (bytes.fromhex(tip) if tip else bytes(32))
+        got = self.op_ctx.all_gather_fixed(mine)
+        if any(g != got[0] for g in got):
+            states = [(struct.unpack('<qq', g[:16]), g[16:].hex()[:16]) for g in got]
+            self.diverged(f'{what}: replica states {states}')
+
+    def replay_ack(self, ok: bool):
+        """Resync checkpoint (long-timeout group): the leader learns that every follower applied the replayed
+        blocks so far; a follower that failed votes 0 and the resync stops on every rank."""
+        n = self.op_ctx.allreduce_sum(1 if ok else 0)
+        if n != self.ctx.world:
+            raise RuntimeError(f'cluster resync: {self.ctx.world - n} replica(s) could not apply the leader\'s chain')
 
     def status(self, db, deep: bool = False, mempool: Optional[int] = None) -> List[dict]:
         """Collective: every rank's height, tip hash and UTXO-set hash. The hash comes from the HBM index
         (K12: compaction + radix sort on the device, host SHA tail), current at the commit point; ``deep``
-        also hashes the SQL replica after the materialisers have caught up (the slow full-table audit)."""
+        also hashes the SQL replica after the materialisers have caught up (the slow full-table audit, on
+        the long-timeout group: it may take longer than the op timeout on a big ledger)."""
         mine = {'rank': self.ctx.rank, 'height': db._tip_id(), 'tip_hash': _tip_hash(db),
                 'utxo_hash': db.utxo.set_hash(_utxo_tag()), 'utxo_entries': len(db.utxo),
                 'mempool': _mempool_size(db) if mempool is None else mempool}
         if deep:
             db.flush()
             mine['sql_utxo_hash'] = db.sql_unspent_outputs_hash()
-        return [json.loads(b.decode()) for b in self.ctx.all_gather_bytes(json.dumps(mine).encode())]
+        g = self.init_ctx if deep else self.op_ctx
+        return [json.loads(b.decode()) for b in g.all_gather_bytes(json.dumps(mine).encode())]
+
+    def info(self) -> dict:
+        """Op-stream counters for /cluster_info: collectives per op (framing + agreements + replies)."""
+        ops = self.ops_sent if self.leader else self.ops_received
+        coll = self.ctx.collectives
+        return {'ops': ops, 'collectives': coll, 'collectives_per_op': round(coll / ops, 3) if ops else None,
+                'commits_agreed': self.commits_agreed}
+
+
+# ---------------------------------------------------------------------------------------------- commit gate
+_GATE: contextvars.ContextVar = contextvars.ContextVar('upow_commit_gate', default=None)
+
+
+class CommitGate:
+    """Agree-before-commit for one block on a cluster node: :meth:`vote` (True) right before the ledger
+    writes, :meth:`close` with the rank's final verdict. Exactly one all-reduce per block per rank."""
+
+    def __init__(self, c: Cluster, what: str):
+        self.c, self.what = c, what
+        self.voted: Optional[bool] = None
+        self.n = 0
+
+    def vote(self, ok: bool) -> bool:
+        """This rank is ready to commit (or not); True only when every replica is."""
+        if self.voted is not None:
+            raise RuntimeError('commit gate: a block voted twice')
+        self.voted = bool(ok)
+        self.n = self.c.op_ctx.allreduce_sum(1 if ok else 0)
+        go = self.voted and self.n == self.c.ctx.world
+        if go:
+            self.c.commits_agreed += 1
+        return go
+
+    def close(self, ok: bool) -> bool:
+        if self.voted is None:  # rejected (or failed) before reaching the commit point
+            self.vote(False)
+        world = self.c.ctx.world
+        if self.n not in (0, world):
+            self.c.diverged(f'{self.what}: {self.n}/{world} replicas ready to commit (none committed)')
+        if self.voted and self.n == world and not ok:
+            self.c.diverged(f'{self.what}: agreed, but the ledger write failed on rank {self.c.ctx.rank}')
+        return bool(ok) and self.n == world
+
+
+def open_gate(what: str = 'block'):
+    """(gate, token) for a block about to be validated; (None, token) outside an active cluster."""
+    c = _cluster
+    gate = CommitGate(c, what) if (c is not None and not c.replaying) else None
+    return gate, _GATE.set(gate)
+
+
+def close_gate(gate: Optional[CommitGate], token, ok: bool) -> bool:
+    _GATE.reset(token)
+    return gate.close(ok) if gate is not None else ok
+
+
+def commit_gate() -> bool:
+    """Called by the block paths right before their ledger writes: True when this block may commit."""
+    g = _GATE.get()
+    return True if g is None else g.vote(True)
 
 
 def _utxo_tag() -> int:
@@ -158,11 +281,51 @@ def active_leader() -> Optional[Cluster]:
 
 
 # ---------------------------------------------------------------------------------------------- leader hooks
-# Replicated mempool rows: (tx_hex, inputs_addresses JSON, fees text, propagation time, [[txid, index], ...])
+# Replicated mempool rows: (tx_hex, inputs_addresses JSON, fees text, propagation time, [[txid, index], ...],
+# tx hash hex); the hash stays on the leader (the outbox edit below), the rest travels packed in binary
 _outbox: List[list] = []
 _outbox_lock = threading.Lock()
 _flush_scheduled = False
 FLUSH_S = float(os.environ.get('UPOW_CLUSTER_TX_FLUSH_MS', '20')) / 1000.0
+
+
+def pack_rows(rows: List[list]) -> bytes:
+    """Mempool rows in binary: u32 count; per row u32 + raw tx bytes, u32 + inputs_addresses UTF-8,
+    u8 + fees text, i64 propagation time, u16 count + (32-byte txid, u16 index) per reserved input."""
+    out = bytearray(struct.pack('<I', len(rows)))
+    for row in rows:
+        raw = bytes.fromhex(row[0])
+        ia = row[1].encode()
+        fees = str(row[2]).encode()
+        out += struct.pack('<I', len(raw)) + raw + struct.pack('<I', len(ia)) + ia
+        out += struct.pack('<B', len(fees)) + fees + struct.pack('<qH', int(row[3]), len(row[4]))
+        for h, i in row[4]:
+            out += bytes.fromhex(h) + struct.pack('<H', int(i))
+    return bytes(out)
+
+
+def unpack_rows(buf: bytes) -> List[list]:
+    mv = memoryview(buf)
+    (n,), at = struct.unpack_from('<I', mv, 0), 4
+    rows = []
+    for _ in range(n):
+        (ln,) = struct.unpack_from('<I', mv, at)
+        tx_hex = mv[at + 4:at + 4 + ln].hex()
+        at += 4 + ln
+        (ln,) = struct.unpack_from('<I', mv, at)
+        ia = bytes(mv[at + 4:at + 4 + ln]).decode()
+        at += 4 + ln
+        ln = mv[at]
+        fees = bytes(mv[at + 1:at + 1 + ln]).decode()
+        at += 1 + ln
+        ptime, k = struct.unpack_from('<qH', mv, at)
+        at += 10
+        ins = []
+        for _ in range(k):
+            ins.append([mv[at:at + 32].hex(), struct.unpack_from('<H', mv, at + 32)[0]])
+            at += 34
+        rows.append([tx_hex, ia, fees, ptime, ins])
+    return rows
 
 
 def on_admit(row: list):
@@ -179,24 +342,32 @@ def on_admit(row: list):
     _on_ledger_loop(lambda loop: loop.call_later(FLUSH_S, _timed_flush), _timed_flush)
 
 
-def on_confirm(hit_tx: list, hit_in: list):
-    """Database hook (``Database.on_confirm``, under the mempool index lock): a block's confirm removed
-    ``hit_tx`` (raw tx hashes) and ``hit_in`` (raw 36-byte outpoints) from the leader's index. Rows still
-    in the outbox were admitted before that confirm, so the followers must see them as the confirm left
-    them: the confirmed tx dropped, the confirmed inputs no longer reserved."""
+def on_confirm(mp, hit_tx: list, hit_in: list):
+    """Database hook (``Database.on_confirm``, under the mempool index lock): a block's confirm just removed
+    ``hit_tx`` (raw tx hashes) and ``hit_in`` (raw 36-byte outpoints) from the leader's index ``mp``. Rows
+    still in the outbox were admitted before that confirm, so the followers must see them as the confirm left
+    them. With the index at hand that is one probe per outbox row, never a set over the block: a row whose
+    tx left the index was confirmed; of its reserved inputs, only those the index still holds stay."""
     if not _outbox:
         return
-    import hashlib
-    txs = set(hit_tx)
-    ins = {(k[:32].hex(), int.from_bytes(k[32:36], 'little')) for k in hit_in}
     with _outbox_lock:
         keep = []
-        for row in _outbox:
-            if hashlib.sha256(bytes.fromhex(row[0])).digest() in txs:
-                continue
-            if ins:
+        if mp is not None:
+            for row in _outbox:
+                if not mp.has_tx(row[5]):
+                    continue
+                if row[4]:
+                    live = {(h, int(i)) for h, i in mp.spent_of(row[4])}
+                    row[4] = [p for p in row[4] if (p[0], int(p[1])) in live]
+                keep.append(row)
+        else:  # no mempool index (its SQL form): the block's own hit lists
+            txs = set(hit_tx)
+            ins = {(k[:32].hex(), int.from_bytes(k[32:36], 'little')) for k in hit_in}
+            for row in _outbox:
+                if bytes.fromhex(row[5]) in txs:
+                    continue
                 row[4] = [p for p in row[4] if (p[0], int(p[1])) not in ins]
-            keep.append(row)
+                keep.append(row)
         _outbox[:] = keep
 
 
@@ -230,7 +401,7 @@ def flush_txs() -> int:
         _outbox.clear()
     if c is None or not rows:
         return 0
-    c.send('txs', json.dumps(rows, separators=(',', ':')).encode())
+    c.send('txs', pack_rows(rows))
     return len(rows)
 
 
@@ -247,13 +418,17 @@ def _heartbeat():
 
 
 async def mirror_gc(pending):
-    """Mempool GC on every replica (manager.clear_pending_transactions)."""
+    """Mempool GC on every replica (manager.clear_pending_transactions), then agreement on the result."""
+    from ..ledger.database import Database
     from ..ledger.manager import clear_pending_transactions
     c = active_leader()
     if c is not None:
         flush_txs()
         c.send('gc', pending=list(pending) if pending is not None else None)
-    return await clear_pending_transactions(pending)
+    res = await clear_pending_transactions(pending)
+    if c is not None:
+        c.agree_state(Database.instance, 'gc')
+    return res
 
 
 async def mirror_rollback(db, block_no: int):
@@ -262,6 +437,8 @@ async def mirror_rollback(db, block_no: int):
         flush_txs()
         c.send('rollback', n=int(block_no))
     await db.remove_blocks(block_no)
+    if c is not None:
+        c.agree_state(db, f'rollback to {block_no}')
 
 
 async def mirror_delete(db, offset: int):
@@ -270,6 +447,8 @@ async def mirror_delete(db, offset: int):
         flush_txs()
         c.send('delete', n=int(offset))
     await db.delete_blocks(offset)
+    if c is not None:
+        c.agree_state(db, f'delete from {offset}')
 
 
 async def status_all(db, deep: bool = False) -> List[dict]:
@@ -288,7 +467,7 @@ async def status_all(db, deep: bool = False) -> List[dict]:
                 _outbox.clear()
             size = len(mp)
         if rows:
-            c.send('txs', json.dumps(rows, separators=(',', ':')).encode())
+            c.send('txs', pack_rows(rows))
     else:
         flush_txs()
         size = None
@@ -324,11 +503,13 @@ async def leader_start(db):
 
 
 async def leader_resync(db) -> dict:
-    """Bring every follower to the leader's chain and mempool, sending only what each lacks."""
+    """Bring every follower to the leader's chain and mempool, sending only what each lacks. The whole resync
+    runs on the long-timeout group, acknowledged every ACK_EVERY replayed blocks."""
     from ..ledger import validate
     c = _cluster
     tip = db._tip_id()
     c.replaying = True
+    c.op_ctx = c.init_ctx
     try:
         c.send('resync')
         st = _gather_tips(c, db)
@@ -360,15 +541,20 @@ async def leader_resync(db) -> dict:
                 c.send('replay_block', pack_txs(info['transactions']), h=h, content=info['block']['content'])
                 sent += 1
                 offset = h + 1
+                if sent % ACK_EVERY == 0:
+                    c.replay_ack(True)
         flush_txs()
         c.send('mempool_reset')
         rows = _mempool_rows(db)
         for k in range(0, len(rows), 512):
-            c.send('txs', json.dumps(rows[k:k + 512], separators=(',', ':')).encode())
-        c.send('replay_end')
+            c.send('txs', pack_rows(rows[k:k + 512]))
+        c.send('replay_end', sent=sent)
+        c.replay_ack(True)
+        c.replaying = False
+        st = c.status(db)
     finally:
         c.replaying = False
-    st = c.status(db)
+        c.op_ctx = c.ctx
     if any((s['height'], s['tip_hash'], s['utxo_hash']) != (st[0]['height'], st[0]['tip_hash'], st[0]['utxo_hash'])
            for s in st):
         raise RuntimeError(f'cluster resync left diverged replicas: {st}')
@@ -387,7 +573,7 @@ def _hash_at(db, h: int) -> Optional[str]:
 
 def _gather_tips(c: Cluster, db) -> List[dict]:
     mine = json.dumps({'rank': c.ctx.rank, 'tip': db._tip_id(), 'tip_hash': _tip_hash(db)}).encode()
-    return [json.loads(b.decode()) for b in c.ctx.all_gather_bytes(mine)]
+    return [json.loads(b.decode()) for b in c.op_ctx.all_gather_bytes(mine)]
 
 
 async def leader_quit():
@@ -443,15 +629,19 @@ async def _follower_fork_window(c: Cluster, db, msg):
 
 
 async def follower_main(c: Cluster, db):
-    """Apply the leader's op stream until 'quit'."""
-    from ..ledger import fastpath, validate
+    """Apply the leader's op stream until 'quit'. The first op is the start-up resync, on the long-timeout
+    group; after 'replay_end' the stream moves to the op group."""
+    from ..ledger import fastpath, pagesync, validate
     from ..ledger.manager import clear_pending_transactions
     from ..models.transaction import Transaction
     c.init_ctx.bind_owner()
     c.ctx.bind_owner()
+    c.op_ctx = c.init_ctx
     c.init_ctx.barrier()  # the leader has opened its ledger too
     logger.info(f'cluster follower rank {c.ctx.rank}/{c.ctx.world} ready at height {db._tip_id()}')
     last_block = None
+    replayed = 0
+    replay_error = None
     while True:
         msg = c.recv()
         op = msg['op']
@@ -463,24 +653,33 @@ async def follower_main(c: Cluster, db):
             c.replaying = True  # local verification, no agreement collectives: the leader is not applying
             validate.set_dist_context(None)
             last_block = None
+            replayed = 0
+            replay_error = None
             _gather_tips(c, db)
         elif op == 'fork_window':
             await _follower_fork_window(c, db, msg)
             _gather_tips(c, db)
         elif op == 'replay_block':
-            if int(msg['h']) <= db._tip_id():
-                continue  # this replica already holds it (same chain: checked by resync)
-            hexes, cb = await _split_coinbase(unpack_txs(msg['_payload']))
-            ok = await fastpath.create_block_from_hex(msg['content'], hexes, coinbase=cb, last_block=last_block,
-                                                      mirror=False)
-            if not ok:
-                raise RuntimeError(f'cluster replay: block {msg["h"]} rejected on rank {c.ctx.rank}')
-            last_block = await db.get_last_block()
+            replayed += 1
+            if replay_error is None and int(msg['h']) > db._tip_id():  # else: this replica already holds it
+                try:
+                    hexes, cb = await _split_coinbase(unpack_txs(msg['_payload']))
+                    if not await fastpath.create_block_from_hex(msg['content'], hexes, coinbase=cb,
+                                                                last_block=last_block, mirror=False):
+                        raise RuntimeError(f'block {msg["h"]} rejected')
+                    last_block = await db.get_last_block()
+                except Exception as e:  # reported at the next acknowledgement, on every rank
+                    replay_error = e
+                    logger.error(f'cluster replay on rank {c.ctx.rank}: {e}')
+            if replayed % ACK_EVERY == 0:
+                c.replay_ack(replay_error is None)
         elif op == 'mempool_reset':
             db.clear_mempool()
         elif op == 'replay_end':
+            c.replay_ack(replay_error is None)
             c.replaying = False
             c.status(db)
+            c.op_ctx = c.ctx
             validate.set_dist_context(c.ctx)
         elif op == 'block':
             cb = None
@@ -488,14 +687,19 @@ async def follower_main(c: Cluster, db):
                 cb = await Transaction.from_hex(msg['cb'])
             # difficulty/last block come from this replica's own ledger (identical to the leader's)
             await fastpath.create_block_from_hex(msg['content'], unpack_txs(msg['_payload']), coinbase=cb, mirror=False)
+        elif op == 'page':
+            await pagesync.create_blocks(Cluster.unpack_page(msg), mirror=False)
         elif op == 'txs':
-            db.admit_replicated(json.loads(msg['_payload'].decode()))
+            db.admit_replicated(unpack_rows(msg['_payload']))
         elif op == 'gc':
             await clear_pending_transactions(msg.get('pending'))
+            c.agree_state(db, 'gc')
         elif op == 'rollback':
             await db.remove_blocks(msg['n'])
+            c.agree_state(db, f'rollback to {msg["n"]}')
         elif op == 'delete':
             await db.delete_blocks(msg['n'])
+            c.agree_state(db, f'delete from {msg["n"]}')
         elif op == 'status':
             c.status(db, bool(msg.get('deep')))
         else:  # pragma: no cover
@@ -503,5 +707,6 @@ async def follower_main(c: Cluster, db):
     logger.info(f'cluster follower rank {c.ctx.rank} stopped at height {db._tip_id()}')
 
 
-__all__ = ['Cluster', 'init', 'get', 'on_admit', 'on_confirm', 'flush_txs', 'mirror_gc', 'mirror_rollback',
-           'mirror_delete', 'status_all', 'leader_start', 'leader_resync', 'leader_quit', 'follower_main']
+__all__ = ['Cluster', 'CommitGate', 'init', 'get', 'on_admit', 'on_confirm', 'flush_txs', 'mirror_gc',
+           'mirror_rollback', 'mirror_delete', 'status_all', 'leader_start', 'leader_resync', 'leader_quit',
+           'follower_main', 'commit_gate', 'open_gate', 'close_gate', 'pack_rows', 'unpack_rows']

@@ -14,10 +14,13 @@ rank that died) must not hang the node forever:
   ledger thread, the follower's op loop). A call from any other thread raises before touching the
   communicator, so two threads can never interleave their collective sequences;
 * the cluster's op traffic runs on a process group created with a timeout (``UPOW_DIST_TIMEOUT_S``, 60 s
-  by default; the leader's idle heartbeat keeps followers inside it), and a collective that fails or times
-  out ends the process loudly with a non-zero status (``UPOW_DIST_FATAL=0`` raises instead, for tests);
-* start-up (ledger open and replica resync) uses the default group with a long timeout
-  (``UPOW_DIST_INIT_TIMEOUT_S``, 1 h).
+  by default, 120 s for a ``--cluster`` node; the leader's idle heartbeat keeps followers inside it), and a
+  collective that fails or times out ends the process loudly with a non-zero status (``UPOW_DIST_FATAL=0``
+  raises instead, for tests). Anything a rank may legitimately wait on between two ops is kept well inside
+  that timeout: the ledger writer's backpressure wait is capped at a quarter of it on cluster ranks
+  (node/__main__.py), and the full-table ``/cluster_info?deep=true`` audit gathers on the long group;
+* start-up (ledger open and replica resync, acknowledged every few replayed blocks) uses the default group
+  with a long timeout (``UPOW_DIST_INIT_TIMEOUT_S``, 1 h).
 """
 from __future__ import annotations
 
@@ -172,6 +175,73 @@ class DistContext:
         raw = bytes(buf.cpu().numpy().tobytes())
         n = int.from_bytes(raw[:4], 'little')
         return raw[4:4 + n]
+
+    FRAME_CAP = int(os.environ.get('UPOW_DIST_FRAME_KB', '64')) << 10
+
+    def broadcast_frame(self, data: Optional[bytes], src: int) -> bytes:
+        """One op frame from ``src`` in ONE fixed-capacity broadcast when it fits (``FRAME_CAP``, 64 KB: the
+        cluster's status, ping, heartbeat and mempool-batch ops), two for larger frames (a block): the first
+        carries the total length and the head of the payload, the second the exact remainder. Receivers keep
+        one device-resident frame buffer across ops (no allocation per op)."""
+        if not self.is_distributed:
+            return bytes(data or b'')
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+        cap = self.FRAME_CAP
+        me = self.rank == src
+        if me:
+            data = bytes(data or b'')
+            total = len(data)
+            head = data[:cap - 4]
+            host, slot = self._staging(cap)
+            h = host.numpy()
+            h[:4] = np.frombuffer(total.to_bytes(4, 'little'), np.uint8)
+            h[4:4 + len(head)] = np.frombuffer(head, np.uint8)
+            if self.comm_device != 'cpu':
+                buf = host[:cap].to(self.comm_device, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                slot[1] = ev
+            else:
+                buf = host[:cap].clone()
+            self._run('broadcast(frame)', dist.broadcast, buf, src=src)
+            if total > cap - 4:
+                rest = data[cap - 4:]
+                host2, slot2 = self._staging(len(rest))
+                host2.numpy()[:len(rest)] = np.frombuffer(rest, np.uint8)
+                if self.comm_device != 'cpu':
+                    buf2 = host2[:len(rest)].to(self.comm_device, non_blocking=True)
+                    ev2 = torch.cuda.Event()
+                    ev2.record()
+                    slot2[1] = ev2
+                else:
+                    buf2 = host2[:len(rest)].clone()
+                self._run('broadcast(frame tail)', dist.broadcast, buf2, src=src)
+            return data
+        buf = self.__dict__.get('_frame_rx')
+        if buf is None or buf.numel() != cap:
+            buf = torch.empty(cap, dtype=torch.uint8, device=self.comm_device)
+            self.__dict__['_frame_rx'] = buf
+        self._run('broadcast(frame)', dist.broadcast, buf, src=src)
+        raw = buf.cpu().numpy()
+        total = int.from_bytes(raw[:4].tobytes(), 'little')
+        if total <= cap - 4:
+            return raw[4:4 + total].tobytes()
+        tail = torch.empty(total - (cap - 4), dtype=torch.uint8, device=self.comm_device)
+        self._run('broadcast(frame tail)', dist.broadcast, tail, src=src)
+        return raw[4:].tobytes() + tail.cpu().numpy().tobytes()
+
+    def all_gather_fixed(self, data: bytes) -> list:
+        """All-gather of a byte string every rank sends with the SAME length: one collective."""
+        if not self.is_distributed:
+            return [bytes(data)]
+        import torch
+        import torch.distributed as dist
+        buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(self.comm_device)
+        outs = [torch.empty_like(buf) for _ in range(self.world)]
+        self._run('all_gather(fixed)', dist.all_gather, outs, buf)
+        return [o.cpu().numpy().tobytes() for o in outs]
 
     def _staging(self, n: int):
         """A pinned host buffer of at least ``n`` bytes and its slot ``[buffer, copy-done event]``, reused

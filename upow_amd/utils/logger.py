@@ -91,7 +91,10 @@ class NativeFileHandler(logging.Handler):
                     self._sec, self._stamp = sec, time.strftime('%Y-%m-%d %H:%M:%S', time.localtime(sec))
                 line = (f'{self._stamp},{int(record.msecs):03d} - {record.filename} - {record.levelname} - '
                         f'{record.getMessage()}')
-            if record.levelno >= logging.ERROR:  # written before returning: not lost if the process dies next
+            if record.levelno >= logging.CRITICAL:
+                # fatal paths (a failed collective, os._exit next): on disk before returning. ERROR lines
+                # (rejected txs and blocks, fired on the HTTP loop, possibly at a client's flood rate) stay
+                # asynchronous: a stalled disk must not stall the loop once per error
                 self.app.write_sync(line + '\n')
             else:
                 self.app.write(line + '\n')
