@@ -15,7 +15,10 @@ one process, measured in the survey sandbox — the reference publishes no numbe
 The default (mine) run then also measures the second BASELINE metric in the same process on every
 rank — tx-verify/s over 2 MB blocks (8,300 signed txs each) through the native push_block path into a
 file-backed ledger — and reports it as extra keys (``verify_tx_per_s`` aggregated over ranks,
-``ecdsa_sig_per_s``, per-block commit latency); ``--verify-steps 0`` skips it.
+``ecdsa_sig_per_s``, per-block commit latency); ``--verify-steps 0`` skips it. Then chain sync:
+``sync_tx_per_s`` of one chain of 200-tx blocks replayed from /get_blocks pages (page-batched,
+ledger/pagesync.py); with N ranks the N GPUs form one cluster node syncing that chain (``--sync-steps 0``
+skips it).
 ``--mode verify`` runs that measurement alone (default 10 blocks); ``--mode sync`` the chain-sync
 throughput of the same blocks replayed from a ``/get_blocks`` page.
 """
@@ -142,6 +145,28 @@ def _verify_side_metrics(args, ctx) -> dict:
     return out
 
 
+def _sync_side_metrics(args, ctx) -> dict:
+    """Chain sync next to the hashrate: ``--sync-steps`` 200-tx blocks (+5 warmup) replayed from /get_blocks
+    pages into a file-backed ledger (ledger/pagesync.py). With N ranks it is ONE chain synced by an N-GPU
+    cluster node (every page's signatures sharded over the GPUs, every block agreed before commit), so the
+    per-N values of the scaling runs compare one chain's sync rate at 1, 2, 4 and 8 GPUs."""
+    import shutil
+    import tempfile
+    from upow_amd.bench_verify import run_cluster_sync_bench, run_sync_bench
+    tmp = tempfile.mkdtemp(prefix='upow_bench_sync_')
+    try:
+        v = argparse.Namespace(**{**vars(args), 'steps': args.sync_steps, 'warmup': 5, 'txs': 200, 'txs_range': None,
+                                  'ledger': tmp, 'keys': 'distinct', 'age_txs': 0, 'sync_page_blocks': 1000})
+        r = run_cluster_sync_bench(v, ctx) if ctx.is_distributed else run_sync_bench(v, ctx)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return {'sync_tx_per_s': r['value'], 'sync_blocks_per_s': r.get('blocks_per_s'),
+            'sync_ms_per_block': r['ms_per_step'],
+            'sync_config': {'metric': r['metric'], 'unit': r['unit'], 'blocks': args.sync_steps, 'warmup': 5,
+                            'txs_per_block': 200, 'scaling': r['scaling'], 'layout': r['config']['parallelism'],
+                            'path': 'page', 'data': r['data']}}
+
+
 def _free_port() -> int:
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -191,6 +216,11 @@ def main(argv=None):
                     help='verify/sync modes: a fresh key pair per tx (default) or a 256-key pool (cache-friendly)')
     ap.add_argument('--verify-pool256', type=int, default=1,
                     help='mine mode: also report the 256-key-pool verify number as a labelled second value')
+    ap.add_argument('--txs-range', default=None,
+                    help='sync mode: per-block tx count uniform in LO-HI (e.g. 0-20, mainnet-shaped) instead of --txs')
+    ap.add_argument('--sync-page-blocks', type=int, default=1000, help='sync mode: blocks per /get_blocks page')
+    ap.add_argument('--sync-steps', type=int, default=500,
+                    help='mine mode: blocks of the chain-sync side measurement (200-tx blocks; 0: skip; GPU only)')
     ap.add_argument('--sync-path', choices=['page', 'block'], default='page',
                     help='sync mode: page-batched (ledger/pagesync.py, default) or the per-block pipeline (A/B)')
     ap.add_argument('--verify-steps', type=int, default=10,
@@ -232,13 +262,16 @@ def main(argv=None):
                     out.update(_verify_side_metrics(args, ctx))
                 except Exception as e:  # the headline number stands on its own; say why the extra is missing
                     out['verify_error'] = f'{type(e).__name__}: {e}'[:300]
+            if args.sync_steps > 0 and out['config']['device'] == 'gpu':
+                out.update(_sync_side_metrics(args, ctx))
         elif args.mode == 'verify':
             out = bench_verify(args, ctx)
         else:
-            from upow_amd.bench_verify import run_sync_bench
+            from upow_amd.bench_verify import run_cluster_sync_bench, run_sync_bench
             from upow_amd.ledger import pagesync
             pagesync.ENABLED = args.sync_path == 'page'
-            out = run_sync_bench(args, ctx)
+            # N ranks sync ONE chain as a cluster node (replicas + sharded page verify), not N private chains
+            out = run_cluster_sync_bench(args, ctx) if ctx.is_distributed else run_sync_bench(args, ctx)
         if ctx.is_main:
             print(json.dumps(out), flush=True)
     finally:

@@ -33,6 +33,8 @@
 #   p256n    kernel trace of quad vs oct at 1,024 / 4,096 / 8,192 / 8,300 signatures
 #   soakc1   cluster node + DP miner under torchrun, forced single-rank RCCL, 40 tx/s (node_soak.py --cluster 1)
 #   soakc1k  the same at 1,200 tx/s
+#   clustersync  page-batched sync on a forced single-rank RCCL cluster vs plain, two interleaved pairs
+#   sprofpage  rocprofv3 kernel trace + stats of the page-batched sync (200-tx blocks)
 #   bench:NAME:--a,1,...  bench.py with extra arguments (output bench_NAME.json)
 #   py:<script.py>  any extra python script under scripts/ (args after a comma: py:x.py,--a,1)
 # Every GPU step has its own time limit and the chain stops at the first failure.
@@ -232,6 +234,27 @@ for s in $STEPS; do
           || { tail -30 "$OUT/soak_$i.log"; exit 1; }
         tail -1 "$OUT/soak_$i.log" | cut -c1-600
       done ;;
+    clustersync)
+      # page-batched sync of one chain on a forced single-rank RCCL cluster node vs the plain node (A/B pair)
+      for k in 1 2; do
+        rm -rf /tmp/upow_bench_ledger
+        UPOW_FORCE_DIST=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+          --master-addr 127.0.0.1 --master-port 2954$k bench.py --gpus 1 --mode sync --txs 200 --steps 1000 --warmup 5 \
+          --ledger /tmp/upow_bench_ledger > "$OUT/sync_cluster_$k.json" 2> "$OUT/sync_cluster_$k.err" \
+          || { tail -20 "$OUT/sync_cluster_$k.err"; exit 1; }
+        grep '^{' "$OUT/sync_cluster_$k.json" | cut -c1-300
+        rm -rf /tmp/upow_bench_ledger
+        timeout -k 10 600 python bench.py --mode sync --txs 200 --steps 1000 --warmup 5 --ledger /tmp/upow_bench_ledger \
+          > "$OUT/sync_plain_$k.json" 2> "$OUT/sync_plain_$k.err" || { tail -20 "$OUT/sync_plain_$k.err"; exit 1; }
+        cut -c1-300 "$OUT/sync_plain_$k.json"
+      done ;;
+    sprofpage)
+      # rocprofv3 kernel trace of the page-batched sync (200-tx blocks)
+      rm -rf /tmp/upow_bench_ledger
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/sprofpage" -o sync -- python3 bench.py --mode sync \
+        --txs 200 --steps 1000 --warmup 5 --ledger /tmp/upow_bench_ledger > "$OUT/sprofpage.json" 2> "$OUT/sprofpage.err" \
+        || { tail -20 "$OUT/sprofpage.err"; exit 1; }
+      find "$OUT/sprofpage" -name '*kernel_stats.csv' | head -1 | xargs -r head -25 ;;
     bench:*)
       # bench:NAME:--arg,value,...  one bench.py run with extra arguments (file ledger under /tmp)
       spec=${s#bench:}; name=${spec%%:*}; rest=${spec#*:}; rest=${rest//,/ }

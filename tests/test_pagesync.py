@@ -15,6 +15,7 @@ import pytest
 
 KA, KB, KC = 0x5A1, 0x5B2, 0x5C3
 START = 1_700_000_000
+PATHS = []  # (blocks on the page path, blocks on the ordinary path) of each page synced in page mode
 
 
 def _addr(k):
@@ -119,6 +120,7 @@ async def _sync(path, pages, mode: str):
         err = []
         if mode == 'page':
             ok = await pagesync.create_blocks(page, err)
+            PATHS.append((pagesync.stats['page_path'], pagesync.stats['ordinary_path']))
         else:
             ok = await node_main.create_blocks_per_block(page, err)
         verdicts.append(ok)
@@ -168,11 +170,12 @@ def _both(tmp_path, pages):
 def test_page_sync_equals_per_block_sync(tmp_path, source_page, small_chunks):
     from upow_amd.ledger import pagesync
     pages = [source_page[:11], source_page[11:]]
+    PATHS.clear()
     a, b = _both(tmp_path, pages)
     assert a == b
     assert a[0] == [True, True] and a[2]['height'] == len(source_page)
-    # the page path carried every block (the plan vouched for all of them, grouped tx included)
-    assert pagesync.stats['ordinary_path'] == 0 and pagesync.stats['page_path'] == len(pages[1])
+    # the page path carried every block — empty ones, the genesis block and the grouped tx included
+    assert PATHS == [(len(pages[0]), 0), (len(pages[1]), 0)], PATHS
 
 
 @pytest.mark.parametrize('where', ['first', 'last', 'middle'])

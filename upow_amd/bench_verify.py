@@ -89,7 +89,8 @@ def _funding_tx(owner_addrs, amount: Decimal, rng):
 
 async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None, device=None, base_ts=None,
                  make_blocks: bool = True, ledger_path: str = None, governance: bool = False, gov_txs: float = 0.0,
-                 age_txs: int = 0, aging: dict = None, distinct_keys: bool = False, grouped_txs: float = 0.0):
+                 age_txs: int = 0, aging: dict = None, distinct_keys: bool = False, grouped_txs: float = 0.0,
+                 tx_counts: list = None):
     """``gov_txs`` > 0: that fraction of every block's txs are governance txs (70 % delegate votes, 10 %
     validator votes, 20 % delegate revokes of seeded ballots, signed by the voters) on a seeded governance
     state; the chain starts four days back so the seeded ballots are past the 48 h revoke window.
@@ -97,7 +98,10 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
     ``distinct_keys``: every plain tx slot gets its own fresh key pair (it owns the two funding outputs the
     tx spends) and pays a fresh recipient address — a 2 MB block then has ~8,300 distinct signers and
     ~16,600 distinct output addresses, as random-keypair traffic does. Default (False): a pool of 256 keys
-    signs every tx and receives every output (cache-friendly: key dedup and the base58 memo hit)."""
+    signs every tx and receives every output (cache-friendly: key dedup and the base58 memo hit).
+
+    ``tx_counts``: a tx count per block (mainnet-shaped chains: most blocks carry 0-20 txs) instead of
+    ``txs_per_block`` for every block."""
     from . import devnet
     from .ledger import manager
     from .ledger.database import Database
@@ -123,7 +127,8 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
     # funding block written straight into the ledger (trusted setup, not part of the measurement)
     # grouped txs (distinct keys only) spend two key slots each: size the funding for the extra slots
     n_grp = int(round(grouped_txs * txs_per_block)) if (grouped_txs > 0 and distinct_keys) else 0
-    n_out = n_blocks * (txs_per_block + n_grp) * 2
+    counts = list(tx_counts) if tx_counts is not None else [txs_per_block] * n_blocks
+    n_out = (sum(counts) + n_blocks * n_grp) * 2
     if distinct_keys:
         # own streams, so the funding set is identical whether or not this rank builds the blocks
         from .utils.codec import bytes_to_string
@@ -167,7 +172,7 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
         if n_gov:
             txs.extend(_governance_txs(seeded, gov_next, n_dv, n_vv, n_rv, rng))
         if distinct_keys:
-            n_plain = txs_per_block - len(txs) - n_grp
+            n_plain = counts[b] - len(txs) - n_grp
             slots = range(j, j + n_plain)
             txs.extend(signed_spend_txs([(outpoints[2 * s], outpoints[2 * s + 1]) for s in slots],
                                         [tx_keys[s] for s in slots], [tx_owner33[s] for s in slots],
@@ -184,7 +189,7 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
                 rng.shuffle(txs)
             blocks.append(txs)
             continue
-        for _ in range(txs_per_block - len(txs)):
+        for _ in range(counts[b] - len(txs)):
             (h1, i1), (h2, i2) = outpoints[2 * j], outpoints[2 * j + 1]
             owner = owners[2 * j]
             j += 1
@@ -751,11 +756,13 @@ async def _run_sync(args, ctx, device, utxo_backend):
     from .ledger import fastpath
     n_blocks = args.steps + args.warmup
     # one block per target interval (60 s, manager.py:26): long chains keep the start difficulty at every
-    # 100-block retarget, as a real chain at equilibrium does
+    # 100-block retarget, as a real chain at equilibrium does; every header is mined at the difficulty the
+    # chain computes for it, so a run of more than 100 blocks crosses retargets
     base_ts = int(time.time()) - 60 * (n_blocks + 10) - 1_000
     seed = 4321 + ctx.rank
+    counts = _tx_counts(args, n_blocks, seed)
     src, addr, blocks, _ = await _setup(n_blocks, args.txs, seed, utxo_backend, device, base_ts=base_ts,
-                                        distinct_keys=_distinct(args))
+                                        distinct_keys=_distinct(args), tx_counts=counts)
     prev = (await src.get_last_block())['hash']
     for b, txs_hex in enumerate(blocks):
         manager.Manager.difficulty = None
@@ -771,12 +778,13 @@ async def _run_sync(args, ctx, device, utxo_backend):
         part = await src.get_blocks(3 + len(page), n_blocks - len(page))
         assert part, 'source ledger returned an empty page'
         page += part
-    assert len(page) == n_blocks and all(len(p['transactions']) == args.txs + 1 for p in page)
+    assert len(page) == n_blocks and all(len(p['transactions']) == counts[b] + 1 for b, p in enumerate(page))
+    retargets = sorted({str(b['block']['difficulty']) for b in page})
     src.close()
     aging = {}
     dst, _, _, _ = await _setup(n_blocks, args.txs, seed, utxo_backend, device, base_ts=base_ts, make_blocks=False,
                                 ledger_path=_ledger_path(args, ctx), age_txs=int(getattr(args, 'age_txs', 0) or 0),
-                                aging=aging, distinct_keys=_distinct(args))
+                                aging=aging, distinct_keys=_distinct(args), tx_counts=counts)
     aging.pop('distinct_key_setup_s', None)
     dst.flush()
     Database.instance = dst
@@ -794,8 +802,11 @@ async def _run_sync(args, ctx, device, utxo_backend):
         prof.enable()
     t0 = time.perf_counter()
     errors = []
-    if not await create_blocks(page[args.warmup:], errors):
-        raise RuntimeError(f'sync rejected: {errors}')
+    per_page = max(1, int(getattr(args, 'sync_page_blocks', 1000) or 1000))  # /get_blocks returns <= 1,000
+    timed = page[args.warmup:]
+    for a in range(0, len(timed), per_page):
+        if not await create_blocks(timed[a:a + per_page], errors):
+            raise RuntimeError(f'sync rejected: {errors}')
     dst.flush()  # the SQL tables hold every block (the journal is the commit point)
     ctx.synchronize()
     ctx.barrier()
@@ -805,7 +816,9 @@ async def _run_sync(args, ctx, device, utxo_backend):
     assert (await dst.get_last_block())['hash'] == page[-1]['block']['hash']
     writer = dst.writer.stats() if dst.writer is not None else {}
     from .ledger import pagesync
-    return args.steps * args.txs, wall, fastpath.last_path, {
+    return sum(counts[args.warmup:]), wall, fastpath.last_path, {
+        'blocks_per_s': round(args.steps / wall, 1), 'tx_counts': _counts_label(args, counts[args.warmup:]),
+        'difficulties': retargets, 'blocks_per_page': per_page,
         'aged_ledger': aging or None, 'journal_rotations': writer.get('rotations'),
         'writer_throttle_s': writer.get('throttle_s'), 'undo_blocks': writer.get('undo_blocks'),
         'sync_path': 'page' if pagesync.ENABLED else 'per-block',
@@ -813,6 +826,28 @@ async def _run_sync(args, ctx, device, utxo_backend):
                  if pagesync.ENABLED else None),
         'journal_fdatasyncs': writer.get('fdatasyncs'), 'journal_group_records': writer.get('group_records'),
         'utxo_deferred_flushes': dst.utxo.deferred_flushes}
+
+
+def _sync_data_label(args) -> str:
+    rng = getattr(args, 'txs_range', None) or f'{args.txs}'
+    keys = 'a fresh random P-256 key pair per tx' if _distinct(args) else 'a 256-key pool'
+    return (f'synthetic chain of {rng}-tx blocks (2-in/2-out signed txs, {keys}), headers mined at the '
+            f'difficulty the chain computes, replayed from /get_blocks pages (coinbase included)')
+
+
+def _tx_counts(args, n_blocks: int, seed: int) -> list:
+    """Per-block tx counts: ``--txs`` for every block, or uniform in ``--txs-range LO-HI`` (seeded)."""
+    spec = getattr(args, 'txs_range', None)
+    if not spec:
+        return [args.txs] * n_blocks
+    lo, hi = (int(x) for x in str(spec).split('-'))
+    rng = random.Random(seed ^ 0x5EED)
+    return [rng.randint(lo, hi) for _ in range(n_blocks)]
+
+
+def _counts_label(args, counts) -> dict:
+    return {'range': getattr(args, 'txs_range', None) or f'{args.txs}-{args.txs}', 'total': sum(counts),
+            'mean': round(sum(counts) / max(1, len(counts)), 2), 'empty_blocks': sum(1 for c in counts if c == 0)}
 
 
 def run_sync_bench(args, ctx):
@@ -833,10 +868,116 @@ def run_sync_bench(args, ctx):
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': 'uint32',
-        'data': 'synthetic 2 MB blocks replayed from a /get_blocks page (coinbase included)',
+        'data': _sync_data_label(args),
         'config': {'model': 'upow chain sync (node.main.create_blocks, trusted coinbase)',
-                   'global_batch': total // max(1, args.steps), 'seq_len': args.txs,
+                   'global_batch': total // max(1, args.steps), 'seq_len': extra['tx_counts']['mean'],
                    'parallelism': f'dp{ctx.world}', 'device': device, 'utxo_backend': utxo_backend,
                    'block_path': path, 'ledger': 'file (WAL)' if getattr(args, 'ledger', None) else 'memory'},
+        **{k: v for k, v in extra.items() if v is not None},
+    }
+
+
+async def _run_cluster_sync(args, ctx, device, utxo_backend):
+    """Chain sync on a G-rank cluster node: ONE chain, G replicas. Rank 0 builds the source chain (untimed);
+    every rank opens an identical destination ledger (same seed: genesis + funding); the leader then syncs the
+    chain page by page through ``node.main.create_blocks`` — each page one 'page' op to the followers, every
+    chunk's signatures sharded over the G GPUs (one all-gather of status bytes), every block agreed before it
+    commits. The timed region is the leader's page loop plus a final status op that every replica answers
+    after applying the last page; the reported tx/s is the chain's."""
+    from . import devnet
+    from .ledger import manager
+    from .ledger.database import Database
+    from .models.block import get_transactions_merkle_tree
+    from .ledger import fastpath, pagesync
+    from .parallel import cluster
+    n_blocks = args.steps + args.warmup
+    base_ts = ctx.allreduce_min(int(time.time()) - 60 * (n_blocks + 10) - 1_000)
+    seed = 4321
+    counts = _tx_counts(args, n_blocks, seed)
+    page = None
+    if ctx.rank == 0:
+        src, addr, blocks, _ = await _setup(n_blocks, args.txs, seed, utxo_backend, device, base_ts=base_ts,
+                                            distinct_keys=_distinct(args), tx_counts=counts)
+        prev = (await src.get_last_block())['hash']
+        for b, txs_hex in enumerate(blocks):
+            manager.Manager.difficulty = None
+            difficulty, _ = await manager.calculate_difficulty()
+            content = devnet.mine_header_raw(prev, addr, get_transactions_merkle_tree(txs_hex),
+                                             base_ts + 60 * (b + 1), difficulty, device=device)
+            errors = []
+            if not await fastpath.create_block_from_hex(content, txs_hex, error_list=errors):
+                raise RuntimeError(f'source block rejected: {errors}')
+            prev = hashlib.sha256(bytes.fromhex(content)).hexdigest()
+        page = []
+        while len(page) < n_blocks:
+            part = await src.get_blocks(3 + len(page), n_blocks - len(page))
+            page += part
+        src.close()
+    dst, _, _, _ = await _setup(n_blocks, args.txs, seed, utxo_backend, device, base_ts=base_ts, make_blocks=False,
+                                ledger_path=_ledger_path(args, ctx), distinct_keys=_distinct(args), tx_counts=counts)
+    dst.flush()
+    Database.instance = dst
+    manager.Manager.difficulty = None
+    c = cluster.init(ctx)
+    per_page = max(1, int(getattr(args, 'sync_page_blocks', 1000) or 1000))
+    if not c.leader:
+        await cluster.follower_main(c, dst)
+        wall = ctx.allreduce_max_f(0.0)
+        st = None
+    else:
+        from .node.main import create_blocks
+        await cluster.leader_start(dst)
+        if args.warmup and not await create_blocks(page[:args.warmup]):
+            raise RuntimeError('cluster sync warmup rejected')
+        c.send('status')
+        c.status(dst)
+        t0 = time.perf_counter()
+        errors = []
+        timed = page[args.warmup:]
+        for a in range(0, len(timed), per_page):
+            if not await create_blocks(timed[a:a + per_page], errors):
+                raise RuntimeError(f'cluster sync rejected: {errors}')
+        dst.flush()
+        c.send('status')
+        st = c.status(dst)  # every replica has applied the last page when it answers
+        wall = time.perf_counter() - t0
+        await cluster.leader_quit()
+        wall = ctx.allreduce_max_f(wall)
+        if any((s['height'], s['utxo_hash']) != (st[0]['height'], st[0]['utxo_hash']) for s in st):
+            raise RuntimeError(f'cluster sync: replicas diverged: {st}')
+    info = c.info()
+    cluster.init(type(ctx)())  # a world-1 context: no cluster
+    dst.close()
+    return sum(counts[args.warmup:]), wall, {
+        'blocks_per_s': round(args.steps / wall, 1), 'tx_counts': _counts_label(args, counts[args.warmup:]),
+        'blocks_per_page': per_page, 'sync_path': 'page', 'op_stream': info,
+        'page': {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pagesync.stats.items()},
+        'replicas': [{'rank': x['rank'], 'height': x['height'], 'utxo_hash': x['utxo_hash']} for x in st] if st else None}
+
+
+def run_cluster_sync_bench(args, ctx):
+    """sync tx/s of ONE chain on a G-rank cluster node (strong scaling: the chain is fixed as G grows)."""
+    from .ops.native import gpu_available
+    device = 'gpu' if gpu_available() else 'cpu'
+    utxo_backend = 'gpu' if device == 'gpu' else 'host'
+    txs, wall, extra = asyncio.run(_run_cluster_sync(args, ctx, device, utxo_backend))
+    return {
+        'metric': 'sync_tx_per_s',
+        'value': round(txs / wall, 1),
+        'unit': 'tx/s',
+        'n_gpus': ctx.world if device == 'gpu' else 0,
+        'world': ctx.world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(wall * 1000 / max(1, args.steps), 3),
+        'higher_is_better': True,
+        'scaling': 'strong',
+        'vs_baseline': None,
+        'dtype': 'uint32',
+        'data': _sync_data_label(args),
+        'config': {'model': 'upow cluster node chain sync: one chain, G replicas, page plans with sharded ECDSA',
+                   'global_batch': txs // max(1, args.steps), 'seq_len': extra['tx_counts']['mean'],
+                   'parallelism': f'replica{ctx.world}+sigshard', 'device': device, 'utxo_backend': utxo_backend,
+                   'ledger': 'file (WAL)' if getattr(args, 'ledger', None) else 'memory'},
         **{k: v for k, v in extra.items() if v is not None},
     }

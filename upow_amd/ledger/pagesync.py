@@ -101,7 +101,9 @@ def prepare(info: dict) -> Item:
     if k is not None:
         cb_hex = hexes[k]
         hexes = hexes[:k] + hexes[k + 1:]
-    dec = fastpath.decode(hexes, threads=1 if len(hexes) < 512 else fastpath.THREADS) if hexes else None
+    # an empty block decodes too (n = 0): it then takes the native path like the others, and the plan models
+    # its coinbase outputs instead of re-planning after it
+    dec = fastpath.decode(hexes, threads=1 if len(hexes) < 512 else fastpath.THREADS)
     if dec is not None:
         dec['merkle_job'].result()
     return Item(info['block'], list(info['transactions']), hexes, cb_hex, dec)
@@ -265,11 +267,14 @@ def build_plan(db, items: List[Item], cbs: list, ctx=None) -> List[Optional[Page
         _record(t0, len(cand), 0, 0)
         return plan
     gpu_min = op.GPU_MIN_BATCH if gpu_available() else 1 << 62
-    kst, rec_bytes = lib().block_signer_records(
-        np.ascontiguousarray(np.concatenate(pa)), np.concatenate(pl), np.ascontiguousarray(np.concatenate(oa)),
-        np.concatenate(ol), np.concatenate(ji), np.ascontiguousarray(np.concatenate(sg)), np.concatenate(sid),
-        np.ascontiguousarray(np.concatenate(dg)), np.concatenate(jt), gpu_min)
     n_jobs = job_base
+    if n_jobs or sum(len(x) for x in ol):
+        kst, rec_bytes = lib().block_signer_records(
+            np.ascontiguousarray(np.concatenate(pa)), np.concatenate(pl), np.ascontiguousarray(np.concatenate(oa)),
+            np.concatenate(ol), np.concatenate(ji), np.ascontiguousarray(np.concatenate(sg)), np.concatenate(sid),
+            np.ascontiguousarray(np.concatenate(dg)), np.concatenate(jt), gpu_min)
+    else:  # empty blocks only: nothing to check or verify
+        kst, rec_bytes = 1, b''
     if ctx is not None and ctx.is_distributed:
         # every replica planned the same chunk from the same state; a difference would desynchronise the
         # sharded verify below, so it is checked (one 16-byte all-reduce per chunk) before anything is shared
