@@ -187,3 +187,101 @@ def test_single_utxo_file_ledger_is_split_on_open(tmp_path, monkeypatch):
     ok, nxt, n_got = asyncio.run(reopen())
     assert ok == (True, 0, 0, True, True), (ok, n_got, len(rows))
     assert nxt == max(r[0] for r in rows) + 1
+
+
+SYNCER = r'''
+import asyncio, hashlib, json, sys
+sys.path.insert(0, sys.argv[3])
+from upow_amd import bench_verify, devnet
+from upow_amd.constants import START_DIFFICULTY
+from upow_amd.ledger import fastpath, manager, pagesync
+from upow_amd.models.block import get_transactions_merkle_tree
+
+async def main(src_path, dst_path, n_blocks, n_txs, out):
+    base_ts = 1_700_000_000
+    src, addr, blocks, _ = await bench_verify._setup(n_blocks, n_txs, 99, 'host', 'cpu', ledger_path=src_path,
+                                                     base_ts=base_ts)
+    prev = (await src.get_last_block())['hash']
+    for b, txs in enumerate(blocks):
+        manager.Manager.difficulty = None
+        content = devnet.mine_header_raw(prev, addr, get_transactions_merkle_tree(txs), base_ts + 60 * (b + 2),
+                                         START_DIFFICULTY, device='cpu')
+        assert await fastpath.create_block_from_hex(content, txs)
+        prev = hashlib.sha256(bytes.fromhex(content)).hexdigest()
+    page = await src.get_blocks(3, n_blocks)
+    with open(out, 'w') as f:
+        json.dump({'page': page, 'utxo': src.sql_unspent_outputs_hash(), 'tip': prev}, f, default=str)
+    src.close()
+    dst, *_ = await bench_verify._setup(n_blocks, n_txs, 99, 'host', 'cpu', ledger_path=dst_path, base_ts=base_ts,
+                                        make_blocks=False)
+    orig = fastpath.create_block_from_hex
+
+    async def traced(*a, **kw):
+        ok = await orig(*a, **kw)
+        print('applied', dst._tip_id(), flush=True)
+        return ok
+    fastpath.create_block_from_hex = traced
+    print('syncing', flush=True)
+    assert await pagesync.create_blocks(page)
+    print('done', flush=True)
+
+asyncio.run(main(sys.argv[1], sys.argv[2], int(sys.argv[4]), int(sys.argv[5]), sys.argv[6]))
+'''
+
+
+@pytest.mark.parametrize('kill_at', [5, 9])
+def test_sigkill_mid_sync_page_resumes_at_the_last_durable_block(tmp_path, kill_at, monkeypatch):
+    """A page-batched sync (ledger/pagesync.py: one fdatasync for the whole page, deferred index writes) is
+    SIGKILLed in the middle of its page. Reopening gives whole blocks only and an index equal to the SQL UTXO
+    set; syncing the rest of the page from the reopened tip (what the node does: fetch from its next block id)
+    ends in the source chain's exact state."""
+    import asyncio
+    import json
+    n_blocks = 14
+    src, dst, out = str(tmp_path / 'src.sqlite3'), str(tmp_path / 'dst.sqlite3'), str(tmp_path / 'page.json')
+    env = dict(os.environ, UPOW_START_DIFFICULTY='1.5', UPOW_DISABLE_GPU='1', UPOW_SYNC_CHUNK='4',
+               UPOW_WAL_CHECKPOINT_PERIOD='0.05', UPOW_SNAPSHOT_EVERY='3')
+    p = subprocess.Popen([sys.executable, '-c', SYNCER, src, dst, ROOT, str(n_blocks), str(TXS), out], env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+    try:
+        tip = 0
+        deadline = time.time() + 240
+        while tip < kill_at and time.time() < deadline:
+            line = p.stdout.readline()
+            if not line:
+                break
+            if line.startswith('applied'):
+                tip = int(line.split()[1])
+        assert tip >= kill_at, f'syncer stopped early at block {tip}'
+        p.send_signal(signal.SIGKILL)
+        p.wait(timeout=30)
+    finally:
+        if p.poll() is None:
+            p.kill()
+    ref = json.load(open(out))
+    sys.path.insert(0, ROOT)
+    from decimal import Decimal
+    from upow_amd.ledger import manager, pagesync
+    from upow_amd.ledger.database import Database
+    monkeypatch.setattr(manager, 'START_DIFFICULTY', Decimal('1.5'))  # the syncer's chain
+
+    async def resume():
+        db = await Database.create(path=dst, utxo_backend='host')
+        manager.Manager.difficulty = None
+        try:
+            t = db._tip_id()
+            assert kill_at <= t <= 2 + n_blocks
+            counts = db._q('SELECT b.id, COUNT(t.tx_hash) FROM blocks b LEFT JOIN transactions t '
+                           'ON t.block_hash = b.hash WHERE b.id > 2 GROUP BY b.id')
+            assert len(counts) == t - 2 and all(c == TXS + 1 for _, c in counts), counts
+            assert db.utxo.set_hash() == db.sql_unspent_outputs_hash()
+            rest = [b for b in ref['page'] if int(b['block']['id']) > t]
+            if rest:
+                assert await pagesync.create_blocks(rest)
+            db.flush()
+            return db._tip_id(), (await db.get_last_block())['hash'], db.sql_unspent_outputs_hash(), db.utxo.set_hash()
+        finally:
+            db.close()
+    tip, h, sql_hash, idx_hash = asyncio.run(resume())
+    assert (tip, h) == (2 + n_blocks, ref['tip'])
+    assert sql_hash == idx_hash == ref['utxo']

@@ -117,7 +117,7 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
     n_dv, n_vv = int(n_gov * 0.7), int(n_gov * 0.1)
     n_rv = n_gov - n_dv - n_vv
     if base_ts is None:
-        base_ts = int(time.time()) - (4 * 86_400 if n_gov else 10_000)
+        base_ts = int(time.time()) - (4 * 86_400 if n_gov else 0) - max(10_000, SPACING_S * (n_blocks + 10))
     genesis_addr = addrs[0]
     await devnet.mine_block(genesis_addr, ts=base_ts, device=device)
     if age_txs:
@@ -205,6 +205,32 @@ async def _setup(n_blocks: int, txs_per_block: int, seed: int, utxo_backend=None
             rng.shuffle(txs)
         blocks.append(txs)
     return db, genesis_addr, blocks, base_ts
+
+
+SPACING_S = 45  # verify benches: block timestamps 45 s apart, so every 100-block retarget raises the difficulty
+
+
+async def premine_headers(db, addr: str, blocks, base_ts: int, device, spacing: int = SPACING_S):
+    """Headers for ``blocks`` on top of ``db``'s tip, timestamps ``spacing`` apart, each mined at the difficulty
+    the chain will require of it (``manager.difficulty_schedule``: calculate_difficulty's retarget arithmetic
+    over the planned timestamps), so a run longer than 100 blocks crosses retargets like a real chain.
+    Returns (headers, difficulties)."""
+    from . import devnet
+    from .ledger import manager
+    from .models.block import get_transactions_merkle_tree
+    rows = db._q('SELECT timestamp, difficulty FROM blocks ORDER BY id')
+    chain = [(int(r[0]), r[1]) for r in rows]
+    ts = [base_ts + spacing * (b + 1) for b in range(len(blocks))]
+    ts = [max(t, chain[-1][0] + 1 + b) for b, t in enumerate(ts)] if chain else ts
+    diffs = manager.difficulty_schedule(chain, ts)
+    prev = (await db.get_last_block())['hash']
+    headers = []
+    for b, txs_hex in enumerate(blocks):
+        content = devnet.mine_header_raw(prev, addr, get_transactions_merkle_tree(txs_hex), ts[b], diffs[b],
+                                         device=device)
+        headers.append(content)
+        prev = hashlib.sha256(bytes.fromhex(content)).hexdigest()
+    return headers, diffs
 
 
 def _governance_txs(seeded, nxt, n_dv, n_vv, n_rv, rng):
@@ -480,18 +506,8 @@ async def _run(args, ctx, device, utxo_backend):
     # together, not scattered over the generator's setup heap (scripts/gov_ab.py, docs/ROUND4.md section 8)
     blocks = [json.loads(json.dumps(b)) for b in blocks]
     gov_probe = await _governance_probe(db) if gov else None
-    # mine every header up front (untimed): block b+1's previous hash is sha256(header_b) and the
-    # difficulty stays at START_DIFFICULTY below block 100
-    from .constants import START_DIFFICULTY
-    from .models.block import get_transactions_merkle_tree
-    last = await db.get_last_block()
-    prev = last['hash']
-    headers = []
-    for b, txs_hex in enumerate(blocks):
-        content = devnet.mine_header_raw(prev, addr, get_transactions_merkle_tree(txs_hex), base_ts + 10 + b,
-                                         START_DIFFICULTY, device=device)
-        headers.append(content)
-        prev = hashlib.sha256(bytes.fromhex(content)).hexdigest()
+    # mine every header up front (untimed), each at the difficulty the chain will require of it
+    headers, difficulties = await premine_headers(db, addr, blocks, base_ts, device)
     stages = []
     paths = set()
     total_txs = 0
@@ -558,6 +574,7 @@ async def _run(args, ctx, device, utxo_backend):
     if writer is not None:
         writer = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in writer.items() if k != 'error'}
     extra = {'drain_s': drain, 'writer': writer, 'window_unix': [unix_start, time.time()], 'governance': gov_probe,
+             'difficulties': sorted({str(d) for d in difficulties}),
              'aging': aging or None, 'queue_trace': queue_trace, 'key_setup_s': key_setup}
     if gov_probe is not None:
         gov_probe['active_inodes_after'] = len(await db.get_active_inodes())
@@ -621,6 +638,7 @@ def run_verify_bench(args, ctx):
         'final_drain_ms': round(extra['drain_s'] * 1000, 2),
         'ledger_writer': extra['writer'],
         'window_unix': extra['window_unix'],
+        'difficulties': extra.get('difficulties'),
         **({'key_setup_s': extra['key_setup_s']} if extra.get('key_setup_s') is not None else {}),
         **({'governance': extra['governance']} if extra['governance'] else {}),
         **({'aged_ledger': extra['aging'], 'writer_lag_after_block': extra['queue_trace']} if extra['aging'] else {}),
@@ -641,7 +659,7 @@ async def _run_cluster(args, ctx, device, utxo_backend):
     from .parallel import cluster
     from .parallel.cluster import unpack_txs
     n_blocks = args.steps + args.warmup
-    base_ts = ctx.allreduce_min(int(time.time()) - 10_000)
+    base_ts = ctx.allreduce_min(int(time.time()) - max(10_000, SPACING_S * (n_blocks + 10)))
     db, addr, blocks, _ = await _setup(n_blocks, args.txs, 1234, utxo_backend, device, base_ts=base_ts,
                                        make_blocks=ctx.rank == 0, ledger_path=_ledger_path(args, ctx),
                                        distinct_keys=_distinct(args))
@@ -652,12 +670,7 @@ async def _run_cluster(args, ctx, device, utxo_backend):
     validate.set_dist_context(ctx)
     headers = []
     if c.leader:
-        prev = (await db.get_last_block())['hash']
-        for b, txs_hex in enumerate(blocks):
-            content = devnet.mine_header_raw(prev, addr, get_transactions_merkle_tree(txs_hex), base_ts + 10 + b,
-                                             START_DIFFICULTY, device=device)
-            headers.append(content)
-            prev = hashlib.sha256(bytes.fromhex(content)).hexdigest()
+        headers, _ = await premine_headers(db, addr, blocks, base_ts, device)
     stages = []
     total_txs = 0
     try:

@@ -86,21 +86,48 @@ async def calculate_difficulty() -> Tuple[Decimal, dict]:
         return START_DIFFICULTY, last_block
     if last_block['id'] % BLOCKS_COUNT == 0:
         last_adjust_block = await database.get_block_by_id(last_block['id'] - BLOCKS_COUNT + 1)
-        elapsed = last_block['timestamp'] - last_adjust_block['timestamp']
-        average_per_block = elapsed / BLOCKS_COUNT
-        last_difficulty = last_block['difficulty']
-        hashrate = difficulty_to_hashrate(last_difficulty)
-        ratio = BLOCK_TIME / average_per_block
-        if last_block['id'] >= 180_000:
-            ratio = min(ratio, 2)
-        hashrate *= ratio
-        new_difficulty = hashrate_to_difficulty(hashrate)
-        if new_difficulty < START_DIFFICULTY and last_block['id'] >= 590600:
-            return START_DIFFICULTY, last_block
+        new_difficulty = retarget(last_block['id'], last_block['difficulty'], last_block['timestamp'],
+                                  last_adjust_block['timestamp'])
         logger.info(f'calculate_difficulty hashrate_to_difficulty block {last_block["id"]}, '
                     f'new_difficulty {new_difficulty}')
         return new_difficulty, last_block
     return last_block['difficulty'], last_block
+
+
+def retarget(last_id: int, last_difficulty, last_ts: int, window_first_ts: int) -> Decimal:
+    """The retarget arithmetic of manager.py:83-121 at a block id divisible by BLOCKS_COUNT: the next
+    difficulty from the last one and the timestamps of the window's first and last blocks."""
+    average_per_block = (last_ts - window_first_ts) / BLOCKS_COUNT
+    hashrate = difficulty_to_hashrate(last_difficulty)
+    ratio = BLOCK_TIME / average_per_block
+    if last_id >= 180_000:
+        ratio = min(ratio, 2)
+    hashrate *= ratio
+    new_difficulty = hashrate_to_difficulty(hashrate)
+    if new_difficulty < START_DIFFICULTY and last_id >= 590600:
+        return START_DIFFICULTY
+    return new_difficulty
+
+
+def difficulty_schedule(chain: List[Tuple[int, Decimal]], timestamps: List[int]) -> List[Decimal]:
+    """The difficulty the chain will require of each of the next blocks, given the (timestamp, difficulty)
+    of every block so far (``chain``, block ids 1..n) and the planned timestamps of the next ones: what
+    calculate_difficulty answers at each of those heights (benches mine headers ahead with it)."""
+    ts = [t for t, _ in chain]
+    ds = [Decimal(d) for _, d in chain]
+    out = []
+    for t in timestamps:
+        last_id = len(ts)
+        if last_id < BLOCKS_COUNT:
+            d = START_DIFFICULTY
+        elif last_id % BLOCKS_COUNT == 0:
+            d = retarget(last_id, ds[-1], ts[-1], ts[last_id - int(BLOCKS_COUNT)])
+        else:
+            d = ds[-1]
+        out.append(d)
+        ts.append(int(t))
+        ds.append(Decimal(d))
+    return out
 
 
 async def get_difficulty() -> Tuple[Decimal, dict]:
