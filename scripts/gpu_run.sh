@@ -35,6 +35,8 @@
 #   soakc1k  the same at 1,200 tx/s
 #   clustersync  page-batched sync on a forced single-rank RCCL cluster vs plain, two interleaved pairs
 #   sprofpage  rocprofv3 kernel trace + stats of the page-batched sync (200-tx blocks)
+#   collat   collective latencies over RCCL (scripts/collective_latency.py, forced single rank)
+#   syncprof cProfile of the timed page sync of 0-20-tx blocks
 #   bench:NAME:--a,1,...  bench.py with extra arguments (output bench_NAME.json)
 #   py:<script.py>  any extra python script under scripts/ (args after a comma: py:x.py,--a,1)
 # Every GPU step has its own time limit and the chain stops at the first failure.
@@ -255,6 +257,19 @@ for s in $STEPS; do
         --txs 200 --steps 1000 --warmup 5 --ledger /tmp/upow_bench_ledger > "$OUT/sprofpage.json" 2> "$OUT/sprofpage.err" \
         || { tail -20 "$OUT/sprofpage.err"; exit 1; }
       find "$OUT/sprofpage" -name '*kernel_stats.csv' | head -1 | xargs -r head -25 ;;
+    collat)
+      # latency of the cluster collectives over RCCL (forced single-rank group on the one GPU)
+      UPOW_FORCE_DIST=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29561 scripts/collective_latency.py > "$OUT/collat.json" \
+        2> "$OUT/collat.err" || { tail -20 "$OUT/collat.err"; exit 1; }
+      grep '^{' "$OUT/collat.json" ;;
+    syncprof)
+      # cProfile of the timed page-batched sync of mainnet-shaped blocks (0-20 txs)
+      rm -rf /tmp/upow_bench_ledger
+      UPOW_BENCH_PROFILE="$OUT/syncprof.txt" timeout -k 10 600 python bench.py --mode sync --txs-range 0-20 \
+        --steps 2000 --warmup 5 --ledger /tmp/upow_bench_ledger > "$OUT/syncprof.json" 2> "$OUT/syncprof.err" \
+        || { tail -20 "$OUT/syncprof.err"; exit 1; }
+      cut -c1-300 "$OUT/syncprof.json" ;;
     bench:*)
       # bench:NAME:--arg,value,...  one bench.py run with extra arguments (file ledger under /tmp)
       spec=${s#bench:}; name=${spec%%:*}; rest=${spec#*:}; rest=${rest//,/ }
