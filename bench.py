@@ -111,7 +111,7 @@ def bench_verify(args, ctx):
     return run_cluster_verify_bench(args, ctx) if ctx.is_distributed else run_verify_bench(args, ctx)
 
 
-def _verify_once(args, ctx, keys: str) -> dict:
+def _verify_once(args, ctx, keys: str, segments: int = 1) -> dict:
     import shutil
     import tempfile
     from upow_amd.bench_verify import run_cluster_verify_bench, run_verify_bench
@@ -119,7 +119,8 @@ def _verify_once(args, ctx, keys: str) -> dict:
     try:
         v = argparse.Namespace(**{**vars(args), 'steps': args.verify_steps, 'warmup': 2, 'ledger': tmp,
                                   'object_path': False, 'from_mempool': False, 'governance': False,
-                                  'governance_txs': 0.0, 'age_txs': 0, 'keys': keys, 'grouped_txs': 0.0})
+                                  'governance_txs': 0.0, 'age_txs': 0, 'keys': keys, 'grouped_txs': 0.0,
+                                  'segments': segments})
         return run_cluster_verify_bench(v, ctx) if ctx.is_distributed else run_verify_bench(v, ctx)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
@@ -127,11 +128,13 @@ def _verify_once(args, ctx, keys: str) -> dict:
 
 def _verify_side_metrics(args, ctx) -> dict:
     """BASELINE metric 2 next to the hashrate: ``--verify-steps`` timed 2 MB blocks (+2 warmup) through the
-    native push_block path on this rank's GPU, file-backed ledger in a temporary directory. The reported
+    native push_block path on this rank's GPU, file-backed ledger in a temporary directory, as the median of
+    ``--verify-segments`` consecutive segments (each ending with its own SQL drain). The reported
     number uses distinct keys (a fresh key pair per tx, fresh output addresses: BASELINE's random-keypair
     data); the 256-key pool run follows as a labelled second number (``verify_pool256_*``)."""
-    r = _verify_once(args, ctx, 'distinct')
+    r = _verify_once(args, ctx, 'distinct', args.verify_segments)
     out = {'verify_tx_per_s': r['value'], 'verify_ms_per_block': r['ms_per_step'],
+           **({'verify_segments_tx_per_s': r['segments_tx_per_s']} if 'segments_tx_per_s' in r else {}),
            'verify_commit_latency_ms': r['commit_latency_ms'], 'validate_tx_per_s': r['validate_tx_per_s'],
            'ecdsa_sig_per_s': r['ecdsa_sig_per_s'], 'verify_stage_ms_avg': r['stage_ms_avg'],
            'verify_config': {'metric': r['metric'], 'unit': r['unit'], 'steps': args.verify_steps, 'warmup': 2,
@@ -223,6 +226,10 @@ def main(argv=None):
                     help='mine mode: blocks of the chain-sync side measurement (200-tx blocks; 0: skip; GPU only)')
     ap.add_argument('--sync-path', choices=['page', 'block'], default='page',
                     help='sync mode: page-batched (ledger/pagesync.py, default) or the per-block pipeline (A/B)')
+    ap.add_argument('--verify-segments', type=int, default=3,
+                    help='mine mode: the verify side metric is the median of this many consecutive segments of '
+                         '--verify-steps blocks (one setup, one process)')
+    ap.add_argument('--segments', type=int, default=1, help='verify mode: median of this many segments of --steps blocks')
     ap.add_argument('--verify-steps', type=int, default=10,
                     help='mine mode: timed 2 MB blocks of the tx-verify side measurement (0: skip; GPU only)')
     args = ap.parse_args(argv)

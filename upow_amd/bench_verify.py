@@ -490,7 +490,8 @@ async def _run(args, ctx, device, utxo_backend):
     from . import devnet
     from .ledger import fastpath, manager, validate
     from .models.transaction import Transaction
-    n_blocks = args.steps + args.warmup
+    segments = max(1, int(getattr(args, 'segments', 1) or 1))
+    n_blocks = args.steps * segments + args.warmup
     gov = getattr(args, 'governance', False)
     gov_txs = float(getattr(args, 'governance_txs', 0.0) or 0.0)
     aging = {}
@@ -518,6 +519,14 @@ async def _run(args, ctx, device, utxo_backend):
     from_mempool = getattr(args, 'from_mempool', False)
     queue_trace = []  # (journal records not yet in SQL, bytes queued) after each timed block
     untimed = 0.0  # mempool admission of the next block's txs happens inside the wall-clock window
+    seg_walls, seg_txs = [], []  # per segment of ``steps`` blocks, each ending with its own SQL drain
+
+    def end_segment():
+        db.flush()
+        ctx.synchronize()
+        seg_walls.append(time.perf_counter() - seg[0] - (untimed - seg[1]))
+        seg_txs.append(total_txs - seg[2])
+    seg = None
     for b, txs_hex in enumerate(blocks):
         if from_mempool:
             ta = time.perf_counter()
@@ -532,6 +541,10 @@ async def _run(args, ctx, device, utxo_backend):
                 prof.enable()
             t_start = time.perf_counter()
             unix_start = time.time()
+        if b >= args.warmup and (b - args.warmup) % args.steps == 0:
+            if seg is not None:
+                end_segment()
+            seg = (time.perf_counter(), untimed, total_txs)
         t0 = time.perf_counter()
         errors = []
         if from_mempool:
@@ -562,9 +575,8 @@ async def _run(args, ctx, device, utxo_backend):
     # the timed region ends when the SQL tables hold every block (the journal is the commit point;
     # the materialiser must have caught up too)
     td = time.perf_counter()
-    db.flush()
+    end_segment()
     drain = time.perf_counter() - td
-    ctx.synchronize()
     ctx.barrier()
     wall = time.perf_counter() - t_start - untimed
     if prof is not None:  # UPOW_BENCH_PROFILE=PATH: cProfile of the timed blocks only (text report)
@@ -575,6 +587,7 @@ async def _run(args, ctx, device, utxo_backend):
         writer = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in writer.items() if k != 'error'}
     extra = {'drain_s': drain, 'writer': writer, 'window_unix': [unix_start, time.time()], 'governance': gov_probe,
              'difficulties': sorted({str(d) for d in difficulties}),
+             'segments': [(t, w) for t, w in zip(seg_txs, seg_walls)],
              'aging': aging or None, 'queue_trace': queue_trace, 'key_setup_s': key_setup}
     if gov_probe is not None:
         gov_probe['active_inodes_after'] = len(await db.get_active_inodes())
@@ -604,7 +617,17 @@ def run_verify_bench(args, ctx):
     else:
         args_cfg = None
     total = ctx.allreduce_sum(total_txs)
-    tps = total / wall
+    segs = extra.get('segments') or []
+    if len(segs) > 1:
+        # the median of the run's segments (each ``steps`` blocks ending in its own SQL drain): separate runs
+        # on the pool's boxes differ by up to +-15 %, interleaved segments of one run far less
+        seg_tps = sorted(ctx.allreduce_sum(t) / ctx.allreduce_max_f(w) for t, w in segs)
+        tps = seg_tps[len(seg_tps) // 2]
+        ms = round(1000 * (total / len(segs)) / tps / max(1, args.steps), 2) if tps else 0.0
+    else:
+        seg_tps = None
+        tps = total / wall
+        ms = round(wall * 1000 / max(1, args.steps), 2)
     avg = {k: round(sum(s[k] for s in stages) / len(stages) * 1000, 2) for k in stages[0]
            if isinstance(stages[0][k], float)}
     return {
@@ -614,7 +637,8 @@ def run_verify_bench(args, ctx):
         'n_gpus': ctx.world if device == 'gpu' else 0,
         'steps': args.steps,
         'warmup': args.warmup,
-        'ms_per_step': round(wall * 1000 / max(1, args.steps), 2),
+        'ms_per_step': ms,
+        **({'segments_tx_per_s': [round(x, 1) for x in seg_tps], 'segment_blocks': args.steps} if seg_tps else {}),
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,

@@ -1966,7 +1966,8 @@ class Database:
 
     def apply_native_block(self, block_row: dict, coinbase_row: tuple, coinbase_outputs: list, n: int,
                            tx_cols: list, out_cols: tuple, in_keys: np.ndarray, spent_payload: np.ndarray,
-                           gov: Optional[dict] = None, addr_pairs: Optional[tuple] = None) -> int:
+                           gov: Optional[dict] = None, addr_pairs: Optional[tuple] = None,
+                           cb_index: Optional[tuple] = None) -> int:
         """The ledger writes of one native-path block (reference manager.py:706-730: add_block,
         add_transaction(coinbase), add_transactions, add_transaction_outputs, remove_pending_transactions,
         remove_outputs, remove_pending_spent_outputs) as ONE journal batch, plus the HBM index update.
@@ -1980,6 +1981,7 @@ class Database:
         outputs land in their tables (stake flag from the output type), spends leave theirs, and the
         governance index follows from these columns — the object path's write set (apply_object_block) in
         the same statement order, so both paths leave identical tables.
+        ``cb_index``: the coinbase outputs' index (records, payloads) when already built (a sync page's plan).
         Returns the journal sequence number (0 without the native writer: written synchronously)."""
         ts = [perf_counter()]  # stage clock: records, statements, encode, journal, index, mempool, governance
         names = ('apply:records', 'apply:stmts', 'apply:encode', 'apply:journal', 'apply:index', 'apply:mempool',
@@ -2007,9 +2009,12 @@ class Database:
         pay = np.frombuffer(pb, dtype=PAYLOAD_DTYPE)
         from .utxo import pack_records
         cb_keys = [(o[0], o[1]) for o in coinbase_outputs]
-        cb_recs = pack_records(cb_keys, tag_u)
-        cb_pay = make_payload([o[4] for o in coinbase_outputs], [_addr_bytes(o[2]) for o in coinbase_outputs],
-                              [bool(o[3]) for o in coinbase_outputs])
+        if cb_index is not None:  # (records, payloads) of the coinbase outputs, built by a sync page's plan
+            cb_recs, cb_pay = cb_index
+        else:
+            cb_recs = pack_records(cb_keys, tag_u)
+            cb_pay = make_payload([o[4] for o in coinbase_outputs], [_addr_bytes(o[2]) for o in coinbase_outputs],
+                                  [bool(o[3]) for o in coinbase_outputs])
         in_keys = np.ascontiguousarray(in_keys, dtype=np.uint8).reshape(-1, 40)
         in_tag = gov['in_tag'].astype(np.uint32) if gov is not None else np.full(n_in, tag_u, dtype=np.uint32)
         sb, ib = lib().spent_index_records(in_keys, np.ascontiguousarray(in_tag, dtype=np.uint32))

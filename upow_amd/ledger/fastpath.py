@@ -277,7 +277,10 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     if hdr is None:
         return False
     block_no, merkle_tree = hdr
-    logger.info(f'{"Syncing" if coinbase is not None else "Creating"} block no. {block_no} (native path, {d["n"]} txs)')
+    if page is None:
+        logger.info(f'{"Syncing" if coinbase is not None else "Creating"} block no. {block_no} (native path, {d["n"]} txs)')
+    elif logger.isEnabledFor(10):  # a sync page logs per chunk (ledger/pagesync.py); per block only at DEBUG
+        logger.debug(f'Syncing block no. {block_no} (page plan, {d["n"]} txs)')
     if block_no in manager.double_spend_dict:
         return None
     n = int(d['n'])
@@ -471,7 +474,9 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
                      'random': int(random), 'difficulty': numeric(difficulty, 1),
                      'reward': numeric(block_reward + fees_total, 6), 'timestamp': int(content_time)}
         cb_row = await database._tx_row(coinbase_transaction, block_hash)
-        cb_outputs = Database.split_outputs([coinbase_transaction])['unspent_outputs']
+        # a sync page's plan already split the trusted coinbase and built its index records (pagesync)
+        pre_cb = coinbase_transaction.__dict__.get('_upow_cb_index')
+        cb_outputs = pre_cb[0] if pre_cb else Database.split_outputs([coinbase_transaction])['unspent_outputs']
         tx_cols = [('hex32', txid, 32, 0), ('hexarena', *d['canon']), ('arena', *in_json), ('arena', *d['out_addr_json']),
                    ('arena', *d['out_amount_json']), fee_str]
         out_cols = (out_index, ('arena', *d['out_addr_str']), txid[out_tx], out_amount, out_addr, out_len)
@@ -479,7 +484,8 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         roctx.pop()
         try:
             seq = database.apply_native_block(block_row, cb_row, cb_outputs, n, tx_cols, out_cols, in_keys, pay,
-                                              gov=gov_cols, addr_pairs=addr_pairs)
+                                              gov=gov_cols, addr_pairs=addr_pairs,
+                                              cb_index=pre_cb[1:] if pre_cb else None)
         except Exception as e:
             if database._submitted != submitted:
                 raise  # committed to the journal: a failure after the commit point is not a rejection

@@ -127,48 +127,63 @@ def build_plan(db, items: List[Item], cbs: list, ctx=None) -> List[Optional[Page
     t0 = perf_counter()
     n_items = len(items)
     plan: List[Optional[PageBlock]] = [None] * n_items
-    cand = []
-    for k, it in enumerate(items):
-        d = it.dec
-        if d is None or cbs[k] is None:
-            continue
-        gov, anyg = lib().gov_block_mask(np.ascontiguousarray(d['_tx_type'], np.uint8),
-                                         np.frombuffer(d['out_type'], np.uint8), _i32(d, 'out_tx'), int(d['n']),
-                                         len(d['out_type']))
-        cand.append((k, bool(anyg)))
-    if not cand:
+    ks = [k for k, it in enumerate(items) if it.dec is not None and cbs[k] is not None]
+    if not ks:
         return plan
-    # ---- the chunk's inputs (block order) and outputs (block txs, then the coinbase), with payloads exactly as
-    #      the apply will insert them (output_index_records / make_payload)
-    in_keys, in_blk, out_keys, out_blk, out_tag, out_pay = [], [], [], [], [], []
+    decs = [items[k].dec for k in ks]
+    # ---- the chunk's columns, concatenated once: per-block slices of one array each, and one native call
+    #      for all the chunk's output records (payloads exactly as the apply will insert them)
     tag_lut = np.full(256, MISSING, np.uint32)
     for t, table in OUTPUT_TABLE.items():
         tag_lut[t] = TAG_BY_TABLE[table]
-    for k, _ in cand:
-        d = items[k].dec
-        ik = np.frombuffer(d['in_keys'], np.uint8).reshape(-1, 40)
-        in_keys.append(ik)
-        in_blk.append(np.full(len(ik), k, np.int32))
-        out_tx, out_start = _i32(d, 'out_tx'), _i32(d, 'out_start')
-        txid = np.frombuffer(d['txid'], np.uint8).reshape(-1, 32)
-        otype = np.frombuffer(d['out_type'], np.uint8)
-        tags = tag_lut[otype]
-        rb, pb = lib().output_index_records(
-            np.ascontiguousarray(txid[out_tx]), (np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]),
-            np.ascontiguousarray(tags, np.uint32), np.frombuffer(d['out_amount'], np.uint64),
-            np.frombuffer(d['out_addr'], np.uint8), np.frombuffer(d['out_len'], np.uint8),
-            (otype == int(OutputType.STAKE)).astype(np.uint8))
-        out_keys.append(np.frombuffer(rb, np.uint8).reshape(-1, 40))
-        out_pay.append(np.frombuffer(pb, PAYLOAD_DTYPE))
-        out_tag.append(tags)
-        out_blk.append(np.full(len(out_tx), k, np.int32))
-        cbo = Database.split_outputs([cbs[k]])['unspent_outputs']
-        if cbo:
-            from .database import _addr_bytes
-            out_keys.append(pack_records([(o[0], o[1]) for o in cbo], TAG_U))
-            out_pay.append(make_payload([o[4] for o in cbo], [_addr_bytes(o[2]) for o in cbo], [bool(o[3]) for o in cbo]))
-            out_tag.append(np.full(len(cbo), TAG_U, np.uint32))
-            out_blk.append(np.full(len(cbo), k, np.int32))
+    n_tx = np.array([int(d['n']) for d in decs], np.int64)
+    n_out = np.array([len(d['out_type']) for d in decs], np.int64)
+    tx_type = np.concatenate([np.asarray(d['_tx_type'], np.uint8) for d in decs])
+    otype = np.concatenate([np.frombuffer(d['out_type'], np.uint8) for d in decs])
+    tx_base = np.concatenate([[0], np.cumsum(n_tx)])
+    out_base = np.concatenate([[0], np.cumsum(n_out)])
+    # a block is governance-relevant when any tx type or any output type is not REGULAR (gov_block_mask)
+    c_tt = np.concatenate([[0], np.cumsum(tx_type != 0)])
+    c_ot = np.concatenate([[0], np.cumsum(otype != 0)])
+    gov_blk = ((c_tt[tx_base[1:]] - c_tt[tx_base[:-1]]) + (c_ot[out_base[1:]] - c_ot[out_base[:-1]])) > 0
+    cand = list(zip(ks, gov_blk.tolist()))
+    txid_all = np.concatenate([np.frombuffer(d['txid'], np.uint8).reshape(-1, 32) for d in decs])
+    out_tx_g = np.concatenate([_i32(d, 'out_tx').astype(np.int64) + tx_base[i] for i, d in enumerate(decs)])
+    out_idx = np.concatenate([np.arange(len(d['out_type']), dtype=np.int64) - _i32(d, 'out_start')[_i32(d, 'out_tx')]
+                              for d in decs])
+    tags_o = tag_lut[otype]
+    rb, pb = lib().output_index_records(
+        np.ascontiguousarray(txid_all[out_tx_g]), out_idx, np.ascontiguousarray(tags_o, np.uint32),
+        np.concatenate([np.frombuffer(d['out_amount'], np.uint64) for d in decs]),
+        np.concatenate([np.frombuffer(d['out_addr'], np.uint8) for d in decs]),
+        np.concatenate([np.frombuffer(d['out_len'], np.uint8) for d in decs]), (otype == int(OutputType.STAKE)).astype(np.uint8))
+    out_keys = [np.frombuffer(rb, np.uint8).reshape(-1, 40)]
+    out_pay = [np.frombuffer(pb, PAYLOAD_DTYPE)]
+    out_tag = [tags_o]
+    out_blk = [np.repeat(np.asarray(ks, np.int32), n_out)]
+    # the coinbase outputs of the chunk (trusted coinbases: unspent_outputs, as the apply writes them)
+    from .database import _addr_bytes
+    cb_keys, cb_amt, cb_addr, cb_stake, cb_blk, cb_rows = [], [], [], [], [], []
+    for k in ks:
+        rows = Database.split_outputs([cbs[k]])['unspent_outputs']
+        cb_rows.append((k, len(cb_keys), rows))
+        for o in rows:
+            cb_keys.append((o[0], o[1]))
+            cb_amt.append(o[4])
+            cb_addr.append(_addr_bytes(o[2]))
+            cb_stake.append(bool(o[3]))
+            cb_blk.append(k)
+    if cb_keys:
+        cb_recs, cb_pay = pack_records(cb_keys, TAG_U), make_payload(cb_amt, cb_addr, cb_stake)
+        out_keys.append(cb_recs)
+        out_pay.append(cb_pay)
+        out_tag.append(np.full(len(cb_keys), TAG_U, np.uint32))
+        out_blk.append(np.asarray(cb_blk, np.int32))
+        # the apply of each block reuses its coinbase's rows and index records (fastpath apply)
+        for k, at, rows in cb_rows:
+            cbs[k].__dict__['_upow_cb_index'] = (rows, cb_recs[at:at + len(rows)], cb_pay[at:at + len(rows)])
+    in_keys = [np.frombuffer(d['in_keys'], np.uint8).reshape(-1, 40) for d in decs]
+    in_blk = [np.full(len(ik), k, np.int32) for k, ik in zip(ks, in_keys)]
     IK = np.ascontiguousarray(np.concatenate(in_keys))
     BI = np.concatenate(in_blk)
     OK_ = np.ascontiguousarray(np.concatenate(out_keys))
@@ -372,6 +387,8 @@ async def create_blocks(blocks: list, error_list: list = None, mirror: bool = Tr
                         it.dec = None
                 cbs.append(cb)
             plan = build_plan(db, items, cbs, ctx)
+            tc = perf_counter()
+            n_page = page_stats['page_path']
             k = 0
             while k < len(items):
                 it = items[k]
@@ -400,6 +417,8 @@ async def create_blocks(blocks: list, error_list: list = None, mirror: bool = Tr
                     page_stats['replans'] += 1
                     rest = build_plan(db, items[k:], cbs[k:], ctx)
                     plan = plan[:k] + rest
+            logger.info(f'Synced blocks {items[0].block["id"]}..{items[-1].block["id"]} '
+                        f'({page_stats["page_path"] - n_page} on the page plan) in {perf_counter() - tc:.3f} s')
         return True
     finally:
         if ahead is not None:  # a failed page: let the helper thread's decode finish before returning

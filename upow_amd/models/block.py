@@ -151,7 +151,13 @@ def check_pow(block_content: Union[str, bytes], prev_hash: Optional[str], diffic
     if prev_hash is None:
         return True
     digest = hashlib.sha256(block_content).hexdigest()
-    return PowTarget.from_difficulty(prev_hash, difficulty).check_hex(digest)
+    # the predicate of PowTarget.check_hex without building the search kernel's word/mask target
+    d = Decimal(str(difficulty)) if not isinstance(difficulty, Decimal) else difficulty
+    di = floor(d)
+    if not digest.startswith(prev_hash[-di:]):
+        return False
+    dec = d % 1
+    return int(digest[di], 16) < ceil(16 * (1 - dec)) if dec > 0 else True
 
 
 def header_prefix(prev_hash: str, address: str, merkle_root: str, ts: int, difficulty) -> bytes:

@@ -92,48 +92,63 @@ class DistContext:
         import torch
         return torch.tensor(values, dtype=dtype or torch.int64, device=self.comm_device)
 
+    def _reduce(self, values, op, dtype=None, what: str = 'all_reduce') -> list:
+        """All-reduce of a short vector through buffers kept for the process (a pinned host staging vector
+        and its device twin for RCCL): no allocation and no pageable copy per call. The per-block commit
+        vote of a cluster node is one of these, so its fixed cost is what a block pays for agreement."""
+        import torch
+        import torch.distributed as dist
+        dtype = dtype or torch.int64
+        key = (dtype, len(values))
+        bufs = self.__dict__.setdefault('_rbuf', {})
+        pair = bufs.get(key)
+        if pair is None:
+            gpu = self.comm_device != 'cpu'
+            host = torch.zeros(len(values), dtype=dtype, pin_memory=gpu)
+            pair = bufs[key] = (host, torch.zeros(len(values), dtype=dtype, device=self.comm_device) if gpu else host)
+        host, dev = pair
+        h = host.numpy()
+        h[:] = values
+        if dev is not host:
+            dev.copy_(host, non_blocking=True)
+        self._run(what, dist.all_reduce, dev, op=op)
+        if dev is not host:
+            host.copy_(dev, non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+        return h.tolist()
+
     def allreduce_min(self, v: int) -> int:
         if not self.is_distributed:
             return int(v)
         import torch.distributed as dist
-        t = self._t([v])
-        self._run('all_reduce(min)', dist.all_reduce, t, op=dist.ReduceOp.MIN)
-        return int(t.item())
+        return int(self._reduce([int(v)], dist.ReduceOp.MIN, what='all_reduce(min)')[0])
 
     def allreduce_min_vec(self, values) -> list:
         """Element-wise MIN of a short int vector: several per-step agreements in ONE collective."""
         if not self.is_distributed:
             return [int(v) for v in values]
         import torch.distributed as dist
-        t = self._t(list(values))
-        self._run('all_reduce(min vec)', dist.all_reduce, t, op=dist.ReduceOp.MIN)
-        return [int(x) for x in t.tolist()]
+        return [int(x) for x in self._reduce([int(v) for v in values], dist.ReduceOp.MIN, what='all_reduce(min vec)')]
 
     def allreduce_sum_vec(self, values) -> list:
         """Element-wise SUM of a short int vector in ONE collective."""
         if not self.is_distributed:
             return [int(v) for v in values]
         import torch.distributed as dist
-        t = self._t(list(values))
-        self._run('all_reduce(sum vec)', dist.all_reduce, t, op=dist.ReduceOp.SUM)
-        return [int(x) for x in t.tolist()]
+        return [int(x) for x in self._reduce([int(v) for v in values], dist.ReduceOp.SUM, what='all_reduce(sum vec)')]
 
     def allreduce_max_f(self, v: float) -> float:
         if not self.is_distributed:
             return float(v)
         import torch
         import torch.distributed as dist
-        t = self._t([v], dtype=torch.float64)
-        self._run('all_reduce(max)', dist.all_reduce, t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        return float(self._reduce([float(v)], dist.ReduceOp.MAX, dtype=torch.float64, what='all_reduce(max)')[0])
 
     def allreduce_sum(self, v: int) -> int:
         if not self.is_distributed:
             return int(v)
         import torch.distributed as dist
-        t = self._t([v])
-        self._run('all_reduce(sum)', dist.all_reduce, t, op=dist.ReduceOp.SUM)
-        return int(t.item())
+        return int(self._reduce([int(v)], dist.ReduceOp.SUM, what='all_reduce(sum)')[0])
 
     def broadcast_bytes(self, data: Optional[bytes], src: int, max_len: int = 256) -> bytes:
         """Broadcast a byte string from ``src``. Payloads up to ``max_len`` (e.g. the 108-byte header)
