@@ -57,15 +57,34 @@ SAN_FLAGS = {'asan': ['-fsanitize=address,undefined', '-fno-sanitize-recover=und
 CLANGXX = '/opt/rocm/llvm/bin/clang++'
 
 
+# Per-file device code generation. The P-256 kernels are long chains of dependent 64-bit multiply-adds and
+# carry chains; gfx950 needs wait states between a v_mad_u64_u32 and the first read of its result, which the
+# default (occupancy-first) scheduler fills with s_nop: 6,865 of the quad verify kernel's 42,629 static
+# instructions. The ILP-first machine scheduler interleaves independent products instead (1,810 s_nop): the
+# block-latency kernels run one wave per SIMD, so the extra registers cost them nothing; the batch kernels
+# keep their __launch_bounds__ occupancy. 'p256occ' builds the old schedule for the A/B
+# (build-ab/native-p256occ, loaded through UPOW_NATIVE_SO).
+DEVICE_FLAGS = {'p256': ['-mllvm', '-amdgpu-sched-strategy=max-ilp']}
+
+
+def _device_flags(src: Path, variant: str) -> list:
+    if variant == 'p256occ':
+        return []
+    return DEVICE_FLAGS.get(src.stem, [])
+
+
 def _build_dir(variant: str) -> Path:
+    if variant == 'p256occ':  # shipped to the GPU box for the A/B (./build is not)
+        return ROOT / 'build-ab' / f'native-{variant}'
     return BUILD if variant == 'release' else ROOT / 'build' / f'native-{variant}'
 
 
 def _compile(src: Path, hdr_digest: str, force: bool, variant: str = 'release') -> Path:
     out = _build_dir(variant)
     out.mkdir(parents=True, exist_ok=True)
+    dev = _device_flags(src, variant) if src.suffix == '.hip' else []
     key = hashlib.sha256(src.read_bytes() + hdr_digest.encode() + ARCH.encode() + variant.encode()
-                         + (CXX.encode() if src.suffix != '.hip' else b'')).hexdigest()[:16]
+                         + ' '.join(dev).encode() + (CXX.encode() if src.suffix != '.hip' else b'')).hexdigest()[:16]
     obj = out / f'{src.stem}.{key}.o'
     if obj.exists() and not force:
         return obj
@@ -73,7 +92,7 @@ def _compile(src: Path, hdr_digest: str, force: bool, variant: str = 'release') 
     if src.suffix == '.hip':
         host = [] if san is None else ['-Xarch_host', '-O0', '-Xarch_host', '-g1',
                                        *[x for f in san for x in ('-Xarch_host', f)]]
-        cmd = [HIPCC, f'--offload-arch={ARCH}', *_flags_common(), *host, '-c', str(src), '-o', str(obj)]
+        cmd = [HIPCC, f'--offload-arch={ARCH}', *_flags_common(), *dev, *host, '-c', str(src), '-o', str(obj)]
     else:
         # host-only translation units: plain C++ (no device pass)
         cxx, extra = (CXX, []) if san is None else (CLANGXX, ['-O1', '-g', '-fno-omit-frame-pointer', *san])
@@ -115,7 +134,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--force', action='store_true')
     ap.add_argument('-j', '--jobs', type=int, default=min(8, os.cpu_count() or 4))
-    ap.add_argument('--variant', choices=['release', 'asan', 'tsan'], default='release')
+    ap.add_argument('--variant', choices=['release', 'asan', 'tsan', 'p256occ'], default='release')
     a = ap.parse_args(argv)
     build(force=a.force, jobs=a.jobs, variant=a.variant)
 

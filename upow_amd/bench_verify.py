@@ -968,6 +968,11 @@ async def _run_cluster_sync(args, ctx, device, utxo_backend):
             raise RuntimeError('cluster sync warmup rejected')
         c.send('status')
         c.status(dst)
+        prof = None
+        if os.environ.get('UPOW_BENCH_PROFILE'):  # cProfile of the leader's timed sync (text report)
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         errors = []
         timed = page[args.warmup:]
@@ -978,6 +983,8 @@ async def _run_cluster_sync(args, ctx, device, utxo_backend):
         c.send('status')
         st = c.status(dst)  # every replica has applied the last page when it answers
         wall = time.perf_counter() - t0
+        if prof is not None:
+            _dump_profile(prof, os.environ['UPOW_BENCH_PROFILE'])
         await cluster.leader_quit()
         wall = ctx.allreduce_max_f(wall)
         if any((s['height'], s['utxo_hash']) != (st[0]['height'], st[0]['utxo_hash']) for s in st):

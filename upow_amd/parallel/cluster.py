@@ -86,6 +86,7 @@ class Cluster:
         self.ops_sent = 0
         self.ops_received = 0
         self.commits_agreed = 0
+        self.vote_s = 0.0  # wall time spent in commit votes (the per-block price of agreement)
         self.last_resync: Optional[dict] = None
 
     @property
@@ -172,7 +173,8 @@ class Cluster:
         ops = self.ops_sent if self.leader else self.ops_received
         coll = self.ctx.collectives
         return {'ops': ops, 'collectives': coll, 'collectives_per_op': round(coll / ops, 3) if ops else None,
-                'commits_agreed': self.commits_agreed}
+                'commits_agreed': self.commits_agreed,
+                'vote_us_avg': round(self.vote_s / self.commits_agreed * 1e6, 1) if self.commits_agreed else None}
 
 
 # ---------------------------------------------------------------------------------------------- commit gate
@@ -193,7 +195,9 @@ class CommitGate:
         if self.voted is not None:
             raise RuntimeError('commit gate: a block voted twice')
         self.voted = bool(ok)
+        t0 = time.perf_counter()
         self.n = self.c.op_ctx.allreduce_sum(1 if ok else 0)
+        self.c.vote_s += time.perf_counter() - t0
         go = self.voted and self.n == self.c.ctx.world
         if go:
             self.c.commits_agreed += 1
