@@ -170,6 +170,38 @@ def _sync_side_metrics(args, ctx) -> dict:
                             'path': 'page', 'data': r['data']}}
 
 
+def _guarded_side_metric(args, ctx, headline: dict) -> dict:
+    """The sync side metric must never cost the headline its one JSON line. With N ranks a failure on one rank
+    would leave the others waiting in a collective, so every rank arms the same deadline after a barrier: if
+    the side metric has not finished by then, rank 0 prints the headline (with ``sync_error``) and every rank
+    exits 0. A Python error on a rank is reported the same way."""
+    import threading
+    deadline = float(os.environ.get('UPOW_BENCH_SIDE_DEADLINE_S', '420'))
+    ctx.barrier()
+
+    def fire():
+        if ctx.is_main:
+            print(json.dumps({**headline, 'sync_error': f'side metric unfinished after {deadline:.0f} s'}), flush=True)
+        os._exit(0)
+    timer = threading.Timer(deadline, fire)
+    timer.daemon = True
+    timer.start()
+    fatal, ctx.fatal = ctx.fatal, False  # a failed collective raises here instead of exiting with status 70
+    try:
+        res = _sync_side_metrics(args, ctx)
+    except Exception as e:
+        if not ctx.is_distributed:
+            timer.cancel()
+            return {'sync_error': f'{type(e).__name__}: {e}'[:300]}
+        if ctx.is_main:  # the other ranks may be waiting in a collective: report and leave together
+            print(json.dumps({**headline, 'sync_error': f'{type(e).__name__}: {e}'[:300]}), flush=True)
+        os._exit(0)
+    finally:
+        ctx.fatal = fatal
+    timer.cancel()
+    return res
+
+
 def _free_port() -> int:
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -270,7 +302,7 @@ def main(argv=None):
                 except Exception as e:  # the headline number stands on its own; say why the extra is missing
                     out['verify_error'] = f'{type(e).__name__}: {e}'[:300]
             if args.sync_steps > 0 and out['config']['device'] == 'gpu':
-                out.update(_sync_side_metrics(args, ctx))
+                out.update(_guarded_side_metric(args, ctx, out))
         elif args.mode == 'verify':
             out = bench_verify(args, ctx)
         else:

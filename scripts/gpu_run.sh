@@ -33,8 +33,11 @@
 #   p256n    kernel trace of quad vs oct at 1,024 / 4,096 / 8,192 / 8,300 signatures
 #   soakc1   cluster node + DP miner under torchrun, forced single-rank RCCL, 40 tx/s (node_soak.py --cluster 1)
 #   soakc1k  the same at 1,200 tx/s
+#   verifyenv:NAME:K=V,...  verify bench (median of 3 segments) with extra environment variables
+#   soakc3pin  three pinned cluster soaks alternating with three pinned plain soaks (1,200 tx/s)
 #   clustersync  page-batched sync on a forced single-rank RCCL cluster vs plain, two interleaved pairs
 #   sprofpage  rocprofv3 kernel trace + stats of the page-batched sync (200-tx blocks)
+#   p256sched  P-256 kernels: ILP-first vs occupancy-first scheduling (latency, throughput, trace, counters)
 #   collat   collective latencies over RCCL (scripts/collective_latency.py, forced single rank)
 #   syncprof cProfile of the timed page sync of 0-20-tx blocks
 #   bench:NAME:--a,1,...  bench.py with extra arguments (output bench_NAME.json)
@@ -187,6 +190,26 @@ for s in $STEPS; do
         --threads 8 --fanout1 255 --fanout2 220 --out "$OUT/soak_cluster1_1200.json" > "$OUT/soak_cluster1_1200.log" 2>&1 \
         || { tail -30 "$OUT/soak_cluster1_1200.log"; exit 1; }
       tail -1 "$OUT/soak_cluster1_1200.log" | cut -c1-900 ;;
+    verifyenv:*)
+      # verifyenv:NAME:K=V,K=V  the verify bench (file ledger, median of 3 segments of 10 blocks) with extra env
+      spec=${s#verifyenv:}; name=${spec%%:*}; envs=${spec#*:}
+      rm -rf /tmp/upow_bench_ledger
+      env ${envs//,/ } timeout -k 10 600 python -u bench.py --mode verify --ledger /tmp/upow_bench_ledger --segments 3 \
+        > "$OUT/verifyenv_$name.json" 2> "$OUT/verifyenv_$name.err" || { tail -20 "$OUT/verifyenv_$name.err"; exit 1; }
+      cut -c1-400 "$OUT/verifyenv_$name.json" ;;
+    soakc3pin)
+      # three cluster soaks (forced single-rank RCCL node + DP miner) with the r4e placement: node on CPUs 0-11,
+      # miner and pushing clients on 12-15 (inside the cgroup quota), alternating with three plain pinned soaks
+      for i in 1 2 3; do
+        UPOW_CPU_AFFINITY=0-11 timeout -k 10 420 python -u scripts/node_soak.py --cluster 1 --rate 1200 --seconds 45 \
+          --difficulty 9 --procs 4 --threads 8 --fanout1 255 --fanout2 220 --client-cpus 12-15 \
+          --out "$OUT/soakc_pin_$i.json" > "$OUT/soakc_pin_$i.log" 2>&1 || { tail -30 "$OUT/soakc_pin_$i.log"; exit 1; }
+        tail -1 "$OUT/soakc_pin_$i.log" | cut -c1-400
+        UPOW_CPU_AFFINITY=0-11 timeout -k 10 420 python -u scripts/node_soak.py --rate 1200 --seconds 45 --difficulty 9 \
+          --procs 4 --threads 8 --fanout1 255 --fanout2 220 --client-cpus 12-15 --out "$OUT/soakp_pin_$i.json" \
+          > "$OUT/soakp_pin_$i.log" 2>&1 || { tail -30 "$OUT/soakp_pin_$i.log"; exit 1; }
+        tail -1 "$OUT/soakp_pin_$i.log" | cut -c1-400
+      done ;;
     p256ab)
       # single-block verify latency, quad (4 lanes/signature) vs oct (8 lanes/signature): wall time, kernel
       # trace, and SQ counters for each kernel (own rocprofv3 pass, no other trace domains)
@@ -270,6 +293,27 @@ for s in $STEPS; do
         --steps 2000 --warmup 5 --ledger /tmp/upow_bench_ledger > "$OUT/syncprof.json" 2> "$OUT/syncprof.err" \
         || { tail -20 "$OUT/syncprof.err"; exit 1; }
       cut -c1-300 "$OUT/syncprof.json" ;;
+    p256sched)
+      # A/B of the P-256 kernels' machine scheduling: ILP-first (the build default) vs the occupancy-first
+      # schedule (build-ab/native-p256occ): block latency, batch throughput, kernel trace, SQ counters
+      OCC=$(ls build-ab/native-p256occ/_native*.so)
+      for v in ilp occ; do
+        SO=""; [ $v = occ ] && SO=$OCC
+        UPOW_NATIVE_SO=$SO timeout -k 10 300 python -u scripts/p256_latency.py 4:64,8:64 > "$OUT/p256lat_$v.txt" 2>&1 \
+          || { tail -20 "$OUT/p256lat_$v.txt"; exit 1; }
+        echo "$v latency $(tail -1 "$OUT/p256lat_$v.txt")"
+        UPOW_NATIVE_SO=$SO timeout -k 10 300 python -u scripts/p256_throughput.py > "$OUT/p256thr_$v.txt" 2>&1 \
+          || { tail -20 "$OUT/p256thr_$v.txt"; exit 1; }
+        echo "$v throughput $(tail -1 "$OUT/p256thr_$v.txt")"
+        UPOW_NATIVE_SO=$SO timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/p256kt_$v" -o p256 \
+          --output-format csv -- python3 scripts/p256_latency.py 4:64,8:64 > "$OUT/p256kt_$v.log" 2>&1 \
+          || { tail -20 "$OUT/p256kt_$v.log"; exit 1; }
+        UPOW_NATIVE_SO=$SO timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+          SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_SALU -d "$OUT/p256pmc_$v" -o pmc \
+          --output-format csv -- python3 scripts/p256_latency.py 4:64,8:64 > "$OUT/p256pmc_$v.log" 2>&1 \
+          || { tail -20 "$OUT/p256pmc_$v.log"; exit 1; }
+      done
+      echo p256sched-ok ;;
     bench:*)
       # bench:NAME:--arg,value,...  one bench.py run with extra arguments (file ledger under /tmp)
       spec=${s#bench:}; name=${spec%%:*}; rest=${spec#*:}; rest=${rest//,/ }

@@ -340,6 +340,7 @@ def main():
         ci = client.get(url + '/cluster_info', params={'deep': 'true'}, timeout=120).json()['result']
         reps = ci['replicas']
         replicas = {'world': ci['world'], 'backend': ci['backend'], 'last_resync': ci.get('last_resync'),
+                    'op_stream': ci.get('op_stream'),
                     'agree': len({(r['height'], r['tip_hash'], r['utxo_hash'], r.get('sql_utxo_hash')) for r in reps}) == 1,
                     'replicas': reps}
     miner.terminate()

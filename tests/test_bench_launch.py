@@ -43,3 +43,52 @@ def test_bench_cluster_verify_one_chain_two_ranks():
     reps = out['replicas']
     assert len(reps) == 2 and reps[0]['utxo_hash'] == reps[1]['utxo_hash'] and reps[0]['height'] == reps[1]['height']
     assert abs(out['value'] - 2 * 120 / (out['ms_per_step'] * 2 / 1000)) / out['value'] < 0.02
+
+
+def test_bench_cluster_sync_one_chain_two_ranks():
+    """--mode sync at N=2: ONE chain synced page by page by a two-replica cluster node (chunk signatures sharded
+    over the ranks, every block agreed before commit); both replicas end at the same height and UTXO hash."""
+    rc, out, p = _run(['--gpus', '2', '--mode', 'sync', '--txs', '30', '--steps', '20', '--warmup', '2'],
+                      env_extra={'UPOW_START_DIFFICULTY': '1.0'})
+    assert rc == 0, p.stderr[-3000:]
+    assert out['metric'] == 'sync_tx_per_s' and out['world'] == 2 and out['scaling'] == 'strong'
+    assert len({(r['height'], r['utxo_hash']) for r in out['replicas']}) == 1
+    assert out['page']['page_path'] == 20 and out['op_stream']['commits_agreed'] >= 22
+
+
+GUARD = r'''
+import os, sys, json
+sys.path.insert(0, sys.argv[1])
+import bench
+from upow_amd.parallel.dist import init_from_env
+ctx = init_from_env(backend='gloo', want_gpu=False)
+
+def side(args, ctx):
+    if ctx.rank == 1:
+        raise RuntimeError('boom on rank 1')
+    ctx.barrier()  # rank 0 waits in a collective rank 1 never joins
+    return {'sync_tx_per_s': 1.0}
+bench._sync_side_metrics = side
+os.environ['UPOW_BENCH_SIDE_DEADLINE_S'] = '20'
+res = bench._guarded_side_metric(None, ctx, {'metric': 'headline', 'value': 1})
+print(json.dumps(res), flush=True)
+'''
+
+
+def test_side_metric_failure_keeps_the_headline_line(tmp_path):
+    """A side metric that fails on one rank of N must still leave rank 0's one headline JSON line (with
+    sync_error) and every rank exiting 0, not a job hung in a collective."""
+    script = tmp_path / 'guard.py'
+    script.write_text(GUARD)
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT')}
+    p = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+                        '--master-addr', '127.0.0.1', '--master-port', str(port), str(script), ROOT],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith('{')]
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert len(lines) == 1 and lines[0]['metric'] == 'headline' and 'sync_error' in lines[0], p.stdout
