@@ -29,6 +29,7 @@
 #   soak3pin the same, node pinned to CPUs 0-11 and miner + clients to 12-15 (inside the cgroup quota)
 #   soakenv:NAME:K=V,...  one pinned soak with extra environment variables
 #   verifyaged90 90 blocks on the aged ledger
+#   verifyaged250 250 blocks on the aged ledger, across the retargets at blocks 100 and 200
 #   p256ab   verify latency quad vs oct kernel: wall time, rocprofv3 kernel trace, SQ counters
 #   p256n    kernel trace of quad vs oct at 1,024 / 4,096 / 8,192 / 8,300 signatures
 #   soakc1   cluster node + DP miner under torchrun, forced single-rank RCCL, 40 tx/s (node_soak.py --cluster 1)
@@ -251,6 +252,14 @@ for s in $STEPS; do
         --age-txs 2500000 --steps 90 --warmup 2 > "$OUT/verify_aged90.json" 2> "$OUT/verify_aged90.err" \
         || { tail -20 "$OUT/verify_aged90.err"; exit 1; }
       cut -c1-400 "$OUT/verify_aged90.json" ;;
+    verifyaged250)
+      # the aged ledger, 250 blocks: the headers are mined at the difficulty the chain computes, so the run
+      # crosses the retargets at blocks 100 and 200 on the native path
+      rm -rf /tmp/upow_bench_ledger
+      timeout -k 10 1000 python -u bench.py --mode verify --ledger /tmp/upow_bench_ledger \
+        --age-txs 2500000 --steps 250 --warmup 2 > "$OUT/verify_aged250.json" 2> "$OUT/verify_aged250.err" \
+        || { tail -20 "$OUT/verify_aged250.err"; exit 1; }
+      cut -c1-600 "$OUT/verify_aged250.json" ;;
     soak3)
       # three consecutive node soaks at 1,200 tx/s (node + GPU miner CLI + 4 x 8 pushing clients)
       for i in 1 2 3; do
@@ -276,7 +285,8 @@ for s in $STEPS; do
     sprofpage)
       # rocprofv3 kernel trace of the page-batched sync (200-tx blocks)
       rm -rf /tmp/upow_bench_ledger
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/sprofpage" -o sync -- python3 bench.py --mode sync \
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/sprofpage" -o sync --output-format csv \
+        -- python3 bench.py --mode sync \
         --txs 200 --steps 1000 --warmup 5 --ledger /tmp/upow_bench_ledger > "$OUT/sprofpage.json" 2> "$OUT/sprofpage.err" \
         || { tail -20 "$OUT/sprofpage.err"; exit 1; }
       find "$OUT/sprofpage" -name '*kernel_stats.csv' | head -1 | xargs -r head -25 ;;
