@@ -41,7 +41,7 @@ async def _grow(db, n_tx: int = 3):
     return a, b, block_txs
 
 
-@pytest.mark.parametrize('n_utxo,n_tx', [(4, 4), (5, 5), (2, 3), (2, 0)])
+@pytest.mark.parametrize('n_utxo,n_tx', [(4, 4), (5, 5), (6, 4), (2, 3), (2, 0)])
 def test_layouts_apply_read_and_roll_back(tmp_path, monkeypatch, n_utxo, n_tx):
     monkeypatch.setenv('UPOW_UTXO_FILES', str(n_utxo))
     monkeypatch.setenv('UPOW_TX_FILES', str(n_tx))

@@ -116,7 +116,9 @@ for _t in OUTPUT_TABLES[1:]:
 #   UTXO files.
 _SQL_READERS = None  # Database._off_loop
 # 5 + 5 (eleven files with the main one; SQLite attaches at most ten): ~20 % faster materialisation of an
-# aged ledger than 4 + 4 (profiles/r4/verify_aged_writer_ab_r4g.json, verify_aged60_s55_r4x.json)
+# aged ledger than 4 + 4 (profiles/r4/verify_aged_writer_ab_r4g.json, verify_aged60_s55_r4x.json), 11 %
+# faster than 6 + 4 on the aged ledger (profiles/r5/verify_aged_split_*_r5i.json). 6 + 4 is 12 % faster on a
+# fresh ledger (three interleaved pairs, profiles/r5/verify_split_*): the aged ledger is what a node runs.
 UTXO_FILES_DEFAULT = 5
 TX_FILES_DEFAULT = 5
 ROUTED = ('unspent_outputs', 'transactions')
