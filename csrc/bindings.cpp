@@ -224,6 +224,17 @@ PYBIND11_MODULE(_native, m) {
         return py::bytes(reinterpret_cast<const char*>(out), 64);
     });
 
+    // s^-1 * 2^256 mod n (32 bytes little-endian in and out, s in [1, n)): the verifier's divsteps inverse,
+    // exposed for its differential test against Python's pow
+    m.def("p256_scalar_inv_mont", [](py::bytes s_le) -> py::bytes {
+        const std::string s = s_le;
+        if (s.size() != 32) throw std::invalid_argument("need 32 bytes little-endian");
+        uint64_t in[4], out[4];
+        std::memcpy(in, s.data(), 32);
+        p256_scalar_inv_mont_host(out, in);
+        return py::bytes(reinterpret_cast<const char*>(out), 32);
+    });
+
     m.def("p256_sign", [](py::bytes d_be, py::bytes digest) -> py::object {
         std::string d = d_be, h = digest;
         if (d.size() != 32 || h.size() != 32) throw std::invalid_argument("need 32-byte key and digest");

@@ -42,6 +42,8 @@ std::vector<uint8_t> p256_verify_host(const uint8_t* items, int64_t n, int threa
 uint8_t p256_verify_one_host64(const uint8_t* item);
 // p256.hip's fixed-base table: 32 x 256 affine points, each x[8] y[8] little-endian u32 words
 const void* p256_g_table_host();
+// s^-1 * 2^256 mod n for s in [1, n) (little-endian 64-bit limbs): the divsteps inverse of p256_field.h
+void p256_scalar_inv_mont_host(uint64_t out[4], const uint64_t s[4]);
 std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n);
 void p256_decompress_host(const uint8_t* in33, int64_t n, uint8_t* out64, uint8_t* ok);
 void p256_decompress_gpu(const uint8_t* in33, int64_t n, uint8_t* out64, uint8_t* ok);

@@ -12,7 +12,8 @@
 //    scratch (1.5-2 KB per signature does not fit LDS at useful occupancy) -> 255 doublings + 52
 //    additions (unsigned 4-bit windows: 252 + 64);
 //  * no field inversion: x(R) == r is tested as X == r*Z^2 (and (r+n)*Z^2 when r+n < p);
-//  * s^-1 mod n by a binary extended Euclid (p256_field.h sc_inv_bgcd_mont);
+//  * s^-1 mod n by Bernstein-Yang divsteps (p256_field.h sc_inv_safegcd_mont: 20 rounds of 30, no
+//    divergence; the binary extended Euclid it replaced, sc_inv_bgcd_mont, stays for the A/B build);
 //  * status per item: 1 valid, 0 invalid, 2 public key not on curve, 3 r/s out of [1, n]
 //    (fastecdsa raises for 2/3; the Python layer turns them into EcdsaError).
 #include <hip/hip_runtime.h>
@@ -87,6 +88,13 @@ static const std::vector<aff>& g_table() {
 
 const void* p256_g_table_host() { return g_table().data(); }
 
+void p256_scalar_inv_mont_host(uint64_t out[4], const uint64_t s[4]) {
+    fe a;
+    std::memcpy(a.v, s, 32);
+    const fe r = sc_inv_safegcd_mont(a);
+    std::memcpy(out, r.v, 32);
+}
+
 UPOW_HD jac mul_g(const fe& k, const aff* tab) {
     jac acc = jac_inf();
     for (int j = 0; j < kGWin; ++j) {
@@ -108,6 +116,11 @@ struct VerifyItem {  // 160 bytes, wire byte order
 };
 static_assert(sizeof(VerifyItem) == 160, "VerifyItem layout");
 
+// 1 builds the previous inverse (binary Euclid) for the A/B (_build.py variant 'p256bgcd')
+#ifndef UPOW_P256_INV_BGCD
+#define UPOW_P256_INV_BGCD 0
+#endif
+
 UPOW_HD uint8_t verify_prologue(const VerifyItem& it, aff& q, fe& r, fe& u1, fe& u2) {
     q.x = fe_from_le(it.qx);
     q.y = fe_from_le(it.qy);
@@ -120,7 +133,7 @@ UPOW_HD uint8_t verify_prologue(const VerifyItem& it, aff& q, fe& r, fe& u1, fe&
     if (fe_is_zero(s) || (fe_geq(s, n) && !fe_eq(s, n))) return 3;
     if (fe_eq(s, n)) return 0;  // s has no inverse mod n
     const fe e = sc_reduce(fe_from_be(it.e));
-    const fe w_m = sc_inv_bgcd_mont(s);         // s^-1 * R
+    const fe w_m = UPOW_P256_INV_BGCD ? sc_inv_bgcd_mont(s) : sc_inv_safegcd_mont(s);  // s^-1 * R
     u1 = sc_mont_mul(e, w_m);                   // e * s^-1
     u2 = sc_mont_mul(sc_reduce(r), w_m);        // r * s^-1
     return 255;                                 // continue

@@ -410,6 +410,155 @@ UPOW_HD fe sc_inv_bgcd_mont(const fe& a) {
     return y;
 }
 
+// a^-1 * R mod n by Bernstein-Yang divsteps (the "safegcd" recurrence, delta starting at 1/2). Values are
+// in signed 30-bit limbs (nine int32, limb 8 signed). 20 rounds of 30 divsteps cover the 590 that any
+// 256-bit input needs; each round runs its 30 divsteps on the low 32 bits of f and g alone (they decide
+// every branch), collecting them into a 2x2 matrix scaled by 2^30, then applies the matrix to the full
+// (f, g) and to (d, e), which track f = d*a*R^-1 and g = e*a*R^-1 (mod n): e starts at R, so d ends at
+// +-a^-1*R, the Montgomery form verify_prologue wants. Fixed trip count, no data-dependent branches:
+// the wave never diverges. Cost per round: 30 divsteps of ~20 full-rate 32-bit ops, and 36 + 54 signed
+// 32x32->64 multiply-adds for the matrix products; about a third of the binary Euclid above.
+struct s30 { int32_t v[9]; };
+static constexpr uint32_t kM30 = 0x3fffffffu;
+static constexpr uint32_t kN30Inv = 0x11ff43b1u;  // n^-1 mod 2^30
+
+UPOW_HD s30 s30_from_fe(const fe& a) {
+    s30 r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const int bit = 30 * i, w = bit >> 5, sh = bit & 31;
+        uint32_t x = a.v[w] >> sh;
+        if (sh > 2 && w + 1 < 8) x |= a.v[w + 1] << (32 - sh);
+        r.v[i] = int32_t(x & kM30);
+    }
+    return r;
+}
+// limbs 0..7 in [0, 2^30), limb 8 in [0, 2^16) (a canonical value below 2^256)
+UPOW_HD fe fe_from_s30(const s30& a) {
+    fe r;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        const int bit = 32 * w, i = bit / 30, sh = bit % 30;
+        uint32_t x = uint32_t(a.v[i]) >> sh;
+        if (i + 1 < 9) x |= uint32_t(a.v[i + 1]) << (30 - sh);
+        if (sh > 28 && i + 2 < 9) x |= uint32_t(a.v[i + 2]) << (60 - sh);
+        r.v[w] = x;
+    }
+    return r;
+}
+
+struct DivMatrix { int32_t u, v, q, r; };
+// 30 divsteps on the low words: returns the new zeta = -(delta + 1/2)
+UPOW_HD int32_t divsteps_30(int32_t zeta, uint32_t f, uint32_t g, DivMatrix& t) {
+    uint32_t u = 1, v = 0, q = 0, r = 1;
+#pragma unroll
+    for (int i = 0; i < 30; ++i) {
+        uint32_t c1 = uint32_t(zeta >> 31);  // all ones when delta > 0
+        const uint32_t c2 = 0u - (g & 1u);   // all ones when g is odd
+        // g odd: g += (delta > 0 ? -f : f), and the same on the matrix rows
+        g += ((f ^ c1) - c1) & c2;
+        q += ((u ^ c1) - c1) & c2;
+        r += ((v ^ c1) - c1) & c2;
+        c1 &= c2;  // delta > 0 and g odd: (f, g) <- (g, g - f), delta <- 1 - delta
+        zeta = int32_t((uint32_t(zeta) ^ c1) - 1u);
+        f += g & c1;
+        u += q & c1;
+        v += r & c1;
+        g >>= 1;
+        u <<= 1;
+        v <<= 1;
+    }
+    t = DivMatrix{int32_t(u), int32_t(v), int32_t(q), int32_t(r)};
+    return zeta;
+}
+
+// (f, g) <- (u f + v g, q f + r g) / 2^30 (exact)
+UPOW_HD void s30_update_fg(s30& f, s30& g, const DivMatrix& t) {
+    int64_t cf = int64_t(t.u) * f.v[0] + int64_t(t.v) * g.v[0];
+    int64_t cg = int64_t(t.q) * f.v[0] + int64_t(t.r) * g.v[0];
+    cf >>= 30;
+    cg >>= 30;
+#pragma unroll
+    for (int i = 1; i < 9; ++i) {
+        cf += int64_t(t.u) * f.v[i] + int64_t(t.v) * g.v[i];
+        cg += int64_t(t.q) * f.v[i] + int64_t(t.r) * g.v[i];
+        f.v[i - 1] = int32_t(uint32_t(cf) & kM30);
+        g.v[i - 1] = int32_t(uint32_t(cg) & kM30);
+        cf >>= 30;
+        cg >>= 30;
+    }
+    f.v[8] = int32_t(cf);
+    g.v[8] = int32_t(cg);
+}
+
+// (d, e) <- (u d + v e, q d + r e) / 2^30 mod n, keeping both in (-2n, n): a multiple of n is added to
+// each numerator to clear its low 30 bits (plus n times the matrix row when d or e is negative)
+UPOW_HD void s30_update_de(s30& d, s30& e, const DivMatrix& t, const s30& n) {
+    const int32_t sd = d.v[8] >> 31, se = e.v[8] >> 31;
+    int32_t md = (t.u & sd) + (t.v & se);
+    int32_t me = (t.q & sd) + (t.r & se);
+    int64_t cd = int64_t(t.u) * d.v[0] + int64_t(t.v) * e.v[0];
+    int64_t ce = int64_t(t.q) * d.v[0] + int64_t(t.r) * e.v[0];
+    md -= int32_t((kN30Inv * uint32_t(cd) + uint32_t(md)) & kM30);
+    me -= int32_t((kN30Inv * uint32_t(ce) + uint32_t(me)) & kM30);
+    cd += int64_t(n.v[0]) * md;
+    ce += int64_t(n.v[0]) * me;
+    cd >>= 30;
+    ce >>= 30;
+#pragma unroll
+    for (int i = 1; i < 9; ++i) {
+        cd += int64_t(t.u) * d.v[i] + int64_t(t.v) * e.v[i] + int64_t(n.v[i]) * md;
+        ce += int64_t(t.q) * d.v[i] + int64_t(t.r) * e.v[i] + int64_t(n.v[i]) * me;
+        d.v[i - 1] = int32_t(uint32_t(cd) & kM30);
+        e.v[i - 1] = int32_t(uint32_t(ce) & kM30);
+        cd >>= 30;
+        ce >>= 30;
+    }
+    d.v[8] = int32_t(cd);
+    e.v[8] = int32_t(ce);
+}
+
+// carry-normalise: limbs 0..7 into [0, 2^30), the sign in limb 8
+UPOW_HD void s30_carry(s30& a) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        a.v[i + 1] += a.v[i] >> 30;
+        a.v[i] = int32_t(uint32_t(a.v[i]) & kM30);
+    }
+}
+// a += n & mask (limb-wise), then carry
+UPOW_HD void s30_add_masked(s30& a, const s30& n, int32_t mask) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) a.v[i] += n.v[i] & mask;
+    s30_carry(a);
+}
+
+UPOW_HD fe sc_inv_safegcd_mont(const fe& a) {
+    const s30 n = s30_from_fe(fe_const_n());
+    s30 f = n, g = s30_from_fe(a), d{{0, 0, 0, 0, 0, 0, 0, 0, 0}}, e = s30_from_fe(fe{P256_RN});
+    int32_t zeta = -1;
+    for (int round = 0; round < 20; ++round) {
+        DivMatrix t;
+        zeta = divsteps_30(zeta, uint32_t(f.v[0]) | (uint32_t(f.v[1]) << 30), uint32_t(g.v[0]) | (uint32_t(g.v[1]) << 30), t);
+        s30_update_de(d, e, t, n);
+        s30_update_fg(f, g, t);
+    }
+    // g = 0 and f = +-1 (f's sign is its top limb's): d = +-a^-1*R in (-2n, n)
+    const int32_t sf = f.v[8] >> 31;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) d.v[i] = (d.v[i] ^ sf) - sf;
+    s30_carry(d);                        // (-n, 2n)
+    s30_add_masked(d, n, d.v[8] >> 31);  // [0, 2n)
+    s30 t = d;                           // d - n, kept when non-negative
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t.v[i] -= n.v[i];
+    s30_carry(t);
+    const bool ge = t.v[8] >= 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) d.v[i] = ge ? t.v[i] : d.v[i];
+    return fe_from_s30(d);
+}
+
 // ------------------------------------------------------------------------------------------------
 // points
 // ------------------------------------------------------------------------------------------------

@@ -251,20 +251,6 @@ void load_be(uint64_t r[4], const uint8_t* b) {
 
 bool is_zero4(const uint64_t a[4]) { return (a[0] | a[1] | a[2] | a[3]) == 0; }
 
-// a^(n-2) * R mod n for a in Montgomery form (Fermat inverse, left-to-right binary)
-void sc_inv_mont(uint64_t r[4], const uint64_t a[4], const Mod& N) {
-    uint64_t e[4];
-    const uint64_t two[4] = {2, 0, 0, 0};
-    sub4(e, N.m, two);
-    uint64_t acc[4];
-    std::memcpy(acc, N.one, 32);
-    for (int i = 255; i >= 0; --i) {
-        mont_mul(acc, acc, acc, N);
-        if ((e[i / 64] >> (i % 64)) & 1) mont_mul(acc, acc, a, N);
-    }
-    std::memcpy(r, acc, 32);
-}
-
 }  // namespace
 
 uint8_t p256_verify_one_host64(const uint8_t* item) {
@@ -297,9 +283,8 @@ uint8_t p256_verify_one_host64(const uint8_t* item) {
     uint64_t r_red[4];
     std::memcpy(r_red, r, 32);
     if (geq(r_red, kN)) sub4(r_red, r_red, kN);
-    uint64_t sm[4], wm[4], u1[4], u2[4];
-    mont_mul(sm, s, N.rr, N);   // s * R
-    sc_inv_mont(wm, sm, N);     // s^-1 * R
+    uint64_t wm[4], u1[4], u2[4];
+    p256_scalar_inv_mont_host(wm, s);  // s^-1 * R (divsteps, p256_field.h)
     mont_mul(u1, e, wm, N);     // e * s^-1
     mont_mul(u2, r_red, wm, N); // r * s^-1
     // u2 * Q: 4-bit fixed window

@@ -38,7 +38,8 @@
 #   soakc3pin  three pinned cluster soaks alternating with three pinned plain soaks (1,200 tx/s)
 #   clustersync  page-batched sync on a forced single-rank RCCL cluster vs plain, two interleaved pairs
 #   sprofpage  rocprofv3 kernel trace + stats of the page-batched sync (200-tx blocks)
-#   p256sched  P-256 kernels: ILP-first vs occupancy-first scheduling (latency, throughput, trace, counters)
+#   p256ab:VARIANT  P-256 kernels: the default build vs build-ab/native-VARIANT (latency, throughput, trace, counters)
+#   isarates  issue cost of v_mad_u64_u32 / carry adds / 64-bit adds / f64 FMA / field products (scripts/isa_rates.hip)
 #   collat   collective latencies over RCCL (scripts/collective_latency.py, forced single rank)
 #   syncprof cProfile of the timed page sync of 0-20-tx blocks
 #   bench:NAME:--a,1,...  bench.py with extra arguments (output bench_NAME.json)
@@ -303,12 +304,14 @@ for s in $STEPS; do
         --steps 2000 --warmup 5 --ledger /tmp/upow_bench_ledger > "$OUT/syncprof.json" 2> "$OUT/syncprof.err" \
         || { tail -20 "$OUT/syncprof.err"; exit 1; }
       cut -c1-300 "$OUT/syncprof.json" ;;
-    p256sched)
-      # A/B of the P-256 kernels' machine scheduling: ILP-first (the build default) vs the occupancy-first
-      # schedule (build-ab/native-p256occ): block latency, batch throughput, kernel trace, SQ counters
-      OCC=$(ls build-ab/native-p256occ/_native*.so)
-      for v in ilp occ; do
-        SO=""; [ $v = occ ] && SO=$OCC
+    p256ab:*)
+      # p256ab:VARIANT  A/B of the P-256 kernels: the build default ("cur") against an A/B build
+      # (build-ab/native-VARIANT, upow_amd/_build.py AB_VARIANTS): block latency, batch throughput, kernel
+      # trace, SQ counters (own rocprofv3 pass, no other trace domains)
+      var=${s#p256ab:}
+      ALT=$(ls build-ab/native-$var/_native*.so)
+      for v in cur $var; do
+        SO=""; [ $v = $var ] && SO=$ALT
         UPOW_NATIVE_SO=$SO timeout -k 10 300 python -u scripts/p256_latency.py 4:64,8:64 > "$OUT/p256lat_$v.txt" 2>&1 \
           || { tail -20 "$OUT/p256lat_$v.txt"; exit 1; }
         echo "$v latency $(tail -1 "$OUT/p256lat_$v.txt")"
@@ -323,7 +326,11 @@ for s in $STEPS; do
           --output-format csv -- python3 scripts/p256_latency.py 4:64,8:64 > "$OUT/p256pmc_$v.log" 2>&1 \
           || { tail -20 "$OUT/p256pmc_$v.log"; exit 1; }
       done
-      echo p256sched-ok ;;
+      echo p256ab-ok ;;
+    isarates)
+      # issue cost of the candidate big-integer instructions (scripts/isa_rates.hip, built into build-ab/)
+      timeout -k 10 120 ./build-ab/isa_rates > "$OUT/isa_rates.json" 2>&1 || { cat "$OUT/isa_rates.json"; exit 1; }
+      cat "$OUT/isa_rates.json" ;;
     bench:*)
       # bench:NAME:--arg,value,...  one bench.py run with extra arguments (file ledger under /tmp)
       spec=${s#bench:}; name=${spec%%:*}; rest=${spec#*:}; rest=${rest//,/ }

@@ -31,6 +31,26 @@ def test_native_sign_pubkey_match_oracle(native):
     assert op.sign(b'sample', RFC6979_D) == o.sign(b'sample', RFC6979_D)
 
 
+def test_scalar_inverse_divsteps_matches_pow(native):
+    """s^-1 * 2^256 mod n by the verifier's divsteps inverse (p256_field.h sc_inv_safegcd_mont) against
+    Python's pow, on random scalars and on the shapes that stress a gcd: small values, powers of two, n - k,
+    values just below 2^256 reduced, and runs of ones."""
+    from upow_amd.ops.native import lib
+    inv = lib().p256_scalar_inv_mont
+    n = o.N
+    R = (1 << 256) % n
+    rng = random.Random(11)
+    cases = [1, 2, 3, n - 1, n - 2, (n - 1) // 2, (1 << 255) % n, (1 << 256) - 1 - n, (1 << 128) - 1]
+    cases += [1 << k for k in range(256)] + [n - (1 << k) for k in range(255)]
+    cases += [((1 << k) - 1) % n for k in range(1, 257)] + [rng.randrange(1, n) for _ in range(3000)]
+    for s in cases:
+        s %= n
+        if s == 0:
+            continue
+        got = int.from_bytes(inv(s.to_bytes(32, 'little')), 'little')
+        assert got == pow(s, -1, n) * R % n, hex(s)
+
+
 def test_verify_semantics(native):
     d = 12345
     q = o.get_public_key(d)

@@ -62,19 +62,21 @@ CLANGXX = '/opt/rocm/llvm/bin/clang++'
 # default (occupancy-first) scheduler fills with s_nop: 6,865 of the quad verify kernel's 42,629 static
 # instructions. The ILP-first machine scheduler interleaves independent products instead (1,810 s_nop): the
 # block-latency kernels run one wave per SIMD, so the extra registers cost them nothing; the batch kernels
-# keep their __launch_bounds__ occupancy. 'p256occ' builds the old schedule for the A/B
-# (build-ab/native-p256occ, loaded through UPOW_NATIVE_SO).
+# keep their __launch_bounds__ occupancy.
 DEVICE_FLAGS = {'p256': ['-mllvm', '-amdgpu-sched-strategy=max-ilp']}
+# A/B builds of the P-256 kernels (build-ab/native-<variant>, shipped to the GPU box and loaded through
+# UPOW_NATIVE_SO): 'p256occ' the occupancy-first schedule, 'p256bgcd' the binary-Euclid s^-1
+AB_VARIANTS = {'p256occ': {'p256': []}, 'p256bgcd': {'p256': DEVICE_FLAGS['p256'] + ['-DUPOW_P256_INV_BGCD=1']}}
 
 
 def _device_flags(src: Path, variant: str) -> list:
-    if variant == 'p256occ':
-        return []
+    if variant in AB_VARIANTS:
+        return AB_VARIANTS[variant].get(src.stem, DEVICE_FLAGS.get(src.stem, []))
     return DEVICE_FLAGS.get(src.stem, [])
 
 
 def _build_dir(variant: str) -> Path:
-    if variant == 'p256occ':  # shipped to the GPU box for the A/B (./build is not)
+    if variant in AB_VARIANTS:  # shipped to the GPU box for the A/B (./build is not)
         return ROOT / 'build-ab' / f'native-{variant}'
     return BUILD if variant == 'release' else ROOT / 'build' / f'native-{variant}'
 
@@ -134,7 +136,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--force', action='store_true')
     ap.add_argument('-j', '--jobs', type=int, default=min(8, os.cpu_count() or 4))
-    ap.add_argument('--variant', choices=['release', 'asan', 'tsan', 'p256occ'], default='release')
+    ap.add_argument('--variant', choices=['release', 'asan', 'tsan', *AB_VARIANTS], default='release')
     a = ap.parse_args(argv)
     build(force=a.force, jobs=a.jobs, variant=a.variant)
 
