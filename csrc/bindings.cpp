@@ -324,6 +324,39 @@ PYBIND11_MODULE(_native, m) {
         { py::gil_scoped_release rel; o = utxo_erase(h, p, n); }
         return py::bytes(reinterpret_cast<const char*>(o.data()), o.size());
     });
+    // ins: a list of (records n x 40, payloads n x 80 or None) groups; all groups carry payloads or none do
+    m.def("utxo_apply_async", [recs_arg](int64_t h, py::list ins, py::buffer dels) {
+        int64_t n_del;
+        const uint8_t* pd = recs_arg(dels, n_del);
+        std::vector<UtxoSeg> segs;
+        std::vector<py::buffer_info> keep;
+        keep.reserve(2 * ins.size());
+        int with_pay = -1;
+        for (py::handle item : ins) {
+            py::tuple t = item.cast<py::tuple>();
+            int64_t n;
+            const uint8_t* pr = recs_arg(t[0].cast<py::buffer>(), n);
+            const uint8_t* pp = nullptr;
+            if (!t[1].is_none()) {
+                keep.push_back(t[1].cast<py::buffer>().request());
+                if (keep.back().size * keep.back().itemsize != n * 80) throw std::invalid_argument("payload must be n x 80 bytes");
+                pp = static_cast<const uint8_t*>(keep.back().ptr);
+            }
+            if (n && with_pay >= 0 && with_pay != (pp != nullptr)) throw std::invalid_argument("payloads for all groups or none");
+            if (n) with_pay = pp != nullptr;
+            segs.push_back(UtxoSeg{pr, pp, n});
+        }
+        uint32_t prev[3];
+        bool had;
+        { py::gil_scoped_release rel; had = utxo_apply_async(h, segs, with_pay == 1, pd, n_del, prev); }
+        return py::make_tuple(had, prev[0], prev[1], prev[2]);
+    }, py::arg("h"), py::arg("ins"), py::arg("dels"));
+    m.def("utxo_apply_wait", [](int64_t h) {
+        uint32_t r[3];
+        bool had;
+        { py::gil_scoped_release rel; had = utxo_apply_wait(h, r); }
+        return py::make_tuple(had, r[0], r[1], r[2]);  // (pending, no free slot, duplicates, erased)
+    });
     m.def("utxo_dump", [](int64_t h) {
         std::vector<uint8_t> o;
         { py::gil_scoped_release rel; o = utxo_dump(h, nullptr); }

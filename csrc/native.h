@@ -65,6 +65,12 @@ uint64_t utxo_insert(int64_t h, const uint8_t* recs, int64_t n, const uint8_t* p
 std::vector<uint8_t> utxo_probe(int64_t h, const uint8_t* recs, int64_t n);  // tag or 0xff
 std::vector<uint8_t> utxo_lookup(int64_t h, const uint8_t* recs, int64_t n, std::vector<uint8_t>& payload_out);
 std::vector<uint8_t> utxo_erase(int64_t h, const uint8_t* recs, int64_t n);  // 1 if erased
+// queue one block's inserts + erases on the node stream and return; prev = the previous async apply's
+// (no free slot, duplicates, erased) counters, collected first (returns whether there was one)
+struct UtxoSeg { const uint8_t* recs; const uint8_t* pay; int64_t n; };  // n x 40 records, n x 80 payloads
+bool utxo_apply_async(int64_t h, const std::vector<UtxoSeg>& ins, bool with_pay, const uint8_t* del, int64_t n_del,
+                      uint32_t prev[3]);
+bool utxo_apply_wait(int64_t h, uint32_t out[3]);  // collect the pending async apply's counters
 std::vector<uint8_t> utxo_dump(int64_t h, std::vector<uint8_t>* payload_out);
 // K14: live outputs whose payload address equals addr[0:len] and whose tag is in tag_mask
 std::vector<uint8_t> utxo_address_scan(int64_t h, const uint8_t* addr, uint32_t len, uint32_t tag_mask,

@@ -352,8 +352,125 @@ int64_t utxo_create(uint32_t log2_cap) {
     return h;
 }
 
+// Asynchronous index update of one committed block (the block path's last GPU step): the inputs are
+// packed into pinned memory owned by the table, ONE H2D copy, the insert and the erase launch and a D2H
+// of their three counters are queued on the node stream and an event is recorded; the call returns
+// without waiting. Every later pass on the table is queued behind it on the same stream, so it reads the
+// updated table with no host round trip in between; the counters are collected (event sync) by
+// utxo_apply_wait, or by the next utxo_apply_async before it reuses the buffers.
+struct AsyncApply {
+    hipEvent_t ev = nullptr;
+    uint8_t* host = nullptr;
+    size_t host_cap = 0;
+    uint8_t* dev = nullptr;
+    size_t dev_cap = 0;
+    const uint32_t* res = nullptr;  // pinned: (entries with no free slot, duplicates skipped, erased)
+    bool live = false;
+};
+static std::unordered_map<int64_t, AsyncApply> g_async;  // by table handle, under g_ut_mu
+
+static bool async_collect(AsyncApply& a, uint32_t out[3]) {
+    out[0] = out[1] = out[2] = 0;
+    if (!a.live) return false;
+    a.live = false;
+    uck(hipEventSynchronize(a.ev), "utxo async apply");
+    out[0] = a.res[0];
+    out[1] = a.res[1];
+    out[2] = a.res[2];
+    return true;
+}
+
+static void async_release(int64_t h) {  // under g_ut_mu
+    auto it = g_async.find(h);
+    if (it == g_async.end()) return;
+    uint32_t r[3];
+    try {
+        async_collect(it->second, r);
+    } catch (...) {
+    }
+    if (it->second.ev) (void)hipEventDestroy(it->second.ev);
+    if (it->second.host) (void)hipHostFree(it->second.host);
+    if (it->second.dev) (void)hipFree(it->second.dev);
+    g_async.erase(it);
+}
+
+static size_t align256(size_t n) { return (n + 255) & ~size_t(255); }
+
+bool utxo_apply_async(int64_t h, const std::vector<UtxoSeg>& ins, bool with_pay, const uint8_t* del, int64_t n_del,
+                      uint32_t prev[3]) {
+    int64_t n_ins = 0;
+    for (const UtxoSeg& g : ins) n_ins += g.n;
+    const bool ins_pay = with_pay && n_ins > 0;
+    std::lock_guard<std::mutex> lk(g_ut_mu);
+    UtxoTableDev& t = table(h);
+    AsyncApply& a = g_async[h];
+    const bool had = async_collect(a, prev);
+    const size_t off_pay = align256(size_t(n_ins) * sizeof(UtxoKeyRec));
+    const size_t off_del = off_pay + align256(ins_pay ? size_t(n_ins) * sizeof(UtxoPayload) : 0);
+    const size_t off_cnt = off_del + align256(size_t(n_del) * sizeof(UtxoKeyRec));
+    const size_t off_st = off_cnt + 256;  // erase status bytes (device only)
+    const size_t dev_need = off_st + align256(size_t(n_del));
+    if (!a.ev) uck(hipEventCreateWithFlags(&a.ev, hipEventDisableTiming), "hipEventCreate");
+    if (off_cnt + 256 > a.host_cap) {
+        if (a.host) uck(hipHostFree(a.host), "hipHostFree");  // the previous apply was collected above
+        a.host = nullptr;
+        a.host_cap = std::max<size_t>(off_cnt + 256, size_t(4) << 20) * 2;
+        uck(hipHostMalloc(reinterpret_cast<void**>(&a.host), a.host_cap, hipHostMallocDefault), "hipHostMalloc");
+    }
+    if (dev_need > a.dev_cap) {
+        if (a.dev) {
+            node_sync("utxo async regrow");
+            uck(hipFree(a.dev), "hipFree");
+        }
+        a.dev = nullptr;
+        a.dev_cap = std::max<size_t>(dev_need, size_t(4) << 20) * 2;
+        uck(hipMalloc(reinterpret_cast<void**>(&a.dev), a.dev_cap), "hipMalloc");
+    }
+    size_t at = 0;  // the groups land back to back: no concatenation on the caller's side
+    for (const UtxoSeg& g : ins) {
+        if (!g.n) continue;
+        std::memcpy(a.host + at * sizeof(UtxoKeyRec), g.recs, size_t(g.n) * sizeof(UtxoKeyRec));
+        if (ins_pay) std::memcpy(a.host + off_pay + at * sizeof(UtxoPayload), g.pay, size_t(g.n) * sizeof(UtxoPayload));
+        at += size_t(g.n);
+    }
+    if (n_del) std::memcpy(a.host + off_del, del, size_t(n_del) * sizeof(UtxoKeyRec));
+    hipStream_t st = node_stream();
+    uck(hipMemcpyAsync(a.dev, a.host, off_cnt, hipMemcpyHostToDevice, st), "async apply h2d");
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(a.dev + off_cnt);
+    uck(hipMemsetAsync(cnt, 0, 16, st), "async apply memset");
+    if (n_ins) {
+        hipLaunchKernelGGL(utxo_insert_kernel, dim3(int((n_ins + 255) / 256)), dim3(256), 0, st, t.tab, t.pay, t.cap - 1,
+                           reinterpret_cast<const UtxoKeyRec*>(a.dev),
+                           ins_pay ? reinterpret_cast<const UtxoPayload*>(a.dev + off_pay) : nullptr, n_ins, cnt);
+        uck(hipGetLastError(), "utxo_insert_kernel (async)");
+    }
+    if (n_del) {
+        hipLaunchKernelGGL(utxo_erase_kernel, dim3(int((n_del + 255) / 256)), dim3(256), 0, st, t.tab, t.cap - 1,
+                           reinterpret_cast<const UtxoKeyRec*>(a.dev + off_del), n_del, a.dev + off_st, cnt + 2);
+        uck(hipGetLastError(), "utxo_erase_kernel (async)");
+    }
+    uint32_t* res = reinterpret_cast<uint32_t*>(a.host + off_cnt);
+    uck(hipMemcpyAsync(res, cnt, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st), "async apply d2h");
+    uck(hipEventRecord(a.ev, st), "hipEventRecord");
+    a.res = res;
+    a.live = true;
+    return had;
+}
+
+bool utxo_apply_wait(int64_t h, uint32_t out[3]) {
+    std::lock_guard<std::mutex> lk(g_ut_mu);
+    (void)table(h);
+    auto it = g_async.find(h);
+    if (it == g_async.end()) {
+        out[0] = out[1] = out[2] = 0;
+        return false;
+    }
+    return async_collect(it->second, out);
+}
+
 void utxo_destroy(int64_t h) {
     std::lock_guard<std::mutex> lk(g_ut_mu);
+    async_release(h);
     auto it = g_tables.find(h);
     if (it == g_tables.end()) return;
     (void)hipFree(it->second.tab);

@@ -220,3 +220,49 @@ def test_scan_fingerprint_after_rehash_and_tombstone_reuse(gpu):
             rg, pg, tg = g.address_outputs(o, (0,), sel)
             rh, ph, th = h.address_outputs(o, (0,), sel)
             assert rg.tobytes() == rh.tobytes() and pg.tobytes() == ph.tobytes() and tg == th
+
+
+def _apply_blocks(backend):
+    """Chained blocks through UtxoIndex.apply_block (the block path's post-commit update; on the GPU an
+    async insert + erase queued on the node stream): spends of earlier blocks' outputs, a spend of an output
+    created in the same block, lookups between blocks, a duplicate insert, then a rehash while an apply
+    is pending."""
+    rng = random.Random(21)
+    idx = UtxoIndex(backend=backend)
+    live = []
+    for b in range(12):
+        new = _keys(900, 100 + b)
+        pay = make_payload([rng.randrange(1, 1 << 40) for _ in new], [bytes([42]) + rng.randbytes(32) for _ in new])
+        spend = [live.pop(rng.randrange(len(live))) for _ in range(min(len(live), 600))] + new[:3]
+        idx.apply_block([(pack_records(new[:700], 0), pay[:700]), (pack_records(new[700:], 0), pay[700:])],
+                        pack_records(spend, 0))
+        live += new[3:]
+        # the next block's lookup sees this block's writes
+        t, p = idx.lookup(live[-50:] + spend[:20])
+        assert (t[:50] == 0).all() and (t[50:] == MISSING).all()
+    before = idx.duplicates
+    idx.apply_block([(pack_records(live[:5], 0), None)], np.zeros((0, 40), np.uint8))  # already live
+    assert len(idx) == len(live)
+    assert idx.duplicates == before + 5
+    # a rehash (growth) right after an apply that is still pending
+    big = _keys(700000, 999)
+    idx.apply_block([(pack_records(big, 1), None)], pack_records(live[:100], 0))
+    idx.insert(_keys(10, 1000), 2)
+    assert len(idx) == len(live) - 100 + len(big) + 10
+    assert (idx.probe(live[100:200]) == 0).all() and (idx.probe(live[:100]) == MISSING).all()
+    assert (idx.probe(big[::1000]) == 1).all()
+    return idx
+
+
+def test_apply_block_host():
+    _apply_blocks('host')
+
+
+@pytest.mark.gpu
+def test_apply_block_gpu_async_matches_host(gpu):
+    g, h = _apply_blocks('gpu'), _apply_blocks('host')
+    rg, pg = g.records_payload()
+    rh, ph = h.records_payload()
+    og = np.lexsort(rg.T[::-1])
+    oh = np.lexsort(rh.T[::-1])
+    assert (rg[og] == rh[oh]).all() and (pg[og].view(np.uint8) == ph[oh].view(np.uint8)).all()

@@ -2151,11 +2151,9 @@ class Database:
             # erase launch when the page ends (or before anything reads the index)
             self.utxo.defer_block([(recs, pay), (cb_recs, cb_pay)], spent if n_in else spent[:0])
         else:
-            self.utxo.insert_records(recs, pay)
-            if len(cb_keys):
-                self.utxo.insert_records(cb_recs, cb_pay)
-            if n_in:
-                self.utxo.erase_records(spent)
+            # one H2D copy + insert + erase launch queued on the node stream, not waited for: the next block's
+            # input lookup runs behind them on the same stream
+            self.utxo.apply_block([(recs, pay), (cb_recs, cb_pay)], spent if n_in else spent[:0])
         stamp()
         tip = dict(b)
         tip['difficulty'], tip['reward'] = Decimal(tip['difficulty']), Decimal(tip['reward'])

@@ -177,12 +177,40 @@ class _GpuBackend:
         self.h = self.L.utxo_create(log2_cap)
         self.count = 0
         self.tombs = 0
+        self.pending = None  # (inserts, erases) of an async block apply not yet booked
 
     def __del__(self):
         try:
             self.L.utxo_destroy(self.h)
         except Exception:
             pass
+
+    def apply_async(self, ins: Sequence[Tuple[np.ndarray, Optional[np.ndarray]]], dels: np.ndarray) -> int:
+        """One committed block's inserts (groups of records + payloads) then erases, queued on the node
+        stream without waiting (csrc/utxo_table.hip utxo_apply_async); every later pass on the table runs
+        behind them. The counters are booked by :meth:`complete` (the caller's next access). Returns the
+        previous apply's duplicates."""
+        dups = self.complete()
+        n_ins = sum(len(r) for r, _ in ins)
+        self._ensure(n_ins)
+        groups = [(np.ascontiguousarray(r), None if p is None else np.ascontiguousarray(p).view(np.uint8))
+                  for r, p in ins]
+        self.L.utxo_apply_async(self.h, groups, np.ascontiguousarray(dels))
+        self.pending = (n_ins, len(dels))
+        return dups
+
+    def complete(self) -> int:
+        """Book the pending async apply's counters (waits for it): returns its duplicates."""
+        if self.pending is None:
+            return 0
+        n_ins, _ = self.pending
+        self.pending = None
+        _, failed, dups, erased = self.L.utxo_apply_wait(self.h)
+        if failed:
+            raise RuntimeError(f'UTXO table insert failed for {failed} entries')
+        self.count += n_ins - dups - erased
+        self.tombs += erased
+        return dups
 
     def _ensure(self, extra: int):
         need = self.count + self.tombs + extra
@@ -274,6 +302,10 @@ def default_backend() -> str:
         return 'host'
 
 
+# UPOW_UTXO_ASYNC=0: the block path's index update as synchronous insert + erase calls (A/B)
+ASYNC_APPLY = os.environ.get('UPOW_UTXO_ASYNC', '1') != '0'
+
+
 def _locked(fn):
     """Run under the index lock, after any deferred writes (:meth:`UtxoIndex.defer_block`) reached the
     backend: every read and every direct write sees the index as the committed blocks left it."""
@@ -282,6 +314,8 @@ def _locked(fn):
         with self.lock:
             if self._pend_ins or self._pend_del:
                 self._apply_pending()
+            if self._gpu and self.be.pending is not None:
+                self._dups(self.be.complete())
             return fn(self, *args, **kwargs)
     return wrapper
 
@@ -292,6 +326,7 @@ class UtxoIndex:
         self.lock = threading.RLock()
         self.backend_name = backend or default_backend()
         self.be = _GpuBackend() if self.backend_name == 'gpu' else _HostBackend()
+        self._gpu = isinstance(self.be, _GpuBackend)
         self.duplicates = 0  # inserts of an outpoint that was already live (skipped; a ledger bug if ever > 0)
         # deferred writes of committed blocks (a sync page's blocks, ledger/pagesync.py): applied as ONE insert
         # launch and ONE erase launch before anything else touches the index
@@ -312,22 +347,45 @@ class UtxoIndex:
                 self._pend_del.append(spent)
 
     def settle(self):
-        """Apply the deferred writes now (no-op when there are none)."""
+        """Apply the deferred writes now and book any async apply (no-op when there is neither)."""
         with self.lock:
             if self._pend_ins or self._pend_del:
                 self._apply_pending()
+            if self._gpu and self.be.pending is not None:
+                self._dups(self.be.complete())
+
+    def apply_block(self, ins: Sequence[Tuple[np.ndarray, Optional[np.ndarray]]], spent: np.ndarray):
+        """The block path's index update after the commit point: the block's created outputs (records +
+        payloads, one or more groups) in, then its spent records out. GPU backend: one H2D copy, one insert
+        and one erase launch queued on the node stream, no wait (``_GpuBackend.apply_async``): the next
+        block's lookup is queued behind them, and its counters are booked at the next access."""
+        with self.lock:
+            if self._pend_ins or self._pend_del:
+                self._apply_pending()
+            self._apply(list(ins), [spent] if len(spent) else [])
+
+    def _apply(self, ins, dels):
+        ins = [(r, p) for r, p in ins if len(r)]
+        if ins and any(p is None for _, p in ins):  # payloads for every group or for none
+            ins = [(r, None) for r, _ in ins]
+        spent = np.ascontiguousarray(np.concatenate(dels)) if len(dels) > 1 else \
+            (np.ascontiguousarray(dels[0]) if dels else np.zeros((0, 40), np.uint8))
+        if self._gpu and ASYNC_APPLY:
+            if ins or len(spent):
+                self._dups(self.be.apply_async(ins, spent))
+            return
+        recs = np.ascontiguousarray(np.concatenate([r for r, _ in ins])) if ins else np.zeros((0, 40), np.uint8)
+        pay = None if (not ins or ins[0][1] is None) else np.ascontiguousarray(np.concatenate([p for _, p in ins]))
+        if len(recs):
+            self._insert_records(recs, pay)
+        if len(spent):
+            self._erase_records(spent)
 
     def _apply_pending(self):
         ins, dels = self._pend_ins, self._pend_del
         self._pend_ins, self._pend_del = [], []
         self.deferred_flushes += 1
-        if ins:
-            recs = np.ascontiguousarray(np.concatenate([r for r, _ in ins]))
-            pays = [p for _, p in ins]
-            pay = None if any(p is None for p in pays) else np.ascontiguousarray(np.concatenate(pays))
-            self._insert_records(recs, pay)
-        if dels:
-            self._erase_records(np.ascontiguousarray(np.concatenate(dels)))
+        self._apply(ins, dels)
 
     def _dups(self, n: int):
         if n:
@@ -505,10 +563,12 @@ class UtxoIndex:
         """K12 at this block, computed later: returns a callable giving the hex digest (the same value
         :meth:`set_hash` gives now). GPU backend: the snapshot is one compaction launch on the node stream;
         the callable (meant for a worker thread) sorts, gathers and hashes on the aux stream."""
-        self.settle()
-        if isinstance(self.be, _GpuBackend):
-            L, sid = self.be.L, self.be.L.utxo_k12_snapshot(self.be.h, tag)
-            return lambda: L.utxo_k12_digest(sid)[0].hex()
+        with self.lock:
+            if self._pend_ins or self._pend_del:
+                self._apply_pending()
+            if isinstance(self.be, _GpuBackend):  # queued behind any async apply on the node stream
+                L, sid = self.be.L, self.be.L.utxo_k12_snapshot(self.be.h, tag)
+                return lambda: L.utxo_k12_digest(sid)[0].hex()
         msg = self.set_message(tag)
         import hashlib
         return lambda: hashlib.sha256(msg).hexdigest()
