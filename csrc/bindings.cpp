@@ -235,6 +235,30 @@ PYBIND11_MODULE(_native, m) {
         return py::bytes(reinterpret_cast<const char*>(out), 32);
     });
 
+    // the kernels' field arithmetic on the host, for its differential test against Python integers
+    m.def("p256_fe_ops", [](py::bytes a_le, py::bytes b_le) -> py::bytes {
+        const std::string a = a_le, b = b_le;
+        if (a.size() != 32 || b.size() != 32) throw std::invalid_argument("need 32-byte little-endian a, b");
+        uint32_t x[8], y[8], out[32];
+        std::memcpy(x, a.data(), 32);
+        std::memcpy(y, b.data(), 32);
+        p256_fe_ops_host(x, y, out);
+        return py::bytes(reinterpret_cast<const char*>(out), sizeof out);
+    });
+    m.def("p256_g16_entries", [](int64_t first, int64_t count) -> py::bytes {
+        std::vector<uint8_t> o;
+        { py::gil_scoped_release rel; o = p256_g16_entries(first, count); }
+        return py::bytes(reinterpret_cast<const char*>(o.data()), o.size());
+    });
+    m.def("p256_fe_reduce", [](py::bytes c_le) -> py::bytes {
+        const std::string c = c_le;
+        if (c.size() != 64) throw std::invalid_argument("need 64 bytes little-endian");
+        uint32_t x[16], out[8];
+        std::memcpy(x, c.data(), 64);
+        p256_fe_reduce_host(x, out);
+        return py::bytes(reinterpret_cast<const char*>(out), sizeof out);
+    });
+
     m.def("p256_sign", [](py::bytes d_be, py::bytes digest) -> py::object {
         std::string d = d_be, h = digest;
         if (d.size() != 32 || h.size() != 32) throw std::invalid_argument("need 32-byte key and digest");

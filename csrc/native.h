@@ -44,6 +44,11 @@ uint8_t p256_verify_one_host64(const uint8_t* item);
 const void* p256_g_table_host();
 // s^-1 * 2^256 mod n for s in [1, n) (little-endian 64-bit limbs): the divsteps inverse of p256_field.h
 void p256_scalar_inv_mont_host(uint64_t out[4], const uint64_t s[4]);
+// a*b, a^2, a+b, a-b mod p (8 little-endian 32-bit limbs each, canonical inputs); c (16 limbs) mod p
+void p256_fe_ops_host(const uint32_t a[8], const uint32_t b[8], uint32_t out[32]);
+void p256_fe_reduce_host(const uint32_t c[16], uint32_t out[8]);
+// entries [first, first + count) of the device's 16-bit fixed-base window table (x, y little-endian each)
+std::vector<uint8_t> p256_g16_entries(int64_t first, int64_t count);
 std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n);
 void p256_decompress_host(const uint8_t* in33, int64_t n, uint8_t* out64, uint8_t* ok);
 void p256_decompress_gpu(const uint8_t* in33, int64_t n, uint8_t* out64, uint8_t* ok);

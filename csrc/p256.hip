@@ -88,6 +88,20 @@ static const std::vector<aff>& g_table() {
 
 const void* p256_g_table_host() { return g_table().data(); }
 
+// field operations on one host thread (the same UPOW_HD code the kernels run), for differential tests:
+// out = a*b, a^2, a+b, a-b (mod p) for canonical a, b; and an arbitrary 512-bit value reduced mod p
+void p256_fe_ops_host(const uint32_t a[8], const uint32_t b[8], uint32_t out[32]) {
+    fe x, y;
+    std::memcpy(x.v, a, 32);
+    std::memcpy(y.v, b, 32);
+    const fe r[4] = {fe_mul(x, y), fe_sqr(x), fe_add(x, y), fe_sub(x, y)};
+    for (int k = 0; k < 4; ++k) std::memcpy(out + 8 * k, r[k].v, 32);
+}
+void p256_fe_reduce_host(const uint32_t c[16], uint32_t out[8]) {
+    const fe r = fe_reduce(c);
+    std::memcpy(out, r.v, 32);
+}
+
 void p256_scalar_inv_mont_host(uint64_t out[4], const uint64_t s[4]) {
     fe a;
     std::memcpy(a.v, s, 32);
@@ -487,6 +501,38 @@ UPOW_HD jac mul_g_quarter(const fe& k, const aff* tab, int quarter) {
     return acc;
 }
 
+// The GPU kernels' u1*G: 16 windows of 16 bits over T16[j][b] = b * 2^(16 j) * G (16 x 65,536 affine
+// points, 64 MiB in HBM, built on the device from the byte-window table: build_g16_kernel). Half the mixed
+// additions of the byte windows (a lane's quarter is 4 windows: 3 additions instead of 7); the table
+// reads are 4 random 64-byte lines per lane, served from the 256 MB Infinity Cache once warm.
+static constexpr int kG16Win = 16;
+static constexpr int kG16Ent = 65536;  // entry 0 unused (zero)
+UPOW_HD jac mul_g16(const fe& k, const aff* tab16) {
+    jac acc = jac_inf();
+    for (int j = 0; j < kG16Win; ++j) {
+        const uint32_t b = (k.v[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+        if (b) acc = jac_madd(acc, tab16[size_t(j) * kG16Ent + b]);
+    }
+    return acc;
+}
+UPOW_HD jac mul_g16_quarter(const fe& k, const aff* tab16, int quarter) {
+    uint32_t lo = k.v[0], hi = k.v[1];  // this quarter's 64 bits, consumed 16 at a time
+#pragma unroll
+    for (int l = 1; l < 4; ++l) {
+        lo = quarter == l ? k.v[2 * l] : lo;
+        hi = quarter == l ? k.v[2 * l + 1] : hi;
+    }
+    const aff* t = tab16 + size_t(quarter) * 4 * kG16Ent;
+    jac acc = jac_inf();
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t b = lo & 0xffffu;
+        lo = (lo >> 16) | (hi << 16);
+        hi >>= 16;
+        if (b) acc = jac_madd(acc, t[size_t(j) * kG16Ent + b]);
+    }
+    return acc;
+}
+
 // Jacobian (X, Y, Z) -> XYZZ (X, Y, Z^2, Z^3): the same affine point, one lane on its own
 UPOW_HD xz jac_to_xz(const jac& p) {
     const fe zz = fe_sqr(p.z);
@@ -588,7 +634,7 @@ __device__ __forceinline__ jac tab_load(const jac* scratch, int64_t n, int64_t i
 
 template <int MIN_WAVES, bool SOA, int WPB = 1>
 __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void p256_verify_kernel(const VerifyItem* __restrict__ items, int64_t n,
-                                                          const aff* __restrict__ gtab, jac* __restrict__ scratch,
+                                                          const aff* __restrict__ gtab16, jac* __restrict__ scratch,
                                                           uint8_t* __restrict__ status, int spw) {
     // spw = signatures per 64-lane wave (lanes >= spw idle; A/B of partially filled waves);
     // WPB = waves per workgroup (a workgroup's waves are spread over the CU's SIMDs)
@@ -617,14 +663,14 @@ __global__ __launch_bounds__(64 * WPB, MIN_WAVES) void p256_verify_kernel(const 
             acc = jac_add(acc, e);
         }
     }
-    const jac R = jac_add(mul_g(u1, gtab), acc);
+    const jac R = jac_add(mul_g16(u1, gtab16), acc);
     status[i] = verify_epilogue(R, r);
 }
 
 // Four lanes per signature, four waves per workgroup (16 signatures per wave). Exits are quad-uniform.
 static constexpr int64_t kQuadMaxBatch = 32 * 1024;  // 2,048 waves of 16 signatures: two per SIMD
 __global__ __launch_bounds__(256, 1) void p256_verify_quad_kernel(const VerifyItem* __restrict__ items, int64_t n,
-                                                                   const aff* __restrict__ gtab,
+                                                                   const aff* __restrict__ gtab16,
                                                                    xz* __restrict__ scratch,
                                                                    uint8_t* __restrict__ status) {
     const int lane = int(threadIdx.x) & 63;
@@ -640,7 +686,7 @@ __global__ __launch_bounds__(256, 1) void p256_verify_quad_kernel(const VerifyIt
         if (role == 0) status[i] = pro;
         return;
     }
-    const xz mine = jac_to_xz(mul_g_quarter(u1, gtab, role));  // this lane's quarter of u1*G
+    const xz mine = jac_to_xz(mul_g16_quarter(u1, gtab16, role));  // this lane's quarter of u1*G
     const uint8_t st = verify_quad_core(pp, q, r, u2, scratch + i * 16, [&](auto K) {
         constexpr int k = decltype(K)::value;
         return xz{fe_quad_bcast<k>(mine.x), fe_quad_bcast<k>(mine.y), fe_quad_bcast<k>(mine.zz), fe_quad_bcast<k>(mine.zzz)};
@@ -652,7 +698,7 @@ __global__ __launch_bounds__(256, 1) void p256_verify_quad_kernel(const VerifyIt
 // octet-uniform. Both quads of an octet hold the same point state; the u1*G quarters are computed by each
 // quad (lane & 3) and broadcast within it.
 __global__ __launch_bounds__(256, 1) void p256_verify_oct_kernel(const VerifyItem* __restrict__ items, int64_t n,
-                                                                  const aff* __restrict__ gtab,
+                                                                  const aff* __restrict__ gtab16,
                                                                   xz* __restrict__ scratch,
                                                                   uint8_t* __restrict__ status) {
     const int lane = int(threadIdx.x) & 63;
@@ -669,7 +715,7 @@ __global__ __launch_bounds__(256, 1) void p256_verify_oct_kernel(const VerifyIte
         if (role == 0 && !upper) status[i] = pro;
         return;
     }
-    const xz mine = jac_to_xz(mul_g_quarter(u1, gtab, role));  // this lane's quarter of u1*G
+    const xz mine = jac_to_xz(mul_g16_quarter(u1, gtab16, role));  // this lane's quarter of u1*G
     const uint8_t st = verify_quad_core(pp, q, r, u2, scratch + i * 16, [&](auto K) {
         constexpr int k = decltype(K)::value;
         return xz{fe_quad_bcast<k>(mine.x), fe_quad_bcast<k>(mine.y), fe_quad_bcast<k>(mine.zz), fe_quad_bcast<k>(mine.zzz)};
@@ -716,7 +762,26 @@ static void hck(hipError_t e, const char* what) {
 struct DeviceGTable {
     int device = -1;
     aff* d_tab = nullptr;
+    aff* d_tab16 = nullptr;
 };
+
+// T16[j][b] = b * 2^(16 j) * G from the byte-window table: b = lo + 256 hi -> T[2j][lo] + T[2j+1][hi] (one
+// mixed addition; the two are never equal or opposite, lo * 256^(2j) < 256^(2j+1) <= hi * 256^(2j+1)), then
+// to affine with the thread's own inversion. One thread per entry; entry 0 of each window stays zero.
+__global__ __launch_bounds__(256) void build_g16_kernel(const aff* __restrict__ tab8, aff* __restrict__ tab16) {
+    const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= int64_t(kG16Win) * kG16Ent) return;
+    const int j = int(e / kG16Ent);
+    const uint32_t b = uint32_t(e % kG16Ent), lo = b & 0xffu, hi = b >> 8;
+    aff out{fe_zero(), fe_zero()};
+    if (b) {
+        jac acc = jac_inf();
+        if (lo) acc = jac_madd(acc, tab8[(2 * j) * kGEnt + lo]);
+        if (hi) acc = jac_madd(acc, tab8[(2 * j + 1) * kGEnt + hi]);
+        (void)jac_to_aff(acc, out);
+    }
+    tab16[e] = out;
+}
 static std::mutex g_dev_mu;
 static DeviceGTable g_dev_tabs[16];
 
@@ -734,6 +799,35 @@ static const aff* device_g_table() {
         t.device = dev;
     }
     return t.d_tab;
+}
+
+static const aff* device_g16_table() {
+    const aff* tab8 = device_g_table();
+    int dev = 0;
+    hck(hipGetDevice(&dev), "hipGetDevice");
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    DeviceGTable& t = g_dev_tabs[dev];
+    if (!t.d_tab16) {
+        const int64_t n = int64_t(kG16Win) * kG16Ent;
+        aff* d = nullptr;
+        hck(hipMalloc(&d, sizeof(aff) * size_t(n)), "hipMalloc gtab16");
+        hipLaunchKernelGGL(build_g16_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, node_stream(), tab8, d);
+        hck(hipGetLastError(), "build_g16_kernel launch");
+        node_sync("gtab16 build");
+        t.d_tab16 = d;
+    }
+    return t.d_tab16;
+}
+
+// entries [first, first + count) of the device's 16-bit-window table, for its differential test
+std::vector<uint8_t> p256_g16_entries(int64_t first, int64_t count) {
+    const int64_t n = int64_t(kG16Win) * kG16Ent;
+    if (first < 0 || count < 0 || first + count > n) throw std::invalid_argument("g16 entry range");
+    node_device_enter();
+    const aff* d = device_g16_table();
+    std::vector<uint8_t> out(size_t(count) * sizeof(aff));
+    node_d2h(out.data(), d + first, out.size(), "d2h gtab16");
+    return out;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -775,7 +869,7 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
     std::vector<uint8_t> st(static_cast<size_t>(n));
     if (n == 0) return st;
     node_device_enter();
-    const aff* d_tab = device_g_table();
+    const aff* d_tab = device_g16_table();
     PooledBuf<VerifyItem> b_items{size_t(n)};
     PooledBuf<uint8_t> b_st{size_t(n)};
     VerifyItem* d_items = b_items.p;

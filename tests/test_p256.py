@@ -51,6 +51,29 @@ def test_scalar_inverse_divsteps_matches_pow(native):
         assert got == pow(s, -1, n) * R % n, hex(s)
 
 
+def test_field_arithmetic_matches_python(native):
+    """The kernels' field code (p256_field.h, run on the host): products, squares, sums and differences
+    mod p against Python integers, and the Solinas reduction of arbitrary 512-bit values — including the
+    words patterns that drive its signed overflow to both ends of [-4, 6] (the h = -1 and h = 1 folds)."""
+    from upow_amd.ops.native import lib
+    L = lib()
+    p = o.P
+    rng = random.Random(13)
+    edge = [0, 1, 2, p - 1, p - 2, (p - 1) // 2, 1 << 255, (1 << 224) - 1, (1 << 96) + 5, p - (1 << 96),
+            (1 << 256) - 1 - (1 << 224) - p // 3]
+    vals = [v % p for v in edge] + [rng.randrange(p) for _ in range(1500)]
+    vals += [sum(rng.choice((0, 0xffffffff, 1)) << (32 * k) for k in range(8)) % p for _ in range(500)]
+    for k in range(len(vals)):
+        a, b = vals[k], vals[rng.randrange(len(vals))]
+        out = L.p256_fe_ops(a.to_bytes(32, 'little'), b.to_bytes(32, 'little'))
+        got = [int.from_bytes(out[32 * i:32 * i + 32], 'little') for i in range(4)]
+        assert got == [a * b % p, a * a % p, (a + b) % p, (a - b) % p], (hex(a), hex(b))
+    words = (0, 1, 0xffffffff, 0x80000000, 0xfffffffe)
+    for _ in range(4000):
+        c = sum(rng.choice(words) << (32 * k) for k in range(16)) if rng.random() < 0.7 else rng.getrandbits(512)
+        assert int.from_bytes(L.p256_fe_reduce(c.to_bytes(64, 'little')), 'little') == c % p, hex(c)
+
+
 def test_verify_semantics(native):
     d = 12345
     q = o.get_public_key(d)
@@ -285,3 +308,21 @@ def test_on_curve_batch_gpu_matches_host(gpu):
         rows.append(x.to_bytes(32, 'little') + y.to_bytes(32, 'little'))
     buf = b''.join(rows)
     assert gpu.p256_on_curve(buf, True) == gpu.p256_on_curve(buf, False, 8)
+
+
+@pytest.mark.gpu
+def test_g16_window_table_matches_python(gpu):
+    """The GPU kernels' fixed-base table T16[j][b] = b * 2^(16 j) * G (built on the device from the byte
+    windows): sampled entries of every window, both byte halves zero / non-zero, against Python."""
+    from upow_amd.ops.native import lib
+    L = lib()
+    rng = random.Random(17)
+    for j in range(16):
+        for b in [0, 1, 2, 255, 256, 257, 0xff00, 0xffff] + [rng.randrange(1, 1 << 16) for _ in range(6)]:
+            raw = L.p256_g16_entries(j * 65536 + b, 1)
+            x, y = int.from_bytes(raw[:32], 'little'), int.from_bytes(raw[32:], 'little')
+            if b == 0:
+                assert x == y == 0
+                continue
+            q = o.get_public_key((b << (16 * j)) % o.N)
+            assert (x, y) == (q.x, q.y), (j, b)
