@@ -270,8 +270,9 @@ for s in $STEPS; do
         tail -1 "$OUT/soak_$i.log" | cut -c1-600
       done ;;
     clustersync)
-      # page-batched sync of one chain on a forced single-rank RCCL cluster node vs the plain node (A/B pair)
-      for k in 1 2; do
+      # page-batched sync of one chain on a forced single-rank RCCL cluster node vs the plain node (three
+      # interleaved A/B pairs)
+      for k in 1 2 3; do
         rm -rf /tmp/upow_bench_ledger
         UPOW_FORCE_DIST=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
           --master-addr 127.0.0.1 --master-port 2954$k bench.py --gpus 1 --mode sync --txs 200 --steps 1000 --warmup 5 \

@@ -115,6 +115,13 @@ for _t in OUTPUT_TABLES[1:]:
 #   before the transactions split keep ``transactions`` in the main file (one "file", no view) and two
 #   UTXO files.
 _SQL_READERS = None  # Database._off_loop
+
+
+def _commit_point():
+    """On a cluster node, the block's agree-before-commit vote resolves here, right before its journal write
+    (parallel/cluster.py ``commit_point``); raises when a replica is not ready."""
+    from ..parallel.cluster import commit_point
+    commit_point()
 # 5 + 5 (eleven files with the main one; SQLite attaches at most ten): ~20 % faster materialisation of an
 # aged ledger than 4 + 4 (profiles/r4/verify_aged_writer_ab_r4g.json, verify_aged60_s55_r4x.json), 11 %
 # faster than 6 + 4 on the aged ledger (profiles/r5/verify_aged_split_*_r5i.json). 6 + 4 is 12 % faster on a
@@ -2131,12 +2138,14 @@ class Database:
         if self.writer is not None:
             enc = self.encode_many(stmts)
             stamp()
+            _commit_point()  # a cluster node: every replica agreed to commit this block (the vote overlapped the encode)
             # the undo record as parts: the writer joins them in one copy off the GIL
             meta = [bytes.fromhex(b['hash']), struct.pack('<qII', int(b['id']), n_out + len(cb_keys), n_in), recs,
                     np.ascontiguousarray(cb_recs), spent, np.ascontiguousarray(spent_payload).view(np.uint8)]
             seq = self.submit_batch(enc, tables, meta, int(b['id']), defer_sync=True)
         else:
             stamp()
+            _commit_point()
             with self.transaction(foreign_keys=False):
                 for sql, cols, nn, order, guard, expect in stmts:
                     if guard is not None and not self._q1(guard)[0]:
@@ -2305,6 +2314,7 @@ class Database:
         enc = [self.encode(*st) for st in stmts]
         meta = bytes.fromhex(b['hash']) + struct.pack('<qII', int(b['id']), len(created_recs), len(spent_recs)) + \
             created_recs.tobytes() + spent_recs.tobytes() + spent_pay.tobytes()
+        _commit_point()
         seq = self.submit_batch(enc, tables, meta, int(b['id']))
         # ---- the indexes and the chain-tip cache follow the commit point
         if len(spent_recs):

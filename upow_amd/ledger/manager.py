@@ -577,7 +577,8 @@ async def _finalize_block(block_no: int, block_content: str, fees, n_txs: int, a
 
 def _commit_gate() -> bool:
     """On a multi-GPU cluster node: every replica agrees to commit this block before any of them writes it
-    (parallel/cluster.py ``commit_gate``); always True on a single node."""
+    (parallel/cluster.py ``commit_gate``: the vote is queued here and resolved at the ledger's commit point,
+    right before the journal write, so preparing the block's batch overlaps it); always True on a single node."""
     from ..parallel import cluster
     return cluster.commit_gate()
 

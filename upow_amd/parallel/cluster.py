@@ -86,7 +86,9 @@ class Cluster:
         self.ops_sent = 0
         self.ops_received = 0
         self.commits_agreed = 0
-        self.vote_s = 0.0  # wall time spent in commit votes (the per-block price of agreement)
+        self.vote_s = 0.0  # wall time from a commit vote's start to its outcome (overlaps the block's batch encode)
+        self.vote_issue_s = 0.0  # host time queueing the votes
+        self.vote_block_s = 0.0  # time the commit point waited for them: the per-block price of agreement
         self.last_resync: Optional[dict] = None
 
     @property
@@ -174,7 +176,11 @@ class Cluster:
         coll = self.ctx.collectives
         return {'ops': ops, 'collectives': coll, 'collectives_per_op': round(coll / ops, 3) if ops else None,
                 'commits_agreed': self.commits_agreed,
-                'vote_us_avg': round(self.vote_s / self.commits_agreed * 1e6, 1) if self.commits_agreed else None}
+                # per agreed block: vote start to outcome (overlapping the batch encode), the host time spent
+                # queueing it, and the time the commit point actually waited for it
+                'vote_us_avg': round(self.vote_s / self.commits_agreed * 1e6, 1) if self.commits_agreed else None,
+                'vote_issue_us_avg': round(self.vote_issue_s / self.commits_agreed * 1e6, 1) if self.commits_agreed else None,
+                'vote_wait_us_avg': round(self.vote_block_s / self.commits_agreed * 1e6, 1) if self.commits_agreed else None}
 
 
 # ---------------------------------------------------------------------------------------------- commit gate
@@ -182,13 +188,39 @@ _GATE: contextvars.ContextVar = contextvars.ContextVar('upow_commit_gate', defau
 
 
 class CommitGate:
-    """Agree-before-commit for one block on a cluster node: :meth:`vote` (True) right before the ledger
-    writes, :meth:`close` with the rank's final verdict. Exactly one all-reduce per block per rank."""
+    """Agree-before-commit for one block on a cluster node: :meth:`start` when the block is ready to commit
+    (the vote's all-reduce is queued, the host goes on preparing the block's ledger batch), :meth:`wait` at the
+    commit point — right before the journal write (``commit_point``) — and :meth:`close` with the rank's final
+    verdict. Exactly one all-reduce per block per rank; a rank that rejects the block votes in :meth:`close`."""
 
     def __init__(self, c: Cluster, what: str):
         self.c, self.what = c, what
         self.voted: Optional[bool] = None
         self.n = 0
+        self._pending = None
+        self._t0 = 0.0
+
+    def start(self):
+        """This rank is ready to commit: queue the vote, do not wait for it."""
+        if self.voted is not None:
+            raise RuntimeError('commit gate: a block voted twice')
+        self.voted = True
+        self._t0 = time.perf_counter()
+        self._pending = self.c.op_ctx.allreduce_sum_start(1)
+        self.c.vote_issue_s += time.perf_counter() - self._t0
+
+    def wait(self) -> bool:
+        """The vote's outcome (waits for a queued one): True only when every replica is ready."""
+        if self._pending is not None:
+            pending, self._pending = self._pending, None
+            tw = time.perf_counter()
+            self.n = self.c.op_ctx.allreduce_sum_finish(pending)
+            t1 = time.perf_counter()
+            self.c.vote_s += t1 - self._t0
+            self.c.vote_block_s += t1 - tw
+            if self.n == self.c.ctx.world:
+                self.c.commits_agreed += 1
+        return bool(self.voted) and self.n == self.c.ctx.world
 
     def vote(self, ok: bool) -> bool:
         """This rank is ready to commit (or not); True only when every replica is."""
@@ -206,6 +238,7 @@ class CommitGate:
     def close(self, ok: bool) -> bool:
         if self.voted is None:  # rejected (or failed) before reaching the commit point
             self.vote(False)
+        self.wait()  # a queued vote always completes: the ranks' collectives pair up
         world = self.c.ctx.world
         if self.n not in (0, world):
             self.c.diverged(f'{self.what}: {self.n}/{world} replicas ready to commit (none committed)')
@@ -227,9 +260,24 @@ def close_gate(gate: Optional[CommitGate], token, ok: bool) -> bool:
 
 
 def commit_gate() -> bool:
-    """Called by the block paths right before their ledger writes: True when this block may commit."""
+    """Called by the block paths once a block has passed validation, before they prepare its ledger writes:
+    queues this rank's vote (the outcome is taken at :func:`commit_point`)."""
     g = _GATE.get()
-    return True if g is None else g.vote(True)
+    if g is not None:
+        g.start()
+    return True
+
+
+class CommitRefused(RuntimeError):
+    """A replica is not ready to commit the block this rank prepared: nothing was written."""
+
+
+def commit_point():
+    """The ledger's commit point (right before a block's journal write): waits for the block's vote and
+    raises :class:`CommitRefused` unless every replica is ready. No-op outside an active cluster gate."""
+    g = _GATE.get()
+    if g is not None and not g.wait():
+        raise CommitRefused(f'{g.what}: {g.n}/{g.c.ctx.world} replicas ready to commit')
 
 
 def _utxo_tag() -> int:

@@ -117,6 +117,43 @@ class DistContext:
             torch.cuda.current_stream().synchronize()
         return h.tolist()
 
+    def allreduce_sum_start(self, v: int):
+        """Split-phase SUM all-reduce of one int: the collective is queued (RCCL: on the communicator's
+        stream, with the copy back into pinned memory behind it) and the host goes on; :meth:`allreduce_sum_finish`
+        waits for it. The cluster's commit vote starts here and is collected right before the journal write,
+        so a block's statement encoding overlaps the vote. Nothing else may be issued in between."""
+        if not self.is_distributed:
+            return ('done', int(v))
+        import torch
+        import torch.distributed as dist
+        bufs = self.__dict__.setdefault('_rbuf', {})
+        pair = bufs.get('vote')
+        if pair is None:
+            gpu = self.comm_device != 'cpu'
+            host = torch.zeros(1, dtype=torch.int64, pin_memory=gpu)
+            pair = bufs['vote'] = (host, torch.zeros(1, dtype=torch.int64, device=self.comm_device) if gpu else host)
+        host, dev = pair
+        host.numpy()[0] = int(v)
+        if dev is host:  # gloo: the collective is synchronous
+            self._run('all_reduce(vote)', dist.all_reduce, dev, op=dist.ReduceOp.SUM)
+            return ('done', int(host.numpy()[0]))
+        dev.copy_(host, non_blocking=True)
+        self._run('all_reduce(vote)', dist.all_reduce, dev, op=dist.ReduceOp.SUM)
+        host.copy_(dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return ('pending', host, ev)
+
+    def allreduce_sum_finish(self, handle) -> int:
+        if handle[0] == 'done':
+            return handle[1]
+        _, host, ev = handle
+        try:
+            ev.synchronize()
+        except Exception as e:
+            self._failed('all_reduce(vote)', e)
+        return int(host.numpy()[0])
+
     def allreduce_min(self, v: int) -> int:
         if not self.is_distributed:
             return int(v)
