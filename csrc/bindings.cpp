@@ -245,6 +245,23 @@ PYBIND11_MODULE(_native, m) {
         p256_fe_ops_host(x, y, out);
         return py::bytes(reinterpret_cast<const char*>(out), sizeof out);
     });
+    m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+    m.def("rccl_vote_create", [](py::bytes uid, int world, int rank) {
+        const std::string u = uid;
+        py::gil_scoped_release rel;  // collective: waits for every rank
+        return rccl_vote_create(u, world, rank);
+    });
+    // queueing a vote takes a few microseconds: done holding the GIL (releasing it would let another
+    // thread take it for up to a switch interval before this one gets it back)
+    m.def("rccl_vote_start", [](int64_t h, int value) { rccl_vote_start(h, value); });
+    m.def("rccl_vote_finish", [](int64_t h, double timeout_s) {
+        py::gil_scoped_release rel;
+        return rccl_vote_finish(h, timeout_s);
+    });
+    m.def("rccl_vote_destroy", [](int64_t h, bool abort) {
+        py::gil_scoped_release rel;
+        rccl_vote_destroy(h, abort);
+    }, py::arg("h"), py::arg("abort") = false);
     m.def("p256_g16_entries", [](int64_t first, int64_t count) -> py::bytes {
         std::vector<uint8_t> o;
         { py::gil_scoped_release rel; o = p256_g16_entries(first, count); }

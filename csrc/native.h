@@ -47,6 +47,12 @@ void p256_scalar_inv_mont_host(uint64_t out[4], const uint64_t s[4]);
 // a*b, a^2, a+b, a-b mod p (8 little-endian 32-bit limbs each, canonical inputs); c (16 limbs) mod p
 void p256_fe_ops_host(const uint32_t a[8], const uint32_t b[8], uint32_t out[32]);
 void p256_fe_reduce_host(const uint32_t c[16], uint32_t out[8]);
+// the cluster's per-block commit vote on a native RCCL communicator of its own (csrc/rccl_vote.hip)
+std::string rccl_unique_id();
+int64_t rccl_vote_create(const std::string& uid, int world, int rank);
+void rccl_vote_start(int64_t h, int value);
+int64_t rccl_vote_finish(int64_t h, double timeout_s);  // SUM of the votes, -1 on timeout
+void rccl_vote_destroy(int64_t h, bool abort);
 // entries [first, first + count) of the device's 16-bit fixed-base window table (x, y little-endian each)
 std::vector<uint8_t> p256_g16_entries(int64_t first, int64_t count);
 std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n);

@@ -1,5 +1,5 @@
 """Latency of the cluster node's collectives (parallel/dist.py) over the job's backend: the per-block commit
-vote (8-byte all-reduce), an idle op frame and a 64 KB frame (one fixed-capacity broadcast), a block-sized
+vote (split-phase all-gather: start to outcome, and the host time of queueing it), an 8-byte all-reduce, an idle op frame and a 64 KB frame (one fixed-capacity broadcast), a block-sized
 frame (two broadcasts), the fixed-size state all-gather. Run under torch.distributed.run (UPOW_FORCE_DIST=1
 for a single-rank RCCL group on one GPU). Prints one JSON line from rank 0: median microseconds per call."""
 import json
@@ -8,6 +8,30 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _issue(ctx, med):
+    """Host time of queueing one vote (its outcome collected outside the timed call)."""
+    pending = []
+
+    def one():
+        if pending:
+            ctx.vote_finish(pending.pop())
+        pending.append(ctx.vote_start(1))
+    # time only the start: finish the previous vote first, outside the clock
+    import time
+    for _ in range(20):
+        one()
+    ts = []
+    for _ in range(int(os.environ.get('LAT_ITERS', '400'))):
+        if pending:
+            ctx.vote_finish(pending.pop())
+        t0 = time.perf_counter()
+        pending.append(ctx.vote_start(1))
+        ts.append(time.perf_counter() - t0)
+    ctx.vote_finish(pending.pop())
+    ts.sort()
+    return round(ts[len(ts) // 2] * 1e6, 1)
 
 
 def main():
@@ -35,6 +59,9 @@ def main():
     out = {
         'backend': ctx.backend, 'world': ctx.world,
         'allreduce_sum_us': med(lambda: ctx.allreduce_sum(1)),
+        'vote_us': med(lambda: ctx.vote_finish(ctx.vote_start(1))),  # the commit vote, start to outcome
+        'vote_native': ctx.__dict__.get('_nv') is not None,
+        'vote_issue_us': _issue(ctx, med),
         'allreduce_min_vec_us': med(lambda: ctx.allreduce_min_vec([1, -1])),
         'frame_ping_us': med(lambda: ctx.broadcast_frame(b'{"op":"ping"}' if me else None, src=0)),
         'frame_60k_us': med(lambda: ctx.broadcast_frame(frame64 if me else None, src=0)),

@@ -206,7 +206,7 @@ class CommitGate:
             raise RuntimeError('commit gate: a block voted twice')
         self.voted = True
         self._t0 = time.perf_counter()
-        self._pending = self.c.op_ctx.allreduce_sum_start(1)
+        self._pending = self.c.op_ctx.vote_start(1)
         self.c.vote_issue_s += time.perf_counter() - self._t0
 
     def wait(self) -> bool:
@@ -214,7 +214,7 @@ class CommitGate:
         if self._pending is not None:
             pending, self._pending = self._pending, None
             tw = time.perf_counter()
-            self.n = self.c.op_ctx.allreduce_sum_finish(pending)
+            self.n = self.c.op_ctx.vote_finish(pending)
             t1 = time.perf_counter()
             self.c.vote_s += t1 - self._t0
             self.c.vote_block_s += t1 - tw
@@ -223,17 +223,16 @@ class CommitGate:
         return bool(self.voted) and self.n == self.c.ctx.world
 
     def vote(self, ok: bool) -> bool:
-        """This rank is ready to commit (or not); True only when every replica is."""
+        """This rank is ready to commit (or not), voted and waited for at once; True only when every
+        replica is."""
         if self.voted is not None:
             raise RuntimeError('commit gate: a block voted twice')
-        self.voted = bool(ok)
-        t0 = time.perf_counter()
-        self.n = self.c.op_ctx.allreduce_sum(1 if ok else 0)
-        self.c.vote_s += time.perf_counter() - t0
-        go = self.voted and self.n == self.c.ctx.world
-        if go:
-            self.c.commits_agreed += 1
-        return go
+        if ok:
+            self.start()
+            return self.wait()
+        self.voted = False
+        self.n = self.c.op_ctx.vote_finish(self.c.op_ctx.vote_start(0))
+        return False
 
     def close(self, ok: bool) -> bool:
         if self.voted is None:  # rejected (or failed) before reaching the commit point

@@ -117,42 +117,79 @@ class DistContext:
             torch.cuda.current_stream().synchronize()
         return h.tolist()
 
-    def allreduce_sum_start(self, v: int):
-        """Split-phase SUM all-reduce of one int: the collective is queued (RCCL: on the communicator's
-        stream, with the copy back into pinned memory behind it) and the host goes on; :meth:`allreduce_sum_finish`
-        waits for it. The cluster's commit vote starts here and is collected right before the journal write,
-        so a block's statement encoding overlaps the vote. Nothing else may be issued in between."""
+    def vote_start(self, v: int):
+        """Split-phase agreement on one small int (the cluster's per-block commit vote): every rank's value is
+        gathered (``all_gather_into_tensor`` from a constant device tensor: no host-to-device copy; the
+        device-to-host copy of the gathered vector into pinned memory and an event are queued behind it) and
+        the host goes on; :meth:`vote_finish` waits and returns the SUM. Every rank votes through this pair,
+        ready or not, so the collectives pair up. Nothing else may be issued in between."""
         if not self.is_distributed:
             return ('done', int(v))
+        nv = self._native_vote()
+        if nv is not None:  # RCCL: the native communicator of csrc/rccl_vote.hip
+            L, h = nv
+            self._enter('vote')
+            try:
+                L.rccl_vote_start(h, 1 if v else 0)
+            except Exception as e:
+                self._failed('vote', e)
+            return ('native', L, h)
         import torch
         import torch.distributed as dist
-        bufs = self.__dict__.setdefault('_rbuf', {})
-        pair = bufs.get('vote')
-        if pair is None:
+        st = self.__dict__.get('_vote')
+        if st is None:
             gpu = self.comm_device != 'cpu'
-            host = torch.zeros(1, dtype=torch.int64, pin_memory=gpu)
-            pair = bufs['vote'] = (host, torch.zeros(1, dtype=torch.int64, device=self.comm_device) if gpu else host)
-        host, dev = pair
-        host.numpy()[0] = int(v)
-        if dev is host:  # gloo: the collective is synchronous
-            self._run('all_reduce(vote)', dist.all_reduce, dev, op=dist.ReduceOp.SUM)
-            return ('done', int(host.numpy()[0]))
-        dev.copy_(host, non_blocking=True)
-        self._run('all_reduce(vote)', dist.all_reduce, dev, op=dist.ReduceOp.SUM)
-        host.copy_(dev, non_blocking=True)
-        ev = torch.cuda.Event()
+            consts = {k: torch.full((1,), k, dtype=torch.int64, device=self.comm_device) for k in (0, 1)}
+            out = torch.zeros(self.world, dtype=torch.int64, device=self.comm_device)
+            host = torch.zeros(self.world, dtype=torch.int64, pin_memory=gpu) if gpu else out
+            ev = torch.cuda.Event() if gpu else None
+            st = self._vote = (consts, out, host, ev)
+        consts, out, host, ev = st
+        src = consts.get(int(v))
+        if src is None:
+            src = torch.full((1,), int(v), dtype=torch.int64, device=self.comm_device)
+        self._run('all_gather(vote)', dist.all_gather_into_tensor, out, src)
+        if ev is None:  # gloo: synchronous
+            return ('done', int(host.sum()))
+        host.copy_(out, non_blocking=True)
         ev.record()
         return ('pending', host, ev)
 
-    def allreduce_sum_finish(self, handle) -> int:
+    def _native_vote(self):
+        """(lib, handle) of this context's native vote communicator on an RCCL job (created at the first
+        vote: rank 0's unique id goes out in one broadcast on this context's group, then every rank joins),
+        None on gloo or with UPOW_NATIVE_VOTE=0."""
+        nv = self.__dict__.get('_nv', False)
+        if nv is not False:
+            return nv
+        nv = None
+        if self.comm_device != 'cpu' and os.environ.get('UPOW_NATIVE_VOTE', '1') != '0':
+            from ..ops.native import lib
+            L = lib()
+            uid = self.broadcast_bytes(L.rccl_unique_id() if self.rank == 0 else None, src=0, max_len=128)
+            self._enter('vote communicator')
+            try:
+                nv = (L, L.rccl_vote_create(uid, self.world, self.rank))
+            except Exception as e:
+                self._failed('vote communicator', e)
+        self._nv = nv
+        return nv
+
+    def vote_finish(self, handle) -> int:
         if handle[0] == 'done':
             return handle[1]
+        if handle[0] == 'native':
+            _, L, h = handle
+            n = L.rccl_vote_finish(h, float(os.environ.get('UPOW_DIST_TIMEOUT_S', '60')))
+            if n < 0:
+                self._failed('vote', TimeoutError('no outcome within UPOW_DIST_TIMEOUT_S'))
+            return int(n)
         _, host, ev = handle
         try:
             ev.synchronize()
         except Exception as e:
-            self._failed('all_reduce(vote)', e)
-        return int(host.numpy()[0])
+            self._failed('all_gather(vote)', e)
+        return int(host.numpy().sum())
 
     def allreduce_min(self, v: int) -> int:
         if not self.is_distributed:
