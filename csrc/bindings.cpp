@@ -258,6 +258,7 @@ PYBIND11_MODULE(_native, m) {
         py::gil_scoped_release rel;
         return rccl_vote_finish(h, timeout_s);
     });
+    m.def("rccl_vote_stats", [](int64_t h) { return rccl_vote_stats(h); });
     m.def("rccl_vote_destroy", [](int64_t h, bool abort) {
         py::gil_scoped_release rel;
         rccl_vote_destroy(h, abort);

@@ -53,6 +53,7 @@ int64_t rccl_vote_create(const std::string& uid, int world, int rank);
 void rccl_vote_start(int64_t h, int value);
 int64_t rccl_vote_finish(int64_t h, double timeout_s);  // SUM of the votes, -1 on timeout
 void rccl_vote_destroy(int64_t h, bool abort);
+std::vector<double> rccl_vote_stats(int64_t h);  // votes, then seconds in the all-gather, copy, event enqueues
 // entries [first, first + count) of the device's 16-bit fixed-base window table (x, y little-endian each)
 std::vector<uint8_t> p256_g16_entries(int64_t first, int64_t count);
 std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n);

@@ -79,6 +79,9 @@ struct Vote {
     int64_t* d_out = nullptr;    // world entries
     int64_t* h_out = nullptr;    // pinned
     bool pending = false;
+    // host time of the three enqueues (all-gather, copy, event) summed over the votes: rccl_vote_stats
+    double t_gather = 0, t_copy = 0, t_event = 0;
+    int64_t votes = 0;
 };
 
 std::mutex g_mu;
@@ -137,10 +140,25 @@ void rccl_vote_start(int64_t h, int value) {
     Vote& v = vote_of(h);
     if (v.pending) throw std::runtime_error("rccl vote: a vote is already pending");
     if (value != 0 && value != 1) throw std::invalid_argument("a vote is 0 or 1");
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     nck(rccl().all_gather(v.d_const + value, v.d_out, 1, ncclInt64, v.comm, v.stream), "ncclAllGather (vote)");
+    const auto t1 = clk::now();
     hck(hipMemcpyAsync(v.h_out, v.d_out, size_t(v.world) * sizeof(int64_t), hipMemcpyDeviceToHost, v.stream), "vote d2h");
+    const auto t2 = clk::now();
     hck(hipEventRecord(v.ev, v.stream), "vote event");
+    const auto t3 = clk::now();
+    v.t_gather += std::chrono::duration<double>(t1 - t0).count();
+    v.t_copy += std::chrono::duration<double>(t2 - t1).count();
+    v.t_event += std::chrono::duration<double>(t3 - t2).count();
+    ++v.votes;
     v.pending = true;
+}
+
+std::vector<double> rccl_vote_stats(int64_t h) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    Vote& v = vote_of(h);
+    return {double(v.votes), v.t_gather, v.t_copy, v.t_event};
 }
 
 // the SUM of the ranks' votes, or -1 when it has not arrived within timeout_s (the caller treats that as a

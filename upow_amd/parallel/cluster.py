@@ -88,6 +88,7 @@ class Cluster:
         self.commits_agreed = 0
         self.vote_s = 0.0  # wall time from a commit vote's start to its outcome (overlaps the block's batch encode)
         self.vote_issue_s = 0.0  # host time queueing the votes
+        self.vote_issue_cpu_s = 0.0  # of which the thread was on a CPU (the rest: waiting for the GIL or a lock)
         self.vote_block_s = 0.0  # time the commit point waited for them: the per-block price of agreement
         self.last_resync: Optional[dict] = None
 
@@ -180,7 +181,22 @@ class Cluster:
                 # queueing it, and the time the commit point actually waited for it
                 'vote_us_avg': round(self.vote_s / self.commits_agreed * 1e6, 1) if self.commits_agreed else None,
                 'vote_issue_us_avg': round(self.vote_issue_s / self.commits_agreed * 1e6, 1) if self.commits_agreed else None,
-                'vote_wait_us_avg': round(self.vote_block_s / self.commits_agreed * 1e6, 1) if self.commits_agreed else None}
+                'vote_issue_cpu_us_avg': round(self.vote_issue_cpu_s / self.commits_agreed * 1e6, 1) if self.commits_agreed else None,
+                'vote_wait_us_avg': round(self.vote_block_s / self.commits_agreed * 1e6, 1) if self.commits_agreed else None,
+                **_native_vote_stats(self.op_ctx)}
+
+
+def _native_vote_stats(ctx) -> dict:
+    """Per-vote host time of the native vote's enqueues (csrc/rccl_vote.hip), when it is in use."""
+    nv = ctx.__dict__.get('_nv')
+    if not nv:
+        return {}
+    L, h = nv
+    n, tg, tc, te = L.rccl_vote_stats(h)
+    if not n:
+        return {}
+    return {'native_vote': {'votes': int(n), 'gather_us': round(tg / n * 1e6, 1), 'copy_us': round(tc / n * 1e6, 1),
+                            'event_us': round(te / n * 1e6, 1)}}
 
 
 # ---------------------------------------------------------------------------------------------- commit gate
@@ -206,8 +222,10 @@ class CommitGate:
             raise RuntimeError('commit gate: a block voted twice')
         self.voted = True
         self._t0 = time.perf_counter()
+        c0 = time.thread_time()
         self._pending = self.c.op_ctx.vote_start(1)
         self.c.vote_issue_s += time.perf_counter() - self._t0
+        self.c.vote_issue_cpu_s += time.thread_time() - c0
 
     def wait(self) -> bool:
         """The vote's outcome (waits for a queued one): True only when every replica is ready."""
