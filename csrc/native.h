@@ -48,6 +48,10 @@ void p256_scalar_inv_mont_host(uint64_t out[4], const uint64_t s[4]);
 void p256_fe_ops_host(const uint32_t a[8], const uint32_t b[8], uint32_t out[32]);
 void p256_fe_reduce_host(const uint32_t c[16], uint32_t out[8]);
 // the cluster's per-block commit vote on a native RCCL communicator of its own (csrc/rccl_vote.hip)
+// one-lane-per-signature batch verify launch (csrc/p256_batch.hip): VerifyItem items, 16-bit G table,
+// 16 window-table entries of scratch per signature, status bytes
+void p256_batch_launch(char variant, const void* items, int64_t n, const void* gtab16, void* scratch, uint8_t* status,
+                       int spw, void* stream);
 std::string rccl_unique_id();
 int64_t rccl_vote_create(const std::string& uid, int world, int rank);
 void rccl_vote_start(int64_t h, int value);

@@ -33,6 +33,7 @@
 #include "thread_pool.h"
 #include "streams.h"
 #include "p256_field.h"
+#include "p256_verify.h"
 #include "sha256_common.h"
 
 namespace upow {
@@ -121,72 +122,6 @@ UPOW_HD jac mul_g(const fe& k, const aff* tab) {
 // ------------------------------------------------------------------------------------------------
 // shared verify core
 // ------------------------------------------------------------------------------------------------
-struct VerifyItem {  // 160 bytes, wire byte order
-    uint8_t qx[32];  // little-endian
-    uint8_t qy[32];  // little-endian
-    uint8_t r[32];   // little-endian
-    uint8_t s[32];   // little-endian
-    uint8_t e[32];   // SHA-256 digest, big-endian
-};
-static_assert(sizeof(VerifyItem) == 160, "VerifyItem layout");
-
-// 1 builds the previous inverse (binary Euclid) for the A/B (_build.py variant 'p256bgcd')
-#ifndef UPOW_P256_INV_BGCD
-#define UPOW_P256_INV_BGCD 0
-#endif
-
-UPOW_HD uint8_t verify_prologue(const VerifyItem& it, aff& q, fe& r, fe& u1, fe& u2) {
-    q.x = fe_from_le(it.qx);
-    q.y = fe_from_le(it.qy);
-    if (!aff_on_curve(q)) return 2;
-    r = fe_from_le(it.r);
-    const fe s = fe_from_le(it.s);
-    const fe n = fe_const_n();
-    // fastecdsa: raise if r > n or r < 1 (same for s)
-    if (fe_is_zero(r) || (fe_geq(r, n) && !fe_eq(r, n))) return 3;
-    if (fe_is_zero(s) || (fe_geq(s, n) && !fe_eq(s, n))) return 3;
-    if (fe_eq(s, n)) return 0;  // s has no inverse mod n
-    const fe e = sc_reduce(fe_from_be(it.e));
-    const fe w_m = UPOW_P256_INV_BGCD ? sc_inv_bgcd_mont(s) : sc_inv_safegcd_mont(s);  // s^-1 * R
-    u1 = sc_mont_mul(e, w_m);                   // e * s^-1
-    u2 = sc_mont_mul(sc_reduce(r), w_m);        // r * s^-1
-    return 255;                                 // continue
-}
-
-UPOW_HD uint8_t verify_epilogue(const jac& R, const fe& r) {
-    if (jac_is_inf(R)) return 0;
-    const fe z2 = fe_sqr(R.z);
-    if (fe_eq(fe_mul(r, z2), R.x)) return 1;
-    // r + n < p ?  (x(R) in [n, p) maps to x mod n = x - n)
-    fe rn;
-    const uint32_t c = raw_add(rn, r, fe_const_n());
-    if (!c && !fe_geq(rn, fe_const_p())) {
-        if (fe_eq(fe_mul(rn, z2), R.x)) return 1;
-    }
-    return 0;
-}
-
-// Signed 5-bit windows of a scalar k < 2^256 (Booth recoding): 52 digits in [-16, 16], top first, with
-// k = sum d_i 32^i. Digit i comes from bits [5i+4 .. 5i-1] of k (bit -1 = 0): d = b0 + b1 + 2 b2 + 4 b3
-// + 8 b4 - 16 b5 of those six bits. They are read from the top of a 288-bit shift register s = k << 28
-// and shifted out five at a time (no dynamic register indexing on the GPU).
-struct BoothW5 {
-    uint32_t s9[9];
-    UPOW_HD explicit BoothW5(const fe& k) {
-        s9[0] = k.v[0] << 28;
-#pragma unroll
-        for (int l = 1; l < 8; ++l) s9[l] = (k.v[l] << 28) | (k.v[l - 1] >> 4);
-        s9[8] = k.v[7] >> 4;
-    }
-    UPOW_HD int next() {
-        const uint32_t v = s9[8] >> 26;
-#pragma unroll
-        for (int l = 8; l > 0; --l) s9[l] = (s9[l] << 5) | (s9[l - 1] >> 27);
-        s9[0] <<= 5;
-        return int((v >> 1) & 15u) + int(v & 1u) - 16 * int(v >> 5);
-    }
-};
-static constexpr int kBoothWindows = 52;
 
 static uint8_t verify_one_host(const VerifyItem& it, const aff* gtab) {
     aff q;
@@ -291,15 +226,17 @@ __device__ __forceinline__ fe fe_quad_bcast(const fe& a) {  // every lane of the
     return r;
 }
 struct QuadDev {
-    bool is1, is2, is3;  // this lane's role in its quad (lane & 3)
+    bool odd, hi;  // this lane's role in its quad (lane & 3): bit 0 and bit 1
+    // a_role as a two-level select tree on the role's bits: the compiler folds a select of two identical
+    // operands, so the schedule's repeated operands cost less than three selects per word — (a, b, c, c)
+    // and (v, v, m, z) take two, (x, y, x, y) one (the linear chain on role == 1/2/3 folded less)
     __device__ __forceinline__ fe pick(const fe& a0, const fe& a1, const fe& a2, const fe& a3) const {
         fe r;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            uint32_t t = a0.v[i];
-            t = is1 ? a1.v[i] : t;
-            t = is2 ? a2.v[i] : t;
-            r.v[i] = is3 ? a3.v[i] : t;
+            const uint32_t lo = odd ? a1.v[i] : a0.v[i];
+            const uint32_t up = odd ? a3.v[i] : a2.v[i];
+            r.v[i] = hi ? up : lo;
         }
         return r;
     }
@@ -501,20 +438,7 @@ UPOW_HD jac mul_g_quarter(const fe& k, const aff* tab, int quarter) {
     return acc;
 }
 
-// The GPU kernels' u1*G: 16 windows of 16 bits over T16[j][b] = b * 2^(16 j) * G (16 x 65,536 affine
-// points, 64 MiB in HBM, built on the device from the byte-window table: build_g16_kernel). Half the mixed
-// additions of the byte windows (a lane's quarter is 4 windows: 3 additions instead of 7); the table
-// reads are 4 random 64-byte lines per lane, served from the 256 MB Infinity Cache once warm.
-static constexpr int kG16Win = 16;
-static constexpr int kG16Ent = 65536;  // entry 0 unused (zero)
-UPOW_HD jac mul_g16(const fe& k, const aff* tab16) {
-    jac acc = jac_inf();
-    for (int j = 0; j < kG16Win; ++j) {
-        const uint32_t b = (k.v[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-        if (b) acc = jac_madd(acc, tab16[size_t(j) * kG16Ent + b]);
-    }
-    return acc;
-}
+
 UPOW_HD jac mul_g16_quarter(const fe& k, const aff* tab16, int quarter) {
     uint32_t lo = k.v[0], hi = k.v[1];  // this quarter's 64 bits, consumed 16 at a time
 #pragma unroll
@@ -603,72 +527,10 @@ static uint8_t verify_one_host_quad(const VerifyItem& it, const aff* gtab) { ret
 // ------------------------------------------------------------------------------------------------
 // device kernels
 // ------------------------------------------------------------------------------------------------
-// Per-lane window table {1..15}Q lives in global scratch. SOA = false: [lane][k] Jacobian entries
-// (each lane's 16 x 96 B contiguous; a table load gathers 64 scattered lines per dword). SOA = true:
-// dword-major [k][dword][lane], so the lanes of a wave that picked the same window digit read one
-// contiguous run per dword (at most 16 distinct runs per load instead of 64 lines).
-template <bool SOA>
-__device__ __forceinline__ void tab_store(jac* scratch, int64_t n, int64_t i, int k, const jac& p) {
-    if (SOA) {
-        uint32_t* s = reinterpret_cast<uint32_t*>(scratch);
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(&p);
-#pragma unroll
-        for (int d = 0; d < 24; ++d) s[(int64_t(k) * 24 + d) * n + i] = src[d];
-    } else {
-        scratch[i * 16 + k] = p;
-    }
-}
-
-template <bool SOA>
-__device__ __forceinline__ jac tab_load(const jac* scratch, int64_t n, int64_t i, int k) {
-    if (SOA) {
-        jac p;
-        const uint32_t* s = reinterpret_cast<const uint32_t*>(scratch);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(&p);
-#pragma unroll
-        for (int d = 0; d < 24; ++d) dst[d] = s[(int64_t(k) * 24 + d) * n + i];
-        return p;
-    }
-    return scratch[i * 16 + k];
-}
-
-template <int MIN_WAVES, bool SOA, int WPB = 1>
-__global__ __launch_bounds__(64 * WPB, MIN_WAVES) void p256_verify_kernel(const VerifyItem* __restrict__ items, int64_t n,
-                                                          const aff* __restrict__ gtab16, jac* __restrict__ scratch,
-                                                          uint8_t* __restrict__ status, int spw) {
-    // spw = signatures per 64-lane wave (lanes >= spw idle; A/B of partially filled waves);
-    // WPB = waves per workgroup (a workgroup's waves are spread over the CU's SIMDs)
-    const int lane = int(threadIdx.x) & 63;
-    const int64_t i = (int64_t(blockIdx.x) * WPB + (threadIdx.x >> 6)) * spw + lane;
-    if (lane >= spw || i >= n) return;
-    const VerifyItem it = items[i];
-    aff q;
-    fe r, u1, u2;
-    const uint8_t pro = verify_prologue(it, q, r, u1, u2);
-    if (pro != 255) { status[i] = pro; return; }
-    jac t = jac_from_aff(q);  // entry k - 1 = k*Q, k = 1..16 (signed 5-bit windows)
-    tab_store<SOA>(scratch, n, i, 0, t);
-    for (int k = 2; k <= 16; ++k) {
-        t = jac_madd(t, q);
-        tab_store<SOA>(scratch, n, i, k - 1, t);
-    }
-    jac acc = jac_inf();
-    BoothW5 bw(u2);
-    for (int w = kBoothWindows - 1; w >= 0; --w) {
-        acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc);
-        const int d = bw.next();
-        if (d) {
-            jac e = tab_load<SOA>(scratch, n, i, (d < 0 ? -d : d) - 1);
-            if (d < 0) e.y = fe_neg(e.y);
-            acc = jac_add(acc, e);
-        }
-    }
-    const jac R = jac_add(mul_g16(u1, gtab16), acc);
-    status[i] = verify_epilogue(R, r);
-}
 
 // Four lanes per signature, four waves per workgroup (16 signatures per wave). Exits are quad-uniform.
 static constexpr int64_t kQuadMaxBatch = 32 * 1024;  // 2,048 waves of 16 signatures: two per SIMD
+static constexpr int64_t kBatchSlice = 4 * 1024 * 1024;  // one-lane batch launches: signatures per launch
 __global__ __launch_bounds__(256, 1) void p256_verify_quad_kernel(const VerifyItem* __restrict__ items, int64_t n,
                                                                    const aff* __restrict__ gtab16,
                                                                    xz* __restrict__ scratch,
@@ -677,7 +539,7 @@ __global__ __launch_bounds__(256, 1) void p256_verify_quad_kernel(const VerifyIt
     const int64_t i = (int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 16 + (lane >> 2);
     if (i >= n) return;
     const int role = lane & 3;
-    const QuadDev pp{role == 1, role == 2, role == 3};
+    const QuadDev pp{(role & 1) != 0, (role & 2) != 0};
     const VerifyItem it = items[i];
     aff q;
     fe r, u1, u2;
@@ -903,30 +765,18 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
         io.finish("verify status");
         return st;
     }
-    PooledBuf<jac> b_scratch(size_t(16) * size_t(n));
-    jac* d_scratch = b_scratch.p;
-    const int block = 64;
     const char* spw_env = std::getenv("UPOW_P256_SPW");
     int spw = spw_env ? std::atoi(spw_env) : 64;
     if (spw < 1 || spw > 64) spw = 64;
-    const int grid = int((n + spw - 1) / spw);
-    // Variant 1 (the one-lane default): __launch_bounds__(64, 4) -> 4 waves/SIMD at 128 VGPRs (a few
-    // spills), 7-9 % faster than the compiler's 142-VGPR / 3-wave choice (variant 0) in the A/B runs of
-    // scripts/p256_throughput.py (profiles/p256_variants_ab.txt). Variant 2: dword-major (SoA)
-    // window tables, slower (the gathers were not the bottleneck).
-    if (v == '0')
-        hipLaunchKernelGGL((p256_verify_kernel<1, false>), dim3(grid), dim3(block), 0, node_stream(), d_items, n, d_tab, d_scratch,
-                           d_st, spw);
-    else if (v == '2')
-        hipLaunchKernelGGL((p256_verify_kernel<1, true>), dim3(grid), dim3(block), 0, node_stream(), d_items, n, d_tab, d_scratch,
-                           d_st, spw);
-    else if (v == '3')  // 4 waves per workgroup
-        hipLaunchKernelGGL((p256_verify_kernel<4, false, 4>), dim3((grid + 3) / 4), dim3(256), 0, node_stream(), d_items, n, d_tab,
-                           d_scratch, d_st, spw);
-    else
-        hipLaunchKernelGGL((p256_verify_kernel<4, false>), dim3(grid), dim3(block), 0, node_stream(), d_items, n, d_tab, d_scratch,
-                           d_st, spw);
-    hck(hipGetLastError(), "p256_verify_kernel launch");
+    // one lane per signature (csrc/p256_batch.hip), one launch per kBatchSlice signatures (UPOW_P256_SLICE
+    // for the A/B): slicing a 531,200-signature batch into 128 k or 256 k launches measured 12 % / 9 % slower
+    // than one launch (each launch ends in a tail of half-idle SIMDs; profiles/r5/p256batch), so the default
+    // slice only bounds the window-table scratch (16 x 96 B per signature)
+    const char* sl_env = std::getenv("UPOW_P256_SLICE");
+    const int64_t slice = std::max<int64_t>(1024, sl_env ? std::atoll(sl_env) : kBatchSlice);
+    PooledBuf<jac> b_scratch(size_t(16) * size_t(std::min(n, slice)));
+    for (int64_t off = 0; off < n; off += slice)
+        p256_batch_launch(v, d_items + off, std::min(slice, n - off), d_tab, b_scratch.p, d_st + off, spw, node_stream());
     node_d2h(st.data(), d_st, size_t(n), "d2h status");
     return st;
 }

@@ -63,10 +63,12 @@ CLANGXX = '/opt/rocm/llvm/bin/clang++'
 # instructions. The ILP-first machine scheduler interleaves independent products instead (1,810 s_nop): the
 # block-latency kernels run one wave per SIMD, so the extra registers cost them nothing; the batch kernels
 # keep their __launch_bounds__ occupancy.
-DEVICE_FLAGS = {'p256': ['-mllvm', '-amdgpu-sched-strategy=max-ilp']}
+DEVICE_FLAGS = {'p256': ['-mllvm', '-amdgpu-sched-strategy=max-ilp']}  # p256_batch.hip: the default schedule
 # A/B builds of the P-256 kernels (build-ab/native-<variant>, shipped to the GPU box and loaded through
-# UPOW_NATIVE_SO): 'p256occ' the occupancy-first schedule, 'p256bgcd' the binary-Euclid s^-1
-AB_VARIANTS = {'p256occ': {'p256': []}, 'p256bgcd': {'p256': DEVICE_FLAGS['p256'] + ['-DUPOW_P256_INV_BGCD=1']}}
+# UPOW_NATIVE_SO): 'p256occ' the occupancy-first schedule, 'p256bgcd' the binary-Euclid s^-1,
+# 'p256batchilp' the one-lane batch kernel under the ILP-first schedule too
+AB_VARIANTS = {'p256occ': {'p256': []}, 'p256bgcd': {'p256': DEVICE_FLAGS['p256'] + ['-DUPOW_P256_INV_BGCD=1']},
+               'p256batchilp': {'p256_batch': ['-mllvm', '-amdgpu-sched-strategy=max-ilp']}}
 
 
 def _device_flags(src: Path, variant: str) -> list:
