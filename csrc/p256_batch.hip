@@ -101,6 +101,9 @@ void p256_batch_launch(char variant, const void* items, int64_t n, const void* g
     else if (variant == '2')
         hipLaunchKernelGGL((p256_verify_kernel<1, true>), dim3(grid), dim3(block), 0, stream_, d_items, n, d_tab, d_scratch,
                            status, spw);
+    else if (variant == '5')  // 3 waves per SIMD: __launch_bounds__(64, 3), up to 168 VGPRs
+        hipLaunchKernelGGL((p256_verify_kernel<3, false>), dim3(grid), dim3(block), 0, stream_, d_items, n, d_tab, d_scratch,
+                           status, spw);
     else if (variant == '3')
         hipLaunchKernelGGL((p256_verify_kernel<4, false, 4>), dim3((grid + 3) / 4), dim3(256), 0, stream_, d_items, n, d_tab,
                            d_scratch, status, spw);

@@ -48,6 +48,12 @@ for var in ('0', '1', '2', '4'):
 os.environ['UPOW_P256_VARIANT'] = 'a'  # the default: quad kernel up to 32k signatures, then one lane
 for n in (8300, 8300 * 4, 8300 * 16, 8300 * 64):  # 64 blocks = 8,300 waves: saturates the chip
     out[f'gpu_{n}'] = rate(base * (n // 8300))
+# the one-lane kernel's occupancy variants at the saturating size: 1 = 4 waves/SIMD (128 VGPRs, spills),
+# 5 = 3 waves (168 VGPRs), 0 = the compiler's choice
+for var in ('0', '1', '5'):
+    os.environ['UPOW_P256_VARIANT'] = var
+    out[f'variant{var}_gpu_531200'] = rate(base * 64)
+os.environ['UPOW_P256_VARIANT'] = 'a'
 # one-lane batch launches sliced (UPOW_P256_SLICE signatures per launch; 2^30 = one launch) at 531,200
 for sl in (131072, 262144, 1 << 30):
     os.environ['UPOW_P256_SLICE'] = str(sl)
