@@ -232,9 +232,10 @@ asyncio.run(main(sys.argv[1], sys.argv[2], int(sys.argv[4]), int(sys.argv[5]), s
 @pytest.mark.parametrize('kill_at', [5, 9])
 def test_sigkill_mid_sync_page_resumes_at_the_last_durable_block(tmp_path, kill_at, monkeypatch):
     """A page-batched sync (ledger/pagesync.py: one fdatasync for the whole page, deferred index writes) is
-    SIGKILLed in the middle of its page. Reopening gives whole blocks only and an index equal to the SQL UTXO
-    set; syncing the rest of the page from the reopened tip (what the node does: fetch from its next block id)
-    ends in the source chain's exact state."""
+    SIGKILLed in the middle of its page. Reopening gives whole blocks only (up to the last record the journal
+    writer had written; any of the page's blocks, since none is promised durable before the page ends) and an
+    index equal to the SQL UTXO set; syncing the rest of the page from the reopened tip (what the node does:
+    fetch from its next block id) ends in the source chain's exact state."""
     import asyncio
     import json
     n_blocks = 14
@@ -270,7 +271,9 @@ def test_sigkill_mid_sync_page_resumes_at_the_last_durable_block(tmp_path, kill_
         manager.Manager.difficulty = None
         try:
             t = db._tip_id()
-            assert kill_at <= t <= 2 + n_blocks
+            # inside a page nothing is promised durable before the page's one fdatasync, and the writer's I/O
+            # thread writes the block records behind the apply: the reopened tip is any whole block of the page
+            assert 2 <= t <= 2 + n_blocks
             counts = db._q('SELECT b.id, COUNT(t.tx_hash) FROM blocks b LEFT JOIN transactions t '
                            'ON t.block_hash = b.hash WHERE b.id > 2 GROUP BY b.id')
             assert len(counts) == t - 2 and all(c == TXS + 1 for _, c in counts), counts
