@@ -35,19 +35,21 @@ stale() {  # $1 = object, rest = inputs: rebuild when any input is newer
   for i in "$@"; do [ "$i" -nt "$o" ] && return 0; done
   return 1
 }
-HDRS="csrc/native.h csrc/sha256_common.h csrc/p256_field.h"
+HDRS="csrc/native.h csrc/sha256_common.h csrc/p256_field.h csrc/p256_verify.h"
 echo "== [1] host selftest (ASan + UBSan) and host pool (TSan)"
-if stale "$OUT/p256.o" csrc/p256.hip $HDRS; then
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -Xarch_host -O0 -g1 -std=c++17 -I/opt/rocm/include $SAN_HOST \
-    -c csrc/p256.hip -o "$OUT/p256.o"
-fi
+for h in p256 p256_batch; do  # the verify TU and the one-lane batch kernel's TU it launches
+  if stale "$OUT/$h.o" csrc/$h.hip $HDRS; then
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -Xarch_host -O0 -g1 -std=c++17 -I/opt/rocm/include $SAN_HOST \
+      -c csrc/$h.hip -o "$OUT/$h.o"
+  fi
+done
 for f in csrc/sha256_host.cpp csrc/sha256_ni.cpp csrc/base58.cpp csrc/p256_host.cpp tools/host_selftest.cpp; do
   o="$OUT/$(basename "${f%.cpp}").o"
   if stale "$o" "$f" $HDRS; then
     $CXX $CFLAGS -fsanitize=address,undefined -fno-sanitize-recover=undefined -pthread -c "$f" -o "$o"
   fi
 done
-$CXX -fsanitize=address,undefined -pthread "$OUT"/host_selftest.o "$OUT"/p256.o "$OUT"/sha256_host.o \
+$CXX -fsanitize=address,undefined -pthread "$OUT"/host_selftest.o "$OUT"/p256.o "$OUT"/p256_batch.o "$OUT"/sha256_host.o \
   "$OUT"/sha256_ni.o "$OUT"/base58.o "$OUT"/p256_host.o -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib -o "$OUT/host_selftest"
 # leak checking off: the HIP runtime keeps process-lifetime allocations
 ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 "$OUT/host_selftest"
