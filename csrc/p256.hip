@@ -744,6 +744,7 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
     // chip is full either way and one lane per signature does half the total work.
     const char* var = std::getenv("UPOW_P256_VARIANT");
     char v = var && var[0] ? var[0] : 'a';
+    const bool autov = v == 'a';
     if (v == 'a') v = n <= kQuadMaxBatch ? '4' : '1';
     if (v == '8') {
         PooledBuf<xz> b_tab(size_t(16) * size_t(n));
@@ -774,9 +775,33 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
     // slice only bounds the window-table scratch (16 x 96 B per signature)
     const char* sl_env = std::getenv("UPOW_P256_SLICE");
     const int64_t slice = std::max<int64_t>(1024, sl_env ? std::atoll(sl_env) : kBatchSlice);
-    PooledBuf<jac> b_scratch(size_t(16) * size_t(std::min(n, slice)));
-    for (int64_t off = 0; off < n; off += slice)
-        p256_batch_launch(v, d_items + off, std::min(slice, n - off), d_tab, b_scratch.p, d_st + off, spw, node_stream());
+    // Every one-lane wave runs the same fixed-window chain, so the kernel takes whole "rounds" of one wave
+    // lifetime: 4 waves per SIMD x 1,024 SIMDs x 64 lanes = 262,144 signatures per round on MI355X. A batch
+    // a little past a multiple of that (531,200 = 2 rounds + 6,912) paid a third round for 3 % of its work.
+    // Auto mode runs the whole rounds on the one-lane kernel and a remainder of at most kQuadMaxBatch on the
+    // four-lanes-per-signature kernel, which finishes it in a quarter of a wave lifetime.
+    int64_t n_one = n, n_quad = 0;
+    if (autov && v == '1' && spw == 64 && !sl_env && std::getenv("UPOW_P256_TAIL") == nullptr) {
+        int dev = 0, cus = 0;
+        hck(hipGetDevice(&dev), "hipGetDevice");
+        hck(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
+        const int64_t round = int64_t(cus) * 4 /* SIMDs */ * 4 /* waves per SIMD */ * 64;
+        const int64_t full = round > 0 ? (n / round) * round : 0, rem = n - full;
+        if (full > 0 && rem > 0 && rem <= kQuadMaxBatch) {
+            n_one = full;
+            n_quad = rem;
+        }
+    }
+    PooledBuf<jac> b_scratch(size_t(16) * size_t(std::min(n_one, slice)));
+    for (int64_t off = 0; off < n_one; off += slice)
+        p256_batch_launch(v, d_items + off, std::min(slice, n_one - off), d_tab, b_scratch.p, d_st + off, spw, node_stream());
+    if (n_quad) {
+        PooledBuf<xz> b_tab(size_t(16) * size_t(n_quad));
+        const int64_t waves = (n_quad + 15) / 16;
+        hipLaunchKernelGGL(p256_verify_quad_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, node_stream(),
+                           d_items + n_one, n_quad, d_tab, b_tab.p, d_st + n_one);
+        hck(hipGetLastError(), "p256_verify_quad_kernel launch (remainder)");
+    }
     node_d2h(st.data(), d_st, size_t(n), "d2h status");
     return st;
 }

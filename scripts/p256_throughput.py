@@ -48,6 +48,13 @@ for var in ('0', '1', '2', '4'):
 os.environ['UPOW_P256_VARIANT'] = 'a'  # the default: quad kernel up to 32k signatures, then one lane
 for n in (8300, 8300 * 4, 8300 * 16, 8300 * 64):  # 64 blocks = 8,300 waves: saturates the chip
     out[f'gpu_{n}'] = rate(base * (n // 8300))
+# the same 531,200 without the round-aligned split (one-lane kernel for everything: a third, 3 %-full round)
+os.environ['UPOW_P256_TAIL'] = '0'
+out['notail_split_gpu_531200'] = rate(base * 64)
+os.environ.pop('UPOW_P256_TAIL')
+# exactly two rounds (524,288) and a bigger batch (1,062,400 = 4 rounds + 14,024)
+out['gpu_524288'] = rate((base * 64)[:160 * 524288])
+out['gpu_1062400'] = rate(base * 128)
 # the one-lane kernel's occupancy variants at the saturating size: 1 = 4 waves/SIMD (128 VGPRs, spills),
 # 5 = 3 waves (168 VGPRs), 0 = the compiler's choice
 for var in ('0', '1', '5'):
