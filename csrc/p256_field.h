@@ -427,8 +427,8 @@ UPOW_HD fe sc_inv_bgcd_mont(const fe& a) {
 // 256-bit input needs; each round runs its 30 divsteps on the low 32 bits of f and g alone (they decide
 // every branch), collecting them into a 2x2 matrix scaled by 2^30, then applies the matrix to the full
 // (f, g) and to (d, e), which track f = d*a*R^-1 and g = e*a*R^-1 (mod n): e starts at R, so d ends at
-// +-a^-1*R, the Montgomery form verify_prologue wants. Fixed trip count, no data-dependent branches:
-// the wave never diverges. Cost per round: 30 divsteps of ~20 full-rate 32-bit ops, and 36 + 54 signed
+// +-a^-1*R, the Montgomery form verify_prologue wants. At most 20 rounds; a round's divsteps have no
+// data-dependent branches, and the loop stops once g is zero (for random scalars after ~18 rounds). Cost per round: 30 divsteps of ~20 full-rate 32-bit ops, and 36 + 54 signed
 // 32x32->64 multiply-adds for the matrix products; about a third of the binary Euclid above.
 struct s30 { int32_t v[9]; };
 static constexpr uint32_t kM30 = 0x3fffffffu;
@@ -550,6 +550,13 @@ UPOW_HD fe sc_inv_safegcd_mont(const fe& a) {
     s30 f = n, g = s30_from_fe(a), d{{0, 0, 0, 0, 0, 0, 0, 0, 0}}, e = s30_from_fe(fe{P256_RN});
     int32_t zeta = -1;
     for (int round = 0; round < 20; ++round) {
+        // g = 0: f = +-1 and the remaining rounds would only keep d, e in range (their matrix is
+        // diag(2^30, 1)); random inputs finish in ~517 divsteps (18 rounds), 590 bounds every input.
+        // Public data, so the exit may depend on it; a wave runs until its last lane is done.
+        uint32_t gz = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) gz |= uint32_t(g.v[i]);
+        if (gz == 0) break;
         DivMatrix t;
         zeta = divsteps_30(zeta, uint32_t(f.v[0]) | (uint32_t(f.v[1]) << 30), uint32_t(g.v[0]) | (uint32_t(g.v[1]) << 30), t);
         s30_update_de(d, e, t, n);
@@ -559,7 +566,8 @@ UPOW_HD fe sc_inv_safegcd_mont(const fe& a) {
     const int32_t sf = f.v[8] >> 31;
 #pragma unroll
     for (int i = 0; i < 9; ++i) d.v[i] = (d.v[i] ^ sf) - sf;
-    s30_carry(d);                        // (-n, 2n)
+    s30_carry(d);                        // (-2n, 2n): d was in (-2n, n) and may have been negated
+    s30_add_masked(d, n, d.v[8] >> 31);  // (-n, 2n)
     s30_add_masked(d, n, d.v[8] >> 31);  // [0, 2n)
     s30 t = d;                           // d - n, kept when non-negative
 #pragma unroll
