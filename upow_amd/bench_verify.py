@@ -837,6 +837,7 @@ async def _run_sync(args, ctx, device, utxo_backend):
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
+    cpu0 = _thread_cpu()
     t0 = time.perf_counter()
     errors = []
     per_page = max(1, int(getattr(args, 'sync_page_blocks', 1000) or 1000))  # /get_blocks returns <= 1,000
@@ -847,7 +848,9 @@ async def _run_sync(args, ctx, device, utxo_backend):
     dst.flush()  # the SQL tables hold every block (the journal is the commit point)
     ctx.synchronize()
     ctx.barrier()
-    wall = ctx.allreduce_max_f(time.perf_counter() - t0)
+    wall_local = time.perf_counter() - t0
+    threads_cpu = _thread_cpu_delta(cpu0, _thread_cpu(), wall_local)
+    wall = ctx.allreduce_max_f(wall_local)
     if prof is not None:
         _dump_profile(prof, os.environ['UPOW_BENCH_PROFILE'])
     assert (await dst.get_last_block())['hash'] == page[-1]['block']['hash']
@@ -862,7 +865,39 @@ async def _run_sync(args, ctx, device, utxo_backend):
         'page': ({k: (round(v, 4) if isinstance(v, float) else v) for k, v in pagesync.stats.items()}
                  if pagesync.ENABLED else None),
         'journal_fdatasyncs': writer.get('fdatasyncs'), 'journal_group_records': writer.get('group_records'),
-        'utxo_deferred_flushes': dst.utxo.deferred_flushes}
+        'utxo_deferred_flushes': dst.utxo.deferred_flushes, 'threads_cpu': threads_cpu}
+
+
+def _thread_cpu() -> dict:
+    """CPU seconds (user + system) per thread of this process, keyed by 'name/tid' (/proc/self/task)."""
+    out = {}
+    tick = os.sysconf('SC_CLK_TCK')
+    try:
+        for tid in os.listdir('/proc/self/task'):
+            try:
+                with open(f'/proc/self/task/{tid}/stat') as f:
+                    st = f.read()
+                with open(f'/proc/self/task/{tid}/comm') as f:
+                    name = f.read().strip()
+            except OSError:
+                continue
+            fields = st[st.rindex(')') + 2:].split()
+            out[f'{name}/{tid}'] = (int(fields[11]) + int(fields[12])) / tick
+    except OSError:
+        pass
+    return out
+
+
+def _thread_cpu_delta(before: dict, after: dict, wall: float, top: int = 12) -> dict:
+    """The threads that used the most CPU over a timed region: {name: cpu seconds}, plus the total as a
+    multiple of the wall time (how many cores the process kept busy)."""
+    d = {k: round(after[k] - before.get(k, 0.0), 3) for k in after}
+    agg = {}
+    for k, v in d.items():
+        name = k.rsplit('/', 1)[0]
+        agg[name] = round(agg.get(name, 0.0) + v, 3)
+    busy = sorted(agg.items(), key=lambda kv: -kv[1])[:top]
+    return {'cores_busy': round(sum(d.values()) / wall, 2) if wall > 0 else None, 'top_threads_cpu_s': dict(busy)}
 
 
 def _sync_data_label(args) -> str:
@@ -973,6 +1008,7 @@ async def _run_cluster_sync(args, ctx, device, utxo_backend):
             import cProfile
             prof = cProfile.Profile()
             prof.enable()
+        cpu0 = _thread_cpu()
         t0 = time.perf_counter()
         errors = []
         timed = page[args.warmup:]
@@ -983,6 +1019,7 @@ async def _run_cluster_sync(args, ctx, device, utxo_backend):
         c.send('status')
         st = c.status(dst)  # every replica has applied the last page when it answers
         wall = time.perf_counter() - t0
+        threads_cpu = _thread_cpu_delta(cpu0, _thread_cpu(), wall)
         if prof is not None:
             _dump_profile(prof, os.environ['UPOW_BENCH_PROFILE'])
         await cluster.leader_quit()
@@ -995,6 +1032,7 @@ async def _run_cluster_sync(args, ctx, device, utxo_backend):
     return sum(counts[args.warmup:]), wall, {
         'blocks_per_s': round(args.steps / wall, 1), 'tx_counts': _counts_label(args, counts[args.warmup:]),
         'blocks_per_page': per_page, 'sync_path': 'page', 'op_stream': info,
+        'threads_cpu': threads_cpu if c.leader else None,
         'page': {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pagesync.stats.items()},
         'replicas': [{'rank': x['rank'], 'height': x['height'], 'utxo_hash': x['utxo_hash']} for x in st] if st else None}
 

@@ -196,7 +196,7 @@ def _native_vote_stats(ctx) -> dict:
     if not n:
         return {}
     return {'native_vote': {'votes': int(n), 'gather_us': round(tg / n * 1e6, 1), 'copy_us': round(tc / n * 1e6, 1),
-                            'event_us': round(te / n * 1e6, 1)}}
+                            'event_us': round(te / n * 1e6, 1), 'call_us': round(ctx.vote_call_s / n * 1e6, 1)}}
 
 
 # ---------------------------------------------------------------------------------------------- commit gate

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import os
 import threading
+import time
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -46,6 +47,7 @@ class DistContext:
     owner: Optional[int] = None  # thread ident allowed to issue collectives (None: any thread)
     fatal: bool = field(default_factory=lambda: os.environ.get('UPOW_DIST_FATAL', '1') != '0')
     collectives: int = 0  # issued so far (tests, /cluster_info)
+    vote_call_s: float = 0.0  # host time inside the native vote's start calls (/cluster_info)
 
     @property
     def is_distributed(self) -> bool:
@@ -129,10 +131,12 @@ class DistContext:
         if nv is not None:  # RCCL: the native communicator of csrc/rccl_vote.hip
             L, h = nv
             self._enter('vote')
+            t0 = time.perf_counter()
             try:
                 L.rccl_vote_start(h, 1 if v else 0)
             except Exception as e:
                 self._failed('vote', e)
+            self.vote_call_s += time.perf_counter() - t0  # the native call alone (cluster info: vote_call_us)
             return ('native', L, h)
         import torch
         import torch.distributed as dist
