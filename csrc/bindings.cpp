@@ -22,6 +22,7 @@ void register_stall_probe(py::module_& m);  // stall_probe.cpp
 void register_log_appender(py::module_& m);  // log_appender.cpp
 void register_http_wire(py::module_& m);  // http_wire.cpp
 void register_mempool_index(py::module_& m);  // mempool_index.cpp
+void register_jsonspan(py::module_& m);  // jsonspan.cpp
 }
 
 static PowJobHost make_job(py::bytes header, uint32_t tmask, uint32_t tword, uint32_t frac_shift,
@@ -62,6 +63,7 @@ PYBIND11_MODULE(_native, m) {
     register_log_appender(m);
     register_http_wire(m);
     register_mempool_index(m);
+    register_jsonspan(m);
 
     // glibc allocator thresholds (mallopt): every 2 MB block's columns are fresh multi-megabyte Python bytes;
     // above the (dynamic) mmap threshold each one is a new mapping whose pages fault in on first write, and

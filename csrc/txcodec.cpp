@@ -166,25 +166,62 @@ struct MerkleJob {
     }
 };
 
+// A zero-copy view of a str's text (compact ASCII str objects expose their buffer).
+static void str_view(PyObject* o, const char*& p, size_t& len) {
+    if (!PyUnicode_Check(o)) throw py::type_error("transaction hex must be str");
+    Py_ssize_t sz = 0;
+    p = PyUnicode_AsUTF8AndSize(o, &sz);
+    if (!p) throw py::error_already_set();
+    len = size_t(sz);
+}
+
+static py::dict decode_views(const std::vector<const char*>& srcp, const std::vector<size_t>& srcl, int threads,
+                             PyObject* hexes);
+
 // decode_block_txs(hexes, threads) -> dict (see module docstring of upow_amd/ledger/fastpath.py)
 static py::dict decode_block_txs(py::list hexes, int threads) {
-    const int64_t n = int64_t(hexes.size());
-    const size_t N = static_cast<size_t>(n);
-    // zero-copy views of the input hex strings (compact ASCII str objects expose their buffer)
+    const size_t N = size_t(hexes.size());
     std::vector<const char*> srcp(N);
     std::vector<size_t> srcl(N);
-    // a reference per str: the views stay valid while the GIL is released even if another thread edits the list
-    std::vector<py::object> keep(N);
-    for (size_t i = 0; i < N; ++i) {
-        PyObject* o = PyList_GET_ITEM(hexes.ptr(), Py_ssize_t(i));
-        keep[i] = py::reinterpret_borrow<py::object>(o);
-        if (!PyUnicode_Check(o)) throw py::type_error("transaction hex must be str");
-        Py_ssize_t sz = 0;
-        const char* p = PyUnicode_AsUTF8AndSize(o, &sz);
-        if (!p) throw py::error_already_set();
-        srcp[i] = p;
-        srcl[i] = size_t(sz);
+    // the list holds a reference per str; the GIL-free pool reads only views taken here, and a copy of the
+    // list (not the caller's) keeps them alive even if another thread edits the caller's list meanwhile
+    py::list own = py::reinterpret_steal<py::list>(PyList_GetSlice(hexes.ptr(), 0, Py_ssize_t(N)));
+    if (!own) throw py::error_already_set();
+    for (size_t i = 0; i < N; ++i) str_view(PyList_GET_ITEM(own.ptr(), Py_ssize_t(i)), srcp[i], srcl[i]);
+    return decode_views(srcp, srcl, threads, own.ptr());
+}
+
+// decode_block_spans(body, spans, extra, threads): the same decode for txs that are (start, length) spans
+// of one request body (csrc/jsonspan.cpp), followed by the str txs of ``extra`` -- no Python str per tx.
+// The returned dict has no "hex" list; "hex_fix" lists (index, canonical hex) for the txs whose text is
+// not already their canonical lowercase hex (upow_amd/utils/hexspans.py builds d['hex'] from it).
+static py::dict decode_block_spans(py::bytes body, py::bytes spans, py::list extra, int threads) {
+    char* b = nullptr;
+    Py_ssize_t blen = 0;
+    if (PyBytes_AsStringAndSize(body.ptr(), &b, &blen) != 0) throw py::error_already_set();
+    const std::string sp = spans;
+    if (sp.size() % 16) throw py::value_error("spans: (start, length) int64 pairs");
+    const size_t ns = sp.size() / 16, ne = size_t(extra.size()), N = ns + ne;
+    std::vector<const char*> srcp(N);
+    std::vector<size_t> srcl(N);
+    for (size_t i = 0; i < ns; ++i) {
+        int64_t st, ln;
+        std::memcpy(&st, sp.data() + 16 * i, 8);
+        std::memcpy(&ln, sp.data() + 16 * i + 8, 8);
+        if (st < 0 || ln < 0 || st > blen || ln > blen - st) throw py::value_error("span outside the body");
+        srcp[i] = b + st;
+        srcl[i] = size_t(ln);
     }
+    py::list own = py::reinterpret_steal<py::list>(PyList_GetSlice(extra.ptr(), 0, Py_ssize_t(ne)));
+    if (!own) throw py::error_already_set();
+    for (size_t i = 0; i < ne; ++i) str_view(PyList_GET_ITEM(own.ptr(), Py_ssize_t(i)), srcp[ns + i], srcl[ns + i]);
+    return decode_views(srcp, srcl, threads, nullptr);
+}
+
+static py::dict decode_views(const std::vector<const char*>& srcp, const std::vector<size_t>& srcl, int threads,
+                             PyObject* hexes) {
+    const size_t N = srcp.size();
+    const int64_t n = int64_t(N);
     auto job = std::make_shared<MerkleJob>();
     job->lease.emplace();
     std::vector<DecTx>& txs = job->lease->get().txs;
@@ -351,20 +388,31 @@ static py::dict decode_block_txs(py::list hexes, int threads) {
     // the stored hex column as str objects (object-path parity, mempool and cluster mirroring): the input
     // string is reused when it already is the canonical lowercase hex of the tx
     auto tA = std::chrono::steady_clock::now();
-    py::list canon_hex = new_list(N);
-    for (size_t i = 0; i < N; ++i) {
-        const DecTx& t = txs[i];
-        if (t.canonical && !t.upper_hex && srcl[i] == 2 * t.canon.size()) {
-            PyObject* obj = PyList_GET_ITEM(hexes.ptr(), Py_ssize_t(i));
-            Py_INCREF(obj);
-            PyList_SET_ITEM(canon_hex.ptr(), Py_ssize_t(i), obj);
-        } else {
-            const std::string h = to_hex(t.canon.data(), t.canon.size());
-            PyList_SET_ITEM(canon_hex.ptr(), Py_ssize_t(i), ascii_str(h.data(), h.size()));
+    if (hexes) {
+        py::list canon_hex = new_list(N);
+        for (size_t i = 0; i < N; ++i) {
+            const DecTx& t = txs[i];
+            if (t.canonical && !t.upper_hex && srcl[i] == 2 * t.canon.size()) {
+                PyObject* obj = PyList_GET_ITEM(hexes, Py_ssize_t(i));
+                Py_INCREF(obj);
+                PyList_SET_ITEM(canon_hex.ptr(), Py_ssize_t(i), obj);
+            } else {
+                const std::string h = to_hex(t.canon.data(), t.canon.size());
+                PyList_SET_ITEM(canon_hex.ptr(), Py_ssize_t(i), ascii_str(h.data(), h.size()));
+            }
         }
+        d["hex"] = canon_hex;
+    } else {
+        py::list fix;
+        for (size_t i = 0; i < N; ++i) {
+            const DecTx& t = txs[i];
+            if (t.canonical && !t.upper_hex && srcl[i] == 2 * t.canon.size()) continue;
+            const std::string h = to_hex(t.canon.data(), t.canon.size());
+            fix.append(py::make_tuple(int64_t(i), py::reinterpret_steal<py::object>(ascii_str(h.data(), h.size()))));
+        }
+        d["hex_fix"] = fix;
     }
     auto tB = std::chrono::steady_clock::now();
-    d["hex"] = canon_hex;
     auto t2 = std::chrono::steady_clock::now();
     d["merkle_job"] = job;
     if (prof) {
@@ -839,19 +887,14 @@ static py::tuple spent_index_records(py::buffer keys_b, py::buffer tag_b) {
 // Cluster op frames (upow_amd/parallel/cluster.py pack_txs / unpack_txs): a block's tx hex strings as raw
 // bytes, u32 count then u32 length + bytes per tx, hex-decoded on the host pool without the GIL; and back
 // to lower-case hex strings on the follower. A string that is not even-length hex raises ValueError.
-static py::bytes pack_tx_hexes(py::list hexes, int threads) {
-    const size_t n = hexes.size();
-    std::vector<const char*> ptr(n);
+// The frame of pack_tx_hexes from text views (the caller keeps the text alive).
+static py::bytes pack_views(const std::vector<const char*>& ptr, const std::vector<size_t>& hexlen, int threads) {
+    const size_t n = ptr.size();
     std::vector<size_t> len(n), off(n + 1);
     off[0] = 4;
     for (size_t i = 0; i < n; ++i) {
-        PyObject* o = hexes[i].ptr();
-        if (!PyUnicode_Check(o)) throw py::type_error("tx hex must be str");
-        Py_ssize_t k = 0;
-        ptr[i] = PyUnicode_AsUTF8AndSize(o, &k);
-        if (!ptr[i]) throw py::error_already_set();
-        if (k % 2) throw py::value_error("tx hex of odd length");
-        len[i] = size_t(k) / 2;
+        if (hexlen[i] % 2) throw py::value_error("tx hex of odd length");
+        len[i] = hexlen[i] / 2;
         off[i + 1] = off[i] + 4 + len[i];
     }
     char* out = nullptr;
@@ -860,7 +903,7 @@ static py::bytes pack_tx_hexes(py::list hexes, int threads) {
     std::memcpy(out, &cnt, 4);
     std::atomic<bool> bad{false};
     {
-        py::gil_scoped_release nogil;  // the str objects stay alive: `hexes` holds them
+        py::gil_scoped_release nogil;
         parallel_for(int64_t(n), threads, [&](int64_t i) {
             uint8_t* d = reinterpret_cast<uint8_t*>(out) + off[size_t(i)];
             const uint32_t l = uint32_t(len[size_t(i)]);
@@ -877,6 +920,40 @@ static py::bytes pack_tx_hexes(py::list hexes, int threads) {
     }
     if (bad.load()) throw py::value_error("tx hex holds a non-hex character");
     return res;
+}
+
+static py::bytes pack_tx_hexes(py::list hexes, int threads) {
+    const size_t n = hexes.size();
+    std::vector<const char*> ptr(n);
+    std::vector<size_t> len(n);
+    py::list own = py::reinterpret_steal<py::list>(PyList_GetSlice(hexes.ptr(), 0, Py_ssize_t(n)));
+    if (!own) throw py::error_already_set();
+    for (size_t i = 0; i < n; ++i) str_view(PyList_GET_ITEM(own.ptr(), Py_ssize_t(i)), ptr[i], len[i]);
+    return pack_views(ptr, len, threads);  // `own` keeps the str objects alive
+}
+
+// pack_tx_hexes for txs given as (start, length) spans of one body, then the str txs of ``extra``.
+static py::bytes pack_tx_spans(py::bytes body, py::bytes spans, py::list extra, int threads) {
+    char* b = nullptr;
+    Py_ssize_t blen = 0;
+    if (PyBytes_AsStringAndSize(body.ptr(), &b, &blen) != 0) throw py::error_already_set();
+    const std::string sp = spans;
+    if (sp.size() % 16) throw py::value_error("spans: (start, length) int64 pairs");
+    const size_t ns = sp.size() / 16, ne = size_t(extra.size());
+    std::vector<const char*> ptr(ns + ne);
+    std::vector<size_t> len(ns + ne);
+    for (size_t i = 0; i < ns; ++i) {
+        int64_t st, ln;
+        std::memcpy(&st, sp.data() + 16 * i, 8);
+        std::memcpy(&ln, sp.data() + 16 * i + 8, 8);
+        if (st < 0 || ln < 0 || st > blen || ln > blen - st) throw py::value_error("span outside the body");
+        ptr[i] = b + st;
+        len[i] = size_t(ln);
+    }
+    py::list own = py::reinterpret_steal<py::list>(PyList_GetSlice(extra.ptr(), 0, Py_ssize_t(ne)));
+    if (!own) throw py::error_already_set();
+    for (size_t i = 0; i < ne; ++i) str_view(PyList_GET_ITEM(own.ptr(), Py_ssize_t(i)), ptr[ns + i], len[ns + i]);
+    return pack_views(ptr, len, threads);
 }
 
 static py::list unpack_tx_hexes(py::bytes frame, int threads) {
@@ -997,6 +1074,7 @@ void register_txcodec(py::module_& m) {
     m.def("resolve_groups", &resolve_groups, py::arg("grouped"), py::arg("in_start"), py::arg("sig_start"),
           py::arg("tx_type"), py::arg("pay_addr"), py::arg("pay_len"), py::arg("job_input"));
     m.def("pack_tx_hexes", &pack_tx_hexes, py::arg("hexes"), py::arg("threads") = 8);
+    m.def("pack_tx_spans", &pack_tx_spans, py::arg("body"), py::arg("spans"), py::arg("extra"), py::arg("threads") = 8);
     m.def("unpack_tx_hexes", &unpack_tx_hexes, py::arg("frame"), py::arg("threads") = 8);
     m.def("output_index_records", &output_index_records, py::arg("txid"), py::arg("index"), py::arg("tag"),
           py::arg("amount"), py::arg("addr"), py::arg("len"), py::arg("stake"));
@@ -1012,6 +1090,8 @@ void register_txcodec(py::module_& m) {
           py::arg("over_len") = py::none());
     m.def("decode_block_txs", &decode_block_txs, py::arg("hexes"), py::arg("threads") = 8,
           "Decode, canonicalise and hash a block's transactions (see csrc/txcodec.cpp)");
+    m.def("decode_block_spans", &decode_block_spans, py::arg("body"), py::arg("spans"), py::arg("extra"),
+          py::arg("threads") = 8, "decode_block_txs for txs given as (start, length) spans of a request body");
     m.def("address_pairs", &address_pairs, py::arg("in_blob"), py::arg("in_off"), py::arg("in_start"),
           py::arg("out_blob"), py::arg("out_off"), py::arg("out_start"), py::arg("threads") = 8);
     m.def("input_address_strings", &input_address_strings, py::arg("addrs64"), py::arg("lens"), py::arg("in_start"),

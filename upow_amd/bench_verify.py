@@ -22,6 +22,7 @@ import time
 from decimal import Decimal
 
 from .constants import SMALLEST
+from .utils import hexspans
 
 
 def batch_keys(n: int, rng, threads: int = 16):
@@ -503,9 +504,12 @@ async def _run(args, ctx, device, utxo_backend):
     key_setup = aging.pop('distinct_key_setup_s', None)
     if aging:
         db.flush()
-    # (untimed) the tx strings as a node holds them: parsed from one JSON body (/push_block, sync), allocated
-    # together, not scattered over the generator's setup heap (scripts/gov_ab.py, docs/ROUND4.md section 8)
-    blocks = [json.loads(json.dumps(b)) for b in blocks]
+    # (untimed) the txs as a node holds them: parsed from a /push_block JSON body (node/main.py _json_body),
+    # which leaves the tx array inside the body bytes (utils/hexspans.py); the parse itself is timed apart
+    bodies = [json.dumps({'block_content': '', 'txs': b}).encode() for b in blocks]
+    extra_parse = _body_parse_ms(bodies[0]) if bodies else None
+    blocks = [hexspans.loads(body)['txs'] for body in bodies]
+    del bodies
     gov_probe = await _governance_probe(db) if gov else None
     # mine every header up front (untimed), each at the difficulty the chain will require of it
     headers, difficulties = await premine_headers(db, addr, blocks, base_ts, device)
@@ -585,7 +589,8 @@ async def _run(args, ctx, device, utxo_backend):
     writer = db.writer.stats() if db.writer is not None else None
     if writer is not None:
         writer = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in writer.items() if k != 'error'}
-    extra = {'drain_s': drain, 'writer': writer, 'window_unix': [unix_start, time.time()], 'governance': gov_probe,
+    extra = {'body_parse': extra_parse, 'drain_s': drain, 'writer': writer, 'window_unix': [unix_start, time.time()],
+             'governance': gov_probe,
              'difficulties': sorted({str(d) for d in difficulties}),
              'segments': [(t, w) for t, w in zip(seg_txs, seg_walls)],
              'aging': aging or None, 'queue_trace': queue_trace, 'key_setup_s': key_setup}
@@ -595,6 +600,25 @@ async def _run(args, ctx, device, utxo_backend):
             db._q1('SELECT outputs_addresses FROM transactions WHERE tx_hex LIKE ? LIMIT 1',
                    ('%' + (await db.get_last_block())['hash'] + '%',))[0]))
     return total_txs, wall, stages, len(blocks[0]), sorted(paths), extra
+
+
+def _as_fetched(page: list) -> list:
+    """(untimed) /get_blocks rows as a syncing node holds them: parsed by peers.fetch_json from the JSON
+    body, each row's tx array left inside the body bytes (utils/hexspans.py)."""
+    return hexspans.loads(json.dumps(page).encode())
+
+
+def _body_parse_ms(body: bytes, reps: int = 5) -> dict:
+    """Median ms to parse one /push_block body: json.loads (what the framework did) against the native
+    parse that keeps the tx array in the body (utils/hexspans.py)."""
+    def med(fn):
+        ts = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            fn(body)
+            ts.append(time.perf_counter() - t)
+        return round(sorted(ts)[len(ts) // 2] * 1000, 3)
+    return {'body_mb': round(len(body) / 2**20, 2), 'json_loads': med(json.loads), 'native_spans': med(hexspans.loads)}
 
 
 def run_verify_bench(args, ctx):
@@ -660,6 +684,7 @@ def run_verify_bench(args, ctx):
         # materialiser's catch-up after the last block (inside the timed region)
         'commit_latency_ms': avg.get('block_s'),
         'final_drain_ms': round(extra['drain_s'] * 1000, 2),
+        **({'push_body_parse_ms': extra['body_parse']} if extra.get('body_parse') else {}),
         'ledger_writer': extra['writer'],
         'window_unix': extra['window_unix'],
         'difficulties': extra.get('difficulties'),
@@ -815,6 +840,7 @@ async def _run_sync(args, ctx, device, utxo_backend):
         part = await src.get_blocks(3 + len(page), n_blocks - len(page))
         assert part, 'source ledger returned an empty page'
         page += part
+    page = _as_fetched(page)
     assert len(page) == n_blocks and all(len(p['transactions']) == counts[b] + 1 for b, p in enumerate(page))
     retargets = sorted({str(b['block']['difficulty']) for b in page})
     src.close()
@@ -984,6 +1010,7 @@ async def _run_cluster_sync(args, ctx, device, utxo_backend):
         while len(page) < n_blocks:
             part = await src.get_blocks(3 + len(page), n_blocks - len(page))
             page += part
+        page = _as_fetched(page)
         src.close()
     dst, _, _, _ = await _setup(n_blocks, args.txs, seed, utxo_backend, device, base_ts=base_ts, make_blocks=False,
                                 ledger_path=_ledger_path(args, ctx), distinct_keys=_distinct(args), tx_counts=counts)

@@ -45,6 +45,7 @@ from ..ops import p256 as op
 from ..ops.native import gpu_available, lib
 from ..utils import metrics, roctx
 from ..utils.codec import TransactionType, get_transaction_type_from_message
+from ..utils.hexspans import HexSpans
 from ..utils.logger import get_logger
 from .govcheck import BlockGovernance
 from ..utils.cpus import cpu_budget  # noqa: F401 (re-exported: node/__main__.py)
@@ -82,13 +83,29 @@ def _i32(d, k):
     return np.frombuffer(d[k], dtype=np.int32)
 
 
+def decode_raw(tx_hexes, threads: int) -> dict:
+    """The codec's dict for a list of str or a :class:`~upow_amd.utils.hexspans.HexSpans` (read in place
+    from its body: csrc/txcodec.cpp ``decode_block_spans``)."""
+    if isinstance(tx_hexes, HexSpans):
+        return lib().decode_block_spans(tx_hexes.buf, np.ascontiguousarray(tx_hexes.spans).tobytes(),
+                                        list(tx_hexes.extra), threads)
+    return lib().decode_block_txs(tx_hexes if isinstance(tx_hexes, list) else list(tx_hexes), threads)
+
+
 def decode(tx_hexes: List[str], threads: int = 0) -> Optional[dict]:
     """Native decode; None when the block needs the object path."""
     if not ENABLED:
         return None
-    d = lib().decode_block_txs(list(tx_hexes), threads or THREADS)
+    d = decode_raw(tx_hexes, threads or THREADS)
     if not d['all_fast']:
         return None
+    if isinstance(tx_hexes, HexSpans):  # the txs' text is the body's; str objects only for the rare fixes
+        fix = d.pop('hex_fix')
+        if fix:
+            tx_hexes = tx_hexes.tolist()
+            for k, h in fix:
+                tx_hexes[k] = h
+        d['hex'] = tx_hexes
     # tx types from the messages: decided natively except for encodings only Python's int() can judge
     tx_type = np.frombuffer(d['tx_type'], dtype=np.uint8).copy()
     ask = np.nonzero(tx_type == 255)[0]
@@ -435,9 +452,11 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         txs_retry = job_tx[retry].astype(np.int64)
         # one native batch (host pool) of SHA-256 over the signed prefix of each failing tx's hex text:
         # a hostile block full of bad signatures costs one pass, not a Python loop per signature
-        rr[:, 128:] = np.frombuffer(lib().sha256_hex_prefixes(d['hex'], txs_retry,
-                                                              2 * signed_len[txs_retry].astype(np.int64), THREADS),
-                                    np.uint8).reshape(-1, 32)
+        hx, at = d['hex'], txs_retry
+        if not isinstance(hx, list):  # a HexSpans: str objects for the failing txs only
+            hx, at = [hx[k] for k in txs_retry.tolist()], np.arange(len(txs_retry), dtype=np.int64)
+        rr[:, 128:] = np.frombuffer(lib().sha256_hex_prefixes(hx, at, 2 * signed_len[txs_retry].astype(np.int64),
+                                                              THREADS), np.uint8).reshape(-1, 32)
         st2 = validate._verify(np.ascontiguousarray(rr).tobytes(), None)
         status[retry] = np.where(st2 == op.VALID, op.VALID, status[retry])
     if np.any(status != op.VALID):

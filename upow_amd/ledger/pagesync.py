@@ -43,6 +43,7 @@ import numpy as np
 from ..ops import p256 as op
 from ..ops.native import gpu_available, lib
 from ..utils.codec import OutputType, TransactionType
+from ..utils.hexspans import HexSpans
 from ..utils.logger import get_logger
 from .utxo import MISSING, PAYLOAD_DTYPE, TAG_BY_TABLE, make_payload, pack_records
 
@@ -85,8 +86,13 @@ def _coinbase_index(hexes: List[str]) -> Optional[int]:
     """The first tx the codec flags as a coinbase (specifier 36). A coinbase's specifier is its last byte, so
     only txs whose hex ends in 24 are decoded to ask."""
     L = lib()
-    for k, h in enumerate(hexes):
-        if h.endswith('24') and L.decode_block_txs([h], 1)['flags'][0] == 3:
+    if isinstance(hexes, HexSpans):  # the tails read from the body: a str only for the candidates
+        tails = hexes.tail2() + [h[-2:].encode() for h in hexes.extra]
+        cand = [k for k, t in enumerate(tails) if t == b'24']
+    else:
+        cand = [k for k, h in enumerate(hexes) if h.endswith('24')]
+    for k in cand:
+        if L.decode_block_txs([hexes[k]], 1)['flags'][0] == 3:
             return k
     return None
 
@@ -95,7 +101,8 @@ def prepare(info: dict) -> Item:
     """Host-thread half of a block (no ledger state): split off the coinbase candidate, decode the rest,
     and finish the merkle root now (the codec's workspace goes back to its pool)."""
     from . import fastpath
-    hexes = list(info['transactions'])
+    txs = info['transactions']
+    hexes = txs if isinstance(txs, HexSpans) else list(txs)
     k = _coinbase_index(hexes)
     cb_hex = None
     if k is not None:
@@ -106,7 +113,7 @@ def prepare(info: dict) -> Item:
     dec = fastpath.decode(hexes, threads=1 if len(hexes) < 512 else fastpath.THREADS)
     if dec is not None:
         dec['merkle_job'].result()
-    return Item(info['block'], list(info['transactions']), hexes, cb_hex, dec)
+    return Item(info['block'], txs if isinstance(txs, HexSpans) else list(txs), hexes, cb_hex, dec)
 
 
 def _key64(keys36: np.ndarray) -> np.ndarray:
@@ -383,7 +390,7 @@ async def create_blocks(blocks: list, error_list: list = None, mirror: bool = Tr
                     if isinstance(cand, CoinbaseTransaction):
                         cb = cand
                     else:  # not what the scan assumed: the whole block goes through the ordinary decode
-                        it.hexes = list(it.all_hexes)
+                        it.hexes = it.all_hexes[:]
                         it.dec = None
                 cbs.append(cb)
             plan = build_plan(db, items, cbs, ctx)

@@ -26,8 +26,10 @@ from decimal import Decimal
 from typing import Annotated, Optional, Union
 from urllib.parse import urlsplit
 
+import numpy as np
 from fastapi import Body, FastAPI, Header, Query
 from fastapi.encoders import jsonable_encoder
+from fastapi.exceptions import RequestValidationError
 from fastapi.responses import PlainTextResponse, RedirectResponse
 from starlette.background import BackgroundTasks
 from starlette.middleware.cors import CORSMiddleware
@@ -50,8 +52,9 @@ from ..ledger.manager import (Manager, block_to_bytes, calculate_difficulty, cle
                               create_block_in_syncing_old, get_circulating_supply, get_difficulty,
                               get_inodes_from_cache, get_transactions_merkle_tree, split_block_content)
 from ..models.transaction import CoinbaseTransaction, Transaction
-from ..utils import codec
+from ..utils import codec, hexspans
 from ..utils.codec import sha256, timestamp
+from ..utils.hexspans import HexSpans
 from ..utils.logger import get_logger
 from ..websocket.endpoint import (broadcast_new_block, broadcast_new_transaction, router as websocket_router,
                                   shutdown_websocket_manager, start_websocket_manager, transaction_listeners)
@@ -242,7 +245,7 @@ async def propagate(path: str, args: dict, ignore_url=None, nodes: list = None):
 def _scan_sync_block(hexes: list):
     """Host-thread half of a sync step (no ledger state involved): find the coinbase candidate
     (txcodec flag 3 = specifier 36) and decode the remaining txs for the native block path."""
-    flags = lib().decode_block_txs(hexes, fastpath.THREADS)['flags'] if hexes else b''
+    flags = fastpath.decode_raw(hexes, fastpath.THREADS)['flags'] if hexes else b''
     k = next((i for i, f in enumerate(flags) if f == 3), None)
     rest = hexes if k is None else hexes[:k] + hexes[k + 1:]
     return k, (fastpath.decode(rest) if rest else None)
@@ -280,7 +283,7 @@ async def create_blocks_per_block(blocks: list, error_list=None) -> bool:
     i = last_block['id'] + 1
     loop = asyncio.get_running_loop()
     pool = _sync_decoder()
-    hexes_of = [list(b['transactions']) for b in blocks]
+    hexes_of = [b['transactions'][:] for b in blocks]  # a list, or a HexSpans read from the page body
     ahead = loop.run_in_executor(pool, _scan_sync_block, hexes_of[0]) if blocks else None
     for n, block_info in enumerate(blocks):
         block = block_info['block']
@@ -294,7 +297,7 @@ async def create_blocks_per_block(blocks: list, error_list=None) -> bool:
             cand = await Transaction.from_hex(hexes[cb_k])
             if isinstance(cand, CoinbaseTransaction):
                 cb_tx = cand
-                del hexes[cb_k]
+                hexes = hexes[:cb_k] + hexes[cb_k + 1:]
             else:
                 dec = None  # not what the scan assumed: decode inline below
         block_content = block.get('content')
@@ -716,11 +719,26 @@ async def send_to_address(request: Request, background_tasks: BackgroundTasks, t
     return await verify_and_push_tx(tx, request, background_tasks)
 
 
+async def _json_body(request: Request):
+    """The request's JSON body as ``Body(False)`` gave it (False when there is none), parsed by
+    ``utils.hexspans.loads``; a malformed body is the framework's 422."""
+    raw = await request.body()
+    if not raw:
+        return False
+    try:
+        return hexspans.loads(raw)
+    except ValueError as e:
+        raise RequestValidationError([{'type': 'json_invalid', 'loc': ('body', 0), 'msg': 'JSON decode error',
+                                       'input': {}, 'ctx': {'error': str(e)}}])
+
+
 @app.post('/push_block')
 @app.get('/push_block')
 async def push_block(request: Request, background_tasks: BackgroundTasks, block_content: str = '', txs='',
-                     block_no: int = None, body=Body(False)):
-    """main.py:521-652."""
+                     block_no: int = None):
+    """main.py:521-652. The JSON body is read here, not by the framework: its tx array stays inside the body
+    bytes (utils/hexspans.py) and the native decoder reads the txs from there."""
+    body = await _json_body(request)
     if is_syncing:
         return {'ok': False, 'error': 'Node is already syncing'}
     if codec.getting_active_inodes:
@@ -758,12 +776,17 @@ async def push_block(request: Request, background_tasks: BackgroundTasks, block_
     # full tx hex and mempool hashes, in the reference's order (full txs first, main.py:587-600); the
     # block then goes through the native block path (ledger/fastpath.py), which defers to the object
     # path for anything beyond plain transfers
-    final_hexes, hashes = [], []
-    for tx_hex in txs:
-        if len(tx_hex) == 64:
-            hashes.append(tx_hex)
-        else:
-            final_hexes.append(tx_hex)
+    if isinstance(txs, HexSpans):
+        is_hash = txs.lengths == 64
+        hashes = [txs[k] for k in np.nonzero(is_hash)[0].tolist()]
+        final_hexes = txs.take(np.nonzero(~is_hash)[0])
+    else:
+        final_hexes, hashes = [], []
+        for tx_hex in txs:
+            if len(tx_hex) == 64:
+                hashes.append(tx_hex)
+            else:
+                final_hexes.append(tx_hex)
     if hashes:
         # on a worker thread: the mempool index lock may be held by a block confirm on the ledger thread
         pending_hexes = await asyncio.to_thread(db.pending_hex_by_hash, hashes)
@@ -773,7 +796,7 @@ async def push_block(request: Request, background_tasks: BackgroundTasks, block_
                 return {'ok': False, 'error': 'Transaction hash not found, had to sync according to sender node, '
                                               'block may have been accepted'}
             return {'ok': False, 'error': 'Transaction hash not found'}
-        final_hexes.extend(pending_hexes)
+        final_hexes = final_hexes + list(pending_hexes)
     error_list = []
     if not await on_ledger(create_block_from_hex, block_content, final_hexes, error_list=error_list):
         return {'ok': False, 'error': error_list[0]} if error_list else {'ok': False}
@@ -793,7 +816,8 @@ async def push_block(request: Request, background_tasks: BackgroundTasks, block_
         peers.book().seen(sender)
     background_tasks.add_task(propagate, 'push_block', {
         'block_content': block_content,
-        'txs': [(await Transaction.from_hex(h)).hex() for h in final_hexes] if len(final_hexes) < 10 else txs,
+        'txs': [(await Transaction.from_hex(h)).hex() for h in final_hexes] if len(final_hexes) < 10 else
+        txs.tolist() if isinstance(txs, HexSpans) else txs,
         'block_no': block_no})
     return {'ok': True}
 

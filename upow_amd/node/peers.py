@@ -32,6 +32,7 @@ from typing import Dict, Iterable, List, Optional
 import httpx
 
 from .. import config
+from ..utils import hexspans
 from ..utils.logger import get_logger
 from ..constants import MAX_BLOCK_SIZE_HEX
 
@@ -327,15 +328,16 @@ def set_client(c: Optional[httpx.AsyncClient]):
 
 
 async def fetch_json(url: str, method: str = 'GET', **kwargs):
-    """A peer's JSON answer, read as a stream and cut at ``FETCH_CAP`` characters."""
+    """A peer's JSON answer, read as a stream and cut at ``FETCH_CAP`` bytes. Tx arrays ('transactions' of a
+    /get_blocks page, 'txs') stay inside the body bytes (utils/hexspans.py): the sync decoder reads them there."""
     parts, size = [], 0
     async with client().stream(method, url, **kwargs) as response:
-        async for chunk in response.aiter_text():
+        async for chunk in response.aiter_bytes():
             parts.append(chunk)
             size += len(chunk)
             if size > FETCH_CAP:
                 break
-    return json.loads(''.join(parts))
+    return hexspans.loads(b''.join(parts))
 
 
 async def is_alive(url: str) -> bool:

@@ -64,6 +64,8 @@ import threading
 import time
 from typing import List, Optional
 
+import numpy as np
+
 from ..utils.logger import get_logger
 from .dist import DistContext
 
@@ -118,7 +120,7 @@ class Cluster:
         """A /get_blocks page (block rows + every tx, coinbase included) as ONE 'page' op."""
         rows = [b['block'] for b in blocks]
         counts = [len(b['transactions']) for b in blocks]
-        self.send('page', pack_txs([h for b in blocks for h in b['transactions']]), rows=rows, counts=counts)
+        self.send('page', pack_groups([b['transactions'] for b in blocks]), rows=rows, counts=counts)
 
     @staticmethod
     def unpack_page(msg: dict) -> list:
@@ -321,7 +323,19 @@ def pack_txs(tx_hexes) -> bytes:
     """Raw tx bytes of a block: u32 count, then u32 length + bytes per tx (hex-decoded natively on the
     host pool, csrc/txcodec.cpp ``pack_tx_hexes``)."""
     from ..ops.native import lib
-    return lib().pack_tx_hexes(list(tx_hexes), _threads())
+    from ..utils.hexspans import HexSpans
+    if isinstance(tx_hexes, HexSpans):  # read in place from the request / page body
+        return lib().pack_tx_spans(tx_hexes.buf, np.ascontiguousarray(tx_hexes.spans).tobytes(),
+                                   list(tx_hexes.extra), _threads())
+    return lib().pack_tx_hexes(tx_hexes if isinstance(tx_hexes, list) else list(tx_hexes), _threads())
+
+
+def pack_groups(groups) -> bytes:
+    """``pack_txs`` of several blocks' tx lists in a row; the blocks of one page body stay spans of it."""
+    from ..utils.hexspans import HexSpans
+    if groups and all(isinstance(g, HexSpans) and g.buf is groups[0].buf and not g.extra for g in groups):
+        return pack_txs(HexSpans(groups[0].buf, np.concatenate([g.spans for g in groups])))
+    return pack_txs([h for g in groups for h in g])
 
 
 def unpack_txs(buf: bytes) -> List[str]:
