@@ -56,6 +56,18 @@ def test_bench_cluster_sync_one_chain_two_ranks():
     assert out['page']['page_path'] == 20 and out['op_stream']['commits_agreed'] >= 22
 
 
+def test_bench_sync_and_verify_hold_txs_as_body_spans():
+    """The single-node sync and verify benches hold their txs as a node does after the native body parse
+    (spans of the /get_blocks or /push_block body) and report the push body's parse times."""
+    rc, out, p = _run(['--mode', 'sync', '--txs', '20', '--steps', '10', '--warmup', '1'],
+                      env_extra={'UPOW_START_DIFFICULTY': '1.0'})
+    assert rc == 0, p.stderr[-3000:]
+    assert out['metric'] == 'sync_tx_per_s' and out['page']['page_path'] == 10
+    rc, out, p = _run(['--mode', 'verify', '--txs', '60', '--steps', '2', '--warmup', '1'])
+    assert rc == 0, p.stderr[-3000:]
+    assert out['config']['block_path'] == 'native' and out['push_body_parse_ms']['native_spans'] > 0
+
+
 GUARD = r'''
 import os, sys, json
 sys.path.insert(0, sys.argv[1])

@@ -508,7 +508,7 @@ async def _run(args, ctx, device, utxo_backend):
     # which leaves the tx array inside the body bytes (utils/hexspans.py); the parse itself is timed apart
     bodies = [json.dumps({'block_content': '', 'txs': b}).encode() for b in blocks]
     extra_parse = _body_parse_ms(bodies[0]) if bodies else None
-    blocks = [hexspans.loads(body)['txs'] for body in bodies]
+    blocks = [(json.loads if _TX_LISTS else hexspans.loads)(body)['txs'] for body in bodies]
     del bodies
     gov_probe = await _governance_probe(db) if gov else None
     # mine every header up front (untimed), each at the difficulty the chain will require of it
@@ -602,10 +602,16 @@ async def _run(args, ctx, device, utxo_backend):
     return total_txs, wall, stages, len(blocks[0]), sorted(paths), extra
 
 
+# A/B switch: hold the txs as json.loads' str lists (the form before the span parse) instead of body spans
+_TX_LISTS = os.environ.get('UPOW_BENCH_TX_LISTS', '0') == '1'
+
+
 def _as_fetched(page: list) -> list:
     """(untimed) /get_blocks rows as a syncing node holds them: parsed by peers.fetch_json from the JSON
     body, each row's tx array left inside the body bytes (utils/hexspans.py)."""
-    return hexspans.loads(json.dumps(page).encode())
+    from fastapi.encoders import jsonable_encoder  # what the /get_blocks answer goes through (Decimal -> number)
+    body = json.dumps(jsonable_encoder(page)).encode()
+    return json.loads(body) if _TX_LISTS else hexspans.loads(body)
 
 
 def _body_parse_ms(body: bytes, reps: int = 5) -> dict:
