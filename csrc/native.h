@@ -2,6 +2,7 @@
 // translation units (*.hip). Only plain host types cross this boundary.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -63,6 +64,10 @@ std::vector<uint8_t> p256_g16_entries(int64_t first, int64_t count);
 std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n);
 void p256_decompress_host(const uint8_t* in33, int64_t n, uint8_t* out64, uint8_t* ok);
 void p256_decompress_gpu(const uint8_t* in33, int64_t n, uint8_t* out64, uint8_t* ok);
+// signer keys decompressed into verify items on the device, output addresses curve-checked, signatures
+// verified: one stream order, one sync (p256.hip); fill(jobkeys33, sigdig96, outkeys33) packs the inputs
+void p256_verify_fused_gpu(int64_t n_jobs, int64_t n_out, const std::function<void(uint8_t*, uint8_t*, uint8_t*)>& fill,
+                           uint8_t* st, uint8_t* out_ok, std::vector<uint8_t>* items_out);
 // on-curve check of 64-byte (version-1) addresses x LE | y LE: ok[i] = 1 iff x, y < p and y^2 = x^3 - 3x + b
 void p256_on_curve_host(const uint8_t* xy64, int64_t n, uint8_t* ok, int threads);
 void p256_on_curve_gpu(const uint8_t* xy64, int64_t n, uint8_t* ok);

@@ -21,7 +21,9 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
+#include <optional>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -604,6 +606,39 @@ __global__ __launch_bounds__(256) void p256_decompress_kernel(const uint8_t* __r
     ok[i] = good ? 1 : 0;
 }
 
+// The key kernel of p256_verify_fused_gpu. Thread t < n_jobs: signer key jobkeys[t] decompressed into verify
+// item t, whose r | s | digest come from sigdig[t]; a key off the curve (or x >= p) gets x = y = 0, which the
+// verify prologue reports as a bad key (status 2), as the separate decompression's failure did. Threads
+// past n_jobs: output address t - n_jobs, curve check only (transaction_output.py: string_to_point).
+__global__ __launch_bounds__(256) void p256_keyrec_kernel(const uint8_t* __restrict__ jobkeys,
+                                                           const uint8_t* __restrict__ sigdig, int64_t n_jobs,
+                                                           const uint8_t* __restrict__ outkeys, int64_t n_out,
+                                                           VerifyItem* __restrict__ items, uint8_t* __restrict__ out_ok) {
+    const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= n_jobs + n_out) return;
+    const bool job = t < n_jobs;
+    const uint8_t* a = job ? jobkeys + 33 * t : outkeys + 33 * (t - n_jobs);
+    const fe x = fe_from_le(a + 1);
+    const bool odd = a[0] == 43;
+    bool good = !fe_geq(x, fe_const_p());
+    const fe x3 = fe_mul(fe_sqr(x), x);
+    const fe rhs = fe_add(fe_sub(x3, fe_add(fe_add(x, x), x)), fe_const_b());
+    fe y = fe_sqrt_candidate(rhs);
+    good = good && fe_eq(fe_sqr(y), rhs);
+    if (!job) {
+        out_ok[t - n_jobs] = good ? 1 : 0;
+        return;
+    }
+    if ((y.v[0] & 1u) != uint32_t(odd)) y = fe_neg(y);
+    VerifyItem* it = items + t;
+    fe_to_le(good ? x : fe_zero(), it->qx);
+    fe_to_le(good ? y : fe_zero(), it->qy);
+    const uint8_t* sd = sigdig + 96 * t;
+    uint8_t* rse = reinterpret_cast<uint8_t*>(it) + 64;  // r | s | e: the item's last 96 bytes
+#pragma unroll 8
+    for (int k = 0; k < 96; ++k) rse[k] = sd[k];
+}
+
 // item: 64-byte full address x LE | y LE (transaction_output.py:25-26, is_point_on_curve per output)
 UPOW_HD uint8_t on_curve_64(const uint8_t* a) {
     const aff q{fe_from_le(a), fe_from_le(a + 32)};
@@ -727,44 +762,37 @@ std::vector<uint8_t> p256_verify_host(const uint8_t* items, int64_t n, int threa
     return st;
 }
 
-std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
-    std::vector<uint8_t> st(static_cast<size_t>(n));
-    if (n == 0) return st;
-    node_device_enter();
-    const aff* d_tab = device_g16_table();
-    PooledBuf<VerifyItem> b_items{size_t(n)};
-    PooledBuf<uint8_t> b_st{size_t(n)};
-    VerifyItem* d_items = b_items.p;
-    uint8_t* d_st = b_st.p;
-    StagedIO io(sizeof(VerifyItem) * size_t(n) + size_t(n));
-    io.h2d(d_items, items, sizeof(VerifyItem) * size_t(n));
-    // Variant (UPOW_P256_VARIANT, read per call): unset/'a' = auto, '4' = four lanes per signature,
-    // '0'..'3' = one lane per signature (below). Auto takes the quad kernel up to 32k signatures
-    // (2,048 waves, two per SIMD): there it cuts the latency of block-sized batches; past that the
-    // chip is full either way and one lane per signature does half the total work.
+// Scratch of one verify launch: kept by the caller until its stream sync.
+struct VerifyScratch {
+    std::optional<PooledBuf<xz>> quad;
+    std::optional<PooledBuf<jac>> one;
+};
+
+// Launches the verify of n device items into d_st on the node stream.
+// Variant (UPOW_P256_VARIANT, read per call): unset/'a' = auto, '4' = four lanes per signature,
+// '8' = eight, '0'..'3' = one lane per signature (below). Auto takes the quad kernel up to 32k signatures
+// (2,048 waves, two per SIMD): there it cuts the latency of block-sized batches; past that the chip is
+// full either way and one lane per signature does half the total work.
+static void verify_launch(const VerifyItem* d_items, int64_t n, const aff* d_tab, uint8_t* d_st, VerifyScratch& sc) {
     const char* var = std::getenv("UPOW_P256_VARIANT");
     char v = var && var[0] ? var[0] : 'a';
     const bool autov = v == 'a';
     if (v == 'a') v = n <= kQuadMaxBatch ? '4' : '1';
     if (v == '8') {
-        PooledBuf<xz> b_tab(size_t(16) * size_t(n));
+        sc.quad.emplace(size_t(16) * size_t(n));
         const int64_t waves = (n + 7) / 8;
         hipLaunchKernelGGL(p256_verify_oct_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, node_stream(), d_items, n,
-                           d_tab, b_tab.p, d_st);
+                           d_tab, sc.quad->p, d_st);
         hck(hipGetLastError(), "p256_verify_oct_kernel launch");
-        io.d2h(st.data(), d_st, size_t(n));
-        io.finish("verify status");
-        return st;
+        return;
     }
     if (v == '4') {
-        PooledBuf<xz> b_tab(size_t(16) * size_t(n));
+        sc.quad.emplace(size_t(16) * size_t(n));
         const int64_t waves = (n + 15) / 16;
         hipLaunchKernelGGL(p256_verify_quad_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, node_stream(), d_items, n,
-                           d_tab, b_tab.p, d_st);
+                           d_tab, sc.quad->p, d_st);
         hck(hipGetLastError(), "p256_verify_quad_kernel launch");
-        io.d2h(st.data(), d_st, size_t(n));
-        io.finish("verify status");
-        return st;
+        return;
     }
     const char* spw_env = std::getenv("UPOW_P256_SPW");
     int spw = spw_env ? std::atoi(spw_env) : 64;
@@ -792,18 +820,65 @@ std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
             n_quad = rem;
         }
     }
-    PooledBuf<jac> b_scratch(size_t(16) * size_t(std::min(n_one, slice)));
+    sc.one.emplace(size_t(16) * size_t(std::min(n_one, slice)));
     for (int64_t off = 0; off < n_one; off += slice)
-        p256_batch_launch(v, d_items + off, std::min(slice, n_one - off), d_tab, b_scratch.p, d_st + off, spw, node_stream());
+        p256_batch_launch(v, d_items + off, std::min(slice, n_one - off), d_tab, sc.one->p, d_st + off, spw, node_stream());
     if (n_quad) {
-        PooledBuf<xz> b_tab(size_t(16) * size_t(n_quad));
+        sc.quad.emplace(size_t(16) * size_t(n_quad));
         const int64_t waves = (n_quad + 15) / 16;
         hipLaunchKernelGGL(p256_verify_quad_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, node_stream(),
-                           d_items + n_one, n_quad, d_tab, b_tab.p, d_st + n_one);
+                           d_items + n_one, n_quad, d_tab, sc.quad->p, d_st + n_one);
         hck(hipGetLastError(), "p256_verify_quad_kernel launch (remainder)");
     }
-    node_d2h(st.data(), d_st, size_t(n), "d2h status");
+}
+
+std::vector<uint8_t> p256_verify_gpu(const uint8_t* items, int64_t n) {
+    std::vector<uint8_t> st(static_cast<size_t>(n));
+    if (n == 0) return st;
+    node_device_enter();
+    const aff* d_tab = device_g16_table();
+    PooledBuf<VerifyItem> b_items{size_t(n)};
+    PooledBuf<uint8_t> b_st{size_t(n)};
+    StagedIO io(sizeof(VerifyItem) * size_t(n) + size_t(n));
+    io.h2d(b_items.p, items, sizeof(VerifyItem) * size_t(n));
+    VerifyScratch sc;
+    verify_launch(b_items.p, n, d_tab, b_st.p, sc);
+    io.d2h(st.data(), b_st.p, size_t(n));
+    io.finish("verify status");
     return st;
+}
+
+// One block's signatures from compressed keys (csrc/txcodec.cpp block_verify_fused): `fill` packs the
+// inputs straight into pinned staging -- n_jobs 33-byte signer keys, n_jobs x 96 B (r | s | digest), n_out
+// 33-byte output addresses -- then ONE stream order runs the key kernel (decompression into the verify items
+// on the device, the outputs' curve check) and the verify, with one sync for the statuses and the output
+// flags. `items_out` receives the device's verify items only when some status is INVALID (0): the caller's
+// ASCII-hex retry rebuilds those records with another digest.
+void p256_verify_fused_gpu(int64_t n_jobs, int64_t n_out, const std::function<void(uint8_t*, uint8_t*, uint8_t*)>& fill,
+                           uint8_t* st, uint8_t* out_ok, std::vector<uint8_t>* items_out) {
+    if (n_jobs + n_out == 0) return;
+    node_device_enter();
+    const aff* d_tab = device_g16_table();
+    const size_t in_bytes = 129 * size_t(n_jobs) + 33 * size_t(n_out);
+    PooledBuf<uint8_t> b_in{in_bytes}, b_st{size_t(n_jobs + n_out)};
+    PooledBuf<VerifyItem> b_items{size_t(n_jobs)};
+    StagedIO io(in_bytes + size_t(n_jobs + n_out));
+    uint8_t* at = io.h2d_take(in_bytes);
+    fill(at, at + 33 * size_t(n_jobs), at + 129 * size_t(n_jobs));
+    io.h2d_issue(b_in.p, at, in_bytes);
+    const int64_t nt = n_jobs + n_out;
+    hipLaunchKernelGGL(p256_keyrec_kernel, dim3(unsigned((nt + 255) / 256)), dim3(256), 0, node_stream(), b_in.p,
+                       b_in.p + 33 * n_jobs, n_jobs, b_in.p + 129 * n_jobs, n_out, b_items.p, b_st.p + n_jobs);
+    hck(hipGetLastError(), "p256_keyrec_kernel launch");
+    VerifyScratch sc;
+    if (n_jobs) verify_launch(b_items.p, n_jobs, d_tab, b_st.p, sc);
+    io.d2h(st, b_st.p, size_t(n_jobs));
+    io.d2h(out_ok, b_st.p + n_jobs, size_t(n_out));
+    io.finish("fused verify");
+    if (items_out && std::find(st, st + n_jobs, uint8_t(0)) != st + n_jobs) {
+        items_out->resize(sizeof(VerifyItem) * size_t(n_jobs));
+        node_d2h(items_out->data(), b_items.p, items_out->size(), "d2h verify items");
+    }
 }
 
 void p256_decompress_host(const uint8_t* in, int64_t n, uint8_t* out, uint8_t* ok) {

@@ -130,6 +130,11 @@ public:
         std::memcpy(at, src, n);
         stream_check(hipMemcpyAsync(dst, at, n, hipMemcpyHostToDevice, node_stream()), "staged h2d");
     }
+    // pinned space for an input the caller writes in place (no staging copy), then issued by h2d_issue
+    uint8_t* h2d_take(size_t n) { return take(n); }
+    void h2d_issue(void* dst, const uint8_t* at, size_t n) {
+        if (n) stream_check(hipMemcpyAsync(dst, at, n, hipMemcpyHostToDevice, node_stream()), "staged h2d");
+    }
     void d2h(void* dst, const void* src, size_t n) {
         if (!n) return;
         uint8_t* at = take(n);

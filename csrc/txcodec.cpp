@@ -819,6 +819,91 @@ static py::tuple block_signer_records(py::buffer pay_addr_b, py::buffer pay_len_
     return py::make_tuple(1, py::bytes(recs));
 }
 
+// The key + verify stages of the native block path fused on the GPU (p256.hip p256_verify_fused_gpu): the
+// signer keys go to the device compressed and are decompressed into the verify items there, next to the
+// curve check of every other 33-byte address of the block (spent outputs' owners and new outputs), and the
+// verify runs behind them in the same stream order -- no host deduplication, no decompressed keys coming
+// back, no host record assembly, one sync. Same verdicts as block_signer_records + p256_verify: a signer key
+// off the curve gives status 2 (bad key), any other address off the curve gives all_ok False.
+// Returns (-1, b"", False, None) when an address is not in the 33-byte form (the caller's general path),
+// else (1, status bytes, all addresses on the curve, verify items when a status is INVALID (0) else None).
+static py::tuple block_verify_fused(py::buffer pay_addr_b, py::buffer pay_len_b, py::buffer out_addr_b,
+                                    py::buffer out_len_b, py::buffer job_input_b, py::buffer sigs_b, py::buffer sig_ids_b,
+                                    py::buffer digest_b, py::buffer job_tx_b, int threads, bool gpu) {
+    auto view = [](py::buffer& b, size_t elem, const char* what) {
+        py::buffer_info bi = b.request();
+        const size_t total = size_t(bi.size) * size_t(bi.itemsize);
+        if (total % elem) throw std::invalid_argument(std::string(what) + ": size is not a multiple of its row");
+        return std::make_pair(static_cast<const uint8_t*>(bi.ptr), total / elem);
+    };
+    const auto [pay_addr, n_in] = view(pay_addr_b, 64, "pay_addr");
+    const auto [pay_len, n_in2] = view(pay_len_b, 1, "pay_len");
+    const auto [out_addr, n_out] = view(out_addr_b, 64, "out_addr");
+    const auto [out_len, n_out2] = view(out_len_b, 1, "out_len");
+    const auto [job_input_p, n_jobs] = view(job_input_b, 8, "job_input");
+    const auto [sigs, n_sig] = view(sigs_b, 64, "sigs");
+    const auto [sig_ids_p, n_jobs2] = view(sig_ids_b, 8, "sig_ids");
+    const auto [digest, n_tx] = view(digest_b, 32, "digest");
+    const auto [job_tx_p, n_jobs3] = view(job_tx_b, 8, "job_tx");
+    if (n_in != n_in2 || n_out != n_out2 || n_jobs != n_jobs2 || n_jobs != n_jobs3)
+        throw std::invalid_argument("block_verify_fused: column lengths differ");
+    const int64_t* job_input = reinterpret_cast<const int64_t*>(job_input_p);
+    const int64_t* sig_ids = reinterpret_cast<const int64_t*>(sig_ids_p);
+    const int64_t* job_tx = reinterpret_cast<const int64_t*>(job_tx_p);
+    for (size_t i = 0; i < n_in; ++i)
+        if (pay_len[i] != 33) return py::make_tuple(-1, py::bytes(), false, py::none());
+    for (size_t i = 0; i < n_out; ++i)
+        if (out_len[i] != 33) return py::make_tuple(-1, py::bytes(), false, py::none());
+    for (size_t j = 0; j < n_jobs; ++j)
+        if (job_input[j] < 0 || size_t(job_input[j]) >= n_in || sig_ids[j] < 0 || size_t(sig_ids[j]) >= n_sig ||
+            job_tx[j] < 0 || size_t(job_tx[j]) >= n_tx)
+            throw std::invalid_argument("block_verify_fused: job index out of range");
+    std::string st(n_jobs, '\0');
+    std::vector<uint8_t> ok(n_in + n_out), items;
+    {
+        py::gil_scoped_release nogil;
+        const size_t nj = n_jobs, nc = n_in + n_out;
+        auto fill = [&](uint8_t* keys, uint8_t* sigdig, uint8_t* checks) {
+            // every job and every checked address in parallel: 2 MB of small gathers into pinned memory
+            parallel_for(int64_t(nj + nc), threads, [&](int64_t ii) {
+                const size_t i = size_t(ii);
+                if (i < nj) {
+                    std::memcpy(keys + 33 * i, pay_addr + 64 * size_t(job_input[i]), 33);
+                    std::memcpy(sigdig + 96 * i, sigs + 64 * size_t(sig_ids[i]), 64);
+                    std::memcpy(sigdig + 96 * i + 64, digest + 32 * size_t(job_tx[i]), 32);
+                } else {
+                    const size_t c = i - nj;
+                    std::memcpy(checks + 33 * c, c < n_in ? pay_addr + 64 * c : out_addr + 64 * (c - n_in), 33);
+                }
+            });
+        };
+        if (gpu) {
+            p256_verify_fused_gpu(int64_t(nj), int64_t(nc), fill, reinterpret_cast<uint8_t*>(&st[0]), ok.data(), &items);
+        } else {  // the same stages on the host (CPU tests of the packing and the verdicts)
+            std::vector<uint8_t> in(129 * nj + 33 * nc), xy(64 * (nj + nc)), kok(nj + nc);
+            fill(in.data(), in.data() + 33 * nj, in.data() + 129 * nj);
+            std::vector<uint8_t> keys(33 * (nj + nc));
+            std::memcpy(keys.data(), in.data(), 33 * nj);
+            std::memcpy(keys.data() + 33 * nj, in.data() + 129 * nj, 33 * nc);
+            p256_decompress_host(keys.data(), int64_t(nj + nc), xy.data(), kok.data());
+            std::vector<uint8_t> rec(160 * nj, 0);
+            for (size_t j = 0; j < nj; ++j) {
+                if (kok[j]) std::memcpy(&rec[160 * j], &xy[64 * j], 64);
+                std::memcpy(&rec[160 * j + 64], in.data() + 33 * nj + 96 * j, 96);
+            }
+            const std::vector<uint8_t> hs = p256_verify_host(rec.data(), int64_t(nj), std::max(1, threads));
+            std::memcpy(&st[0], hs.data(), nj);
+            std::memcpy(ok.data(), kok.data() + nj, nc);
+            if (std::find(hs.begin(), hs.end(), uint8_t(0)) != hs.end()) items = std::move(rec);
+        }
+    }
+    bool all_ok = true;
+    for (uint8_t f : ok) all_ok &= f != 0;
+    py::object it = items.empty() ? py::object(py::none())
+                                  : py::object(py::bytes(reinterpret_cast<const char*>(items.data()), items.size()));
+    return py::make_tuple(1, py::bytes(st), all_ok, it);
+}
+
 // HBM index records of a block's created outputs: 40-byte keys (txid | index u32 | table tag u32) and
 // 80-byte payloads (amount u64 | address length u32 | flags u32 | address, prefix normalised as
 // bytes_to_string does) in one pass, instead of a dozen numpy passes over the block's outputs.
@@ -1088,6 +1173,9 @@ void register_txcodec(py::module_& m) {
           py::arg("out_len"), py::arg("job_input"), py::arg("sigs"), py::arg("sig_ids"), py::arg("digest"),
           py::arg("job_tx"), py::arg("gpu_min"), py::arg("over_idx") = py::none(), py::arg("over_addr") = py::none(),
           py::arg("over_len") = py::none());
+    m.def("block_verify_fused", &block_verify_fused, py::arg("pay_addr"), py::arg("pay_len"), py::arg("out_addr"),
+          py::arg("out_len"), py::arg("job_input"), py::arg("sigs"), py::arg("sig_ids"), py::arg("digest"),
+          py::arg("job_tx"), py::arg("threads") = 8, py::arg("gpu") = true);
     m.def("decode_block_txs", &decode_block_txs, py::arg("hexes"), py::arg("threads") = 8,
           "Decode, canonicalise and hash a block's transactions (see csrc/txcodec.cpp)");
     m.def("decode_block_spans", &decode_block_spans, py::arg("body"), py::arg("spans"), py::arg("extra"),

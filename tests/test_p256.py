@@ -326,3 +326,97 @@ def test_g16_window_table_matches_python(gpu):
                 continue
             q = o.get_public_key((b << (16 * j)) % o.N)
             assert (x, y) == (q.x, q.y), (j, b)
+
+
+def _addr33(q) -> bytes:
+    return bytes([42 if q.y % 2 == 0 else 43]) + q.x.to_bytes(32, 'little')
+
+
+def _off_curve_x(rng) -> int:
+    """An x with no curve point (x^3 - 3x + b a non-residue mod p)."""
+    while True:
+        x = rng.randrange(1, o.P)
+        rhs = (x ** 3 - 3 * x + o.B) % o.P
+        if pow(rhs, (o.P - 1) // 2, o.P) != 1:
+            return x
+
+
+def _fused_block(seed, bad_out=False, bad_signer=False):
+    """Block-path columns (csrc/txcodec.cpp block_signer_records / block_verify_fused) for 48 jobs over 60
+    inputs and 70 outputs, with bad signatures, a wrong key, r = n and r = 0 among them."""
+    rng = random.Random(seed)
+    keys = [rng.randrange(1, o.N) for _ in range(6)]
+    pubs = [o.get_public_key(k) for k in keys]
+    n_jobs, n_in, n_out = 48, 60, 70
+    pay = np.zeros((n_in, 64), np.uint8)
+    owner = [j % 6 for j in range(n_in)]
+    for i in range(n_in):
+        pay[i, :33] = np.frombuffer(_addr33(pubs[owner[i]]), np.uint8)
+    if bad_signer:
+        pay[5, :33] = np.frombuffer(bytes([42]) + _off_curve_x(rng).to_bytes(32, 'little'), np.uint8)
+    out = np.zeros((n_out, 64), np.uint8)
+    for i in range(n_out):
+        out[i, :33] = np.frombuffer(_addr33(o.get_public_key(rng.randrange(1, o.N))), np.uint8)
+    if bad_out:
+        out[7, :33] = np.frombuffer(bytes([43]) + _off_curve_x(rng).to_bytes(32, 'little'), np.uint8)
+    job_input = np.array(rng.sample(range(n_in), n_jobs), np.int64)
+    digest = np.frombuffer(b''.join(rng.randbytes(32) for _ in range(n_jobs)), np.uint8).reshape(-1, 32)
+    job_tx = np.arange(n_jobs, dtype=np.int64)[::-1].copy()
+    sigs = np.zeros((n_jobs, 64), np.uint8)
+    for j in range(n_jobs):
+        k = owner[int(job_input[j])]
+        msg_e = digest[job_tx[j]].tobytes()
+        z = int.from_bytes(msg_e, 'big')
+        kk = rng.randrange(1, o.N)
+        r = o.get_public_key(kk).x % o.N
+        s = pow(kk, -1, o.N) * (z + r * keys[k]) % o.N
+        kind = j % 6
+        if kind == 1:
+            s = (s * 3) % o.N or 1
+        elif kind == 2:
+            r = o.N
+        elif kind == 3:
+            r = 0
+        sigs[j] = np.frombuffer(r.to_bytes(32, 'little') + s.to_bytes(32, 'little'), np.uint8)
+    return (pay, np.full(n_in, 33, np.uint8), out, np.full(n_out, 33, np.uint8), job_input, sigs,
+            np.arange(n_jobs, dtype=np.int64), digest, job_tx)
+
+
+def _fused_reference(native, cols):
+    pay, pay_len, out, out_len, job_input, sigs, sig_ids, digest, job_tx = cols
+    kst, recs = native.block_signer_records(pay, pay_len, out, out_len, job_input, sigs, sig_ids, digest, job_tx,
+                                            1 << 62)
+    return kst, recs
+
+
+@pytest.mark.parametrize('case', ['plain', 'bad_out', 'bad_signer'])
+def test_fused_block_verify_host_matches_separate_stages(native, case):
+    """block_verify_fused (keys decompressed into the verify items, every address curve-checked, signatures
+    verified) gives the verdicts of block_signer_records + p256_verify; its items, returned when a signature
+    fails, are the separate path's records."""
+    cols = _fused_block(7, bad_out=case == 'bad_out', bad_signer=case == 'bad_signer')
+    code, st, ok, items = native.block_verify_fused(*cols, threads=3, gpu=False)
+    kst, recs = _fused_reference(native, cols)
+    assert code == 1
+    if case == 'plain':
+        assert kst == 1 and ok
+        exp = op.verify_records(recs, device='cpu', threads=2)
+        assert np.frombuffer(st, np.uint8).tolist() == exp.tolist()
+        assert set(exp.tolist()) == {0, 1, 3} and items == recs
+    elif case == 'bad_out':
+        assert kst == 0 and not ok
+    else:  # every spent output's owner is curve-checked too; the signer's own job also says bad key
+        assert kst == 0 and not ok
+        assert all(st[j] == 2 for j in range(len(cols[4])) if cols[4][j] == 5)
+    # a 64-byte address hands the block to the general path, as block_signer_records does
+    pay_len = cols[1].copy()
+    pay_len[0] = 64
+    assert native.block_verify_fused(cols[0], pay_len, *cols[2:], gpu=False)[0] == -1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', ['plain', 'bad_out', 'bad_signer'])
+def test_fused_block_verify_gpu_matches_host(gpu, case):
+    from upow_amd.ops.native import lib
+    cols = _fused_block(9, bad_out=case == 'bad_out', bad_signer=case == 'bad_signer')
+    assert lib().block_verify_fused(*cols, threads=3, gpu=True) == lib().block_verify_fused(*cols, threads=3, gpu=False)

@@ -83,6 +83,12 @@ def _i32(d, k):
     return np.frombuffer(d[k], dtype=np.int32)
 
 
+# signer keys decompressed, curve checks and the signature verify in one GPU stream order for a block whose
+# addresses are all 33-byte keys (UPOW_FUSED_VERIFY=0: the host key stage + separate verify, the A/B form)
+FUSED_VERIFY = os.environ.get('UPOW_FUSED_VERIFY', '1') != '0'
+_FUSED_HOST = os.environ.get('UPOW_FUSED_VERIFY') == 'host'  # the same stages on the host (CPU tests of this path)
+
+
 def decode_raw(tx_hexes, threads: int) -> dict:
     """The codec's dict for a list of str or a :class:`~upow_amd.utils.hexspans.HexSpans` (read in place
     from its body: csrc/txcodec.cpp ``decode_block_spans``)."""
@@ -381,10 +387,16 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         over = {'over_idx': np.fromiter(signers.keys(), dtype=np.int64, count=len(signers)), 'over_addr': ov_addr,
                 'over_len': np.fromiter(map(len, raws), dtype=np.uint8, count=len(raws))}
     pre_status = None
+    fused = False
     if page is not None and not signers and page.n_jobs == n_jobs:
         # the page verified this block's signatures in its one batch, with these very keys (and checked every
         # output address of the page on the curve)
         kst, rec_bytes, pre_status = 1, page.recs, page.status
+    elif (FUSED_VERIFY and not signers and n_jobs and (n_jobs >= gpu_min or _FUSED_HOST) and validate.overlappable(n_jobs)
+          and bool(np.all(pay['len'] == 33)) and bool(np.all(out_len == 33))):
+        # keys, records and verify in one GPU stream order (csrc/txcodec.cpp block_verify_fused), issued below
+        # on the verify thread: the key stage leaves the host path
+        fused, kst, rec_bytes = True, 1, None
     else:
         kst, rec_bytes = lib().block_signer_records(
             np.ascontiguousarray(pay['addr']), pay['len'].astype(np.uint8), out_addr, out_len,
@@ -398,7 +410,7 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
                                             gpu_min)
         if rec_bytes is None:
             return None
-    recs = np.frombuffer(rec_bytes, dtype=np.uint8).reshape(-1, 160)
+    recs = np.frombuffer(rec_bytes, dtype=np.uint8).reshape(-1, 160) if rec_bytes is not None else None
     if np.any(out_amount == 0):
         return None
     t3 = perf_counter()
@@ -413,8 +425,14 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     # the block to the object path before anything is rendered
     if np.any(fee < 0):
         return None
-    vfut = _verify_pool().submit(validate._verify, rec_bytes, None) \
-        if n_jobs and pre_status is None and validate.overlappable(n_jobs) else None
+    if fused:
+        vfut = _verify_pool().submit(lib().block_verify_fused, np.ascontiguousarray(pay['addr']),
+                                     np.ascontiguousarray(pay['len'], dtype=np.uint8), out_addr, out_len,
+                                     job_input.astype(np.int64), sigs, sig_ids, digest, job_tx.astype(np.int64), THREADS,
+                                     not _FUSED_HOST)
+    else:
+        vfut = _verify_pool().submit(validate._verify, rec_bytes, None) \
+            if n_jobs and pre_status is None and validate.overlappable(n_jobs) else None
     try:
         # ---- columns for the ledger writes: views of the codec's buffers, encoded natively into one journal
         #      batch by csrc/ledger_writer.cpp (tx hashes rendered from the raw digests, text arenas for strings)
@@ -443,8 +461,16 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
             wait([vfut])
         raise
     # the verify's verdict
-    status = (pre_status if pre_status is not None else vfut.result() if vfut is not None else
-              validate._verify(rec_bytes, None) if n_jobs else np.zeros(0, np.uint8)).copy()
+    if fused:
+        _, st_b, keys_ok, items = vfut.result()
+        if not keys_ok:  # an address off the curve: the object path decides
+            return None
+        status = np.frombuffer(st_b, dtype=np.uint8).copy()
+        if items is not None:  # some signature failed: its record, for the ASCII-hex retry
+            recs = np.frombuffer(items, dtype=np.uint8).reshape(-1, 160)
+    else:
+        status = (pre_status if pre_status is not None else vfut.result() if vfut is not None else
+                  validate._verify(rec_bytes, None) if n_jobs else np.zeros(0, np.uint8)).copy()
     retry = np.nonzero(status == op.INVALID)[0]
     if len(retry):
         signed_len = _i32(d, 'signed_len')
