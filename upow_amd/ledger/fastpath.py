@@ -428,8 +428,10 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     if fused:
         vfut = _verify_pool().submit(lib().block_verify_fused, np.ascontiguousarray(pay['addr']),
                                      np.ascontiguousarray(pay['len'], dtype=np.uint8), out_addr, out_len,
-                                     job_input.astype(np.int64), sigs, sig_ids, digest, job_tx.astype(np.int64), THREADS,
-                                     not _FUSED_HOST)
+                                     job_input.astype(np.int64), sigs, sig_ids, digest, job_tx.astype(np.int64),
+                                     # the packing runs on this verify thread alone: the host pool takes one
+                                     # parallel region at a time, and the apply strings below hold it
+                                     1, not _FUSED_HOST)
     else:
         vfut = _verify_pool().submit(validate._verify, rec_bytes, None) \
             if n_jobs and pre_status is None and validate.overlappable(n_jobs) else None
