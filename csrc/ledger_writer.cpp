@@ -364,7 +364,7 @@ EncodedStmt encode_stmt(const std::string& sql, py::sequence cols, int64_t n, py
                         py::object expect, int shard, int route) {
     if (n < 0) throw std::invalid_argument("n < 0");
     if (shard < 0 || shard > 15) throw std::invalid_argument("shard must be in [0, 15]");
-    if (route < 0 || route > 8 || shard + route > 16) throw std::invalid_argument("route must be in [0, 8]");
+    if (route < 0 || route > 15 || shard + route > 16) throw std::invalid_argument("route must be in [0, 15]");
     Out o;
     o.str(sql);
     // route > 1: the rows are spread over files shard .. shard+route-1 by the first byte of column 0

@@ -41,10 +41,16 @@ async def _grow(db, n_tx: int = 3):
     return a, b, block_txs
 
 
-@pytest.mark.parametrize('n_utxo,n_tx', [(4, 4), (5, 5), (6, 4), (2, 3), (2, 0)])
-def test_layouts_apply_read_and_roll_back(tmp_path, monkeypatch, n_utxo, n_tx):
-    monkeypatch.setenv('UPOW_UTXO_FILES', str(n_utxo))
-    monkeypatch.setenv('UPOW_TX_FILES', str(n_tx))
+@pytest.mark.parametrize('n_utxo,n_tx,mixed', [(4, 4, False), (5, 5, False), (6, 4, False), (2, 3, False),
+                                                (2, 0, False), (10, 10, True), (3, 3, True)])
+def test_layouts_apply_read_and_roll_back(tmp_path, monkeypatch, n_utxo, n_tx, mixed):
+    """Separate layouts (each split table in files of its own) and mixed ones (UPOW_LEDGER_MIXED: every split
+    file holds both tables for one hash range)."""
+    monkeypatch.setenv('UPOW_LEDGER_MIXED', '1' if mixed else '0')
+    if mixed:
+        monkeypatch.setenv('UPOW_LEDGER_FILES', str(n_utxo))
+    monkeypatch.setenv('UPOW_UTXO_FILES', str(n_utxo if not mixed else 5))
+    monkeypatch.setenv('UPOW_TX_FILES', str(n_tx if not mixed else 5))
     path = str(tmp_path / 'ledger.sqlite3')
 
     async def go():
@@ -80,15 +86,18 @@ def test_layouts_apply_read_and_roll_back(tmp_path, monkeypatch, n_utxo, n_tx):
         assert await db.get_address_balance(a) == Decimal(18)
         assert db.utxo.set_hash(0) == db.sql_unspent_outputs_hash()
         db.close()
+        assert db.mixed == mixed and len(db.writer.stats()['shards']) == 1 + n_utxo + (0 if mixed else n_tx)
+        db.close()
         # reopened: the recorded layout wins over the environment
         monkeypatch.setenv('UPOW_TX_FILES', '1')
+        monkeypatch.setenv('UPOW_LEDGER_MIXED', '0' if mixed else '1')
         db = await Database.create(path=path, utxo_backend='host')
-        assert (len(db.utxo_schemas), len(db.tx_schemas)) == (n_utxo, n_tx)
+        assert (len(db.utxo_schemas), len(db.tx_schemas), db.mixed) == (n_utxo, n_tx, mixed)
         assert await db.get_address_balance(a) == Decimal(18)
         db.close()
     asyncio.run(go())
     names = [os.path.basename(f) for f in ledger_files(path)]
-    assert sum(n.startswith('ledger.sqlite3-tx') for n in names) == n_tx
+    assert sum(n.startswith('ledger.sqlite3-tx') for n in names) == (0 if mixed else n_tx)
     assert sum(n.startswith('ledger.sqlite3-utxo') for n in names) == n_utxo
     if n_tx == 0:  # the pre-split layout: transactions in the main file
         c = sqlite3.connect(path)

@@ -128,6 +128,9 @@ def _commit_point():
 # fresh ledger (three interleaved pairs, profiles/r5/verify_split_*): the aged ledger is what a node runs.
 UTXO_FILES_DEFAULT = 5
 TX_FILES_DEFAULT = 5
+# the mixed layout (new ledgers): LEDGER_FILES_DEFAULT files, each with both split tables of one hash range
+LEDGER_MIXED_DEFAULT = '0'
+LEDGER_FILES_DEFAULT = 10
 ROUTED = ('unspent_outputs', 'transactions')
 
 
@@ -450,22 +453,30 @@ class Database:
         bg = os.environ.get('UPOW_WAL_CHECKPOINT_THREAD', '1') != '0'
         auto = int(os.environ.get('UPOW_WAL_AUTOCHECKPOINT', '100000' if bg else '10000'))
         self._conn.execute(f'PRAGMA wal_autocheckpoint = {auto}')
-        n_utxo, n_tx = self._layout()
+        n_utxo, n_tx, self.mixed = self._layout()
         self._conn.executescript(SCHEMA)
         self.utxo_schemas, sfx = _names('utxo', n_utxo)
         self.utxo_files = [self.file + x for x in sfx]
         self.utxo_file = self.utxo_files[0]
-        # n_tx == 0: a ledger from before the transactions split keeps the table in its main file
-        self.tx_schemas, sfx = _names('tx', n_tx)
-        self.tx_files = [self.file + x for x in sfx]
-        fresh2 = n_utxo == 2 and not os.path.exists(self.utxo_files[1])
-        for schema, f in [*zip(self.utxo_schemas, self.utxo_files), *zip(self.tx_schemas, self.tx_files)]:
+        if self.mixed:
+            # every split file holds both split tables for one hash range (the UTXO rows and the txs of the
+            # same tx hashes): each materialiser gets an equal share of both workloads, whatever their ratio
+            self.tx_schemas, self.tx_files = list(self.utxo_schemas), list(self.utxo_files)
+        else:
+            # n_tx == 0: a ledger from before the transactions split keeps the table in its main file
+            self.tx_schemas, sfx = _names('tx', n_tx)
+            self.tx_files = [self.file + x for x in sfx]
+        fresh2 = n_utxo == 2 and not self.mixed and not os.path.exists(self.utxo_files[1])
+        for schema, f in self._split_files():
             self._conn.execute(f'ATTACH DATABASE ? AS {schema}', (f,))
             self._conn.execute(f'PRAGMA {schema}.page_size = {page}')
             self._conn.execute(f'PRAGMA {schema}.journal_mode = WAL')
             self._conn.execute(f'PRAGMA {schema}.synchronous = ' + ('OFF' if path == ':memory:' else 'NORMAL'))
             self._conn.execute(f'PRAGMA {schema}.cache_size = -{cache_mb * 1024}')
-            self._conn.executescript(utxo_schema(schema) if schema.startswith('utxo') else tx_schema(schema))
+            if self.mixed:
+                self._conn.executescript(utxo_schema(schema) + tx_schema(schema))
+            else:
+                self._conn.executescript(utxo_schema(schema) if schema.startswith('utxo') else tx_schema(schema))
         if not n_tx:
             self._conn.executescript(tx_schema('main', legacy=True))
         else:
@@ -481,7 +492,7 @@ class Database:
         # table -> writer files holding it (main file = 0); routed tables: (first file, number of files)
         self._routed = {'unspent_outputs': (1, n_utxo)}
         if n_tx:
-            self._routed['transactions'] = (1 + n_utxo, n_tx)
+            self._routed['transactions'] = (1, n_utxo) if self.mixed else (1 + n_utxo, n_tx)
         self._shard_of = {t: tuple(range(a, a + k)) for t, (a, k) in self._routed.items()}
         if bg:
             self._start_checkpointer(float(os.environ.get('UPOW_WAL_CHECKPOINT_PERIOD', '0.5')))
@@ -518,16 +529,25 @@ class Database:
         # of the journal batches only advance an existing watermark
         self._address_index_height()
 
-    def _layout(self) -> Tuple[int, int]:
-        """(UTXO files, transaction files; 0 = in the main file) of this ledger, recorded at creation."""
+    def _layout(self) -> Tuple[int, int, bool]:
+        """(UTXO files, transaction files; 0 = in the main file, mixed) of this ledger, recorded at creation.
+        A mixed layout (``UPOW_LEDGER_MIXED=1``) has ``UPOW_LEDGER_FILES`` files each holding both split
+        tables for one tx-hash range, so its materialisers share the UTXO and the transaction workloads
+        evenly; the separate layout gives each table files of its own."""
         c = self._conn
         c.execute('CREATE TABLE IF NOT EXISTS upow_layout (k TEXT PRIMARY KEY, v INTEGER NOT NULL)')
         got = {r[0]: int(r[1]) for r in c.execute('SELECT k, v FROM upow_layout')}
         if 'utxo_files' in got and 'tx_files' in got:
-            return got['utxo_files'], got['tx_files']
+            return got['utxo_files'], got['tx_files'], bool(got.get('mixed', 0))
         legacy = c.execute("SELECT 1 FROM main.sqlite_master WHERE type = 'table' AND name = 'blocks'").fetchone()
+        mixed = False
         if legacy:
             n_utxo, n_tx = 2, 0
+        elif os.environ.get('UPOW_LEDGER_MIXED', LEDGER_MIXED_DEFAULT) == '1':
+            mixed = True
+            n_utxo = n_tx = int(os.environ.get('UPOW_LEDGER_FILES', str(LEDGER_FILES_DEFAULT)))
+            if not 2 <= n_utxo <= 10:
+                raise ValueError('UPOW_LEDGER_FILES must be in 2..10 (SQLite attaches at most 10 files to a connection)')
         else:
             n_utxo = int(os.environ.get('UPOW_UTXO_FILES', str(UTXO_FILES_DEFAULT)))
             n_tx = int(os.environ.get('UPOW_TX_FILES', str(TX_FILES_DEFAULT)))
@@ -536,8 +556,14 @@ class Database:
                 raise ValueError('UPOW_UTXO_FILES must be in 2..8, UPOW_TX_FILES in 0..8, and their sum at most 10 '
                                  '(SQLite attaches at most 10 files to a connection)')
         c.executemany('INSERT OR REPLACE INTO upow_layout (k, v) VALUES (?, ?)',
-                      [('utxo_files', n_utxo), ('tx_files', n_tx)])
-        return n_utxo, n_tx
+                      [('utxo_files', n_utxo), ('tx_files', n_tx), ('mixed', int(mixed))])
+        return n_utxo, n_tx, mixed
+
+    def _split_files(self) -> List[Tuple[str, str]]:
+        """(schema, file) of every attached split file, each once."""
+        if self.mixed:
+            return list(zip(self.utxo_schemas, self.utxo_files))
+        return [*zip(self.utxo_schemas, self.utxo_files), *zip(self.tx_schemas, self.tx_files)]
 
     def _migrate_single_file_utxo(self):
         """Ledgers written before the UTXO table got its own file keep ``unspent_outputs`` in the main
@@ -595,7 +621,7 @@ class Database:
         self._journal_sync_mode = mode
         journal = os.environ.get('UPOW_JOURNAL_PATH') or os.path.join(os.path.dirname(os.path.abspath(self.file)),
                                                                        os.path.basename(self.file) + '.journal')
-        self.writer = lib().LedgerWriter([self.file, *self.utxo_files, *self.tx_files], journal, mode, cache_mb,
+        self.writer = lib().LedgerWriter([self.file, *(f for _, f in self._split_files())], journal, mode, cache_mb,
                                          # records per materialiser transaction: a lagging materialiser takes
                                          # up to this many per commit (an aged 5 M-row ledger: 32 vs 8 halves the
                                          # commit time, profiles/r4/verify_aged_writer_ab_r4g.json)
@@ -653,7 +679,7 @@ class Database:
         block's COMMIT). sqlite3 releases the GIL while the checkpoint runs."""
         self._ckpt_stop = threading.Event()
         path = self.file
-        files = [*zip(self.utxo_schemas, self.utxo_files), *zip(self.tx_schemas, self.tx_files)]
+        files = self._split_files()
 
         # one file per period, round-robin: a checkpoint of every attached file at once (11 WALs copied back
         # and fsync'd in one statement) made readers of those files wait for ~200 ms at a time, among them
