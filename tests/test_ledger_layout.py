@@ -107,7 +107,12 @@ def test_layouts_apply_read_and_roll_back(tmp_path, monkeypatch, n_utxo, n_tx, m
 
 def test_layout_beyond_sqlite_attach_limit_is_refused(tmp_path, monkeypatch):
     # one ATTACH per split file; SQLite allows 10, so 8 + 8 must fail loudly at creation, not on ATTACH
+    monkeypatch.setenv('UPOW_LEDGER_MIXED', '0')
     monkeypatch.setenv('UPOW_UTXO_FILES', '8')
     monkeypatch.setenv('UPOW_TX_FILES', '8')
     with pytest.raises(ValueError, match='at most 10'):
         asyncio.run(Database.create(path=str(tmp_path / 'ledger.sqlite3'), utxo_backend='host'))
+    monkeypatch.setenv('UPOW_LEDGER_MIXED', '1')
+    monkeypatch.setenv('UPOW_LEDGER_FILES', '11')
+    with pytest.raises(ValueError, match='at most 10'):
+        asyncio.run(Database.create(path=str(tmp_path / 'ledger2.sqlite3'), utxo_backend='host'))
