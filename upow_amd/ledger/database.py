@@ -128,8 +128,12 @@ def _commit_point():
 # fresh ledger (three interleaved pairs, profiles/r5/verify_split_*): the aged ledger is what a node runs.
 UTXO_FILES_DEFAULT = 5
 TX_FILES_DEFAULT = 5
-# the mixed layout (new ledgers): LEDGER_FILES_DEFAULT files, each with both split tables of one hash range
-LEDGER_MIXED_DEFAULT = '0'
+# New ledgers take the mixed layout: LEDGER_FILES_DEFAULT files, each with both split tables of one hash
+# range, so every materialiser carries the same share of UTXO and transaction rows whatever their cost ratio
+# (fresh: the UTXO files of 5 + 5 were busy 9-10 ms per block against 6-7 for the tx files). Interleaved A/Bs
+# against 5 + 5 (profiles/r5/ledger_mixed_ab/): fresh 10.02-10.58 vs 10.76-12.35 ms per block (five pairs,
+# one noisy mixed run at 12.93), aged 60-block run 19.01 vs 20.85 ms per block.
+LEDGER_MIXED_DEFAULT = '1'
 LEDGER_FILES_DEFAULT = 10
 ROUTED = ('unspent_outputs', 'transactions')
 
