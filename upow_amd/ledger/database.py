@@ -117,6 +117,14 @@ for _t in OUTPUT_TABLES[1:]:
 _SQL_READERS = None  # Database._off_loop
 
 
+class _Pre:
+    """A block statement encoded before the block's verdict (:meth:`Database.prepare_native_block`)."""
+    __slots__ = ('enc',)
+
+    def __init__(self, enc):
+        self.enc = enc
+
+
 def _commit_point():
     """On a cluster node, the block's agree-before-commit vote resolves here, right before its journal write
     (parallel/cluster.py ``commit_point``); raises when a replica is not ready."""
@@ -1005,18 +1013,21 @@ class Database:
         """:meth:`encode` of a block's statements, the large ones concurrently: each encode copies its
         columns with the GIL released, so a block's ~4 multi-MB statements (tx rows, UTXO rows, spends,
         address rows) are copied on pool threads side by side instead of one after another."""
-        big = [k for k, st in enumerate(stmts) if st[2] >= 1024]
+        out = [st.enc if isinstance(st, _Pre) else None for st in stmts]  # encoded ahead of the verdict
+        todo = [k for k, st in enumerate(stmts) if not isinstance(st, _Pre)]
+        big = [k for k in todo if stmts[k][2] >= 1024]
         if len(big) < 2 or _ENCODE_THREADS < 2:
-            return [self.encode(*st) for st in stmts]
+            for k in todo:
+                out[k] = self.encode(*stmts[k])
+            return out
         global _ENCODE_POOL
         if _ENCODE_POOL is None:
             from concurrent.futures import ThreadPoolExecutor
             _ENCODE_POOL = ThreadPoolExecutor(max_workers=_ENCODE_THREADS, thread_name_prefix='upow-encode')
         futs = {k: _ENCODE_POOL.submit(self.encode, *stmts[k]) for k in big[1:]}
-        out = [None] * len(stmts)
-        for k, st in enumerate(stmts):
+        for k in todo:
             if k not in futs:
-                out[k] = self.encode(*st)  # the first big one and the small ones on this thread meanwhile
+                out[k] = self.encode(*stmts[k])  # the first big one and the small ones on this thread meanwhile
         for k, f in futs.items():
             out[k] = f.result()
         return out
@@ -2003,10 +2014,66 @@ class Database:
                                            'EXISTS(SELECT 1 FROM pending_spent_outputs)')[0] == 0
         return self._pending_empty
 
+    def prepare_native_block(self, block_hash: str, block_id: int, n: int, tx_cols: list, out_cols: tuple,
+                             in_keys: np.ndarray, addr_pairs: Optional[tuple]) -> dict:
+        """The part of :meth:`apply_native_block` that does not depend on the block's verdict, its reward or the
+        mempool, for a block without governance txs: the index records of its outputs and spends, its row
+        ids, and its four large statements (tx rows, UTXO inserts, UTXO deletes, the txs' address rows)
+        encoded. The native block path runs it while the GPU verifies the block's signatures; a block that is
+        then rejected hands its row ids back (:meth:`release_prepared`)."""
+        from ..ops.native import lib
+        out_index, out_addr_spec, out_txid, out_amount, out_addr, out_len = out_cols
+        n_out, n_in = len(out_index), len(in_keys)
+        tag_u = TAG_BY_TABLE['unspent_outputs']
+        rb, pb = lib().output_index_records(
+            np.ascontiguousarray(out_txid, dtype=np.uint8), np.ascontiguousarray(out_index, dtype=np.int64),
+            np.full(n_out, tag_u, dtype=np.uint32), np.ascontiguousarray(out_amount, dtype=np.uint64),
+            np.ascontiguousarray(out_addr, dtype=np.uint8), np.ascontiguousarray(out_len, dtype=np.uint8),
+            np.zeros(0, np.uint8))
+        in_keys = np.ascontiguousarray(in_keys, dtype=np.uint8).reshape(-1, 40)
+        sb, ib = lib().spent_index_records(in_keys, np.full(n_in, tag_u, dtype=np.uint32))
+        in_idx = np.frombuffer(ib, dtype=np.int64)
+        tx_start = self._tx_rowids(n + 1)
+        utxo_start = self._utxo_rowids(n_out)
+        names, stmts = ['tx'], [(self._TX_INSERT, [tx_cols[0], block_hash, *tx_cols[1:],
+                                                   np.arange(tx_start + 1, tx_start + 1 + n, dtype=np.int64)],
+                                 n, None, None, None)]
+        if n_out:
+            names.append('utxo_ins')
+            stmts.append(('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake, rowid) VALUES (?, ?, ?, ?, ?)',
+                          [('hex32', np.ascontiguousarray(out_txid), 32, 0), np.ascontiguousarray(out_index, dtype=np.int64),
+                           out_addr_spec, 0, np.arange(utxo_start, utxo_start + n_out, dtype=np.int64)],
+                          n_out, None, None, None))
+        if n_in:
+            names.append('utxo_del')
+            stmts.append(('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
+                          [('hex32', in_keys, 40, 0), in_idx], n_in, 'key', None, n_in))
+        if addr_pairs is not None:
+            ab, ao, at = addr_pairs
+            rows = self._address_index_stmts(block_hash, int(block_id), [
+                (('arena', ab, ao), ('hex32', tx_cols[0][1], 32, 0, np.frombuffer(at, dtype=np.int64)), len(at) // 8)])
+            if len(rows) == 2:  # inline address index on: the txs' rows (the watermark is built at commit)
+                names.append('addr')
+                stmts.append(rows[0])
+        return {'recs': np.frombuffer(rb, dtype=np.uint8).reshape(-1, 40), 'pay': np.frombuffer(pb, dtype=PAYLOAD_DTYPE),
+                'spent': np.frombuffer(sb, dtype=np.uint8).reshape(-1, 40), 'in_idx': in_idx, 'tx_base': tx_start,
+                'rowids': (tx_start, tx_start + n + 1, utxo_start, utxo_start + n_out),
+                'enc': dict(zip(names, self.encode_many(stmts)))}
+
+    def release_prepared(self, pre: dict):
+        """A prepared block that was not applied: its row ids go back when nothing was allocated after them
+        (the ledger lock is held from prepare to here, so nothing was)."""
+        t0, t1, u0, u1 = pre['rowids']
+        with self._seq_lock:
+            if self._tx_next_rowid == t1:
+                self._tx_next_rowid = t0
+            if self._utxo_next_rowid == u1:
+                self._utxo_next_rowid = u0
+
     def apply_native_block(self, block_row: dict, coinbase_row: tuple, coinbase_outputs: list, n: int,
                            tx_cols: list, out_cols: tuple, in_keys: np.ndarray, spent_payload: np.ndarray,
                            gov: Optional[dict] = None, addr_pairs: Optional[tuple] = None,
-                           cb_index: Optional[tuple] = None) -> int:
+                           cb_index: Optional[tuple] = None, pre: Optional[dict] = None) -> int:
         """The ledger writes of one native-path block (reference manager.py:706-730: add_block,
         add_transaction(coinbase), add_transactions, add_transaction_outputs, remove_pending_transactions,
         remove_outputs, remove_pending_spent_outputs) as ONE journal batch, plus the HBM index update.
@@ -2021,6 +2088,8 @@ class Database:
         governance index follows from these columns — the object path's write set (apply_object_block) in
         the same statement order, so both paths leave identical tables.
         ``cb_index``: the coinbase outputs' index (records, payloads) when already built (a sync page's plan).
+        ``pre``: :meth:`prepare_native_block` of this block (index records, row ids and the large statements
+        encoded while the GPU verified it).
         Returns the journal sequence number (0 without the native writer: written synchronously)."""
         ts = [perf_counter()]  # stage clock: records, statements, encode, journal, index, mempool, governance
         names = ('apply:records', 'apply:stmts', 'apply:encode', 'apply:journal', 'apply:index', 'apply:mempool',
@@ -2038,14 +2107,19 @@ class Database:
         out_tag = gov['out_tag'] if gov is not None else np.full(n_out, tag_u, dtype=np.uint32)
         # ---- index records: created outputs (block txs + coinbase) and spent inputs
         from ..ops.native import lib
-        stake = (np.asarray(gov['out_type']) == int(OutputType.STAKE)).astype(np.uint8) if gov is not None \
-            else np.zeros(0, np.uint8)
-        rb, pb = lib().output_index_records(
-            np.ascontiguousarray(out_txid, dtype=np.uint8), np.ascontiguousarray(out_index, dtype=np.int64),
-            np.ascontiguousarray(out_tag, dtype=np.uint32), np.ascontiguousarray(out_amount, dtype=np.uint64),
-            np.ascontiguousarray(out_addr, dtype=np.uint8), np.ascontiguousarray(out_len, dtype=np.uint8), stake)
-        recs = np.frombuffer(rb, dtype=np.uint8).reshape(-1, 40)
-        pay = np.frombuffer(pb, dtype=PAYLOAD_DTYPE)
+        if pre is not None and (gov is not None or self.writer is None):
+            raise ValueError('a prepared block has no governance txs and goes through the journal')
+        if pre is not None:
+            recs, pay = pre['recs'], pre['pay']
+        else:
+            stake = (np.asarray(gov['out_type']) == int(OutputType.STAKE)).astype(np.uint8) if gov is not None \
+                else np.zeros(0, np.uint8)
+            rb, pb = lib().output_index_records(
+                np.ascontiguousarray(out_txid, dtype=np.uint8), np.ascontiguousarray(out_index, dtype=np.int64),
+                np.ascontiguousarray(out_tag, dtype=np.uint32), np.ascontiguousarray(out_amount, dtype=np.uint64),
+                np.ascontiguousarray(out_addr, dtype=np.uint8), np.ascontiguousarray(out_len, dtype=np.uint8), stake)
+            recs = np.frombuffer(rb, dtype=np.uint8).reshape(-1, 40)
+            pay = np.frombuffer(pb, dtype=PAYLOAD_DTYPE)
         from .utxo import pack_records
         cb_keys = [(o[0], o[1]) for o in coinbase_outputs]
         if cb_index is not None:  # (records, payloads) of the coinbase outputs, built by a sync page's plan
@@ -2056,9 +2130,12 @@ class Database:
                                   [bool(o[3]) for o in coinbase_outputs])
         in_keys = np.ascontiguousarray(in_keys, dtype=np.uint8).reshape(-1, 40)
         in_tag = gov['in_tag'].astype(np.uint32) if gov is not None else np.full(n_in, tag_u, dtype=np.uint32)
-        sb, ib = lib().spent_index_records(in_keys, np.ascontiguousarray(in_tag, dtype=np.uint32))
-        spent = np.frombuffer(sb, dtype=np.uint8).reshape(-1, 40)
-        in_idx = np.frombuffer(ib, dtype=np.int64)
+        if pre is not None:
+            spent, in_idx = pre['spent'], pre['in_idx']
+        else:
+            sb, ib = lib().spent_index_records(in_keys, np.ascontiguousarray(in_tag, dtype=np.uint32))
+            spent = np.frombuffer(sb, dtype=np.uint8).reshape(-1, 40)
+            in_idx = np.frombuffer(ib, dtype=np.int64)
         # the spends' key order (B-tree locality) is computed by the materialiser ('key': a stable sort of the
         # statement's rows by the leading 8 bytes of column 0, so a row selection keeps the global key order)
         in_order = 'key'
@@ -2066,7 +2143,8 @@ class Database:
 
         # ---- statements (schema.sql write set of one block)
         b = block_row
-        tx_base = self._tx_rowids(n + 1)  # the coinbase row first, then the block's txs (insertion order)
+        # the coinbase row first, then the block's txs (insertion order)
+        tx_base = pre['tx_base'] if pre is not None else self._tx_rowids(n + 1)
         stmts = [
             ('INSERT INTO blocks (id, hash, content, address, random, difficulty, reward, timestamp) '
              'VALUES (?, ?, ?, ?, ?, ?, ?, ?)',
@@ -2075,12 +2153,19 @@ class Database:
             (self._TX_INSERT, [coinbase_row[1], coinbase_row[0], *coinbase_row[2:], tx_base], 1, None, None, None),
         ]
         self.checkpoint('block')
-        stmts.append((self._TX_INSERT, [tx_cols[0], b['hash'], *tx_cols[1:],
-                                        np.arange(tx_base + 1, tx_base + 1 + n, dtype=np.int64)], n, None, None, None))
+        if pre is not None:
+            stmts.append(_Pre(pre['enc']['tx']))
+        else:
+            stmts.append((self._TX_INSERT, [tx_cols[0], b['hash'], *tx_cols[1:],
+                                            np.arange(tx_base + 1, tx_base + 1 + n, dtype=np.int64)], n, None, None,
+                          None))
         self.checkpoint('transactions')
         # explicit row ids from the ledger-wide counter: the rows land in several files (see UTXO_FILES_DEFAULT)
         ins_u = 'INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake, rowid) VALUES (?, ?, ?, ?, ?)'
-        if gov is None:
+        if pre is not None:
+            if n_out:
+                stmts.append(_Pre(pre['enc']['utxo_ins']))
+        elif gov is None:
             if n_out:
                 base = self._utxo_rowids(n_out)
                 stmts.append((ins_u, [('hex32', np.ascontiguousarray(out_txid), 32, 0),
@@ -2137,7 +2222,9 @@ class Database:
         if 'inode_registration_output' in gov_spent:
             spend_stmt('inode_registration_output')
         sel_u = np.nonzero(in_tag == tag_u)[0] if gov is not None else None
-        if gov is None and n_in:
+        if pre is not None and n_in:
+            stmts.append(_Pre(pre['enc']['utxo_del']))
+        elif gov is None and n_in:
             stmts.append(('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
                           [('hex32', in_keys, 40, 0), in_idx], n_in, in_order, None, n_in))
         elif gov is not None and len(sel_u):
@@ -2156,11 +2243,14 @@ class Database:
         # address index rows: the coinbase's, then the txs' (txcodec.address_pairs: blob, offsets, tx index)
         ca, ch = self.address_rows([coinbase_row])
         parts = [(ca, ch, len(ca))]
-        if addr_pairs is not None:
+        if addr_pairs is not None and pre is None:
             ab, ao, at = addr_pairs
             parts.append((('arena', ab, ao), ('hex32', tx_cols[0][1], 32, 0, np.frombuffer(at, dtype=np.int64)),
                           len(at) // 8))
-        stmts.extend(self._address_index_stmts(b['hash'], int(b['id']), parts))
+        addr_stmts = self._address_index_stmts(b['hash'], int(b['id']), parts)
+        if pre is not None and pre['enc'].get('addr') is not None and addr_stmts:
+            addr_stmts.insert(len(addr_stmts) - 1, _Pre(pre['enc']['addr']))  # the txs' rows, then the watermark
+        stmts.extend(addr_stmts)
         tables |= {'address_transactions', 'address_index_state'}
 
         seq = 0

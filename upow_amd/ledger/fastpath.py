@@ -44,7 +44,7 @@ from ..models.transaction import Transaction
 from ..ops import p256 as op
 from ..ops.native import gpu_available, lib
 from ..utils import metrics, roctx
-from ..utils.codec import TransactionType, get_transaction_type_from_message
+from ..utils.codec import TransactionType, get_transaction_type_from_message, sha256
 from ..utils.hexspans import HexSpans
 from ..utils.logger import get_logger
 from .govcheck import BlockGovernance
@@ -87,6 +87,8 @@ def _i32(d, k):
 # addresses are all 33-byte keys (UPOW_FUSED_VERIFY=0: the host key stage + separate verify, the A/B form)
 FUSED_VERIFY = os.environ.get('UPOW_FUSED_VERIFY', '1') != '0'
 _FUSED_HOST = os.environ.get('UPOW_FUSED_VERIFY') == 'host'  # the same stages on the host (CPU tests of this path)
+# encode a block's large statements while its signatures verify (UPOW_PRE_ENCODE=0: after the verdict)
+PRE_ENCODE = os.environ.get('UPOW_PRE_ENCODE', '1') != '0'
 
 
 def decode_raw(tx_hexes, threads: int) -> dict:
@@ -287,7 +289,19 @@ async def _create_block_from_hex(block_content: str, tx_hexes: List[str], error_
 
 async def _create_block_fast(block_content: str, d: dict, error_list: list, last_block: Optional[dict],
                              t0: float, coinbase=None, page=None) -> Optional[bool]:
-    """True/False for a decided block; None = hand over to the object path."""
+    """True/False for a decided block; None = hand over to the object path. Row ids taken by a block prepared
+    ahead of its verdict (``prepare_native_block``) go back when the block is not applied."""
+    box = {}
+    try:
+        return await _create_block_fast_inner(block_content, d, error_list, last_block, t0, coinbase, page, box)
+    finally:
+        if box.get('pre') is not None and not box.get('used'):
+            from .database import Database
+            Database.instance.release_prepared(box['pre'])
+
+
+async def _create_block_fast_inner(block_content: str, d: dict, error_list: list, last_block: Optional[dict],
+                                   t0: float, coinbase, page, box: dict) -> Optional[bool]:
     from . import manager, validate
     from .database import Database
     database: Database = Database.instance
@@ -455,6 +469,18 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
                         'in_str': in_str[2:]}
         strings_s = perf_counter() - ts0
         roctx.pop()
+        tx_cols = [('hex32', txid, 32, 0), ('hexarena', *d['canon']), ('arena', *in_json), ('arena', *d['out_addr_json']),
+                   ('arena', *d['out_amount_json']), fee_str]
+        out_cols = (out_index, ('arena', *d['out_addr_str']), txid[out_tx], out_amount, out_addr, out_len)
+        if PRE_ENCODE and vfut is not None and gov_cols is None and database.writer is not None:
+            # the GPU is still verifying: build the block's index records and encode its large statements now
+            # (verdict-independent), not after the verdict
+            roctx.push('apply:prepare')
+            tp = perf_counter()
+            box['pre'] = database.prepare_native_block(sha256(block_content), block_no, n, tx_cols, out_cols, in_keys,
+                                                       addr_pairs)
+            timings['prepare_s'] = perf_counter() - tp
+            roctx.pop()
     except BaseException:
         # no launch outlives this block, but the first error is the one that propagates: a failure of the
         # overlapped verify must not replace the apply-columns error being raised here
@@ -524,15 +550,16 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
         # a sync page's plan already split the trusted coinbase and built its index records (pagesync)
         pre_cb = coinbase_transaction.__dict__.get('_upow_cb_index')
         cb_outputs = pre_cb[0] if pre_cb else Database.split_outputs([coinbase_transaction])['unspent_outputs']
-        tx_cols = [('hex32', txid, 32, 0), ('hexarena', *d['canon']), ('arena', *in_json), ('arena', *d['out_addr_json']),
-                   ('arena', *d['out_amount_json']), fee_str]
-        out_cols = (out_index, ('arena', *d['out_addr_str']), txid[out_tx], out_amount, out_addr, out_len)
+        pre = box.get('pre')
+        if pre is not None and block_hash != sha256(block_content):
+            raise RuntimeError('prepared block statements for another block hash')
         submitted = database._submitted
+        box['used'] = True
         roctx.pop()
         try:
             seq = database.apply_native_block(block_row, cb_row, cb_outputs, n, tx_cols, out_cols, in_keys, pay,
                                               gov=gov_cols, addr_pairs=addr_pairs,
-                                              cb_index=pre_cb[1:] if pre_cb else None)
+                                              cb_index=pre_cb[1:] if pre_cb else None, pre=pre)
         except Exception as e:
             if database._submitted != submitted:
                 raise  # committed to the journal: a failure after the commit point is not a rejection
