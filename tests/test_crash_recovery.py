@@ -146,6 +146,7 @@ def test_single_utxo_file_ledger_is_split_on_open(tmp_path, monkeypatch):
     """A ledger written with one UTXO file (before the 00-7f / 80-ff split) opens with the rows of the
     high half moved to the second file (row ids kept), the same UTXO set and K12 hash, and keeps
     applying blocks. (Built in the layout of that era: transactions in the main file, two UTXO files.)"""
+    monkeypatch.setenv('UPOW_LEDGER_MIXED', '0')
     monkeypatch.setenv('UPOW_UTXO_FILES', '2')
     monkeypatch.setenv('UPOW_TX_FILES', '0')
     import asyncio
