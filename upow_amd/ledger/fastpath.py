@@ -87,8 +87,11 @@ def _i32(d, k):
 # addresses are all 33-byte keys (UPOW_FUSED_VERIFY=0: the host key stage + separate verify, the A/B form)
 FUSED_VERIFY = os.environ.get('UPOW_FUSED_VERIFY', '1') != '0'
 _FUSED_HOST = os.environ.get('UPOW_FUSED_VERIFY') == 'host'  # the same stages on the host (CPU tests of this path)
-# encode a block's large statements while its signatures verify (UPOW_PRE_ENCODE=0: after the verdict)
-PRE_ENCODE = os.environ.get('UPOW_PRE_ENCODE', '1') != '0'
+# UPOW_PRE_ENCODE=1: encode a block's large statements while its signatures verify instead of after the
+# verdict. Off by default: in three interleaved pairs on the GPU box the host work (apply strings + this,
+# ~2.8 ms) outlasted the GPU's ~1.4 ms, and the commit latency came out 9.1-9.5 ms against 8.8-8.9 without
+# it (profiles/r5/pre_encode_ab_r5zy/)
+PRE_ENCODE = os.environ.get('UPOW_PRE_ENCODE', '0') == '1'
 
 
 def decode_raw(tx_hexes, threads: int) -> dict:
