@@ -2015,12 +2015,33 @@ class Database:
         return self._pending_empty
 
     def prepare_native_block(self, block_hash: str, block_id: int, n: int, tx_cols: list, out_cols: tuple,
-                             in_keys: np.ndarray, addr_pairs: Optional[tuple]) -> dict:
+                             in_keys: np.ndarray, addr_pairs: Optional[tuple], outputs: Optional[dict] = None) -> dict:
         """The part of :meth:`apply_native_block` that does not depend on the block's verdict, its reward or the
         mempool, for a block without governance txs: the index records of its outputs and spends, its row
         ids, and its four large statements (tx rows, UTXO inserts, UTXO deletes, the txs' address rows)
         encoded. The native block path runs it while the GPU verifies the block's signatures; a block that is
-        then rejected hands its row ids back (:meth:`release_prepared`)."""
+        then rejected hands its row ids back (:meth:`release_prepared`). ``outputs``: the
+        :meth:`prepare_native_outputs` half, computed ahead on another thread."""
+        pre = outputs if outputs is not None else self.prepare_native_outputs(out_cols, in_keys)
+        tx_start = self._tx_rowids(n + 1)
+        names, stmts = ['tx'], [(self._TX_INSERT, [tx_cols[0], block_hash, *tx_cols[1:],
+                                                   np.arange(tx_start + 1, tx_start + 1 + n, dtype=np.int64)],
+                                 n, None, None, None)]
+        if addr_pairs is not None:
+            ab, ao, at = addr_pairs
+            rows = self._address_index_stmts(block_hash, int(block_id), [
+                (('arena', ab, ao), ('hex32', tx_cols[0][1], 32, 0, np.frombuffer(at, dtype=np.int64)), len(at) // 8)])
+            if len(rows) == 2:  # inline address index on: the txs' rows (the watermark is built at commit)
+                names.append('addr')
+                stmts.append(rows[0])
+        pre['enc'].update(zip(names, self.encode_many(stmts)))
+        pre['tx_base'] = tx_start
+        pre['rowids'] = (tx_start, tx_start + n + 1, *pre['rowids'][2:])
+        return pre
+
+    def prepare_native_outputs(self, out_cols: tuple, in_keys: np.ndarray) -> dict:
+        """The half of :meth:`prepare_native_block` that needs neither the block's hash nor its apply strings:
+        index records, UTXO row ids, and the UTXO insert and delete statements encoded."""
         from ..ops.native import lib
         out_index, out_addr_spec, out_txid, out_amount, out_addr, out_len = out_cols
         n_out, n_in = len(out_index), len(in_keys)
@@ -2033,11 +2054,8 @@ class Database:
         in_keys = np.ascontiguousarray(in_keys, dtype=np.uint8).reshape(-1, 40)
         sb, ib = lib().spent_index_records(in_keys, np.full(n_in, tag_u, dtype=np.uint32))
         in_idx = np.frombuffer(ib, dtype=np.int64)
-        tx_start = self._tx_rowids(n + 1)
         utxo_start = self._utxo_rowids(n_out)
-        names, stmts = ['tx'], [(self._TX_INSERT, [tx_cols[0], block_hash, *tx_cols[1:],
-                                                   np.arange(tx_start + 1, tx_start + 1 + n, dtype=np.int64)],
-                                 n, None, None, None)]
+        names, stmts = [], []
         if n_out:
             names.append('utxo_ins')
             stmts.append(('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake, rowid) VALUES (?, ?, ?, ?, ?)',
@@ -2048,24 +2066,17 @@ class Database:
             names.append('utxo_del')
             stmts.append(('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
                           [('hex32', in_keys, 40, 0), in_idx], n_in, 'key', None, n_in))
-        if addr_pairs is not None:
-            ab, ao, at = addr_pairs
-            rows = self._address_index_stmts(block_hash, int(block_id), [
-                (('arena', ab, ao), ('hex32', tx_cols[0][1], 32, 0, np.frombuffer(at, dtype=np.int64)), len(at) // 8)])
-            if len(rows) == 2:  # inline address index on: the txs' rows (the watermark is built at commit)
-                names.append('addr')
-                stmts.append(rows[0])
         return {'recs': np.frombuffer(rb, dtype=np.uint8).reshape(-1, 40), 'pay': np.frombuffer(pb, dtype=PAYLOAD_DTYPE),
-                'spent': np.frombuffer(sb, dtype=np.uint8).reshape(-1, 40), 'in_idx': in_idx, 'tx_base': tx_start,
-                'rowids': (tx_start, tx_start + n + 1, utxo_start, utxo_start + n_out),
-                'enc': dict(zip(names, self.encode_many(stmts)))}
+                'spent': np.frombuffer(sb, dtype=np.uint8).reshape(-1, 40), 'in_idx': in_idx,
+                'rowids': (None, None, utxo_start, utxo_start + n_out),
+                'enc': dict(zip(names, [self.encode(*st) for st in stmts]))}
 
     def release_prepared(self, pre: dict):
         """A prepared block that was not applied: its row ids go back when nothing was allocated after them
         (the ledger lock is held from prepare to here, so nothing was)."""
         t0, t1, u0, u1 = pre['rowids']
         with self._seq_lock:
-            if self._tx_next_rowid == t1:
+            if t1 is not None and self._tx_next_rowid == t1:
                 self._tx_next_rowid = t0
             if self._utxo_next_rowid == u1:
                 self._utxo_next_rowid = u0

@@ -70,6 +70,18 @@ AMOUNT_LIMIT = 1 << 52  # > max supply in smallest units; keeps per-tx int64 sum
 _VERIFY_POOL = None
 
 
+_PREPARE_POOL = None
+
+
+def _prepare_pool():
+    """One helper thread for the verdict-independent half of a block's apply (UPOW_PRE_ENCODE=1)."""
+    global _PREPARE_POOL
+    if _PREPARE_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _PREPARE_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix='upow-block-prepare')
+    return _PREPARE_POOL
+
+
 def _verify_pool():
     """One helper thread for the block's signature verify (overlapped with the apply strings)."""
     global _VERIFY_POOL
@@ -298,6 +310,11 @@ async def _create_block_fast(block_content: str, d: dict, error_list: list, last
     try:
         return await _create_block_fast_inner(block_content, d, error_list, last_block, t0, coinbase, page, box)
     finally:
+        if 'pre_fut' in box:  # the helper's half, never joined (an error on the way): wait for it, then hand back
+            try:
+                box['pre'] = box.pop('pre_fut').result()
+            except Exception:
+                pass
         if box.get('pre') is not None and not box.get('used'):
             from .database import Database
             Database.instance.release_prepared(box['pre'])
@@ -452,6 +469,12 @@ async def _create_block_fast_inner(block_content: str, d: dict, error_list: list
     else:
         vfut = _verify_pool().submit(validate._verify, rec_bytes, None) \
             if n_jobs and pre_status is None and validate.overlappable(n_jobs) else None
+    out_index = np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]
+    out_cols = (out_index, ('arena', *d['out_addr_str']), txid[out_tx], out_amount, out_addr, out_len)
+    if PRE_ENCODE and vfut is not None and not bg.any and database.writer is not None:
+        # while the GPU verifies: the block's index records and UTXO statements on a helper thread, its tx and
+        # address statements on this one once the apply strings are rendered (prepare_native_block below)
+        box['pre_fut'] = _prepare_pool().submit(database.prepare_native_outputs, out_cols, in_keys)
     try:
         # ---- columns for the ledger writes: views of the codec's buffers, encoded natively into one journal
         #      batch by csrc/ledger_writer.cpp (tx hashes rendered from the raw digests, text arenas for strings)
@@ -464,7 +487,6 @@ async def _create_block_fast_inner(block_content: str, d: dict, error_list: list
         # the block's address_transactions rows (each tx's distinct input owners and output addresses)
         addr_pairs = L.address_pairs(in_str[2], in_str[3], d['in_start'], *d['out_addr_str'], d['out_start'], THREADS)
         fee_str = ('arena', *L.fee_strings(np.ascontiguousarray(fee, dtype=np.int64).tobytes()))
-        out_index = np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]
         gov_cols = None
         if bg.any:
             gov_cols = {'out_tag': bg.output_tags(TAG_BY_TABLE), 'out_type': out_type, 'in_tag': in_tag,
@@ -474,14 +496,14 @@ async def _create_block_fast_inner(block_content: str, d: dict, error_list: list
         roctx.pop()
         tx_cols = [('hex32', txid, 32, 0), ('hexarena', *d['canon']), ('arena', *in_json), ('arena', *d['out_addr_json']),
                    ('arena', *d['out_amount_json']), fee_str]
-        out_cols = (out_index, ('arena', *d['out_addr_str']), txid[out_tx], out_amount, out_addr, out_len)
-        if PRE_ENCODE and vfut is not None and gov_cols is None and database.writer is not None:
-            # the GPU is still verifying: build the block's index records and encode its large statements now
-            # (verdict-independent), not after the verdict
+        if 'pre_fut' in box:
+            # the GPU is still verifying: the rest of the verdict-independent apply work now, not after the verdict
             roctx.push('apply:prepare')
             tp = perf_counter()
+            outputs = box.pop('pre_fut').result()
+            box['pre'] = outputs  # its row ids go back if what follows fails
             box['pre'] = database.prepare_native_block(sha256(block_content), block_no, n, tx_cols, out_cols, in_keys,
-                                                       addr_pairs)
+                                                       addr_pairs, outputs=outputs)
             timings['prepare_s'] = perf_counter() - tp
             roctx.pop()
     except BaseException:
