@@ -102,7 +102,7 @@ _FUSED_HOST = os.environ.get('UPOW_FUSED_VERIFY') == 'host'  # the same stages o
 # UPOW_PRE_ENCODE=1: encode a block's large statements while its signatures verify instead of after the
 # verdict. Off by default: in three interleaved pairs on the GPU box the host work (apply strings + this,
 # ~2.8 ms) outlasted the GPU's ~1.4 ms, and the commit latency came out 9.1-9.5 ms against 8.8-8.9 without
-# it (profiles/r5/pre_encode_ab_r5zy/)
+# it (profiles/r5/pre_encode_ab_r5zy/; with the UTXO half on a helper thread, profiles/r5/pre_encode_split_ab_r6a/)
 PRE_ENCODE = os.environ.get('UPOW_PRE_ENCODE', '0') == '1'
 
 
