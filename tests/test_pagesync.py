@@ -107,13 +107,14 @@ def _missing_input_tx() -> str:
     return signed_spend_txs(spend, [KA], [string_to_bytes(_addr(KA))], [string_to_bytes(_addr(KC))])[0]
 
 
-async def _sync(path, pages, mode: str):
+async def _sync(path, pages, mode: str, backend: str = 'host'):
     """Apply ``pages`` (each a list of /get_blocks entries) to a fresh ledger; returns (verdicts, errors,
     state)."""
     from upow_amd.ledger import manager, pagesync
     from upow_amd.ledger.database import Database
     from upow_amd.node import main as node_main
-    db = await Database.create(path=str(path), utxo_backend='host')
+    db = await Database.create(path=str(path), utxo_backend=backend)
+    assert db.utxo.backend_name == backend
     manager.Manager.difficulty = None
     verdicts, errors = [], []
     for page in pages:
@@ -161,17 +162,28 @@ def small_chunks(monkeypatch):
     monkeypatch.setattr(pagesync, 'CHUNK', 5)  # several chunks per page; spends cross chunk boundaries
 
 
-def _both(tmp_path, pages):
-    a = asyncio.run(_sync(tmp_path / 'page' / 'l.sqlite3', pages, 'page'))
+@pytest.fixture(params=['host', pytest.param('gpu', marks=pytest.mark.gpu)])
+def backend(request, monkeypatch):
+    """The page path's UTXO table: host, or the HBM table with every signature batch on the GPU kernel."""
+    if request.param == 'gpu':
+        request.getfixturevalue('gpu')
+        from upow_amd.ops import p256 as op
+        monkeypatch.setattr(op, 'GPU_MIN_BATCH', 1)
+    return request.param
+
+
+def _both(tmp_path, pages, backend='host'):
+    """(page path on ``backend``, per-block path on the host table: the reference's semantics)."""
+    a = asyncio.run(_sync(tmp_path / 'page' / 'l.sqlite3', pages, 'page', backend))
     b = asyncio.run(_sync(tmp_path / 'block' / 'l.sqlite3', pages, 'block'))
     return a, b
 
 
-def test_page_sync_equals_per_block_sync(tmp_path, source_page, small_chunks):
+def test_page_sync_equals_per_block_sync(tmp_path, source_page, small_chunks, backend):
     from upow_amd.ledger import pagesync
     pages = [source_page[:11], source_page[11:]]
     PATHS.clear()
-    a, b = _both(tmp_path, pages)
+    a, b = _both(tmp_path, pages, backend)
     assert a == b
     assert a[0] == [True, True] and a[2]['height'] == len(source_page)
     # the page path carried every block — empty ones, the genesis block and the grouped tx included
@@ -179,28 +191,59 @@ def test_page_sync_equals_per_block_sync(tmp_path, source_page, small_chunks):
 
 
 @pytest.mark.parametrize('where', ['first', 'last', 'middle'])
-def test_forged_signature_at_page_edges(tmp_path, source_page, small_chunks, where):
+def test_forged_signature_at_page_edges(tmp_path, source_page, small_chunks, where, backend):
     at = {'first': 12, 'last': 17, 'middle': 15}[where]
     victim = source_page[at]['transactions'][1]  # a plain tx (index 0 is the coinbase)
     forged = _forge(source_page, at, [_bad_sig(victim)], tail=where != 'last')
     pages = [forged[:12], forged[12:]]
-    a, b = _both(tmp_path, pages)
+    a, b = _both(tmp_path, pages, backend)
     assert a == b
     assert a[0][-1] is False and 'has been not verified' in a[1][-1][0]
     assert a[2]['height'] == at  # every block before the forged one applied, nothing after
 
 
-def test_missing_input_and_cross_block_double_spend(tmp_path, source_page, small_chunks):
+def test_missing_input_and_cross_block_double_spend(tmp_path, source_page, small_chunks, backend):
     # a spend of an outpoint that never existed
     forged = _forge(source_page, 14, [_missing_input_tx()])
-    a, b = _both(tmp_path / 'missing', [forged[:14], forged[14:]])
+    a, b = _both(tmp_path / 'missing', [forged[:14], forged[14:]], backend)
     assert a == b and a[0] == [True, False] and a[2]['height'] == 14
     # block 16 re-spends an input block 15 (same page, same chunk) already spent
     spent_again = source_page[14]['transactions'][1]
     forged = _forge(source_page, 15, [spent_again])
-    a, b = _both(tmp_path / 'double', [forged[:13], forged[13:]])
+    a, b = _both(tmp_path / 'double', [forged[:13], forged[13:]], backend)
     assert a == b and a[0] == [True, False] and a[2]['height'] == 15
     assert 'double spend' in a[1][-1][0]
+
+
+def test_block_without_coinbase_stops_the_page(tmp_path, source_page, small_chunks, backend):
+    """Block 15 carries no coinbase and spends a live output; block 16 spends it again. The reference's sync
+    stops at block 15 (create_block_in_syncing_old dereferences the coinbase, manager.py:790): neither path
+    may mint a coinbase for it (the push variant), and the page plan never applies block 16 on a plan that
+    did not model block 15."""
+    spend = source_page[15]['transactions'][1]
+    forged = _forge(source_page, 14, [spend])
+    forged[14]['transactions'] = forged[14]['transactions'][1:]  # the header's merkle root excludes the coinbase
+    forged = _forge(forged, 15, [spend])
+    a, b = _both(tmp_path, [forged[:12], forged[12:]], backend)
+    assert a == b
+    assert a[0] == [True, False] and a[2]['height'] == 14
+    assert 'no coinbase' in a[1][-1][0]
+
+
+def test_coinbase_with_trailing_bytes_is_split_off_on_both_paths(tmp_path, source_page, small_chunks, backend):
+    """A coinbase (specifier 36) followed by extra bytes, placed after the block's txs: the codec flags it
+    a coinbase (txdecode.h TX_COINBASE), so both sync paths split it off the same way."""
+    from upow_amd.ledger.pagesync import _coinbase_index
+    forged = _forge(source_page, 14, [source_page[14]['transactions'][1]])
+    cb, *txs = forged[14]['transactions']
+    odd = cb + 'abcd'
+    forged[14]['transactions'] = txs + [odd]
+    assert _coinbase_index(forged[14]['transactions']) == len(txs)
+    # two coinbases: the trailing-bytes one comes first in the list, so it is the one the reference trusts
+    assert _coinbase_index([odd, cb]) == 0
+    a, b = _both(tmp_path, [forged[:12], forged[12:]], backend)
+    assert a == b
+    assert a[0][0] is True
 
 
 def _cluster_worker(rank, world, port, tmp, q):
@@ -262,3 +305,76 @@ def test_page_sync_on_a_gloo_cluster_matches_single_node(tmp_path, source_page, 
     assert [verdicts, errors] == [ref[0], ref[1]]
     assert all(s == ref[2] for s in states), (states, ref[2])
     assert ref[2]['height'] == 17 and stats['page_path'] > 0
+
+
+RCCL_PAGE = r'''
+import asyncio, json, os, sys
+sys.path.insert(0, sys.argv[1])
+tmp = sys.argv[2]
+from upow_amd.ops.native import lib
+lib()
+from upow_amd.ledger import pagesync
+from upow_amd.ledger.database import Database
+from upow_amd.parallel import cluster
+from upow_amd.parallel.dist import init_from_env, op_context, shutdown
+from test_pagesync import _state
+ctx = init_from_env()
+assert ctx.is_distributed and ctx.backend == 'nccl', (ctx.is_distributed, ctx.backend)
+c = cluster.init(op_context(ctx), ctx)  # as the node does: op traffic on its own group
+with open(os.path.join(tmp, 'pages.json')) as f:
+    pages = json.load(f)
+
+
+async def go():
+    db = await Database.create(path=os.path.join(tmp, 'r0', 'l.sqlite3'), utxo_backend='gpu')
+    await cluster.leader_start(db)
+    verdicts, errors = [], []
+    for page in pages:
+        err = []
+        verdicts.append(await pagesync.create_blocks(page, err))
+        errors.append(err[:1])
+        if not verdicts[-1]:
+            break
+    info = c.info()
+    await cluster.leader_quit()
+    st = await _state(db)
+    db.close()
+    return {'verdicts': verdicts, 'errors': errors, 'state': st, 'info': info, 'stats': dict(pagesync.stats)}
+res = asyncio.run(go())
+print(json.dumps(res, default=str), flush=True)
+shutdown(ctx)
+'''
+
+
+@pytest.mark.gpu
+def test_page_sync_on_a_single_rank_rccl_cluster(gpu, tmp_path, source_page, small_chunks):
+    """The page path of a cluster node on a real RCCL communicator (forced single-rank job): every chunk's
+    signature batch through ``verify_records_dp`` (GPU kernel + status all-gather), the plan's all-reduce,
+    and one native commit vote per block, against the host per-block reference."""
+    import subprocess
+    import sys
+    from test_rccl_vote import _port
+    victim = source_page[17]['transactions'][1]
+    forged = _forge(source_page, 17, [_bad_sig(victim)])
+    pages = [forged[:9], forged[9:]]
+    (tmp_path / 'c').mkdir()
+    with open(tmp_path / 'c' / 'pages.json', 'w') as f:
+        json.dump(pages, f)
+    script = tmp_path / 'rccl_page.py'
+    script.write_text(RCCL_PAGE)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT')}
+    env.update(UPOW_FORCE_DIST='1', HSA_ENABLE_IPC_MODE_LEGACY='0', UPOW_START_DIFFICULTY='1.0', UPOW_CORE_URL='',
+               UPOW_SYNC_CHUNK='5', UPOW_P256_GPU_MIN_BATCH='1',
+               PYTHONPATH=os.pathsep.join([root, os.path.join(root, 'tests')]))
+    p = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '1',
+                        '--master-addr', '127.0.0.1', '--master-port', str(_port()), str(script), root,
+                        str(tmp_path / 'c')], cwd=root, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith('{')][-1]
+    ref = asyncio.run(_sync(tmp_path / 'ref' / 'l.sqlite3', pages, 'block'))
+    assert [res['verdicts'], res['errors']] == [ref[0], ref[1]]
+    assert res['state'] == ref[2], (res['state'], ref[2])
+    assert ref[2]['height'] == 17 and res['stats']['page_path'] > 0
+    # every applied block of the sync was agreed on the native communicator
+    assert res['info']['commits_agreed'] == 17 and res['info']['native_vote']['votes'] >= 17, res['info']

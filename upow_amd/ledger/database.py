@@ -2269,7 +2269,7 @@ class Database:
         if self.writer is not None:
             enc = self.encode_many(stmts)
             stamp()
-            _commit_point()  # a cluster node: every replica agreed to commit this block (the vote overlapped the encode)
+            _commit_point()  # a cluster node: every replica votes to commit this block, now that nothing but the write can fail
             # the undo record as parts: the writer joins them in one copy off the GIL
             meta = [bytes.fromhex(b['hash']), struct.pack('<qII', int(b['id']), n_out + len(cb_keys), n_in), recs,
                     np.ascontiguousarray(cb_recs), spent, np.ascontiguousarray(spent_payload).view(np.uint8)]

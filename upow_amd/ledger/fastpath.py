@@ -237,7 +237,7 @@ async def create_block_from_hex(block_content: str, tx_hexes: List[str], error_l
 
     On a multi-GPU cluster node (parallel/cluster.py) the leader first broadcasts the block to the
     follower replicas (``mirror``); every rank validates it, and the replicas agree in one all-reduce
-    right BEFORE any of them commits it (``cluster.commit_gate``)."""
+    right BEFORE any of them commits it (``cluster.commit_point``)."""
     from ..parallel import cluster
     c = cluster.get()
     if c is not None and c.leader and mirror and not c.replaying:
@@ -245,8 +245,8 @@ async def create_block_from_hex(block_content: str, tx_hexes: List[str], error_l
         flush_txs()  # the followers' mempools first: block rules consult pending txs
         c.send('block', pack_txs(tx_hexes), content=block_content, cb=coinbase.hex() if coinbase is not None else None)
     err = None
-    # agree before commit: every replica votes right before its ledger writes (manager._finalize_* →
-    # cluster.commit_gate) and writes only if all voted yes; a replica that rejects votes no at the end
+    # agree before commit: every replica votes right before its journal write (cluster.commit_point) and
+    # writes only if all voted yes; a replica that rejects (or fails before that point) votes no at the end
     gate, token = cluster.open_gate('block')
     try:
         ok = await _create_block_from_hex(block_content, tx_hexes, error_list, last_block, coinbase, decoded, page)

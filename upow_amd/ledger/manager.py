@@ -417,6 +417,8 @@ async def _apply_block(block_no, block_hash, block_content, address, random, dif
             Manager.difficulty = None
             return False
         return True
+    from .database import _commit_point
+    _commit_point()  # a cluster node: every replica ready to write this block (no-op on a single node)
     try:
         with database.transaction():
             await database.add_block(block_no, block_hash, block_content, address, random, difficulty,
@@ -577,8 +579,9 @@ async def _finalize_block(block_no: int, block_content: str, fees, n_txs: int, a
 
 def _commit_gate() -> bool:
     """On a multi-GPU cluster node: every replica agrees to commit this block before any of them writes it
-    (parallel/cluster.py ``commit_gate``: the vote is queued here and resolved at the ledger's commit point,
-    right before the journal write, so preparing the block's batch overlaps it); always True on a single node."""
+    (parallel/cluster.py ``commit_gate``: the block is marked ready here; the vote is cast at the ledger's
+    commit point, right before the journal write, after everything that can fail without writing); always
+    True on a single node."""
     from ..parallel import cluster
     return cluster.commit_gate()
 

@@ -83,18 +83,30 @@ def _i32(d, k):
 
 
 def _coinbase_index(hexes: List[str]) -> Optional[int]:
-    """The first tx the codec flags as a coinbase (specifier 36). A coinbase's specifier is its last byte, so
-    only txs whose hex ends in 24 are decoded to ask."""
+    """The first tx the codec flags as a coinbase (specifier 36, whatever bytes follow it: the reference's
+    parser, transaction.py:548-555, and txdecode.h TX_COINBASE). A well-formed coinbase ends in its specifier,
+    so the txs whose hex ends in 24 are asked first; the txs before the first such coinbase (all of them when
+    there is none) are then decoded for their flags, so a coinbase with trailing bytes ahead of it is still
+    the one split off, as the reference and ``node/main.py _scan_sync_block`` split it."""
+    from .fastpath import THREADS, decode_raw
     L = lib()
     if isinstance(hexes, HexSpans):  # the tails read from the body: a str only for the candidates
         tails = hexes.tail2() + [h[-2:].encode() for h in hexes.extra]
         cand = [k for k, t in enumerate(tails) if t == b'24']
     else:
         cand = [k for k, h in enumerate(hexes) if h.endswith('24')]
+    first = None
     for k in cand:
         if L.decode_block_txs([hexes[k]], 1)['flags'][0] == 3:
+            first = k
+            break
+    upto = len(hexes) if first is None else first
+    if upto:
+        flags = decode_raw(hexes[:upto], 1 if upto < 512 else THREADS)['flags']
+        k = next((i for i, f in enumerate(flags) if f == 3), None)
+        if k is not None:
             return k
-    return None
+    return first
 
 
 def prepare(info: dict) -> Item:
@@ -406,6 +418,14 @@ async def create_blocks(blocks: list, error_list: list = None, mirror: bool = Tr
                     block['merkle_tree'] = get_transactions_merkle_tree([tx.hex() for tx in txs])
                     block_content = block_to_bytes(last_block['hash'], block)
                 assert i == block['id'], (i, block['id'])
+                if cbs[k] is None:
+                    # a sync block carries its coinbase (create_block_in_syncing_old dereferences it,
+                    # reference manager.py:790): without one the page stops here, as the reference's sync does.
+                    # It never reaches the push variant, and the plan never modelled it (build_plan only plans
+                    # blocks with a coinbase), so no later block of the chunk is applied on a stale plan
+                    error_list.append(error := f'block {block["id"]} has no coinbase transaction')
+                    logger.error(error)
+                    return False
                 pb = plan[k]
                 if not await fastpath.create_block_from_hex(
                         block_content.hex() if isinstance(block_content, bytes) else block_content, it.hexes,

@@ -300,6 +300,14 @@ async def create_blocks_per_block(blocks: list, error_list=None) -> bool:
                 hexes = hexes[:cb_k] + hexes[cb_k + 1:]
             else:
                 dec = None  # not what the scan assumed: decode inline below
+        if cb_tx is None:
+            # the reference's sync dereferences the coinbase (manager.py:790): a block without one ends the
+            # sync; it never takes the push variant (which would mint its own coinbase)
+            if ahead is not None:
+                await ahead
+            error_list.append(error := f'block {block["id"]} has no coinbase transaction')
+            logger.error(error)
+            return False
         block_content = block.get('content')
         if not block_content:
             txs = [await Transaction.from_hex(h) for h in hexes]

@@ -32,8 +32,8 @@ timeout, and every ``ACK_EVERY`` replayed blocks the leader and the followers me
 also carries each follower's success, so no broadcast stays queued for long and a follower that cannot
 apply the leader's chain stops the resync instead of hanging it.
 
-Agree before commit. A block (push or sync form) is validated on every replica; right before its ledger
-writes each replica votes in one all-reduce (``commit_gate``, called by ``manager._finalize_*``), and
+Agree before commit. A block (push or sync form) is validated on every replica; right before its journal
+write each replica votes in one all-reduce (``commit_point``, once the block's batch is encoded), and
 writes only when every replica voted to. A replica that rejected the block votes no when it finishes. A
 split vote is a replica divergence: nothing was committed anywhere, and every rank exits with status 70
 (``DistContext._failed``); a relaunch resyncs the replicas from that common state. Rollbacks, chain
@@ -144,9 +144,15 @@ class Cluster:
 
     def agree_state(self, db, what: str):
         """After a rollback, a chain deletion or a mempool GC: every replica at the same (height, tip hash,
-        mempool size), checked in one fixed-size all-gather."""
+        mempool size), checked in one fixed-size all-gather.
+
+        The leader's HTTP loop keeps admitting txs while the op runs: an admission made after the op was sent
+        sits in the leader's index but only in the outbox, not yet on the followers. So the leader counts what
+        the followers hold at this op: its index minus the outbox rows still in it, read under the index lock
+        the admissions take (outbox rows the op itself removed from the index are dropped, they never ship)."""
         tip = _tip_hash(db)
-        mine = struct.pack('<qq', db._tip_id(), _mempool_size(db)) + (bytes.fromhex(tip) if tip else bytes(32))
+        size = _replicated_mempool_size(db) if self.leader else _mempool_size(db)
+        mine = struct.pack('<qq', db._tip_id(), size) + (bytes.fromhex(tip) if tip else bytes(32))
         got = self.op_ctx.all_gather_fixed(mine)
         if any(g != got[0] for g in got):
             states = [(struct.unpack('<qq', g[:16]), g[16:].hex()[:16]) for g in got]
@@ -206,13 +212,15 @@ _GATE: contextvars.ContextVar = contextvars.ContextVar('upow_commit_gate', defau
 
 
 class CommitGate:
-    """Agree-before-commit for one block on a cluster node: :meth:`start` when the block is ready to commit
-    (the vote's all-reduce is queued, the host goes on preparing the block's ledger batch), :meth:`wait` at the
-    commit point — right before the journal write (``commit_point``) — and :meth:`close` with the rank's final
-    verdict. Exactly one all-reduce per block per rank; a rank that rejects the block votes in :meth:`close`."""
+    """Agree-before-commit for one block on a cluster node: :meth:`start` + :meth:`wait` at the commit point —
+    right before the journal write (``commit_point``), once the block's batch is encoded — and :meth:`close`
+    with the rank's final verdict. Exactly one all-reduce per block per rank; a rank that rejects the block, or
+    fails before its commit point, votes no in :meth:`close`, so a failure every replica shares is a clean
+    rejection and only a split is a divergence."""
 
     def __init__(self, c: Cluster, what: str):
         self.c, self.what = c, what
+        self.ready = False  # passed validation (commit_gate); the vote itself is cast at the commit point
         self.voted: Optional[bool] = None
         self.n = 0
         self._pending = None
@@ -279,11 +287,14 @@ def close_gate(gate: Optional[CommitGate], token, ok: bool) -> bool:
 
 
 def commit_gate() -> bool:
-    """Called by the block paths once a block has passed validation, before they prepare its ledger writes:
-    queues this rank's vote (the outcome is taken at :func:`commit_point`)."""
+    """Called by the block paths once a block has passed validation, before they prepare its ledger writes.
+    Casts no vote: the vote is taken at :func:`commit_point`, after every step that can still fail without
+    writing (statement building and encoding). A vote queued here instead would let a replica vote yes and
+    then fail before its journal write; a failure every replica shares would then look like a split (all
+    voted yes, none committed) and stop the cluster on a block a single node simply rejects."""
     g = _GATE.get()
     if g is not None:
-        g.start()
+        g.ready = True
     return True
 
 
@@ -292,10 +303,15 @@ class CommitRefused(RuntimeError):
 
 
 def commit_point():
-    """The ledger's commit point (right before a block's journal write): waits for the block's vote and
-    raises :class:`CommitRefused` unless every replica is ready. No-op outside an active cluster gate."""
+    """The ledger's commit point (right before a block's journal write): votes, waits for the outcome and
+    raises :class:`CommitRefused` unless every replica is ready. Past this point the only failure is the
+    journal write itself, which is a local I/O fault (a divergence, status 70). No-op outside an active
+    cluster gate."""
     g = _GATE.get()
-    if g is not None and not g.wait():
+    if g is None:
+        return
+    g.start()
+    if not g.wait():
         raise CommitRefused(f'{g.what}: {g.n}/{g.c.ctx.world} replicas ready to commit')
 
 
@@ -317,6 +333,18 @@ def _mempool_size(db) -> int:
     if mp is not None:
         return len(mp)
     return int(db._q1('SELECT COUNT(*) FROM pending_transactions')[0])
+
+
+def _replicated_mempool_size(db) -> int:
+    """The leader's mempool size as the followers see it at the current op (see ``Cluster.agree_state``)."""
+    mp = db._mempool()
+    if mp is None:
+        with _outbox_lock:
+            return _mempool_size(db) - len(_outbox)
+    with mp.lock:
+        with _outbox_lock:
+            _outbox[:] = [row for row in _outbox if mp.has_tx(row[5])]
+            return len(mp) - len(_outbox)
 
 
 def pack_txs(tx_hexes) -> bytes:
@@ -747,6 +775,8 @@ async def follower_main(c: Cluster, db):
             if replay_error is None and int(msg['h']) > db._tip_id():  # else: this replica already holds it
                 try:
                     hexes, cb = await _split_coinbase(unpack_txs(msg['_payload']))
+                    if cb is None:  # a replayed block is the sync form: it carries its coinbase
+                        raise RuntimeError(f'block {msg["h"]} has no coinbase transaction')
                     if not await fastpath.create_block_from_hex(msg['content'], hexes, coinbase=cb,
                                                                 last_block=last_block, mirror=False):
                         raise RuntimeError(f'block {msg["h"]} rejected')
