@@ -284,6 +284,19 @@ for s in $STEPS; do
           > "$OUT/sync_plain_$k.json" 2> "$OUT/sync_plain_$k.err" || { tail -20 "$OUT/sync_plain_$k.err"; exit 1; }
         cut -c1-300 "$OUT/sync_plain_$k.json"
       done ;;
+    leansync:*)
+      # page-batched sync of one chain on an N-rank cluster node sharing this one GPU (host collectives:
+      # UPOW_DIST_BACKEND=gloo; every rank's P-256, UTXO and decompression work on the GPU), lean followers
+      # (default) vs full followers (UPOW_CLUSTER_LEAN=0): per-rank host CPU per block
+      N=${s#leansync:}
+      for mode in 1 0; do
+        rm -rf /tmp/upow_bench_ledger
+        UPOW_CLUSTER_LEAN=$mode UPOW_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
+          --nproc-per-node "$N" --master-addr 127.0.0.1 --master-port 2957$mode bench.py --gpus "$N" --mode sync \
+          --txs 200 --steps 1000 --warmup 5 --ledger /tmp/upow_bench_ledger > "$OUT/leansync_${N}_lean$mode.json" \
+          2> "$OUT/leansync_${N}_lean$mode.err" || { tail -20 "$OUT/leansync_${N}_lean$mode.err"; exit 1; }
+        grep '^{' "$OUT/leansync_${N}_lean$mode.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print({k: d.get(k) for k in ('world','value','ms_per_step','blocks_per_s','rank_cpu_ms_per_block','rank_cpu_ms_per_block_ex_p256','follower_cpu_vs_leader','lean_followers')})"
+      done ;;
     sprofpage)
       # rocprofv3 kernel trace of the page-batched sync (200-tx blocks)
       rm -rf /tmp/upow_bench_ledger

@@ -115,7 +115,8 @@ def _tips(tmp_path):
     from upow_amd.ledger.database import Database
 
     async def go(path):
-        db = await Database.create(path=str(path), utxo_backend='host')
+        from upow_amd.tools import open_ledger
+        db = await open_ledger(str(path))  # a lean follower's op log is materialised first
         try:
             return db._tip_id()
         finally:

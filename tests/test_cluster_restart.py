@@ -41,9 +41,10 @@ def _start(tmp_path, world, tag):
 
 def _stop(p, log, follower_dir=None):
     """SIGTERM to the whole job (torchrun itself exits 1 on a signal); the follower must stop gracefully:
-    the leader's shutdown sends 'quit', the follower snapshots its UTXO index at its tip and closes."""
-    snap = os.path.join(follower_dir, 'utxo_snapshot.bin') if follower_dir else None
-    before = os.path.getmtime(snap) if snap and os.path.exists(snap) else None
+    the leader's shutdown sends 'quit', and the follower either snapshots its UTXO index at its tip (a full
+    replica) or, a lean one (ledger/lean.py), closes its op log with a final tip marker."""
+    snaps = [os.path.join(follower_dir, f) for f in ('utxo_snapshot.bin', 'ledger.sqlite3.oplog')] if follower_dir else []
+    before = [os.path.getmtime(f) if os.path.exists(f) else None for f in snaps]
     try:
         os.killpg(p.pid, signal.SIGTERM)
         p.wait(60)
@@ -52,8 +53,9 @@ def _stop(p, log, follower_dir=None):
         raise
     finally:
         log.close()
-    if snap:
-        assert os.path.exists(snap) and os.path.getmtime(snap) != before, 'follower did not stop gracefully'
+    if snaps:
+        assert any(os.path.exists(f) and os.path.getmtime(f) != b for f, b in zip(snaps, before)), \
+            'follower did not stop gracefully'
 
 
 def _info(url):
@@ -62,10 +64,11 @@ def _info(url):
 
 def _edit_follower(path, fn):
     from upow_amd.ledger import manager
-    from upow_amd.ledger.database import Database
 
     async def go():
-        db = await Database.create(path=str(path), utxo_backend='host')
+        from upow_amd.tools import open_ledger
+        db = await open_ledger(str(path))  # a lean follower's op log is materialised first
+        assert db.utxo.backend_name == 'host'
         manager.Manager.difficulty = None
         try:
             await fn(db)

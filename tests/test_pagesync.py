@@ -264,6 +264,9 @@ def _cluster_worker(rank, world, port, tmp, q):
             db = await Database.create(path=os.path.join(tmp, f'r{rank}', 'l.sqlite3'), utxo_backend='host')
             if rank != 0:
                 await cluster.follower_main(c, db)
+                from upow_amd.ledger import lean
+                assert db.lean  # a lean replica: its SQL tables are materialised from its op log (promotion)
+                await lean.materialise(db)
             else:
                 await cluster.leader_start(db)
                 verdicts, errors = [], []

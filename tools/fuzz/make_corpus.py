@@ -72,8 +72,27 @@ def tx_seeds():
     return out
 
 
+def json_seeds(tx_hexes):
+    """Request and page bodies the span parser sees (csrc/jsonspan.cpp): /push_block bodies, /get_blocks
+    pages, and JSON outside the plain subset (escapes, UTF-8, numbers, nesting, duplicate keys)."""
+    import json
+    hexes = [h[1:].hex() if h[:1] == b'\x00' else None for h in tx_hexes]
+    hexes = [h for h in hexes if h]
+    push = {'block_content': 'ab' * 108, 'txs': hexes, 'block_no': 7}
+    page = {'ok': True, 'result': [{'block': {'id': 5, 'hash': 'cd' * 32, 'content': 'ef' * 108, 'address': 'D' * 45,
+                                              'random': 0, 'difficulty': 6.3, 'reward': 6.0, 'timestamp': 1700000000},
+                                    'transactions': hexes[:3]}, {'block': {'id': 6}, 'transactions': []}]}
+    docs = [json.dumps(push).encode(), json.dumps(push, separators=(',', ':')).encode(), json.dumps(page).encode(),
+            json.dumps(page, indent=2).encode(), b'{"txs": ["ab", "c\\"d"], "txs": ["x"]}',
+            '{"k": "\u00e9\u2603", "txs": ["\u00e9"], "n": [-0.0, 1e400, 12345678901234567890, 1E-5]}'.encode(),
+            b'[[[[[[{"transactions": [ ]}]]]]]]', b' {"a":true,"b":false,"c":null} ', b'{"txs": "ab"}',
+            b'{"txs": [1, "a"]}', b'"\\ud800"', b'{"transactions": ["a" ,"b" , "c"]}']
+    return docs
+
+
 def main(out_dir):
-    for name, seeds in (('http', http_seeds()), ('tx', tx_seeds())):
+    tx = tx_seeds()
+    for name, seeds in (('http', http_seeds()), ('tx', tx), ('json', json_seeds(tx))):
         d = os.path.join(out_dir, name)
         os.makedirs(d, exist_ok=True)
         for k, s in enumerate(seeds):

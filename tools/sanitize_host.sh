@@ -8,7 +8,11 @@
 # 2. libFuzzer + ASan + UBSan on the parsers of untrusted network input: the tx decoder every pushed tx and
 #    every peer block goes through (csrc/txdecode.h, tools/fuzz/fuzz_txdecode.cpp) and the HTTP/1.1 +
 #    WebSocket framing of every request (csrc/http_wire.h, tools/fuzz/fuzz_http.cpp), seeded with valid
-#    txs / requests / frames (tools/fuzz/make_corpus.py). ASan's global redzones are off for these builds
+#    txs / requests / frames (tools/fuzz/make_corpus.py); and the span JSON parser of every /push_block body
+#    and /get_blocks page (csrc/jsonspan.cpp, tools/fuzz/fuzz_jsonspan.cpp: an embedded interpreter, every
+#    accepted input checked against json.loads), seeded with the committed corpus tools/fuzz/corpus/jsonspan
+#    plus generated bodies, run for FUZZ_JSONSPAN_RUNS executions (default 10 M) over FUZZ_JOBS forked
+#    workers. ASan's global redzones are off for these builds
 #    (-mllvm -asan-globals=0): the fuzzer runtime and the target register some header-defined globals
 #    twice, which ASan reports as an ODR violation before the first input.
 # 3. The whole native extension built instrumented (python -m upow_amd._build --variant asan|tsan) and
@@ -67,6 +71,11 @@ fi
 if stale "$OUT/fuzz_txdecode" tools/fuzz/fuzz_txdecode.cpp csrc/txdecode.h csrc/base58.cpp csrc/sha256_host.cpp $HDRS; then
   $CXX $FZ tools/fuzz/fuzz_txdecode.cpp csrc/base58.cpp csrc/sha256_ni.cpp csrc/sha256_host.cpp -pthread -o "$OUT/fuzz_txdecode"
 fi
+PYINC=$(python3 -c 'import sysconfig; print(sysconfig.get_paths()["include"])')
+PBINC=$(python3 -c 'import pybind11; print(pybind11.get_include())')
+if stale "$OUT/fuzz_jsonspan" tools/fuzz/fuzz_jsonspan.cpp csrc/jsonspan.cpp; then
+  $CXX $FZ -I"$PYINC" -I"$PBINC" tools/fuzz/fuzz_jsonspan.cpp -L/usr/lib/x86_64-linux-gnu -lpython3.10 -o "$OUT/fuzz_jsonspan"
+fi
 UPOW_NO_TORCH=1 python3 tools/fuzz/make_corpus.py "$OUT/corpus" > /dev/null
 for t in http txdecode; do
   seeds=$OUT/corpus/${t#txdecode}; [ "$t" = txdecode ] && seeds=$OUT/corpus/tx
@@ -75,6 +84,19 @@ for t in http txdecode; do
     || { tail -40 "$OUT/fuzz_$t.log"; exit 1; }
   echo "fuzz $t: $(grep -E '^Done [0-9]+ runs' "$OUT/fuzz_$t.log") (corpus $(ls "$OUT/work_$t" | wc -l) inputs, no crash)"
 done
+# the span parser: a run-count target over forked workers (each execution calls into the interpreter, ~5 k/s
+# per worker); the committed corpus grows by what this run finds (merged, minimised: -merge=1)
+RUNS=${FUZZ_JSONSPAN_RUNS:-10000000}
+JOBS=${FUZZ_JOBS:-8}
+mkdir -p "$OUT/work_jsonspan"
+(cd "$OUT" && PYTHONMALLOC=malloc ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 \
+  ./fuzz_jsonspan -fork="$JOBS" -runs="$RUNS" -ignore_crashes=0 -print_final_stats=1 work_jsonspan \
+  "$ROOT/tools/fuzz/corpus/jsonspan" "$ROOT/$OUT/corpus/json" > fuzz_jsonspan.log 2>&1) \
+  || { tail -40 "$OUT/fuzz_jsonspan.log"; exit 1; }
+echo "fuzz jsonspan: $(grep -cE '^#[0-9]+: cov' "$OUT/fuzz_jsonspan.log") fork rounds, $(grep -oE 'exec/s: [0-9]+' "$OUT/fuzz_jsonspan.log" | tail -1), no crash, no json.loads difference"
+if [ -n "${FUZZ_MERGE:-}" ]; then  # fold what the run found into the committed corpus
+  (cd "$OUT" && ./fuzz_jsonspan -merge=1 "$ROOT/tools/fuzz/corpus/jsonspan" work_jsonspan > fuzz_jsonspan_merge.log 2>&1)
+fi
 
 echo "== [3] the native extension instrumented, its Python tests under ASan + UBSan and TSan"
 python3 -m upow_amd._build --variant asan -j 8 > /dev/null

@@ -1026,7 +1026,14 @@ async def _run_cluster_sync(args, ctx, device, utxo_backend):
     c = cluster.init(ctx)
     per_page = max(1, int(getattr(args, 'sync_page_blocks', 1000) or 1000))
     if not c.leader:
+        fprof = None
+        if os.environ.get('UPOW_BENCH_PROFILE_FOLLOWER') and ctx.rank == 1:  # cProfile of one follower's op loop
+            import cProfile
+            fprof = cProfile.Profile()
+            fprof.enable()
         await cluster.follower_main(c, dst)
+        if fprof is not None:
+            _dump_profile(fprof, os.environ['UPOW_BENCH_PROFILE_FOLLOWER'])
         wall = ctx.allreduce_max_f(0.0)
         st = None
     else:
@@ -1035,7 +1042,7 @@ async def _run_cluster_sync(args, ctx, device, utxo_backend):
         if args.warmup and not await create_blocks(page[:args.warmup]):
             raise RuntimeError('cluster sync warmup rejected')
         c.send('status')
-        c.status(dst)
+        st0 = c.status(dst)  # every replica's process CPU seconds at the start of the timed region
         prof = None
         if os.environ.get('UPOW_BENCH_PROFILE'):  # cProfile of the leader's timed sync (text report)
             import cProfile
@@ -1059,15 +1066,32 @@ async def _run_cluster_sync(args, ctx, device, utxo_backend):
         wall = ctx.allreduce_max_f(wall)
         if any((s['height'], s['utxo_hash']) != (st[0]['height'], st[0]['utxo_hash']) for s in st):
             raise RuntimeError(f'cluster sync: replicas diverged: {st}')
+        # host CPU per synced block of every replica (process time of all its threads over the timed region)
+        rank_cpu = [round((b['cpu_s'] - a['cpu_s']) * 1000 / max(1, args.steps), 3) for a, b in zip(st0, st)]
+        # the same without the page plans' P-256 work (key decompression, curve checks, the rank's verify shard):
+        # host CPU on a CPU-only node, GPU kernels on an MI355X node
+        ex = [round(c - (b['crypto_cpu_s'] - a['crypto_cpu_s']) * 1000 / max(1, args.steps), 3)
+              for c, a, b in zip(rank_cpu, st0, st)]
+        many = len(st) > 1
+        cpu = {'rank_cpu_ms_per_block': rank_cpu, 'rank_cpu_ms_per_block_ex_p256': ex,
+               'lean_followers': all(s['lean'] for s in st[1:]) if many else None,
+               'follower_cpu_vs_leader': round(max(rank_cpu[1:]) / rank_cpu[0], 3) if many and rank_cpu[0] else None,
+               'follower_cpu_vs_leader_ex_p256': round(max(ex[1:]) / ex[0], 3) if many and ex[0] > 0 else None}
     info = c.info()
     cluster.init(type(ctx)())  # a world-1 context: no cluster
     dst.close()
     return sum(counts[args.warmup:]), wall, {
         'blocks_per_s': round(args.steps / wall, 1), 'tx_counts': _counts_label(args, counts[args.warmup:]),
         'blocks_per_page': per_page, 'sync_path': 'page', 'op_stream': info,
-        'threads_cpu': threads_cpu if c.leader else None,
+        'threads_cpu': threads_cpu if c.leader else None, **(cpu if c.leader else {}),
         'page': {k: (round(v, 4) if isinstance(v, float) else v) for k, v in pagesync.stats.items()},
         'replicas': [{'rank': x['rank'], 'height': x['height'], 'utxo_hash': x['utxo_hash']} for x in st] if st else None}
+
+
+def _gpus_used(ctx) -> int:
+    """Distinct GPUs under the job's ranks (a multi-rank cluster may share one GPU over host collectives)."""
+    import torch
+    return min(ctx.world, max(1, torch.cuda.device_count()))
 
 
 def run_cluster_sync_bench(args, ctx):
@@ -1080,7 +1104,7 @@ def run_cluster_sync_bench(args, ctx):
         'metric': 'sync_tx_per_s',
         'value': round(txs / wall, 1),
         'unit': 'tx/s',
-        'n_gpus': ctx.world if device == 'gpu' else 0,
+        'n_gpus': _gpus_used(ctx) if device == 'gpu' else 0,
         'world': ctx.world,
         'steps': args.steps,
         'warmup': args.warmup,

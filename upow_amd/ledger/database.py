@@ -117,14 +117,6 @@ for _t in OUTPUT_TABLES[1:]:
 _SQL_READERS = None  # Database._off_loop
 
 
-class _Pre:
-    """A block statement encoded before the block's verdict (:meth:`Database.prepare_native_block`)."""
-    __slots__ = ('enc',)
-
-    def __init__(self, enc):
-        self.enc = enc
-
-
 def _commit_point():
     """On a cluster node, the block's agree-before-commit vote resolves here, right before its journal write
     (parallel/cluster.py ``commit_point``); raises when a replica is not ready."""
@@ -436,6 +428,13 @@ class Database:
         self._genesis_cache: Optional[str] = None
         self._pending_empty: Optional[bool] = None
         self._mempool_ver = 0
+        # lean cluster follower (ledger/lean.py): blocks go to the HBM/governance/mempool indexes, the chain-tip
+        # header rows below and the op log, not to SQL; _lean_tip is the tip row while lean
+        self.lean = False
+        self.lean_log = None
+        self._lean_rows: Dict[int, dict] = {}
+        self._lean_by_hash: Dict[str, int] = {}
+        self._lean_tip: Optional[dict] = None
         self.on_admit = None  # cluster leader: row hook of every admission (parallel/cluster.py)
         self.on_confirm = None  # cluster leader: hook (index, hit txs, hit inputs) of a block's mempool confirm
         self._mp: Optional[MempoolIndex] = None  # ledger/mempool.py; None: (re)load from SQL on next use
@@ -676,7 +675,7 @@ class Database:
         return Database.instance
 
     def _tip_id(self) -> int:
-        tip = self._tip_cache
+        tip = self._lean_tip if self._lean_tip is not None else self._tip_cache
         if tip is not None:
             return int(tip['id'])
         row = self._q1('SELECT MAX(id) FROM blocks')
@@ -719,6 +718,8 @@ class Database:
         self._ckpt_thread.start()
 
     def close(self):
+        if self.lean_log is not None:
+            self.lean_log.close()
         if self._ckpt_stop is not None:
             self._ckpt_stop.set()
             self._ckpt_thread.join(timeout=10)
@@ -1013,8 +1014,8 @@ class Database:
         """:meth:`encode` of a block's statements, the large ones concurrently: each encode copies its
         columns with the GIL released, so a block's ~4 multi-MB statements (tx rows, UTXO rows, spends,
         address rows) are copied on pool threads side by side instead of one after another."""
-        out = [st.enc if isinstance(st, _Pre) else None for st in stmts]  # encoded ahead of the verdict
-        todo = [k for k, st in enumerate(stmts) if not isinstance(st, _Pre)]
+        out = [None] * len(stmts)
+        todo = list(range(len(stmts)))
         big = [k for k in todo if stmts[k][2] >= 1024]
         if len(big) < 2 or _ENCODE_THREADS < 2:
             for k in todo:
@@ -1896,6 +1897,8 @@ class Database:
     def _last_block_row(self) -> Optional[dict]:
         """The tip row, from the chain-tip cache the native block path keeps (no wait for the SQL
         materialiser) or from SQL."""
+        if self._lean_tip is not None:
+            return dict(self._lean_tip)
         tip = self._tip_cache
         if tip is None:
             gen = self._tip_gen
@@ -1912,6 +1915,8 @@ class Database:
         return (tip['id'] if tip is not None else 0) + 1
 
     async def get_block(self, block_hash: str) -> Optional[dict]:
+        if block_hash in self._lean_by_hash:
+            return dict(self._lean_rows[self._lean_by_hash[block_hash]])
         return self._block_row(self._q1('SELECT * FROM blocks WHERE hash = ?', (block_hash,)))
 
     async def get_blocks(self, offset: int, limit: int, tx_details: bool = False) -> list:
@@ -1937,10 +1942,23 @@ class Database:
 
     async def get_block_by_id(self, block_id: int) -> Optional[dict]:
         # calculate_difficulty passes `id - BLOCKS_COUNT + 1` as a Decimal (manager.py:95-97)
+        row = self._lean_rows.get(int(block_id))
+        if row is not None:
+            return dict(row)
         tip = self._tip_cache
         if tip is not None and tip['id'] == int(block_id):
             return dict(tip)
         return self._block_row(self._q1('SELECT * FROM blocks WHERE id = ?', (int(block_id),)))
+
+    def block_hash_at(self, block_id: int) -> Optional[str]:
+        """The hash of block ``block_id`` (lean header rows first, then SQL); None when there is none."""
+        if not block_id:
+            return None
+        row = self._lean_rows.get(int(block_id))
+        if row is not None:
+            return row['hash']
+        r = self._q1('SELECT hash FROM blocks WHERE id = ?', (int(block_id),))
+        return r[0] if r else None
 
     def block_tx_hexes(self, block_hash: str) -> List[str]:
         """The block's tx hex strings in block order (synchronous: callable from a worker thread)."""
@@ -2014,77 +2032,10 @@ class Database:
                                            'EXISTS(SELECT 1 FROM pending_spent_outputs)')[0] == 0
         return self._pending_empty
 
-    def prepare_native_block(self, block_hash: str, block_id: int, n: int, tx_cols: list, out_cols: tuple,
-                             in_keys: np.ndarray, addr_pairs: Optional[tuple], outputs: Optional[dict] = None) -> dict:
-        """The part of :meth:`apply_native_block` that does not depend on the block's verdict, its reward or the
-        mempool, for a block without governance txs: the index records of its outputs and spends, its row
-        ids, and its four large statements (tx rows, UTXO inserts, UTXO deletes, the txs' address rows)
-        encoded. The native block path runs it while the GPU verifies the block's signatures; a block that is
-        then rejected hands its row ids back (:meth:`release_prepared`). ``outputs``: the
-        :meth:`prepare_native_outputs` half, computed ahead on another thread."""
-        pre = outputs if outputs is not None else self.prepare_native_outputs(out_cols, in_keys)
-        tx_start = self._tx_rowids(n + 1)
-        names, stmts = ['tx'], [(self._TX_INSERT, [tx_cols[0], block_hash, *tx_cols[1:],
-                                                   np.arange(tx_start + 1, tx_start + 1 + n, dtype=np.int64)],
-                                 n, None, None, None)]
-        if addr_pairs is not None:
-            ab, ao, at = addr_pairs
-            rows = self._address_index_stmts(block_hash, int(block_id), [
-                (('arena', ab, ao), ('hex32', tx_cols[0][1], 32, 0, np.frombuffer(at, dtype=np.int64)), len(at) // 8)])
-            if len(rows) == 2:  # inline address index on: the txs' rows (the watermark is built at commit)
-                names.append('addr')
-                stmts.append(rows[0])
-        pre['enc'].update(zip(names, self.encode_many(stmts)))
-        pre['tx_base'] = tx_start
-        pre['rowids'] = (tx_start, tx_start + n + 1, *pre['rowids'][2:])
-        return pre
-
-    def prepare_native_outputs(self, out_cols: tuple, in_keys: np.ndarray) -> dict:
-        """The half of :meth:`prepare_native_block` that needs neither the block's hash nor its apply strings:
-        index records, UTXO row ids, and the UTXO insert and delete statements encoded."""
-        from ..ops.native import lib
-        out_index, out_addr_spec, out_txid, out_amount, out_addr, out_len = out_cols
-        n_out, n_in = len(out_index), len(in_keys)
-        tag_u = TAG_BY_TABLE['unspent_outputs']
-        rb, pb = lib().output_index_records(
-            np.ascontiguousarray(out_txid, dtype=np.uint8), np.ascontiguousarray(out_index, dtype=np.int64),
-            np.full(n_out, tag_u, dtype=np.uint32), np.ascontiguousarray(out_amount, dtype=np.uint64),
-            np.ascontiguousarray(out_addr, dtype=np.uint8), np.ascontiguousarray(out_len, dtype=np.uint8),
-            np.zeros(0, np.uint8))
-        in_keys = np.ascontiguousarray(in_keys, dtype=np.uint8).reshape(-1, 40)
-        sb, ib = lib().spent_index_records(in_keys, np.full(n_in, tag_u, dtype=np.uint32))
-        in_idx = np.frombuffer(ib, dtype=np.int64)
-        utxo_start = self._utxo_rowids(n_out)
-        names, stmts = [], []
-        if n_out:
-            names.append('utxo_ins')
-            stmts.append(('INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake, rowid) VALUES (?, ?, ?, ?, ?)',
-                          [('hex32', np.ascontiguousarray(out_txid), 32, 0), np.ascontiguousarray(out_index, dtype=np.int64),
-                           out_addr_spec, 0, np.arange(utxo_start, utxo_start + n_out, dtype=np.int64)],
-                          n_out, None, None, None))
-        if n_in:
-            names.append('utxo_del')
-            stmts.append(('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
-                          [('hex32', in_keys, 40, 0), in_idx], n_in, 'key', None, n_in))
-        return {'recs': np.frombuffer(rb, dtype=np.uint8).reshape(-1, 40), 'pay': np.frombuffer(pb, dtype=PAYLOAD_DTYPE),
-                'spent': np.frombuffer(sb, dtype=np.uint8).reshape(-1, 40), 'in_idx': in_idx,
-                'rowids': (None, None, utxo_start, utxo_start + n_out),
-                'enc': dict(zip(names, [self.encode(*st) for st in stmts]))}
-
-    def release_prepared(self, pre: dict):
-        """A prepared block that was not applied: its row ids go back when nothing was allocated after them
-        (the ledger lock is held from prepare to here, so nothing was)."""
-        t0, t1, u0, u1 = pre['rowids']
-        with self._seq_lock:
-            if t1 is not None and self._tx_next_rowid == t1:
-                self._tx_next_rowid = t0
-            if self._utxo_next_rowid == u1:
-                self._utxo_next_rowid = u0
-
     def apply_native_block(self, block_row: dict, coinbase_row: tuple, coinbase_outputs: list, n: int,
                            tx_cols: list, out_cols: tuple, in_keys: np.ndarray, spent_payload: np.ndarray,
                            gov: Optional[dict] = None, addr_pairs: Optional[tuple] = None,
-                           cb_index: Optional[tuple] = None, pre: Optional[dict] = None) -> int:
+                           cb_index: Optional[tuple] = None) -> int:
         """The ledger writes of one native-path block (reference manager.py:706-730: add_block,
         add_transaction(coinbase), add_transactions, add_transaction_outputs, remove_pending_transactions,
         remove_outputs, remove_pending_spent_outputs) as ONE journal batch, plus the HBM index update.
@@ -2099,8 +2050,6 @@ class Database:
         governance index follows from these columns — the object path's write set (apply_object_block) in
         the same statement order, so both paths leave identical tables.
         ``cb_index``: the coinbase outputs' index (records, payloads) when already built (a sync page's plan).
-        ``pre``: :meth:`prepare_native_block` of this block (index records, row ids and the large statements
-        encoded while the GPU verified it).
         Returns the journal sequence number (0 without the native writer: written synchronously)."""
         ts = [perf_counter()]  # stage clock: records, statements, encode, journal, index, mempool, governance
         names = ('apply:records', 'apply:stmts', 'apply:encode', 'apply:journal', 'apply:index', 'apply:mempool',
@@ -2118,19 +2067,14 @@ class Database:
         out_tag = gov['out_tag'] if gov is not None else np.full(n_out, tag_u, dtype=np.uint32)
         # ---- index records: created outputs (block txs + coinbase) and spent inputs
         from ..ops.native import lib
-        if pre is not None and (gov is not None or self.writer is None):
-            raise ValueError('a prepared block has no governance txs and goes through the journal')
-        if pre is not None:
-            recs, pay = pre['recs'], pre['pay']
-        else:
-            stake = (np.asarray(gov['out_type']) == int(OutputType.STAKE)).astype(np.uint8) if gov is not None \
-                else np.zeros(0, np.uint8)
-            rb, pb = lib().output_index_records(
-                np.ascontiguousarray(out_txid, dtype=np.uint8), np.ascontiguousarray(out_index, dtype=np.int64),
-                np.ascontiguousarray(out_tag, dtype=np.uint32), np.ascontiguousarray(out_amount, dtype=np.uint64),
-                np.ascontiguousarray(out_addr, dtype=np.uint8), np.ascontiguousarray(out_len, dtype=np.uint8), stake)
-            recs = np.frombuffer(rb, dtype=np.uint8).reshape(-1, 40)
-            pay = np.frombuffer(pb, dtype=PAYLOAD_DTYPE)
+        stake = (np.asarray(gov['out_type']) == int(OutputType.STAKE)).astype(np.uint8) if gov is not None \
+            else np.zeros(0, np.uint8)
+        rb, pb = lib().output_index_records(
+            np.ascontiguousarray(out_txid, dtype=np.uint8), np.ascontiguousarray(out_index, dtype=np.int64),
+            np.ascontiguousarray(out_tag, dtype=np.uint32), np.ascontiguousarray(out_amount, dtype=np.uint64),
+            np.ascontiguousarray(out_addr, dtype=np.uint8), np.ascontiguousarray(out_len, dtype=np.uint8), stake)
+        recs = np.frombuffer(rb, dtype=np.uint8).reshape(-1, 40)
+        pay = np.frombuffer(pb, dtype=PAYLOAD_DTYPE)
         from .utxo import pack_records
         cb_keys = [(o[0], o[1]) for o in coinbase_outputs]
         if cb_index is not None:  # (records, payloads) of the coinbase outputs, built by a sync page's plan
@@ -2141,12 +2085,9 @@ class Database:
                                   [bool(o[3]) for o in coinbase_outputs])
         in_keys = np.ascontiguousarray(in_keys, dtype=np.uint8).reshape(-1, 40)
         in_tag = gov['in_tag'].astype(np.uint32) if gov is not None else np.full(n_in, tag_u, dtype=np.uint32)
-        if pre is not None:
-            spent, in_idx = pre['spent'], pre['in_idx']
-        else:
-            sb, ib = lib().spent_index_records(in_keys, np.ascontiguousarray(in_tag, dtype=np.uint32))
-            spent = np.frombuffer(sb, dtype=np.uint8).reshape(-1, 40)
-            in_idx = np.frombuffer(ib, dtype=np.int64)
+        sb, ib = lib().spent_index_records(in_keys, np.ascontiguousarray(in_tag, dtype=np.uint32))
+        spent = np.frombuffer(sb, dtype=np.uint8).reshape(-1, 40)
+        in_idx = np.frombuffer(ib, dtype=np.int64)
         # the spends' key order (B-tree locality) is computed by the materialiser ('key': a stable sort of the
         # statement's rows by the leading 8 bytes of column 0, so a row selection keeps the global key order)
         in_order = 'key'
@@ -2155,7 +2096,7 @@ class Database:
         # ---- statements (schema.sql write set of one block)
         b = block_row
         # the coinbase row first, then the block's txs (insertion order)
-        tx_base = pre['tx_base'] if pre is not None else self._tx_rowids(n + 1)
+        tx_base = self._tx_rowids(n + 1)
         stmts = [
             ('INSERT INTO blocks (id, hash, content, address, random, difficulty, reward, timestamp) '
              'VALUES (?, ?, ?, ?, ?, ?, ?, ?)',
@@ -2164,19 +2105,12 @@ class Database:
             (self._TX_INSERT, [coinbase_row[1], coinbase_row[0], *coinbase_row[2:], tx_base], 1, None, None, None),
         ]
         self.checkpoint('block')
-        if pre is not None:
-            stmts.append(_Pre(pre['enc']['tx']))
-        else:
-            stmts.append((self._TX_INSERT, [tx_cols[0], b['hash'], *tx_cols[1:],
-                                            np.arange(tx_base + 1, tx_base + 1 + n, dtype=np.int64)], n, None, None,
-                          None))
+        stmts.append((self._TX_INSERT, [tx_cols[0], b['hash'], *tx_cols[1:],
+                                        np.arange(tx_base + 1, tx_base + 1 + n, dtype=np.int64)], n, None, None, None))
         self.checkpoint('transactions')
         # explicit row ids from the ledger-wide counter: the rows land in several files (see UTXO_FILES_DEFAULT)
         ins_u = 'INSERT INTO unspent_outputs (tx_hash, "index", address, is_stake, rowid) VALUES (?, ?, ?, ?, ?)'
-        if pre is not None:
-            if n_out:
-                stmts.append(_Pre(pre['enc']['utxo_ins']))
-        elif gov is None:
+        if gov is None:
             if n_out:
                 base = self._utxo_rowids(n_out)
                 stmts.append((ins_u, [('hex32', np.ascontiguousarray(out_txid), 32, 0),
@@ -2233,9 +2167,7 @@ class Database:
         if 'inode_registration_output' in gov_spent:
             spend_stmt('inode_registration_output')
         sel_u = np.nonzero(in_tag == tag_u)[0] if gov is not None else None
-        if pre is not None and n_in:
-            stmts.append(_Pre(pre['enc']['utxo_del']))
-        elif gov is None and n_in:
+        if gov is None and n_in:
             stmts.append(('DELETE FROM unspent_outputs WHERE tx_hash = ? AND "index" = ?',
                           [('hex32', in_keys, 40, 0), in_idx], n_in, in_order, None, n_in))
         elif gov is not None and len(sel_u):
@@ -2254,13 +2186,11 @@ class Database:
         # address index rows: the coinbase's, then the txs' (txcodec.address_pairs: blob, offsets, tx index)
         ca, ch = self.address_rows([coinbase_row])
         parts = [(ca, ch, len(ca))]
-        if addr_pairs is not None and pre is None:
+        if addr_pairs is not None:
             ab, ao, at = addr_pairs
             parts.append((('arena', ab, ao), ('hex32', tx_cols[0][1], 32, 0, np.frombuffer(at, dtype=np.int64)),
                           len(at) // 8))
         addr_stmts = self._address_index_stmts(b['hash'], int(b['id']), parts)
-        if pre is not None and pre['enc'].get('addr') is not None and addr_stmts:
-            addr_stmts.insert(len(addr_stmts) - 1, _Pre(pre['enc']['addr']))  # the txs' rows, then the watermark
         stmts.extend(addr_stmts)
         tables |= {'address_transactions', 'address_index_state'}
 
@@ -2338,6 +2268,116 @@ class Database:
         self.last_apply_stages = dict(zip(('ap_records_s', 'ap_stmts_s', 'ap_encode_s', 'ap_journal_s', 'ap_index_s',
                                            'ap_mempool_s', 'ap_gov_s'), np.diff(ts).tolist()))
         return seq
+
+    # ------------------------------------------------------------------ lean replica (ledger/lean.py)
+    def enter_lean(self):
+        """From now on blocks are applied lean (:meth:`apply_lean_block`): indexes, tip rows and the op log
+        only. The SQL tables stay where they are until ``lean.materialise``."""
+        from . import lean
+        lean.open_log(self)
+        self.flush()  # the tables hold every record journaled so far: lean blocks come after them
+        self.lean = True
+
+    def leave_lean(self):
+        """Back to the SQL state: drop the lean tip rows and rebuild the HBM and governance indexes from the
+        tables (a snapshot of exactly that state when one is there). ``lean.materialise`` then replays the op
+        log on top of it."""
+        self.utxo.settle()
+        self.lean = False
+        self._lean_rows.clear()
+        self._lean_by_hash.clear()
+        self._lean_tip = None
+        self._invalidate_for(None)
+        from . import manager
+        manager.Manager.difficulty = None
+        restored = False
+        if self.path != ':memory:' and os.environ.get('UPOW_SNAPSHOT', '1') != '0':
+            from . import snapshot
+            restored = snapshot.try_restore(self)
+        if not restored:
+            self._rebuild_utxo_index()
+        if self.gov is not None:
+            self.gov.rebuild()
+
+    def apply_lean_block(self, block_row: dict, coinbase_outputs: list, n: int, out_cols: tuple,
+                         in_keys: np.ndarray, spent_payload: np.ndarray, txids: np.ndarray,
+                         gov: Optional[dict] = None, cb_index: Optional[tuple] = None) -> int:
+        """A lean follower's block apply (ledger/lean.py): what :meth:`apply_native_block` does to the indexes
+        and the chain tip — the same index records (outputs, coinbase outputs, spends with their payloads),
+        the same mempool confirm (its SQL deletes journaled: the pending tables stay the index's), the same
+        governance-index update — and no block statements, no journal record, no SQL materialisation.
+        The commit point (the cluster's vote) is where the journal write would be. Returns 0."""
+        from ..ops.native import lib
+        from .utxo import pack_records
+        ts = [perf_counter()]
+        out_index, out_addr_spec, out_txid, out_amount, out_addr, out_len = out_cols
+        n_out, n_in = len(out_index), len(in_keys)
+        tag_u = TAG_BY_TABLE['unspent_outputs']
+        out_tag = gov['out_tag'] if gov is not None else np.full(n_out, tag_u, dtype=np.uint32)
+        stake = (np.asarray(gov['out_type']) == int(OutputType.STAKE)).astype(np.uint8) if gov is not None \
+            else np.zeros(0, np.uint8)
+        rb, pb = lib().output_index_records(
+            np.ascontiguousarray(out_txid, dtype=np.uint8), np.ascontiguousarray(out_index, dtype=np.int64),
+            np.ascontiguousarray(out_tag, dtype=np.uint32), np.ascontiguousarray(out_amount, dtype=np.uint64),
+            np.ascontiguousarray(out_addr, dtype=np.uint8), np.ascontiguousarray(out_len, dtype=np.uint8), stake)
+        recs = np.frombuffer(rb, dtype=np.uint8).reshape(-1, 40)
+        pay = np.frombuffer(pb, dtype=PAYLOAD_DTYPE)
+        if cb_index is not None:
+            cb_recs, cb_pay = cb_index
+        else:
+            cb_recs = pack_records([(o[0], o[1]) for o in coinbase_outputs], tag_u)
+            cb_pay = make_payload([o[4] for o in coinbase_outputs], [_addr_bytes(o[2]) for o in coinbase_outputs],
+                                  [bool(o[3]) for o in coinbase_outputs])
+        in_keys = np.ascontiguousarray(in_keys, dtype=np.uint8).reshape(-1, 40)
+        in_tag = gov['in_tag'].astype(np.uint32) if gov is not None else np.full(n_in, tag_u, dtype=np.uint32)
+        sb, _ = lib().spent_index_records(in_keys, np.ascontiguousarray(in_tag, dtype=np.uint32))
+        spent = np.frombuffer(sb, dtype=np.uint8).reshape(-1, 40)
+        ts.append(perf_counter())
+        _commit_point()
+        ts.append(perf_counter())
+        if self.utxo_defer:
+            self.utxo.defer_block([(recs, pay), (cb_recs, cb_pay)], spent if n_in else spent[:0])
+        else:
+            self.utxo.apply_block([(recs, pay), (cb_recs, cb_pay)], spent if n_in else spent[:0])
+        b = block_row
+        tip = dict(b)
+        tip['difficulty'], tip['reward'] = Decimal(tip['difficulty']), Decimal(tip['reward'])
+        tip = normalize_block(tip)
+        bid = int(b['id'])
+        self._lean_rows[bid] = tip
+        self._lean_by_hash[b['hash']] = bid
+        self._lean_tip = tip
+        self._tip_gen += 1
+        self._tip_cache = tip
+        ts.append(perf_counter())
+        if n:
+            self._mempool_confirm(False, txids=np.asarray(txids, np.uint8).reshape(-1, 32), in_keys=in_keys)
+        ts.append(perf_counter())
+        if self.gov is not None and gov is not None:
+            _, blob, off = out_addr_spec
+            off = np.frombuffer(off, dtype=np.int64) if isinstance(off, (bytes, bytearray)) else np.asarray(off, np.int64)
+            args = (np.ascontiguousarray(gov['out_type'], dtype=np.uint8), np.ascontiguousarray(txids),
+                    np.ascontiguousarray(gov['out_tx'], dtype=np.int32), np.ascontiguousarray(gov['out_start'], np.int32),
+                    np.ascontiguousarray(out_amount, dtype=np.uint64), np.ascontiguousarray(out_addr, dtype=np.uint8),
+                    np.ascontiguousarray(out_len, dtype=np.uint8), blob, np.ascontiguousarray(off),
+                    np.ascontiguousarray(gov['in_start'], np.int32), np.ascontiguousarray(spent_payload).view(np.uint8),
+                    in_keys, np.ascontiguousarray(gov['in_tag'], dtype=np.uint8), gov['in_str'][0],
+                    np.frombuffer(gov['in_str'][1], dtype=np.int64), n, int(b['timestamp']))
+            g = self.gov
+
+            def gov_apply():
+                g.store.apply_block(*args)
+                g.version += 1
+                g.inodes_with_power(False)
+            g.defer(gov_apply)
+        elif self.gov is not None and n_in:
+            hit = self._stake_spent(spent, spent_payload)
+            if hit:
+                self.gov.removed(STAKE, hit)
+        ts.append(perf_counter())
+        self.last_apply_stages = dict(zip(('ap_records_s', 'ap_vote_s', 'ap_index_s', 'ap_mempool_s', 'ap_gov_s'),
+                                          np.diff(ts).tolist()))
+        return 0
 
     def _stake_spent(self, spent: np.ndarray, spent_payload: np.ndarray) -> List[Tuple[str, int]]:
         """Which of a block's spent outpoints (n x 40 records) are staked outputs: the stake flag their index
@@ -2695,7 +2735,8 @@ class Database:
     SMALL_LOOKUP = 16
 
     def _filter_outputs(self, table: str, outputs):
-        if len(outputs) > self.SMALL_LOOKUP or self.utxo.backend_name != 'gpu' or not self._fresh(table):
+        if (self.lean or len(outputs) > self.SMALL_LOOKUP or self.utxo.backend_name != 'gpu'
+                or not self._fresh(table)):
             return self.utxo.filter(outputs, TAG_BY_TABLE[table])
         uniq = list(dict.fromkeys((h, int(i)) for h, i in outputs))
         found = set(self._select_outpoints(table, uniq))
@@ -3101,6 +3142,8 @@ class Database:
 
     # ------------------------------------------------------------------ inodes (database.py:1348-1438)
     async def get_genesis_block(self):
+        if self._genesis_cache is None and 1 in self._lean_rows:
+            return self._lean_rows[1]['content']
         if self._genesis_cache is None:
             r = self._q1('SELECT content FROM blocks WHERE id = 1')
             self._genesis_cache = r[0] if r else None

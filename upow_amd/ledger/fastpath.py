@@ -70,18 +70,6 @@ AMOUNT_LIMIT = 1 << 52  # > max supply in smallest units; keeps per-tx int64 sum
 _VERIFY_POOL = None
 
 
-_PREPARE_POOL = None
-
-
-def _prepare_pool():
-    """One helper thread for the verdict-independent half of a block's apply (UPOW_PRE_ENCODE=1)."""
-    global _PREPARE_POOL
-    if _PREPARE_POOL is None:
-        from concurrent.futures import ThreadPoolExecutor
-        _PREPARE_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix='upow-block-prepare')
-    return _PREPARE_POOL
-
-
 def _verify_pool():
     """One helper thread for the block's signature verify (overlapped with the apply strings)."""
     global _VERIFY_POOL
@@ -99,11 +87,6 @@ def _i32(d, k):
 # addresses are all 33-byte keys (UPOW_FUSED_VERIFY=0: the host key stage + separate verify, the A/B form)
 FUSED_VERIFY = os.environ.get('UPOW_FUSED_VERIFY', '1') != '0'
 _FUSED_HOST = os.environ.get('UPOW_FUSED_VERIFY') == 'host'  # the same stages on the host (CPU tests of this path)
-# UPOW_PRE_ENCODE=1: encode a block's large statements while its signatures verify instead of after the
-# verdict. Off by default: in three interleaved pairs on the GPU box the host work (apply strings + this,
-# ~2.8 ms) outlasted the GPU's ~1.4 ms, and the commit latency came out 9.1-9.5 ms against 8.8-8.9 without
-# it (profiles/r5/pre_encode_ab_r5zy/; with the UTXO half on a helper thread, profiles/r5/pre_encode_split_ab_r6a/)
-PRE_ENCODE = os.environ.get('UPOW_PRE_ENCODE', '0') == '1'
 
 
 def decode_raw(tx_hexes, threads: int) -> dict:
@@ -279,9 +262,14 @@ async def _create_block_from_hex(block_content: str, tx_hexes: List[str], error_
     dec = decoded if decoded is not None else (decode(tx_hexes) if tx_hexes else None)
     roctx.pop()
     timings['decode_s'] = perf_counter() - t0
+    from .database import Database
     if dec is None:
         last_path = 'object'
-        return await object_path(False)
+        if not Database.instance.lean:
+            return await object_path(False)
+        async with manager.ledger_lock():
+            await _leave_lean(Database.instance)
+            return await object_path(True)
     async with manager.ledger_lock():
         d0 = roctx.depth()
         try:
@@ -296,32 +284,24 @@ async def _create_block_from_hex(block_content: str, tx_hexes: List[str], error_
         last_path = 'native'
         if ok is None:
             last_path = 'object'
+            await _leave_lean(Database.instance)
             ok = await object_path(True)
         label = ('sync' if coinbase is not None else 'push') if last_path == 'object' else 'native'
         manager._record_block_metrics(ok, perf_counter() - t0, len(tx_hexes), label)
         return ok
 
 
+async def _leave_lean(db):
+    """The object path reads the SQL tables (inputs resolved from ``transactions``): a lean cluster follower
+    (ledger/lean.py) first brings them to its tip, and this block continues in full mode."""
+    if db.lean:
+        from . import lean
+        await lean.materialise(db, online=True)
+
+
 async def _create_block_fast(block_content: str, d: dict, error_list: list, last_block: Optional[dict],
                              t0: float, coinbase=None, page=None) -> Optional[bool]:
-    """True/False for a decided block; None = hand over to the object path. Row ids taken by a block prepared
-    ahead of its verdict (``prepare_native_block``) go back when the block is not applied."""
-    box = {}
-    try:
-        return await _create_block_fast_inner(block_content, d, error_list, last_block, t0, coinbase, page, box)
-    finally:
-        if 'pre_fut' in box:  # the helper's half, never joined (an error on the way): wait for it, then hand back
-            try:
-                box['pre'] = box.pop('pre_fut').result()
-            except Exception:
-                pass
-        if box.get('pre') is not None and not box.get('used'):
-            from .database import Database
-            Database.instance.release_prepared(box['pre'])
-
-
-async def _create_block_fast_inner(block_content: str, d: dict, error_list: list, last_block: Optional[dict],
-                                   t0: float, coinbase, page, box: dict) -> Optional[bool]:
+    """True/False for a decided block; None = hand over to the object path."""
     from . import manager, validate
     from .database import Database
     database: Database = Database.instance
@@ -471,22 +451,26 @@ async def _create_block_fast_inner(block_content: str, d: dict, error_list: list
             if n_jobs and pre_status is None and validate.overlappable(n_jobs) else None
     out_index = np.arange(len(out_tx), dtype=np.int64) - out_start[out_tx]
     out_cols = (out_index, ('arena', *d['out_addr_str']), txid[out_tx], out_amount, out_addr, out_len)
-    if PRE_ENCODE and vfut is not None and not bg.any and database.writer is not None:
-        # while the GPU verifies: the block's index records and UTXO statements on a helper thread, its tx and
-        # address statements on this one once the apply strings are rendered (prepare_native_block below)
-        box['pre_fut'] = _prepare_pool().submit(database.prepare_native_outputs, out_cols, in_keys)
+    lean = database.lean  # a lean cluster follower (ledger/lean.py): no SQL rows, so no apply strings
     try:
         # ---- columns for the ledger writes: views of the codec's buffers, encoded natively into one journal
         #      batch by csrc/ledger_writer.cpp (tx hashes rendered from the raw digests, text arenas for strings)
         roctx.push('apply:strings')
         ts0 = perf_counter()
         L = lib()
-        in_str = L.input_address_strings(np.ascontiguousarray(pay['addr']),
-                                         np.ascontiguousarray(pay['len'], dtype=np.uint8), d['in_start'], THREADS, True)
-        in_json = in_str[:2]
-        # the block's address_transactions rows (each tx's distinct input owners and output addresses)
-        addr_pairs = L.address_pairs(in_str[2], in_str[3], d['in_start'], *d['out_addr_str'], d['out_start'], THREADS)
-        fee_str = ('arena', *L.fee_strings(np.ascontiguousarray(fee, dtype=np.int64).tobytes()))
+        in_str = addr_pairs = tx_cols = None
+        if not lean or bg.any:  # a lean replica's governance index still takes the input owners' strings
+            in_str = L.input_address_strings(np.ascontiguousarray(pay['addr']),
+                                             np.ascontiguousarray(pay['len'], dtype=np.uint8), d['in_start'], THREADS,
+                                             True)
+        if not lean:
+            in_json = in_str[:2]
+            # the block's address_transactions rows (each tx's distinct input owners and output addresses)
+            addr_pairs = L.address_pairs(in_str[2], in_str[3], d['in_start'], *d['out_addr_str'], d['out_start'],
+                                         THREADS)
+            fee_str = ('arena', *L.fee_strings(np.ascontiguousarray(fee, dtype=np.int64).tobytes()))
+            tx_cols = [('hex32', txid, 32, 0), ('hexarena', *d['canon']), ('arena', *in_json),
+                       ('arena', *d['out_addr_json']), ('arena', *d['out_amount_json']), fee_str]
         gov_cols = None
         if bg.any:
             gov_cols = {'out_tag': bg.output_tags(TAG_BY_TABLE), 'out_type': out_type, 'in_tag': in_tag,
@@ -494,18 +478,6 @@ async def _create_block_fast_inner(block_content: str, d: dict, error_list: list
                         'in_str': in_str[2:]}
         strings_s = perf_counter() - ts0
         roctx.pop()
-        tx_cols = [('hex32', txid, 32, 0), ('hexarena', *d['canon']), ('arena', *in_json), ('arena', *d['out_addr_json']),
-                   ('arena', *d['out_amount_json']), fee_str]
-        if 'pre_fut' in box:
-            # the GPU is still verifying: the rest of the verdict-independent apply work now, not after the verdict
-            roctx.push('apply:prepare')
-            tp = perf_counter()
-            outputs = box.pop('pre_fut').result()
-            box['pre'] = outputs  # its row ids go back if what follows fails
-            box['pre'] = database.prepare_native_block(sha256(block_content), block_no, n, tx_cols, out_cols, in_keys,
-                                                       addr_pairs, outputs=outputs)
-            timings['prepare_s'] = perf_counter() - tp
-            roctx.pop()
     except BaseException:
         # no launch outlives this block, but the first error is the one that propagates: a failure of the
         # overlapped verify must not replace the apply-columns error being raised here
@@ -571,20 +543,20 @@ async def _create_block_fast_inner(block_content: str, d: dict, error_list: list
         block_row = {'id': block_no, 'hash': block_hash, 'content': block_content, 'address': address,
                      'random': int(random), 'difficulty': numeric(difficulty, 1),
                      'reward': numeric(block_reward + fees_total, 6), 'timestamp': int(content_time)}
-        cb_row = await database._tx_row(coinbase_transaction, block_hash)
         # a sync page's plan already split the trusted coinbase and built its index records (pagesync)
         pre_cb = coinbase_transaction.__dict__.get('_upow_cb_index')
         cb_outputs = pre_cb[0] if pre_cb else Database.split_outputs([coinbase_transaction])['unspent_outputs']
-        pre = box.get('pre')
-        if pre is not None and block_hash != sha256(block_content):
-            raise RuntimeError('prepared block statements for another block hash')
         submitted = database._submitted
-        box['used'] = True
         roctx.pop()
         try:
-            seq = database.apply_native_block(block_row, cb_row, cb_outputs, n, tx_cols, out_cols, in_keys, pay,
-                                              gov=gov_cols, addr_pairs=addr_pairs,
-                                              cb_index=pre_cb[1:] if pre_cb else None, pre=pre)
+            if lean:
+                seq = database.apply_lean_block(block_row, cb_outputs, n, out_cols, in_keys, pay, txid, gov=gov_cols,
+                                                cb_index=pre_cb[1:] if pre_cb else None)
+            else:
+                cb_row = await database._tx_row(coinbase_transaction, block_hash)
+                seq = database.apply_native_block(block_row, cb_row, cb_outputs, n, tx_cols, out_cols, in_keys, pay,
+                                                  gov=gov_cols, addr_pairs=addr_pairs,
+                                                  cb_index=pre_cb[1:] if pre_cb else None)
         except Exception as e:
             if database._submitted != submitted:
                 raise  # committed to the journal: a failure after the commit point is not a rejection

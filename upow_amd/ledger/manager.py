@@ -9,6 +9,7 @@ prefetches all point decompressions in one kernel, and still runs each tx's rule
 from __future__ import annotations
 
 import asyncio
+import contextvars
 import decimal
 import os
 import weakref
@@ -445,7 +446,37 @@ async def _apply_block(block_no, block_hash, block_content, address, random, dif
 _ledger_locks: 'weakref.WeakKeyDictionary' = weakref.WeakKeyDictionary()
 
 
-def ledger_lock() -> asyncio.Lock:
+_LOCK_OWNER: 'contextvars.ContextVar' = contextvars.ContextVar('upow_ledger_lock_owner', default=None)
+
+
+class _LedgerLock:
+    """``async with`` form of the loop's ledger lock, re-entrant for the task that holds it (a lean cluster
+    follower materialising its op log from inside a block's critical section, ledger/lean.py). Another task
+    — a child task included, which inherits the context — still waits for the lock."""
+    __slots__ = ('lk', 'token')
+
+    def __init__(self, lk: asyncio.Lock):
+        self.lk, self.token = lk, None
+
+    async def __aenter__(self):
+        me = asyncio.current_task()
+        if _LOCK_OWNER.get() is me and self.lk.locked():
+            return self
+        await self.lk.acquire()
+        self.token = _LOCK_OWNER.set(me)
+        return self
+
+    async def __aexit__(self, *exc):
+        if self.token is not None:
+            _LOCK_OWNER.reset(self.token)
+            self.token = None
+            self.lk.release()
+
+    def locked(self) -> bool:
+        return self.lk.locked()
+
+
+def ledger_lock() -> _LedgerLock:
     """One lock per event loop serialising every ledger mutation (block apply, rollback).
 
     The reference guards nothing: two concurrent ``/push_block`` calls can both pass ``check_block``
@@ -455,7 +486,7 @@ def ledger_lock() -> asyncio.Lock:
     lk = _ledger_locks.get(loop)
     if lk is None:
         lk = _ledger_locks[loop] = asyncio.Lock()
-    return lk
+    return _LedgerLock(lk)
 
 
 async def create_block(block_content: str, transactions: List[Transaction], last_block: dict = None,
@@ -563,7 +594,7 @@ async def _finalize_block(block_no: int, block_content: str, fees, n_txs: int, a
     roctx.push('finalize:post')
     logger.info(f'Added {n_txs} transactions in block {block_no}. Reward: {block_reward}, Fees: {fees} '
                 f'in {perf_counter() - create_start_time:.3f} seconds')
-    if block_no % 10 == 0:
+    if block_no % 10 == 0 and not database.lean:  # a lean follower leaves the K12 line to the leader
         await _log_utxo_hash(database, block_no)
     _maybe_snapshot(database, block_no)
     Manager.difficulty = None
@@ -614,7 +645,8 @@ SNAPSHOT_EVERY = int(os.environ.get('UPOW_SNAPSHOT_EVERY', '1000'))
 
 def _maybe_snapshot(database, block_no: int):
     """Periodic UTXO-index checkpoint (ledger/snapshot.py); never fails the block."""
-    if SNAPSHOT_EVERY <= 0 or block_no % SNAPSHOT_EVERY or database.path == ':memory:':
+    if SNAPSHOT_EVERY <= 0 or block_no % SNAPSHOT_EVERY or database.path == ':memory:' or database.lean:
+        # a lean follower's index is ahead of its SQL tables: a snapshot is taken of a materialised state only
         return
     try:
         from . import snapshot
@@ -672,7 +704,7 @@ async def _finalize_sync_block(block_no: int, block_content: str, fees, n_txs: i
         return False
     logger.info(f'Added {n_txs} transactions in block {block_no}. Reward: {block_reward}, Fees: {fees} '
                 f'in {perf_counter() - create_start_time:.3f} seconds')
-    if block_no % 10 == 0:
+    if block_no % 10 == 0 and not Database.instance.lean:
         await _log_utxo_hash(Database.instance, block_no)
     _maybe_snapshot(Database.instance, block_no)
     Manager.difficulty = None

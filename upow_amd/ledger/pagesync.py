@@ -35,7 +35,7 @@ from __future__ import annotations
 import asyncio
 import os
 from dataclasses import dataclass
-from time import perf_counter
+from time import perf_counter, process_time
 from typing import List, Optional
 
 import numpy as np
@@ -302,6 +302,7 @@ def build_plan(db, items: List[Item], cbs: list, ctx=None) -> List[Optional[Page
         return plan
     gpu_min = op.GPU_MIN_BATCH if gpu_available() else 1 << 62
     n_jobs = job_base
+    cpu0 = process_time()  # host CPU of the P-256 work (key decompression, curve checks, verify) of the plan
     if n_jobs or sum(len(x) for x in ol):
         kst, rec_bytes = lib().block_signer_records(
             np.ascontiguousarray(np.concatenate(pa)), np.concatenate(pl), np.ascontiguousarray(np.concatenate(oa)),
@@ -327,6 +328,7 @@ def build_plan(db, items: List[Item], cbs: list, ctx=None) -> List[Optional[Page
     else:
         status = op.verify_records(recs.reshape(-1))
     verify_s = perf_counter() - tv
+    stats['plan_crypto_cpu_s'] = stats.get('plan_crypto_cpu_s', 0.0) + (process_time() - cpu0)
     tags_u = np.full(ni, TAG_U, np.uint8)
     for k, j0, j1, a, b in per:
         plan[k] = PageBlock(tags=tags_u[a:b], pay=pay[a:b], fee=fees[k], n_jobs=j1 - j0,

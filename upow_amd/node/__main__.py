@@ -143,9 +143,12 @@ async def _follow(c):
     signal.signal(signal.SIGINT, lambda *_: None)
     db = await Database.create(path=follower_ledger_path(c.ctx.rank))
     try:
+        # a lean replica (ledger/lean.py) first materialises what its previous run logged
         await cluster.follower_main(c, db)
     finally:
-        if db.path != ':memory:' and os.environ.get('UPOW_SNAPSHOT', '1') != '0':
+        from ..ledger import lean
+        # a lean replica's index is ahead of its SQL tables: the next start materialises its op log instead
+        if db.path != ':memory:' and os.environ.get('UPOW_SNAPSHOT', '1') != '0' and not lean.pending(db):
             try:  # the next start restores the index from here instead of rebuilding it from SQL
                 from ..ledger import snapshot
                 snapshot.save(db)

@@ -210,6 +210,9 @@ async def startup():
     db = await Database.create(path=path)
     # block validation/apply and every cluster collective run on the ledger thread
     ledger_worker.start()
+    from ..ledger import lean
+    if lean.pending(db):  # a lean follower's ledger opened as this node's (promotion): its op log into SQL first
+        await on_ledger(lean.materialise, db)
     if cluster.get() is not None:  # multi-GPU node: the replicas get only what they lack (parallel/cluster.py)
         await on_ledger(cluster.leader_start, db)
     # what exists now (ledger caches, indexes, modules) lives for the process: keep it out of the

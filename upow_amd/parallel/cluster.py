@@ -113,6 +113,7 @@ class Cluster:
         n = int.from_bytes(raw[:4], 'little')
         msg = json.loads(raw[4:4 + n].decode())
         msg['_payload'] = raw[4 + n:]
+        msg['_raw'] = raw  # a lean follower logs the frame as it arrived (ledger/lean.py)
         self.ops_received += 1
         return msg
 
@@ -172,7 +173,10 @@ class Cluster:
         the long-timeout group: it may take longer than the op timeout on a big ledger)."""
         mine = {'rank': self.ctx.rank, 'height': db._tip_id(), 'tip_hash': _tip_hash(db),
                 'utxo_hash': db.utxo.set_hash(_utxo_tag()), 'utxo_entries': len(db.utxo),
-                'mempool': _mempool_size(db) if mempool is None else mempool}
+                'mempool': _mempool_size(db) if mempool is None else mempool,
+                # process CPU seconds (every thread) so far: what each replica costs the host, per op stream
+                'lean': bool(db.lean), 'cpu_s': round(time.process_time(), 4),
+                'crypto_cpu_s': round(_pagesync_stats().get('plan_crypto_cpu_s', 0.0), 4)}
         if deep:
             db.flush()
             mine['sql_utxo_hash'] = db.sql_unspent_outputs_hash()
@@ -315,17 +319,18 @@ def commit_point():
         raise CommitRefused(f'{g.what}: {g.n}/{g.c.ctx.world} replicas ready to commit')
 
 
+def _pagesync_stats() -> dict:
+    from ..ledger import pagesync
+    return pagesync.stats
+
+
 def _utxo_tag() -> int:
     from ..ledger.utxo import TAG_BY_TABLE
     return TAG_BY_TABLE['unspent_outputs']
 
 
 def _tip_hash(db) -> Optional[str]:
-    tip = db._tip_id()
-    if not tip:
-        return None
-    row = db._q1('SELECT hash FROM blocks WHERE id = ?', (tip,))
-    return row[0] if row else None
+    return db.block_hash_at(db._tip_id())
 
 
 def _mempool_size(db) -> int:
@@ -678,8 +683,7 @@ async def leader_resync(db) -> dict:
 
 
 def _hash_at(db, h: int) -> Optional[str]:
-    row = db._q1('SELECT hash FROM blocks WHERE id = ?', (h,))
-    return row[0] if row else None
+    return db.block_hash_at(h)
 
 
 def _gather_tips(c: Cluster, db) -> List[dict]:
@@ -739,20 +743,31 @@ async def _follower_fork_window(c: Cluster, db, msg):
         await db.delete_blockchain()
 
 
+LEDGER_OPS = ('block', 'page', 'replay_block')  # ops that move the chain tip: a lean follower logs them
+SQL_OPS = ('rollback', 'delete', 'fork_window')  # ops that need the SQL tables: a lean follower materialises first
+
+
 async def follower_main(c: Cluster, db):
     """Apply the leader's op stream until 'quit'. The first op is the start-up resync, on the long-timeout
-    group; after 'replay_end' the stream moves to the op group."""
-    from ..ledger import fastpath, pagesync, validate
-    from ..ledger.manager import clear_pending_transactions
-    from ..models.transaction import Transaction
+    group; after 'replay_end' the stream moves to the op group.
+
+    A lean follower (ledger/lean.py, the default) applies blocks to its indexes only and logs every
+    tip-moving op as it arrived, with the tip it reached; ops that need its SQL tables (rollbacks, chain
+    deletions, fork windows, deep audits) first materialise the log. It starts by materialising whatever a
+    previous run logged."""
+    from ..ledger import lean
+    want_lean = lean.enabled()
+    if lean.pending(db):
+        await lean.materialise(db)
+    if want_lean:
+        db.enter_lean()
     c.init_ctx.bind_owner()
     c.ctx.bind_owner()
     c.op_ctx = c.init_ctx
     c.init_ctx.barrier()  # the leader has opened its ledger too
-    logger.info(f'cluster follower rank {c.ctx.rank}/{c.ctx.world} ready at height {db._tip_id()}')
-    last_block = None
-    replayed = 0
-    replay_error = None
+    logger.info(f'cluster follower rank {c.ctx.rank}/{c.ctx.world} ready at height {db._tip_id()}'
+                f'{" (lean replica)" if db.lean else ""}')
+    f = _Follower(c, db)
     while True:
         msg = c.recv()
         op = msg['op']
@@ -760,36 +775,67 @@ async def follower_main(c: Cluster, db):
             continue
         if op == 'quit':
             break
+        if db.lean and (op in SQL_OPS or (op == 'status' and msg.get('deep'))):
+            await lean.materialise(db, online=True)
+        if db.lean and op in LEDGER_OPS:
+            db.lean_log.op(msg['_raw'])
+        await f.apply(msg)
+        if op in LEDGER_OPS and db.lean_log is not None and (db.lean or want_lean):
+            db.lean_log.tip(db._tip_id(), _tip_hash(db))
+        if want_lean and not db.lean and op not in ('resync', 'fork_window'):
+            db.enter_lean()  # after an op that needed the full ledger (its log was materialised)
+        elif op in ('status', 'replay_end') and db.lean_log is not None:
+            db.lean_log.sync()
+    if db.lean_log is not None:  # a graceful stop: the log ends on a durable tip marker
+        db.lean_log.tip(db._tip_id(), _tip_hash(db))
+        db.lean_log.sync()
+    logger.info(f'cluster follower rank {c.ctx.rank} stopped at height {db._tip_id()}')
+
+
+class _Follower:
+    """One follower's op handlers (the replay state lives across the ops of a resync)."""
+
+    def __init__(self, c: Cluster, db):
+        self.c, self.db = c, db
+        self.last_block = None
+        self.replayed = 0
+        self.replay_error = None
+
+    async def apply(self, msg: dict):
+        from ..ledger import fastpath, pagesync, validate
+        from ..ledger.manager import clear_pending_transactions
+        from ..models.transaction import Transaction
+        c, db, op = self.c, self.db, msg['op']
         if op == 'resync':
             c.replaying = True  # local verification, no agreement collectives: the leader is not applying
             validate.set_dist_context(None)
-            last_block = None
-            replayed = 0
-            replay_error = None
+            self.last_block = None
+            self.replayed = 0
+            self.replay_error = None
             _gather_tips(c, db)
         elif op == 'fork_window':
             await _follower_fork_window(c, db, msg)
             _gather_tips(c, db)
         elif op == 'replay_block':
-            replayed += 1
-            if replay_error is None and int(msg['h']) > db._tip_id():  # else: this replica already holds it
+            self.replayed += 1
+            if self.replay_error is None and int(msg['h']) > db._tip_id():  # else: this replica already holds it
                 try:
                     hexes, cb = await _split_coinbase(unpack_txs(msg['_payload']))
                     if cb is None:  # a replayed block is the sync form: it carries its coinbase
                         raise RuntimeError(f'block {msg["h"]} has no coinbase transaction')
                     if not await fastpath.create_block_from_hex(msg['content'], hexes, coinbase=cb,
-                                                                last_block=last_block, mirror=False):
+                                                                last_block=self.last_block, mirror=False):
                         raise RuntimeError(f'block {msg["h"]} rejected')
-                    last_block = await db.get_last_block()
+                    self.last_block = await db.get_last_block()
                 except Exception as e:  # reported at the next acknowledgement, on every rank
-                    replay_error = e
+                    self.replay_error = e
                     logger.error(f'cluster replay on rank {c.ctx.rank}: {e}')
-            if replayed % ACK_EVERY == 0:
-                c.replay_ack(replay_error is None)
+            if self.replayed % ACK_EVERY == 0:
+                c.replay_ack(self.replay_error is None)
         elif op == 'mempool_reset':
             db.clear_mempool()
         elif op == 'replay_end':
-            c.replay_ack(replay_error is None)
+            c.replay_ack(self.replay_error is None)
             c.replaying = False
             c.status(db)
             c.op_ctx = c.ctx
@@ -817,7 +863,6 @@ async def follower_main(c: Cluster, db):
             c.status(db, bool(msg.get('deep')))
         else:  # pragma: no cover
             raise RuntimeError(f'unknown cluster op {op}')
-    logger.info(f'cluster follower rank {c.ctx.rank} stopped at height {db._tip_id()}')
 
 
 __all__ = ['Cluster', 'CommitGate', 'init', 'get', 'on_admit', 'on_confirm', 'flush_txs', 'mirror_gc',

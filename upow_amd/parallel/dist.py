@@ -410,7 +410,9 @@ def init_from_env(backend: Optional[str] = None, want_gpu: bool = True) -> DistC
         ctx.forced = world == 1
         import torch.distributed as dist
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        be = backend or ('nccl' if gpu else 'gloo')
+        # UPOW_DIST_BACKEND=gloo: host collectives with GPU compute (several ranks sharing one GPU, e.g. a
+        # multi-rank cluster measured on a one-GPU box; RCCL needs one GPU per rank)
+        be = backend or os.environ.get('UPOW_DIST_BACKEND') or ('nccl' if gpu else 'gloo')
         from datetime import timedelta
         init_timeout = timedelta(seconds=float(os.environ.get('UPOW_DIST_INIT_TIMEOUT_S', '3600')))
         if not dist.is_initialized():

@@ -7,6 +7,8 @@ block order (reference: create_unspent_outputs.py:9-45, database.py:846-862).
 ``python -m upow_amd.tools verify-utxo``: audit the UTXO index against the SQL tables (K12 hash + sets).
 ``python -m upow_amd.tools address-utxos ADDRESS``: the address's live outputs in all seven output tables,
 straight from the UTXO index (on a GPU node one ``utxo_address_scan`` over the HBM table, K14).
+``python -m upow_amd.tools materialise --db <rankN ledger>``: bring a lean cluster follower's SQL tables to its
+tip from its op log (ledger/lean.py); every other command does this first when the ledger has an op log.
 """
 from __future__ import annotations
 
@@ -20,6 +22,16 @@ from .constants import SMALLEST
 from .ledger.database import Database
 
 
+async def open_ledger(path: str = None) -> Database:
+    """The ledger at ``path``, its SQL tables brought to the tip first when it is a lean follower's (op log)."""
+    from .ledger import lean
+    db = await Database.create(path=path)
+    if lean.pending(db):
+        n = await lean.materialise(db)
+        print(f'materialised {n} block(s) from the op log', file=sys.stderr)
+    return db
+
+
 async def address_utxos(address: str, path: str = None, db: Database = None) -> dict:
     """Live outputs owned by ``address`` in all seven output tables, from the UTXO index (K14; one
     ``utxo_address_scan`` per address form on a GPU node). Both string forms of the key are matched
@@ -28,7 +40,7 @@ async def address_utxos(address: str, path: str = None, db: Database = None) -> 
     is_stake NULL/0); ``stake`` and each governance table are summed separately."""
     from .ledger.utxo import STAKE_ONLY, TABLE_BY_TAG
     from .utils.codec import address_search_hex
-    db = db or await Database.create(path=path)
+    db = db or await open_ledger(path)
     try:
         forms = [bytes.fromhex(h) for h in address_search_hex(address)]
     except Exception:
@@ -55,7 +67,7 @@ async def address_utxos(address: str, path: str = None, db: Database = None) -> 
 
 
 async def rebuild_utxo(path: str = None):
-    db = await Database.create(path=path)
+    db = await open_ledger(path)
     outputs = await db.get_unspent_outputs_from_all_transactions()
     with db.transaction():
         db._x('DELETE FROM unspent_outputs')
@@ -68,7 +80,8 @@ async def rebuild_utxo(path: str = None):
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument('command', choices=['rebuild-utxo', 'utxo-hash', 'snapshot', 'verify-utxo', 'address-utxos'])
+    ap.add_argument('command', choices=['rebuild-utxo', 'utxo-hash', 'snapshot', 'verify-utxo', 'address-utxos',
+                                        'materialise'])
     ap.add_argument('address', nargs='?')
     ap.add_argument('--db', default=None)
     ap.add_argument('--out', default=None)
@@ -83,14 +96,21 @@ def main(argv=None):
         from .ledger import snapshot
 
         async def s():
-            db = await Database.create(path=a.db)
+            db = await open_ledger(a.db)
             res = snapshot.save(db, a.out) if a.command == 'snapshot' else snapshot.verify(db)
             print(json.dumps(res))
             return 0 if res.get('ok', True) else 1
         return asyncio.run(s())
+    elif a.command == 'materialise':
+        async def m():
+            db = await open_ledger(a.db)
+            db.flush()
+            print(json.dumps({'height': db._tip_id(), 'unspent_outputs_hash': await db.get_unspent_outputs_hash()}))
+            db.close()
+        asyncio.run(m())
     else:
         async def h():
-            db = await Database.create(path=a.db)
+            db = await open_ledger(a.db)
             print(await db.get_unspent_outputs_hash())
         asyncio.run(h())
 
