@@ -134,7 +134,8 @@ def _verify_side_metrics(args, ctx) -> dict:
     data); the 256-key pool run follows as a labelled second number (``verify_pool256_*``)."""
     r = _verify_once(args, ctx, 'distinct', args.verify_segments)
     out = {'verify_tx_per_s': r['value'], 'verify_ms_per_block': r['ms_per_step'],
-           **({'verify_segments_tx_per_s': r['segments_tx_per_s']} if 'segments_tx_per_s' in r else {}),
+           **({'verify_segments_tx_per_s': r['segments_tx_per_s'], 'verify_segment_diag': r.get('segment_diag')}
+              if 'segments_tx_per_s' in r else {}),
            'verify_commit_latency_ms': r['commit_latency_ms'], 'validate_tx_per_s': r['validate_tx_per_s'],
            'ecdsa_sig_per_s': r['ecdsa_sig_per_s'], 'verify_stage_ms_avg': r['stage_ms_avg'],
            'verify_config': {'metric': r['metric'], 'unit': r['unit'], 'steps': args.verify_steps, 'warmup': 2,

@@ -153,6 +153,17 @@ for s in $STEPS; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o pow --output-format csv \
         -- python3 bench.py --steps 5 --warmup 1 > "$OUT/prof.log" 2>&1 || { tail -20 "$OUT/prof.log"; exit 1; }
       echo prof-ok ;;
+    powpmc)
+      # counters of the PoW search kernel (one pass per counter group; the mining bench only): VALU
+      # instructions per wave and per nonce, wave cycles, busy cycles, VALU-active cycles, GPU clock
+      for grp in "SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_ACTIVE_INST_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT" \
+                 "SQ_INST_CYCLES_VALU SQ_INSTS_LDS"; do
+        tag=$(echo "$grp" | cut -d' ' -f1 | tr 'A-Z' 'a-z')
+        timeout -s KILL 120 rocprofv3 --pmc $grp -d "$OUT/powpmc_$tag" -o pow --output-format csv \
+          -- python3 bench.py --steps 2 --warmup 1 --verify-steps 0 --sync-steps 0 > "$OUT/powpmc_$tag.log" 2>&1 \
+          || { tail -20 "$OUT/powpmc_$tag.log"; exit 1; }
+        find "$OUT/powpmc_$tag" -name '*counter_collection.csv' | head -1 | xargs -r grep -m 12 -E 'pow_search_kernel|Counter_Name' | cut -c1-400
+      done ;;
     vprof)
       rm -rf /tmp/upow_bench_ledger
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/vprof" -o verify --output-format csv \

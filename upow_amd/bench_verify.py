@@ -524,12 +524,44 @@ async def _run(args, ctx, device, utxo_backend):
     queue_trace = []  # (journal records not yet in SQL, bytes queued) after each timed block
     untimed = 0.0  # mempool admission of the next block's txs happens inside the wall-clock window
     seg_walls, seg_txs = [], []  # per segment of ``steps`` blocks, each ending with its own SQL drain
+    seg_diag = []  # per segment: where its wall time went (the spread between segments of one run)
+
+    def writer_snapshot():
+        if db.writer is None:
+            return None
+        w = db.writer.stats()
+        busy = [sh['apply_s'] + sh['commit_s'] for sh in w['shards']]
+        return {'t': time.perf_counter(), 'submitted': w['submitted'], 'applied': w['applied'],
+                'throttle_s': w['throttle_s'], 'fdatasync_s': w['fdatasync_s'], 'busy': busy}
 
     def end_segment():
+        lag = None
+        w0 = seg[3]
+        if db.writer is not None:
+            st = db.writer.stats()
+            lag = st['submitted'] - st['applied']
+        tf = time.perf_counter()
         db.flush()
         ctx.synchronize()
-        seg_walls.append(time.perf_counter() - seg[0] - (untimed - seg[1]))
+        te = time.perf_counter()
+        seg_walls.append(te - seg[0] - (untimed - seg[1]))
         seg_txs.append(total_txs - seg[2])
+        blocks_in = stages[seg[4]:]
+        d = {'wall_ms': round(seg_walls[-1] * 1000, 2), 'tx_per_s': round(seg_txs[-1] / seg_walls[-1], 1),
+             'commit_latency_ms': round(1000 * sum(x['block_s'] for x in blocks_in) / max(1, len(blocks_in)), 3),
+             'drain_ms': round((te - tf) * 1000, 2), 'lag_records_before_drain': lag}
+        for k in ('decode_s', 'utxo_s', 'ecdsa_s', 'apply_commit_s'):
+            vals = [x[k] for x in blocks_in if isinstance(x.get(k), float)]
+            if vals:
+                d[k.replace('_s', '_ms')] = round(1000 * sum(vals) / len(vals), 3)
+        w1 = writer_snapshot()
+        if w0 is not None and w1 is not None:
+            nb = max(1, len(blocks_in))
+            busy = [(b - a) * 1000 / nb for a, b in zip(w0['busy'], w1['busy'])]
+            d.update({'throttle_ms': round((w1['throttle_s'] - w0['throttle_s']) * 1000, 2),
+                      'fdatasync_ms_per_block': round((w1['fdatasync_s'] - w0['fdatasync_s']) * 1000 / nb, 3),
+                      'materialiser_busy_ms_per_block': [round(x, 2) for x in busy]})
+        seg_diag.append(d)
     seg = None
     for b, txs_hex in enumerate(blocks):
         if from_mempool:
@@ -548,7 +580,7 @@ async def _run(args, ctx, device, utxo_backend):
         if b >= args.warmup and (b - args.warmup) % args.steps == 0:
             if seg is not None:
                 end_segment()
-            seg = (time.perf_counter(), untimed, total_txs)
+            seg = (time.perf_counter(), untimed, total_txs, writer_snapshot(), len(stages))
         t0 = time.perf_counter()
         errors = []
         if from_mempool:
@@ -592,7 +624,7 @@ async def _run(args, ctx, device, utxo_backend):
     extra = {'body_parse': extra_parse, 'drain_s': drain, 'writer': writer, 'window_unix': [unix_start, time.time()],
              'governance': gov_probe,
              'difficulties': sorted({str(d) for d in difficulties}),
-             'segments': [(t, w) for t, w in zip(seg_txs, seg_walls)],
+             'segments': [(t, w) for t, w in zip(seg_txs, seg_walls)], 'segment_diag': seg_diag,
              'aging': aging or None, 'queue_trace': queue_trace, 'key_setup_s': key_setup}
     if gov_probe is not None:
         gov_probe['active_inodes_after'] = len(await db.get_active_inodes())
@@ -668,7 +700,8 @@ def run_verify_bench(args, ctx):
         'steps': args.steps,
         'warmup': args.warmup,
         'ms_per_step': ms,
-        **({'segments_tx_per_s': [round(x, 1) for x in seg_tps], 'segment_blocks': args.steps} if seg_tps else {}),
+        **({'segments_tx_per_s': [round(x, 1) for x in seg_tps], 'segment_blocks': args.steps,
+            'segment_diag': extra.get('segment_diag')} if seg_tps else {}),
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
