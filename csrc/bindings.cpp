@@ -406,31 +406,35 @@ PYBIND11_MODULE(_native, m) {
         { py::gil_scoped_release rel; o = utxo_dump(h, nullptr); }
         return py::bytes(reinterpret_cast<const char*>(o.data()), o.size());
     });
-    m.def("utxo_block_inputs", [recs_arg](int64_t h, py::buffer keys, py::bytes in_start, py::bytes out_amount,
-                                          py::bytes out_start, uint32_t want_tag) {
+    // The whole-block input pass: reads the segment arrays in place (any buffer: the codec's bytes or numpy
+    // arrays) and returns numpy arrays the pass wrote straight out of its pinned staging (one copy each).
+    m.def("utxo_block_inputs", [recs_arg](int64_t h, py::buffer keys, py::buffer in_start, py::buffer out_amount,
+                                          py::buffer out_start, uint32_t want_tag) {
         int64_t n_in; const uint8_t* kp = recs_arg(keys, n_in);
-        std::string is = in_start, oa = out_amount, os = out_start;
-        if (is.size() % 4 || is.size() < 4 || os.size() != is.size() || oa.size() % 8)
-            throw std::invalid_argument("bad segment arrays");
-        const int64_t n_tx = int64_t(is.size() / 4) - 1;
-        const int32_t* isp = reinterpret_cast<const int32_t*>(is.data());
-        const int32_t* osp = reinterpret_cast<const int32_t*>(os.data());
-        const int64_t n_out = int64_t(oa.size() / 8);
+        py::buffer_info bi = in_start.request(), bo = out_start.request(), ba = out_amount.request();
+        const size_t is_n = size_t(bi.size * bi.itemsize), os_n = size_t(bo.size * bo.itemsize);
+        const size_t oa_n = size_t(ba.size * ba.itemsize);
+        if (is_n % 4 || is_n < 4 || os_n != is_n || oa_n % 8) throw std::invalid_argument("bad segment arrays");
+        const int64_t n_tx = int64_t(is_n / 4) - 1;
+        const int32_t* isp = static_cast<const int32_t*>(bi.ptr);
+        const int32_t* osp = static_cast<const int32_t*>(bo.ptr);
+        const uint64_t* oap = static_cast<const uint64_t*>(ba.ptr);
+        const int64_t n_out = int64_t(oa_n / 8);
         for (int64_t t = 0; t < n_tx; ++t)  // the kernels index with these: validate them on the host
             if (isp[t] < 0 || isp[t + 1] < isp[t] || osp[t] < 0 || osp[t + 1] < osp[t])
                 throw std::invalid_argument("segment offsets must be non-decreasing");
         if (isp[n_tx] != n_in || osp[n_tx] != n_out || isp[0] != 0 || osp[0] != 0)
             throw std::invalid_argument("segment offsets do not cover the arrays");
-        BlockInputsResult r;
+        py::array_t<uint8_t> tags(n_in), pay(n_in * 80);
+        py::array_t<uint32_t> dup(n_in), miss(std::max<int64_t>(n_tx, 0));
+        py::array_t<int64_t> fee(std::max<int64_t>(n_tx, 0));
+        BlockInputsOut r{tags.mutable_data(), pay.mutable_data(), dup.mutable_data(), fee.mutable_data(),
+                         miss.mutable_data()};
         {
             py::gil_scoped_release rel;
-            r = utxo_block_inputs(h, kp, n_in, isp, reinterpret_cast<const uint64_t*>(oa.data()), n_out, osp, n_tx,
-                                  want_tag);
+            utxo_block_inputs(h, kp, n_in, isp, oap, n_out, osp, n_tx, want_tag, r);
         }
-        auto b = [](const void* p, size_t n) { return py::bytes(static_cast<const char*>(p), n); };
-        return py::make_tuple(b(r.tags.data(), r.tags.size()), b(r.payload.data(), r.payload.size()),
-                              b(r.dup_of.data(), 4 * r.dup_of.size()), b(r.fee.data(), 8 * r.fee.size()),
-                              b(r.missing.data(), 4 * r.missing.size()), r.n_dup);
+        return py::make_tuple(tags, pay, dup, fee, miss, r.n_dup);
     });
     m.def("utxo_set_hash", [](int64_t h, uint32_t tag) {
         std::vector<uint8_t> d;

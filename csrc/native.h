@@ -98,16 +98,18 @@ std::vector<uint8_t> utxo_address_scan(int64_t h, const uint8_t* addr, uint32_t 
                                        uint32_t stake_sel, std::vector<uint8_t>& payload_out, uint64_t* total_out);
 
 // whole-block input pass: lookup (K7) + duplicate candidates (K10) + per-tx fees (K11) in one round trip
-struct BlockInputsResult {
-    std::vector<uint8_t> tags, payload;  // per input: table tag (0xff absent), 80-byte payload
-    std::vector<uint32_t> dup_of;        // per input: 1 + index of the earlier identical input, else 0
-    std::vector<int64_t> fee;            // per tx: sum(spent) - sum(outputs), smallest units
-    std::vector<uint32_t> missing;       // per tx: inputs not found with want_tag (or without payload)
+// Outputs of the whole-block input pass, written in place (the caller's arrays: no intermediate copies)
+struct BlockInputsOut {
+    uint8_t* tags;      // per input: table tag (0xff absent)
+    uint8_t* payload;   // per input: 80-byte payload
+    uint32_t* dup_of;   // per input: 1 + index of the earlier identical input, else 0
+    int64_t* fee;       // per tx: sum(spent) - sum(outputs), smallest units
+    uint32_t* missing;  // per tx: inputs not found with want_tag (or without payload)
     uint32_t n_dup = 0;
 };
-BlockInputsResult utxo_block_inputs(int64_t h, const uint8_t* keys, int64_t n_in, const int32_t* in_start,
-                                    const uint64_t* out_amount, int64_t n_out, const int32_t* out_start,
-                                    int64_t n_tx, uint32_t want_tag);
+void utxo_block_inputs(int64_t h, const uint8_t* keys, int64_t n_in, const int32_t* in_start,
+                       const uint64_t* out_amount, int64_t n_out, const int32_t* out_start, int64_t n_tx,
+                       uint32_t want_tag, BlockInputsOut& r);
 // K12: SHA-256 over (txid || index byte) of the entries with `tag`, sorted by (txid, index)
 std::vector<uint8_t> utxo_set_hash(int64_t h, uint32_t tag, uint64_t* count_out);
 // the (txid || index byte) message of table `tag` sorted by (txid, index): K12 without its hash tail

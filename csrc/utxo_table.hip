@@ -676,18 +676,15 @@ __global__ __launch_bounds__(256) void block_fee_kernel(const uint8_t* __restric
     missing[t] = miss;
 }
 
-BlockInputsResult utxo_block_inputs(int64_t h, const uint8_t* keys, int64_t n_in, const int32_t* in_start,
-                                    const uint64_t* out_amount, int64_t n_out, const int32_t* out_start,
-                                    int64_t n_tx, uint32_t want_tag) {
+void utxo_block_inputs(int64_t h, const uint8_t* keys, int64_t n_in, const int32_t* in_start,
+                       const uint64_t* out_amount, int64_t n_out, const int32_t* out_start, int64_t n_tx,
+                       uint32_t want_tag, BlockInputsOut& r) {
     std::lock_guard<std::mutex> lk(g_ut_mu);
     UtxoTableDev& t = table(h);
-    BlockInputsResult r;
-    r.tags.assign(size_t(n_in), 0xff);
-    r.payload.assign(size_t(n_in) * sizeof(UtxoPayload), 0);
-    r.dup_of.assign(size_t(n_in), 0);
-    r.fee.assign(size_t(n_tx), 0);
-    r.missing.assign(size_t(n_tx), 0);
-    if (n_tx == 0) return r;
+    r.n_dup = 0;
+    if (n_tx == 0) {  // no tx, so no input either: nothing to write
+        return;
+    }
     if (n_in >= (int64_t(1) << 24)) throw std::invalid_argument("too many inputs for one block pass");
     uint32_t log2 = 8;
     while ((int64_t(1) << log2) < 2 * n_in) ++log2;
@@ -720,24 +717,23 @@ BlockInputsResult utxo_block_inputs(int64_t h, const uint8_t* keys, int64_t n_in
                        d_in_start.p, d_out.p, d_out_start.p, n_tx, want_tag, d_fee.p, d_miss.p);
     uck(hipGetLastError(), "block_fee_kernel");
     if (n_in) {
-        io.d2h(r.tags.data(), d_tags.p, size_t(n_in));
-        io.d2h(r.payload.data(), d_pay.p, r.payload.size());
-        io.d2h(r.dup_of.data(), d_dup.p, 4 * size_t(n_in));
+        io.d2h(r.tags, d_tags.p, size_t(n_in));
+        io.d2h(r.payload, d_pay.p, size_t(n_in) * sizeof(UtxoPayload));
+        io.d2h(r.dup_of, d_dup.p, 4 * size_t(n_in));
     }
-    io.d2h(r.fee.data(), d_fee.p, 8 * size_t(n_tx));
-    io.d2h(r.missing.data(), d_miss.p, 4 * size_t(n_tx));
-    io.finish("block inputs");
+    io.d2h(r.fee, d_fee.p, 8 * size_t(n_tx));
+    io.d2h(r.missing, d_miss.p, 4 * size_t(n_tx));
+    io.finish("block inputs");  // one sync, then each output copied once out of the pinned staging
     // exact confirmation of duplicate candidates (full 36-byte key compare)
     const UtxoKeyRec* kr = reinterpret_cast<const UtxoKeyRec*>(keys);
     for (int64_t i = 0; i < n_in; ++i) {
-        if (!r.dup_of[size_t(i)]) continue;
-        const uint32_t w = r.dup_of[size_t(i)] - 1;
+        if (!r.dup_of[i]) continue;
+        const uint32_t w = r.dup_of[i] - 1;
         if (std::memcmp(kr[i].txid, kr[w].txid, 32) != 0 || (kr[i].index & 0xffu) != (kr[w].index & 0xffu))
-            r.dup_of[size_t(i)] = 0;  // fingerprint collision, not a duplicate
+            r.dup_of[i] = 0;  // fingerprint collision, not a duplicate
         else
             ++r.n_dup;
     }
-    return r;
 }
 
 // K12: SHA-256 over (txid || index byte) of every entry with `tag`, sorted by (txid, index).

@@ -265,8 +265,9 @@ def _cluster_worker(rank, world, port, tmp, q):
             if rank != 0:
                 await cluster.follower_main(c, db)
                 from upow_amd.ledger import lean
-                assert db.lean  # a lean replica: its SQL tables are materialised from its op log (promotion)
-                await lean.materialise(db)
+                assert db.lean == lean.enabled()
+                if db.lean:  # a lean replica: its SQL tables are materialised from its op log (promotion)
+                    await lean.materialise(db)
             else:
                 await cluster.leader_start(db)
                 verdicts, errors = [], []
@@ -292,8 +293,10 @@ def _cluster_worker(rank, world, port, tmp, q):
         q.put((rank, traceback.format_exc()))
 
 
-def test_page_sync_on_a_gloo_cluster_matches_single_node(tmp_path, source_page, small_chunks):
+@pytest.mark.parametrize('replica', ['lean', 'full'])
+def test_page_sync_on_a_gloo_cluster_matches_single_node(tmp_path, source_page, small_chunks, replica, monkeypatch):
     from test_parallel import _spawn
+    monkeypatch.setenv('UPOW_CLUSTER_LEAN', '1' if replica == 'lean' else '0')  # the followers' replica form
     victim = source_page[17]['transactions'][1]
     forged = _forge(source_page, 17, [_bad_sig(victim)])
     pages = [forged[:9], forged[9:]]

@@ -19,6 +19,7 @@ import json
 import os
 import random
 import time
+from typing import Optional
 from decimal import Decimal
 
 from .constants import SMALLEST
@@ -232,6 +233,18 @@ async def premine_headers(db, addr: str, blocks, base_ts: int, device, spacing: 
         headers.append(content)
         prev = hashlib.sha256(bytes.fromhex(content)).hexdigest()
     return headers, diffs
+
+
+def _io_write_mb() -> Optional[float]:
+    """Bytes this process has caused to be written to storage so far (/proc/self/io write_bytes), in MB."""
+    try:
+        with open('/proc/self/io') as f:
+            for line in f:
+                if line.startswith('write_bytes:'):
+                    return int(line.split()[1]) / 2**20
+    except OSError:
+        pass
+    return None
 
 
 def _governance_txs(seeded, nxt, n_dv, n_vv, n_rv, rng):
@@ -529,10 +542,13 @@ async def _run(args, ctx, device, utxo_backend):
     def writer_snapshot():
         if db.writer is None:
             return None
+        import resource
         w = db.writer.stats()
-        busy = [sh['apply_s'] + sh['commit_s'] for sh in w['shards']]
+        ru = resource.getrusage(resource.RUSAGE_SELF)
         return {'t': time.perf_counter(), 'submitted': w['submitted'], 'applied': w['applied'],
-                'throttle_s': w['throttle_s'], 'fdatasync_s': w['fdatasync_s'], 'busy': busy}
+                'throttle_s': w['throttle_s'], 'fdatasync_s': w['fdatasync_s'],
+                'apply': [sh['apply_s'] for sh in w['shards']], 'commit': [sh['commit_s'] for sh in w['shards']],
+                'cpu_s': ru.ru_utime + ru.ru_stime, 'nivcsw': ru.ru_nivcsw, 'write_mb': _io_write_mb()}
 
     def end_segment():
         lag = None
@@ -557,10 +573,18 @@ async def _run(args, ctx, device, utxo_backend):
         w1 = writer_snapshot()
         if w0 is not None and w1 is not None:
             nb = max(1, len(blocks_in))
-            busy = [(b - a) * 1000 / nb for a, b in zip(w0['busy'], w1['busy'])]
+            ap = [(b - a) * 1000 / nb for a, b in zip(w0['apply'], w1['apply'])]
+            cm = [(b - a) * 1000 / nb for a, b in zip(w0['commit'], w1['commit'])]
+            wall = w1['t'] - w0['t']
             d.update({'throttle_ms': round((w1['throttle_s'] - w0['throttle_s']) * 1000, 2),
                       'fdatasync_ms_per_block': round((w1['fdatasync_s'] - w0['fdatasync_s']) * 1000 / nb, 3),
-                      'materialiser_busy_ms_per_block': [round(x, 2) for x in busy]})
+                      'materialiser_busy_ms_per_block': [round(a + c, 2) for a, c in zip(ap, cm)],
+                      'materialiser_apply_ms_per_block': round(max(ap[1:] or ap), 2),
+                      'materialiser_commit_ms_per_block': round(max(cm[1:] or cm), 2),
+                      'process_cores_busy': round((w1['cpu_s'] - w0['cpu_s']) / wall, 2) if wall > 0 else None,
+                      'involuntary_switches': w1['nivcsw'] - w0['nivcsw'],
+                      'write_mb_per_block': round((w1['write_mb'] - w0['write_mb']) / nb, 2)
+                      if w1['write_mb'] is not None and w0['write_mb'] is not None else None})
         seg_diag.append(d)
     seg = None
     for b, txs_hex in enumerate(blocks):

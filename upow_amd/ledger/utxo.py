@@ -522,11 +522,10 @@ class UtxoIndex:
         out_start = np.ascontiguousarray(out_start, dtype=np.int32)
         out_amount = np.ascontiguousarray(out_amount, dtype=np.uint64)
         if isinstance(self.be, _GpuBackend):
-            t, p, d, f, m, nd = self.be.L.utxo_block_inputs(self.be.h, np.ascontiguousarray(in_keys),
-                                                            in_start.tobytes(), out_amount.tobytes(),
-                                                            out_start.tobytes(), want_tag)
-            return (np.frombuffer(t, np.uint8), np.frombuffer(p, PAYLOAD_DTYPE), np.frombuffer(d, np.uint32),
-                    np.frombuffer(f, np.int64), np.frombuffer(m, np.uint32), int(nd))
+            # the segment arrays are read in place; the outputs are arrays the pass filled from its pinned staging
+            t, p, d, f, m, nd = self.be.L.utxo_block_inputs(self.be.h, np.ascontiguousarray(in_keys), in_start,
+                                                            out_amount, out_start, want_tag)
+            return t, p.view(PAYLOAD_DTYPE), d, f, m, int(nd)
         tags, pay = self.lookup_records(in_keys)
         n_in = len(in_keys)
         dup_of = np.zeros(n_in, dtype=np.uint32)
