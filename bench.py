@@ -117,7 +117,7 @@ def _verify_once(args, ctx, keys: str, segments: int = 1) -> dict:
     from upow_amd.bench_verify import run_cluster_verify_bench, run_verify_bench
     tmp = tempfile.mkdtemp(prefix='upow_bench_verify_')
     try:
-        v = argparse.Namespace(**{**vars(args), 'steps': args.verify_steps, 'warmup': 2, 'ledger': tmp,
+        v = argparse.Namespace(**{**vars(args), 'steps': args.verify_steps, 'warmup': args.verify_warmup, 'ledger': tmp,
                                   'object_path': False, 'from_mempool': False, 'governance': False,
                                   'governance_txs': 0.0, 'age_txs': 0, 'keys': keys, 'grouped_txs': 0.0,
                                   'segments': segments})
@@ -138,7 +138,8 @@ def _verify_side_metrics(args, ctx) -> dict:
               if 'segments_tx_per_s' in r else {}),
            'verify_commit_latency_ms': r['commit_latency_ms'], 'validate_tx_per_s': r['validate_tx_per_s'],
            'ecdsa_sig_per_s': r['ecdsa_sig_per_s'], 'verify_stage_ms_avg': r['stage_ms_avg'],
-           'verify_config': {'metric': r['metric'], 'unit': r['unit'], 'steps': args.verify_steps, 'warmup': 2,
+           'verify_config': {'metric': r['metric'], 'unit': r['unit'], 'steps': args.verify_steps,
+                             'warmup': args.verify_warmup,
                              'txs_per_block': r['config']['seq_len'], 'ledger': r['config']['ledger'],
                              'block_path': r['config']['block_path'], 'scaling': r['scaling'],
                              'layout': r['config']['parallelism'], 'keys': 'distinct', 'data': r['data']}}
@@ -263,6 +264,8 @@ def main(argv=None):
                     help='mine mode: the verify side metric is the median of this many consecutive segments of '
                          '--verify-steps blocks (one setup, one process)')
     ap.add_argument('--segments', type=int, default=1, help='verify mode: median of this many segments of --steps blocks')
+    ap.add_argument('--verify-warmup', type=int, default=2,
+                    help='mine mode: untimed 2 MB blocks before the verify side metric\'s segments')
     ap.add_argument('--verify-steps', type=int, default=10,
                     help='mine mode: timed 2 MB blocks of the tx-verify side measurement (0: skip; GPU only)')
     args = ap.parse_args(argv)

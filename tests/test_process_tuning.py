@@ -74,3 +74,26 @@ def test_stall_probe_heartbeat_gates_sampling(tmp_path):
     assert fresh == 0 and total >= 20
     lines = [json.loads(x) for x in path.read_text().splitlines()]
     assert len(lines) == total and all(r['late_ms'] > 20.0 for r in lines)
+
+
+def test_cpu_budget_splits_a_cluster_node_by_role(monkeypatch):
+    """utils/cpus.py: ranks sharing one affinity set split it, local rank 0 (a cluster node's leader, the rank
+    that materialises SQL and serves HTTP) taking half and the lean followers the rest; UPOW_CPU_ROLE_SPLIT=0
+    restores the equal split."""
+    import builtins
+    from upow_amd.utils import cpus
+    monkeypatch.setattr(os, 'sched_getaffinity', lambda pid: set(range(64)))
+    monkeypatch.setattr(os, 'cpu_count', lambda: 64)
+    real_open = builtins.open
+    monkeypatch.setattr(builtins, 'open', lambda p, *a, **k: (_ for _ in ()).throw(OSError())
+                        if p == '/sys/fs/cgroup/cpu.max' else real_open(p, *a, **k))
+    monkeypatch.setenv('LOCAL_WORLD_SIZE', '8')
+    got = []
+    for r in range(8):
+        monkeypatch.setenv('LOCAL_RANK', str(r))
+        got.append(cpus.cpu_budget())
+    assert got == [32] + [4] * 7
+    monkeypatch.setenv('UPOW_CPU_ROLE_SPLIT', '0')
+    assert cpus.cpu_budget() == 8
+    monkeypatch.setenv('LOCAL_WORLD_SIZE', '1')
+    assert cpus.cpu_budget() == 64

@@ -21,7 +21,16 @@ def cpu_budget(per_rank: bool = True) -> int:
         pass
     local = int(os.environ.get('LOCAL_WORLD_SIZE', '1') or 1)
     if per_rank and local > 1 and (aff is None or len(aff) >= (os.cpu_count() or 1) // 2):
-        avail = max(1, avail // local)  # not pinned per rank: split the node's budget
+        # not pinned per rank: split the node's budget. By role (UPOW_CPU_ROLE_SPLIT, default on): local rank 0
+        # — a cluster node's leader, the one rank that renders, encodes and materialises the SQL ledger and
+        # serves HTTP — takes half, the lean followers (ledger/lean.py: decode, index updates, their verify
+        # shard) share the other half; an equal split gave the leader 1/8 of an 8-GPU host for 8x the host work
+        if os.environ.get('UPOW_CPU_ROLE_SPLIT', '1') != '0':
+            lead = max(1, avail // 2)
+            if int(os.environ.get('LOCAL_RANK', '0') or 0) == 0:
+                return lead
+            return max(1, (avail - lead) // (local - 1))
+        avail = max(1, avail // local)
     return avail
 
 
