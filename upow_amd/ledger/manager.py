@@ -19,8 +19,8 @@ from math import ceil, floor, log
 from time import perf_counter
 from typing import List, Optional, Tuple, Union
 
-from ..constants import (BLOCK_TIME, BLOCKS_COUNT, LAST_BLOCK_FOR_GENESIS_KEY, MAX_BLOCK_SIZE_HEX, MAX_SUPPLY,
-                         START_DIFFICULTY)
+from ..constants import (BLOCK_TIME, BLOCKS_COUNT, HALVING_INTERVAL, LAST_BLOCK_FOR_GENESIS_KEY, MAX_BLOCK_SIZE_HEX,
+                         MAX_SUPPLY, NINE_HALVING_INTERVAL, START_DIFFICULTY)
 from ..models.block import (block_to_bytes, check_pow, get_transactions_merkle_tree,
                             get_transactions_merkle_tree_ordered, split_block_content)
 from ..models.transaction import CoinbaseTransaction, Transaction, TransactionOutput
@@ -148,73 +148,71 @@ async def check_block_is_valid(block_content: str, mining_info: tuple = None) ->
 
 
 # ---------------------------------------------------------------------------------------------- emission
+HALVING_BLOCKS = HALVING_INTERVAL  # one halving era: three years of 60 s blocks (1,576,800)
+LAST_REWARD_BLOCK = NINE_HALVING_INTERVAL  # 14,191,200: no block reward after the ninth halving
+
+
+def _era(block_no: int) -> int:
+    """Halvings before ``block_no``: the last block of an era still pays the era's reward."""
+    return (int(block_no) - 1) // HALVING_BLOCKS
+
+
 def get_block_reward(block_no) -> Decimal:
-    """manager.py:154-168."""
+    """Block subsidy (reference manager.py:154-168): 6 coins, halved every era, nothing past the ninth
+    halving. The reference divides in binary floating point (``6 / 2 ** n``) and converts; every value of that
+    sequence is exact in binary, and it is kept as written."""
     assert block_no > 0
-    halving_interval = 1576800
-    nine_halving_interval = 14191200
-    if block_no > nine_halving_interval:
+    if block_no > LAST_REWARD_BLOCK:
         return Decimal(0)
-    coins_per_block = 6
-    num_halvings = block_no // halving_interval
-    if block_no % halving_interval == 0:
-        num_halvings = num_halvings - 1
-    return Decimal(coins_per_block / (2 ** num_halvings))
+    return Decimal(6 / (1 << _era(block_no)))
 
 
 def get_inode_rewards(reward, inode_address_details, block_no=1):
-    """manager.py:171-212 (Decimal contexts and the <1 % redistribution reproduced verbatim)."""
-    total_percent = sum(entry['emission'] for entry in inode_address_details)
-    if not inode_address_details or total_percent <= 0:
+    """Miner / inode split of a block reward (reference manager.py:171-212), as the same Decimal operation
+    sequence: half to the miner; the other half over the inodes by emission share, rounded up (8 decimals,
+    9 significant digits and the newer rounding after block 39,000). The shares of inodes under 1 % are pooled
+    and, inside the per-inode pass as in the reference, the pool so far is re-spread over every inode at or
+    above 1 % each time it is non-empty — so an early pool is paid more than once, and a >= 1 % inode listed
+    after a < 1 % one is not in the result yet when the pool is spread (a KeyError, as in the reference).
+    ``tests/test_consensus.py`` pins the results (including those errors) against golden outputs."""
+    total = sum(d['emission'] for d in inode_address_details)
+    if not inode_address_details or total <= 0:
         return reward, {}
     miner_reward = reward * Decimal(0.5)
-    distribution_reward = reward * Decimal(0.5)
-    distributed_rewards = {}
-    redistribution_reward = Decimal(0)
+    inode_half = reward * Decimal(0.5)
+    newer = block_no > 39000
+    round_up = round_up_decimal_new if newer else round_up_decimal
+    big = [d['wallet'] for d in inode_address_details if d['emission'] >= 1]  # in list order, repeats kept
+    shares = {}
+    pooled = Decimal(0)
     with decimal.localcontext() as ctx:
-        ctx.prec = 9 if block_no > 39000 else ctx.prec
-        for address_detail in inode_address_details:
-            percent = address_detail['emission']
-            address_reward = distribution_reward * Decimal(percent) / Decimal(total_percent)
-            if block_no > 39000:
-                address_reward = round_up_decimal_new(address_reward)
+        if newer:
+            ctx.prec = 9
+        for d in inode_address_details:
+            exact = inode_half * Decimal(d['emission']) / Decimal(total)
+            if d['emission'] >= 1:
+                shares[d['wallet']] = round_up(exact)
             else:
-                address_reward = round_up_decimal(address_reward)
-            if percent >= 1:
-                distributed_rewards[address_detail['wallet']] = address_reward
-            else:
-                redistribution_reward += distribution_reward * Decimal(percent) / Decimal(total_percent)
-            if redistribution_reward > 0:
-                num_eligible = sum(1 for e in inode_address_details if e['emission'] >= 1)
-                redistribution_amount = redistribution_reward / num_eligible
-                if block_no > 39000:
-                    redistribution_amount = round_up_decimal_new(redistribution_amount)
-                else:
-                    redistribution_amount = round_up_decimal(redistribution_amount)
-                for d in inode_address_details:
-                    if d['emission'] >= 1:
-                        distributed_rewards[d['wallet']] += redistribution_amount
-    return miner_reward, distributed_rewards
+                pooled += exact
+            if pooled > 0:
+                bonus = round_up(pooled / len(big))
+                for w in big:
+                    shares[w] += bonus
+    return miner_reward, shares
 
 
 def get_circulating_supply(block_no):
-    """manager.py:215-234."""
-    halving_interval = 3 * 365 * 24 * 60
-    initial_coins_per_block = 6
-    if block_no > halving_interval * 9:
+    """Coins minted up to ``block_no`` (reference manager.py:215-234): every completed era at its per-block
+    reward plus the current era's blocks so far, summed era by era in binary floating point as the reference
+    does (the result type and rounding are the reference's); the maximum supply past the ninth halving."""
+    if block_no > LAST_REWARD_BLOCK:
         return Decimal(MAX_SUPPLY)
-    circulating_supply = 0
-    num_halvings = block_no // halving_interval
-    remaining_blocks = block_no % halving_interval
-    if remaining_blocks == 0:
-        num_halvings = num_halvings - 1
-    for i in range(num_halvings + 1):
-        current_reward = initial_coins_per_block / (2 ** i)
-        if i == num_halvings and remaining_blocks > 0:
-            circulating_supply += current_reward * remaining_blocks
-        else:
-            circulating_supply += current_reward * halving_interval
-    return circulating_supply
+    done, into = divmod(block_no, HALVING_BLOCKS)
+    blocks_per_era = [HALVING_BLOCKS] * done + ([into] if into else [])
+    minted = 0
+    for era, blocks in enumerate(blocks_per_era):
+        minted += (6 / 2 ** era) * blocks
+    return minted
 
 
 # ---------------------------------------------------------------------------------------------- mempool GC
