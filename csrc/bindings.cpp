@@ -23,6 +23,7 @@ void register_log_appender(py::module_& m);  // log_appender.cpp
 void register_http_wire(py::module_& m);  // http_wire.cpp
 void register_mempool_index(py::module_& m);  // mempool_index.cpp
 void register_jsonspan(py::module_& m);  // jsonspan.cpp
+void register_utxo_host(py::module_& m);  // utxo_host.cpp
 }
 
 static PowJobHost make_job(py::bytes header, uint32_t tmask, uint32_t tword, uint32_t frac_shift,
@@ -64,6 +65,7 @@ PYBIND11_MODULE(_native, m) {
     register_http_wire(m);
     register_mempool_index(m);
     register_jsonspan(m);
+    register_utxo_host(m);
 
     // glibc allocator thresholds (mallopt): every 2 MB block's columns are fresh multi-megabyte Python bytes;
     // above the (dynamic) mmap threshold each one is a new mapping whose pages fault in on first write, and

@@ -293,10 +293,16 @@ def _cluster_worker(rank, world, port, tmp, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize('replica', ['lean', 'full'])
-def test_page_sync_on_a_gloo_cluster_matches_single_node(tmp_path, source_page, small_chunks, replica, monkeypatch):
+@pytest.mark.parametrize('replica,shard', [('lean', '1'), ('full', '1'), ('lean', '0')],
+                         ids=['lean', 'full', 'lean-unsharded-keys'])
+def test_page_sync_on_a_gloo_cluster_matches_single_node(tmp_path, source_page, small_chunks, replica, shard,
+                                                         monkeypatch):
+    """Four ranks sync two pages (a forged signature in block 17) and reach the single node's ledger. With
+    sharded keys (the default) each rank builds the records of its own verify shard only, and the block with the
+    failing signature leaves the plan for the ordinary path on every rank."""
     from test_parallel import _spawn
     monkeypatch.setenv('UPOW_CLUSTER_LEAN', '1' if replica == 'lean' else '0')  # the followers' replica form
+    monkeypatch.setenv('UPOW_SHARD_KEYS', shard)
     victim = source_page[17]['transactions'][1]
     forged = _forge(source_page, 17, [_bad_sig(victim)])
     pages = [forged[:9], forged[9:]]

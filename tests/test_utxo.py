@@ -1,4 +1,5 @@
-"""UTXO index: host dict backend vs the HBM hash-table kernels (probe / insert / erase / grow)."""
+"""UTXO index: the host C++ table (csrc/utxo_host.cpp), the Python dict and the HBM hash-table kernels (probe /
+insert / erase / grow) against one another."""
 import random
 
 import numpy as np
@@ -55,8 +56,12 @@ def _exercise(backend):
     return idx
 
 
-def test_host_backend():
-    idx = _exercise('host')
+HOSTS = ['host', 'host-py']
+
+
+@pytest.mark.parametrize('backend', HOSTS)
+def test_host_backend(backend):
+    idx = _exercise(backend)
     assert len(idx) == 5000 + 300 - len([1 for t in range(3000, 3100) if t % 7 == 3])
 
 
@@ -95,8 +100,9 @@ def _block_inputs_case(idx, seed):
     return pack_records(spend), np.array(in_start, np.int32), out_amount, np.array(out_start, np.int32)
 
 
-def test_block_inputs_host():
-    idx = UtxoIndex(backend='host')
+@pytest.mark.parametrize('backend', HOSTS)
+def test_block_inputs_host(backend):
+    idx = UtxoIndex(backend=backend)
     recs, ins, outs, ost = _block_inputs_case(idx, 11)
     tags, pay, dup_of, fee, missing, n_dup = idx.block_inputs(recs, ins, outs, ost, 0)
     assert n_dup == 4 and int((dup_of > 0).sum()) == 4
@@ -154,8 +160,9 @@ def _check_address_outputs(idx, owners, want):
     assert idx.address_outputs(b'\x42' + bytes(32))[2] == 0
 
 
-def test_address_outputs_host():
-    idx = UtxoIndex(backend='host')
+@pytest.mark.parametrize('backend', HOSTS)
+def test_address_outputs_host(backend):
+    idx = UtxoIndex(backend=backend)
     _check_address_outputs(idx, *_address_case(idx, 21))
 
 
@@ -175,7 +182,7 @@ def test_address_outputs_gpu_scan(gpu):
     assert len(recs) == 5000 and tot == 35000
 
 
-@pytest.mark.parametrize('backend', ['host', pytest.param('gpu', marks=pytest.mark.gpu)])
+@pytest.mark.parametrize('backend', HOSTS + [pytest.param('gpu', marks=pytest.mark.gpu)])
 def test_duplicate_insert_is_skipped(backend, request):
     """Inserting an outpoint that is already live leaves the entry (tag, payload) as it was and is
     counted, on both index backends (csrc/utxo_table.hip utxo_insert_kernel walks the probe chain)."""
@@ -254,8 +261,52 @@ def _apply_blocks(backend):
     return idx
 
 
-def test_apply_block_host():
-    _apply_blocks('host')
+@pytest.mark.parametrize('backend', HOSTS)
+def test_apply_block_host(backend):
+    _apply_blocks(backend)
+
+
+def test_host_tables_agree_under_random_operations():
+    """The C++ host table against the dict over random batches of inserts (with payloads, stake flags and
+    re-inserts of live outpoints), tag-filtered erases, lookups and K14 scans; both key on the index byte."""
+    from upow_amd.ledger.utxo import STAKE_EXCLUDE, STAKE_ONLY, _HostBackend, _NativeHostBackend
+    n, d = UtxoIndex(backend='host'), UtxoIndex(backend='host-py')
+    assert isinstance(n.be, _NativeHostBackend) and isinstance(d.be, _HostBackend)
+    rng = random.Random(77)
+    owners = [bytes([42]) + rng.randbytes(32) for _ in range(6)] + [rng.randbytes(64) for _ in range(2)]
+    pool = _keys(3000, 78)
+    for step in range(40):
+        op = rng.random()
+        ks = rng.sample(pool, rng.randint(1, 200))
+        if op < 0.45:
+            tag = rng.choice((0, 0, 1, 3, 6))
+            pay = make_payload([rng.randrange(1, 1 << 50) for _ in ks], [rng.choice(owners) for _ in ks],
+                               [rng.random() < 0.3 for _ in ks])
+            for i in (n, d):
+                i.insert(ks, tag, pay)
+        elif op < 0.75:
+            tag = rng.choice((None, 0, 3))
+            assert (n.erase(ks, tag) == d.erase(ks, tag)).all()
+        else:
+            tn, pn = n.lookup(ks)
+            td, pd = d.lookup(ks)
+            assert (tn == td).all() and pn.tobytes() == pd.tobytes()
+        assert len(n) == len(d) and n.duplicates == d.duplicates
+    for o in owners:
+        for sel in (0, STAKE_EXCLUDE, STAKE_ONLY):
+            rn, pn, tn = n.address_outputs(o, (0, 1, 3), sel)
+            rd, pd, td = d.address_outputs(o, (0, 1, 3), sel)
+            assert rn.tobytes() == rd.tobytes() and pn.tobytes() == pd.tobytes() and tn == td
+    rn, pn = n.records_payload()
+    rd, pd = d.records_payload()
+    assert rn.tobytes() == rd.tobytes() and pn.tobytes() == pd.tobytes()
+    for tag in (0, 1, 3, 6):
+        assert n.set_hash(tag) == d.set_hash(tag)
+    # index bytes: the tables key on (txid, index & 0xff), as the HBM table does
+    h = pool[0][0]
+    n.erase([(h, i) for i in range(256)])
+    n.insert([(h, 7)], 0)
+    assert n.probe([(h, 7 + 256)])[0] == 0
 
 
 @pytest.mark.gpu

@@ -51,6 +51,8 @@ logger = get_logger(__name__)
 
 ENABLED = os.environ.get('UPOW_PAGE_SYNC', '1') != '0'
 CHUNK = max(1, int(os.environ.get('UPOW_SYNC_CHUNK', '128')))
+# UPOW_SHARD_KEYS=0: every cluster rank decompresses and checks ALL of a chunk's keys (the A/B of the shard)
+SHARD_KEYS = os.environ.get('UPOW_SHARD_KEYS', '1') != '0'
 TAG_U = TAG_BY_TABLE['unspent_outputs']
 _REVOKE = (int(TransactionType.REVOKE_AS_VALIDATOR), int(TransactionType.REVOKE_AS_DELEGATE))
 _HASH_MUL = np.uint64(0x9E3779B97F4A7C15)
@@ -65,7 +67,7 @@ class PageBlock:
     pay: np.ndarray
     fee: np.ndarray
     n_jobs: int
-    recs: bytes
+    recs: Optional[bytes]  # None on a cluster rank that built the records of its own verify shard only
     status: np.ndarray
 
 
@@ -140,7 +142,7 @@ def _key64(keys36: np.ndarray) -> np.ndarray:
 def build_plan(db, items: List[Item], cbs: list, ctx=None) -> List[Optional[PageBlock]]:
     """Plan a chunk (see the module docstring). ``cbs[k]``: block k's parsed CoinbaseTransaction (or None).
     Returns one PageBlock per block, None for the blocks that take the ordinary path."""
-    from ..parallel.verify_dp import verify_records_dp
+    from ..parallel.verify_dp import shard_bounds, verify_records_dp, verify_shard_dp
     from .database import Database
     from .govcheck import OUTPUT_TABLE
     t0 = perf_counter()
@@ -303,19 +305,39 @@ def build_plan(db, items: List[Item], cbs: list, ctx=None) -> List[Optional[Page
     gpu_min = op.GPU_MIN_BATCH if gpu_available() else 1 << 62
     n_jobs = job_base
     cpu0 = process_time()  # host CPU of the P-256 work (key decompression, curve checks, verify) of the plan
-    if n_jobs or sum(len(x) for x in ol):
+    p_addr, p_len = np.ascontiguousarray(np.concatenate(pa)), np.concatenate(pl)
+    o_addr, o_len = np.ascontiguousarray(np.concatenate(oa)), np.concatenate(ol)
+    ji_all, sid_all, jt_all = np.concatenate(ji), np.concatenate(sid), np.concatenate(jt)
+    sigs_all, dg_all = np.ascontiguousarray(np.concatenate(sg)), np.ascontiguousarray(np.concatenate(dg))
+    sharded = ctx is not None and ctx.is_distributed and SHARD_KEYS
+    if sharded:
+        # each rank decompresses and curve-checks a shard of the chunk's keys only: the signer keys of its
+        # verify shard, its shard of the spent outputs' owners and its shard of the new outputs. The shards
+        # cover every key of the chunk, so the MIN of the ranks' verdicts below is the whole chunk's verdict;
+        # each rank ends up with the records of its own verify shard, which is all it verifies
+        lo, hi = shard_bounds(n_jobs, ctx.world, ctx.rank)
+        ilo, ihi = shard_bounds(len(p_len), ctx.world, ctx.rank)
+        olo, ohi = shard_bounds(len(o_len), ctx.world, ctx.rank)
+        sub = np.concatenate([ji_all[lo:hi], np.arange(ilo, ihi, dtype=np.int64)])
         kst, rec_bytes = lib().block_signer_records(
-            np.ascontiguousarray(np.concatenate(pa)), np.concatenate(pl), np.ascontiguousarray(np.concatenate(oa)),
-            np.concatenate(ol), np.concatenate(ji), np.ascontiguousarray(np.concatenate(sg)), np.concatenate(sid),
-            np.ascontiguousarray(np.concatenate(dg)), np.concatenate(jt), gpu_min)
+            np.ascontiguousarray(p_addr[sub]), np.ascontiguousarray(p_len[sub]), np.ascontiguousarray(o_addr[olo:ohi]),
+            np.ascontiguousarray(o_len[olo:ohi]), np.arange(hi - lo, dtype=np.int64), sigs_all, sid_all[lo:hi],
+            dg_all, jt_all[lo:hi], gpu_min)
+        # one 24-byte all-reduce: the replicas planned the same chunk (a difference would desynchronise the
+        # sharded verify) and the chunk's key verdict (-1 a 64-byte address, 0 off the curve, 1 all good)
+        mn = ctx.allreduce_min_vec([n_jobs, -n_jobs, kst])
+        if mn[0] != -mn[1]:
+            raise RuntimeError(f'page plan differs across cluster replicas ({n_jobs} jobs here)')
+        kst = int(mn[2])
+    elif n_jobs or len(o_len):
+        kst, rec_bytes = lib().block_signer_records(p_addr, p_len, o_addr, o_len, ji_all, sigs_all, sid_all, dg_all,
+                                                    jt_all, gpu_min)
+        if ctx is not None and ctx.is_distributed:
+            lo_hi = ctx.allreduce_min_vec([n_jobs * 4 + (kst + 1), -(n_jobs * 4 + (kst + 1))])
+            if lo_hi[0] != -lo_hi[1]:
+                raise RuntimeError(f'page plan differs across cluster replicas ({n_jobs} jobs, kst {kst} here)')
     else:  # empty blocks only: nothing to check or verify
         kst, rec_bytes = 1, b''
-    if ctx is not None and ctx.is_distributed:
-        # every replica planned the same chunk from the same state; a difference would desynchronise the
-        # sharded verify below, so it is checked (one 16-byte all-reduce per chunk) before anything is shared
-        lo_hi = ctx.allreduce_min_vec([n_jobs * 4 + (kst + 1), -(n_jobs * 4 + (kst + 1))])
-        if lo_hi[0] != -lo_hi[1]:
-            raise RuntimeError(f'page plan differs across cluster replicas ({n_jobs} jobs, kst {kst} here)')
     if kst != 1:  # an off-curve key or a 64-byte address among the chunk's keys: the ordinary path decides
         _record(t0, len(cand), 0, n_jobs)
         return plan
@@ -323,6 +345,8 @@ def build_plan(db, items: List[Item], cbs: list, ctx=None) -> List[Optional[Page
     tv = perf_counter()
     if n_jobs == 0:
         status = np.zeros(0, np.uint8)
+    elif sharded:
+        status = verify_shard_dp(ctx, recs.reshape(-1), n_jobs)
     elif ctx is not None and ctx.is_distributed:
         status = verify_records_dp(ctx, recs.reshape(-1))
     else:
@@ -331,8 +355,14 @@ def build_plan(db, items: List[Item], cbs: list, ctx=None) -> List[Optional[Page
     stats['plan_crypto_cpu_s'] = stats.get('plan_crypto_cpu_s', 0.0) + (process_time() - cpu0)
     tags_u = np.full(ni, TAG_U, np.uint8)
     for k, j0, j1, a, b in per:
-        plan[k] = PageBlock(tags=tags_u[a:b], pay=pay[a:b], fee=fees[k], n_jobs=j1 - j0,
-                            recs=recs[j0:j1].tobytes(), status=np.asarray(status[j0:j1], np.uint8))
+        st = np.asarray(status[j0:j1], np.uint8)
+        if sharded:
+            if np.any(st != op.VALID):  # its retry needs records other ranks hold: the ordinary path decides
+                continue
+            rb = None
+        else:
+            rb = recs[j0:j1].tobytes()
+        plan[k] = PageBlock(tags=tags_u[a:b], pay=pay[a:b], fee=fees[k], n_jobs=j1 - j0, recs=rb, status=st)
     _record(t0, len(cand), len(keep), n_jobs, verify_s)
     return plan
 

@@ -6,7 +6,8 @@ reference: the reference answers every "is this outpoint unspent, and in which t
 
 * ``gpu``  — the HBM open-addressing table of ``csrc/utxo_table.hip`` (probe/insert/erase kernels,
   one lane per outpoint; a whole block's inputs are one launch);
-* ``host`` — a Python dict (CPU-only containers and small test ledgers).
+* ``host`` — the same table in C++ on the host (``csrc/utxo_host.cpp``; CPU-only nodes and the test
+  suite), or a Python dict (``host-py``, and when the extension is not built).
 
 Both expose the same batch API; the SQLite tables stay authoritative for address queries and the
 index is rebuilt from them after a rollback.
@@ -167,6 +168,73 @@ class _HostBackend:
         return len(self.d)
 
 
+class _NativeHostBackend:
+    """The host table in C++ (csrc/utxo_host.cpp ``HostUtxo``): the HBM table's record contract — keys
+    (txid, index & 0xff), tag-filtered erase, zero payload when absent, an owner-address index for K14 — as
+    one call per batch of packed records, so the CPU block path never walks its outpoints in Python."""
+
+    def __init__(self):
+        from ..ops.native import lib
+        self.L = lib()
+        self.t = self.L.HostUtxo()
+
+    def reset(self, keys, tags, payload=None):
+        self.t.clear()
+        return self.insert(keys, tags, payload)
+
+    def insert(self, keys, tags, payload=None) -> int:
+        if not len(keys):
+            return 0
+        return self.insert_records(pack_records(keys, list(tags)), payload)
+
+    def insert_records(self, recs: np.ndarray, payload=None) -> int:
+        if not len(recs):
+            return 0
+        pay = None if payload is None else np.ascontiguousarray(payload).view(np.uint8)
+        return int(self.t.insert(np.ascontiguousarray(recs), pay))
+
+    def lookup_records(self, recs: np.ndarray):
+        tags, pay = self.t.lookup(np.ascontiguousarray(recs))
+        return tags, pay.view(PAYLOAD_DTYPE)
+
+    def lookup(self, keys):
+        if not len(keys):
+            return np.zeros(0, dtype=np.uint8), np.zeros(0, dtype=PAYLOAD_DTYPE)
+        return self.lookup_records(pack_records(keys))
+
+    def probe_records(self, recs: np.ndarray) -> np.ndarray:
+        return self.t.probe(np.ascontiguousarray(recs))
+
+    def probe(self, keys) -> np.ndarray:
+        if not len(keys):
+            return np.zeros(0, dtype=np.uint8)
+        return self.probe_records(pack_records(keys))
+
+    def erase_records(self, recs: np.ndarray) -> np.ndarray:
+        if not len(recs):
+            return np.zeros(0, dtype=np.uint8)
+        return self.t.erase(np.ascontiguousarray(recs))
+
+    def erase(self, keys, tag=None) -> np.ndarray:
+        if not len(keys):
+            return np.zeros(0, dtype=np.uint8)
+        return self.erase_records(pack_records(keys, MISSING if tag is None else tag))
+
+    def records(self) -> np.ndarray:
+        return self.t.dump(False)[0].reshape(-1, 40)
+
+    def records_payload(self):
+        raw, pay = self.t.dump(True)
+        return raw.reshape(-1, 40), pay.view(PAYLOAD_DTYPE)
+
+    def address_scan(self, addr: bytes, tag_mask: int, stake_sel: int = STAKE_ANY):
+        raw, pay = self.t.address_scan(bytes(addr), tag_mask, stake_sel)
+        return raw.reshape(-1, 40), pay.view(PAYLOAD_DTYPE)
+
+    def __len__(self):
+        return len(self.t)
+
+
 class _GpuBackend:
     """HBM table; grows (rehash via dump + re-insert) past 50 % load."""
 
@@ -291,6 +359,18 @@ class _GpuBackend:
         return self.count
 
 
+def _host_backend(name: str):
+    """``host``: the C++ table when the extension is built, else the dict; ``host-py``: the dict."""
+    if name != 'host-py':
+        try:
+            from ..ops.native import lib
+            if hasattr(lib(), 'HostUtxo'):
+                return _NativeHostBackend()
+        except Exception:
+            pass
+    return _HostBackend()
+
+
 def default_backend() -> str:
     env = os.environ.get('UPOW_UTXO_BACKEND')
     if env:
@@ -325,8 +405,9 @@ class UtxoIndex:
         import threading
         self.lock = threading.RLock()
         self.backend_name = backend or default_backend()
-        self.be = _GpuBackend() if self.backend_name == 'gpu' else _HostBackend()
+        self.be = _GpuBackend() if self.backend_name == 'gpu' else _host_backend(self.backend_name)
         self._gpu = isinstance(self.be, _GpuBackend)
+        self._rec = self._gpu or isinstance(self.be, _NativeHostBackend)  # packed records in, no Python walk
         self.duplicates = 0  # inserts of an outpoint that was already live (skipped; a ledger bug if ever > 0)
         # deferred writes of committed blocks (a sync page's blocks, ledger/pagesync.py): applied as ONE insert
         # launch and ONE erase launch before anything else touches the index
@@ -409,7 +490,7 @@ class UtxoIndex:
         self._insert_records(recs, payload)
 
     def _insert_records(self, recs: np.ndarray, payload: Optional[np.ndarray] = None):
-        if isinstance(self.be, _GpuBackend):
+        if self._rec:
             self._dups(self.be.insert_records(recs, payload))
             return
         idx = recs[:, 32:36].copy().view(np.uint32).ravel()
@@ -424,7 +505,7 @@ class UtxoIndex:
 
     @_locked
     def lookup_records(self, recs: np.ndarray):
-        if isinstance(self.be, _GpuBackend):
+        if self._rec:
             return self.be.lookup_records(recs)
         idx = recs[:, 32:36].copy().view(np.uint32).ravel()
         return self.be.lookup([(bytes(recs[n, :32]).hex(), int(idx[n])) for n in range(len(recs))])
@@ -442,6 +523,8 @@ class UtxoIndex:
             self.be.count -= k
             self.be.tombs += k
             return out
+        if self._rec:
+            return self.be.erase_records(recs)
         if not len(recs):
             return np.zeros(0, dtype=np.uint8)
         idx = recs[:, 32:36].copy().view(np.uint32).ravel()
@@ -500,7 +583,7 @@ class UtxoIndex:
     def reset_records(self, recs: np.ndarray, payload: Optional[np.ndarray] = None):
         """Replace the whole index with packed records (snapshot restore: one H2D copy + insert launch)."""
         recs = np.ascontiguousarray(recs, dtype=np.uint8).reshape(-1, 40)
-        if isinstance(self.be, _GpuBackend):
+        if self._rec:
             self.be.reset([], [])
             if len(recs):
                 self.be.insert_records(recs, payload)
@@ -529,13 +612,12 @@ class UtxoIndex:
         tags, pay = self.lookup_records(in_keys)
         n_in = len(in_keys)
         dup_of = np.zeros(n_in, dtype=np.uint32)
-        first = {}
-        for i in range(n_in):
-            k = bytes(in_keys[i, :33])
-            if k in first:
-                dup_of[i] = first[k] + 1
-            else:
-                first[k] = i
+        if n_in > 1:  # K10: (txid, index byte) seen earlier in the block -> 1 + the first occurrence
+            k = np.ascontiguousarray(in_keys[:, :33]).view(np.dtype((np.void, 33))).ravel()
+            _, first, inv = np.unique(k, return_index=True, return_inverse=True)
+            first = first[inv.ravel()]
+            later = first != np.arange(n_in)
+            dup_of[later] = first[later] + 1
         bad = ((tags != want_tag) | (pay['len'] == 0)).astype(np.int64)
         amt = pay['amount'].astype(np.int64)
 

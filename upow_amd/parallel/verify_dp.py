@@ -52,6 +52,19 @@ def verify_records_dp(ctx: DistContext, records, device: Optional[str] = None) -
     return out
 
 
+def verify_shard_dp(ctx: DistContext, local_records, n_total: int, device: Optional[str] = None) -> np.ndarray:
+    """Like :func:`verify_records_dp` for a rank that holds the records of its own shard only
+    (``shard_bounds(n_total, world, rank)``, ledger/pagesync.py builds no others): verify them, all-gather
+    the status bytes, return the FULL status vector on every rank."""
+    buf = local_records if isinstance(local_records, np.ndarray) else np.frombuffer(bytes(local_records), np.uint8)
+    lo, hi = shard_bounds(n_total, ctx.world, ctx.rank)
+    assert buf.size == (hi - lo) * RECORD, (buf.size, lo, hi)
+    local = op.verify_records(buf, device=device) if hi > lo else np.zeros(0, np.uint8)
+    out = np.frombuffer(b''.join(ctx.all_gather_bytes(local.tobytes())), dtype=np.uint8)
+    assert out.size == n_total, (out.size, n_total)
+    return out
+
+
 def first_failure(ctx: DistContext, local_status: np.ndarray, lo: int, n_total: int) -> int:
     """All-reduce(MIN) of the first non-valid global index; ``-1`` when every signature is valid."""
     bad = np.nonzero(local_status != op.VALID)[0]
@@ -69,4 +82,4 @@ def verify_shard_first_failure(ctx: DistContext, records, device: Optional[str] 
     return first_failure(ctx, local, lo, n)
 
 
-__all__ = ['shard_bounds', 'verify_records_dp', 'first_failure', 'verify_shard_first_failure']
+__all__ = ['shard_bounds', 'verify_records_dp', 'verify_shard_dp', 'first_failure', 'verify_shard_first_failure']
