@@ -449,6 +449,9 @@ struct MismatchError : std::runtime_error {
 
 // ------------------------------------------------------------------------------------------ journal
 constexpr uint32_t kMagic = 0x314a5055;  // "UPJ1"
+// records at least this large (a block's) are written in kWriteChunk slices with the checksum computed alongside
+constexpr size_t kSplitWriteBytes = size_t(1) << 20;
+constexpr size_t kWriteChunk = size_t(1) << 20;
 struct RecHeader {
     uint32_t magic;
     uint32_t crc;       // CRC-32C over seq, block_id, meta_len, payload_len and both sections
@@ -604,6 +607,50 @@ void pwritev_all(int fd, const RecHeader& h, const std::vector<Part>& parts, off
                 w = 0;
             }
         }
+    }
+}
+
+// The body of a record (its parts, without the header) from `at`, in slices of about `chunk` bytes; with
+// `writeback`, each slice's writeback to the device is started as soon as it is in the page cache
+// (sync_file_range WRITE: no wait), so the commit's fdatasync finds most of the record already on its way.
+void pwrite_body_chunked(int fd, const std::vector<Part>& parts, off_t at, size_t chunk, bool writeback) {
+    std::vector<iovec> iov;
+    size_t pi = 0, po = 0;  // next part, offset inside it
+    while (pi < parts.size()) {
+        iov.clear();
+        size_t n = 0;
+        while (pi < parts.size() && n < chunk && iov.size() < size_t(IOV_MAX)) {
+            const std::string& pt = *parts[pi];
+            const size_t take = std::min(pt.size() - po, chunk - n);
+            if (take) iov.push_back({const_cast<char*>(pt.data() + po), take});
+            n += take;
+            po += take;
+            if (po == pt.size()) {
+                ++pi;
+                po = 0;
+            }
+        }
+        const off_t start = at;
+        size_t i = 0;
+        while (i < iov.size()) {
+            ssize_t w = ::pwritev(fd, &iov[i], int(iov.size() - i), at);
+            if (w < 0) {
+                if (errno == EINTR) continue;
+                throw std::runtime_error(std::string("journal write failed: ") + strerror(errno));
+            }
+            at += w;
+            while (w > 0 && i < iov.size()) {
+                if (size_t(w) >= iov[i].iov_len) {
+                    w -= ssize_t(iov[i].iov_len);
+                    ++i;
+                } else {
+                    iov[i].iov_base = static_cast<char*>(iov[i].iov_base) + w;
+                    iov[i].iov_len -= size_t(w);
+                    w = 0;
+                }
+            }
+        }
+        if (writeback && at > start) ::sync_file_range(fd, start, at - start, SYNC_FILE_RANGE_WRITE);
     }
 }
 
@@ -972,14 +1019,47 @@ class LedgerWriter {
     // (`before_publish`: a helper thread joined after the write and before the record is published)
     std::string write_record(Batch& b, off_t at, int64_t block_id, std::thread* before_publish = nullptr) {
         RecHeader h{kMagic, 0, b.seq, block_id, 0, b.size};
-        h.crc = record_crc_parts(h, b.parts);
+        const auto t0 = std::chrono::steady_clock::now();
         std::string werr;
-        try {
-            pwritev_all(fd_, h, b.parts, at);
-        } catch (const std::exception& e) {
-            werr = e.what();
+        auto t1 = t0;
+        if (b.size >= kSplitWriteBytes) {
+            // a block-sized record: the checksum (a pass over the whole body) runs on a helper thread while
+            // this one writes the body slice by slice, starting each slice's writeback; the header (with the
+            // checksum) goes last. Recovery reads header + body and checks the sum, as for any record.
+            uint32_t crc = 0;
+            std::thread sum([&] { crc = record_crc_parts(h, b.parts); });
+            try {
+                pwrite_body_chunked(fd_, b.parts, at + off_t(sizeof h), kWriteChunk, early_writeback_ && sync_ != SYNC_OFF);
+            } catch (const std::exception& e) {
+                werr = e.what();
+            }
+            t1 = std::chrono::steady_clock::now();
+            sum.join();
+            h.crc = crc;
+            if (werr.empty()) {
+                try {
+                    pwrite_all(fd_, reinterpret_cast<const char*>(&h), sizeof h, at);
+                } catch (const std::exception& e) {
+                    werr = e.what();
+                }
+            }
+        } else {
+            h.crc = record_crc_parts(h, b.parts);
+            t1 = std::chrono::steady_clock::now();
+            try {
+                pwritev_all(fd_, h, b.parts, at);
+            } catch (const std::exception& e) {
+                werr = e.what();
+            }
         }
+        const auto t2 = std::chrono::steady_clock::now();
         if (before_publish && before_publish->joinable()) before_publish->join();
+        const auto t3 = std::chrono::steady_clock::now();
+        auto ns = [](auto a, auto b) { return std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count(); };
+        const bool split = b.size >= kSplitWriteBytes;  // split: t0..t1 the body write, t1..t2 the rest of the sum
+        io_crc_ns_ += split ? ns(t1, t2) : ns(t0, t1);
+        io_write_ns_ += split ? ns(t0, t1) : ns(t1, t2);
+        io_undo_wait_ns_ += ns(t2, t3);
         {
             std::lock_guard<std::mutex> jl(jmu_);
             --inflight_;
@@ -1004,6 +1084,7 @@ class LedgerWriter {
         int64_t block_id;
         std::string meta;
         bool group = false;  // group commit: no per-record fdatasync (durable() syncs the prefix)
+        std::chrono::steady_clock::time_point queued = std::chrono::steady_clock::now();
     };
 
     // The journal I/O thread: deferred (block) records in submission order. The undo data is stored before
@@ -1019,6 +1100,9 @@ class LedgerWriter {
                 job = std::move(io_q_.front());
                 io_q_.pop_front();
             }
+            io_queue_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() -
+                                                                                 job.queued).count();
+            ++io_records_;
             const uint64_t seq = job.batch.seq;
             std::string err;
             // the undo record (its own file) is written alongside the journal record; both finish before
@@ -1166,6 +1250,13 @@ class LedgerWriter {
             d["fdatasyncs"] = syncs_.load();
             d["group_records"] = group_records_.load();
             d["fdatasync_s"] = sync_total_ns_.load() / 1e9;
+            // the journal I/O thread's deferred records: wait in its queue, checksum, write, wait for the undo
+            // record's writer (block records)
+            d["io_records"] = io_records_.load();
+            d["io_queue_s"] = io_queue_ns_.load() / 1e9;
+            d["io_crc_s"] = io_crc_ns_.load() / 1e9;
+            d["io_write_s"] = io_write_ns_.load() / 1e9;
+            d["io_undo_wait_s"] = io_undo_wait_ns_.load() / 1e9;
             d["shards"] = per;
             py::dict st;
             for (auto& kv : stmt_stats_) st[py::str(kv.first)] = py::make_tuple(kv.second.first / 1e9, kv.second.second);
@@ -1679,6 +1770,12 @@ class LedgerWriter {
     std::atomic<uint64_t> synced_{0};
     std::atomic<int64_t> synced_bytes_{0};
     std::atomic<int64_t> syncs_{0}, sync_total_ns_{0}, group_records_{0};
+    // UPOW_JOURNAL_EARLY_WRITEBACK=0: block records written without starting their writeback slice by slice
+    const bool early_writeback_ = [] {
+        const char* v = std::getenv("UPOW_JOURNAL_EARLY_WRITEBACK");
+        return !(v && std::string(v) == "0");
+    }();
+    std::atomic<int64_t> io_records_{0}, io_queue_ns_{0}, io_crc_ns_{0}, io_write_ns_{0}, io_undo_wait_ns_{0};
     std::map<std::string, std::pair<int64_t, int64_t>> stmt_stats_;  // sql prefix -> (ns, rows)
     // journal I/O thread (deferred block records)
     std::mutex io_mu_;

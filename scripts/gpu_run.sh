@@ -37,6 +37,7 @@
 #   verifyenv:NAME:K=V,...  verify bench (median of 3 segments) with extra environment variables
 #   soakc3pin  three pinned cluster soaks alternating with three pinned plain soaks (1,200 tx/s)
 #   clustersync  page-batched sync on a forced single-rank RCCL cluster vs plain, two interleaved pairs
+#   leanshard:N  the N-rank lean node with the page plan's key stage sharded (default) vs replicated (UPOW_SHARD_KEYS=0)
 #   sprofpage  rocprofv3 kernel trace + stats of the page-batched sync (200-tx blocks)
 #   p256ab:VARIANT  P-256 kernels: the default build vs build-ab/native-VARIANT (latency, throughput, trace, counters)
 #   isarates  issue cost of v_mad_u64_u32 / carry adds / 64-bit adds / f64 FMA / field products (scripts/isa_rates.hip)
@@ -307,6 +308,18 @@ for s in $STEPS; do
           --txs 200 --steps 1000 --warmup 5 --ledger /tmp/upow_bench_ledger > "$OUT/leansync_${N}_lean$mode.json" \
           2> "$OUT/leansync_${N}_lean$mode.err" || { tail -20 "$OUT/leansync_${N}_lean$mode.err"; exit 1; }
         grep '^{' "$OUT/leansync_${N}_lean$mode.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print({k: d.get(k) for k in ('world','value','ms_per_step','blocks_per_s','rank_cpu_ms_per_block','rank_cpu_ms_per_block_ex_p256','follower_cpu_vs_leader','lean_followers')})"
+      done ;;
+    leanshard:*)
+      # the same N-rank lean node with the page plan's key stage sharded over the ranks (default) vs replicated
+      # on every rank (UPOW_SHARD_KEYS=0)
+      N=${s#leanshard:}
+      for mode in 1 0; do
+        rm -rf /tmp/upow_bench_ledger
+        UPOW_SHARD_KEYS=$mode UPOW_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
+          --nproc-per-node "$N" --master-addr 127.0.0.1 --master-port 2958$mode bench.py --gpus "$N" --mode sync \
+          --txs 200 --steps 1000 --warmup 5 --ledger /tmp/upow_bench_ledger > "$OUT/leanshard_${N}_shard$mode.json" \
+          2> "$OUT/leanshard_${N}_shard$mode.err" || { tail -20 "$OUT/leanshard_${N}_shard$mode.err"; exit 1; }
+        grep '^{' "$OUT/leanshard_${N}_shard$mode.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print({k: d.get(k) for k in ('world','value','ms_per_step','blocks_per_s','rank_cpu_ms_per_block','rank_cpu_ms_per_block_ex_p256','follower_cpu_vs_leader','lean_followers')})"
       done ;;
     sprofpage)
       # rocprofv3 kernel trace of the page-batched sync (200-tx blocks)

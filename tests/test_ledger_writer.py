@@ -229,3 +229,56 @@ def test_hexarena_column_binds_lowercase_hex(tmp_path):
     w.close()
     got = sqlite3.connect(dbs[0]).execute('SELECT i, h FROM t ORDER BY rowid').fetchall()
     assert got == [(0, ''), (1, '00ff'), (2, bytes(range(200)).hex()), (7, bytes(range(200)).hex()), (8, '00ff')]
+
+
+@pytest.mark.parametrize('early', ['1', '0'])
+def test_block_sized_record_is_written_in_slices_and_replays(tmp_path, monkeypatch, early):
+    """A record of at least 1 MB (a block's) is written body first, in 1 MB slices whose writeback starts at
+    once, with its checksum computed alongside, and its header last. Replayed from the journal alone (fresh
+    database files) it gives the same rows; cut anywhere inside it (a crash before the header or mid-body),
+    recovery drops it and keeps the records before it."""
+    monkeypatch.setenv('UPOW_JOURNAL_EARLY_WRITEBACK', early)
+    w, dbs = _writer(tmp_path, sync_mode=3)
+    w.submit([lib().ledger_encode_stmt('CREATE TABLE IF NOT EXISTS t (x TEXT)', [], 1)], b'', -1)
+    rng = np.random.default_rng(5)
+    vals = [rng.integers(97, 123, n, dtype=np.uint8).tobytes().decode() for n in (700_000, 1_300_001, 5, 999_999)]
+    parts = [lib().ledger_encode_stmt('INSERT INTO t (x) VALUES (?)', [[v]], 1) for v in vals]
+    first = w.submit([parts[2]], b'', -1)
+    w.durable(first)
+    before = w.stats()['journal_bytes']
+    seq = w.submit(parts, _meta(9), 9, False)  # the I/O thread's split write (3 MB over four parts)
+    w.durable(seq)
+    seq2 = w.submit(parts[::-1], _meta(10), 10)  # the inline path, split too
+    w.durable(seq2)
+    w.wait(seq2)
+    st = w.stats()
+    w.close()
+    journal = str(tmp_path / 'w.journal')
+    want = [vals[2]] + vals + vals[::-1]
+    assert [r[0] for r in sqlite3.connect(dbs[0]).execute('SELECT x FROM t ORDER BY rowid')] == want
+    assert st['io_records'] >= 1 and st['io_write_s'] > 0
+    size = os.path.getsize(journal)
+
+    def replay(cut_at=None, zero_header_at=None):
+        d = tmp_path / f'replay{cut_at}{zero_header_at}'
+        d.mkdir()
+        shutil.copy(journal, d / 'w.journal')
+        if cut_at is not None:
+            with open(d / 'w.journal', 'r+b') as f:
+                f.truncate(cut_at)
+        if zero_header_at is not None:  # the body is on disk, its header is not yet
+            with open(d / 'w.journal', 'r+b') as f:
+                f.seek(zero_header_at)
+                f.write(bytes(48))
+        w2, dbs2 = _writer(d, sync_mode=3)
+        w2.wait(w2.stats()['submitted'], -1, 60.0)
+        rows = [r[0] for r in sqlite3.connect(dbs2[0]).execute('SELECT x FROM t ORDER BY rowid')]
+        jb = w2.stats()['journal_bytes']
+        w2.close()
+        return rows, jb
+
+    assert replay() == (want, size)
+    rows, jb = replay(cut_at=before + 1_500_000)  # mid-body of the deferred record
+    assert rows == [vals[2]] and jb == before
+    rows, jb = replay(zero_header_at=before)
+    assert rows == [vals[2]] and jb == before

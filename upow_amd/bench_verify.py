@@ -547,6 +547,7 @@ async def _run(args, ctx, device, utxo_backend):
         ru = resource.getrusage(resource.RUSAGE_SELF)
         return {'t': time.perf_counter(), 'submitted': w['submitted'], 'applied': w['applied'],
                 'throttle_s': w['throttle_s'], 'fdatasync_s': w['fdatasync_s'],
+                'io': [w.get(k, 0.0) for k in ('io_queue_s', 'io_crc_s', 'io_write_s', 'io_undo_wait_s')],
                 'apply': [sh['apply_s'] for sh in w['shards']], 'commit': [sh['commit_s'] for sh in w['shards']],
                 'cpu_s': ru.ru_utime + ru.ru_stime, 'nivcsw': ru.ru_nivcsw, 'write_mb': _io_write_mb()}
 
@@ -578,6 +579,9 @@ async def _run(args, ctx, device, utxo_backend):
             wall = w1['t'] - w0['t']
             d.update({'throttle_ms': round((w1['throttle_s'] - w0['throttle_s']) * 1000, 2),
                       'fdatasync_ms_per_block': round((w1['fdatasync_s'] - w0['fdatasync_s']) * 1000 / nb, 3),
+                      # the journal I/O thread per block: queue wait, checksum, write, undo-writer wait
+                      'journal_io_ms_per_block': dict(zip(('queue', 'crc', 'write', 'undo_wait'),
+                                                          [round((b - a) * 1000 / nb, 3) for a, b in zip(w0['io'], w1['io'])])),
                       'materialiser_busy_ms_per_block': [round(a + c, 2) for a, c in zip(ap, cm)],
                       'materialiser_apply_ms_per_block': round(max(ap[1:] or ap), 2),
                       'materialiser_commit_ms_per_block': round(max(cm[1:] or cm), 2),
