@@ -639,6 +639,8 @@ async def _log_utxo_hash(database, block_no: int):
 
 
 SNAPSHOT_EVERY = int(os.environ.get('UPOW_SNAPSHOT_EVERY', '1000'))
+# UPOW_SNAPSHOT_ASYNC=0: the periodic snapshot sorts, hashes and writes on the block path (A/B)
+SNAPSHOT_ASYNC = os.environ.get('UPOW_SNAPSHOT_ASYNC', '1') != '0'
 
 
 def _maybe_snapshot(database, block_no: int):
@@ -648,7 +650,10 @@ def _maybe_snapshot(database, block_no: int):
         return
     try:
         from . import snapshot
-        snapshot.save(database)
+        res = snapshot.save(database, background=SNAPSHOT_ASYNC)
+        if res is not None and SNAPSHOT_ASYNC:  # a failure of the background write is logged when it happens
+            res.add_done_callback(lambda f: f.exception() and logger.error(
+                f'UTXO snapshot at block {block_no} failed: {f.exception()}'))
     except Exception as e:
         logger.error(f'UTXO snapshot at block {block_no} failed: {e}')
 

@@ -43,18 +43,58 @@ def _tip(db):
     return (int(row['id']), row['hash']) if row else (0, '')
 
 
-def save(db, path: Optional[str] = None) -> dict:
-    """Write the index at the current tip. Returns the header."""
+_POOL = None
+_pending = None  # the background save in flight (a Future), if any
+
+
+def save(db, path: Optional[str] = None, background: bool = False):
+    """Write the index at the current tip. Returns the header; with ``background`` the Future of it (None when
+    skipped).
+
+    Only the dump of the index (one D2H copy on the GPU backend) happens under the ledger's lock, at the tip
+    it is taken for; the canonical sort, the K12 hash of those very records, the checksum and the file write
+    follow on the caller's thread or, with ``background``, on a snapshot thread, so the block path does not
+    wait for them (a 5 M-outpoint index is ~600 MB to sort, hash and write). A background save finding the
+    previous one still running is skipped: the next period takes it."""
+    global _POOL, _pending
     path = path or default_path(db)
     if path is None:
         raise ValueError('in-memory ledger: give an explicit snapshot path')
+    if background and _pending is not None and not _pending.done():
+        return None
     with db.lock:
         height, tip = _tip(db)
-        recs, pay = db.utxo.records_payload()
+        recs, pay = db.utxo.records_payload(sort=False)
+    if not background:
+        return _write(path, height, tip, recs, pay)
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix='upow-snapshot')
+    _pending = _POOL.submit(_write, path, height, tip, recs, pay)  # fresh arrays of the dump: no copy
+    return _pending
+
+
+def wait_pending(timeout: Optional[float] = None):
+    """The background save in flight, finished (its header), or None when there is none."""
+    f = _pending
+    return f.result(timeout) if f is not None else None
+
+
+def _k12(recs: np.ndarray) -> str:
+    """K12 (reference database.py:827-830) of canonically ordered records: SHA-256 over (txid || index byte)
+    of the unspent_outputs entries — what ``UtxoIndex.set_hash`` gives for the same index."""
+    tags = recs[:, 36:40].copy().view(np.uint32).ravel()
+    m = recs[tags == TAG_BY_TABLE['unspent_outputs']]
+    return hashlib.sha256(np.ascontiguousarray(np.concatenate([m[:, :32], m[:, 32:33]], axis=1)).tobytes()).hexdigest()
+
+
+def _write(path: str, height: int, tip: str, recs: np.ndarray, pay: np.ndarray) -> dict:
+    from .utxo import sort_order
+    order = sort_order(np.ascontiguousarray(recs))
+    recs, pay = np.ascontiguousarray(recs[order]), np.ascontiguousarray(pay[order])
     payload = recs.tobytes() + pay.tobytes()
     header = {'magic': MAGIC, 'version': VERSION, 'height': height, 'tip_hash': tip, 'count': int(len(recs)),
-              'utxo_hash': db.utxo.set_hash(TAG_BY_TABLE['unspent_outputs']),
-              'payload_sha256': hashlib.sha256(payload).hexdigest()}
+              'utxo_hash': _k12(recs), 'payload_sha256': hashlib.sha256(payload).hexdigest()}
     tmp = path + '.tmp'
     with open(tmp, 'wb') as f:
         f.write(json.dumps(header, separators=(',', ':')).encode() + b'\n')
@@ -136,4 +176,4 @@ def verify(db) -> dict:
             'mismatched_tables': mismatched, 'payload_mismatches': bad_payload, 'entries': int(len(recs))}
 
 
-__all__ = ['save', 'read', 'try_restore', 'verify', 'default_path']
+__all__ = ['save', 'wait_pending', 'read', 'try_restore', 'verify', 'default_path']

@@ -573,9 +573,12 @@ class UtxoIndex:
         return recs, pay, int(pay['amount'].sum()) if len(pay) else 0
 
     @_locked
-    def records_payload(self):
-        """(records, payloads) of every live entry, in canonical (txid, index) order."""
+    def records_payload(self, sort: bool = True):
+        """(records, payloads) of every live entry, in canonical (txid, index) order (``sort=False``: in the
+        backend's own order, for a caller that sorts later off the ledger's critical path)."""
         recs, pay = self.be.records_payload()
+        if not sort:
+            return recs, pay
         order = sort_order(np.ascontiguousarray(recs))
         return np.ascontiguousarray(recs[order]), np.ascontiguousarray(pay[order])
 
