@@ -1661,13 +1661,14 @@ class LedgerWriter {
         Shard& sh = *shards_[i];
         pthread_setname_np(pthread_self(), ("upow-wr-" + std::to_string(i)).c_str());
         // materialising is background work: below the block path and the HTTP loop in the CPU share the
-        // process gets (GPU boxes run a node under a CPU quota far below the core count)
-        if (const char* nv = std::getenv("UPOW_WRITER_NICE")) {
-            const int n = std::atoi(nv);
-            if (n > 0) setpriority(PRIO_PROCESS, pid_t(syscall(SYS_gettid)), n);
-        } else {
-            setpriority(PRIO_PROCESS, pid_t(syscall(SYS_gettid)), 5);
-        }
+        // process gets (GPU boxes run a node under a CPU quota far below the core count). Ten materialisers
+        // keep ~10 cores busy behind a stream of 2 MB blocks; at nice 19 (CFS weight 15 against the block
+        // path's 1024) they take what the block path leaves: the verify bench ran at 732-820 k tx/s against
+        // 638-730 k at nice 5 in three interleaved pairs on one box (profiles/r6/writer_nice/). The writer's
+        // queue bound (UPOW_WRITER_MAX_QUEUE_MB) still holds blocks back if they fall too far behind.
+        int nice_level = 19;
+        if (const char* nv = std::getenv("UPOW_WRITER_NICE")) nice_level = std::atoi(nv);
+        if (nice_level > 0) setpriority(PRIO_PROCESS, pid_t(syscall(SYS_gettid)), std::min(nice_level, 19));
         for (;;) {
             std::vector<Batch> group;
             {
