@@ -70,7 +70,7 @@ def test_periodic_snapshot_is_written_off_the_block_path(tmp_path, monkeypatch):
     async def go():
         path = tmp_path / 'ledger.sqlite3'
         db = await _chain(path)  # block 5 takes the periodic snapshot
-        hdr = snapshot.wait_pending(60)
+        hdr = snapshot.wait_pending(60, snapshot.default_path(db))
         assert hdr is not None and hdr['height'] == 5 and hdr['utxo_hash'] == await db.get_unspent_outputs_hash()
         bg = open(snapshot.default_path(db), 'rb').read()
         sync_hdr = snapshot.save(db)

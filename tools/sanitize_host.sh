@@ -17,7 +17,7 @@
 #    twice, which ASan reports as an ODR violation before the first input.
 # 3. The whole native extension built instrumented (python -m upow_amd._build --variant asan|tsan) and
 #    loaded by an interpreter linked with the same runtime (tools/pysan.c, UPOW_NATIVE_SO): the Python
-#    tests of every pybind11 module run under ASan + UBSan (txcodec, jsonspan, http_wire, mempool_index,
+#    tests of every pybind11 module run under ASan + UBSan (txcodec, jsonspan, http_wire, mempool_index, utxo_host,
 #    ledger_writer, gov_index, log_appender, the block path) and the threaded ones under TSan
 #    (mempool index lookups racing a GIL-free confirm, the journal writer's I/O and materialiser threads,
 #    the log appender's writer thread).
@@ -115,7 +115,7 @@ UPOW_NATIVE_SO=$ROOT/build/native-asan/_native$EXT ASAN_OPTIONS=detect_leaks=0:d
   UBSAN_OPTIONS=print_stacktrace=1 timeout -k 10 1500 "$OUT/pysan_asan" -m pytest -q -x -m "not gpu" -p no:cacheprovider \
   tests/test_txcodec.py tests/test_hexspans.py tests/test_http_server.py tests/test_mempool_index.py tests/test_ledger_writer.py \
   tests/test_gov_cascade.py tests/test_log_appender.py tests/test_fastpath.py tests/test_fastpath_governance.py \
-  tests/test_rollback_undo.py tests/test_crash_recovery.py tests/test_process_tuning.py > "$OUT/pytest_asan.log" 2>&1 \
+  tests/test_rollback_undo.py tests/test_crash_recovery.py tests/test_process_tuning.py tests/test_utxo.py > "$OUT/pytest_asan.log" 2>&1 \
   || { tail -60 "$OUT/pytest_asan.log"; exit 1; }
 echo "python tests under ASan + UBSan: $(tail -1 "$OUT/pytest_asan.log")"
 UPOW_NATIVE_SO=$ROOT/build/native-tsan/_native$EXT TSAN_OPTIONS=halt_on_error=1:report_signal_unsafe=0 \

@@ -44,7 +44,7 @@ def _tip(db):
 
 
 _POOL = None
-_pending = None  # the background save in flight (a Future), if any
+_pending: dict = {}  # snapshot path -> the background save in flight (a Future)
 
 
 def save(db, path: Optional[str] = None, background: bool = False):
@@ -56,11 +56,12 @@ def save(db, path: Optional[str] = None, background: bool = False):
     follow on the caller's thread or, with ``background``, on a snapshot thread, so the block path does not
     wait for them (a 5 M-outpoint index is ~600 MB to sort, hash and write). A background save finding the
     previous one still running is skipped: the next period takes it."""
-    global _POOL, _pending
+    global _POOL
     path = path or default_path(db)
     if path is None:
         raise ValueError('in-memory ledger: give an explicit snapshot path')
-    if background and _pending is not None and not _pending.done():
+    prev = _pending.get(path)
+    if background and prev is not None and not prev.done():
         return None
     with db.lock:
         height, tip = _tip(db)
@@ -70,14 +71,18 @@ def save(db, path: Optional[str] = None, background: bool = False):
     if _POOL is None:
         from concurrent.futures import ThreadPoolExecutor
         _POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix='upow-snapshot')
-    _pending = _POOL.submit(_write, path, height, tip, recs, pay)  # fresh arrays of the dump: no copy
-    return _pending
+    fut = _pending[path] = _POOL.submit(_write, path, height, tip, recs, pay)  # fresh arrays of the dump: no copy
+    return fut
 
 
-def wait_pending(timeout: Optional[float] = None):
-    """The background save in flight, finished (its header), or None when there is none."""
-    f = _pending
-    return f.result(timeout) if f is not None else None
+def wait_pending(timeout: Optional[float] = None, path: Optional[str] = None):
+    """The last background save (of ``path``, or of any ledger), finished: its header, or None when there was
+    none."""
+    futs = [_pending[path]] if path in _pending else ([] if path else list(_pending.values()))
+    out = None
+    for f in futs:
+        out = f.result(timeout)
+    return out
 
 
 def _k12(recs: np.ndarray) -> str:
