@@ -26,6 +26,10 @@ reached; then the log is cleared. It runs
     window, a deep status audit, and a block the native path hands to the object path (that path resolves
     inputs from the SQL transactions table). The block being validated then continues in full mode.
 
+Size: the log holds the raw ops since the last materialisation, about the raw size of those blocks (a full
+replica's SQL files hold three to four times that); a long-running follower's restart replays all of it, so an
+operator can materialise a follower at a quiet time with ``python -m upow_amd.tools materialise``.
+
 Durability: the leader is the durable copy. The op log is written (page cache) before an op is applied and
 fdatasync'd at status / quit / every ``SYNC_BYTES``; a torn tail is dropped on open (record lengths, and a
 CRC over each record's header and the first and last 4 KB of its body). A replayed op is validated in full
@@ -139,7 +143,7 @@ class OpLog:
                 if kind == KIND_TIP:
                     prev = recs[k][1]
                 continue
-            nxt = next((r for r in recs[k + 1:] if r[0] == KIND_TIP or r[0] == KIND_OP), None)
+            nxt = recs[k + 1] if k + 1 < len(recs) else None  # every record is an op or a tip marker
             if nxt is not None and nxt[0] == KIND_TIP and nxt[1] == prev:
                 continue
             yield self.read(off, n)
