@@ -237,9 +237,41 @@ static py::dict decode_views(const std::vector<const char*>& srcp, const std::ve
     if (txs.size() < N) txs.resize(N);
     const bool prof = std::getenv("UPOW_TXCODEC_PROFILE") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
+    // each decoding thread also writes its txs' sizes and scalars into one contiguous array: the serial passes
+    // below (segment starts, arena offsets, the hex list) read that instead of every tx's scattered buffers
+    struct TxSum {
+        uint8_t flag, version, tx_type, grouped, canonical, upper_hex;
+        int32_t n_in, n_out, n_sig, signed_len, msg_off, msg_len, canon, ajson, mjson, addr_bytes;
+    };
+    std::vector<TxSum> sum(N);
     {
         py::gil_scoped_release rel;
-        parallel_for(n, threads, [&](int64_t i) { decode_one(srcp[size_t(i)], srcl[size_t(i)], txs[size_t(i)]); });
+        parallel_for(n, threads, [&](int64_t i) {
+            {
+                DecTx& t = txs[size_t(i)];
+                decode_one(srcp[size_t(i)], srcl[size_t(i)], t);
+                TxSum& u = sum[size_t(i)];
+                u.flag = t.flag;
+                u.version = t.version;
+                u.tx_type = t.tx_type;
+                u.grouped = t.grouped;
+                u.canonical = t.canonical;
+                u.upper_hex = t.upper_hex;
+                u.n_in = int32_t(t.ins.size());
+                u.n_out = int32_t(t.outs.size());
+                u.n_sig = int32_t(t.sigs.size() / 64);
+                u.signed_len = t.signed_len;
+                u.msg_off = t.msg_off;
+                u.msg_len = t.msg_len;
+                u.canon = int32_t(t.canon.size());
+                u.ajson = int32_t(t.out_addr_json.size());
+                u.mjson = int32_t(t.out_amount_json.size());
+                int32_t ab = 0;  // the address strings exist for the fast-path form only
+                if (t.flag == TX_FAST)
+                    for (size_t j = 0; j < t.outs.size() && j < t.out_addr.size(); ++j) ab += int32_t(t.out_addr[j].size());
+                u.addr_bytes = ab;
+            }
+        });
     }
     auto t1 = std::chrono::steady_clock::now();
     py::dict d;
@@ -249,7 +281,7 @@ static py::dict decode_views(const std::vector<const char*>& srcp, const std::ve
     int64_t n_in = 0, n_out = 0, n_sig = 0;
     bool all_fast = true;
     for (int64_t i = 0; i < n; ++i) {
-        const DecTx& t = txs[size_t(i)];
+        const TxSum& t = sum[size_t(i)];
         flags[size_t(i)] = t.flag;
         all_fast &= t.flag == TX_FAST;
         version[size_t(i)] = t.version;
@@ -258,13 +290,13 @@ static py::dict decode_views(const std::vector<const char*>& srcp, const std::ve
         in_start[size_t(i)] = int32_t(n_in);
         out_start[size_t(i)] = int32_t(n_out);
         sig_start[size_t(i)] = int32_t(n_sig);
-        n_in += int64_t(t.ins.size());
-        n_out += int64_t(t.outs.size());
-        n_sig += int64_t(t.sigs.size() / 64);
+        n_in += t.n_in;
+        n_out += t.n_out;
+        n_sig += t.n_sig;
         signed_len[size_t(i)] = t.signed_len;
         msg_off[size_t(i)] = t.msg_off;
         msg_len[size_t(i)] = t.msg_len;
-        hex_len[size_t(i)] = int32_t(2 * t.canon.size());
+        hex_len[size_t(i)] = 2 * t.canon;
     }
     in_start[size_t(n)] = int32_t(n_in);
     out_start[size_t(n)] = int32_t(n_out);
@@ -291,10 +323,12 @@ static py::dict decode_views(const std::vector<const char*>& srcp, const std::ve
     // The merkle root (a sort of the canonical bytes, then one SHA-256 over the txids) runs on its own
     // thread while the pool fills the flat columns below (both only read `txs`) and beyond: the job owns
     // the thread and the workspace (an exception below joins it in the job's destructor).
+    auto tM0 = std::chrono::steady_clock::now();
     {
         MerkleJob* j = job.get();
         j->th = std::thread([j, &txs, N] { j->root = merkle_of(txs, N); });
     }
+    auto tM1 = std::chrono::steady_clock::now();
     // Every column is filled in place inside its final Python bytes object (allocated here, with the GIL;
     // written by the pool without it): no staging vector and no copy on the way out.
     auto pyb = [](size_t len, char*& p) {
@@ -333,27 +367,31 @@ static py::dict decode_views(const std::vector<const char*>& srcp, const std::ve
     uint64_t* out_amount = reinterpret_cast<uint64_t*>(c_out_amount);
     // text arenas (offsets serial and cheap, blobs filled in parallel): output address strings, the two
     // per-tx JSON columns, and the canonical tx bytes (the stored tx_hex column, hex-rendered by the writer)
-    std::vector<int64_t> addr_off(NO + 1), ajson_off(N + 1), mjson_off(N + 1), canon_off(N + 1);
-    addr_off[0] = ajson_off[0] = mjson_off[0] = canon_off[0] = 0;
+    // per-tx arena offsets from the summary; the per-output address offsets are written by the fill pass
+    std::vector<int64_t> addr_base(N + 1), ajson_off(N + 1), mjson_off(N + 1), canon_off(N + 1);
+    addr_base[0] = ajson_off[0] = mjson_off[0] = canon_off[0] = 0;
     for (size_t i = 0; i < N; ++i) {
-        const DecTx& t = txs[i];
-        size_t o = size_t(out_start[i]);
-        for (size_t j = 0; j < t.outs.size(); ++j, ++o) addr_off[o + 1] = addr_off[o] + int64_t(t.out_addr[j].size());
-        ajson_off[i + 1] = ajson_off[i] + int64_t(t.out_addr_json.size());
-        mjson_off[i + 1] = mjson_off[i] + int64_t(t.out_amount_json.size());
-        canon_off[i + 1] = canon_off[i] + int64_t(t.canon.size());
+        const TxSum& t = sum[i];
+        addr_base[i + 1] = addr_base[i] + t.addr_bytes;
+        ajson_off[i + 1] = ajson_off[i] + t.ajson;
+        mjson_off[i + 1] = mjson_off[i] + t.mjson;
+        canon_off[i + 1] = canon_off[i] + t.canon;
     }
     auto offs = [](const std::vector<int64_t>& v) {
         return py::bytes(reinterpret_cast<const char*>(v.data()), v.size() * 8);
     };
-    char *addr_blob, *ajson_blob, *mjson_blob, *canon_blob;
-    d["out_addr_str"] = py::make_tuple(pyb(size_t(addr_off[NO]), addr_blob), offs(addr_off));
+    char *addr_blob, *ajson_blob, *mjson_blob, *canon_blob, *addr_off_p;
+    py::bytes addr_off_b = pyb((NO + 1) * 8, addr_off_p);
+    int64_t* addr_off = reinterpret_cast<int64_t*>(addr_off_p);
+    addr_off[0] = 0;
+    d["out_addr_str"] = py::make_tuple(pyb(size_t(addr_base[N]), addr_blob), addr_off_b);
     d["out_addr_json"] = py::make_tuple(pyb(size_t(ajson_off[N]), ajson_blob), offs(ajson_off));
     d["out_amount_json"] = py::make_tuple(pyb(size_t(mjson_off[N]), mjson_blob), offs(mjson_off));
     d["canon"] = py::make_tuple(pyb(size_t(canon_off[N]), canon_blob), offs(canon_off));
+    auto tF0 = std::chrono::steady_clock::now();
     {
         py::gil_scoped_release rel;
-        parallel_for_grain(n, threads, 512, [&](int64_t ii) {  // a few small copies per tx
+        auto fill_one = [&](int64_t ii) {  // a few small copies per tx
             const size_t i = size_t(ii);
             const DecTx& t = txs[i];
             std::memcpy(&txid[32 * i], t.txid, 32);
@@ -380,6 +418,7 @@ static py::dict decode_views(const std::vector<const char*>& srcp, const std::ve
                 for (size_t g = 0; g < t.sigs.size() / 64; ++g) sig_first_in[size_t(sig_start[i]) + g] = -1;
             if (!t.sigs.empty()) std::memcpy(&sigs[64 * size_t(sig_start[i])], t.sigs.data(), t.sigs.size());
             size_t o = size_t(out_start[i]);
+            int64_t a = addr_base[i];
             for (size_t j = 0; j < t.outs.size(); ++j, ++o) {
                 std::memset(&out_addr[64 * o], 0, 64);
                 std::memcpy(&out_addr[64 * o], t.outs[j].addr, t.outs[j].len);
@@ -387,12 +426,15 @@ static py::dict decode_views(const std::vector<const char*>& srcp, const std::ve
                 out_type[o] = t.outs[j].type;
                 out_amount[o] = t.outs[j].amount;
                 out_tx[o] = int32_t(i);
-                std::memcpy(addr_blob + addr_off[o], t.out_addr[j].data(), t.out_addr[j].size());
+                std::memcpy(addr_blob + a, t.out_addr[j].data(), t.out_addr[j].size());
+                a += int64_t(t.out_addr[j].size());
+                addr_off[o + 1] = a;
             }
             std::memcpy(ajson_blob + ajson_off[i], t.out_addr_json.data(), t.out_addr_json.size());
             std::memcpy(mjson_blob + mjson_off[i], t.out_amount_json.data(), t.out_amount_json.size());
             std::memcpy(canon_blob + canon_off[i], t.canon.data(), t.canon.size());
-        });
+        };
+        parallel_for_grain(n, threads, 512, fill_one);
     }
     // the stored hex column as str objects (object-path parity, mempool and cluster mirroring): the input
     // string is reused when it already is the canonical lowercase hex of the tx
@@ -400,12 +442,13 @@ static py::dict decode_views(const std::vector<const char*>& srcp, const std::ve
     if (hexes) {
         py::list canon_hex = new_list(N);
         for (size_t i = 0; i < N; ++i) {
-            const DecTx& t = txs[i];
-            if (t.canonical && !t.upper_hex && srcl[i] == 2 * t.canon.size()) {
+            const TxSum& u = sum[i];
+            if (u.canonical && !u.upper_hex && srcl[i] == 2 * size_t(u.canon)) {
                 PyObject* obj = PyList_GET_ITEM(hexes, Py_ssize_t(i));
                 Py_INCREF(obj);
                 PyList_SET_ITEM(canon_hex.ptr(), Py_ssize_t(i), obj);
             } else {
+                const DecTx& t = txs[i];
                 const std::string h = to_hex(t.canon.data(), t.canon.size());
                 PyList_SET_ITEM(canon_hex.ptr(), Py_ssize_t(i), ascii_str(h.data(), h.size()));
             }
@@ -414,8 +457,9 @@ static py::dict decode_views(const std::vector<const char*>& srcp, const std::ve
     } else {
         py::list fix;
         for (size_t i = 0; i < N; ++i) {
+            const TxSum& u = sum[i];
+            if (u.canonical && !u.upper_hex && srcl[i] == 2 * size_t(u.canon)) continue;
             const DecTx& t = txs[i];
-            if (t.canonical && !t.upper_hex && srcl[i] == 2 * t.canon.size()) continue;
             const std::string h = to_hex(t.canon.data(), t.canon.size());
             fix.append(py::make_tuple(int64_t(i), py::reinterpret_steal<py::object>(ascii_str(h.data(), h.size()))));
         }
@@ -426,8 +470,9 @@ static py::dict decode_views(const std::vector<const char*>& srcp, const std::ve
     d["merkle_job"] = job;
     if (prof) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        std::fprintf(stderr, "[txcodec] decode %.2f ms, columns %.2f ms (fill %.2f, hex list %.2f)\n", ms(t0, t1),
-                     ms(t1, t2), ms(t1, tA), ms(tA, tB));
+        std::fprintf(stderr, "[txcodec] decode %.2f ms, columns %.2f ms (fill %.2f [head %.2f, merkle spawn %.2f, "
+                     "alloc %.2f, copies %.2f], hex list %.2f)\n", ms(t0, t1), ms(t1, t2), ms(t1, tA), ms(t1, tM0),
+                     ms(tM0, tM1), ms(tM1, tF0), ms(tF0, tA), ms(tA, tB));
     }
     return d;
 }
