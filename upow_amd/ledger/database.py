@@ -930,12 +930,18 @@ class Database:
 
     def _split_target(self, sql: str) -> Optional[str]:
         """The split table a write statement targets (None: an ordinary table, or ``transactions`` of a
-        ledger that keeps it in the main file)."""
+        ledger that keeps it in the main file). Memoised per statement text: the block path encodes the same
+        handful of statements for every block."""
+        cache = self.__dict__.setdefault('_split_cache', {})
+        hit = cache.get(sql, cache)
+        if hit is not cache:
+            return hit
         m = self._SPLIT_INSERT.match(sql) or self._SPLIT_TARGET.match(sql)
-        if m is None:
-            return None
-        t = m.group(2).lower()
-        return t if t in self._routed else None
+        t = None if m is None else m.group(2).lower()
+        t = t if t in self._routed else None
+        if len(cache) < 4096:
+            cache[sql] = t
+        return t
 
     def _utxo_rowids(self, n: int) -> int:
         """First of ``n`` consecutive row ids from the ledger-wide UTXO counter."""
