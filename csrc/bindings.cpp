@@ -338,6 +338,11 @@ PYBIND11_MODULE(_native, m) {
     m.def("utxo_create", &utxo_create);
     m.def("utxo_destroy", &utxo_destroy);
     m.def("utxo_capacity", &utxo_capacity);
+    m.def("utxo_rehash", [](int64_t h, uint32_t log2_cap) {
+        uint64_t r;
+        { py::gil_scoped_release rel; r = utxo_rehash(h, log2_cap); }
+        return py::make_tuple(uint32_t(r), uint32_t(r >> 32));  // (entries moved, no free slot)
+    });
     m.def("utxo_insert", [recs_arg](int64_t h, py::buffer recs, py::object payload) {
         int64_t n; const uint8_t* p = recs_arg(recs, n);
         const uint8_t* pp = nullptr;

@@ -81,6 +81,7 @@ bool p256_sign(const uint8_t d_be[32], const uint8_t digest[32], uint8_t r_le[32
 int64_t utxo_create(uint32_t log2_cap);
 void utxo_destroy(int64_t h);
 uint32_t utxo_capacity(int64_t h);
+uint64_t utxo_rehash(int64_t h, uint32_t log2_cap);  // #moved | (#no slot << 32)
 // payload records: 80 bytes {u64 amount, u32 address length, u32 pad, address[64]} (nullptr = zeros)
 uint64_t utxo_insert(int64_t h, const uint8_t* recs, int64_t n, const uint8_t* payload);  // #full | (#duplicates << 32)
 std::vector<uint8_t> utxo_probe(int64_t h, const uint8_t* recs, int64_t n);  // tag or 0xff

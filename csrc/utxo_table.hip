@@ -94,15 +94,12 @@ __device__ __forceinline__ uint32_t addr_fingerprint(const uint8_t* addr) { retu
 // walks the chain again. counter[0] counts entries that found no slot (table full).
 // Lanes of one launch never insert the same outpoint twice (block validation rejects duplicate inputs,
 // hence duplicate txids), so the chain walk only has to see entries published by earlier launches.
-__global__ __launch_bounds__(256) void utxo_insert_kernel(UtxoSlot* __restrict__ tab, UtxoPayload* __restrict__ pay,
-                                                          uint32_t mask, const UtxoKeyRec* __restrict__ recs,
-                                                          const UtxoPayload* __restrict__ in_pay, int64_t n,
-                                                          uint32_t* __restrict__ counter) {
-    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint32_t k[8];
-    load_key(recs[i], k);
-    const uint32_t idx = recs[i].index & 0xffu, tag = recs[i].tag & 0xffu;
+// one entry into the table (the insert kernel's lane body, shared with the rehash): `p` = its payload or
+// nullptr, `fp` = its owner fingerprint
+__device__ __forceinline__ void insert_one(UtxoSlot* __restrict__ tab, UtxoPayload* __restrict__ pay, uint32_t mask,
+                                           const uint32_t k[8], uint32_t idx, uint32_t tag,
+                                           const UtxoPayload* __restrict__ p, uint32_t fp,
+                                           uint32_t* __restrict__ counter) {
     const uint32_t home = slot_hash(k, idx) & mask;
     for (int attempt = 0; attempt < 64; ++attempt) {
         uint32_t s = home, free_slot = 0xffffffffu, free_meta = 0;
@@ -125,19 +122,48 @@ __global__ __launch_bounds__(256) void utxo_insert_kernel(UtxoSlot* __restrict__
         if (atomicCAS(mp, free_meta, ST_BUSY) != free_meta) continue;  // lost the race: walk again
 #pragma unroll
         for (int w = 0; w < 8; ++w) tab[free_slot].k[w] = k[w];
-        if (in_pay) {
-            pay[free_slot] = in_pay[i];
-            tab[free_slot].pad[0] = addr_fingerprint(in_pay[i].addr);
+        if (p) {
+            pay[free_slot] = *p;
         } else {
             UtxoPayload z{};
             pay[free_slot] = z;
-            tab[free_slot].pad[0] = 0;
         }
+        tab[free_slot].pad[0] = fp;
         __threadfence();
         atomicExch(mp, ST_FULL | (idx << 8) | (tag << 16));
         return;
     }
     atomicAdd(counter, 1u);
+}
+
+__global__ __launch_bounds__(256) void utxo_insert_kernel(UtxoSlot* __restrict__ tab, UtxoPayload* __restrict__ pay,
+                                                          uint32_t mask, const UtxoKeyRec* __restrict__ recs,
+                                                          const UtxoPayload* __restrict__ in_pay, int64_t n,
+                                                          uint32_t* __restrict__ counter) {
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t k[8];
+    load_key(recs[i], k);
+    const uint32_t idx = recs[i].index & 0xffu, tag = recs[i].tag & 0xffu;
+    insert_one(tab, pay, mask, k, idx, tag, in_pay ? &in_pay[i] : nullptr, in_pay ? addr_fingerprint(in_pay[i].addr) : 0u,
+               counter);
+}
+
+// Rehash: one lane per slot of the old table; a live entry goes into the new table with its payload and its
+// owner fingerprint as they are (tombstones and empty slots are dropped)
+__global__ __launch_bounds__(256) void utxo_migrate_kernel(const UtxoSlot* __restrict__ old_tab,
+                                                           const UtxoPayload* __restrict__ old_pay, uint32_t old_cap,
+                                                           UtxoSlot* __restrict__ tab, UtxoPayload* __restrict__ pay,
+                                                           uint32_t mask, uint32_t* __restrict__ counter) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= old_cap) return;
+    const uint32_t m = old_tab[s].meta;
+    if ((m & 3u) != ST_FULL) return;
+    uint32_t k[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) k[w] = old_tab[s].k[w];
+    insert_one(tab, pay, mask, k, (m >> 8) & 0xffu, (m >> 16) & 0xffu, &old_pay[s], old_tab[s].pad[0], counter);
+    atomicAdd(counter + 2, 1u);
 }
 
 // tags_out[i] = tag of the outpoint, 0xff when absent
@@ -477,6 +503,42 @@ void utxo_destroy(int64_t h) {
     (void)hipFree(it->second.pay);
     (void)hipFree(it->second.d_counter);
     g_tables.erase(it);
+}
+
+// Rebuild the table at capacity 2^log2_cap on the device (growth, or the same size to drop tombstones): the
+// live entries move from the old arrays into fresh ones in one launch, no host round trip (the dump + host
+// re-insert it replaces moved the whole set over PCIe twice: ~0.5 GB at 5 M outpoints). Queued on the node
+// stream behind any pending async apply, so the handle stays valid throughout. Returns (live entries moved) |
+// (entries that found no slot << 32).
+uint64_t utxo_rehash(int64_t h, uint32_t log2_cap) {
+    if (log2_cap < 8 || log2_cap > 31) throw std::invalid_argument("log2 capacity must be in [8, 31]");
+    std::lock_guard<std::mutex> lk(g_ut_mu);
+    UtxoTableDev& t = table(h);
+    const uint32_t cap = 1u << log2_cap;
+    UtxoSlot* tab = nullptr;
+    UtxoPayload* pay = nullptr;
+    uck(hipMalloc(&tab, sizeof(UtxoSlot) * size_t(cap)), "hipMalloc utxo table (rehash)");
+    try {
+        uck(hipMalloc(&pay, sizeof(UtxoPayload) * size_t(cap)), "hipMalloc utxo payload (rehash)");
+    } catch (...) {
+        (void)hipFree(tab);
+        throw;
+    }
+    node_memset(tab, 0, sizeof(UtxoSlot) * size_t(cap), "memset utxo table (rehash)");
+    node_memset(pay, 0, sizeof(UtxoPayload) * size_t(cap), "memset utxo payload (rehash)");
+    PooledBuf<uint32_t> cnt(4);
+    node_memset(cnt.p, 0, 4 * sizeof(uint32_t), "memset");
+    hipLaunchKernelGGL(utxo_migrate_kernel, dim3(int((t.cap + 255) / 256)), dim3(256), 0, node_stream(), t.tab, t.pay,
+                       t.cap, tab, pay, cap - 1, cnt.p);
+    uck(hipGetLastError(), "utxo_migrate_kernel");
+    uint32_t c[4] = {0, 0, 0, 0};
+    node_d2h(c, cnt.p, sizeof c, "d2h rehash counters");  // synchronises the node stream: the old arrays are idle
+    (void)hipFree(t.tab);
+    (void)hipFree(t.pay);
+    t.tab = tab;
+    t.pay = pay;
+    t.cap = cap;
+    return uint64_t(c[2] - c[0]) | (uint64_t(c[0]) << 32);
 }
 
 uint32_t utxo_capacity(int64_t h) {
