@@ -141,6 +141,12 @@ public:
         stream_check(hipMemcpyAsync(at, src, n, hipMemcpyDeviceToHost, node_stream()), "staged d2h");
         outs_[n_out_++] = {dst, at, n};
     }
+    // one D2H of a whole device arena into pinned space; the caller unpacks it after finish()
+    const uint8_t* d2h_arena(const void* src, size_t n) {
+        uint8_t* at = take(n);
+        if (n) stream_check(hipMemcpyAsync(at, src, n, hipMemcpyDeviceToHost, node_stream()), "staged d2h");
+        return at;
+    }
     // one sync for every transfer of the call, then the outputs are unpacked
     void finish(const char* what = "staged sync") {
         node_sync(what);

@@ -751,41 +751,55 @@ void utxo_block_inputs(int64_t h, const uint8_t* keys, int64_t n_in, const int32
     uint32_t log2 = 8;
     while ((int64_t(1) << log2) < 2 * n_in) ++log2;
     const uint32_t scap = 1u << log2;
-    DevBuf<UtxoKeyRec> d_keys(n_in);
-    DevBuf<uint8_t> d_tags(n_in);
-    DevBuf<UtxoPayload> d_pay(n_in);
-    DevBuf<uint32_t> d_dup(n_in);
+    // Two arenas, one transfer each: the four inputs are packed into one pinned region laid out as the
+    // device arena (one H2D), the five outputs are written into one device arena (one D2H), instead of
+    // a copy call per array (each hipMemcpyAsync is ~5 us of host time on the block path).
+    size_t in_off[5] = {0}, out_off[6] = {0};
+    {
+        const size_t in_n[4] = {sizeof(UtxoKeyRec) * size_t(n_in), 8 * size_t(n_out), 4 * size_t(n_tx + 1),
+                                4 * size_t(n_tx + 1)};
+        for (int i = 0; i < 4; ++i) in_off[i + 1] = ((in_off[i] + in_n[i]) + 255) & ~size_t(255);
+        const size_t out_n[5] = {size_t(n_in), sizeof(UtxoPayload) * size_t(n_in), 4 * size_t(n_in),
+                                 8 * size_t(n_tx), 4 * size_t(n_tx)};
+        for (int i = 0; i < 5; ++i) out_off[i + 1] = ((out_off[i] + out_n[i]) + 255) & ~size_t(255);
+    }
+    DevBuf<uint8_t> d_in(in_off[4]), d_outa(out_off[5]);
     DevBuf<unsigned long long> d_scratch(scap);
-    DevBuf<int32_t> d_in_start(n_tx + 1), d_out_start(n_tx + 1);
-    DevBuf<uint64_t> d_out(n_out);
-    DevBuf<int64_t> d_fee(n_tx);
-    DevBuf<uint32_t> d_miss(n_tx);
-    StagedIO io(sizeof(UtxoKeyRec) * size_t(n_in) + 8 * size_t(n_out) + 8 * size_t(n_tx + 1) +
-                size_t(n_in) * (1 + sizeof(UtxoPayload) + 4) + 12 * size_t(n_tx));
-    io.h2d(d_keys.p, keys, sizeof(UtxoKeyRec) * size_t(n_in));
-    io.h2d(d_out.p, out_amount, 8 * size_t(n_out));
-    io.h2d(d_in_start.p, in_start, 4 * size_t(n_tx + 1));
-    io.h2d(d_out_start.p, out_start, 4 * size_t(n_tx + 1));
+    auto* d_keys = reinterpret_cast<UtxoKeyRec*>(d_in.p + in_off[0]);
+    auto* d_out = reinterpret_cast<uint64_t*>(d_in.p + in_off[1]);
+    auto* d_in_start = reinterpret_cast<int32_t*>(d_in.p + in_off[2]);
+    auto* d_out_start = reinterpret_cast<int32_t*>(d_in.p + in_off[3]);
+    auto* d_tags = d_outa.p + out_off[0];
+    auto* d_pay = reinterpret_cast<UtxoPayload*>(d_outa.p + out_off[1]);
+    auto* d_dup = reinterpret_cast<uint32_t*>(d_outa.p + out_off[2]);
+    auto* d_fee = reinterpret_cast<int64_t*>(d_outa.p + out_off[3]);
+    auto* d_miss = reinterpret_cast<uint32_t*>(d_outa.p + out_off[4]);
+    StagedIO io(in_off[4] + out_off[5]);
+    uint8_t* hin = io.h2d_take(in_off[4]);
+    std::memcpy(hin + in_off[0], keys, sizeof(UtxoKeyRec) * size_t(n_in));
+    std::memcpy(hin + in_off[1], out_amount, 8 * size_t(n_out));
+    std::memcpy(hin + in_off[2], in_start, 4 * size_t(n_tx + 1));
+    std::memcpy(hin + in_off[3], out_start, 4 * size_t(n_tx + 1));
+    io.h2d_issue(d_in.p, hin, in_off[4]);
     node_memset(d_scratch.p, 0, sizeof(unsigned long long) * scap, "memset scratch");
     if (n_in) {
         const dim3 g(unsigned((n_in + 255) / 256));
-        hipLaunchKernelGGL(utxo_lookup_kernel, g, dim3(256), 0, node_stream(), t.tab, t.pay, t.cap - 1, d_keys.p, n_in, d_tags.p,
-                           d_pay.p);
+        hipLaunchKernelGGL(utxo_lookup_kernel, g, dim3(256), 0, node_stream(), t.tab, t.pay, t.cap - 1, d_keys, n_in, d_tags,
+                           d_pay);
         uck(hipGetLastError(), "utxo_lookup_kernel");
-        hipLaunchKernelGGL(block_dup_kernel, g, dim3(256), 0, node_stream(), d_keys.p, n_in, d_scratch.p, scap - 1, d_dup.p);
+        hipLaunchKernelGGL(block_dup_kernel, g, dim3(256), 0, node_stream(), d_keys, n_in, d_scratch.p, scap - 1, d_dup);
         uck(hipGetLastError(), "block_dup_kernel");
     }
-    hipLaunchKernelGGL(block_fee_kernel, dim3(unsigned((n_tx + 255) / 256)), dim3(256), 0, node_stream(), d_tags.p, d_pay.p,
-                       d_in_start.p, d_out.p, d_out_start.p, n_tx, want_tag, d_fee.p, d_miss.p);
+    hipLaunchKernelGGL(block_fee_kernel, dim3(unsigned((n_tx + 255) / 256)), dim3(256), 0, node_stream(), d_tags, d_pay,
+                       d_in_start, d_out, d_out_start, n_tx, want_tag, d_fee, d_miss);
     uck(hipGetLastError(), "block_fee_kernel");
-    if (n_in) {
-        io.d2h(r.tags, d_tags.p, size_t(n_in));
-        io.d2h(r.payload, d_pay.p, size_t(n_in) * sizeof(UtxoPayload));
-        io.d2h(r.dup_of, d_dup.p, 4 * size_t(n_in));
-    }
-    io.d2h(r.fee, d_fee.p, 8 * size_t(n_tx));
-    io.d2h(r.missing, d_miss.p, 4 * size_t(n_tx));
+    const uint8_t* hout = io.d2h_arena(d_outa.p, out_off[5]);
     io.finish("block inputs");  // one sync, then each output copied once out of the pinned staging
+    std::memcpy(r.tags, hout + out_off[0], size_t(n_in));
+    std::memcpy(r.payload, hout + out_off[1], sizeof(UtxoPayload) * size_t(n_in));
+    std::memcpy(r.dup_of, hout + out_off[2], 4 * size_t(n_in));
+    std::memcpy(r.fee, hout + out_off[3], 8 * size_t(n_tx));
+    std::memcpy(r.missing, hout + out_off[4], 4 * size_t(n_tx));
     // exact confirmation of duplicate candidates (full 36-byte key compare)
     const UtxoKeyRec* kr = reinterpret_cast<const UtxoKeyRec*>(keys);
     for (int64_t i = 0; i < n_in; ++i) {
