@@ -872,9 +872,11 @@ void p256_verify_fused_gpu(int64_t n_jobs, int64_t n_out, const std::function<vo
     hck(hipGetLastError(), "p256_keyrec_kernel launch");
     VerifyScratch sc;
     if (n_jobs) verify_launch(b_items.p, n_jobs, d_tab, b_st.p, sc);
-    io.d2h(st, b_st.p, size_t(n_jobs));
-    io.d2h(out_ok, b_st.p + n_jobs, size_t(n_out));
+    // statuses and output flags are adjacent on the device: one D2H for both
+    const uint8_t* hst = io.d2h_arena(b_st.p, size_t(n_jobs + n_out));
     io.finish("fused verify");
+    std::memcpy(st, hst, size_t(n_jobs));
+    std::memcpy(out_ok, hst + n_jobs, size_t(n_out));
     if (items_out && std::find(st, st + n_jobs, uint8_t(0)) != st + n_jobs) {
         items_out->resize(sizeof(VerifyItem) * size_t(n_jobs));
         node_d2h(items_out->data(), b_items.p, items_out->size(), "d2h verify items");
