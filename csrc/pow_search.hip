@@ -258,6 +258,7 @@ PowResult pow_search_gpu(const PowJobHost& hj, uint64_t start, uint64_t count, i
                          uint32_t chunk_iters, uint32_t cap, int variant) {
     PowJobDev job = make_pow_job(hj);
     const bool v2 = hj.header.size() == 108;
+    node_device_enter();  // a rank's search from any of its threads runs on the rank's own GPU
     PowDeviceBuffers& buf = pow_buffers(cap);
     hipStream_t st = miner_stream();  // least priority: node kernels go first (csrc/streams.h)
     hip_check(hipMemsetAsync(buf.d_count, 0, sizeof(uint32_t), st), "memset");
