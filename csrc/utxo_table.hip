@@ -795,9 +795,11 @@ void utxo_block_inputs(int64_t h, const uint8_t* keys, int64_t n_in, const int32
     uck(hipGetLastError(), "block_fee_kernel");
     const uint8_t* hout = io.d2h_arena(d_outa.p, out_off[5]);
     io.finish("block inputs");  // one sync, then each output copied once out of the pinned staging
-    std::memcpy(r.tags, hout + out_off[0], size_t(n_in));
-    std::memcpy(r.payload, hout + out_off[1], sizeof(UtxoPayload) * size_t(n_in));
-    std::memcpy(r.dup_of, hout + out_off[2], 4 * size_t(n_in));
+    if (n_in) {  // (an empty numpy array's data pointer may be null)
+        std::memcpy(r.tags, hout + out_off[0], size_t(n_in));
+        std::memcpy(r.payload, hout + out_off[1], sizeof(UtxoPayload) * size_t(n_in));
+        std::memcpy(r.dup_of, hout + out_off[2], 4 * size_t(n_in));
+    }
     std::memcpy(r.fee, hout + out_off[3], 8 * size_t(n_tx));
     std::memcpy(r.missing, hout + out_off[4], 4 * size_t(n_tx));
     // exact confirmation of duplicate candidates (full 36-byte key compare)

@@ -126,6 +126,21 @@ def test_block_inputs_and_set_hash_gpu_match_host(gpu):
         assert h.set_hash(tag) == g.set_hash(tag)
 
 
+@pytest.mark.parametrize('backend', [*HOSTS, pytest.param('gpu', marks=pytest.mark.gpu)])
+def test_block_inputs_without_inputs(backend, request):
+    """Txs with no inputs at all (n_in = 0, the arenas' input regions empty): fees are minus the outputs."""
+    if backend == 'gpu':
+        request.getfixturevalue('gpu')
+    idx = UtxoIndex(backend=backend)
+    idx.insert(_keys(10, 3), 0, make_payload([5] * 10, [bytes([42]) + bytes(32)] * 10))
+    ins = np.zeros(4, np.int32)
+    ost = np.array([0, 1, 3, 3], np.int32)
+    outs = np.array([7, 11, 13], np.uint64)
+    tags, pay, dup_of, fee, missing, n_dup = idx.block_inputs(np.zeros((0, 40), np.uint8), ins, outs, ost, 0)
+    assert len(tags) == len(pay) == len(dup_of) == 0 and n_dup == 0
+    assert list(fee) == [-7, -24, 0] and list(missing) == [0, 0, 0]
+
+
 def _address_case(idx, seed):
     """3000 outputs over 40 owners (33-byte and 64-byte addresses) in three tables, some spent."""
     rng = random.Random(seed)
