@@ -285,6 +285,8 @@ def main(argv=None):
         sys.exit(2)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    # log lines go through the native console writer, as in a node process (upow_amd/utils/logger.py)
+    os.environ.setdefault('UPOW_NATIVE_CONSOLE', '1')
     from upow_amd.ops.native import lib
     lib()  # loads torch's HIP runtime first, then the extension (fails loudly if not built)
     from upow_amd.utils.cpus import presize_fd_table, tune_malloc

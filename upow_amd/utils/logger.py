@@ -33,7 +33,19 @@ def _configure():
         console.setLevel(logging.WARNING if '--nologs' in sys.argv else logging.INFO)
     console.setFormatter(fmt)
     logger.addHandler(console)
-    if os.environ.get('UPOW_FILE_LOG', '0') == '1':
+    file_log = os.environ.get('UPOW_FILE_LOG', '0') == '1'
+    # the logger's own level is the lowest level any of its handlers writes: without the DEBUG file a debug
+    # call returns at isEnabledFor instead of building a record that every handler then drops (~15 us per call;
+    # the sync path made one per block, profiles/r6/syncprof200_r6o.txt)
+    logger.setLevel(logging.DEBUG if file_log else console.level)
+    if not file_log and os.environ.get('UPOW_NATIVE_CONSOLE') == '1':
+        # library use that asks for it (bench.py): the console lines go through the native writer thread, as
+        # a node's do, instead of a format + write + flush of stderr on the calling thread
+        native_console = _native_console(fmt, console.level)
+        if native_console is not None:
+            logger.removeHandler(console)
+            logger.addHandler(native_console)
+    if file_log:
         data = os.environ.get('UPOW_DATA_DIR')
         log_dir = os.environ.get('UPOW_LOG_DIR') or (os.path.join(data, 'logs') if data else 'logs')
         try:
