@@ -121,3 +121,28 @@ def test_rollback_300_blocks_across_journal_rotation(fast_chain, monkeypatch, tm
         finally:
             db.close()
     asyncio.run(go())
+
+
+def test_recent_block_rows_match_sql_and_follow_a_rollback(fast_chain):
+    """The recent-rows cache that serves the retarget's block lookup (Database._recent_rows) returns the row
+    SQL holds, and a rollback drops the rows it removed."""
+    async def go():
+        db = await Database.create(utxo_backend='host')
+        try:
+            A = B.address_of(KA)
+            for k in range(130):
+                await devnet.mine_block(A, [], ts=1_700_000_000 + 60 * (k + 1))
+            assert 31 in db._recent_rows and 130 in db._recent_rows
+            cached = {i: await db.get_block_by_id(i) for i in (31, 100, 129, 130)}
+            db._recent_rows.clear()
+            for i, row in cached.items():
+                assert row == await db.get_block_by_id(i), i
+            for k in range(130, 135):
+                await devnet.mine_block(A, [], ts=1_700_000_000 + 60 * (k + 1))
+            await db.remove_blocks(133)
+            assert all(i < 133 for i in db._recent_rows)
+            assert await db.get_block_by_id(133) is None
+            assert (await db.get_block_by_id(132))['id'] == 132
+        finally:
+            db.close()
+    asyncio.run(go())
