@@ -130,19 +130,19 @@ def test_recent_block_rows_match_sql_and_follow_a_rollback(fast_chain):
         db = await Database.create(utxo_backend='host')
         try:
             A = B.address_of(KA)
-            for k in range(130):
+            for k in range(40):
                 await devnet.mine_block(A, [], ts=1_700_000_000 + 60 * (k + 1))
-            assert 31 in db._recent_rows and 130 in db._recent_rows
-            cached = {i: await db.get_block_by_id(i) for i in (31, 100, 129, 130)}
+            assert 1 in db._recent_rows and 40 in db._recent_rows
+            cached = {i: await db.get_block_by_id(i) for i in (1, 20, 39, 40)}
             db._recent_rows.clear()
             for i, row in cached.items():
                 assert row == await db.get_block_by_id(i), i
-            for k in range(130, 135):
+            for k in range(40, 45):
                 await devnet.mine_block(A, [], ts=1_700_000_000 + 60 * (k + 1))
-            await db.remove_blocks(133)
-            assert all(i < 133 for i in db._recent_rows)
-            assert await db.get_block_by_id(133) is None
-            assert (await db.get_block_by_id(132))['id'] == 132
+            await db.remove_blocks(43)
+            assert all(i < 43 for i in db._recent_rows)
+            assert await db.get_block_by_id(43) is None
+            assert (await db.get_block_by_id(42))['id'] == 42
         finally:
             db.close()
     asyncio.run(go())
