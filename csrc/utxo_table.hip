@@ -776,10 +776,13 @@ void utxo_block_inputs(int64_t h, const uint8_t* keys, int64_t n_in, const int32
     auto* d_miss = reinterpret_cast<uint32_t*>(d_outa.p + out_off[4]);
     StagedIO io(in_off[4] + out_off[5]);
     uint8_t* hin = io.h2d_take(in_off[4]);
-    std::memcpy(hin + in_off[0], keys, sizeof(UtxoKeyRec) * size_t(n_in));
-    std::memcpy(hin + in_off[1], out_amount, 8 * size_t(n_out));
-    std::memcpy(hin + in_off[2], in_start, 4 * size_t(n_tx + 1));
-    std::memcpy(hin + in_off[3], out_start, 4 * size_t(n_tx + 1));
+    auto put = [&](int i, const void* src, size_t n) {  // (an empty input array's pointer may be null)
+        if (n) std::memcpy(hin + in_off[i], src, n);
+    };
+    put(0, keys, sizeof(UtxoKeyRec) * size_t(n_in));
+    put(1, out_amount, 8 * size_t(n_out));
+    put(2, in_start, 4 * size_t(n_tx + 1));
+    put(3, out_start, 4 * size_t(n_tx + 1));
     io.h2d_issue(d_in.p, hin, in_off[4]);
     node_memset(d_scratch.p, 0, sizeof(unsigned long long) * scap, "memset scratch");
     if (n_in) {
