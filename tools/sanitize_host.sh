@@ -111,12 +111,33 @@ for v in asan tsan; do
 done
 EXT=$(python3 -c 'import sysconfig; print(sysconfig.get_config_var("EXT_SUFFIX"))')
 export UPOW_NO_TORCH=1 UPOW_DISABLE_GPU=1 PYTHONMALLOC=malloc
-UPOW_NATIVE_SO=$ROOT/build/native-asan/_native$EXT ASAN_OPTIONS=detect_leaks=0:detect_odr_violation=0:abort_on_error=1 \
-  UBSAN_OPTIONS=print_stacktrace=1 timeout -k 10 1500 "$OUT/pysan_asan" -m pytest -q -x -m "not gpu" -p no:cacheprovider \
-  tests/test_txcodec.py tests/test_hexspans.py tests/test_http_server.py tests/test_mempool_index.py tests/test_ledger_writer.py \
-  tests/test_gov_cascade.py tests/test_log_appender.py tests/test_fastpath.py tests/test_fastpath_governance.py \
-  tests/test_rollback_undo.py tests/test_crash_recovery.py tests/test_process_tuning.py tests/test_utxo.py > "$OUT/pytest_asan.log" 2>&1 \
-  || { tail -60 "$OUT/pytest_asan.log"; exit 1; }
+# three groups of test files in parallel processes (one ASan interpreter each; the files use ephemeral ports
+# and their own temporary directories), so the stage takes the time of its slowest group
+ASAN_GROUPS=("tests/test_utxo.py tests/test_txcodec.py tests/test_hexspans.py tests/test_http_server.py"
+  "tests/test_fastpath.py tests/test_fastpath_governance.py tests/test_rollback_undo.py tests/test_gov_cascade.py"
+  "tests/test_crash_recovery.py tests/test_ledger_writer.py tests/test_mempool_index.py tests/test_log_appender.py tests/test_process_tuning.py")
+pids=()
+for g in 0 1 2; do
+  UPOW_NATIVE_SO=$ROOT/build/native-asan/_native$EXT ASAN_OPTIONS=detect_leaks=0:detect_odr_violation=0:abort_on_error=1 \
+    UBSAN_OPTIONS=print_stacktrace=1 timeout -k 10 1500 "$OUT/pysan_asan" -m pytest -q -x -m "not gpu" -p no:cacheprovider \
+    ${ASAN_GROUPS[$g]} > "$OUT/pytest_asan_$g.log" 2>&1 &
+  pids+=($!)
+done
+asan_ok=1
+for g in 0 1 2; do
+  wait "${pids[$g]}" || { echo "ASan group $g failed:"; tail -60 "$OUT/pytest_asan_$g.log"; asan_ok=0; }
+done
+[ $asan_ok = 1 ] || exit 1
+python3 - "$OUT" > "$OUT/pytest_asan.log" <<'PYEOF'
+import re, sys
+total = 0
+for g in range(3):
+    last = open(f'{sys.argv[1]}/pytest_asan_{g}.log').read().strip().splitlines()[-1]
+    m = re.search(r'(\d+) passed', last)
+    total += int(m.group(1)) if m else 0
+    print(f'group {g}: {last}')
+print(f'{total} passed in 3 parallel groups')
+PYEOF
 echo "python tests under ASan + UBSan: $(tail -1 "$OUT/pytest_asan.log")"
 UPOW_NATIVE_SO=$ROOT/build/native-tsan/_native$EXT TSAN_OPTIONS=halt_on_error=1:report_signal_unsafe=0 \
   timeout -k 10 900 "$OUT/pysan_tsan" -m pytest -q -x -m "not gpu" -p no:cacheprovider \
